@@ -1,0 +1,39 @@
+"""Host codec dispatch for the interactive (one-record-at-a-time) path.
+
+Uses the native C++ host codec (``csrc/host/zk_host_codec.cpp``, built
+in-tree as ``zkmi/_zkhost*.so``) when present, else the pure-Python oracle in
+:mod:`zkmi.jute`.  Both expose identical functions and produce identical
+objects; ``tests/test_host_codec.py`` checks byte/record parity.
+
+``ZKMI_HOST_CODEC=python`` forces the oracle (used by the parity tests).
+"""
+
+import os
+
+from . import jute
+
+IMPL = 'python'
+
+encode_request = jute.encode_request
+decode_response = jute.decode_response
+encode_connect_request = jute.encode_connect_request
+decode_connect_response = jute.decode_connect_response
+decode_connect_request = jute.decode_connect_request
+encode_connect_response = jute.encode_connect_response
+decode_request = jute.decode_request
+encode_response = jute.encode_response
+scan_frames = jute.scan_frames
+frame = jute.frame
+
+if os.environ.get('ZKMI_HOST_CODEC', 'native') != 'python':
+    try:
+        from . import _zkhost  # noqa: F401  (built by __graft_entry__.build)
+    except ImportError:
+        _zkhost = None
+    if _zkhost is not None:
+        _zkhost.init(jute.Stat)
+        encode_request = _zkhost.encode_request
+        decode_response = _zkhost.decode_response
+        scan_frames = _zkhost.scan_frames
+        frame = _zkhost.frame
+        IMPL = 'native'

@@ -1,0 +1,39 @@
+"""Tunables the reference hard-codes, exposed with the reference's defaults
+(SURVEY §5 "Config / flags").  Tests shrink the time constants so that
+expiry / ping-timeout scenarios run in seconds."""
+
+from dataclasses import dataclass, field
+
+
+@dataclass
+class RecoveryPolicy(object):
+    timeout: int = 5000      # ms allowed for one attempt
+    retries: int = 3         # attempts before a backend counts as failed
+    delay: int = 1000        # initial backoff, doubled per failure
+    max_delay: int = 30000   # backoff cap (monitor mode)
+
+
+@dataclass
+class ClientConfig(object):
+    # lib/connection-fsm.js:201-203 — ping every max(T/4, floor)
+    ping_interval_divisor: float = 4.0
+    ping_floor_ms: int = 2000
+    # lib/connection-fsm.js:439-441 — ping timeout max(T/8, floor)
+    ping_timeout_divisor: float = 8.0
+    ping_timeout_floor_ms: int = 2000
+    # lib/zk-streams.js:23
+    max_packet: int = 16 * 1024 * 1024
+    # lib/zk-session.js:35-36 — watcher double-check 4h + U(0, 8h)
+    doublecheck_ms: int = 4 * 3600 * 1000
+    doublecheck_rand_ms: int = 8 * 3600 * 1000
+    # lib/client.js:93-114 — cueball ConnectionSet options
+    connect_policy: RecoveryPolicy = field(
+        default_factory=lambda: RecoveryPolicy(3000, 3, 500))
+    default_policy: RecoveryPolicy = field(
+        default_factory=lambda: RecoveryPolicy(5000, 3, 1000))
+    target: int = 1
+    maximum: int = 3
+    decoherence_interval_s: float = 600.0
+    shuffle_backends: bool = False
+    # lib/client.js:173-176 — closing progress log interval
+    close_log_interval_ms: int = 5000

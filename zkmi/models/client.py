@@ -1,0 +1,490 @@
+"""L6 — the public ``Client`` (lifecycle FSM + data API).
+
+Parity: ``ZKClient`` (``lib/client.js:31-601``): option handling
+(``:34-83``), connection management (``:88-118``, ``:275-309``), lifecycle
+states ``normal`` / ``closing`` / ``closed`` (``:127-181``), session event
+wiring (``:187-262``) and the data API (``:318-601``).
+
+Threading: every FSM runs on the client's :class:`~zkmi.runtime.loop.Loop`
+thread.  Public methods may be called from any thread: arguments are
+validated synchronously in the caller (bad arguments raise, like the
+reference's ``assert-plus`` checks, ``test/nasty.test.js:197-221``), then
+the operation is marshalled onto the loop.  Callbacks and events always run
+on the loop thread.  ``*_sync`` helpers block the calling thread for a
+result (they must not be called from the loop thread itself).
+"""
+
+import threading
+
+from .. import consts
+from ..config import ClientConfig
+from ..errors import ZKNotConnectedError
+from ..jute import DEFAULT_ACL, Stat  # noqa: F401  (re-export)
+from ..runtime.fsm import FSM
+from ..runtime.loop import default_loop
+from ..utils.log import create_logger
+from ..utils.metrics import create_collector, METRIC_ZK_EVENT_COUNTER
+from .connection import ZKConnectionFSM
+from .connection_set import ConnectionSet, StaticResolver
+from .session import ZKSession
+
+
+def _check_str(v, name):
+    if not isinstance(v, str):
+        raise TypeError('%s (string) is required' % name)
+
+
+def _check_func(v, name='callback'):
+    if not callable(v):
+        raise TypeError('%s (func) is required' % name)
+
+
+def _check_bytes(v, name):
+    if not isinstance(v, (bytes, bytearray, memoryview)):
+        raise TypeError('%s (buffer) is required' % name)
+
+
+def _check_int(v, name, optional=False):
+    if v is None and optional:
+        return
+    if isinstance(v, bool) or not isinstance(v, int):
+        raise TypeError('%s (number) is required' % name)
+
+
+def _norm_options(options):
+    if options is None:
+        options = {}
+    if not isinstance(options, dict):
+        raise TypeError('options (object) is required')
+    options = dict(options)
+    acl = options.get('acl')
+    if acl is not None and (not isinstance(acl, list) or
+                            not all(isinstance(a, dict) for a in acl)):
+        raise TypeError('options.acl ([object]) is required')
+    flags = options.get('flags')
+    if flags is not None and (not isinstance(flags, list) or
+                              not all(isinstance(f, str) for f in flags)):
+        raise TypeError('options.flags ([string]) is required')
+    if acl is None:
+        options['acl'] = [dict(a) for a in DEFAULT_ACL]
+    if flags is None:
+        options['flags'] = []
+    for f in options['flags']:
+        if f not in consts.CREATE_FLAGS:
+            raise ValueError('unknown flag %r' % (f,))
+    return options
+
+
+class Client(FSM):
+    """A ZooKeeper client.
+
+    ``Client(address='127.0.0.1', port=2181)`` or
+    ``Client(servers=[{'address':..., 'port':...}, ...])``; optional
+    ``sessionTimeout`` (ms, default 30000), ``log``, ``collector``,
+    ``loop``, ``config`` (:class:`~zkmi.config.ClientConfig`) and
+    ``session`` (credentials from :meth:`credentials` to resume an existing
+    session)."""
+
+    def __init__(self, opts=None, **kw):
+        o = dict(opts or {})
+        o.update(kw)
+        log = o.get('log')
+        if log is None:
+            self.log = create_logger('zkmi', component='ZKClient')
+        else:
+            self.log = log.child(component='ZKClient')
+        self.collector = o.get('collector') or create_collector()
+        self.collector.counter(METRIC_ZK_EVENT_COUNTER,
+                               'Total number of zookeeper events')
+        servers = o.get('servers')
+        if servers is None:
+            _check_str(o.get('address'), 'options.address')
+            _check_int(o.get('port'), 'options.port')
+            self.servers = [{'address': o['address'], 'port': o['port']}]
+        else:
+            if not isinstance(servers, list) or not servers:
+                raise TypeError('options.servers ([object]) is required')
+            for s in servers:
+                _check_str(s.get('address'), 'servers[].address')
+                _check_int(s.get('port'), 'servers[].port')
+            self.servers = [dict(s) for s in servers]
+        st = o.get('sessionTimeout')
+        _check_int(st, 'options.sessionTimeout', optional=True)
+        self.session_timeout = consts.DEFAULT_SESSION_TIMEOUT if st is None \
+            else st
+        self.config = o.get('config') or ClientConfig()
+        self.loop = o.get('loop') or default_loop()
+        self.tracer = o.get('tracer')
+        self._resume_cred = o.get('session')
+        self.session = None
+        self.old_session = None
+        self.conns = {}
+        self.hdls = {}
+        self.loop.run(self._init_on_loop)
+
+    def _init_on_loop(self):
+        self.resolver = StaticResolver(self.servers, consts.DEFAULT_PORT)
+        self.cset = ConnectionSet(self.resolver, self._makeConnection,
+                                 self.loop, self.log, self.config)
+        self.cset.on('added', self._onSetAdded)
+        self.cset.on('removed', self._onSetRemoved)
+        self.cset.on('stateChanged', self._onSetStateChanged)
+        FSM.__init__(self, 'normal', self.loop)
+
+    # aliases matching the reference's private field names used by tests
+    @property
+    def zc_set(self):
+        return self.cset
+
+    # -- lifecycle -------------------------------------------------------------
+
+    def state_normal(self, S):
+        self._newSession()
+        if self._resume_cred is not None:
+            self.session.adopt_credentials(self._resume_cred)
+            self._resume_cred = None
+        self.resolver.start()
+        S.on(self, 'closeAsserted', lambda: S.gotoState('closing'))
+
+    def state_closing(self, S):
+        box = {'done': 0}
+
+        def bump():
+            box['done'] += 1
+            if box['done'] == 3:
+                S.gotoState('closed')
+
+        S.on(self.session, 'stateChanged',
+             lambda st: bump() if st in ('closed', 'expired') else None)
+        S.on(self.cset, 'stateChanged',
+             lambda st: bump() if st == 'stopped' else None)
+        S.on(self.resolver, 'stateChanged',
+             lambda st: bump() if st == 'stopped' else None)
+        if self.session.isInState('closed') or \
+                self.session.isInState('expired'):
+            box['done'] += 1
+        if self.cset.isInState('stopped'):
+            box['done'] += 1
+        if self.resolver.isInState('stopped'):
+            box['done'] += 1
+        if box['done'] == 3:
+            S.gotoState('closed')
+            return
+        self.cset.stop()
+        self.resolver.stop()
+        self.session.close()
+        S.interval(self.config.close_log_interval_ms,
+                   lambda: self.log.trace('still waiting for zk client to '
+                                          'shut down, %d/3 done',
+                                          box['done']))
+
+    def state_closed(self, S):
+        self.emit('close')
+
+    def close(self, cb=None):
+        """Close the client; ``cb`` (optional) runs on ``'close'`` (the
+        reference documents it but ignores it)."""
+        def go():
+            if cb is not None:
+                if self.isInState('closed'):
+                    self.loop.call_soon(cb)
+                else:
+                    self.once('close', cb)
+            self.emit('closeAsserted')
+        self.loop.call_soon(go) if not self.loop.in_loop() else go()
+
+    def _newSession(self):
+        if not self.isInState('normal'):
+            return
+        s = ZKSession(self.session_timeout, self.log, self.collector,
+                      self.loop, self.config)
+        self.session = s
+
+        def final_handler(st):
+            if st == 'attached':
+                self._emitAfterConnected('connect')
+            elif st == 'detached':
+                self.emit('disconnect')
+            elif st == 'expired':
+                self.emit('expire')
+
+        def initial_handler(st):
+            if st == 'attached':
+                s.removeListener('stateChanged', initial_handler)
+                s.on('stateChanged', final_handler)
+                self._emitAfterConnected('session')
+                self._emitAfterConnected('connect')
+        s.on('stateChanged', initial_handler)
+
+    def isConnected(self):
+        conn = self.currentConnection()
+        return conn is not None and conn.isInState('connected')
+
+    is_connected = isConnected
+
+    def _eventTrack(self, evt):
+        if evt not in ('session', 'connect', 'failed'):
+            return
+        self.collector.getCollector(METRIC_ZK_EVENT_COUNTER).increment(
+            {'evtype': evt})
+
+    def _emitAfterConnected(self, evt):
+        # Don't emit until list() etc. can safely be called
+        # (client.js:237-262).
+        c = self.currentConnection()
+        if c is None:
+            return
+        if c.isInState('connected'):
+            def later():
+                self._eventTrack(evt)
+                self.emit(evt)
+            self.loop.call_soon(later)
+        else:
+            def on_conn_ch(cst):
+                if cst == 'connected':
+                    c.removeListener('stateChanged', on_conn_ch)
+                    self._eventTrack(evt)
+                    self.emit(evt)
+            c.on('stateChanged', on_conn_ch)
+
+    def getSession(self):
+        if not self.isInState('normal'):
+            return None
+        if self.session.isInState('expired') or \
+                self.session.isInState('closed'):
+            self.old_session = self.session
+            self._newSession()
+        return self.session
+
+    get_session = getSession
+
+    def credentials(self):
+        """Session credentials for resumption elsewhere (R3)."""
+        return self.loop.run(lambda: self.session.credentials())
+
+    def _onSetAdded(self, key, conn, hdl):
+        self.conns[key] = conn
+        self.hdls[key] = hdl
+
+    def _onSetRemoved(self, key):
+        hdl = self.hdls.pop(key, None)
+        conn = self.conns.pop(key, None)
+        if conn is not None:
+            conn.destroy()
+        if hdl is not None:
+            hdl.release()
+
+    def _onSetStateChanged(self, st):
+        if st == 'failed':
+            def later():
+                self._eventTrack('failed')
+                self.emit('failed', Exception(
+                    'Failed to connect to ZK (exhausted initial retry '
+                    'policy)'))
+            self.loop.call_soon(later)
+
+    def _makeConnection(self, backend):
+        c = ZKConnectionFSM(self, backend, self.log, self.loop, self.config,
+                            tracer=self.tracer)
+        c.connect()
+        return c
+
+    def currentConnection(self):
+        sess = self.getSession()
+        if sess is None:
+            return None
+        return sess.getConnection()
+
+    # -- event registration is thread-safe enough under the GIL; events are
+    # emitted on the loop thread.
+
+    # -- data API ------------------------------------------------------------
+
+    def _dispatch(self, fn):
+        if self.loop.in_loop():
+            fn()
+        else:
+            self.loop.call_soon(fn)
+
+    def _not_connected(self, cb):
+        self.loop.call_soon(cb, ZKNotConnectedError())
+
+    def _request(self, pkt, cb, on_reply):
+        def go():
+            conn = self.currentConnection()
+            if conn is None or not conn.isInState('connected'):
+                self._not_connected(cb)
+                return
+            req = conn.request(pkt)
+            req.once('reply', on_reply)
+            req.once('error', lambda err, *_: cb(err))
+        self._dispatch(go)
+
+    def ping(self, cb):
+        _check_func(cb)
+
+        def go():
+            conn = self.currentConnection()
+            if conn is None or not conn.isInState('connected'):
+                self._not_connected(cb)
+                return
+            conn.ping(lambda err=None, latency=None: cb(err))
+        self._dispatch(go)
+
+    def list(self, path, cb):
+        _check_str(path, 'path')
+        _check_func(cb)
+        self._request({'opcode': 'GET_CHILDREN2', 'path': path,
+                       'watch': False}, cb,
+                      lambda pkt: cb(None, pkt['children'], pkt['stat']))
+
+    def get(self, path, cb):
+        _check_str(path, 'path')
+        _check_func(cb)
+        self._request({'opcode': 'GET_DATA', 'path': path, 'watch': False},
+                      cb, lambda pkt: cb(None, pkt['data'], pkt['stat']))
+
+    def create(self, path, data, options, cb):
+        _check_str(path, 'path')
+        _check_bytes(data, 'data')
+        _check_func(cb)
+        options = _norm_options(options)
+        self._request({'opcode': 'CREATE', 'path': path, 'data': bytes(data),
+                       'acl': options['acl'], 'flags': options['flags']},
+                      cb, lambda pkt: cb(None, pkt['path']))
+
+    def createWithEmptyParents(self, path, data, options, cb):
+        """Create ``path`` and any missing parents (``client.js:412-481``).
+
+        Parents are persistent nodes holding ``b'null'``; NODE_EXISTS on a
+        parent is ignored; ``options`` apply to the final node only."""
+        _check_str(path, 'path')
+        _check_bytes(data, 'data')
+        _check_func(cb)
+        options = _norm_options(options)
+        nodes = path.split('/')[1:]
+        null = b'null'
+
+        def go():
+            conn = self.currentConnection()
+            if conn is None or not conn.isInState('connected'):
+                self._not_connected(cb)
+                return
+            state = {'i': 0, 'cur': '', 'last_path': None}
+
+            def step():
+                i = state['i']
+                if i >= len(nodes):
+                    cb(None, state['last_path'])
+                    return
+                state['cur'] = state['cur'] + '/' + nodes[i]
+                last = (i == len(nodes) - 1)
+                node_data = bytes(data) if last else null
+                opts = options if last else {}
+
+                def done(err, pkt_path=None):
+                    if err is not None and (last or
+                                            err.code != 'NODE_EXISTS'):
+                        cb(err)
+                        return
+                    state['last_path'] = pkt_path
+                    state['i'] += 1
+                    step()
+                self.create(state['cur'], node_data, opts, done)
+            step()
+        self._dispatch(go)
+
+    create_with_empty_parents = createWithEmptyParents
+
+    def set(self, path, data, version, cb):
+        """``cb(err)``: the reference passes ``pkt.path`` which is always
+        undefined for SET_DATA."""
+        _check_str(path, 'path')
+        _check_bytes(data, 'data')
+        _check_int(version, 'version', optional=True)
+        _check_func(cb)
+        if version is None:
+            version = -1
+        self._request({'opcode': 'SET_DATA', 'path': path,
+                       'data': bytes(data), 'version': version},
+                      cb, lambda pkt: cb(None))
+
+    def delete(self, path, version, cb):
+        _check_str(path, 'path')
+        _check_int(version, 'version')
+        _check_func(cb)
+        self._request({'opcode': 'DELETE', 'path': path, 'version': version},
+                      cb, lambda pkt: cb(None))
+
+    def stat(self, path, cb):
+        _check_str(path, 'path')
+        _check_func(cb)
+        self._request({'opcode': 'EXISTS', 'path': path, 'watch': False},
+                      cb, lambda pkt: cb(None, pkt['stat']))
+
+    def getACL(self, path, cb):
+        _check_str(path, 'path')
+        _check_func(cb)
+        self._request({'opcode': 'GET_ACL', 'path': path}, cb,
+                      lambda pkt: cb(None, pkt['acl']))
+
+    get_acl = getACL
+
+    def sync(self, path, cb):
+        _check_str(path, 'path')
+        _check_func(cb)
+        self._request({'opcode': 'SYNC', 'path': path}, cb,
+                      lambda pkt: cb(None))
+
+    def watcher(self, path):
+        _check_str(path, 'path')
+        return self.loop.run(lambda: self.getSession().watcher(path))
+
+    # -- blocking helpers -------------------------------------------------------
+
+    def call_sync(self, method, *args, timeout=30.0):
+        """Call ``method(*args, cb)`` and block for the callback.  Returns the
+        callback's non-error arguments (a single value is unwrapped); raises
+        the callback's error."""
+        if self.loop.in_loop():
+            raise RuntimeError('call_sync must not be used on the loop '
+                               'thread')
+        ev = threading.Event()
+        box = {}
+
+        def cb(err=None, *res):
+            box['err'] = err
+            box['res'] = res
+            ev.set()
+        getattr(self, method)(*args, cb)
+        if not ev.wait(timeout):
+            raise TimeoutError('%s%r timed out' % (method, args))
+        if box['err'] is not None:
+            raise box['err']
+        res = box['res']
+        if len(res) == 0:
+            return None
+        if len(res) == 1:
+            return res[0]
+        return res
+
+    def wait_connected(self, timeout=30.0):
+        """Block until the client is connected (or raise TimeoutError)."""
+        ev = threading.Event()
+
+        def check():
+            if self.isConnected():
+                ev.set()
+            else:
+                self.once('connect', lambda *_: ev.set())
+        self.loop.run(check)
+        if not ev.wait(timeout):
+            raise TimeoutError('client did not connect within %.1fs'
+                               % timeout)
+        return self
+
+    def close_sync(self, timeout=30.0):
+        ev = threading.Event()
+        self.close(lambda *_: ev.set())
+        if not ev.wait(timeout):
+            raise TimeoutError('client did not close within %.1fs' % timeout)

@@ -1,0 +1,430 @@
+"""L4 — one TCP connection to one ZooKeeper server.
+
+Parity: ``ZKConnectionFSM`` (``lib/connection-fsm.js:27-351``), ``ZKRequest``
+and reply routing (``:353-413``), ping / liveness (``:201-207``,
+``:415-463``), ``setWatches`` (``:465-499``).
+
+State graph (same as the reference)::
+
+    init -> connecting -> handshaking -> connected -> closing -> closed
+                 \\             \\             \\__________> error -> closed
+                  \\_____________\\__________________________^
+
+Per-connection state: the xid counter (starts at 0), the outstanding request
+table keyed by xid, and the xid->opcode map the reply decoder needs because
+ZooKeeper replies are not self-describing (SURVEY §7.4 hard part 1).
+"""
+
+import time
+
+from .. import consts
+from .. import codec
+from ..errors import ZKError, ZKProtocolError, ZKPingTimeoutError, \
+    ZKDecodeError
+from ..runtime.emitter import EventEmitter
+from ..runtime.fsm import FSM
+from ..runtime.tcp import TcpSocket
+from ..streams import ZKDecoder, ZKEncoder
+
+
+class ZKRequest(EventEmitter):
+    """An outstanding request; emits ``reply(pkt)`` or ``error(err, pkt)``
+    (``lib/connection-fsm.js:378-382``)."""
+
+    __slots__ = ('packet', 't_submit')
+
+    def __init__(self, packet):
+        EventEmitter.__init__(self)
+        self.packet = packet
+        self.t_submit = time.perf_counter()
+
+
+class ZKConnectionFSM(FSM):
+
+    def __init__(self, client, backend, log, loop, config, tracer=None):
+        self.client = client
+        self.server = backend                 # {'address':..., 'port':...}
+        self.log = log.child(component='ZKConnectionFSM')
+        self.config = config
+        self.tracer = tracer
+        self.decoder = None
+        self.encoder = None
+        self.xid_map = {}
+        self.xid = 0
+        self.reqs = {}
+        self.socket = None
+        self.session = None
+        self.wanted = True
+        self.last_error = None
+        FSM.__init__(self, 'init', loop)
+
+    # -- reference method names ---------------------------------------------
+
+    def connect(self):
+        assert self.isInState('closed') or self.isInState('init')
+        self.emit('connectAsserted')
+
+    def setUnwanted(self):
+        self.wanted = False
+        self.log.debug('connection now unwanted')
+        self.emit('unwanted')
+
+    def close(self):
+        if self.isInState('closed'):
+            return
+        self.emit('closeAsserted')
+
+    def destroy(self):
+        if self.isInState('closed'):
+            return
+        self.emit('destroyAsserted')
+
+    def nextXid(self):
+        x = self.xid
+        self.xid = (self.xid + 1) & 0x7fffffff
+        return x
+
+    # -- inbound plumbing -----------------------------------------------------
+
+    def _on_data(self, chunk):
+        dec = self.decoder
+        if dec is None:
+            return
+        bodies, err = dec.feed(chunk)
+        n = len(bodies)
+        for i, body in enumerate(bodies):
+            if self.decoder is not dec:
+                return              # torn down mid-chunk
+            self.emit('_rx', body, n - i - 1)
+        if err is not None and self.decoder is dec:
+            self.emit('_rxerr', err)
+
+    def _decode_reply(self, body):
+        try:
+            pkt = codec.decode_response(body, self.xid_map)
+        except (ZKDecodeError, ValueError, KeyError, UnicodeDecodeError) as e:
+            raise ZKProtocolError('BAD_DECODE', 'Failed to decode Response: '
+                                  '%s: %s' % (type(e).__name__, e))
+        xid = pkt['xid']
+        if xid >= 0:
+            self.xid_map.pop(xid, None)
+        return pkt
+
+    # -- states ----------------------------------------------------------------
+
+    def state_init(self, S):
+        S.on(self, 'connectAsserted', lambda: S.gotoState('connecting'))
+
+    def state_connecting(self, S):
+        self.decoder = ZKDecoder(self.config.max_packet)
+        self.encoder = ZKEncoder(self.xid_map)
+        self.log = self.log.child(zkAddress=self.server['address'],
+                                  zkPort=self.server['port'])
+        self.log.trace('attempting new connection')
+        sock = TcpSocket(self.fsm_loop)
+        self.socket = sock
+        sock.on('data', self._on_data)
+
+        def on_error(err):
+            self.last_error = err
+            S.gotoState('error')
+        S.on(sock, 'connect', lambda: S.gotoState('handshaking'))
+        S.on(sock, 'error', on_error)
+        S.on(sock, 'close', lambda: S.gotoState('closed'))
+        S.on(self, 'closeAsserted', lambda: S.gotoState('closed'))
+        S.on(self, 'destroyAsserted', lambda: S.gotoState('closed'))
+        sock.connect(self.server['address'], self.server['port'])
+
+    def state_handshaking(self, S):
+        if not self.wanted:
+            S.gotoState('closed')
+            return
+
+        def on_rx(body, more):
+            if more > 0:
+                self.last_error = ZKProtocolError(
+                    'UNEXPECTED_PACKET', 'Received unexpected additional '
+                    'packet during connect phase')
+                S.gotoState('error')
+                return
+            try:
+                pkt = codec.decode_connect_response(body)
+            except (ZKDecodeError, ValueError) as e:
+                self.last_error = ZKProtocolError(
+                    'BAD_DECODE', 'Failed to decode ConnectResponse: %s: %s'
+                    % (type(e).__name__, e))
+                S.gotoState('error')
+                return
+            if pkt['protocolVersion'] != 0:
+                self.last_error = ZKProtocolError(
+                    'VERSION_INCOMPAT', 'Server version is not compatible')
+                S.gotoState('error')
+                return
+            self.emit('packet', pkt)
+
+        def on_error(err):
+            self.last_error = err
+            S.gotoState('error')
+
+        def on_end():
+            self.last_error = ZKProtocolError(
+                'CONNECTION_LOSS', 'Connection closed unexpectedly.')
+            S.gotoState('error')
+
+        S.on(self, '_rx', on_rx)
+        S.on(self, '_rxerr', on_error)
+        S.on(self.socket, 'error', on_error)
+        S.on(self.socket, 'end', on_end)
+        S.on(self.socket, 'close', on_end)
+        S.on(self, 'closeAsserted', lambda: S.gotoState('closed'))
+        S.on(self, 'destroyAsserted', lambda: S.gotoState('closed'))
+        S.on(self, 'unwanted', lambda: S.gotoState('closed'))
+
+        self.session = self.client.getSession()
+        if self.session is None:
+            S.gotoState('closed')
+            return
+        if self.session.isAttaching():
+            self.log.debug('found ZKSession in state %s while handshaking',
+                           self.session.getState())
+            self.last_error = Exception('ZKSession attaching to another '
+                                        'connection')
+            S.gotoState('error')
+            return
+
+        def on_session(st):
+            if st == 'attached':
+                S.gotoState('connected')
+        S.on(self.session, 'stateChanged', on_session)
+        self.session.attachAndSendCR(self)
+
+    def state_connected(self, S):
+        T = self.session.getTimeout()
+        cfg = self.config
+        interval = max(T / cfg.ping_interval_divisor, cfg.ping_floor_ms)
+        S.interval(interval, lambda: self.ping()).unref()
+        self.log = self.log.child(sessionId=self.session.getSessionId())
+
+        def on_rx(body, more):
+            try:
+                pkt = self._decode_reply(body)
+            except ZKProtocolError as e:
+                self.last_error = e
+                S.gotoState('error')
+                return
+            self.emit('packet', pkt)
+            # Notifications are handled by the session (watchers).
+            if pkt['opcode'] == 'NOTIFICATION':
+                return
+            self.processReply(pkt)
+
+        def on_error(err):
+            self.last_error = err
+            S.gotoState('error')
+
+        def on_end():
+            self.last_error = ZKProtocolError(
+                'CONNECTION_LOSS', 'Connection closed unexpectedly.')
+            S.gotoState('error')
+
+        def on_ping_timeout():
+            self.last_error = ZKPingTimeoutError()
+            S.gotoState('error')
+
+        S.on(self, '_rx', on_rx)
+        S.on(self, '_rxerr', on_error)
+        S.on(self.socket, 'error', on_error)
+        S.on(self.socket, 'end', on_end)
+        S.on(self.socket, 'close', on_end)
+        S.on(self, 'closeAsserted', lambda: S.gotoState('closing'))
+        S.on(self, 'destroyAsserted', lambda: S.gotoState('closed'))
+        S.on(self, 'pingTimeout', on_ping_timeout)
+        S.immediate(lambda: self.emit('connect'))
+
+    def state_closing(self, S):
+        box = {'xid': None}
+
+        def send_close_session():
+            if box['xid'] is not None:
+                return
+            box['xid'] = xid = self.nextXid()
+            self.log.info({'xid': xid}, 'sent CLOSE_SESSION request')
+            data = self.encoder.request({'opcode': 'CLOSE_SESSION',
+                                         'xid': xid})
+            self.socket.end(data)
+
+        def on_rx(body, more):
+            try:
+                pkt = self._decode_reply(body)
+            except ZKProtocolError as e:
+                self.last_error = e
+                S.gotoState('closed')
+                return
+            if box['xid'] is None or pkt['xid'] != box['xid']:
+                self.processReply(pkt)
+                if len(self.reqs) < 1:
+                    send_close_session()
+            else:
+                S.gotoState('closed')
+
+        def on_error(err):
+            self.last_error = err
+            S.gotoState('closed')
+
+        S.on(self, '_rx', on_rx)
+        S.on(self, '_rxerr', on_error)
+        S.on(self.socket, 'error', on_error)
+        S.on(self.socket, 'end', lambda: S.gotoState('closed'))
+        S.on(self.socket, 'close', lambda: S.gotoState('closed'))
+        # destroy() is ignored while closing, as in the reference: the
+        # CLOSE_SESSION exchange completes (or the socket dies).
+        if len(self.reqs) < 1:
+            send_close_session()
+
+    def state_error(self, S):
+        err = self.last_error
+        self.log.warn(err if isinstance(err, BaseException) else {},
+                      'error communicating with ZK')
+        reqs, self.reqs = self.reqs, {}
+        for req in list(reqs.values()):
+            req.emit('error', err)
+        # Not S.immediate: this must be emitted even though we leave the
+        # state right away (lib/connection-fsm.js:318-323).
+        self.fsm_loop.call_soon(self._emit_error, err)
+        S.gotoState('closed')
+
+    def _emit_error(self, err):
+        if self.listenerCount('error') > 0:
+            self.emit('error', err)
+
+    def state_closed(self, S):
+        self.encoder = None
+        if self.socket is not None:
+            self.socket.destroy()
+        self.socket = None
+        self.decoder = None
+
+        def later():
+            self.emit('close')
+            err = ZKProtocolError('CONNECTION_LOSS', 'Connection closed.')
+            reqs, self.reqs = self.reqs, {}
+            for req in list(reqs.values()):
+                req.emit('error', err)
+        S.immediate(later)
+
+    # -- requests ---------------------------------------------------------------
+
+    def processReply(self, pkt):
+        req = self.reqs.get(pkt['xid'])
+        if self.tracer is not None and req is not None:
+            self.tracer.record(pkt['xid'], pkt['opcode'], req.t_submit,
+                               pkt['err'])
+        self.log.trace({'xid': pkt['xid'], 'opcode': pkt['opcode'],
+                        'errorCode': pkt['err']},
+                       'server replied to request')
+        if req is None:
+            return
+        if pkt['err'] == 'OK':
+            req.emit('reply', pkt)
+            return
+        code = pkt['err']
+        err = ZKError(code, consts.ERR_TEXT.get(code, str(code)))
+        req.emit('error', err, pkt)
+
+    def request(self, pkt):
+        if not self.isInState('connected'):
+            raise Exception('Client must be connected to send requests')
+        req = ZKRequest(pkt)
+        xid = self.nextXid()
+        pkt['xid'] = xid
+        self.reqs[xid] = req
+
+        def end_request(*_):
+            if self.reqs.get(xid) is req:
+                del self.reqs[xid]
+        req.once('reply', end_request)
+        req.once('error', end_request)
+        self.log.trace({'xid': xid, 'opcode': pkt['opcode']},
+                       'sent request to server')
+        self.socket.write(self.encoder.request(pkt))
+        return req
+
+    def send(self, pkt):
+        """Raw write of a handshake record (ConnectRequest)."""
+        self.socket.write(self.encoder.connect_request(pkt))
+
+    def ping(self, cb=None):
+        if not self.isInState('connected'):
+            raise Exception('Client must be connected to send packets')
+        xid = consts.XID_PING
+        cur = self.reqs.get(xid)
+        if cur is not None:
+            # Coalesce onto the outstanding ping (connection-fsm.js:425-435).
+            cur.once('reply', lambda *_: cb and cb(None))
+            cur.once('error', lambda err, *_: cb and cb(err))
+            return
+        pkt = {'xid': xid, 'opcode': 'PING'}
+        req = ZKRequest(pkt)
+        self.reqs[xid] = req
+        T = self.session.getTimeout()
+        cfg = self.config
+        timeout = max(T / cfg.ping_timeout_divisor, cfg.ping_timeout_floor_ms)
+        t1 = time.monotonic()
+
+        def on_packet(pkt2):
+            if self.reqs.get(xid) is req:
+                del self.reqs[xid]
+            timer.cancel()
+            ms = (time.monotonic() - t1) * 1000.0
+            self.log.trace('ping ok in %d ms', ms)
+            if cb:
+                cb(None, ms)
+
+        def on_timeout():
+            req.removeListener('reply', on_packet)
+            self.emit('pingTimeout')
+
+        def on_error(err, *_):
+            if self.reqs.get(xid) is req:
+                del self.reqs[xid]
+            timer.cancel()
+            if cb:
+                cb(err)
+        req.once('reply', on_packet)
+        req.once('error', on_error)
+        timer = self.fsm_loop.call_later(timeout, on_timeout)
+        self.socket.write(self.encoder.request(pkt))
+
+    def setWatches(self, events, zxid, cb):
+        if not self.isInState('connected'):
+            raise Exception('Client must be connected to send packets (is '
+                            'in state %s)' % self.getState())
+        xid = consts.XID_SET_WATCHES
+        cur = self.reqs.get(xid)
+        if cur is not None:
+            cur.once('reply', lambda *_: self.setWatches(events, zxid, cb))
+            cur.once('error', lambda err, *_: cb(err))
+            return
+        pkt = {'xid': xid, 'opcode': 'SET_WATCHES', 'relZxid': zxid,
+               'events': events}
+        req = ZKRequest(pkt)
+        self.reqs[xid] = req
+
+        def on_packet(_pkt):
+            if self.reqs.get(xid) is req:
+                del self.reqs[xid]
+            cb(None)
+
+        def on_error(err, *_):
+            if self.reqs.get(xid) is req:
+                del self.reqs[xid]
+            cb(err)
+        req.once('reply', on_packet)
+        req.once('error', on_error)
+        self.socket.write(self.encoder.request(pkt))
+
+    # -- test hooks (the reference tests poke conn.zcf_socket directly) ------
+
+    @property
+    def zcf_socket(self):
+        return self.socket

@@ -1,0 +1,178 @@
+"""TCP socket with Node ``net.Socket``-like events, on the zkmi loop.
+
+Events: ``connect``, ``data(bytes)``, ``end`` (peer half-closed; the socket
+stays writable — the reference connects with ``allowHalfOpen: true``,
+``lib/connection-fsm.js:99-103``), ``error(exc)``, ``close``.
+
+Test hooks replace the reference tests' direct pokes at the socket
+(``sock.emit('error')``, ``sock.destroy()``, ``sock.unpipe()``;
+``test/basic.test.js:1059-1062``, ``:1260``, ``:1374``):
+:meth:`inject_error`, :meth:`destroy`, :meth:`pause_reading`.
+"""
+
+import asyncio
+import socket as _socket
+
+from .emitter import EventEmitter
+
+
+class _Proto(asyncio.Protocol):
+
+    def __init__(self, sock):
+        self.sock = sock
+
+    def connection_made(self, transport):
+        self.sock._on_made(transport)
+
+    def data_received(self, data):
+        self.sock._on_data(data)
+
+    def eof_received(self):
+        self.sock._on_eof()
+        return True
+
+    def connection_lost(self, exc):
+        self.sock._on_lost(exc)
+
+
+class TcpSocket(EventEmitter):
+
+    def __init__(self, loop):
+        EventEmitter.__init__(self)
+        self.loop = loop
+        self.transport = None
+        self.closed = False
+        self.connecting = False
+        self._task = None
+        self._paused = False
+        self._held = []
+        self.remote = None
+        self.bytes_in = 0
+        self.bytes_out = 0
+
+    # -- client side ----------------------------------------------------------
+
+    def connect(self, host, port):
+        self.connecting = True
+        self.remote = (host, port)
+        self._task = self.loop.aio.create_task(self._connect(host, port))
+        return self
+
+    async def _connect(self, host, port):
+        try:
+            await self.loop.aio.create_connection(lambda: _Proto(self),
+                                                  host, port)
+        except asyncio.CancelledError:
+            return
+        except OSError as e:
+            self.connecting = False
+            if not self.closed:
+                self._fail(e)
+
+    # -- server side ----------------------------------------------------------
+
+    @classmethod
+    def protocol_for(cls, loop, on_accept):
+        """asyncio protocol factory for a server: ``on_accept(sock)`` is
+        called with a connected :class:`TcpSocket`."""
+        def factory():
+            s = cls(loop)
+            s._on_accept = on_accept
+            return _Proto(s)
+        return factory
+
+    # -- transport callbacks --------------------------------------------------
+
+    def _on_made(self, transport):
+        self.transport = transport
+        self.connecting = False
+        sk = transport.get_extra_info('socket')
+        if sk is not None:
+            try:
+                sk.setsockopt(_socket.IPPROTO_TCP, _socket.TCP_NODELAY, 1)
+            except OSError:
+                pass
+        if self.closed:
+            transport.abort()
+            return
+        acc = getattr(self, '_on_accept', None)
+        if acc is not None:
+            acc(self)
+        else:
+            self.emit('connect')
+
+    def _on_data(self, data):
+        if self.closed:
+            return
+        self.bytes_in += len(data)
+        if self._paused:
+            self._held.append(data)
+            return
+        self.emit('data', data)
+
+    def _on_eof(self):
+        if not self.closed:
+            self.emit('end')
+
+    def _on_lost(self, exc):
+        if self.closed:
+            return
+        if exc is not None:
+            self._fail(exc)
+        else:
+            self.closed = True
+            self.emit('close')
+
+    def _fail(self, exc):
+        self.closed = True
+        if self.transport is not None:
+            self.transport.abort()
+        self.emit('error', exc)
+        self.emit('close')
+
+    # -- API -----------------------------------------------------------------
+
+    def write(self, data):
+        if self.closed or self.transport is None:
+            return False
+        self.bytes_out += len(data)
+        self.transport.write(data)
+        return True
+
+    def end(self, data=None):
+        """Half-close after writing ``data`` (Node ``socket.end``)."""
+        if data:
+            self.write(data)
+        if self.transport is not None and not self.closed:
+            try:
+                if self.transport.can_write_eof():
+                    self.transport.write_eof()
+            except (OSError, RuntimeError):
+                pass
+
+    def destroy(self):
+        if self.closed:
+            return
+        self.closed = True
+        if self._task is not None and not self._task.done():
+            self._task.cancel()
+        if self.transport is not None:
+            self.transport.abort()
+        self.loop.call_soon(self.emit, 'close')
+
+    def pause_reading(self):
+        """Stop delivering ``data`` events (the reference test #46 unpipes
+        the socket, ``test/basic.test.js:1374``)."""
+        self._paused = True
+
+    def resume_reading(self):
+        self._paused = False
+        held, self._held = self._held, []
+        for d in held:
+            self.emit('data', d)
+
+    def inject_error(self, err):
+        """Emit ``error`` then close, as a real socket failure would."""
+        if self.closed:
+            return
+        self._fail(err)

@@ -1,0 +1,157 @@
+#!/usr/bin/env python3
+"""zkmi headline benchmark (BASELINE.json): "ZK ops/sec (whole node) + p50
+get() RTT, 1M-znode synthetic tree".
+
+Config (BASELINE.json configs[1]): batched get() over a 1M-znode synthetic
+tree with the Jute-decode HIP kernels on each MI355X.  One step = one batch
+of ``--batch`` GET_DATA requests per GPU pushed through the full ZooKeeper
+wire path on the GPU (see zkmi/bench/synthetic.py): client request encode
+(K10) -> server frame scan + request decode (K1, K12) -> tree lookup in HBM
+-> server reply encode (K13) -> client frame scan + reply decode (K1,
+K2-K4) -> on-device check of every reply.  Synthetic data: random 100-byte
+node payloads, uniformly random node per request.
+
+One process per GPU (torchrun); per-GPU work is fixed (weak scaling).  The
+whole-node aggregate (sum over ranks of ops / max-rank time) is reported.
+``p50_get_rtt_us`` is the interactive path: one blocking ``Client.get``
+round trip over loopback TCP to the in-process fake server (host CPU), also
+reported for honesty about where the GPU helps.
+"""
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+# Reference point (locally measured, not published): the
+# reference's own ZKDecodeStream frame+decode on one Xeon core, best case
+# 0.51 M packets/s.  The reference publishes no headline number.
+REF_PKTS_PER_S = 0.51e6
+
+
+def measure_rtt(n=2000):
+    from zkmi import Client
+    from zkmi.server import FakeZKServer
+    srv = FakeZKServer()
+    try:
+        c = Client(address='127.0.0.1', port=srv.port)
+        c.wait_connected(10)
+        c.call_sync('create', '/rtt', b'x' * 100, {})
+        for _ in range(200):
+            c.call_sync('get', '/rtt')
+        lat = []
+        for _ in range(n):
+            t = time.perf_counter()
+            c.call_sync('get', '/rtt')
+            lat.append((time.perf_counter() - t) * 1e6)
+        c.close_sync(10)
+        lat.sort()
+        return statistics.median(lat), lat[int(0.99 * len(lat))]
+    finally:
+        srv.shutdown()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=20)
+    ap.add_argument('--warmup', type=int, default=3)
+    ap.add_argument('--batch', type=int, default=1 << 20,
+                    help='GET_DATA requests per GPU per step')
+    ap.add_argument('--nodes', type=int, default=1_000_000)
+    ap.add_argument('--data-bytes', type=int, default=100)
+    ap.add_argument('--no-rtt', action='store_true')
+    a = ap.parse_args()
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    dev = torch.device('cuda', local)
+    torch.cuda.set_device(dev)
+
+    from zkmi.bench.synthetic import GpuTree, GetPipeline
+    tree = GpuTree(a.nodes, a.data_bytes, device=dev, seed=rank)
+    pipe = GetPipeline(tree, a.batch, seed=rank)
+
+    ok_total = torch.zeros(1, dtype=torch.int64, device=dev)
+    for _ in range(a.warmup):
+        ok_total += pipe.step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ok_total.zero_()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        ok_total += pipe.step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+
+    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    ok = ok_total.clone()
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        dist.all_reduce(ok, op=dist.ReduceOp.SUM)   # R4: node-level counters
+    elapsed = el.item()
+    ops = a.batch * a.steps * world
+    ok = int(ok.item())
+    if ok != ops:
+        raise SystemExit('validation failed: %d of %d replies wrong'
+                         % (ops - ok, ops))
+    value = ops / elapsed
+
+    rtt50 = rtt99 = None
+    if rank == 0 and not a.no_rtt:
+        rtt50, rtt99 = measure_rtt()
+
+    if rank == 0:
+        line = {
+            'metric': 'ZK ops/sec (whole node) + p50 get() RTT, 1M-znode '
+                      'synthetic tree',
+            'value': value,
+            'unit': 'ops/s',
+            'n_gpus': world,
+            'steps': a.steps,
+            'warmup': a.warmup,
+            'ms_per_step': elapsed / a.steps * 1e3,
+            'higher_is_better': True,
+            'scaling': 'weak',
+            'vs_baseline': value / REF_PKTS_PER_S,
+            'dtype': 'bf16',
+            'data': 'synthetic',
+            'config': {
+                'model': 'zk-get %dk-znode tree, %dB data' % (
+                    a.nodes // 1000, a.data_bytes),
+                'global_batch': a.batch * world,
+                'seq_len': 1,
+                'parallelism': 'dp%d' % world,
+            },
+            'p50_get_rtt_us': rtt50,
+            'p99_get_rtt_us': rtt99,
+            'batch_latency_ms': elapsed / a.steps * 1e3,
+            'baseline_note': 'vs_baseline = value / 0.51M pkts/s, the '
+                             'reference ZKDecodeStream frame+decode on one '
+                             'Xeon core (BASELINE.md, local, unpublished)',
+            'dtype_note': 'integer byte codec; no floating-point compute',
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

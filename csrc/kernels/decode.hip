@@ -1,0 +1,375 @@
+// Batched Jute decoders: client replies (K2 header + opcode resolve, K3 Stat,
+// K4 GET_DATA, K5 children, K6 ACL, K7 create/exists/set_data, K8
+// notifications) and server-mode requests (K12).
+// Reference: lib/zk-buffer.js:275-442 (replies), :58-253 (requests).
+//
+// One thread per frame; inputs come from the frame table produced by
+// frame_scan.hip (body offset + length into the RX buffer).  Payloads are
+// never copied: data, paths and string vectors are returned as (offset,
+// length) into the RX buffer, so a GET_DATA reply costs its 16-byte header,
+// 4-byte length and 68-byte Stat in loads regardless of the data size.
+// Outputs are SoA so the consumer (Python / the next kernel) reads them
+// coalesced.  Ragged vectors (children, ACL entries, SET_WATCHES paths) are
+// expanded by a second pass after a scan of the per-frame counts.
+#include "zk_common.h"
+#include "zk_batch.h"
+
+namespace zk {
+
+constexpr int DEC_T = 256;
+
+ZK_DEV bool read_stat(const uint8_t* p, const ZkReplyOut& o, int64_t i) {
+  const int64_t c = o.cap;
+  o.stat64[0 * c + i] = ld_be64(p + 0);
+  o.stat64[1 * c + i] = ld_be64(p + 8);
+  o.stat64[2 * c + i] = ld_be64(p + 16);
+  o.stat64[3 * c + i] = ld_be64(p + 24);
+  o.stat32[0 * c + i] = ld_be32(p + 32);
+  o.stat32[1 * c + i] = ld_be32(p + 36);
+  o.stat32[2 * c + i] = ld_be32(p + 40);
+  o.stat64[4 * c + i] = ld_be64(p + 44);
+  o.stat32[3 * c + i] = ld_be32(p + 52);
+  o.stat32[4 * c + i] = ld_be32(p + 56);
+  o.stat64[5 * c + i] = ld_be64(p + 60);
+  return true;
+}
+
+// Walk `count` ustrings starting at p; returns bytes consumed or -1.
+ZK_DEV int64_t skip_strings(const uint8_t* p, int64_t avail, int32_t count) {
+  int64_t k = 0;
+  for (int32_t j = 0; j < count; ++j) {
+    if (k + 4 > avail) return -1;
+    int32_t l = ld_be32(p + k);
+    if (l < 0) l = 0;
+    k += 4 + l;
+    if (k > avail) return -1;
+  }
+  return k;
+}
+
+// ACL vector entries: perms i32, scheme ustring, id ustring.
+ZK_DEV int64_t skip_acl(const uint8_t* p, int64_t avail, int32_t count) {
+  int64_t k = 0;
+  for (int32_t j = 0; j < count; ++j) {
+    if (k + 4 > avail) return -1;
+    k += 4;
+    int64_t s = skip_strings(p + k, avail - k, 2);
+    if (s < 0) return -1;
+    k += s;
+  }
+  return k;
+}
+
+__global__ __launch_bounds__(DEC_T) void decode_replies_k(
+    const uint8_t* __restrict__ buf, const int64_t* __restrict__ foff,
+    const int32_t* __restrict__ flen, const int64_t* __restrict__ n_dev,
+    int64_t ncap, const int64_t* __restrict__ xid_tab, int64_t xid_mask,
+    ZkReplyOut o) {
+  const uint32_t nwg = gridDim.x;
+  const int64_t i = (int64_t)xcd_remap(blockIdx.x, nwg) * DEC_T + threadIdx.x;
+  if (i >= ncap || i >= *n_dev) return;
+  const uint8_t* p = buf + foff[i];
+  const int64_t L = flen[i];
+  int32_t status = ST_OK;
+  int32_t op = OP_UNKNOWN;
+  int64_t poff = -1;
+  int32_t plen = 0, a0 = 0, a1 = 0;
+  int32_t xid = 0, err = 0;
+  int64_t zxid = 0;
+  if (L < 16) {
+    status = ST_BAD_DECODE;
+  } else {
+    xid = ld_be32(p);
+    zxid = ld_be64(p + 4);
+    err = ld_be32(p + 12);
+    switch (xid) {
+      case XID_NOTIFICATION: op = OP_NOTIFICATION; break;
+      case XID_PING: op = OP_PING; break;
+      case XID_AUTH: op = OP_AUTH; break;
+      case XID_SET_WATCHES: op = OP_SET_WATCHES; break;
+      default: {
+        const int64_t e = xid_tab[xid & xid_mask];
+        if (xid >= 0 && (int32_t)(e >> 32) == xid) op = (int32_t)e;
+        else status = ST_NO_XID;
+      }
+    }
+  }
+  if (status == ST_OK && err == ERR_OK) {
+    const uint8_t* b = p + 16;
+    const int64_t A = L - 16;
+    switch (op) {
+      case OP_GET_DATA: {
+        if (A < 4) { status = ST_BAD_DECODE; break; }
+        int32_t dl = ld_be32(b);
+        if (dl < 0) dl = 0;
+        if (4 + (int64_t)dl + STAT_BYTES > A) { status = ST_BAD_DECODE; break; }
+        poff = foff[i] + 20;
+        plen = dl;
+        read_stat(b + 4 + dl, o, i);
+        break;
+      }
+      case OP_EXISTS: case OP_SET_DATA:
+        if (A < STAT_BYTES) { status = ST_BAD_DECODE; break; }
+        read_stat(b, o, i);
+        break;
+      case OP_CREATE: {
+        if (A < 4) { status = ST_BAD_DECODE; break; }
+        int32_t l = ld_be32(b);
+        if (l < 0) l = 0;
+        if (4 + (int64_t)l > A) { status = ST_BAD_DECODE; break; }
+        poff = foff[i] + 20;
+        plen = l;
+        break;
+      }
+      case OP_GET_CHILDREN: case OP_GET_CHILDREN2: {
+        if (A < 4) { status = ST_BAD_DECODE; break; }
+        const int32_t cnt = max(ld_be32(b), 0);
+        const int64_t k = skip_strings(b + 4, A - 4, cnt);
+        if (k < 0) { status = ST_BAD_DECODE; break; }
+        poff = foff[i] + 20;
+        plen = (int32_t)k;
+        a0 = cnt;
+        if (op == OP_GET_CHILDREN2) {
+          if (4 + k + STAT_BYTES > A) { status = ST_BAD_DECODE; break; }
+          read_stat(b + 4 + k, o, i);
+        }
+        break;
+      }
+      case OP_GET_ACL: {
+        if (A < 4) { status = ST_BAD_DECODE; break; }
+        const int32_t cnt = max(ld_be32(b), 0);
+        const int64_t k = skip_acl(b + 4, A - 4, cnt);
+        if (k < 0 || 4 + k + STAT_BYTES > A) { status = ST_BAD_DECODE; break; }
+        poff = foff[i] + 20;
+        plen = (int32_t)k;
+        a0 = cnt;
+        read_stat(b + 4 + k, o, i);
+        break;
+      }
+      case OP_NOTIFICATION: {
+        if (A < 12) { status = ST_BAD_DECODE; break; }
+        a0 = ld_be32(b);
+        a1 = ld_be32(b + 4);
+        int32_t l = ld_be32(b + 8);
+        if (l < 0) l = 0;
+        if (12 + (int64_t)l > A) { status = ST_BAD_DECODE; break; }
+        poff = foff[i] + 28;
+        plen = l;
+        break;
+      }
+      case OP_PING: case OP_SYNC: case OP_DELETE: case OP_SET_WATCHES:
+      case OP_CLOSE_SESSION: case OP_AUTH:
+        break;
+      default:
+        status = ST_BAD_OPCODE;
+    }
+  }
+  o.xid[i] = xid;
+  o.err[i] = err;
+  o.opcode[i] = op;
+  o.zxid[i] = zxid;
+  o.status[i] = status;
+  o.pay_off[i] = poff;
+  o.pay_len[i] = plen;
+  o.aux0[i] = a0;
+  o.aux1[i] = a1;
+}
+
+// Expand string vectors: region (offset of first string) + count per row ->
+// (off,len) of every string, rows laid out by the scanned `base`.
+__global__ __launch_bounds__(DEC_T) void expand_strings_k(
+    const uint8_t* __restrict__ buf, const int64_t* __restrict__ region,
+    const int32_t* __restrict__ count, const int64_t* __restrict__ base,
+    int64_t n, int64_t* __restrict__ soff, int32_t* __restrict__ slen) {
+  const int64_t i = (int64_t)blockIdx.x * DEC_T + threadIdx.x;
+  if (i >= n) return;
+  const int32_t c = count[i];
+  if (c <= 0 || region[i] < 0) return;
+  int64_t k = region[i];
+  int64_t w = base[i];
+  for (int32_t j = 0; j < c; ++j) {
+    int32_t l = ld_be32(buf + k);
+    if (l < 0) l = 0;
+    soff[w + j] = k + 4;
+    slen[w + j] = l;
+    k += 4 + l;
+  }
+}
+
+// Expand ACL vectors: perms, scheme (off,len), id (off,len) per entry.
+__global__ __launch_bounds__(DEC_T) void expand_acl_k(
+    const uint8_t* __restrict__ buf, const int64_t* __restrict__ region,
+    const int32_t* __restrict__ count, const int64_t* __restrict__ base,
+    int64_t n, int32_t* __restrict__ perms, int64_t* __restrict__ s_off,
+    int32_t* __restrict__ s_len, int64_t* __restrict__ i_off,
+    int32_t* __restrict__ i_len) {
+  const int64_t i = (int64_t)blockIdx.x * DEC_T + threadIdx.x;
+  if (i >= n) return;
+  const int32_t c = count[i];
+  if (c <= 0 || region[i] < 0) return;
+  int64_t k = region[i];
+  int64_t w = base[i];
+  for (int32_t j = 0; j < c; ++j) {
+    perms[w + j] = ld_be32(buf + k);
+    k += 4;
+    int32_t l = max(ld_be32(buf + k), 0);
+    s_off[w + j] = k + 4;
+    s_len[w + j] = l;
+    k += 4 + l;
+    l = max(ld_be32(buf + k), 0);
+    i_off[w + j] = k + 4;
+    i_len[w + j] = l;
+    k += 4 + l;
+  }
+}
+
+// ---------------------------------------------------------------- K12
+__global__ __launch_bounds__(DEC_T) void decode_requests_k(
+    const uint8_t* __restrict__ buf, const int64_t* __restrict__ foff,
+    const int32_t* __restrict__ flen, const int64_t* __restrict__ n_dev,
+    int64_t ncap, ZkReqOut o) {
+  const uint32_t nwg = gridDim.x;
+  const int64_t i = (int64_t)xcd_remap(blockIdx.x, nwg) * DEC_T + threadIdx.x;
+  if (i >= ncap || i >= *n_dev) return;
+  const int64_t base = foff[i];
+  const uint8_t* p = buf + base;
+  const int64_t L = flen[i];
+  int32_t status = ST_OK, xid = 0, op = OP_UNKNOWN, arg = 0;
+  int64_t poff = -1, doff = -1, voff = -1, rel = 0;
+  int32_t pl = 0, dl = 0, vc = 0;
+  if (L < 8) {
+    status = ST_BAD_DECODE;
+  } else {
+    xid = ld_be32(p);
+    op = ld_be32(p + 4);
+    int64_t k = 8;
+    auto get_str = [&](int64_t& off, int32_t& len) -> bool {
+      if (k + 4 > L) return false;
+      int32_t l = ld_be32(p + k);
+      if (l < 0) l = 0;
+      if (k + 4 + l > L) return false;
+      off = base + k + 4;
+      len = l;
+      k += 4 + l;
+      return true;
+    };
+    auto get_i32 = [&](int32_t& v) -> bool {
+      if (k + 4 > L) return false;
+      v = ld_be32(p + k);
+      k += 4;
+      return true;
+    };
+    bool ok = true;
+    switch (op) {
+      case OP_GET_DATA: case OP_EXISTS: case OP_GET_CHILDREN:
+      case OP_GET_CHILDREN2:
+        ok = get_str(poff, pl) && k + 1 <= L;
+        if (ok) { arg = p[k]; ok = (arg == 0 || arg == 1); ++k; }
+        break;
+      case OP_CREATE: {
+        ok = get_str(poff, pl) && get_str(doff, dl) && get_i32(vc);
+        if (!ok) break;
+        if (vc < 0) vc = 0;
+        voff = base + k;
+        const int64_t s = skip_acl(p + k, L - k, vc);
+        ok = s >= 0;
+        if (ok) { k += s; ok = get_i32(arg); }
+        break;
+      }
+      case OP_DELETE:
+        ok = get_str(poff, pl) && get_i32(arg);
+        break;
+      case OP_SET_DATA:
+        ok = get_str(poff, pl) && get_str(doff, dl) && get_i32(arg);
+        break;
+      case OP_GET_ACL: case OP_SYNC:
+        ok = get_str(poff, pl);
+        break;
+      case OP_SET_WATCHES: {
+        if (k + 8 > L) { ok = false; break; }
+        rel = ld_be64(p + k);
+        k += 8;
+        voff = base + k;
+        for (int g = 0; g < 3 && ok; ++g) {
+          int32_t c;
+          ok = get_i32(c);
+          if (!ok) break;
+          c = max(c, 0);
+          const int64_t s = skip_strings(p + k, L - k, c);
+          ok = s >= 0;
+          k += s;
+          vc += c;
+        }
+        break;
+      }
+      case OP_PING: case OP_CLOSE_SESSION:
+        break;
+      default:
+        status = ST_BAD_OPCODE;
+    }
+    if (!ok) status = ST_BAD_DECODE;
+  }
+  o.xid[i] = xid;
+  o.opcode[i] = op;
+  o.status[i] = status;
+  o.path_off[i] = poff;
+  o.path_len[i] = pl;
+  o.data_off[i] = doff;
+  o.data_len[i] = dl;
+  o.arg[i] = arg;
+  o.vec_off[i] = voff;
+  o.vec_count[i] = vc;
+  o.rel_zxid[i] = rel;
+}
+
+static inline unsigned nblk(int64_t n) {
+  return (unsigned)((n + DEC_T - 1) / DEC_T);
+}
+
+}  // namespace zk
+
+extern "C" {
+
+int zk_decode_replies(const uint8_t* buf, const int64_t* foff,
+                      const int32_t* flen, const int64_t* n_dev, int64_t ncap,
+                      const int64_t* xid_tab, int64_t xid_mask,
+                      const ZkReplyOut* o, hipStream_t st) {
+  if (ncap <= 0) return 0;
+  zk::decode_replies_k<<<zk::nblk(ncap), zk::DEC_T, 0, st>>>(
+      buf, foff, flen, n_dev, ncap, xid_tab, xid_mask, *o);
+  ZK_LAUNCH_CHECK();
+  return 0;
+}
+
+int zk_expand_strings(const uint8_t* buf, const int64_t* region,
+                      const int32_t* count, const int64_t* base, int64_t n,
+                      int64_t* soff, int32_t* slen, hipStream_t st) {
+  if (n <= 0) return 0;
+  zk::expand_strings_k<<<zk::nblk(n), zk::DEC_T, 0, st>>>(buf, region, count,
+                                                          base, n, soff, slen);
+  ZK_LAUNCH_CHECK();
+  return 0;
+}
+
+int zk_expand_acl(const uint8_t* buf, const int64_t* region,
+                  const int32_t* count, const int64_t* base, int64_t n,
+                  int32_t* perms, int64_t* s_off, int32_t* s_len,
+                  int64_t* i_off, int32_t* i_len, hipStream_t st) {
+  if (n <= 0) return 0;
+  zk::expand_acl_k<<<zk::nblk(n), zk::DEC_T, 0, st>>>(
+      buf, region, count, base, n, perms, s_off, s_len, i_off, i_len);
+  ZK_LAUNCH_CHECK();
+  return 0;
+}
+
+int zk_decode_requests(const uint8_t* buf, const int64_t* foff,
+                       const int32_t* flen, const int64_t* n_dev,
+                       int64_t ncap, const ZkReqOut* o, hipStream_t st) {
+  if (ncap <= 0) return 0;
+  zk::decode_requests_k<<<zk::nblk(ncap), zk::DEC_T, 0, st>>>(
+      buf, foff, flen, n_dev, ncap, *o);
+  ZK_LAUNCH_CHECK();
+  return 0;
+}
+
+}  // extern "C"

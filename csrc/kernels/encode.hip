@@ -1,0 +1,313 @@
+// Batched Jute encoders (client requests K10, SET_WATCHES K11, server replies
+// K13).  Reference: lib/zk-buffer.js:97-273 (requests), jute-buffer.js:107-189
+// (primitives, length prefix), zk-streams.js:121-148 (framing + xid map).
+//
+// Shape: one thread per record in three phases — framed size, device-wide
+// exclusive scan (scan.hip), then write at the scanned offset.  Consecutive
+// records are adjacent in the output, so a wave's stores cover a contiguous
+// span that the L2 merges into full lines.  The write pass also records
+// xid -> opcode in the connection's HBM table (the reply decoder needs it:
+// replies are not self-describing, zk-buffer.js:288-291).
+#include "zk_common.h"
+#include "zk_batch.h"
+
+extern "C" int zk_scan_excl_i64(const int64_t*, int64_t*, int64_t, int64_t*,
+                                int64_t*, hipStream_t);
+
+namespace zk {
+
+constexpr int ENC_T = 256;
+
+ZK_DEV int64_t req_body_size(const ZkReqBatch& b, int64_t i, bool* ok) {
+  const int32_t op = b.opcode[i];
+  const int64_t pl = b.path_len ? max(b.path_len[i], 0) : 0;
+  *ok = true;
+  switch (op) {
+    case OP_GET_DATA: case OP_EXISTS: case OP_GET_CHILDREN:
+    case OP_GET_CHILDREN2:
+      return 8 + 4 + pl + 1;
+    case OP_CREATE: {
+      const int64_t dl = max(b.data_len[i], 0);
+      const int64_t al = b.acl_len[b.acl_id[i]];
+      return 8 + 4 + pl + 4 + dl + al + 4;
+    }
+    case OP_DELETE:
+      return 8 + 4 + pl + 4;
+    case OP_SET_DATA: {
+      const int64_t dl = max(b.data_len[i], 0);
+      return 8 + 4 + pl + 4 + dl + 4;
+    }
+    case OP_GET_ACL: case OP_SYNC:
+      return 8 + 4 + pl;
+    case OP_PING: case OP_CLOSE_SESSION:
+      return 8;
+    default:
+      *ok = false;
+      return 0;
+  }
+}
+
+__global__ __launch_bounds__(ENC_T) void req_sizes(ZkReqBatch b, int64_t n,
+                                                  int64_t* __restrict__ sizes,
+                                                  int32_t* __restrict__ err) {
+  const int64_t i = (int64_t)blockIdx.x * ENC_T + threadIdx.x;
+  if (i >= n) return;
+  bool ok;
+  const int64_t s = req_body_size(b, i, &ok);
+  sizes[i] = ok ? 4 + s : 0;
+  if (!ok) atomicOr(err, 1);
+}
+
+__global__ __launch_bounds__(ENC_T) void req_write(
+    ZkReqBatch b, int64_t n, const int64_t* __restrict__ off,
+    const int64_t* __restrict__ total, uint8_t* __restrict__ out, int64_t cap,
+    int64_t* __restrict__ xid_tab, int64_t xid_mask, int32_t* __restrict__ err) {
+  const int64_t i = (int64_t)blockIdx.x * ENC_T + threadIdx.x;
+  if (i >= n) return;
+  if (*total > cap) {                       // capacity guard (whole batch)
+    if (i == 0) atomicOr(err, 2);
+    return;
+  }
+  bool ok;
+  const int64_t body = req_body_size(b, i, &ok);
+  if (!ok) return;
+  uint8_t* o = out + off[i];
+  const int32_t op = b.opcode[i];
+  const int32_t xid = b.xid[i];
+  st_be32(o, (int32_t)body);
+  st_be32(o + 4, xid);
+  st_be32(o + 8, op);
+  o += 12;
+  if (op == OP_PING || op == OP_CLOSE_SESSION) {
+    // header only
+  } else {
+    const int32_t pl = b.path_len[i];
+    o = put_buffer(o, b.path_arena + b.path_off[i], pl);
+    switch (op) {
+      case OP_GET_DATA: case OP_EXISTS: case OP_GET_CHILDREN:
+      case OP_GET_CHILDREN2:
+        *o = b.arg[i] ? 1 : 0;
+        break;
+      case OP_CREATE: {
+        o = put_buffer(o, b.data_arena + b.data_off[i], b.data_len[i]);
+        const int32_t a = b.acl_id[i];
+        copy_bytes(o, b.acl_arena + b.acl_off[a], b.acl_len[a]);
+        o += b.acl_len[a];
+        st_be32(o, b.arg[i]);
+        break;
+      }
+      case OP_DELETE:
+        st_be32(o, b.arg[i]);
+        break;
+      case OP_SET_DATA:
+        o = put_buffer(o, b.data_arena + b.data_off[i], b.data_len[i]);
+        st_be32(o, b.arg[i]);
+        break;
+      default:
+        break;
+    }
+  }
+  if (xid_tab != nullptr && xid >= 0)
+    xid_tab[xid & xid_mask] = ((int64_t)xid << 32) | (uint32_t)op;
+}
+
+// ---------------------------------------------------------------- K11
+// SET_WATCHES: relZxid + three string vectors (data, exist, child), one
+// frame.  Paths are given as (off,len) lists; kind[i] in {0,1,2}; the host
+// passes them grouped by kind (counts c0,c1,c2) so the vector order is
+// implicit.  Each thread writes one path at its scanned offset.
+__global__ __launch_bounds__(ENC_T) void sw_sizes(const int32_t* __restrict__ plen,
+                                                 int64_t n,
+                                                 int64_t* __restrict__ sizes) {
+  const int64_t i = (int64_t)blockIdx.x * ENC_T + threadIdx.x;
+  if (i < n) sizes[i] = 4 + max(plen[i], 0);
+}
+
+__global__ __launch_bounds__(ENC_T) void sw_write(
+    const int64_t* __restrict__ poff, const int32_t* __restrict__ plen,
+    const uint8_t* __restrict__ arena, int64_t n, int64_t c0, int64_t c1,
+    const int64_t* __restrict__ off, const int64_t* __restrict__ total,
+    int64_t rel_zxid, uint8_t* __restrict__ out, int64_t cap,
+    int32_t* __restrict__ err) {
+  const int64_t i = (int64_t)blockIdx.x * ENC_T + threadIdx.x;
+  const int64_t strings = *total;
+  // layout: len | xid | op | relZxid | c0 | v0.. | c1 | v1.. | c2 | v2..
+  const int64_t frame = 4 + 8 + 8 + 12 + strings;
+  if (frame > cap) {
+    if (i == 0) atomicOr(err, 2);
+    return;
+  }
+  if (i == 0) {
+    st_be32(out, (int32_t)(frame - 4));
+    st_be32(out + 4, XID_SET_WATCHES);
+    st_be32(out + 8, OP_SET_WATCHES);
+    st_be64(out + 12, rel_zxid);
+  }
+  const int64_t c2 = n - c0 - c1;
+  // vector-count words sit before each group
+  if (i == 0) {
+    int64_t s1 = (c0 > 0) ? off[c0 - 1] + 4 + max(plen[c0 - 1], 0) : 0;
+    int64_t s2 = (c1 > 0) ? off[c0 + c1 - 1] + 4 + max(plen[c0 + c1 - 1], 0)
+                          : s1;
+    st_be32(out + 20, (int32_t)c0);
+    st_be32(out + 24 + s1, (int32_t)c1);
+    st_be32(out + 28 + s2, (int32_t)c2);
+  }
+  if (i >= n) return;
+  const int64_t g = (i < c0) ? 0 : (i < c0 + c1 ? 1 : 2);
+  uint8_t* o = out + 24 + 4 * g + off[i];
+  put_buffer(o, arena + poff[i], plen[i]);
+}
+
+// ---------------------------------------------------------------- K13
+// Server-mode reply encode (absent from the reference, zk-streams.js:140).
+ZK_DEV int64_t resp_body_size(const ZkRespBatch& r, const ZkNodeStore& s,
+                              int64_t i) {
+  int64_t sz = 16;                              // xid, zxid, err
+  if (r.err[i] != ERR_OK) return sz;
+  switch (r.opcode[i]) {
+    case OP_GET_DATA: {
+      const int64_t nd = r.node[i];
+      return sz + 4 + max(s.data_len[nd], 0) + STAT_BYTES;
+    }
+    case OP_EXISTS: case OP_SET_DATA:
+      return sz + STAT_BYTES;
+    case OP_CREATE:
+      return sz + 4 + max(r.path_len[i], 0);
+    case OP_NOTIFICATION:
+      return sz + 8 + 4 + max(r.path_len[i], 0);
+    default:
+      return sz;                                // header-only replies
+  }
+}
+
+ZK_DEV uint8_t* put_stat(uint8_t* o, const ZkNodeStore& s, int64_t nd) {
+  const int64_t c = s.cap;
+  st_be64(o + 0, s.stat64[0 * c + nd]);   // czxid
+  st_be64(o + 8, s.stat64[1 * c + nd]);   // mzxid
+  st_be64(o + 16, s.stat64[2 * c + nd]);  // ctime
+  st_be64(o + 24, s.stat64[3 * c + nd]);  // mtime
+  st_be32(o + 32, s.stat32[0 * c + nd]);  // version
+  st_be32(o + 36, s.stat32[1 * c + nd]);  // cversion
+  st_be32(o + 40, s.stat32[2 * c + nd]);  // aversion
+  st_be64(o + 44, s.stat64[4 * c + nd]);  // ephemeralOwner
+  st_be32(o + 52, s.stat32[3 * c + nd]);  // dataLength
+  st_be32(o + 56, s.stat32[4 * c + nd]);  // numChildren
+  st_be64(o + 60, s.stat64[5 * c + nd]);  // pzxid
+  return o + STAT_BYTES;
+}
+
+__global__ __launch_bounds__(ENC_T) void resp_sizes(ZkRespBatch r,
+                                                   ZkNodeStore s,
+                                                   const int64_t* __restrict__ n_dev,
+                                                   int64_t ncap,
+                                                   int64_t* __restrict__ sizes) {
+  const int64_t i = (int64_t)blockIdx.x * ENC_T + threadIdx.x;
+  if (i >= ncap) return;
+  sizes[i] = (i < *n_dev) ? 4 + resp_body_size(r, s, i) : 0;
+}
+
+__global__ __launch_bounds__(ENC_T) void resp_write(
+    ZkRespBatch r, ZkNodeStore s, const int64_t* __restrict__ n_dev,
+    int64_t ncap, const int64_t* __restrict__ off,
+    const int64_t* __restrict__ total, uint8_t* __restrict__ out, int64_t cap,
+    int32_t* __restrict__ err) {
+  const int64_t i = (int64_t)blockIdx.x * ENC_T + threadIdx.x;
+  if (i >= ncap || i >= *n_dev) return;
+  if (*total > cap) {
+    if (i == 0) atomicOr(err, 2);
+    return;
+  }
+  const int64_t body = resp_body_size(r, s, i);
+  uint8_t* o = out + off[i];
+  st_be32(o, (int32_t)body);
+  st_be32(o + 4, r.xid[i]);
+  st_be64(o + 8, r.zxid[i]);
+  st_be32(o + 16, r.err[i]);
+  o += 20;
+  if (r.err[i] != ERR_OK) return;
+  switch (r.opcode[i]) {
+    case OP_GET_DATA: {
+      const int64_t nd = r.node[i];
+      o = put_buffer(o, s.data_arena + s.data_off[nd], s.data_len[nd]);
+      put_stat(o, s, nd);
+      break;
+    }
+    case OP_EXISTS: case OP_SET_DATA:
+      put_stat(o, s, r.node[i]);
+      break;
+    case OP_CREATE:
+      put_buffer(o, r.path_arena + r.path_off[i], r.path_len[i]);
+      break;
+    case OP_NOTIFICATION:
+      st_be32(o, r.aux[i]);
+      st_be32(o + 4, 3 /* SYNC_CONNECTED */);
+      put_buffer(o + 8, r.path_arena + r.path_off[i], r.path_len[i]);
+      break;
+    default:
+      break;
+  }
+}
+
+static inline unsigned nblk(int64_t n) {
+  return (unsigned)((n + ENC_T - 1) / ENC_T);
+}
+
+}  // namespace zk
+
+extern "C" {
+
+int zk_encode_requests(const ZkReqBatch* b, int64_t n, int64_t* sizes,
+                       int64_t* rec_off, int64_t* total, int64_t* scan_ws,
+                       uint8_t* out, int64_t out_cap, int64_t* xid_tab,
+                       int64_t xid_mask, int32_t* err, hipStream_t st) {
+  if (n <= 0) return hipMemsetAsync(total, 0, 8, st);
+  zk::req_sizes<<<zk::nblk(n), zk::ENC_T, 0, st>>>(*b, n, sizes, err);
+  ZK_LAUNCH_CHECK();
+  int rc = zk_scan_excl_i64(sizes, rec_off, n, total, scan_ws, st);
+  if (rc) return rc;
+  zk::req_write<<<zk::nblk(n), zk::ENC_T, 0, st>>>(
+      *b, n, rec_off, total, out, out_cap, xid_tab, xid_mask, err);
+  ZK_LAUNCH_CHECK();
+  return 0;
+}
+
+// Returns the frame length through *frame_len (device int64): 4 + body.
+int zk_encode_set_watches(const int64_t* poff, const int32_t* plen,
+                          const uint8_t* arena, int64_t n, int64_t c0,
+                          int64_t c1, int64_t rel_zxid, int64_t* sizes,
+                          int64_t* off, int64_t* total, int64_t* scan_ws,
+                          uint8_t* out, int64_t out_cap, int32_t* err,
+                          hipStream_t st) {
+  if (n > 0) {
+    zk::sw_sizes<<<zk::nblk(n), zk::ENC_T, 0, st>>>(plen, n, sizes);
+    ZK_LAUNCH_CHECK();
+    int rc = zk_scan_excl_i64(sizes, off, n, total, scan_ws, st);
+    if (rc) return rc;
+  } else {
+    hipMemsetAsync(total, 0, 8, st);
+  }
+  zk::sw_write<<<zk::nblk(n > 0 ? n : 1), zk::ENC_T, 0, st>>>(
+      poff, plen, arena, n, c0, c1, off, total, rel_zxid, out, out_cap, err);
+  ZK_LAUNCH_CHECK();
+  return 0;
+}
+
+int zk_encode_responses(const ZkRespBatch* r, const ZkNodeStore* s,
+                        const int64_t* n_dev, int64_t ncap, int64_t* sizes,
+                        int64_t* rec_off, int64_t* total, int64_t* scan_ws,
+                        uint8_t* out, int64_t out_cap, int32_t* err,
+                        hipStream_t st) {
+  if (ncap <= 0) return hipMemsetAsync(total, 0, 8, st);
+  zk::resp_sizes<<<zk::nblk(ncap), zk::ENC_T, 0, st>>>(*r, *s, n_dev, ncap,
+                                                        sizes);
+  ZK_LAUNCH_CHECK();
+  int rc = zk_scan_excl_i64(sizes, rec_off, ncap, total, scan_ws, st);
+  if (rc) return rc;
+  zk::resp_write<<<zk::nblk(ncap), zk::ENC_T, 0, st>>>(
+      *r, *s, n_dev, ncap, rec_off, total, out, out_cap, err);
+  ZK_LAUNCH_CHECK();
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,436 @@
+// K1 — parallel length-prefixed frame scan.
+//
+// Reference: ZKDecodeStream._transform (lib/zk-streams.js:39-65) walks the
+// i32-BE length chain one frame at a time and memmoves the remainder per
+// packet (O(bytes x packets)).  The chain is inherently
+// sequential; we make it parallel without speculation errors:
+//
+//  A  fs_exits   one workgroup per 16 KiB tile: stage the tile in LDS, build
+//                next(p) = p + 4 + be32(p) for EVERY byte position, and
+//                pointer-jump (in place, racy but monotone) until each
+//                position maps to the first chain position outside the tile
+//                or to a terminal (bad length / partial frame / end).  Keep
+//                the result for the first W positions of the tile (the only
+//                place a chain can enter when frames are <= W bytes) as a
+//                compact uint16 table.
+//  B  fs_compose hierarchical function composition: a level-(l+1) unit is 16
+//                level-l units; for each window entry point, walk the 16
+//                sub-unit functions.  Log-depth, O(W) work per unit.
+//  C  fs_top/fs_down  serial walk over the (few) top units from the stream
+//                start, then push the exact entry position down to every tile.
+//  D  fs_mark    per tile, re-stage and mark the chain from its entry with
+//                doubling (double-buffered, so round r marks distances
+//                [2^r, 2^(r+1)) — complete after log2(frames) rounds); emit a
+//                frame-start bitmap and a count.
+//  E  scan of counts (scan.hip) + fs_write: bitmap -> (body_off, len) table.
+//
+// Frames longer than W (2 KiB) fall back to walking the byte chain in global
+// memory for the tile they land in; results stay exact.  BAD_LENGTH is
+// reported at the exact frame (result[1] = its offset, result[2] = 1), the
+// consumed prefix ends at the last complete frame, and a partial trailing
+// frame is left for the next call (carry), like the reference's buffer.
+#include "zk_common.h"
+
+extern "C" int zk_scan_excl_i64(const int64_t*, int64_t*, int64_t, int64_t*,
+                                int64_t*, hipStream_t);
+extern "C" int64_t zk_scan_workspace(int64_t);
+
+namespace zk {
+
+constexpr int64_t FS_S = 16384;          // tile bytes
+constexpr int64_t FS_W = 2048;           // window (entry points) per tile
+constexpr int FS_G = 16;                 // fan-in per composition level
+constexpr int FS_MAXL = 6;               // levels (16 KiB * 16^5 = 16 GiB)
+constexpr int FS_TOPMAX = 256;           // serial walk bound at the top
+constexpr int FS_T = 1024;               // threads per tile workgroup
+constexpr int64_t TERM = (int64_t)1 << 62;
+constexpr int64_t NONE = -1;
+constexpr uint16_t F0_TERM = 0x8000;     // | rel position (< 16384)
+constexpr uint16_t F0_ESC = 0xFFFF;      // exit beyond next tile: walk
+
+struct FsCtx {
+  const uint8_t* buf;
+  int64_t n;
+  int64_t maxp;
+  int levels;                      // number of levels (>= 1)
+  int64_t usize[FS_MAXL];          // unit size in bytes per level
+  int64_t units[FS_MAXL];          // unit count per level
+  const uint16_t* f0;              // [units0][W]
+  int64_t* fl[FS_MAXL];            // [units_l][W] for l >= 1 (absolute)
+  int64_t* ent[FS_MAXL];           // entry position per unit (or NONE)
+};
+
+ZK_DEV bool is_term(int64_t v) { return (v & TERM) != 0; }
+ZK_DEV int64_t pos_of(int64_t v) { return v & ~TERM; }
+
+// One step of the chain in global memory.
+ZK_DEV int64_t next_global(const FsCtx& c, int64_t P) {
+  if (P >= c.n) return TERM | c.n;
+  if (P + 4 > c.n) return TERM | P;
+  const int32_t len = ld_be32(c.buf + P);
+  if (len < 0 || (int64_t)len > c.maxp) return TERM | P;
+  const int64_t nx = P + 4 + len;
+  if (nx > c.n) return TERM | P;
+  return nx >= c.n ? (TERM | c.n) : nx;
+}
+
+ZK_DEV int64_t walk_until(const FsCtx& c, int64_t P, int64_t end) {
+  while (!is_term(P) && P < end) P = next_global(c, P);
+  return P;
+}
+
+template <int L>
+ZK_DEV int64_t apply_unit(const FsCtx& c, int64_t u, int64_t P) {
+  if (is_term(P)) return P;
+  if (P >= c.n) return TERM | c.n;
+  const int64_t us = u * c.usize[L];
+  const int64_t ue = min(us + c.usize[L], c.n);
+  const int64_t off = P - us;
+  if constexpr (L == 0) {
+    if (off < FS_W) {
+      const uint16_t v = c.f0[u * FS_W + off];
+      if (v == F0_ESC) return walk_until(c, P, ue);
+      if (v & F0_TERM) return TERM | (us + (v & 0x7FFF));
+      const int64_t x = us + FS_S + v;
+      return x >= c.n ? (TERM | c.n) : x;
+    }
+    return walk_until(c, P, ue);
+  } else {
+    if (off < FS_W) return c.fl[L][u * FS_W + off];
+    while (!is_term(P) && P < ue) {
+      const int64_t sub = P / c.usize[L - 1];
+      P = apply_unit<L - 1>(c, sub, P);
+    }
+    return P;
+  }
+}
+
+ZK_DEV int64_t apply_level(const FsCtx& c, int l, int64_t u, int64_t P) {
+  switch (l) {
+    case 0: return apply_unit<0>(c, u, P);
+    case 1: return apply_unit<1>(c, u, P);
+    case 2: return apply_unit<2>(c, u, P);
+    case 3: return apply_unit<3>(c, u, P);
+    case 4: return apply_unit<4>(c, u, P);
+    default: return apply_unit<5>(c, u, P);
+  }
+}
+
+// Stage tile bytes [ts, ts+S+4) into LDS (zero beyond n).
+ZK_DEV void stage_tile(const uint8_t* buf, int64_t n, int64_t ts, uint8_t* sb) {
+  const int64_t lim = min(FS_S + 4, n - ts);
+  for (int64_t k = (int64_t)threadIdx.x * 16; k < FS_S + 16;
+       k += (int64_t)blockDim.x * 16) {
+    if (k + 16 <= lim) {
+      uint4 v; __builtin_memcpy(&v, buf + ts + k, 16);
+      *(uint4*)(sb + k) = v;
+    } else {
+      for (int j = 0; j < 16; ++j)
+        sb[k + j] = (k + j < lim) ? buf[ts + k + j] : 0;
+    }
+  }
+}
+
+// next() of every tile position relative to the tile (>= S: leaves tile;
+// == p: terminal).
+ZK_DEV int32_t next_rel(const uint8_t* sb, int64_t ts, int64_t n, int64_t maxp,
+                        int32_t p) {
+  const int64_t P = ts + p;
+  if (P + 4 > n) return p;
+  const uint32_t raw = ((uint32_t)sb[p] << 24) | ((uint32_t)sb[p + 1] << 16) |
+                       ((uint32_t)sb[p + 2] << 8) | (uint32_t)sb[p + 3];
+  const int32_t len = (int32_t)raw;
+  if (len < 0 || (int64_t)len > maxp) return p;
+  if (P + 4 + len > n) return p;
+  const int64_t nx = (int64_t)p + 4 + len;
+  return nx > 0x7FFFFFF0LL ? 0x7FFFFFF0 : (int32_t)nx;
+}
+
+__global__ __launch_bounds__(FS_T) void fs_exits(const uint8_t* __restrict__ buf,
+                                                int64_t n, int64_t maxp,
+                                                uint16_t* __restrict__ f0) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  int32_t* J = (int32_t*)smem;                       // [S]
+  uint8_t* sb = smem + FS_S * 4;                     // [S + 16]
+  const int64_t t = blockIdx.x;
+  const int64_t ts = t * FS_S;
+  stage_tile(buf, n, ts, sb);
+  __syncthreads();
+  for (int32_t p = threadIdx.x; p < FS_S; p += FS_T)
+    J[p] = next_rel(sb, ts, n, maxp, p);
+  __syncthreads();
+  // In-place pointer jumping to the first position >= S (or a terminal).
+  for (int it = 0; it < 32; ++it) {
+    int changed = 0;
+    for (int32_t p = threadIdx.x; p < FS_S; p += FS_T) {
+      const int32_t j = J[p];
+      if (j < FS_S) {
+        const int32_t jj = J[j];
+        if (jj != j) { J[p] = jj; changed = 1; }
+      }
+    }
+    if (!__syncthreads_or(changed)) break;
+  }
+  for (int32_t p = threadIdx.x; p < FS_W; p += FS_T) {
+    const int32_t j = J[p];
+    uint16_t v;
+    if (j < FS_S) v = F0_TERM | (uint16_t)j;
+    else if (j - FS_S < 0x4000) v = (uint16_t)(j - FS_S);
+    else v = F0_ESC;
+    f0[t * FS_W + p] = v;
+  }
+}
+
+// Level l -> l+1: fl[l+1][u][p] = position after leaving unit u from us+p.
+__global__ __launch_bounds__(FS_T) void fs_compose(FsCtx c, int l) {
+  const int64_t u = blockIdx.x;
+  const int64_t us = u * c.usize[l + 1];
+  const int64_t ue = min(us + c.usize[l + 1], c.n);
+  for (int64_t p = threadIdx.x; p < FS_W; p += blockDim.x) {
+    int64_t P = us + p;
+    if (P >= c.n) P = TERM | c.n;
+    while (!is_term(P) && P < ue) {
+      const int64_t sub = P / c.usize[l];
+      P = apply_level(c, l, sub, P);
+    }
+    c.fl[l + 1][u * FS_W + p] = P;
+  }
+}
+
+// Serial walk over the top level; writes entries and the final status.
+__global__ void fs_top(FsCtx c, int64_t* __restrict__ result) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const int L = c.levels - 1;
+  int64_t P = c.n > 0 ? 0 : (TERM | 0);
+  for (int64_t u = 0; u < c.units[L]; ++u) {
+    const int64_t us = u * c.usize[L];
+    const int64_t ue = min(us + c.usize[L], c.n);
+    if (!is_term(P) && P >= us && P < ue) {
+      c.ent[L][u] = P;
+      P = apply_level(c, L, u, P);
+    } else {
+      c.ent[L][u] = NONE;
+    }
+  }
+  const int64_t q = pos_of(P);
+  result[1] = q;                       // consumed / stop position
+  int64_t bad = 0;
+  if (q + 4 <= c.n) {
+    const int32_t len = ld_be32(c.buf + q);
+    if (len < 0 || (int64_t)len > c.maxp) bad = 1;
+  }
+  result[2] = bad;
+}
+
+// Push entries from level l+1 down to level l (one thread per parent).
+__global__ void fs_down(FsCtx c, int l) {
+  const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= c.units[l + 1]) return;
+  int64_t P = c.ent[l + 1][u];
+  const int64_t s0 = u * FS_G;
+  const int64_t s1 = min(s0 + FS_G, c.units[l]);
+  for (int64_t s = s0; s < s1; ++s) {
+    const int64_t ss = s * c.usize[l];
+    const int64_t se = min(ss + c.usize[l], c.n);
+    if (P != NONE && !is_term(P) && P >= ss && P < se) {
+      c.ent[l][s] = P;
+      P = apply_level(c, l, s, P);
+    } else {
+      c.ent[l][s] = NONE;
+    }
+  }
+}
+
+// Mark the chain inside each tile from its entry; bitmap of frame starts.
+__global__ __launch_bounds__(FS_T) void fs_mark(const uint8_t* __restrict__ buf,
+                                               int64_t n, int64_t maxp,
+                                               const int64_t* __restrict__ ent,
+                                               uint32_t* __restrict__ bits,
+                                               int64_t* __restrict__ counts) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint16_t* A = (uint16_t*)smem;                       // [S]
+  uint16_t* B = A + FS_S;                              // [S]
+  uint8_t* mk = smem + FS_S * 4;                       // [S]
+  uint8_t* sb = mk + FS_S;                             // [S + 16]
+  const int64_t t = blockIdx.x;
+  const int64_t ts = t * FS_S;
+  const int64_t e = ent[t];
+  uint32_t* tb = bits + t * (FS_S / 32);
+  if (e == NONE) {
+    for (int k = threadIdx.x; k < FS_S / 32; k += FS_T) tb[k] = 0;
+    if (threadIdx.x == 0) counts[t] = 0;
+    return;
+  }
+  stage_tile(buf, n, ts, sb);
+  __syncthreads();
+  // A[p] in [0,S]: next within tile, S = leaves tile; p itself = terminal.
+  for (int32_t p = threadIdx.x; p < FS_S; p += FS_T) {
+    const int32_t j = next_rel(sb, ts, n, maxp, p);
+    A[p] = (uint16_t)(j >= FS_S ? FS_S : j);
+    mk[p] = 0;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) mk[e - ts] = 1;
+  __syncthreads();
+  for (int r = 0; r < 16; ++r) {
+    int added = 0;
+    for (int32_t p = threadIdx.x; p < FS_S; p += FS_T) {
+      if (mk[p]) {
+        const int32_t j = A[p];
+        if (j < FS_S && j != p && !mk[j]) { mk[j] = 1; added = 1; }
+      }
+    }
+    if (!__syncthreads_or(added)) break;
+    for (int32_t p = threadIdx.x; p < FS_S; p += FS_T) {
+      const int32_t j = A[p];
+      B[p] = (j < FS_S && j != p) ? A[j] : (uint16_t)j;
+    }
+    __syncthreads();
+    uint16_t* tmp = A; A = B; B = tmp;
+  }
+  // A frame starts at every marked position that is not a terminal.
+  int64_t cnt = 0;
+  for (int32_t k = threadIdx.x; k < FS_S / 32; k += FS_T) {
+    uint32_t w = 0;
+    for (int b = 0; b < 32; ++b) {
+      const int32_t p = k * 32 + b;
+      if (mk[p] && next_rel(sb, ts, n, maxp, p) != p) w |= 1u << b;
+    }
+    tb[k] = w;
+    cnt += __popc(w);
+  }
+  int64_t* red = (int64_t*)(smem + FS_S * 6 + 16);   // dynamic LDS only
+  int64_t tot;
+  block_excl_scan(cnt, red, &tot);
+  if (threadIdx.x == 0) counts[t] = tot;
+}
+
+__global__ __launch_bounds__(256) void fs_write(const uint8_t* __restrict__ buf,
+                                               const uint32_t* __restrict__ bits,
+                                               const int64_t* __restrict__ base,
+                                               int64_t* __restrict__ foff,
+                                               int32_t* __restrict__ flen,
+                                               int64_t cap,
+                                               int64_t* __restrict__ result) {
+  __shared__ int64_t red[256 / 64 + 1];
+  const int64_t t = blockIdx.x;
+  const int64_t ts = t * FS_S;
+  const uint32_t* tb = bits + t * (FS_S / 32);
+  // 512 words per tile, 2 per thread
+  const int k0 = threadIdx.x * 2;
+  const uint32_t w0 = tb[k0], w1 = tb[k0 + 1];
+  int64_t tot;
+  int64_t idx = base[t] + block_excl_scan(__popc(w0) + __popc(w1), red, &tot);
+  for (int h = 0; h < 2; ++h) {
+    uint32_t w = h ? w1 : w0;
+    while (w) {
+      const int b = __ffs(w) - 1;
+      w &= w - 1;
+      const int64_t P = ts + (int64_t)(k0 + h) * 32 + b;
+      if (idx < cap) {
+        foff[idx] = P + 4;
+        flen[idx] = ld_be32(buf + P);
+      } else {
+        result[3] = 1;
+      }
+      ++idx;
+    }
+  }
+}
+
+struct FsPlan {
+  int levels;
+  int64_t units[FS_MAXL];
+  int64_t usize[FS_MAXL];
+  size_t off_f0, off_fl[FS_MAXL], off_ent[FS_MAXL], off_bits, off_cnt,
+      off_base, off_scan, total;
+};
+
+static FsPlan fs_plan(int64_t n) {
+  FsPlan p{};
+  const int64_t tiles = n > 0 ? (n + FS_S - 1) / FS_S : 1;
+  p.units[0] = tiles;
+  p.usize[0] = FS_S;
+  p.levels = 1;
+  while (p.units[p.levels - 1] > FS_TOPMAX && p.levels < FS_MAXL) {
+    const int l = p.levels;
+    p.usize[l] = p.usize[l - 1] * FS_G;
+    p.units[l] = (p.units[l - 1] + FS_G - 1) / FS_G;
+    p.levels++;
+  }
+  size_t o = 0;
+  auto take = [&](size_t bytes) { size_t r = o; o += (bytes + 255) & ~(size_t)255; return r; };
+  p.off_f0 = take((size_t)tiles * FS_W * 2);
+  for (int l = 1; l < p.levels; ++l)
+    p.off_fl[l] = take((size_t)p.units[l] * FS_W * 8);
+  for (int l = 0; l < p.levels; ++l) p.off_ent[l] = take((size_t)p.units[l] * 8);
+  p.off_bits = take((size_t)tiles * (FS_S / 32) * 4);
+  p.off_cnt = take((size_t)tiles * 8);
+  p.off_base = take((size_t)tiles * 8);
+  p.off_scan = take((size_t)zk_scan_workspace(tiles) * 8);
+  p.total = o;
+  return p;
+}
+
+}  // namespace zk
+
+extern "C" {
+
+int64_t zk_frame_scan_workspace(int64_t n) { return (int64_t)zk::fs_plan(n).total; }
+
+// result (device int64[4]): [0] frames written, [1] stop offset (consumed
+// bytes; start of the carry or of the bad frame), [2] 1 if the stop is a
+// BAD_LENGTH frame, [3] 1 if the frame table overflowed `cap`.
+int zk_frame_scan(const uint8_t* buf, int64_t n, int64_t maxp, uint8_t* ws,
+                  int64_t ws_bytes, int64_t* foff, int32_t* flen, int64_t cap,
+                  int64_t* result, hipStream_t st) {
+  using namespace zk;
+  FsPlan p = fs_plan(n);
+  if ((int64_t)p.total > ws_bytes) return -1;
+  hipMemsetAsync(result, 0, 4 * sizeof(int64_t), st);
+  if (n <= 0) return 0;
+  FsCtx c{};
+  c.buf = buf;
+  c.n = n;
+  c.maxp = maxp;
+  c.levels = p.levels;
+  for (int l = 0; l < p.levels; ++l) {
+    c.units[l] = p.units[l];
+    c.usize[l] = p.usize[l];
+    c.ent[l] = (int64_t*)(ws + p.off_ent[l]);
+    if (l > 0) c.fl[l] = (int64_t*)(ws + p.off_fl[l]);
+  }
+  c.f0 = (const uint16_t*)(ws + p.off_f0);
+  const int64_t tiles = p.units[0];
+  const size_t lds_a = FS_S * 4 + FS_S + 16;
+  fs_exits<<<(unsigned)tiles, FS_T, lds_a, st>>>(buf, n, maxp,
+                                                (uint16_t*)(ws + p.off_f0));
+  ZK_LAUNCH_CHECK();
+  for (int l = 0; l + 1 < p.levels; ++l) {
+    fs_compose<<<(unsigned)p.units[l + 1], FS_T, 0, st>>>(c, l);
+    ZK_LAUNCH_CHECK();
+  }
+  fs_top<<<1, 64, 0, st>>>(c, result);
+  ZK_LAUNCH_CHECK();
+  for (int l = p.levels - 2; l >= 0; --l) {
+    const int64_t np = p.units[l + 1];
+    fs_down<<<(unsigned)((np + 255) / 256), 256, 0, st>>>(c, l);
+    ZK_LAUNCH_CHECK();
+  }
+  const size_t lds_d = FS_S * 6 + 16 + (FS_T / 64 + 1) * 8;
+  uint32_t* bits = (uint32_t*)(ws + p.off_bits);
+  int64_t* cnt = (int64_t*)(ws + p.off_cnt);
+  int64_t* base = (int64_t*)(ws + p.off_base);
+  fs_mark<<<(unsigned)tiles, FS_T, lds_d, st>>>(buf, n, maxp, c.ent[0], bits,
+                                               cnt);
+  ZK_LAUNCH_CHECK();
+  int rc = zk_scan_excl_i64(cnt, base, tiles, result + 0,
+                            (int64_t*)(ws + p.off_scan), st);
+  if (rc) return rc;
+  fs_write<<<(unsigned)tiles, 256, 0, st>>>(buf, bits, base, foff, flen, cap,
+                                           result);
+  ZK_LAUNCH_CHECK();
+  return 0;
+}
+
+}  // extern "C"

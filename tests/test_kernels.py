@@ -1,0 +1,242 @@
+"""Numerics of the HIP batch codec (K1-K13) against the pure-Python Jute
+oracle (zkmi/jute.py), which itself is pinned to the reference's golden
+vectors in test_proto.py.  All tests here need an MI355X."""
+
+import numpy as np
+import pytest
+import torch
+
+from zkmi import consts, jute
+from zkmi.utils import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev_bytes(b, dev):
+    a = np.frombuffer(bytes(b) if b else b'\0', np.uint8).copy()
+    return torch.from_numpy(a).to(dev)
+
+
+def _norm(pkt):
+    out = dict(pkt)
+    for k in ('stat',):
+        if k in out and out[k] is not None:
+            out[k] = out[k].as_tuple()
+    return out
+
+
+def test_encode_requests_matches_oracle(gpu):
+    from zkmi.ops import batch as B
+    r = synth.rng(1)
+    pkts = [synth.rand_request(r, xid) for xid in range(2000)]
+    rb = B.pack_requests(pkts, gpu)
+    xt = B.XidTable(bits=12, device=gpu)
+    out, rec_off, total, err = B.encode_requests(rb, xt)
+    torch.cuda.synchronize()
+    assert err.item() == 0
+    want = b''.join(jute.frame(jute.encode_request(p)) for p in pkts)
+    got = bytes(out[:total.item()].cpu().numpy().tobytes())
+    assert got == want
+    # xid table records the opcode of every request
+    tab = xt.tab.cpu().tolist()
+    for p in pkts[-100:]:
+        e = tab[p['xid'] & xt.mask]
+        assert (e >> 32) == p['xid']
+        assert (e & 0xffffffff) - (1 << 32 if e & 0x80000000 else 0) == \
+            consts.OP_CODES[p['opcode']]
+
+
+def test_encode_set_watches_matches_oracle(gpu):
+    from zkmi.ops import batch as B
+    ev = {'dataChanged': ['/d', '/d2/x'], 'createdOrDestroyed': ['/e'],
+          'childrenChanged': ['/c', '/', '/zz']}
+    got = B.encode_set_watches(0x517, ev['dataChanged'],
+                               ev['createdOrDestroyed'],
+                               ev['childrenChanged'], gpu)
+    want = jute.frame(jute.encode_request(
+        {'xid': -8, 'opcode': 'SET_WATCHES', 'relZxid': 0x517,
+         'events': ev}))
+    assert bytes(got.cpu().numpy().tobytes()) == want
+    got0 = B.encode_set_watches(5, [], [], [], gpu)
+    want0 = jute.frame(jute.encode_request(
+        {'xid': -8, 'opcode': 'SET_WATCHES', 'relZxid': 5,
+         'events': {}}))
+    assert bytes(got0.cpu().numpy().tobytes()) == want0
+
+
+def _frames_stream(r, n, maxbody):
+    parts = []
+    for _ in range(n):
+        k = r.choice([0, 1, 16, r.randint(0, maxbody)])
+        parts.append(jute.frame(bytes(r.getrandbits(8) for _ in range(k))))
+    return b''.join(parts)
+
+
+@pytest.mark.parametrize('maxbody,n', [(64, 3000), (600, 800), (5000, 120),
+                                       (40000, 12)])
+def test_frame_scan_matches_oracle(gpu, maxbody, n):
+    from zkmi.ops import batch as B
+    r = synth.rng(maxbody)
+    s = _frames_stream(r, n, maxbody)
+    # add a partial trailing frame (carry)
+    tail = jute.frame(b'x' * 50)[:-7]
+    s = s + tail
+    frames, consumed, bad = jute.scan_frames(s)
+    buf = _dev_bytes(s, gpu)
+    ft = B.frame_scan(buf, len(s))
+    res = ft.host_result()
+    assert res['frames'] == len(frames)
+    assert res['consumed'] == consumed == len(s) - len(tail)
+    assert not res['bad']
+    off = ft.off[:len(frames)].cpu().tolist()
+    ln = ft.length[:len(frames)].cpu().tolist()
+    assert list(zip(off, ln)) == frames
+
+
+def test_frame_scan_bad_length_exact(gpu):
+    from zkmi.ops import batch as B
+    r = synth.rng(7)
+    good = _frames_stream(r, 500, 300)
+    bad = b'\xff\xff\xff\xfe\x01\x02'
+    s = good + bad + _frames_stream(r, 50, 30)
+    frames, consumed, bad_at = jute.scan_frames(s)
+    assert bad_at == len(good)
+    ft = B.frame_scan(_dev_bytes(s, gpu), len(s))
+    res = ft.host_result()
+    assert res['bad'] and res['consumed'] == len(good)
+    assert res['frames'] == len(frames)
+    # too-large length
+    s2 = good + b'\x7f\x00\x00\x00' + b'\0' * 100
+    ft2 = B.frame_scan(_dev_bytes(s2, gpu), len(s2))
+    res2 = ft2.host_result()
+    assert res2['bad'] and res2['consumed'] == len(good)
+
+
+def test_frame_scan_large_multi_level(gpu):
+    """> 256 tiles forces the hierarchical composition path."""
+    from zkmi.ops import batch as B
+    r = synth.rng(3)
+    bodies = [bytes([i & 0xff]) * r.randint(16, 400) for i in range(40000)]
+    s = b''.join(jute.frame(b) for b in bodies)
+    assert len(s) > 256 * 16384
+    ft = B.frame_scan(_dev_bytes(s, gpu), len(s))
+    res = ft.host_result()
+    assert res['frames'] == len(bodies)
+    assert res['consumed'] == len(s)
+    ln = ft.length[:len(bodies)].cpu().numpy()
+    assert (ln == np.array([len(b) for b in bodies])).all()
+
+
+def test_decode_replies_matches_oracle(gpu):
+    from zkmi.ops import batch as B
+    r = synth.rng(11)
+    reps = []
+    xid_map = {}
+    for xid in range(3000):
+        if r.random() < 0.1:
+            reps.append(synth.rand_notification(r))
+            continue
+        rep = synth.rand_reply(r, xid)
+        xid_map[xid] = rep['opcode']
+        reps.append(rep)
+    reps.append({'xid': -2, 'zxid': 77, 'err': 'OK', 'opcode': 'PING'})
+    s = b''.join(jute.frame(jute.encode_response(p)) for p in reps)
+    want = [jute.decode_response(jute.encode_response(p), xid_map)
+            for p in reps]
+    buf = _dev_bytes(s, gpu)
+    xt = B.XidTable(bits=12, device=gpu)
+    # populate the xid table the way the encoder would
+    tab = xt.tab.cpu()
+    for xid, op in xid_map.items():
+        tab[xid & xt.mask] = (xid << 32) | (consts.OP_CODES[op] & 0xffffffff)
+    xt.tab.copy_(tab)
+    ft = B.frame_scan(buf, len(s))
+    rep = B.decode_replies(buf, ft, xt)
+    got = B.replies_to_packets(buf, rep)
+    assert len(got) == len(want)
+    for g, w in zip(got, want):
+        assert _norm(g) == _norm(w)
+
+
+def test_expand_children_and_acl(gpu):
+    from zkmi.ops import batch as B
+    r = synth.rng(5)
+    reps = []
+    xid_map = {}
+    for xid in range(500):
+        op = 'GET_CHILDREN2' if xid % 2 else 'GET_ACL'
+        rep = {'xid': xid, 'zxid': 1, 'err': 'OK', 'opcode': op,
+               'stat': synth.rand_stat(r)}
+        if op == 'GET_CHILDREN2':
+            rep['children'] = ['c%d' % k for k in range(xid % 7)]
+        else:
+            rep['acl'] = synth.rand_acl(r)
+            for a in rep['acl']:
+                a['perms'] = [p.upper() for p in a['perms']]
+        xid_map[xid] = op
+        reps.append(rep)
+    s = b''.join(jute.frame(jute.encode_response(p)) for p in reps)
+    buf = _dev_bytes(s, gpu)
+    xt = B.XidTable(bits=10, device=gpu)
+    tab = xt.tab.cpu()
+    for xid, op in xid_map.items():
+        tab[xid] = (xid << 32) | consts.OP_CODES[op]
+    xt.tab.copy_(tab)
+    ft = B.frame_scan(buf, len(s))
+    rb = B.decode_replies(buf, ft, xt)
+    n = len(reps)
+    ch = torch.where(rb.opcode[:n] == 12, rb.aux0[:n],
+                     torch.zeros_like(rb.aux0[:n]))
+    base, soff, slen = B.expand_strings(buf, rb.pay_off[:n], ch)
+    hb = s
+    so, sl, bs = soff.cpu().tolist(), slen.cpu().tolist(), \
+        base.cpu().tolist()
+    for i, rep in enumerate(reps):
+        if rep['opcode'] == 'GET_CHILDREN2':
+            kids = [hb[so[bs[i] + k]:so[bs[i] + k] + sl[bs[i] + k]].decode()
+                    for k in range(len(rep['children']))]
+            assert kids == rep['children']
+    ac = torch.where(rb.opcode[:n] == 6, rb.aux0[:n],
+                     torch.zeros_like(rb.aux0[:n]))
+    base, perms, s_o, s_l, i_o, i_l = B.expand_acl(buf, rb.pay_off[:n], ac)
+    pm, so, sl, io, il, bs = (x.cpu().tolist() for x in
+                              (perms, s_o, s_l, i_o, i_l, base))
+    for i, rep in enumerate(reps):
+        if rep['opcode'] == 'GET_ACL':
+            for k, a in enumerate(rep['acl']):
+                j = bs[i] + k
+                assert pm[j] == jute.perms_to_mask(a['perms'])
+                assert hb[so[j]:so[j] + sl[j]].decode() == a['id']['scheme']
+                assert hb[io[j]:io[j] + il[j]].decode() == a['id']['id']
+
+
+def test_decode_requests_matches_oracle(gpu):
+    from zkmi.ops import batch as B
+    r = synth.rng(13)
+    pkts = [synth.rand_request(r, xid) for xid in range(2000)]
+    s = b''.join(jute.frame(jute.encode_request(p)) for p in pkts)
+    buf = _dev_bytes(s, gpu)
+    ft = B.frame_scan(buf, len(s))
+    rt = B.decode_requests(buf, ft)
+    n = len(pkts)
+    cols = {k: getattr(rt, k)[:n].cpu().tolist() for k in (
+        'xid', 'opcode', 'status', 'path_off', 'path_len', 'data_off',
+        'data_len', 'arg', 'vec_count')}
+    for i, p in enumerate(pkts):
+        w = jute.decode_request(jute.encode_request(p))
+        assert cols['status'][i] == 0
+        assert cols['xid'][i] == w['xid']
+        assert cols['opcode'][i] == consts.OP_CODES[w['opcode']]
+        if 'path' in w:
+            po, pl = cols['path_off'][i], cols['path_len'][i]
+            assert s[po:po + pl].decode() == w['path']
+        if 'data' in w:
+            do, dl = cols['data_off'][i], cols['data_len'][i]
+            assert s[do:do + dl] == w['data']
+        if 'watch' in w:
+            assert cols['arg'][i] == int(w['watch'])
+        if 'version' in w:
+            assert cols['arg'][i] == w['version']
+        if w['opcode'] == 'CREATE':
+            assert cols['arg'][i] == jute.flags_to_mask(w['flags'])
+            assert cols['vec_count'][i] == len(w['acl'])

@@ -1,0 +1,100 @@
+"""Build the native parts of zkmi in-tree.
+
+* ``zkmi/ops/libzkmi_hip.so`` — the HIP/CDNA4 batch codec kernels
+  (csrc/kernels/*.hip), compiled with ``hipcc --offload-arch=gfx950``.  It
+  links libamdhip64.so.7, which resolves to the copy torch already loaded
+  (same soname), so torch and zkmi share one HIP runtime.
+* ``zkmi/_zkhost*.so`` — the C++ host codec for the interactive path
+  (csrc/host), a CPython extension (no torch headers).
+
+Usage: ``python tools/build_native.py [--hip-only|--host-only] [-j N]``.
+Objects are cached under ``build/`` by source mtime.
+"""
+
+import argparse
+import concurrent.futures as cf
+import os
+import subprocess
+import sys
+import sysconfig
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KDIR = os.path.join(ROOT, 'csrc', 'kernels')
+HDIR = os.path.join(ROOT, 'csrc', 'host')
+BDIR = os.path.join(ROOT, 'build')
+HIP_SO = os.path.join(ROOT, 'zkmi', 'ops', 'libzkmi_hip.so')
+ARCH = os.environ.get('ZKMI_OFFLOAD_ARCH', 'gfx950')
+HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
+
+
+def _run(cmd):
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                       text=True)
+    if r.returncode != 0:
+        sys.stderr.write(' '.join(cmd) + '\n' + r.stdout)
+        raise RuntimeError('command failed: %s' % cmd[0])
+    return r.stdout
+
+
+def _stale(out, deps):
+    if not os.path.exists(out):
+        return True
+    t = os.path.getmtime(out)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build_hip(jobs=4):
+    os.makedirs(BDIR, exist_ok=True)
+    srcs = sorted(f for f in os.listdir(KDIR) if f.endswith('.hip'))
+    hdrs = [os.path.join(KDIR, f) for f in os.listdir(KDIR)
+            if f.endswith('.h')]
+    flags = ['--offload-arch=' + ARCH, '-O3', '-fPIC', '-std=c++17',
+             '-Wno-unused-result', '-Wno-unused-value', '-munsafe-fp-atomics']
+    objs = []
+    todo = []
+    for s in srcs:
+        src = os.path.join(KDIR, s)
+        obj = os.path.join(BDIR, s.replace('.hip', '.o'))
+        objs.append(obj)
+        if _stale(obj, [src] + hdrs):
+            todo.append([HIPCC] + flags + ['-c', src, '-o', obj])
+    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        list(ex.map(_run, todo))
+    if todo or _stale(HIP_SO, objs):
+        _run([HIPCC, '--offload-arch=' + ARCH, '-shared', '-fPIC', '-o',
+              HIP_SO] + objs)
+    return HIP_SO
+
+
+def host_so_path():
+    suffix = sysconfig.get_config_var('EXT_SUFFIX') or '.so'
+    return os.path.join(ROOT, 'zkmi', '_zkhost' + suffix)
+
+
+def build_host():
+    src = os.path.join(HDIR, 'zk_host_codec.cpp')
+    if not os.path.exists(src):
+        return None
+    out = host_so_path()
+    deps = [src] + [os.path.join(HDIR, f) for f in os.listdir(HDIR)]
+    if _stale(out, deps):
+        inc = sysconfig.get_paths()['include']
+        _run(['g++', '-O3', '-fPIC', '-shared', '-std=c++17', '-Wall',
+              '-fno-strict-aliasing', '-I' + inc, src, '-o', out])
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--hip-only', action='store_true')
+    ap.add_argument('--host-only', action='store_true')
+    ap.add_argument('-j', type=int, default=4)
+    a = ap.parse_args()
+    if not a.host_only:
+        print(build_hip(a.j))
+    if not a.hip_only:
+        print(build_host())
+
+
+if __name__ == '__main__':
+    main()

@@ -1,0 +1,516 @@
+"""Batched GPU codec: torch-tensor API over the HIP kernels.
+
+Every function here runs on the current HIP stream and allocates its outputs
+with the torch caching allocator (cheap after warm-up).  Record counts that
+the GPU discovers (frames in a byte stream) stay on the device as int64
+scalars, so a pipeline of these calls needs no host synchronisation; call
+``.item()`` only where a host decision is needed.
+
+Kernel map: K1 :func:`frame_scan`; K2-K8
+:func:`decode_replies` (+ :func:`expand_strings` / :func:`expand_acl` for the
+ragged vectors); K9 handshake records stay on the host (one per connect);
+K10 :func:`encode_requests`; K11 :func:`encode_set_watches`; K12
+:func:`decode_requests`; K13 :func:`encode_responses`.
+"""
+
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from .. import consts
+from .. import jute
+from . import _lib
+from ._lib import ptr, check, stream_ptr
+
+SENTINEL_XID = -(1 << 63)          # xid table entry that matches no xid
+I64 = torch.int64
+I32 = torch.int32
+U8 = torch.uint8
+
+
+def _dev(device):
+    return torch.device(device) if device is not None else \
+        torch.device('cuda', torch.cuda.current_device())
+
+
+class XidTable(object):
+    """Per-connection xid -> opcode map in HBM (``zk-streams.js:145``).
+
+    A direct-mapped ring of ``2**bits`` int64 entries ``(xid << 32) | op``;
+    the decoder verifies the stored xid, so a stale slot can never be
+    mistaken for a live request."""
+
+    def __init__(self, bits=20, device=None):
+        self.bits = bits
+        self.mask = (1 << bits) - 1
+        self.tab = torch.full((1 << bits,), SENTINEL_XID, dtype=I64,
+                              device=_dev(device))
+
+    def reset(self):
+        self.tab.fill_(SENTINEL_XID)
+
+
+# ---------------------------------------------------------------------------
+# Request batches (K10)
+# ---------------------------------------------------------------------------
+
+@dataclass
+class RequestBatch:
+    n: int
+    opcode: torch.Tensor
+    xid: torch.Tensor
+    arg: torch.Tensor
+    path_off: torch.Tensor
+    path_len: torch.Tensor
+    data_off: torch.Tensor
+    data_len: torch.Tensor
+    acl_id: torch.Tensor
+    path_arena: torch.Tensor
+    data_arena: torch.Tensor
+    acl_off: torch.Tensor
+    acl_len: torch.Tensor
+    acl_arena: torch.Tensor
+
+    def struct(self):
+        return _lib.ZkReqBatch(*[t.data_ptr() for t in (
+            self.opcode, self.xid, self.arg, self.path_off, self.path_len,
+            self.data_off, self.data_len, self.acl_id, self.path_arena,
+            self.data_arena, self.acl_off, self.acl_len, self.acl_arena)])
+
+
+def _acl_bytes(acl):
+    w = jute.JuteWriter()
+    w.write_acl(acl)
+    return w.getvalue()
+
+
+def pack_requests(pkts, device=None):
+    """Host packing of request dicts (as :func:`zkmi.jute.encode_request`
+    takes them) into a device :class:`RequestBatch`.  Used by tests and by
+    the client's batched API; the benchmark builds its batches on the GPU."""
+    n = len(pkts)
+    opcode = np.zeros(n, np.int32)
+    xid = np.zeros(n, np.int32)
+    arg = np.zeros(n, np.int32)
+    path_off = np.zeros(n, np.int64)
+    path_len = np.zeros(n, np.int32)
+    data_off = np.zeros(n, np.int64)
+    data_len = np.zeros(n, np.int32)
+    acl_id = np.zeros(n, np.int32)
+    parena = bytearray()
+    darena = bytearray()
+    acls = {}
+    acl_blobs = []
+    for i, p in enumerate(pkts):
+        op = p['opcode']
+        opcode[i] = consts.OP_CODES[op]
+        xid[i] = p['xid']
+        path = p.get('path', '').encode('utf-8')
+        path_off[i] = len(parena)
+        path_len[i] = len(path)
+        parena += path
+        d = p.get('data', b'') or b''
+        data_off[i] = len(darena)
+        data_len[i] = len(d)
+        darena += d
+        if op in ('GET_DATA', 'EXISTS', 'GET_CHILDREN', 'GET_CHILDREN2'):
+            arg[i] = 1 if p.get('watch') else 0
+        elif op == 'CREATE':
+            arg[i] = jute.flags_to_mask(p.get('flags', []))
+            blob = _acl_bytes(p.get('acl', []))
+            if blob not in acls:
+                acls[blob] = len(acl_blobs)
+                acl_blobs.append(blob)
+            acl_id[i] = acls[blob]
+        elif op in ('DELETE', 'SET_DATA'):
+            arg[i] = p.get('version', -1)
+    if not acl_blobs:
+        acl_blobs.append(_acl_bytes([]))
+    aoff = np.zeros(len(acl_blobs), np.int64)
+    alen = np.zeros(len(acl_blobs), np.int32)
+    aarena = bytearray()
+    for k, b in enumerate(acl_blobs):
+        aoff[k] = len(aarena)
+        alen[k] = len(b)
+        aarena += b
+    dev = _dev(device)
+
+    def T(a):
+        return torch.from_numpy(a).to(dev)
+
+    def B(b):
+        a = np.frombuffer(bytes(b) if b else b'\0', np.uint8)
+        return torch.from_numpy(a.copy()).to(dev)
+    return RequestBatch(n, T(opcode), T(xid), T(arg), T(path_off),
+                        T(path_len), T(data_off), T(data_len), T(acl_id),
+                        B(parena), B(darena), T(aoff), T(alen), B(aarena))
+
+
+def encode_requests(batch, xid_table=None, out=None, stream=None):
+    """K10: encode ``batch`` into one framed byte stream.
+
+    Returns ``(stream_bytes, rec_off, total)`` — ``total`` is a device
+    int64 scalar; ``stream_bytes`` is the full output buffer (use
+    ``[:total]``).  When ``out`` is None a buffer sized on the host from the
+    batch is allocated (one small D2H copy)."""
+    L = _lib.lib()
+    n = batch.n
+    dev = batch.opcode.device
+    sizes = torch.empty(max(n, 1), dtype=I64, device=dev)
+    rec_off = torch.empty(max(n, 1), dtype=I64, device=dev)
+    total = torch.zeros(1, dtype=I64, device=dev)
+    ws = torch.empty(L.zk_scan_workspace(max(n, 1)), dtype=I64, device=dev)
+    err = torch.zeros(1, dtype=I32, device=dev)
+    if out is None:
+        # Upper bound: 4+8 header, 4+path, 4+data, acl, 8 ints.
+        ub = int(n * 40 + batch.path_arena.numel() + batch.data_arena.numel()
+                 + int(batch.acl_len.max().item() if n else 0) * max(n, 1))
+        out = torch.empty(max(ub, 16), dtype=U8, device=dev)
+    tab = xid_table.tab if xid_table is not None else None
+    mask = xid_table.mask if xid_table is not None else 0
+    s = batch.struct()
+    check(L.zk_encode_requests(ctypes_ref(s), n, ptr(sizes), ptr(rec_off),
+                               ptr(total), ptr(ws), ptr(out), out.numel(),
+                               ptr(tab), mask, ptr(err), stream_ptr(stream)),
+          'zk_encode_requests')
+    batch._keep = (s, sizes, ws, err)
+    return out, rec_off[:n], total, err
+
+
+def ctypes_ref(s):
+    import ctypes
+    return ctypes.byref(s)
+
+
+def encode_set_watches(rel_zxid, data_paths, exist_paths, child_paths,
+                       device=None, stream=None):
+    """K11: one SET_WATCHES frame (xid -8) for three path lists."""
+    L = _lib.lib()
+    dev = _dev(device)
+    paths = list(data_paths) + list(exist_paths) + list(child_paths)
+    n = len(paths)
+    arena = bytearray()
+    poff = np.zeros(max(n, 1), np.int64)
+    plen = np.zeros(max(n, 1), np.int32)
+    for i, p in enumerate(paths):
+        b = p.encode('utf-8')
+        poff[i] = len(arena)
+        plen[i] = len(b)
+        arena += b
+    t_poff = torch.from_numpy(poff).to(dev)
+    t_plen = torch.from_numpy(plen).to(dev)
+    t_ar = torch.from_numpy(np.frombuffer(bytes(arena) or b'\0',
+                                          np.uint8).copy()).to(dev)
+    sizes = torch.empty(max(n, 1), dtype=I64, device=dev)
+    off = torch.zeros(max(n, 1), dtype=I64, device=dev)
+    total = torch.zeros(1, dtype=I64, device=dev)
+    ws = torch.empty(L.zk_scan_workspace(max(n, 1)), dtype=I64, device=dev)
+    cap = 64 + len(arena) + 4 * n
+    out = torch.empty(cap, dtype=U8, device=dev)
+    err = torch.zeros(1, dtype=I32, device=dev)
+    check(L.zk_encode_set_watches(ptr(t_poff), ptr(t_plen), ptr(t_ar), n,
+                                  len(data_paths), len(exist_paths),
+                                  rel_zxid, ptr(sizes), ptr(off), ptr(total),
+                                  ptr(ws), ptr(out), cap, ptr(err),
+                                  stream_ptr(stream)),
+          'zk_encode_set_watches')
+    frame_len = 32 + len(arena) + 4 * n
+    return out[:frame_len]
+
+
+# ---------------------------------------------------------------------------
+# K1 frame scan
+# ---------------------------------------------------------------------------
+
+@dataclass
+class FrameTable:
+    off: torch.Tensor        # int64 [cap] body offsets
+    length: torch.Tensor     # int32 [cap] body lengths
+    result: torch.Tensor     # int64 [4]: n_frames, consumed, bad, overflow
+
+    @property
+    def count(self):
+        return self.result[0:1]
+
+    def host_result(self):
+        r = self.result.cpu().tolist()
+        return {'frames': r[0], 'consumed': r[1], 'bad': bool(r[2]),
+                'overflow': bool(r[3])}
+
+
+def frame_scan(buf, n=None, max_packet=consts.MAX_PACKET, cap=None,
+               stream=None, workspace=None):
+    """K1: split ``buf[:n]`` (uint8 device tensor) into frames.
+
+    ``cap`` bounds the frame table (default: ``n // 4``, the most frames a
+    stream of ``n`` bytes can hold)."""
+    L = _lib.lib()
+    if n is None:
+        n = buf.numel()
+    dev = buf.device
+    if cap is None:
+        cap = max(n // 4, 1)
+    wsb = L.zk_frame_scan_workspace(n)
+    if workspace is None or workspace.numel() < wsb:
+        workspace = torch.empty(max(wsb, 256), dtype=U8, device=dev)
+    off = torch.empty(cap, dtype=I64, device=dev)
+    ln = torch.empty(cap, dtype=I32, device=dev)
+    res = torch.zeros(4, dtype=I64, device=dev)
+    check(L.zk_frame_scan(ptr(buf), n, max_packet, ptr(workspace),
+                          workspace.numel(), ptr(off), ptr(ln), cap,
+                          ptr(res), stream_ptr(stream)), 'zk_frame_scan')
+    return FrameTable(off, ln, res)
+
+
+# ---------------------------------------------------------------------------
+# K2-K8 reply decode
+# ---------------------------------------------------------------------------
+
+STAT64 = ('czxid', 'mzxid', 'ctime', 'mtime', 'ephemeralOwner', 'pzxid')
+STAT32 = ('version', 'cversion', 'aversion', 'dataLength', 'numChildren')
+
+
+@dataclass
+class ReplyBatch:
+    xid: torch.Tensor
+    err: torch.Tensor
+    opcode: torch.Tensor
+    status: torch.Tensor
+    zxid: torch.Tensor
+    stat64: torch.Tensor     # [6, cap]
+    stat32: torch.Tensor     # [5, cap]
+    pay_off: torch.Tensor
+    pay_len: torch.Tensor
+    aux0: torch.Tensor
+    aux1: torch.Tensor
+    count: torch.Tensor      # device int64 [1]
+
+    def struct(self):
+        return _lib.ZkReplyOut(*[t.data_ptr() for t in (
+            self.xid, self.err, self.opcode, self.status, self.zxid,
+            self.stat64, self.stat32, self.pay_off, self.pay_len, self.aux0,
+            self.aux1)], self.xid.numel())
+
+
+def alloc_replies(cap, device):
+    dev = _dev(device)
+    return ReplyBatch(
+        torch.empty(cap, dtype=I32, device=dev),
+        torch.empty(cap, dtype=I32, device=dev),
+        torch.empty(cap, dtype=I32, device=dev),
+        torch.empty(cap, dtype=I32, device=dev),
+        torch.empty(cap, dtype=I64, device=dev),
+        torch.zeros(6, cap, dtype=I64, device=dev),
+        torch.zeros(5, cap, dtype=I32, device=dev),
+        torch.empty(cap, dtype=I64, device=dev),
+        torch.empty(cap, dtype=I32, device=dev),
+        torch.empty(cap, dtype=I32, device=dev),
+        torch.empty(cap, dtype=I32, device=dev),
+        None)
+
+
+def decode_replies(buf, frames, xid_table, out=None, stream=None):
+    """K2-K8: decode every frame of ``frames`` as a reply."""
+    L = _lib.lib()
+    cap = frames.off.numel()
+    if out is None:
+        out = alloc_replies(cap, buf.device)
+    out.count = frames.count
+    s = out.struct()
+    check(L.zk_decode_replies(ptr(buf), ptr(frames.off), ptr(frames.length),
+                              ptr(frames.count), cap, ptr(xid_table.tab),
+                              xid_table.mask, ctypes_ref(s),
+                              stream_ptr(stream)), 'zk_decode_replies')
+    return out
+
+
+def _scan_i32(counts, stream=None):
+    L = _lib.lib()
+    n = counts.numel()
+    dev = counts.device
+    base = torch.empty(max(n, 1), dtype=I64, device=dev)
+    total = torch.zeros(1, dtype=I64, device=dev)
+    ws = torch.empty(L.zk_scan_workspace(max(n, 1)), dtype=I64, device=dev)
+    check(L.zk_scan_excl_i32(ptr(counts), ptr(base), n, ptr(total), ptr(ws),
+                             stream_ptr(stream)), 'zk_scan_excl_i32')
+    return base, total
+
+
+def expand_strings(buf, region, count, stream=None):
+    """Ragged string vectors (children lists) -> (row_base, off, len)."""
+    L = _lib.lib()
+    n = region.numel()
+    base, total = _scan_i32(count, stream)
+    m = int(total.item())
+    soff = torch.empty(max(m, 1), dtype=I64, device=buf.device)
+    slen = torch.empty(max(m, 1), dtype=I32, device=buf.device)
+    check(L.zk_expand_strings(ptr(buf), ptr(region), ptr(count), ptr(base),
+                              n, ptr(soff), ptr(slen), stream_ptr(stream)),
+          'zk_expand_strings')
+    return base[:n], soff[:m], slen[:m]
+
+
+def expand_acl(buf, region, count, stream=None):
+    """Ragged ACL vectors -> (row_base, perms, scheme off/len, id off/len)."""
+    L = _lib.lib()
+    n = region.numel()
+    base, total = _scan_i32(count, stream)
+    m = int(total.item())
+    dev = buf.device
+    perms = torch.empty(max(m, 1), dtype=I32, device=dev)
+    so = torch.empty(max(m, 1), dtype=I64, device=dev)
+    sl = torch.empty(max(m, 1), dtype=I32, device=dev)
+    io = torch.empty(max(m, 1), dtype=I64, device=dev)
+    il = torch.empty(max(m, 1), dtype=I32, device=dev)
+    check(L.zk_expand_acl(ptr(buf), ptr(region), ptr(count), ptr(base), n,
+                          ptr(perms), ptr(so), ptr(sl), ptr(io), ptr(il),
+                          stream_ptr(stream)), 'zk_expand_acl')
+    return base[:n], perms[:m], so[:m], sl[:m], io[:m], il[:m]
+
+
+# ---------------------------------------------------------------------------
+# K12 / K13 server mode
+# ---------------------------------------------------------------------------
+
+@dataclass
+class RequestTable:
+    xid: torch.Tensor
+    opcode: torch.Tensor
+    status: torch.Tensor
+    path_off: torch.Tensor
+    path_len: torch.Tensor
+    data_off: torch.Tensor
+    data_len: torch.Tensor
+    arg: torch.Tensor
+    vec_off: torch.Tensor
+    vec_count: torch.Tensor
+    rel_zxid: torch.Tensor
+    count: torch.Tensor
+
+    def struct(self):
+        return _lib.ZkReqOut(*[t.data_ptr() for t in (
+            self.xid, self.opcode, self.status, self.path_off,
+            self.path_len, self.data_off, self.data_len, self.arg,
+            self.vec_off, self.vec_count, self.rel_zxid)], self.xid.numel())
+
+
+def alloc_request_table(cap, device):
+    dev = _dev(device)
+    e32 = lambda: torch.empty(cap, dtype=I32, device=dev)  # noqa: E731
+    e64 = lambda: torch.empty(cap, dtype=I64, device=dev)  # noqa: E731
+    return RequestTable(e32(), e32(), e32(), e64(), e32(), e64(), e32(),
+                        e32(), e64(), e32(), e64(), None)
+
+
+def decode_requests(buf, frames, out=None, stream=None):
+    L = _lib.lib()
+    cap = frames.off.numel()
+    if out is None:
+        out = alloc_request_table(cap, buf.device)
+    out.count = frames.count
+    s = out.struct()
+    check(L.zk_decode_requests(ptr(buf), ptr(frames.off), ptr(frames.length),
+                               ptr(frames.count), cap, ctypes_ref(s),
+                               stream_ptr(stream)), 'zk_decode_requests')
+    return out
+
+
+@dataclass
+class ResponseBatch:
+    opcode: torch.Tensor
+    xid: torch.Tensor
+    err: torch.Tensor
+    node: torch.Tensor
+    zxid: torch.Tensor
+    path_off: torch.Tensor
+    path_len: torch.Tensor
+    path_arena: torch.Tensor
+    aux: torch.Tensor
+    count: torch.Tensor
+
+    def struct(self):
+        return _lib.ZkRespBatch(*[t.data_ptr() for t in (
+            self.opcode, self.xid, self.err, self.node, self.zxid,
+            self.path_off, self.path_len, self.path_arena, self.aux)])
+
+
+def encode_responses(resp, store_struct, out_cap, out=None, stream=None):
+    """K13: server-mode reply encode -> (bytes, rec_off, total, err)."""
+    L = _lib.lib()
+    cap = resp.opcode.numel()
+    dev = resp.opcode.device
+    sizes = torch.empty(cap, dtype=I64, device=dev)
+    rec_off = torch.empty(cap, dtype=I64, device=dev)
+    total = torch.zeros(1, dtype=I64, device=dev)
+    ws = torch.empty(L.zk_scan_workspace(cap), dtype=I64, device=dev)
+    err = torch.zeros(1, dtype=I32, device=dev)
+    if out is None:
+        out = torch.empty(out_cap, dtype=U8, device=dev)
+    s = resp.struct()
+    check(L.zk_encode_responses(ctypes_ref(s), ctypes_ref(store_struct),
+                                ptr(resp.count), cap, ptr(sizes),
+                                ptr(rec_off), ptr(total), ptr(ws), ptr(out),
+                                out.numel(), ptr(err), stream_ptr(stream)),
+          'zk_encode_responses')
+    return out, rec_off, total, err
+
+
+# ---------------------------------------------------------------------------
+# Host views (tests, the client's batched API)
+# ---------------------------------------------------------------------------
+
+def replies_to_packets(buf, replies, n=None, children=None, acls=None):
+    """Convert a decoded :class:`ReplyBatch` to the dicts
+    :func:`zkmi.jute.decode_response` produces (for parity checks and for
+    the client's batched calls)."""
+    if n is None:
+        n = int(replies.count.item())
+    hb = bytes(buf.cpu().numpy().tobytes())
+    cols = {k: getattr(replies, k)[:n].cpu().tolist() for k in (
+        'xid', 'err', 'opcode', 'status', 'zxid', 'pay_off', 'pay_len',
+        'aux0', 'aux1')}
+    s64 = replies.stat64[:, :n].cpu().tolist()
+    s32 = replies.stat32[:, :n].cpu().tolist()
+    out = []
+    for i in range(n):
+        st = cols['status'][i]
+        op = consts.OP_CODE_LOOKUP.get(cols['opcode'][i])
+        if st != 0:
+            out.append({'xid': cols['xid'][i], 'status': st})
+            continue
+        err = consts.ERR_LOOKUP.get(cols['err'][i], cols['err'][i])
+        pkt = {'xid': cols['xid'][i], 'zxid': cols['zxid'][i], 'err': err,
+               'opcode': op}
+        if err == 'OK':
+            po, pl = cols['pay_off'][i], cols['pay_len'][i]
+
+            def stat():
+                return jute.Stat(s64[0][i], s64[1][i], s64[2][i], s64[3][i],
+                                 s32[0][i], s32[1][i], s32[2][i], s64[4][i],
+                                 s32[3][i], s32[4][i], s64[5][i])
+            if op == 'GET_DATA':
+                pkt['data'] = hb[po:po + pl]
+                pkt['stat'] = stat()
+            elif op in ('EXISTS', 'SET_DATA'):
+                pkt['stat'] = stat()
+            elif op == 'CREATE':
+                pkt['path'] = hb[po:po + pl].decode('utf-8')
+            elif op in ('GET_CHILDREN', 'GET_CHILDREN2'):
+                r = jute.JuteReader(hb, po, po + pl)
+                pkt['children'] = [r.read_ustring()
+                                   for _ in range(cols['aux0'][i])]
+                if op == 'GET_CHILDREN2':
+                    pkt['stat'] = stat()
+            elif op == 'GET_ACL':
+                r = jute.JuteReader(hb, po - 4, po + pl)
+                pkt['acl'] = r.read_acl()
+                pkt['stat'] = stat()
+            elif op == 'NOTIFICATION':
+                pkt['type'] = consts.NOTIFICATION_TYPE_LOOKUP.get(
+                    cols['aux0'][i], cols['aux0'][i])
+                pkt['state'] = consts.STATE_LOOKUP.get(cols['aux1'][i],
+                                                       cols['aux1'][i])
+                pkt['path'] = hb[po:po + pl].decode('utf-8')
+        out.append(pkt)
+    return out

@@ -207,46 +207,188 @@ __global__ __launch_bounds__(ENC_T) void resp_sizes(ZkRespBatch r,
   sizes[i] = (i < *n_dev) ? 4 + resp_body_size(r, s, i) : 0;
 }
 
+// ---- record sinks ----------------------------------------------------------
+// The same record-emission code writes either straight to global memory
+// (GSink: one thread's stores are scattered across the wave -> poorly
+// coalesced) or into an LDS image of the block's contiguous output span
+// (LSink) that the block then streams out with 16-byte coalesced stores.
+// LSink packs bytes into aligned dwords; only a record's first and last
+// dword can be shared with a neighbour, and those are OR-ed into the
+// zero-initialised image (ds_or_b32), everything else is a plain ds_write.
+struct GSink {
+  uint8_t* o;
+  ZK_DEV void be32(int32_t v) { st_be32(o, v); o += 4; }
+  ZK_DEV void be64(int64_t v) { st_be64(o, v); o += 8; }
+  ZK_DEV void u8(uint32_t b) { *o++ = (uint8_t)b; }
+  ZK_DEV void bytes(const uint8_t* s, int64_t n) { copy_bytes(o, s, n); o += n; }
+  ZK_DEV void finish() {}
+};
+
+struct LSink {
+  uint32_t* w;
+  int64_t widx;
+  uint64_t acc;
+  int nb;
+  bool first;
+  ZK_DEV LSink(uint32_t* lds, int64_t rel) : w(lds), widx(rel >> 2), acc(0),
+                                             nb((int)(rel & 3)), first(true) {}
+  ZK_DEV void flush() {
+    const uint32_t v = (uint32_t)acc;
+    if (first) { atomicOr(&w[widx], v); first = false; }
+    else w[widx] = v;
+    ++widx;
+    acc >>= 32;
+    nb -= 4;
+  }
+  ZK_DEV void put4(uint32_t x) {          // 4 bytes in memory order
+    acc |= (uint64_t)x << (8 * nb);
+    nb += 4;
+    flush();
+  }
+  ZK_DEV void u8(uint32_t b) {
+    acc |= (uint64_t)(b & 0xffu) << (8 * nb);
+    if (++nb == 4) flush();
+  }
+  ZK_DEV void be32(int32_t v) { put4(bswap32((uint32_t)v)); }
+  ZK_DEV void be64(int64_t v) {
+    put4(bswap32((uint32_t)((uint64_t)v >> 32)));
+    put4(bswap32((uint32_t)v));
+  }
+  ZK_DEV void bytes(const uint8_t* s, int64_t n) {
+    int64_t i = 0;
+    for (; i + 16 <= n; i += 16) {
+      uint4 v; __builtin_memcpy(&v, s + i, 16);
+      put4(v.x); put4(v.y); put4(v.z); put4(v.w);
+    }
+    for (; i + 4 <= n; i += 4) {
+      uint32_t v; __builtin_memcpy(&v, s + i, 4);
+      put4(v);
+    }
+    for (; i < n; ++i) u8(s[i]);
+  }
+  ZK_DEV void finish() {
+    if (nb > 0) atomicOr(&w[widx], (uint32_t)acc);
+  }
+};
+
+template <class K>
+ZK_DEV void k_buffer(K& k, const uint8_t* src, int32_t len) {
+  if (len <= 0) { k.be32(-1); return; }
+  k.be32(len);
+  k.bytes(src, len);
+}
+
+template <class K>
+ZK_DEV void k_stat(K& k, const ZkNodeStore& s, int64_t nd) {
+  const int64_t c = s.cap;
+  k.be64(s.stat64[0 * c + nd]);   // czxid
+  k.be64(s.stat64[1 * c + nd]);   // mzxid
+  k.be64(s.stat64[2 * c + nd]);   // ctime
+  k.be64(s.stat64[3 * c + nd]);   // mtime
+  k.be32(s.stat32[0 * c + nd]);   // version
+  k.be32(s.stat32[1 * c + nd]);   // cversion
+  k.be32(s.stat32[2 * c + nd]);   // aversion
+  k.be64(s.stat64[4 * c + nd]);   // ephemeralOwner
+  k.be32(s.stat32[3 * c + nd]);   // dataLength
+  k.be32(s.stat32[4 * c + nd]);   // numChildren
+  k.be64(s.stat64[5 * c + nd]);   // pzxid
+}
+
+template <class K>
+ZK_DEV void emit_response(K& k, const ZkRespBatch& r, const ZkNodeStore& s,
+                          int64_t i, int64_t body) {
+  k.be32((int32_t)body);
+  k.be32(r.xid[i]);
+  k.be64(r.zxid[i]);
+  k.be32(r.err[i]);
+  if (r.err[i] == ERR_OK) {
+    switch (r.opcode[i]) {
+      case OP_GET_DATA: {
+        const int64_t nd = r.node[i];
+        k_buffer(k, s.data_arena + s.data_off[nd], s.data_len[nd]);
+        k_stat(k, s, nd);
+        break;
+      }
+      case OP_EXISTS: case OP_SET_DATA:
+        k_stat(k, s, r.node[i]);
+        break;
+      case OP_CREATE:
+        k_buffer(k, r.path_arena + r.path_off[i], r.path_len[i]);
+        break;
+      case OP_NOTIFICATION:
+        k.be32(r.aux[i]);
+        k.be32(3 /* SYNC_CONNECTED */);
+        k_buffer(k, r.path_arena + r.path_off[i], r.path_len[i]);
+        break;
+      default:
+        break;
+    }
+  }
+  k.finish();
+}
+
+constexpr int64_t STAGE_BYTES = 64 * 1024;   // LDS image per block
+
+// Stream the block's LDS image [B0, B1) (image base a0 = B0 & ~15) out to
+// global memory: 16-byte aligned interior with dwordx4 stores, the <= 15
+// head / tail bytes with byte stores (they abut other blocks' spans).
+ZK_DEV void stage_out(const uint32_t* lw, int64_t a0, int64_t B0, int64_t B1,
+                      uint8_t* __restrict__ out) {
+  const int64_t c0 = (B0 + 15) & ~(int64_t)15;
+  const int64_t c1 = B1 & ~(int64_t)15;
+  const uint8_t* lb = (const uint8_t*)lw;
+  if (c0 < c1) {
+    for (int64_t x = c0 + (int64_t)threadIdx.x * 16; x < c1;
+         x += (int64_t)blockDim.x * 16)
+      *(uint4*)(out + x) = *(const uint4*)(lb + (x - a0));
+    const int64_t hb = c0 - B0, tb = B1 - c1;
+    if ((int64_t)threadIdx.x < hb) {
+      const int64_t x = B0 + threadIdx.x;
+      out[x] = lb[x - a0];
+    } else if ((int64_t)threadIdx.x >= 16 && (int64_t)threadIdx.x < 16 + tb) {
+      const int64_t x = c1 + threadIdx.x - 16;
+      out[x] = lb[x - a0];
+    }
+  } else {
+    for (int64_t x = B0 + threadIdx.x; x < B1; x += blockDim.x)
+      out[x] = lb[x - a0];
+  }
+}
+
 __global__ __launch_bounds__(ENC_T) void resp_write(
     ZkRespBatch r, ZkNodeStore s, const int64_t* __restrict__ n_dev,
     int64_t ncap, const int64_t* __restrict__ off,
-    const int64_t* __restrict__ total, uint8_t* __restrict__ out, int64_t cap,
-    int32_t* __restrict__ err) {
-  const int64_t i = (int64_t)blockIdx.x * ENC_T + threadIdx.x;
-  if (i >= ncap || i >= *n_dev) return;
+    const int64_t* __restrict__ sizes, const int64_t* __restrict__ total,
+    uint8_t* __restrict__ out, int64_t cap, int32_t* __restrict__ err) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lw[];
+  const int64_t n = min(*n_dev, ncap);
+  const int64_t r0 = (int64_t)blockIdx.x * ENC_T;
+  if (r0 >= n) return;
   if (*total > cap) {
-    if (i == 0) atomicOr(err, 2);
+    if (r0 == 0 && threadIdx.x == 0) atomicOr(err, 2);
     return;
   }
-  const int64_t body = resp_body_size(r, s, i);
-  uint8_t* o = out + off[i];
-  st_be32(o, (int32_t)body);
-  st_be32(o + 4, r.xid[i]);
-  st_be64(o + 8, r.zxid[i]);
-  st_be32(o + 16, r.err[i]);
-  o += 20;
-  if (r.err[i] != ERR_OK) return;
-  switch (r.opcode[i]) {
-    case OP_GET_DATA: {
-      const int64_t nd = r.node[i];
-      o = put_buffer(o, s.data_arena + s.data_off[nd], s.data_len[nd]);
-      put_stat(o, s, nd);
-      break;
+  const int64_t r1 = min(r0 + ENC_T, n);
+  const int64_t i = r0 + threadIdx.x;
+  const int64_t B0 = off[r0];
+  const int64_t B1 = off[r1 - 1] + sizes[r1 - 1];
+  const int64_t a0 = B0 & ~(int64_t)15;
+  const int64_t nw = (B1 - a0 + 3) >> 2;
+  if (nw * 4 + 16 > STAGE_BYTES) {              // oversized block: direct
+    if (i < r1) {
+      GSink g{out + off[i]};
+      emit_response(g, r, s, i, sizes[i] - 4);
     }
-    case OP_EXISTS: case OP_SET_DATA:
-      put_stat(o, s, r.node[i]);
-      break;
-    case OP_CREATE:
-      put_buffer(o, r.path_arena + r.path_off[i], r.path_len[i]);
-      break;
-    case OP_NOTIFICATION:
-      st_be32(o, r.aux[i]);
-      st_be32(o + 4, 3 /* SYNC_CONNECTED */);
-      put_buffer(o + 8, r.path_arena + r.path_off[i], r.path_len[i]);
-      break;
-    default:
-      break;
+    return;
   }
+  for (int64_t k = threadIdx.x; k <= nw; k += blockDim.x) lw[k] = 0;
+  __syncthreads();
+  if (i < r1) {
+    LSink l(lw, off[i] - a0);
+    emit_response(l, r, s, i, sizes[i] - 4);
+  }
+  __syncthreads();
+  stage_out(lw, a0, B0, B1, out);
 }
 
 static inline unsigned nblk(int64_t n) {
@@ -304,8 +446,8 @@ int zk_encode_responses(const ZkRespBatch* r, const ZkNodeStore* s,
   ZK_LAUNCH_CHECK();
   int rc = zk_scan_excl_i64(sizes, rec_off, ncap, total, scan_ws, st);
   if (rc) return rc;
-  zk::resp_write<<<zk::nblk(ncap), zk::ENC_T, 0, st>>>(
-      *r, *s, n_dev, ncap, rec_off, total, out, out_cap, err);
+  zk::resp_write<<<zk::nblk(ncap), zk::ENC_T, zk::STAGE_BYTES, st>>>(
+      *r, *s, n_dev, ncap, rec_off, sizes, total, out, out_cap, err);
   ZK_LAUNCH_CHECK();
   return 0;
 }

@@ -146,36 +146,56 @@ ZK_DEV int32_t next_rel(const uint8_t* sb, int64_t ts, int64_t n, int64_t maxp,
   return nx > 0x7FFFFFF0LL ? 0x7FFFFFF0 : (int32_t)nx;
 }
 
+constexpr int FS_PT = FS_S / FS_T;      // positions per thread (16)
+
+// In-place pointer jumping over a uint16 successor table whose fixed points
+// are the sinks.  Each thread batches its 16 gathers before any store so the
+// LDS reads of one round are all in flight together (the compiler cannot
+// reorder them across the aliasing stores itself).
+ZK_DEV void jump_to_sinks(uint16_t* J) {
+  for (int it = 0; it < 16; ++it) {
+    uint16_t v[FS_PT], w[FS_PT];
+#pragma unroll
+    for (int k = 0; k < FS_PT; ++k) v[k] = J[threadIdx.x + k * FS_T];
+#pragma unroll
+    for (int k = 0; k < FS_PT; ++k) w[k] = J[v[k]];
+    int changed = 0;
+#pragma unroll
+    for (int k = 0; k < FS_PT; ++k) {
+      if (w[k] != v[k]) { J[threadIdx.x + k * FS_T] = w[k]; changed = 1; }
+    }
+    if (!__syncthreads_or(changed)) break;
+  }
+}
+
+// A: per-tile exits.  J[p] = in-tile successor, or p itself when p is a
+// terminal or its frame leaves the tile (a sink).  After jumping, J[p] is
+// the last in-tile chain element of p; its next() is the exit (or it is a
+// terminal).  16-bit table: 32 KiB + 16 KiB staged bytes -> 3 blocks / CU.
 __global__ __launch_bounds__(FS_T) void fs_exits(const uint8_t* __restrict__ buf,
                                                 int64_t n, int64_t maxp,
                                                 uint16_t* __restrict__ f0) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  int32_t* J = (int32_t*)smem;                       // [S]
-  uint8_t* sb = smem + FS_S * 4;                     // [S + 16]
+  uint16_t* J = (uint16_t*)smem;                     // [S]
+  uint8_t* sb = smem + FS_S * 2;                     // [S + 16]
   const int64_t t = blockIdx.x;
   const int64_t ts = t * FS_S;
   stage_tile(buf, n, ts, sb);
   __syncthreads();
-  for (int32_t p = threadIdx.x; p < FS_S; p += FS_T)
-    J[p] = next_rel(sb, ts, n, maxp, p);
-  __syncthreads();
-  // In-place pointer jumping to the first position >= S (or a terminal).
-  for (int it = 0; it < 32; ++it) {
-    int changed = 0;
-    for (int32_t p = threadIdx.x; p < FS_S; p += FS_T) {
-      const int32_t j = J[p];
-      if (j < FS_S) {
-        const int32_t jj = J[j];
-        if (jj != j) { J[p] = jj; changed = 1; }
-      }
-    }
-    if (!__syncthreads_or(changed)) break;
+#pragma unroll
+  for (int k = 0; k < FS_PT; ++k) {
+    const int32_t p = threadIdx.x + k * FS_T;
+    const int32_t nx = next_rel(sb, ts, n, maxp, p);
+    J[p] = (uint16_t)((nx < FS_S) ? nx : p);
   }
+  __syncthreads();
+  jump_to_sinks(J);
   for (int32_t p = threadIdx.x; p < FS_W; p += FS_T) {
-    const int32_t j = J[p];
+    const int32_t q = J[p];
+    const int32_t nx = next_rel(sb, ts, n, maxp, q);
     uint16_t v;
-    if (j < FS_S) v = F0_TERM | (uint16_t)j;
-    else if (j - FS_S < 0x4000) v = (uint16_t)(j - FS_S);
+    if (nx == q) v = F0_TERM | (uint16_t)q;          // terminal
+    else if (nx - FS_S < 0x4000) v = (uint16_t)(nx - FS_S);
     else v = F0_ESC;
     f0[t * FS_W + p] = v;
   }
@@ -247,11 +267,14 @@ __global__ __launch_bounds__(FS_T) void fs_mark(const uint8_t* __restrict__ buf,
                                                const int64_t* __restrict__ ent,
                                                uint32_t* __restrict__ bits,
                                                int64_t* __restrict__ counts) {
+  // LDS: A, B (uint16 [S] each), mk (uint8 [S]); the staged bytes live in
+  // B's space until A is built.  80 KiB -> 2 blocks / CU.  Each thread owns
+  // 16 CONTIGUOUS positions so mk / A / B move as 16-byte LDS vectors.
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint16_t* A = (uint16_t*)smem;                       // [S]
   uint16_t* B = A + FS_S;                              // [S]
-  uint8_t* mk = smem + FS_S * 4;                       // [S]
-  uint8_t* sb = mk + FS_S;                             // [S + 16]
+  uint8_t* mk = smem + FS_S * 4;                       // [S] bit0 mark, bit1 terminal
+  uint8_t* sb = (uint8_t*)B;                           // [S + 16] (aliases B)
   const int64_t t = blockIdx.x;
   const int64_t ts = t * FS_S;
   const int64_t e = ent[t];
@@ -261,47 +284,75 @@ __global__ __launch_bounds__(FS_T) void fs_mark(const uint8_t* __restrict__ buf,
     if (threadIdx.x == 0) counts[t] = 0;
     return;
   }
+  const int32_t p0 = threadIdx.x * FS_PT;
   stage_tile(buf, n, ts, sb);
   __syncthreads();
-  // A[p] in [0,S]: next within tile, S = leaves tile; p itself = terminal.
-  for (int32_t p = threadIdx.x; p < FS_S; p += FS_T) {
-    const int32_t j = next_rel(sb, ts, n, maxp, p);
-    A[p] = (uint16_t)(j >= FS_S ? FS_S : j);
-    mk[p] = 0;
+  // A[p]: next within tile; S = leaves the tile; p itself = terminal.
+  {
+    uint16_t a[FS_PT];
+    uint8_t m[FS_PT];
+#pragma unroll
+    for (int k = 0; k < FS_PT; ++k) {
+      const int32_t p = p0 + k;
+      const int32_t j = next_rel(sb, ts, n, maxp, p);
+      a[k] = (uint16_t)(j >= FS_S ? FS_S : j);
+      m[k] = (j == p) ? 2 : 0;
+    }
+    __syncthreads();                                   // sb (in B) is dead
+#pragma unroll
+    for (int k = 0; k < FS_PT; k += 8)
+      *(uint4*)(A + p0 + k) = *(uint4*)(a + k);
+    *(uint4*)(mk + p0) = *(uint4*)m;
   }
   __syncthreads();
-  if (threadIdx.x == 0) mk[e - ts] = 1;
+  if (threadIdx.x == 0) mk[e - ts] |= 1;
   __syncthreads();
   for (int r = 0; r < 16; ++r) {
+    // mark: every marked position marks its 2^r-th successor
     int added = 0;
-    for (int32_t p = threadIdx.x; p < FS_S; p += FS_T) {
-      if (mk[p]) {
-        const int32_t j = A[p];
-        if (j < FS_S && j != p && !mk[j]) { mk[j] = 1; added = 1; }
+    const uint4 mv = *(const uint4*)(mk + p0);
+    const uint32_t mw[4] = {mv.x, mv.y, mv.z, mv.w};
+    if ((mw[0] | mw[1] | mw[2] | mw[3]) & 0x01010101u) {
+#pragma unroll
+      for (int k = 0; k < FS_PT; ++k) {
+        if ((mw[k >> 2] >> (8 * (k & 3))) & 1u) {
+          const int32_t j = A[p0 + k];
+          if (j < FS_S && j != p0 + k && !(mk[j] & 1)) {
+            mk[j] |= 1;
+            added = 1;
+          }
+        }
       }
     }
     if (!__syncthreads_or(added)) break;
-    for (int32_t p = threadIdx.x; p < FS_S; p += FS_T) {
-      const int32_t j = A[p];
-      B[p] = (j < FS_S && j != p) ? A[j] : (uint16_t)j;
+    // jump: B = A o A
+    uint16_t a[FS_PT], b[FS_PT];
+    *(uint4*)a = *(const uint4*)(A + p0);
+    *(uint4*)(a + 8) = *(const uint4*)(A + p0 + 8);
+#pragma unroll
+    for (int k = 0; k < FS_PT; ++k) {
+      const int32_t j = a[k];
+      b[k] = (j < FS_S && j != p0 + k) ? A[j] : (uint16_t)j;
     }
+    *(uint4*)(B + p0) = *(uint4*)b;
+    *(uint4*)(B + p0 + 8) = *(uint4*)(b + 8);
     __syncthreads();
     uint16_t* tmp = A; A = B; B = tmp;
   }
   // A frame starts at every marked position that is not a terminal.
-  int64_t cnt = 0;
-  for (int32_t k = threadIdx.x; k < FS_S / 32; k += FS_T) {
-    uint32_t w = 0;
-    for (int b = 0; b < 32; ++b) {
-      const int32_t p = k * 32 + b;
-      if (mk[p] && next_rel(sb, ts, n, maxp, p) != p) w |= 1u << b;
-    }
-    tb[k] = w;
-    cnt += __popc(w);
-  }
-  int64_t* red = (int64_t*)(smem + FS_S * 6 + 16);   // dynamic LDS only
+  const uint4 mv = *(const uint4*)(mk + p0);
+  const uint32_t mw[4] = {mv.x, mv.y, mv.z, mv.w};
+  uint32_t half = 0;
+#pragma unroll
+  for (int k = 0; k < FS_PT; ++k)
+    if (((mw[k >> 2] >> (8 * (k & 3))) & 3u) == 1u) half |= 1u << k;
+  const uint32_t other = __shfl_xor(half, 1, 64);
+  const uint32_t w = (threadIdx.x & 1) ? 0u : (half | (other << 16));
+  if (!(threadIdx.x & 1)) tb[threadIdx.x >> 1] = w;
+  __syncthreads();                                     // mk reads done
+  int64_t* red = (int64_t*)mk;                         // reuse mk space
   int64_t tot;
-  block_excl_scan(cnt, red, &tot);
+  block_excl_scan((int64_t)__popc(w), red, &tot);
   if (threadIdx.x == 0) counts[t] = tot;
 }
 
@@ -402,7 +453,7 @@ int zk_frame_scan(const uint8_t* buf, int64_t n, int64_t maxp, uint8_t* ws,
   }
   c.f0 = (const uint16_t*)(ws + p.off_f0);
   const int64_t tiles = p.units[0];
-  const size_t lds_a = FS_S * 4 + FS_S + 16;
+  const size_t lds_a = FS_S * 2 + FS_S + 16;
   fs_exits<<<(unsigned)tiles, FS_T, lds_a, st>>>(buf, n, maxp,
                                                 (uint16_t*)(ws + p.off_f0));
   ZK_LAUNCH_CHECK();
@@ -417,7 +468,7 @@ int zk_frame_scan(const uint8_t* buf, int64_t n, int64_t maxp, uint8_t* ws,
     fs_down<<<(unsigned)((np + 255) / 256), 256, 0, st>>>(c, l);
     ZK_LAUNCH_CHECK();
   }
-  const size_t lds_d = FS_S * 6 + 16 + (FS_T / 64 + 1) * 8;
+  const size_t lds_d = FS_S * 5;
   uint32_t* bits = (uint32_t*)(ws + p.off_bits);
   int64_t* cnt = (int64_t*)(ws + p.off_cnt);
   int64_t* base = (int64_t*)(ws + p.off_base);

@@ -240,3 +240,77 @@ def test_decode_requests_matches_oracle(gpu):
         if w['opcode'] == 'CREATE':
             assert cols['arg'][i] == jute.flags_to_mask(w['flags'])
             assert cols['vec_count'][i] == len(w['acl'])
+
+
+def _small_tree(gpu, n=5000, data=100):
+    from zkmi.bench.synthetic import GpuTree
+    return GpuTree(n, data, fanout=100, device=gpu)
+
+
+def test_encode_responses_matches_oracle(gpu):
+    """K13 (LDS-staged writer) against jute.encode_response."""
+    from zkmi.ops import batch as B
+    tree = _small_tree(gpu)
+    r = synth.rng(21)
+    n = 3000
+    ops, errs, nodes, zx, paths = [], [], [], [], []
+    for i in range(n):
+        op = r.choice(['GET_DATA', 'EXISTS', 'SET_DATA', 'CREATE', 'DELETE',
+                       'NOTIFICATION'])
+        ops.append(op)
+        errs.append(0 if r.random() < 0.8 else -101)
+        nodes.append(r.randrange(tree.leaf0, tree.n_static))
+        zx.append(r.randint(0, 2**40))
+        paths.append(synth.rand_path(r))
+    parena = b''.join(p.encode() for p in paths)
+    poff = np.cumsum([0] + [len(p.encode()) for p in paths[:-1]])
+    T = lambda a, dt: torch.tensor(a, dtype=dt, device=gpu)  # noqa: E731
+    resp = B.ResponseBatch(
+        T([consts.OP_CODES[o] for o in ops], torch.int32),
+        T(list(range(n)), torch.int32), T(errs, torch.int32),
+        T(nodes, torch.int64), T(zx, torch.int64),
+        T(poff.tolist(), torch.int64),
+        T([len(p.encode()) for p in paths], torch.int32),
+        _dev_bytes(parena, gpu),
+        T([r.choice([1, 2, 3, 4]) for _ in range(n)], torch.int32),
+        T([n], torch.int64))
+    out, rec_off, total, err = B.encode_responses(resp, tree.store, 1 << 22)
+    torch.cuda.synchronize()
+    assert err.item() == 0
+    got = bytes(out[:total.item()].cpu().numpy().tobytes())
+    s64 = tree.stat64.cpu().numpy()
+    s32 = tree.stat32.cpu().numpy()
+    darena = tree.data_arena.cpu().numpy()
+    doff = tree.data_off.cpu().numpy()
+    dlen = tree.data_len.cpu().numpy()
+    want = []
+    for i in range(n):
+        nd = nodes[i]
+        st = jute.Stat(*[int(s64[0, nd]), int(s64[1, nd]), int(s64[2, nd]),
+                         int(s64[3, nd]), int(s32[0, nd]), int(s32[1, nd]),
+                         int(s32[2, nd]), int(s64[4, nd]), int(s32[3, nd]),
+                         int(s32[4, nd]), int(s64[5, nd])])
+        rep = {'xid': i, 'zxid': zx[i], 'err': errs[i], 'opcode': ops[i],
+               'stat': st, 'path': paths[i],
+               'data': bytes(darena[doff[nd]:doff[nd] + dlen[nd]]),
+               'type': int(resp.aux[i].item()), 'state': 'SYNC_CONNECTED'}
+        want.append(jute.frame(jute.encode_response(rep)))
+    assert got == b''.join(want)
+
+
+def test_gpu_get_pipeline_end_to_end(gpu):
+    from zkmi.bench.synthetic import GetPipeline
+    tree = _small_tree(gpu, 20000, 37)
+    pipe = GetPipeline(tree, 8192)
+    for _ in range(3):
+        ok = pipe.step()
+        assert int(ok.item()) == 8192
+    idx, rep, rx, ft = pipe.last
+    # data bytes returned equal the node's data
+    n = 64
+    po = rep.pay_off[:n].cpu().tolist()
+    hb = rx.cpu().numpy()
+    darena = tree.data_arena.cpu().numpy()
+    doff = tree.data_off.cpu().numpy()
+    for k, nd in enumerate(idx[:n].cpu().tolist()):
+        assert (hb[po[k]:po[k] + 37] == darena[doff[nd]:doff[nd] + 37]).all()

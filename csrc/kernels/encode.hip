@@ -181,22 +181,6 @@ ZK_DEV int64_t resp_body_size(const ZkRespBatch& r, const ZkNodeStore& s,
   }
 }
 
-ZK_DEV uint8_t* put_stat(uint8_t* o, const ZkNodeStore& s, int64_t nd) {
-  const int64_t c = s.cap;
-  st_be64(o + 0, s.stat64[0 * c + nd]);   // czxid
-  st_be64(o + 8, s.stat64[1 * c + nd]);   // mzxid
-  st_be64(o + 16, s.stat64[2 * c + nd]);  // ctime
-  st_be64(o + 24, s.stat64[3 * c + nd]);  // mtime
-  st_be32(o + 32, s.stat32[0 * c + nd]);  // version
-  st_be32(o + 36, s.stat32[1 * c + nd]);  // cversion
-  st_be32(o + 40, s.stat32[2 * c + nd]);  // aversion
-  st_be64(o + 44, s.stat64[4 * c + nd]);  // ephemeralOwner
-  st_be32(o + 52, s.stat32[3 * c + nd]);  // dataLength
-  st_be32(o + 56, s.stat32[4 * c + nd]);  // numChildren
-  st_be64(o + 60, s.stat64[5 * c + nd]);  // pzxid
-  return o + STAT_BYTES;
-}
-
 __global__ __launch_bounds__(ENC_T) void resp_sizes(ZkRespBatch r,
                                                    ZkNodeStore s,
                                                    const int64_t* __restrict__ n_dev,
@@ -279,22 +263,6 @@ ZK_DEV void k_buffer(K& k, const uint8_t* src, int32_t len) {
 }
 
 template <class K>
-ZK_DEV void k_stat(K& k, const ZkNodeStore& s, int64_t nd) {
-  const int64_t c = s.cap;
-  k.be64(s.stat64[0 * c + nd]);   // czxid
-  k.be64(s.stat64[1 * c + nd]);   // mzxid
-  k.be64(s.stat64[2 * c + nd]);   // ctime
-  k.be64(s.stat64[3 * c + nd]);   // mtime
-  k.be32(s.stat32[0 * c + nd]);   // version
-  k.be32(s.stat32[1 * c + nd]);   // cversion
-  k.be32(s.stat32[2 * c + nd]);   // aversion
-  k.be64(s.stat64[4 * c + nd]);   // ephemeralOwner
-  k.be32(s.stat32[3 * c + nd]);   // dataLength
-  k.be32(s.stat32[4 * c + nd]);   // numChildren
-  k.be64(s.stat64[5 * c + nd]);   // pzxid
-}
-
-template <class K>
 ZK_DEV void emit_response(K& k, const ZkRespBatch& r, const ZkNodeStore& s,
                           int64_t i, int64_t body) {
   k.be32((int32_t)body);
@@ -304,13 +272,15 @@ ZK_DEV void emit_response(K& k, const ZkRespBatch& r, const ZkNodeStore& s,
   if (r.err[i] == ERR_OK) {
     switch (r.opcode[i]) {
       case OP_GET_DATA: {
+        // wire-format slot: [len | data] then Stat — two contiguous copies
         const int64_t nd = r.node[i];
-        k_buffer(k, s.data_arena + s.data_off[nd], s.data_len[nd]);
-        k_stat(k, s, nd);
+        const uint8_t* slot = s.slab + s.slot_off[nd];
+        k.bytes(slot + ZK_SLOT_LEN, 4 + (int64_t)max(s.data_len[nd], 0));
+        k.bytes(slot + ZK_SLOT_STAT, STAT_BYTES);
         break;
       }
       case OP_EXISTS: case OP_SET_DATA:
-        k_stat(k, s, r.node[i]);
+        k.bytes(s.slab + s.slot_off[r.node[i]] + ZK_SLOT_STAT, STAT_BYTES);
         break;
       case OP_CREATE:
         k_buffer(k, r.path_arena + r.path_off[i], r.path_len[i]);

@@ -41,7 +41,7 @@ constexpr int64_t FS_S = 16384;          // tile bytes
 constexpr int64_t FS_W = 2048;           // window (entry points) per tile
 constexpr int FS_G = 16;                 // fan-in per composition level
 constexpr int FS_MAXL = 6;               // levels (16 KiB * 16^5 = 16 GiB)
-constexpr int FS_TOPMAX = 256;           // serial walk bound at the top
+constexpr int FS_TOPMAX = 16;            // serial walk bound at the top
 constexpr int FS_T = 1024;               // threads per tile workgroup
 constexpr int64_t TERM = (int64_t)1 << 62;
 constexpr int64_t NONE = -1;
@@ -60,8 +60,17 @@ struct FsCtx {
   int64_t* ent[FS_MAXL];           // entry position per unit (or NONE)
 };
 
+// LATE: composition stopped at position pos (a landing outside the next
+// unit's window, i.e. after a frame > W bytes).  Only the walkers that follow
+// the TRUE chain (fs_top / fs_down) resolve it, by walking on from pos; the
+// composition of the ~2000 speculative entry points per unit never walks
+// bytes, so a garbage chain that merges into the real one outside a window
+// costs one table lookup instead of a hop-by-hop global-memory walk.
+constexpr int64_t LATE = (int64_t)1 << 61;
+
 ZK_DEV bool is_term(int64_t v) { return (v & TERM) != 0; }
-ZK_DEV int64_t pos_of(int64_t v) { return v & ~TERM; }
+ZK_DEV bool is_late(int64_t v) { return (v & LATE) != 0; }
+ZK_DEV int64_t pos_of(int64_t v) { return v & ~(TERM | LATE); }
 
 // One step of the chain in global memory.
 ZK_DEV int64_t next_global(const FsCtx& c, int64_t P) {
@@ -79,9 +88,12 @@ ZK_DEV int64_t walk_until(const FsCtx& c, int64_t P, int64_t end) {
   return P;
 }
 
-template <int L>
+// Apply unit u of level L to position P (inside u).  RES = resolve: walk
+// bytes / LATE values to the exact result (true-chain walkers); !RES =
+// stop with LATE at the first position no table covers (composition).
+template <int L, bool RES>
 ZK_DEV int64_t apply_unit(const FsCtx& c, int64_t u, int64_t P) {
-  if (is_term(P)) return P;
+  if (is_term(P) || is_late(P)) return P;
   if (P >= c.n) return TERM | c.n;
   const int64_t us = u * c.usize[L];
   const int64_t ue = min(us + c.usize[L], c.n);
@@ -89,30 +101,37 @@ ZK_DEV int64_t apply_unit(const FsCtx& c, int64_t u, int64_t P) {
   if constexpr (L == 0) {
     if (off < FS_W) {
       const uint16_t v = c.f0[u * FS_W + off];
-      if (v == F0_ESC) return walk_until(c, P, ue);
+      if (v == F0_ESC) return RES ? walk_until(c, P, ue) : (LATE | P);
       if (v & F0_TERM) return TERM | (us + (v & 0x7FFF));
       const int64_t x = us + FS_S + v;
       return x >= c.n ? (TERM | c.n) : x;
     }
-    return walk_until(c, P, ue);
+    return RES ? walk_until(c, P, ue) : (LATE | P);
   } else {
-    if (off < FS_W) return c.fl[L][u * FS_W + off];
+    if (off < FS_W) {
+      const int64_t v = c.fl[L][u * FS_W + off];
+      if (!RES || !is_late(v)) return v;
+      P = pos_of(v);                      // resume the true chain here
+    } else if (!RES) {
+      return LATE | P;
+    }
     while (!is_term(P) && P < ue) {
       const int64_t sub = P / c.usize[L - 1];
-      P = apply_unit<L - 1>(c, sub, P);
+      P = apply_unit<L - 1, RES>(c, sub, P);
     }
     return P;
   }
 }
 
+template <bool RES>
 ZK_DEV int64_t apply_level(const FsCtx& c, int l, int64_t u, int64_t P) {
   switch (l) {
-    case 0: return apply_unit<0>(c, u, P);
-    case 1: return apply_unit<1>(c, u, P);
-    case 2: return apply_unit<2>(c, u, P);
-    case 3: return apply_unit<3>(c, u, P);
-    case 4: return apply_unit<4>(c, u, P);
-    default: return apply_unit<5>(c, u, P);
+    case 0: return apply_unit<0, RES>(c, u, P);
+    case 1: return apply_unit<1, RES>(c, u, P);
+    case 2: return apply_unit<2, RES>(c, u, P);
+    case 3: return apply_unit<3, RES>(c, u, P);
+    case 4: return apply_unit<4, RES>(c, u, P);
+    default: return apply_unit<5, RES>(c, u, P);
   }
 }
 
@@ -152,8 +171,16 @@ constexpr int FS_PT = FS_S / FS_T;      // positions per thread (16)
 // are the sinks.  Each thread batches its 16 gathers before any store so the
 // LDS reads of one round are all in flight together (the compiler cannot
 // reorder them across the aliasing stores itself).
-ZK_DEV void jump_to_sinks(uint16_t* J) {
-  for (int it = 0; it < 16; ++it) {
+//
+// Real streams have few long chains: in a GET_DATA reply stream ~70 % of the
+// positions are sinks from the start and only the true frame chain (~90
+// positions per 16 KiB tile) needs more than 3 doublings.  So: 2 full rounds,
+// then compact the still-moving positions into an LDS list and iterate only
+// over it (full rounds again if the list would overflow).
+constexpr int FS_LIST = 4096;            // compacted active-position capacity
+
+ZK_DEV void jump_to_sinks(uint16_t* J, uint16_t* act, int64_t* red) {
+  for (int it = 0; it < 2; ++it) {
     uint16_t v[FS_PT], w[FS_PT];
 #pragma unroll
     for (int k = 0; k < FS_PT; ++k) v[k] = J[threadIdx.x + k * FS_T];
@@ -164,7 +191,47 @@ ZK_DEV void jump_to_sinks(uint16_t* J) {
     for (int k = 0; k < FS_PT; ++k) {
       if (w[k] != v[k]) { J[threadIdx.x + k * FS_T] = w[k]; changed = 1; }
     }
-    if (!__syncthreads_or(changed)) break;
+    if (!__syncthreads_or(changed)) return;
+  }
+  // compact positions that have not reached their sink
+  uint16_t v[FS_PT];
+  uint32_t mask = 0;
+#pragma unroll
+  for (int k = 0; k < FS_PT; ++k) v[k] = J[threadIdx.x + k * FS_T];
+#pragma unroll
+  for (int k = 0; k < FS_PT; ++k)
+    if (J[v[k]] != v[k]) mask |= 1u << k;
+  int64_t tot;
+  int64_t o = block_excl_scan(__popc(mask), red, &tot);
+  if (tot > FS_LIST) {
+    for (int it = 0; it < 16; ++it) {
+      uint16_t a[FS_PT], b[FS_PT];
+#pragma unroll
+      for (int k = 0; k < FS_PT; ++k) a[k] = J[threadIdx.x + k * FS_T];
+#pragma unroll
+      for (int k = 0; k < FS_PT; ++k) b[k] = J[a[k]];
+      int changed = 0;
+#pragma unroll
+      for (int k = 0; k < FS_PT; ++k)
+        if (b[k] != a[k]) { J[threadIdx.x + k * FS_T] = b[k]; changed = 1; }
+      if (!__syncthreads_or(changed)) return;
+    }
+    return;
+  }
+#pragma unroll
+  for (int k = 0; k < FS_PT; ++k)
+    if (mask & (1u << k)) act[o++] = (uint16_t)(threadIdx.x + k * FS_T);
+  __syncthreads();
+  const int cnt = (int)tot;
+  for (int it = 0; it < 16; ++it) {
+    int changed = 0;
+    for (int i = threadIdx.x; i < cnt; i += FS_T) {
+      const int p = act[i];
+      const uint16_t a = J[p];
+      const uint16_t b = J[a];
+      if (b != a) { J[p] = b; changed = 1; }
+    }
+    if (!__syncthreads_or(changed)) return;
   }
 }
 
@@ -177,26 +244,60 @@ __global__ __launch_bounds__(FS_T) void fs_exits(const uint8_t* __restrict__ buf
                                                 uint16_t* __restrict__ f0) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint16_t* J = (uint16_t*)smem;                     // [S]
-  uint8_t* sb = smem + FS_S * 2;                     // [S + 16]
+  uint16_t* act = (uint16_t*)(smem + FS_S * 2);      // [FS_LIST]
+  int64_t* red = (int64_t*)(smem + FS_S * 2 + FS_LIST * 2);
   const int64_t t = blockIdx.x;
   const int64_t ts = t * FS_S;
-  stage_tile(buf, n, ts, sb);
-  __syncthreads();
+  // Each thread owns 16 contiguous positions: one 16-byte + one 4-byte
+  // global load cover the 19 bytes their length prefixes span; the BE32 at
+  // every byte offset is rebuilt with v_alignbyte (no LDS byte staging).
+  {
+    const int32_t p0 = threadIdx.x * FS_PT;
+    const int64_t B = ts + p0;
+    uint32_t w[5];
+    if (B + 20 <= n) {
+      uint4 v; __builtin_memcpy(&v, buf + B, 16);
+      w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+      __builtin_memcpy(&w[4], buf + B + 16, 4);
+    } else {
 #pragma unroll
-  for (int k = 0; k < FS_PT; ++k) {
-    const int32_t p = threadIdx.x + k * FS_T;
-    const int32_t nx = next_rel(sb, ts, n, maxp, p);
-    J[p] = (uint16_t)((nx < FS_S) ? nx : p);
+      for (int d = 0; d < 5; ++d) {
+        uint32_t x = 0;
+        for (int b = 0; b < 4; ++b) {
+          const int64_t a = B + 4 * d + b;
+          x |= (a < n ? (uint32_t)buf[a] : 0u) << (8 * b);
+        }
+        w[d] = x;
+      }
+    }
+    uint16_t j[FS_PT];
+#pragma unroll
+    for (int k = 0; k < FS_PT; ++k) {
+      const uint32_t le = __builtin_amdgcn_alignbyte(w[(k >> 2) + 1],
+                                                     w[k >> 2], k & 3);
+      const int32_t len = (int32_t)bswap32(le);
+      const int64_t P = B + k;
+      const bool ok = (P + 4 <= n) && len >= 0 && (int64_t)len <= maxp &&
+                      P + 4 + len <= n;
+      const int64_t nx = ok ? (int64_t)(p0 + k) + 4 + len : (int64_t)(p0 + k);
+      j[k] = (uint16_t)(nx < FS_S ? nx : p0 + k);
+    }
+    *(uint4*)(J + p0) = *(uint4*)j;
+    *(uint4*)(J + p0 + 8) = *(uint4*)(j + 8);
   }
   __syncthreads();
-  jump_to_sinks(J);
+  jump_to_sinks(J, act, red);
   for (int32_t p = threadIdx.x; p < FS_W; p += FS_T) {
     const int32_t q = J[p];
-    const int32_t nx = next_rel(sb, ts, n, maxp, q);
-    uint16_t v;
-    if (nx == q) v = F0_TERM | (uint16_t)q;          // terminal
-    else if (nx - FS_S < 0x4000) v = (uint16_t)(nx - FS_S);
-    else v = F0_ESC;
+    const int64_t Q = ts + q;
+    uint16_t v = F0_TERM | (uint16_t)q;              // terminal by default
+    if (Q + 4 <= n) {
+      const int32_t len = ld_be32(buf + Q);
+      if (len >= 0 && (int64_t)len <= maxp && Q + 4 + len <= n) {
+        const int64_t x = (int64_t)q + 4 + len - FS_S;   // >= 0: leaves tile
+        v = x < 0x4000 ? (uint16_t)x : F0_ESC;
+      }
+    }
     f0[t * FS_W + p] = v;
   }
 }
@@ -211,7 +312,7 @@ __global__ __launch_bounds__(FS_T) void fs_compose(FsCtx c, int l) {
     if (P >= c.n) P = TERM | c.n;
     while (!is_term(P) && P < ue) {
       const int64_t sub = P / c.usize[l];
-      P = apply_level(c, l, sub, P);
+      P = apply_level<false>(c, l, sub, P);
     }
     c.fl[l + 1][u * FS_W + p] = P;
   }
@@ -227,7 +328,7 @@ __global__ void fs_top(FsCtx c, int64_t* __restrict__ result) {
     const int64_t ue = min(us + c.usize[L], c.n);
     if (!is_term(P) && P >= us && P < ue) {
       c.ent[L][u] = P;
-      P = apply_level(c, L, u, P);
+      P = apply_level<true>(c, L, u, P);
     } else {
       c.ent[L][u] = NONE;
     }
@@ -254,7 +355,7 @@ __global__ void fs_down(FsCtx c, int l) {
     const int64_t se = min(ss + c.usize[l], c.n);
     if (P != NONE && !is_term(P) && P >= ss && P < se) {
       c.ent[l][s] = P;
-      P = apply_level(c, l, s, P);
+      P = apply_level<true>(c, l, s, P);
     } else {
       c.ent[l][s] = NONE;
     }
@@ -389,12 +490,106 @@ __global__ __launch_bounds__(256) void fs_write(const uint8_t* __restrict__ buf,
   }
 }
 
+// D' (default) — walk the chain of every tile from its entry, one lane per
+// tile, straight from global memory.  Once the entries are known the walk is
+// ~frames-per-tile dependent loads (the tile's lines come from L2 / the
+// Infinity Cache, where the producer just wrote them), and all tiles walk
+// concurrently, so the kernel is latency- not work-bound: it replaces the
+// O(log) full-tile doubling passes of fs_mark (kept for A/B,
+// ZKMI_FS_MARK=double).  Frame starts go to a per-tile uint16 list.
+constexpr int64_t FS_LMAX = FS_S / 4;    // most frame starts a tile can hold
+
+// One wave per tile: the wave stages the tile into its own 16 KiB of LDS
+// with 16-byte loads, then lane 0 follows the chain there (an LDS hop is
+// ~40 ns against ~250+ ns for an Infinity-Cache hit), 4 tiles per block.
+constexpr int FS_WALK_TPB = 4;
+
+__global__ __launch_bounds__(256) void fs_walk(const uint8_t* __restrict__ buf,
+                                              int64_t n, int64_t maxp,
+                                              int64_t tiles,
+                                              const int64_t* __restrict__ ent,
+                                              uint16_t* __restrict__ list,
+                                              int64_t* __restrict__ counts) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t t = (int64_t)blockIdx.x * FS_WALK_TPB + wv;
+  if (t >= tiles) return;
+  const int64_t e = ent[t];
+  if (e == NONE) {
+    if (lane == 0) counts[t] = 0;
+    return;
+  }
+  uint8_t* sb = smem + wv * (FS_S + 16);
+  const int64_t ts = t * FS_S;
+  const int64_t lim = min(FS_S + 4, n - ts);
+  for (int64_t k = (int64_t)lane * 16; k < FS_S + 16; k += 64 * 16) {
+    if (k + 16 <= lim) {
+      uint4 v; __builtin_memcpy(&v, buf + ts + k, 16);
+      *(uint4*)(sb + k) = v;
+    } else {
+      for (int j = 0; j < 16; ++j)
+        sb[k + j] = (k + j < lim) ? buf[ts + k + j] : 0;
+    }
+  }
+  // Wave-local staging (no workgroup barrier: sibling waves may have exited):
+  // drain this wave's LDS writes before lane 0 reads them.
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+  if (lane != 0) return;
+  const int32_t te = (int32_t)(min(ts + FS_S, n) - ts);   // tile-relative
+  const int64_t nrel = n - ts;
+  uint16_t* L = list + t * FS_LMAX;
+  int64_t cnt = 0;
+  int32_t c = (int32_t)(e - ts);
+  // One LDS round trip per hop: two aligned dword reads + v_alignbyte give
+  // the unaligned big-endian length (4 dependent ds_read_u8 before).
+  while (c < te) {
+    const int32_t a = c & ~3;
+    const uint32_t lo = *(const uint32_t*)(sb + a);
+    const uint32_t hi = *(const uint32_t*)(sb + a + 4);
+    const int32_t len = (int32_t)bswap32(__builtin_amdgcn_alignbyte(hi, lo,
+                                                                    c & 3));
+    const int64_t nx = (int64_t)c + 4 + len;
+    if (((int64_t)c + 4 > nrel) | (len < 0) | ((int64_t)len > maxp) |
+        (nx > nrel))
+      break;
+    L[cnt++] = (uint16_t)c;
+    c = nx > FS_S ? FS_S : (int32_t)nx;
+  }
+  counts[t] = cnt;
+}
+
+// E' — list -> (body offset, length) table; one wave per tile, coalesced.
+__global__ __launch_bounds__(256) void fs_write_list(
+    const uint8_t* __restrict__ buf, int64_t tiles,
+    const uint16_t* __restrict__ list, const int64_t* __restrict__ counts,
+    const int64_t* __restrict__ base, int64_t* __restrict__ foff,
+    int32_t* __restrict__ flen, int64_t cap, int64_t* __restrict__ result) {
+  const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (t >= tiles) return;
+  const int lane = threadIdx.x & 63;
+  const int64_t cnt = counts[t];
+  const int64_t b = base[t];
+  const int64_t ts = t * FS_S;
+  const uint16_t* L = list + t * FS_LMAX;
+  for (int64_t k = lane; k < cnt; k += 64) {
+    const int64_t P = ts + L[k];
+    const int64_t idx = b + k;
+    if (idx < cap) {
+      foff[idx] = P + 4;
+      flen[idx] = ld_be32(buf + P);
+    } else {
+      result[3] = 1;
+    }
+  }
+}
+
 struct FsPlan {
   int levels;
   int64_t units[FS_MAXL];
   int64_t usize[FS_MAXL];
   size_t off_f0, off_fl[FS_MAXL], off_ent[FS_MAXL], off_bits, off_cnt,
-      off_base, off_scan, total;
+      off_base, off_scan, off_list, total;
 };
 
 static FsPlan fs_plan(int64_t n) {
@@ -419,6 +614,7 @@ static FsPlan fs_plan(int64_t n) {
   p.off_cnt = take((size_t)tiles * 8);
   p.off_base = take((size_t)tiles * 8);
   p.off_scan = take((size_t)zk_scan_workspace(tiles) * 8);
+  p.off_list = take((size_t)tiles * FS_LMAX * 2);
   p.total = o;
   return p;
 }
@@ -453,7 +649,7 @@ int zk_frame_scan(const uint8_t* buf, int64_t n, int64_t maxp, uint8_t* ws,
   }
   c.f0 = (const uint16_t*)(ws + p.off_f0);
   const int64_t tiles = p.units[0];
-  const size_t lds_a = FS_S * 2 + FS_S + 16;
+  const size_t lds_a = FS_S * 2 + FS_LIST * 2 + (FS_T / 64 + 1) * 8;
   fs_exits<<<(unsigned)tiles, FS_T, lds_a, st>>>(buf, n, maxp,
                                                 (uint16_t*)(ws + p.off_f0));
   ZK_LAUNCH_CHECK();
@@ -468,18 +664,34 @@ int zk_frame_scan(const uint8_t* buf, int64_t n, int64_t maxp, uint8_t* ws,
     fs_down<<<(unsigned)((np + 255) / 256), 256, 0, st>>>(c, l);
     ZK_LAUNCH_CHECK();
   }
-  const size_t lds_d = FS_S * 5;
   uint32_t* bits = (uint32_t*)(ws + p.off_bits);
   int64_t* cnt = (int64_t*)(ws + p.off_cnt);
   int64_t* base = (int64_t*)(ws + p.off_base);
-  fs_mark<<<(unsigned)tiles, FS_T, lds_d, st>>>(buf, n, maxp, c.ent[0], bits,
-                                               cnt);
+  uint16_t* list = (uint16_t*)(ws + p.off_list);
+  static int mode = -1;
+  if (mode < 0) {
+    const char* m = getenv("ZKMI_FS_MARK");
+    mode = (m && m[0] == 'd') ? 1 : 0;
+  }
+  if (mode == 1) {
+    fs_mark<<<(unsigned)tiles, FS_T, FS_S * 5, st>>>(buf, n, maxp, c.ent[0],
+                                                    bits, cnt);
+  } else {
+    fs_walk<<<(unsigned)((tiles + FS_WALK_TPB - 1) / FS_WALK_TPB), 256,
+              FS_WALK_TPB * (FS_S + 16), st>>>(buf, n, maxp, tiles, c.ent[0],
+                                               list, cnt);
+  }
   ZK_LAUNCH_CHECK();
   int rc = zk_scan_excl_i64(cnt, base, tiles, result + 0,
                             (int64_t*)(ws + p.off_scan), st);
   if (rc) return rc;
-  fs_write<<<(unsigned)tiles, 256, 0, st>>>(buf, bits, base, foff, flen, cap,
-                                           result);
+  if (mode == 1) {
+    fs_write<<<(unsigned)tiles, 256, 0, st>>>(buf, bits, base, foff, flen,
+                                             cap, result);
+  } else {
+    fs_write_list<<<(unsigned)((tiles + 3) / 4), 256, 0, st>>>(
+        buf, tiles, list, cnt, base, foff, flen, cap, result);
+  }
   ZK_LAUNCH_CHECK();
   return 0;
 }

@@ -24,15 +24,23 @@ struct ZkReqBatch {
   const uint8_t* acl_arena;
 };
 
-// Node store of the GPU-resident synthetic server (HBM), SoA.
+// Node store of the GPU-resident synthetic server (HBM).  Each node owns a
+// 16-byte aligned slot in `slab` laid out in WIRE format, so a reply is two
+// contiguous copies, not 13 field gathers from SoA arrays (a random node is
+// then 2-3 cache lines instead of ~13):
+//   [0,68)   Stat, big-endian (version at +32, 4-byte aligned for CAS)
+//   [72,76)  data length, big-endian (-1 when empty, as Jute writes it)
+//   [76,..)  data bytes (capacity slot_cap)
 struct ZkNodeStore {
-  int64_t* stat64;    // [6][cap]: czxid mzxid ctime mtime ephemeralOwner pzxid
-  int32_t* stat32;    // [5][cap]: version cversion aversion dataLength numChildren
-  int64_t* data_off;  // [cap] offset of the node's data in data_arena
-  int32_t* data_len;  // [cap]
-  uint8_t* data_arena;
+  uint8_t* slab;
+  int64_t* slot_off;  // [cap] byte offset of the node's slot in slab
+  int32_t* data_len;  // [cap] host-endian copy of the data length
+  int32_t* slot_cap;  // [cap] data capacity of the slot
   int64_t cap;
 };
+#define ZK_SLOT_STAT 0
+#define ZK_SLOT_LEN 72
+#define ZK_SLOT_DATA 76
 
 // K13 — reply descriptors for server-mode encode.
 struct ZkRespBatch {

@@ -278,21 +278,16 @@ def test_encode_responses_matches_oracle(gpu):
     torch.cuda.synchronize()
     assert err.item() == 0
     got = bytes(out[:total.item()].cpu().numpy().tobytes())
-    s64 = tree.stat64.cpu().numpy()
-    s32 = tree.stat32.cpu().numpy()
-    darena = tree.data_arena.cpu().numpy()
-    doff = tree.data_off.cpu().numpy()
-    dlen = tree.data_len.cpu().numpy()
+    slots = {}
     want = []
     for i in range(n):
         nd = nodes[i]
-        st = jute.Stat(*[int(s64[0, nd]), int(s64[1, nd]), int(s64[2, nd]),
-                         int(s64[3, nd]), int(s32[0, nd]), int(s32[1, nd]),
-                         int(s32[2, nd]), int(s64[4, nd]), int(s32[3, nd]),
-                         int(s32[4, nd]), int(s64[5, nd])])
+        if nd not in slots:
+            slots[nd] = tree.node_slot_host(nd)
+        data, st = slots[nd]
+        assert st.czxid == nd + 1 and st.dataLength == len(data) == 100
         rep = {'xid': i, 'zxid': zx[i], 'err': errs[i], 'opcode': ops[i],
-               'stat': st, 'path': paths[i],
-               'data': bytes(darena[doff[nd]:doff[nd] + dlen[nd]]),
+               'stat': st, 'path': paths[i], 'data': data,
                'type': int(resp.aux[i].item()), 'state': 'SYNC_CONNECTED'}
         want.append(jute.frame(jute.encode_response(rep)))
     assert got == b''.join(want)
@@ -310,7 +305,67 @@ def test_gpu_get_pipeline_end_to_end(gpu):
     n = 64
     po = rep.pay_off[:n].cpu().tolist()
     hb = rx.cpu().numpy()
-    darena = tree.data_arena.cpu().numpy()
-    doff = tree.data_off.cpu().numpy()
     for k, nd in enumerate(idx[:n].cpu().tolist()):
-        assert (hb[po[k]:po[k] + 37] == darena[doff[nd]:doff[nd] + 37]).all()
+        data, st = tree.node_slot_host(nd)
+        assert bytes(hb[po[k]:po[k] + 37].tobytes()) == data
+
+
+def test_gpu_tree_mutations(gpu):
+    """SET_DATA version CAS, CREATE (parent must exist, NODE_EXISTS),
+    DELETE through the GPU server, checked reply by reply."""
+    from zkmi.ops import batch as B
+    from zkmi.bench.synthetic import GpuServer
+    tree = _small_tree(gpu, 1000, 16)
+    leaf = '/bench/d000000/n000000003'
+    pk = [
+        {'xid': 0, 'opcode': 'SET_DATA', 'path': leaf, 'data': b'new!',
+         'version': 0},
+        {'xid': 1, 'opcode': 'SET_DATA', 'path': '/bench/d000000/n000000004',
+         'data': b'x', 'version': 7},                        # BAD_VERSION
+        {'xid': 2, 'opcode': 'CREATE', 'path': '/bench/d000000/new',
+         'data': b'hello', 'acl': [], 'flags': []},
+        {'xid': 3, 'opcode': 'CREATE', 'path': '/nope/x', 'data': b'',
+         'acl': [], 'flags': []},                            # NO_NODE
+        {'xid': 4, 'opcode': 'CREATE', 'path': leaf, 'data': b'',
+         'acl': [], 'flags': []},                            # NODE_EXISTS
+        {'xid': 5, 'opcode': 'DELETE', 'path': '/bench/d000000/n000000005',
+         'version': -1},
+        {'xid': 6, 'opcode': 'GET_DATA', 'path': '/bench/d000000/missing',
+         'watch': False},                                    # NO_NODE
+        {'xid': 7, 'opcode': 'EXISTS', 'path': '/bench', 'watch': False},
+    ]
+    s = b''.join(jute.frame(jute.encode_request(p)) for p in pk)
+    buf = _dev_bytes(s, gpu)
+    srv = GpuServer(tree, 64, 1 << 16)
+    out, total, err, _ = srv.serve(buf, len(s))
+    torch.cuda.synchronize()
+    rx = bytes(out[:total.item()].cpu().numpy().tobytes())
+    frames, consumed, bad = jute.scan_frames(rx)
+    xmap = {p['xid']: p['opcode'] for p in pk}
+    reps = [jute.decode_response(rx[o:o + ln], xmap) for o, ln in frames]
+    errs = [r['err'] for r in reps]
+    assert errs == ['OK', 'BAD_VERSION', 'OK', 'NO_NODE', 'NODE_EXISTS',
+                    'OK', 'NO_NODE', 'OK']
+    assert reps[0]['stat'].version == 1 and reps[0]['stat'].dataLength == 4
+    assert reps[2]['path'] == '/bench/d000000/new'
+    assert reps[7]['stat'].numChildren == 10
+    data, st = tree.node_slot_host(tree.leaf0 + 3)
+    assert data == b'new!' and st.version == 1
+    # the new node is visible and the deleted one is gone
+    pk2 = [{'xid': 10, 'opcode': 'GET_DATA', 'path': '/bench/d000000/new',
+            'watch': False},
+           {'xid': 11, 'opcode': 'EXISTS', 'path':
+            '/bench/d000000/n000000005', 'watch': False},
+           {'xid': 12, 'opcode': 'EXISTS', 'path': '/bench/d000000',
+            'watch': False}]
+    s2 = b''.join(jute.frame(jute.encode_request(p)) for p in pk2)
+    out, total, err, _ = srv.serve(_dev_bytes(s2, gpu), len(s2))
+    rx = bytes(out[:total.item()].cpu().numpy().tobytes())
+    frames, _, _ = jute.scan_frames(rx)
+    xmap = {p['xid']: p['opcode'] for p in pk2}
+    reps = [jute.decode_response(rx[o:o + ln], xmap) for o, ln in frames]
+    assert reps[0]['err'] == 'OK' and reps[0]['data'] == b'hello'
+    assert reps[1]['err'] == 'NO_NODE'
+    # d000000 had 100 children (fanout 100); +1 create -1 delete
+    assert reps[2]['stat'].numChildren == 100
+    assert reps[2]['stat'].cversion == 102

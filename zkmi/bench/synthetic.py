@@ -40,9 +40,15 @@ def _next_pow2(x):
     return p
 
 
+def slot_bytes(data_cap):
+    """Bytes of one wire-format node slot (zk_batch.h ZkNodeStore)."""
+    return _lib.SLOT_DATA + ((data_cap + 15) & ~15) + 4
+
+
 class GpuTree(object):
-    """``n_nodes`` znodes ``/bench/dDDDD/nNNNNNNN`` (``fanout`` children per
-    directory) with ``data_bytes`` of random data each."""
+    """``n_nodes`` znodes ``/bench/dDDDDD/nNNNNNNNN`` (``fanout`` children per
+    directory) with ``data_bytes`` of random data each.  Node ``v`` has
+    ``czxid == v + 1``."""
 
     def __init__(self, n_nodes=1_000_000, data_bytes=100, fanout=1000,
                  device=None, spare=0.25, seed=0):
@@ -52,91 +58,93 @@ class GpuTree(object):
         L = _lib.lib()
         ndirs = (n_nodes + fanout - 1) // fanout
         # node order: 0 = /bench, 1..ndirs = dirs, then leaves
-        paths = ['/bench'] + ['/bench/d%05d' % d for d in range(ndirs)]
+        paths = ['/bench'] + ['/bench/d%06d' % d for d in range(ndirs)]
         leaf0 = len(paths)
-        paths += ['/bench/d%05d/n%08d' % (i // fanout, i)
+        paths += ['/bench/d%06d/n%09d' % (i // fanout, i)
                   for i in range(n_nodes)]
-        parents = np.empty(len(paths), np.int64)
+        nst = len(paths)
+        parents = np.empty(nst, np.int64)
         parents[0] = -1
         parents[1:leaf0] = 0
         parents[leaf0:] = 1 + np.arange(n_nodes) // fanout
-        self.n_static = len(paths)
+        self.n_static = nst
         self.leaf0 = leaf0
         self.n_leaves = n_nodes
-        cap = int(self.n_static * (1 + spare)) + 1024
+        self.data_bytes = data_bytes
+        cap = int(nst * (1 + spare)) + 1024
         self.cap = cap
         enc = [p.encode() for p in paths]
-        plen = np.fromiter((len(e) for e in enc), np.int32, len(enc))
-        poff = np.zeros(len(enc), np.int64)
+        plen = np.fromiter((len(e) for e in enc), np.int32, nst)
+        poff = np.zeros(nst, np.int64)
         np.cumsum(plen[:-1], out=poff[1:])
         arena = b''.join(enc)
         self.path_cap = int(len(arena) * (1 + spare)) + (1 << 16)
-        path_arena = torch.zeros(self.path_cap, dtype=U8, device=dev)
-        path_arena[:len(arena)] = torch.frombuffer(bytearray(arena),
-                                                   dtype=U8).to(dev)
-        self.path_arena = path_arena
+        self.path_arena = torch.zeros(self.path_cap, dtype=U8, device=dev)
+        self.path_arena[:len(arena)] = torch.frombuffer(
+            bytearray(arena), dtype=U8).to(dev)
         self.node_path_off = torch.zeros(cap, dtype=I64, device=dev)
         self.node_path_len = torch.zeros(cap, dtype=I32, device=dev)
-        self.node_path_off[:len(enc)] = torch.from_numpy(poff).to(dev)
-        self.node_path_len[:len(enc)] = torch.from_numpy(plen).to(dev)
+        self.node_path_off[:nst] = torch.from_numpy(poff).to(dev)
+        self.node_path_len[:nst] = torch.from_numpy(plen).to(dev)
         self.node_parent = torch.full((cap,), -1, dtype=I64, device=dev)
-        self.node_parent[:len(enc)] = torch.from_numpy(parents).to(dev)
-        # data slots, 16-byte aligned, >= 128 bytes so sets can grow
-        slot = max((data_bytes + 15) & ~15, 128)
-        self.slot = slot
-        self.data_cap = cap * slot
+        self.node_parent[:nst] = torch.from_numpy(parents).to(dev)
+        # wire-format slots; data capacity >= 128 so sets can grow
+        dcap = max(data_bytes, 128)
+        sb = slot_bytes(dcap)
+        self.slot = sb
+        self.slab_cap = cap * sb
         g = torch.Generator(device=dev)
         g.manual_seed(seed)
-        self.data_arena = torch.randint(0, 256, (self.data_cap,), dtype=U8,
-                                        device=dev, generator=g)
-        self.data_off = torch.arange(cap, dtype=I64, device=dev) * slot
+        self.slab = torch.randint(0, 256, (self.slab_cap,), dtype=U8,
+                                  device=dev, generator=g)
+        self.slot_off = torch.arange(cap, dtype=I64, device=dev) * sb
         self.data_len = torch.zeros(cap, dtype=I32, device=dev)
-        self.data_len[leaf0:len(enc)] = data_bytes
-        self.node_slot_cap = torch.full((cap,), slot, dtype=I32, device=dev)
-        now = int(time.time() * 1000)
-        self.stat64 = torch.zeros(6, cap, dtype=I64, device=dev)
-        self.stat32 = torch.zeros(5, cap, dtype=I32, device=dev)
-        z = torch.arange(1, len(enc) + 1, dtype=I64, device=dev)
-        self.stat64[0, :len(enc)] = z          # czxid
-        self.stat64[1, :len(enc)] = z          # mzxid
-        self.stat64[2, :len(enc)] = now
-        self.stat64[3, :len(enc)] = now
-        self.stat64[5, :len(enc)] = z          # pzxid
-        self.stat32[3] = self.data_len
-        nkids = np.zeros(len(enc), np.int32)
+        self.data_len[leaf0:nst] = data_bytes
+        self.slot_cap = torch.full((cap,), dcap, dtype=I32, device=dev)
+        nkids = np.zeros(nst, np.int32)
         nkids[0] = ndirs
         nkids[1:leaf0] = np.bincount(np.arange(n_nodes) // fanout,
                                      minlength=ndirs)[:ndirs]
-        self.stat32[4, :len(enc)] = torch.from_numpy(nkids).to(dev)
-        self.stat32[1, :len(enc)] = self.stat32[4, :len(enc)]  # cversion
+        nk = torch.from_numpy(nkids).to(dev)
         hcap = _next_pow2(2 * cap)
         self.keys = torch.zeros(hcap, dtype=I64, device=dev)
         self.vals = torch.full((hcap,), -3, dtype=I64, device=dev)
-        self.counters = torch.tensor([len(enc), len(enc), len(arena),
-                                      len(enc) * slot], dtype=I64,
-                                     device=dev)
+        self.counters = torch.tensor([nst, nst, len(arena), nst * sb],
+                                     dtype=I64, device=dev)
         self._struct = self._make_struct(hcap - 1)
-        _lib.check(L.zk_tree_build(ctypes.byref(self._struct), 0, len(enc),
-                                   _lib.stream_ptr()), 'zk_tree_build')
+        sp = _lib.stream_ptr()
+        _lib.check(L.zk_tree_fill(ctypes.byref(self._struct), 0, nst,
+                                  _lib.ptr(nk), int(time.time() * 1000), sp),
+                   'zk_tree_fill')
+        _lib.check(L.zk_tree_build(ctypes.byref(self._struct), 0, nst, sp),
+                   'zk_tree_build')
         torch.cuda.synchronize(dev)
 
     def _make_struct(self, mask):
-        st = _lib.ZkNodeStore(self.stat64.data_ptr(), self.stat32.data_ptr(),
-                              self.data_off.data_ptr(),
+        st = _lib.ZkNodeStore(self.slab.data_ptr(), self.slot_off.data_ptr(),
                               self.data_len.data_ptr(),
-                              self.data_arena.data_ptr(), self.cap)
+                              self.slot_cap.data_ptr(), self.cap)
         self.store = st
         return _lib.ZkTree(self.keys.data_ptr(), self.vals.data_ptr(), mask,
                            self.node_path_off.data_ptr(),
                            self.node_path_len.data_ptr(),
                            self.node_parent.data_ptr(),
-                           self.node_slot_cap.data_ptr(),
                            self.path_arena.data_ptr(), self.path_cap,
-                           self.data_cap, self.counters.data_ptr(), st)
+                           self.slab_cap, self.counters.data_ptr(), st)
 
     @property
     def struct(self):
         return self._struct
+
+    def node_slot_host(self, v):
+        """(data bytes, Stat) of node ``v`` read back from HBM (tests)."""
+        from .. import jute
+        off = int(self.slot_off[v].item())
+        raw = bytes(self.slab[off:off + self.slot].cpu().numpy().tobytes())
+        r = jute.JuteReader(raw, 0)
+        st = r.read_stat()
+        r.off = _lib.SLOT_LEN
+        return r.read_buffer(), st
 
 
 class GpuServer(object):
@@ -202,8 +210,8 @@ class GetPipeline(object):
         self.acl_arena = torch.zeros(16, dtype=U8, device=dev)
         maxpath = int(tree.node_path_len.max().item())
         self.tx = torch.empty(n * (17 + maxpath) + 64, dtype=U8, device=dev)
-        slot = tree.slot
-        self.server = GpuServer(tree, n, n * (4 + 16 + 4 + slot + 68) + 64)
+        dmax = max(tree.data_bytes, 128)
+        self.server = GpuServer(tree, n, n * (4 + 16 + 4 + dmax + 68) + 64)
         self.reply = B.alloc_replies(n, dev)
         self.xid_base = 0
         self.last = None
@@ -219,7 +227,7 @@ class GetPipeline(object):
         rb = B.RequestBatch(n, self.opcode, xid, self.arg,
                             t.node_path_off[idx], t.node_path_len[idx],
                             self.zero64, self.zero32, self.zero32,
-                            t.path_arena, t.data_arena, self.acl_off,
+                            t.path_arena, t.slab, self.acl_off,
                             self.acl_len, self.acl_arena)
         tx, rec_off, total, err = B.encode_requests(rb, self.xt, out=self.tx)
         ntx = int(total.item())
@@ -232,7 +240,7 @@ class GetPipeline(object):
             ok = ((rep.status[:n] == 0) & (rep.err[:n] == 0) &
                   (rep.opcode[:n] == consts.OP_CODES['GET_DATA']) &
                   (rep.xid[:n] == xid) &
-                  (rep.stat64[0, :n] == t.stat64[0][idx]) &
+                  (rep.stat64[0, :n] == idx + 1) &
                   (rep.pay_len[:n] == t.data_len[idx]))
             return ok.sum()
         return None

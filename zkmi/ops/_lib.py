@@ -30,8 +30,14 @@ class ZkReqBatch(ctypes.Structure):
 
 
 class ZkNodeStore(ctypes.Structure):
-    _fields_ = [('stat64', P), ('stat32', P), ('data_off', P),
-                ('data_len', P), ('data_arena', P), ('cap', I64)]
+    _fields_ = [('slab', P), ('slot_off', P), ('data_len', P),
+                ('slot_cap', P), ('cap', I64)]
+
+
+# wire-format node slot layout (csrc/kernels/zk_batch.h)
+SLOT_STAT = 0
+SLOT_LEN = 72
+SLOT_DATA = 76
 
 
 class ZkRespBatch(ctypes.Structure):
@@ -56,9 +62,8 @@ class ZkReqOut(ctypes.Structure):
 class ZkTree(ctypes.Structure):
     _fields_ = [('keys', P), ('vals', P), ('mask', I64),
                 ('node_path_off', P), ('node_path_len', P),
-                ('node_parent', P), ('node_slot_cap', P),
-                ('path_arena', P), ('path_cap', I64), ('data_cap', I64),
-                ('counters', P), ('store', ZkNodeStore)]
+                ('node_parent', P), ('path_arena', P), ('path_cap', I64),
+                ('slab_cap', I64), ('counters', P), ('store', ZkNodeStore)]
 
 
 _SIGS = {
@@ -76,6 +81,7 @@ _SIGS = {
     'zk_expand_acl': (I32, [P, P, P, P, I64, P, P, P, P, P, P]),
     'zk_decode_requests': (I32, [P, P, P, P, I64, P, P]),
     'zk_tree_build': (I32, [P, I64, I64, P]),
+    'zk_tree_fill': (I32, [P, I64, I64, P, I64, P]),
     'zk_tree_serve': (I32, [P, P, P, P, I64, P, P, P, P, P, I64, P]),
 }
 

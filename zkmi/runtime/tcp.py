@@ -42,6 +42,7 @@ class TcpSocket(EventEmitter):
         self.loop = loop
         self.transport = None
         self.closed = False
+        self.ended = False
         self.connecting = False
         self._task = None
         self._paused = False
@@ -133,17 +134,27 @@ class TcpSocket(EventEmitter):
     # -- API -----------------------------------------------------------------
 
     def write(self, data):
-        if self.closed or self.transport is None:
+        """Queue ``data``; never raises (a write on a half-closed or dying
+        socket is dropped, as Node drops writes after ``end()``).  An
+        exception here would otherwise surface in whatever transport
+        callback triggered the write and kill *that* connection."""
+        if self.closed or self.ended or self.transport is None or \
+                self.transport.is_closing():
             return False
         self.bytes_out += len(data)
-        self.transport.write(data)
+        try:
+            self.transport.write(data)
+        except (OSError, RuntimeError):
+            return False
         return True
 
     def end(self, data=None):
         """Half-close after writing ``data`` (Node ``socket.end``)."""
         if data:
             self.write(data)
-        if self.transport is not None and not self.closed:
+        if self.transport is not None and not self.closed and \
+                not self.ended:
+            self.ended = True
             try:
                 if self.transport.can_write_eof():
                     self.transport.write_eof()

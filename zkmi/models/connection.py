@@ -193,7 +193,12 @@ class ZKConnectionFSM(FSM):
             return
 
         def on_session(st):
-            if st == 'attached':
+            # Only when the session attached through THIS connection.  The
+            # reference advances on any 'attached', so after a reattach
+            # revert (zk-session.js:298-320) the rejected connection would
+            # turn 'connected', get preferred by the set, and kill the
+            # connection the session actually lives on.
+            if st == 'attached' and self.session.conn is self:
                 S.gotoState('connected')
         S.on(self.session, 'stateChanged', on_session)
         self.session.attachAndSendCR(self)

@@ -262,6 +262,16 @@ class Client(FSM):
         """Session credentials for resumption elsewhere (R3)."""
         return self.loop.run(lambda: self.session.credentials())
 
+    def abandon(self):
+        """Drop every connection WITHOUT closing the session on the server
+        (a crash, or handing the session to another process that resumes it
+        from :meth:`credentials`).  The client is unusable afterwards."""
+        def go():
+            self._resume_cred = None
+            self.cset.stop()
+            self.resolver.stop()
+        self.loop.run(go)
+
     def _onSetAdded(self, key, conn, hdl):
         self.conns[key] = conn
         self.hdls[key] = hdl

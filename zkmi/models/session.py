@@ -425,11 +425,23 @@ class ZKWatcher(EventEmitter):
             raise TypeError('event must be a string')
         if not callable(cb):
             raise TypeError('callback must be a function')
+        loop = self.session.fsm_loop
+        if not loop.in_loop():
+            # Arming drives FSMs, which live on the loop thread only.
+            loop.run(lambda: self.on(evt, cb))
+            return self
         first = self.listenerCount(evt) < 1
         EventEmitter.on(self, evt, cb)
         if evt != 'error' and first:
             self._armEvent(evt)
         return self
+
+    def removeListener(self, evt, cb):
+        loop = self.session.fsm_loop
+        if not loop.in_loop():
+            loop.run(lambda: EventEmitter.removeListener(self, evt, cb))
+            return self
+        return EventEmitter.removeListener(self, evt, cb)
 
     addListener = on
 

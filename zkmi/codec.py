@@ -31,7 +31,8 @@ if os.environ.get('ZKMI_HOST_CODEC', 'native') != 'python':
     except ImportError:
         _zkhost = None
     if _zkhost is not None:
-        _zkhost.init(jute.Stat)
+        from .errors import ZKDecodeError
+        _zkhost.init(jute.Stat, ZKDecodeError)
         encode_request = _zkhost.encode_request
         decode_response = _zkhost.decode_response
         scan_frames = _zkhost.scan_frames

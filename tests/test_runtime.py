@@ -1,0 +1,191 @@
+"""FSM runtime (the re-provided mooremachine contract), event emitter,
+watcher double-check, tracing, metrics and logging."""
+
+import threading
+import time
+
+import pytest
+
+from zkmi.runtime.emitter import EventEmitter
+from zkmi.runtime.fsm import FSM
+from zkmi.runtime.loop import default_loop, wait_for
+from zkmi.server import FakeZKServer
+from zkmi.utils.log import create_logger
+from zkmi.utils.metrics import create_collector
+from zkmi.utils.trace import RequestTracer
+
+from zkhelpers import client, fast_config
+
+
+class Toy(FSM):
+    def __init__(self, loop, log):
+        self.log = log
+        self.ext = EventEmitter()
+        FSM.__init__(self, 'a', loop)
+
+    def state_a(self, S):
+        self.log.append('enter a')
+        S.on(self.ext, 'go', lambda: S.gotoState('b'))
+        S.on(self.ext, 'sub', lambda: S.gotoState('a.sub'))
+
+    def state_a__sub(self, S):
+        self.log.append('enter a.sub')
+        S.on(self.ext, 'up', lambda: S.gotoState('a'))
+
+    def state_b(self, S):
+        self.log.append('enter b')
+        S.gotoState('c')           # synchronous transition in an entry
+        self.log.append('after goto in b')
+
+    def state_c(self, S):
+        self.log.append('enter c')
+        self.cb = S.callback(lambda: self.log.append('cb ran'))
+        S.timeout(30, lambda: self.log.append('timeout fired'))
+        S.on(self.ext, 'back', lambda: S.gotoState('a'))
+
+
+def test_fsm_semantics():
+    loop = default_loop()
+    log = []
+    changes = []
+
+    def build():
+        t = Toy(loop, log)
+        t.on('stateChanged', changes.append)
+        return t
+    t = loop.run(build)
+    assert t.isInState('a')
+    loop.run(lambda: t.ext.emit('sub'))
+    assert t.getState() == 'a.sub' and t.isInState('a')
+    # parent handlers stay live in the sub-state
+    assert t.ext.listenerCount('go') == 1
+    loop.run(lambda: t.ext.emit('go'))
+    # queued synchronous transition: b's entry completes before c enters,
+    # and stateChanged follows entry order
+    assert log[-4:] == ['enter b', 'after goto in b', 'enter c'][-3:] or \
+        log[-3:] == ['enter b', 'after goto in b', 'enter c']
+    assert changes[-2:] == ['b', 'c']
+    # leaving a state disposes its listeners / timers / callbacks
+    assert t.ext.listenerCount('go') == 0
+    cb = t.cb
+    loop.run(lambda: t.ext.emit('back'))
+    time.sleep(0.08)
+    loop.run(cb)
+    assert 'timeout fired' not in log and 'cb ran' not in log
+    assert t.getState() == 'a'
+
+
+def test_fsm_stale_handle_raises():
+    loop = default_loop()
+
+    class T(FSM):
+        def state_x(self, S):
+            self.S = S
+
+        def state_y(self, S):
+            pass
+    t = loop.run(lambda: T('x', loop))
+    S = t.S
+    loop.run(lambda: S.gotoState('y'))
+    with pytest.raises(AssertionError):
+        loop.run(lambda: S.gotoState('x'))
+
+
+def test_emitter_semantics():
+    e = EventEmitter()
+    got = []
+    f = lambda *a: got.append(('f', a))   # noqa: E731
+    e.on('x', f)
+    e.once('x', lambda *a: got.append(('once', a)))
+    e.emit('x', 1)
+    e.emit('x', 2)
+    assert got == [('f', (1,)), ('once', (1,)), ('f', (2,))]
+    e.removeListener('x', f)
+    assert not e.emit('x', 3)
+    with pytest.raises(ValueError):
+        e.emit('error', ValueError('boom'))
+
+
+def test_watch_double_check_ok_and_miss():
+    """armed -> armed.doublecheck (4h + U(0,8h) in production, ms here):
+    the re-read zxid must match, else the missed wakeup is fatal
+    (zk-session.js:923-970)."""
+    zk = FakeZKServer(tick_ms=250)
+    loop = default_loop()
+    try:
+        cfg = fast_config(doublecheck_ms=150, doublecheck_rand_ms=0)
+        c = client(zk.servers(), config=cfg)
+        c.wait_connected(10)
+        zk.cli_create('/dc', b'1')
+        seen = []
+        c.watcher('/dc').on('dataChanged', lambda d, s: seen.append(d))
+        assert wait_for(lambda: seen == [b'1'], 5)
+        ev = c.watcher('/dc').evts['dataChanged']
+        assert wait_for(lambda: 'armed.doublecheck' in ev.fsm_history, 5)
+        assert wait_for(lambda: ev.getState() == 'armed', 5)
+        # now change the node WITHOUT notifying the client (a lost wakeup)
+        before = len(loop.errors)
+
+        def sneaky():
+            n = zk.db.nodes['/dc']
+            zk.db.zxid += 1
+            n.data = b'2'
+            n.stat.mzxid = zk.db.zxid
+            zk.db.data_watches.pop('/dc', None)
+        zk.run(sneaky)
+        assert wait_for(lambda: len(loop.errors) > before, 5)
+        err = loop.errors.pop()
+        assert 'double-check failed' in str(err)
+        c.close_sync(10)
+    finally:
+        zk.shutdown()
+
+
+def test_request_tracer_and_metrics():
+    zk = FakeZKServer(tick_ms=250)
+    try:
+        tr = RequestTracer()
+        col = create_collector()
+        c = client(zk.servers(), tracer=tr, collector=col)
+        c.wait_connected(10)
+        for _ in range(20):
+            c.call_sync('ping')
+        c.call_sync('create', '/t', b'x', {})
+        for _ in range(30):
+            c.call_sync('get', '/t')
+        s = tr.summary()
+        assert s['GET_DATA']['n'] == 30 and s['PING']['n'] >= 20
+        assert s['GET_DATA']['p99_us'] >= s['GET_DATA']['p50_us'] > 0
+        assert col.getCollector('zookeeper_events').get(
+            {'evtype': 'connect'}) == 1
+        c.close_sync(10)
+    finally:
+        zk.shutdown()
+
+
+def test_structured_logger_children():
+    import io
+    buf = io.StringIO()
+    log = create_logger('t', level='trace', stream=buf, a=1)
+    recs = log.capture()
+    ch = log.child(component='X', b=2)
+    ch.info({'k': 'v'}, 'hello %s', 'world')
+    ch.trace('t')
+    assert recs[0]['msg'] == 'hello world' and recs[0]['a'] == 1
+    assert recs[0]['component'] == 'X' and recs[0]['k'] == 'v'
+    assert recs[1]['level'] == 10
+    assert '"msg": "hello world"' in buf.getvalue()
+
+
+def test_loop_run_from_threads():
+    loop = default_loop()
+    out = []
+
+    def worker(i):
+        out.append(loop.run(lambda: (loop.in_loop(), i)))
+    ts = [threading.Thread(target=worker, args=(i,)) for i in range(8)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert sorted(out) == [(True, i) for i in range(8)]

@@ -322,6 +322,37 @@ __global__ __launch_bounds__(DEC_T) void decode_requests_k(
   o.rel_zxid[i] = rel;
 }
 
+// ---------------------------------------------------------------- K9
+// ConnectResponse batch decode (zk-buffer.js:41-48): protocolVersion,
+// timeOut, sessionId, passwd (offset/len into buf).  One row per session
+// handshake — control plane, batched across a node's sessions.
+__global__ __launch_bounds__(DEC_T) void decode_connect_k(
+    const uint8_t* __restrict__ buf, const int64_t* __restrict__ foff,
+    const int32_t* __restrict__ flen, int64_t n, int32_t* __restrict__ proto,
+    int32_t* __restrict__ tmo, int64_t* __restrict__ sid,
+    int64_t* __restrict__ pw_off, int32_t* __restrict__ pw_len,
+    int32_t* __restrict__ status) {
+  const int64_t i = (int64_t)blockIdx.x * DEC_T + threadIdx.x;
+  if (i >= n) return;
+  const uint8_t* p = buf + foff[i];
+  const int64_t L = flen[i];
+  int32_t st = ST_OK, pv = 0, to = 0, pl = 0;
+  int64_t s = 0, po = -1;
+  if (L < 20) {
+    st = ST_BAD_DECODE;
+  } else {
+    pv = ld_be32(p);
+    to = ld_be32(p + 4);
+    s = ld_be64(p + 8);
+    int32_t l = ld_be32(p + 16);
+    if (l < 0) l = 0;
+    if (20 + (int64_t)l > L) st = ST_BAD_DECODE;   // a trailing readOnly
+    else { po = foff[i] + 20; pl = l; }            // byte is tolerated
+  }
+  proto[i] = pv; tmo[i] = to; sid[i] = s; pw_off[i] = po; pw_len[i] = pl;
+  status[i] = st;
+}
+
 static inline unsigned nblk(int64_t n) {
   return (unsigned)((n + DEC_T - 1) / DEC_T);
 }
@@ -358,6 +389,18 @@ int zk_expand_acl(const uint8_t* buf, const int64_t* region,
   if (n <= 0) return 0;
   zk::expand_acl_k<<<zk::nblk(n), zk::DEC_T, 0, st>>>(
       buf, region, count, base, n, perms, s_off, s_len, i_off, i_len);
+  ZK_LAUNCH_CHECK();
+  return 0;
+}
+
+int zk_decode_connect_responses(const uint8_t* buf, const int64_t* foff,
+                                const int32_t* flen, int64_t n,
+                                int32_t* proto, int32_t* tmo, int64_t* sid,
+                                int64_t* pw_off, int32_t* pw_len,
+                                int32_t* status, hipStream_t st) {
+  if (n <= 0) return 0;
+  zk::decode_connect_k<<<zk::nblk(n), zk::DEC_T, 0, st>>>(
+      buf, foff, flen, n, proto, tmo, sid, pw_off, pw_len, status);
   ZK_LAUNCH_CHECK();
   return 0;
 }

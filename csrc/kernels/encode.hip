@@ -361,6 +361,33 @@ __global__ __launch_bounds__(ENC_T) void resp_write(
   stage_out(lw, a0, B0, B1, out);
 }
 
+// ---------------------------------------------------------------- K9
+// ConnectRequest batch encode (zk-buffer.js:32-39): one handshake record
+// per session (node-wide session (re)attach after a failover, R3).
+__global__ __launch_bounds__(ENC_T) void cr_sizes(const int32_t* __restrict__ pwl,
+                                                 int64_t n,
+                                                 int64_t* __restrict__ sizes) {
+  const int64_t i = (int64_t)blockIdx.x * ENC_T + threadIdx.x;
+  if (i < n) sizes[i] = 4 + 28 + 4 + max(pwl[i], 0);
+}
+
+__global__ __launch_bounds__(ENC_T) void cr_write(
+    const int32_t* __restrict__ proto, const int64_t* __restrict__ zxid,
+    const int32_t* __restrict__ tmo, const int64_t* __restrict__ sid,
+    const int64_t* __restrict__ pwo, const int32_t* __restrict__ pwl,
+    const uint8_t* __restrict__ arena, int64_t n,
+    const int64_t* __restrict__ off, uint8_t* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * ENC_T + threadIdx.x;
+  if (i >= n) return;
+  GSink g{out + off[i]};
+  g.be32(28 + 4 + max(pwl[i], 0));
+  g.be32(proto[i]);
+  g.be64(zxid[i]);
+  g.be32(tmo[i]);
+  g.be64(sid[i]);
+  k_buffer(g, arena + pwo[i], pwl[i]);
+}
+
 static inline unsigned nblk(int64_t n) {
   return (unsigned)((n + ENC_T - 1) / ENC_T);
 }
@@ -401,6 +428,23 @@ int zk_encode_set_watches(const int64_t* poff, const int32_t* plen,
   }
   zk::sw_write<<<zk::nblk(n > 0 ? n : 1), zk::ENC_T, 0, st>>>(
       poff, plen, arena, n, c0, c1, off, total, rel_zxid, out, out_cap, err);
+  ZK_LAUNCH_CHECK();
+  return 0;
+}
+
+int zk_encode_connect_requests(const int32_t* proto, const int64_t* zxid,
+                               const int32_t* tmo, const int64_t* sid,
+                               const int64_t* pwo, const int32_t* pwl,
+                               const uint8_t* arena, int64_t n, int64_t* sizes,
+                               int64_t* off, int64_t* total, int64_t* scan_ws,
+                               uint8_t* out, hipStream_t st) {
+  if (n <= 0) return hipMemsetAsync(total, 0, 8, st);
+  zk::cr_sizes<<<zk::nblk(n), zk::ENC_T, 0, st>>>(pwl, n, sizes);
+  ZK_LAUNCH_CHECK();
+  int rc = zk_scan_excl_i64(sizes, off, n, total, scan_ws, st);
+  if (rc) return rc;
+  zk::cr_write<<<zk::nblk(n), zk::ENC_T, 0, st>>>(proto, zxid, tmo, sid, pwo,
+                                                  pwl, arena, n, off, out);
   ZK_LAUNCH_CHECK();
   return 0;
 }

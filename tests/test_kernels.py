@@ -369,3 +369,30 @@ def test_gpu_tree_mutations(gpu):
     # d000000 had 100 children (fanout 100); +1 create -1 delete
     assert reps[2]['stat'].numChildren == 100
     assert reps[2]['stat'].cversion == 102
+
+
+def test_handshake_records_k9(gpu):
+    from zkmi.ops import batch as B
+    r = synth.rng(31)
+    reqs = [{'protocolVersion': 0, 'lastZxidSeen': r.randint(0, 2**40),
+             'timeOut': r.randint(1000, 40000),
+             'sessionId': r.randint(0, 2**62),
+             'passwd': bytes(r.getrandbits(8) for _ in range(
+                 r.choice([8, 16])))} for _ in range(300)]
+    got = B.encode_connect_requests(reqs, gpu)
+    want = b''.join(jute.frame(jute.encode_connect_request(q)) for q in reqs)
+    assert bytes(got.cpu().numpy().tobytes()) == want
+    resps = [{'protocolVersion': 0, 'timeOut': q['timeOut'],
+              'sessionId': q['sessionId'], 'passwd': q['passwd']}
+             for q in reqs]
+    s = b''.join(jute.frame(jute.encode_connect_response(
+        p, read_only=(i % 2 == 0))) for i, p in enumerate(resps))
+    buf = _dev_bytes(s, gpu)
+    ft = B.frame_scan(buf, len(s))
+    o = B.decode_connect_responses(buf, ft, len(resps))
+    sid = o['sessionId'].cpu().tolist()
+    po, pl = o['passwd_off'].cpu().tolist(), o['passwd_len'].cpu().tolist()
+    assert o['status'].cpu().tolist() == [0] * len(resps)
+    for i, p in enumerate(resps):
+        assert sid[i] == p['sessionId']
+        assert s[po[i]:po[i] + pl[i]] == p['passwd']

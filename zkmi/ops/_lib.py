@@ -80,6 +80,10 @@ _SIGS = {
     'zk_expand_strings': (I32, [P, P, P, P, I64, P, P, P]),
     'zk_expand_acl': (I32, [P, P, P, P, I64, P, P, P, P, P, P]),
     'zk_decode_requests': (I32, [P, P, P, P, I64, P, P]),
+    'zk_encode_connect_requests': (I32, [P, P, P, P, P, P, P, I64, P, P, P,
+                                         P, P, P]),
+    'zk_decode_connect_responses': (I32, [P, P, P, I64, P, P, P, P, P, P,
+                                          P]),
     'zk_tree_build': (I32, [P, I64, I64, P]),
     'zk_tree_fill': (I32, [P, I64, I64, P, I64, P]),
     'zk_tree_serve': (I32, [P, P, P, P, I64, P, P, P, P, P, I64, P]),

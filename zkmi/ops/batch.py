@@ -220,6 +220,60 @@ def encode_set_watches(rel_zxid, data_paths, exist_paths, child_paths,
 
 
 # ---------------------------------------------------------------------------
+# K9 handshake records (batched across a node's sessions)
+# ---------------------------------------------------------------------------
+
+def encode_connect_requests(reqs, device=None, stream=None):
+    """``reqs``: list of dicts as :func:`zkmi.jute.encode_connect_request`
+    takes them.  Returns the framed stream (uint8 device tensor)."""
+    L = _lib.lib()
+    dev = _dev(device)
+    n = len(reqs)
+    arena = bytearray()
+    pwo, pwl = [], []
+    for r in reqs:
+        pw = r.get('passwd', b'\0' * 8)
+        pwo.append(len(arena))
+        pwl.append(len(pw))
+        arena += pw
+    T = lambda v, dt: torch.tensor(v, dtype=dt, device=dev)  # noqa: E731
+    proto = T([r.get('protocolVersion', 0) for r in reqs], I32)
+    zx = T([r.get('lastZxidSeen', 0) for r in reqs], I64)
+    tmo = T([r['timeOut'] for r in reqs], I32)
+    sid = T([r.get('sessionId', 0) for r in reqs], I64)
+    t_pwo, t_pwl = T(pwo, I64), T(pwl, I32)
+    t_ar = torch.from_numpy(np.frombuffer(bytes(arena) or b'\0',
+                                          np.uint8).copy()).to(dev)
+    sizes = torch.empty(max(n, 1), dtype=I64, device=dev)
+    off = torch.empty(max(n, 1), dtype=I64, device=dev)
+    total = torch.zeros(1, dtype=I64, device=dev)
+    ws = torch.empty(L.zk_scan_workspace(max(n, 1)), dtype=I64, device=dev)
+    cap = n * 36 + len(arena) + 16
+    out = torch.empty(cap, dtype=U8, device=dev)
+    check(L.zk_encode_connect_requests(
+        ptr(proto), ptr(zx), ptr(tmo), ptr(sid), ptr(t_pwo), ptr(t_pwl),
+        ptr(t_ar), n, ptr(sizes), ptr(off), ptr(total), ptr(ws), ptr(out),
+        stream_ptr(stream)), 'zk_encode_connect_requests')
+    return out[:n * 36 + len(arena)]
+
+
+def decode_connect_responses(buf, frames, n, stream=None):
+    """Decode ``n`` ConnectResponse frames -> dict of device tensors
+    (protocolVersion, timeOut, sessionId, passwd_off, passwd_len, status)."""
+    L = _lib.lib()
+    dev = buf.device
+    e = lambda dt: torch.empty(max(n, 1), dtype=dt, device=dev)  # noqa
+    o = {'protocolVersion': e(I32), 'timeOut': e(I32), 'sessionId': e(I64),
+         'passwd_off': e(I64), 'passwd_len': e(I32), 'status': e(I32)}
+    check(L.zk_decode_connect_responses(
+        ptr(buf), ptr(frames.off), ptr(frames.length), n,
+        ptr(o['protocolVersion']), ptr(o['timeOut']), ptr(o['sessionId']),
+        ptr(o['passwd_off']), ptr(o['passwd_len']), ptr(o['status']),
+        stream_ptr(stream)), 'zk_decode_connect_responses')
+    return {k: v[:n] for k, v in o.items()}
+
+
+# ---------------------------------------------------------------------------
 # K1 frame scan
 # ---------------------------------------------------------------------------
 

@@ -2,8 +2,11 @@
 """zkmi headline benchmark (BASELINE.json): "ZK ops/sec (whole node) + p50
 get() RTT, 1M-znode synthetic tree".
 
-Config (BASELINE.json configs[1]): batched get() over a 1M-znode synthetic
-tree with the Jute-decode HIP kernels on each MI355X.  One step = one batch
+Default config (BASELINE.json configs[1]): batched get() over a 1M-znode
+synthetic tree with the Jute-decode HIP kernels on each MI355X.
+``--workload mix`` is configs[2] (create/set/delete with version CAS and ACL
+encode on the same 1M-znode tree) and ``--workload storm`` configs[4]
+(EPHEMERAL|SEQUENTIAL create storm with per-step session expiry).  One step = one batch
 of ``--batch`` GET_DATA requests per GPU pushed through the full ZooKeeper
 wire path on the GPU (see zkmi/bench/synthetic.py): client request encode
 (K10) -> server frame scan + request decode (K1, K12) -> tree lookup in HBM
@@ -69,6 +72,8 @@ def main():
     ap.add_argument('--nodes', type=int, default=1_000_000)
     ap.add_argument('--data-bytes', type=int, default=100)
     ap.add_argument('--no-rtt', action='store_true')
+    ap.add_argument('--workload', choices=('get', 'mix', 'storm'),
+                    default='get')
     a = ap.parse_args()
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -80,9 +85,23 @@ def main():
     dev = torch.device('cuda', local)
     torch.cuda.set_device(dev)
 
-    from zkmi.bench.synthetic import GpuTree, GetPipeline
-    tree = GpuTree(a.nodes, a.data_bytes, device=dev, seed=rank)
-    pipe = GetPipeline(tree, a.batch, seed=rank)
+    from zkmi.bench import synthetic as S
+    if a.workload == 'get':
+        tree = S.GpuTree(a.nodes, a.data_bytes, device=dev, seed=rank)
+        pipe = S.GetPipeline(tree, a.batch, seed=rank)
+        per_step = a.batch
+    else:
+        # room for the write working set next to the 1M static nodes: the
+        # mix keeps 3 generations of batch/3 nodes, the storm 2 sessions'
+        spare = (a.batch * (1 if a.workload == 'mix' else 2) + 8192) / a.nodes
+        tree = S.GpuTree(a.nodes, a.data_bytes, device=dev, seed=rank,
+                         spare=spare + 0.05)
+        if a.workload == 'mix':
+            pipe = S.MixPipeline(tree, a.batch, a.data_bytes, seed=rank)
+            per_step = pipe.n
+        else:
+            pipe = S.StormPipeline(tree, a.batch, seed=rank)
+            per_step = pipe.n
 
     ok_total = torch.zeros(1, dtype=torch.int64, device=dev)
     for _ in range(a.warmup):
@@ -107,9 +126,11 @@ def main():
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
         dist.all_reduce(ok, op=dist.ReduceOp.SUM)   # R4: node-level counters
     elapsed = el.item()
-    ops = a.batch * a.steps * world
+    ops = per_step * a.steps * world
     ok = int(ok.item())
     if ok != ops:
+        if hasattr(pipe, 'diagnose'):
+            print('diagnose:', pipe.diagnose(), file=sys.stderr)
         raise SystemExit('validation failed: %d of %d replies wrong'
                          % (ops - ok, ops))
     value = ops / elapsed
@@ -134,9 +155,9 @@ def main():
             'dtype': 'bf16',
             'data': 'synthetic',
             'config': {
-                'model': 'zk-get %dk-znode tree, %dB data' % (
-                    a.nodes // 1000, a.data_bytes),
-                'global_batch': a.batch * world,
+                'model': 'zk-%s %dk-znode tree, %dB data' % (
+                    a.workload, a.nodes // 1000, a.data_bytes),
+                'global_batch': per_step * world,
                 'seq_len': 1,
                 'parallelism': 'dp%d' % world,
             },

@@ -368,7 +368,7 @@ __global__ __launch_bounds__(ENC_T) void cr_sizes(const int32_t* __restrict__ pw
                                                  int64_t n,
                                                  int64_t* __restrict__ sizes) {
   const int64_t i = (int64_t)blockIdx.x * ENC_T + threadIdx.x;
-  if (i < n) sizes[i] = 4 + 28 + 4 + max(pwl[i], 0);
+  if (i < n) sizes[i] = 4 + 28 + max(pwl[i], 0);   // frame + body
 }
 
 __global__ __launch_bounds__(ENC_T) void cr_write(
@@ -380,7 +380,7 @@ __global__ __launch_bounds__(ENC_T) void cr_write(
   const int64_t i = (int64_t)blockIdx.x * ENC_T + threadIdx.x;
   if (i >= n) return;
   GSink g{out + off[i]};
-  g.be32(28 + 4 + max(pwl[i], 0));
+  g.be32(28 + max(pwl[i], 0));   // 4+8+4+8 fixed + 4-byte passwd length
   g.be32(proto[i]);
   g.be64(zxid[i]);
   g.be32(tmo[i]);

@@ -535,28 +535,39 @@ __global__ __launch_bounds__(256) void fs_walk(const uint8_t* __restrict__ buf,
   // drain this wave's LDS writes before lane 0 reads them.
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_wave_barrier();
-  if (lane != 0) return;
   const int32_t te = (int32_t)(min(ts + FS_S, n) - ts);   // tile-relative
   const int64_t nrel = n - ts;
-  uint16_t* L = list + t * FS_LMAX;
-  int64_t cnt = 0;
-  int32_t c = (int32_t)(e - ts);
-  // One LDS round trip per hop: two aligned dword reads + v_alignbyte give
-  // the unaligned big-endian length (4 dependent ds_read_u8 before).
-  while (c < te) {
-    const int32_t a = c & ~3;
-    const uint32_t lo = *(const uint32_t*)(sb + a);
-    const uint32_t hi = *(const uint32_t*)(sb + a + 4);
-    const int32_t len = (int32_t)bswap32(__builtin_amdgcn_alignbyte(hi, lo,
-                                                                    c & 3));
-    const int64_t nx = (int64_t)c + 4 + len;
-    if (((int64_t)c + 4 > nrel) | (len < 0) | ((int64_t)len > maxp) |
-        (nx > nrel))
-      break;
-    L[cnt++] = (uint16_t)c;
-    c = nx > FS_S ? FS_S : (int32_t)nx;
+  int32_t cnt = 0;
+  if (lane == 0) {
+    // The frame-start list is written IN PLACE over bytes already passed:
+    // entry k lands at byte 2k while the walk is at >= 4k, so no byte still
+    // to be read is overwritten, and no global store (with its vmcnt
+    // back-pressure) sits inside the dependent-hop loop.
+    uint16_t* Ls = (uint16_t*)sb;
+    int32_t c = (int32_t)(e - ts);
+    // One LDS round trip per hop: two aligned dword reads + v_alignbyte
+    // give the unaligned big-endian length.
+    while (c < te) {
+      const int32_t a = c & ~3;
+      const uint32_t lo = *(const uint32_t*)(sb + a);
+      const uint32_t hi = *(const uint32_t*)(sb + a + 4);
+      const int32_t len = (int32_t)bswap32(
+          __builtin_amdgcn_alignbyte(hi, lo, c & 3));
+      const int64_t nx = (int64_t)c + 4 + len;
+      if (((int64_t)c + 4 > nrel) | (len < 0) | ((int64_t)len > maxp) |
+          (nx > nrel))
+        break;
+      Ls[cnt++] = (uint16_t)c;
+      c = nx > FS_S ? FS_S : (int32_t)nx;
+    }
   }
-  counts[t] = cnt;
+  cnt = __shfl(cnt, 0, 64);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+  const uint16_t* Ls = (const uint16_t*)sb;
+  uint16_t* L = list + t * FS_LMAX;
+  for (int32_t k = lane; k < cnt; k += 64) L[k] = Ls[k];
+  if (lane == 0) counts[t] = cnt;
 }
 
 // E' — list -> (body offset, length) table; one wave per tile, coalesced.

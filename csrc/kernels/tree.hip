@@ -1,7 +1,7 @@
 // GPU-resident synthetic ZooKeeper tree (the server side of the 1M-znode
-// benchmark and of the create/set/delete mix).  Not part of the reference —
-// it stands in for the JVM server the reference tests talk to, so that the
-// whole request -> reply path can be driven at HBM speed.
+// benchmark, the create/set/delete mix and the ephemeral create storm).  Not
+// part of the reference — it stands in for the JVM server the reference's
+// tests talk to, so that the whole request -> reply path runs at HBM speed.
 //
 // Layout (HBM, sized by the caller for 288 GB parts):
 //   * open-addressing hash table: keys = FNV-1a(path) | 1, vals = node index
@@ -9,12 +9,32 @@
 //   * node slots in wire format (zk_batch.h ZkNodeStore), so replies are
 //     contiguous copies;
 //   * a path arena holding each node's path for exact-match verification;
-//   * counters: [0] node count, [1] zxid, [2] path-arena top, [3] slab top.
+//   * counters (TC_*): node high-water mark, zxid, path-arena top, slab top,
+//     the free-node ring (head / tail / published tail) and the dirty count;
+//   * a free-node ring: DELETE (and session expiry) push the node index,
+//     CREATE pops one published by an EARLIER launch (tree_publish_k runs
+//     between batches), reusing its slot and path storage when they fit;
+//   * host-endian shadows of each node's cversion / numChildren / pzxid.
+//     Children come and go with plain atomicAdd / atomicMax on these (a
+//     big-endian Stat word would need a CAS retry loop, and ~1000 parents
+//     shared by a million writes contend); every parent touched in a launch
+//     is put on a dirty list once, and tree_fixup_k rewrites the wire-format
+//     Stat words of exactly those parents before replies are encoded.
+//
+// Single-address counters (free ring, node bump, dirty list) are claimed
+// once per BLOCK (ballot/mbcnt ranks + an LDS prefix, one atomic), the rare
+// byte claims of the arena bump allocators once per wave (64-lane shuffle
+// scan); zxids need no atomic at all (base + request index).  For that the
+// serve and expire kernels keep every thread alive to the end (out-of-range
+// threads carry a no-op).
+//
 // Requests are applied concurrently within a batch; conflicting operations
-// on the same path inside ONE batch are unordered (the benchmark generator
-// never emits them).  Version CAS is an atomicCAS on the slot's big-endian
+// on the same path inside ONE batch are unordered (the benchmark generators
+// never emit them).  Version CAS is an atomicCAS on the slot's big-endian
 // version word, so exactly one of several same-version SET_DATAs wins (the
-// others get BAD_VERSION), matching ZooKeeper's conditional set.
+// others get BAD_VERSION), matching ZooKeeper's conditional set.  Every
+// write request is assigned a zxid, failed ones included (ZooKeeper logs an
+// error txn for them).
 #include "zk_common.h"
 #include "zk_batch.h"
 
@@ -25,23 +45,91 @@ struct ZkTree {
   int64_t mask;
   int64_t* node_path_off;
   int32_t* node_path_len;
-  int64_t* node_parent;        // parent node index (-1 for roots)
+  int64_t* node_parent;        // parent node index, -1 = root, -2 = free
   uint8_t* path_arena;
   int64_t path_cap;
   int64_t slab_cap;
-  int64_t* counters;
+  int64_t* counters;           // see TC_* below
   ZkNodeStore store;
+  int64_t* free_list;          // ring of deleted node indices
+  int64_t free_cap;
+  int32_t* cver;               // [cap] host-endian cversion
+  int32_t* nchild;             // [cap] host-endian numChildren
+  int64_t* pzxid;              // [cap] host-endian pzxid
+  int32_t* dirty;              // [cap] parent-on-dirty-list flag
+  int64_t* dirty_list;         // [cap]
 };
 }
 
 namespace zk {
 
 constexpr int TR_T = 256;
+enum : int {
+  TC_NODES = 0, TC_ZXID = 1, TC_PATH_TOP = 2, TC_SLAB_TOP = 3,
+  TC_FREE_HEAD = 4, TC_FREE_TAIL = 5, TC_FREE_PUB = 6, TC_DIRTY = 7,
+  TC_N = 8
+};
+constexpr int64_t NODE_FREE = -2;
 
 ZK_DEV int64_t slot_bytes(int32_t data_cap) {
   return ZK_SLOT_DATA + (((int64_t)data_cap + 15) & ~(int64_t)15) + 4;
 }
 
+// ---- aggregated claims (all threads of the block must be active) ---------
+ZK_DEV int lane_id() {
+  return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0));
+}
+
+// One ticket per thread with `want`: returns base + rank, or -1.  Ranks come
+// from ballot/mbcnt within a wave and an LDS prefix over the block's waves;
+// ONE atomic per 256-thread block (a single word sustains only ~88
+// returning atomics/us, MI355X_MICROARCH.md "dequeue").  Every thread of the
+// block must call it.
+ZK_DEV int64_t block_ticket(int64_t* ctr, bool want) {
+  __shared__ int64_t part[TR_T / 64 + 1];
+  const int w = threadIdx.x >> 6;
+  const uint64_t m = __ballot(want);
+  const int rank = __builtin_amdgcn_mbcnt_hi(
+      (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+  if (lane_id() == 0) part[w] = __popcll(m);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int64_t tot = 0;
+    for (int k = 0; k < TR_T / 64; ++k) {
+      const int64_t c = part[k];
+      part[k] = tot;
+      tot += c;
+    }
+    part[TR_T / 64] = tot ? (int64_t)atomicAdd((unsigned long long*)ctr,
+                                               (unsigned long long)tot)
+                          : 0;
+  }
+  __syncthreads();
+  const int64_t r = want ? part[TR_T / 64] + part[w] + rank : -1;
+  __syncthreads();                                 // part[] reusable
+  return r;
+}
+
+// Claim `amount` (>= 0) bytes per lane; returns this lane's offset or -1.
+ZK_DEV int64_t wave_bytes(int64_t* ctr, int64_t amount) {
+  const int lane = lane_id();
+  int64_t incl = amount;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int64_t y = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += y;
+  }
+  const int64_t tot = __shfl(incl, 63, 64);
+  if (tot == 0) return -1;
+  int64_t base = 0;
+  if (lane == 63)
+    base = (int64_t)atomicAdd((unsigned long long*)ctr,
+                              (unsigned long long)tot);
+  base = __shfl(base, 63, 64);
+  return amount > 0 ? base + incl - amount : -1;
+}
+
+// ---- hash index -----------------------------------------------------------
 ZK_DEV uint64_t fnv1a(const uint8_t* p, int32_t n) {
   uint64_t h = 1469598103934665603ull;
   int32_t i = 0;
@@ -119,30 +207,23 @@ ZK_DEV int64_t tree_insert(const ZkTree& t, int64_t v, const uint8_t* p,
   return -1;
 }
 
-ZK_DEV void tree_erase(const ZkTree& t, int64_t v, const uint8_t* p,
+// Tombstone node `v`'s hash entry.  Returns true for exactly one caller when
+// several erase the same node concurrently (the CAS winner owns the free).
+ZK_DEV bool tree_erase(const ZkTree& t, int64_t v, const uint8_t* p,
                        int32_t n) {
   const int64_t key = (int64_t)(fnv1a(p, n) | 1ull);
   int64_t s = key & t.mask;
   for (int64_t probe = 0; probe <= t.mask; ++probe) {
     const int64_t k = t.keys[s];
-    if (k == 0) return;
-    if (k == key && t.vals[s] == v) {
-      atomicExch((unsigned long long*)&t.vals[s], (unsigned long long)-2);
-      return;
-    }
+    if (k == 0) return false;
+    if (k == key && atomicCAS((unsigned long long*)&t.vals[s],
+                              (unsigned long long)v,
+                              (unsigned long long)-2) ==
+                        (unsigned long long)v)
+      return true;
     s = (s + 1) & t.mask;
   }
-}
-
-// Atomic add on a big-endian 32-bit field (cversion / numChildren).
-ZK_DEV void be32_atomic_add(uint8_t* p, int32_t d) {
-  unsigned int* w = (unsigned int*)p;
-  unsigned int old = *w, assumed;
-  do {
-    assumed = old;
-    const unsigned int nv = bswap32((uint32_t)((int32_t)bswap32(assumed) + d));
-    old = atomicCAS(w, assumed, nv);
-  } while (old != assumed);
+  return false;
 }
 
 ZK_DEV void fill_stat(uint8_t* st, int64_t cz, int64_t mz, int64_t ct,
@@ -152,6 +233,34 @@ ZK_DEV void fill_stat(uint8_t* st, int64_t cz, int64_t mz, int64_t ct,
   st_be64(st + 24, mt); st_be32(st + 32, ver); st_be32(st + 36, cver);
   st_be32(st + 40, aver); st_be64(st + 44, owner); st_be32(st + 52, dlen);
   st_be32(st + 56, nkids); st_be64(st + 60, pz);
+}
+
+// ---- parent bookkeeping ----------------------------------------------------
+// Child added (dkids = 1) / removed (-1) under `par` by the txn `zx`;
+// `bump_cver` is false when a SEQUENTIAL create already took the cversion.
+ZK_DEV void parent_touch(const ZkTree& t, int64_t par, int32_t dkids,
+                         bool bump_cver, int64_t zx) {
+  if (bump_cver) atomicAdd(&t.cver[par], 1);
+  atomicAdd(&t.nchild[par], dkids);
+  atomicMax((unsigned long long*)&t.pzxid[par], (unsigned long long)zx);
+}
+
+// Put every distinct parent this block touched on the dirty list once
+// (block-uniform call).
+ZK_DEV void wave_mark_dirty(const ZkTree& t, int64_t par) {
+  bool first = false;
+  if (par >= 0 && __hip_atomic_load(&t.dirty[par], __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_AGENT) == 0)
+    first = atomicExch(&t.dirty[par], 1) == 0;
+  const int64_t k = block_ticket(&t.counters[TC_DIRTY], first);
+  if (first) t.dirty_list[k] = par;
+}
+
+// Free `v` (block-uniform call; `v < 0` = nothing to free).
+ZK_DEV void wave_free(const ZkTree& t, int64_t v) {
+  if (v >= 0) t.node_parent[v] = NODE_FREE;
+  const int64_t k = block_ticket(&t.counters[TC_FREE_TAIL], v >= 0);
+  if (v >= 0) t.free_list[k % t.free_cap] = v;
 }
 
 __global__ __launch_bounds__(TR_T) void tree_fill_k(ZkTree t, int64_t n0,
@@ -167,140 +276,293 @@ __global__ __launch_bounds__(TR_T) void tree_fill_k(ZkTree t, int64_t n0,
             nkids[v], v + 1);
   st_be32(slot + 68, 0);
   st_be32(slot + ZK_SLOT_LEN, dl > 0 ? dl : -1);
+  t.cver[v] = nkids[v];
+  t.nchild[v] = nkids[v];
+  t.pzxid[v] = v + 1;
+  t.dirty[v] = 0;
 }
 
 __global__ __launch_bounds__(TR_T) void tree_build_k(ZkTree t, int64_t n0,
                                                     int64_t n) {
   const int64_t v = n0 + (int64_t)blockIdx.x * TR_T + threadIdx.x;
-  if (v >= n) return;
+  if (v >= n || t.node_parent[v] == NODE_FREE) return;
   tree_insert(t, v, t.path_arena + t.node_path_off[v], t.node_path_len[v]);
 }
 
+// Write "%010d" of a non-negative sequence number (ZooKeeper's sequential
+// suffix; the counter is the parent's cversion).
+ZK_DEV void put_seq10(uint8_t* d, int32_t x) {
+  uint32_t u = (uint32_t)x;
+#pragma unroll
+  for (int k = 9; k >= 0; --k) { d[k] = (uint8_t)('0' + u % 10); u /= 10; }
+}
+
+// Per-lane state of one request through the three phases of tree_serve_k.
+struct Lane {
+  int32_t op, err, pl, dl, flags;
+  int64_t node, zx, par;
+  const uint8_t* path;
+};
+
+// CREATE (lib/zk-buffer.js:97-136 request shape; semantics of the server the
+// reference talks to): parent must exist and not be ephemeral, ACL must be
+// non-empty, SEQUENTIAL appends the parent's cversion, EPHEMERAL records the
+// owning session in the Stat.  `v` (with storage `po` / `so`) was claimed
+// for this lane in phase A; on failure the caller frees it.
+ZK_DEV int32_t do_create(const ZkTree& t, Lane& L, const uint8_t* data,
+                         int32_t nacl, int64_t session, int64_t now_ms,
+                         int64_t v) {
+  const ZkNodeStore& s = t.store;
+  const bool eph = L.flags & CF_EPHEMERAL, seq = L.flags & CF_SEQUENTIAL;
+  if (nacl <= 0) return ERR_INVALID_ACL;
+  if (v < 0) return ERR_SYSTEM;                       // tree full
+  const uint8_t* path = L.path;
+  const int32_t pl = L.pl;
+  int32_t cut = pl - 1;
+  while (cut > 0 && path[cut] != '/') --cut;
+  const int64_t par = cut > 0 ? tree_find(t, path, cut) : -1;
+  if (cut > 0 && par < 0) return ERR_NO_NODE;
+  if (par >= 0 && ld_be64(s.slab + s.slot_off[par] + 44) != 0)
+    return ERR_NO_CHILDREN_FOR_EPHEMERALS;
+  if (!seq && tree_find(t, path, pl) >= 0) return ERR_NODE_EXISTS;
+  const int32_t npl = pl + (seq ? 10 : 0);
+  const int32_t seqno = seq && par >= 0 ? atomicAdd(&t.cver[par], 1) : 0;
+  uint8_t* pd = t.path_arena + t.node_path_off[v];
+  copy_bytes(pd, path, pl);
+  if (seq) put_seq10(pd + pl, seqno);
+  const int32_t dl = L.dl;
+  uint8_t* slot = s.slab + s.slot_off[v];
+  fill_stat(slot, L.zx, L.zx, now_ms, now_ms, 0, 0, 0, eph ? session : 0, dl,
+            0, L.zx);
+  st_be32(slot + ZK_SLOT_LEN, dl > 0 ? dl : -1);
+  copy_bytes(slot + ZK_SLOT_DATA, data, dl);
+  t.node_path_len[v] = npl;
+  s.data_len[v] = dl;
+  t.cver[v] = 0;
+  t.nchild[v] = 0;
+  t.pzxid[v] = L.zx;
+  t.node_parent[v] = par;
+  // No fence before publishing v in the hash: only a same-batch reader of
+  // this very path could observe the half-written node (unordered by the
+  // batch contract; every field it could read is in bounds), and the next
+  // launch sees everything.  A __threadfence here is an XCD-L2 writeback
+  // per wave (MI355X_MICROARCH.md: ~3.5 us each) and cost milliseconds.
+  if (tree_insert(t, v, pd, npl) != v) return ERR_NODE_EXISTS;
+  if (par >= 0) parent_touch(t, par, 1, !seq, L.zx);
+  L.par = par;
+  L.node = v;
+  return ERR_OK;
+}
+
 // Apply one batch of decoded requests; produce reply descriptors for K13.
+// r_path_off/len (may be null) receive the created node's path in the tree's
+// path arena (SEQUENTIAL names differ from the requested one).
 __global__ __launch_bounds__(TR_T) void tree_serve_k(
     ZkTree t, const uint8_t* __restrict__ rx, ZkReqOut q,
     const int64_t* __restrict__ n_dev, int64_t ncap, int32_t* __restrict__ r_op,
     int32_t* __restrict__ r_xid, int32_t* __restrict__ r_err,
     int64_t* __restrict__ r_node, int64_t* __restrict__ r_zxid,
-    int64_t now_ms) {
+    int64_t* __restrict__ r_path_off, int32_t* __restrict__ r_path_len,
+    int64_t session, int64_t now_ms) {
   const int64_t i = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * TR_T +
                     threadIdx.x;
-  if (i >= ncap || i >= *n_dev) return;
-  const int32_t op = q.opcode[i];
-  int32_t err = ERR_OK;
-  int64_t node = -1;
-  int64_t zx = __hip_atomic_load(&t.counters[1], __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_AGENT);
+  const bool live = i < ncap && i < *n_dev;
+  const bool ok_req = live && q.status[i] == ST_OK;
   const ZkNodeStore& s = t.store;
-  if (q.status[i] != ST_OK) {
-    err = -8;                                       // BAD_ARGUMENTS
-  } else {
-    const uint8_t* path = rx + q.path_off[i];
-    const int32_t pl = q.path_len[i];
-    switch (op) {
-      case OP_GET_DATA: case OP_EXISTS:
-        node = tree_find(t, path, pl);
-        if (node < 0) err = ERR_NO_NODE;
-        break;
-      case OP_SET_DATA: {
-        node = tree_find(t, path, pl);
-        if (node < 0) { err = ERR_NO_NODE; break; }
-        const int32_t dl = max(q.data_len[i], 0);
-        if (dl > s.slot_cap[node]) { err = -8; break; }
-        uint8_t* slot = s.slab + s.slot_off[node];
-        unsigned int* ver = (unsigned int*)(slot + 32);
-        const int32_t want = q.arg[i];
-        if (want == -1) {
-          be32_atomic_add(slot + 32, 1);
-        } else if (atomicCAS(ver, bswap32((uint32_t)want),
-                             bswap32((uint32_t)(want + 1))) !=
-                   bswap32((uint32_t)want)) {
-          err = ERR_BAD_VERSION;
-          break;
-        }
-        zx = atomicAdd((unsigned long long*)&t.counters[1], 1ull) + 1;
-        copy_bytes(slot + ZK_SLOT_DATA, rx + q.data_off[i], dl);
-        st_be32(slot + ZK_SLOT_LEN, dl > 0 ? dl : -1);
-        s.data_len[node] = dl;
-        st_be64(slot + 8, zx);                      // mzxid
-        st_be64(slot + 24, now_ms);                 // mtime
-        st_be32(slot + 52, dl);                     // dataLength
-        break;
-      }
-      case OP_CREATE: {
-        int32_t cut = pl - 1;                       // parent must exist
-        while (cut > 0 && path[cut] != '/') --cut;
-        const int64_t par = cut > 0 ? tree_find(t, path, cut) : -1;
-        if (cut > 0 && par < 0) { err = ERR_NO_NODE; break; }
-        if (tree_find(t, path, pl) >= 0) { err = ERR_NODE_EXISTS; break; }
-        const int32_t dl = max(q.data_len[i], 0);
-        const int32_t cap = max(dl, 128);
-        const int64_t v = atomicAdd((unsigned long long*)&t.counters[0], 1ull);
-        const int64_t po = atomicAdd((unsigned long long*)&t.counters[2],
-                                     (unsigned long long)pl);
-        const int64_t so = atomicAdd((unsigned long long*)&t.counters[3],
-                                     (unsigned long long)slot_bytes(cap));
-        if (v >= s.cap || po + pl > t.path_cap ||
-            so + slot_bytes(cap) > t.slab_cap) {
-          err = -1;                                 // SYSTEM_ERROR: full
-          break;
-        }
-        copy_bytes(t.path_arena + po, path, pl);
-        uint8_t* slot = s.slab + so;
-        zx = atomicAdd((unsigned long long*)&t.counters[1], 1ull) + 1;
-        fill_stat(slot, zx, zx, now_ms, now_ms, 0, 0, 0, 0, dl, 0, zx);
-        st_be32(slot + ZK_SLOT_LEN, dl > 0 ? dl : -1);
-        copy_bytes(slot + ZK_SLOT_DATA, rx + q.data_off[i], dl);
+  Lane L;
+  L.op = live ? q.opcode[i] : OP_PING;
+  L.err = live && !ok_req ? ERR_BAD_ARGUMENTS : ERR_OK;
+  L.node = -1;
+  L.par = -1;
+  L.flags = 0;
+  L.path = nullptr;
+  L.pl = L.dl = 0;
+  if (ok_req) {
+    L.path = rx + q.path_off[i];
+    L.pl = q.path_len[i];
+    L.dl = max(q.data_len[i], 0);
+    L.flags = q.arg[i];
+  }
+  // ---- phase A: wave-aggregated claims -----------------------------------
+  // zxids without atomics: write i of the batch is txn base + i + 1, reads
+  // see base; tree_publish_k advances the counter by the batch size.
+  const bool write = ok_req && (L.op == OP_CREATE || L.op == OP_SET_DATA ||
+                                L.op == OP_DELETE);
+  const int64_t zbase = t.counters[TC_ZXID];
+  L.zx = write ? zbase + i + 1 : zbase;
+  const bool create = ok_req && L.op == OP_CREATE;
+  int64_t v = -1;
+  int32_t npl = 0, cap = 0;
+  if (create) {
+    npl = L.pl + ((L.flags & CF_SEQUENTIAL) ? 10 : 0);
+    cap = max(L.dl, 128);
+  }
+  {
+    const int64_t pub = t.counters[TC_FREE_PUB];
+    const int64_t h = block_ticket(&t.counters[TC_FREE_HEAD], create);
+    if (create && h < pub) v = t.free_list[h % t.free_cap];
+    const bool fresh = create && v < 0;
+    const int64_t nv = block_ticket(&t.counters[TC_NODES], fresh);
+    if (fresh && nv < s.cap) v = nv;
+    // storage: reuse the recycled node's when it fits
+    const bool new_path = v >= 0 && (fresh || npl > t.node_path_len[v]);
+    const bool new_slot = v >= 0 && (fresh || cap > s.slot_cap[v]);
+    const int64_t po = wave_bytes(&t.counters[TC_PATH_TOP],
+                                  new_path ? npl : 0);
+    const int64_t sb = new_slot ? slot_bytes(cap) : 0;
+    const int64_t so = wave_bytes(&t.counters[TC_SLAB_TOP], sb);
+    if (new_path) {
+      if (po + npl <= t.path_cap) {
         t.node_path_off[v] = po;
-        t.node_path_len[v] = pl;
-        t.node_parent[v] = par;
+        t.node_path_len[v] = npl;
+      } else {
+        t.node_path_len[v] = 0;                     // storage-less free node
+      }
+    }
+    if (new_slot) {
+      if (so + sb <= t.slab_cap) {
         s.slot_off[v] = so;
         s.slot_cap[v] = cap;
-        s.data_len[v] = dl;
-        __threadfence();
-        const int64_t got = tree_insert(t, v, t.path_arena + po, pl);
-        if (got != v) { err = ERR_NODE_EXISTS; break; }
-        if (par >= 0) {
-          uint8_t* ps = s.slab + s.slot_off[par];
-          be32_atomic_add(ps + 36, 1);              // cversion
-          be32_atomic_add(ps + 56, 1);              // numChildren
-          st_be64(ps + 60, zx);                     // pzxid (last writer)
+      } else {
+        s.slot_cap[v] = -1;
+      }
+    }
+    if (v >= 0 && ((new_path && po + npl > t.path_cap) ||
+                   (new_slot && so + sb > t.slab_cap))) {
+      L.err = ERR_SYSTEM;                           // arena full
+    }
+  }
+  // ---- phase B: the operation -------------------------------------------
+  int64_t freed = -1;
+  if (ok_req && L.err == ERR_OK) {
+    switch (L.op) {
+      case OP_GET_DATA: case OP_EXISTS:
+        L.node = tree_find(t, L.path, L.pl);
+        if (L.node < 0) L.err = ERR_NO_NODE;
+        break;
+      case OP_SET_DATA: {
+        const int64_t node = tree_find(t, L.path, L.pl);
+        if (node < 0) { L.err = ERR_NO_NODE; break; }
+        if (L.dl > s.slot_cap[node]) { L.err = ERR_BAD_ARGUMENTS; break; }
+        uint8_t* slot = s.slab + s.slot_off[node];
+        unsigned int* ver = (unsigned int*)(slot + 32);
+        const int32_t want = L.flags;
+        unsigned int old = *ver, cmp;
+        do {                                          // version CAS
+          cmp = old;
+          if (want != -1 && cmp != bswap32((uint32_t)want)) break;
+          old = atomicCAS(ver, cmp, bswap32(bswap32(cmp) + 1));
+        } while (old != cmp);
+        if (old != cmp || (want != -1 && cmp != bswap32((uint32_t)want))) {
+          L.err = ERR_BAD_VERSION;
+          break;
         }
-        node = v;
+        copy_bytes(slot + ZK_SLOT_DATA, rx + q.data_off[i], L.dl);
+        st_be32(slot + ZK_SLOT_LEN, L.dl > 0 ? L.dl : -1);
+        s.data_len[node] = L.dl;
+        st_be64(slot + 8, L.zx);                      // mzxid
+        st_be64(slot + 24, now_ms);                   // mtime
+        st_be32(slot + 52, L.dl);                     // dataLength
+        L.node = node;
         break;
       }
+      case OP_CREATE:
+        L.err = do_create(t, L, rx + q.data_off[i], q.vec_count[i], session,
+                          now_ms, v);
+        if (L.err == ERR_OK && r_path_off != nullptr) {
+          r_path_off[i] = t.node_path_off[v];
+          r_path_len[i] = t.node_path_len[v];
+        }
+        break;
       case OP_DELETE: {
-        node = tree_find(t, path, pl);
-        if (node < 0) { err = ERR_NO_NODE; break; }
-        uint8_t* slot = s.slab + s.slot_off[node];
-        if (ld_be32(slot + 56) > 0) { err = ERR_NOT_EMPTY; node = -1; break; }
-        const int32_t want = q.arg[i];
-        if (want != -1 && ld_be32(slot + 32) != want) {
-          err = ERR_BAD_VERSION; node = -1; break;
+        const int64_t node = tree_find(t, L.path, L.pl);
+        if (node < 0) { L.err = ERR_NO_NODE; break; }
+        if (__hip_atomic_load(&t.nchild[node], __ATOMIC_RELAXED,
+                              __HIP_MEMORY_SCOPE_AGENT) > 0) {
+          L.err = ERR_NOT_EMPTY;
+          break;
         }
-        tree_erase(t, node, path, pl);
-        zx = atomicAdd((unsigned long long*)&t.counters[1], 1ull) + 1;
-        const int64_t par = t.node_parent[node];
-        if (par >= 0) {
-          uint8_t* ps = s.slab + s.slot_off[par];
-          be32_atomic_add(ps + 36, 1);
-          be32_atomic_add(ps + 56, -1);
-          st_be64(ps + 60, zx);
+        const int32_t want = L.flags;
+        if (want != -1 && ld_be32(s.slab + s.slot_off[node] + 32) != want) {
+          L.err = ERR_BAD_VERSION;
+          break;
         }
-        node = -1;
+        if (!tree_erase(t, node, L.path, L.pl)) { L.err = ERR_NO_NODE; break; }
+        L.par = t.node_parent[node];
+        if (L.par >= 0) parent_touch(t, L.par, -1, true, L.zx);
+        st_be64(s.slab + s.slot_off[node] + 44, 0);   // ephemeralOwner
+        freed = node;
         break;
       }
       case OP_SYNC: case OP_PING:
         break;
       default:
-        err = -6;                                   // UNIMPLEMENTED
+        L.err = ERR_UNIMPLEMENTED;
     }
   }
-  r_op[i] = op;
+  // ---- phase C: wave-aggregated frees and dirty parents -----------------
+  if (create && L.err != ERR_OK && v >= 0) freed = v;  // return the claim
+  wave_free(t, freed);
+  wave_mark_dirty(t, L.err == ERR_OK ? L.par : -1);
+  if (!live) return;
+  r_op[i] = L.op;
   r_xid[i] = q.xid[i];
-  r_err[i] = err;
-  r_node[i] = node;
-  r_zxid[i] = zx;
+  r_err[i] = L.err;
+  r_node[i] = L.op == OP_DELETE ? -1 : L.node;
+  r_zxid[i] = L.zx;
+}
+
+// Rewrite the wire-format Stat words of every dirty parent from the shadows.
+__global__ __launch_bounds__(TR_T) void tree_fixup_k(ZkTree t, int64_t ncap) {
+  const int64_t k = (int64_t)blockIdx.x * TR_T + threadIdx.x;
+  if (k >= ncap || k >= t.counters[TC_DIRTY]) return;
+  const int64_t p = t.dirty_list[k];
+  uint8_t* slot = t.store.slab + t.store.slot_off[p];
+  st_be32(slot + 36, t.cver[p]);
+  st_be32(slot + 56, t.nchild[p]);
+  st_be64(slot + 60, t.pzxid[p]);
+  t.dirty[p] = 0;
+}
+
+// Between batches: make the nodes freed by the last launch poppable, clamp
+// a head that overshot the previously published tail, reset the dirty list
+// and consume the launch's zxids (`*n_dev` for a batch of requests, 1 for a
+// session expiry, which is one closeSession txn).
+__global__ void tree_publish_k(ZkTree t, const int64_t* n_dev,
+                               int64_t bump_zxid) {
+  int64_t* c = t.counters;
+  if (c[TC_FREE_HEAD] > c[TC_FREE_PUB]) c[TC_FREE_HEAD] = c[TC_FREE_PUB];
+  c[TC_FREE_PUB] = c[TC_FREE_TAIL];
+  c[TC_DIRTY] = 0;
+  c[TC_ZXID] += n_dev != nullptr ? *n_dev : bump_zxid;
+}
+
+// Session expiry: remove every ephemeral node owned by `session`
+// (lib/zk-session.js expiry; the server side deletes the session's
+// ephemerals as ONE closeSession txn: all removals share zxid + 1).  One
+// pass over the node table; `removed` counts deletions.
+__global__ __launch_bounds__(TR_T) void tree_expire_k(
+    ZkTree t, int64_t session, int64_t ncap,
+    unsigned long long* __restrict__ removed) {
+  const int64_t v = (int64_t)blockIdx.x * TR_T + threadIdx.x;
+  const ZkNodeStore& s = t.store;
+  bool hit = v < ncap && v < t.counters[TC_NODES] &&
+             t.node_parent[v] != NODE_FREE &&
+             ld_be64(s.slab + s.slot_off[v] + 44) == session;
+  const int64_t zx = t.counters[TC_ZXID] + 1;
+  int64_t par = -1;
+  if (hit) {
+    hit = tree_erase(t, v, t.path_arena + t.node_path_off[v],
+                     t.node_path_len[v]);
+    if (hit) {
+      par = t.node_parent[v];
+      if (par >= 0) parent_touch(t, par, -1, true, zx);
+      st_be64(s.slab + s.slot_off[v] + 44, 0);
+    }
+  }
+  wave_free(t, hit ? v : -1);
+  wave_mark_dirty(t, par);
+  block_ticket((int64_t*)removed, hit);
 }
 
 }  // namespace zk
@@ -326,16 +588,38 @@ int zk_tree_build(const ZkTree* t, int64_t n0, int64_t n, hipStream_t st) {
   return 0;
 }
 
+static int finish_launch(const ZkTree* t, int64_t ncap, const int64_t* n_dev,
+                         int64_t bump_zxid, hipStream_t st) {
+  zk::tree_fixup_k<<<(unsigned)((ncap + zk::TR_T - 1) / zk::TR_T), zk::TR_T,
+                     0, st>>>(*t, ncap);
+  ZK_LAUNCH_CHECK();
+  zk::tree_publish_k<<<1, 1, 0, st>>>(*t, n_dev, bump_zxid);
+  ZK_LAUNCH_CHECK();
+  return 0;
+}
+
 int zk_tree_serve(const ZkTree* t, const uint8_t* rx, const ZkReqOut* q,
                   const int64_t* n_dev, int64_t ncap, int32_t* r_op,
                   int32_t* r_xid, int32_t* r_err, int64_t* r_node,
-                  int64_t* r_zxid, int64_t now_ms, hipStream_t st) {
+                  int64_t* r_zxid, int64_t* r_path_off, int32_t* r_path_len,
+                  int64_t session, int64_t now_ms, hipStream_t st) {
   if (ncap <= 0) return 0;
   zk::tree_serve_k<<<(unsigned)((ncap + zk::TR_T - 1) / zk::TR_T), zk::TR_T,
                      0, st>>>(*t, rx, *q, n_dev, ncap, r_op, r_xid, r_err,
-                              r_node, r_zxid, now_ms);
+                              r_node, r_zxid, r_path_off, r_path_len, session,
+                              now_ms);
   ZK_LAUNCH_CHECK();
-  return 0;
+  // at most one dirty parent per request
+  return finish_launch(t, ncap, n_dev, 0, st);
+}
+
+int zk_tree_expire(const ZkTree* t, int64_t session, int64_t ncap,
+                   unsigned long long* removed, hipStream_t st) {
+  if (ncap <= 0) return 0;
+  zk::tree_expire_k<<<(unsigned)((ncap + zk::TR_T - 1) / zk::TR_T), zk::TR_T,
+                      0, st>>>(*t, session, ncap, removed);
+  ZK_LAUNCH_CHECK();
+  return finish_launch(t, ncap, nullptr, 1, st);
 }
 
 }  // extern "C"

@@ -27,8 +27,13 @@ enum : int32_t {
 enum : int32_t {
   XID_NOTIFICATION = -1, XID_PING = -2, XID_AUTH = -4, XID_SET_WATCHES = -8
 };
-enum : int32_t { ERR_OK = 0, ERR_NO_NODE = -101, ERR_BAD_VERSION = -103,
-                 ERR_NODE_EXISTS = -110, ERR_NOT_EMPTY = -111 };
+enum : int32_t { ERR_OK = 0, ERR_SYSTEM = -1, ERR_UNIMPLEMENTED = -6,
+                 ERR_BAD_ARGUMENTS = -8, ERR_NO_NODE = -101,
+                 ERR_BAD_VERSION = -103, ERR_NO_CHILDREN_FOR_EPHEMERALS = -108,
+                 ERR_NODE_EXISTS = -110, ERR_NOT_EMPTY = -111,
+                 ERR_INVALID_ACL = -114 };
+// CREATE flags (lib/zk-buffer.js createFlags mapping)
+enum : int32_t { CF_EPHEMERAL = 1, CF_SEQUENTIAL = 2 };
 // per-record decode status
 enum : int32_t { ST_OK = 0, ST_BAD_DECODE = 1, ST_NO_XID = 2,
                  ST_BAD_OPCODE = 3 };

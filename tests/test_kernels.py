@@ -242,9 +242,9 @@ def test_decode_requests_matches_oracle(gpu):
             assert cols['vec_count'][i] == len(w['acl'])
 
 
-def _small_tree(gpu, n=5000, data=100):
+def _small_tree(gpu, n=5000, data=100, spare=0.25):
     from zkmi.bench.synthetic import GpuTree
-    return GpuTree(n, data, fanout=100, device=gpu)
+    return GpuTree(n, data, fanout=100, device=gpu, spare=spare)
 
 
 def test_encode_responses_matches_oracle(gpu):
@@ -323,16 +323,18 @@ def test_gpu_tree_mutations(gpu):
         {'xid': 1, 'opcode': 'SET_DATA', 'path': '/bench/d000000/n000000004',
          'data': b'x', 'version': 7},                        # BAD_VERSION
         {'xid': 2, 'opcode': 'CREATE', 'path': '/bench/d000000/new',
-         'data': b'hello', 'acl': [], 'flags': []},
+         'data': b'hello', 'acl': jute.DEFAULT_ACL, 'flags': []},
         {'xid': 3, 'opcode': 'CREATE', 'path': '/nope/x', 'data': b'',
-         'acl': [], 'flags': []},                            # NO_NODE
+         'acl': jute.DEFAULT_ACL, 'flags': []},                            # NO_NODE
         {'xid': 4, 'opcode': 'CREATE', 'path': leaf, 'data': b'',
-         'acl': [], 'flags': []},                            # NODE_EXISTS
+         'acl': jute.DEFAULT_ACL, 'flags': []},                            # NODE_EXISTS
         {'xid': 5, 'opcode': 'DELETE', 'path': '/bench/d000000/n000000005',
          'version': -1},
         {'xid': 6, 'opcode': 'GET_DATA', 'path': '/bench/d000000/missing',
          'watch': False},                                    # NO_NODE
         {'xid': 7, 'opcode': 'EXISTS', 'path': '/bench', 'watch': False},
+        {'xid': 8, 'opcode': 'CREATE', 'path': '/bench/d000000/noacl',
+         'data': b'', 'acl': [], 'flags': []},               # INVALID_ACL
     ]
     s = b''.join(jute.frame(jute.encode_request(p)) for p in pk)
     buf = _dev_bytes(s, gpu)
@@ -345,7 +347,7 @@ def test_gpu_tree_mutations(gpu):
     reps = [jute.decode_response(rx[o:o + ln], xmap) for o, ln in frames]
     errs = [r['err'] for r in reps]
     assert errs == ['OK', 'BAD_VERSION', 'OK', 'NO_NODE', 'NODE_EXISTS',
-                    'OK', 'NO_NODE', 'OK']
+                    'OK', 'NO_NODE', 'OK', 'INVALID_ACL']
     assert reps[0]['stat'].version == 1 and reps[0]['stat'].dataLength == 4
     assert reps[2]['path'] == '/bench/d000000/new'
     assert reps[7]['stat'].numChildren == 10
@@ -396,3 +398,104 @@ def test_handshake_records_k9(gpu):
     for i, p in enumerate(resps):
         assert sid[i] == p['sessionId']
         assert s[po[i]:po[i] + pl[i]] == p['passwd']
+
+
+def test_gpu_free_ring_recycles_nodes(gpu):
+    """DELETE pushes the node on the free ring, the NEXT batch's CREATE pops
+    it (same batch never does) and reuses its slot and path storage."""
+    from zkmi.bench.synthetic import GpuServer
+    from zkmi.ops import _lib
+    tree = _small_tree(gpu, 1000, 16)
+    srv = GpuServer(tree, 64, 1 << 16)
+    leaf = '/bench/d000000/n000000007'
+    v = tree.find_host(leaf)
+    hw = int(tree.counters[_lib.TC_NODES].item())
+
+    def serve(pk):
+        s = b''.join(jute.frame(jute.encode_request(p)) for p in pk)
+        out, total, _, _ = srv.serve(_dev_bytes(s, gpu), len(s))
+        rx = bytes(out[:total.item()].cpu().numpy().tobytes())
+        frames, _, _ = jute.scan_frames(rx)
+        xmap = {p['xid']: p['opcode'] for p in pk}
+        return [jute.decode_response(rx[o:o + ln], xmap) for o, ln in frames]
+    reps = serve([{'xid': 1, 'opcode': 'DELETE', 'path': leaf,
+                   'version': 0},
+                  {'xid': 2, 'opcode': 'DELETE', 'path': leaf,
+                   'version': -1}])
+    # exactly one of two concurrent deletes of the same node wins
+    assert sorted(r['err'] for r in reps) == ['NO_NODE', 'OK']
+    assert tree.find_host(leaf) == -1
+    reps = serve([{'xid': 3, 'opcode': 'CREATE', 'path':
+                   '/bench/d000000/recycled01', 'data': b'r' * 20,
+                   'acl': jute.DEFAULT_ACL, 'flags': []}])
+    assert reps[0]['err'] == 'OK'
+    assert tree.find_host('/bench/d000000/recycled01') == v
+    assert int(tree.counters[_lib.TC_NODES].item()) == hw   # no growth
+    data, st = tree.node_slot_host(v)
+    assert data == b'r' * 20 and st.version == 0
+
+
+def test_gpu_ephemeral_sequential_and_expire(gpu):
+    """SEQUENTIAL appends the parent's cversion as %010d, EPHEMERAL records
+    the session, children of ephemerals are refused, and expiring the
+    session removes exactly its ephemerals."""
+    from zkmi.bench.synthetic import GpuServer
+    tree = _small_tree(gpu, 1000, 16)
+    srv = GpuServer(tree, 64, 1 << 16)
+    E = ['EPHEMERAL']
+    ES = ['EPHEMERAL', 'SEQUENTIAL']
+
+    def serve(pk, session):
+        s = b''.join(jute.frame(jute.encode_request(p)) for p in pk)
+        out, total, _, _ = srv.serve(_dev_bytes(s, gpu), len(s),
+                                     session=session)
+        rx = bytes(out[:total.item()].cpu().numpy().tobytes())
+        frames, _, _ = jute.scan_frames(rx)
+        xmap = {p['xid']: p['opcode'] for p in pk}
+        return [jute.decode_response(rx[o:o + ln], xmap) for o, ln in frames]
+
+    def create(x, path, flags):
+        return {'xid': x, 'opcode': 'CREATE', 'path': path, 'data': b'e',
+                'acl': jute.DEFAULT_ACL, 'flags': flags}
+    reps = serve([create(i, '/bench/d000001/q-', ES) for i in range(5)] +
+                 [create(9, '/bench/d000001/eph', E)], session=0x1234)
+    assert all(r['err'] == 'OK' for r in reps)
+    seqs = sorted(r['path'] for r in reps[:5])
+    # d000001 has 100 children, cversion 100 after the fill
+    assert seqs == ['/bench/d000001/q-%010d' % k for k in range(100, 105)]
+    reps = serve([create(10, '/bench/d000001/eph/child', [])], session=0x1234)
+    assert reps[0]['err'] == 'NO_CHILDREN_FOR_EPHEMERALS'
+    reps = serve([create(11, '/bench/d000001/other', E)], session=0x999)
+    v = tree.find_host('/bench/d000001/eph')
+    assert tree.node_slot_host(v)[1].ephemeralOwner == 0x1234
+    removed = tree.expire(0x1234)
+    assert int(removed.item()) == 6
+    assert tree.find_host('/bench/d000001/eph') == -1
+    assert tree.find_host('/bench/d000001/other') >= 0
+    reps = serve([{'xid': 12, 'opcode': 'EXISTS', 'path': '/bench/d000001',
+                   'watch': False}], session=0)
+    assert reps[0]['stat'].numChildren == 101
+
+
+def test_gpu_mix_pipeline(gpu):
+    from zkmi.bench.synthetic import MixPipeline
+    from zkmi.ops import _lib
+    tree = _small_tree(gpu, 20000, 37, spare=1.0)
+    pipe = MixPipeline(tree, 3 * 4096, ndirs=64)
+    hw = None
+    for s in range(6):
+        ok = pipe.step()
+        assert int(ok.item()) == 3 * 4096
+        if s == 2:
+            hw = int(tree.counters[_lib.TC_NODES].item())
+    # steady state: recycled nodes, no growth of the node table
+    assert int(tree.counters[_lib.TC_NODES].item()) == hw
+
+
+def test_gpu_storm_pipeline(gpu):
+    from zkmi.bench.synthetic import StormPipeline
+    tree = _small_tree(gpu, 20000, 37, spare=1.0)
+    pipe = StormPipeline(tree, 8192, ndirs=64)
+    for _ in range(12):                 # crosses at least one rehash
+        ok = pipe.step()
+        assert int(ok.item()) == 8192

@@ -8,8 +8,10 @@ OUT=gpurun_out
 mkdir -p $OUT
 timeout -k 10 300 python -m pytest tests -x -q -m gpu > $OUT/gpu_tests.log 2>&1
 rc=$?; tail -3 $OUT/gpu_tests.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 600 python -m pytest tests -x -q -m "not gpu" > $OUT/cpu_tests.log 2>&1
-rc=$?; tail -3 $OUT/cpu_tests.log; [ $rc -eq 0 ] || exit $rc
+if [ -z "$SKIP_CPU" ]; then
+  timeout -k 10 600 python -m pytest tests -x -q -m "not gpu" > $OUT/cpu_tests.log 2>&1
+  rc=$?; tail -3 $OUT/cpu_tests.log; [ $rc -eq 0 ] || exit $rc
+fi
 timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
 rc=$?; tail -1 $OUT/smoke.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python bench.py ${BENCH_ARGS:-} > $OUT/bench.log 2>&1

@@ -78,7 +78,8 @@ class GpuTree(object):
         poff = np.zeros(nst, np.int64)
         np.cumsum(plen[:-1], out=poff[1:])
         arena = b''.join(enc)
-        self.path_cap = int(len(arena) * (1 + spare)) + (1 << 16)
+        # every spare node may need a fresh path (up to 64 bytes each)
+        self.path_cap = len(arena) + (cap - nst) * 64 + (1 << 16)
         self.path_arena = torch.zeros(self.path_cap, dtype=U8, device=dev)
         self.path_arena[:len(arena)] = torch.frombuffer(
             bytearray(arena), dtype=U8).to(dev)
@@ -109,8 +110,18 @@ class GpuTree(object):
         hcap = _next_pow2(2 * cap)
         self.keys = torch.zeros(hcap, dtype=I64, device=dev)
         self.vals = torch.full((hcap,), -3, dtype=I64, device=dev)
-        self.counters = torch.tensor([nst, nst, len(arena), nst * sb],
-                                     dtype=I64, device=dev)
+        cnt = [0] * _lib.TC_N
+        cnt[_lib.TC_NODES], cnt[_lib.TC_ZXID] = nst, nst
+        cnt[_lib.TC_PATH_TOP], cnt[_lib.TC_SLAB_TOP] = len(arena), nst * sb
+        self.counters = torch.tensor(cnt, dtype=I64, device=dev)
+        self.free_list = torch.empty(cap, dtype=I64, device=dev)
+        # host-endian cversion / numChildren / pzxid shadows + dirty list
+        self.cver = torch.zeros(cap, dtype=I32, device=dev)
+        self.nchild = torch.zeros(cap, dtype=I32, device=dev)
+        self.pzxid = torch.zeros(cap, dtype=I64, device=dev)
+        self.dirty = torch.zeros(cap, dtype=I32, device=dev)
+        self.dirty_list = torch.empty(cap, dtype=I64, device=dev)
+        self.hcap = hcap
         self._struct = self._make_struct(hcap - 1)
         sp = _lib.stream_ptr()
         _lib.check(L.zk_tree_fill(ctypes.byref(self._struct), 0, nst,
@@ -130,11 +141,52 @@ class GpuTree(object):
                            self.node_path_len.data_ptr(),
                            self.node_parent.data_ptr(),
                            self.path_arena.data_ptr(), self.path_cap,
-                           self.slab_cap, self.counters.data_ptr(), st)
+                           self.slab_cap, self.counters.data_ptr(), st,
+                           self.free_list.data_ptr(), self.cap,
+                           self.cver.data_ptr(), self.nchild.data_ptr(),
+                           self.pzxid.data_ptr(), self.dirty.data_ptr(),
+                           self.dirty_list.data_ptr())
 
     @property
     def struct(self):
         return self._struct
+
+    def expire(self, session, removed=None):
+        """Delete every ephemeral node owned by ``session`` (server side of
+        session expiry).  ``removed`` (device int64 [1]) accumulates the
+        number of nodes removed."""
+        if removed is None:
+            removed = torch.zeros(1, dtype=I64, device=self.device)
+        _lib.check(_lib.lib().zk_tree_expire(
+            ctypes.byref(self._struct), session, self.cap, _lib.ptr(removed),
+            _lib.stream_ptr()), 'zk_tree_expire')
+        return removed
+
+    def rehash(self):
+        """Rebuild the hash index from the live nodes (drops tombstones left
+        by deleted paths that are never re-created, e.g. SEQUENTIAL names).
+        One host read of the node high-water mark."""
+        n = int(self.counters[_lib.TC_NODES].item())
+        self.keys.zero_()
+        self.vals.fill_(-3)
+        _lib.check(_lib.lib().zk_tree_build(ctypes.byref(self._struct), 0,
+                                            min(n, self.cap),
+                                            _lib.stream_ptr()),
+                   'zk_tree_build')
+
+    def find_host(self, path):
+        """Node index of ``path`` (host scan of the path table; tests)."""
+        n = min(int(self.counters[_lib.TC_NODES].item()), self.cap)
+        want = path.encode()
+        po = self.node_path_off[:n].cpu().numpy()
+        pl = self.node_path_len[:n].cpu().numpy()
+        par = self.node_parent[:n].cpu().numpy()
+        arena = self.path_arena.cpu().numpy().tobytes()
+        for v in range(n):
+            if par[v] != -2 and pl[v] == len(want) and \
+                    arena[po[v]:po[v] + pl[v]] == want:
+                return v
+        return -1
 
     def node_slot_host(self, v):
         """(data bytes, Stat) of node ``v`` read back from HBM (tests)."""
@@ -155,31 +207,37 @@ class GpuServer(object):
         self.tree = tree
         dev = tree.device
         self.rt = B.alloc_request_table(cap_frames, dev)
+        # CREATE replies carry the created path from the tree's arena
+        # (a SEQUENTIAL name differs from the requested one)
         self.resp = B.ResponseBatch(
             torch.empty(cap_frames, dtype=I32, device=dev),
             torch.empty(cap_frames, dtype=I32, device=dev),
             torch.empty(cap_frames, dtype=I32, device=dev),
             torch.empty(cap_frames, dtype=I64, device=dev),
             torch.empty(cap_frames, dtype=I64, device=dev),
-            None, None, None,
+            torch.zeros(cap_frames, dtype=I64, device=dev),
+            torch.zeros(cap_frames, dtype=I32, device=dev),
+            tree.path_arena,
             torch.zeros(cap_frames, dtype=I32, device=dev), None)
         self.out = torch.empty(out_cap, dtype=U8, device=dev)
         self.cap_frames = cap_frames
         self.ws = None
 
-    def serve(self, rx, n):
+    def serve(self, rx, n, session=0):
+        """Serve the request stream ``rx[:n]`` for ``session`` (the owner of
+        any EPHEMERAL node it creates)."""
         L = _lib.lib()
         ft = B.frame_scan(rx, n, cap=self.cap_frames, workspace=self.ws)
         rt = B.decode_requests(rx, ft, out=self.rt)
         r = self.resp
-        r.path_off, r.path_len, r.path_arena = rt.path_off, rt.path_len, rx
         r.count = ft.count
         q = rt.struct()
         _lib.check(L.zk_tree_serve(
             ctypes.byref(self.tree.struct), _lib.ptr(rx), ctypes.byref(q),
             _lib.ptr(ft.count), self.cap_frames, _lib.ptr(r.opcode),
             _lib.ptr(r.xid), _lib.ptr(r.err), _lib.ptr(r.node),
-            _lib.ptr(r.zxid), int(time.time() * 1000), _lib.stream_ptr()),
+            _lib.ptr(r.zxid), _lib.ptr(r.path_off), _lib.ptr(r.path_len),
+            session, int(time.time() * 1000), _lib.stream_ptr()),
             'zk_tree_serve')
         out, rec_off, total, err = B.encode_responses(
             r, self.tree.store, self.out.numel(), out=self.out)
@@ -244,3 +302,275 @@ class GetPipeline(object):
                   (rep.pay_len[:n] == t.data_len[idx]))
             return ok.sum()
         return None
+
+
+def _arena(strings, dev):
+    """Pack host strings into (arena u8, off i64, len i32) device tensors."""
+    enc = [x.encode() for x in strings]
+    ln = np.fromiter((len(e) for e in enc), np.int32, len(enc))
+    off = np.zeros(len(enc), np.int64)
+    if len(enc) > 1:
+        np.cumsum(ln[:-1], out=off[1:])
+    blob = b''.join(enc) or b'\0'
+    arena = torch.frombuffer(bytearray(blob), dtype=U8).to(dev)
+    return arena, torch.from_numpy(off).to(dev), torch.from_numpy(ln).to(dev)
+
+
+def _acl_table(acls, dev):
+    blobs = [B._acl_bytes(a) for a in acls]
+    raw = b''.join(blobs)
+    lens = np.array([len(b) for b in blobs], np.int32)
+    offs = np.zeros(len(blobs), np.int64)
+    np.cumsum(lens[:-1], out=offs[1:])
+    arena = torch.frombuffer(bytearray(raw), dtype=U8).to(dev)
+    return arena, torch.from_numpy(offs).to(dev), torch.from_numpy(lens).to(dev)
+
+
+# ACLs the mix alternates between (K10 encodes them from the pre-encoded
+# vectors; the server rejects an empty one with INVALID_ACL)
+MIX_ACLS = (
+    [{'perms': consts.PERM_ALL, 'id': {'scheme': 'world', 'id': 'anyone'}}],
+    [{'perms': ['READ'], 'id': {'scheme': 'world', 'id': 'anyone'}},
+     {'perms': consts.PERM_ALL, 'id': {'scheme': 'digest',
+                               'id': 'bench:kQq8nOxk1NC8y2GdzFjp0v4ZbVY='}}],
+)
+
+
+class _Driver(object):
+    """Client half shared by the write pipelines: K10 encode of a request
+    batch (xids recorded in the HBM xid table), the GPU server, then K1 +
+    K2-K8 decode of the reply stream."""
+
+    def __init__(self, tree, batch, max_path, data_bytes, seed):
+        self.tree = tree
+        self.batch = batch
+        self.dev = dev = tree.device
+        self.xt = B.XidTable(bits=max(20, (batch - 1).bit_length() + 1),
+                             device=dev)
+        self.tx = torch.empty(batch * (33 + max_path + data_bytes + 128) + 64,
+                              dtype=U8, device=dev)
+        dmax = max(tree.data_bytes, 128, data_bytes)
+        self.server = GpuServer(
+            tree, batch, batch * (4 + 16 + 4 + max(dmax, max_path + 16) + 68)
+            + 64)
+        self.reply = B.alloc_replies(batch, dev)
+        self.xid_base = 0
+        self.iota = torch.arange(batch, dtype=I32, device=dev)
+
+    def xids(self, n):
+        x = (self.iota[:n] + self.xid_base) & 0x7fffffff
+        self.xid_base = (self.xid_base + n) & 0x7fffffff
+        return x
+
+    def create_dirs(self, levels, acl):
+        """CREATE persistent directories, one batch per level (a parent must
+        exist before its children's batch runs).  ``acl`` = (arena, off,
+        len) pre-encoded ACL table."""
+        dev = self.dev
+        aarena, aoff, alen = acl
+        for level in levels:
+            n = len(level)
+            arena, off, ln = _arena(level, dev)
+            z32 = torch.zeros(n, dtype=I32, device=dev)
+            rb = B.RequestBatch(
+                n, torch.full((n,), consts.OP_CODES['CREATE'], dtype=I32,
+                              device=dev),
+                self.xids(n), z32, off, ln,
+                torch.zeros(n, dtype=I64, device=dev), z32, z32, arena,
+                arena, aoff, alen, aarena)
+            rep, _ = self.run(rb)
+            errs = rep.err[:n]
+            if not bool(((errs == 0) |
+                         (errs == consts.ERR_CODES['NODE_EXISTS'])).all()):
+                raise RuntimeError('directory create failed: %r' % (
+                    errs.unique().cpu().tolist(),))
+
+    def run(self, rb, session=0):
+        tx, _, total, _ = B.encode_requests(rb, self.xt, out=self.tx)
+        ntx = int(total.item())
+        rx, rtotal, _, _ = self.server.serve(tx, ntx, session=session)
+        nrx = int(rtotal.item())
+        ft = B.frame_scan(rx, nrx, cap=self.batch)
+        rep = B.decode_replies(rx, ft, self.xt, out=self.reply)
+        return rep, rx
+
+
+class MixPipeline(object):
+    """create / set(version CAS) / delete mix with ACL encode (BASELINE
+    config 3) over the synthetic tree.
+
+    Every step issues ``m = batch // 3`` of each op on three rotating
+    generations of ``m`` nodes ``/mix/dDDDD/gG_KKKKKKKKK``: step ``s``
+    CREATEs generation ``s % 3`` (alternating two ACL vectors), SET_DATAs
+    generation ``s-1`` with expected version 0 (every 16th with a stale
+    version, which must fail with BAD_VERSION) and DELETEs generation ``s-2``
+    with its exact current version.  Node slots, paths and hash entries are
+    recycled through the tree's free ring, so the tree size is steady.
+    Every reply is checked on the device against its expected error code,
+    xid and opcode (and version 1 for successful sets)."""
+
+    def __init__(self, tree, batch, data_bytes=100, ndirs=1024, seed=0):
+        m = max(batch // 3, 1)
+        self.m = m
+        self.n = 3 * m
+        dev = tree.device
+        self.tree = tree
+        self.ndirs = ndirs
+        paths = ['/mix/d%05d/g%d_%09d' % (k % ndirs, g, k)
+                 for g in range(3) for k in range(m)]
+        maxp = max(len(p) for p in paths)
+        self.drv = _Driver(tree, self.n, maxp, data_bytes, seed)
+        self.path_arena, poff, plen = _arena(paths, dev)
+        g = torch.Generator(device=dev)
+        g.manual_seed(seed + 7)
+        nblk = 1024
+        self.data_arena = torch.randint(0, 256, (nblk * data_bytes + 16,),
+                                        dtype=U8, device=dev, generator=g)
+        self.acl_arena, self.acl_off, self.acl_len = _acl_table(MIX_ACLS, dev)
+        k = torch.arange(m, dtype=I64, device=dev)
+        stale = (k % 16) == 15
+        ops = consts.OP_CODES
+        self.opcode = torch.cat([
+            torch.full((m,), ops['CREATE'], dtype=I32, device=dev),
+            torch.full((m,), ops['SET_DATA'], dtype=I32, device=dev),
+            torch.full((m,), ops['DELETE'], dtype=I32, device=dev)])
+        self.arg = torch.cat([torch.zeros(m, dtype=I64, device=dev),
+                              torch.where(stale, 7, 0),
+                              torch.where(stale, 0, 1)]).to(I32)
+        self.data_off = torch.cat([(k % nblk) * data_bytes,
+                                   ((k + 7) % nblk) * data_bytes,
+                                   torch.zeros(m, dtype=I64, device=dev)])
+        self.data_len = torch.cat([
+            torch.full((2 * m,), data_bytes, dtype=I32, device=dev),
+            torch.zeros(m, dtype=I32, device=dev)])
+        self.acl_id = torch.cat([(k % 2).to(I32),
+                                 torch.zeros(2 * m, dtype=I32, device=dev)])
+        bad = consts.ERR_CODES['BAD_VERSION']
+        self.want_err = torch.cat([
+            torch.zeros(m, dtype=I32, device=dev),
+            torch.where(stale, bad, 0).to(I32),
+            torch.zeros(m, dtype=I32, device=dev)])
+        self.is_set_ok = torch.cat([
+            torch.zeros(m, dtype=torch.bool, device=dev), ~stale,
+            torch.zeros(m, dtype=torch.bool, device=dev)])
+        # path offsets per rotation r = s % 3: (create, set, delete) gens
+        po = poff.view(3, m)
+        self.path_off = [torch.cat([po[r], po[(r - 1) % 3], po[(r - 2) % 3]])
+                         for r in range(3)]
+        self.path_len = plen[:m].repeat(3)
+        self.s = -2
+        self.drv.create_dirs(
+            [['/mix'], ['/mix/d%05d' % d for d in range(ndirs)]],
+            (self.acl_arena, self.acl_off, self.acl_len))
+        # prime: s = -2 creates generation 1, s = -1 creates 2 and sets 1
+        self.step(validate=False, n=m)
+        self.step(validate=False, n=2 * m)
+
+    def _batch(self, n, r):
+        d = self.drv
+        return B.RequestBatch(n, self.opcode[:n], d.xids(n), self.arg[:n],
+                              self.path_off[r][:n], self.path_len[:n],
+                              self.data_off[:n], self.data_len[:n],
+                              self.acl_id[:n], self.path_arena,
+                              self.data_arena, self.acl_off, self.acl_len,
+                              self.acl_arena)
+
+    def step(self, validate=True, n=None):
+        n = self.n if n is None else n
+        rb = self._batch(n, self.s % 3)
+        rep, _ = self.drv.run(rb)
+        self.last = (rb, rep)
+        self.s += 1
+        if not validate:
+            return None
+        ok = ((rep.status[:n] == 0) & (rep.err[:n] == self.want_err[:n]) &
+              (rep.xid[:n] == rb.xid) & (rep.opcode[:n] == rb.opcode) &
+              (~self.is_set_ok[:n] | (rep.stat32[0, :n] == 1)))
+        return ok.sum()
+
+    def diagnose(self):
+        rb, rep = self.last
+        n = rb.n
+        bad = rep.err[:n] != self.want_err[:n]
+        e, c = torch.unique(rep.err[:n][bad], return_counts=True)
+        return {'wrong_err': dict(zip(e.cpu().tolist(), c.cpu().tolist())),
+                'status_bad': int((rep.status[:n] != 0).sum().item()),
+                'counters': self.tree.counters.cpu().tolist()}
+
+
+class StormPipeline(object):
+    """EPHEMERAL|SEQUENTIAL create storm with session expiry (BASELINE
+    config 5, nasty.test.js shape).
+
+    Step ``s``: session ``s+1`` creates ``batch`` ephemeral sequential nodes
+    ``/storm/dDDDDD/e-<seq>`` (the server appends the parent's cversion),
+    then session ``s`` expires and the server removes the ephemerals it
+    created one step earlier.  The hash index is rebuilt whenever the
+    tombstones left by never-reused sequential names would fill it."""
+
+    def __init__(self, tree, batch, ndirs=1024, data_bytes=16, seed=0):
+        dev = tree.device
+        self.tree = tree
+        self.n = batch
+        self.ndirs = ndirs
+        self.drv = _Driver(tree, batch, 32, data_bytes, seed)
+        prefixes = ['/storm/d%05d/e-' % (k % ndirs) for k in range(batch)]
+        self.path_arena, self.path_off, self.path_len = _arena(prefixes, dev)
+        self.data_arena = torch.full((data_bytes + 16,), 0x5a, dtype=U8,
+                                     device=dev)
+        self.acl_arena, self.acl_off, self.acl_len = _acl_table(MIX_ACLS[:1],
+                                                                dev)
+        flags = consts.CREATE_FLAGS['EPHEMERAL'] | \
+            consts.CREATE_FLAGS['SEQUENTIAL']
+        self.opcode = torch.full((batch,), consts.OP_CODES['CREATE'],
+                                 dtype=I32, device=dev)
+        self.arg = torch.full((batch,), flags, dtype=I32, device=dev)
+        self.data_off = torch.zeros(batch, dtype=I64, device=dev)
+        self.data_len = torch.full((batch,), data_bytes, dtype=I32,
+                                   device=dev)
+        self.acl_id = torch.zeros(batch, dtype=I32, device=dev)
+        self.want_len = self.path_len + 10
+        self.removed = torch.zeros(1, dtype=I64, device=dev)
+        self.session = 1
+        self.inserted = 0
+        self.drv.create_dirs(
+            [['/storm'], ['/storm/d%05d' % d for d in range(ndirs)]],
+            (self.acl_arena, self.acl_off, self.acl_len))
+        self.step(validate=False)            # first session's nodes
+
+    def step(self, validate=True):
+        t = self.tree
+        n = self.n
+        if (self.inserted + 2 * n) > 0.6 * t.hcap:
+            t.rehash()
+            self.inserted = 0
+        rb = B.RequestBatch(n, self.opcode, self.drv.xids(n), self.arg,
+                            self.path_off, self.path_len, self.data_off,
+                            self.data_len, self.acl_id, self.path_arena,
+                            self.data_arena, self.acl_off, self.acl_len,
+                            self.acl_arena)
+        rep, _ = self.drv.run(rb, session=self.session + 1)
+        self.last = (rb, rep)
+        self.inserted += n
+        # the previous session expires: its ephemerals go
+        self.removed.zero_()
+        t.expire(self.session, self.removed)
+        self.session += 1
+        if not validate:
+            return None
+        ok = ((rep.status[:n] == 0) & (rep.err[:n] == 0) &
+              (rep.xid[:n] == rb.xid) &
+              (rep.pay_len[:n] == self.want_len)).sum()
+        # the expiry must have removed exactly one step's nodes
+        return torch.where(self.removed[0] == n, ok, 0)
+
+    def diagnose(self):
+        rb, rep = self.last
+        n = self.n
+        e, c = torch.unique(rep.err[:n], return_counts=True)
+        return {'removed': int(self.removed.item()),
+                'err_hist': dict(zip(e.cpu().tolist(), c.cpu().tolist())),
+                'status_bad': int((rep.status[:n] != 0).sum().item()),
+                'pay_len_bad': int((rep.pay_len[:n] != self.want_len)
+                                   .sum().item()),
+                'counters': self.tree.counters.cpu().tolist()}

@@ -63,7 +63,14 @@ class ZkTree(ctypes.Structure):
     _fields_ = [('keys', P), ('vals', P), ('mask', I64),
                 ('node_path_off', P), ('node_path_len', P),
                 ('node_parent', P), ('path_arena', P), ('path_cap', I64),
-                ('slab_cap', I64), ('counters', P), ('store', ZkNodeStore)]
+                ('slab_cap', I64), ('counters', P), ('store', ZkNodeStore),
+                ('free_list', P), ('free_cap', I64), ('cver', P),
+                ('nchild', P), ('pzxid', P), ('dirty', P), ('dirty_list', P)]
+
+
+# ZkTree counters (csrc/kernels/tree.hip TC_*)
+TC_NODES, TC_ZXID, TC_PATH_TOP, TC_SLAB_TOP = 0, 1, 2, 3
+TC_FREE_HEAD, TC_FREE_TAIL, TC_FREE_PUB, TC_DIRTY, TC_N = 4, 5, 6, 7, 8
 
 
 _SIGS = {
@@ -86,7 +93,9 @@ _SIGS = {
                                           P]),
     'zk_tree_build': (I32, [P, I64, I64, P]),
     'zk_tree_fill': (I32, [P, I64, I64, P, I64, P]),
-    'zk_tree_serve': (I32, [P, P, P, P, I64, P, P, P, P, P, I64, P]),
+    'zk_tree_serve': (I32, [P, P, P, P, I64, P, P, P, P, P, P, P, I64, I64,
+                            P]),
+    'zk_tree_expire': (I32, [P, I64, I64, P, P]),
 }
 
 _lib = None

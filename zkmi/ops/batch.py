@@ -248,13 +248,14 @@ def encode_connect_requests(reqs, device=None, stream=None):
     off = torch.empty(max(n, 1), dtype=I64, device=dev)
     total = torch.zeros(1, dtype=I64, device=dev)
     ws = torch.empty(L.zk_scan_workspace(max(n, 1)), dtype=I64, device=dev)
-    cap = n * 36 + len(arena) + 16
+    size = n * 32 + len(arena)           # frame len + 28 fixed + passwd
+    cap = size + 16
     out = torch.empty(cap, dtype=U8, device=dev)
     check(L.zk_encode_connect_requests(
         ptr(proto), ptr(zx), ptr(tmo), ptr(sid), ptr(t_pwo), ptr(t_pwl),
         ptr(t_ar), n, ptr(sizes), ptr(off), ptr(total), ptr(ws), ptr(out),
         stream_ptr(stream)), 'zk_encode_connect_requests')
-    return out[:n * 36 + len(arena)]
+    return out[:size]
 
 
 def decode_connect_responses(buf, frames, n, stream=None):

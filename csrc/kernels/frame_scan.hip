@@ -5,24 +5,26 @@
 // packet (O(bytes x packets)).  The chain is inherently
 // sequential; we make it parallel without speculation errors:
 //
-//  A  fs_exits   one workgroup per 16 KiB tile: stage the tile in LDS, build
-//                next(p) = p + 4 + be32(p) for EVERY byte position, and
-//                pointer-jump (in place, racy but monotone) until each
-//                position maps to the first chain position outside the tile
-//                or to a terminal (bad length / partial frame / end).  Keep
-//                the result for the first W positions of the tile (the only
-//                place a chain can enter when frames are <= W bytes) as a
-//                compact uint16 table.
+//  A  per-tile exit table f0[tile][e] for the W window entry points e (the
+//     only places a chain can enter a tile when frames are <= W bytes):
+//     fs_frontier + fs_survivor (default; merging frontier walk, see below)
+//     or fs_exits (ZKMI_FS_SCAN=jump|double; pointer jumping over every
+//     position of the tile):
+//     fs_exits   one workgroup per 16 KiB tile: build next(p) = p + 4 +
+//                be32(p) for EVERY byte position and pointer-jump (in place,
+//                racy but monotone) until each position maps to the first
+//                chain position outside the tile or to a terminal.
 //  B  fs_compose hierarchical function composition: a level-(l+1) unit is 16
 //                level-l units; for each window entry point, walk the 16
 //                sub-unit functions.  Log-depth, O(W) work per unit.
 //  C  fs_top/fs_down  serial walk over the (few) top units from the stream
 //                start, then push the exact entry position down to every tile.
-//  D  fs_mark    per tile, re-stage and mark the chain from its entry with
-//                doubling (double-buffered, so round r marks distances
-//                [2^r, 2^(r+1)) — complete after log2(frames) rounds); emit a
-//                frame-start bitmap and a count.
-//  E  scan of counts (scan.hip) + fs_write: bitmap -> (body_off, len) table.
+//  D  frame starts per tile from its exact entry: fs_join (default: walk from
+//     the entry to the survivor's hand-off point, then reuse the survivor's
+//     recorded path), fs_walk (jump: wave-uniform walk of the staged tile) or
+//     fs_mark (double: doubling marks on the full tile + bitmap).
+//  E  scan of counts (scan.hip) + fs_write_join / fs_write_list / fs_write:
+//     frame starts -> (body_off, len) table.
 //
 // Frames longer than W (2 KiB) fall back to walking the byte chain in global
 // memory for the tile they land in; results stay exact.  BAD_LENGTH is
@@ -135,19 +137,31 @@ ZK_DEV int64_t apply_level(const FsCtx& c, int l, int64_t u, int64_t P) {
   }
 }
 
-// Stage tile bytes [ts, ts+S+4) into LDS (zero beyond n).
-ZK_DEV void stage_tile(const uint8_t* buf, int64_t n, int64_t ts, uint8_t* sb) {
-  const int64_t lim = min(FS_S + 4, n - ts);
-  for (int64_t k = (int64_t)threadIdx.x * 16; k < FS_S + 16;
-       k += (int64_t)blockDim.x * 16) {
-    if (k + 16 <= lim) {
-      uint4 v; __builtin_memcpy(&v, buf + ts + k, 16);
-      *(uint4*)(sb + k) = v;
-    } else {
-      for (int j = 0; j < 16; ++j)
-        sb[k + j] = (k + j < lim) ? buf[ts + k + j] : 0;
-    }
+// Stage tile bytes [ts, ts+S+16) into LDS (zero beyond n) with NT threads
+// (thread index `tid`).  Full tiles issue ALL their 16-byte loads before the
+// first LDS write: a load -> wait -> ds_write loop serialises one HBM
+// latency per iteration (it made staging the dominant cost of the walks).
+template <int NT>
+ZK_DEV void stage_tile(const uint8_t* buf, int64_t n, int64_t ts, uint8_t* sb,
+                       int tid) {
+  constexpr int CH = (int)(FS_S / 16);        // + one pad chunk at CH
+  constexpr int PER = CH / NT;
+  static_assert(CH % NT == 0, "tile chunks must split evenly");
+  if (ts + FS_S + 16 <= n) {
+    uint4 v[PER];
+#pragma unroll
+    for (int j = 0; j < PER; ++j)
+      __builtin_memcpy(&v[j], buf + ts + 16 * (int64_t)(tid + j * NT), 16);
+    uint4 pad = make_uint4(0, 0, 0, 0);
+    if (tid == 0) __builtin_memcpy(&pad, buf + ts + FS_S, 16);
+#pragma unroll
+    for (int j = 0; j < PER; ++j) *(uint4*)(sb + 16 * (tid + j * NT)) = v[j];
+    if (tid == 0) *(uint4*)(sb + FS_S) = pad;
+    return;
   }
+  const int64_t lim = min(FS_S + 4, n - ts);
+  for (int k = tid; k < FS_S + 16; k += NT)
+    sb[k] = k < lim ? buf[ts + k] : 0;
 }
 
 // next() of every tile position relative to the tile (>= S: leaves tile;
@@ -302,6 +316,241 @@ __global__ __launch_bounds__(FS_T) void fs_exits(const uint8_t* __restrict__ buf
   }
 }
 
+// A' (default) — the same f0 table by a MERGING FRONTIER WALK instead of
+// pointer jumping over all 16 Ki positions.  One walker per window entry
+// e < W starts at e; every round each live walker takes one hop in the
+// staged tile and claims the position it lands on in an owner table.  A
+// walker that lands on a claimed position has the same future as the
+// claimant: it stops and records "merged into <claimant>".  Walkers end on
+// a terminal (bad length / partial frame) or on leaving the tile.
+// Afterwards merge links are resolved by pointer jumping over W entries.
+//
+// Work is O(W + positions claimed) instead of O(S log S): in real streams
+// nearly every speculative entry dies or leaves the tile on its first hop
+// (ASCII or random bytes read as a length are huge) and the rest merge into
+// the true chain within a few hops, so after 1-3 block-wide rounds <= 64
+// walkers remain and wave 0 finishes them alone, one LDS round trip per hop
+// (owner word and next length read together), no block barriers.  The walk
+// is bounded: each hop claims a fresh position, so <= S hops in total.
+constexpr int FE_T = 256;
+constexpr int FE_K = FS_W / FE_T;            // walkers per thread (8)
+constexpr uint16_t F0_MERGE = 0x4000;        // | parent walker id (< 2048)
+constexpr size_t FE_LDS = (FS_S + 16) + FS_S * 2 + FS_W * 2 + 66 * 4;
+
+ZK_DEV bool f0_is_merge(uint16_t v) { return (v & 0xF800) == F0_MERGE; }
+
+// One hop from tile-relative p.  Returns the f0 code when the walk ends
+// here (terminal / leaves the tile), else 0xFFFE and q (in-tile successor).
+constexpr uint16_t FE_GO = 0xFFFE;
+constexpr uint16_t FE_PENDING = 0xFFFD;      // the survivor: fs_survivor
+ZK_DEV uint16_t fe_hop(uint32_t lo, uint32_t hi, int32_t p, int32_t nrel,
+                       int32_t maxp, int32_t& q) {
+  // 32-bit throughout: p < 2^14, len <= maxp <= 2^30, nrel clamped to 2^30
+  const int32_t len = (int32_t)bswap32(__builtin_amdgcn_alignbyte(hi, lo,
+                                                                  p & 3));
+  const int32_t nx = p + 4 + len;
+  if ((p + 4 > nrel) | (len < 0) | (len > maxp) | (nx > nrel))
+    return (uint16_t)(F0_TERM | p);
+  if (nx >= FS_S) {
+    const int32_t x = nx - (int32_t)FS_S;
+    return x < 0x4000 ? (uint16_t)x : F0_ESC;
+  }
+  q = nx;
+  return FE_GO;
+}
+
+ZK_DEV void fe_words(const uint8_t* sb, int32_t p, uint32_t& lo, uint32_t& hi) {
+  const int32_t a = p & ~3;
+  lo = *(const uint32_t*)(sb + a);
+  hi = *(const uint32_t*)(sb + a + 4);
+}
+
+// One 256-thread block per tile.  Block-wide rounds (8 walkers per thread,
+// LDS reads batched) run while more than 64 walkers live; then wave 0 moves
+// the survivors one per lane and hops them together, claiming positions,
+// until one is left; that one is handed to fs_survivor.  Merge links are
+// then resolved (entries rooted at the survivor become FE_PENDING).
+// (A wave-per-tile variant without barriers was slower: 53 KiB of LDS per
+// tile leaves 3 waves per CU, too few to hide the LDS latency chains.)
+__global__ __launch_bounds__(FE_T) void fs_frontier(
+    const uint8_t* __restrict__ buf, int64_t n, int64_t maxp,
+    uint16_t* __restrict__ f0, int32_t* __restrict__ surv) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint8_t* sb = smem;                                      // [S + 16]
+  uint16_t* own = (uint16_t*)(smem + FS_S + 16);           // [S] id+1 / 0
+  uint16_t* res = own + FS_S;                              // [W]
+  uint32_t* hand = (uint32_t*)(res + FS_W);                // [64] + 2 ctrs
+  const int64_t t = blockIdx.x;
+  const int64_t ts = t * FS_S;
+  const int32_t nrel = (int32_t)min(n - ts, (int64_t)1 << 30);
+  const int32_t maxp32 = (int32_t)min(maxp, (int64_t)1 << 30);
+  stage_tile<FE_T>(buf, n, ts, sb, threadIdx.x);
+  for (int k = threadIdx.x; k < FS_S / 8; k += FE_T)
+    ((uint4*)own)[k] = make_uint4(0, 0, 0, 0);
+  if (threadIdx.x < 2) hand[64 + threadIdx.x] = 0;
+  __syncthreads();
+  int32_t pos[FE_K], nq[FE_K];
+  uint32_t act = 0;
+#pragma unroll
+  for (int k = 0; k < FE_K; ++k) {
+    const int32_t e = threadIdx.x + k * FE_T;
+    pos[k] = e;
+    own[e] = (uint16_t)(e + 1);
+    act |= 1u << k;
+  }
+  __syncthreads();
+  // ---- block-wide rounds while many walkers live ------------------------
+  for (int r = 0;; ++r) {
+    // phase 1: hop, then claim the landing position (racy; phase 2 decides).
+    // All of a thread's LDS reads are issued before any of its writes, so
+    // the 8 walkers' round trips overlap instead of chaining.
+    uint32_t lo[FE_K], hi[FE_K];
+#pragma unroll
+    for (int k = 0; k < FE_K; ++k)
+      if (act & (1u << k)) fe_words(sb, pos[k], lo[k], hi[k]);
+    uint16_t code[FE_K];
+#pragma unroll
+    for (int k = 0; k < FE_K; ++k) {
+      nq[k] = 0;
+      code[k] = (act & (1u << k))
+                    ? fe_hop(lo[k], hi[k], pos[k], nrel, maxp32, nq[k])
+                    : FE_GO;
+    }
+    uint16_t o[FE_K];
+#pragma unroll
+    for (int k = 0; k < FE_K; ++k)
+      o[k] = ((act & (1u << k)) && code[k] == FE_GO) ? own[nq[k]] : 0;
+#pragma unroll
+    for (int k = 0; k < FE_K; ++k) {
+      if (!(act & (1u << k))) continue;
+      const int32_t e = threadIdx.x + k * FE_T;
+      if (code[k] != FE_GO) {
+        res[e] = code[k];
+        act &= ~(1u << k);
+      } else if (o[k] != 0) {
+        res[e] = (uint16_t)(F0_MERGE | (o[k] - 1));
+        act &= ~(1u << k);
+      } else {
+        own[nq[k]] = (uint16_t)(e + 1);
+      }
+    }
+    if (__popc(act)) atomicAdd(&hand[64 + (r & 1)], (uint32_t)__popc(act));
+    __syncthreads();
+    const uint32_t live = hand[64 + (r & 1)];
+    if (threadIdx.x == 0) hand[64 + ((r + 1) & 1)] = 0;
+    // phase 2: the last writer of own[q] owns it; the others merge into it
+    uint16_t o2[FE_K];
+#pragma unroll
+    for (int k = 0; k < FE_K; ++k) o2[k] = (act & (1u << k)) ? own[nq[k]] : 0;
+#pragma unroll
+    for (int k = 0; k < FE_K; ++k) {
+      if (!(act & (1u << k))) continue;
+      const int32_t e = threadIdx.x + k * FE_T;
+      if (o2[k] != (uint16_t)(e + 1)) {
+        res[e] = (uint16_t)(F0_MERGE | (o2[k] - 1));
+        act &= ~(1u << k);
+      } else {
+        pos[k] = nq[k];
+      }
+    }
+    if (live <= 64) break;
+    __syncthreads();                    // counter reset visible next round
+  }
+  // ---- hand the survivors to wave 0 ---------------------------------------
+  __syncthreads();
+  if (threadIdx.x == 0) hand[64] = 0;
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < FE_K; ++k) {
+    if (!(act & (1u << k))) continue;
+    const uint32_t slot = atomicAdd(&hand[64], 1u);
+    hand[slot] = ((uint32_t)(threadIdx.x + k * FE_T) << 16) | (uint32_t)pos[k];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) surv[t] = -1;
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    const int cnt = (int)hand[64];
+    bool a = lane < cnt;
+    int32_t e = 0, p = 0;
+    if (a) {
+      e = (int32_t)(hand[lane] >> 16);
+      p = (int32_t)(hand[lane] & 0xFFFF);
+    }
+    for (;;) {
+      const uint64_t am = __ballot(a);
+      if (am == 0) break;
+      if (__popcll(am) == 1) {
+        // one walker left (the usual case after a few hops): hand it to
+        // fs_survivor, which walks it with only the tile bytes in LDS
+        const int L = __ffsll((unsigned long long)am) - 1;
+        const int32_t ue = __builtin_amdgcn_readlane(e, L);
+        const int32_t up = __builtin_amdgcn_readlane(p, L);
+        if (lane == 0) {
+          res[ue] = FE_PENDING;
+          surv[t] = (ue << 16) | up;
+        }
+        break;
+      }
+      int32_t q = 0;
+      bool claim = false;
+      uint16_t ow = 0;
+      if (a) {
+        uint32_t lo, hi;
+        fe_words(sb, p, lo, hi);
+        const uint16_t code = fe_hop(lo, hi, p, nrel, maxp32, q);
+        if (code != FE_GO) {
+          res[e] = code;
+          a = false;
+        } else {
+          ow = own[q];
+          claim = true;
+        }
+      }
+      if (claim && ow != 0) {
+        res[e] = (uint16_t)(F0_MERGE | (ow - 1));
+        a = false;
+        claim = false;
+      }
+      if (claim) own[q] = (uint16_t)(e + 1);
+      if (__popcll(__ballot(claim)) > 1) {
+        // several lanes may have claimed the same q: LDS ops of a wave
+        // execute in order, so this re-read sees every lane's write
+        if (claim) {
+          // volatile: the compiler must not forward this lane's own store
+          const uint16_t o2 = *(volatile const uint16_t*)&own[q];
+          if (o2 != (uint16_t)(e + 1)) {
+            res[e] = (uint16_t)(F0_MERGE | (o2 - 1));
+            a = false;
+            claim = false;
+          }
+        }
+      }
+      if (claim) p = q;
+    }
+  }
+  __syncthreads();
+  // ---- resolve merge links: the links are final now, so each thread just
+  // follows its entries' chains (no barriers); the 8 chains advance together
+  // so their LDS reads overlap.  Entries rooted at the survivor end at
+  // FE_PENDING, which fs_survivor replaces with its final code.
+  {
+    uint16_t v[FE_K];
+#pragma unroll
+    for (int k = 0; k < FE_K; ++k) v[k] = res[threadIdx.x + k * FE_T];
+    for (;;) {
+      bool any = false;
+#pragma unroll
+      for (int k = 0; k < FE_K; ++k)
+        if (f0_is_merge(v[k])) { v[k] = res[v[k] & 0x7FF]; any = true; }
+      if (!any) break;
+    }
+    uint16_t* out = f0 + t * FS_W;
+#pragma unroll
+    for (int k = 0; k < FE_K; ++k) out[threadIdx.x + k * FE_T] = v[k];
+  }
+}
+
 // Level l -> l+1: fl[l+1][u][p] = position after leaving unit u from us+p.
 __global__ __launch_bounds__(FS_T) void fs_compose(FsCtx c, int l) {
   const int64_t u = blockIdx.x;
@@ -386,7 +635,7 @@ __global__ __launch_bounds__(FS_T) void fs_mark(const uint8_t* __restrict__ buf,
     return;
   }
   const int32_t p0 = threadIdx.x * FS_PT;
-  stage_tile(buf, n, ts, sb);
+  stage_tile<FS_T>(buf, n, ts, sb, threadIdx.x);
   __syncthreads();
   // A[p]: next within tile; S = leaves the tile; p itself = terminal.
   {
@@ -521,50 +770,39 @@ __global__ __launch_bounds__(256) void fs_walk(const uint8_t* __restrict__ buf,
   }
   uint8_t* sb = smem + wv * (FS_S + 16);
   const int64_t ts = t * FS_S;
-  const int64_t lim = min(FS_S + 4, n - ts);
-  for (int64_t k = (int64_t)lane * 16; k < FS_S + 16; k += 64 * 16) {
-    if (k + 16 <= lim) {
-      uint4 v; __builtin_memcpy(&v, buf + ts + k, 16);
-      *(uint4*)(sb + k) = v;
-    } else {
-      for (int j = 0; j < 16; ++j)
-        sb[k + j] = (k + j < lim) ? buf[ts + k + j] : 0;
-    }
-  }
+  stage_tile<64>(buf, n, ts, sb, lane);
   // Wave-local staging (no workgroup barrier: sibling waves may have exited):
   // drain this wave's LDS writes before lane 0 reads them.
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_wave_barrier();
   const int32_t te = (int32_t)(min(ts + FS_S, n) - ts);   // tile-relative
-  const int64_t nrel = n - ts;
+  const int32_t nrel = (int32_t)min(n - ts, (int64_t)1 << 30);
+  const int32_t maxp32 = (int32_t)min(maxp, (int64_t)1 << 30);
+  // The walk is wave-UNIFORM: every lane runs it on scalar copies
+  // (readfirstlane), so the loop is ~25 mostly-SALU instructions around one
+  // LDS round trip per hop instead of a divergent lane-0 loop of ~45 VALU +
+  // exec-mask instructions (measured ~500 cycles/hop).
+  // The frame-start list is written IN PLACE over bytes already passed:
+  // entry k lands at byte 2k while the walk is at >= 4k, so no byte still to
+  // be read is overwritten, and no global store (with its vmcnt
+  // back-pressure) sits inside the dependent-hop loop.
+  uint16_t* Ls = (uint16_t*)sb;
+  int32_t c = __builtin_amdgcn_readfirstlane((int32_t)(e - ts));
   int32_t cnt = 0;
-  if (lane == 0) {
-    // The frame-start list is written IN PLACE over bytes already passed:
-    // entry k lands at byte 2k while the walk is at >= 4k, so no byte still
-    // to be read is overwritten, and no global store (with its vmcnt
-    // back-pressure) sits inside the dependent-hop loop.
-    uint16_t* Ls = (uint16_t*)sb;
-    int32_t c = (int32_t)(e - ts);
-    // One LDS round trip per hop: two aligned dword reads + v_alignbyte
-    // give the unaligned big-endian length.
-    while (c < te) {
-      const int32_t a = c & ~3;
-      const uint32_t lo = *(const uint32_t*)(sb + a);
-      const uint32_t hi = *(const uint32_t*)(sb + a + 4);
-      const int32_t len = (int32_t)bswap32(
-          __builtin_amdgcn_alignbyte(hi, lo, c & 3));
-      const int64_t nx = (int64_t)c + 4 + len;
-      if (((int64_t)c + 4 > nrel) | (len < 0) | ((int64_t)len > maxp) |
-          (nx > nrel))
-        break;
-      Ls[cnt++] = (uint16_t)c;
-      c = nx > FS_S ? FS_S : (int32_t)nx;
-    }
+  while (c < te) {
+    const int32_t a = c & ~3;
+    const uint32_t lo = *(const uint32_t*)(sb + a);
+    const uint32_t hi = *(const uint32_t*)(sb + a + 4);
+    const int32_t len = __builtin_amdgcn_readfirstlane(
+        (int32_t)bswap32(__builtin_amdgcn_alignbyte(hi, lo, c & 3)));
+    const int32_t nx = c + 4 + len;
+    if ((c + 4 > nrel) | (len < 0) | (len > maxp32) | (nx > nrel)) break;
+    if (lane == 0) Ls[cnt] = (uint16_t)c;
+    ++cnt;
+    c = nx;                                   // >= S ends the loop
   }
-  cnt = __shfl(cnt, 0, 64);
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_wave_barrier();
-  const uint16_t* Ls = (const uint16_t*)sb;
   uint16_t* L = list + t * FS_LMAX;
   for (int32_t k = lane; k < cnt; k += 64) L[k] = Ls[k];
   if (lane == 0) counts[t] = cnt;
@@ -595,12 +833,154 @@ __global__ __launch_bounds__(256) void fs_write_list(
   }
 }
 
+// ---- frontier pipeline, stages 2-4 -----------------------------------------
+// A2 fs_survivor: one wave per tile.  Walks the tile's single surviving
+// walker (if fs_frontier handed one off) to its end with the wave-uniform
+// scalar hop loop, records its frame starts R (in place in LDS, then to
+// `list`) and writes its final f0 code into every window entry rooted at
+// it.  16 KiB of LDS -> 9 tiles per CU.
+constexpr size_t FV_LDS = FS_S + 16;
+
+__global__ __launch_bounds__(64) void fs_survivor(
+    const uint8_t* __restrict__ buf, int64_t n, int64_t maxp,
+    uint16_t* __restrict__ f0, const int32_t* __restrict__ surv,
+    uint16_t* __restrict__ list, int32_t* __restrict__ rcount) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint8_t* sb = smem;                                      // [S + 16]
+  const int lane = threadIdx.x;
+  const int64_t t = blockIdx.x;
+  const int64_t ts = t * FS_S;
+  uint16_t* row = f0 + t * FS_W;
+  const int32_t sv = __builtin_amdgcn_readfirstlane(surv[t]);
+  if (sv < 0) {                              // nothing pending in this tile
+    if (lane == 0) rcount[t] = 0;
+    return;
+  }
+  stage_tile<64>(buf, n, ts, sb, lane);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+  const int32_t nrel = (int32_t)min(n - ts, (int64_t)1 << 30);
+  const int32_t maxp32 = (int32_t)min(maxp, (int64_t)1 << 30);
+  int32_t c = sv & 0xFFFF;
+  int32_t m = 0;
+  uint16_t fin;
+  uint16_t* Ls = (uint16_t*)sb;              // in place: entry k at byte 2k
+  for (;;) {
+    uint32_t lo, hi;
+    fe_words(sb, c, lo, hi);
+    lo = __builtin_amdgcn_readfirstlane(lo);
+    hi = __builtin_amdgcn_readfirstlane(hi);
+    int32_t q = 0;
+    const uint16_t code = fe_hop(lo, hi, c, nrel, maxp32, q);
+    if (code != FE_GO && (code & F0_TERM) && code != F0_ESC) {
+      fin = code;                            // terminal: not a frame start
+      break;
+    }
+    if (lane == 0) Ls[m] = (uint16_t)c;
+    ++m;
+    if (code != FE_GO) { fin = code; break; }  // leaves the tile
+    c = q;
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+  uint16_t* L = list + t * FS_LMAX;
+  for (int32_t k = lane; k < m; k += 64) L[k] = Ls[k];
+  if (lane == 0) rcount[t] = m;
+  // every window entry rooted at the survivor gets its final code
+#pragma unroll
+  for (int j = 0; j < FS_W * 2 / 16 / 64; ++j) {
+    uint4 v = ((const uint4*)row)[lane + 64 * j];
+    uint16_t* h = (uint16_t*)&v;
+    bool any = false;
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (h[k] == FE_PENDING) { h[k] = fin; any = true; }
+    if (any) ((uint4*)row)[lane + 64 * j] = v;
+  }
+}
+
+// D'' fs_join: the tile's frame starts from its exact entry e*.  Every chain
+// that reaches the survivor's tree passes through the survivor's hand-off
+// position r0 = R[0] (merges into it all happened at positions <= r0), so
+// walk from e* (uniform scalar loop, global memory, usually 0-5 hops) until
+// r0, then the rest is R.  A chain that misses r0 (bad frame, or a tile
+// whose survivor was a garbage walker) is simply walked to its end.
+__global__ __launch_bounds__(256) void fs_join(
+    const uint8_t* __restrict__ buf, int64_t n, int64_t maxp, int64_t tiles,
+    const int64_t* __restrict__ ent, const uint16_t* __restrict__ list,
+    const int32_t* __restrict__ rcount, uint16_t* __restrict__ pre,
+    int32_t* __restrict__ npre_out, int64_t* __restrict__ counts) {
+  const int lane = threadIdx.x & 63;
+  const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (t >= tiles) return;
+  const int64_t e = ent[t];
+  if (e == NONE) {
+    if (lane == 0) { counts[t] = 0; npre_out[t] = 0; }
+    return;
+  }
+  const int64_t ts = t * FS_S;
+  const int32_t te = (int32_t)(min(ts + FS_S, n) - ts);
+  const int32_t nrel = (int32_t)min(n - ts, (int64_t)1 << 30);
+  const int32_t maxp32 = (int32_t)min(maxp, (int64_t)1 << 30);
+  const int32_t m = __builtin_amdgcn_readfirstlane(rcount[t]);
+  int32_t r0 = m > 0 ? __builtin_amdgcn_readfirstlane(
+                           (int32_t)list[t * FS_LMAX]) : -1;
+  int32_t c = __builtin_amdgcn_readfirstlane((int32_t)(e - ts));
+  int32_t np = 0;
+  bool useR = false;
+  uint16_t* P = pre + t * FS_LMAX;
+  while (c < te) {
+    if (c == r0) { useR = true; break; }
+    if (c > r0) r0 = -1;                   // not in the survivor's tree
+    if (c + 4 > nrel) break;               // partial length at the end
+    const int32_t len = __builtin_amdgcn_readfirstlane(ld_be32(buf + ts + c));
+    const int32_t nx = c + 4 + len;
+    if ((len < 0) | (len > maxp32) | (nx > nrel)) break;
+    if (lane == 0) P[np] = (uint16_t)c;
+    ++np;
+    c = nx;
+  }
+  if (lane == 0) {
+    npre_out[t] = np;
+    counts[t] = np + (useR ? m : 0);
+  }
+}
+
+// E'' list -> (body offset, length): prefix from fs_join, then R.
+__global__ __launch_bounds__(256) void fs_write_join(
+    const uint8_t* __restrict__ buf, int64_t tiles,
+    const uint16_t* __restrict__ pre, const int32_t* __restrict__ npre,
+    const uint16_t* __restrict__ list, const int64_t* __restrict__ counts,
+    const int64_t* __restrict__ base, int64_t* __restrict__ foff,
+    int32_t* __restrict__ flen, int64_t cap, int64_t* __restrict__ result) {
+  const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (t >= tiles) return;
+  const int lane = threadIdx.x & 63;
+  const int64_t cnt = counts[t];
+  const int32_t np = npre[t];
+  const int64_t b = base[t];
+  const int64_t ts = t * FS_S;
+  const uint16_t* Pp = pre + t * FS_LMAX;
+  const uint16_t* R = list + t * FS_LMAX;
+  for (int64_t k = lane; k < cnt; k += 64) {
+    const int64_t P = ts + (k < np ? Pp[k] : R[k - np]);
+    const int64_t idx = b + k;
+    if (idx < cap) {
+      foff[idx] = P + 4;
+      flen[idx] = ld_be32(buf + P);
+    } else {
+      result[3] = 1;
+    }
+  }
+}
+
 struct FsPlan {
   int levels;
   int64_t units[FS_MAXL];
   int64_t usize[FS_MAXL];
   size_t off_f0, off_fl[FS_MAXL], off_ent[FS_MAXL], off_bits, off_cnt,
-      off_base, off_scan, off_list, total;
+      off_base, off_scan, off_list, off_pre, off_surv, off_rcnt, off_npre,
+      total;
 };
 
 static FsPlan fs_plan(int64_t n) {
@@ -626,6 +1006,10 @@ static FsPlan fs_plan(int64_t n) {
   p.off_base = take((size_t)tiles * 8);
   p.off_scan = take((size_t)zk_scan_workspace(tiles) * 8);
   p.off_list = take((size_t)tiles * FS_LMAX * 2);
+  p.off_pre = take((size_t)tiles * FS_LMAX * 2);
+  p.off_surv = take((size_t)tiles * 4);
+  p.off_rcnt = take((size_t)tiles * 4);
+  p.off_npre = take((size_t)tiles * 4);
   p.total = o;
   return p;
 }
@@ -660,9 +1044,32 @@ int zk_frame_scan(const uint8_t* buf, int64_t n, int64_t maxp, uint8_t* ws,
   }
   c.f0 = (const uint16_t*)(ws + p.off_f0);
   const int64_t tiles = p.units[0];
-  const size_t lds_a = FS_S * 2 + FS_LIST * 2 + (FS_T / 64 + 1) * 8;
-  fs_exits<<<(unsigned)tiles, FS_T, lds_a, st>>>(buf, n, maxp,
-                                                (uint16_t*)(ws + p.off_f0));
+  // ZKMI_FS_SCAN: "frontier" (default) | "jump" (fs_exits + fs_walk) |
+  // "double" (fs_exits + fs_mark doubling) — the older paths stay for A/B.
+  static int mode = -1;
+  if (mode < 0) {
+    const char* m = getenv("ZKMI_FS_SCAN");
+    mode = !m ? 0 : (m[0] == 'j' ? 1 : (m[0] == 'd' ? 2 : 0));
+  }
+  uint16_t* f0w = (uint16_t*)(ws + p.off_f0);
+  uint32_t* bits = (uint32_t*)(ws + p.off_bits);
+  int64_t* cnt = (int64_t*)(ws + p.off_cnt);
+  int64_t* base = (int64_t*)(ws + p.off_base);
+  uint16_t* list = (uint16_t*)(ws + p.off_list);
+  uint16_t* pre = (uint16_t*)(ws + p.off_pre);
+  int32_t* surv = (int32_t*)(ws + p.off_surv);
+  int32_t* rcnt = (int32_t*)(ws + p.off_rcnt);
+  int32_t* npre = (int32_t*)(ws + p.off_npre);
+  if (mode == 0) {
+    fs_frontier<<<(unsigned)tiles, FE_T, FE_LDS, st>>>(buf, n, maxp, f0w,
+                                                      surv);
+    ZK_LAUNCH_CHECK();
+    fs_survivor<<<(unsigned)tiles, 64, FV_LDS, st>>>(buf, n, maxp, f0w, surv,
+                                                    list, rcnt);
+  } else {
+    const size_t lds_a = FS_S * 2 + FS_LIST * 2 + (FS_T / 64 + 1) * 8;
+    fs_exits<<<(unsigned)tiles, FS_T, lds_a, st>>>(buf, n, maxp, f0w);
+  }
   ZK_LAUNCH_CHECK();
   for (int l = 0; l + 1 < p.levels; ++l) {
     fs_compose<<<(unsigned)p.units[l + 1], FS_T, 0, st>>>(c, l);
@@ -675,16 +1082,11 @@ int zk_frame_scan(const uint8_t* buf, int64_t n, int64_t maxp, uint8_t* ws,
     fs_down<<<(unsigned)((np + 255) / 256), 256, 0, st>>>(c, l);
     ZK_LAUNCH_CHECK();
   }
-  uint32_t* bits = (uint32_t*)(ws + p.off_bits);
-  int64_t* cnt = (int64_t*)(ws + p.off_cnt);
-  int64_t* base = (int64_t*)(ws + p.off_base);
-  uint16_t* list = (uint16_t*)(ws + p.off_list);
-  static int mode = -1;
-  if (mode < 0) {
-    const char* m = getenv("ZKMI_FS_MARK");
-    mode = (m && m[0] == 'd') ? 1 : 0;
-  }
-  if (mode == 1) {
+  const unsigned wblocks = (unsigned)((tiles + 3) / 4);
+  if (mode == 0) {
+    fs_join<<<wblocks, 256, 0, st>>>(buf, n, maxp, tiles, c.ent[0], list,
+                                     rcnt, pre, npre, cnt);
+  } else if (mode == 2) {
     fs_mark<<<(unsigned)tiles, FS_T, FS_S * 5, st>>>(buf, n, maxp, c.ent[0],
                                                     bits, cnt);
   } else {
@@ -696,12 +1098,15 @@ int zk_frame_scan(const uint8_t* buf, int64_t n, int64_t maxp, uint8_t* ws,
   int rc = zk_scan_excl_i64(cnt, base, tiles, result + 0,
                             (int64_t*)(ws + p.off_scan), st);
   if (rc) return rc;
-  if (mode == 1) {
+  if (mode == 0) {
+    fs_write_join<<<wblocks, 256, 0, st>>>(buf, tiles, pre, npre, list, cnt,
+                                           base, foff, flen, cap, result);
+  } else if (mode == 2) {
     fs_write<<<(unsigned)tiles, 256, 0, st>>>(buf, bits, base, foff, flen,
                                              cap, result);
   } else {
-    fs_write_list<<<(unsigned)((tiles + 3) / 4), 256, 0, st>>>(
-        buf, tiles, list, cnt, base, foff, flen, cap, result);
+    fs_write_list<<<wblocks, 256, 0, st>>>(buf, tiles, list, cnt, base, foff,
+                                           flen, cap, result);
   }
   ZK_LAUNCH_CHECK();
   return 0;

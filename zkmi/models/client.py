@@ -115,6 +115,8 @@ class Client(FSM):
         self.config = o.get('config') or ClientConfig()
         self.loop = o.get('loop') or default_loop()
         self.tracer = o.get('tracer')
+        # bulk codec device: None = the current GPU if any, False = host
+        self.bulk_device = o.get('device')
         self._resume_cred = o.get('session')
         self.session = None
         self.old_session = None
@@ -445,6 +447,67 @@ class Client(FSM):
         _check_func(cb)
         self._request({'opcode': 'SYNC', 'path': path}, cb,
                       lambda pkt: cb(None))
+
+    # -- bulk (GPU-coded, pipelined) API (models/bulk.py) ----------------------
+
+    BULK_OPS = ('GET_DATA', 'EXISTS', 'GET_CHILDREN', 'GET_CHILDREN2',
+                'CREATE', 'SET_DATA', 'DELETE', 'SYNC', 'GET_ACL')
+
+    def bulk(self, requests, cb):
+        """Pipeline many requests as one batch on the current connection:
+        encoded by K10 on the GPU, one socket write, replies collected by
+        xid range and decoded by K1-K8 on the GPU.  ``requests`` are dicts
+        ``{'opcode': 'GET_DATA', 'path': ...}`` (CREATE: ``data``, ``acl``,
+        ``flags``; SET_DATA / DELETE: ``version``, default -1).  Watches are
+        not supported here (use :meth:`watcher`).  ``cb(err, BulkResult)``;
+        replies are in request order.  Not in the reference, whose requests
+        go one by one through ``ZKEncodeStream`` (lib/zk-streams.js:109-148).
+        """
+        from .bulk import BulkBatch
+        _check_func(cb)
+        if not isinstance(requests, (list, tuple)):
+            raise TypeError('requests ([object]) is required')
+        pkts = []
+        for r in requests:
+            if not isinstance(r, dict) or r.get('opcode') not in self.BULK_OPS:
+                raise ValueError('bulk request needs opcode in %r' %
+                                 (self.BULK_OPS,))
+            if 'path' in r:
+                _check_str(r['path'], 'path')
+            if r.get('watch'):
+                raise ValueError('watches are not supported in bulk()')
+            p = dict(r)
+            op = p['opcode']
+            p.setdefault('path', '')
+            if op in ('GET_DATA', 'EXISTS', 'GET_CHILDREN', 'GET_CHILDREN2'):
+                p['watch'] = False
+            elif op == 'CREATE':
+                o = _norm_options({'acl': p.get('acl'), 'flags': p.get('flags')})
+                p['acl'], p['flags'] = o['acl'], o['flags']
+                p['data'] = bytes(p.get('data') or b'')
+            elif op == 'SET_DATA':
+                p['data'] = bytes(p.get('data') or b'')
+                p['version'] = p.get('version', -1)
+            elif op == 'DELETE':
+                p['version'] = p.get('version', -1)
+            pkts.append(p)
+
+        def go():
+            conn = self.currentConnection()
+            if conn is None or not conn.isInState('connected'):
+                self._not_connected(cb)
+                return
+            try:
+                conn.bulk_submit(BulkBatch(pkts, self.bulk_device), cb)
+            except Exception as e:
+                self.loop.call_soon(cb, e)
+        self._dispatch(go)
+
+    def bulk_get(self, paths, cb):
+        """:meth:`bulk` of GET_DATA for every path."""
+        if not isinstance(paths, (list, tuple)):
+            raise TypeError('paths ([string]) is required')
+        self.bulk([{'opcode': 'GET_DATA', 'path': p} for p in paths], cb)
 
     def watcher(self, path):
         _check_str(path, 'path')

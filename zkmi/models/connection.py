@@ -51,6 +51,7 @@ class ZKConnectionFSM(FSM):
         self.encoder = None
         self.xid_map = {}
         self.xid = 0
+        self.bulks = []                 # in-flight BulkBatch (models/bulk.py)
         self.reqs = {}
         self.socket = None
         self.session = None
@@ -211,6 +212,10 @@ class ZKConnectionFSM(FSM):
         self.log = self.log.child(sessionId=self.session.getSessionId())
 
         def on_rx(body, more):
+            if self.bulks and len(body) >= 16:
+                xid = int.from_bytes(body[0:4], 'big', signed=True)
+                if xid >= 0 and self._bulk_rx(xid, body):
+                    return
             try:
                 pkt = self._decode_reply(body)
             except ZKProtocolError as e:
@@ -259,6 +264,12 @@ class ZKConnectionFSM(FSM):
             self.socket.end(data)
 
         def on_rx(body, more):
+            if self.bulks and len(body) >= 16:
+                xid = int.from_bytes(body[0:4], 'big', signed=True)
+                if xid >= 0 and self._bulk_rx(xid, body):
+                    if len(self.reqs) < 1 and not self.bulks:
+                        send_close_session()
+                    return
             try:
                 pkt = self._decode_reply(body)
             except ZKProtocolError as e:
@@ -267,7 +278,7 @@ class ZKConnectionFSM(FSM):
                 return
             if box['xid'] is None or pkt['xid'] != box['xid']:
                 self.processReply(pkt)
-                if len(self.reqs) < 1:
+                if len(self.reqs) < 1 and not self.bulks:
                     send_close_session()
             else:
                 S.gotoState('closed')
@@ -282,8 +293,9 @@ class ZKConnectionFSM(FSM):
         S.on(self.socket, 'end', lambda: S.gotoState('closed'))
         S.on(self.socket, 'close', lambda: S.gotoState('closed'))
         # destroy() is ignored while closing, as in the reference: the
-        # CLOSE_SESSION exchange completes (or the socket dies).
-        if len(self.reqs) < 1:
+        # CLOSE_SESSION exchange completes (or the socket dies).  In-flight
+        # bulk batches drain like ordinary requests.
+        if len(self.reqs) < 1 and not self.bulks:
             send_close_session()
 
     def state_error(self, S):
@@ -293,6 +305,7 @@ class ZKConnectionFSM(FSM):
         reqs, self.reqs = self.reqs, {}
         for req in list(reqs.values()):
             req.emit('error', err)
+        self._fail_bulks(err)
         # Not S.immediate: this must be emitted even though we leave the
         # state right away (lib/connection-fsm.js:318-323).
         self.fsm_loop.call_soon(self._emit_error, err)
@@ -315,6 +328,7 @@ class ZKConnectionFSM(FSM):
             reqs, self.reqs = self.reqs, {}
             for req in list(reqs.values()):
                 req.emit('error', err)
+            self._fail_bulks(err)
         S.immediate(later)
 
     # -- requests ---------------------------------------------------------------
@@ -353,6 +367,53 @@ class ZKConnectionFSM(FSM):
                        'sent request to server')
         self.socket.write(self.encoder.request(pkt))
         return req
+
+    # -- bulk (GPU-coded, pipelined) batches ------------------------------------
+
+    def bulk_submit(self, batch, cb):
+        """Send a :class:`~zkmi.models.bulk.BulkBatch`: reserve a contiguous
+        xid range, encode (K10 on the GPU), one socket write.  ``cb(err,
+        result)`` runs on the loop thread once every reply arrived."""
+        if not self.isInState('connected'):
+            raise ZKProtocolError('CONNECTION_LOSS', 'Not connected.')
+        n = batch.n
+        x0 = self.xid
+        if x0 + n > 0x7fffffff:
+            x0 = 0
+        self.xid = (x0 + n) & 0x7fffffff
+        wire = batch.encode(x0)
+        batch.cb = cb
+        batch.t_submit = time.perf_counter()
+        if n == 0:
+            self.loop.call_soon(lambda: cb(None, batch.finish()))
+            return
+        self.bulks.append(batch)
+        self.log.trace({'xid0': x0, 'n': n, 'bytes': len(wire)},
+                       'sent bulk batch')
+        self.socket.write(wire)
+
+    def _bulk_rx(self, xid, body):
+        for b in self.bulks:
+            if b.owns(xid):
+                # header zxid keeps the session's lastZxid / expiry current
+                self.emit('packet', {'xid': xid, 'opcode': 'BULK',
+                                     'zxid': int.from_bytes(body[4:12], 'big',
+                                                            signed=True)})
+                if b.add(body):
+                    self.bulks.remove(b)
+                    try:
+                        res = b.finish()
+                    except Exception as e:      # decode failure -> caller
+                        b.cb(e)
+                        return True
+                    b.cb(None, res)
+                return True
+        return False
+
+    def _fail_bulks(self, err):
+        bulks, self.bulks = self.bulks, []
+        for b in bulks:
+            b.cb(err)
 
     def send(self, pkt):
         """Raw write of a handshake record (ConnectRequest)."""

@@ -1,0 +1,37 @@
+# zkmi developer entry points (the role of the reference's Makefile /
+# tools/mk: all, test, check).  GPU targets need an MI355X (run them through
+# gpurun on this pool).
+PY ?= python
+
+.PHONY: all build test test-gpu check lint sanitize bench bench-all prof clean
+
+all: build
+
+build:                    ## HIP kernels (gfx950) + C++ host codec, in-tree
+	$(PY) tools/build_native.py
+
+test:                     ## CPU suite (fake ZooKeeper, gloo, host codec)
+	$(PY) -m pytest tests -x -q -m "not gpu"
+
+test-gpu:                 ## kernel numerics + GPU pipelines (needs a GPU)
+	$(PY) -m pytest tests -x -q -m gpu
+
+check: lint sanitize      ## style + sanitizer runs
+
+lint:
+	$(PY) tools/lint.py
+
+sanitize:                 ## host codec suites under ASan + UBSan
+	bash tools/sanitize_host.sh
+
+bench:                    ## headline benchmark, 1 GPU
+	$(PY) bench.py
+
+bench-all:                ## get / mix / storm workloads + tests (needs a GPU)
+	bash tools/gpu_bench_all.sh
+
+prof:                     ## rocprofv3 kernel stats for the three workloads
+	PROF=prof bash tools/gpu_bench_all.sh
+
+clean:
+	rm -rf build zkmi/ops/libzkmi_hip.so zkmi/_zkhost*.so

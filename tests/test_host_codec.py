@@ -16,6 +16,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 @pytest.fixture(scope='module')
 def native():
+    if os.environ.get('ZKMI_HOST_CODEC_PATH'):
+        # the sanitizer build (tools/sanitize_host.sh), loaded by zkmi.codec
+        from zkmi import codec
+        assert codec.IMPL == 'native'
+        return codec._zkhost
     sys.path.insert(0, os.path.join(ROOT, 'tools'))
     import build_native
     build_native.build_host()

@@ -325,9 +325,9 @@ def test_gpu_tree_mutations(gpu):
         {'xid': 2, 'opcode': 'CREATE', 'path': '/bench/d000000/new',
          'data': b'hello', 'acl': jute.DEFAULT_ACL, 'flags': []},
         {'xid': 3, 'opcode': 'CREATE', 'path': '/nope/x', 'data': b'',
-         'acl': jute.DEFAULT_ACL, 'flags': []},                            # NO_NODE
+         'acl': jute.DEFAULT_ACL, 'flags': []},          # NO_NODE
         {'xid': 4, 'opcode': 'CREATE', 'path': leaf, 'data': b'',
-         'acl': jute.DEFAULT_ACL, 'flags': []},                            # NODE_EXISTS
+         'acl': jute.DEFAULT_ACL, 'flags': []},          # NODE_EXISTS
         {'xid': 5, 'opcode': 'DELETE', 'path': '/bench/d000000/n000000005',
          'version': -1},
         {'xid': 6, 'opcode': 'GET_DATA', 'path': '/bench/d000000/missing',

@@ -163,7 +163,7 @@ def _missing(c, p):
         return getattr(e, 'code', None) == 'NO_NODE'
 
 
-# -- tests ---------------------------------------------------------------------
+# -- tests --------------------------------------------------------------------
 
 @pytest.mark.parametrize('scenario', ['metrics', 'batched_get',
                                       'watch_fanout'])

@@ -1,0 +1,32 @@
+"""Host-side sanitizer run (SURVEY §5 race detection / sanitizers): the C++
+host codec rebuilt with ASan + UBSan and the codec suites (parity, golden
+vectors, hypothesis fuzz) run against it in a child process."""
+
+import os
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _have_asan():
+    if shutil.which('gcc') is None or shutil.which('g++') is None:
+        return False
+    lib = subprocess.run(['gcc', '-print-file-name=libasan.so'],
+                         capture_output=True, text=True).stdout.strip()
+    return os.path.isabs(lib) and os.path.exists(lib)
+
+
+@pytest.mark.slow
+@pytest.mark.skipif(not _have_asan(), reason='no gcc ASan runtime')
+def test_host_codec_under_asan_ubsan():
+    env = dict(os.environ)
+    env.pop('ZKMI_HOST_CODEC', None)
+    r = subprocess.run(['bash', os.path.join(ROOT, 'tools',
+                                             'sanitize_host.sh')],
+                       cwd=ROOT, env=env, capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert ' passed' in r.stdout

@@ -7,7 +7,8 @@
 * ``zkmi/_zkhost*.so`` — the C++ host codec for the interactive path
   (csrc/host), a CPython extension (no torch headers).
 
-Usage: ``python tools/build_native.py [--hip-only|--host-only] [-j N]``.
+Usage: ``python tools/build_native.py [--hip-only|--host-only|--sanitize]
+[-j N]``.
 Objects are cached under ``build/`` by source mtime.
 """
 
@@ -84,12 +85,38 @@ def build_host():
     return out
 
 
+SANITIZE_DIR = os.path.join(BDIR, 'sanitize')
+
+
+def build_host_sanitized():
+    """The host codec built with AddressSanitizer + UndefinedBehaviorSanitizer
+    (host code only — GPU sanitizers are not used).  Load it with
+    ``ZKMI_HOST_CODEC_PATH=<this .so>`` and the sanitizer runtimes preloaded
+    (see tools/sanitize_host.sh)."""
+    src = os.path.join(HDIR, 'zk_host_codec.cpp')
+    os.makedirs(SANITIZE_DIR, exist_ok=True)
+    suffix = sysconfig.get_config_var('EXT_SUFFIX') or '.so'
+    out = os.path.join(SANITIZE_DIR, '_zkhost' + suffix)
+    if _stale(out, [src]):
+        inc = sysconfig.get_paths()['include']
+        _run(['g++', '-O1', '-g', '-fPIC', '-shared', '-std=c++17', '-Wall',
+              '-fno-strict-aliasing', '-fno-omit-frame-pointer',
+              '-fsanitize=address,undefined', '-fno-sanitize-recover=all',
+              '-I' + inc, src, '-o', out])
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--hip-only', action='store_true')
     ap.add_argument('--host-only', action='store_true')
+    ap.add_argument('--sanitize', action='store_true',
+                    help='build only the ASan/UBSan host codec')
     ap.add_argument('-j', type=int, default=4)
     a = ap.parse_args()
+    if a.sanitize:
+        print(build_host_sanitized())
+        return
     if not a.host_only:
         print(build_hip(a.j))
     if not a.hip_only:

@@ -323,7 +323,8 @@ def _acl_table(acls, dev):
     offs = np.zeros(len(blobs), np.int64)
     np.cumsum(lens[:-1], out=offs[1:])
     arena = torch.frombuffer(bytearray(raw), dtype=U8).to(dev)
-    return arena, torch.from_numpy(offs).to(dev), torch.from_numpy(lens).to(dev)
+    return (arena, torch.from_numpy(offs).to(dev),
+            torch.from_numpy(lens).to(dev))
 
 
 # ACLs the mix alternates between (K10 encodes them from the pre-encoded

@@ -25,11 +25,25 @@ encode_response = jute.encode_response
 scan_frames = jute.scan_frames
 frame = jute.frame
 
-if os.environ.get('ZKMI_HOST_CODEC', 'native') != 'python':
+def _load_native():
+    """The in-tree extension, or the one at ``ZKMI_HOST_CODEC_PATH`` (the
+    sanitizer build, tools/sanitize_host.sh)."""
+    path = os.environ.get('ZKMI_HOST_CODEC_PATH')
+    if path:
+        import importlib.util
+        spec = importlib.util.spec_from_file_location('_zkhost', path)
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+        return mod
     try:
-        from . import _zkhost  # noqa: F401  (built by __graft_entry__.build)
+        from . import _zkhost as mod  # built by __graft_entry__.build
     except ImportError:
-        _zkhost = None
+        return None
+    return mod
+
+
+if os.environ.get('ZKMI_HOST_CODEC', 'native') != 'python':
+    _zkhost = _load_native()
     if _zkhost is not None:
         from .errors import ZKDecodeError
         _zkhost.init(jute.Stat, ZKDecodeError)

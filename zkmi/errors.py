@@ -1,6 +1,7 @@
 """L0 — error classes.
 
-Parity: ``lib/errors.js:19-54``.  ``message = code + ': ' + msg`` exactly as the
+Parity: ``lib/errors.js:19-54``.  ``message = code + ': ' + msg`` exactly as
+the
 reference formats it, and ``.code`` / ``.name`` carry the same strings so
 callers can switch on them the same way.
 """
@@ -57,4 +58,5 @@ class ZKNotConnectedError(ZKProtocolError):
 
 class ZKDecodeError(Exception):
     """Raised by the codecs on malformed input; the framing layer turns it
-    into ``ZKProtocolError('BAD_DECODE', ...)`` (``lib/zk-streams.js:74-95``)."""
+    into ``ZKProtocolError('BAD_DECODE', ...)``
+    (``lib/zk-streams.js:74-95``)."""

@@ -96,7 +96,7 @@ class BulkBatch(object):
         self.xid_map = None
         self.xt = None
 
-    # -- encode -----------------------------------------------------------------
+    # -- encode ---------------------------------------------------------------
 
     def encode(self, x0):
         """Assign xids ``x0 .. x0+n-1`` and return the framed request
@@ -124,7 +124,7 @@ class BulkBatch(object):
                                       'bulk request encode failed')
             return bytes(tx[:ntx].cpu().numpy().tobytes())
 
-    # -- collect ----------------------------------------------------------------
+    # -- collect --------------------------------------------------------------
 
     def owns(self, xid):
         return self.x0 <= xid < self.x0 + self.n
@@ -136,7 +136,7 @@ class BulkBatch(object):
         self.got += 1
         return self.got >= self.n
 
-    # -- decode -----------------------------------------------------------------
+    # -- decode ---------------------------------------------------------------
 
     def finish(self):
         if self.device is None:

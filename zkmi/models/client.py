@@ -138,7 +138,7 @@ class Client(FSM):
     def zc_set(self):
         return self.cset
 
-    # -- lifecycle -------------------------------------------------------------
+    # -- lifecycle ------------------------------------------------------------
 
     def state_normal(self, S):
         self._newSession()
@@ -448,7 +448,7 @@ class Client(FSM):
         self._request({'opcode': 'SYNC', 'path': path}, cb,
                       lambda pkt: cb(None))
 
-    # -- bulk (GPU-coded, pipelined) API (models/bulk.py) ----------------------
+    # -- bulk (GPU-coded, pipelined) API (models/bulk.py) ---------------------
 
     BULK_OPS = ('GET_DATA', 'EXISTS', 'GET_CHILDREN', 'GET_CHILDREN2',
                 'CREATE', 'SET_DATA', 'DELETE', 'SYNC', 'GET_ACL')
@@ -482,7 +482,8 @@ class Client(FSM):
             if op in ('GET_DATA', 'EXISTS', 'GET_CHILDREN', 'GET_CHILDREN2'):
                 p['watch'] = False
             elif op == 'CREATE':
-                o = _norm_options({'acl': p.get('acl'), 'flags': p.get('flags')})
+                o = _norm_options({'acl': p.get('acl'),
+                                   'flags': p.get('flags')})
                 p['acl'], p['flags'] = o['acl'], o['flags']
                 p['data'] = bytes(p.get('data') or b'')
             elif op == 'SET_DATA':
@@ -513,7 +514,7 @@ class Client(FSM):
         _check_str(path, 'path')
         return self.loop.run(lambda: self.getSession().watcher(path))
 
-    # -- blocking helpers -------------------------------------------------------
+    # -- blocking helpers -----------------------------------------------------
 
     def call_sync(self, method, *args, timeout=30.0):
         """Call ``method(*args, cb)`` and block for the callback.  Returns the

@@ -111,7 +111,7 @@ class ZKConnectionFSM(FSM):
             self.xid_map.pop(xid, None)
         return pkt
 
-    # -- states ----------------------------------------------------------------
+    # -- states ---------------------------------------------------------------
 
     def state_init(self, S):
         S.on(self, 'connectAsserted', lambda: S.gotoState('connecting'))
@@ -331,7 +331,7 @@ class ZKConnectionFSM(FSM):
             self._fail_bulks(err)
         S.immediate(later)
 
-    # -- requests ---------------------------------------------------------------
+    # -- requests -------------------------------------------------------------
 
     def processReply(self, pkt):
         req = self.reqs.get(pkt['xid'])
@@ -368,7 +368,7 @@ class ZKConnectionFSM(FSM):
         self.socket.write(self.encoder.request(pkt))
         return req
 
-    # -- bulk (GPU-coded, pipelined) batches ------------------------------------
+    # -- bulk (GPU-coded, pipelined) batches ----------------------------------
 
     def bulk_submit(self, batch, cb):
         """Send a :class:`~zkmi.models.bulk.BulkBatch`: reserve a contiguous

@@ -157,7 +157,7 @@ class ConnectionSet(EventEmitter):
             self._set_state('stopped')
         self.loop.call_soon(finish)
 
-    # -- core ------------------------------------------------------------------
+    # -- core -----------------------------------------------------------------
 
     def _now(self):
         return self.loop.time_ms()

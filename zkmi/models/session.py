@@ -15,9 +15,9 @@ SURVEY §7.1 "Expiry is a deadline, not a timer per packet").
 
 import random
 import re
+import threading
 import time
 
-from .. import consts
 from ..runtime.emitter import EventEmitter
 from ..runtime.fsm import FSM
 from ..utils.metrics import METRIC_ZK_NOTIFICATION_COUNTER
@@ -84,7 +84,7 @@ class ZKSession(FSM):
                           'Notifications received from ZooKeeper')
         FSM.__init__(self, 'detached', loop)
 
-    # -- queries ----------------------------------------------------------------
+    # -- queries --------------------------------------------------------------
 
     def isAttaching(self):
         return self.isInState('attaching') or self.isInState('reattaching')
@@ -140,7 +140,7 @@ class ZKSession(FSM):
                 'timeOut': self.timeout, 'sessionId': self.session_id,
                 'passwd': self.passwd}
 
-    # -- states ----------------------------------------------------------------
+    # -- states ---------------------------------------------------------------
 
     def state_detached(self, S):
         if self.conn is not None:
@@ -302,7 +302,7 @@ class ZKSession(FSM):
         self.expiry.cancel()
         self.log.info('ZK session closed')
 
-    # -- watches ---------------------------------------------------------------
+    # -- watches --------------------------------------------------------------
 
     def watchersDisconnected(self):
         for w in list(self.watchers.values()):
@@ -391,6 +391,7 @@ class ZKWatcher(EventEmitter):
 
     def __init__(self, session, path, log):
         EventEmitter.__init__(self)
+        self._lk = threading.Lock()
         self.path = path
         self.session = session
         self.evts = {}
@@ -425,23 +426,25 @@ class ZKWatcher(EventEmitter):
             raise TypeError('event must be a string')
         if not callable(cb):
             raise TypeError('callback must be a function')
-        loop = self.session.fsm_loop
-        if not loop.in_loop():
-            # Arming drives FSMs, which live on the loop thread only.
-            loop.run(lambda: self.on(evt, cb))
-            return self
-        first = self.listenerCount(evt) < 1
-        EventEmitter.on(self, evt, cb)
+        # The listener is registered right here, in the caller's thread, so
+        # several on() calls in a row are all in place before any reply to
+        # the arming they trigger can be dispatched (the reference registers
+        # synchronously within one tick).  Arming drives FSMs, which live on
+        # the loop thread only: it is queued there.
+        with self._lk:
+            first = self.listenerCount(evt) < 1
+            EventEmitter.on(self, evt, cb)
         if evt != 'error' and first:
-            self._armEvent(evt)
+            loop = self.session.fsm_loop
+            if loop.in_loop():
+                self._armEvent(evt)
+            else:
+                loop.call_soon(self._armEvent, evt)
         return self
 
     def removeListener(self, evt, cb):
-        loop = self.session.fsm_loop
-        if not loop.in_loop():
-            loop.run(lambda: EventEmitter.removeListener(self, evt, cb))
-            return self
-        return EventEmitter.removeListener(self, evt, cb)
+        with self._lk:
+            return EventEmitter.removeListener(self, evt, cb)
 
     addListener = on
 

@@ -25,10 +25,7 @@ relies on:
   reply protocolVersion=1, pause reads, close/relisten on a schedule.
 """
 
-import asyncio
 import os
-import struct
-import threading
 import time
 
 from .. import consts
@@ -124,7 +121,7 @@ class ZKDatabase(object):
     def _mono(self):
         return self.loop.time_ms()
 
-    # -- sessions ---------------------------------------------------------------
+    # -- sessions -------------------------------------------------------------
 
     def _arm_expiry(self):
         iv = max(self.tick_ms / 4.0, 5)
@@ -147,7 +144,8 @@ class ZKDatabase(object):
 
     def new_session(self, timeout):
         self._sid_ctr += 1
-        sid = (self._server_id << 56) | ((self.now_ms() & 0xffffffffff) << 16) \
+        sid = (self._server_id << 56) | \
+            ((self.now_ms() & 0xffffffffff) << 16) \
             | (self._sid_ctr & 0xffff)
         passwd = os.urandom(16)
         s = SessionRec(sid, passwd, self.negotiate_timeout(timeout),
@@ -185,7 +183,7 @@ class ZKDatabase(object):
                 if not table[path]:
                     del table[path]
 
-    # -- watches ----------------------------------------------------------------
+    # -- watches --------------------------------------------------------------
 
     def _add_watch(self, table, path, sid):
         if sid is None:
@@ -211,7 +209,7 @@ class ZKDatabase(object):
         self.stats['notifications'] += 1
         s.conn.send_notification(evtype, path)
 
-    # -- tree -------------------------------------------------------------------
+    # -- tree -----------------------------------------------------------------
 
     def _mk(self, path, data, acl, owner):
         self.zxid += 1
@@ -347,7 +345,7 @@ class ZKDatabase(object):
             else:
                 self._add_watch(self.child_watches, path, sid)
 
-    # -- request dispatch ---------------------------------------------------------
+    # -- request dispatch -----------------------------------------------------
 
     def handle(self, pkt, sid):
         """Apply one decoded request; returns the reply packet dict."""
@@ -528,7 +526,7 @@ class FakeZKServer(object):
         self._srv = None
         self.start()
 
-    # -- lifecycle ----------------------------------------------------------------
+    # -- lifecycle ------------------------------------------------------------
 
     def start(self):
         async def go():
@@ -572,7 +570,7 @@ class FakeZKServer(object):
     def servers(self):
         return [self.address]
 
-    # -- faults -----------------------------------------------------------------
+    # -- faults ---------------------------------------------------------------
 
     def set_mode(self, mode, raw_writes=None, reply_version=None):
         """``normal`` | ``close`` (accept then close) | ``hang`` | ``write``
@@ -618,7 +616,7 @@ class FakeZKServer(object):
         c = _ServerConn(self, sock)
         self.conns.add(c)
 
-    # -- out-of-band mutations (the reference tests' zk.cli(...)) ---------------
+    # -- out-of-band mutations (the reference tests' zk.cli(...)) -------------
 
     def cli_create(self, path, data=b'', ephemeral_sid=None, flags=()):
         return self.run(lambda: self.db.create(

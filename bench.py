@@ -6,7 +6,8 @@ Default config (BASELINE.json configs[1]): batched get() over a 1M-znode
 synthetic tree with the Jute-decode HIP kernels on each MI355X.
 ``--workload mix`` is configs[2] (create/set/delete with version CAS and ACL
 encode on the same 1M-znode tree) and ``--workload storm`` configs[4]
-(EPHEMERAL|SEQUENTIAL create storm with per-step session expiry).  One step = one batch
+(EPHEMERAL|SEQUENTIAL create storm with per-step session expiry).
+One step = one batch
 of ``--batch`` GET_DATA requests per GPU pushed through the full ZooKeeper
 wire path on the GPU (see zkmi/bench/synthetic.py): client request encode
 (K10) -> server frame scan + request decode (K1, K12) -> tree lookup in HBM
@@ -105,7 +106,7 @@ def main():
 
     ok_total = torch.zeros(1, dtype=torch.int64, device=dev)
     for _ in range(a.warmup):
-        ok_total += pipe.step()
+        pipe.step(acc=ok_total)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -113,7 +114,7 @@ def main():
     ok_total.zero_()
     t0 = time.perf_counter()
     for _ in range(a.steps):
-        ok_total += pipe.step()
+        pipe.step(acc=ok_total)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

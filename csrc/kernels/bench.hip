@@ -1,0 +1,90 @@
+// Benchmark-side helpers for the synthetic GET pipeline
+// (zkmi/bench/synthetic.py GetPipeline): request generation and the
+// per-reply validation, each ONE fused kernel instead of ~15 small torch
+// element-wise launches per step.  Semantics are those of the torch code
+// they replace: uniform random node per request, consecutive xids, and a
+// reply counts as OK only if it decoded cleanly, carries err OK, opcode
+// GET_DATA, the request's xid, czxid == node + 1 and the node's data length.
+#include "zk_common.h"
+
+namespace zk {
+
+constexpr int BG_T = 256;
+
+// splitmix64: counter-based, so step s / request i always draw the same node
+ZK_DEV uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+__global__ __launch_bounds__(BG_T) void bench_gen_get(
+    int64_t n, uint64_t seed, int64_t leaf0, int64_t nleaves,
+    int32_t xid_base, const int64_t* __restrict__ node_path_off,
+    const int32_t* __restrict__ node_path_len, int64_t* __restrict__ idx,
+    int32_t* __restrict__ xid, int64_t* __restrict__ path_off,
+    int32_t* __restrict__ path_len) {
+  const int64_t i = (int64_t)blockIdx.x * BG_T + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t r = splitmix64(seed ^ (uint64_t)i * 0xD1B54A32D192ED03ull);
+  // multiply-shift range reduction (bias < 2^-32 for 1M leaves)
+  const int64_t v = leaf0 + (int64_t)(((r >> 32) * (uint64_t)nleaves) >> 32);
+  idx[i] = v;
+  xid[i] = (int32_t)(((uint32_t)xid_base + (uint32_t)i) & 0x7fffffffu);
+  path_off[i] = node_path_off[v];
+  path_len[i] = node_path_len[v];
+}
+
+__global__ __launch_bounds__(BG_T) void bench_check_get(
+    int64_t n, const int32_t* __restrict__ status,
+    const int32_t* __restrict__ err, const int32_t* __restrict__ opcode,
+    const int32_t* __restrict__ rxid, const int64_t* __restrict__ czxid,
+    const int32_t* __restrict__ pay_len, const int64_t* __restrict__ idx,
+    const int32_t* __restrict__ xid, const int32_t* __restrict__ data_len,
+    unsigned long long* __restrict__ ok) {
+  __shared__ int64_t sm[BG_T / 64 + 1];
+  const int64_t i = (int64_t)blockIdx.x * BG_T + threadIdx.x;
+  int64_t good = 0;
+  if (i < n) {
+    const int64_t v = idx[i];
+    good = status[i] == 0 && err[i] == 0 && opcode[i] == OP_GET_DATA &&
+           rxid[i] == xid[i] && czxid[i] == v + 1 &&
+           pay_len[i] == data_len[v];
+  }
+  int64_t tot;
+  block_excl_scan(good, sm, &tot);
+  if (threadIdx.x == 0 && tot) atomicAdd(ok, (unsigned long long)tot);
+}
+
+}  // namespace zk
+
+extern "C" {
+
+int zk_bench_gen_get(int64_t n, uint64_t seed, int64_t leaf0, int64_t nleaves,
+                     int32_t xid_base, const int64_t* node_path_off,
+                     const int32_t* node_path_len, int64_t* idx, int32_t* xid,
+                     int64_t* path_off, int32_t* path_len, hipStream_t st) {
+  if (n <= 0) return 0;
+  zk::bench_gen_get<<<(unsigned)((n + zk::BG_T - 1) / zk::BG_T), zk::BG_T, 0,
+                      st>>>(n, seed, leaf0, nleaves, xid_base, node_path_off,
+                            node_path_len, idx, xid, path_off, path_len);
+  ZK_LAUNCH_CHECK();
+  return 0;
+}
+
+int zk_bench_check_get(int64_t n, const int32_t* status, const int32_t* err,
+                       const int32_t* opcode, const int32_t* rxid,
+                       const int64_t* czxid, const int32_t* pay_len,
+                       const int64_t* idx, const int32_t* xid,
+                       const int32_t* data_len, unsigned long long* ok,
+                       hipStream_t st) {
+  if (n <= 0) return 0;
+  zk::bench_check_get<<<(unsigned)((n + zk::BG_T - 1) / zk::BG_T), zk::BG_T,
+                        0, st>>>(n, status, err, opcode, rxid, czxid, pay_len,
+                                 idx, xid, data_len, ok);
+  ZK_LAUNCH_CHECK();
+  return 0;
+}
+
+}  // extern "C"

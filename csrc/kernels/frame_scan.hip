@@ -339,10 +339,28 @@ constexpr size_t FE_LDS = (FS_S + 16) + FS_S * 2 + FS_W * 2 + 66 * 4;
 
 ZK_DEV bool f0_is_merge(uint16_t v) { return (v & 0xF800) == F0_MERGE; }
 
+// Phase timestamps of fs_frontier for tools/microbench/frontier_bench.hip
+// (compiled in only with -DZKMI_FE_PROFILE).
+#ifdef ZKMI_FE_PROFILE
+__device__ uint64_t* g_fe_prof;
+#define FE_MARK(k) do { if (threadIdx.x == 0 && g_fe_prof) \
+    g_fe_prof[blockIdx.x * 8 + (k)] = wall_clock64(); } while (0)
+#define FE_NOTE(k, v) do { if (threadIdx.x == 0 && g_fe_prof) \
+    g_fe_prof[blockIdx.x * 8 + (k)] = (v); } while (0)
+#else
+#define FE_MARK(k) do {} while (0)
+#define FE_NOTE(k, v) do {} while (0)
+#endif
+
 // One hop from tile-relative p.  Returns the f0 code when the walk ends
 // here (terminal / leaves the tile), else 0xFFFE and q (in-tile successor).
 constexpr uint16_t FE_GO = 0xFFFE;
-constexpr uint16_t FE_PENDING = 0xFFFD;      // the survivor: fs_survivor
+constexpr uint16_t FE_PENDING = 0xFFFD;      // | ... slot s = 0xFFFD - s
+#ifndef ZKMI_FE_NSURV
+#define ZKMI_FE_NSURV 1
+#endif
+constexpr int FE_NSURV = ZKMI_FE_NSURV;      // survivors handed off per tile
+ZK_DEV uint16_t fe_pending(int slot) { return (uint16_t)(FE_PENDING - slot); }
 ZK_DEV uint16_t fe_hop(uint32_t lo, uint32_t hi, int32_t p, int32_t nrel,
                        int32_t maxp, int32_t& q) {
   // 32-bit throughout: p < 2^14, len <= maxp <= 2^30, nrel clamped to 2^30
@@ -357,6 +375,25 @@ ZK_DEV uint16_t fe_hop(uint32_t lo, uint32_t hi, int32_t p, int32_t nrel,
   }
   q = nx;
   return FE_GO;
+}
+
+// fe_hop for a length already extracted (wave-uniform walks: the length is
+// built in VALU and moved to an SGPR once, instead of moving both words).
+ZK_DEV uint16_t fe_hop_len(int32_t len, int32_t p, int32_t nrel, int32_t maxp,
+                           int32_t& q) {
+  const int32_t nx = p + 4 + len;
+  if ((p + 4 > nrel) | (len < 0) | (len > maxp) | (nx > nrel))
+    return (uint16_t)(F0_TERM | p);
+  if (nx >= FS_S) {
+    const int32_t x = nx - (int32_t)FS_S;
+    return x < 0x4000 ? (uint16_t)x : F0_ESC;
+  }
+  q = nx;
+  return FE_GO;
+}
+
+ZK_DEV int32_t fe_len(uint32_t lo, uint32_t hi, int32_t p) {
+  return (int32_t)bswap32(__builtin_amdgcn_alignbyte(hi, lo, p & 3));
 }
 
 ZK_DEV void fe_words(const uint8_t* sb, int32_t p, uint32_t& lo, uint32_t& hi) {
@@ -381,6 +418,7 @@ __global__ __launch_bounds__(FE_T) void fs_frontier(
   uint16_t* res = own + FS_S;                              // [W]
   uint32_t* hand = (uint32_t*)(res + FS_W);                // [64] + 2 ctrs
   const int64_t t = blockIdx.x;
+  FE_MARK(0);
   const int64_t ts = t * FS_S;
   const int32_t nrel = (int32_t)min(n - ts, (int64_t)1 << 30);
   const int32_t maxp32 = (int32_t)min(maxp, (int64_t)1 << 30);
@@ -399,8 +437,11 @@ __global__ __launch_bounds__(FE_T) void fs_frontier(
     act |= 1u << k;
   }
   __syncthreads();
+  FE_MARK(1);
   // ---- block-wide rounds while many walkers live ------------------------
+  int nrounds = 0;
   for (int r = 0;; ++r) {
+    ++nrounds;
     // phase 1: hop, then claim the landing position (racy; phase 2 decides).
     // All of a thread's LDS reads are issued before any of its writes, so
     // the 8 walkers' round trips overlap instead of chaining.
@@ -456,6 +497,8 @@ __global__ __launch_bounds__(FE_T) void fs_frontier(
     if (live <= 64) break;
     __syncthreads();                    // counter reset visible next round
   }
+  FE_MARK(2);
+  FE_NOTE(5, nrounds);
   // ---- hand the survivors to wave 0 ---------------------------------------
   __syncthreads();
   if (threadIdx.x == 0) hand[64] = 0;
@@ -467,7 +510,7 @@ __global__ __launch_bounds__(FE_T) void fs_frontier(
     hand[slot] = ((uint32_t)(threadIdx.x + k * FE_T) << 16) | (uint32_t)pos[k];
   }
   __syncthreads();
-  if (threadIdx.x == 0) surv[t] = -1;
+  if (threadIdx.x < FE_NSURV) surv[t * FE_NSURV + threadIdx.x] = -1;
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x;
     const int cnt = (int)hand[64];
@@ -477,18 +520,22 @@ __global__ __launch_bounds__(FE_T) void fs_frontier(
       e = (int32_t)(hand[lane] >> 16);
       p = (int32_t)(hand[lane] & 0xFFFF);
     }
+    int iters = 0;
     for (;;) {
       const uint64_t am = __ballot(a);
       if (am == 0) break;
-      if (__popcll(am) == 1) {
-        // one walker left (the usual case after a few hops): hand it to
-        // fs_survivor, which walks it with only the tile bytes in LDS
-        const int L = __ffsll((unsigned long long)am) - 1;
-        const int32_t ue = __builtin_amdgcn_readlane(e, L);
-        const int32_t up = __builtin_amdgcn_readlane(p, L);
-        if (lane == 0) {
-          res[ue] = FE_PENDING;
-          surv[t] = (ue << 16) | up;
+      ++iters;
+      FE_NOTE(6, iters);
+      if (__popcll(am) <= FE_NSURV) {
+        // one or two walkers left (the usual case after a few hops): hand
+        // them to fs_survivor, which walks them without the owner table (a
+        // second survivor is typically a garbage chain running beside the
+        // true one for a long way without merging)
+        if (a) {
+          const int slot = __builtin_amdgcn_mbcnt_hi(
+              (uint32_t)(am >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)am, 0));
+          res[e] = fe_pending(slot);
+          surv[t * FE_NSURV + slot] = (e << 16) | p;
         }
         break;
       }
@@ -530,10 +577,15 @@ __global__ __launch_bounds__(FE_T) void fs_frontier(
     }
   }
   __syncthreads();
-  // ---- resolve merge links: the links are final now, so each thread just
-  // follows its entries' chains (no barriers); the 8 chains advance together
-  // so their LDS reads overlap.  Entries rooted at the survivor end at
-  // FE_PENDING, which fs_survivor replaces with its final code.
+  FE_MARK(3);
+  // ---- resolve merge links: the links are final now, so no barriers: each
+  // thread advances its 8 entries (LDS reads overlapping) and writes every
+  // step back, so chains compress for everyone (racy but monotone pointer
+  // jumping).  Chains are long: every window start is a walker, so in a
+  // stream of 42-byte frames ~48 starts merge one into the next along the
+  // true chain; following them hop by hop cost ~17 us per tile.  Entries
+  // rooted at a survivor end at fe_pending(slot), which fs_survivor
+  // replaces with its final code.
   {
     uint16_t v[FE_K];
 #pragma unroll
@@ -543,12 +595,15 @@ __global__ __launch_bounds__(FE_T) void fs_frontier(
 #pragma unroll
       for (int k = 0; k < FE_K; ++k)
         if (f0_is_merge(v[k])) { v[k] = res[v[k] & 0x7FF]; any = true; }
+#pragma unroll
+      for (int k = 0; k < FE_K; ++k) res[threadIdx.x + k * FE_T] = v[k];
       if (!any) break;
     }
     uint16_t* out = f0 + t * FS_W;
 #pragma unroll
     for (int k = 0; k < FE_K; ++k) out[threadIdx.x + k * FE_T] = v[k];
   }
+  FE_MARK(4);
 }
 
 // Level l -> l+1: fl[l+1][u][p] = position after leaving unit u from us+p.
@@ -834,11 +889,32 @@ __global__ __launch_bounds__(256) void fs_write_list(
 }
 
 // ---- frontier pipeline, stages 2-4 -----------------------------------------
-// A2 fs_survivor: one wave per tile.  Walks the tile's single surviving
-// walker (if fs_frontier handed one off) to its end with the wave-uniform
-// scalar hop loop, records its frame starts R (in place in LDS, then to
-// `list`) and writes its final f0 code into every window entry rooted at
-// it.  16 KiB of LDS -> 9 tiles per CU.
+// Survivor slot s of tile t: surv[t*2+s] = (walker id << 16) | position, or
+// -1; its frame starts R_s go to list[(t*2+s)*FS_LMAX ...], its count to
+// rcount[t*2+s].
+
+// Replace fe_pending(slot) in the tile's f0 row by the slot's final code.
+ZK_DEV void fe_patch_row(uint16_t* row, int lane, const uint16_t fin[FE_NSURV]) {
+#pragma unroll
+  for (int j = 0; j < FS_W * 2 / 16 / 64; ++j) {
+    uint4 v = ((const uint4*)row)[lane + 64 * j];
+    uint16_t* h = (uint16_t*)&v;
+    bool any = false;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+#pragma unroll
+      for (int sl = 0; sl < FE_NSURV; ++sl)
+        if (h[k] == fe_pending(sl)) { h[k] = fin[sl]; any = true; }
+    }
+    if (any) ((uint4*)row)[lane + 64 * j] = v;
+  }
+}
+
+// A2 fs_survivor (LDS): one wave per tile; lane s walks survivor slot s of
+// the staged tile (the two walks advance in lockstep, one LDS round trip per
+// hop).  Frame starts go straight to global memory: those stores count in
+// vmcnt, which the LDS hop loop never waits on.  16 KiB of LDS -> 9 tiles
+// per CU: the variant for streams with few tiles (long chains per tile).
 constexpr size_t FV_LDS = FS_S + 16;
 
 __global__ __launch_bounds__(64) void fs_survivor(
@@ -850,10 +926,9 @@ __global__ __launch_bounds__(64) void fs_survivor(
   const int lane = threadIdx.x;
   const int64_t t = blockIdx.x;
   const int64_t ts = t * FS_S;
-  uint16_t* row = f0 + t * FS_W;
-  const int32_t sv = __builtin_amdgcn_readfirstlane(surv[t]);
-  if (sv < 0) {                              // nothing pending in this tile
-    if (lane == 0) rcount[t] = 0;
+  const int32_t sv = lane < FE_NSURV ? surv[t * FE_NSURV + lane] : -1;
+  if (!__ballot(sv >= 0)) {                  // nothing pending in this tile
+    if (lane < FE_NSURV) rcount[t * FE_NSURV + lane] = 0;
     return;
   }
   stage_tile<64>(buf, n, ts, sb, lane);
@@ -861,50 +936,134 @@ __global__ __launch_bounds__(64) void fs_survivor(
   __builtin_amdgcn_wave_barrier();
   const int32_t nrel = (int32_t)min(n - ts, (int64_t)1 << 30);
   const int32_t maxp32 = (int32_t)min(maxp, (int64_t)1 << 30);
-  int32_t c = sv & 0xFFFF;
   int32_t m = 0;
-  uint16_t fin;
-  uint16_t* Ls = (uint16_t*)sb;              // in place: entry k at byte 2k
-  for (;;) {
-    uint32_t lo, hi;
-    fe_words(sb, c, lo, hi);
-    lo = __builtin_amdgcn_readfirstlane(lo);
-    hi = __builtin_amdgcn_readfirstlane(hi);
-    int32_t q = 0;
-    const uint16_t code = fe_hop(lo, hi, c, nrel, maxp32, q);
-    if (code != FE_GO && (code & F0_TERM) && code != F0_ESC) {
-      fin = code;                            // terminal: not a frame start
-      break;
+  uint16_t fin = 0;
+  if constexpr (FE_NSURV == 1) {
+    // one survivor: wave-uniform scalar walk (~25 mostly-SALU instructions
+    // around one LDS round trip per hop); its frame starts are written IN
+    // PLACE over tile bytes already passed (entry k at byte 2k while the
+    // walk is at >= 4k) and copied out once.
+    int32_t c = __builtin_amdgcn_readfirstlane(sv) & 0xFFFF;
+    uint16_t* Ls = (uint16_t*)sb;
+    for (;;) {
+      uint32_t lo, hi;
+      fe_words(sb, c, lo, hi);
+      const int32_t len = __builtin_amdgcn_readfirstlane(fe_len(lo, hi, c));
+      int32_t q = 0;
+      const uint16_t code = fe_hop_len(len, c, nrel, maxp32, q);
+      if (code != FE_GO && (code & F0_TERM) && code != F0_ESC) {
+        fin = code;                          // terminal: not a frame start
+        break;
+      }
+      if (lane == 0) Ls[m] = (uint16_t)c;
+      ++m;
+      if (code != FE_GO) { fin = code; break; }   // leaves the tile
+      c = q;
     }
-    if (lane == 0) Ls[m] = (uint16_t)c;
-    ++m;
-    if (code != FE_GO) { fin = code; break; }  // leaves the tile
-    c = q;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    uint16_t* L = list + t * FS_LMAX;
+    for (int32_t k = lane; k < m; k += 64) L[k] = Ls[k];
+    if (lane != 0) m = 0;                    // slot 0 lives in lane 0
+  } else {
+  bool a = sv >= 0;
+  int32_t c = sv & 0xFFFF;
+  uint16_t* L = list + (t * FE_NSURV + lane) * FS_LMAX;
+  while (__ballot(a)) {
+    if (a) {
+      uint32_t lo, hi;
+      fe_words(sb, c, lo, hi);
+      int32_t q = 0;
+      const uint16_t code = fe_hop(lo, hi, c, nrel, maxp32, q);
+      if (code != FE_GO && (code & F0_TERM) && code != F0_ESC) {
+        fin = code;                          // terminal: not a frame start
+        a = false;
+      } else {
+        L[m++] = (uint16_t)c;
+        if (code != FE_GO) { fin = code; a = false; }   // leaves the tile
+        else c = q;
+      }
+    }
   }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_wave_barrier();
-  uint16_t* L = list + t * FS_LMAX;
-  for (int32_t k = lane; k < m; k += 64) L[k] = Ls[k];
-  if (lane == 0) rcount[t] = m;
-  // every window entry rooted at the survivor gets its final code
-#pragma unroll
-  for (int j = 0; j < FS_W * 2 / 16 / 64; ++j) {
-    uint4 v = ((const uint4*)row)[lane + 64 * j];
-    uint16_t* h = (uint16_t*)&v;
-    bool any = false;
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
-      if (h[k] == FE_PENDING) { h[k] = fin; any = true; }
-    if (any) ((uint4*)row)[lane + 64 * j] = v;
   }
+  if (lane < FE_NSURV) rcount[t * FE_NSURV + lane] = m;
+  uint16_t fins[FE_NSURV];
+#pragma unroll
+  for (int sl = 0; sl < FE_NSURV; ++sl)
+    fins[sl] = (uint16_t)__builtin_amdgcn_readlane((int)fin, sl);
+  fe_patch_row(f0 + t * FS_W, lane, fins);
+}
+
+// A2' fs_survivor_g: the same walks straight from global memory, no LDS.  A
+// dependent hop costs more from L2 than from LDS (~0.4 vs ~0.1 us under
+// load), but without the 16 KiB LDS tile a CU holds 32 walking waves instead
+// of 9 and nothing is staged: the variant for streams with many tiles.
+// Each slot is walked by a wave-uniform loop (two aligned dwords per hop +
+// v_alignbyte); its frame starts collect in a VGPR (entry k in lane k & 63,
+// one v_cndmask) and leave in one coalesced store per 64 hops.  4 tiles
+// (waves) per block.
+__global__ __launch_bounds__(256) void fs_survivor_g(
+    const uint8_t* __restrict__ buf, int64_t n, int64_t maxp, int64_t tiles,
+    uint16_t* __restrict__ f0, const int32_t* __restrict__ surv,
+    uint16_t* __restrict__ list, int32_t* __restrict__ rcount) {
+  const int lane = threadIdx.x & 63;
+  const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (t >= tiles) return;
+  const int64_t ts = t * FS_S;
+  const uint8_t* tb = buf + ts;
+  const int32_t nrel = (int32_t)min(n - ts, (int64_t)1 << 30);
+  const int32_t maxp32 = (int32_t)min(maxp, (int64_t)1 << 30);
+  uint16_t fins[FE_NSURV];
+  bool any_sv = false;
+#pragma unroll
+  for (int sl = 0; sl < FE_NSURV; ++sl) {
+    const int32_t sv = __builtin_amdgcn_readfirstlane(
+        surv[t * FE_NSURV + sl]);
+    fins[sl] = 0;
+    if (sv < 0) {
+      if (lane == 0) rcount[t * FE_NSURV + sl] = 0;
+      continue;
+    }
+    any_sv = true;
+    uint16_t* L = list + (t * FE_NSURV + sl) * FS_LMAX;
+    int32_t c = sv & 0xFFFF;
+    int32_t m = 0;
+    uint32_t ent = 0;
+    uint16_t fin;
+    for (;;) {
+      if (c + 4 > nrel) { fin = (uint16_t)(F0_TERM | c); break; }
+      // the address, not the load, is selected: both loads issue together
+      // (a second dword starting at/after the stream end is never needed)
+      const int32_t a = c & ~3;
+      const int32_t a2 = (a + 4 < nrel) ? a + 4 : a;
+      const uint32_t w0 = *(const uint32_t*)(tb + a);
+      const uint32_t w1 = *(const uint32_t*)(tb + a2);
+      const int32_t len = __builtin_amdgcn_readfirstlane(fe_len(w0, w1, c));
+      int32_t q = 0;
+      const uint16_t code = fe_hop_len(len, c, nrel, maxp32, q);
+      if (code != FE_GO && (code & F0_TERM) && code != F0_ESC) {
+        fin = code;                          // terminal: not a frame start
+        break;
+      }
+      ent = lane == (m & 63) ? (uint32_t)c : ent;   // entry m -> lane m&63
+      ++m;
+      if ((m & 63) == 0) L[m - 64 + lane] = (uint16_t)ent;
+      if (code != FE_GO) { fin = code; break; }    // leaves the tile
+      c = q;
+    }
+    if (lane < (m & 63)) L[(m & ~63) + lane] = (uint16_t)ent;
+    if (lane == 0) rcount[t * FE_NSURV + sl] = m;
+    fins[sl] = fin;
+  }
+  if (any_sv) fe_patch_row(f0 + t * FS_W, lane, fins);
 }
 
 // D'' fs_join: the tile's frame starts from its exact entry e*.  Every chain
-// that reaches the survivor's tree passes through the survivor's hand-off
+// that reaches a survivor's tree passes through that survivor's hand-off
 // position r0 = R[0] (merges into it all happened at positions <= r0), so
 // walk from e* (uniform scalar loop, global memory, usually 0-5 hops) until
-// r0, then the rest is R.  A chain that misses r0 (bad frame, or a tile
-// whose survivor was a garbage walker) is simply walked to its end.
+// one of the r0, then the rest is that R.  A chain that meets neither (bad
+// frame, or survivors that were garbage chains) is simply walked to its end.
 __global__ __launch_bounds__(256) void fs_join(
     const uint8_t* __restrict__ buf, int64_t n, int64_t maxp, int64_t tiles,
     const int64_t* __restrict__ ent, const uint16_t* __restrict__ list,
@@ -922,16 +1081,24 @@ __global__ __launch_bounds__(256) void fs_join(
   const int32_t te = (int32_t)(min(ts + FS_S, n) - ts);
   const int32_t nrel = (int32_t)min(n - ts, (int64_t)1 << 30);
   const int32_t maxp32 = (int32_t)min(maxp, (int64_t)1 << 30);
-  const int32_t m = __builtin_amdgcn_readfirstlane(rcount[t]);
-  int32_t r0 = m > 0 ? __builtin_amdgcn_readfirstlane(
-                           (int32_t)list[t * FS_LMAX]) : -1;
+  const int32_t m0 = __builtin_amdgcn_readfirstlane(rcount[t * FE_NSURV]);
+  int32_t r0 = m0 > 0 ? __builtin_amdgcn_readfirstlane(
+                            (int32_t)list[(t * FE_NSURV) * FS_LMAX]) : -1;
+  int32_t m1 = 0, r1 = -1;
+  if constexpr (FE_NSURV > 1) {
+    m1 = __builtin_amdgcn_readfirstlane(rcount[t * FE_NSURV + 1]);
+    r1 = m1 > 0 ? __builtin_amdgcn_readfirstlane(
+                      (int32_t)list[(t * FE_NSURV + 1) * FS_LMAX]) : -1;
+  }
   int32_t c = __builtin_amdgcn_readfirstlane((int32_t)(e - ts));
   int32_t np = 0;
-  bool useR = false;
+  int32_t use = -1;
   uint16_t* P = pre + t * FS_LMAX;
   while (c < te) {
-    if (c == r0) { useR = true; break; }
-    if (c > r0) r0 = -1;                   // not in the survivor's tree
+    if (c == r0) { use = 0; break; }
+    if (c == r1) { use = 1; break; }
+    if (c > r0) r0 = -1;                   // not in that survivor's tree
+    if (c > r1) r1 = -1;
     if (c + 4 > nrel) break;               // partial length at the end
     const int32_t len = __builtin_amdgcn_readfirstlane(ld_be32(buf + ts + c));
     const int32_t nx = c + 4 + len;
@@ -941,12 +1108,13 @@ __global__ __launch_bounds__(256) void fs_join(
     c = nx;
   }
   if (lane == 0) {
-    npre_out[t] = np;
-    counts[t] = np + (useR ? m : 0);
+    // npre: prefix length | the survivor slot whose R follows (-1: none)
+    npre_out[t] = np | ((use + 1) << 28);
+    counts[t] = np + (use == 0 ? m0 : (use == 1 ? m1 : 0));
   }
 }
 
-// E'' list -> (body offset, length): prefix from fs_join, then R.
+// E'' list -> (body offset, length): prefix from fs_join, then that R.
 __global__ __launch_bounds__(256) void fs_write_join(
     const uint8_t* __restrict__ buf, int64_t tiles,
     const uint16_t* __restrict__ pre, const int32_t* __restrict__ npre,
@@ -957,11 +1125,13 @@ __global__ __launch_bounds__(256) void fs_write_join(
   if (t >= tiles) return;
   const int lane = threadIdx.x & 63;
   const int64_t cnt = counts[t];
-  const int32_t np = npre[t];
+  const int32_t pk = npre[t];
+  const int32_t np = pk & 0x0FFFFFFF;
+  const int32_t use = (pk >> 28) - 1;
   const int64_t b = base[t];
   const int64_t ts = t * FS_S;
   const uint16_t* Pp = pre + t * FS_LMAX;
-  const uint16_t* R = list + t * FS_LMAX;
+  const uint16_t* R = list + (t * FE_NSURV + (use < 0 ? 0 : use)) * FS_LMAX;
   for (int64_t k = lane; k < cnt; k += 64) {
     const int64_t P = ts + (k < np ? Pp[k] : R[k - np]);
     const int64_t idx = b + k;
@@ -1005,10 +1175,10 @@ static FsPlan fs_plan(int64_t n) {
   p.off_cnt = take((size_t)tiles * 8);
   p.off_base = take((size_t)tiles * 8);
   p.off_scan = take((size_t)zk_scan_workspace(tiles) * 8);
-  p.off_list = take((size_t)tiles * FS_LMAX * 2);
+  p.off_list = take((size_t)tiles * FE_NSURV * FS_LMAX * 2);
   p.off_pre = take((size_t)tiles * FS_LMAX * 2);
-  p.off_surv = take((size_t)tiles * 4);
-  p.off_rcnt = take((size_t)tiles * 4);
+  p.off_surv = take((size_t)tiles * FE_NSURV * 4);
+  p.off_rcnt = take((size_t)tiles * FE_NSURV * 4);
   p.off_npre = take((size_t)tiles * 4);
   p.total = o;
   return p;
@@ -1064,8 +1234,23 @@ int zk_frame_scan(const uint8_t* buf, int64_t n, int64_t maxp, uint8_t* ws,
     fs_frontier<<<(unsigned)tiles, FE_T, FE_LDS, st>>>(buf, n, maxp, f0w,
                                                       surv);
     ZK_LAUNCH_CHECK();
-    fs_survivor<<<(unsigned)tiles, 64, FV_LDS, st>>>(buf, n, maxp, f0w, surv,
-                                                    list, rcnt);
+    // Survivor walk: LDS-staged (one LDS round trip per hop, but the 16 KiB
+    // tile caps a CU at 9 walks) when every tile can walk at once, global
+    // (slower hops, 32 walks per CU) when tiles outnumber the LDS slots.
+    // ZKMI_FS_SURVIVOR=lds|global forces one.
+    static int sv_force = -1;
+    if (sv_force < 0) {
+      const char* m = getenv("ZKMI_FS_SURVIVOR");
+      sv_force = !m ? 0 : (m[0] == 'l' ? 1 : (m[0] == 'g' ? 2 : 0));
+    }
+    const int64_t lds_slots = 9LL * 256;
+    const int sv_mode = sv_force ? sv_force : (tiles <= 2 * lds_slots ? 1 : 2);
+    if (sv_mode == 1)
+      fs_survivor<<<(unsigned)tiles, 64, FV_LDS, st>>>(buf, n, maxp, f0w,
+                                                      surv, list, rcnt);
+    else
+      fs_survivor_g<<<(unsigned)((tiles + 3) / 4), 256, 0, st>>>(
+          buf, n, maxp, tiles, f0w, surv, list, rcnt);
   } else {
     const size_t lds_a = FS_S * 2 + FS_LIST * 2 + (FS_T / 64 + 1) * 8;
     fs_exits<<<(unsigned)tiles, FS_T, lds_a, st>>>(buf, n, maxp, f0w);

@@ -112,20 +112,21 @@ int main(int argc, char** argv) {
   hipEvent_t a, b; CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
   const unsigned grid = (unsigned)((tiles + TPB - 1) / TPB);
   const size_t lds = TPB * (S + 16);
-  auto run = [&](auto kern, const char* name) {
-    for (int i = 0; i < 3; ++i) kern<<<grid, 256, lds>>>(d, n, tiles, de, dl, dc);
+  auto run = [&](auto kern, const char* name, size_t lds_bytes) {
+    for (int i = 0; i < 3; ++i) kern<<<grid, 256, lds_bytes>>>(d, n, tiles, de, dl, dc);
     CK(hipEventRecord(a));
     const int R = 10;
-    for (int i = 0; i < R; ++i) kern<<<grid, 256, lds>>>(d, n, tiles, de, dl, dc);
+    for (int i = 0; i < R; ++i) kern<<<grid, 256, lds_bytes>>>(d, n, tiles, de, dl, dc);
     CK(hipEventRecord(b)); CK(hipEventSynchronize(b));
     float ms; CK(hipEventElapsedTime(&ms, a, b));
     int64_t c0; CK(hipMemcpy(&c0, dc, 8, hipMemcpyDeviceToHost));
     printf("%-28s %8.1f us  (tile0 frames %lld)\n", name, ms * 1000 / R, (long long)c0);
   };
   printf("frame %d B, %lld frames, %lld tiles\n", frame, (long long)nframes, (long long)tiles);
-  run(walk<0>, "stage only");
-  run(walk<1>, "stage + lane0 walk");
-  run(walk<2>, "stage + uniform walk");
-  run(walk<3>, "uniform walk from global");
+  run(walk<0>, "stage only", lds);
+  run(walk<1>, "stage + lane0 walk", lds);
+  run(walk<2>, "stage + uniform walk", lds);
+  run(walk<3>, "uniform walk from global", lds);
+  run(walk<3>, "global walk, no LDS", 0);
   return 0;
 }

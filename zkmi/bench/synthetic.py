@@ -254,8 +254,6 @@ class GetPipeline(object):
         self.dev = dev
         self.xt = B.XidTable(bits=max(20, (batch - 1).bit_length() + 1),
                              device=dev)
-        self.gen = torch.Generator(device=dev)
-        self.gen.manual_seed(seed + 1)
         n = batch
         # request descriptors (reused every step)
         self.opcode = torch.full((n,), consts.OP_CODES['GET_DATA'],
@@ -273,18 +271,33 @@ class GetPipeline(object):
         self.reply = B.alloc_replies(n, dev)
         self.xid_base = 0
         self.last = None
+        self.seed = seed
+        self.step_no = 0
+        self.idx = torch.empty(n, dtype=I64, device=dev)
+        self.xid = torch.empty(n, dtype=I32, device=dev)
+        self.poff = torch.empty(n, dtype=I64, device=dev)
+        self.plen = torch.empty(n, dtype=I32, device=dev)
 
-    def step(self, validate=True):
+    def step(self, validate=True, acc=None):
+        """One batch.  With ``validate`` the number of correct replies is
+        added to ``acc`` (device int64 [1]; a fresh one when None), which is
+        returned.  Request generation and the reply check are one fused
+        kernel each (csrc/kernels/bench.hip)."""
         t = self.tree
         n = self.batch
-        idx = torch.randint(t.leaf0, t.leaf0 + t.n_leaves, (n,),
-                            generator=self.gen, device=self.dev)
-        xid = (torch.arange(n, dtype=I32, device=self.dev) +
-               self.xid_base) & 0x7fffffff
+        L = _lib.lib()
+        sp = _lib.stream_ptr()
+        seed = (self.seed * 0x9E3779B97F4A7C15 + self.step_no) & (2**64 - 1)
+        self.step_no += 1
+        _lib.check(L.zk_bench_gen_get(
+            n, seed, t.leaf0, t.n_leaves, self.xid_base,
+            _lib.ptr(t.node_path_off), _lib.ptr(t.node_path_len),
+            _lib.ptr(self.idx), _lib.ptr(self.xid), _lib.ptr(self.poff),
+            _lib.ptr(self.plen), sp), 'zk_bench_gen_get')
+        xid = self.xid
         self.xid_base = (self.xid_base + n) & 0x7fffffff
-        rb = B.RequestBatch(n, self.opcode, xid, self.arg,
-                            t.node_path_off[idx], t.node_path_len[idx],
-                            self.zero64, self.zero32, self.zero32,
+        rb = B.RequestBatch(n, self.opcode, xid, self.arg, self.poff,
+                            self.plen, self.zero64, self.zero32, self.zero32,
                             t.path_arena, t.slab, self.acl_off,
                             self.acl_len, self.acl_arena)
         tx, rec_off, total, err = B.encode_requests(rb, self.xt, out=self.tx)
@@ -293,15 +306,17 @@ class GetPipeline(object):
         nrx = int(rtotal.item())
         ft = B.frame_scan(rx, nrx, cap=n)
         rep = B.decode_replies(rx, ft, self.xt, out=self.reply)
-        self.last = (idx, rep, rx, ft)
-        if validate:
-            ok = ((rep.status[:n] == 0) & (rep.err[:n] == 0) &
-                  (rep.opcode[:n] == consts.OP_CODES['GET_DATA']) &
-                  (rep.xid[:n] == xid) &
-                  (rep.stat64[0, :n] == idx + 1) &
-                  (rep.pay_len[:n] == t.data_len[idx]))
-            return ok.sum()
-        return None
+        self.last = (self.idx, rep, rx, ft)
+        if not validate:
+            return None
+        if acc is None:
+            acc = torch.zeros(1, dtype=I64, device=self.dev)
+        _lib.check(L.zk_bench_check_get(
+            n, _lib.ptr(rep.status), _lib.ptr(rep.err), _lib.ptr(rep.opcode),
+            _lib.ptr(rep.xid), _lib.ptr(rep.stat64[0]), _lib.ptr(rep.pay_len),
+            _lib.ptr(self.idx), _lib.ptr(xid), _lib.ptr(t.data_len),
+            _lib.ptr(acc), sp), 'zk_bench_check_get')
+        return acc
 
 
 def _arena(strings, dev):
@@ -476,7 +491,7 @@ class MixPipeline(object):
                               self.data_arena, self.acl_off, self.acl_len,
                               self.acl_arena)
 
-    def step(self, validate=True, n=None):
+    def step(self, validate=True, n=None, acc=None):
         n = self.n if n is None else n
         rb = self._batch(n, self.s % 3)
         rep, _ = self.drv.run(rb)
@@ -487,7 +502,10 @@ class MixPipeline(object):
         ok = ((rep.status[:n] == 0) & (rep.err[:n] == self.want_err[:n]) &
               (rep.xid[:n] == rb.xid) & (rep.opcode[:n] == rb.opcode) &
               (~self.is_set_ok[:n] | (rep.stat32[0, :n] == 1)))
-        return ok.sum()
+        if acc is None:
+            return ok.sum()
+        acc += ok.sum()
+        return acc
 
     def diagnose(self):
         rb, rep = self.last
@@ -539,7 +557,7 @@ class StormPipeline(object):
             (self.acl_arena, self.acl_off, self.acl_len))
         self.step(validate=False)            # first session's nodes
 
-    def step(self, validate=True):
+    def step(self, validate=True, acc=None):
         t = self.tree
         n = self.n
         if (self.inserted + 2 * n) > 0.6 * t.hcap:
@@ -563,7 +581,11 @@ class StormPipeline(object):
               (rep.xid[:n] == rb.xid) &
               (rep.pay_len[:n] == self.want_len)).sum()
         # the expiry must have removed exactly one step's nodes
-        return torch.where(self.removed[0] == n, ok, 0)
+        ok = torch.where(self.removed[0] == n, ok, 0)
+        if acc is None:
+            return ok
+        acc += ok
+        return acc
 
     def diagnose(self):
         rb, rep = self.last

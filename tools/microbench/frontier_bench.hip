@@ -27,13 +27,17 @@ static void fill(std::vector<uint8_t>& h, int kind, int64_t nframes) {
                (long long)i);
       const int pl = (int)strlen(path);
       len = 4 + 4 + 4 + 4 + pl + 1;
-      auto be = [&](int o, uint32_t v) { f[o] = v >> 24; f[o+1] = v >> 16; f[o+2] = v >> 8; f[o+3] = v; };
+      auto be = [&](int o, uint32_t v) {
+        f[o] = v >> 24; f[o + 1] = v >> 16; f[o + 2] = v >> 8; f[o + 3] = v;
+      };
       be(0, len - 4); be(4, (uint32_t)i); be(8, 4); be(12, pl);
       memcpy(f + 16, path, pl); f[16 + pl] = 0;
     } else {                         // GET_DATA reply: 100 B data + Stat
       len = 192;
       for (int k = 0; k < len; ++k) f[k] = rand() & 0xff;
-      auto be = [&](int o, uint32_t v) { f[o] = v >> 24; f[o+1] = v >> 16; f[o+2] = v >> 8; f[o+3] = v; };
+      auto be = [&](int o, uint32_t v) {
+        f[o] = v >> 24; f[o + 1] = v >> 16; f[o + 2] = v >> 8; f[o + 3] = v;
+      };
       be(0, 188); be(4, (uint32_t)i); be(8, 0); be(12, 5000000 + (uint32_t)i); be(16, 0);
       be(20, 100);
       memset(f + 124, 0, 68);        // Stat: mostly zeros / small values

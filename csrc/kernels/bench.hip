@@ -36,6 +36,12 @@ __global__ __launch_bounds__(BG_T) void bench_gen_get(
   path_len[i] = node_path_len[v];
 }
 
+// Grid-stride with a bounded grid: one device-scope atomic per block, and a
+// single counter word sustains only ~88 returning atomics per microsecond
+// (MI355X_MICROARCH.md "dequeue"), so 4096 one-shot blocks would serialise
+// ~46 us on it.
+constexpr int BG_CHECK_BLOCKS = 512;
+
 __global__ __launch_bounds__(BG_T) void bench_check_get(
     int64_t n, const int32_t* __restrict__ status,
     const int32_t* __restrict__ err, const int32_t* __restrict__ opcode,
@@ -44,13 +50,13 @@ __global__ __launch_bounds__(BG_T) void bench_check_get(
     const int32_t* __restrict__ xid, const int32_t* __restrict__ data_len,
     unsigned long long* __restrict__ ok) {
   __shared__ int64_t sm[BG_T / 64 + 1];
-  const int64_t i = (int64_t)blockIdx.x * BG_T + threadIdx.x;
   int64_t good = 0;
-  if (i < n) {
+  for (int64_t i = (int64_t)blockIdx.x * BG_T + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * BG_T) {
     const int64_t v = idx[i];
-    good = status[i] == 0 && err[i] == 0 && opcode[i] == OP_GET_DATA &&
-           rxid[i] == xid[i] && czxid[i] == v + 1 &&
-           pay_len[i] == data_len[v];
+    good += status[i] == 0 && err[i] == 0 && opcode[i] == OP_GET_DATA &&
+            rxid[i] == xid[i] && czxid[i] == v + 1 &&
+            pay_len[i] == data_len[v];
   }
   int64_t tot;
   block_excl_scan(good, sm, &tot);
@@ -80,9 +86,10 @@ int zk_bench_check_get(int64_t n, const int32_t* status, const int32_t* err,
                        const int32_t* data_len, unsigned long long* ok,
                        hipStream_t st) {
   if (n <= 0) return 0;
-  zk::bench_check_get<<<(unsigned)((n + zk::BG_T - 1) / zk::BG_T), zk::BG_T,
-                        0, st>>>(n, status, err, opcode, rxid, czxid, pay_len,
-                                 idx, xid, data_len, ok);
+  const int64_t nb = min((n + zk::BG_T - 1) / zk::BG_T,
+                         (int64_t)zk::BG_CHECK_BLOCKS);
+  zk::bench_check_get<<<(unsigned)nb, zk::BG_T, 0, st>>>(
+      n, status, err, opcode, rxid, czxid, pay_len, idx, xid, data_len, ok);
   ZK_LAUNCH_CHECK();
   return 0;
 }

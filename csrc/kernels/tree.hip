@@ -4,8 +4,10 @@
 // tests talk to, so that the whole request -> reply path runs at HBM speed.
 //
 // Layout (HBM, sized by the caller for 288 GB parts):
-//   * open-addressing hash table: keys = FNV-1a(path) | 1, vals = node index
-//     (-2 = tombstone, -3 = being published), linear probing, pow2 capacity;
+//   * open-addressing hash table of 16-byte entries {key, val} (one load per
+//     probe): key = word-wise multiply-xorshift hash of the path | 1, val =
+//     node index (-2 = tombstone, -3 = being published), linear probing,
+//     pow2 capacity;
 //   * node slots in wire format (zk_batch.h ZkNodeStore), so replies are
 //     contiguous copies;
 //   * a path arena holding each node's path for exact-match verification;
@@ -40,8 +42,7 @@
 
 extern "C" {
 struct ZkTree {
-  int64_t* keys;
-  int64_t* vals;
+  int64_t* ht;                 // [2 * (mask + 1)] interleaved {key, val}
   int64_t mask;
   int64_t* node_path_off;
   int32_t* node_path_len;
@@ -130,41 +131,55 @@ ZK_DEV int64_t wave_bytes(int64_t* ctr, int64_t amount) {
 }
 
 // ---- hash index -----------------------------------------------------------
-ZK_DEV uint64_t fnv1a(const uint8_t* p, int32_t n) {
-  uint64_t h = 1469598103934665603ull;
+// Path hash: 8 bytes per step (unaligned loads), a multiply-xorshift per
+// word and a final avalanche — 4 multiplies for a 25-byte path where a
+// byte-serial FNV-1a needs 25.
+ZK_DEV uint64_t path_hash(const uint8_t* p, int32_t n) {
+  uint64_t h = 0x9E3779B97F4A7C15ull ^ (uint64_t)n;
   int32_t i = 0;
-  for (; i + 4 <= n; i += 4) {
-    uint32_t w; __builtin_memcpy(&w, p + i, 4);
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      h ^= (w >> (8 * b)) & 0xff;
-      h *= 1099511628211ull;
-    }
+  for (; i + 8 <= n; i += 8) {
+    uint64_t w; __builtin_memcpy(&w, p + i, 8);
+    h = (h ^ w) * 0xFF51AFD7ED558CCDull;
+    h ^= h >> 32;
   }
-  for (; i < n; ++i) { h ^= p[i]; h *= 1099511628211ull; }
+  if (i < n) {
+    uint64_t w = 0;
+    for (int32_t k = 0; i + k < n; ++k) w |= (uint64_t)p[i + k] << (8 * k);
+    h = (h ^ w) * 0xFF51AFD7ED558CCDull;
+    h ^= h >> 32;
+  }
+  h ^= h >> 33;
+  h *= 0xC4CEB9FE1A85EC53ull;
+  h ^= h >> 33;
   return h;
 }
 
 ZK_DEV bool bytes_eq(const uint8_t* a, const uint8_t* b, int32_t n) {
   int32_t i = 0;
-  for (; i + 4 <= n; i += 4) {
-    uint32_t x, y; __builtin_memcpy(&x, a + i, 4); __builtin_memcpy(&y, b + i, 4);
+  for (; i + 8 <= n; i += 8) {
+    uint64_t x, y; __builtin_memcpy(&x, a + i, 8); __builtin_memcpy(&y, b + i, 8);
     if (x != y) return false;
   }
   for (; i < n; ++i) if (a[i] != b[i]) return false;
   return true;
 }
 
+ZK_DEV int64_t* ht_key(const ZkTree& t, int64_t s) { return &t.ht[2 * s]; }
+ZK_DEV int64_t* ht_val(const ZkTree& t, int64_t s) { return &t.ht[2 * s + 1]; }
+
 ZK_DEV int64_t tree_find(const ZkTree& t, const uint8_t* p, int32_t n) {
-  const int64_t key = (int64_t)(fnv1a(p, n) | 1ull);
+  const int64_t key = (int64_t)(path_hash(p, n) | 1ull);
   int64_t s = key & t.mask;
   for (int64_t probe = 0; probe <= t.mask; ++probe) {
-    const int64_t k = __hip_atomic_load(&t.keys[s], __ATOMIC_RELAXED,
-                                        __HIP_MEMORY_SCOPE_AGENT);
+    // one 16-byte load per probe; entries being written concurrently in
+    // this launch may read torn (val -3): not found, as the batch contract
+    // allows for same-batch conflicts
+    const int4 e = *(const int4*)ht_key(t, s);
+    const int64_t k = (int64_t)(((uint64_t)(uint32_t)e.y << 32) | (uint32_t)e.x);
     if (k == 0) return -1;
     if (k == key) {
-      const int64_t v = __hip_atomic_load(&t.vals[s], __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_AGENT);
+      const int64_t v = (int64_t)(((uint64_t)(uint32_t)e.w << 32) |
+                                  (uint32_t)e.z);
       if (v >= 0 && t.node_path_len[v] == n &&
           bytes_eq(t.path_arena + t.node_path_off[v], p, n))
         return v;
@@ -178,27 +193,27 @@ ZK_DEV int64_t tree_find(const ZkTree& t, const uint8_t* p, int32_t n) {
 // the path is present (NODE_EXISTS), else v.
 ZK_DEV int64_t tree_insert(const ZkTree& t, int64_t v, const uint8_t* p,
                            int32_t n) {
-  const int64_t key = (int64_t)(fnv1a(p, n) | 1ull);
+  const int64_t key = (int64_t)(path_hash(p, n) | 1ull);
   int64_t s = key & t.mask;
   for (int64_t probe = 0; probe <= t.mask; ++probe) {
-    const int64_t k = atomicCAS((unsigned long long*)&t.keys[s], 0ull,
+    const int64_t k = atomicCAS((unsigned long long*)ht_key(t, s), 0ull,
                                 (unsigned long long)key);
     if (k == 0) {                         // claimed an empty slot
-      __hip_atomic_store(&t.vals[s], v, __ATOMIC_RELAXED,
+      __hip_atomic_store(ht_val(t, s), v, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
       return v;
     }
     if (k == key) {
       int64_t w = -3;
-      // The claimer may not have published vals yet: bounded wait.
+      // The claimer may not have published the val yet: bounded wait.
       for (int spin = 0; spin < 1000000 && w == -3; ++spin)
-        w = __hip_atomic_load(&t.vals[s], __ATOMIC_RELAXED,
+        w = __hip_atomic_load(ht_val(t, s), __ATOMIC_RELAXED,
                               __HIP_MEMORY_SCOPE_AGENT);
       if (w >= 0 && t.node_path_len[w] == n &&
           bytes_eq(t.path_arena + t.node_path_off[w], p, n))
         return w;
       if (w == -2 &&                      // tombstone of the same key: reuse
-          atomicCAS((unsigned long long*)&t.vals[s], (unsigned long long)-2,
+          atomicCAS((unsigned long long*)ht_val(t, s), (unsigned long long)-2,
                     (unsigned long long)v) == (unsigned long long)-2)
         return v;
     }
@@ -211,12 +226,12 @@ ZK_DEV int64_t tree_insert(const ZkTree& t, int64_t v, const uint8_t* p,
 // several erase the same node concurrently (the CAS winner owns the free).
 ZK_DEV bool tree_erase(const ZkTree& t, int64_t v, const uint8_t* p,
                        int32_t n) {
-  const int64_t key = (int64_t)(fnv1a(p, n) | 1ull);
+  const int64_t key = (int64_t)(path_hash(p, n) | 1ull);
   int64_t s = key & t.mask;
   for (int64_t probe = 0; probe <= t.mask; ++probe) {
-    const int64_t k = t.keys[s];
+    const int64_t k = *ht_key(t, s);
     if (k == 0) return false;
-    if (k == key && atomicCAS((unsigned long long*)&t.vals[s],
+    if (k == key && atomicCAS((unsigned long long*)ht_val(t, s),
                               (unsigned long long)v,
                               (unsigned long long)-2) ==
                         (unsigned long long)v)

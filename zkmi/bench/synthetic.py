@@ -108,8 +108,9 @@ class GpuTree(object):
                                      minlength=ndirs)[:ndirs]
         nk = torch.from_numpy(nkids).to(dev)
         hcap = _next_pow2(2 * cap)
-        self.keys = torch.zeros(hcap, dtype=I64, device=dev)
-        self.vals = torch.full((hcap,), -3, dtype=I64, device=dev)
+        # interleaved {key, val} entries (csrc/kernels/tree.hip)
+        self.ht = torch.zeros(2 * hcap, dtype=I64, device=dev)
+        self.ht.view(-1, 2)[:, 1] = -3
         cnt = [0] * _lib.TC_N
         cnt[_lib.TC_NODES], cnt[_lib.TC_ZXID] = nst, nst
         cnt[_lib.TC_PATH_TOP], cnt[_lib.TC_SLAB_TOP] = len(arena), nst * sb
@@ -136,7 +137,7 @@ class GpuTree(object):
                               self.data_len.data_ptr(),
                               self.slot_cap.data_ptr(), self.cap)
         self.store = st
-        return _lib.ZkTree(self.keys.data_ptr(), self.vals.data_ptr(), mask,
+        return _lib.ZkTree(self.ht.data_ptr(), mask,
                            self.node_path_off.data_ptr(),
                            self.node_path_len.data_ptr(),
                            self.node_parent.data_ptr(),
@@ -167,8 +168,8 @@ class GpuTree(object):
         by deleted paths that are never re-created, e.g. SEQUENTIAL names).
         One host read of the node high-water mark."""
         n = int(self.counters[_lib.TC_NODES].item())
-        self.keys.zero_()
-        self.vals.fill_(-3)
+        self.ht.zero_()
+        self.ht.view(-1, 2)[:, 1] = -3
         _lib.check(_lib.lib().zk_tree_build(ctypes.byref(self._struct), 0,
                                             min(n, self.cap),
                                             _lib.stream_ptr()),

@@ -60,7 +60,7 @@ class ZkReqOut(ctypes.Structure):
 
 
 class ZkTree(ctypes.Structure):
-    _fields_ = [('keys', P), ('vals', P), ('mask', I64),
+    _fields_ = [('ht', P), ('mask', I64),
                 ('node_path_off', P), ('node_path_len', P),
                 ('node_parent', P), ('path_arena', P), ('path_cap', I64),
                 ('slab_cap', I64), ('counters', P), ('store', ZkNodeStore),

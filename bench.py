@@ -80,11 +80,20 @@ def main():
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
-    dev = torch.device('cuda', local)
+    # One rank per GPU over RCCL ("nccl").  ZKMI_BENCH_BACKEND=gloo (host
+    # collectives, ranks may share a GPU) exists only to rehearse the
+    # multi-rank path on a one-GPU box.
+    backend = os.environ.get('ZKMI_BENCH_BACKEND', 'nccl')
+    ndev = torch.cuda.device_count()
+    gpu = local % ndev if backend == 'gloo' else local
+    dev = torch.device('cuda', gpu)
     torch.cuda.set_device(dev)
+    if world > 1:
+        if backend == 'nccl':
+            dist.init_process_group('nccl', device_id=dev)
+        else:
+            dist.init_process_group(backend)
+    cdev = dev if backend == 'nccl' else torch.device('cpu')
 
     from zkmi.bench import synthetic as S
     if a.workload == 'get':
@@ -121,8 +130,8 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
 
-    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    ok = ok_total.clone()
+    el = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
+    ok = ok_total.to(cdev)
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
         dist.all_reduce(ok, op=dist.ReduceOp.SUM)   # R4: node-level counters

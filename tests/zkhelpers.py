@@ -28,19 +28,39 @@ def client(servers, session_timeout=None, config=None, **kw):
     if session_timeout is not None:
         o['sessionTimeout'] = session_timeout
     o.update(kw)
-    return Client(o)
+    rec = Recorder(None)
+    o['listeners'] = rec.listeners()
+    c = Client(o)
+    c._test_recorder = rec
+    return c
 
 
 class Recorder(object):
     """Collects client events in order (the reference tests push event
-    names into an array, test/basic.test.js:1001-1004)."""
+    names into an array, test/basic.test.js:1001-1004).  ``client()``
+    attaches one before the client starts; ``Recorder(c)`` returns it, so
+    no early 'session'/'connect' is lost to the loop thread."""
 
-    def __init__(self, c, events=('session', 'connect', 'disconnect',
-                                  'expire', 'failed', 'close')):
+    EVENTS = ('session', 'connect', 'disconnect', 'expire', 'failed', 'close')
+
+    def __new__(cls, c, events=EVENTS):
+        pre = getattr(c, '_test_recorder', None)
+        if pre is not None:
+            return pre
+        return object.__new__(cls)
+
+    def __init__(self, c, events=EVENTS):
+        if getattr(self, 'events', None) is not None:
+            return
         self.events = []
         self.lock = threading.Lock()
-        for e in events:
-            c.on(e, self._mk(e))
+        self._names = events
+        if c is not None:
+            for e in events:
+                c.on(e, self._mk(e))
+
+    def listeners(self):
+        return [(e, self._mk(e)) for e in self._names]
 
     def _mk(self, e):
         def f(*a):

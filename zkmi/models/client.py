@@ -20,6 +20,7 @@ from .. import consts
 from ..config import ClientConfig
 from ..errors import ZKNotConnectedError
 from ..jute import DEFAULT_ACL, Stat  # noqa: F401  (re-export)
+from ..runtime.emitter import EventEmitter
 from ..runtime.fsm import FSM
 from ..runtime.loop import default_loop
 from ..utils.log import create_logger
@@ -83,7 +84,8 @@ class Client(FSM):
     ``sessionTimeout`` (ms, default 30000), ``log``, ``collector``,
     ``loop``, ``config`` (:class:`~zkmi.config.ClientConfig`) and
     ``session`` (credentials from :meth:`credentials` to resume an existing
-    session)."""
+    session) and ``listeners`` (``{event: fn}`` or ``[(event, fn)]``,
+    attached before the client starts, so none of its events is missed)."""
 
     def __init__(self, opts=None, **kw):
         o = dict(opts or {})
@@ -118,6 +120,12 @@ class Client(FSM):
         # bulk codec device: None = the current GPU if any, False = host
         self.bulk_device = o.get('device')
         self._resume_cred = o.get('session')
+        # listeners attached before the FSM starts: a JS caller attaching
+        # in the constructor's tick sees every event; on a loop thread that
+        # only holds if the listeners are in place before the resolver runs
+        self._early = list((o.get('listeners') or {}).items()) \
+            if isinstance(o.get('listeners'), dict) \
+            else list(o.get('listeners') or ())
         self.session = None
         self.old_session = None
         self.conns = {}
@@ -125,6 +133,10 @@ class Client(FSM):
         self.loop.run(self._init_on_loop)
 
     def _init_on_loop(self):
+        EventEmitter.__init__(self)
+        for evt, fn in self._early:
+            self.on(evt, fn)
+        self._early = None
         self.resolver = StaticResolver(self.servers, consts.DEFAULT_PORT)
         self.cset = ConnectionSet(self.resolver, self._makeConnection,
                                  self.loop, self.log, self.config)

@@ -75,6 +75,7 @@ TC_FREE_HEAD, TC_FREE_TAIL, TC_FREE_PUB, TC_DIRTY, TC_N = 4, 5, 6, 7, 8
 
 _SIGS = {
     'zk_scan_workspace': (I64, [I64]),
+    'zk_scan_set_mode': (I32, [I32]),
     'zk_scan_excl_i64': (I32, [P, P, I64, P, P, P]),
     'zk_scan_excl_i32': (I32, [P, P, I64, P, P, P]),
     'zk_encode_requests': (I32, [P, I64, P, P, P, P, P, I64, P, I64, P, P]),
@@ -118,7 +119,19 @@ def lib():
             f.restype = res
             f.argtypes = args
         _lib = L
+        # ZKMI_SCAN=shfl selects the shuffle scan engine instead of the
+        # MFMA byte-plane one (csrc/kernels/scan.hip)
+        L.zk_scan_set_mode(0 if os.environ.get('ZKMI_SCAN') == 'shfl' else 1)
     return _lib
+
+
+SCAN_SHFL, SCAN_MFMA, SCAN_MFMA_W1, SCAN_MFMA_W4 = 0, 1, 2, 3
+
+
+def set_scan_mode(mode):
+    """Select the prefix-scan engine used by every encoder; returns the
+    previous mode."""
+    return lib().zk_scan_set_mode(mode)
 
 
 def available():

@@ -380,6 +380,24 @@ def decode_replies(buf, frames, xid_table, out=None, stream=None):
     return out
 
 
+def exclusive_scan(x, stream=None):
+    """Device-wide exclusive prefix sum of an int32/int64 vector -> (int64
+    prefix, int64 total).  The engine (MFMA byte-plane or shuffle) is the
+    one selected by :func:`zkmi.ops._lib.set_scan_mode`."""
+    L = _lib.lib()
+    n = x.numel()
+    dev = x.device
+    base = torch.empty(max(n, 1), dtype=I64, device=dev)
+    total = torch.zeros(1, dtype=I64, device=dev)
+    ws = torch.empty(L.zk_scan_workspace(max(n, 1)), dtype=I64, device=dev)
+    fn = L.zk_scan_excl_i32 if x.dtype == torch.int32 else L.zk_scan_excl_i64
+    if x.dtype not in (torch.int32, torch.int64):
+        raise TypeError('exclusive_scan: int32 or int64 input')
+    check(fn(ptr(x), ptr(base), n, ptr(total), ptr(ws), stream_ptr(stream)),
+          'zk_scan_excl')
+    return base[:n], total
+
+
 def _scan_i32(counts, stream=None):
     L = _lib.lib()
     n = counts.numel()

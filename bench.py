@@ -18,14 +18,17 @@ node payloads, uniformly random node per request.
 One process per GPU (torchrun); per-GPU work is fixed (weak scaling).  The
 whole-node aggregate (sum over ranks of ops / max-rank time) is reported.
 ``p50_get_rtt_us`` is the interactive path: one blocking ``Client.get``
-round trip over loopback TCP to the in-process fake server (host CPU), also
-reported for honesty about where the GPU helps.
+round trip over loopback TCP to the fake server running as its own process
+(``python -m zkmi.server``, started before the GPU is touched), with the
+client on the native epoll loop; reported for honesty about where the GPU
+helps.
 """
 
 import argparse
 import json
 import os
 import statistics
+import subprocess
 import sys
 import time
 
@@ -41,26 +44,34 @@ sys.path.insert(0, ROOT)
 REF_PKTS_PER_S = 0.51e6
 
 
-def measure_rtt(n=2000):
+def start_rtt_server():
+    """The fake ZooKeeper in a child process (a real ZooKeeper does not share
+    the client's interpreter).  Started before any GPU call."""
+    p = subprocess.Popen([sys.executable, '-m', 'zkmi.server'], cwd=ROOT,
+                         stdin=subprocess.PIPE, stdout=subprocess.PIPE,
+                         text=True)
+    line = p.stdout.readline().split()
+    if len(line) != 2 or line[0] != 'PORT':
+        p.kill()
+        raise SystemExit('fake server did not start: %r' % line)
+    return p, int(line[1])
+
+
+def measure_rtt(port, n=2000):
     from zkmi import Client
-    from zkmi.server import FakeZKServer
-    srv = FakeZKServer()
-    try:
-        c = Client(address='127.0.0.1', port=srv.port)
-        c.wait_connected(10)
-        c.call_sync('create', '/rtt', b'x' * 100, {})
-        for _ in range(200):
-            c.call_sync('get', '/rtt')
-        lat = []
-        for _ in range(n):
-            t = time.perf_counter()
-            c.call_sync('get', '/rtt')
-            lat.append((time.perf_counter() - t) * 1e6)
-        c.close_sync(10)
-        lat.sort()
-        return statistics.median(lat), lat[int(0.99 * len(lat))]
-    finally:
-        srv.shutdown()
+    c = Client(address='127.0.0.1', port=port)
+    c.wait_connected(10)
+    c.call_sync('create', '/rtt', b'x' * 100, {})
+    for _ in range(200):
+        c.call_sync('get', '/rtt')
+    lat = []
+    for _ in range(n):
+        t = time.perf_counter()
+        c.call_sync('get', '/rtt')
+        lat.append((time.perf_counter() - t) * 1e6)
+    c.close_sync(10)
+    lat.sort()
+    return statistics.median(lat), lat[int(0.99 * len(lat))]
 
 
 def main():
@@ -80,6 +91,7 @@ def main():
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    rtt_srv = start_rtt_server() if rank == 0 and not a.no_rtt else None
     # One rank per GPU over RCCL ("nccl").  ZKMI_BENCH_BACKEND=gloo (host
     # collectives, ranks may share a GPU) exists only to rehearse the
     # multi-rank path on a one-GPU box.
@@ -146,8 +158,12 @@ def main():
     value = ops / elapsed
 
     rtt50 = rtt99 = None
-    if rank == 0 and not a.no_rtt:
-        rtt50, rtt99 = measure_rtt()
+    if rtt_srv is not None:
+        try:
+            rtt50, rtt99 = measure_rtt(rtt_srv[1])
+        finally:
+            rtt_srv[0].stdin.close()
+            rtt_srv[0].wait(10)
 
     if rank == 0:
         line = {

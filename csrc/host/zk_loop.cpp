@@ -1,0 +1,1070 @@
+// zkmi native event loop — epoll + eventfd + timer heap + TCP transports.
+//
+// The reference runs every FSM, timer and socket callback on Node's event
+// loop (libuv, native code): net.connect (lib/connection-fsm.js:99-103),
+// setTimeout / setImmediate / setInterval (lib/connection-fsm.js:201-207,
+// lib/zk-session.js:99-108), socket 'data' / 'end' / 'error' / 'close'.
+// This is zkmi's equivalent: one loop thread per Loop, all callbacks on it,
+// so the Python FSMs above it need no locks.
+//
+// Python surface (module _zkloop, wrapped by zkmi/runtime/nloop.py):
+//   Loop(on_exception)
+//     .run()                          blocks; call on the loop thread
+//     .stop()                         any thread
+//     .call_soon(fn, args)            -> Handle      any thread
+//     .call_later(ms, fn, args)       -> Handle      any thread
+//     .time_ms()                      monotonic milliseconds
+//     .connect(host, port, protocol, on_fail) -> Transport
+//     .listen(host, port, factory)    -> Server
+//   Handle .cancel() / .clear() / .unref() / .cancelled
+//   Transport (asyncio-Protocol-shaped callbacks on `protocol`:
+//     connection_made(tr), data_received(bytes), eof_received(),
+//     connection_lost(exc|None))
+//     .write(b) -> bool, .write_eof(), .can_write_eof(), .abort(), .close(),
+//     .cancel(), .is_closing(), .pause_reading(), .resume_reading(),
+//     .get_extra_info(name, default=None)
+//   Server .port, .close()
+//
+// Concurrency: the loop thread holds the GIL except inside epoll_wait; every
+// other entry point is a Python call and holds the GIL too, so the GIL
+// serialises all access to the queues, the timer heap and the fd table.
+// Threads other than the loop thread wake it through the eventfd.
+// epoll events carry a registration id, not the fd, so an event for an fd
+// that was closed (and its number reused) while the loop slept is dropped.
+#define PY_SSIZE_T_CLEAN
+#include <Python.h>
+
+#include <arpa/inet.h>
+#include <errno.h>
+#include <fcntl.h>
+#include <netdb.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <pthread.h>
+#include <sys/epoll.h>
+#include <sys/eventfd.h>
+#include <sys/socket.h>
+#include <time.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <deque>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+namespace {
+
+double mono_ms() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return ts.tv_sec * 1e3 + ts.tv_nsec / 1e6;
+}
+
+PyObject* os_error(int err) {
+  return PyObject_CallFunction(PyExc_OSError, "is", err, strerror(err));
+}
+
+// ---------------------------------------------------------------------------
+// Handle
+// ---------------------------------------------------------------------------
+
+struct Handle {
+  PyObject_HEAD
+  PyObject* fn;
+  PyObject* args;
+  double when;
+  uint64_t seq;
+  bool cancelled;
+};
+
+void Handle_dealloc(Handle* h) {
+  Py_XDECREF(h->fn);
+  Py_XDECREF(h->args);
+  Py_TYPE(h)->tp_free((PyObject*)h);
+}
+
+PyObject* Handle_cancel(Handle* h, PyObject*) {
+  if (!h->cancelled) {
+    h->cancelled = true;
+    Py_CLEAR(h->fn);
+    Py_CLEAR(h->args);
+  }
+  Py_RETURN_NONE;
+}
+
+PyObject* Handle_unref(Handle* h, PyObject*) {
+  // loop threads are daemons: a pending timer never keeps the process up
+  // (Node's timer.unref(), used at lib/connection-fsm.js:204)
+  Py_INCREF(h);
+  return (PyObject*)h;
+}
+
+PyObject* Handle_get_cancelled(Handle* h, void*) {
+  return PyBool_FromLong(h->cancelled);
+}
+
+PyMethodDef Handle_methods[] = {
+    {"cancel", (PyCFunction)Handle_cancel, METH_NOARGS, "cancel"},
+    {"clear", (PyCFunction)Handle_cancel, METH_NOARGS, "cancel"},
+    {"unref", (PyCFunction)Handle_unref, METH_NOARGS, "no-op, returns self"},
+    {nullptr, nullptr, 0, nullptr}};
+
+PyGetSetDef Handle_getset[] = {
+    {"cancelled", (getter)Handle_get_cancelled, nullptr, nullptr, nullptr},
+    {nullptr, nullptr, nullptr, nullptr, nullptr}};
+
+PyTypeObject HandleType = {PyVarObject_HEAD_INIT(nullptr, 0)};
+
+// ---------------------------------------------------------------------------
+// Loop / Transport / Server
+// ---------------------------------------------------------------------------
+
+struct Loop;
+
+enum Kind { K_TRANSPORT = 1, K_SERVER = 2 };
+
+// Common head of the objects registered with epoll.
+struct Watched {
+  PyObject_HEAD
+  int kind;
+  int fd;
+  uint64_t reg;          // registration id (0 = not registered)
+  uint32_t events;       // epoll mask currently registered
+  Loop* loop;            // borrowed (the loop outlives its watched objects)
+};
+
+struct Transport {
+  Watched w;
+  PyObject* protocol;
+  PyObject* on_fail;
+  std::string* wbuf;     // pending output
+  size_t woff;
+  bool connecting, connected, paused, rd_eof, eof_pending, wr_shut;
+  bool closing, closed;
+  PyObject* peer;        // (host, port) tuple
+};
+
+struct Server {
+  Watched w;
+  PyObject* factory;
+  int port;
+};
+
+struct TimerCmp {
+  bool operator()(const Handle* a, const Handle* b) const {
+    return a->when != b->when ? a->when > b->when : a->seq > b->seq;
+  }
+};
+
+struct Loop {
+  PyObject_HEAD
+  int epfd;
+  int evfd;
+  bool running;
+  bool stopping;
+  pthread_t thread;
+  uint64_t seq;
+  uint64_t next_reg;
+  PyObject* on_exception;
+  std::deque<Handle*>* ready;
+  std::vector<Handle*>* timers;                  // min-heap by (when, seq)
+  std::unordered_map<uint64_t, Watched*>* regs;  // strong refs
+};
+
+bool on_loop_thread(Loop* L) {
+  return L->running && pthread_equal(L->thread, pthread_self());
+}
+
+void wake(Loop* L) {
+  if (on_loop_thread(L)) return;
+  uint64_t one = 1;
+  ssize_t r = write(L->evfd, &one, sizeof one);
+  (void)r;
+}
+
+void report_exception(Loop* L) {
+  PyObject *t, *v, *tb;
+  PyErr_Fetch(&t, &v, &tb);
+  PyErr_NormalizeException(&t, &v, &tb);
+  if (tb != nullptr && v != nullptr) PyException_SetTraceback(v, tb);
+  if (L->on_exception != nullptr && v != nullptr) {
+    PyObject* r = PyObject_CallOneArg(L->on_exception, v);
+    if (r == nullptr) PyErr_Print();
+    Py_XDECREF(r);
+  }
+  Py_XDECREF(t);
+  Py_XDECREF(v);
+  Py_XDECREF(tb);
+}
+
+// Call obj.name(*args) on the loop thread; failures go to on_exception.
+void invoke(Loop* L, PyObject* obj, const char* name, PyObject* arg) {
+  if (obj == nullptr) return;
+  PyObject* m = PyObject_GetAttrString(obj, name);
+  if (m == nullptr) { report_exception(L); return; }
+  PyObject* r = arg ? PyObject_CallOneArg(m, arg) : PyObject_CallNoArgs(m);
+  Py_DECREF(m);
+  if (r == nullptr) report_exception(L);
+  Py_XDECREF(r);
+}
+
+Handle* new_handle(PyObject* fn, PyObject* args) {
+  Handle* h = PyObject_New(Handle, &HandleType);
+  if (h == nullptr) return nullptr;
+  Py_INCREF(fn);
+  h->fn = fn;
+  if (args == nullptr) args = PyTuple_New(0);
+  else Py_INCREF(args);
+  h->args = args;
+  h->when = 0;
+  h->seq = 0;
+  h->cancelled = false;
+  return h;
+}
+
+// queue h (a new reference is taken)
+void push_ready(Loop* L, Handle* h) {
+  Py_INCREF(h);
+  L->ready->push_back(h);
+  wake(L);
+}
+
+void push_timer(Loop* L, Handle* h) {
+  Py_INCREF(h);
+  h->seq = ++L->seq;
+  L->timers->push_back(h);
+  std::push_heap(L->timers->begin(), L->timers->end(), TimerCmp());
+  wake(L);
+}
+
+// Defer fn(*args) to the loop's ready queue (used for callbacks that must
+// not run inside the caller's stack, as asyncio defers them).
+void defer(Loop* L, PyObject* fn, PyObject* args) {
+  Handle* h = new_handle(fn, args);
+  if (h == nullptr) { report_exception(L); return; }
+  push_ready(L, h);
+  Py_DECREF(h);
+}
+
+void defer_method(Loop* L, PyObject* obj, const char* name, PyObject* arg) {
+  PyObject* m = PyObject_GetAttrString(obj, name);
+  if (m == nullptr) { report_exception(L); return; }
+  PyObject* args = arg ? PyTuple_Pack(1, arg) : PyTuple_New(0);
+  defer(L, m, args);
+  Py_DECREF(m);
+  Py_XDECREF(args);
+}
+
+int set_events(Watched* w, uint32_t ev) {
+  if (w->reg == 0 || w->events == ev) return 0;
+  epoll_event e;
+  e.events = ev;
+  e.data.u64 = w->reg;
+  if (epoll_ctl(w->loop->epfd, EPOLL_CTL_MOD, w->fd, &e) != 0) return -1;
+  w->events = ev;
+  return 0;
+}
+
+int add_watch(Loop* L, Watched* w, uint32_t ev) {
+  w->reg = ++L->next_reg;
+  epoll_event e;
+  e.events = ev;
+  e.data.u64 = w->reg;
+  if (epoll_ctl(L->epfd, EPOLL_CTL_ADD, w->fd, &e) != 0) {
+    w->reg = 0;
+    return -1;
+  }
+  w->events = ev;
+  Py_INCREF(w);
+  (*L->regs)[w->reg] = w;
+  return 0;
+}
+
+// Unregister and close the fd.  Drops the table's reference (the caller
+// must hold its own if it still uses w).
+void drop_watch(Watched* w) {
+  Loop* L = w->loop;
+  if (w->fd >= 0) {
+    if (w->reg != 0) epoll_ctl(L->epfd, EPOLL_CTL_DEL, w->fd, nullptr);
+    close(w->fd);
+    w->fd = -1;
+  }
+  if (w->reg != 0) {
+    L->regs->erase(w->reg);
+    w->reg = 0;
+    Py_DECREF(w);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Transport
+// ---------------------------------------------------------------------------
+
+PyTypeObject TransportType = {PyVarObject_HEAD_INIT(nullptr, 0)};
+PyTypeObject ServerType = {PyVarObject_HEAD_INIT(nullptr, 0)};
+PyTypeObject LoopType = {PyVarObject_HEAD_INIT(nullptr, 0)};
+
+Transport* new_transport(Loop* L, int fd) {
+  Transport* t = PyObject_New(Transport, &TransportType);
+  if (t == nullptr) return nullptr;
+  t->w.kind = K_TRANSPORT;
+  t->w.fd = fd;
+  t->w.reg = 0;
+  t->w.events = 0;
+  t->w.loop = L;
+  t->protocol = nullptr;
+  t->on_fail = nullptr;
+  t->wbuf = new std::string();
+  t->woff = 0;
+  t->connecting = t->connected = t->paused = t->rd_eof = false;
+  t->eof_pending = t->wr_shut = t->closing = t->closed = false;
+  t->peer = nullptr;
+  return t;
+}
+
+void Transport_dealloc(Transport* t) {
+  if (t->w.fd >= 0) close(t->w.fd);
+  delete t->wbuf;
+  Py_XDECREF(t->protocol);
+  Py_XDECREF(t->on_fail);
+  Py_XDECREF(t->peer);
+  Py_TYPE(t)->tp_free((PyObject*)t);
+}
+
+uint32_t wanted(Transport* t) {
+  uint32_t ev = 0;
+  if (t->connecting) return EPOLLOUT;
+  if (!t->paused && !t->rd_eof) ev |= EPOLLIN | EPOLLRDHUP;
+  if (t->woff < t->wbuf->size()) ev |= EPOLLOUT;
+  return ev;
+}
+
+void refresh(Transport* t) {
+  if (t->closed) return;
+  set_events(&t->w, wanted(t));
+}
+
+// Terminal: close the socket and tell the protocol (exc may be nullptr for a
+// clean close).  Runs connection_lost now (we are on the loop thread).
+void finish(Transport* t, PyObject* exc) {
+  if (t->closed) return;
+  t->closed = true;
+  Py_INCREF(t);
+  drop_watch(&t->w);
+  if (t->connected && t->protocol != nullptr)
+    invoke(t->w.loop, t->protocol, "connection_lost", exc ? exc : Py_None);
+  Py_DECREF(t);
+}
+
+void fatal(Transport* t, int err) {
+  PyObject* exc = os_error(err);
+  if (exc == nullptr) { report_exception(t->w.loop); return; }
+  finish(t, exc);
+  Py_DECREF(exc);
+}
+
+void shut_wr(Transport* t) {
+  if (!t->wr_shut && t->w.fd >= 0) {
+    shutdown(t->w.fd, SHUT_WR);
+    t->wr_shut = true;
+  }
+}
+
+// Write as much of the buffer as the socket takes; returns errno or 0.
+int flush(Transport* t) {
+  std::string& b = *t->wbuf;
+  while (t->woff < b.size()) {
+    ssize_t n = send(t->w.fd, b.data() + t->woff, b.size() - t->woff,
+                     MSG_NOSIGNAL | MSG_DONTWAIT);
+    if (n > 0) { t->woff += (size_t)n; continue; }
+    if (n < 0 && errno == EINTR) continue;
+    if (n < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) break;
+    return n < 0 ? errno : EPIPE;
+  }
+  if (t->woff == b.size()) {
+    b.clear();
+    t->woff = 0;
+    if (t->eof_pending) shut_wr(t);
+  } else if (t->woff > (1u << 20) && t->woff * 2 > b.size()) {
+    b.erase(0, t->woff);
+    t->woff = 0;
+  }
+  return 0;
+}
+
+void on_connected(Transport* t) {
+  t->connecting = false;
+  t->connected = true;
+  int one = 1;
+  setsockopt(t->w.fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+  Py_CLEAR(t->on_fail);
+  Py_INCREF(t);
+  invoke(t->w.loop, t->protocol, "connection_made", (PyObject*)t);
+  if (!t->closed) {
+    int err = t->woff < t->wbuf->size() ? flush(t) : 0;
+    if (err) fatal(t, err);
+    else refresh(t);
+  }
+  Py_DECREF(t);
+}
+
+void connect_failed(Transport* t, int err) {
+  Loop* L = t->w.loop;
+  PyObject* cb = t->on_fail;
+  t->on_fail = nullptr;
+  t->closed = true;
+  Py_INCREF(t);
+  drop_watch(&t->w);
+  if (cb != nullptr) {
+    PyObject* exc = os_error(err);
+    if (exc != nullptr) {
+      PyObject* r = PyObject_CallOneArg(cb, exc);
+      if (r == nullptr) report_exception(L);
+      Py_XDECREF(r);
+      Py_DECREF(exc);
+    } else {
+      report_exception(L);
+    }
+    Py_DECREF(cb);
+  }
+  Py_DECREF(t);
+}
+
+void transport_event(Transport* t, uint32_t ev) {
+  Py_INCREF(t);
+  if (t->connecting) {
+    int err = 0;
+    socklen_t len = sizeof err;
+    getsockopt(t->w.fd, SOL_SOCKET, SO_ERROR, &err, &len);
+    if (err != 0) connect_failed(t, err);
+    else if (ev & (EPOLLOUT | EPOLLERR | EPOLLHUP)) on_connected(t);
+    Py_DECREF(t);
+    return;
+  }
+  if ((ev & (EPOLLIN | EPOLLRDHUP | EPOLLHUP | EPOLLERR)) && !t->paused &&
+      !t->rd_eof) {
+    char buf[1 << 16];
+    for (int rounds = 0; rounds < 64 && !t->closed && !t->paused; ++rounds) {
+      ssize_t n = recv(t->w.fd, buf, sizeof buf, MSG_DONTWAIT);
+      if (n > 0) {
+        PyObject* b = PyBytes_FromStringAndSize(buf, n);
+        if (b == nullptr) { report_exception(t->w.loop); break; }
+        invoke(t->w.loop, t->protocol, "data_received", b);
+        Py_DECREF(b);
+        if ((size_t)n < sizeof buf) break;
+        continue;
+      }
+      if (n == 0) {
+        t->rd_eof = true;
+        invoke(t->w.loop, t->protocol, "eof_received", nullptr);
+        break;
+      }
+      if (errno == EINTR) continue;
+      if (errno != EAGAIN && errno != EWOULDBLOCK) fatal(t, errno);
+      break;
+    }
+  }
+  if (!t->closed && (ev & EPOLLOUT)) {
+    int err = flush(t);
+    if (err) fatal(t, err);
+  }
+  if (!t->closed && (ev & EPOLLERR)) {
+    int err = 0;
+    socklen_t len = sizeof err;
+    getsockopt(t->w.fd, SOL_SOCKET, SO_ERROR, &err, &len);
+    if (err) fatal(t, err);
+  }
+  if (!t->closed && (ev & EPOLLHUP) && t->rd_eof) {
+    // both directions are down: nothing more can arrive or leave
+    int err = 0;
+    socklen_t len = sizeof err;
+    getsockopt(t->w.fd, SOL_SOCKET, SO_ERROR, &err, &len);
+    if (err) fatal(t, err);
+    else finish(t, nullptr);
+  }
+  if (!t->closed && t->closing && t->woff == t->wbuf->size())
+    finish(t, nullptr);
+  refresh(t);
+  Py_DECREF(t);
+}
+
+PyObject* Transport_write(Transport* t, PyObject* arg) {
+  Py_buffer v;
+  if (PyObject_GetBuffer(arg, &v, PyBUF_SIMPLE) != 0) return nullptr;
+  if (t->closed || t->closing || t->wr_shut || t->eof_pending) {
+    PyBuffer_Release(&v);
+    Py_RETURN_FALSE;
+  }
+  t->wbuf->append((const char*)v.buf, (size_t)v.len);
+  PyBuffer_Release(&v);
+  if (t->connected) {
+    int err = flush(t);
+    if (err) {
+      // report from the loop, never from inside the caller's stack
+      PyObject* e = PyLong_FromLong(err);
+      defer_method(t->w.loop, (PyObject*)t, "_fatal", e);
+      Py_XDECREF(e);
+      t->closing = true;
+      Py_RETURN_FALSE;
+    }
+    refresh(t);
+  }
+  Py_RETURN_TRUE;
+}
+
+PyObject* Transport_fatal(Transport* t, PyObject* arg) {
+  int err = (int)PyLong_AsLong(arg);
+  if (err == -1 && PyErr_Occurred()) return nullptr;
+  fatal(t, err);
+  Py_RETURN_NONE;
+}
+
+PyObject* Transport_write_eof(Transport* t, PyObject*) {
+  if (t->closed || t->wr_shut) Py_RETURN_NONE;
+  t->eof_pending = true;
+  if (t->connected && t->woff == t->wbuf->size()) shut_wr(t);
+  Py_RETURN_NONE;
+}
+
+PyObject* Transport_can_write_eof(Transport*, PyObject*) { Py_RETURN_TRUE; }
+
+// Close now, drop unsent output; connection_lost(None) follows from the loop
+// (asyncio's abort() contract, which TcpSocket relies on).
+PyObject* Transport_abort(Transport* t, PyObject*) {
+  if (t->closed) Py_RETURN_NONE;
+  const bool was_connected = t->connected;
+  t->closed = true;
+  Py_CLEAR(t->on_fail);
+  Py_INCREF(t);
+  drop_watch(&t->w);
+  if (was_connected && t->protocol != nullptr)
+    defer_method(t->w.loop, t->protocol, "connection_lost", Py_None);
+  Py_DECREF(t);
+  Py_RETURN_NONE;
+}
+
+// Cancel a connect in progress or close: no callbacks at all.
+PyObject* Transport_cancel(Transport* t, PyObject*) {
+  if (t->closed) Py_RETURN_NONE;
+  t->closed = true;
+  Py_CLEAR(t->on_fail);
+  Py_INCREF(t);
+  drop_watch(&t->w);
+  Py_DECREF(t);
+  Py_RETURN_NONE;
+}
+
+PyObject* Transport_close(Transport* t, PyObject*) {
+  if (t->closed || t->closing) Py_RETURN_NONE;
+  t->closing = true;
+  if (!t->connected || t->woff == t->wbuf->size()) {
+    Py_INCREF(t);
+    const bool was_connected = t->connected;
+    t->closed = true;
+    drop_watch(&t->w);
+    if (was_connected && t->protocol != nullptr)
+      defer_method(t->w.loop, t->protocol, "connection_lost", Py_None);
+    Py_DECREF(t);
+  } else {
+    refresh(t);
+  }
+  Py_RETURN_NONE;
+}
+
+PyObject* Transport_is_closing(Transport* t, PyObject*) {
+  return PyBool_FromLong(t->closed || t->closing);
+}
+
+PyObject* Transport_pause(Transport* t, PyObject*) {
+  t->paused = true;
+  refresh(t);
+  Py_RETURN_NONE;
+}
+
+PyObject* Transport_resume(Transport* t, PyObject*) {
+  t->paused = false;
+  refresh(t);
+  Py_RETURN_NONE;
+}
+
+PyObject* Transport_extra(Transport* t, PyObject* args) {
+  const char* name;
+  PyObject* dflt = Py_None;
+  if (!PyArg_ParseTuple(args, "s|O", &name, &dflt)) return nullptr;
+  if (strcmp(name, "peername") == 0 && t->peer != nullptr) {
+    Py_INCREF(t->peer);
+    return t->peer;
+  }
+  if (strcmp(name, "fd") == 0) return PyLong_FromLong(t->w.fd);
+  Py_INCREF(dflt);
+  return dflt;
+}
+
+PyObject* Transport_get_pending(Transport* t, void*) {
+  return PyLong_FromSize_t(t->wbuf->size() - t->woff);
+}
+
+PyMethodDef Transport_methods[] = {
+    {"write", (PyCFunction)Transport_write, METH_O, "queue bytes"},
+    {"write_eof", (PyCFunction)Transport_write_eof, METH_NOARGS, "half-close"},
+    {"can_write_eof", (PyCFunction)Transport_can_write_eof, METH_NOARGS, ""},
+    {"abort", (PyCFunction)Transport_abort, METH_NOARGS, "close now"},
+    {"cancel", (PyCFunction)Transport_cancel, METH_NOARGS, "close, no events"},
+    {"close", (PyCFunction)Transport_close, METH_NOARGS, "flush then close"},
+    {"is_closing", (PyCFunction)Transport_is_closing, METH_NOARGS, ""},
+    {"pause_reading", (PyCFunction)Transport_pause, METH_NOARGS, ""},
+    {"resume_reading", (PyCFunction)Transport_resume, METH_NOARGS, ""},
+    {"get_extra_info", (PyCFunction)Transport_extra, METH_VARARGS, ""},
+    {"_fatal", (PyCFunction)Transport_fatal, METH_O, "internal"},
+    {nullptr, nullptr, 0, nullptr}};
+
+PyGetSetDef Transport_getset[] = {
+    {"pending", (getter)Transport_get_pending, nullptr, "unsent bytes",
+     nullptr},
+    {nullptr, nullptr, nullptr, nullptr, nullptr}};
+
+// ---------------------------------------------------------------------------
+// Server
+// ---------------------------------------------------------------------------
+
+void Server_dealloc(Server* s) {
+  if (s->w.fd >= 0) close(s->w.fd);
+  Py_XDECREF(s->factory);
+  Py_TYPE(s)->tp_free((PyObject*)s);
+}
+
+PyObject* peer_tuple(const sockaddr_storage& ss) {
+  char host[INET6_ADDRSTRLEN] = {0};
+  int port = 0;
+  if (ss.ss_family == AF_INET) {
+    const sockaddr_in* a = (const sockaddr_in*)&ss;
+    inet_ntop(AF_INET, &a->sin_addr, host, sizeof host);
+    port = ntohs(a->sin_port);
+  } else if (ss.ss_family == AF_INET6) {
+    const sockaddr_in6* a = (const sockaddr_in6*)&ss;
+    inet_ntop(AF_INET6, &a->sin6_addr, host, sizeof host);
+    port = ntohs(a->sin6_port);
+  }
+  return Py_BuildValue("(si)", host, port);
+}
+
+void server_event(Server* s) {
+  Loop* L = s->w.loop;
+  Py_INCREF(s);
+  for (int i = 0; i < 64 && s->w.fd >= 0; ++i) {
+    sockaddr_storage ss;
+    socklen_t sl = sizeof ss;
+    int fd = accept4(s->w.fd, (sockaddr*)&ss, &sl,
+                     SOCK_NONBLOCK | SOCK_CLOEXEC);
+    if (fd < 0) {
+      if (errno == EINTR) continue;
+      break;                     // EAGAIN, or a transient accept error
+    }
+    int one = 1;
+    setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+    Transport* t = new_transport(L, fd);
+    if (t == nullptr) { close(fd); report_exception(L); break; }
+    t->connected = true;
+    t->peer = peer_tuple(ss);
+    PyObject* proto = PyObject_CallNoArgs(s->factory);
+    if (proto == nullptr) {
+      report_exception(L);
+      Py_DECREF(t);
+      continue;
+    }
+    t->protocol = proto;
+    if (add_watch(L, &t->w, EPOLLIN | EPOLLRDHUP) != 0) {
+      Py_DECREF(t);
+      continue;
+    }
+    invoke(L, proto, "connection_made", (PyObject*)t);
+    Py_DECREF(t);
+  }
+  Py_DECREF(s);
+}
+
+PyObject* Server_close(Server* s, PyObject*) {
+  Py_INCREF(s);
+  drop_watch(&s->w);
+  Py_DECREF(s);
+  Py_RETURN_NONE;
+}
+
+PyObject* Server_get_port(Server* s, void*) { return PyLong_FromLong(s->port); }
+
+PyMethodDef Server_methods[] = {
+    {"close", (PyCFunction)Server_close, METH_NOARGS, "stop listening"},
+    {nullptr, nullptr, 0, nullptr}};
+
+PyGetSetDef Server_getset[] = {
+    {"port", (getter)Server_get_port, nullptr, "bound port", nullptr},
+    {nullptr, nullptr, nullptr, nullptr, nullptr}};
+
+// ---------------------------------------------------------------------------
+// Loop
+// ---------------------------------------------------------------------------
+
+PyObject* Loop_new(PyTypeObject* type, PyObject* args, PyObject*) {
+  PyObject* on_exc = nullptr;
+  if (!PyArg_ParseTuple(args, "|O", &on_exc)) return nullptr;
+  Loop* L = (Loop*)type->tp_alloc(type, 0);
+  if (L == nullptr) return nullptr;
+  L->epfd = epoll_create1(EPOLL_CLOEXEC);
+  L->evfd = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
+  if (L->epfd < 0 || L->evfd < 0) {
+    PyErr_SetFromErrno(PyExc_OSError);
+    Py_DECREF(L);
+    return nullptr;
+  }
+  epoll_event e;
+  e.events = EPOLLIN;
+  e.data.u64 = 0;                       // reg 0 = the wake-up eventfd
+  epoll_ctl(L->epfd, EPOLL_CTL_ADD, L->evfd, &e);
+  L->running = L->stopping = false;
+  L->seq = 0;
+  L->next_reg = 0;
+  L->on_exception = (on_exc && on_exc != Py_None) ? on_exc : nullptr;
+  Py_XINCREF(L->on_exception);
+  L->ready = new std::deque<Handle*>();
+  L->timers = new std::vector<Handle*>();
+  L->regs = new std::unordered_map<uint64_t, Watched*>();
+  return (PyObject*)L;
+}
+
+void clear_all(Loop* L) {
+  for (Handle* h : *L->ready) Py_DECREF(h);
+  L->ready->clear();
+  for (Handle* h : *L->timers) Py_DECREF(h);
+  L->timers->clear();
+  std::vector<Watched*> ws;
+  for (auto& kv : *L->regs) ws.push_back(kv.second);
+  for (Watched* w : ws) {
+    Py_INCREF(w);
+    if (w->kind == K_TRANSPORT) ((Transport*)w)->closed = true;
+    drop_watch(w);
+    Py_DECREF(w);
+  }
+}
+
+void Loop_dealloc(Loop* L) {
+  if (L->ready != nullptr) clear_all(L);
+  delete L->ready;
+  delete L->timers;
+  delete L->regs;
+  if (L->epfd >= 0) close(L->epfd);
+  if (L->evfd >= 0) close(L->evfd);
+  Py_XDECREF(L->on_exception);
+  Py_TYPE(L)->tp_free((PyObject*)L);
+}
+
+void run_handle(Loop* L, Handle* h) {
+  if (h->cancelled || h->fn == nullptr) return;
+  PyObject* fn = h->fn;
+  PyObject* args = h->args;
+  Py_INCREF(fn);
+  Py_INCREF(args);
+  PyObject* r = PyObject_Call(fn, args, nullptr);
+  if (r == nullptr) report_exception(L);
+  Py_XDECREF(r);
+  Py_DECREF(fn);
+  Py_DECREF(args);
+}
+
+PyObject* Loop_run(Loop* L, PyObject*) {
+  if (L->running) {
+    PyErr_SetString(PyExc_RuntimeError, "loop already running");
+    return nullptr;
+  }
+  L->thread = pthread_self();
+  L->running = true;
+  std::vector<epoll_event> evs(256);
+  std::vector<Handle*> due;
+  while (!L->stopping) {
+    int timeout = -1;
+    if (!L->ready->empty()) {
+      timeout = 0;
+    } else {
+      // drop cancelled timers at the top so they do not shorten the wait
+      while (!L->timers->empty() && L->timers->front()->cancelled) {
+        std::pop_heap(L->timers->begin(), L->timers->end(), TimerCmp());
+        Py_DECREF(L->timers->back());
+        L->timers->pop_back();
+      }
+      if (!L->timers->empty()) {
+        const double d = L->timers->front()->when - mono_ms();
+        timeout = d <= 0 ? 0 : (int)std::ceil(d);
+      }
+    }
+    int n;
+    Py_BEGIN_ALLOW_THREADS
+    n = epoll_wait(L->epfd, evs.data(), (int)evs.size(), timeout);
+    Py_END_ALLOW_THREADS
+    if (n < 0 && errno != EINTR) {
+      PyErr_SetFromErrno(PyExc_OSError);
+      L->running = false;
+      return nullptr;
+    }
+    for (int i = 0; i < n && !L->stopping; ++i) {
+      const uint64_t reg = evs[i].data.u64;
+      if (reg == 0) {
+        uint64_t v;
+        while (read(L->evfd, &v, sizeof v) > 0) {
+        }
+        continue;
+      }
+      auto it = L->regs->find(reg);
+      if (it == L->regs->end()) continue;        // closed while we slept
+      Watched* w = it->second;
+      if (w->kind == K_TRANSPORT) transport_event((Transport*)w, evs[i].events);
+      else server_event((Server*)w);
+    }
+    // timers that are due
+    const double now = mono_ms();
+    while (!L->timers->empty() && L->timers->front()->when <= now) {
+      std::pop_heap(L->timers->begin(), L->timers->end(), TimerCmp());
+      due.push_back(L->timers->back());
+      L->timers->pop_back();
+    }
+    for (Handle* h : due) {
+      if (!L->stopping) run_handle(L, h);
+      Py_DECREF(h);
+    }
+    due.clear();
+    // the ready queue as it stands now (new entries wait for the next turn)
+    size_t k = L->ready->size();
+    while (k-- > 0 && !L->ready->empty() && !L->stopping) {
+      Handle* h = L->ready->front();
+      L->ready->pop_front();
+      run_handle(L, h);
+      Py_DECREF(h);
+    }
+  }
+  clear_all(L);
+  L->running = false;
+  Py_RETURN_NONE;
+}
+
+PyObject* Loop_stop(Loop* L, PyObject*) {
+  L->stopping = true;
+  uint64_t one = 1;
+  ssize_t r = write(L->evfd, &one, sizeof one);
+  (void)r;
+  Py_RETURN_NONE;
+}
+
+PyObject* Loop_call_soon(Loop* L, PyObject* args) {
+  PyObject *fn, *fargs = nullptr;
+  if (!PyArg_ParseTuple(args, "O|O!", &fn, &PyTuple_Type, &fargs))
+    return nullptr;
+  Handle* h = new_handle(fn, fargs);
+  if (h == nullptr) return nullptr;
+  push_ready(L, h);
+  return (PyObject*)h;
+}
+
+PyObject* Loop_call_later(Loop* L, PyObject* args) {
+  double ms;
+  PyObject *fn, *fargs = nullptr;
+  if (!PyArg_ParseTuple(args, "dO|O!", &ms, &fn, &PyTuple_Type, &fargs))
+    return nullptr;
+  Handle* h = new_handle(fn, fargs);
+  if (h == nullptr) return nullptr;
+  h->when = mono_ms() + (ms > 0 ? ms : 0);
+  push_timer(L, h);
+  return (PyObject*)h;
+}
+
+PyObject* Loop_time_ms(Loop*, PyObject*) { return PyFloat_FromDouble(mono_ms()); }
+
+PyObject* Loop_in_loop(Loop* L, PyObject*) {
+  return PyBool_FromLong(on_loop_thread(L));
+}
+
+int resolve(const char* host, int port, sockaddr_storage* ss, socklen_t* sl) {
+  addrinfo hints;
+  memset(&hints, 0, sizeof hints);
+  hints.ai_family = AF_UNSPEC;
+  hints.ai_socktype = SOCK_STREAM;
+  hints.ai_flags = AI_NUMERICSERV;
+  char ps[16];
+  snprintf(ps, sizeof ps, "%d", port);
+  addrinfo* res = nullptr;
+  int rc;
+  Py_BEGIN_ALLOW_THREADS
+  rc = getaddrinfo(host, ps, &hints, &res);
+  Py_END_ALLOW_THREADS
+  if (rc != 0 || res == nullptr) return rc != 0 ? rc : EAI_NONAME;
+  memcpy(ss, res->ai_addr, res->ai_addrlen);
+  *sl = res->ai_addrlen;
+  freeaddrinfo(res);
+  return 0;
+}
+
+PyObject* Loop_connect(Loop* L, PyObject* args) {
+  const char* host;
+  int port;
+  PyObject *proto, *on_fail;
+  if (!PyArg_ParseTuple(args, "siOO", &host, &port, &proto, &on_fail))
+    return nullptr;
+  Transport* t = new_transport(L, -1);
+  if (t == nullptr) return nullptr;
+  Py_INCREF(proto);
+  t->protocol = proto;
+  Py_INCREF(on_fail);
+  t->on_fail = on_fail;
+  t->peer = Py_BuildValue("(si)", host, port);
+  sockaddr_storage ss;
+  socklen_t sl;
+  int err = 0;
+  const int rc = resolve(host, port, &ss, &sl);
+  int fd = -1;
+  if (rc != 0) {
+    err = EHOSTUNREACH;
+  } else {
+    fd = socket(ss.ss_family, SOCK_STREAM | SOCK_NONBLOCK | SOCK_CLOEXEC, 0);
+    if (fd < 0) err = errno;
+  }
+  if (fd >= 0) {
+    t->w.fd = fd;
+    t->connecting = true;
+    if (connect(fd, (sockaddr*)&ss, sl) != 0 && errno != EINPROGRESS)
+      err = errno;
+    // the outcome (success or failure) is always reported from the loop,
+    // like asyncio's create_connection, never inside this call
+    if (err == 0 && add_watch(L, &t->w, EPOLLOUT) != 0) err = errno;
+  }
+  if (err != 0) {
+    t->closed = true;
+    if (t->w.fd >= 0) { close(t->w.fd); t->w.fd = -1; }
+    PyObject* exc = os_error(err);
+    PyObject* cb = t->on_fail;
+    t->on_fail = nullptr;
+    if (exc != nullptr && cb != nullptr) {
+      PyObject* a = PyTuple_Pack(1, exc);
+      defer(L, cb, a);
+      Py_XDECREF(a);
+    }
+    Py_XDECREF(exc);
+    Py_XDECREF(cb);
+  }
+  return (PyObject*)t;
+}
+
+PyObject* Loop_listen(Loop* L, PyObject* args) {
+  const char* host;
+  int port;
+  PyObject* factory;
+  if (!PyArg_ParseTuple(args, "siO", &host, &port, &factory)) return nullptr;
+  sockaddr_storage ss;
+  socklen_t sl;
+  if (resolve(host, port, &ss, &sl) != 0) {
+    PyErr_Format(PyExc_OSError, "cannot resolve %s", host);
+    return nullptr;
+  }
+  int fd = socket(ss.ss_family, SOCK_STREAM | SOCK_NONBLOCK | SOCK_CLOEXEC, 0);
+  if (fd < 0) return PyErr_SetFromErrno(PyExc_OSError);
+  int one = 1;
+  setsockopt(fd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
+  if (bind(fd, (sockaddr*)&ss, sl) != 0 || listen(fd, 128) != 0) {
+    const int e = errno;
+    close(fd);
+    errno = e;
+    return PyErr_SetFromErrno(PyExc_OSError);
+  }
+  sockaddr_storage bs;
+  socklen_t bl = sizeof bs;
+  getsockname(fd, (sockaddr*)&bs, &bl);
+  Server* s = PyObject_New(Server, &ServerType);
+  if (s == nullptr) { close(fd); return nullptr; }
+  s->w.kind = K_SERVER;
+  s->w.fd = fd;
+  s->w.reg = 0;
+  s->w.events = 0;
+  s->w.loop = L;
+  Py_INCREF(factory);
+  s->factory = factory;
+  s->port = bs.ss_family == AF_INET6 ? ntohs(((sockaddr_in6*)&bs)->sin6_port)
+                                     : ntohs(((sockaddr_in*)&bs)->sin_port);
+  if (add_watch(L, &s->w, EPOLLIN) != 0) {
+    Py_DECREF(s);
+    return PyErr_SetFromErrno(PyExc_OSError);
+  }
+  wake(L);
+  return (PyObject*)s;
+}
+
+PyObject* Loop_stats(Loop* L, PyObject*) {
+  return Py_BuildValue("{s:n,s:n,s:n}", "ready", (Py_ssize_t)L->ready->size(),
+                       "timers", (Py_ssize_t)L->timers->size(), "fds",
+                       (Py_ssize_t)L->regs->size());
+}
+
+PyMethodDef Loop_methods[] = {
+    {"run", (PyCFunction)Loop_run, METH_NOARGS, "run until stop()"},
+    {"stop", (PyCFunction)Loop_stop, METH_NOARGS, "stop (any thread)"},
+    {"call_soon", (PyCFunction)Loop_call_soon, METH_VARARGS,
+     "call_soon(fn, args=()) -> Handle"},
+    {"call_later", (PyCFunction)Loop_call_later, METH_VARARGS,
+     "call_later(ms, fn, args=()) -> Handle"},
+    {"time_ms", (PyCFunction)Loop_time_ms, METH_NOARGS, "monotonic ms"},
+    {"in_loop", (PyCFunction)Loop_in_loop, METH_NOARGS, "on the loop thread?"},
+    {"connect", (PyCFunction)Loop_connect, METH_VARARGS,
+     "connect(host, port, protocol, on_fail) -> Transport"},
+    {"listen", (PyCFunction)Loop_listen, METH_VARARGS,
+     "listen(host, port, factory) -> Server"},
+    {"stats", (PyCFunction)Loop_stats, METH_NOARGS, "queue / timer / fd counts"},
+    {nullptr, nullptr, 0, nullptr}};
+
+PyModuleDef mod = {PyModuleDef_HEAD_INIT, "_zkloop",
+                   "zkmi native event loop (epoll)", -1, nullptr};
+
+}  // namespace
+
+PyMODINIT_FUNC PyInit__zkloop(void) {
+  HandleType.tp_name = "_zkloop.Handle";
+  HandleType.tp_basicsize = sizeof(Handle);
+  HandleType.tp_flags = Py_TPFLAGS_DEFAULT;
+  HandleType.tp_dealloc = (destructor)Handle_dealloc;
+  HandleType.tp_methods = Handle_methods;
+  HandleType.tp_getset = Handle_getset;
+
+  TransportType.tp_name = "_zkloop.Transport";
+  TransportType.tp_basicsize = sizeof(Transport);
+  TransportType.tp_flags = Py_TPFLAGS_DEFAULT;
+  TransportType.tp_dealloc = (destructor)Transport_dealloc;
+  TransportType.tp_methods = Transport_methods;
+  TransportType.tp_getset = Transport_getset;
+
+  ServerType.tp_name = "_zkloop.Server";
+  ServerType.tp_basicsize = sizeof(Server);
+  ServerType.tp_flags = Py_TPFLAGS_DEFAULT;
+  ServerType.tp_dealloc = (destructor)Server_dealloc;
+  ServerType.tp_methods = Server_methods;
+  ServerType.tp_getset = Server_getset;
+
+  LoopType.tp_name = "_zkloop.Loop";
+  LoopType.tp_basicsize = sizeof(Loop);
+  LoopType.tp_flags = Py_TPFLAGS_DEFAULT;
+  LoopType.tp_new = Loop_new;
+  LoopType.tp_dealloc = (destructor)Loop_dealloc;
+  LoopType.tp_methods = Loop_methods;
+
+  if (PyType_Ready(&HandleType) < 0 || PyType_Ready(&TransportType) < 0 ||
+      PyType_Ready(&ServerType) < 0 || PyType_Ready(&LoopType) < 0)
+    return nullptr;
+  PyObject* m = PyModule_Create(&mod);
+  if (m == nullptr) return nullptr;
+  Py_INCREF(&LoopType);
+  PyModule_AddObject(m, "Loop", (PyObject*)&LoopType);
+  Py_INCREF(&HandleType);
+  PyModule_AddObject(m, "Handle", (PyObject*)&HandleType);
+  Py_INCREF(&TransportType);
+  PyModule_AddObject(m, "Transport", (PyObject*)&TransportType);
+  Py_INCREF(&ServerType);
+  PyModule_AddObject(m, "Server", (PyObject*)&ServerType);
+  return m;
+}

@@ -31,15 +31,20 @@ def zkc(zk):
 # -- connect / ping (basic.test.js:36-120) --------------------------------
 
 def test_simple_connect_and_ping(zk):
-    c = client(zk.servers())
+    # JS attaches listeners in the constructor's tick, before any event can
+    # fire; with the client on its own loop thread the equivalent is the
+    # ``listeners`` option (attached before the client starts)
     pinged = Box()
     closed = Box()
-    c.on('close', closed)
+    box = {}
 
     def on_connect():
+        assert wait_for(lambda: 'c' in box, 5)
+        c = box['c']
         assert c.isConnected()
         c.ping(lambda err: (pinged(err), c.close()))
-    c.on('connect', on_connect)
+    c = box['c'] = client(zk.servers(), listeners=[('connect', on_connect),
+                                                    ('close', closed)])
     assert pinged.wait()[0] is None
     closed.wait()
     assert not c.isConnected()

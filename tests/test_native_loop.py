@@ -1,0 +1,197 @@
+"""The native epoll loop (csrc/host/zk_loop.cpp via zkmi/runtime/nloop.py):
+scheduling, timers, exception capture, TCP transports (connect, refuse,
+half-close, abort, pause, bulk writes) and the client/fake-server stack on
+both loop implementations.  CPU only."""
+
+import os
+import threading
+import time
+
+import pytest
+
+from zkmi.runtime import nloop
+from zkmi.runtime.loop import Loop, wait_for
+from zkmi.server import FakeZKServer
+
+from zkhelpers import client
+
+pytestmark = pytest.mark.skipif(not nloop.available(),
+                                reason='native loop not built')
+
+
+@pytest.fixture
+def nl():
+    lp = nloop.NativeLoop('test-native')
+    yield lp
+    lp.stop()
+
+
+def test_call_soon_order_and_threads(nl):
+    seen = []
+    done = threading.Event()
+    nl.call_soon(seen.append, 1)
+    nl.call_soon(seen.append, 2)
+    h = nl.call_soon(seen.append, 'cancelled')
+    h.cancel()
+    nl.call_soon(lambda: (seen.append(nl.in_loop()), done.set()))
+    assert done.wait(5)
+    assert seen == [1, 2, True]
+    assert not nl.in_loop()
+    assert nl.run(lambda: 41 + 1) == 42
+    with pytest.raises(KeyError):
+        nl.run(lambda: {}['x'])
+
+
+def test_timers_fire_in_deadline_order(nl):
+    seen = []
+    t0 = nl.time_ms()
+    nl.call_later(60, seen.append, 'c')
+    nl.call_later(20, seen.append, 'a')
+    nl.call_later(40, seen.append, 'b')
+    x = nl.call_later(30, seen.append, 'never')
+    x.cancel()
+    assert x.cancelled
+    assert wait_for(lambda: len(seen) == 3, 5)
+    assert seen == ['a', 'b', 'c']
+    assert nl.time_ms() - t0 >= 60
+    # a timer armed from the loop thread, chained
+    box = []
+
+    def chain(k):
+        box.append(k)
+        if k < 5:
+            nl.call_later(1, chain, k + 1)
+    nl.call_soon(chain, 0)
+    assert wait_for(lambda: len(box) == 6, 5)
+    assert nl.stats()['timers'] == 0
+
+
+def test_callback_exceptions_are_recorded(nl):
+    nl.call_soon(lambda: 1 / 0)
+    nl.call_soon(lambda: None)
+    assert wait_for(lambda: len(nl.errors) == 1, 5)
+    assert isinstance(nl.errors[0], ZeroDivisionError)
+    assert nl.run(lambda: 'alive') == 'alive'
+
+
+class Proto(object):
+    def __init__(self):
+        self.events = []
+        self.data = bytearray()
+        self.tr = None
+
+    def connection_made(self, tr):
+        self.tr = tr
+        self.events.append('made')
+
+    def data_received(self, b):
+        self.data += b
+
+    def eof_received(self):
+        self.events.append('eof')
+        return True
+
+    def connection_lost(self, exc):
+        self.events.append(('lost', exc))
+
+
+def _pair(lp):
+    srv_protos = []
+
+    def factory():
+        p = Proto()
+        srv_protos.append(p)
+        return p
+    srv = lp.start_server(factory, '127.0.0.1', 0)
+    cp = Proto()
+    fails = []
+    lp.run(lambda: lp.open_connection(cp, '127.0.0.1', srv.port,
+                                      fails.append))
+    assert wait_for(lambda: cp.tr is not None and srv_protos, 5), fails
+    assert wait_for(lambda: srv_protos[0].tr is not None, 5)
+    return srv, cp, srv_protos[0]
+
+
+@pytest.mark.parametrize('kind', ['native', 'asyncio'])
+def test_tcp_roundtrip_halfclose_and_bulk(kind):
+    lp = nloop.NativeLoop('t') if kind == 'native' else Loop('t')
+    try:
+        srv, cp, sp = _pair(lp)
+        big = os.urandom(3 << 20)                 # forces EPOLLOUT flushing
+        lp.run(lambda: cp.tr.write(b'hello ' + big))
+        assert wait_for(lambda: len(sp.data) == 6 + len(big), 10)
+        assert bytes(sp.data) == b'hello ' + big
+        # half-close: the peer sees EOF and can still answer
+        lp.run(cp.tr.write_eof)
+        assert wait_for(lambda: 'eof' in sp.events, 5)
+        lp.run(lambda: sp.tr.write(b'bye'))
+        assert wait_for(lambda: bytes(cp.data) == b'bye', 5)
+        lp.run(sp.tr.abort)
+        assert wait_for(lambda: 'eof' in cp.events, 5)
+        if kind == 'native':
+            # both directions are down: the native loop closes the socket
+            # and reports a clean loss (asyncio keeps it half-open)
+            assert wait_for(lambda: ('lost', None) in cp.events, 5)
+        lp.run(srv.close)
+    finally:
+        lp.stop()
+
+
+def test_connect_refused_reports_on_loop(nl):
+    import socket
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()                                   # nothing listens there
+    fails = []
+    p = Proto()
+    nl.run(lambda: nl.open_connection(p, '127.0.0.1', port,
+                                      lambda e: fails.append(
+                                          (e, nl.in_loop()))))
+    assert wait_for(lambda: fails, 5)
+    exc, on_loop = fails[0]
+    assert isinstance(exc, ConnectionRefusedError) and on_loop
+    assert p.events == []
+
+
+def test_pause_resume_and_cancelled_connect(nl):
+    srv, cp, sp = _pair(nl)
+    nl.run(sp.tr.pause_reading)
+    nl.run(lambda: cp.tr.write(b'x' * 1000))
+    time.sleep(0.1)
+    assert len(sp.data) == 0
+    nl.run(sp.tr.resume_reading)
+    assert wait_for(lambda: len(sp.data) == 1000, 5)
+    # an abandoned connect reports nothing
+    p = Proto()
+    fails = []
+    nl.run(lambda: nl.open_connection(p, '127.0.0.1', srv.port,
+                                      fails.append).cancel())
+    time.sleep(0.1)
+    assert p.events == [] and fails == []
+    nl.run(srv.close)
+
+
+@pytest.mark.parametrize('kind', ['native', 'asyncio'])
+def test_client_stack_on_both_loops(kind):
+    lp = nloop.NativeLoop('c') if kind == 'native' else Loop('c')
+    slp = nloop.NativeLoop('s') if kind == 'native' else Loop('s')
+    srv = FakeZKServer(loop=slp)
+    try:
+        c = client(srv.servers(), loop=lp)
+        c.wait_connected(10)
+        c.call_sync('create', '/loopkind', kind.encode(), {})
+        data, stat = c.call_sync('get', '/loopkind')
+        assert data == kind.encode() and stat.version == 0
+        got = []
+        c.watcher('/loopkind').on('dataChanged', lambda d, s: got.append(d))
+        assert wait_for(lambda: got == [kind.encode()], 5)
+        c.call_sync('set', '/loopkind', b'v2', -1)
+        assert wait_for(lambda: got[-1:] == [b'v2'], 5)
+        c.close_sync(10)
+        assert c._test_recorder.events == ['session', 'connect', 'close']
+        assert lp.errors == [] and slp.errors == []
+    finally:
+        srv.stop()
+        lp.stop()
+        slp.stop()

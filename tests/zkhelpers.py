@@ -29,7 +29,7 @@ def client(servers, session_timeout=None, config=None, **kw):
         o['sessionTimeout'] = session_timeout
     o.update(kw)
     rec = Recorder(None)
-    o['listeners'] = rec.listeners()
+    o['listeners'] = rec.listeners() + list(o.get('listeners') or ())
     c = Client(o)
     c._test_recorder = rec
     return c

@@ -68,42 +68,57 @@ def build_hip(jobs=4):
 
 
 def host_so_path():
+    return _ext_path('_zkhost')
+
+
+def _ext_path(name):
     suffix = sysconfig.get_config_var('EXT_SUFFIX') or '.so'
-    return os.path.join(ROOT, 'zkmi', '_zkhost' + suffix)
+    return os.path.join(ROOT, 'zkmi', name + suffix)
+
+
+# CPython extensions built from csrc/host: module name -> source
+HOST_EXTS = {'_zkhost': 'zk_host_codec.cpp',     # Jute host codec
+             '_zkloop': 'zk_loop.cpp'}           # epoll event loop
 
 
 def build_host():
-    src = os.path.join(HDIR, 'zk_host_codec.cpp')
-    if not os.path.exists(src):
-        return None
-    out = host_so_path()
-    deps = [src] + [os.path.join(HDIR, f) for f in os.listdir(HDIR)]
-    if _stale(out, deps):
-        inc = sysconfig.get_paths()['include']
-        _run(['g++', '-O3', '-fPIC', '-shared', '-std=c++17', '-Wall',
-              '-fno-strict-aliasing', '-I' + inc, src, '-o', out])
-    return out
+    outs = []
+    inc = sysconfig.get_paths()['include']
+    for name, src in HOST_EXTS.items():
+        src = os.path.join(HDIR, src)
+        out = _ext_path(name)
+        if _stale(out, [src]):
+            _run(['g++', '-O3', '-fPIC', '-shared', '-std=c++17', '-Wall',
+                  '-Wextra', '-Wno-missing-field-initializers',
+                  '-Wno-cast-function-type', '-fno-strict-aliasing',
+                  '-I' + inc, src, '-o', out])
+        outs.append(out)
+    return outs
 
 
 SANITIZE_DIR = os.path.join(BDIR, 'sanitize')
 
 
 def build_host_sanitized():
-    """The host codec built with AddressSanitizer + UndefinedBehaviorSanitizer
-    (host code only — GPU sanitizers are not used).  Load it with
-    ``ZKMI_HOST_CODEC_PATH=<this .so>`` and the sanitizer runtimes preloaded
-    (see tools/sanitize_host.sh)."""
-    src = os.path.join(HDIR, 'zk_host_codec.cpp')
+    """The host extensions (codec and event loop) built with
+    AddressSanitizer + UndefinedBehaviorSanitizer (host code only — GPU
+    sanitizers are not used).  Load them with ``ZKMI_HOST_CODEC_PATH`` /
+    ``ZKMI_NATIVE_LOOP_PATH`` and the sanitizer runtimes preloaded (see
+    tools/sanitize_host.sh).  Returns the two paths."""
     os.makedirs(SANITIZE_DIR, exist_ok=True)
     suffix = sysconfig.get_config_var('EXT_SUFFIX') or '.so'
-    out = os.path.join(SANITIZE_DIR, '_zkhost' + suffix)
-    if _stale(out, [src]):
-        inc = sysconfig.get_paths()['include']
-        _run(['g++', '-O1', '-g', '-fPIC', '-shared', '-std=c++17', '-Wall',
-              '-fno-strict-aliasing', '-fno-omit-frame-pointer',
-              '-fsanitize=address,undefined', '-fno-sanitize-recover=all',
-              '-I' + inc, src, '-o', out])
-    return out
+    inc = sysconfig.get_paths()['include']
+    outs = []
+    for name, src in HOST_EXTS.items():
+        src = os.path.join(HDIR, src)
+        out = os.path.join(SANITIZE_DIR, name + suffix)
+        if _stale(out, [src]):
+            _run(['g++', '-O1', '-g', '-fPIC', '-shared', '-std=c++17',
+                  '-Wall', '-fno-strict-aliasing', '-fno-omit-frame-pointer',
+                  '-fsanitize=address,undefined', '-fno-sanitize-recover=all',
+                  '-I' + inc, src, '-o', out])
+        outs.append(out)
+    return outs
 
 
 def main():
@@ -115,7 +130,7 @@ def main():
     ap.add_argument('-j', type=int, default=4)
     a = ap.parse_args()
     if a.sanitize:
-        print(build_host_sanitized())
+        print(' '.join(build_host_sanitized()))
         return
     if not a.host_only:
         print(build_hip(a.j))

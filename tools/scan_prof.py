@@ -21,7 +21,8 @@ def main(path):
     print('| kernel | workgroups | calls | median us |')
     print('|---|---|---|---|')
     for (k, g), v in sorted(rows.items(), key=lambda x: (x[0][1], x[0][0])):
-        print('| `%s` | %d | %d | %.2f |' % (k, g, len(v), statistics.median(v)))
+        print('| `%s` | %d | %d | %.2f |'
+              % (k, g, len(v), statistics.median(v)))
 
 
 if __name__ == '__main__':

@@ -339,9 +339,7 @@ class Client(FSM):
             if conn is None or not conn.isInState('connected'):
                 self._not_connected(cb)
                 return
-            req = conn.request(pkt)
-            req.once('reply', on_reply)
-            req.once('error', lambda err, *_: cb(err))
+            conn.request(pkt).then(on_reply, lambda err, *_: cb(err))
         self._dispatch(go)
 
     def ping(self, cb):
@@ -535,15 +533,18 @@ class Client(FSM):
         if self.loop.in_loop():
             raise RuntimeError('call_sync must not be used on the loop '
                                'thread')
-        ev = threading.Event()
+        # a bare lock, released by the loop thread: the cheapest cross-thread
+        # wake-up CPython has (threading.Event adds a Condition round)
+        done = threading.Lock()
+        done.acquire()
         box = {}
 
         def cb(err=None, *res):
             box['err'] = err
             box['res'] = res
-            ev.set()
+            done.release()
         getattr(self, method)(*args, cb)
-        if not ev.wait(timeout):
+        if not done.acquire(timeout=timeout):
             raise TimeoutError('%s%r timed out' % (method, args))
         if box['err'] is not None:
             raise box['err']

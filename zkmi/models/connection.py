@@ -29,14 +29,31 @@ from ..streams import ZKDecoder, ZKEncoder
 
 class ZKRequest(EventEmitter):
     """An outstanding request; emits ``reply(pkt)`` or ``error(err, pkt)``
-    (``lib/connection-fsm.js:378-382``)."""
+    (``lib/connection-fsm.js:378-382``).
 
-    __slots__ = ('packet', 't_submit')
+    :meth:`then` registers a (reply, error) pair called directly, without
+    listener bookkeeping — the client data API's per-request path."""
+
+    __slots__ = ('packet', 't_submit', 'fast')
 
     def __init__(self, packet):
         EventEmitter.__init__(self)
         self.packet = packet
         self.t_submit = time.perf_counter()
+        self.fast = None
+
+    def then(self, on_reply, on_error):
+        self.fast = (on_reply, on_error)
+        return self
+
+    def settle(self, evt, *args):
+        f = self.fast
+        if f is None:
+            self.emit(evt, *args)
+            return
+        f[0 if evt == 'reply' else 1](*args)
+        if self._listeners.get(evt):
+            self.emit(evt, *args)
 
 
 class ZKConnectionFSM(FSM):
@@ -304,7 +321,7 @@ class ZKConnectionFSM(FSM):
                       'error communicating with ZK')
         reqs, self.reqs = self.reqs, {}
         for req in list(reqs.values()):
-            req.emit('error', err)
+            req.settle('error', err)
         self._fail_bulks(err)
         # Not S.immediate: this must be emitted even though we leave the
         # state right away (lib/connection-fsm.js:318-323).
@@ -327,14 +344,16 @@ class ZKConnectionFSM(FSM):
             err = ZKProtocolError('CONNECTION_LOSS', 'Connection closed.')
             reqs, self.reqs = self.reqs, {}
             for req in list(reqs.values()):
-                req.emit('error', err)
+                req.settle('error', err)
             self._fail_bulks(err)
         S.immediate(later)
 
     # -- requests -------------------------------------------------------------
 
     def processReply(self, pkt):
-        req = self.reqs.get(pkt['xid'])
+        # the entry goes before the reply is delivered, as endRequest (the
+        # first 'reply' listener) does at lib/connection-fsm.js:405-407
+        req = self.reqs.pop(pkt['xid'], None)
         if self.tracer is not None and req is not None:
             self.tracer.record(pkt['xid'], pkt['opcode'], req.t_submit,
                                pkt['err'])
@@ -344,11 +363,11 @@ class ZKConnectionFSM(FSM):
         if req is None:
             return
         if pkt['err'] == 'OK':
-            req.emit('reply', pkt)
+            req.settle('reply', pkt)
             return
         code = pkt['err']
         err = ZKError(code, consts.ERR_TEXT.get(code, str(code)))
-        req.emit('error', err, pkt)
+        req.settle('error', err, pkt)
 
     def request(self, pkt):
         if not self.isInState('connected'):
@@ -356,13 +375,7 @@ class ZKConnectionFSM(FSM):
         req = ZKRequest(pkt)
         xid = self.nextXid()
         pkt['xid'] = xid
-        self.reqs[xid] = req
-
-        def end_request(*_):
-            if self.reqs.get(xid) is req:
-                del self.reqs[xid]
-        req.once('reply', end_request)
-        req.once('error', end_request)
+        self.reqs[xid] = req      # removed by processReply / the fail paths
         self.log.trace({'xid': xid, 'opcode': pkt['opcode']},
                        'sent request to server')
         self.socket.write(self.encoder.request(pkt))

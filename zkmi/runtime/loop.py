@@ -1,4 +1,8 @@
-"""Event-loop runtime: one asyncio loop on a dedicated thread.
+"""Event-loop runtime: one loop on a dedicated thread.
+
+Two implementations with one surface: the native epoll loop
+(:mod:`zkmi.runtime.nloop`, ``csrc/host/zk_loop.cpp``; the default when
+built) and the asyncio loop below (``ZKMI_LOOP=asyncio``, and the fallback).
 
 The reference is single-threaded on the Node event loop; every FSM, timer and
 socket callback runs there.  We keep that model exactly — all
@@ -118,6 +122,34 @@ class Loop(object):
             raise box['e']
         return box.get('r')
 
+    # -- sockets (same surface as the native loop) ---------------------------
+
+    def open_connection(self, protocol, host, port, on_fail):
+        """Start a TCP connect (any thread).  ``protocol`` gets the asyncio
+        callbacks; ``on_fail(OSError)`` runs on the loop if the connect
+        fails.  Returns a handle whose ``cancel()`` abandons the attempt."""
+        async def go():
+            try:
+                await self._loop.create_connection(lambda: protocol, host,
+                                                   port)
+            except asyncio.CancelledError:
+                return
+            except OSError as e:
+                on_fail(e)
+        if self.in_loop():
+            return self._loop.create_task(go())
+        return asyncio.run_coroutine_threadsafe(go(), self._loop)
+
+    def start_server(self, factory, host, port):
+        """Listen on ``host:port`` (0 = any free port); call from a thread
+        other than the loop's.  Returns an object with ``port`` and
+        ``close()`` (close on the loop thread)."""
+        async def go():
+            return await self._loop.create_server(factory, host, port,
+                                                  reuse_address=True)
+        srv = asyncio.run_coroutine_threadsafe(go(), self._loop).result(10)
+        return _AioServer(srv)
+
     def spawn(self, coro):
         """Schedule a coroutine on the loop (thread-safe)."""
         if self.in_loop():
@@ -131,6 +163,28 @@ class Loop(object):
         self._thread.join(timeout=5)
 
 
+class _AioServer(object):
+    __slots__ = ('_srv', 'port')
+
+    def __init__(self, srv):
+        self._srv = srv
+        self.port = srv.sockets[0].getsockname()[1]
+
+    def close(self):
+        self._srv.close()
+
+
+def new_loop(name='zkmi-loop'):
+    """A new loop thread: native (epoll, csrc/host/zk_loop.cpp) when the
+    extension is built, unless ``ZKMI_LOOP=asyncio``."""
+    import os
+    from . import nloop
+    if os.environ.get('ZKMI_LOOP', 'native') != 'asyncio' and \
+            nloop.available():
+        return nloop.NativeLoop(name)
+    return Loop(name)
+
+
 _default = None
 _default_lock = threading.Lock()
 
@@ -141,7 +195,7 @@ def default_loop():
     global _default
     with _default_lock:
         if _default is None:
-            _default = Loop()
+            _default = new_loop()
         return _default
 
 

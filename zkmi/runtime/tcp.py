@@ -56,26 +56,21 @@ class TcpSocket(EventEmitter):
     def connect(self, host, port):
         self.connecting = True
         self.remote = (host, port)
-        self._task = self.loop.aio.create_task(self._connect(host, port))
+        self._task = self.loop.open_connection(_Proto(self), host, port,
+                                               self._connect_failed)
         return self
 
-    async def _connect(self, host, port):
-        try:
-            await self.loop.aio.create_connection(lambda: _Proto(self),
-                                                  host, port)
-        except asyncio.CancelledError:
-            return
-        except OSError as e:
-            self.connecting = False
-            if not self.closed:
-                self._fail(e)
+    def _connect_failed(self, e):
+        self.connecting = False
+        if not self.closed:
+            self._fail(e)
 
     # -- server side ----------------------------------------------------------
 
     @classmethod
     def protocol_for(cls, loop, on_accept):
-        """asyncio protocol factory for a server: ``on_accept(sock)`` is
-        called with a connected :class:`TcpSocket`."""
+        """Protocol factory for ``loop.start_server``: ``on_accept(sock)``
+        is called with a connected :class:`TcpSocket`."""
         def factory():
             s = cls(loop)
             s._on_accept = on_accept
@@ -165,7 +160,7 @@ class TcpSocket(EventEmitter):
         if self.closed:
             return
         self.closed = True
-        if self._task is not None and not self._task.done():
+        if self._task is not None and self.connecting:
             self._task.cancel()
         if self.transport is not None:
             self.transport.abort()

@@ -32,7 +32,7 @@ from .. import consts
 from .. import jute
 from ..errors import ZKDecodeError
 from ..jute import Stat
-from ..runtime.loop import Loop
+from ..runtime.loop import new_loop
 from ..runtime.tcp import TcpSocket
 from ..streams import ZKDecoder
 
@@ -510,7 +510,7 @@ class FakeZKServer(object):
 
     def __init__(self, db=None, host='127.0.0.1', port=0, loop=None,
                  tick_ms=2000, server_id=1):
-        self.loop = loop or Loop(name='fakezk')
+        self.loop = loop or new_loop(name='fakezk')
         self._own_loop = loop is None
         self.db = db or self.loop.run(lambda: ZKDatabase(self.loop, tick_ms,
                                                          server_id))
@@ -529,15 +529,9 @@ class FakeZKServer(object):
     # -- lifecycle ------------------------------------------------------------
 
     def start(self):
-        async def go():
-            factory = TcpSocket.protocol_for(self.loop, self._on_accept)
-            srv = await self.loop.aio.create_server(factory, self.host,
-                                                    self.port,
-                                                    reuse_address=True)
-            self._srv = srv
-            self.port = srv.sockets[0].getsockname()[1]
-        fut = self.loop.spawn(go())
-        fut.result(10)
+        factory = TcpSocket.protocol_for(self.loop, self._on_accept)
+        self._srv = self.loop.start_server(factory, self.host, self.port)
+        self.port = self._srv.port
         return self
 
     def stop(self, kill_sessions=False):
@@ -651,7 +645,7 @@ class FakeEnsemble(object):
     ``test/multi-node.test.js``)."""
 
     def __init__(self, n=3, tick_ms=2000):
-        self.loop = Loop(name='fakezk-ens')
+        self.loop = new_loop(name='fakezk-ens')
         self.db = self.loop.run(lambda: ZKDatabase(self.loop, tick_ms, 1))
         self.members = [FakeZKServer(db=self.db, loop=self.loop,
                                      server_id=i + 1) for i in range(n)]

@@ -58,59 +58,6 @@ __global__ __launch_bounds__(ENC_T) void req_sizes(ZkReqBatch b, int64_t n,
   if (!ok) atomicOr(err, 1);
 }
 
-__global__ __launch_bounds__(ENC_T) void req_write(
-    ZkReqBatch b, int64_t n, const int64_t* __restrict__ off,
-    const int64_t* __restrict__ total, uint8_t* __restrict__ out, int64_t cap,
-    int64_t* __restrict__ xid_tab, int64_t xid_mask, int32_t* __restrict__ err) {
-  const int64_t i = (int64_t)blockIdx.x * ENC_T + threadIdx.x;
-  if (i >= n) return;
-  if (*total > cap) {                       // capacity guard (whole batch)
-    if (i == 0) atomicOr(err, 2);
-    return;
-  }
-  bool ok;
-  const int64_t body = req_body_size(b, i, &ok);
-  if (!ok) return;
-  uint8_t* o = out + off[i];
-  const int32_t op = b.opcode[i];
-  const int32_t xid = b.xid[i];
-  st_be32(o, (int32_t)body);
-  st_be32(o + 4, xid);
-  st_be32(o + 8, op);
-  o += 12;
-  if (op == OP_PING || op == OP_CLOSE_SESSION) {
-    // header only
-  } else {
-    const int32_t pl = b.path_len[i];
-    o = put_buffer(o, b.path_arena + b.path_off[i], pl);
-    switch (op) {
-      case OP_GET_DATA: case OP_EXISTS: case OP_GET_CHILDREN:
-      case OP_GET_CHILDREN2:
-        *o = b.arg[i] ? 1 : 0;
-        break;
-      case OP_CREATE: {
-        o = put_buffer(o, b.data_arena + b.data_off[i], b.data_len[i]);
-        const int32_t a = b.acl_id[i];
-        copy_bytes(o, b.acl_arena + b.acl_off[a], b.acl_len[a]);
-        o += b.acl_len[a];
-        st_be32(o, b.arg[i]);
-        break;
-      }
-      case OP_DELETE:
-        st_be32(o, b.arg[i]);
-        break;
-      case OP_SET_DATA:
-        o = put_buffer(o, b.data_arena + b.data_off[i], b.data_len[i]);
-        st_be32(o, b.arg[i]);
-        break;
-      default:
-        break;
-    }
-  }
-  if (xid_tab != nullptr && xid >= 0)
-    xid_tab[xid & xid_mask] = ((int64_t)xid << 32) | (uint32_t)op;
-}
-
 // ---------------------------------------------------------------- K11
 // SET_WATCHES: relZxid + three string vectors (data, exist, child), one
 // frame.  Paths are given as (off,len) lists; kind[i] in {0,1,2}; the host
@@ -199,6 +146,14 @@ __global__ __launch_bounds__(ENC_T) void resp_sizes(ZkRespBatch r,
 // LSink packs bytes into aligned dwords; only a record's first and last
 // dword can be shared with a neighbour, and those are OR-ed into the
 // zero-initialised image (ds_or_b32), everything else is a plain ds_write.
+//
+// The image is bank-swizzled: dword w lives at swz(w), which XORs bits 2-5
+// with the 64-dword row number.  Lanes emit their records in lockstep, so
+// their k-th dwords sit one record apart; at 192-byte records (48 dwords)
+// that put 4 lanes on every bank (measured: 23.6 M conflict cycles per 1M
+// GET_DATA replies).  The XOR keeps each aligned 4-dword group together, so
+// the read-out still moves 16-byte vectors.
+ZK_DEV int64_t swz(int64_t w) { return w ^ (((w >> 6) & 15) << 2); }
 struct GSink {
   uint8_t* o;
   ZK_DEV void be32(int32_t v) { st_be32(o, v); o += 4; }
@@ -218,8 +173,8 @@ struct LSink {
                                              nb((int)(rel & 3)), first(true) {}
   ZK_DEV void flush() {
     const uint32_t v = (uint32_t)acc;
-    if (first) { atomicOr(&w[widx], v); first = false; }
-    else w[widx] = v;
+    if (first) { atomicOr(&w[swz(widx)], v); first = false; }
+    else w[swz(widx)] = v;
     ++widx;
     acc >>= 32;
     nb -= 4;
@@ -251,7 +206,7 @@ struct LSink {
     for (; i < n; ++i) u8(s[i]);
   }
   ZK_DEV void finish() {
-    if (nb > 0) atomicOr(&w[widx], (uint32_t)acc);
+    if (nb > 0) atomicOr(&w[swz(widx)], (uint32_t)acc);
   }
 };
 
@@ -297,7 +252,11 @@ ZK_DEV void emit_response(K& k, const ZkRespBatch& r, const ZkNodeStore& s,
   k.finish();
 }
 
-constexpr int64_t STAGE_BYTES = 64 * 1024;   // LDS image per block
+constexpr int64_t STAGE_BYTES = 32 * 1024;   // LDS image per block
+
+ZK_DEV uint8_t lds_byte(const uint32_t* lw, int64_t b) {
+  return ((const uint8_t*)(lw + swz(b >> 2)))[b & 3];
+}
 
 // Stream the block's LDS image [B0, B1) (image base a0 = B0 & ~15) out to
 // global memory: 16-byte aligned interior with dwordx4 stores, the <= 15
@@ -306,22 +265,62 @@ ZK_DEV void stage_out(const uint32_t* lw, int64_t a0, int64_t B0, int64_t B1,
                       uint8_t* __restrict__ out) {
   const int64_t c0 = (B0 + 15) & ~(int64_t)15;
   const int64_t c1 = B1 & ~(int64_t)15;
-  const uint8_t* lb = (const uint8_t*)lw;
   if (c0 < c1) {
     for (int64_t x = c0 + (int64_t)threadIdx.x * 16; x < c1;
          x += (int64_t)blockDim.x * 16)
-      *(uint4*)(out + x) = *(const uint4*)(lb + (x - a0));
+      *(uint4*)(out + x) = *(const uint4*)(lw + swz((x - a0) >> 2));
     const int64_t hb = c0 - B0, tb = B1 - c1;
     if ((int64_t)threadIdx.x < hb) {
       const int64_t x = B0 + threadIdx.x;
-      out[x] = lb[x - a0];
+      out[x] = lds_byte(lw, x - a0);
     } else if ((int64_t)threadIdx.x >= 16 && (int64_t)threadIdx.x < 16 + tb) {
       const int64_t x = c1 + threadIdx.x - 16;
-      out[x] = lb[x - a0];
+      out[x] = lds_byte(lw, x - a0);
     }
   } else {
     for (int64_t x = B0 + threadIdx.x; x < B1; x += blockDim.x)
-      out[x] = lb[x - a0];
+      out[x] = lds_byte(lw, x - a0);
+  }
+}
+
+// Emit records [r0, r1) (one per thread, <= blockDim) through the block's
+// LDS image.  Records are staged in runs that fit the image (record i ends
+// at off[i] + sizes[i]; ends grow with i, so "fits" is a prefix of the
+// run, counted with one barrier); a single record larger than the image is
+// written straight to global memory.
+template <class F>
+ZK_DEV void staged_emit(int64_t r0, int64_t r1, const int64_t* __restrict__ off,
+                        const int64_t* __restrict__ sizes,
+                        uint8_t* __restrict__ out, uint32_t* lw, F emit) {
+  int64_t rs = r0;
+  while (rs < r1) {                              // block-uniform
+    const int64_t B0 = off[rs];
+    const int64_t a0 = B0 & ~(int64_t)15;
+    const int64_t i = rs + threadIdx.x;
+    const bool fits = i < r1 && off[i] + sizes[i] - a0 + 16 <= STAGE_BYTES;
+    const int k = __syncthreads_count(fits);
+    if (k == 0) {
+      if (threadIdx.x == 0) {
+        GSink g{out + off[rs]};
+        emit(g, rs);
+      }
+      rs += 1;
+      continue;
+    }
+    const int64_t re = rs + k;
+    const int64_t B1 = off[re - 1] + sizes[re - 1];
+    const int64_t nrow = ((B1 - a0 + 3) >> 8) + 1;     // 64-dword rows
+    for (int64_t x = threadIdx.x; x < nrow * 16; x += blockDim.x)
+      ((uint4*)lw)[x] = make_uint4(0, 0, 0, 0);
+    __syncthreads();
+    if (i < re) {
+      LSink l(lw, off[i] - a0);
+      emit(l, i);
+    }
+    __syncthreads();
+    stage_out(lw, a0, B0, B1, out);
+    __syncthreads();                             // image reused next run
+    rs = re;
   }
 }
 
@@ -339,26 +338,75 @@ __global__ __launch_bounds__(ENC_T) void resp_write(
     return;
   }
   const int64_t r1 = min(r0 + ENC_T, n);
-  const int64_t i = r0 + threadIdx.x;
-  const int64_t B0 = off[r0];
-  const int64_t B1 = off[r1 - 1] + sizes[r1 - 1];
-  const int64_t a0 = B0 & ~(int64_t)15;
-  const int64_t nw = (B1 - a0 + 3) >> 2;
-  if (nw * 4 + 16 > STAGE_BYTES) {              // oversized block: direct
-    if (i < r1) {
-      GSink g{out + off[i]};
-      emit_response(g, r, s, i, sizes[i] - 4);
-    }
+  staged_emit(r0, r1, off, sizes, out, lw, [&](auto& k, int64_t i) {
+    emit_response(k, r, s, i, sizes[i] - 4);
+  });
+}
+
+// ---------------------------------------------------------------- K10 write
+template <class K>
+ZK_DEV void emit_request(K& k, const ZkReqBatch& b, int64_t i, int64_t body) {
+  const int32_t op = b.opcode[i];
+  k.be32((int32_t)body);
+  k.be32(b.xid[i]);
+  k.be32(op);
+  if (op == OP_PING || op == OP_CLOSE_SESSION) {
+    k.finish();
     return;
   }
-  for (int64_t k = threadIdx.x; k <= nw; k += blockDim.x) lw[k] = 0;
-  __syncthreads();
-  if (i < r1) {
-    LSink l(lw, off[i] - a0);
-    emit_response(l, r, s, i, sizes[i] - 4);
+  k_buffer(k, b.path_arena + b.path_off[i], b.path_len[i]);
+  switch (op) {
+    case OP_GET_DATA: case OP_EXISTS: case OP_GET_CHILDREN:
+    case OP_GET_CHILDREN2:
+      k.u8(b.arg[i] ? 1 : 0);
+      break;
+    case OP_CREATE: {
+      k_buffer(k, b.data_arena + b.data_off[i], b.data_len[i]);
+      const int32_t a = b.acl_id[i];
+      k.bytes(b.acl_arena + b.acl_off[a], b.acl_len[a]);
+      k.be32(b.arg[i]);
+      break;
+    }
+    case OP_DELETE:
+      k.be32(b.arg[i]);
+      break;
+    case OP_SET_DATA:
+      k_buffer(k, b.data_arena + b.data_off[i], b.data_len[i]);
+      k.be32(b.arg[i]);
+      break;
+    default:
+      break;
   }
-  __syncthreads();
-  stage_out(lw, a0, B0, B1, out);
+  k.finish();
+}
+
+// Records are staged through the block's LDS image and streamed out with
+// 16-byte stores (a thread's own scattered 4-byte / byte stores wrote ~7x
+// the frame bytes as partial-line writes: WRITE_SIZE 254 MB for a 36 MB
+// GET_DATA stream).  Unknown opcodes were flagged by req_sizes and get
+// size 0 (nothing written).
+__global__ __launch_bounds__(ENC_T) void req_write(
+    ZkReqBatch b, int64_t n, const int64_t* __restrict__ off,
+    const int64_t* __restrict__ sizes, const int64_t* __restrict__ total,
+    uint8_t* __restrict__ out, int64_t cap, int64_t* __restrict__ xid_tab,
+    int64_t xid_mask, int32_t* __restrict__ err) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lw[];
+  const int64_t r0 = (int64_t)blockIdx.x * ENC_T;
+  if (r0 >= n) return;
+  if (*total > cap) {                       // capacity guard (whole batch)
+    if (r0 == 0 && threadIdx.x == 0) atomicOr(err, 2);
+    return;
+  }
+  const int64_t r1 = min(r0 + ENC_T, n);
+  staged_emit(r0, r1, off, sizes, out, lw, [&](auto& k, int64_t i) {
+    if (sizes[i] > 0) emit_request(k, b, i, sizes[i] - 4);
+  });
+  const int64_t i = r0 + threadIdx.x;
+  if (i < r1 && xid_tab != nullptr && sizes[i] > 0) {
+    const int32_t xid = b.xid[i];
+    if (xid >= 0)
+      xid_tab[xid & xid_mask] = ((int64_t)xid << 32) | (uint32_t)b.opcode[i];
+  }
 }
 
 // ---------------------------------------------------------------- K9
@@ -405,8 +453,8 @@ int zk_encode_requests(const ZkReqBatch* b, int64_t n, int64_t* sizes,
   ZK_LAUNCH_CHECK();
   int rc = zk_scan_excl_i64(sizes, rec_off, n, total, scan_ws, st);
   if (rc) return rc;
-  zk::req_write<<<zk::nblk(n), zk::ENC_T, 0, st>>>(
-      *b, n, rec_off, total, out, out_cap, xid_tab, xid_mask, err);
+  zk::req_write<<<zk::nblk(n), zk::ENC_T, zk::STAGE_BYTES, st>>>(
+      *b, n, rec_off, sizes, total, out, out_cap, xid_tab, xid_mask, err);
   ZK_LAUNCH_CHECK();
   return 0;
 }

@@ -5,8 +5,11 @@ get() RTT, 1M-znode synthetic tree".
 Default config (BASELINE.json configs[1]): batched get() over a 1M-znode
 synthetic tree with the Jute-decode HIP kernels on each MI355X.
 ``--workload mix`` is configs[2] (create/set/delete with version CAS and ACL
-encode on the same 1M-znode tree) and ``--workload storm`` configs[4]
-(EPHEMERAL|SEQUENTIAL create storm with per-step session expiry).
+encode on the same 1M-znode tree), ``--workload storm`` configs[4]
+(EPHEMERAL|SEQUENTIAL create storm with per-step session expiry) and
+``--workload watch`` the watch fan-out of configs[3] (every rank's
+notifications all-gathered over RCCL and decoded by every rank; the value
+counts node-wide deliveries).
 One step = one batch
 of ``--batch`` GET_DATA requests per GPU pushed through the full ZooKeeper
 wire path on the GPU (see zkmi/bench/synthetic.py): client request encode
@@ -84,7 +87,7 @@ def main():
     ap.add_argument('--nodes', type=int, default=1_000_000)
     ap.add_argument('--data-bytes', type=int, default=100)
     ap.add_argument('--no-rtt', action='store_true')
-    ap.add_argument('--workload', choices=('get', 'mix', 'storm'),
+    ap.add_argument('--workload', choices=('get', 'mix', 'storm', 'watch'),
                     default='get')
     a = ap.parse_args()
 
@@ -112,6 +115,11 @@ def main():
         tree = S.GpuTree(a.nodes, a.data_bytes, device=dev, seed=rank)
         pipe = S.GetPipeline(tree, a.batch, seed=rank)
         per_step = a.batch
+    elif a.workload == 'watch':
+        tree = S.GpuTree(a.nodes, a.data_bytes, device=dev, seed=rank)
+        pipe = S.WatchPipeline(tree, a.batch, seed=rank,
+                               coll_device=cdev if world > 1 else None)
+        per_step = a.batch * world      # notifications decoded per rank
     else:
         # room for the write working set next to the 1M static nodes: the
         # mix keeps 3 generations of batch/3 nodes, the storm 2 sessions'

@@ -1,7 +1,7 @@
-// Benchmark-side helpers for the synthetic GET pipeline
-// (zkmi/bench/synthetic.py GetPipeline): request generation and the
-// per-reply validation, each ONE fused kernel instead of ~15 small torch
-// element-wise launches per step.  Semantics are those of the torch code
+// Benchmark-side helpers for the synthetic pipelines
+// (zkmi/bench/synthetic.py GetPipeline, WatchPipeline): request generation
+// and the per-reply validation, each ONE fused kernel instead of ~15 small
+// torch element-wise launches per step.  Semantics are those of the torch code
 // they replace: uniform random node per request, consecutive xids, and a
 // reply counts as OK only if it decoded cleanly, carries err OK, opcode
 // GET_DATA, the request's xid, czxid == node + 1 and the node's data length.
@@ -63,9 +63,67 @@ __global__ __launch_bounds__(BG_T) void bench_check_get(
   if (threadIdx.x == 0 && tot) atomicAdd(ok, (unsigned long long)tot);
 }
 
+// Watch fan-out (zkmi/bench/synthetic.py WatchPipeline): every rank
+// receives the notification streams of all ranks (R1 all-gather), decodes
+// them (K1 + K8) and checks each record against the node its producer drew:
+// record i belongs to producer rank i / n_per, index i % n_per, drawn with
+// seeds[rank] exactly as bench_gen_get draws it.  OK = clean decode,
+// NOTIFICATION, err OK, type NodeDataChanged, state SyncConnected and the
+// path bytes equal to the node's path.
+__global__ __launch_bounds__(BG_T) void bench_check_notif(
+    int64_t total, int64_t n_per, const uint64_t* __restrict__ seeds,
+    int64_t leaf0, int64_t nleaves, const int64_t* __restrict__ node_path_off,
+    const int32_t* __restrict__ node_path_len,
+    const uint8_t* __restrict__ path_arena, const uint8_t* __restrict__ rx,
+    const int32_t* __restrict__ status, const int32_t* __restrict__ err,
+    const int32_t* __restrict__ opcode, const int32_t* __restrict__ aux0,
+    const int32_t* __restrict__ aux1, const int64_t* __restrict__ pay_off,
+    const int32_t* __restrict__ pay_len, unsigned long long* __restrict__ ok) {
+  __shared__ int64_t sm[BG_T / 64 + 1];
+  int64_t good = 0;
+  for (int64_t i = (int64_t)blockIdx.x * BG_T + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * BG_T) {
+    const int64_t r = i / n_per, j = i - r * n_per;
+    const uint64_t h = splitmix64(seeds[r] ^ (uint64_t)j * 0xD1B54A32D192ED03ull);
+    const int64_t v = leaf0 + (int64_t)(((h >> 32) * (uint64_t)nleaves) >> 32);
+    const int32_t pl = node_path_len[v];
+    bool g = status[i] == 0 && err[i] == 0 && opcode[i] == OP_NOTIFICATION &&
+             aux0[i] == 3 && aux1[i] == 3 && pay_len[i] == pl;
+    if (g) {
+      const uint8_t* a = rx + pay_off[i];
+      const uint8_t* b = path_arena + node_path_off[v];
+      for (int32_t k = 0; k < pl && g; ++k) g = a[k] == b[k];
+    }
+    good += g;
+  }
+  int64_t tot;
+  block_excl_scan(good, sm, &tot);
+  if (threadIdx.x == 0 && tot) atomicAdd(ok, (unsigned long long)tot);
+}
+
 }  // namespace zk
 
 extern "C" {
+
+int zk_bench_check_notif(int64_t total, int64_t n_per, const uint64_t* seeds,
+                         int64_t leaf0, int64_t nleaves,
+                         const int64_t* node_path_off,
+                         const int32_t* node_path_len,
+                         const uint8_t* path_arena, const uint8_t* rx,
+                         const int32_t* status, const int32_t* err,
+                         const int32_t* opcode, const int32_t* aux0,
+                         const int32_t* aux1, const int64_t* pay_off,
+                         const int32_t* pay_len, unsigned long long* ok,
+                         hipStream_t st) {
+  if (total <= 0 || n_per <= 0) return 0;
+  const int64_t nb = min((total + zk::BG_T - 1) / zk::BG_T,
+                         (int64_t)zk::BG_CHECK_BLOCKS);
+  zk::bench_check_notif<<<(unsigned)nb, zk::BG_T, 0, st>>>(
+      total, n_per, seeds, leaf0, nleaves, node_path_off, node_path_len,
+      path_arena, rx, status, err, opcode, aux0, aux1, pay_off, pay_len, ok);
+  ZK_LAUNCH_CHECK();
+  return 0;
+}
 
 int zk_bench_gen_get(int64_t n, uint64_t seed, int64_t leaf0, int64_t nleaves,
                      int32_t xid_base, const int64_t* node_path_off,

@@ -499,3 +499,63 @@ def test_gpu_storm_pipeline(gpu):
     for _ in range(12):                 # crosses at least one rehash
         ok = pipe.step()
         assert int(ok.item()) == 8192
+
+
+def test_gpu_watch_pipeline_single_rank(gpu):
+    """Notification fan-out data path on one rank: K13 notification encode,
+    K1 + K8 decode, device check; a few records against the Jute oracle."""
+    from zkmi.bench.synthetic import WatchPipeline
+    tree = _small_tree(gpu, 20000, 37)
+    pipe = WatchPipeline(tree, 5000)
+    for _ in range(2):
+        ok = pipe.step()
+        assert int(ok.item()) == 5000
+    rep, rx, ft = pipe.last
+    assert ft.host_result()['frames'] == 5000
+    hb = bytes(rx[:4096].cpu().numpy().tobytes())
+    frames, _, _ = jute.scan_frames(hb)
+    for (o, ln) in frames[:20]:
+        pkt = jute.decode_response(hb[o:o + ln], {})
+        assert pkt['opcode'] == 'NOTIFICATION'
+        assert pkt['type'] == 'DATA_CHANGED'
+        assert pkt['state'] == 'SYNC_CONNECTED'
+        assert pkt['path'].startswith('/bench/d')
+
+
+def _watch_rank(rank, world, port, q):
+    import os
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        from zkmi.bench.synthetic import GpuTree, WatchPipeline
+        dev = torch.device('cuda', 0)
+        tree = GpuTree(20000, 37, fanout=100, device=dev, seed=rank)
+        pipe = WatchPipeline(tree, 3000, coll_device='cpu')
+        ok = pipe.step()
+        q.put((rank, int(ok.item())))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gpu_watch_pipeline_two_ranks_gloo(gpu):
+    """Two ranks sharing the GPU, collective on gloo (the RCCL path needs
+    one GPU per rank): every rank decodes and checks BOTH ranks'
+    notifications (each rank drew its own nodes)."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_watch_rank, args=(r, 2, port, q))
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(180)
+    assert all(p.exitcode == 0 for p in procs)
+    got = dict(q.get(timeout=5) for _ in range(2))
+    assert got == {0: 6000, 1: 6000}

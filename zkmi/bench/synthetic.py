@@ -598,3 +598,130 @@ class StormPipeline(object):
                 'pay_len_bad': int((rep.pay_len[:n] != self.want_len)
                                    .sum().item()),
                 'counters': self.tree.counters.cpu().tolist()}
+
+
+class WatchPipeline(object):
+    """Watch fan-out across the node (BASELINE config 4's data path, R1 at
+    scale): every rank fires ``batch`` NodeDataChanged notifications for
+    random nodes of its tree, encodes them as wire records on the GPU (K13,
+    xid -1), and the streams of all ranks are all-gathered over RCCL
+    (``torch.distributed``, backend ``nccl`` = RCCL over xGMI); every rank
+    then frame-scans and decodes ALL ranks' notifications (K1 + K8) and
+    checks each one on the device (producer rank, node path, type, state).
+
+    One step moves ``world * batch`` notifications into every rank, i.e.
+    ``world**2 * batch`` deliveries node-wide.  ``coll_device='cpu'`` runs
+    the collective on host tensors (gloo rehearsal)."""
+
+    def __init__(self, tree, batch, seed=0, group=None, coll_device=None):
+        import torch.distributed as dist
+        self.dist = dist
+        self.group = group
+        on = dist.is_available() and dist.is_initialized()
+        self.world = dist.get_world_size(group) if on else 1
+        self.rank = dist.get_rank(group) if on else 0
+        self.tree = tree
+        self.n = batch
+        dev = tree.device
+        self.dev = dev
+        self.coll_device = torch.device(coll_device) if coll_device else dev
+        n = batch
+        self.idx = torch.empty(n, dtype=I64, device=dev)
+        self.xid = torch.empty(n, dtype=I32, device=dev)
+        self.poff = torch.empty(n, dtype=I64, device=dev)
+        self.plen = torch.empty(n, dtype=I32, device=dev)
+        self.resp = B.ResponseBatch(
+            torch.zeros(n, dtype=I32, device=dev),            # NOTIFICATION
+            torch.full((n,), consts.XID_NOTIFICATION, dtype=I32, device=dev),
+            torch.zeros(n, dtype=I32, device=dev),
+            torch.full((n,), -1, dtype=I64, device=dev),
+            torch.full((n,), -1, dtype=I64, device=dev),      # zxid -1
+            self.poff, self.plen, tree.path_arena,
+            torch.full((n,), consts.NOTIFICATION_TYPE['DATA_CHANGED'],
+                       dtype=I32, device=dev),
+            torch.tensor([n], dtype=I64, device=dev))
+        maxpath = int(tree.node_path_len.max().item())
+        self.rec_max = 16 + 4 + 4 + 4 + maxpath + 4
+        self.tx = torch.empty(n * self.rec_max + 64, dtype=U8, device=dev)
+        self.rx = torch.empty(self.world * self.tx.numel(), dtype=U8,
+                              device=dev)
+        self.xt = B.XidTable(bits=10, device=dev)
+        self.reply = B.alloc_replies(self.world * n, dev)
+        self.seeds = torch.empty(self.world, dtype=I64, device=dev)
+        self.seed = seed
+        self.step_no = 0
+        self.last = None
+
+    def _seed(self, rank):
+        return ((rank * 0x9E3779B97F4A7C15 + self.step_no) & (2**64 - 1))
+
+    def _gather(self, total):
+        """All-gather the ranks' encoded streams into ``self.rx``; returns
+        the gathered byte count (contiguous, rank order)."""
+        dist, W, cd = self.dist, self.world, self.coll_device
+        if W == 1:
+            return self.tx, int(total.item())
+        sz = torch.empty(W, dtype=I64, device=cd)
+        dist.all_gather_into_tensor(sz, total.to(cd), group=self.group)
+        sizes = sz.tolist()
+        mx = max(sizes)
+        if cd == self.dev:
+            dist.all_gather_into_tensor(self.rx[:W * mx], self.tx[:mx],
+                                        group=self.group)
+            big = self.rx
+        else:
+            big = torch.empty(W * mx, dtype=U8, device=cd)
+            dist.all_gather_into_tensor(big, self.tx[:mx].to(cd),
+                                        group=self.group)
+        if all(s == mx for s in sizes):
+            if big is not self.rx:
+                self.rx[:W * mx].copy_(big)
+            return self.rx, W * mx
+        # uneven streams: close the gaps (rank order is kept)
+        out = torch.empty(sum(sizes), dtype=U8, device=self.dev)
+        o = 0
+        for r, s in enumerate(sizes):
+            out[o:o + s].copy_(big[r * mx:r * mx + s])
+            o += s
+        self.rx[:o].copy_(out)
+        return self.rx, o
+
+    def step(self, validate=True, acc=None):
+        t = self.tree
+        n = self.n
+        L = _lib.lib()
+        sp = _lib.stream_ptr()
+        seeds = [self._seed(r) for r in range(self.world)]
+        self.step_no += 1
+        _lib.check(L.zk_bench_gen_get(
+            n, seeds[self.rank], t.leaf0, t.n_leaves, 0,
+            _lib.ptr(t.node_path_off), _lib.ptr(t.node_path_len),
+            _lib.ptr(self.idx), _lib.ptr(self.xid), _lib.ptr(self.poff),
+            _lib.ptr(self.plen), sp), 'zk_bench_gen_get')
+        _, _, total, err = B.encode_responses(self.resp, t.store,
+                                              self.tx.numel(), out=self.tx)
+        rx, nrx = self._gather(total)
+        ft = B.frame_scan(rx, nrx, cap=self.world * n)
+        rep = B.decode_replies(rx, ft, self.xt, out=self.reply)
+        self.last = (rep, rx, ft)
+        if not validate:
+            return None
+        if acc is None:
+            acc = torch.zeros(1, dtype=I64, device=self.dev)
+        self.seeds.copy_(torch.tensor(
+            [s - (1 << 64) if s >= (1 << 63) else s for s in seeds],
+            dtype=I64))
+        _lib.check(L.zk_bench_check_notif(
+            self.world * n, n, _lib.ptr(self.seeds), t.leaf0, t.n_leaves,
+            _lib.ptr(t.node_path_off), _lib.ptr(t.node_path_len),
+            _lib.ptr(t.path_arena), _lib.ptr(rx), _lib.ptr(rep.status),
+            _lib.ptr(rep.err), _lib.ptr(rep.opcode), _lib.ptr(rep.aux0),
+            _lib.ptr(rep.aux1), _lib.ptr(rep.pay_off), _lib.ptr(rep.pay_len),
+            _lib.ptr(acc), sp), 'zk_bench_check_notif')
+        return acc
+
+    def diagnose(self):
+        rep, rx, ft = self.last
+        return {'frames': ft.host_result(),
+                'status_bad': int((rep.status != 0).sum().item()),
+                'opcodes': torch.unique(rep.opcode).cpu().tolist()}

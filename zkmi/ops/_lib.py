@@ -100,6 +100,8 @@ _SIGS = {
     'zk_bench_gen_get': (I32, [I64, ctypes.c_uint64, I64, I64, I32, P, P, P,
                                P, P, P, P]),
     'zk_bench_check_get': (I32, [I64, P, P, P, P, P, P, P, P, P, P, P]),
+    'zk_bench_check_notif': (I32, [I64, I64, P, I64, I64, P, P, P, P, P, P,
+                                   P, P, P, P, P, P, P]),
 }
 
 _lib = None

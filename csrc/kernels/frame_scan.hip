@@ -939,27 +939,43 @@ __global__ __launch_bounds__(64) void fs_survivor(
   int32_t m = 0;
   uint16_t fin = 0;
   if constexpr (FE_NSURV == 1) {
-    // one survivor: wave-uniform scalar walk (~25 mostly-SALU instructions
-    // around one LDS round trip per hop); its frame starts are written IN
-    // PLACE over tile bytes already passed (entry k at byte 2k while the
-    // walk is at >= 4k) and copied out once.
+    // one survivor: wave-uniform scalar walk.  The hot loop keeps only what
+    // a clean hop needs (one unsigned length bound, one position bound that
+    // folds "stays in the tile" and "fits the stream"); the hop that ends
+    // the walk is re-classified exactly by fe_hop_len after the loop.  Frame
+    // starts collect in a VGPR (entry k in lane k & 63, a v_cndmask, no exec
+    // branching) and go out 64 at a time, IN PLACE over tile bytes already
+    // passed (entry k at byte 2k while the walk is at >= 4k).
     int32_t c = __builtin_amdgcn_readfirstlane(sv) & 0xFFFF;
     uint16_t* Ls = (uint16_t*)sb;
+    const int32_t lim = min(nrel + 1, (int32_t)FS_S);
+    const uint32_t umax = (uint32_t)maxp32;
+    uint32_t ent = 0;
     for (;;) {
+      uint32_t lo, hi;
+      fe_words(sb, c, lo, hi);
+      const int32_t len = __builtin_amdgcn_readfirstlane(fe_len(lo, hi, c));
+      const int32_t nx = c + 4 + len;
+      if (((uint32_t)len > umax) | (nx >= lim)) break;
+      ent = lane == (m & 63) ? (uint32_t)c : ent;
+      ++m;
+      if ((m & 63) == 0) Ls[m - 64 + lane] = (uint16_t)ent;
+      c = nx;
+    }
+    {
       uint32_t lo, hi;
       fe_words(sb, c, lo, hi);
       const int32_t len = __builtin_amdgcn_readfirstlane(fe_len(lo, hi, c));
       int32_t q = 0;
       const uint16_t code = fe_hop_len(len, c, nrel, maxp32, q);
-      if (code != FE_GO && (code & F0_TERM) && code != F0_ESC) {
-        fin = code;                          // terminal: not a frame start
-        break;
+      if (!((code & F0_TERM) && code != F0_ESC)) {
+        ent = lane == (m & 63) ? (uint32_t)c : ent;   // leaves the tile
+        ++m;
+        if ((m & 63) == 0) Ls[m - 64 + lane] = (uint16_t)ent;
       }
-      if (lane == 0) Ls[m] = (uint16_t)c;
-      ++m;
-      if (code != FE_GO) { fin = code; break; }   // leaves the tile
-      c = q;
+      fin = code;
     }
+    if (lane < (m & 63)) Ls[(m & ~63) + lane] = (uint16_t)ent;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
     uint16_t* L = list + t * FS_LMAX;
@@ -1030,26 +1046,40 @@ __global__ __launch_bounds__(256) void fs_survivor_g(
     int32_t m = 0;
     uint32_t ent = 0;
     uint16_t fin;
+    // fast loop: one unsigned length bound and one position bound (stay in
+    // the tile AND leave room for the next length word); the ending hop is
+    // classified exactly afterwards
+    const int32_t lim = min(nrel - 3, (int32_t)FS_S);
+    const uint32_t umax = (uint32_t)maxp32;
     for (;;) {
-      if (c + 4 > nrel) { fin = (uint16_t)(F0_TERM | c); break; }
-      // the address, not the load, is selected: both loads issue together
-      // (a second dword starting at/after the stream end is never needed)
+      if (c >= lim) break;
+      const int32_t a = c & ~3;
+      const int32_t a2 = (a + 4 < nrel) ? a + 4 : a;
+      const uint32_t w0 = *(const uint32_t*)(tb + a);
+      const uint32_t w1 = *(const uint32_t*)(tb + a2);
+      const int32_t len = __builtin_amdgcn_readfirstlane(fe_len(w0, w1, c));
+      const int32_t nx = c + 4 + len;
+      if (((uint32_t)len > umax) | (nx > nrel) | (nx >= (int32_t)FS_S)) break;
+      ent = lane == (m & 63) ? (uint32_t)c : ent;   // entry m -> lane m&63
+      ++m;
+      if ((m & 63) == 0) L[m - 64 + lane] = (uint16_t)ent;
+      c = nx;
+    }
+    if (c + 4 > nrel) {
+      fin = (uint16_t)(F0_TERM | c);
+    } else {
       const int32_t a = c & ~3;
       const int32_t a2 = (a + 4 < nrel) ? a + 4 : a;
       const uint32_t w0 = *(const uint32_t*)(tb + a);
       const uint32_t w1 = *(const uint32_t*)(tb + a2);
       const int32_t len = __builtin_amdgcn_readfirstlane(fe_len(w0, w1, c));
       int32_t q = 0;
-      const uint16_t code = fe_hop_len(len, c, nrel, maxp32, q);
-      if (code != FE_GO && (code & F0_TERM) && code != F0_ESC) {
-        fin = code;                          // terminal: not a frame start
-        break;
+      fin = fe_hop_len(len, c, nrel, maxp32, q);
+      if (!((fin & F0_TERM) && fin != F0_ESC)) {   // leaves: a frame start
+        ent = lane == (m & 63) ? (uint32_t)c : ent;
+        ++m;
+        if ((m & 63) == 0) L[m - 64 + lane] = (uint16_t)ent;
       }
-      ent = lane == (m & 63) ? (uint32_t)c : ent;   // entry m -> lane m&63
-      ++m;
-      if ((m & 63) == 0) L[m - 64 + lane] = (uint16_t)ent;
-      if (code != FE_GO) { fin = code; break; }    // leaves the tile
-      c = q;
     }
     if (lane < (m & 63)) L[(m & ~63) + lane] = (uint16_t)ent;
     if (lane == 0) rcount[t * FE_NSURV + sl] = m;

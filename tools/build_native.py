@@ -121,14 +121,38 @@ def build_host_sanitized():
     return outs
 
 
+TSAN_DIR = os.path.join(BDIR, 'tsan')
+
+
+def build_loop_tsan():
+    """The native event loop (the only threaded host code) built with
+    ThreadSanitizer.  CPython's GIL is a pthread mutex/condvar pair, which
+    TSan intercepts, so GIL hand-offs count as synchronisation and only
+    genuinely unsynchronised accesses are reported."""
+    os.makedirs(TSAN_DIR, exist_ok=True)
+    suffix = sysconfig.get_config_var('EXT_SUFFIX') or '.so'
+    src = os.path.join(HDIR, HOST_EXTS['_zkloop'])
+    out = os.path.join(TSAN_DIR, '_zkloop' + suffix)
+    if _stale(out, [src]):
+        inc = sysconfig.get_paths()['include']
+        _run(['g++', '-O1', '-g', '-fPIC', '-shared', '-std=c++17', '-Wall',
+              '-fsanitize=thread', '-I' + inc, src, '-o', out])
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--hip-only', action='store_true')
     ap.add_argument('--host-only', action='store_true')
     ap.add_argument('--sanitize', action='store_true',
                     help='build only the ASan/UBSan host codec')
+    ap.add_argument('--tsan', action='store_true',
+                    help='build only the ThreadSanitizer event loop')
     ap.add_argument('-j', type=int, default=4)
     a = ap.parse_args()
+    if a.tsan:
+        print(build_loop_tsan())
+        return
     if a.sanitize:
         print(' '.join(build_host_sanitized()))
         return

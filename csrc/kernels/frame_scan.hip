@@ -54,6 +54,7 @@ struct FsCtx {
   const uint8_t* buf;
   int64_t n;
   int64_t maxp;
+  int64_t W;                       // window: entry points per unit (<= FS_W)
   int levels;                      // number of levels (>= 1)
   int64_t usize[FS_MAXL];          // unit size in bytes per level
   int64_t units[FS_MAXL];          // unit count per level
@@ -101,8 +102,8 @@ ZK_DEV int64_t apply_unit(const FsCtx& c, int64_t u, int64_t P) {
   const int64_t ue = min(us + c.usize[L], c.n);
   const int64_t off = P - us;
   if constexpr (L == 0) {
-    if (off < FS_W) {
-      const uint16_t v = c.f0[u * FS_W + off];
+    if (off < c.W) {
+      const uint16_t v = c.f0[u * c.W + off];
       if (v == F0_ESC) return RES ? walk_until(c, P, ue) : (LATE | P);
       if (v & F0_TERM) return TERM | (us + (v & 0x7FFF));
       const int64_t x = us + FS_S + v;
@@ -110,8 +111,8 @@ ZK_DEV int64_t apply_unit(const FsCtx& c, int64_t u, int64_t P) {
     }
     return RES ? walk_until(c, P, ue) : (LATE | P);
   } else {
-    if (off < FS_W) {
-      const int64_t v = c.fl[L][u * FS_W + off];
+    if (off < c.W) {
+      const int64_t v = c.fl[L][u * c.W + off];
       if (!RES || !is_late(v)) return v;
       P = pos_of(v);                      // resume the true chain here
     } else if (!RES) {
@@ -333,9 +334,11 @@ __global__ __launch_bounds__(FS_T) void fs_exits(const uint8_t* __restrict__ buf
 // (owner word and next length read together), no block barriers.  The walk
 // is bounded: each hop claims a fresh position, so <= S hops in total.
 constexpr int FE_T = 256;
-constexpr int FE_K = FS_W / FE_T;            // walkers per thread (8)
+// LDS of fs_frontier<W>: staged tile, owner table, W results, hand-off area
+inline size_t fe_lds(int W) {
+  return (FS_S + 16) + FS_S * 2 + (size_t)W * 2 + 66 * 4;
+}
 constexpr uint16_t F0_MERGE = 0x4000;        // | parent walker id (< 2048)
-constexpr size_t FE_LDS = (FS_S + 16) + FS_S * 2 + FS_W * 2 + 66 * 4;
 
 ZK_DEV bool f0_is_merge(uint16_t v) { return (v & 0xF800) == F0_MERGE; }
 
@@ -409,14 +412,17 @@ ZK_DEV void fe_words(const uint8_t* sb, int32_t p, uint32_t& lo, uint32_t& hi) {
 // then resolved (entries rooted at the survivor become FE_PENDING).
 // (A wave-per-tile variant without barriers was slower: 53 KiB of LDS per
 // tile leaves 3 waves per CU, too few to hide the LDS latency chains.)
+template <int W>
 __global__ __launch_bounds__(FE_T) void fs_frontier(
     const uint8_t* __restrict__ buf, int64_t n, int64_t maxp,
     uint16_t* __restrict__ f0, int32_t* __restrict__ surv) {
+  constexpr int FE_K = W / FE_T;             // walkers per thread (1..8)
+  static_assert(W % FE_T == 0 && FE_K >= 1 && FE_K <= 8, "window");
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint8_t* sb = smem;                                      // [S + 16]
   uint16_t* own = (uint16_t*)(smem + FS_S + 16);           // [S] id+1 / 0
   uint16_t* res = own + FS_S;                              // [W]
-  uint32_t* hand = (uint32_t*)(res + FS_W);                // [64] + 2 ctrs
+  uint32_t* hand = (uint32_t*)(res + W);                   // [64] + 2 ctrs
   const int64_t t = blockIdx.x;
   FE_MARK(0);
   const int64_t ts = t * FS_S;
@@ -599,7 +605,7 @@ __global__ __launch_bounds__(FE_T) void fs_frontier(
       for (int k = 0; k < FE_K; ++k) res[threadIdx.x + k * FE_T] = v[k];
       if (!any) break;
     }
-    uint16_t* out = f0 + t * FS_W;
+    uint16_t* out = f0 + t * W;
 #pragma unroll
     for (int k = 0; k < FE_K; ++k) out[threadIdx.x + k * FE_T] = v[k];
   }
@@ -611,14 +617,14 @@ __global__ __launch_bounds__(FS_T) void fs_compose(FsCtx c, int l) {
   const int64_t u = blockIdx.x;
   const int64_t us = u * c.usize[l + 1];
   const int64_t ue = min(us + c.usize[l + 1], c.n);
-  for (int64_t p = threadIdx.x; p < FS_W; p += blockDim.x) {
+  for (int64_t p = threadIdx.x; p < c.W; p += blockDim.x) {
     int64_t P = us + p;
     if (P >= c.n) P = TERM | c.n;
     while (!is_term(P) && P < ue) {
       const int64_t sub = P / c.usize[l];
       P = apply_level<false>(c, l, sub, P);
     }
-    c.fl[l + 1][u * FS_W + p] = P;
+    c.fl[l + 1][u * c.W + p] = P;
   }
 }
 
@@ -894,10 +900,10 @@ __global__ __launch_bounds__(256) void fs_write_list(
 // rcount[t*2+s].
 
 // Replace fe_pending(slot) in the tile's f0 row by the slot's final code.
-ZK_DEV void fe_patch_row(uint16_t* row, int lane, const uint16_t fin[FE_NSURV]) {
-#pragma unroll
-  for (int j = 0; j < FS_W * 2 / 16 / 64; ++j) {
-    uint4 v = ((const uint4*)row)[lane + 64 * j];
+ZK_DEV void fe_patch_row(uint16_t* row, int W, int lane,
+                         const uint16_t fin[FE_NSURV]) {
+  for (int j = lane; j < W / 8; j += 64) {
+    uint4 v = ((const uint4*)row)[j];
     uint16_t* h = (uint16_t*)&v;
     bool any = false;
 #pragma unroll
@@ -906,7 +912,7 @@ ZK_DEV void fe_patch_row(uint16_t* row, int lane, const uint16_t fin[FE_NSURV]) 
       for (int sl = 0; sl < FE_NSURV; ++sl)
         if (h[k] == fe_pending(sl)) { h[k] = fin[sl]; any = true; }
     }
-    if (any) ((uint4*)row)[lane + 64 * j] = v;
+    if (any) ((uint4*)row)[j] = v;
   }
 }
 
@@ -918,7 +924,7 @@ ZK_DEV void fe_patch_row(uint16_t* row, int lane, const uint16_t fin[FE_NSURV]) 
 constexpr size_t FV_LDS = FS_S + 16;
 
 __global__ __launch_bounds__(64) void fs_survivor(
-    const uint8_t* __restrict__ buf, int64_t n, int64_t maxp,
+    const uint8_t* __restrict__ buf, int64_t n, int64_t maxp, int32_t W,
     uint16_t* __restrict__ f0, const int32_t* __restrict__ surv,
     uint16_t* __restrict__ list, int32_t* __restrict__ rcount) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -1007,7 +1013,7 @@ __global__ __launch_bounds__(64) void fs_survivor(
 #pragma unroll
   for (int sl = 0; sl < FE_NSURV; ++sl)
     fins[sl] = (uint16_t)__builtin_amdgcn_readlane((int)fin, sl);
-  fe_patch_row(f0 + t * FS_W, lane, fins);
+  fe_patch_row(f0 + t * W, W, lane, fins);
 }
 
 // A2' fs_survivor_g: the same walks straight from global memory, no LDS.  A
@@ -1019,7 +1025,7 @@ __global__ __launch_bounds__(64) void fs_survivor(
 // one v_cndmask) and leave in one coalesced store per 64 hops.  4 tiles
 // (waves) per block.
 __global__ __launch_bounds__(256) void fs_survivor_g(
-    const uint8_t* __restrict__ buf, int64_t n, int64_t maxp, int64_t tiles,
+    const uint8_t* __restrict__ buf, int64_t n, int64_t maxp, int32_t W, int64_t tiles,
     uint16_t* __restrict__ f0, const int32_t* __restrict__ surv,
     uint16_t* __restrict__ list, int32_t* __restrict__ rcount) {
   const int lane = threadIdx.x & 63;
@@ -1085,7 +1091,7 @@ __global__ __launch_bounds__(256) void fs_survivor_g(
     if (lane == 0) rcount[t * FE_NSURV + sl] = m;
     fins[sl] = fin;
   }
-  if (any_sv) fe_patch_row(f0 + t * FS_W, lane, fins);
+  if (any_sv) fe_patch_row(f0 + t * W, W, lane, fins);
 }
 
 // D'' fs_join: the tile's frame starts from its exact entry e*.  Every chain
@@ -1183,7 +1189,7 @@ struct FsPlan {
       total;
 };
 
-static FsPlan fs_plan(int64_t n) {
+static FsPlan fs_plan(int64_t n, int64_t W) {
   FsPlan p{};
   const int64_t tiles = n > 0 ? (n + FS_S - 1) / FS_S : 1;
   p.units[0] = tiles;
@@ -1197,9 +1203,9 @@ static FsPlan fs_plan(int64_t n) {
   }
   size_t o = 0;
   auto take = [&](size_t bytes) { size_t r = o; o += (bytes + 255) & ~(size_t)255; return r; };
-  p.off_f0 = take((size_t)tiles * FS_W * 2);
+  p.off_f0 = take((size_t)tiles * W * 2);
   for (int l = 1; l < p.levels; ++l)
-    p.off_fl[l] = take((size_t)p.units[l] * FS_W * 8);
+    p.off_fl[l] = take((size_t)p.units[l] * W * 8);
   for (int l = 0; l < p.levels; ++l) p.off_ent[l] = take((size_t)p.units[l] * 8);
   p.off_bits = take((size_t)tiles * (FS_S / 32) * 4);
   p.off_cnt = take((size_t)tiles * 8);
@@ -1218,16 +1224,29 @@ static FsPlan fs_plan(int64_t n) {
 
 extern "C" {
 
-int64_t zk_frame_scan_workspace(int64_t n) { return (int64_t)zk::fs_plan(n).total; }
+// Sized for the largest window (FS_W), an upper bound for any window.
+int64_t zk_frame_scan_workspace(int64_t n) {
+  return (int64_t)zk::fs_plan(n, zk::FS_W).total;
+}
 
 // result (device int64[4]): [0] frames written, [1] stop offset (consumed
 // bytes; start of the carry or of the bad frame), [2] 1 if the stop is a
 // BAD_LENGTH frame, [3] 1 if the frame table overflowed `cap`.
-int zk_frame_scan(const uint8_t* buf, int64_t n, int64_t maxp, uint8_t* ws,
-                  int64_t ws_bytes, int64_t* foff, int32_t* flen, int64_t cap,
-                  int64_t* result, hipStream_t st) {
+//
+// `window` (256 / 512 / 1024 / 2048 bytes) is the fast-path entry window per
+// 16 KiB tile: a chain can only enter a tile inside it when frames are <=
+// window bytes, so the frontier walks `window` speculative entry points per
+// tile and the composition tables hold `window` entries per unit.  Frames
+// longer than the window stay exact (walked in global memory for the tiles
+// they land in), so the window is a performance hint: the smallest one
+// covering the stream's usual frame size makes the scan cheapest.
+int zk_frame_scan2(const uint8_t* buf, int64_t n, int64_t maxp, uint8_t* ws,
+                   int64_t ws_bytes, int64_t* foff, int32_t* flen, int64_t cap,
+                   int64_t* result, int32_t window, hipStream_t st) {
   using namespace zk;
-  FsPlan p = fs_plan(n);
+  const int W = window <= 256 ? 256 : window <= 512 ? 512
+              : window <= 1024 ? 1024 : (int)FS_W;
+  FsPlan p = fs_plan(n, W);
   if ((int64_t)p.total > ws_bytes) return -1;
   hipMemsetAsync(result, 0, 4 * sizeof(int64_t), st);
   if (n <= 0) return 0;
@@ -1235,6 +1254,7 @@ int zk_frame_scan(const uint8_t* buf, int64_t n, int64_t maxp, uint8_t* ws,
   c.buf = buf;
   c.n = n;
   c.maxp = maxp;
+  c.W = W;
   c.levels = p.levels;
   for (int l = 0; l < p.levels; ++l) {
     c.units[l] = p.units[l];
@@ -1251,6 +1271,7 @@ int zk_frame_scan(const uint8_t* buf, int64_t n, int64_t maxp, uint8_t* ws,
     const char* m = getenv("ZKMI_FS_SCAN");
     mode = !m ? 0 : (m[0] == 'j' ? 1 : (m[0] == 'd' ? 2 : 0));
   }
+  if (mode != 0 && W != FS_W) return -2;       // A/B paths: full window only
   uint16_t* f0w = (uint16_t*)(ws + p.off_f0);
   uint32_t* bits = (uint32_t*)(ws + p.off_bits);
   int64_t* cnt = (int64_t*)(ws + p.off_cnt);
@@ -1261,8 +1282,23 @@ int zk_frame_scan(const uint8_t* buf, int64_t n, int64_t maxp, uint8_t* ws,
   int32_t* rcnt = (int32_t*)(ws + p.off_rcnt);
   int32_t* npre = (int32_t*)(ws + p.off_npre);
   if (mode == 0) {
-    fs_frontier<<<(unsigned)tiles, FE_T, FE_LDS, st>>>(buf, n, maxp, f0w,
-                                                      surv);
+    switch (W) {
+      case 256:
+        fs_frontier<256><<<(unsigned)tiles, FE_T, fe_lds(256), st>>>(
+            buf, n, maxp, f0w, surv);
+        break;
+      case 512:
+        fs_frontier<512><<<(unsigned)tiles, FE_T, fe_lds(512), st>>>(
+            buf, n, maxp, f0w, surv);
+        break;
+      case 1024:
+        fs_frontier<1024><<<(unsigned)tiles, FE_T, fe_lds(1024), st>>>(
+            buf, n, maxp, f0w, surv);
+        break;
+      default:
+        fs_frontier<(int)FS_W><<<(unsigned)tiles, FE_T, fe_lds((int)FS_W),
+                                 st>>>(buf, n, maxp, f0w, surv);
+    }
     ZK_LAUNCH_CHECK();
     // Survivor walk: LDS-staged (one LDS round trip per hop, but the 16 KiB
     // tile caps a CU at 9 walks) when every tile can walk at once, global
@@ -1276,18 +1312,18 @@ int zk_frame_scan(const uint8_t* buf, int64_t n, int64_t maxp, uint8_t* ws,
     const int64_t lds_slots = 9LL * 256;
     const int sv_mode = sv_force ? sv_force : (tiles <= 2 * lds_slots ? 1 : 2);
     if (sv_mode == 1)
-      fs_survivor<<<(unsigned)tiles, 64, FV_LDS, st>>>(buf, n, maxp, f0w,
+      fs_survivor<<<(unsigned)tiles, 64, FV_LDS, st>>>(buf, n, maxp, W, f0w,
                                                       surv, list, rcnt);
     else
       fs_survivor_g<<<(unsigned)((tiles + 3) / 4), 256, 0, st>>>(
-          buf, n, maxp, tiles, f0w, surv, list, rcnt);
+          buf, n, maxp, W, tiles, f0w, surv, list, rcnt);
   } else {
     const size_t lds_a = FS_S * 2 + FS_LIST * 2 + (FS_T / 64 + 1) * 8;
     fs_exits<<<(unsigned)tiles, FS_T, lds_a, st>>>(buf, n, maxp, f0w);
   }
   ZK_LAUNCH_CHECK();
   for (int l = 0; l + 1 < p.levels; ++l) {
-    fs_compose<<<(unsigned)p.units[l + 1], FS_T, 0, st>>>(c, l);
+    fs_compose<<<(unsigned)p.units[l + 1], min(W, FS_T), 0, st>>>(c, l);
     ZK_LAUNCH_CHECK();
   }
   fs_top<<<1, 64, 0, st>>>(c, result);
@@ -1325,6 +1361,13 @@ int zk_frame_scan(const uint8_t* buf, int64_t n, int64_t maxp, uint8_t* ws,
   }
   ZK_LAUNCH_CHECK();
   return 0;
+}
+
+int zk_frame_scan(const uint8_t* buf, int64_t n, int64_t maxp, uint8_t* ws,
+                  int64_t ws_bytes, int64_t* foff, int32_t* flen, int64_t cap,
+                  int64_t* result, hipStream_t st) {
+  return zk_frame_scan2(buf, n, maxp, ws, ws_bytes, foff, flen, cap, result,
+                        (int32_t)zk::FS_W, st);
 }
 
 }  // extern "C"

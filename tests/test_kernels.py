@@ -72,9 +72,15 @@ def _frames_stream(r, n, maxbody):
     return b''.join(parts)
 
 
+# K1 entry windows: frames longer than the window take the slow path and
+# must stay exact (the 600 / 5000 / 40000-byte cases at window 256)
+WINDOWS = [256, 1024, 2048]
+
+
+@pytest.mark.parametrize('window', WINDOWS)
 @pytest.mark.parametrize('maxbody,n', [(64, 3000), (600, 800), (5000, 120),
                                        (40000, 12)])
-def test_frame_scan_matches_oracle(gpu, maxbody, n):
+def test_frame_scan_matches_oracle(gpu, maxbody, n, window):
     from zkmi.ops import batch as B
     r = synth.rng(maxbody)
     s = _frames_stream(r, n, maxbody)
@@ -83,7 +89,7 @@ def test_frame_scan_matches_oracle(gpu, maxbody, n):
     s = s + tail
     frames, consumed, bad = jute.scan_frames(s)
     buf = _dev_bytes(s, gpu)
-    ft = B.frame_scan(buf, len(s))
+    ft = B.frame_scan(buf, len(s), window=window)
     res = ft.host_result()
     assert res['frames'] == len(frames)
     assert res['consumed'] == consumed == len(s) - len(tail)
@@ -93,7 +99,8 @@ def test_frame_scan_matches_oracle(gpu, maxbody, n):
     assert list(zip(off, ln)) == frames
 
 
-def test_frame_scan_bad_length_exact(gpu):
+@pytest.mark.parametrize('window', WINDOWS)
+def test_frame_scan_bad_length_exact(gpu, window):
     from zkmi.ops import batch as B
     r = synth.rng(7)
     good = _frames_stream(r, 500, 300)
@@ -101,25 +108,26 @@ def test_frame_scan_bad_length_exact(gpu):
     s = good + bad + _frames_stream(r, 50, 30)
     frames, consumed, bad_at = jute.scan_frames(s)
     assert bad_at == len(good)
-    ft = B.frame_scan(_dev_bytes(s, gpu), len(s))
+    ft = B.frame_scan(_dev_bytes(s, gpu), len(s), window=window)
     res = ft.host_result()
     assert res['bad'] and res['consumed'] == len(good)
     assert res['frames'] == len(frames)
     # too-large length
     s2 = good + b'\x7f\x00\x00\x00' + b'\0' * 100
-    ft2 = B.frame_scan(_dev_bytes(s2, gpu), len(s2))
+    ft2 = B.frame_scan(_dev_bytes(s2, gpu), len(s2), window=window)
     res2 = ft2.host_result()
     assert res2['bad'] and res2['consumed'] == len(good)
 
 
-def test_frame_scan_large_multi_level(gpu):
+@pytest.mark.parametrize('window', [256, 2048])
+def test_frame_scan_large_multi_level(gpu, window):
     """> 256 tiles forces the hierarchical composition path."""
     from zkmi.ops import batch as B
     r = synth.rng(3)
     bodies = [bytes([i & 0xff]) * r.randint(16, 400) for i in range(40000)]
     s = b''.join(jute.frame(b) for b in bodies)
     assert len(s) > 256 * 16384
-    ft = B.frame_scan(_dev_bytes(s, gpu), len(s))
+    ft = B.frame_scan(_dev_bytes(s, gpu), len(s), window=window)
     res = ft.host_result()
     assert res['frames'] == len(bodies)
     assert res['consumed'] == len(s)

@@ -63,9 +63,9 @@ int main(int argc, char** argv) {
     CK(hipMemcpyToSymbol(HIP_SYMBOL(zk::g_fe_prof), &prof, sizeof(prof)));
     hipEvent_t a, b; CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
     for (int i = 0; i < 2; ++i)
-      zk::fs_frontier<<<(unsigned)tiles, zk::FE_T, zk::FE_LDS>>>(d, n, 16 << 20, f0, surv);
+      zk::fs_frontier<(int)zk::FS_W><<<(unsigned)tiles, zk::FE_T, zk::fe_lds((int)zk::FS_W)>>>(d, n, 16 << 20, f0, surv);
     CK(hipEventRecord(a));
-    zk::fs_frontier<<<(unsigned)tiles, zk::FE_T, zk::FE_LDS>>>(d, n, 16 << 20, f0, surv);
+    zk::fs_frontier<(int)zk::FS_W><<<(unsigned)tiles, zk::FE_T, zk::fe_lds((int)zk::FS_W)>>>(d, n, 16 << 20, f0, surv);
     CK(hipEventRecord(b)); CK(hipEventSynchronize(b));
     float ms; CK(hipEventElapsedTime(&ms, a, b));
     std::vector<uint64_t> p(tiles * 8);
@@ -90,11 +90,12 @@ int main(int argc, char** argv) {
       for (int i = 0; i < 3; ++i) {
         if (i == 2) CK(hipEventRecord(a));
         if (v == 0)
-          zk::fs_survivor<<<(unsigned)tiles, 64, zk::FV_LDS>>>(d, n, 16 << 20, f0, surv,
-                                                              list, rc);
+          zk::fs_survivor<<<(unsigned)tiles, 64, zk::FV_LDS>>>(d, n, 16 << 20,
+                                                              (int)zk::FS_W, f0,
+                                                              surv, list, rc);
         else
-          zk::fs_survivor_g<<<(unsigned)((tiles + 3) / 4), 256, 0>>>(d, n, 16 << 20, tiles,
-                                                                    f0, surv, list, rc);
+          zk::fs_survivor_g<<<(unsigned)((tiles + 3) / 4), 256, 0>>>(
+              d, n, 16 << 20, (int)zk::FS_W, tiles, f0, surv, list, rc);
       }
       CK(hipEventRecord(b)); CK(hipEventSynchronize(b));
       CK(hipEventElapsedTime(&ms, a, b));

@@ -204,8 +204,9 @@ class GpuServer(object):
     """Server half of the pipeline: frame-scan + decode requests, apply them
     to a :class:`GpuTree`, encode replies."""
 
-    def __init__(self, tree, cap_frames, out_cap):
+    def __init__(self, tree, cap_frames, out_cap, window=2048):
         self.tree = tree
+        self.window = window              # K1 entry window of the requests
         dev = tree.device
         self.rt = B.alloc_request_table(cap_frames, dev)
         # CREATE replies carry the created path from the tree's arena
@@ -228,7 +229,8 @@ class GpuServer(object):
         """Serve the request stream ``rx[:n]`` for ``session`` (the owner of
         any EPHEMERAL node it creates)."""
         L = _lib.lib()
-        ft = B.frame_scan(rx, n, cap=self.cap_frames, workspace=self.ws)
+        ft = B.frame_scan(rx, n, cap=self.cap_frames, workspace=self.ws,
+                          window=self.window)
         rt = B.decode_requests(rx, ft, out=self.rt)
         r = self.resp
         r.count = ft.count
@@ -268,7 +270,10 @@ class GetPipeline(object):
         maxpath = int(tree.node_path_len.max().item())
         self.tx = torch.empty(n * (17 + maxpath) + 64, dtype=U8, device=dev)
         dmax = max(tree.data_bytes, 128)
-        self.server = GpuServer(tree, n, n * (4 + 16 + 4 + dmax + 68) + 64)
+        # K1 windows: the largest request / reply frame of this workload
+        self.server = GpuServer(tree, n, n * (4 + 16 + 4 + dmax + 68) + 64,
+                                window=B.frame_window(17 + maxpath))
+        self.rwindow = B.frame_window(4 + 16 + 4 + dmax + 68)
         self.reply = B.alloc_replies(n, dev)
         self.xid_base = 0
         self.last = None
@@ -305,7 +310,7 @@ class GetPipeline(object):
         ntx = int(total.item())
         rx, rtotal, rerr, _ = self.server.serve(tx, ntx)
         nrx = int(rtotal.item())
-        ft = B.frame_scan(rx, nrx, cap=n)
+        ft = B.frame_scan(rx, nrx, cap=n, window=self.rwindow)
         rep = B.decode_replies(rx, ft, self.xt, out=self.reply)
         self.last = (self.idx, rep, rx, ft)
         if not validate:
@@ -367,9 +372,13 @@ class _Driver(object):
         self.tx = torch.empty(batch * (33 + max_path + data_bytes + 128) + 64,
                               dtype=U8, device=dev)
         dmax = max(tree.data_bytes, 128, data_bytes)
+        # K1 windows from the largest frames (CREATE with data and a
+        # two-entry ACL; a GET_DATA-sized reply)
         self.server = GpuServer(
             tree, batch, batch * (4 + 16 + 4 + max(dmax, max_path + 16) + 68)
-            + 64)
+            + 64, window=B.frame_window(33 + max_path + data_bytes + 128))
+        self.rwindow = B.frame_window(4 + 16 + 4 + max(dmax, max_path + 16)
+                                      + 68)
         self.reply = B.alloc_replies(batch, dev)
         self.xid_base = 0
         self.iota = torch.arange(batch, dtype=I32, device=dev)
@@ -407,7 +416,7 @@ class _Driver(object):
         ntx = int(total.item())
         rx, rtotal, _, _ = self.server.serve(tx, ntx, session=session)
         nrx = int(rtotal.item())
-        ft = B.frame_scan(rx, nrx, cap=self.batch)
+        ft = B.frame_scan(rx, nrx, cap=self.batch, window=self.rwindow)
         rep = B.decode_replies(rx, ft, self.xt, out=self.reply)
         return rep, rx
 
@@ -701,7 +710,8 @@ class WatchPipeline(object):
         _, _, total, err = B.encode_responses(self.resp, t.store,
                                               self.tx.numel(), out=self.tx)
         rx, nrx = self._gather(total)
-        ft = B.frame_scan(rx, nrx, cap=self.world * n)
+        ft = B.frame_scan(rx, nrx, cap=self.world * n,
+                          window=B.frame_window(self.rec_max))
         rep = B.decode_replies(rx, ft, self.xt, out=self.reply)
         self.last = (rep, rx, ft)
         if not validate:

@@ -294,12 +294,27 @@ class FrameTable:
                 'overflow': bool(r[3])}
 
 
+FS_WINDOWS = (256, 512, 1024, 2048)
+
+
+def frame_window(max_frame):
+    """The smallest K1 entry window covering frames of ``max_frame`` bytes
+    (length prefix included); larger frames stay exact, only slower."""
+    for w in FS_WINDOWS:
+        if max_frame <= w:
+            return w
+    return FS_WINDOWS[-1]
+
+
 def frame_scan(buf, n=None, max_packet=consts.MAX_PACKET, cap=None,
-               stream=None, workspace=None):
+               stream=None, workspace=None, window=2048):
     """K1: split ``buf[:n]`` (uint8 device tensor) into frames.
 
     ``cap`` bounds the frame table (default: ``n // 4``, the most frames a
-    stream of ``n`` bytes can hold)."""
+    stream of ``n`` bytes can hold).  ``window`` is the per-tile fast-path
+    entry window (256..2048 bytes, see :func:`frame_window`): a hint for
+    the usual frame size, never a limit — longer frames are framed exactly
+    on a slower path."""
     L = _lib.lib()
     if n is None:
         n = buf.numel()
@@ -312,9 +327,10 @@ def frame_scan(buf, n=None, max_packet=consts.MAX_PACKET, cap=None,
     off = torch.empty(cap, dtype=I64, device=dev)
     ln = torch.empty(cap, dtype=I32, device=dev)
     res = torch.zeros(4, dtype=I64, device=dev)
-    check(L.zk_frame_scan(ptr(buf), n, max_packet, ptr(workspace),
-                          workspace.numel(), ptr(off), ptr(ln), cap,
-                          ptr(res), stream_ptr(stream)), 'zk_frame_scan')
+    check(L.zk_frame_scan2(ptr(buf), n, max_packet, ptr(workspace),
+                           workspace.numel(), ptr(off), ptr(ln), cap,
+                           ptr(res), int(window), stream_ptr(stream)),
+          'zk_frame_scan')
     return FrameTable(off, ln, res)
 
 

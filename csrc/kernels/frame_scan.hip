@@ -16,9 +16,11 @@
 //                chain position outside the tile or to a terminal.
 //  B  fs_compose hierarchical function composition: a level-(l+1) unit is 16
 //                level-l units; for each window entry point, walk the 16
-//                sub-unit functions.  Log-depth, O(W) work per unit.
+//                sub-unit functions.  Log-depth, O(W) work per unit.  The 16
+//                child tables are staged in LDS first (fs_compose_staged).
 //  C  fs_top/fs_down  serial walk over the (few) top units from the stream
-//                start, then push the exact entry position down to every tile.
+//                start, then push the exact entry position down to every tile
+//                (fs_down_staged: one wave per parent, children in LDS).
 //  D  frame starts per tile from its exact entry: fs_join (default: walk from
 //     the entry to the survivor's hand-off point, then reuse the survivor's
 //     recorded path), fs_walk (jump: wave-uniform walk of the staged tile) or
@@ -625,6 +627,98 @@ __global__ __launch_bounds__(FS_T) void fs_compose(FsCtx c, int l) {
       P = apply_level<false>(c, l, sub, P);
     }
     c.fl[l + 1][u * c.W + p] = P;
+  }
+}
+
+// Staged composition / push-down: a parent's FS_G child tables are pulled
+// into LDS in one parallel burst, so the dependent chain of child lookups
+// runs at LDS latency instead of one global round trip per child (these
+// chains were the whole cost of fs_compose / fs_down).  Level-0 rows are the
+// uint16 f0 codes, higher levels the int64 fl positions; a level whose rows
+// do not fit FS_STAGE_MAX uses the global kernels above.
+constexpr size_t FS_STAGE_MAX = 64 * 1024;
+
+inline size_t fs_stage_bytes(int l, int64_t W) {
+  return (size_t)FS_G * (size_t)W * (l == 0 ? 2 : 8);
+}
+
+template <bool RES>
+ZK_DEV int64_t apply_staged(const FsCtx& c, int l, int64_t s, int64_t P,
+                            const uint16_t* t16, const int64_t* t64) {
+  if (is_term(P) || is_late(P)) return P;
+  if (P >= c.n) return TERM | c.n;
+  const int64_t us = s * c.usize[l];
+  const int64_t off = P - us;
+  if (off >= c.W) return RES ? apply_level<true>(c, l, s, P) : (LATE | P);
+  if (l == 0) {
+    const uint16_t v = t16[off];
+    if (v == F0_ESC) return RES ? apply_level<true>(c, 0, s, P) : (LATE | P);
+    if (v & F0_TERM) return TERM | (us + (v & 0x7FFF));
+    const int64_t x = us + FS_S + v;
+    return x >= c.n ? (TERM | c.n) : x;
+  }
+  const int64_t v = t64[off];
+  if (!RES || !is_late(v)) return v;
+  return apply_level<true>(c, l, s, P);    // LATE: resolve via global tables
+}
+
+// Pull the child rows [s0, s1) of level l into LDS (zero rows past s1).
+ZK_DEV void stage_children(const FsCtx& c, int l, int64_t s0, int64_t s1,
+                           uint8_t* lds) {
+  const int64_t W = c.W;
+  const int64_t es = l == 0 ? 2 : 8;
+  const int64_t nvec = (s1 - s0) * W * es / 16;
+  const uint4* src = l == 0 ? (const uint4*)(c.f0 + s0 * W)
+                            : (const uint4*)(c.fl[l] + s0 * W);
+  for (int64_t k = threadIdx.x; k < nvec; k += blockDim.x)
+    ((uint4*)lds)[k] = src[k];
+}
+
+__global__ __launch_bounds__(FS_T) void fs_compose_staged(FsCtx c, int l) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int64_t u = blockIdx.x;
+  const int64_t us = u * c.usize[l + 1];
+  const int64_t ue = min(us + c.usize[l + 1], c.n);
+  const int64_t s0 = u * FS_G;
+  const int64_t s1 = min(s0 + FS_G, c.units[l]);
+  stage_children(c, l, s0, s1, lds);
+  __syncthreads();
+  const uint16_t* t16 = (const uint16_t*)lds;
+  const int64_t* t64 = (const int64_t*)lds;
+  for (int64_t p = threadIdx.x; p < c.W; p += blockDim.x) {
+    int64_t P = us + p;
+    if (P >= c.n) P = TERM | c.n;
+    while (!is_term(P) && P < ue) {
+      const int64_t sub = P / c.usize[l];
+      const int64_t r = (sub - s0) * c.W;
+      P = apply_staged<false>(c, l, sub, P, t16 + r, t64 + r);
+    }
+    c.fl[l + 1][u * c.W + p] = P;
+  }
+}
+
+// One wave per parent: stage its children, lane 0 walks them.
+__global__ __launch_bounds__(64) void fs_down_staged(FsCtx c, int l) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int64_t u = blockIdx.x;
+  const int64_t s0 = u * FS_G;
+  const int64_t s1 = min(s0 + FS_G, c.units[l]);
+  stage_children(c, l, s0, s1, lds);
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  const uint16_t* t16 = (const uint16_t*)lds;
+  const int64_t* t64 = (const int64_t*)lds;
+  int64_t P = c.ent[l + 1][u];
+  for (int64_t s = s0; s < s1; ++s) {
+    const int64_t ss = s * c.usize[l];
+    const int64_t se = min(ss + c.usize[l], c.n);
+    if (P != NONE && !is_term(P) && P >= ss && P < se) {
+      c.ent[l][s] = P;
+      const int64_t r = (s - s0) * c.W;
+      P = apply_staged<true>(c, l, s, P, t16 + r, t64 + r);
+    } else {
+      c.ent[l][s] = NONE;
+    }
   }
 }
 
@@ -1323,14 +1417,23 @@ int zk_frame_scan2(const uint8_t* buf, int64_t n, int64_t maxp, uint8_t* ws,
   }
   ZK_LAUNCH_CHECK();
   for (int l = 0; l + 1 < p.levels; ++l) {
-    fs_compose<<<(unsigned)p.units[l + 1], min(W, FS_T), 0, st>>>(c, l);
+    const size_t sb = fs_stage_bytes(l, W);
+    if (sb <= FS_STAGE_MAX)
+      fs_compose_staged<<<(unsigned)p.units[l + 1], min(W, FS_T), sb, st>>>(
+          c, l);
+    else
+      fs_compose<<<(unsigned)p.units[l + 1], min(W, FS_T), 0, st>>>(c, l);
     ZK_LAUNCH_CHECK();
   }
   fs_top<<<1, 64, 0, st>>>(c, result);
   ZK_LAUNCH_CHECK();
   for (int l = p.levels - 2; l >= 0; --l) {
     const int64_t np = p.units[l + 1];
-    fs_down<<<(unsigned)((np + 255) / 256), 256, 0, st>>>(c, l);
+    const size_t sb = fs_stage_bytes(l, W);
+    if (sb <= FS_STAGE_MAX)
+      fs_down_staged<<<(unsigned)np, 64, sb, st>>>(c, l);
+    else
+      fs_down<<<(unsigned)((np + 255) / 256), 256, 0, st>>>(c, l);
     ZK_LAUNCH_CHECK();
   }
   const unsigned wblocks = (unsigned)((tiles + 3) / 4);

@@ -410,6 +410,9 @@ class _ServerConn(object):
         s = self.db.sessions.get(self.sid) if self.sid is not None else None
         if s is not None and s.conn is self:
             s.conn = None
+            # ZooKeeper keeps watches on the connection (ServerCnxn): they
+            # die with it and the client re-registers them with SET_WATCHES.
+            self.db._drop_watches(s.sid)
 
     def close_from_server(self):
         if not self.closed:
@@ -472,6 +475,7 @@ class _ServerConn(object):
             # A session moving to this connection drops its old one.
             if s.conn is not None and s.conn is not self:
                 s.conn.close_from_server()
+            self.db._drop_watches(s.sid)
             s.last_seen = db._mono()
         s.conn = self
         self.sid = s.sid

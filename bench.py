@@ -87,6 +87,9 @@ def main():
     ap.add_argument('--nodes', type=int, default=1_000_000)
     ap.add_argument('--data-bytes', type=int, default=100)
     ap.add_argument('--no-rtt', action='store_true')
+    ap.add_argument('--streams', type=int, default=1,
+                    help='get: pipelined connections per GPU, one HIP '
+                         'stream each (the batch is split between them)')
     ap.add_argument('--workload', choices=('get', 'mix', 'storm', 'watch'),
                     default='get')
     a = ap.parse_args()
@@ -113,7 +116,7 @@ def main():
     from zkmi.bench import synthetic as S
     if a.workload == 'get':
         tree = S.GpuTree(a.nodes, a.data_bytes, device=dev, seed=rank)
-        pipe = S.GetPipeline(tree, a.batch, seed=rank)
+        pipe = S.GetPipeline(tree, a.batch, seed=rank, streams=a.streams)
         per_step = a.batch
     elif a.workload == 'watch':
         tree = S.GpuTree(a.nodes, a.data_bytes, device=dev, seed=rank)

@@ -1188,6 +1188,145 @@ __global__ __launch_bounds__(256) void fs_survivor_g(
   if (any_sv) fe_patch_row(f0 + t * W, W, lane, fins);
 }
 
+// A2'' fs_survivor_r (default): the LDS walk of fs_survivor through a 4 KiB
+// ring instead of the whole staged tile.  The survivor only moves forward,
+// so the ring holds the 2 KiB chunk it walks in and the next one; the chunk
+// after that is prefetched into registers (32 bytes per lane) while the
+// walk runs and written into the ring slot just vacated when the walk
+// crosses a chunk boundary (a frame longer than a chunk restages at its
+// landing point).  4 KiB of LDS per tile lets a CU hold as many walks as it
+// holds waves (32) instead of the 9 the 16 KiB tile allowed, so every tile
+// of a 42 MB request stream walks in one round (2688 tiles, formerly two
+// LDS rounds), and the 12288 tiles of a 192 MB reply stream walk with LDS
+// hop latency instead of L2 latency.  The hot loop is fs_survivor's, with
+// the chunk end folded into its position bound.
+constexpr int FR_CH = 2048;                  // ring chunk (bytes)
+constexpr int FR_RING = 2 * FR_CH;
+constexpr int FR_KMAX = (int)(FS_S / FR_CH);  // last chunk (bytes past tile)
+
+// Chunk k (tile-relative bytes [k*CH, (k+1)*CH)) of the tile at ts: 32 bytes
+// per lane, zero past the stream end.
+ZK_DEV void fr_load(const uint8_t* __restrict__ buf, int64_t n, int64_t ts,
+                    int k, int lane, uint4& a, uint4& b) {
+  const int64_t g = ts + (int64_t)k * FR_CH + lane * 32;
+  if (g + 32 <= n) {
+    __builtin_memcpy(&a, buf + g, 16);
+    __builtin_memcpy(&b, buf + g + 16, 16);
+    return;
+  }
+  uint32_t w[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    uint32_t x = 0;
+    for (int q = 0; q < 4; ++q) {
+      const int64_t y = g + 4 * j + q;
+      if (y < n) x |= (uint32_t)buf[y] << (8 * q);
+    }
+    w[j] = x;
+  }
+  a = make_uint4(w[0], w[1], w[2], w[3]);
+  b = make_uint4(w[4], w[5], w[6], w[7]);
+}
+
+ZK_DEV void fr_store(uint8_t* ring, int k, int lane, const uint4& a,
+                     const uint4& b) {
+  uint8_t* d = ring + (k & 1) * FR_CH + lane * 32;
+  *(uint4*)d = a;
+  *(uint4*)(d + 16) = b;
+}
+
+ZK_DEV int32_t fr_len(const uint8_t* ring, int32_t c) {
+  const int32_t a = c & ~3;
+  const uint32_t lo = *(const uint32_t*)(ring + (a & (FR_RING - 1)));
+  const uint32_t hi = *(const uint32_t*)(ring + ((a + 4) & (FR_RING - 1)));
+  return __builtin_amdgcn_readfirstlane(fe_len(lo, hi, c));
+}
+
+__global__ __launch_bounds__(64) void fs_survivor_r(
+    const uint8_t* __restrict__ buf, int64_t n, int64_t maxp, int32_t W,
+    uint16_t* __restrict__ f0, const int32_t* __restrict__ surv,
+    uint16_t* __restrict__ list, int32_t* __restrict__ rcount) {
+  __shared__ __attribute__((aligned(16))) uint8_t ring[FR_RING];
+  const int lane = threadIdx.x;
+  const int64_t t = blockIdx.x;
+  const int64_t ts = t * FS_S;
+  // one survivor per tile (FE_NSURV == 1; the launcher checks)
+  const int32_t sv = __builtin_amdgcn_readfirstlane(surv[t * FE_NSURV]);
+  if (sv < 0) {
+    if (lane == 0) rcount[t * FE_NSURV] = 0;
+    return;
+  }
+  const int32_t nrel = (int32_t)min(n - ts, (int64_t)1 << 30);
+  const int32_t maxp32 = (int32_t)min(maxp, (int64_t)1 << 30);
+  const uint32_t umax = (uint32_t)maxp32;
+  const int32_t lim = min(nrel + 1, (int32_t)FS_S);
+  uint16_t* L = list + t * FE_NSURV * FS_LMAX;
+  int32_t c = sv & 0xFFFF;
+  int32_t lo = c / FR_CH;                       // ring = chunks lo, lo + 1
+  uint4 pa, pb;                                 // prefetched chunk lo + 2
+  {
+    uint4 a0, b0, a1, b1;
+    fr_load(buf, n, ts, lo, lane, a0, b0);
+    fr_load(buf, n, ts, lo + 1, lane, a1, b1);
+    fr_store(ring, lo, lane, a0, b0);
+    fr_store(ring, lo + 1, lane, a1, b1);
+    if (lo + 2 <= FR_KMAX) fr_load(buf, n, ts, lo + 2, lane, pa, pb);
+  }
+  int32_t m = 0;
+  uint32_t ent = 0;
+  for (;;) {
+    const int32_t bound = min(lim, (lo + 1) * FR_CH);
+    for (;;) {                                  // hot: hops inside chunk lo
+      const int32_t len = fr_len(ring, c);
+      const int32_t nx = c + 4 + len;
+      if (((uint32_t)len > umax) | (nx >= bound)) break;
+      ent = lane == (m & 63) ? (uint32_t)c : ent;
+      ++m;
+      if ((m & 63) == 0) L[m - 64 + lane] = (uint16_t)ent;
+      c = nx;
+    }
+    const int32_t len = fr_len(ring, c);
+    const int32_t nx = c + 4 + len;
+    if (((uint32_t)len > umax) | (nx >= lim)) break;   // the ending hop
+    // a clean hop out of chunk lo (still inside the tile)
+    ent = lane == (m & 63) ? (uint32_t)c : ent;
+    ++m;
+    if ((m & 63) == 0) L[m - 64 + lane] = (uint16_t)ent;
+    c = nx;
+    const int32_t nlo = c / FR_CH;
+    if (nlo == lo + 1) {
+      // chunk lo's slot takes chunk lo + 2 (prefetched); prefetch lo + 3
+      if (lo + 2 <= FR_KMAX) fr_store(ring, lo + 2, lane, pa, pb);
+      lo = nlo;
+      if (lo + 2 <= FR_KMAX) fr_load(buf, n, ts, lo + 2, lane, pa, pb);
+    } else {
+      // a frame longer than a chunk: restage around the landing point
+      lo = nlo;
+      uint4 a0, b0, a1, b1;
+      fr_load(buf, n, ts, lo, lane, a0, b0);
+      fr_load(buf, n, ts, lo + 1, lane, a1, b1);
+      fr_store(ring, lo, lane, a0, b0);
+      fr_store(ring, lo + 1, lane, a1, b1);
+      if (lo + 2 <= FR_KMAX) fr_load(buf, n, ts, lo + 2, lane, pa, pb);
+    }
+  }
+  uint16_t fin;
+  {
+    const int32_t len = fr_len(ring, c);
+    int32_t q = 0;
+    fin = fe_hop_len(len, c, nrel, maxp32, q);
+    if (!((fin & F0_TERM) && fin != F0_ESC)) {  // leaves the tile: a start
+      ent = lane == (m & 63) ? (uint32_t)c : ent;
+      ++m;
+      if ((m & 63) == 0) L[m - 64 + lane] = (uint16_t)ent;
+    }
+  }
+  if (lane < (m & 63)) L[(m & ~63) + lane] = (uint16_t)ent;
+  if (lane == 0) rcount[t * FE_NSURV] = m;
+  uint16_t fins[FE_NSURV] = {fin};
+  fe_patch_row(f0 + t * W, W, lane, fins);
+}
+
 // D'' fs_join: the tile's frame starts from its exact entry e*.  Every chain
 // that reaches a survivor's tree passes through that survivor's hand-off
 // position r0 = R[0] (merges into it all happened at positions <= r0), so
@@ -1394,18 +1533,20 @@ int zk_frame_scan2(const uint8_t* buf, int64_t n, int64_t maxp, uint8_t* ws,
                                  st>>>(buf, n, maxp, f0w, surv);
     }
     ZK_LAUNCH_CHECK();
-    // Survivor walk: LDS-staged (one LDS round trip per hop, but the 16 KiB
-    // tile caps a CU at 9 walks) when every tile can walk at once, global
-    // (slower hops, 32 walks per CU) when tiles outnumber the LDS slots.
-    // ZKMI_FS_SURVIVOR=lds|global forces one.
+    // Survivor walk: through a 4 KiB LDS ring (default; LDS hop latency at
+    // up to 32 walks per CU).  ZKMI_FS_SURVIVOR=lds|global|ring selects the
+    // whole-tile LDS walk (9 walks per CU) or the L2 walk for A/B runs.
     static int sv_force = -1;
     if (sv_force < 0) {
       const char* m = getenv("ZKMI_FS_SURVIVOR");
-      sv_force = !m ? 0 : (m[0] == 'l' ? 1 : (m[0] == 'g' ? 2 : 0));
+      sv_force = !m ? 0 : (m[0] == 'l' ? 1 : (m[0] == 'g' ? 2
+                                               : (m[0] == 'r' ? 3 : 0)));
     }
-    const int64_t lds_slots = 9LL * 256;
-    const int sv_mode = sv_force ? sv_force : (tiles <= 2 * lds_slots ? 1 : 2);
-    if (sv_mode == 1)
+    const int sv_mode = sv_force ? sv_force : 3;
+    if (sv_mode == 3 && FE_NSURV == 1)
+      fs_survivor_r<<<(unsigned)tiles, 64, 0, st>>>(buf, n, maxp, W, f0w,
+                                                   surv, list, rcnt);
+    else if (sv_mode == 1)
       fs_survivor<<<(unsigned)tiles, 64, FV_LDS, st>>>(buf, n, maxp, W, f0w,
                                                       surv, list, rcnt);
     else

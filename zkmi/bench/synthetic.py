@@ -250,11 +250,25 @@ class GpuServer(object):
 class GetPipeline(object):
     """Batched get() over the synthetic tree (BASELINE config 2)."""
 
-    def __init__(self, tree, batch, seed=0):
+    def __init__(self, tree, batch, seed=0, streams=1):
         self.tree = tree
         self.batch = batch
         dev = tree.device
         self.dev = dev
+        self.subs = []
+        if streams > 1:
+            # `streams` independent pipelined connections, each with its own
+            # HIP stream, buffers and xid table, sharing the tree.  Their
+            # phases are issued round-robin (see step), so one connection's
+            # latency-bound kernels (frame-scan walks, composition, scans)
+            # and host read-backs overlap another's bandwidth-bound ones.
+            per = [batch // streams + (1 if k < batch % streams else 0)
+                   for k in range(streams)]
+            self.subs = [GetPipeline(tree, m, seed=seed * streams + k)
+                         for k, m in enumerate(per)]
+            self.streams = [torch.cuda.Stream(dev) for _ in per]
+            self.last = None
+            return
         self.xt = B.XidTable(bits=max(20, (batch - 1).bit_length() + 1),
                              device=dev)
         n = batch
@@ -289,6 +303,31 @@ class GetPipeline(object):
         added to ``acc`` (device int64 [1]; a fresh one when None), which is
         returned.  Request generation and the reply check are one fused
         kernel each (csrc/kernels/bench.hip)."""
+        if validate and acc is None:
+            acc = torch.zeros(1, dtype=I64, device=self.dev)
+        if not self.subs:
+            for _ in self._phases(validate, acc):
+                pass
+            return acc if validate else None
+        cur = torch.cuda.current_stream(self.dev)
+        live = []
+        for p, s in zip(self.subs, self.streams):
+            s.wait_stream(cur)
+            live.append((s, p._phases(validate, acc)))
+        while live:
+            nxt = []
+            for s, g in live:
+                with torch.cuda.stream(s):
+                    if next(g, StopIteration) is not StopIteration:
+                        nxt.append((s, g))
+            live = nxt
+        for s in self.streams:
+            cur.wait_stream(s)
+        return acc if validate else None
+
+    def _phases(self, validate, acc):
+        """The step as a generator that yields before each host read-back
+        (the two stream lengths), on the caller's current stream."""
         t = self.tree
         n = self.batch
         L = _lib.lib()
@@ -307,22 +346,21 @@ class GetPipeline(object):
                             t.path_arena, t.slab, self.acl_off,
                             self.acl_len, self.acl_arena)
         tx, rec_off, total, err = B.encode_requests(rb, self.xt, out=self.tx)
+        yield
         ntx = int(total.item())
         rx, rtotal, rerr, _ = self.server.serve(tx, ntx)
+        yield
         nrx = int(rtotal.item())
         ft = B.frame_scan(rx, nrx, cap=n, window=self.rwindow)
         rep = B.decode_replies(rx, ft, self.xt, out=self.reply)
         self.last = (self.idx, rep, rx, ft)
         if not validate:
-            return None
-        if acc is None:
-            acc = torch.zeros(1, dtype=I64, device=self.dev)
+            return
         _lib.check(L.zk_bench_check_get(
             n, _lib.ptr(rep.status), _lib.ptr(rep.err), _lib.ptr(rep.opcode),
             _lib.ptr(rep.xid), _lib.ptr(rep.stat64[0]), _lib.ptr(rep.pay_len),
             _lib.ptr(self.idx), _lib.ptr(xid), _lib.ptr(t.data_len),
             _lib.ptr(acc), sp), 'zk_bench_check_get')
-        return acc
 
 
 def _arena(strings, dev):

@@ -13,6 +13,8 @@
 
 extern "C" int zk_scan_excl_i64(const int64_t*, int64_t*, int64_t, int64_t*,
                                 int64_t*, hipStream_t);
+extern "C" int zk_scan_small_i64(const int64_t*, int64_t*, int64_t, int64_t*,
+                                 hipStream_t);
 
 namespace zk {
 
@@ -47,15 +49,28 @@ ZK_DEV int64_t req_body_size(const ZkReqBatch& b, int64_t i, bool* ok) {
   }
 }
 
+// Offsets are reduce-then-scan fused into the producer and the consumer:
+// the sizes kernel also writes its block's sum, one workgroup scans the
+// block sums (zk_scan_small_i64), and the write kernel adds its block base
+// to a block scan of the sizes.  Three launches where a separate device-wide
+// scan made five.
 __global__ __launch_bounds__(ENC_T) void req_sizes(ZkReqBatch b, int64_t n,
                                                   int64_t* __restrict__ sizes,
-                                                  int32_t* __restrict__ err) {
+                                                  int32_t* __restrict__ err,
+                                                  int64_t* __restrict__ bsum) {
+  __shared__ int64_t sm[ENC_T / 64 + 1];
   const int64_t i = (int64_t)blockIdx.x * ENC_T + threadIdx.x;
-  if (i >= n) return;
-  bool ok;
-  const int64_t s = req_body_size(b, i, &ok);
-  sizes[i] = ok ? 4 + s : 0;
-  if (!ok) atomicOr(err, 1);
+  int64_t sz = 0;
+  if (i < n) {
+    bool ok;
+    const int64_t s = req_body_size(b, i, &ok);
+    sz = ok ? 4 + s : 0;
+    sizes[i] = sz;
+    if (!ok) atomicOr(err, 1);
+  }
+  int64_t tot;
+  block_excl_scan(sz, sm, &tot);
+  if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
 }
 
 // ---------------------------------------------------------------- K11
@@ -132,10 +147,18 @@ __global__ __launch_bounds__(ENC_T) void resp_sizes(ZkRespBatch r,
                                                    ZkNodeStore s,
                                                    const int64_t* __restrict__ n_dev,
                                                    int64_t ncap,
-                                                   int64_t* __restrict__ sizes) {
+                                                   int64_t* __restrict__ sizes,
+                                                   int64_t* __restrict__ bsum) {
+  __shared__ int64_t sm[ENC_T / 64 + 1];
   const int64_t i = (int64_t)blockIdx.x * ENC_T + threadIdx.x;
-  if (i >= ncap) return;
-  sizes[i] = (i < *n_dev) ? 4 + resp_body_size(r, s, i) : 0;
+  int64_t sz = 0;
+  if (i < ncap) {
+    sz = (i < *n_dev) ? 4 + resp_body_size(r, s, i) : 0;
+    sizes[i] = sz;
+  }
+  int64_t tot;
+  block_excl_scan(sz, sm, &tot);
+  if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
 }
 
 // ---- record sinks ----------------------------------------------------------
@@ -227,15 +250,18 @@ ZK_DEV void emit_response(K& k, const ZkRespBatch& r, const ZkNodeStore& s,
   if (r.err[i] == ERR_OK) {
     switch (r.opcode[i]) {
       case OP_GET_DATA: {
-        // wire-format slot: [len | data] then Stat — two contiguous copies
-        const int64_t nd = r.node[i];
-        const uint8_t* slot = s.slab + s.slot_off[nd];
-        k.bytes(slot + ZK_SLOT_LEN, 4 + (int64_t)max(s.data_len[nd], 0));
+        // wire-format slot: [len | data] then Stat — two contiguous copies.
+        // The data length is implied by the frame size (header 16, length
+        // word 4, Stat 68), so only the slot itself is read.
+        const uint8_t* slot = s.slab + (r.slot ? r.slot[i]
+                                               : s.slot_off[r.node[i]]);
+        k.bytes(slot + ZK_SLOT_LEN, body - 16 - STAT_BYTES);
         k.bytes(slot + ZK_SLOT_STAT, STAT_BYTES);
         break;
       }
       case OP_EXISTS: case OP_SET_DATA:
-        k.bytes(s.slab + s.slot_off[r.node[i]] + ZK_SLOT_STAT, STAT_BYTES);
+        k.bytes(s.slab + (r.slot ? r.slot[i] : s.slot_off[r.node[i]]) +
+                    ZK_SLOT_STAT, STAT_BYTES);
         break;
       case OP_CREATE:
         k_buffer(k, r.path_arena + r.path_off[i], r.path_len[i]);
@@ -252,7 +278,31 @@ ZK_DEV void emit_response(K& k, const ZkRespBatch& r, const ZkNodeStore& s,
   k.finish();
 }
 
-constexpr int64_t STAGE_BYTES = 32 * 1024;   // LDS image per block
+// LDS image per block; with the block's offset table (EncLocal, 4 KiB) a
+// block holds 32 KiB, 5 blocks per CU.
+constexpr int64_t STAGE_BYTES = 28 * 1024;
+
+// The block's record offsets and sizes (index k = record r0 + k).
+struct EncLocal {
+  int64_t off[ENC_T];
+  int64_t sz[ENC_T];
+  int64_t sm[ENC_T / 64 + 1];
+};
+
+// off = bbase[block] + block scan of sizes; also written to rec_off.
+ZK_DEV void block_offsets(int64_t r0, int64_t r1,
+                          const int64_t* __restrict__ sizes,
+                          const int64_t* __restrict__ bbase,
+                          int64_t* __restrict__ rec_off, EncLocal& E) {
+  const int64_t i = r0 + threadIdx.x;
+  const int64_t sz = i < r1 ? sizes[i] : 0;
+  int64_t tot;
+  const int64_t o = bbase[blockIdx.x] + block_excl_scan(sz, E.sm, &tot);
+  E.off[threadIdx.x] = o;
+  E.sz[threadIdx.x] = sz;
+  if (i < r1 && rec_off != nullptr) rec_off[i] = o;
+  __syncthreads();
+}
 
 ZK_DEV uint8_t lds_byte(const uint32_t* lw, int64_t b) {
   return ((const uint8_t*)(lw + swz(b >> 2)))[b & 3];
@@ -287,34 +337,36 @@ ZK_DEV void stage_out(const uint32_t* lw, int64_t a0, int64_t B0, int64_t B1,
 // LDS image.  Records are staged in runs that fit the image (record i ends
 // at off[i] + sizes[i]; ends grow with i, so "fits" is a prefix of the
 // run, counted with one barrier); a single record larger than the image is
-// written straight to global memory.
+// written straight to global memory.  off / sizes are the block's EncLocal
+// tables (index i - r0).
 template <class F>
-ZK_DEV void staged_emit(int64_t r0, int64_t r1, const int64_t* __restrict__ off,
-                        const int64_t* __restrict__ sizes,
-                        uint8_t* __restrict__ out, uint32_t* lw, F emit) {
+ZK_DEV void staged_emit(int64_t r0, int64_t r1, const int64_t* off,
+                        const int64_t* sizes, uint8_t* __restrict__ out,
+                        uint32_t* lw, F emit) {
   int64_t rs = r0;
   while (rs < r1) {                              // block-uniform
-    const int64_t B0 = off[rs];
+    const int64_t B0 = off[rs - r0];
     const int64_t a0 = B0 & ~(int64_t)15;
     const int64_t i = rs + threadIdx.x;
-    const bool fits = i < r1 && off[i] + sizes[i] - a0 + 16 <= STAGE_BYTES;
+    const bool fits = i < r1 &&
+                      off[i - r0] + sizes[i - r0] - a0 + 16 <= STAGE_BYTES;
     const int k = __syncthreads_count(fits);
     if (k == 0) {
       if (threadIdx.x == 0) {
-        GSink g{out + off[rs]};
+        GSink g{out + B0};
         emit(g, rs);
       }
       rs += 1;
       continue;
     }
     const int64_t re = rs + k;
-    const int64_t B1 = off[re - 1] + sizes[re - 1];
+    const int64_t B1 = off[re - 1 - r0] + sizes[re - 1 - r0];
     const int64_t nrow = ((B1 - a0 + 3) >> 8) + 1;     // 64-dword rows
     for (int64_t x = threadIdx.x; x < nrow * 16; x += blockDim.x)
       ((uint4*)lw)[x] = make_uint4(0, 0, 0, 0);
     __syncthreads();
     if (i < re) {
-      LSink l(lw, off[i] - a0);
+      LSink l(lw, off[i - r0] - a0);
       emit(l, i);
     }
     __syncthreads();
@@ -326,10 +378,12 @@ ZK_DEV void staged_emit(int64_t r0, int64_t r1, const int64_t* __restrict__ off,
 
 __global__ __launch_bounds__(ENC_T) void resp_write(
     ZkRespBatch r, ZkNodeStore s, const int64_t* __restrict__ n_dev,
-    int64_t ncap, const int64_t* __restrict__ off,
-    const int64_t* __restrict__ sizes, const int64_t* __restrict__ total,
-    uint8_t* __restrict__ out, int64_t cap, int32_t* __restrict__ err) {
+    int64_t ncap, const int64_t* __restrict__ sizes,
+    const int64_t* __restrict__ bbase, int64_t* __restrict__ rec_off,
+    const int64_t* __restrict__ total, uint8_t* __restrict__ out, int64_t cap,
+    int32_t* __restrict__ err) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lw[];
+  __shared__ EncLocal E;
   const int64_t n = min(*n_dev, ncap);
   const int64_t r0 = (int64_t)blockIdx.x * ENC_T;
   if (r0 >= n) return;
@@ -338,8 +392,9 @@ __global__ __launch_bounds__(ENC_T) void resp_write(
     return;
   }
   const int64_t r1 = min(r0 + ENC_T, n);
-  staged_emit(r0, r1, off, sizes, out, lw, [&](auto& k, int64_t i) {
-    emit_response(k, r, s, i, sizes[i] - 4);
+  block_offsets(r0, r1, sizes, bbase, rec_off, E);
+  staged_emit(r0, r1, E.off, E.sz, out, lw, [&](auto& k, int64_t i) {
+    emit_response(k, r, s, i, E.sz[i - r0] - 4);
   });
 }
 
@@ -386,11 +441,13 @@ ZK_DEV void emit_request(K& k, const ZkReqBatch& b, int64_t i, int64_t body) {
 // GET_DATA stream).  Unknown opcodes were flagged by req_sizes and get
 // size 0 (nothing written).
 __global__ __launch_bounds__(ENC_T) void req_write(
-    ZkReqBatch b, int64_t n, const int64_t* __restrict__ off,
-    const int64_t* __restrict__ sizes, const int64_t* __restrict__ total,
-    uint8_t* __restrict__ out, int64_t cap, int64_t* __restrict__ xid_tab,
-    int64_t xid_mask, int32_t* __restrict__ err) {
+    ZkReqBatch b, int64_t n, const int64_t* __restrict__ sizes,
+    const int64_t* __restrict__ bbase, int64_t* __restrict__ rec_off,
+    const int64_t* __restrict__ total, uint8_t* __restrict__ out, int64_t cap,
+    int64_t* __restrict__ xid_tab, int64_t xid_mask,
+    int32_t* __restrict__ err) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lw[];
+  __shared__ EncLocal E;
   const int64_t r0 = (int64_t)blockIdx.x * ENC_T;
   if (r0 >= n) return;
   if (*total > cap) {                       // capacity guard (whole batch)
@@ -398,8 +455,10 @@ __global__ __launch_bounds__(ENC_T) void req_write(
     return;
   }
   const int64_t r1 = min(r0 + ENC_T, n);
-  staged_emit(r0, r1, off, sizes, out, lw, [&](auto& k, int64_t i) {
-    if (sizes[i] > 0) emit_request(k, b, i, sizes[i] - 4);
+  block_offsets(r0, r1, sizes, bbase, rec_off, E);
+  staged_emit(r0, r1, E.off, E.sz, out, lw, [&](auto& k, int64_t i) {
+    const int64_t sz = E.sz[i - r0];
+    if (sz > 0) emit_request(k, b, i, sz - 4);
   });
   const int64_t i = r0 + threadIdx.x;
   if (i < r1 && xid_tab != nullptr && sizes[i] > 0) {
@@ -449,12 +508,16 @@ int zk_encode_requests(const ZkReqBatch* b, int64_t n, int64_t* sizes,
                        uint8_t* out, int64_t out_cap, int64_t* xid_tab,
                        int64_t xid_mask, int32_t* err, hipStream_t st) {
   if (n <= 0) return hipMemsetAsync(total, 0, 8, st);
-  zk::req_sizes<<<zk::nblk(n), zk::ENC_T, 0, st>>>(*b, n, sizes, err);
+  const unsigned nb = zk::nblk(n);
+  int64_t* bsum = scan_ws;                 // zk_scan_workspace(n) >= 2 nb
+  int64_t* bbase = scan_ws + nb;
+  zk::req_sizes<<<nb, zk::ENC_T, 0, st>>>(*b, n, sizes, err, bsum);
   ZK_LAUNCH_CHECK();
-  int rc = zk_scan_excl_i64(sizes, rec_off, n, total, scan_ws, st);
+  int rc = zk_scan_small_i64(bsum, bbase, nb, total, st);
   if (rc) return rc;
-  zk::req_write<<<zk::nblk(n), zk::ENC_T, zk::STAGE_BYTES, st>>>(
-      *b, n, rec_off, sizes, total, out, out_cap, xid_tab, xid_mask, err);
+  zk::req_write<<<nb, zk::ENC_T, zk::STAGE_BYTES, st>>>(
+      *b, n, sizes, bbase, rec_off, total, out, out_cap, xid_tab, xid_mask,
+      err);
   ZK_LAUNCH_CHECK();
   return 0;
 }
@@ -497,21 +560,38 @@ int zk_encode_connect_requests(const int32_t* proto, const int64_t* zxid,
   return 0;
 }
 
+// presized != 0: `sizes` (frame size per reply, 0 past *n_dev) and the
+// per-256-reply block sums in scan_ws[0, nblk(ncap)) were already written
+// by the producer (zk_tree_serve), so the sizes pass is skipped.
+int zk_encode_responses2(const ZkRespBatch* r, const ZkNodeStore* s,
+                         const int64_t* n_dev, int64_t ncap, int64_t* sizes,
+                         int64_t* rec_off, int64_t* total, int64_t* scan_ws,
+                         uint8_t* out, int64_t out_cap, int32_t* err,
+                         int32_t presized, hipStream_t st) {
+  if (ncap <= 0) return hipMemsetAsync(total, 0, 8, st);
+  const unsigned nb = zk::nblk(ncap);
+  int64_t* bsum = scan_ws;
+  int64_t* bbase = scan_ws + nb;
+  if (!presized) {
+    zk::resp_sizes<<<nb, zk::ENC_T, 0, st>>>(*r, *s, n_dev, ncap, sizes,
+                                             bsum);
+    ZK_LAUNCH_CHECK();
+  }
+  int rc = zk_scan_small_i64(bsum, bbase, nb, total, st);
+  if (rc) return rc;
+  zk::resp_write<<<nb, zk::ENC_T, zk::STAGE_BYTES, st>>>(
+      *r, *s, n_dev, ncap, sizes, bbase, rec_off, total, out, out_cap, err);
+  ZK_LAUNCH_CHECK();
+  return 0;
+}
+
 int zk_encode_responses(const ZkRespBatch* r, const ZkNodeStore* s,
                         const int64_t* n_dev, int64_t ncap, int64_t* sizes,
                         int64_t* rec_off, int64_t* total, int64_t* scan_ws,
                         uint8_t* out, int64_t out_cap, int32_t* err,
                         hipStream_t st) {
-  if (ncap <= 0) return hipMemsetAsync(total, 0, 8, st);
-  zk::resp_sizes<<<zk::nblk(ncap), zk::ENC_T, 0, st>>>(*r, *s, n_dev, ncap,
-                                                        sizes);
-  ZK_LAUNCH_CHECK();
-  int rc = zk_scan_excl_i64(sizes, rec_off, ncap, total, scan_ws, st);
-  if (rc) return rc;
-  zk::resp_write<<<zk::nblk(ncap), zk::ENC_T, zk::STAGE_BYTES, st>>>(
-      *r, *s, n_dev, ncap, rec_off, sizes, total, out, out_cap, err);
-  ZK_LAUNCH_CHECK();
-  return 0;
+  return zk_encode_responses2(r, s, n_dev, ncap, sizes, rec_off, total,
+                              scan_ws, out, out_cap, err, 0, st);
 }
 
 }  // extern "C"

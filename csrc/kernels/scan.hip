@@ -71,6 +71,42 @@ __global__ __launch_bounds__(SCAN_T) void scan_apply(const T* __restrict__ in,
     *total = p;
 }
 
+// One workgroup scans any n in one launch: 1024 threads x 8 values per
+// chunk, a running carry across chunks.  Used for the short scans (frame
+// counts per tile, the encoders' block sums), where the reduce / scan /
+// apply chain was three launches of ~5 us each for a few thousand values.
+constexpr int SB_T = 1024;
+constexpr int SB_V = 8;
+constexpr int64_t SCAN_ONE_MAX = 1 << 16;       // use it up to this n
+
+template <typename T>
+__global__ __launch_bounds__(SB_T) void scan_one_block(
+    const T* __restrict__ in, int64_t n, int64_t* __restrict__ out,
+    int64_t* __restrict__ total) {
+  __shared__ int64_t sm[SB_T / 64 + 1];
+  int64_t carry = 0;
+  for (int64_t c0 = 0; c0 < n; c0 += (int64_t)SB_T * SB_V) {   // uniform
+    // thread t owns values c0 + t*V .. +V-1 (its own run: the scan order)
+    const int64_t b = c0 + (int64_t)threadIdx.x * SB_V;
+    int64_t v[SB_V];
+    int64_t s = 0;
+#pragma unroll
+    for (int j = 0; j < SB_V; ++j) {
+      v[j] = b + j < n ? (int64_t)in[b + j] : 0;
+      s += v[j];
+    }
+    int64_t tot;
+    int64_t p = carry + block_excl_scan(s, sm, &tot);
+#pragma unroll
+    for (int j = 0; j < SB_V; ++j) {
+      if (b + j < n) out[b + j] = p;
+      p += v[j];
+    }
+    carry += tot;
+  }
+  if (total != nullptr && threadIdx.x == 0) *total = carry;
+}
+
 // ---------------------------------------------------------------------------
 // MFMA byte-plane engine
 // ---------------------------------------------------------------------------
@@ -251,7 +287,7 @@ template <typename T, int NT>
 static int scan_rec_mfma(const T* in, int64_t* out, int64_t n, int64_t* total,
                          int64_t* ws, hipStream_t st) {
   constexpr int64_t E = (int64_t)NT * MS_V;
-  if (n <= SCAN_E) return scan_rec<T>(in, out, n, total, ws, st);
+  if (n <= SCAN_ONE_MAX) return scan_rec<T>(in, out, n, total, ws, st);
   const int64_t nb = (n + E - 1) / E;
   int64_t* bsum = ws;
   int64_t* bbase = ws + nb;
@@ -290,6 +326,11 @@ static int scan_rec(const T* in, int64_t* out, int64_t n, int64_t* total,
     ZK_LAUNCH_CHECK();
     return 0;
   }
+  if (n <= SCAN_ONE_MAX) {
+    scan_one_block<T><<<1, SB_T, 0, st>>>(in, n, out, total);
+    ZK_LAUNCH_CHECK();
+    return 0;
+  }
   int64_t* bsum = ws;
   int64_t* bbase = ws + nb;
   scan_reduce<T><<<(unsigned)nb, SCAN_T, 0, st>>>(in, n, bsum);
@@ -308,14 +349,30 @@ extern "C" {
 // Workspace (int64 elements) needed by zk_scan_* for n inputs.
 // Sized for the smallest block of any engine (one MFMA wave, 1024 values),
 // an upper bound for the others.
+// Also covers the encoders' per-256-record block sums and bases
+// (2 * ceil(n / 256)).
 int64_t zk_scan_workspace(int64_t n) {
+  const int64_t enc = 2 * ((n + 255) / 256) + 2;
   int64_t w = 0;
   while (n > zk::SCAN_E) {
     const int64_t nb = (n + zk::MS_WAVE_E - 1) / zk::MS_WAVE_E;
     w += 2 * nb;
     n = nb;
   }
-  return w + 2;
+  return w + 2 > enc ? w + 2 : enc;
+}
+
+// Exclusive scan of n values (any n) by one workgroup, one launch: the
+// encoders' block sums.
+int zk_scan_small_i64(const int64_t* in, int64_t* out, int64_t n,
+                      int64_t* total, hipStream_t st) {
+  if (n <= 0) {
+    if (total) return hipMemsetAsync(total, 0, sizeof(int64_t), st);
+    return 0;
+  }
+  zk::scan_one_block<int64_t><<<1, zk::SB_T, 0, st>>>(in, n, out, total);
+  ZK_LAUNCH_CHECK();
+  return 0;
 }
 
 // 0 = shuffle engine, 1 = MFMA byte-plane engine; returns the old mode.

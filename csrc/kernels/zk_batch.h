@@ -53,6 +53,8 @@ struct ZkRespBatch {
   const int32_t* path_len;
   const uint8_t* path_arena;
   const int32_t* aux;       // NOTIFICATION type
+  const int64_t* slot;      // node's slot offset in the slab (null: look
+                            // it up through node -> slot_off)
 };
 
 // K2-K8 — decoded replies (SoA, `cap` rows).

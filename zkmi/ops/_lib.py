@@ -43,7 +43,7 @@ SLOT_DATA = 76
 class ZkRespBatch(ctypes.Structure):
     _fields_ = [(n, P) for n in (
         'opcode', 'xid', 'err', 'node', 'zxid', 'path_off', 'path_len',
-        'path_arena', 'aux')]
+        'path_arena', 'aux', 'slot')]
 
 
 class ZkReplyOut(ctypes.Structure):
@@ -82,6 +82,8 @@ _SIGS = {
     'zk_encode_set_watches': (I32, [P, P, P, I64, I64, I64, I64, P, P, P, P,
                                     P, I64, P, P]),
     'zk_encode_responses': (I32, [P, P, P, I64, P, P, P, P, P, I64, P, P]),
+    'zk_encode_responses2': (I32, [P, P, P, I64, P, P, P, P, P, I64, P, I32,
+                                   P]),
     'zk_frame_scan_workspace': (I64, [I64]),
     'zk_frame_scan': (I32, [P, I64, I64, P, I64, P, P, I64, P, P]),
     'zk_frame_scan2': (I32, [P, I64, I64, P, I64, P, P, I64, P, I32, P]),

@@ -147,6 +147,14 @@ def pack_requests(pkts, device=None):
                         B(parena), B(darena), T(aoff), T(alen), B(aarena))
 
 
+def _total_err(dev):
+    """The encoders' (total, err) device scalars.  ``total`` is always
+    written by the launcher (scan or memset); ``err`` is OR-ed into, so it
+    starts at zero — one fill for both."""
+    z = torch.zeros(2, dtype=I64, device=dev)
+    return z[0:1], z[1:2].view(I32)[0:1]
+
+
 def encode_requests(batch, xid_table=None, out=None, stream=None):
     """K10: encode ``batch`` into one framed byte stream.
 
@@ -159,9 +167,8 @@ def encode_requests(batch, xid_table=None, out=None, stream=None):
     dev = batch.opcode.device
     sizes = torch.empty(max(n, 1), dtype=I64, device=dev)
     rec_off = torch.empty(max(n, 1), dtype=I64, device=dev)
-    total = torch.zeros(1, dtype=I64, device=dev)
+    total, err = _total_err(dev)
     ws = torch.empty(L.zk_scan_workspace(max(n, 1)), dtype=I64, device=dev)
-    err = torch.zeros(1, dtype=I32, device=dev)
     if out is None:
         # Upper bound: 4+8 header, 4+path, 4+data, acl, 8 ints.
         ub = int(n * 40 + batch.path_arena.numel() + batch.data_arena.numel()
@@ -326,7 +333,7 @@ def frame_scan(buf, n=None, max_packet=consts.MAX_PACKET, cap=None,
         workspace = torch.empty(max(wsb, 256), dtype=U8, device=dev)
     off = torch.empty(cap, dtype=I64, device=dev)
     ln = torch.empty(cap, dtype=I32, device=dev)
-    res = torch.zeros(4, dtype=I64, device=dev)
+    res = torch.empty(4, dtype=I64, device=dev)     # zeroed by the launcher
     check(L.zk_frame_scan2(ptr(buf), n, max_packet, ptr(workspace),
                            workspace.numel(), ptr(off), ptr(ln), cap,
                            ptr(res), int(window), stream_ptr(stream)),
@@ -517,30 +524,47 @@ class ResponseBatch:
     path_arena: torch.Tensor
     aux: torch.Tensor
     count: torch.Tensor
+    slot: torch.Tensor = None   # slot offsets (from the tree lookup) or None
 
     def struct(self):
         return _lib.ZkRespBatch(*[t.data_ptr() for t in (
             self.opcode, self.xid, self.err, self.node, self.zxid,
-            self.path_off, self.path_len, self.path_arena, self.aux)])
+            self.path_off, self.path_len, self.path_arena, self.aux)],
+            self.slot.data_ptr() if self.slot is not None else None)
 
 
-def encode_responses(resp, store_struct, out_cap, out=None, stream=None):
-    """K13: server-mode reply encode -> (bytes, rec_off, total, err)."""
+def response_workspace(cap, device):
+    """(sizes, scan workspace) a producer fills for a presized
+    :func:`encode_responses` (zk_tree_serve writes both)."""
+    L = _lib.lib()
+    return (torch.empty(cap, dtype=I64, device=device),
+            torch.empty(L.zk_scan_workspace(cap), dtype=I64, device=device))
+
+
+def encode_responses(resp, store_struct, out_cap, out=None, stream=None,
+                     presized=None):
+    """K13: server-mode reply encode -> (bytes, rec_off, total, err).
+    ``presized``: the (sizes, workspace) pair of :func:`response_workspace`
+    already filled by the producer; the sizes pass is then skipped."""
     L = _lib.lib()
     cap = resp.opcode.numel()
     dev = resp.opcode.device
-    sizes = torch.empty(cap, dtype=I64, device=dev)
+    if presized is not None:
+        sizes, ws = presized
+    else:
+        sizes = torch.empty(cap, dtype=I64, device=dev)
+        ws = torch.empty(L.zk_scan_workspace(cap), dtype=I64, device=dev)
     rec_off = torch.empty(cap, dtype=I64, device=dev)
-    total = torch.zeros(1, dtype=I64, device=dev)
-    ws = torch.empty(L.zk_scan_workspace(cap), dtype=I64, device=dev)
-    err = torch.zeros(1, dtype=I32, device=dev)
+    total, err = _total_err(dev)
     if out is None:
         out = torch.empty(out_cap, dtype=U8, device=dev)
     s = resp.struct()
-    check(L.zk_encode_responses(ctypes_ref(s), ctypes_ref(store_struct),
-                                ptr(resp.count), cap, ptr(sizes),
-                                ptr(rec_off), ptr(total), ptr(ws), ptr(out),
-                                out.numel(), ptr(err), stream_ptr(stream)),
+    check(L.zk_encode_responses2(ctypes_ref(s), ctypes_ref(store_struct),
+                                 ptr(resp.count), cap, ptr(sizes),
+                                 ptr(rec_off), ptr(total), ptr(ws), ptr(out),
+                                 out.numel(), ptr(err),
+                                 1 if presized is not None else 0,
+                                 stream_ptr(stream)),
           'zk_encode_responses')
     return out, rec_off, total, err
 

@@ -68,7 +68,7 @@ constexpr int TR_T = 256;
 enum : int {
   TC_NODES = 0, TC_ZXID = 1, TC_PATH_TOP = 2, TC_SLAB_TOP = 3,
   TC_FREE_HEAD = 4, TC_FREE_TAIL = 5, TC_FREE_PUB = 6, TC_DIRTY = 7,
-  TC_N = 8
+  TC_DONE = 8, TC_N = 9
 };
 constexpr int64_t NODE_FREE = -2;
 
@@ -166,27 +166,36 @@ ZK_DEV bool bytes_eq(const uint8_t* a, const uint8_t* b, int32_t n) {
 
 ZK_DEV int64_t* ht_key(const ZkTree& t, int64_t s) { return &t.ht[2 * s]; }
 ZK_DEV int64_t* ht_val(const ZkTree& t, int64_t s) { return &t.ht[2 * s + 1]; }
+ZK_DEV bool path_is(const ZkTree& t, int64_t v, const uint8_t* p, int32_t n) {
+  return t.node_path_len[v] == n &&
+         bytes_eq(t.path_arena + t.node_path_off[v], p, n);
+}
 
-ZK_DEV int64_t tree_find(const ZkTree& t, const uint8_t* p, int32_t n) {
+// Node of path p (node -1 if absent) and its slot offset.
+struct Found {
+  int64_t node, slot;
+};
+
+ZK_DEV Found tree_lookup(const ZkTree& t, const uint8_t* p, int32_t n) {
   const int64_t key = (int64_t)(path_hash(p, n) | 1ull);
   int64_t s = key & t.mask;
   for (int64_t probe = 0; probe <= t.mask; ++probe) {
-    // one 16-byte load per probe; entries being written concurrently in
-    // this launch may read torn (val -3): not found, as the batch contract
-    // allows for same-batch conflicts
-    const int4 e = *(const int4*)ht_key(t, s);
-    const int64_t k = (int64_t)(((uint64_t)(uint32_t)e.y << 32) | (uint32_t)e.x);
-    if (k == 0) return -1;
-    if (k == key) {
-      const int64_t v = (int64_t)(((uint64_t)(uint32_t)e.w << 32) |
-                                  (uint32_t)e.z);
-      if (v >= 0 && t.node_path_len[v] == n &&
-          bytes_eq(t.path_arena + t.node_path_off[v], p, n))
-        return v;
-    }
+    // one 16-byte {key, val} entry per probe; entries being written
+    // concurrently in this launch may read torn (val -3): not found, as the
+    // batch contract allows for same-batch conflicts on one path
+    const int64_t* ent = ht_key(t, s);
+    const int64_t k = ent[0];
+    const int64_t v = ent[1];
+    if (k == 0) break;
+    if (k == key && v >= 0 && path_is(t, v, p, n))
+      return Found{v, t.store.slot_off[v]};
     s = (s + 1) & t.mask;
   }
-  return -1;
+  return Found{-1, -1};
+}
+
+ZK_DEV int64_t tree_find(const ZkTree& t, const uint8_t* p, int32_t n) {
+  return tree_lookup(t, p, n).node;
 }
 
 // Insert node `v` (path already in the arena).  Returns the existing node if
@@ -209,9 +218,7 @@ ZK_DEV int64_t tree_insert(const ZkTree& t, int64_t v, const uint8_t* p,
       for (int spin = 0; spin < 1000000 && w == -3; ++spin)
         w = __hip_atomic_load(ht_val(t, s), __ATOMIC_RELAXED,
                               __HIP_MEMORY_SCOPE_AGENT);
-      if (w >= 0 && t.node_path_len[w] == n &&
-          bytes_eq(t.path_arena + t.node_path_off[w], p, n))
-        return w;
+      if (w >= 0 && path_is(t, w, p, n)) return w;
       if (w == -2 &&                      // tombstone of the same key: reuse
           atomicCAS((unsigned long long*)ht_val(t, s), (unsigned long long)-2,
                     (unsigned long long)v) == (unsigned long long)-2)
@@ -315,9 +322,23 @@ ZK_DEV void put_seq10(uint8_t* d, int32_t x) {
 // Per-lane state of one request through the three phases of tree_serve_k.
 struct Lane {
   int32_t op, err, pl, dl, flags;
-  int64_t node, zx, par;
+  int64_t node, zx, par, slot;
   const uint8_t* path;
 };
+
+// Reply frame size (length word included) of a served request, as
+// encode.hip's resp_body_size computes it from the reply descriptors.
+ZK_DEV int64_t served_reply_size(int32_t op, int32_t err, int32_t dl,
+                                 int32_t rpl) {
+  const int64_t sz = 4 + 16;                    // length, xid, zxid, err
+  if (err != ERR_OK) return sz;
+  switch (op) {
+    case OP_GET_DATA: return sz + 4 + max(dl, 0) + STAT_BYTES;
+    case OP_EXISTS: case OP_SET_DATA: return sz + STAT_BYTES;
+    case OP_CREATE: return sz + 4 + max(rpl, 0);
+    default: return sz;
+  }
+}
 
 // CREATE (lib/zk-buffer.js:97-136 request shape; semantics of the server the
 // reference talks to): parent must exist and not be ephemeral, ACL must be
@@ -366,21 +387,27 @@ ZK_DEV int32_t do_create(const ZkTree& t, Lane& L, const uint8_t* data,
   if (par >= 0) parent_touch(t, par, 1, !seq, L.zx);
   L.par = par;
   L.node = v;
+  L.slot = s.slot_off[v];
   return ERR_OK;
 }
 
 // Apply one batch of decoded requests; produce reply descriptors for K13.
 // r_path_off/len (may be null) receive the created node's path in the tree's
-// path arena (SEQUENTIAL names differ from the requested one).
+// path arena (SEQUENTIAL names differ from the requested one).  r_slot,
+// r_sizes and r_bsum (may be null) receive each reply's slot offset, its
+// frame size and the block's size sum, so the reply encoder needs neither
+// its sizes pass nor a lookup of the node's slot (zk_encode_responses2
+// presized).
 __global__ __launch_bounds__(TR_T) void tree_serve_k(
     ZkTree t, const uint8_t* __restrict__ rx, ZkReqOut q,
     const int64_t* __restrict__ n_dev, int64_t ncap, int32_t* __restrict__ r_op,
     int32_t* __restrict__ r_xid, int32_t* __restrict__ r_err,
     int64_t* __restrict__ r_node, int64_t* __restrict__ r_zxid,
     int64_t* __restrict__ r_path_off, int32_t* __restrict__ r_path_len,
-    int64_t session, int64_t now_ms) {
-  const int64_t i = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * TR_T +
-                    threadIdx.x;
+    int64_t* __restrict__ r_slot, int64_t* __restrict__ r_sizes,
+    int64_t* __restrict__ r_bsum, int64_t session, int64_t now_ms) {
+  const uint32_t blk = xcd_remap(blockIdx.x, gridDim.x);
+  const int64_t i = (int64_t)blk * TR_T + threadIdx.x;
   const bool live = i < ncap && i < *n_dev;
   const bool ok_req = live && q.status[i] == ST_OK;
   const ZkNodeStore& s = t.store;
@@ -388,6 +415,7 @@ __global__ __launch_bounds__(TR_T) void tree_serve_k(
   L.op = live ? q.opcode[i] : OP_PING;
   L.err = live && !ok_req ? ERR_BAD_ARGUMENTS : ERR_OK;
   L.node = -1;
+  L.slot = -1;
   L.par = -1;
   L.flags = 0;
   L.path = nullptr;
@@ -452,14 +480,20 @@ __global__ __launch_bounds__(TR_T) void tree_serve_k(
   if (ok_req && L.err == ERR_OK) {
     switch (L.op) {
       case OP_GET_DATA: case OP_EXISTS:
-        L.node = tree_find(t, L.path, L.pl);
+        {
+          const Found f = tree_lookup(t, L.path, L.pl);
+          L.node = f.node;
+          L.slot = f.slot;
+        }
         if (L.node < 0) L.err = ERR_NO_NODE;
         break;
       case OP_SET_DATA: {
-        const int64_t node = tree_find(t, L.path, L.pl);
+        const Found f = tree_lookup(t, L.path, L.pl);
+        const int64_t node = f.node;
         if (node < 0) { L.err = ERR_NO_NODE; break; }
+        L.slot = f.slot;
         if (L.dl > s.slot_cap[node]) { L.err = ERR_BAD_ARGUMENTS; break; }
-        uint8_t* slot = s.slab + s.slot_off[node];
+        uint8_t* slot = s.slab + L.slot;
         unsigned int* ver = (unsigned int*)(slot + 32);
         const int32_t want = L.flags;
         unsigned int old = *ver, cmp;
@@ -490,7 +524,8 @@ __global__ __launch_bounds__(TR_T) void tree_serve_k(
         }
         break;
       case OP_DELETE: {
-        const int64_t node = tree_find(t, L.path, L.pl);
+        const Found f = tree_lookup(t, L.path, L.pl);
+        const int64_t node = f.node, so = f.slot;
         if (node < 0) { L.err = ERR_NO_NODE; break; }
         if (__hip_atomic_load(&t.nchild[node], __ATOMIC_RELAXED,
                               __HIP_MEMORY_SCOPE_AGENT) > 0) {
@@ -498,14 +533,14 @@ __global__ __launch_bounds__(TR_T) void tree_serve_k(
           break;
         }
         const int32_t want = L.flags;
-        if (want != -1 && ld_be32(s.slab + s.slot_off[node] + 32) != want) {
+        if (want != -1 && ld_be32(s.slab + so + 32) != want) {
           L.err = ERR_BAD_VERSION;
           break;
         }
         if (!tree_erase(t, node, L.path, L.pl)) { L.err = ERR_NO_NODE; break; }
         L.par = t.node_parent[node];
         if (L.par >= 0) parent_touch(t, L.par, -1, true, L.zx);
-        st_be64(s.slab + s.slot_off[node] + 44, 0);   // ephemeralOwner
+        st_be64(s.slab + so + 44, 0);                 // ephemeralOwner
         freed = node;
         break;
       }
@@ -519,37 +554,70 @@ __global__ __launch_bounds__(TR_T) void tree_serve_k(
   if (create && L.err != ERR_OK && v >= 0) freed = v;  // return the claim
   wave_free(t, freed);
   wave_mark_dirty(t, L.err == ERR_OK ? L.par : -1);
+  if (r_sizes != nullptr) {                       // block-uniform
+    __shared__ int64_t sm[TR_T / 64 + 1];
+    int64_t sz = 0;
+    if (live) {
+      const bool get = L.err == ERR_OK && L.op == OP_GET_DATA;
+      const bool mk = L.err == ERR_OK && L.op == OP_CREATE;
+      sz = served_reply_size(L.op, L.err, get ? s.data_len[L.node] : 0,
+                             mk ? t.node_path_len[L.node] : 0);
+    }
+    if (i < ncap) r_sizes[i] = sz;
+    int64_t tot;
+    block_excl_scan(sz, sm, &tot);
+    if (threadIdx.x == 0) r_bsum[blk] = tot;
+  }
   if (!live) return;
   r_op[i] = L.op;
   r_xid[i] = q.xid[i];
   r_err[i] = L.err;
   r_node[i] = L.op == OP_DELETE ? -1 : L.node;
   r_zxid[i] = L.zx;
+  if (r_slot != nullptr) r_slot[i] = L.op == OP_DELETE ? -1 : L.slot;
 }
 
-// Rewrite the wire-format Stat words of every dirty parent from the shadows.
-__global__ __launch_bounds__(TR_T) void tree_fixup_k(ZkTree t, int64_t ncap) {
-  const int64_t k = (int64_t)blockIdx.x * TR_T + threadIdx.x;
-  if (k >= ncap || k >= t.counters[TC_DIRTY]) return;
-  const int64_t p = t.dirty_list[k];
-  uint8_t* slot = t.store.slab + t.store.slot_off[p];
-  st_be32(slot + 36, t.cver[p]);
-  st_be32(slot + 56, t.nchild[p]);
-  st_be64(slot + 60, t.pzxid[p]);
-  t.dirty[p] = 0;
-}
+// After a serve / expire launch, one kernel (grid-stride over a bounded
+// grid):
+//  1. rewrite the wire-format Stat words of every dirty parent from the
+//     shadows;
+//  2. the last block to finish publishes: make the nodes freed by the launch
+//     poppable, clamp a head that overshot the previously published tail,
+//     reset the dirty list and consume the launch's zxids (`*n_dev` for a
+//     batch of requests, 1 for a session expiry, which is one closeSession
+//     txn).  Every block reads the dirty count before it signs off on
+//     TC_DONE, so the reset cannot race a reader.
+constexpr int FIN_BLOCKS = 64;   // <= 64 sign-offs on one counter word
 
-// Between batches: make the nodes freed by the last launch poppable, clamp
-// a head that overshot the previously published tail, reset the dirty list
-// and consume the launch's zxids (`*n_dev` for a batch of requests, 1 for a
-// session expiry, which is one closeSession txn).
-__global__ void tree_publish_k(ZkTree t, const int64_t* n_dev,
-                               int64_t bump_zxid) {
+__global__ __launch_bounds__(TR_T) void tree_finish_k(ZkTree t,
+                                                     const int64_t* n_dev,
+                                                     int64_t bump_zxid) {
+  __shared__ int last;
   int64_t* c = t.counters;
+  const int64_t nd = c[TC_DIRTY];
+  for (int64_t k = (int64_t)blockIdx.x * TR_T + threadIdx.x; k < nd;
+       k += (int64_t)gridDim.x * TR_T) {
+    const int64_t p = t.dirty_list[k];
+    uint8_t* slot = t.store.slab + t.store.slot_off[p];
+    st_be32(slot + 36, t.cver[p]);
+    st_be32(slot + 56, t.nchild[p]);
+    st_be64(slot + 60, t.pzxid[p]);
+    t.dirty[p] = 0;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    last = atomicAdd((unsigned long long*)&c[TC_DONE], 1ull) ==
+           (unsigned long long)gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last || threadIdx.x != 0) return;
+  __threadfence();
   if (c[TC_FREE_HEAD] > c[TC_FREE_PUB]) c[TC_FREE_HEAD] = c[TC_FREE_PUB];
   c[TC_FREE_PUB] = c[TC_FREE_TAIL];
   c[TC_DIRTY] = 0;
   c[TC_ZXID] += n_dev != nullptr ? *n_dev : bump_zxid;
+  c[TC_DONE] = 0;
 }
 
 // Session expiry: remove every ephemeral node owned by `session`
@@ -605,24 +673,28 @@ int zk_tree_build(const ZkTree* t, int64_t n0, int64_t n, hipStream_t st) {
 
 static int finish_launch(const ZkTree* t, int64_t ncap, const int64_t* n_dev,
                          int64_t bump_zxid, hipStream_t st) {
-  zk::tree_fixup_k<<<(unsigned)((ncap + zk::TR_T - 1) / zk::TR_T), zk::TR_T,
-                     0, st>>>(*t, ncap);
-  ZK_LAUNCH_CHECK();
-  zk::tree_publish_k<<<1, 1, 0, st>>>(*t, n_dev, bump_zxid);
+  // the dirty list holds at most one parent per request
+  const int64_t nb = min((ncap + zk::TR_T - 1) / zk::TR_T,
+                         (int64_t)zk::FIN_BLOCKS);
+  zk::tree_finish_k<<<(unsigned)nb, zk::TR_T, 0, st>>>(*t, n_dev, bump_zxid);
   ZK_LAUNCH_CHECK();
   return 0;
 }
 
+// r_slot / r_sizes / r_bsum may be null (see tree_serve_k); r_bsum needs
+// ceil(ncap / 256) entries.
 int zk_tree_serve(const ZkTree* t, const uint8_t* rx, const ZkReqOut* q,
                   const int64_t* n_dev, int64_t ncap, int32_t* r_op,
                   int32_t* r_xid, int32_t* r_err, int64_t* r_node,
                   int64_t* r_zxid, int64_t* r_path_off, int32_t* r_path_len,
+                  int64_t* r_slot, int64_t* r_sizes, int64_t* r_bsum,
                   int64_t session, int64_t now_ms, hipStream_t st) {
   if (ncap <= 0) return 0;
+  if ((r_sizes == nullptr) != (r_bsum == nullptr)) return -1;
   zk::tree_serve_k<<<(unsigned)((ncap + zk::TR_T - 1) / zk::TR_T), zk::TR_T,
                      0, st>>>(*t, rx, *q, n_dev, ncap, r_op, r_xid, r_err,
-                              r_node, r_zxid, r_path_off, r_path_len, session,
-                              now_ms);
+                              r_node, r_zxid, r_path_off, r_path_len, r_slot,
+                              r_sizes, r_bsum, session, now_ms);
   ZK_LAUNCH_CHECK();
   // at most one dirty parent per request
   return finish_launch(t, ncap, n_dev, 0, st);

@@ -1,0 +1,84 @@
+"""Diagnostic: run the GET pipeline's server half step by step and check
+the serve kernel's reply descriptors on the host before the reply encode."""
+import ctypes
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), '..', '..'))
+from zkmi.ops import _lib  # noqa: E402
+from zkmi.ops import batch as B  # noqa: E402
+from zkmi.bench import synthetic as S  # noqa: E402
+
+
+def main():
+    dev = torch.device('cuda', 0)
+    tree = S.GpuTree(20000, 37, fanout=100, device=dev)
+    n = 8192
+    ht = tree.ht.view(-1, 4).cpu()
+    live = ht[:, 1] >= 0
+    print('entries', int(live.sum()), 'slot range',
+          int(ht[live, 3].min()), int(ht[live, 3].max()), 'slab',
+          tree.slab_cap, flush=True)
+    p = S.GetPipeline(tree, n)
+    g = p._phases(True, torch.zeros(1, dtype=torch.int64, device=dev))
+    next(g)                       # request encode issued
+    torch.cuda.synchronize()
+    print('encode ok', flush=True)
+    srv = p.server
+    tx = p.tx
+    L = _lib.lib()
+    # the server half by hand; the paused generator holds `total`
+    total = g.gi_frame.f_locals['total']
+    ntx = int(total.item())
+    ft = B.frame_scan(tx, ntx, cap=srv.cap_frames, window=srv.window)
+    rt = B.decode_requests(tx, ft, out=srv.rt)
+    torch.cuda.synchronize()
+    print('scan+decode ok, frames', int(ft.count.item()), flush=True)
+    r = srv.resp
+    r.count = ft.count
+    r.slot.fill_(-7)
+    q = rt.struct()
+    _lib.check(L.zk_tree_serve(
+        ctypes.byref(tree.struct), _lib.ptr(tx), ctypes.byref(q),
+        _lib.ptr(ft.count), srv.cap_frames, _lib.ptr(r.opcode),
+        _lib.ptr(r.xid), _lib.ptr(r.err), _lib.ptr(r.node),
+        _lib.ptr(r.zxid), _lib.ptr(r.path_off), _lib.ptr(r.path_len),
+        _lib.ptr(r.slot), None if os.environ.get('NOSIZES') else _lib.ptr(srv.presized[0]),
+        None if os.environ.get('NOSIZES') else _lib.ptr(srv.presized[1]), 0, int(time.time() * 1000),
+        _lib.stream_ptr()), 'serve')
+    torch.cuda.synchronize()
+    print('serve ok', flush=True)
+    print('raw slot head', r.slot[:4].cpu().tolist(), 'want', tree.slot_off[r.node[:4]].cpu().tolist(), flush=True)
+    if os.environ.get('NOSIZES'):
+        idx = r.slot[:4].cpu().tolist()
+        for k in idx:
+            print('row', k, tree.ht.view(-1, 4)[k].cpu().tolist(), flush=True)
+        print('nodes', r.node[:4].cpu().tolist(), flush=True)
+        return
+    err = r.err[:n].cpu()
+    slot = r.slot[:n].cpu()
+    node = r.node[:n].cpu()
+    sizes = srv.presized[0][:n].cpu()
+    nb = (n + 255) // 256
+    bsum = srv.presized[1][:nb].cpu()
+    print('err!=0', int((err != 0).sum()), 'slot', int(slot.min()),
+          int(slot.max()), 'node', int(node.min()), int(node.max()),
+          'sizes', int(sizes.min()), int(sizes.max()),
+          'bsum ok', bool((bsum == sizes.view(nb, 256).sum(1)).all()),
+          flush=True)
+    want = tree.slot_off[node.to(dev)].cpu()
+    good = bool((want == slot).all())
+    print('slot==slot_off[node]', good, flush=True)
+    if not good:
+        return
+    p2 = S.GetPipeline(tree, n)
+    for _ in range(3):
+        acc = p2.step()
+        print('step ok', int(acc.item()), flush=True)
+
+
+if __name__ == '__main__':
+    main()

@@ -108,9 +108,9 @@ class GpuTree(object):
                                      minlength=ndirs)[:ndirs]
         nk = torch.from_numpy(nkids).to(dev)
         hcap = _next_pow2(2 * cap)
-        # interleaved {key, val} entries (csrc/kernels/tree.hip)
-        self.ht = torch.zeros(2 * hcap, dtype=I64, device=dev)
-        self.ht.view(-1, 2)[:, 1] = -3
+        # interleaved 16-byte {key, val} entries (csrc/kernels/tree.hip)
+        self.ht = torch.zeros(_lib.HT_WORDS * hcap, dtype=I64, device=dev)
+        self.ht.view(-1, _lib.HT_WORDS)[:, 1] = -3
         cnt = [0] * _lib.TC_N
         cnt[_lib.TC_NODES], cnt[_lib.TC_ZXID] = nst, nst
         cnt[_lib.TC_PATH_TOP], cnt[_lib.TC_SLAB_TOP] = len(arena), nst * sb
@@ -169,7 +169,7 @@ class GpuTree(object):
         One host read of the node high-water mark."""
         n = int(self.counters[_lib.TC_NODES].item())
         self.ht.zero_()
-        self.ht.view(-1, 2)[:, 1] = -3
+        self.ht.view(-1, _lib.HT_WORDS)[:, 1] = -3
         _lib.check(_lib.lib().zk_tree_build(ctypes.byref(self._struct), 0,
                                             min(n, self.cap),
                                             _lib.stream_ptr()),
@@ -220,7 +220,10 @@ class GpuServer(object):
             torch.zeros(cap_frames, dtype=I64, device=dev),
             torch.zeros(cap_frames, dtype=I32, device=dev),
             tree.path_arena,
-            torch.zeros(cap_frames, dtype=I32, device=dev), None)
+            torch.zeros(cap_frames, dtype=I32, device=dev), None,
+            torch.empty(cap_frames, dtype=I64, device=dev))
+        # the serve kernel sizes the replies itself (presized K13 encode)
+        self.presized = B.response_workspace(cap_frames, dev)
         self.out = torch.empty(out_cap, dtype=U8, device=dev)
         self.cap_frames = cap_frames
         self.ws = None
@@ -240,10 +243,13 @@ class GpuServer(object):
             _lib.ptr(ft.count), self.cap_frames, _lib.ptr(r.opcode),
             _lib.ptr(r.xid), _lib.ptr(r.err), _lib.ptr(r.node),
             _lib.ptr(r.zxid), _lib.ptr(r.path_off), _lib.ptr(r.path_len),
+            _lib.ptr(r.slot), _lib.ptr(self.presized[0]),
+            _lib.ptr(self.presized[1]),
             session, int(time.time() * 1000), _lib.stream_ptr()),
             'zk_tree_serve')
         out, rec_off, total, err = B.encode_responses(
-            r, self.tree.store, self.out.numel(), out=self.out)
+            r, self.tree.store, self.out.numel(), out=self.out,
+            presized=self.presized)
         return out, total, err, ft
 
 

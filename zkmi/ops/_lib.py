@@ -70,7 +70,9 @@ class ZkTree(ctypes.Structure):
 
 # ZkTree counters (csrc/kernels/tree.hip TC_*)
 TC_NODES, TC_ZXID, TC_PATH_TOP, TC_SLAB_TOP = 0, 1, 2, 3
-TC_FREE_HEAD, TC_FREE_TAIL, TC_FREE_PUB, TC_DIRTY, TC_N = 4, 5, 6, 7, 8
+TC_FREE_HEAD, TC_FREE_TAIL, TC_FREE_PUB, TC_DIRTY = 4, 5, 6, 7
+TC_DONE, TC_N = 8, 9
+HT_WORDS = 2     # int64 words per hash entry {key, val}
 
 
 _SIGS = {
@@ -97,8 +99,8 @@ _SIGS = {
                                           P]),
     'zk_tree_build': (I32, [P, I64, I64, P]),
     'zk_tree_fill': (I32, [P, I64, I64, P, I64, P]),
-    'zk_tree_serve': (I32, [P, P, P, P, I64, P, P, P, P, P, P, P, I64, I64,
-                            P]),
+    'zk_tree_serve': (I32, [P, P, P, P, I64, P, P, P, P, P, P, P, P, P, P,
+                            I64, I64, P]),
     'zk_tree_expire': (I32, [P, I64, I64, P, P]),
     'zk_bench_gen_get': (I32, [I64, ctypes.c_uint64, I64, I64, I32, P, P, P,
                                P, P, P, P]),

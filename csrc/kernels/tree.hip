@@ -59,6 +59,7 @@ struct ZkTree {
   int64_t* pzxid;              // [cap] host-endian pzxid
   int32_t* dirty;              // [cap] parent-on-dirty-list flag
   int64_t* dirty_list;         // [cap]
+  int64_t* node_pw;            // [cap] path word: offset << 24 | length
 };
 }
 
@@ -166,10 +167,27 @@ ZK_DEV bool bytes_eq(const uint8_t* a, const uint8_t* b, int32_t n) {
 
 ZK_DEV int64_t* ht_key(const ZkTree& t, int64_t s) { return &t.ht[2 * s]; }
 ZK_DEV int64_t* ht_val(const ZkTree& t, int64_t s) { return &t.ht[2 * s + 1]; }
-ZK_DEV bool path_is(const ZkTree& t, int64_t v, const uint8_t* p, int32_t n) {
-  return t.node_path_len[v] == n &&
-         bytes_eq(t.path_arena + t.node_path_off[v], p, n);
+// Node v's path as one word (offset << 24 | length; paths < 16 MiB like
+// the frames that carry them): a lookup verifies against it with one random
+// read instead of two (node_path_off / node_path_len stay the primary
+// record; create keeps the word in step).
+ZK_DEV int64_t pw_pack(int64_t off, int32_t len) {
+  return (off << 24) | (int64_t)(uint32_t)len;
 }
+ZK_DEV bool path_is(const ZkTree& t, int64_t v, const uint8_t* p, int32_t n) {
+  const int64_t pw = t.node_pw[v];
+  return (int32_t)(pw & 0xFFFFFF) == n &&
+         bytes_eq(t.path_arena + (pw >> 24), p, n);
+}
+
+// A hash val holds the node index (low 32 bits) and its slot offset / 16
+// (high 32; slots are 16-byte aligned), so a hit needs no slot_off[v] read.
+// Tombstone (-2) and being-published (-3) stay negative.
+ZK_DEV int64_t val_pack(int64_t v, int64_t slot) {
+  return (int64_t)(((uint64_t)slot >> 4) << 32) | v;
+}
+ZK_DEV int64_t val_node(int64_t x) { return x & 0xFFFFFFFFll; }
+ZK_DEV int64_t val_slot(int64_t x) { return (int64_t)((uint64_t)x >> 32) << 4; }
 
 // Node of path p (node -1 if absent) and its slot offset.
 struct Found {
@@ -187,8 +205,8 @@ ZK_DEV Found tree_lookup(const ZkTree& t, const uint8_t* p, int32_t n) {
     const int64_t k = ent[0];
     const int64_t v = ent[1];
     if (k == 0) break;
-    if (k == key && v >= 0 && path_is(t, v, p, n))
-      return Found{v, t.store.slot_off[v]};
+    if (k == key && v >= 0 && path_is(t, val_node(v), p, n))
+      return Found{val_node(v), val_slot(v)};
     s = (s + 1) & t.mask;
   }
   return Found{-1, -1};
@@ -203,12 +221,13 @@ ZK_DEV int64_t tree_find(const ZkTree& t, const uint8_t* p, int32_t n) {
 ZK_DEV int64_t tree_insert(const ZkTree& t, int64_t v, const uint8_t* p,
                            int32_t n) {
   const int64_t key = (int64_t)(path_hash(p, n) | 1ull);
+  const int64_t pv = val_pack(v, t.store.slot_off[v]);
   int64_t s = key & t.mask;
   for (int64_t probe = 0; probe <= t.mask; ++probe) {
     const int64_t k = atomicCAS((unsigned long long*)ht_key(t, s), 0ull,
                                 (unsigned long long)key);
     if (k == 0) {                         // claimed an empty slot
-      __hip_atomic_store(ht_val(t, s), v, __ATOMIC_RELAXED,
+      __hip_atomic_store(ht_val(t, s), pv, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
       return v;
     }
@@ -218,10 +237,10 @@ ZK_DEV int64_t tree_insert(const ZkTree& t, int64_t v, const uint8_t* p,
       for (int spin = 0; spin < 1000000 && w == -3; ++spin)
         w = __hip_atomic_load(ht_val(t, s), __ATOMIC_RELAXED,
                               __HIP_MEMORY_SCOPE_AGENT);
-      if (w >= 0 && path_is(t, w, p, n)) return w;
+      if (w >= 0 && path_is(t, val_node(w), p, n)) return val_node(w);
       if (w == -2 &&                      // tombstone of the same key: reuse
           atomicCAS((unsigned long long*)ht_val(t, s), (unsigned long long)-2,
-                    (unsigned long long)v) == (unsigned long long)-2)
+                    (unsigned long long)pv) == (unsigned long long)-2)
         return v;
     }
     s = (s + 1) & t.mask;
@@ -238,11 +257,15 @@ ZK_DEV bool tree_erase(const ZkTree& t, int64_t v, const uint8_t* p,
   for (int64_t probe = 0; probe <= t.mask; ++probe) {
     const int64_t k = *ht_key(t, s);
     if (k == 0) return false;
-    if (k == key && atomicCAS((unsigned long long*)ht_val(t, s),
-                              (unsigned long long)v,
-                              (unsigned long long)-2) ==
-                        (unsigned long long)v)
-      return true;
+    if (k == key) {
+      const int64_t cur = __hip_atomic_load(ht_val(t, s), __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT);
+      if (cur >= 0 && val_node(cur) == v &&
+          atomicCAS((unsigned long long*)ht_val(t, s),
+                    (unsigned long long)cur,
+                    (unsigned long long)-2) == (unsigned long long)cur)
+        return true;
+    }
     s = (s + 1) & t.mask;
   }
   return false;
@@ -378,6 +401,7 @@ ZK_DEV int32_t do_create(const ZkTree& t, Lane& L, const uint8_t* data,
   t.nchild[v] = 0;
   t.pzxid[v] = L.zx;
   t.node_parent[v] = par;
+  t.node_pw[v] = pw_pack(pd - t.path_arena, npl);
   // No fence before publishing v in the hash: only a same-batch reader of
   // this very path could observe the half-written node (unordered by the
   // batch contract; every field it could read is in bounds), and the next

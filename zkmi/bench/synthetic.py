@@ -87,6 +87,10 @@ class GpuTree(object):
         self.node_path_len = torch.zeros(cap, dtype=I32, device=dev)
         self.node_path_off[:nst] = torch.from_numpy(poff).to(dev)
         self.node_path_len[:nst] = torch.from_numpy(plen).to(dev)
+        # path word (offset << 24 | length) the hash lookups verify against
+        self.node_pw = torch.zeros(cap, dtype=I64, device=dev)
+        self.node_pw[:nst] = torch.from_numpy(
+            (poff << 24) | plen.astype(np.int64)).to(dev)
         self.node_parent = torch.full((cap,), -1, dtype=I64, device=dev)
         self.node_parent[:nst] = torch.from_numpy(parents).to(dev)
         # wire-format slots; data capacity >= 128 so sets can grow
@@ -94,6 +98,8 @@ class GpuTree(object):
         sb = slot_bytes(dcap)
         self.slot = sb
         self.slab_cap = cap * sb
+        # hash vals pack node (32 bits) and slot offset / 16 (31 bits)
+        assert cap < (1 << 31) and self.slab_cap < (1 << 35), 'tree too big'
         g = torch.Generator(device=dev)
         g.manual_seed(seed)
         self.slab = torch.randint(0, 256, (self.slab_cap,), dtype=U8,
@@ -146,7 +152,8 @@ class GpuTree(object):
                            self.free_list.data_ptr(), self.cap,
                            self.cver.data_ptr(), self.nchild.data_ptr(),
                            self.pzxid.data_ptr(), self.dirty.data_ptr(),
-                           self.dirty_list.data_ptr())
+                           self.dirty_list.data_ptr(),
+                           self.node_pw.data_ptr())
 
     @property
     def struct(self):

@@ -65,7 +65,8 @@ class ZkTree(ctypes.Structure):
                 ('node_parent', P), ('path_arena', P), ('path_cap', I64),
                 ('slab_cap', I64), ('counters', P), ('store', ZkNodeStore),
                 ('free_list', P), ('free_cap', I64), ('cver', P),
-                ('nchild', P), ('pzxid', P), ('dirty', P), ('dirty_list', P)]
+                ('nchild', P), ('pzxid', P), ('dirty', P), ('dirty_list', P),
+                ('node_pw', P)]
 
 
 # ZkTree counters (csrc/kernels/tree.hip TC_*)

@@ -233,14 +233,13 @@ class GpuServer(object):
         self.presized = B.response_workspace(cap_frames, dev)
         self.out = torch.empty(out_cap, dtype=U8, device=dev)
         self.cap_frames = cap_frames
-        self.ws = None
+        self.scanner = B.FrameScanner(cap_frames, dev, window=window)
 
     def serve(self, rx, n, session=0):
         """Serve the request stream ``rx[:n]`` for ``session`` (the owner of
         any EPHEMERAL node it creates)."""
         L = _lib.lib()
-        ft = B.frame_scan(rx, n, cap=self.cap_frames, workspace=self.ws,
-                          window=self.window)
+        ft = self.scanner.scan(rx, n)
         rt = B.decode_requests(rx, ft, out=self.rt)
         r = self.resp
         r.count = ft.count
@@ -301,6 +300,7 @@ class GetPipeline(object):
         self.server = GpuServer(tree, n, n * (4 + 16 + 4 + dmax + 68) + 64,
                                 window=B.frame_window(17 + maxpath))
         self.rwindow = B.frame_window(4 + 16 + 4 + dmax + 68)
+        self.rscanner = B.FrameScanner(n, dev, window=self.rwindow)
         self.reply = B.alloc_replies(n, dev)
         self.xid_base = 0
         self.last = None
@@ -364,7 +364,7 @@ class GetPipeline(object):
         rx, rtotal, rerr, _ = self.server.serve(tx, ntx)
         yield
         nrx = int(rtotal.item())
-        ft = B.frame_scan(rx, nrx, cap=n, window=self.rwindow)
+        ft = self.rscanner.scan(rx, nrx)
         rep = B.decode_replies(rx, ft, self.xt, out=self.reply)
         self.last = (self.idx, rep, rx, ft)
         if not validate:

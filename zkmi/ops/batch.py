@@ -313,6 +313,39 @@ def frame_window(max_frame):
     return FS_WINDOWS[-1]
 
 
+class FrameScanner:
+    """Reusable K1 state for a stream that is scanned again and again (a
+    connection's RX ring, the benchmark's request / reply streams): the
+    workspace and the frame table are allocated once and grown on demand,
+    so a scan issued right after a host read-back starts with one launch
+    instead of four allocations."""
+
+    def __init__(self, cap, device, window=2048,
+                 max_packet=consts.MAX_PACKET):
+        self.cap = cap
+        self.window = window
+        self.max_packet = max_packet
+        self.table = FrameTable(torch.empty(cap, dtype=I64, device=device),
+                                torch.empty(cap, dtype=I32, device=device),
+                                torch.empty(4, dtype=I64, device=device))
+        self.ws = torch.empty(0, dtype=U8, device=device)
+        self.ws_for = -1            # stream length the workspace covers
+
+    def scan(self, buf, n, stream=None):
+        L = _lib.lib()
+        if n > self.ws_for:
+            wsb = L.zk_frame_scan_workspace(max(n, 2 * self.ws_for))
+            self.ws = torch.empty(max(wsb, 256), dtype=U8,
+                                  device=buf.device)
+            self.ws_for = max(n, 2 * self.ws_for)
+        t = self.table
+        check(L.zk_frame_scan2(ptr(buf), n, self.max_packet, ptr(self.ws),
+                               self.ws.numel(), ptr(t.off), ptr(t.length),
+                               self.cap, ptr(t.result), int(self.window),
+                               stream_ptr(stream)), 'zk_frame_scan')
+        return t
+
+
 def frame_scan(buf, n=None, max_packet=consts.MAX_PACKET, cap=None,
                stream=None, workspace=None, window=2048):
     """K1: split ``buf[:n]`` (uint8 device tensor) into frames.
@@ -321,7 +354,8 @@ def frame_scan(buf, n=None, max_packet=consts.MAX_PACKET, cap=None,
     stream of ``n`` bytes can hold).  ``window`` is the per-tile fast-path
     entry window (256..2048 bytes, see :func:`frame_window`): a hint for
     the usual frame size, never a limit — longer frames are framed exactly
-    on a slower path."""
+    on a slower path.  (:class:`FrameScanner` keeps the buffers across
+    calls.)"""
     L = _lib.lib()
     if n is None:
         n = buf.numel()

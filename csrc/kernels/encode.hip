@@ -183,6 +183,7 @@ struct GSink {
   ZK_DEV void be64(int64_t v) { st_be64(o, v); o += 8; }
   ZK_DEV void u8(uint32_t b) { *o++ = (uint8_t)b; }
   ZK_DEV void bytes(const uint8_t* s, int64_t n) { copy_bytes(o, s, n); o += n; }
+  ZK_DEV void put4(uint32_t x) { __builtin_memcpy(o, &x, 4); o += 4; }
   ZK_DEV void finish() {}
 };
 
@@ -240,22 +241,74 @@ ZK_DEV void k_buffer(K& k, const uint8_t* src, int32_t len) {
   k.bytes(src, len);
 }
 
+// dword k of a register array of 16-byte vectors (k constant after
+// unrolling, so the array stays in VGPRs)
+ZK_DEV uint32_t vword(const uint4* v, int k) {
+  const uint4& q = v[k >> 2];
+  switch (k & 3) {
+    case 0: return q.x;
+    case 1: return q.y;
+    case 2: return q.z;
+    default: return q.w;
+  }
+}
+
+// GET_DATA replies with up to this much data are emitted from registers.
+constexpr int GET_REG_DATA = 128;
+
 template <class K>
 ZK_DEV void emit_response(K& k, const ZkRespBatch& r, const ZkNodeStore& s,
                           int64_t i, int64_t body) {
+  const int32_t xid = r.xid[i], err = r.err[i], op = r.opcode[i];
+  const int64_t zxid = r.zxid[i];
+  const int64_t nd = body - 16 - STAT_BYTES;          // GET: 4 + data length
+  if (err == ERR_OK && op == OP_GET_DATA && nd <= 4 + GET_REG_DATA) {
+    // Fast path: every load of the record is issued before the first
+    // sink write (the generic copy below waits on each 16-byte load in
+    // turn, ~11 dependent round trips per reply).  Whole 16-byte vectors
+    // from the slot start to the end of the data stay inside the slot:
+    // slot_bytes rounds the data capacity up to 16 and adds 4.
+    constexpr int NV = (ZK_SLOT_DATA + GET_REG_DATA + 15) / 16;
+    constexpr int W0 = ZK_SLOT_LEN / 4;               // [len | data] dword
+    const uint8_t* slot = s.slab + (r.slot ? r.slot[i]
+                                           : s.slot_off[r.node[i]]);
+    const int nv = (int)((ZK_SLOT_LEN + nd + 15) >> 4);
+    uint4 v[NV];
+#pragma unroll
+    for (int j = 0; j < NV; ++j)
+      v[j] = j < nv ? *(const uint4*)(slot + 16 * j) : make_uint4(0, 0, 0, 0);
+    k.be32((int32_t)body);
+    k.be32(xid);
+    k.be64(zxid);
+    k.be32(err);
+    const int wfull = (int)(nd >> 2), tb = (int)(nd & 3);
+#pragma unroll
+    for (int w = 0; w < NV * 4 - W0; ++w) {
+      if (w < wfull) {
+        k.put4(vword(v, W0 + w));
+      } else if (w == wfull && tb) {
+        const uint32_t x = vword(v, W0 + w);
+        for (int b = 0; b < tb; ++b) k.u8(x >> (8 * b));
+      }
+    }
+#pragma unroll
+    for (int w = 0; w < STAT_BYTES / 4; ++w) k.put4(vword(v, w));
+    k.finish();
+    return;
+  }
   k.be32((int32_t)body);
-  k.be32(r.xid[i]);
-  k.be64(r.zxid[i]);
-  k.be32(r.err[i]);
-  if (r.err[i] == ERR_OK) {
-    switch (r.opcode[i]) {
+  k.be32(xid);
+  k.be64(zxid);
+  k.be32(err);
+  if (err == ERR_OK) {
+    switch (op) {
       case OP_GET_DATA: {
         // wire-format slot: [len | data] then Stat — two contiguous copies.
         // The data length is implied by the frame size (header 16, length
         // word 4, Stat 68), so only the slot itself is read.
         const uint8_t* slot = s.slab + (r.slot ? r.slot[i]
                                                : s.slot_off[r.node[i]]);
-        k.bytes(slot + ZK_SLOT_LEN, body - 16 - STAT_BYTES);
+        k.bytes(slot + ZK_SLOT_LEN, nd);
         k.bytes(slot + ZK_SLOT_STAT, STAT_BYTES);
         break;
       }

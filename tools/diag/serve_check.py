@@ -17,11 +17,9 @@ def main():
     dev = torch.device('cuda', 0)
     tree = S.GpuTree(20000, 37, fanout=100, device=dev)
     n = 8192
-    ht = tree.ht.view(-1, 4).cpu()
+    ht = tree.ht.view(-1, _lib.HT_WORDS).cpu()
     live = ht[:, 1] >= 0
-    print('entries', int(live.sum()), 'slot range',
-          int(ht[live, 3].min()), int(ht[live, 3].max()), 'slab',
-          tree.slab_cap, flush=True)
+    print('entries', int(live.sum()), flush=True)
     p = S.GetPipeline(tree, n)
     g = p._phases(True, torch.zeros(1, dtype=torch.int64, device=dev))
     next(g)                       # request encode issued
@@ -46,18 +44,11 @@ def main():
         _lib.ptr(ft.count), srv.cap_frames, _lib.ptr(r.opcode),
         _lib.ptr(r.xid), _lib.ptr(r.err), _lib.ptr(r.node),
         _lib.ptr(r.zxid), _lib.ptr(r.path_off), _lib.ptr(r.path_len),
-        _lib.ptr(r.slot), None if os.environ.get('NOSIZES') else _lib.ptr(srv.presized[0]),
-        None if os.environ.get('NOSIZES') else _lib.ptr(srv.presized[1]), 0, int(time.time() * 1000),
+        _lib.ptr(r.slot), _lib.ptr(srv.presized[0]),
+        _lib.ptr(srv.presized[1]), 0, int(time.time() * 1000),
         _lib.stream_ptr()), 'serve')
     torch.cuda.synchronize()
     print('serve ok', flush=True)
-    print('raw slot head', r.slot[:4].cpu().tolist(), 'want', tree.slot_off[r.node[:4]].cpu().tolist(), flush=True)
-    if os.environ.get('NOSIZES'):
-        idx = r.slot[:4].cpu().tolist()
-        for k in idx:
-            print('row', k, tree.ht.view(-1, 4)[k].cpu().tolist(), flush=True)
-        print('nodes', r.node[:4].cpu().tolist(), flush=True)
-        return
     err = r.err[:n].cpu()
     slot = r.slot[:n].cpu()
     node = r.node[:n].cpu()

@@ -62,10 +62,14 @@ int main(int argc, char** argv) {
     CK(hipMemset(prof, 0, tiles * 64));
     CK(hipMemcpyToSymbol(HIP_SYMBOL(zk::g_fe_prof), &prof, sizeof(prof)));
     hipEvent_t a, b; CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
+    constexpr int W = (int)zk::FS_W;
+    const size_t lds = zk::fe_lds(W);
     for (int i = 0; i < 2; ++i)
-      zk::fs_frontier<(int)zk::FS_W><<<(unsigned)tiles, zk::FE_T, zk::fe_lds((int)zk::FS_W)>>>(d, n, 16 << 20, f0, surv);
+      zk::fs_frontier<W><<<(unsigned)tiles, zk::FE_T, lds>>>(
+          d, n, 16 << 20, f0, surv);
     CK(hipEventRecord(a));
-    zk::fs_frontier<(int)zk::FS_W><<<(unsigned)tiles, zk::FE_T, zk::fe_lds((int)zk::FS_W)>>>(d, n, 16 << 20, f0, surv);
+    zk::fs_frontier<W><<<(unsigned)tiles, zk::FE_T, lds>>>(
+        d, n, 16 << 20, f0, surv);
     CK(hipEventRecord(b)); CK(hipEventSynchronize(b));
     float ms; CK(hipEventElapsedTime(&ms, a, b));
     std::vector<uint64_t> p(tiles * 8);

@@ -21,10 +21,9 @@ ZK_DEV uint64_t splitmix64(uint64_t x) {
 
 __global__ __launch_bounds__(BG_T) void bench_gen_get(
     int64_t n, uint64_t seed, int64_t leaf0, int64_t nleaves,
-    int32_t xid_base, const int64_t* __restrict__ node_path_off,
-    const int32_t* __restrict__ node_path_len, int64_t* __restrict__ idx,
-    int32_t* __restrict__ xid, int64_t* __restrict__ path_off,
-    int32_t* __restrict__ path_len) {
+    int32_t xid_base, const int64_t* __restrict__ node_pw,
+    int64_t* __restrict__ idx, int32_t* __restrict__ xid,
+    int64_t* __restrict__ path_off, int32_t* __restrict__ path_len) {
   const int64_t i = (int64_t)blockIdx.x * BG_T + threadIdx.x;
   if (i >= n) return;
   const uint64_t r = splitmix64(seed ^ (uint64_t)i * 0xD1B54A32D192ED03ull);
@@ -32,8 +31,9 @@ __global__ __launch_bounds__(BG_T) void bench_gen_get(
   const int64_t v = leaf0 + (int64_t)(((r >> 32) * (uint64_t)nleaves) >> 32);
   idx[i] = v;
   xid[i] = (int32_t)(((uint32_t)xid_base + (uint32_t)i) & 0x7fffffffu);
-  path_off[i] = node_path_off[v];
-  path_len[i] = node_path_len[v];
+  const int64_t pw = node_pw[v];           // offset << 24 | length (tree.hip)
+  path_off[i] = pw >> 24;
+  path_len[i] = (int32_t)(pw & 0xFFFFFF);
 }
 
 // Grid-stride with a bounded grid: one device-scope atomic per block, and a
@@ -126,13 +126,13 @@ int zk_bench_check_notif(int64_t total, int64_t n_per, const uint64_t* seeds,
 }
 
 int zk_bench_gen_get(int64_t n, uint64_t seed, int64_t leaf0, int64_t nleaves,
-                     int32_t xid_base, const int64_t* node_path_off,
-                     const int32_t* node_path_len, int64_t* idx, int32_t* xid,
-                     int64_t* path_off, int32_t* path_len, hipStream_t st) {
+                     int32_t xid_base, const int64_t* node_pw, int64_t* idx,
+                     int32_t* xid, int64_t* path_off, int32_t* path_len,
+                     hipStream_t st) {
   if (n <= 0) return 0;
   zk::bench_gen_get<<<(unsigned)((n + zk::BG_T - 1) / zk::BG_T), zk::BG_T, 0,
-                      st>>>(n, seed, leaf0, nleaves, xid_base, node_path_off,
-                            node_path_len, idx, xid, path_off, path_len);
+                      st>>>(n, seed, leaf0, nleaves, xid_base, node_pw, idx,
+                            xid, path_off, path_len);
   ZK_LAUNCH_CHECK();
   return 0;
 }

@@ -452,11 +452,44 @@ __global__ __launch_bounds__(ENC_T) void resp_write(
 }
 
 // ---------------------------------------------------------------- K10 write
+constexpr int REQ_REG_PATH = 64;   // read-request paths emitted from registers
+
 template <class K>
 ZK_DEV void emit_request(K& k, const ZkReqBatch& b, int64_t i, int64_t body) {
   const int32_t op = b.opcode[i];
+  const int32_t xid = b.xid[i];
+  if ((op == OP_GET_DATA || op == OP_EXISTS || op == OP_GET_CHILDREN ||
+       op == OP_GET_CHILDREN2) && b.path_len[i] > 0 &&
+      b.path_len[i] <= REQ_REG_PATH) {
+    // Fast path for the read requests: the path (<= 64 bytes) is loaded as
+    // unaligned dwords inside its own bytes, all before the first sink
+    // write, instead of one dependent round trip per 16-byte piece.
+    const int32_t pl = b.path_len[i];
+    const uint8_t* src = b.path_arena + b.path_off[i];
+    const int32_t watch = b.arg[i];
+    uint32_t w[REQ_REG_PATH / 4];
+#pragma unroll
+    for (int j = 0; j < REQ_REG_PATH / 4; ++j) {
+      w[j] = 0;
+      if (4 * j + 4 <= pl) __builtin_memcpy(&w[j], src + 4 * j, 4);
+    }
+    uint32_t tail = 0;
+    const int32_t nw = pl >> 2, tb = pl & 3;
+    for (int q = 0; q < tb; ++q) tail |= (uint32_t)src[4 * nw + q] << (8 * q);
+    k.be32((int32_t)body);
+    k.be32(xid);
+    k.be32(op);
+    k.be32(pl);
+#pragma unroll
+    for (int j = 0; j < REQ_REG_PATH / 4; ++j)
+      if (j < nw) k.put4(w[j]);
+    for (int q = 0; q < tb; ++q) k.u8(tail >> (8 * q));
+    k.u8(watch ? 1 : 0);
+    k.finish();
+    return;
+  }
   k.be32((int32_t)body);
-  k.be32(b.xid[i]);
+  k.be32(xid);
   k.be32(op);
   if (op == OP_PING || op == OP_CLOSE_SESSION) {
     k.finish();

@@ -349,9 +349,9 @@ class GetPipeline(object):
         self.step_no += 1
         _lib.check(L.zk_bench_gen_get(
             n, seed, t.leaf0, t.n_leaves, self.xid_base,
-            _lib.ptr(t.node_path_off), _lib.ptr(t.node_path_len),
-            _lib.ptr(self.idx), _lib.ptr(self.xid), _lib.ptr(self.poff),
-            _lib.ptr(self.plen), sp), 'zk_bench_gen_get')
+            _lib.ptr(t.node_pw), _lib.ptr(self.idx), _lib.ptr(self.xid),
+            _lib.ptr(self.poff), _lib.ptr(self.plen), sp),
+            'zk_bench_gen_get')
         xid = self.xid
         self.xid_base = (self.xid_base + n) & 0x7fffffff
         rb = B.RequestBatch(n, self.opcode, xid, self.arg, self.poff,
@@ -755,9 +755,9 @@ class WatchPipeline(object):
         self.step_no += 1
         _lib.check(L.zk_bench_gen_get(
             n, seeds[self.rank], t.leaf0, t.n_leaves, 0,
-            _lib.ptr(t.node_path_off), _lib.ptr(t.node_path_len),
-            _lib.ptr(self.idx), _lib.ptr(self.xid), _lib.ptr(self.poff),
-            _lib.ptr(self.plen), sp), 'zk_bench_gen_get')
+            _lib.ptr(t.node_pw), _lib.ptr(self.idx), _lib.ptr(self.xid),
+            _lib.ptr(self.poff), _lib.ptr(self.plen), sp),
+            'zk_bench_gen_get')
         _, _, total, err = B.encode_responses(self.resp, t.store,
                                               self.tx.numel(), out=self.tx)
         rx, nrx = self._gather(total)

@@ -103,7 +103,7 @@ _SIGS = {
     'zk_tree_serve': (I32, [P, P, P, P, I64, P, P, P, P, P, P, P, P, P, P,
                             I64, I64, P]),
     'zk_tree_expire': (I32, [P, I64, I64, P, P]),
-    'zk_bench_gen_get': (I32, [I64, ctypes.c_uint64, I64, I64, I32, P, P, P,
+    'zk_bench_gen_get': (I32, [I64, ctypes.c_uint64, I64, I64, I32, P, P,
                                P, P, P, P]),
     'zk_bench_check_get': (I32, [I64, P, P, P, P, P, P, P, P, P, P, P]),
     'zk_bench_check_notif': (I32, [I64, I64, P, I64, I64, P, P, P, P, P, P,

@@ -18,6 +18,27 @@ namespace zk {
 
 constexpr int DEC_T = 256;
 
+// A Stat already in registers: the frame's last 68 bytes as 17 dwords in
+// memory order (see decode_replies_k).
+ZK_DEV void read_stat_regs(const uint32_t* w, const ZkReplyOut& o, int64_t i) {
+  const int64_t c = o.cap;
+  auto b32 = [&](int k) { return (int32_t)bswap32(w[k]); };
+  auto b64 = [&](int k) {
+    return (int64_t)(((uint64_t)bswap32(w[k]) << 32) | bswap32(w[k + 1]));
+  };
+  o.stat64[0 * c + i] = b64(0);
+  o.stat64[1 * c + i] = b64(2);
+  o.stat64[2 * c + i] = b64(4);
+  o.stat64[3 * c + i] = b64(6);
+  o.stat32[0 * c + i] = b32(8);
+  o.stat32[1 * c + i] = b32(9);
+  o.stat32[2 * c + i] = b32(10);
+  o.stat64[4 * c + i] = b64(11);
+  o.stat32[3 * c + i] = b32(13);
+  o.stat32[4 * c + i] = b32(14);
+  o.stat64[5 * c + i] = b64(15);
+}
+
 ZK_DEV bool read_stat(const uint8_t* p, const ZkReplyOut& o, int64_t i) {
   const int64_t c = o.cap;
   o.stat64[0 * c + i] = ld_be64(p + 0);
@@ -76,12 +97,23 @@ __global__ __launch_bounds__(DEC_T) void decode_replies_k(
   int32_t plen = 0, a0 = 0, a1 = 0;
   int32_t xid = 0, err = 0;
   int64_t zxid = 0;
+  // Every reply that carries a Stat ends with it (data + Stat, Stat,
+  // children + Stat, ACL + Stat: zk-buffer.js:333-362), so the frame's last
+  // 68 bytes are loaded together with the header instead of after the
+  // opcode lookup and the data length; they are used when the body is
+  // exactly "prefix + Stat" (else the Stat is read where the prefix ends).
+  // (issued after the opcode lookup's load: vmcnt retires loads in order,
+  // so the Stat loads then overlap that lookup instead of delaying it)
+  uint32_t hw[4] = {0, 0, 0, 0};
+  if (L >= 16) __builtin_memcpy(hw, p, 16);
+  const bool tail_ok = L >= 16 + STAT_BYTES;
+  uint32_t sw[STAT_BYTES / 4];
   if (L < 16) {
     status = ST_BAD_DECODE;
   } else {
-    xid = ld_be32(p);
-    zxid = ld_be64(p + 4);
-    err = ld_be32(p + 12);
+    xid = (int32_t)bswap32(hw[0]);
+    zxid = (int64_t)(((uint64_t)bswap32(hw[1]) << 32) | bswap32(hw[2]));
+    err = (int32_t)bswap32(hw[3]);
     switch (xid) {
       case XID_NOTIFICATION: op = OP_NOTIFICATION; break;
       case XID_PING: op = OP_PING; break;
@@ -94,6 +126,7 @@ __global__ __launch_bounds__(DEC_T) void decode_replies_k(
       }
     }
   }
+  if (tail_ok) __builtin_memcpy(sw, p + L - STAT_BYTES, STAT_BYTES);
   if (status == ST_OK && err == ERR_OK) {
     const uint8_t* b = p + 16;
     const int64_t A = L - 16;
@@ -105,12 +138,14 @@ __global__ __launch_bounds__(DEC_T) void decode_replies_k(
         if (4 + (int64_t)dl + STAT_BYTES > A) { status = ST_BAD_DECODE; break; }
         poff = foff[i] + 20;
         plen = dl;
-        read_stat(b + 4 + dl, o, i);
+        if (tail_ok && 4 + (int64_t)dl + STAT_BYTES == A) read_stat_regs(sw, o, i);
+        else read_stat(b + 4 + dl, o, i);
         break;
       }
       case OP_EXISTS: case OP_SET_DATA:
         if (A < STAT_BYTES) { status = ST_BAD_DECODE; break; }
-        read_stat(b, o, i);
+        if (tail_ok && A == STAT_BYTES) read_stat_regs(sw, o, i);
+        else read_stat(b, o, i);
         break;
       case OP_CREATE: {
         if (A < 4) { status = ST_BAD_DECODE; break; }
@@ -131,7 +166,8 @@ __global__ __launch_bounds__(DEC_T) void decode_replies_k(
         a0 = cnt;
         if (op == OP_GET_CHILDREN2) {
           if (4 + k + STAT_BYTES > A) { status = ST_BAD_DECODE; break; }
-          read_stat(b + 4 + k, o, i);
+          if (tail_ok && 4 + k + STAT_BYTES == A) read_stat_regs(sw, o, i);
+          else read_stat(b + 4 + k, o, i);
         }
         break;
       }
@@ -143,7 +179,8 @@ __global__ __launch_bounds__(DEC_T) void decode_replies_k(
         poff = foff[i] + 20;
         plen = (int32_t)k;
         a0 = cnt;
-        read_stat(b + 4 + k, o, i);
+        if (tail_ok && 4 + k + STAT_BYTES == A) read_stat_regs(sw, o, i);
+        else read_stat(b + 4 + k, o, i);
         break;
       }
       case OP_NOTIFICATION: {

@@ -192,8 +192,13 @@ ZK_DEV int64_t val_slot(int64_t x) { return (int64_t)((uint64_t)x >> 32) << 4; }
 // Node of path p (node -1 if absent) and its slot offset.
 struct Found {
   int64_t node, slot;
+  int32_t dlen;      // data length (DLEN lookups only)
 };
 
+// DLEN: also fetch the node's data length, issued with the path-word load
+// right after the hash hit (before verification) so a GET's reply size is
+// not one more dependent round trip.
+template <bool DLEN = false>
 ZK_DEV Found tree_lookup(const ZkTree& t, const uint8_t* p, int32_t n) {
   const int64_t key = (int64_t)(path_hash(p, n) | 1ull);
   int64_t s = key & t.mask;
@@ -205,11 +210,14 @@ ZK_DEV Found tree_lookup(const ZkTree& t, const uint8_t* p, int32_t n) {
     const int64_t k = ent[0];
     const int64_t v = ent[1];
     if (k == 0) break;
-    if (k == key && v >= 0 && path_is(t, val_node(v), p, n))
-      return Found{val_node(v), val_slot(v)};
+    if (k == key && v >= 0) {
+      const int64_t node = val_node(v);
+      const int32_t dl = DLEN ? t.store.data_len[node] : 0;
+      if (path_is(t, node, p, n)) return Found{node, val_slot(v), dl};
+    }
     s = (s + 1) & t.mask;
   }
-  return Found{-1, -1};
+  return Found{-1, -1, 0};
 }
 
 ZK_DEV int64_t tree_find(const ZkTree& t, const uint8_t* p, int32_t n) {
@@ -344,7 +352,7 @@ ZK_DEV void put_seq10(uint8_t* d, int32_t x) {
 
 // Per-lane state of one request through the three phases of tree_serve_k.
 struct Lane {
-  int32_t op, err, pl, dl, flags;
+  int32_t op, err, pl, dl, flags, dlen;
   int64_t node, zx, par, slot;
   const uint8_t* path;
 };
@@ -440,6 +448,7 @@ __global__ __launch_bounds__(TR_T) void tree_serve_k(
   L.err = live && !ok_req ? ERR_BAD_ARGUMENTS : ERR_OK;
   L.node = -1;
   L.slot = -1;
+  L.dlen = 0;
   L.par = -1;
   L.flags = 0;
   L.path = nullptr;
@@ -505,9 +514,10 @@ __global__ __launch_bounds__(TR_T) void tree_serve_k(
     switch (L.op) {
       case OP_GET_DATA: case OP_EXISTS:
         {
-          const Found f = tree_lookup(t, L.path, L.pl);
+          const Found f = tree_lookup<true>(t, L.path, L.pl);
           L.node = f.node;
           L.slot = f.slot;
+          L.dlen = f.dlen;
         }
         if (L.node < 0) L.err = ERR_NO_NODE;
         break;
@@ -584,7 +594,7 @@ __global__ __launch_bounds__(TR_T) void tree_serve_k(
     if (live) {
       const bool get = L.err == ERR_OK && L.op == OP_GET_DATA;
       const bool mk = L.err == ERR_OK && L.op == OP_CREATE;
-      sz = served_reply_size(L.op, L.err, get ? s.data_len[L.node] : 0,
+      sz = served_reply_size(L.op, L.err, get ? L.dlen : 0,
                              mk ? t.node_path_len[L.node] : 0);
     }
     if (i < ncap) r_sizes[i] = sz;

@@ -429,16 +429,28 @@ ZK_DEV void staged_emit(int64_t r0, int64_t r1, const int64_t* off,
   }
 }
 
+// Terminated streams: four 0xFF bytes (frame length -1, BAD_LENGTH) right
+// after the stream when they fit.  A frame scan run over a host-known upper
+// bound of the stream length then stops exactly at the stream end, so the
+// pipeline needs no device-to-host read of the length before scanning.
+ZK_DEV void put_terminator(bool term, const int64_t* total, uint8_t* out,
+                           int64_t cap) {
+  if (!term || blockIdx.x != 0 || threadIdx.x != 0) return;
+  const int64_t T = *total;
+  if (T + 4 <= cap) st_be32(out + T, -1);
+}
+
 __global__ __launch_bounds__(ENC_T) void resp_write(
     ZkRespBatch r, ZkNodeStore s, const int64_t* __restrict__ n_dev,
     int64_t ncap, const int64_t* __restrict__ sizes,
     const int64_t* __restrict__ bbase, int64_t* __restrict__ rec_off,
     const int64_t* __restrict__ total, uint8_t* __restrict__ out, int64_t cap,
-    int32_t* __restrict__ err) {
+    int32_t* __restrict__ err, int32_t term) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lw[];
   __shared__ EncLocal E;
   const int64_t n = min(*n_dev, ncap);
   const int64_t r0 = (int64_t)blockIdx.x * ENC_T;
+  put_terminator(term, total, out, cap);
   if (r0 >= n) return;
   if (*total > cap) {
     if (r0 == 0 && threadIdx.x == 0) atomicOr(err, 2);
@@ -531,10 +543,11 @@ __global__ __launch_bounds__(ENC_T) void req_write(
     const int64_t* __restrict__ bbase, int64_t* __restrict__ rec_off,
     const int64_t* __restrict__ total, uint8_t* __restrict__ out, int64_t cap,
     int64_t* __restrict__ xid_tab, int64_t xid_mask,
-    int32_t* __restrict__ err) {
+    int32_t* __restrict__ err, int32_t term) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lw[];
   __shared__ EncLocal E;
   const int64_t r0 = (int64_t)blockIdx.x * ENC_T;
+  put_terminator(term, total, out, cap);
   if (r0 >= n) return;
   if (*total > cap) {                       // capacity guard (whole batch)
     if (r0 == 0 && threadIdx.x == 0) atomicOr(err, 2);
@@ -589,11 +602,17 @@ static inline unsigned nblk(int64_t n) {
 
 extern "C" {
 
-int zk_encode_requests(const ZkReqBatch* b, int64_t n, int64_t* sizes,
-                       int64_t* rec_off, int64_t* total, int64_t* scan_ws,
-                       uint8_t* out, int64_t out_cap, int64_t* xid_tab,
-                       int64_t xid_mask, int32_t* err, hipStream_t st) {
-  if (n <= 0) return hipMemsetAsync(total, 0, 8, st);
+// terminate != 0: four 0xFF bytes follow the stream (put_terminator).
+int zk_encode_requests2(const ZkReqBatch* b, int64_t n, int64_t* sizes,
+                        int64_t* rec_off, int64_t* total, int64_t* scan_ws,
+                        uint8_t* out, int64_t out_cap, int64_t* xid_tab,
+                        int64_t xid_mask, int32_t* err, int32_t terminate,
+                        hipStream_t st) {
+  if (n <= 0) {
+    int rc = hipMemsetAsync(total, 0, 8, st);
+    if (!rc && terminate && out_cap >= 4) rc = hipMemsetAsync(out, 0xFF, 4, st);
+    return rc;
+  }
   const unsigned nb = zk::nblk(n);
   int64_t* bsum = scan_ws;                 // zk_scan_workspace(n) >= 2 nb
   int64_t* bbase = scan_ws + nb;
@@ -603,9 +622,17 @@ int zk_encode_requests(const ZkReqBatch* b, int64_t n, int64_t* sizes,
   if (rc) return rc;
   zk::req_write<<<nb, zk::ENC_T, zk::STAGE_BYTES, st>>>(
       *b, n, sizes, bbase, rec_off, total, out, out_cap, xid_tab, xid_mask,
-      err);
+      err, terminate);
   ZK_LAUNCH_CHECK();
   return 0;
+}
+
+int zk_encode_requests(const ZkReqBatch* b, int64_t n, int64_t* sizes,
+                       int64_t* rec_off, int64_t* total, int64_t* scan_ws,
+                       uint8_t* out, int64_t out_cap, int64_t* xid_tab,
+                       int64_t xid_mask, int32_t* err, hipStream_t st) {
+  return zk_encode_requests2(b, n, sizes, rec_off, total, scan_ws, out,
+                             out_cap, xid_tab, xid_mask, err, 0, st);
 }
 
 // Returns the frame length through *frame_len (device int64): 4 + body.
@@ -653,8 +680,12 @@ int zk_encode_responses2(const ZkRespBatch* r, const ZkNodeStore* s,
                          const int64_t* n_dev, int64_t ncap, int64_t* sizes,
                          int64_t* rec_off, int64_t* total, int64_t* scan_ws,
                          uint8_t* out, int64_t out_cap, int32_t* err,
-                         int32_t presized, hipStream_t st) {
-  if (ncap <= 0) return hipMemsetAsync(total, 0, 8, st);
+                         int32_t presized, int32_t terminate, hipStream_t st) {
+  if (ncap <= 0) {
+    int rc = hipMemsetAsync(total, 0, 8, st);
+    if (!rc && terminate && out_cap >= 4) rc = hipMemsetAsync(out, 0xFF, 4, st);
+    return rc;
+  }
   const unsigned nb = zk::nblk(ncap);
   int64_t* bsum = scan_ws;
   int64_t* bbase = scan_ws + nb;
@@ -666,7 +697,8 @@ int zk_encode_responses2(const ZkRespBatch* r, const ZkNodeStore* s,
   int rc = zk_scan_small_i64(bsum, bbase, nb, total, st);
   if (rc) return rc;
   zk::resp_write<<<nb, zk::ENC_T, zk::STAGE_BYTES, st>>>(
-      *r, *s, n_dev, ncap, sizes, bbase, rec_off, total, out, out_cap, err);
+      *r, *s, n_dev, ncap, sizes, bbase, rec_off, total, out, out_cap, err,
+      terminate);
   ZK_LAUNCH_CHECK();
   return 0;
 }
@@ -677,7 +709,7 @@ int zk_encode_responses(const ZkRespBatch* r, const ZkNodeStore* s,
                         uint8_t* out, int64_t out_cap, int32_t* err,
                         hipStream_t st) {
   return zk_encode_responses2(r, s, n_dev, ncap, sizes, rec_off, total,
-                              scan_ws, out, out_cap, err, 0, st);
+                              scan_ws, out, out_cap, err, 0, 0, st);
 }
 
 }  // extern "C"

@@ -120,6 +120,33 @@ def test_frame_scan_bad_length_exact(gpu, window):
 
 
 @pytest.mark.parametrize('window', [256, 2048])
+def test_terminated_stream_scans_over_a_bound(gpu, window):
+    """K10 terminate=True + K1 over a host upper bound (stale bytes after
+    the terminator) frames exactly the encoded stream: the sync-free
+    pipeline contract."""
+    from zkmi.ops import batch as B
+    r = synth.rng(11)
+    pkts = [{'xid': i, 'opcode': 'GET_DATA', 'watch': bool(i & 1),
+             'path': '/p/%d' % r.randint(0, 10 ** r.randint(1, 9))}
+            for i in range(5000)]
+    rb = B.pack_requests(pkts, gpu)
+    cap = 64 * len(pkts) + (1 << 16)
+    out = torch.randint(0, 256, (cap,), dtype=torch.uint8, device=gpu)
+    tx, _, total, err = B.encode_requests(rb, out=out, terminate=True)
+    ft = B.frame_scan(tx, cap, window=window)
+    res = ft.host_result()
+    want = b''.join(jute.frame(jute.encode_request(p)) for p in pkts)
+    assert int(total.item()) == len(want) and int(err.item()) == 0
+    assert bytes(tx[:len(want)].cpu().numpy().tobytes()) == want
+    assert res['frames'] == len(pkts)
+    assert res['consumed'] == len(want) and res['bad']
+    frames, _, _ = jute.scan_frames(want)
+    got = list(zip(ft.off[:len(pkts)].cpu().tolist(),
+                   ft.length[:len(pkts)].cpu().tolist()))
+    assert got == frames
+
+
+@pytest.mark.parametrize('window', [256, 2048])
 def test_frame_scan_large_multi_level(gpu, window):
     """> 256 tiles forces the hierarchical composition path."""
     from zkmi.ops import batch as B

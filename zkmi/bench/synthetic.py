@@ -13,8 +13,9 @@ ZooKeeper wire format:
           (via the xid table), data (offset/length) and Stat
 
 plus a device-side check that every reply is OK and carries the node the
-request asked for.  Nothing is skipped inside a step; the only host work is
-reading back the two stream lengths (needed to size the frame-scan grids).
+request asked for.  Nothing is skipped inside a step, and a step makes no
+device-to-host read: both streams are terminated and frame-scanned over
+host-known upper bounds of their lengths.
 
 :class:`MixPipeline` does the same for the create/set/delete mix with
 version CAS and ACL encode (BASELINE config 3).
@@ -235,9 +236,11 @@ class GpuServer(object):
         self.cap_frames = cap_frames
         self.scanner = B.FrameScanner(cap_frames, dev, window=window)
 
-    def serve(self, rx, n, session=0):
+    def serve(self, rx, n, session=0, terminate=False):
         """Serve the request stream ``rx[:n]`` for ``session`` (the owner of
-        any EPHEMERAL node it creates)."""
+        any EPHEMERAL node it creates).  ``n`` may be an upper bound of a
+        terminated stream (see :func:`zkmi.ops.batch.encode_requests`);
+        ``terminate`` terminates the reply stream the same way."""
         L = _lib.lib()
         ft = self.scanner.scan(rx, n)
         rt = B.decode_requests(rx, ft, out=self.rt)
@@ -255,7 +258,7 @@ class GpuServer(object):
             'zk_tree_serve')
         out, rec_off, total, err = B.encode_responses(
             r, self.tree.store, self.out.numel(), out=self.out,
-            presized=self.presized)
+            presized=self.presized, terminate=terminate)
         return out, total, err, ft
 
 
@@ -301,6 +304,16 @@ class GetPipeline(object):
                                 window=B.frame_window(17 + maxpath))
         self.rwindow = B.frame_window(4 + 16 + 4 + dmax + 68)
         self.rscanner = B.FrameScanner(n, dev, window=self.rwindow)
+        # Both streams are terminated (four 0xFF bytes after the last
+        # frame) and scanned over host-known upper bounds of their lengths,
+        # so a step has no device-to-host read at all.  The reply bound uses
+        # the largest data length in the tree now: a GET pipeline does not
+        # mutate it (a reply beyond the bound would be missed and fail the
+        # per-reply check, never pass silently).
+        maxdata = int(tree.data_len.max().item())
+        self.req_bound = min(n * (17 + maxpath) + 4, self.tx.numel())
+        self.rep_bound = min(n * (4 + 16 + 4 + max(maxdata, 0) + 68) + 4,
+                             self.server.out.numel())
         self.reply = B.alloc_replies(n, dev)
         self.xid_base = 0
         self.last = None
@@ -339,8 +352,9 @@ class GetPipeline(object):
         return acc if validate else None
 
     def _phases(self, validate, acc):
-        """The step as a generator that yields before each host read-back
-        (the two stream lengths), on the caller's current stream."""
+        """The step as a generator on the caller's current stream, yielding
+        between client encode, server and client decode (a multi-stream
+        step interleaves the connections' phases)."""
         t = self.tree
         n = self.batch
         L = _lib.lib()
@@ -358,13 +372,13 @@ class GetPipeline(object):
                             self.plen, self.zero64, self.zero32, self.zero32,
                             t.path_arena, t.slab, self.acl_off,
                             self.acl_len, self.acl_arena)
-        tx, rec_off, total, err = B.encode_requests(rb, self.xt, out=self.tx)
+        tx, rec_off, total, err = B.encode_requests(rb, self.xt, out=self.tx,
+                                                    terminate=True)
         yield
-        ntx = int(total.item())
-        rx, rtotal, rerr, _ = self.server.serve(tx, ntx)
+        rx, rtotal, rerr, _ = self.server.serve(tx, self.req_bound,
+                                                terminate=True)
         yield
-        nrx = int(rtotal.item())
-        ft = self.rscanner.scan(rx, nrx)
+        ft = self.rscanner.scan(rx, self.rep_bound)
         rep = B.decode_replies(rx, ft, self.xt, out=self.reply)
         self.last = (self.idx, rep, rx, ft)
         if not validate:

@@ -82,11 +82,13 @@ _SIGS = {
     'zk_scan_excl_i64': (I32, [P, P, I64, P, P, P]),
     'zk_scan_excl_i32': (I32, [P, P, I64, P, P, P]),
     'zk_encode_requests': (I32, [P, I64, P, P, P, P, P, I64, P, I64, P, P]),
+    'zk_encode_requests2': (I32, [P, I64, P, P, P, P, P, I64, P, I64, P, I32,
+                                  P]),
     'zk_encode_set_watches': (I32, [P, P, P, I64, I64, I64, I64, P, P, P, P,
                                     P, I64, P, P]),
     'zk_encode_responses': (I32, [P, P, P, I64, P, P, P, P, P, I64, P, P]),
     'zk_encode_responses2': (I32, [P, P, P, I64, P, P, P, P, P, I64, P, I32,
-                                   P]),
+                                   I32, P]),
     'zk_frame_scan_workspace': (I64, [I64]),
     'zk_frame_scan': (I32, [P, I64, I64, P, I64, P, P, I64, P, P]),
     'zk_frame_scan2': (I32, [P, I64, I64, P, I64, P, P, I64, P, I32, P]),

@@ -155,13 +155,16 @@ def _total_err(dev):
     return z[0:1], z[1:2].view(I32)[0:1]
 
 
-def encode_requests(batch, xid_table=None, out=None, stream=None):
+def encode_requests(batch, xid_table=None, out=None, stream=None,
+                    terminate=False):
     """K10: encode ``batch`` into one framed byte stream.
 
     Returns ``(stream_bytes, rec_off, total)`` — ``total`` is a device
     int64 scalar; ``stream_bytes`` is the full output buffer (use
     ``[:total]``).  When ``out`` is None a buffer sized on the host from the
-    batch is allocated (one small D2H copy)."""
+    batch is allocated (one small D2H copy).  ``terminate``: four 0xFF bytes
+    follow the stream when they fit, so :func:`frame_scan` over any host
+    upper bound of its length stops exactly at its end (BAD_LENGTH there)."""
     L = _lib.lib()
     n = batch.n
     dev = batch.opcode.device
@@ -177,9 +180,10 @@ def encode_requests(batch, xid_table=None, out=None, stream=None):
     tab = xid_table.tab if xid_table is not None else None
     mask = xid_table.mask if xid_table is not None else 0
     s = batch.struct()
-    check(L.zk_encode_requests(ctypes_ref(s), n, ptr(sizes), ptr(rec_off),
-                               ptr(total), ptr(ws), ptr(out), out.numel(),
-                               ptr(tab), mask, ptr(err), stream_ptr(stream)),
+    check(L.zk_encode_requests2(ctypes_ref(s), n, ptr(sizes), ptr(rec_off),
+                                ptr(total), ptr(ws), ptr(out), out.numel(),
+                                ptr(tab), mask, ptr(err),
+                                1 if terminate else 0, stream_ptr(stream)),
           'zk_encode_requests')
     batch._keep = (s, sizes, ws, err)
     return out, rec_off[:n], total, err
@@ -576,7 +580,7 @@ def response_workspace(cap, device):
 
 
 def encode_responses(resp, store_struct, out_cap, out=None, stream=None,
-                     presized=None):
+                     presized=None, terminate=False):
     """K13: server-mode reply encode -> (bytes, rec_off, total, err).
     ``presized``: the (sizes, workspace) pair of :func:`response_workspace`
     already filled by the producer; the sizes pass is then skipped."""
@@ -598,7 +602,7 @@ def encode_responses(resp, store_struct, out_cap, out=None, stream=None,
                                  ptr(rec_off), ptr(total), ptr(ws), ptr(out),
                                  out.numel(), ptr(err),
                                  1 if presized is not None else 0,
-                                 stream_ptr(stream)),
+                                 1 if terminate else 0, stream_ptr(stream)),
           'zk_encode_responses')
     return out, rec_off, total, err
 

@@ -18,6 +18,11 @@ wire path on the GPU (see zkmi/bench/synthetic.py): client request encode
 K2-K4) -> on-device check of every reply.  Synthetic data: random 100-byte
 node payloads, uniformly random node per request.
 
+Each GPU serves its batch over ``--streams`` (default 2) pipelined
+connections, each on its own HIP stream with its own buffers and xid table;
+a step makes no device-to-host read (terminated streams, frame-scanned over
+host-known length bounds), so the connections' kernels overlap.
+
 One process per GPU (torchrun); per-GPU work is fixed (weak scaling).  The
 whole-node aggregate (sum over ranks of ops / max-rank time) is reported.
 ``p50_get_rtt_us`` is the interactive path: one blocking ``Client.get``
@@ -87,9 +92,13 @@ def main():
     ap.add_argument('--nodes', type=int, default=1_000_000)
     ap.add_argument('--data-bytes', type=int, default=100)
     ap.add_argument('--no-rtt', action='store_true')
-    ap.add_argument('--streams', type=int, default=1,
+    ap.add_argument('--streams', type=int, default=2,
                     help='get: pipelined connections per GPU, one HIP '
-                         'stream each (the batch is split between them)')
+                         'stream each (the batch is split between them; 2 '
+                         'overlaps one connection\'s latency-bound kernels '
+                         'with the other\'s bandwidth-bound ones, more '
+                         'streams than GPU_MAX_HW_QUEUES allows were '
+                         'unstable)')
     ap.add_argument('--workload', choices=('get', 'mix', 'storm', 'watch'),
                     default='get')
     a = ap.parse_args()

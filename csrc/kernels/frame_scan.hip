@@ -337,9 +337,57 @@ __global__ __launch_bounds__(FS_T) void fs_exits(const uint8_t* __restrict__ buf
 // is bounded: each hop claims a fresh position, so <= S hops in total.
 constexpr int FE_T = 256;
 // LDS of fs_frontier<W>: staged tile, owner table, W results, hand-off area
+// Windows of <= 256 entries keep walker ids in bytes plus a claimed-bit
+// map ("narrow" owner table: 18 KiB instead of 32 KiB, and only the 2 KiB
+// bit map is zeroed per tile), so a CU holds 4 frontier blocks, not 3.
+constexpr bool fe_narrow(int W) { return W <= 256; }
 inline size_t fe_lds(int W) {
-  return (FS_S + 16) + FS_S * 2 + (size_t)W * 2 + 66 * 4;
+  const size_t own = fe_narrow(W) ? FS_S + FS_S / 8 : FS_S * 2;
+  return (FS_S + 16) + own + (size_t)W * 2 + 66 * 4;
 }
+
+// Owner table of fs_frontier: get(q) = claiming walker id + 1, 0 = none.
+// Narrow: set() writes the id byte, then ORs the claimed bit with release
+// order; get() reads the bit with acquire order, then the byte, so a bit
+// seen set always comes with its (last) writer's byte.  Wide: one uint16
+// per position, written and read whole.
+template <bool NARROW>
+struct FeOwners {
+  uint8_t* base;                     // NARROW: [S] bytes, then [S/32] bits
+  ZK_DEV uint32_t* bits() const { return (uint32_t*)(base + FS_S); }
+  ZK_DEV uint32_t get(int32_t q) const {
+    if constexpr (NARROW) {
+      const uint32_t w = __hip_atomic_load(&bits()[q >> 5], __ATOMIC_ACQUIRE,
+                                           __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (!((w >> (q & 31)) & 1u)) return 0;
+      return (uint32_t)*(volatile const uint8_t*)(base + q) + 1u;
+    } else {
+      return ((const uint16_t*)base)[q];
+    }
+  }
+  // re-read by the lane that just claimed q (its own bit is set)
+  ZK_DEV uint32_t get_claimed(int32_t q) const {
+    if constexpr (NARROW)
+      return (uint32_t)*(volatile const uint8_t*)(base + q) + 1u;
+    else
+      return *(volatile const uint16_t*)((const uint16_t*)base + q);
+  }
+  ZK_DEV void set(int32_t q, int32_t e) const {
+    if constexpr (NARROW) {
+      *(volatile uint8_t*)(base + q) = (uint8_t)e;
+      __hip_atomic_fetch_or(&bits()[q >> 5], 1u << (q & 31),
+                            __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    } else {
+      ((uint16_t*)base)[q] = (uint16_t)(e + 1);
+    }
+  }
+  // zero before use (narrow: the bits only)
+  ZK_DEV void clear(int tid, int nt) const {
+    const int n16 = NARROW ? FS_S / 128 : FS_S / 8;
+    uint4* z = NARROW ? (uint4*)bits() : (uint4*)base;
+    for (int k = tid; k < n16; k += nt) z[k] = make_uint4(0, 0, 0, 0);
+  }
+};
 constexpr uint16_t F0_MERGE = 0x4000;        // | parent walker id (< 2048)
 
 ZK_DEV bool f0_is_merge(uint16_t v) { return (v & 0xF800) == F0_MERGE; }
@@ -420,10 +468,12 @@ __global__ __launch_bounds__(FE_T) void fs_frontier(
     uint16_t* __restrict__ f0, int32_t* __restrict__ surv) {
   constexpr int FE_K = W / FE_T;             // walkers per thread (1..8)
   static_assert(W % FE_T == 0 && FE_K >= 1 && FE_K <= 8, "window");
+  constexpr bool NARROW = fe_narrow(W);
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint8_t* sb = smem;                                      // [S + 16]
-  uint16_t* own = (uint16_t*)(smem + FS_S + 16);           // [S] id+1 / 0
-  uint16_t* res = own + FS_S;                              // [W]
+  const FeOwners<NARROW> own{smem + FS_S + 16};            // owner table
+  uint16_t* res = (uint16_t*)(smem + FS_S + 16 +
+                              (NARROW ? FS_S + FS_S / 8 : FS_S * 2));  // [W]
   uint32_t* hand = (uint32_t*)(res + W);                   // [64] + 2 ctrs
   const int64_t t = blockIdx.x;
   FE_MARK(0);
@@ -431,8 +481,7 @@ __global__ __launch_bounds__(FE_T) void fs_frontier(
   const int32_t nrel = (int32_t)min(n - ts, (int64_t)1 << 30);
   const int32_t maxp32 = (int32_t)min(maxp, (int64_t)1 << 30);
   stage_tile<FE_T>(buf, n, ts, sb, threadIdx.x);
-  for (int k = threadIdx.x; k < FS_S / 8; k += FE_T)
-    ((uint4*)own)[k] = make_uint4(0, 0, 0, 0);
+  own.clear(threadIdx.x, FE_T);
   if (threadIdx.x < 2) hand[64 + threadIdx.x] = 0;
   __syncthreads();
   int32_t pos[FE_K], nq[FE_K];
@@ -441,7 +490,7 @@ __global__ __launch_bounds__(FE_T) void fs_frontier(
   for (int k = 0; k < FE_K; ++k) {
     const int32_t e = threadIdx.x + k * FE_T;
     pos[k] = e;
-    own[e] = (uint16_t)(e + 1);
+    own.set(e, e);
     act |= 1u << k;
   }
   __syncthreads();
@@ -465,10 +514,10 @@ __global__ __launch_bounds__(FE_T) void fs_frontier(
                     ? fe_hop(lo[k], hi[k], pos[k], nrel, maxp32, nq[k])
                     : FE_GO;
     }
-    uint16_t o[FE_K];
+    uint32_t o[FE_K];
 #pragma unroll
     for (int k = 0; k < FE_K; ++k)
-      o[k] = ((act & (1u << k)) && code[k] == FE_GO) ? own[nq[k]] : 0;
+      o[k] = ((act & (1u << k)) && code[k] == FE_GO) ? own.get(nq[k]) : 0;
 #pragma unroll
     for (int k = 0; k < FE_K; ++k) {
       if (!(act & (1u << k))) continue;
@@ -480,7 +529,7 @@ __global__ __launch_bounds__(FE_T) void fs_frontier(
         res[e] = (uint16_t)(F0_MERGE | (o[k] - 1));
         act &= ~(1u << k);
       } else {
-        own[nq[k]] = (uint16_t)(e + 1);
+        own.set(nq[k], e);
       }
     }
     if (__popc(act)) atomicAdd(&hand[64 + (r & 1)], (uint32_t)__popc(act));
@@ -488,14 +537,14 @@ __global__ __launch_bounds__(FE_T) void fs_frontier(
     const uint32_t live = hand[64 + (r & 1)];
     if (threadIdx.x == 0) hand[64 + ((r + 1) & 1)] = 0;
     // phase 2: the last writer of own[q] owns it; the others merge into it
-    uint16_t o2[FE_K];
+    uint32_t o2[FE_K];
 #pragma unroll
-    for (int k = 0; k < FE_K; ++k) o2[k] = (act & (1u << k)) ? own[nq[k]] : 0;
+    for (int k = 0; k < FE_K; ++k) o2[k] = (act & (1u << k)) ? own.get(nq[k]) : 0;
 #pragma unroll
     for (int k = 0; k < FE_K; ++k) {
       if (!(act & (1u << k))) continue;
       const int32_t e = threadIdx.x + k * FE_T;
-      if (o2[k] != (uint16_t)(e + 1)) {
+      if (o2[k] != (uint32_t)(e + 1)) {
         res[e] = (uint16_t)(F0_MERGE | (o2[k] - 1));
         act &= ~(1u << k);
       } else {
@@ -549,7 +598,7 @@ __global__ __launch_bounds__(FE_T) void fs_frontier(
       }
       int32_t q = 0;
       bool claim = false;
-      uint16_t ow = 0;
+      uint32_t ow = 0;
       if (a) {
         uint32_t lo, hi;
         fe_words(sb, p, lo, hi);
@@ -558,7 +607,7 @@ __global__ __launch_bounds__(FE_T) void fs_frontier(
           res[e] = code;
           a = false;
         } else {
-          ow = own[q];
+          ow = own.get(q);
           claim = true;
         }
       }
@@ -567,14 +616,14 @@ __global__ __launch_bounds__(FE_T) void fs_frontier(
         a = false;
         claim = false;
       }
-      if (claim) own[q] = (uint16_t)(e + 1);
+      if (claim) own.set(q, e);
       if (__popcll(__ballot(claim)) > 1) {
         // several lanes may have claimed the same q: LDS ops of a wave
         // execute in order, so this re-read sees every lane's write
         if (claim) {
           // volatile: the compiler must not forward this lane's own store
-          const uint16_t o2 = *(volatile const uint16_t*)&own[q];
-          if (o2 != (uint16_t)(e + 1)) {
+          const uint32_t o2 = own.get_claimed(q);
+          if (o2 != (uint32_t)(e + 1)) {
             res[e] = (uint16_t)(F0_MERGE | (o2 - 1));
             a = false;
             claim = false;

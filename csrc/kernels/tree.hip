@@ -586,6 +586,8 @@ __global__ __launch_bounds__(TR_T) void tree_serve_k(
   }
   // ---- phase C: wave-aggregated frees and dirty parents -----------------
   if (create && L.err != ERR_OK && v >= 0) freed = v;  // return the claim
+  // (A read-only block could skip these claims, but guarding them with a
+  // block vote cost the create storm 10% in measurement; they stay.)
   wave_free(t, freed);
   wave_mark_dirty(t, L.err == ERR_OK ? L.par : -1);
   if (r_sizes != nullptr) {                       // block-uniform

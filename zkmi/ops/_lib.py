@@ -15,7 +15,9 @@ import os
 import torch  # noqa: F401  (must precede the HIP library load)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, 'libzkmi_hip.so')
+# ZKMI_HIP_LIB: an alternative build of the same library (A/B runs)
+LIB_PATH = os.environ.get('ZKMI_HIP_LIB') or os.path.join(_HERE,
+                                                          'libzkmi_hip.so')
 
 P = ctypes.c_void_p
 I64 = ctypes.c_int64

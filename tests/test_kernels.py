@@ -345,6 +345,21 @@ def test_gpu_get_pipeline_end_to_end(gpu):
         assert bytes(hb[po[k]:po[k] + 37].tobytes()) == data
 
 
+def test_gpu_get_pipeline_two_connections(gpu):
+    """The bench's default shape: the batch split over two pipelined
+    connections (own HIP streams, buffers, xid tables), no host read-back
+    inside a step; every reply checked on the device, the accumulator read
+    on the caller's stream."""
+    from zkmi.bench.synthetic import GetPipeline
+    tree = _small_tree(gpu, 20000, 37)
+    pipe = GetPipeline(tree, 8193, streams=2)
+    acc = torch.zeros(1, dtype=torch.int64, device=gpu)
+    for _ in range(3):
+        pipe.step(acc=acc)
+    assert int(acc.item()) == 3 * 8193
+    assert [p.batch for p in pipe.subs] == [4097, 4096]
+
+
 def test_gpu_tree_mutations(gpu):
     """SET_DATA version CAS, CREATE (parent must exist, NODE_EXISTS),
     DELETE through the GPU server, checked reply by reply."""

@@ -22,6 +22,7 @@ version CAS and ACL encode (BASELINE config 3).
 """
 
 import ctypes
+import os
 import time
 
 import numpy as np
@@ -32,6 +33,11 @@ from ..ops import _lib
 from ..ops import batch as B
 
 I64, I32, U8 = torch.int64, torch.int32, torch.uint8
+
+# ZKMI_SYNC_STREAMS=1: the write pipelines read the stream lengths back
+# instead of scanning terminated streams over bounds (A/B runs)
+_SYNC_STREAMS = os.environ.get('ZKMI_SYNC_STREAMS') == '1'
+
 
 
 def _next_pow2(x):
@@ -309,7 +315,10 @@ class GetPipeline(object):
         # so a step has no device-to-host read at all.  The reply bound uses
         # the largest data length in the tree now: a GET pipeline does not
         # mutate it (a reply beyond the bound would be missed and fail the
-        # per-reply check, never pass silently).
+        # per-reply check, never pass silently).  The synthetic tree's leaf
+        # paths and data have one length, so both bounds are the exact
+        # stream lengths: no slack of stale bytes past the terminator for
+        # the speculative K1 walkers to hop through (see MixPipeline).
         maxdata = int(tree.data_len.max().item())
         self.req_bound = min(n * (17 + maxpath) + 4, self.tx.numel())
         self.rep_bound = min(n * (4 + 16 + 4 + max(maxdata, 0) + 68) + 4,
@@ -445,6 +454,7 @@ class _Driver(object):
         self.rwindow = B.frame_window(4 + 16 + 4 + max(dmax, max_path + 16)
                                       + 68)
         self.reply = B.alloc_replies(batch, dev)
+        self.rscanner = None
         self.xid_base = 0
         self.iota = torch.arange(batch, dtype=I32, device=dev)
 
@@ -476,12 +486,29 @@ class _Driver(object):
                 raise RuntimeError('directory create failed: %r' % (
                     errs.unique().cpu().tolist(),))
 
-    def run(self, rb, session=0):
-        tx, _, total, _ = B.encode_requests(rb, self.xt, out=self.tx)
-        ntx = int(total.item())
-        rx, rtotal, _, _ = self.server.serve(tx, ntx, session=session)
-        nrx = int(rtotal.item())
-        ft = B.frame_scan(rx, nrx, cap=self.batch, window=self.rwindow)
+    def run(self, rb, session=0, bounds=None):
+        """One batch through encode -> server -> decode.  ``bounds`` =
+        host-known upper bounds (request stream, reply stream) in bytes:
+        both streams are then terminated and scanned over the bounds, with
+        no device-to-host read (as GetPipeline does); without them the two
+        stream lengths are read back."""
+        if bounds is not None and not _SYNC_STREAMS:
+            rq, rp = bounds
+            tx, _, _, _ = B.encode_requests(rb, self.xt, out=self.tx,
+                                            terminate=True)
+            rx, _, _, _ = self.server.serve(
+                tx, min(rq + 4, self.tx.numel()), session=session,
+                terminate=True)
+            if self.rscanner is None:
+                self.rscanner = B.FrameScanner(self.batch, self.dev,
+                                               window=self.rwindow)
+            ft = self.rscanner.scan(rx, min(rp + 4, rx.numel()))
+        else:
+            tx, _, total, _ = B.encode_requests(rb, self.xt, out=self.tx)
+            ntx = int(total.item())
+            rx, rtotal, _, _ = self.server.serve(tx, ntx, session=session)
+            nrx = int(rtotal.item())
+            ft = B.frame_scan(rx, nrx, cap=self.batch, window=self.rwindow)
         rep = B.decode_replies(rx, ft, self.xt, out=self.reply)
         return rep, rx
 
@@ -549,6 +576,11 @@ class MixPipeline(object):
         self.path_off = [torch.cat([po[r], po[(r - 1) % 3], po[(r - 2) % 3]])
                          for r in range(3)]
         self.path_len = plen[:m].repeat(3)
+        # The mix keeps the two stream-length read-backs: its host bounds
+        # overshoot (alternating ACL sizes, stale-version replies), and the
+        # slack past the terminator holds stale bytes, often zeros, i.e.
+        # 4-byte empty frames, that the speculative K1 walkers then hop
+        # through 4 bytes at a time (measured 3x slower than the read-back).
         self.s = -2
         self.drv.create_dirs(
             [['/mix'], ['/mix/d%05d' % d for d in range(ndirs)]],
@@ -624,6 +656,12 @@ class StormPipeline(object):
                                    device=dev)
         self.acl_id = torch.zeros(batch, dtype=I32, device=dev)
         self.want_len = self.path_len + 10
+        # every request and reply of a step has the same size, so these
+        # bounds are the exact stream lengths (no slack past the terminator)
+        pl = max(len(x) for x in prefixes)
+        acl = len(B._acl_bytes(MIX_ACLS[0]))
+        self.bounds = (batch * (4 + 8 + 4 + pl + 4 + data_bytes + acl + 4),
+                       batch * (4 + 16 + 4 + pl + 10))
         self.removed = torch.zeros(1, dtype=I64, device=dev)
         self.session = 1
         self.inserted = 0
@@ -643,7 +681,8 @@ class StormPipeline(object):
                             self.data_len, self.acl_id, self.path_arena,
                             self.data_arena, self.acl_off, self.acl_len,
                             self.acl_arena)
-        rep, _ = self.drv.run(rb, session=self.session + 1)
+        rep, _ = self.drv.run(rb, session=self.session + 1,
+                              bounds=self.bounds)
         self.last = (rb, rep)
         self.inserted += n
         # the previous session expires: its ephemerals go

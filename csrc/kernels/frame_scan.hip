@@ -3,36 +3,34 @@
 // Reference: ZKDecodeStream._transform (lib/zk-streams.js:39-65) walks the
 // i32-BE length chain one frame at a time and memmoves the remainder per
 // packet (O(bytes x packets)).  The chain is inherently
-// sequential; we make it parallel without speculation errors:
+// sequential; we make it parallel without speculation errors, in three
+// launches over 16 KiB tiles:
 //
-//  A  per-tile exit table f0[tile][e] for the W window entry points e (the
-//     only places a chain can enter a tile when frames are <= W bytes):
-//     fs_frontier + fs_survivor (default; merging frontier walk, see below)
-//     or fs_exits (ZKMI_FS_SCAN=jump|double; pointer jumping over every
-//     position of the tile):
-//     fs_exits   one workgroup per 16 KiB tile: build next(p) = p + 4 +
-//                be32(p) for EVERY byte position and pointer-jump (in place,
-//                racy but monotone) until each position maps to the first
-//                chain position outside the tile or to a terminal.
-//  B  fs_compose hierarchical function composition: a level-(l+1) unit is 16
-//                level-l units; for each window entry point, walk the 16
-//                sub-unit functions.  Log-depth, O(W) work per unit.  The 16
-//                child tables are staged in LDS first (fs_compose_staged).
-//  C  fs_top/fs_down  serial walk over the (few) top units from the stream
-//                start, then push the exact entry position down to every tile
-//                (fs_down_staged: one wave per parent, children in LDS).
-//  D  frame starts per tile from its exact entry: fs_join (default: walk from
-//     the entry to the survivor's hand-off point, then reuse the survivor's
-//     recorded path), fs_walk (jump: wave-uniform walk of the staged tile) or
-//     fs_mark (double: doubling marks on the full tile + bitmap).
-//  E  scan of counts (scan.hip) + fs_write_join / fs_write_list / fs_write:
-//     frame starts -> (body_off, len) table.
+//  A  fs_frontier  one block per tile: a merging frontier walk from the W
+//                  window entry points (the only places a chain can enter
+//                  a tile when frames are <= W bytes) -> per-entry exit code
+//                  table f0 and ONE surviving walker (all others ended or
+//                  merged into it).
+//  B  fs_survivor_r  one wave per tile walks the survivor to the tile end
+//                  through a 4 KiB LDS ring, records its frame starts, and
+//                  summarises the tile: its exit is "constant" when every
+//                  non-terminal entry leaves at one position.
+//  C  fs_chain     one wave per tile, tiles in order (atomic counter),
+//                  decoupled look-back: the constant exit of the tile
+//                  before is this tile's entry (validated through the
+//                  look-back, repaired when a frame longer than the window
+//                  breaks it), a short walk joins the survivor's path, the
+//                  inclusive frame count comes from a 64-tile-wide look-back,
+//                  and the tile writes its (body offset, length) rows.
 //
-// Frames longer than W (2 KiB) fall back to walking the byte chain in global
-// memory for the tile they land in; results stay exact.  BAD_LENGTH is
-// reported at the exact frame (result[1] = its offset, result[2] = 1), the
-// consumed prefix ends at the last complete frame, and a partial trailing
-// frame is left for the next call (carry), like the reference's buffer.
+// The stream length is read on the device (zk_frame_scan3's n_dev, e.g. an
+// encoder's total), the grids cover the buffer capacity and tiles past the
+// length return at once.  BAD_LENGTH is reported at the exact frame
+// (result[1] = its offset, result[2] = 1), the consumed prefix ends at the
+// last complete frame, and a partial trailing frame is left for the next
+// call (carry), like the reference's buffer.  The round-1 composition path
+// (fs_compose / fs_top / fs_down / fs_join + a count scan, 13-15 launches)
+// stays selectable for A/B runs (ZKMI_FS_SCAN=compose, host lengths).
 #include "zk_common.h"
 
 extern "C" int zk_scan_excl_i64(const int64_t*, int64_t*, int64_t, int64_t*,
@@ -76,6 +74,14 @@ constexpr int64_t LATE = (int64_t)1 << 61;
 ZK_DEV bool is_term(int64_t v) { return (v & TERM) != 0; }
 ZK_DEV bool is_late(int64_t v) { return (v & LATE) != 0; }
 ZK_DEV int64_t pos_of(int64_t v) { return v & ~(TERM | LATE); }
+
+// The scanned length: a producer's device-side byte count clamped to the
+// buffer capacity (null: the capacity itself, a host-known length).
+ZK_DEV int64_t stream_len(const int64_t* n_dev, int64_t n_cap) {
+  if (n_dev == nullptr) return n_cap;
+  const int64_t v = *n_dev;
+  return v < 0 ? 0 : (v < n_cap ? v : n_cap);
+}
 
 // One step of the chain in global memory.
 ZK_DEV int64_t next_global(const FsCtx& c, int64_t P) {
@@ -165,158 +171,6 @@ ZK_DEV void stage_tile(const uint8_t* buf, int64_t n, int64_t ts, uint8_t* sb,
   const int64_t lim = min(FS_S + 4, n - ts);
   for (int k = tid; k < FS_S + 16; k += NT)
     sb[k] = k < lim ? buf[ts + k] : 0;
-}
-
-// next() of every tile position relative to the tile (>= S: leaves tile;
-// == p: terminal).
-ZK_DEV int32_t next_rel(const uint8_t* sb, int64_t ts, int64_t n, int64_t maxp,
-                        int32_t p) {
-  const int64_t P = ts + p;
-  if (P + 4 > n) return p;
-  const uint32_t raw = ((uint32_t)sb[p] << 24) | ((uint32_t)sb[p + 1] << 16) |
-                       ((uint32_t)sb[p + 2] << 8) | (uint32_t)sb[p + 3];
-  const int32_t len = (int32_t)raw;
-  if (len < 0 || (int64_t)len > maxp) return p;
-  if (P + 4 + len > n) return p;
-  const int64_t nx = (int64_t)p + 4 + len;
-  return nx > 0x7FFFFFF0LL ? 0x7FFFFFF0 : (int32_t)nx;
-}
-
-constexpr int FS_PT = FS_S / FS_T;      // positions per thread (16)
-
-// In-place pointer jumping over a uint16 successor table whose fixed points
-// are the sinks.  Each thread batches its 16 gathers before any store so the
-// LDS reads of one round are all in flight together (the compiler cannot
-// reorder them across the aliasing stores itself).
-//
-// Real streams have few long chains: in a GET_DATA reply stream ~70 % of the
-// positions are sinks from the start and only the true frame chain (~90
-// positions per 16 KiB tile) needs more than 3 doublings.  So: 2 full rounds,
-// then compact the still-moving positions into an LDS list and iterate only
-// over it (full rounds again if the list would overflow).
-constexpr int FS_LIST = 4096;            // compacted active-position capacity
-
-ZK_DEV void jump_to_sinks(uint16_t* J, uint16_t* act, int64_t* red) {
-  for (int it = 0; it < 2; ++it) {
-    uint16_t v[FS_PT], w[FS_PT];
-#pragma unroll
-    for (int k = 0; k < FS_PT; ++k) v[k] = J[threadIdx.x + k * FS_T];
-#pragma unroll
-    for (int k = 0; k < FS_PT; ++k) w[k] = J[v[k]];
-    int changed = 0;
-#pragma unroll
-    for (int k = 0; k < FS_PT; ++k) {
-      if (w[k] != v[k]) { J[threadIdx.x + k * FS_T] = w[k]; changed = 1; }
-    }
-    if (!__syncthreads_or(changed)) return;
-  }
-  // compact positions that have not reached their sink
-  uint16_t v[FS_PT];
-  uint32_t mask = 0;
-#pragma unroll
-  for (int k = 0; k < FS_PT; ++k) v[k] = J[threadIdx.x + k * FS_T];
-#pragma unroll
-  for (int k = 0; k < FS_PT; ++k)
-    if (J[v[k]] != v[k]) mask |= 1u << k;
-  int64_t tot;
-  int64_t o = block_excl_scan(__popc(mask), red, &tot);
-  if (tot > FS_LIST) {
-    for (int it = 0; it < 16; ++it) {
-      uint16_t a[FS_PT], b[FS_PT];
-#pragma unroll
-      for (int k = 0; k < FS_PT; ++k) a[k] = J[threadIdx.x + k * FS_T];
-#pragma unroll
-      for (int k = 0; k < FS_PT; ++k) b[k] = J[a[k]];
-      int changed = 0;
-#pragma unroll
-      for (int k = 0; k < FS_PT; ++k)
-        if (b[k] != a[k]) { J[threadIdx.x + k * FS_T] = b[k]; changed = 1; }
-      if (!__syncthreads_or(changed)) return;
-    }
-    return;
-  }
-#pragma unroll
-  for (int k = 0; k < FS_PT; ++k)
-    if (mask & (1u << k)) act[o++] = (uint16_t)(threadIdx.x + k * FS_T);
-  __syncthreads();
-  const int cnt = (int)tot;
-  for (int it = 0; it < 16; ++it) {
-    int changed = 0;
-    for (int i = threadIdx.x; i < cnt; i += FS_T) {
-      const int p = act[i];
-      const uint16_t a = J[p];
-      const uint16_t b = J[a];
-      if (b != a) { J[p] = b; changed = 1; }
-    }
-    if (!__syncthreads_or(changed)) return;
-  }
-}
-
-// A: per-tile exits.  J[p] = in-tile successor, or p itself when p is a
-// terminal or its frame leaves the tile (a sink).  After jumping, J[p] is
-// the last in-tile chain element of p; its next() is the exit (or it is a
-// terminal).  16-bit table: 32 KiB + 16 KiB staged bytes -> 3 blocks / CU.
-__global__ __launch_bounds__(FS_T) void fs_exits(const uint8_t* __restrict__ buf,
-                                                int64_t n, int64_t maxp,
-                                                uint16_t* __restrict__ f0) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  uint16_t* J = (uint16_t*)smem;                     // [S]
-  uint16_t* act = (uint16_t*)(smem + FS_S * 2);      // [FS_LIST]
-  int64_t* red = (int64_t*)(smem + FS_S * 2 + FS_LIST * 2);
-  const int64_t t = blockIdx.x;
-  const int64_t ts = t * FS_S;
-  // Each thread owns 16 contiguous positions: one 16-byte + one 4-byte
-  // global load cover the 19 bytes their length prefixes span; the BE32 at
-  // every byte offset is rebuilt with v_alignbyte (no LDS byte staging).
-  {
-    const int32_t p0 = threadIdx.x * FS_PT;
-    const int64_t B = ts + p0;
-    uint32_t w[5];
-    if (B + 20 <= n) {
-      uint4 v; __builtin_memcpy(&v, buf + B, 16);
-      w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
-      __builtin_memcpy(&w[4], buf + B + 16, 4);
-    } else {
-#pragma unroll
-      for (int d = 0; d < 5; ++d) {
-        uint32_t x = 0;
-        for (int b = 0; b < 4; ++b) {
-          const int64_t a = B + 4 * d + b;
-          x |= (a < n ? (uint32_t)buf[a] : 0u) << (8 * b);
-        }
-        w[d] = x;
-      }
-    }
-    uint16_t j[FS_PT];
-#pragma unroll
-    for (int k = 0; k < FS_PT; ++k) {
-      const uint32_t le = __builtin_amdgcn_alignbyte(w[(k >> 2) + 1],
-                                                     w[k >> 2], k & 3);
-      const int32_t len = (int32_t)bswap32(le);
-      const int64_t P = B + k;
-      const bool ok = (P + 4 <= n) && len >= 0 && (int64_t)len <= maxp &&
-                      P + 4 + len <= n;
-      const int64_t nx = ok ? (int64_t)(p0 + k) + 4 + len : (int64_t)(p0 + k);
-      j[k] = (uint16_t)(nx < FS_S ? nx : p0 + k);
-    }
-    *(uint4*)(J + p0) = *(uint4*)j;
-    *(uint4*)(J + p0 + 8) = *(uint4*)(j + 8);
-  }
-  __syncthreads();
-  jump_to_sinks(J, act, red);
-  for (int32_t p = threadIdx.x; p < FS_W; p += FS_T) {
-    const int32_t q = J[p];
-    const int64_t Q = ts + q;
-    uint16_t v = F0_TERM | (uint16_t)q;              // terminal by default
-    if (Q + 4 <= n) {
-      const int32_t len = ld_be32(buf + Q);
-      if (len >= 0 && (int64_t)len <= maxp && Q + 4 + len <= n) {
-        const int64_t x = (int64_t)q + 4 + len - FS_S;   // >= 0: leaves tile
-        v = x < 0x4000 ? (uint16_t)x : F0_ESC;
-      }
-    }
-    f0[t * FS_W + p] = v;
-  }
 }
 
 // A' (default) — the same f0 table by a MERGING FRONTIER WALK instead of
@@ -462,10 +316,19 @@ ZK_DEV void fe_words(const uint8_t* sb, int32_t p, uint32_t& lo, uint32_t& hi) {
 // then resolved (entries rooted at the survivor become FE_PENDING).
 // (A wave-per-tile variant without barriers was slower: 53 KiB of LDS per
 // tile leaves 3 waves per CU, too few to hide the LDS latency chains.)
+//
+// The stream length is n = min(*n_dev, n_cap) (n_dev may be null: n_cap):
+// the grid covers the capacity and tiles at or past n leave at once, so a
+// producer's device-side byte count bounds the scan without a host read and
+// no stale byte past it is walked.  When `lbw` is given (one-pass chain,
+// fs_chain) every block also zeroes its tile's look-back words and block 0
+// the result and the chain's tile counter.
 template <int W>
 __global__ __launch_bounds__(FE_T) void fs_frontier(
-    const uint8_t* __restrict__ buf, int64_t n, int64_t maxp,
-    uint16_t* __restrict__ f0, int32_t* __restrict__ surv) {
+    const uint8_t* __restrict__ buf, const int64_t* __restrict__ n_dev,
+    int64_t n_cap, int64_t maxp, uint16_t* __restrict__ f0,
+    int32_t* __restrict__ surv, uint64_t* __restrict__ lbw,
+    int64_t* __restrict__ result) {
   constexpr int FE_K = W / FE_T;             // walkers per thread (1..8)
   static_assert(W % FE_T == 0 && FE_K >= 1 && FE_K <= 8, "window");
   constexpr bool NARROW = fe_narrow(W);
@@ -477,7 +340,19 @@ __global__ __launch_bounds__(FE_T) void fs_frontier(
   uint32_t* hand = (uint32_t*)(res + W);                   // [64] + 2 ctrs
   const int64_t t = blockIdx.x;
   FE_MARK(0);
+  const int64_t n = stream_len(n_dev, n_cap);
+  if (lbw != nullptr) {
+    if (threadIdx.x < 2) lbw[2 * t + threadIdx.x] = 0;
+    if (t == 0 && threadIdx.x >= 64 && threadIdx.x < 68)
+      result[threadIdx.x - 64] = 0;
+    if (t == 0 && threadIdx.x >= 128 && threadIdx.x < 132)
+      lbw[2 * (int64_t)gridDim.x + threadIdx.x - 128] = 0;
+  }
   const int64_t ts = t * FS_S;
+  if (ts >= n) {
+    if (threadIdx.x < FE_NSURV) surv[t * FE_NSURV + threadIdx.x] = -1;
+    return;
+  }
   const int32_t nrel = (int32_t)min(n - ts, (int64_t)1 << 30);
   const int32_t maxp32 = (int32_t)min(maxp, (int64_t)1 << 30);
   stage_tile<FE_T>(buf, n, ts, sb, threadIdx.x);
@@ -815,236 +690,36 @@ __global__ void fs_down(FsCtx c, int l) {
   }
 }
 
-// Mark the chain inside each tile from its entry; bitmap of frame starts.
-__global__ __launch_bounds__(FS_T) void fs_mark(const uint8_t* __restrict__ buf,
-                                               int64_t n, int64_t maxp,
-                                               const int64_t* __restrict__ ent,
-                                               uint32_t* __restrict__ bits,
-                                               int64_t* __restrict__ counts) {
-  // LDS: A, B (uint16 [S] each), mk (uint8 [S]); the staged bytes live in
-  // B's space until A is built.  80 KiB -> 2 blocks / CU.  Each thread owns
-  // 16 CONTIGUOUS positions so mk / A / B move as 16-byte LDS vectors.
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  uint16_t* A = (uint16_t*)smem;                       // [S]
-  uint16_t* B = A + FS_S;                              // [S]
-  uint8_t* mk = smem + FS_S * 4;                       // [S] bit0 mark, bit1 terminal
-  uint8_t* sb = (uint8_t*)B;                           // [S + 16] (aliases B)
-  const int64_t t = blockIdx.x;
-  const int64_t ts = t * FS_S;
-  const int64_t e = ent[t];
-  uint32_t* tb = bits + t * (FS_S / 32);
-  if (e == NONE) {
-    for (int k = threadIdx.x; k < FS_S / 32; k += FS_T) tb[k] = 0;
-    if (threadIdx.x == 0) counts[t] = 0;
-    return;
-  }
-  const int32_t p0 = threadIdx.x * FS_PT;
-  stage_tile<FS_T>(buf, n, ts, sb, threadIdx.x);
-  __syncthreads();
-  // A[p]: next within tile; S = leaves the tile; p itself = terminal.
-  {
-    uint16_t a[FS_PT];
-    uint8_t m[FS_PT];
-#pragma unroll
-    for (int k = 0; k < FS_PT; ++k) {
-      const int32_t p = p0 + k;
-      const int32_t j = next_rel(sb, ts, n, maxp, p);
-      a[k] = (uint16_t)(j >= FS_S ? FS_S : j);
-      m[k] = (j == p) ? 2 : 0;
-    }
-    __syncthreads();                                   // sb (in B) is dead
-#pragma unroll
-    for (int k = 0; k < FS_PT; k += 8)
-      *(uint4*)(A + p0 + k) = *(uint4*)(a + k);
-    *(uint4*)(mk + p0) = *(uint4*)m;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) mk[e - ts] |= 1;
-  __syncthreads();
-  for (int r = 0; r < 16; ++r) {
-    // mark: every marked position marks its 2^r-th successor
-    int added = 0;
-    const uint4 mv = *(const uint4*)(mk + p0);
-    const uint32_t mw[4] = {mv.x, mv.y, mv.z, mv.w};
-    if ((mw[0] | mw[1] | mw[2] | mw[3]) & 0x01010101u) {
-#pragma unroll
-      for (int k = 0; k < FS_PT; ++k) {
-        if ((mw[k >> 2] >> (8 * (k & 3))) & 1u) {
-          const int32_t j = A[p0 + k];
-          if (j < FS_S && j != p0 + k && !(mk[j] & 1)) {
-            mk[j] |= 1;
-            added = 1;
-          }
-        }
-      }
-    }
-    if (!__syncthreads_or(added)) break;
-    // jump: B = A o A
-    uint16_t a[FS_PT], b[FS_PT];
-    *(uint4*)a = *(const uint4*)(A + p0);
-    *(uint4*)(a + 8) = *(const uint4*)(A + p0 + 8);
-#pragma unroll
-    for (int k = 0; k < FS_PT; ++k) {
-      const int32_t j = a[k];
-      b[k] = (j < FS_S && j != p0 + k) ? A[j] : (uint16_t)j;
-    }
-    *(uint4*)(B + p0) = *(uint4*)b;
-    *(uint4*)(B + p0 + 8) = *(uint4*)(b + 8);
-    __syncthreads();
-    uint16_t* tmp = A; A = B; B = tmp;
-  }
-  // A frame starts at every marked position that is not a terminal.
-  const uint4 mv = *(const uint4*)(mk + p0);
-  const uint32_t mw[4] = {mv.x, mv.y, mv.z, mv.w};
-  uint32_t half = 0;
-#pragma unroll
-  for (int k = 0; k < FS_PT; ++k)
-    if (((mw[k >> 2] >> (8 * (k & 3))) & 3u) == 1u) half |= 1u << k;
-  const uint32_t other = __shfl_xor(half, 1, 64);
-  const uint32_t w = (threadIdx.x & 1) ? 0u : (half | (other << 16));
-  if (!(threadIdx.x & 1)) tb[threadIdx.x >> 1] = w;
-  __syncthreads();                                     // mk reads done
-  int64_t* red = (int64_t*)mk;                         // reuse mk space
-  int64_t tot;
-  block_excl_scan((int64_t)__popc(w), red, &tot);
-  if (threadIdx.x == 0) counts[t] = tot;
-}
-
-__global__ __launch_bounds__(256) void fs_write(const uint8_t* __restrict__ buf,
-                                               const uint32_t* __restrict__ bits,
-                                               const int64_t* __restrict__ base,
-                                               int64_t* __restrict__ foff,
-                                               int32_t* __restrict__ flen,
-                                               int64_t cap,
-                                               int64_t* __restrict__ result) {
-  __shared__ int64_t red[256 / 64 + 1];
-  const int64_t t = blockIdx.x;
-  const int64_t ts = t * FS_S;
-  const uint32_t* tb = bits + t * (FS_S / 32);
-  // 512 words per tile, 2 per thread
-  const int k0 = threadIdx.x * 2;
-  const uint32_t w0 = tb[k0], w1 = tb[k0 + 1];
-  int64_t tot;
-  int64_t idx = base[t] + block_excl_scan(__popc(w0) + __popc(w1), red, &tot);
-  for (int h = 0; h < 2; ++h) {
-    uint32_t w = h ? w1 : w0;
-    while (w) {
-      const int b = __ffs(w) - 1;
-      w &= w - 1;
-      const int64_t P = ts + (int64_t)(k0 + h) * 32 + b;
-      if (idx < cap) {
-        foff[idx] = P + 4;
-        flen[idx] = ld_be32(buf + P);
-      } else {
-        result[3] = 1;
-      }
-      ++idx;
-    }
-  }
-}
-
-// D' (default) — walk the chain of every tile from its entry, one lane per
-// tile, straight from global memory.  Once the entries are known the walk is
-// ~frames-per-tile dependent loads (the tile's lines come from L2 / the
-// Infinity Cache, where the producer just wrote them), and all tiles walk
-// concurrently, so the kernel is latency- not work-bound: it replaces the
-// O(log) full-tile doubling passes of fs_mark (kept for A/B,
-// ZKMI_FS_MARK=double).  Frame starts go to a per-tile uint16 list.
 constexpr int64_t FS_LMAX = FS_S / 4;    // most frame starts a tile can hold
 
-// One wave per tile: the wave stages the tile into its own 16 KiB of LDS
-// with 16-byte loads, then lane 0 follows the chain there (an LDS hop is
-// ~40 ns against ~250+ ns for an Infinity-Cache hit), 4 tiles per block.
-constexpr int FS_WALK_TPB = 4;
-
-__global__ __launch_bounds__(256) void fs_walk(const uint8_t* __restrict__ buf,
-                                              int64_t n, int64_t maxp,
-                                              int64_t tiles,
-                                              const int64_t* __restrict__ ent,
-                                              uint16_t* __restrict__ list,
-                                              int64_t* __restrict__ counts) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int64_t t = (int64_t)blockIdx.x * FS_WALK_TPB + wv;
-  if (t >= tiles) return;
-  const int64_t e = ent[t];
-  if (e == NONE) {
-    if (lane == 0) counts[t] = 0;
-    return;
-  }
-  uint8_t* sb = smem + wv * (FS_S + 16);
-  const int64_t ts = t * FS_S;
-  stage_tile<64>(buf, n, ts, sb, lane);
-  // Wave-local staging (no workgroup barrier: sibling waves may have exited):
-  // drain this wave's LDS writes before lane 0 reads them.
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_wave_barrier();
-  const int32_t te = (int32_t)(min(ts + FS_S, n) - ts);   // tile-relative
-  const int32_t nrel = (int32_t)min(n - ts, (int64_t)1 << 30);
-  const int32_t maxp32 = (int32_t)min(maxp, (int64_t)1 << 30);
-  // The walk is wave-UNIFORM: every lane runs it on scalar copies
-  // (readfirstlane), so the loop is ~25 mostly-SALU instructions around one
-  // LDS round trip per hop instead of a divergent lane-0 loop of ~45 VALU +
-  // exec-mask instructions (measured ~500 cycles/hop).
-  // The frame-start list is written IN PLACE over bytes already passed:
-  // entry k lands at byte 2k while the walk is at >= 4k, so no byte still to
-  // be read is overwritten, and no global store (with its vmcnt
-  // back-pressure) sits inside the dependent-hop loop.
-  uint16_t* Ls = (uint16_t*)sb;
-  int32_t c = __builtin_amdgcn_readfirstlane((int32_t)(e - ts));
-  int32_t cnt = 0;
-  while (c < te) {
-    const int32_t a = c & ~3;
-    const uint32_t lo = *(const uint32_t*)(sb + a);
-    const uint32_t hi = *(const uint32_t*)(sb + a + 4);
-    const int32_t len = __builtin_amdgcn_readfirstlane(
-        (int32_t)bswap32(__builtin_amdgcn_alignbyte(hi, lo, c & 3)));
-    const int32_t nx = c + 4 + len;
-    if ((c + 4 > nrel) | (len < 0) | (len > maxp32) | (nx > nrel)) break;
-    if (lane == 0) Ls[cnt] = (uint16_t)c;
-    ++cnt;
-    c = nx;                                   // >= S ends the loop
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_wave_barrier();
-  uint16_t* L = list + t * FS_LMAX;
-  for (int32_t k = lane; k < cnt; k += 64) L[k] = Ls[k];
-  if (lane == 0) counts[t] = cnt;
-}
-
-// E' — list -> (body offset, length) table; one wave per tile, coalesced.
-__global__ __launch_bounds__(256) void fs_write_list(
-    const uint8_t* __restrict__ buf, int64_t tiles,
-    const uint16_t* __restrict__ list, const int64_t* __restrict__ counts,
-    const int64_t* __restrict__ base, int64_t* __restrict__ foff,
-    int32_t* __restrict__ flen, int64_t cap, int64_t* __restrict__ result) {
-  const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (t >= tiles) return;
-  const int lane = threadIdx.x & 63;
-  const int64_t cnt = counts[t];
-  const int64_t b = base[t];
-  const int64_t ts = t * FS_S;
-  const uint16_t* L = list + t * FS_LMAX;
-  for (int64_t k = lane; k < cnt; k += 64) {
-    const int64_t P = ts + L[k];
-    const int64_t idx = b + k;
-    if (idx < cap) {
-      foff[idx] = P + 4;
-      flen[idx] = ld_be32(buf + P);
-    } else {
-      result[3] = 1;
-    }
-  }
-}
-
 // ---- frontier pipeline, stages 2-4 -----------------------------------------
-// Survivor slot s of tile t: surv[t*2+s] = (walker id << 16) | position, or
-// -1; its frame starts R_s go to list[(t*2+s)*FS_LMAX ...], its count to
-// rcount[t*2+s].
+// Survivor of tile t: surv[t] = (walker id << 16) | position, or -1; its
+// frame starts R go to list[t*FS_LMAX ...], their count to rcount[t].
 
-// Replace fe_pending(slot) in the tile's f0 row by the slot's final code.
-ZK_DEV void fe_patch_row(uint16_t* row, int W, int lane,
-                         const uint16_t fin[FE_NSURV]) {
+// Wave-wide min / max of a 32-bit value.
+ZK_DEV uint32_t wave_min_u32(uint32_t v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, d, 64));
+  return v;
+}
+ZK_DEV uint32_t wave_max_u32(uint32_t v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, d, 64));
+  return v;
+}
+
+// Replace fe_pending(slot) in the tile's f0 row by the slot's final code and
+// summarise the patched row: the tile's exit is CONSTANT when every entry
+// whose chain does not end in the tile (terminal codes are ignored: a true
+// chain entering there makes the stream bad before any later tile matters)
+// leaves it at one position.  Returns that absolute position, or -1 (two
+// exits, an ESC code, or every entry terminal).  Every real stream tile has
+// a constant exit unless a frame is longer than the window: all the true
+// frame starts in the window merge within a hop or two.
+ZK_DEV int64_t fe_patch_row(uint16_t* row, int W, int lane,
+                            const uint16_t fin[FE_NSURV], int64_t ts) {
+  uint32_t lo = 0x10000u, hi = 0u;
+  bool esc = false;
   for (int j = lane; j < W / 8; j += 64) {
     uint4 v = ((const uint4*)row)[j];
     uint16_t* h = (uint16_t*)&v;
@@ -1054,187 +729,20 @@ ZK_DEV void fe_patch_row(uint16_t* row, int W, int lane,
 #pragma unroll
       for (int sl = 0; sl < FE_NSURV; ++sl)
         if (h[k] == fe_pending(sl)) { h[k] = fin[sl]; any = true; }
+      const uint16_t c = h[k];
+      if (c == F0_ESC) {
+        esc = true;
+      } else if (!(c & F0_TERM)) {
+        lo = min(lo, (uint32_t)c);
+        hi = max(hi, (uint32_t)c + 1u);
+      }
     }
     if (any) ((uint4*)row)[j] = v;
   }
-}
-
-// A2 fs_survivor (LDS): one wave per tile; lane s walks survivor slot s of
-// the staged tile (the two walks advance in lockstep, one LDS round trip per
-// hop).  Frame starts go straight to global memory: those stores count in
-// vmcnt, which the LDS hop loop never waits on.  16 KiB of LDS -> 9 tiles
-// per CU: the variant for streams with few tiles (long chains per tile).
-constexpr size_t FV_LDS = FS_S + 16;
-
-__global__ __launch_bounds__(64) void fs_survivor(
-    const uint8_t* __restrict__ buf, int64_t n, int64_t maxp, int32_t W,
-    uint16_t* __restrict__ f0, const int32_t* __restrict__ surv,
-    uint16_t* __restrict__ list, int32_t* __restrict__ rcount) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  uint8_t* sb = smem;                                      // [S + 16]
-  const int lane = threadIdx.x;
-  const int64_t t = blockIdx.x;
-  const int64_t ts = t * FS_S;
-  const int32_t sv = lane < FE_NSURV ? surv[t * FE_NSURV + lane] : -1;
-  if (!__ballot(sv >= 0)) {                  // nothing pending in this tile
-    if (lane < FE_NSURV) rcount[t * FE_NSURV + lane] = 0;
-    return;
-  }
-  stage_tile<64>(buf, n, ts, sb, lane);
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_wave_barrier();
-  const int32_t nrel = (int32_t)min(n - ts, (int64_t)1 << 30);
-  const int32_t maxp32 = (int32_t)min(maxp, (int64_t)1 << 30);
-  int32_t m = 0;
-  uint16_t fin = 0;
-  if constexpr (FE_NSURV == 1) {
-    // one survivor: wave-uniform scalar walk.  The hot loop keeps only what
-    // a clean hop needs (one unsigned length bound, one position bound that
-    // folds "stays in the tile" and "fits the stream"); the hop that ends
-    // the walk is re-classified exactly by fe_hop_len after the loop.  Frame
-    // starts collect in a VGPR (entry k in lane k & 63, a v_cndmask, no exec
-    // branching) and go out 64 at a time, IN PLACE over tile bytes already
-    // passed (entry k at byte 2k while the walk is at >= 4k).
-    int32_t c = __builtin_amdgcn_readfirstlane(sv) & 0xFFFF;
-    uint16_t* Ls = (uint16_t*)sb;
-    const int32_t lim = min(nrel + 1, (int32_t)FS_S);
-    const uint32_t umax = (uint32_t)maxp32;
-    uint32_t ent = 0;
-    for (;;) {
-      uint32_t lo, hi;
-      fe_words(sb, c, lo, hi);
-      const int32_t len = __builtin_amdgcn_readfirstlane(fe_len(lo, hi, c));
-      const int32_t nx = c + 4 + len;
-      if (((uint32_t)len > umax) | (nx >= lim)) break;
-      ent = lane == (m & 63) ? (uint32_t)c : ent;
-      ++m;
-      if ((m & 63) == 0) Ls[m - 64 + lane] = (uint16_t)ent;
-      c = nx;
-    }
-    {
-      uint32_t lo, hi;
-      fe_words(sb, c, lo, hi);
-      const int32_t len = __builtin_amdgcn_readfirstlane(fe_len(lo, hi, c));
-      int32_t q = 0;
-      const uint16_t code = fe_hop_len(len, c, nrel, maxp32, q);
-      if (!((code & F0_TERM) && code != F0_ESC)) {
-        ent = lane == (m & 63) ? (uint32_t)c : ent;   // leaves the tile
-        ++m;
-        if ((m & 63) == 0) Ls[m - 64 + lane] = (uint16_t)ent;
-      }
-      fin = code;
-    }
-    if (lane < (m & 63)) Ls[(m & ~63) + lane] = (uint16_t)ent;
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
-    uint16_t* L = list + t * FS_LMAX;
-    for (int32_t k = lane; k < m; k += 64) L[k] = Ls[k];
-    if (lane != 0) m = 0;                    // slot 0 lives in lane 0
-  } else {
-  bool a = sv >= 0;
-  int32_t c = sv & 0xFFFF;
-  uint16_t* L = list + (t * FE_NSURV + lane) * FS_LMAX;
-  while (__ballot(a)) {
-    if (a) {
-      uint32_t lo, hi;
-      fe_words(sb, c, lo, hi);
-      int32_t q = 0;
-      const uint16_t code = fe_hop(lo, hi, c, nrel, maxp32, q);
-      if (code != FE_GO && (code & F0_TERM) && code != F0_ESC) {
-        fin = code;                          // terminal: not a frame start
-        a = false;
-      } else {
-        L[m++] = (uint16_t)c;
-        if (code != FE_GO) { fin = code; a = false; }   // leaves the tile
-        else c = q;
-      }
-    }
-  }
-  }
-  if (lane < FE_NSURV) rcount[t * FE_NSURV + lane] = m;
-  uint16_t fins[FE_NSURV];
-#pragma unroll
-  for (int sl = 0; sl < FE_NSURV; ++sl)
-    fins[sl] = (uint16_t)__builtin_amdgcn_readlane((int)fin, sl);
-  fe_patch_row(f0 + t * W, W, lane, fins);
-}
-
-// A2' fs_survivor_g: the same walks straight from global memory, no LDS.  A
-// dependent hop costs more from L2 than from LDS (~0.4 vs ~0.1 us under
-// load), but without the 16 KiB LDS tile a CU holds 32 walking waves instead
-// of 9 and nothing is staged: the variant for streams with many tiles.
-// Each slot is walked by a wave-uniform loop (two aligned dwords per hop +
-// v_alignbyte); its frame starts collect in a VGPR (entry k in lane k & 63,
-// one v_cndmask) and leave in one coalesced store per 64 hops.  4 tiles
-// (waves) per block.
-__global__ __launch_bounds__(256) void fs_survivor_g(
-    const uint8_t* __restrict__ buf, int64_t n, int64_t maxp, int32_t W, int64_t tiles,
-    uint16_t* __restrict__ f0, const int32_t* __restrict__ surv,
-    uint16_t* __restrict__ list, int32_t* __restrict__ rcount) {
-  const int lane = threadIdx.x & 63;
-  const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (t >= tiles) return;
-  const int64_t ts = t * FS_S;
-  const uint8_t* tb = buf + ts;
-  const int32_t nrel = (int32_t)min(n - ts, (int64_t)1 << 30);
-  const int32_t maxp32 = (int32_t)min(maxp, (int64_t)1 << 30);
-  uint16_t fins[FE_NSURV];
-  bool any_sv = false;
-#pragma unroll
-  for (int sl = 0; sl < FE_NSURV; ++sl) {
-    const int32_t sv = __builtin_amdgcn_readfirstlane(
-        surv[t * FE_NSURV + sl]);
-    fins[sl] = 0;
-    if (sv < 0) {
-      if (lane == 0) rcount[t * FE_NSURV + sl] = 0;
-      continue;
-    }
-    any_sv = true;
-    uint16_t* L = list + (t * FE_NSURV + sl) * FS_LMAX;
-    int32_t c = sv & 0xFFFF;
-    int32_t m = 0;
-    uint32_t ent = 0;
-    uint16_t fin;
-    // fast loop: one unsigned length bound and one position bound (stay in
-    // the tile AND leave room for the next length word); the ending hop is
-    // classified exactly afterwards
-    const int32_t lim = min(nrel - 3, (int32_t)FS_S);
-    const uint32_t umax = (uint32_t)maxp32;
-    for (;;) {
-      if (c >= lim) break;
-      const int32_t a = c & ~3;
-      const int32_t a2 = (a + 4 < nrel) ? a + 4 : a;
-      const uint32_t w0 = *(const uint32_t*)(tb + a);
-      const uint32_t w1 = *(const uint32_t*)(tb + a2);
-      const int32_t len = __builtin_amdgcn_readfirstlane(fe_len(w0, w1, c));
-      const int32_t nx = c + 4 + len;
-      if (((uint32_t)len > umax) | (nx > nrel) | (nx >= (int32_t)FS_S)) break;
-      ent = lane == (m & 63) ? (uint32_t)c : ent;   // entry m -> lane m&63
-      ++m;
-      if ((m & 63) == 0) L[m - 64 + lane] = (uint16_t)ent;
-      c = nx;
-    }
-    if (c + 4 > nrel) {
-      fin = (uint16_t)(F0_TERM | c);
-    } else {
-      const int32_t a = c & ~3;
-      const int32_t a2 = (a + 4 < nrel) ? a + 4 : a;
-      const uint32_t w0 = *(const uint32_t*)(tb + a);
-      const uint32_t w1 = *(const uint32_t*)(tb + a2);
-      const int32_t len = __builtin_amdgcn_readfirstlane(fe_len(w0, w1, c));
-      int32_t q = 0;
-      fin = fe_hop_len(len, c, nrel, maxp32, q);
-      if (!((fin & F0_TERM) && fin != F0_ESC)) {   // leaves: a frame start
-        ent = lane == (m & 63) ? (uint32_t)c : ent;
-        ++m;
-        if ((m & 63) == 0) L[m - 64 + lane] = (uint16_t)ent;
-      }
-    }
-    if (lane < (m & 63)) L[(m & ~63) + lane] = (uint16_t)ent;
-    if (lane == 0) rcount[t * FE_NSURV + sl] = m;
-    fins[sl] = fin;
-  }
-  if (any_sv) fe_patch_row(f0 + t * W, W, lane, fins);
+  lo = wave_min_u32(lo);
+  hi = wave_max_u32(hi);
+  if (__ballot(esc) != 0 || lo == 0x10000u || hi != lo + 1u) return -1;
+  return ts + FS_S + (int64_t)lo;
 }
 
 // A2'' fs_survivor_r (default): the LDS walk of fs_survivor through a 4 KiB
@@ -1291,19 +799,34 @@ ZK_DEV int32_t fr_len(const uint8_t* ring, int32_t c) {
   return __builtin_amdgcn_readfirstlane(fe_len(lo, hi, c));
 }
 
-__global__ __launch_bounds__(64) void fs_survivor_r(
-    const uint8_t* __restrict__ buf, int64_t n, int64_t maxp, int32_t W,
-    uint16_t* __restrict__ f0, const int32_t* __restrict__ surv,
-    uint16_t* __restrict__ list, int32_t* __restrict__ rcount) {
-  __shared__ __attribute__((aligned(16))) uint8_t ring[FR_RING];
-  const int lane = threadIdx.x;
-  const int64_t t = blockIdx.x;
+//
+// fs_survive is the walk itself (one wave, tile t): it records the
+// survivor's frame starts in list[t], their count in rcount[t], patches and
+// summarises the tile's f0 row, and returns the speculated exit (the
+// survivor's exit when it leaves the tile, else the constant-row exit, -1
+// when there is none) and the survivor's end `send`: the absolute position
+// its last frame leaves the tile at, or TERM | pos (| TBAD when the length
+// at pos is invalid rather than cut off by the stream end), -1 without a
+// survivor.  The survivor is the chain nearly every window entry merged
+// into; a garbage entry whose random "length" jumps out of the tile makes
+// the f0 row non-constant in most real tiles, so the constant-row rule is
+// only the fallback for tiles without one.
+constexpr int64_t TBAD = (int64_t)1 << 60;
+
+ZK_DEV int64_t fs_survive(const uint8_t* __restrict__ buf, int64_t n,
+                          int64_t maxp, int32_t W, uint16_t* __restrict__ f0,
+                          const int32_t* __restrict__ surv,
+                          uint16_t* __restrict__ list,
+                          int32_t* __restrict__ rcount, int64_t t,
+                          uint8_t* ring, int lane, int64_t& send) {
   const int64_t ts = t * FS_S;
   // one survivor per tile (FE_NSURV == 1; the launcher checks)
   const int32_t sv = __builtin_amdgcn_readfirstlane(surv[t * FE_NSURV]);
   if (sv < 0) {
     if (lane == 0) rcount[t * FE_NSURV] = 0;
-    return;
+    const uint16_t none[FE_NSURV] = {0};
+    send = -1;
+    return fe_patch_row(f0 + t * W, W, lane, none, ts);
   }
   const int32_t nrel = (int32_t)min(n - ts, (int64_t)1 << 30);
   const int32_t maxp32 = (int32_t)min(maxp, (int64_t)1 << 30);
@@ -1368,12 +891,30 @@ __global__ __launch_bounds__(64) void fs_survivor_r(
       ent = lane == (m & 63) ? (uint32_t)c : ent;
       ++m;
       if ((m & 63) == 0) L[m - 64 + lane] = (uint16_t)ent;
+      send = ts + c + 4 + len;
+    } else {
+      const bool bad = (c + 4 <= nrel) && ((uint32_t)len > umax);
+      send = TERM | (bad ? TBAD : 0) | (ts + c);
     }
   }
   if (lane < (m & 63)) L[(m & ~63) + lane] = (uint16_t)ent;
   if (lane == 0) rcount[t * FE_NSURV] = m;
   uint16_t fins[FE_NSURV] = {fin};
-  fe_patch_row(f0 + t * W, W, lane, fins);
+  const int64_t k = fe_patch_row(f0 + t * W, W, lane, fins, ts);
+  return (send & TERM) ? k : send;
+}
+
+// Composition path: one wave per tile (blockIdx), host length.
+__global__ __launch_bounds__(64) void fs_survivor_r(
+    const uint8_t* __restrict__ buf, int64_t n, int64_t maxp, int32_t W,
+    uint16_t* __restrict__ f0, const int32_t* __restrict__ surv,
+    uint16_t* __restrict__ list, int32_t* __restrict__ rcount) {
+  __shared__ __attribute__((aligned(16))) uint8_t ring[FR_RING];
+  const int64_t t = blockIdx.x;
+  if (t * FS_S >= n) return;
+  int64_t send;
+  (void)fs_survive(buf, n, maxp, W, f0, surv, list, rcount, t, ring,
+                   threadIdx.x, send);
 }
 
 // D'' fs_join: the tile's frame starts from its exact entry e*.  Every chain
@@ -1462,15 +1003,370 @@ __global__ __launch_bounds__(256) void fs_write_join(
   }
 }
 
+// ---- chain resolution (default): fs_tile, fs_link, fs_rows ------------------
+// Replaces composition / push-down / join / count scan / write (13-15
+// launches per scan) with three:
+//
+//  fs_tile   one wave per tile, tiles in order from an atomic counter: the
+//            survivor walk (fs_survive), then publish the tile's speculated
+//            exit X[t] and take the tile before's X[t-1] as this tile's
+//            entry (a one-step wait: that tile started earlier and does the
+//            same work).  The entry is exact unless a frame longer than the
+//            window ends in the tile before, or its chain is not the
+//            survivor's.  Walk from the entry through a 1 KiB LDS window
+//            until the chain meets the survivor's recorded path (merge-walk
+//            against the sorted list), leaves the tile, or ends in a
+//            terminal; record (entry used, exit, count, walked starts).
+//  fs_link   one workgroup: every link is checked in parallel (tile k's
+//            entry must be tile k-1's exit); the leftmost broken links are
+//            repaired by re-walking those tiles from the exact exit (wave 0,
+//            serial, rare), then a block scan of the counts up to the first
+//            terminal gives every tile its row base and result[0..3].
+//  fs_rows   one wave per tile writes its (body offset, length) rows.
+//
+// (A single-pass decoupled look-back was tried first: with every tile of a
+// 200 MB stream resident at once, each tile looked back across all the
+// tiles before it, 64 per round trip: ~100 us per scan.)
+constexpr int FC_WIN = 1024;                 // staged walk window (bytes)
+constexpr int64_t FC_MAXP = (int64_t)1 << 24;
+constexpr int FL_T = 1024;                   // fs_link threads
+
+ZK_DEV uint64_t lb_load(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+ZK_DEV void lb_store(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+ZK_DEV int64_t ld_agent(const int64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+ZK_DEV void st_agent(int64_t* p, int64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Chain statistics after the tile counter: [1] tiles without a speculated
+// entry, [2] tiles re-walked by fs_link, [3] fs_link repair rounds
+// (zk_frame_scan_stats reads them).
+ZK_DEV void fc_stat(uint64_t* stats, int k, uint32_t v) {
+  __hip_atomic_fetch_add((uint32_t*)&stats[k], v, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+}
+
+struct FcWalk {
+  int64_t exit;      // exit position, or the terminal's position
+  int32_t cnt;       // frame starts in the tile on the chain
+  int32_t np;        // of which walked here (pre[0..np))
+  int32_t js;        // survivor list index the rest starts at (-1: none)
+  bool term, bad;
+};
+
+// per-tile record: meta = cnt | np << 13 | (js + 1) << 26 | term << 39 |
+// bad << 40; entry = the entry used (-1: none, the tile before had no
+// speculated exit)
+ZK_DEV int64_t fc_meta(const FcWalk& w) {
+  return (int64_t)w.cnt | ((int64_t)w.np << 13) | ((int64_t)(w.js + 1) << 26) |
+         ((int64_t)w.term << 39) | ((int64_t)w.bad << 40);
+}
+ZK_DEV int32_t m_cnt(int64_t m) { return (int32_t)(m & 0x1FFF); }
+ZK_DEV int32_t m_np(int64_t m) { return (int32_t)((m >> 13) & 0x1FFF); }
+ZK_DEV int32_t m_js(int64_t m) { return (int32_t)((m >> 26) & 0x1FFF) - 1; }
+ZK_DEV bool m_term(int64_t m) { return (m >> 39) & 1; }
+ZK_DEV bool m_bad(int64_t m) { return (m >> 40) & 1; }
+
+// Stage [wb, wb + FC_WIN) (zero past n) into the wave's window.
+ZK_DEV void fc_stage(const uint8_t* __restrict__ buf, int64_t n, int64_t wb,
+                     uint8_t* win, int lane) {
+  const int64_t g = wb + 16 * lane;
+  uint4 v = make_uint4(0, 0, 0, 0);
+  if (g + 16 <= n) {
+    __builtin_memcpy(&v, buf + g, 16);
+  } else if (g < n) {
+    uint8_t* b = (uint8_t*)&v;
+    for (int k = 0; k < 16; ++k) b[k] = g + k < n ? buf[g + k] : 0;
+  }
+  *(uint4*)(win + 16 * lane) = v;
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// Walk tile [ts, ts + S)'s chain from E (one wave, wave-uniform control).
+// Frame starts walked before meeting the survivor's path L[0..m0) go to
+// pre[] (tile-relative, written by lane 0).
+ZK_DEV FcWalk fc_walk(const uint8_t* __restrict__ buf, int64_t n,
+                      int64_t maxp, int64_t ts, int64_t E, const uint16_t* L,
+                      int32_t m0, int64_t send, uint8_t* win, uint16_t* pre,
+                      int lane) {
+  FcWalk r{E, 0, 0, -1, false, false};
+  const int64_t tend = ts + FS_S;
+  int64_t c = E;
+  int64_t wb = -(int64_t)FC_WIN;
+  int32_t lb = 0;                             // survivor list window base
+  uint32_t lv = lane < m0 ? (uint32_t)L[lane] : 0xFFFFFFFFu;
+  int32_t np = 0;
+  for (;;) {
+    if (c >= tend) { r.exit = c; break; }
+    if (c >= n) { r.exit = n; break; }        // the stream ends cleanly
+    const uint32_t crel = (uint32_t)(c - ts);
+    if (m0 > 0) {
+      // merge-walk against the sorted survivor list
+      while (lb + 64 < m0 &&
+             crel > (uint32_t)__builtin_amdgcn_readlane((int)lv, 63)) {
+        lb += 64;
+        lv = lb + lane < m0 ? (uint32_t)L[lb + lane] : 0xFFFFFFFFu;
+      }
+      const uint64_t hit = __ballot(lv == crel);
+      if (hit) {
+        r.js = lb + (int32_t)__builtin_ctzll(hit);
+        break;
+      }
+    }
+    if (c + 4 > n) { r.exit = c; r.term = true; break; }
+    if (c < wb || c + 8 > wb + FC_WIN) {
+      wb = c & ~(int64_t)15;
+      fc_stage(buf, n, wb, win, lane);
+    }
+    const int32_t o = (int32_t)(c - wb);
+    const uint32_t raw = ((uint32_t)win[o] << 24) | ((uint32_t)win[o + 1] << 16) |
+                         ((uint32_t)win[o + 2] << 8) | (uint32_t)win[o + 3];
+    const int32_t len = __builtin_amdgcn_readfirstlane((int32_t)raw);
+    if (len < 0 || (int64_t)len > maxp) {
+      r.exit = c; r.term = true; r.bad = true; break;
+    }
+    const int64_t nx = c + 4 + len;
+    if (nx > n) { r.exit = c; r.term = true; break; }
+    if (lane == 0) pre[np] = (uint16_t)crel;
+    ++np;
+    c = nx;
+  }
+  r.np = np;
+  r.cnt = np;
+  if (r.js >= 0) {
+    r.cnt = np + (m0 - r.js);
+    if (send & TERM) {
+      const int64_t q = send & ~(TERM | TBAD);
+      if (q >= n && !(send & TBAD)) {
+        r.exit = n;                           // clean end of the stream
+      } else {
+        r.exit = q; r.term = true; r.bad = (send & TBAD) != 0;
+      }
+    } else {
+      r.exit = send;
+    }
+  }
+  return r;
+}
+
+__global__ __launch_bounds__(64) void fs_tile(
+    const uint8_t* __restrict__ buf, const int64_t* __restrict__ n_dev,
+    int64_t n_cap, int64_t maxp, int32_t W, uint16_t* __restrict__ f0,
+    const int32_t* __restrict__ surv, uint16_t* __restrict__ list,
+    int32_t* __restrict__ rcount, int64_t* __restrict__ sx, uint64_t* lbw,
+    uint16_t* __restrict__ pre, int64_t* __restrict__ rec_entry,
+    int64_t* __restrict__ rec_exit, int64_t* __restrict__ rec_meta,
+    int64_t* __restrict__ dbg) {
+  __shared__ __attribute__((aligned(16))) uint8_t ring[FR_RING];
+  __shared__ __attribute__((aligned(16))) uint8_t win[FC_WIN + 16];
+  const int64_t t_0 = dbg ? wall_clock64() : 0;
+  const int lane = threadIdx.x;
+  const int64_t n = stream_len(n_dev, n_cap);
+  const int64_t ntiles = (n + FS_S - 1) / FS_S;
+  uint64_t* stats = &lbw[2 * (int64_t)gridDim.x];
+  uint32_t tid = 0;
+  if (lane == 0)
+    tid = __hip_atomic_fetch_add((uint32_t*)stats, 1u, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+  const int64_t t = (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)tid);
+  if (t >= ntiles) return;
+  const int64_t ts = t * FS_S;
+  int64_t send;
+  const int64_t cxt = fs_survive(buf, n, maxp, W, f0, surv, list, rcount, t,
+                                 ring, lane, send);
+  if (lane == 0) {
+    sx[t] = send;
+    lb_store(&lbw[2 * t], (uint64_t)(cxt + 2));      // X[t] (0 = not yet)
+  }
+  const int64_t t_1 = dbg ? wall_clock64() : 0;
+  int64_t E = 0;
+  bool none = false;
+  if (t > 0) {
+    uint64_t x;
+    for (;;) {                                // tile t-1 is running or done
+      x = lb_load(&lbw[2 * (t - 1)]);
+      if (x != 0) break;
+      __builtin_amdgcn_s_sleep(1);
+    }
+    E = (int64_t)x - 2;
+    none = E < 0;
+  }
+  const int64_t t_2 = dbg ? wall_clock64() : 0;
+  FcWalk w{E, 0, 0, -1, false, false};
+  if (!none) {
+    // this wave wrote list[t] and rcount[t] itself (every lane rereads
+    // only the list entries it stored)
+    const int32_t m0 = __builtin_amdgcn_readfirstlane(rcount[t]);
+    w = fc_walk(buf, n, maxp, ts, E, list + t * FS_LMAX, m0, send, win,
+                pre + t * FS_LMAX, lane);
+  } else if (lane == 0) {
+    fc_stat(stats, 1, 1);
+  }
+  if (lane == 0) {
+    rec_entry[t] = none ? -1 : E;
+    rec_exit[t] = w.exit;
+    rec_meta[t] = fc_meta(w);
+    if (dbg) {
+      dbg[6 * t + 0] = t_0;
+      dbg[6 * t + 1] = t_1;
+      dbg[6 * t + 2] = t_2;
+      dbg[6 * t + 3] = wall_clock64();
+      dbg[6 * t + 4] = w.np;
+      dbg[6 * t + 5] = w.js;
+    }
+  }
+}
+
+__global__ __launch_bounds__(FL_T) void fs_link(
+    const uint8_t* __restrict__ buf, const int64_t* __restrict__ n_dev,
+    int64_t n_cap, int64_t maxp, const int64_t* __restrict__ sx,
+    const uint16_t* __restrict__ list, const int32_t* __restrict__ rcount,
+    uint16_t* pre, int64_t* rec_entry, int64_t* rec_exit, int64_t* rec_meta,
+    int64_t* __restrict__ base, int64_t cap, int64_t* __restrict__ result,
+    uint64_t* stats) {
+  __shared__ __attribute__((aligned(16))) uint8_t win[FC_WIN + 16];
+  __shared__ int64_t red[2 * (FL_T / 64) + 2];
+  __shared__ int64_t s_next;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int64_t n = stream_len(n_dev, n_cap);
+  const int64_t ntiles = (n + FS_S - 1) / FS_S;
+  if (ntiles == 0) return;                    // result zeroed by fs_frontier
+  const int64_t INF = INT64_MAX;
+  int64_t from = 1, ft = INF;
+  for (;;) {
+    // leftmost terminal, and leftmost broken link at or after `from` (tile
+    // k's entry must be tile k-1's exit; links before `from` hold)
+    int64_t fb = INF, fterm = INF;
+    for (int64_t k = tid; k < ntiles; k += FL_T) {
+      const int64_t mk = ld_agent(&rec_meta[k]);
+      if (m_term(mk)) {
+        fterm = min(fterm, k);
+      } else if (k + 1 < ntiles && k + 1 >= from) {
+        const int64_t e = ld_agent(&rec_entry[k + 1]);
+        if (e < 0 || e != ld_agent(&rec_exit[k])) fb = min(fb, k + 1);
+      }
+    }
+    for (int d = 32; d >= 1; d >>= 1) {
+      fb = min(fb, (int64_t)__shfl_xor(fb, d, 64));
+      fterm = min(fterm, (int64_t)__shfl_xor(fterm, d, 64));
+    }
+    if (lane == 0) { red[wv] = fb; red[FL_T / 64 + wv] = fterm; }
+    __syncthreads();
+    fb = INF;
+    fterm = INF;
+    for (int j = 0; j < FL_T / 64; ++j) {
+      fb = min(fb, red[j]);
+      fterm = min(fterm, red[FL_T / 64 + j]);
+    }
+    __syncthreads();
+    if (fb == INF || fb > fterm) {            // every live link holds
+      ft = fterm;
+      break;
+    }
+    // repair: re-walk tiles from fb while their links stay broken
+    if (wv == 0) {
+      int64_t k = fb;
+      uint32_t walked = 0;
+      for (;;) {
+        const int64_t E = ld_agent(&rec_exit[k - 1]);
+        const int32_t m0 = __builtin_amdgcn_readfirstlane(rcount[k]);
+        const FcWalk w = fc_walk(buf, n, maxp, k * FS_S, E,
+                                 list + k * FS_LMAX, m0, sx[k], win,
+                                 pre + k * FS_LMAX, lane);
+        ++walked;
+        if (lane == 0) {
+          st_agent(&rec_entry[k], E);
+          st_agent(&rec_exit[k], w.exit);
+          st_agent(&rec_meta[k], fc_meta(w));
+        }
+        ++k;
+        if (w.term || k >= ntiles) break;
+        if (ld_agent(&rec_entry[k]) == w.exit) break;   // link k holds
+      }
+      if (lane == 0) {
+        s_next = k;
+        fc_stat(stats, 2, walked);
+        fc_stat(stats, 3, 1);
+      }
+    }
+    __syncthreads();
+    from = s_next;
+  }
+  // exclusive scan of the counts of tiles 0..ft; tiles after ft are dead
+  const int64_t last = ft == INF ? ntiles - 1 : ft;
+  const int64_t per = (last + 1 + FL_T - 1) / FL_T;
+  const int64_t k0 = (int64_t)tid * per;
+  const int64_t k1 = min(k0 + per, last + 1);
+  int64_t sum = 0;
+  for (int64_t k = k0; k < k1; ++k) sum += m_cnt(ld_agent(&rec_meta[k]));
+  int64_t tot;
+  int64_t run = block_excl_scan(sum, red, &tot);
+  for (int64_t k = k0; k < k1; ++k) {
+    base[k] = run;
+    run += m_cnt(ld_agent(&rec_meta[k]));
+  }
+  for (int64_t k = last + 1 + tid; k < ntiles; k += FL_T) base[k] = -1;
+  if (tid == 0) {
+    result[0] = tot;
+    result[3] = tot > cap ? 1 : 0;
+    if (ft == INF) {
+      result[1] = n;
+      result[2] = 0;
+    } else {
+      result[1] = ld_agent(&rec_exit[ft]);
+      result[2] = m_bad(ld_agent(&rec_meta[ft])) ? 1 : 0;
+    }
+  }
+}
+
+// (body offset, length) rows: one wave per tile, 4 tiles per block.
+__global__ __launch_bounds__(256) void fs_rows(
+    const uint8_t* __restrict__ buf, const int64_t* __restrict__ n_dev,
+    int64_t n_cap, const uint16_t* __restrict__ list,
+    const uint16_t* __restrict__ pre, const int64_t* __restrict__ rec_meta,
+    const int64_t* __restrict__ base, int64_t* __restrict__ foff,
+    int32_t* __restrict__ flen, int64_t cap) {
+  const int lane = threadIdx.x & 63;
+  const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t n = stream_len(n_dev, n_cap);
+  if (t * FS_S >= n) return;
+  const int64_t b = base[t];
+  if (b < 0) return;
+  const int64_t m = rec_meta[t];
+  const int32_t cnt = m_cnt(m), np = m_np(m), js = m_js(m);
+  const int64_t ts = t * FS_S;
+  const uint16_t* P = pre + t * FS_LMAX;
+  const uint16_t* R = list + t * FS_LMAX + (js < 0 ? 0 : js);
+  for (int32_t k = lane; k < cnt; k += 64) {
+    const int64_t pos = ts + (k < np ? P[k] : R[k - np]);
+    const int64_t idx = b + k;
+    if (idx < cap) {
+      foff[idx] = pos + 4;
+      flen[idx] = ld_be32(buf + pos);
+    }
+  }
+}
+
 struct FsPlan {
   int levels;
   int64_t units[FS_MAXL];
   int64_t usize[FS_MAXL];
-  size_t off_f0, off_fl[FS_MAXL], off_ent[FS_MAXL], off_bits, off_cnt,
-      off_base, off_scan, off_list, off_pre, off_surv, off_rcnt, off_npre,
-      total;
+  size_t off_f0, off_fl[FS_MAXL], off_ent[FS_MAXL], off_cnt, off_base,
+      off_scan, off_list, off_pre, off_surv, off_rcnt, off_npre, off_cx,
+      off_sx, off_lbw, off_rent, off_rexit, off_rmeta, total;
 };
 
+// Workspace of a scan over a buffer of n bytes.  The one-pass chain needs
+// f0, the survivor lists and 40 bytes per tile; the composition path (A/B)
+// its level tables, entries and count scan on top.
 static FsPlan fs_plan(int64_t n, int64_t W) {
   FsPlan p{};
   const int64_t tiles = n > 0 ? (n + FS_S - 1) / FS_S : 1;
@@ -1486,51 +1382,65 @@ static FsPlan fs_plan(int64_t n, int64_t W) {
   size_t o = 0;
   auto take = [&](size_t bytes) { size_t r = o; o += (bytes + 255) & ~(size_t)255; return r; };
   p.off_f0 = take((size_t)tiles * W * 2);
+  p.off_list = take((size_t)tiles * FE_NSURV * FS_LMAX * 2);
+  p.off_surv = take((size_t)tiles * FE_NSURV * 4);
+  p.off_rcnt = take((size_t)tiles * FE_NSURV * 4);
+  p.off_cx = take((size_t)tiles * 8);
+  p.off_sx = take((size_t)tiles * 8);
+  p.off_lbw = take((size_t)(2 * tiles + 4) * 8);
+  p.off_rent = take((size_t)tiles * 8);
+  p.off_rexit = take((size_t)tiles * 8);
+  p.off_rmeta = take((size_t)tiles * 8);
+  p.off_pre = take((size_t)tiles * FS_LMAX * 2);
+  p.off_base = take((size_t)tiles * 8);
   for (int l = 1; l < p.levels; ++l)
     p.off_fl[l] = take((size_t)p.units[l] * W * 8);
   for (int l = 0; l < p.levels; ++l) p.off_ent[l] = take((size_t)p.units[l] * 8);
-  p.off_bits = take((size_t)tiles * (FS_S / 32) * 4);
   p.off_cnt = take((size_t)tiles * 8);
-  p.off_base = take((size_t)tiles * 8);
   p.off_scan = take((size_t)zk_scan_workspace(tiles) * 8);
-  p.off_list = take((size_t)tiles * FE_NSURV * FS_LMAX * 2);
-  p.off_pre = take((size_t)tiles * FS_LMAX * 2);
-  p.off_surv = take((size_t)tiles * FE_NSURV * 4);
-  p.off_rcnt = take((size_t)tiles * FE_NSURV * 4);
   p.off_npre = take((size_t)tiles * 4);
   p.total = o;
   return p;
 }
 
-}  // namespace zk
-
-extern "C" {
-
-// Sized for the largest window (FS_W), an upper bound for any window.
-int64_t zk_frame_scan_workspace(int64_t n) {
-  return (int64_t)zk::fs_plan(n, zk::FS_W).total;
+static int fs_window(int32_t window) {
+  return window <= 256 ? 256 : window <= 512 ? 512
+       : window <= 1024 ? 1024 : (int)FS_W;
 }
 
-// result (device int64[4]): [0] frames written, [1] stop offset (consumed
-// bytes; start of the carry or of the bad frame), [2] 1 if the stop is a
-// BAD_LENGTH frame, [3] 1 if the frame table overflowed `cap`.
-//
-// `window` (256 / 512 / 1024 / 2048 bytes) is the fast-path entry window per
-// 16 KiB tile: a chain can only enter a tile inside it when frames are <=
-// window bytes, so the frontier walks `window` speculative entry points per
-// tile and the composition tables hold `window` entries per unit.  Frames
-// longer than the window stay exact (walked in global memory for the tiles
-// they land in), so the window is a performance hint: the smallest one
-// covering the stream's usual frame size makes the scan cheapest.
-int zk_frame_scan2(const uint8_t* buf, int64_t n, int64_t maxp, uint8_t* ws,
-                   int64_t ws_bytes, int64_t* foff, int32_t* flen, int64_t cap,
-                   int64_t* result, int32_t window, hipStream_t st) {
-  using namespace zk;
-  const int W = window <= 256 ? 256 : window <= 512 ? 512
-              : window <= 1024 ? 1024 : (int)FS_W;
+static void fs_launch_frontier(int W, int64_t tiles, const uint8_t* buf,
+                               const int64_t* n_dev, int64_t n_cap,
+                               int64_t maxp, uint16_t* f0, int32_t* surv,
+                               uint64_t* lbw, int64_t* result,
+                               hipStream_t st) {
+  switch (W) {
+    case 256:
+      fs_frontier<256><<<(unsigned)tiles, FE_T, fe_lds(256), st>>>(
+          buf, n_dev, n_cap, maxp, f0, surv, lbw, result);
+      break;
+    case 512:
+      fs_frontier<512><<<(unsigned)tiles, FE_T, fe_lds(512), st>>>(
+          buf, n_dev, n_cap, maxp, f0, surv, lbw, result);
+      break;
+    case 1024:
+      fs_frontier<1024><<<(unsigned)tiles, FE_T, fe_lds(1024), st>>>(
+          buf, n_dev, n_cap, maxp, f0, surv, lbw, result);
+      break;
+    default:
+      fs_frontier<(int)FS_W><<<(unsigned)tiles, FE_T, fe_lds((int)FS_W),
+                               st>>>(buf, n_dev, n_cap, maxp, f0, surv, lbw,
+                                     result);
+  }
+}
+
+// The composition path (ZKMI_FS_SCAN=compose, A/B only): host length n.
+static int fs_scan_compose(const uint8_t* buf, int64_t n, int64_t maxp,
+                           uint8_t* ws, int64_t ws_bytes, int64_t* foff,
+                           int32_t* flen, int64_t cap, int64_t* result, int W,
+                           hipStream_t st) {
   FsPlan p = fs_plan(n, W);
   if ((int64_t)p.total > ws_bytes) return -1;
-  hipMemsetAsync(result, 0, 4 * sizeof(int64_t), st);
+  (void)hipMemsetAsync(result, 0, 4 * sizeof(int64_t), st);
   if (n <= 0) return 0;
   FsCtx c{};
   c.buf = buf;
@@ -1546,16 +1456,7 @@ int zk_frame_scan2(const uint8_t* buf, int64_t n, int64_t maxp, uint8_t* ws,
   }
   c.f0 = (const uint16_t*)(ws + p.off_f0);
   const int64_t tiles = p.units[0];
-  // ZKMI_FS_SCAN: "frontier" (default) | "jump" (fs_exits + fs_walk) |
-  // "double" (fs_exits + fs_mark doubling) — the older paths stay for A/B.
-  static int mode = -1;
-  if (mode < 0) {
-    const char* m = getenv("ZKMI_FS_SCAN");
-    mode = !m ? 0 : (m[0] == 'j' ? 1 : (m[0] == 'd' ? 2 : 0));
-  }
-  if (mode != 0 && W != FS_W) return -2;       // A/B paths: full window only
   uint16_t* f0w = (uint16_t*)(ws + p.off_f0);
-  uint32_t* bits = (uint32_t*)(ws + p.off_bits);
   int64_t* cnt = (int64_t*)(ws + p.off_cnt);
   int64_t* base = (int64_t*)(ws + p.off_base);
   uint16_t* list = (uint16_t*)(ws + p.off_list);
@@ -1563,48 +1464,11 @@ int zk_frame_scan2(const uint8_t* buf, int64_t n, int64_t maxp, uint8_t* ws,
   int32_t* surv = (int32_t*)(ws + p.off_surv);
   int32_t* rcnt = (int32_t*)(ws + p.off_rcnt);
   int32_t* npre = (int32_t*)(ws + p.off_npre);
-  if (mode == 0) {
-    switch (W) {
-      case 256:
-        fs_frontier<256><<<(unsigned)tiles, FE_T, fe_lds(256), st>>>(
-            buf, n, maxp, f0w, surv);
-        break;
-      case 512:
-        fs_frontier<512><<<(unsigned)tiles, FE_T, fe_lds(512), st>>>(
-            buf, n, maxp, f0w, surv);
-        break;
-      case 1024:
-        fs_frontier<1024><<<(unsigned)tiles, FE_T, fe_lds(1024), st>>>(
-            buf, n, maxp, f0w, surv);
-        break;
-      default:
-        fs_frontier<(int)FS_W><<<(unsigned)tiles, FE_T, fe_lds((int)FS_W),
-                                 st>>>(buf, n, maxp, f0w, surv);
-    }
-    ZK_LAUNCH_CHECK();
-    // Survivor walk: through a 4 KiB LDS ring (default; LDS hop latency at
-    // up to 32 walks per CU).  ZKMI_FS_SURVIVOR=lds|global|ring selects the
-    // whole-tile LDS walk (9 walks per CU) or the L2 walk for A/B runs.
-    static int sv_force = -1;
-    if (sv_force < 0) {
-      const char* m = getenv("ZKMI_FS_SURVIVOR");
-      sv_force = !m ? 0 : (m[0] == 'l' ? 1 : (m[0] == 'g' ? 2
-                                               : (m[0] == 'r' ? 3 : 0)));
-    }
-    const int sv_mode = sv_force ? sv_force : 3;
-    if (sv_mode == 3 && FE_NSURV == 1)
-      fs_survivor_r<<<(unsigned)tiles, 64, 0, st>>>(buf, n, maxp, W, f0w,
-                                                   surv, list, rcnt);
-    else if (sv_mode == 1)
-      fs_survivor<<<(unsigned)tiles, 64, FV_LDS, st>>>(buf, n, maxp, W, f0w,
-                                                      surv, list, rcnt);
-    else
-      fs_survivor_g<<<(unsigned)((tiles + 3) / 4), 256, 0, st>>>(
-          buf, n, maxp, W, tiles, f0w, surv, list, rcnt);
-  } else {
-    const size_t lds_a = FS_S * 2 + FS_LIST * 2 + (FS_T / 64 + 1) * 8;
-    fs_exits<<<(unsigned)tiles, FS_T, lds_a, st>>>(buf, n, maxp, f0w);
-  }
+  fs_launch_frontier(W, tiles, buf, nullptr, n, maxp, f0w, surv, nullptr,
+                     nullptr, st);
+  ZK_LAUNCH_CHECK();
+  fs_survivor_r<<<(unsigned)tiles, 64, 0, st>>>(buf, n, maxp, W, f0w, surv,
+                                               list, rcnt);
   ZK_LAUNCH_CHECK();
   for (int l = 0; l + 1 < p.levels; ++l) {
     const size_t sb = fs_stage_bytes(l, W);
@@ -1627,40 +1491,144 @@ int zk_frame_scan2(const uint8_t* buf, int64_t n, int64_t maxp, uint8_t* ws,
     ZK_LAUNCH_CHECK();
   }
   const unsigned wblocks = (unsigned)((tiles + 3) / 4);
-  if (mode == 0) {
-    fs_join<<<wblocks, 256, 0, st>>>(buf, n, maxp, tiles, c.ent[0], list,
-                                     rcnt, pre, npre, cnt);
-  } else if (mode == 2) {
-    fs_mark<<<(unsigned)tiles, FS_T, FS_S * 5, st>>>(buf, n, maxp, c.ent[0],
-                                                    bits, cnt);
-  } else {
-    fs_walk<<<(unsigned)((tiles + FS_WALK_TPB - 1) / FS_WALK_TPB), 256,
-              FS_WALK_TPB * (FS_S + 16), st>>>(buf, n, maxp, tiles, c.ent[0],
-                                               list, cnt);
-  }
+  fs_join<<<wblocks, 256, 0, st>>>(buf, n, maxp, tiles, c.ent[0], list, rcnt,
+                                   pre, npre, cnt);
   ZK_LAUNCH_CHECK();
   int rc = zk_scan_excl_i64(cnt, base, tiles, result + 0,
                             (int64_t*)(ws + p.off_scan), st);
   if (rc) return rc;
-  if (mode == 0) {
-    fs_write_join<<<wblocks, 256, 0, st>>>(buf, tiles, pre, npre, list, cnt,
-                                           base, foff, flen, cap, result);
-  } else if (mode == 2) {
-    fs_write<<<(unsigned)tiles, 256, 0, st>>>(buf, bits, base, foff, flen,
-                                             cap, result);
-  } else {
-    fs_write_list<<<wblocks, 256, 0, st>>>(buf, tiles, list, cnt, base, foff,
-                                           flen, cap, result);
-  }
+  fs_write_join<<<wblocks, 256, 0, st>>>(buf, tiles, pre, npre, list, cnt,
+                                         base, foff, flen, cap, result);
   ZK_LAUNCH_CHECK();
   return 0;
+}
+
+}  // namespace zk
+
+extern "C" {
+
+// Sized for the largest window (FS_W), an upper bound for any window.
+int64_t zk_frame_scan_workspace(int64_t n) {
+  return (int64_t)zk::fs_plan(n, zk::FS_W).total;
+}
+
+// K1 over buf[0, n) with n = min(*n_dev, n_cap) read ON THE DEVICE (n_dev
+// null: n = n_cap).  Four launches: fs_frontier, fs_tile, fs_link, fs_rows;
+// the grid covers n_cap and tiles past n return at once, so a producer's
+// device byte count (an encoder's `total`) is scanned with no host read and
+// no byte past it is touched.
+//
+// result (device int64[4]): [0] frames found, [1] stop offset (consumed
+// bytes; start of the carry or of the bad frame), [2] 1 if the stop is a
+// BAD_LENGTH frame, [3] 1 if the frame table overflowed `cap` (rows past
+// cap are dropped).
+//
+// `window` (256 / 512 / 1024 / 2048 bytes) is the fast-path entry window per
+// 16 KiB tile: a chain can only enter a tile inside it when frames are <=
+// window bytes, so the frontier walks `window` speculative entry points per
+// tile.  Longer frames stay exact (their tiles' entries come from the exact
+// look-back instead of a constant exit), so the window is a performance
+// hint: the smallest one covering the stream's usual frame size makes the
+// scan cheapest.  maxp must be <= 16 MiB (the protocol's frame limit).
+// ZKMI_FS_DBG=1: fs_tile writes per-tile timestamps (start, survivor done,
+// entry known, walk done) and the walk's (np, js) into a debug buffer
+// (zk_frame_scan_dbg copies it out).  Diagnostics only.
+static int64_t* g_dbg = nullptr;
+static int64_t g_dbg_tiles = 0;
+static int64_t* fs_dbg_buf(int64_t tiles) {
+  static int on = -1;
+  if (on < 0) on = getenv("ZKMI_FS_DBG") != nullptr;
+  if (!on) return nullptr;
+  if (tiles > g_dbg_tiles) {
+    if (g_dbg) (void)hipFree(g_dbg);
+    if (hipMalloc(&g_dbg, tiles * 6 * 8) != hipSuccess) return nullptr;
+    g_dbg_tiles = tiles;
+  }
+  return g_dbg;
+}
+
+int zk_frame_scan_dbg(int64_t* host, int64_t tiles) {
+  if (!g_dbg || tiles > g_dbg_tiles) return -1;
+  return hipMemcpy(host, g_dbg, tiles * 6 * 8, hipMemcpyDeviceToHost) ==
+                 hipSuccess ? 0 : -1;
+}
+
+int zk_frame_scan3(const uint8_t* buf, const int64_t* n_dev, int64_t n_cap,
+                   int64_t maxp, uint8_t* ws, int64_t ws_bytes, int64_t* foff,
+                   int32_t* flen, int64_t cap, int64_t* result, int32_t window,
+                   hipStream_t st) {
+  using namespace zk;
+  const int W = fs_window(window);
+  if (maxp > FC_MAXP || maxp < 0) return -3;
+  // ZKMI_FS_SCAN=compose: the round-1 composition path (host length only)
+  static int mode = -1;
+  if (mode < 0) {
+    const char* m = getenv("ZKMI_FS_SCAN");
+    mode = (m && m[0] == 'c') ? 1 : 0;
+  }
+  if (mode == 1 && n_dev == nullptr)
+    return fs_scan_compose(buf, n_cap, maxp, ws, ws_bytes, foff, flen, cap,
+                           result, W, st);
+  FsPlan p = fs_plan(n_cap, W);
+  if ((int64_t)p.total > ws_bytes) return -1;
+  const int64_t tiles = p.units[0];
+  uint16_t* f0w = (uint16_t*)(ws + p.off_f0);
+  uint16_t* list = (uint16_t*)(ws + p.off_list);
+  int32_t* surv = (int32_t*)(ws + p.off_surv);
+  int32_t* rcnt = (int32_t*)(ws + p.off_rcnt);
+  int64_t* cx = (int64_t*)(ws + p.off_cx);
+  int64_t* sx = (int64_t*)(ws + p.off_sx);
+  uint64_t* lbw = (uint64_t*)(ws + p.off_lbw);
+  uint16_t* pre = (uint16_t*)(ws + p.off_pre);
+  int64_t* rent = (int64_t*)(ws + p.off_rent);
+  int64_t* rexit = (int64_t*)(ws + p.off_rexit);
+  int64_t* rmeta = (int64_t*)(ws + p.off_rmeta);
+  int64_t* base = (int64_t*)(ws + p.off_base);
+  (void)cx;
+  fs_launch_frontier(W, tiles, buf, n_dev, n_cap, maxp, f0w, surv, lbw,
+                     result, st);
+  ZK_LAUNCH_CHECK();
+  fs_tile<<<(unsigned)tiles, 64, 0, st>>>(buf, n_dev, n_cap, maxp, W, f0w,
+                                         surv, list, rcnt, sx, lbw, pre, rent,
+                                         rexit, rmeta, fs_dbg_buf(tiles));
+  ZK_LAUNCH_CHECK();
+  fs_link<<<1, FL_T, 0, st>>>(buf, n_dev, n_cap, maxp, sx, list, rcnt, pre,
+                              rent, rexit, rmeta, base, cap, result,
+                              lbw + 2 * tiles);
+  ZK_LAUNCH_CHECK();
+  fs_rows<<<(unsigned)((tiles + 3) / 4), 256, 0, st>>>(
+      buf, n_dev, n_cap, list, pre, rmeta, base, foff, flen, cap);
+  ZK_LAUNCH_CHECK();
+  return 0;
+}
+
+// Copy the chain statistics of the last scan of workspace `ws` over a
+// buffer of n_cap bytes (window W) into out3 (host): tiles without a
+// speculated entry, tiles re-walked, repair rounds.
+int zk_frame_scan_stats(const uint8_t* ws, int64_t n_cap, int32_t window,
+                        uint32_t* out3, hipStream_t st) {
+  using namespace zk;
+  FsPlan p = fs_plan(n_cap, fs_window(window));
+  const uint64_t* lbw = (const uint64_t*)(ws + p.off_lbw);
+  for (int k = 0; k < 3; ++k)
+    if (hipMemcpyAsync(out3 + k, lbw + 2 * p.units[0] + 1 + k, 4,
+                       hipMemcpyDeviceToHost, st) != hipSuccess)
+      return -1;
+  return hipStreamSynchronize(st) == hipSuccess ? 0 : -1;
+}
+
+int zk_frame_scan2(const uint8_t* buf, int64_t n, int64_t maxp, uint8_t* ws,
+                   int64_t ws_bytes, int64_t* foff, int32_t* flen, int64_t cap,
+                   int64_t* result, int32_t window, hipStream_t st) {
+  return zk_frame_scan3(buf, nullptr, n, maxp, ws, ws_bytes, foff, flen, cap,
+                        result, window, st);
 }
 
 int zk_frame_scan(const uint8_t* buf, int64_t n, int64_t maxp, uint8_t* ws,
                   int64_t ws_bytes, int64_t* foff, int32_t* flen, int64_t cap,
                   int64_t* result, hipStream_t st) {
-  return zk_frame_scan2(buf, n, maxp, ws, ws_bytes, foff, flen, cap, result,
-                        (int32_t)zk::FS_W, st);
+  return zk_frame_scan3(buf, nullptr, n, maxp, ws, ws_bytes, foff, flen, cap,
+                        result, (int32_t)zk::FS_W, st);
 }
 
 }  // extern "C"

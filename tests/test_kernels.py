@@ -146,6 +146,85 @@ def test_terminated_stream_scans_over_a_bound(gpu, window):
     assert got == frames
 
 
+@pytest.mark.parametrize('window', [256, 1024])
+@pytest.mark.parametrize('maxbody,n', [(64, 4000), (300, 2000), (5000, 150),
+                                       (40000, 12)])
+def test_frame_scan_device_length_garbage_tail(gpu, window, maxbody, n):
+    """K1 over a DEVICE length (an encoder's total): the buffer's capacity
+    is 4x the stream and the tail past the length is random garbage, which
+    must neither be walked into frames nor change the result."""
+    from zkmi.ops import batch as B
+    r = synth.rng(maxbody + window)
+    s = _frames_stream(r, n, maxbody)
+    tail = jute.frame(b'y' * 40)[:-5]          # partial frame: carry
+    s = s + tail
+    frames, consumed, bad = jute.scan_frames(s)
+    cap = 4 * len(s) + 16384
+    buf = torch.randint(0, 256, (cap,), dtype=torch.uint8, device=gpu)
+    buf[:len(s)] = _dev_bytes(s, gpu)
+    n_dev = torch.tensor([len(s)], dtype=torch.int64, device=gpu)
+    sc = B.FrameScanner(len(frames) + 8, gpu, window=window)
+    for _ in range(2):                 # a reused scanner: words re-zeroed
+        ft = sc.scan(buf, n_dev)
+        res = ft.host_result()
+        assert res['frames'] == len(frames)
+        assert res['consumed'] == consumed == len(s) - len(tail)
+        assert not res['bad'] and not res['overflow']
+        got = list(zip(ft.off[:len(frames)].cpu().tolist(),
+                       ft.length[:len(frames)].cpu().tolist()))
+        assert got == frames
+    # the same scanner over a shorter device length (a cut stream)
+    cut = frames[len(frames) // 2][0] - 4 + 2
+    n_dev.fill_(cut)
+    res = sc.scan(buf, n_dev).host_result()
+    want, wc, _ = jute.scan_frames(s[:cut])
+    assert res['frames'] == len(want) and res['consumed'] == wc
+
+
+def test_frame_scan_device_length_bad_frame(gpu):
+    from zkmi.ops import batch as B
+    r = synth.rng(77)
+    good = _frames_stream(r, 3000, 200)
+    s = good + b'\x80\x00\x00\x01' + _frames_stream(r, 300, 200)
+    cap = 2 * len(s)
+    buf = torch.randint(0, 256, (cap,), dtype=torch.uint8, device=gpu)
+    buf[:len(s)] = _dev_bytes(s, gpu)
+    n_dev = torch.tensor([len(s)], dtype=torch.int64, device=gpu)
+    ft = B.frame_scan(buf, n_dev, window=256)
+    res = ft.host_result()
+    frames, consumed, bad_at = jute.scan_frames(s)
+    assert res['bad'] and res['consumed'] == len(good) == bad_at
+    assert res['frames'] == len(frames)
+    # zero length: nothing framed
+    n_dev.zero_()
+    res = B.frame_scan(buf, n_dev).host_result()
+    assert res == {'frames': 0, 'consumed': 0, 'bad': False,
+                   'overflow': False}
+
+
+def test_frame_scan_encoder_total_no_sync(gpu):
+    """encode_requests' device total feeds K1 directly: the sync-free
+    pipeline contract without a terminator or a host bound."""
+    from zkmi.ops import batch as B
+    r = synth.rng(12)
+    pkts = [{'xid': i, 'opcode': 'GET_DATA', 'watch': bool(i & 1),
+             'path': '/p/%d' % r.randint(0, 10 ** r.randint(1, 9))}
+            for i in range(20000)]
+    rb = B.pack_requests(pkts, gpu)
+    cap = 64 * len(pkts) + (1 << 16)
+    out = torch.randint(0, 256, (cap,), dtype=torch.uint8, device=gpu)
+    tx, _, total, err = B.encode_requests(rb, out=out)
+    ft = B.frame_scan(tx, total, window=256)
+    res = ft.host_result()
+    want = b''.join(jute.frame(jute.encode_request(p)) for p in pkts)
+    assert res['frames'] == len(pkts) and res['consumed'] == len(want)
+    assert not res['bad']
+    frames, _, _ = jute.scan_frames(want)
+    got = list(zip(ft.off[:len(pkts)].cpu().tolist(),
+                   ft.length[:len(pkts)].cpu().tolist()))
+    assert got == frames
+
+
 @pytest.mark.parametrize('window', [256, 2048])
 def test_frame_scan_large_multi_level(gpu, window):
     """> 256 tiles forces the hierarchical composition path."""

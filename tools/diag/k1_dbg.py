@@ -1,0 +1,61 @@
+"""Per-tile timing of fs_tile (ZKMI_FS_DBG=1): survivor walk, wait for the
+tile before's exit, join walk; for the benchmark's request and reply
+streams."""
+import ctypes
+import os
+import sys
+
+os.environ['ZKMI_FS_DBG'] = '1'
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(
+    os.path.abspath(__file__)))))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from zkmi.ops import _lib  # noqa: E402
+from zkmi.ops import batch as B  # noqa: E402
+from zkmi.bench import synthetic as S  # noqa: E402
+
+
+def dump(name, scanner, nbytes):
+    torch.cuda.synchronize()
+    tiles = (scanner.last_cap + 16383) // 16384
+    a = np.zeros(tiles * 6, np.int64)
+    _lib.check(_lib.lib().zk_frame_scan_dbg(
+        a.ctypes.data_as(ctypes.c_void_p), tiles), 'dbg')
+    a = a.reshape(tiles, 6)
+    nt = (nbytes + 16383) // 16384
+    a = a[:nt]
+    t0 = a[:, 0].min()
+    clk = 100.0    # wall_clock64 MHz
+    surv = (a[:, 1] - a[:, 0]) / clk
+    wait = (a[:, 2] - a[:, 1]) / clk
+    walk = (a[:, 3] - a[:, 2]) / clk
+    end = (a[:, 3] - t0) / clk
+    start = (a[:, 0] - t0) / clk
+    print(name, 'tiles', nt)
+    for k, v in (('start', start), ('survivor', surv), ('wait', wait),
+                 ('walk', walk), ('end', end), ('np', a[:, 4]),
+                 ('js', a[:, 5])):
+        print('  %-9s p50 %8.2f p90 %8.2f max %8.2f mean %8.2f' % (
+            k, np.percentile(v, 50), np.percentile(v, 90), v.max(),
+            v.mean()))
+
+
+def main():
+    dev = torch.device('cuda', 0)
+    tree = S.GpuTree(1_000_000, 100, device=dev)
+    pipe = S.GetPipeline(tree, 1 << 19)
+    for _ in range(2):
+        pipe.step()
+    torch.cuda.synchronize()
+    # the reply scan ran last
+    _, rep, rx, ft = pipe.last
+    nrx = int(ft.result[1].item())
+    dump('reply', pipe.rscanner, nrx)
+    tx_len = int(pipe.server.scanner.table.result[1].item())
+    pipe.server.scanner.scan(pipe.tx, tx_len)
+    dump('request', pipe.server.scanner, tx_len)
+
+
+if __name__ == '__main__':
+    main()

@@ -14,8 +14,9 @@ ZooKeeper wire format:
 
 plus a device-side check that every reply is OK and carries the node the
 request asked for.  Nothing is skipped inside a step, and a step makes no
-device-to-host read: both streams are terminated and frame-scanned over
-host-known upper bounds of their lengths.
+device-to-host read: K1 reads each stream's length from the device-side
+byte count its encoder produced (``total``), so any frame-size mix scans
+sync-free and no byte past a stream's end is walked.
 
 :class:`MixPipeline` does the same for the create/set/delete mix with
 version CAS and ACL encode (BASELINE config 3).
@@ -34,9 +35,15 @@ from ..ops import batch as B
 
 I64, I32, U8 = torch.int64, torch.int32, torch.uint8
 
-# ZKMI_SYNC_STREAMS=1: the write pipelines read the stream lengths back
-# instead of scanning terminated streams over bounds (A/B runs)
+# ZKMI_SYNC_STREAMS=1: the pipelines read the stream lengths back to the
+# host instead of handing K1 the encoders' device totals (A/B runs)
 _SYNC_STREAMS = os.environ.get('ZKMI_SYNC_STREAMS') == '1'
+
+
+def _len(total):
+    """A stream length for K1: the encoder's device total, or (A/B) its
+    host value."""
+    return int(total.item()) if _SYNC_STREAMS else total
 
 
 
@@ -244,9 +251,10 @@ class GpuServer(object):
 
     def serve(self, rx, n, session=0, terminate=False):
         """Serve the request stream ``rx[:n]`` for ``session`` (the owner of
-        any EPHEMERAL node it creates).  ``n`` may be an upper bound of a
-        terminated stream (see :func:`zkmi.ops.batch.encode_requests`);
-        ``terminate`` terminates the reply stream the same way."""
+        any EPHEMERAL node it creates).  ``n`` is a host length or the
+        request encoder's device total (no host read).  Returns the reply
+        stream buffer, its device total, the encoder error flag and the
+        request frame table."""
         L = _lib.lib()
         ft = self.scanner.scan(rx, n)
         rt = B.decode_requests(rx, ft, out=self.rt)
@@ -310,19 +318,6 @@ class GetPipeline(object):
                                 window=B.frame_window(17 + maxpath))
         self.rwindow = B.frame_window(4 + 16 + 4 + dmax + 68)
         self.rscanner = B.FrameScanner(n, dev, window=self.rwindow)
-        # Both streams are terminated (four 0xFF bytes after the last
-        # frame) and scanned over host-known upper bounds of their lengths,
-        # so a step has no device-to-host read at all.  The reply bound uses
-        # the largest data length in the tree now: a GET pipeline does not
-        # mutate it (a reply beyond the bound would be missed and fail the
-        # per-reply check, never pass silently).  The synthetic tree's leaf
-        # paths and data have one length, so both bounds are the exact
-        # stream lengths: no slack of stale bytes past the terminator for
-        # the speculative K1 walkers to hop through (see MixPipeline).
-        maxdata = int(tree.data_len.max().item())
-        self.req_bound = min(n * (17 + maxpath) + 4, self.tx.numel())
-        self.rep_bound = min(n * (4 + 16 + 4 + max(maxdata, 0) + 68) + 4,
-                             self.server.out.numel())
         self.reply = B.alloc_replies(n, dev)
         self.xid_base = 0
         self.last = None
@@ -381,13 +376,11 @@ class GetPipeline(object):
                             self.plen, self.zero64, self.zero32, self.zero32,
                             t.path_arena, t.slab, self.acl_off,
                             self.acl_len, self.acl_arena)
-        tx, rec_off, total, err = B.encode_requests(rb, self.xt, out=self.tx,
-                                                    terminate=True)
+        tx, rec_off, total, err = B.encode_requests(rb, self.xt, out=self.tx)
         yield
-        rx, rtotal, rerr, _ = self.server.serve(tx, self.req_bound,
-                                                terminate=True)
+        rx, rtotal, rerr, _ = self.server.serve(tx, _len(total))
         yield
-        ft = self.rscanner.scan(rx, self.rep_bound)
+        ft = self.rscanner.scan(rx, _len(rtotal))
         rep = B.decode_replies(rx, ft, self.xt, out=self.reply)
         self.last = (self.idx, rep, rx, ft)
         if not validate:
@@ -486,29 +479,17 @@ class _Driver(object):
                 raise RuntimeError('directory create failed: %r' % (
                     errs.unique().cpu().tolist(),))
 
-    def run(self, rb, session=0, bounds=None):
-        """One batch through encode -> server -> decode.  ``bounds`` =
-        host-known upper bounds (request stream, reply stream) in bytes:
-        both streams are then terminated and scanned over the bounds, with
-        no device-to-host read (as GetPipeline does); without them the two
-        stream lengths are read back."""
-        if bounds is not None and not _SYNC_STREAMS:
-            rq, rp = bounds
-            tx, _, _, _ = B.encode_requests(rb, self.xt, out=self.tx,
-                                            terminate=True)
-            rx, _, _, _ = self.server.serve(
-                tx, min(rq + 4, self.tx.numel()), session=session,
-                terminate=True)
-            if self.rscanner is None:
-                self.rscanner = B.FrameScanner(self.batch, self.dev,
-                                               window=self.rwindow)
-            ft = self.rscanner.scan(rx, min(rp + 4, rx.numel()))
-        else:
-            tx, _, total, _ = B.encode_requests(rb, self.xt, out=self.tx)
-            ntx = int(total.item())
-            rx, rtotal, _, _ = self.server.serve(tx, ntx, session=session)
-            nrx = int(rtotal.item())
-            ft = B.frame_scan(rx, nrx, cap=self.batch, window=self.rwindow)
+    def run(self, rb, session=0):
+        """One batch through encode -> server -> decode.  Both streams are
+        scanned over their encoders' device totals: no device-to-host read
+        (``ZKMI_SYNC_STREAMS=1`` reads them back instead, for A/B)."""
+        tx, _, total, _ = B.encode_requests(rb, self.xt, out=self.tx)
+        rx, rtotal, _, _ = self.server.serve(tx, _len(total),
+                                             session=session)
+        if self.rscanner is None:
+            self.rscanner = B.FrameScanner(self.batch, self.dev,
+                                           window=self.rwindow)
+        ft = self.rscanner.scan(rx, _len(rtotal))
         rep = B.decode_replies(rx, ft, self.xt, out=self.reply)
         return rep, rx
 
@@ -576,11 +557,6 @@ class MixPipeline(object):
         self.path_off = [torch.cat([po[r], po[(r - 1) % 3], po[(r - 2) % 3]])
                          for r in range(3)]
         self.path_len = plen[:m].repeat(3)
-        # The mix keeps the two stream-length read-backs: its host bounds
-        # overshoot (alternating ACL sizes, stale-version replies), and the
-        # slack past the terminator holds stale bytes, often zeros, i.e.
-        # 4-byte empty frames, that the speculative K1 walkers then hop
-        # through 4 bytes at a time (measured 3x slower than the read-back).
         self.s = -2
         self.drv.create_dirs(
             [['/mix'], ['/mix/d%05d' % d for d in range(ndirs)]],
@@ -656,12 +632,6 @@ class StormPipeline(object):
                                    device=dev)
         self.acl_id = torch.zeros(batch, dtype=I32, device=dev)
         self.want_len = self.path_len + 10
-        # every request and reply of a step has the same size, so these
-        # bounds are the exact stream lengths (no slack past the terminator)
-        pl = max(len(x) for x in prefixes)
-        acl = len(B._acl_bytes(MIX_ACLS[0]))
-        self.bounds = (batch * (4 + 8 + 4 + pl + 4 + data_bytes + acl + 4),
-                       batch * (4 + 16 + 4 + pl + 10))
         self.removed = torch.zeros(1, dtype=I64, device=dev)
         self.session = 1
         self.inserted = 0
@@ -681,8 +651,7 @@ class StormPipeline(object):
                             self.data_len, self.acl_id, self.path_arena,
                             self.data_arena, self.acl_off, self.acl_len,
                             self.acl_arena)
-        rep, _ = self.drv.run(rb, session=self.session + 1,
-                              bounds=self.bounds)
+        rep, _ = self.drv.run(rb, session=self.session + 1)
         self.last = (rb, rep)
         self.inserted += n
         # the previous session expires: its ephemerals go

@@ -94,6 +94,10 @@ _SIGS = {
     'zk_frame_scan_workspace': (I64, [I64]),
     'zk_frame_scan': (I32, [P, I64, I64, P, I64, P, P, I64, P, P]),
     'zk_frame_scan2': (I32, [P, I64, I64, P, I64, P, P, I64, P, I32, P]),
+    'zk_frame_scan3': (I32, [P, P, I64, I64, P, I64, P, P, I64, P, I32,
+                             P]),
+    'zk_frame_scan_stats': (I32, [P, I64, I32, P, P]),
+    'zk_frame_scan_dbg': (I32, [P, I64]),
     'zk_decode_replies': (I32, [P, P, P, P, I64, P, I64, P, P]),
     'zk_expand_strings': (I32, [P, P, P, P, I64, P, P, P]),
     'zk_expand_acl': (I32, [P, P, P, P, I64, P, P, P, P, P, P]),

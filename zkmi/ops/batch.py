@@ -317,6 +317,25 @@ def frame_window(max_frame):
     return FS_WINDOWS[-1]
 
 
+def _scan_len(buf, n):
+    """(device length pointer or None, capacity) of a K1 call: ``n`` is a
+    host int (scan ``buf[:n]``) or a device int64 scalar tensor holding the
+    length (an encoder's ``total``; the scan reads it on the GPU and
+    covers at most ``buf.numel()`` bytes)."""
+    if n is None:
+        return None, buf.numel()
+    if isinstance(n, torch.Tensor):
+        if n.dtype != I64 or n.device != buf.device or n.numel() < 1:
+            raise TypeError('frame_scan: device length must be an int64 '
+                            'tensor on the buffer\'s device')
+        return n, buf.numel()
+    n = int(n)
+    if n > buf.numel():
+        raise ValueError('frame_scan: n=%d past the buffer (%d bytes)'
+                         % (n, buf.numel()))
+    return None, n
+
+
 class FrameScanner:
     """Reusable K1 state for a stream that is scanned again and again (a
     connection's RX ring, the benchmark's request / reply streams): the
@@ -336,46 +355,64 @@ class FrameScanner:
         self.ws_for = -1            # stream length the workspace covers
 
     def scan(self, buf, n, stream=None):
+        """Frame ``buf[:n]``; ``n`` may be a device int64 length (see
+        :func:`frame_scan`) — then nothing is read back to the host."""
         L = _lib.lib()
-        if n > self.ws_for:
-            wsb = L.zk_frame_scan_workspace(max(n, 2 * self.ws_for))
+        n_dev, ncap = _scan_len(buf, n)
+        if ncap > self.ws_for:
+            cover = max(ncap, 2 * self.ws_for)
+            wsb = L.zk_frame_scan_workspace(cover)
             self.ws = torch.empty(max(wsb, 256), dtype=U8,
                                   device=buf.device)
-            self.ws_for = max(n, 2 * self.ws_for)
+            self.ws_for = cover
         t = self.table
-        check(L.zk_frame_scan2(ptr(buf), n, self.max_packet, ptr(self.ws),
-                               self.ws.numel(), ptr(t.off), ptr(t.length),
-                               self.cap, ptr(t.result), int(self.window),
-                               stream_ptr(stream)), 'zk_frame_scan')
+        check(L.zk_frame_scan3(ptr(buf), ptr(n_dev), ncap, self.max_packet,
+                               ptr(self.ws), self.ws.numel(), ptr(t.off),
+                               ptr(t.length), self.cap, ptr(t.result),
+                               int(self.window), stream_ptr(stream)),
+              'zk_frame_scan')
+        self.last_cap = ncap
         return t
+
+    def chain_stats(self, stream=None):
+        """K1 one-pass chain counters of the last scan (host sync): tiles
+        without a speculated entry, tiles re-walked, repair rounds."""
+        import ctypes
+        L = _lib.lib()
+        out = (ctypes.c_uint32 * 3)()
+        check(L.zk_frame_scan_stats(ptr(self.ws), self.last_cap,
+                                    int(self.window), ctypes.byref(out),
+                                    stream_ptr(stream)), 'frame_scan_stats')
+        return {'no_spec': out[0], 'rewalked': out[1], 'rounds': out[2]}
 
 
 def frame_scan(buf, n=None, max_packet=consts.MAX_PACKET, cap=None,
                stream=None, workspace=None, window=2048):
     """K1: split ``buf[:n]`` (uint8 device tensor) into frames.
 
-    ``cap`` bounds the frame table (default: ``n // 4``, the most frames a
-    stream of ``n`` bytes can hold).  ``window`` is the per-tile fast-path
-    entry window (256..2048 bytes, see :func:`frame_window`): a hint for
-    the usual frame size, never a limit — longer frames are framed exactly
-    on a slower path.  (:class:`FrameScanner` keeps the buffers across
-    calls.)"""
+    ``n``: a host int, or a device int64 tensor holding the stream length
+    (e.g. the ``total`` an encoder returned): the scan then reads it on the
+    GPU, covers at most ``buf.numel()`` bytes and needs no host sync.
+    ``cap`` bounds the frame table (default: a quarter of the bytes, the
+    most frames they can hold).  ``window`` is the per-tile fast-path entry
+    window (256..2048 bytes, see :func:`frame_window`): a hint for the usual
+    frame size, never a limit — longer frames are framed exactly on a
+    slower path.  (:class:`FrameScanner` keeps the buffers across calls.)"""
     L = _lib.lib()
-    if n is None:
-        n = buf.numel()
+    n_dev, ncap = _scan_len(buf, n)
     dev = buf.device
     if cap is None:
-        cap = max(n // 4, 1)
-    wsb = L.zk_frame_scan_workspace(n)
+        cap = max(ncap // 4, 1)
+    wsb = L.zk_frame_scan_workspace(ncap)
     if workspace is None or workspace.numel() < wsb:
         workspace = torch.empty(max(wsb, 256), dtype=U8, device=dev)
     off = torch.empty(cap, dtype=I64, device=dev)
     ln = torch.empty(cap, dtype=I32, device=dev)
-    res = torch.empty(4, dtype=I64, device=dev)     # zeroed by the launcher
-    check(L.zk_frame_scan2(ptr(buf), n, max_packet, ptr(workspace),
-                           workspace.numel(), ptr(off), ptr(ln), cap,
-                           ptr(res), int(window), stream_ptr(stream)),
-          'zk_frame_scan')
+    res = torch.empty(4, dtype=I64, device=dev)     # zeroed by the kernels
+    check(L.zk_frame_scan3(ptr(buf), ptr(n_dev), ncap, max_packet,
+                           ptr(workspace), workspace.numel(), ptr(off),
+                           ptr(ln), cap, ptr(res), int(window),
+                           stream_ptr(stream)), 'zk_frame_scan')
     return FrameTable(off, ln, res)
 
 

@@ -198,7 +198,7 @@ def main():
             'higher_is_better': True,
             'scaling': 'weak',
             'vs_baseline': value / REF_PKTS_PER_S,
-            'dtype': 'bf16',
+            'dtype': 'uint8',
             'data': 'synthetic',
             'config': {
                 'model': 'zk-%s %dk-znode tree, %dB data' % (
@@ -213,7 +213,8 @@ def main():
             'baseline_note': 'vs_baseline = value / 0.51M pkts/s, the '
                              'reference ZKDecodeStream frame+decode on one '
                              'Xeon core (BASELINE.md, local, unpublished)',
-            'dtype_note': 'integer byte codec; no floating-point compute',
+            'dtype_note': 'byte codec over uint8 wire streams and int32/int64 '
+                          'tables; no floating-point compute',
         }
         print(json.dumps(line), flush=True)
     if world > 1:

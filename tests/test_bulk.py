@@ -156,3 +156,17 @@ def test_bulk_gpu_codec(zk, gpu):
         assert res.ok_count() == 2000 - 2000 // 20     # n0002 was deleted
     finally:
         c.close_sync(10)
+
+
+def test_bulk_empty_batch(zk):
+    """An empty bulk completes with an empty result and reserves no xids
+    (it used to fail on a missing attribute)."""
+    c = client(zk.servers())
+    c.wait_connected(10)
+    err, res = _run(c, 'bulk', [])
+    assert err is None
+    assert res.n == 0 and res.packets() == []
+    # the connection keeps working afterwards
+    c.call_sync('create', '/after', b'ok', {})
+    assert c.call_sync('get', '/after')[0] == b'ok'
+    c.close_sync(10)

@@ -176,7 +176,9 @@ def test_session_failover_between_ranks():
 
 
 def test_watch_fanout_uses_one_server_watch():
-    """Only the owner holds the ZooKeeper watch: checked from the server."""
-    from zkmi.parallel import owner_of
-    assert owner_of('/fan', 2) in (0, 1)
-    assert owner_of('/fan', 2) == owner_of('/fan', 2)
+    """Only the owner rank arms the ZooKeeper watch (R1: one server watch
+    per path, the node fans the events out): checked in the fake server's
+    log of the sessions that armed a data watch on the path."""
+    zk = _run('watch_fanout')
+    sids = zk.db.watch_log.get('/fan', set())
+    assert len(sids) == 1, sids

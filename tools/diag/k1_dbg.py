@@ -18,24 +18,27 @@ from zkmi.bench import synthetic as S  # noqa: E402
 
 def dump(name, scanner, nbytes):
     torch.cuda.synchronize()
-    tiles = (scanner.last_cap + 16383) // 16384
-    a = np.zeros(tiles * 6, np.int64)
+    tiles = (scanner.last_cap + 4095) // 4096
+    a = np.zeros(tiles * 8, np.int64)
     _lib.check(_lib.lib().zk_frame_scan_dbg(
         a.ctypes.data_as(ctypes.c_void_p), tiles), 'dbg')
-    a = a.reshape(tiles, 6)
-    nt = (nbytes + 16383) // 16384
+    a = a.reshape(tiles, 8)
+    nt = (nbytes + 4095) // 4096
     a = a[:nt]
     t0 = a[:, 0].min()
     clk = 100.0    # wall_clock64 MHz
-    surv = (a[:, 1] - a[:, 0]) / clk
+    stage = (a[:, 6] - a[:, 0]) / clk
+    front = (a[:, 7] - a[:, 6]) / clk
+    surv = (a[:, 1] - a[:, 7]) / clk
     wait = (a[:, 2] - a[:, 1]) / clk
     walk = (a[:, 3] - a[:, 2]) / clk
     end = (a[:, 3] - t0) / clk
     start = (a[:, 0] - t0) / clk
     print(name, 'tiles', nt)
-    for k, v in (('start', start), ('survivor', surv), ('wait', wait),
+    for k, v in (('start', start), ('stage', stage), ('frontier', front),
+                 ('survivor', surv), ('wait', wait),
                  ('walk', walk), ('end', end), ('np', a[:, 4]),
-                 ('js', a[:, 5])):
+                 ('surv', a[:, 5])):
         print('  %-9s p50 %8.2f p90 %8.2f max %8.2f mean %8.2f' % (
             k, np.percentile(v, 50), np.percentile(v, 90), v.max(),
             v.mean()))

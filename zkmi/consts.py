@@ -2,8 +2,9 @@
 
 Parity: ``lib/zk-consts.js:13-138`` of the reference (perm masks, create flags,
 error codes + text, opcodes, notification types, keeper states, special xids).
-The same numbers are mirrored for native code in ``csrc/proto/zk_proto.h``;
-``tests/test_proto.py`` checks the two tables agree.
+The same numbers are mirrored for native code in ``csrc/kernels/zk_common.h``
+(HIP kernels) and ``csrc/host/zk_host_codec.cpp``; ``tests/test_proto.py``
+checks the tables agree.
 """
 
 PERM_MASKS = {

@@ -390,16 +390,17 @@ class ZKConnectionFSM(FSM):
         if not self.isInState('connected'):
             raise ZKProtocolError('CONNECTION_LOSS', 'Not connected.')
         n = batch.n
+        batch.cb = cb
+        batch.t_submit = time.perf_counter()
+        if n == 0:
+            # nothing to send: no xids, no encode, an empty result
+            self.fsm_loop.call_soon(lambda: cb(None, batch.finish()))
+            return
         x0 = self.xid
         if x0 + n > 0x7fffffff:
             x0 = 0
         self.xid = (x0 + n) & 0x7fffffff
         wire = batch.encode(x0)
-        batch.cb = cb
-        batch.t_submit = time.perf_counter()
-        if n == 0:
-            self.loop.call_soon(lambda: cb(None, batch.finish()))
-            return
         self.bulks.append(batch)
         self.log.trace({'xid0': x0, 'n': n, 'bytes': len(wire)},
                        'sent bulk batch')

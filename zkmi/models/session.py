@@ -35,8 +35,15 @@ class ExpiryTimer(EventEmitter):
 
     def reset(self, timeout_ms):
         now = self.loop.time_ms()
+        shorter = self.timeout_ms is not None and timeout_ms < self.timeout_ms
         self.timeout_ms = timeout_ms
         self.deadline = now + timeout_ms
+        if self._h is not None and shorter:
+            # a shorter negotiated timeout (a reattach to another server):
+            # the pending wake-up would fire late, re-arm it
+            # (lib/zk-session.js:99-108 clears and re-sets on every reset)
+            self._h.cancel()
+            self._h = None
         if self._h is None:
             self._h = self.loop.call_later(timeout_ms, self._fire)
 

@@ -75,23 +75,25 @@ class SessionGroup(object):
     # -- low level: variable-size all-gather of byte strings --------------
 
     def _allgather_bytes(self, payload):
+        """Variable-size all-gather: one size exchange (a single host read
+        of the world's sizes), one padded payload all-gather, one copy of
+        the gathered block to the host."""
         dev = self.device
+        W = self.world
         n = torch.tensor([len(payload)], dtype=torch.int64, device=dev)
-        sizes = [torch.zeros(1, dtype=torch.int64, device=dev)
-                 for _ in range(self.world)]
-        dist.all_gather(sizes, n, group=self.group)
-        sizes = [int(s.item()) for s in sizes]
+        sizes_t = torch.empty(W, dtype=torch.int64, device=dev)
+        dist.all_gather_into_tensor(sizes_t, n, group=self.group)
+        sizes = sizes_t.cpu().tolist()
         mx = max(max(sizes), 1)
         buf = torch.zeros(mx, dtype=torch.uint8, device=dev)
         if payload:
             buf[:len(payload)] = torch.frombuffer(bytearray(payload),
                                                   dtype=torch.uint8).to(dev)
-        outs = [torch.empty(mx, dtype=torch.uint8, device=dev)
-                for _ in range(self.world)]
-        dist.all_gather(outs, buf, group=self.group)
+        outs = torch.empty(W * mx, dtype=torch.uint8, device=dev)
+        dist.all_gather_into_tensor(outs, buf, group=self.group)
         self.stats['allgather_bytes'] += sum(sizes)
-        return [bytes(o[:s].cpu().numpy().tobytes())
-                for o, s in zip(outs, sizes)]
+        host = outs.cpu().numpy().tobytes()
+        return [host[r * mx:r * mx + s] for r, s in enumerate(sizes)]
 
     def _broadcast_bytes(self, payload, src):
         dev = self.device
@@ -170,7 +172,12 @@ class SessionGroup(object):
         mine = [p for p in uniq if owner_of(p, self.world) == self.rank]
         self.stats['batched_get_unique'] += len(uniq)
         self.stats['batched_get_requested'] += sum(len(x) for x in lists)
-        results = self._fetch_all(mine, timeout)
+        # never raise between the two collectives: a rank that left here
+        # would leave every other rank blocked in the second all-gather
+        try:
+            results = self._fetch_all(mine, timeout)
+        except Exception as e:                  # noqa: BLE001
+            results = {p: e for p in mine}
         out = jute.JuteWriter()
         out.write_int(len(mine))
         for p in mine:
@@ -217,7 +224,13 @@ class SessionGroup(object):
                 self.client.get(p, mk(p))
         self.client.loop.run(go)
         if not done.wait(timeout):
-            raise TimeoutError('batched_get timed out')
+            # the paths still outstanding fail with OPERATION_TIMEOUT; the
+            # collective goes on (late callbacks only overwrite res entries)
+            from ..errors import ZKError
+            from .. import consts
+            err = ZKError('OPERATION_TIMEOUT',
+                          consts.ERR_TEXT.get('OPERATION_TIMEOUT', ''))
+            return {p: res.get(p, err) for p in paths}
         return res
 
     # -- R1 -----------------------------------------------------------------

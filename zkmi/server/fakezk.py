@@ -103,6 +103,9 @@ class ZKDatabase(object):
         self._sid_ctr = 0
         self._server_id = server_id
         self.stats = {'requests': 0, 'notifications': 0}
+        # path -> every session that ever armed a data watch on it (tests:
+        # "only the owner rank holds the ZooKeeper watch")
+        self.watch_log = {}
         root = Node(b'', [self._world()], Stat())
         self.nodes['/'] = root
         self._mk('/zookeeper', b'', [self._world()], 0)
@@ -189,6 +192,8 @@ class ZKDatabase(object):
         if sid is None:
             return
         table.setdefault(path, set()).add(sid)
+        if table is self.data_watches:
+            self.watch_log.setdefault(path, set()).add(sid)
 
     def _trigger(self, table, path, evtype, suppress=None):
         sids = table.pop(path, None)

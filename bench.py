@@ -82,6 +82,99 @@ def measure_rtt(port, n=2000):
     return statistics.median(lat), lat[int(0.99 * len(lat))]
 
 
+def run_ensemble(a):
+    """BASELINE config 4 (zkmi/parallel/ensemble.py): 3-server ensemble,
+    one session per rank, member failover with watch replay, every event
+    fanned out to every rank (R1: wire frames all-gathered on the collective
+    device, K1 + K2-K8 decoded on each GPU).  Value: watch-event deliveries
+    per second over the node (events x ranks).  Runs without a GPU too
+    (gloo rehearsal: host decode)."""
+    from zkmi.parallel import ensemble as E
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    # the ensemble process starts before anything touches the GPU
+    ctl = E.EnsembleControl(3) if rank == 0 else None
+    backend = os.environ.get('ZKMI_BENCH_BACKEND', 'nccl')
+    ndev = torch.cuda.device_count()
+    if ndev == 0:
+        backend, dev = 'gloo', None
+    else:
+        dev = torch.device('cuda', local % ndev if backend == 'gloo'
+                           else local)
+        torch.cuda.set_device(dev)
+    if world > 1:
+        if backend == 'nccl':
+            dist.init_process_group('nccl', device_id=dev)
+        else:
+            dist.init_process_group('gloo')
+    try:
+        wl = E.EnsembleWorkload(ctl, n_paths=a.paths, writes=a.writes,
+                                failover_every=a.failover_every,
+                                codec_device=dev)
+        for _ in range(a.warmup):
+            wl.step()
+        if world > 1:
+            dist.barrier()
+        if dev is not None:
+            torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        got = 0
+        for _ in range(a.steps):
+            got += wl.step()
+        if world > 1:
+            dist.barrier()
+        if dev is not None:
+            torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        bad = wl.verify()
+        stats = torch.tensor([elapsed * 1e6, got, 1 if bad else 0,
+                              wl.failovers, wl.rearmed(),
+                              wl.fan.stats['decoded_gpu'],
+                              wl.fan.stats['decoded_host']],
+                             dtype=torch.float64, device=wl.coll)
+        if world > 1:
+            mx = stats[:1].clone()
+            dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+            dist.all_reduce(stats, op=dist.ReduceOp.SUM)
+            stats[0] = mx[0]
+        el_us, total, nbad, fo, rep, dg, dh = stats.cpu().tolist()
+        if nbad:
+            raise SystemExit('ensemble: rank %d saw %r' % (rank, bad)
+                             if bad else 'ensemble: a rank failed')
+        codec_calls = wl.client.loop.run(
+            lambda: dict(getattr(wl.client.getSession().getConnection(),
+                                 'gpu', None).calls)
+            if dev is not None else {})
+        wl.close()
+    finally:
+        if ctl is not None:
+            ctl.close()
+    value = total / (el_us / 1e6)
+    if rank == 0:
+        print(json.dumps({
+            'metric': 'ZK ops/sec (whole node) + p50 get() RTT, 1M-znode '
+                      'synthetic tree',
+            'value': value, 'unit': 'ops/s', 'n_gpus': world,
+            'steps': a.steps, 'warmup': a.warmup,
+            'ms_per_step': el_us / 1e3 / a.steps,
+            'higher_is_better': True, 'scaling': 'weak',
+            'vs_baseline': None, 'dtype': 'uint8', 'data': 'synthetic',
+            'config': {'model': 'zk-ensemble 3-server failover + watch '
+                                'replay, %d znodes' % a.paths,
+                       'global_batch': a.writes, 'seq_len': 1,
+                       'parallelism': 'dp%d' % world},
+            'ops_note': 'watch-event deliveries over the node (every event '
+                        'reaches every rank exactly once, checked)',
+            'failovers': int(fo // world),
+            'watches_rearmed_by_set_watches': int(rep),
+            'events_decoded_on_gpu': int(dg), 'events_decoded_on_host': int(dh),
+            'rank0_gpu_codec_calls': codec_calls,
+            'backend': backend if world > 1 else None}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -99,9 +192,20 @@ def main():
                          'with the other\'s bandwidth-bound ones, more '
                          'streams than GPU_MAX_HW_QUEUES allows were '
                          'unstable)')
-    ap.add_argument('--workload', choices=('get', 'mix', 'storm', 'watch'),
+    ap.add_argument('--workload', choices=('get', 'mix', 'storm', 'watch',
+                                           'ensemble'),
                     default='get')
+    ap.add_argument('--paths', type=int, default=512,
+                    help='ensemble: watched znodes (one owner rank each)')
+    ap.add_argument('--writes', type=int, default=128,
+                    help='ensemble: znodes set per step')
+    ap.add_argument('--failover-every', type=int, default=4,
+                    help='ensemble: every k-th step kills the member rank 0 '
+                         'is on and makes that step\'s writes during the '
+                         'outage (replayed through SET_WATCHES)')
     a = ap.parse_args()
+    if a.workload == 'ensemble':
+        return run_ensemble(a)
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))

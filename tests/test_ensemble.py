@@ -1,0 +1,114 @@
+"""BASELINE config 4 as a multi-rank workload (zkmi/parallel/ensemble.py):
+a 3-member ensemble, one session per rank, member failover with watch
+replay through SET_WATCHES, every event fanned out to every rank.
+
+CPU: gloo, world 2 and 4, host decode of the fanned-out wire frames.  GPU:
+one rank with the live connection's K9 / K11 records and the fan-out's K1 +
+K2-K8 decode on the device."""
+
+import os
+import socket
+import sys
+import traceback
+
+import pytest
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, mport, steps, errq, outq):
+    try:
+        sys.path.insert(0, ROOT)
+        import torch.distributed as dist
+        dist.init_process_group('gloo', init_method='tcp://127.0.0.1:%d'
+                                % mport, rank=rank, world_size=world)
+        from zkmi.parallel import ensemble as E
+        ctl = E.EnsembleControl(3) if rank == 0 else None
+        try:
+            wl = E.EnsembleWorkload(ctl, n_paths=48, writes=12,
+                                    failover_every=2, codec_device=None)
+            got = [wl.step() for _ in range(steps)]
+            bad = wl.verify()
+            outq.put((rank, bad, got, wl.failovers, wl.rearmed(),
+                      len(wl.replayed), dict(wl.fan.stats)))
+            dist.barrier()
+            wl.close()
+        finally:
+            if ctl is not None:
+                ctl.close()
+        dist.destroy_process_group()
+    except BaseException:
+        errq.put((rank, traceback.format_exc()))
+        raise
+
+
+def _run(world, steps):
+    ctx = mp.get_context('spawn')
+    errq, outq = ctx.SimpleQueue(), ctx.SimpleQueue()
+    try:
+        mp.start_processes(_worker, args=(world, _free_port(), steps, errq,
+                                          outq),
+                           nprocs=world, join=True, start_method='spawn')
+    except Exception:
+        msgs = []
+        while not errq.empty():
+            msgs.append('rank %d:\n%s' % errq.get())
+        raise AssertionError('\n'.join(msgs) or 'worker failed')
+    res = {}
+    while not outq.empty():
+        r = outq.get()
+        res[r[0]] = r[1:]
+    return res
+
+
+@pytest.mark.parametrize('world', [2, 4])
+def test_ensemble_failover_replay_fanout(world):
+    steps = 4                               # failovers at steps 1 and 3
+    res = _run(world, steps)
+    assert sorted(res) == list(range(world))
+    rearmed = 0
+    for rank, (bad, got, fo, rea, replayed, st) in res.items():
+        # every event (initial arm, live, replayed) exactly once per rank
+        assert bad is None, (rank, bad)
+        assert got == [12] * steps, (rank, got)
+        assert fo == 2 and replayed == 24
+        assert st['decoded_host'] == 48 + 12 * steps
+        rearmed += rea
+    # the killed members' sessions resumed their watches (SET_WATCHES)
+    assert rearmed > 0
+
+
+@pytest.mark.gpu
+def test_ensemble_gpu_codec_and_fanout_decode():
+    """One rank on the GPU: its reconnects run K9 (ConnectRequest encode,
+    ConnectResponse decode) and its watch resume K11 (SET_WATCHES); the
+    fan-out frames are decoded by K1 + K2-K8."""
+    import torch
+    from zkmi.parallel import ensemble as E
+    dev = torch.device('cuda', 0)
+    ctl = E.EnsembleControl(3)
+    try:
+        wl = E.EnsembleWorkload(ctl, n_paths=40, writes=10,
+                                failover_every=2, codec_device=dev)
+        for _ in range(4):
+            assert wl.step() == 10
+        assert wl.verify() is None
+        assert wl.fan.stats['decoded_gpu'] == 40 + 40
+        assert wl.rearmed() == 40 * 2        # one resume per failover
+        from zkmi.models import gpucodec
+        calls = gpucodec.for_device(dev).calls
+        assert calls['connect_request'] >= 3          # initial + 2 failovers
+        assert calls['connect_response'] >= 3
+        assert calls['set_watches'] >= 2
+        wl.close()
+    finally:
+        ctl.close()

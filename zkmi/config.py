@@ -3,6 +3,7 @@
 expiry / ping-timeout scenarios run in seconds."""
 
 from dataclasses import dataclass, field
+from typing import Optional
 
 
 @dataclass
@@ -37,3 +38,7 @@ class ClientConfig(object):
     shuffle_backends: bool = False
     # lib/client.js:173-176 — closing progress log interval
     close_log_interval_ms: int = 5000
+    # not in the reference: a GPU (e.g. 'cuda:0') whose HIP kernels encode
+    # the ConnectRequest (K9) and SET_WATCHES (K11) records and decode the
+    # ConnectResponse (K9) of every (re)connect (models/gpucodec.py)
+    codec_device: Optional[str] = None

@@ -25,6 +25,7 @@ from ..runtime.emitter import EventEmitter
 from ..runtime.fsm import FSM
 from ..runtime.tcp import TcpSocket
 from ..streams import ZKDecoder, ZKEncoder
+from . import gpucodec
 
 
 class ZKRequest(EventEmitter):
@@ -66,6 +67,7 @@ class ZKConnectionFSM(FSM):
         self.tracer = tracer
         self.decoder = None
         self.encoder = None
+        self.gpu = None
         self.xid_map = {}
         self.xid = 0
         self.bulks = []                 # in-flight BulkBatch (models/bulk.py)
@@ -135,7 +137,8 @@ class ZKConnectionFSM(FSM):
 
     def state_connecting(self, S):
         self.decoder = ZKDecoder(self.config.max_packet)
-        self.encoder = ZKEncoder(self.xid_map)
+        self.gpu = gpucodec.for_device(self.config.codec_device)
+        self.encoder = ZKEncoder(self.xid_map, self.gpu)
         self.log = self.log.child(zkAddress=self.server['address'],
                                   zkPort=self.server['port'])
         self.log.trace('attempting new connection')
@@ -166,7 +169,10 @@ class ZKConnectionFSM(FSM):
                 S.gotoState('error')
                 return
             try:
-                pkt = codec.decode_connect_response(body)
+                if self.gpu is not None:
+                    pkt = self.gpu.connect_response(body)
+                else:
+                    pkt = codec.decode_connect_response(body)
             except (ZKDecodeError, ValueError) as e:
                 self.last_error = ZKProtocolError(
                     'BAD_DECODE', 'Failed to decode ConnectResponse: %s: %s'

@@ -85,6 +85,7 @@ class ZKSession(FSM):
         self.config = config
         self.last_attach = 0
         self.last_zxid = 0
+        self.rearmed = 0            # watches re-armed by SET_WATCHES resumes
         self.session_id = 0
         self.passwd = b'\0' * 8
         collector.counter(METRIC_ZK_NOTIFICATION_COUNTER,
@@ -360,6 +361,7 @@ class ZKSession(FSM):
             return
         zxid = self.last_zxid
         self.log.info('re-arming %d node watchers at zxid %x', count, zxid)
+        self.rearmed += count
 
         def done(err):
             if err is not None:

@@ -665,6 +665,26 @@ class FakeEnsemble(object):
     def servers(self):
         return [m.address for m in self.members]
 
+    def index_of(self, port):
+        for i, m in enumerate(self.members):
+            if m.port == port:
+                return i
+        return -1
+
+    def outage(self, i, sets=()):
+        """Kill member ``i`` (its sockets close, its sessions stay alive, as
+        a killed ZooKeeper server, test/multi-node.test.js:309-316) and apply
+        ``sets`` = [(path, data)] in the same loop turn, so every write lands
+        while the member's clients are detached: their reconnect must replay
+        the changes through SET_WATCHES (zk-session.js:421-471).  Returns
+        the zxid after the writes."""
+        def go():
+            self.members[i].stop()
+            for p, d in sets:
+                self.db.set_data(p, d, -1)
+            return self.db.zxid
+        return self.loop.run(go)
+
     def shutdown(self):
         for m in self.members:
             m.stop()

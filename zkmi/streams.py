@@ -76,21 +76,29 @@ class ZKEncoder(object):
     """Outbound framing; records ``xid -> opcode`` for the decoder
     (``zk-streams.js:145``)."""
 
-    __slots__ = ('xid_map', 'frames_out')
+    __slots__ = ('xid_map', 'frames_out', 'gpu')
 
-    def __init__(self, xid_map):
+    def __init__(self, xid_map, gpu=None):
         self.xid_map = xid_map
         self.frames_out = 0
+        # GpuControlCodec (models/gpucodec.py): K9 / K11 for the handshake
+        # and SET_WATCHES records when the client has a codec device
+        self.gpu = gpu
 
     def connect_request(self, pkt):
         self.frames_out += 1
+        if self.gpu is not None:
+            return self.gpu.connect_request(pkt)
         return codec.frame(codec.encode_connect_request(pkt))
 
     def request(self, pkt):
         xid = pkt['xid']
         if not isinstance(xid, int):
             raise TypeError('xid must be an int')
-        out = codec.frame(codec.encode_request(pkt))
+        if self.gpu is not None and pkt['opcode'] == 'SET_WATCHES':
+            out = self.gpu.set_watches(pkt)
+        else:
+            out = codec.frame(codec.encode_request(pkt))
         self.xid_map[xid] = pkt['opcode']
         self.frames_out += 1
         return out

@@ -168,7 +168,8 @@ def run_ensemble(a):
                         'reaches every rank exactly once, checked)',
             'failovers': int(fo // world),
             'watches_rearmed_by_set_watches': int(rep),
-            'events_decoded_on_gpu': int(dg), 'events_decoded_on_host': int(dh),
+            'events_decoded_on_gpu': int(dg),
+            'events_decoded_on_host': int(dh),
             'rank0_gpu_codec_calls': codec_calls,
             'backend': backend if world > 1 else None}), flush=True)
     if world > 1:
@@ -195,6 +196,12 @@ def main():
     ap.add_argument('--workload', choices=('get', 'mix', 'storm', 'watch',
                                            'ensemble'),
                     default='get')
+    ap.add_argument('--sharded', action='store_true',
+                    help='get: one tree sharded by path hash over the '
+                         'ranks; every read is routed to its owner rank '
+                         'with all_to_all over RCCL/xGMI (R2, '
+                         'zkmi/parallel/sharded.py) instead of served by '
+                         'the local replica')
     ap.add_argument('--paths', type=int, default=512,
                     help='ensemble: watched znodes (one owner rank each)')
     ap.add_argument('--writes', type=int, default=128,
@@ -227,7 +234,16 @@ def main():
     cdev = dev if backend == 'nccl' else torch.device('cpu')
 
     from zkmi.bench import synthetic as S
-    if a.workload == 'get':
+    if a.workload == 'get' and a.sharded:
+        from zkmi.parallel.sharded import ShardedGetPipeline
+        # every rank holds the same layout and data; its index covers only
+        # the leaves whose path hashes to it
+        tree = S.GpuTree(a.nodes, a.data_bytes, device=dev, seed=0,
+                         shard=(rank, world))
+        pipe = ShardedGetPipeline(tree, a.batch, seed=rank,
+                                  coll_device=cdev)
+        per_step = a.batch
+    elif a.workload == 'get':
         tree = S.GpuTree(a.nodes, a.data_bytes, device=dev, seed=rank)
         pipe = S.GetPipeline(tree, a.batch, seed=rank, streams=a.streams)
         per_step = a.batch
@@ -305,12 +321,14 @@ def main():
             'dtype': 'uint8',
             'data': 'synthetic',
             'config': {
-                'model': 'zk-%s %dk-znode tree, %dB data' % (
-                    a.workload, a.nodes // 1000, a.data_bytes),
+                'model': 'zk-%s%s %dk-znode tree, %dB data' % (
+                    a.workload, ' sharded' if a.sharded else '',
+                    a.nodes // 1000, a.data_bytes),
                 'global_batch': per_step * world,
                 'seq_len': 1,
                 'parallelism': 'dp%d' % world,
             },
+            'r2_bytes_sent': getattr(pipe, 'stats', {}).get('bytes_sent'),
             'p50_get_rtt_us': rtt50,
             'p99_get_rtt_us': rtt99,
             'batch_latency_ms': elapsed / a.steps * 1e3,

@@ -54,6 +54,27 @@ def _next_pow2(x):
     return p
 
 
+NODE_FREE = -2           # node_parent of an unused node (tree.hip)
+
+
+def path_owner(paths, world):
+    """Owner rank of every path: FNV-1a 32 of the bytes mod ``world`` —
+    the host mirror of csrc/kernels/route.hip's router."""
+    out = np.empty(len(paths), np.int64)
+    by_len = {}
+    for i, p in enumerate(paths):
+        by_len.setdefault(len(p), []).append(i)
+    for ln, ids in by_len.items():
+        m = np.frombuffer(b''.join(paths[i] for i in ids),
+                          np.uint8).reshape(len(ids), ln) if ln else \
+            np.zeros((len(ids), 0), np.uint8)
+        h = np.full(len(ids), 2166136261, np.uint64)
+        for k in range(ln):
+            h = ((h ^ m[:, k]) * np.uint64(16777619)) & np.uint64(0xffffffff)
+        out[ids] = (h % np.uint64(world)).astype(np.int64)
+    return out
+
+
 def slot_bytes(data_cap):
     """Bytes of one wire-format node slot (zk_batch.h ZkNodeStore)."""
     return _lib.SLOT_DATA + ((data_cap + 15) & ~15) + 4
@@ -65,7 +86,7 @@ class GpuTree(object):
     ``czxid == v + 1``."""
 
     def __init__(self, n_nodes=1_000_000, data_bytes=100, fanout=1000,
-                 device=None, spare=0.25, seed=0):
+                 device=None, spare=0.25, seed=0, shard=None, ctime_ms=None):
         dev = torch.device(device) if device is not None else \
             torch.device('cuda', torch.cuda.current_device())
         self.device = dev
@@ -145,9 +166,18 @@ class GpuTree(object):
         self.hcap = hcap
         self._struct = self._make_struct(hcap - 1)
         sp = _lib.stream_ptr()
+        now = int(time.time() * 1000) if ctime_ms is None else ctime_ms
         _lib.check(L.zk_tree_fill(ctypes.byref(self._struct), 0, nst,
-                                  _lib.ptr(nk), int(time.time() * 1000), sp),
+                                  _lib.ptr(nk), now, sp),
                    'zk_tree_fill')
+        # shard = (rank, world): this replica indexes only the leaves whose
+        # path hashes to `rank` (zkmi/parallel/sharded.py routes every read
+        # there); the rest stay in the layout, unreachable by lookup
+        self.shard = shard
+        if shard is not None and shard[1] > 1:
+            own = path_owner(enc[leaf0:], shard[1])
+            gone = np.nonzero(own != shard[0])[0] + leaf0
+            self.node_parent[torch.from_numpy(gone).to(dev)] = NODE_FREE
         _lib.check(L.zk_tree_build(ctypes.byref(self._struct), 0, nst, sp),
                    'zk_tree_build')
         torch.cuda.synchronize(dev)
@@ -273,6 +303,7 @@ class GpuServer(object):
         out, rec_off, total, err = B.encode_responses(
             r, self.tree.store, self.out.numel(), out=self.out,
             presized=self.presized, terminate=terminate)
+        self.last_rec_off = rec_off         # reply frame starts (R2 splits)
         return out, total, err, ft
 
 

@@ -111,6 +111,9 @@ _SIGS = {
     'zk_tree_serve': (I32, [P, P, P, P, I64, P, P, P, P, P, P, P, P, P, P,
                             I64, I64, P]),
     'zk_tree_expire': (I32, [P, I64, I64, P, P]),
+    'zk_route_workspace': (I64, [I64, I32]),
+    'zk_route_requests': (I32, [I64, I32, P, P, P, P, P, P, P, P, P, P, P, P,
+                                P]),
     'zk_bench_gen_get': (I32, [I64, ctypes.c_uint64, I64, I64, I32, P, P,
                                P, P, P, P]),
     'zk_bench_check_get': (I32, [I64, P, P, P, P, P, P, P, P, P, P, P]),

@@ -99,7 +99,7 @@ class WireFanout(object):
                 'opcode': 'GET_DATA', 'data': data, 'stat': stat})))
         return b''.join(parts)
 
-    # -- the collective ------------------------------------------------------
+    # -- the collective -------------------------------------------------------
 
     def exchange(self, events):
         """Send this rank's ``events`` (at most :data:`KMAX`), receive every
@@ -330,7 +330,7 @@ class EnsembleWorkload(object):
         self.expected.update((p, b'init') for p in self.paths)
         self._deliver_until(len(self.paths))
 
-    # -- plumbing --------------------------------------------------------------
+    # -- plumbing -------------------------------------------------------------
 
     def _barrier(self):
         if self.world > 1:
@@ -398,7 +398,7 @@ class EnsembleWorkload(object):
         port = self.client.loop.run(go)
         return self.ports.index(port) if port in self.ports else -1
 
-    # -- one step ------------------------------------------------------------
+    # -- one step -------------------------------------------------------------
 
     def step(self):
         """One step (collective); returns the events this rank received."""

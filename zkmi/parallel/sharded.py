@@ -105,7 +105,7 @@ class ShardedGetPipeline(object):
             dist.all_to_all_single(out, inp, out_splits, in_splits,
                                    group=self.group)
             return out
-        o = torch.empty(out.numel(), dtype=out.dtype, device=self.coll)
+        o = torch.empty(out.shape, dtype=out.dtype, device=self.coll)
         dist.all_to_all_single(o, inp.to(self.coll), out_splits, in_splits,
                                group=self.group)
         out.copy_(o)

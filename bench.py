@@ -254,8 +254,9 @@ def main():
         per_step = a.batch * world      # notifications decoded per rank
     else:
         # room for the write working set next to the 1M static nodes: the
-        # mix keeps 3 generations of batch/3 nodes, the storm 2 sessions'
-        spare = (a.batch * (1 if a.workload == 'mix' else 2) + 8192) / a.nodes
+        # mix keeps 3 generations of batch/3 nodes, the storm up to 3
+        # batches (the expiring session's two, the new session's first)
+        spare = (a.batch * (1 if a.workload == 'mix' else 3) + 8192) / a.nodes
         tree = S.GpuTree(a.nodes, a.data_bytes, device=dev, seed=rank,
                          spare=spare + 0.05)
         if a.workload == 'mix':

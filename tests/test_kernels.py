@@ -623,11 +623,56 @@ def test_gpu_mix_pipeline(gpu):
 
 def test_gpu_storm_pipeline(gpu):
     from zkmi.bench.synthetic import StormPipeline
-    tree = _small_tree(gpu, 20000, 37, spare=1.0)
+    tree = _small_tree(gpu, 20000, 37, spare=1.5)
     pipe = StormPipeline(tree, 8192, ndirs=64)
     for _ in range(12):                 # crosses at least one rehash
         ok = pipe.step()
         assert int(ok.item()) == 8192
+    # 13 steps: 7 sessions born, 6 resumed (5 next to a refused expired
+    # one), 6 expired with exactly their two batches
+    assert pipe.stats == {'born': 7, 'resumed': 6, 'expired': 6,
+                          'expired_resume_refused': 5}
+    assert bool(pipe.hs_ok.item())
+
+
+def test_gpu_session_handshake_k9_server(gpu):
+    """The GPU server's handshake against the oracle's records: new
+    session, resume with the right password, wrong password and unknown id
+    get the expired answer, a too-new lastZxidSeen is refused."""
+    from zkmi.bench.synthetic import GpuSessionTable
+    from zkmi.ops import _lib
+    tree = _small_tree(gpu, 1000, 16)
+    st = GpuSessionTable(tree)
+
+    def hs(reqs, n_new):
+        raw = b''.join(jute.frame(jute.encode_connect_request(q))
+                       for q in reqs)
+        buf = _dev_bytes(raw, gpu)
+        resp, bound, oc = st.connect(buf, len(raw), n_new)
+        rb = bytes(resp[:41 * len(reqs)].cpu().numpy().tobytes())
+        frames, _, bad = jute.scan_frames(rb)
+        assert bad < 0 and len(frames) == len(reqs)
+        return ([jute.decode_connect_response(rb[o:o + n])
+                 for o, n in frames], oc[:len(reqs)].cpu().tolist())
+    base = {'protocolVersion': 0, 'lastZxidSeen': 0, 'timeOut': 100000,
+            'sessionId': 0, 'passwd': b'\0' * 8}
+    (r,), oc = hs([base], 1)
+    assert oc == [_lib.SC_NEW] and r['sessionId'] == st.sid_of(0)
+    assert r['timeOut'] == 40000 and len(r['passwd']) == 16
+    sid, pw = r['sessionId'], r['passwd']
+    reqs = [dict(base, sessionId=sid, passwd=pw, timeOut=1000),
+            dict(base, sessionId=sid, passwd=b'x' * 16),
+            dict(base, sessionId=st.sid_of(7), passwd=pw),
+            dict(base, sessionId=sid, passwd=pw, lastZxidSeen=1 << 50)]
+    rs, oc = hs(reqs, 0)
+    assert oc == [_lib.SC_RESUMED, _lib.SC_EXPIRED, _lib.SC_EXPIRED,
+                  _lib.SC_REFUSED]
+    assert rs[0] == {'protocolVersion': 0, 'timeOut': 4000,
+                     'sessionId': sid, 'passwd': pw}
+    assert [x['sessionId'] for x in rs[1:]] == [0, 0, 0]
+    st.close(torch.tensor([sid], dtype=torch.int64, device=gpu))
+    (r,), oc = hs([dict(base, sessionId=sid, passwd=pw)], 0)
+    assert oc == [_lib.SC_EXPIRED] and r['sessionId'] == 0
 
 
 def test_gpu_watch_pipeline_single_rank(gpu):

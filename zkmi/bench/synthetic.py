@@ -631,22 +631,102 @@ class MixPipeline(object):
                 'counters': self.tree.counters.cpu().tolist()}
 
 
-class StormPipeline(object):
-    """EPHEMERAL|SEQUENTIAL create storm with session expiry (BASELINE
-    config 5, nasty.test.js shape).
+class GpuSessionTable(object):
+    """The GPU server's session table in HBM and its handshake (K9 server
+    side, csrc/kernels/session.hip): ConnectRequest frames in,
+    ConnectResponse frames out, new / resumed / expired decided on the
+    device.  Session ids are ``server_id << 56 | (index + 1)`` in allocation
+    order, so the server's host side knows the id it handed out without a
+    read-back."""
 
-    Step ``s``: session ``s+1`` creates ``batch`` ephemeral sequential nodes
-    ``/storm/dDDDDD/e-<seq>`` (the server appends the parent's cversion),
-    then session ``s`` expires and the server removes the ephemerals it
-    created one step earlier.  The hash index is rebuilt whenever the
-    tombstones left by never-reused sequential names would fill it."""
+    MIN_TO, MAX_TO = 4000, 40000        # 2 and 20 ticks of 2 s
+
+    def __init__(self, tree, cap=1 << 16, server_id=1, secret=0x5A4B1D):
+        dev = tree.device
+        self.tree = tree
+        self.dev = dev
+        self.cap = cap
+        self.server_id = server_id
+        self.secret = secret
+        self.sid = torch.zeros(cap, dtype=I64, device=dev)
+        self.passwd = torch.zeros(cap * 16, dtype=U8, device=dev)
+        self.timeout = torch.zeros(cap, dtype=I32, device=dev)
+        self.state = torch.zeros(cap, dtype=I32, device=dev)
+        self.next = torch.zeros(1, dtype=I64, device=dev)
+        self.allocated = 0              # host mirror of `next`
+        self._st = _lib.ZkSessionTable(
+            self.sid.data_ptr(), self.passwd.data_ptr(),
+            self.timeout.data_ptr(), self.state.data_ptr(),
+            self.next.data_ptr(), cap)
+        self.scanner = B.FrameScanner(64, dev, window=256)
+        self.resp = torch.empty(64 * _lib.CR_RESP_BYTES, dtype=U8, device=dev)
+        self.resp_sid = torch.empty(64, dtype=I64, device=dev)
+        self.outcome = torch.empty(64, dtype=I32, device=dev)
+
+    def sid_of(self, index):
+        return (self.server_id << 56) | (index + 1)
+
+    def connect(self, rx, nbytes, n_new):
+        """Serve the ConnectRequest stream ``rx[:nbytes]`` (at most 64
+        frames); ``n_new`` = how many of them ask for a new session (host
+        bookkeeping of the allocation counter).  Returns (response stream
+        [41 * frames], bound session ids, outcome codes)."""
+        ft = self.scanner.scan(rx, nbytes)
+        _lib.check(_lib.lib().zk_session_connect(
+            _lib.ptr(rx), _lib.ptr(ft.off), _lib.ptr(ft.length),
+            _lib.ptr(ft.count), 64, ctypes.byref(self._st), self.server_id,
+            self.secret, self.MIN_TO, self.MAX_TO,
+            _lib.ptr(self.tree.counters[_lib.TC_ZXID:]), _lib.ptr(self.resp),
+            _lib.ptr(self.resp_sid), _lib.ptr(self.outcome),
+            _lib.stream_ptr()), 'zk_session_connect')
+        self.allocated += n_new
+        return self.resp, self.resp_sid, self.outcome
+
+    def close(self, sids):
+        """Expire / close sessions (device int64 tensor of ids)."""
+        _lib.check(_lib.lib().zk_session_close(
+            ctypes.byref(self._st), _lib.ptr(sids), sids.numel(),
+            _lib.stream_ptr()), 'zk_session_close')
+
+
+class StormPipeline(object):
+    """EPHEMERAL|SEQUENTIAL create storm with session expire AND resume
+    (BASELINE config 5; lib/zk-session.js:147-205, :265-339,
+    test/nasty.test.js:40-103).
+
+    Session ``k`` lives three steps:
+
+      step 2k    born: the client K9-encodes a ConnectRequest with
+                 sessionId 0, the GPU server's handshake kernel allocates
+                 the session (K9 server side), the client K9-decodes the
+                 ConnectResponse; the session creates ``batch`` ephemeral
+                 sequential nodes ``/storm/dDDDDD/e-<seq>``; session ``k-1``
+                 expires and the server removes its ephemerals, which must
+                 be exactly its TWO batches (the one made before its resume
+                 survived it)
+      step 2k+1  its connection drops; a new one resumes it: ConnectRequest
+                 with the id and password from the last ConnectResponse,
+                 all on the device; the server answers RESUMED with the same
+                 id and password.  In the same handshake batch the client
+                 also tries the session that expired at step 2k, which must
+                 get the expired answer (id 0).  The resumed session creates
+                 its second batch.
+
+    Every check (replies, handshake outcome, ids, password, removed count)
+    runs on the device; a step makes no device-to-host read.  The hash
+    index is rebuilt whenever the tombstones left by never-reused sequential
+    names would fill it."""
+
+    TIMEOUT = 30000
 
     def __init__(self, tree, batch, ndirs=1024, data_bytes=16, seed=0):
         dev = tree.device
         self.tree = tree
+        self.dev = dev
         self.n = batch
         self.ndirs = ndirs
         self.drv = _Driver(tree, batch, 32, data_bytes, seed)
+        self.sessions = GpuSessionTable(tree)
         prefixes = ['/storm/d%05d/e-' % (k % ndirs) for k in range(batch)]
         self.path_arena, self.path_off, self.path_len = _arena(prefixes, dev)
         self.data_arena = torch.full((data_bytes + 16,), 0x5a, dtype=U8,
@@ -664,41 +744,140 @@ class StormPipeline(object):
         self.acl_id = torch.zeros(batch, dtype=I32, device=dev)
         self.want_len = self.path_len + 10
         self.removed = torch.zeros(1, dtype=I64, device=dev)
-        self.session = 1
+        self.prev_sid = torch.zeros(1, dtype=I64, device=dev)
+        # client-side credentials, device only: [cur, prev] session ids and
+        # passwords (what the last ConnectResponses carried)
+        self.cred_sid = torch.zeros(2, dtype=I64, device=dev)
+        self.cred_pw = torch.zeros(32, dtype=U8, device=dev)
+        self.last_zxid = torch.zeros(1, dtype=I64, device=dev)
+        self.hs_ok = torch.ones(1, dtype=torch.bool, device=dev)
+        self.cr_tx = torch.empty(256, dtype=U8, device=dev)
+        self.cr_ws = torch.empty(_lib.lib().zk_scan_workspace(2),
+                                 dtype=I64, device=dev)
+        self.rscan = B.FrameScanner(4, dev, window=256)
+        # K9 encode arguments per handshake shape (m requests, pwl bytes)
+        self.zero_sid = torch.zeros(1, dtype=I64, device=dev)
+        self.zero_pw = torch.zeros(8, dtype=U8, device=dev)
+        self.cr_args = {}
+        for m, pwl in ((1, 8), (1, 16), (2, 16)):
+            self.cr_args[(m, pwl)] = (
+                torch.zeros(m, dtype=I32, device=dev),
+                torch.full((m,), self.TIMEOUT, dtype=I32, device=dev),
+                torch.arange(m, dtype=I64, device=dev) * pwl,
+                torch.full((m,), pwl, dtype=I32, device=dev),
+                torch.empty(m, dtype=I64, device=dev),
+                torch.empty(m, dtype=I64, device=dev),
+                torch.zeros(1, dtype=I64, device=dev))
+        self.k = -1                       # index of the current session
+        self.step_no = 0
         self.inserted = 0
+        self.stats = {'born': 0, 'resumed': 0, 'expired': 0,
+                      'expired_resume_refused': 0}
         self.drv.create_dirs(
             [['/storm'], ['/storm/d%05d' % d for d in range(ndirs)]],
             (self.acl_arena, self.acl_off, self.acl_len))
-        self.step(validate=False)            # first session's nodes
+        self.step(validate=False)            # session 0 born, first batch
+
+    # -- the client / server handshake, all on the device ---------------------
+
+    def _handshake(self, resume):
+        """K9 client encode -> K9 server handshake -> K9 client decode.
+        Birth: one request (id 0, 8 zero password bytes as zkstream sends,
+        lib/zk-session.js:59).  Resume: [current session, the session that
+        expired last step] with their ids and passwords."""
+        L = _lib.lib()
+        # the first session has no expired predecessor to try
+        m = 2 if resume and self.k >= 1 else 1
+        pwl = 16 if resume else 8
+        if resume:
+            sid = self.cred_sid[:m]
+            arena = self.cred_pw[:16 * m]
+        else:
+            sid = self.zero_sid
+            arena = self.zero_pw
+        proto, tmo, pwo, pwlt, sizes, off, total = self.cr_args[(m, pwl)]
+        zx = self.last_zxid.expand(m).contiguous()
+        _lib.check(L.zk_encode_connect_requests(
+            _lib.ptr(proto), _lib.ptr(zx), _lib.ptr(tmo), _lib.ptr(sid),
+            _lib.ptr(pwo), _lib.ptr(pwlt), _lib.ptr(arena), m,
+            _lib.ptr(sizes), _lib.ptr(off), _lib.ptr(total),
+            _lib.ptr(self.cr_ws), _lib.ptr(self.cr_tx), _lib.stream_ptr()),
+            'zk_encode_connect_requests')
+        nbytes = m * (32 + pwl)
+        resp, bound, outcome = self.sessions.connect(
+            self.cr_tx[:nbytes], nbytes, 0 if resume else 1)
+        rb = m * _lib.CR_RESP_BYTES
+        ft = self.rscan.scan(resp[:rb], rb)
+        o = B.decode_connect_responses(resp, ft, m)
+        return o, bound, outcome, resp
 
     def step(self, validate=True, acc=None):
         t = self.tree
         n = self.n
+        dev = self.dev
+        s = self.step_no
+        self.step_no += 1
+        resume = s % 2 == 1
         if (self.inserted + 2 * n) > 0.6 * t.hcap:
             t.rehash()
             self.inserted = 0
+        o, bound, outcome, resp = self._handshake(resume)
+        if resume:
+            # current session back with the same id and password; the
+            # expired one refused (only once there is one)
+            pw = resp[24:40]
+            ok = ((o['status'][0] == 0) & (o['sessionId'][0] ==
+                                             self.cred_sid[0]) &
+                  (outcome[0] == _lib.SC_RESUMED) &
+                  (o['timeOut'][0] == self.TIMEOUT) &
+                  (pw == self.cred_pw[:16]).all())
+            if self.k >= 1:
+                ok &= (outcome[1] == _lib.SC_EXPIRED) & \
+                    (o['sessionId'][1] == 0)
+            self.stats['resumed'] += 1
+            self.stats['expired_resume_refused'] += int(self.k >= 1)
+        else:
+            self.k += 1
+            want = self.sessions.sid_of(self.sessions.allocated - 1)
+            ok = ((o['status'][0] == 0) & (outcome[0] == _lib.SC_NEW) &
+                  (o['sessionId'][0] == want) & (bound[0] == want))
+            # credentials: the new session becomes current, the old one prev
+            self.cred_sid[1:2].copy_(self.cred_sid[0:1])
+            self.cred_pw[16:32].copy_(self.cred_pw[0:16])
+            self.cred_sid[0:1].copy_(o['sessionId'][0:1])
+            self.cred_pw[0:16].copy_(resp[24:40])
+            self.stats['born'] += 1
+        self.hs_ok &= ok
+        cur = self.sessions.sid_of(self.k)
         rb = B.RequestBatch(n, self.opcode, self.drv.xids(n), self.arg,
                             self.path_off, self.path_len, self.data_off,
                             self.data_len, self.acl_id, self.path_arena,
                             self.data_arena, self.acl_off, self.acl_len,
                             self.acl_arena)
-        rep, _ = self.drv.run(rb, session=self.session + 1)
+        rep, _ = self.drv.run(rb, session=cur)
         self.last = (rb, rep)
         self.inserted += n
-        # the previous session expires: its ephemerals go
-        self.removed.zero_()
-        t.expire(self.session, self.removed)
-        self.session += 1
+        torch.maximum(self.last_zxid, rep.zxid[:n].max().view(1),
+                      out=self.last_zxid)
+        expire_ok = True
+        if not resume and self.k >= 1:
+            # the previous session expires: both of its batches go
+            prev = self.sessions.sid_of(self.k - 1)
+            self.removed.zero_()
+            t.expire(prev, self.removed)
+            self.prev_sid.fill_(prev)
+            self.sessions.close(self.prev_sid)
+            self.stats['expired'] += 1
+            expire_ok = self.removed[0] == 2 * n
         if not validate:
             return None
-        ok = ((rep.status[:n] == 0) & (rep.err[:n] == 0) &
-              (rep.xid[:n] == rb.xid) &
-              (rep.pay_len[:n] == self.want_len)).sum()
-        # the expiry must have removed exactly one step's nodes
-        ok = torch.where(self.removed[0] == n, ok, 0)
+        good = ((rep.status[:n] == 0) & (rep.err[:n] == 0) &
+                (rep.xid[:n] == rb.xid) &
+                (rep.pay_len[:n] == self.want_len)).sum()
+        good = torch.where(self.hs_ok[0] & expire_ok, good, 0)
         if acc is None:
-            return ok
-        acc += ok
+            return good
+        acc += good
         return acc
 
     def diagnose(self):
@@ -706,10 +885,13 @@ class StormPipeline(object):
         n = self.n
         e, c = torch.unique(rep.err[:n], return_counts=True)
         return {'removed': int(self.removed.item()),
+                'handshakes_ok': bool(self.hs_ok.item()),
+                'outcome': self.sessions.outcome[:2].cpu().tolist(),
                 'err_hist': dict(zip(e.cpu().tolist(), c.cpu().tolist())),
                 'status_bad': int((rep.status[:n] != 0).sum().item()),
                 'pay_len_bad': int((rep.pay_len[:n] != self.want_len)
                                    .sum().item()),
+                'stats': dict(self.stats),
                 'counters': self.tree.counters.cpu().tolist()}
 
 

@@ -71,6 +71,16 @@ class ZkTree(ctypes.Structure):
                 ('node_pw', P)]
 
 
+class ZkSessionTable(ctypes.Structure):
+    _fields_ = [('sid', P), ('passwd', P), ('timeout', P), ('state', P),
+                ('next', P), ('cap', I64)]
+
+
+# session handshake outcomes (csrc/kernels/session.hip SC_*)
+SC_NEW, SC_RESUMED, SC_EXPIRED, SC_REFUSED, SC_BAD, SC_FULL = range(6)
+CR_RESP_BYTES = 41
+
+
 # ZkTree counters (csrc/kernels/tree.hip TC_*)
 TC_NODES, TC_ZXID, TC_PATH_TOP, TC_SLAB_TOP = 0, 1, 2, 3
 TC_FREE_HEAD, TC_FREE_TAIL, TC_FREE_PUB, TC_DIRTY = 4, 5, 6, 7
@@ -112,6 +122,9 @@ _SIGS = {
                             I64, I64, P]),
     'zk_tree_expire': (I32, [P, I64, I64, P, P]),
     'zk_route_workspace': (I64, [I64, I32]),
+    'zk_session_connect': (I32, [P, P, P, P, I64, P, I64, ctypes.c_uint64,
+                                 I32, I32, P, P, P, P, P]),
+    'zk_session_close': (I32, [P, P, I64, P]),
     'zk_route_requests': (I32, [I64, I32, P, P, P, P, P, P, P, P, P, P, P, P,
                                 P]),
     'zk_bench_gen_get': (I32, [I64, ctypes.c_uint64, I64, I64, I32, P, P,

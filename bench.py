@@ -65,6 +65,59 @@ def start_rtt_server():
     return p, int(line[1])
 
 
+def start_fast_server(nodes, data_bytes):
+    """The native wire server (csrc/host/zk_fastserver.cpp) preloaded with
+    the synthetic tree; None when it is not built."""
+    from zkmi.server import fast
+    if not fast.available():
+        return None
+    return fast.FastZKServer(preload=nodes, data_bytes=data_bytes)
+
+
+def measure_bulk_tcp(port, nodes, batch, iters, dev):
+    """``Client.bulk_get`` over loopback TCP to the native server: every
+    batch is ``batch`` GET_DATA of random existing nodes, device-resident
+    paths -> K10 -> pinned TX -> socket -> server -> native-loop capture
+    into pinned RX -> K1 + K2-K8 on the GPU; every reply checked OK.
+    Returns (ops/s, ms per batch)."""
+    import threading
+    import numpy as np
+    from zkmi import Client
+    c = Client(address='127.0.0.1', port=port, device=dev)
+    c.wait_connected(10)
+    i = np.arange(nodes)
+    paths = np.char.add(np.char.add('/bench/d', np.char.zfill(
+        (i // 1000).astype(str), 6)), np.char.add('/n', np.char.zfill(
+            i.astype(str), 9)))
+    blob = ''.join(paths.tolist()).encode()
+    plen = len(paths[0])
+    arena = torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(dev)
+    ln = torch.full((batch,), plen, dtype=torch.int32, device=dev)
+
+    def one(seed):
+        g = torch.Generator(device=dev)
+        g.manual_seed(seed)
+        idx = torch.randint(0, nodes, (batch,), device=dev, generator=g)
+        box, ev = [], threading.Event()
+        c.bulk_get((arena, idx * plen, ln),
+                   lambda err, res=None: (box.append((err, res)), ev.set()))
+        if not ev.wait(120):
+            raise SystemExit('bulk_get timed out')
+        err, res = box[0]
+        if err is not None:
+            raise SystemExit('bulk_get failed: %r' % (err,))
+        if res.ok_count() != batch:
+            raise SystemExit('bulk_get: %d of %d replies OK'
+                             % (res.ok_count(), batch))
+    one(0)                                   # warm-up (allocations)
+    t0 = time.perf_counter()
+    for k in range(iters):
+        one(k + 1)
+    el = time.perf_counter() - t0
+    c.close_sync(10)
+    return batch * iters / el, el / iters * 1e3
+
+
 def measure_rtt(port, n=2000):
     from zkmi import Client
     c = Client(address='127.0.0.1', port=port)
@@ -185,7 +238,11 @@ def main():
                     help='GET_DATA requests per GPU per step')
     ap.add_argument('--nodes', type=int, default=1_000_000)
     ap.add_argument('--data-bytes', type=int, default=100)
-    ap.add_argument('--no-rtt', action='store_true')
+    ap.add_argument('--no-rtt', action='store_true',
+                    help='skip the interactive RTT and bulk-TCP runs')
+    ap.add_argument('--bulk-batch', type=int, default=1 << 20,
+                    help='requests per Client.bulk_get batch of the '
+                         'bulk-TCP measurement')
     ap.add_argument('--streams', type=int, default=2,
                     help='get: pipelined connections per GPU, one HIP '
                          'stream each (the batch is split between them; 2 '
@@ -218,6 +275,8 @@ def main():
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
     rtt_srv = start_rtt_server() if rank == 0 and not a.no_rtt else None
+    fast_srv = start_fast_server(a.nodes, a.data_bytes) \
+        if rank == 0 and not a.no_rtt and a.workload == 'get' else None
     # One rank per GPU over RCCL ("nccl").  ZKMI_BENCH_BACKEND=gloo (host
     # collectives, ranks may share a GPU) exists only to rehearse the
     # multi-rank path on a one-GPU box.
@@ -298,13 +357,22 @@ def main():
                          % (ops - ok, ops))
     value = ops / elapsed
 
-    rtt50 = rtt99 = None
+    rtt50 = rtt99 = py50 = py99 = bulk_ops = bulk_ms = None
     if rtt_srv is not None:
         try:
-            rtt50, rtt99 = measure_rtt(rtt_srv[1])
+            py50, py99 = measure_rtt(rtt_srv[1])
         finally:
             rtt_srv[0].stdin.close()
             rtt_srv[0].wait(10)
+    if fast_srv is not None:
+        try:
+            rtt50, rtt99 = measure_rtt(fast_srv.port)
+            bulk_ops, bulk_ms = measure_bulk_tcp(
+                fast_srv.port, a.nodes, a.bulk_batch, 3, dev)
+        finally:
+            fast_srv.shutdown()
+    elif rtt_srv is not None:
+        rtt50, rtt99 = py50, py99
 
     if rank == 0:
         line = {
@@ -332,6 +400,17 @@ def main():
             'r2_bytes_sent': getattr(pipe, 'stats', {}).get('bytes_sent'),
             'p50_get_rtt_us': rtt50,
             'p99_get_rtt_us': rtt99,
+            'rtt_note': 'one blocking Client.get over loopback TCP to the '
+                        'native server (zk_fastserver); *_fakezk: to the '
+                        'Python fake server',
+            'p50_get_rtt_us_fakezk': py50,
+            'p99_get_rtt_us_fakezk': py99,
+            'bulk_tcp_ops_s': bulk_ops,
+            'bulk_tcp_ms_per_batch': bulk_ms,
+            'bulk_tcp_note': 'Client.bulk_get of %d random nodes per batch '
+                             'over loopback TCP to the native server: GPU '
+                             'encode/decode, pinned TX/RX, replies captured '
+                             'by the native loop' % a.bulk_batch,
             'batch_latency_ms': elapsed / a.steps * 1e3,
             'baseline_note': 'vs_baseline = value / 0.51M pkts/s, the '
                              'reference ZKDecodeStream frame+decode on one '

@@ -137,6 +137,25 @@ struct Watched {
   Loop* loop;            // borrowed (the loop outlives its watched objects)
 };
 
+// Bulk reply capture (Transport.capture): while on, the read path frames
+// the inbound stream itself and copies every frame whose xid is in
+// [x0, x0 + n) — length prefix included — into a caller-owned buffer (the
+// pinned host buffer a GPU batch decodes from), so those replies never
+// become Python objects; every other frame (notifications, pings, ordinary
+// requests) still goes to data_received, in order.  `carry` holds a partial
+// frame between reads.  Ends when n frames arrived, the buffer is full (the
+// rest flows to Python) or a frame length is bad (Python's framer reports
+// it); done(status, nbytes, nframes, last_off) is called on the loop.
+struct Capture {
+  bool on = false;
+  int64_t x0 = 0, n = 0, got = 0, max_packet = 0;
+  uint8_t* dst = nullptr;
+  size_t size = 0, len = 0, last_off = 0;
+  std::string carry;
+  PyObject* done = nullptr;
+};
+enum { CAP_DONE = 0, CAP_FULL = 1, CAP_BAD = 2, CAP_CANCEL = 3 };
+
 struct Transport {
   Watched w;
   PyObject* protocol;
@@ -146,6 +165,7 @@ struct Transport {
   bool connecting, connected, paused, rd_eof, eof_pending, wr_shut;
   bool closing, closed;
   PyObject* peer;        // (host, port) tuple
+  Capture* cap;
 };
 
 struct Server {
@@ -323,12 +343,15 @@ Transport* new_transport(Loop* L, int fd) {
   t->connecting = t->connected = t->paused = t->rd_eof = false;
   t->eof_pending = t->wr_shut = t->closing = t->closed = false;
   t->peer = nullptr;
+  t->cap = new Capture();
   return t;
 }
 
 void Transport_dealloc(Transport* t) {
   if (t->w.fd >= 0) close(t->w.fd);
   delete t->wbuf;
+  Py_XDECREF(t->cap->done);
+  delete t->cap;
   Py_XDECREF(t->protocol);
   Py_XDECREF(t->on_fail);
   Py_XDECREF(t->peer);
@@ -353,6 +376,11 @@ void refresh(Transport* t) {
 void finish(Transport* t, PyObject* exc) {
   if (t->closed) return;
   t->closed = true;
+  // a capture dies with the connection (its batch fails with the requests)
+  t->cap->on = false;
+  t->cap->dst = nullptr;
+  t->cap->carry.clear();
+  Py_CLEAR(t->cap->done);
   Py_INCREF(t);
   drop_watch(&t->w);
   if (t->connected && t->protocol != nullptr)
@@ -434,6 +462,78 @@ void connect_failed(Transport* t, int err) {
   Py_DECREF(t);
 }
 
+void deliver_raw(Transport* t, const char* p, size_t n) {
+  if (n == 0 || t->closed) return;
+  PyObject* b = PyBytes_FromStringAndSize(p, (Py_ssize_t)n);
+  if (b == nullptr) { report_exception(t->w.loop); return; }
+  invoke(t->w.loop, t->protocol, "data_received", b);
+  Py_DECREF(b);
+}
+
+int32_t be32(const char* p) {
+  uint32_t v;
+  memcpy(&v, p, 4);
+  return (int32_t)ntohl(v);
+}
+
+// End the capture: done(status, nbytes, nframes, last_off), then the bytes
+// after the last parsed frame go to Python.
+void capture_end(Transport* t, int status) {
+  Capture& c = *t->cap;
+  c.on = false;
+  c.dst = nullptr;
+  std::string rest;
+  rest.swap(c.carry);
+  PyObject* cb = c.done;
+  c.done = nullptr;
+  if (cb != nullptr) {
+    PyObject* r = PyObject_CallFunction(cb, "inLn", status, (Py_ssize_t)c.len,
+                                        (long long)c.got,
+                                        (Py_ssize_t)c.last_off);
+    if (r == nullptr) report_exception(t->w.loop);
+    Py_XDECREF(r);
+    Py_DECREF(cb);
+  }
+  if (!t->closed) deliver_raw(t, rest.data(), rest.size());
+}
+
+void deliver(Transport* t, const char* p, size_t n) {
+  Capture& c = *t->cap;
+  if (!c.on) { deliver_raw(t, p, n); return; }
+  std::string buf;
+  const char* s = p;
+  size_t len = n;
+  if (!c.carry.empty()) {
+    buf.swap(c.carry);
+    buf.append(p, n);
+    s = buf.data();
+    len = buf.size();
+  }
+  std::string pass;               // frames that are not the batch's
+  size_t i = 0;
+  int status = -1;
+  while (len - i >= 4 && c.got < c.n) {
+    const int32_t fl = be32(s + i);
+    if (fl < 0 || fl > c.max_packet) { status = CAP_BAD; break; }
+    if (len - i < 4 + (size_t)fl) break;
+    const int64_t xid = fl >= 4 ? be32(s + i + 4) : -1;
+    if (fl >= 16 && xid >= c.x0 && xid < c.x0 + c.n) {
+      if (c.len + 4 + (size_t)fl > c.size) { status = CAP_FULL; break; }
+      memcpy(c.dst + c.len, s + i, 4 + (size_t)fl);
+      c.last_off = c.len;
+      c.len += 4 + (size_t)fl;
+      ++c.got;
+    } else {
+      pass.append(s + i, 4 + (size_t)fl);
+    }
+    i += 4 + (size_t)fl;
+  }
+  if (status < 0 && c.got >= c.n) status = CAP_DONE;
+  c.carry.assign(s + i, len - i);
+  deliver_raw(t, pass.data(), pass.size());
+  if (status >= 0 && c.on && !t->closed) capture_end(t, status);
+}
+
 void transport_event(Transport* t, uint32_t ev) {
   Py_INCREF(t);
   if (t->connecting) {
@@ -451,10 +551,7 @@ void transport_event(Transport* t, uint32_t ev) {
     for (int rounds = 0; rounds < 64 && !t->closed && !t->paused; ++rounds) {
       ssize_t n = recv(t->w.fd, buf, sizeof buf, MSG_DONTWAIT);
       if (n > 0) {
-        PyObject* b = PyBytes_FromStringAndSize(buf, n);
-        if (b == nullptr) { report_exception(t->w.loop); break; }
-        invoke(t->w.loop, t->protocol, "data_received", b);
-        Py_DECREF(b);
+        deliver(t, buf, (size_t)n);
         if ((size_t)n < sizeof buf) break;
         continue;
       }
@@ -514,6 +611,76 @@ PyObject* Transport_write(Transport* t, PyObject* arg) {
     refresh(t);
   }
   Py_RETURN_TRUE;
+}
+
+// write_from(addr, n): queue n bytes read from raw memory (a pinned host
+// buffer the GPU encoder filled) without a Python bytes object.
+PyObject* Transport_write_from(Transport* t, PyObject* args) {
+  unsigned long long addr;
+  Py_ssize_t n;
+  if (!PyArg_ParseTuple(args, "Kn", &addr, &n)) return nullptr;
+  if (n < 0 || (addr == 0 && n > 0)) {
+    PyErr_SetString(PyExc_ValueError, "write_from: bad buffer");
+    return nullptr;
+  }
+  if (t->closed || t->closing || t->wr_shut || t->eof_pending)
+    Py_RETURN_FALSE;
+  t->wbuf->append((const char*)(uintptr_t)addr, (size_t)n);
+  if (t->connected) {
+    int err = flush(t);
+    if (err) {
+      PyObject* e = PyLong_FromLong(err);
+      defer_method(t->w.loop, (PyObject*)t, "_fatal", e);
+      Py_XDECREF(e);
+      t->closing = true;
+      Py_RETURN_FALSE;
+    }
+    refresh(t);
+  }
+  Py_RETURN_TRUE;
+}
+
+// capture(x0, n, addr, size, max_packet, done, prefix): see Capture.  The
+// buffer must stay valid until done() runs or the transport closes.
+// `prefix` = bytes the caller's framer already holds (a partial frame),
+// parsed first.
+PyObject* Transport_capture(Transport* t, PyObject* args) {
+  long long x0, n, maxp;
+  unsigned long long addr;
+  Py_ssize_t size;
+  PyObject* done;
+  Py_buffer pre;
+  if (!PyArg_ParseTuple(args, "LLKnLOy*", &x0, &n, &addr, &size, &maxp, &done,
+                        &pre))
+    return nullptr;
+  Capture& c = *t->cap;
+  if (c.on || t->closed || n <= 0 || addr == 0 || size <= 0 ||
+      !PyCallable_Check(done)) {
+    PyBuffer_Release(&pre);
+    PyErr_SetString(PyExc_ValueError, "capture: busy, closed or bad args");
+    return nullptr;
+  }
+  c.on = true;
+  c.x0 = x0;
+  c.n = n;
+  c.got = 0;
+  c.max_packet = maxp;
+  c.dst = (uint8_t*)(uintptr_t)addr;
+  c.size = (size_t)size;
+  c.len = c.last_off = 0;
+  c.carry.clear();
+  Py_INCREF(done);
+  c.done = done;
+  std::string head((const char*)pre.buf, (size_t)pre.len);
+  PyBuffer_Release(&pre);
+  if (!head.empty()) deliver(t, head.data(), head.size());
+  Py_RETURN_NONE;
+}
+
+// capture_cancel(): end an active capture (done gets CAP_CANCEL).
+PyObject* Transport_capture_cancel(Transport* t, PyObject*) {
+  if (t->cap->on) capture_end(t, CAP_CANCEL);
+  Py_RETURN_NONE;
 }
 
 PyObject* Transport_fatal(Transport* t, PyObject* arg) {
@@ -620,6 +787,12 @@ PyMethodDef Transport_methods[] = {
     {"resume_reading", (PyCFunction)Transport_resume, METH_NOARGS, ""},
     {"get_extra_info", (PyCFunction)Transport_extra, METH_VARARGS, ""},
     {"_fatal", (PyCFunction)Transport_fatal, METH_O, "internal"},
+    {"write_from", (PyCFunction)Transport_write_from, METH_VARARGS,
+     "queue bytes from raw memory"},
+    {"capture", (PyCFunction)Transport_capture, METH_VARARGS,
+     "route an xid range of reply frames into a buffer"},
+    {"capture_cancel", (PyCFunction)Transport_capture_cancel, METH_NOARGS,
+     "end the active capture"},
     {nullptr, nullptr, 0, nullptr}};
 
 PyGetSetDef Transport_getset[] = {

@@ -170,3 +170,49 @@ def test_bulk_empty_batch(zk):
     c.call_sync('create', '/after', b'ok', {})
     assert c.call_sync('get', '/after')[0] == b'ok'
     c.close_sync(10)
+
+
+@pytest.mark.gpu
+def test_bulk_gpu_capture_native_server(gpu):
+    """The GPU bulk path on the live connection against the native server:
+    K10 into a pinned TX buffer, replies captured by the native loop into a
+    pinned RX buffer (no reply frame routed through Python), K1 + K2-K8 on
+    the GPU; device-tensor paths; a second batch with replies bigger than
+    the RX reservation falls back to per-frame collection and stays exact."""
+    import torch
+    from zkmi.server import fast
+    from zkmi.runtime import nloop
+    if not (fast.available() and nloop.available()):
+        pytest.skip('native server / loop not built')
+    srv = fast.FastZKServer(preload=20000, data_bytes=100)
+    try:
+        c = client(srv.servers(), device=gpu)
+        c.wait_connected(10)
+        n = 20000
+        paths = ['/bench/d%06d/n%09d' % (i // 1000, i) for i in range(n)]
+        blob = ''.join(paths).encode()
+        arena = torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(gpu)
+        idx = torch.randperm(n, device=gpu)
+        off = idx * 25
+        ln = torch.full((n,), 25, dtype=torch.int32, device=gpu)
+        err, res = _run(c, 'bulk_get', (arena, off, ln))
+        assert err is None and res.replies is not None
+        assert res.ok_count() == n
+        conn = c.loop.run(lambda: c.getSession().getConnection())
+        assert conn.bulk_frames_py == 0
+        # the replies are the requested nodes: czxid order follows the
+        # preload order (node i was created after i + dirs + 3 nodes)
+        r = res.replies
+        czx = r.stat64[0, :n]
+        assert bool((czx - czx.min() == idx - idx.min()).all())
+        assert bool((r.pay_len[:n] == 100).all())
+        # big values: the RX reservation overflows, per-frame fallback
+        c.call_sync('create', '/big', b'x' * 5000, {})
+        err, res = _run(c, 'bulk_get', ['/big'] * 300)
+        assert err is None and res.ok_count() == 300
+        assert conn.bulk_frames_py > 0
+        pk = res.packets()
+        assert pk[7]['data'] == b'x' * 5000
+        c.close_sync(10)
+    finally:
+        srv.shutdown()

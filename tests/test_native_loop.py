@@ -195,3 +195,76 @@ def test_client_stack_on_both_loops(kind):
         srv.stop()
         lp.stop()
         slp.stop()
+
+
+def _fast_server():
+    from zkmi.server import fast
+    if not fast.available():
+        pytest.skip('zk_fastserver not built')
+    return fast.FastZKServer(preload=3000, data_bytes=50)
+
+
+def test_transport_capture_routes_xid_range(nl):
+    """Transport.capture: the reply frames of an xid range land in a raw
+    buffer (length prefix included, in order) inside the loop's read path;
+    other frames (a ping in the middle) still reach Python; a too-small
+    buffer ends the capture with status 1 and the rest flows to Python."""
+    import ctypes
+    from zkmi import jute
+    from zkmi.runtime.tcp import TcpSocket
+    from zkmi.streams import ZKDecoder
+    srv = _fast_server()
+    try:
+        sock = TcpSocket(nl)
+        dec = ZKDecoder()
+        got = []
+        sock.on('data', lambda d: got.extend(dec.feed(d)[0]))
+        up = threading.Event()
+        sock.on('connect', up.set)
+        nl.run(lambda: sock.connect('127.0.0.1', srv.port))
+        assert up.wait(5)
+        nl.run(lambda: sock.write(jute.frame(jute.encode_connect_request({
+            'protocolVersion': 0, 'lastZxidSeen': 0, 'timeOut': 30000,
+            'sessionId': 0, 'passwd': b'\0' * 8}))))
+        assert wait_for(lambda: len(got) == 1, 5)
+
+        def gets(x0, n, ping_at):
+            out = []
+            for k in range(n):
+                if k == ping_at:
+                    out.append(jute.frame(jute.encode_request(
+                        {'xid': -2, 'opcode': 'PING'})))
+                out.append(jute.frame(jute.encode_request({
+                    'xid': x0 + k, 'opcode': 'GET_DATA', 'watch': False,
+                    'path': '/bench/d%06d/n%09d' % (k // 1000, k)})))
+            return b''.join(out)
+        # reference bytes: the same requests without capture
+        got.clear()
+        nl.run(lambda: sock.write(gets(100, 500, 250)))
+        assert wait_for(lambda: len(got) == 501, 10)
+        want = b''.join(jute.frame(b) for b in got
+                        if b[:4] != b'\xff\xff\xff\xfe')
+        # captured run
+        for size, status_want in ((1 << 20, 0), (20000, 1)):
+            got.clear()
+            done = []
+            buf = ctypes.create_string_buffer(size)
+            nl.run(lambda: sock.capture(
+                100, 500, ctypes.addressof(buf), size, 1 << 24,
+                lambda *a: done.append(a), b''))
+            nl.run(lambda: sock.write(gets(100, 500, 250)))
+            assert wait_for(lambda: done, 10)
+            st, nbytes, nframes, last = done[0]
+            assert st == status_want
+            assert buf.raw[:nbytes] == want[:nbytes]
+            if st == 0:
+                assert nframes == 500 and nbytes == len(want)
+                assert wait_for(lambda: len(got) == 1, 5)   # the ping only
+                assert got[0][:4] == b'\xff\xff\xff\xfe'
+                assert buf.raw[last:last + 4] == want[last:last + 4]
+            else:
+                # the frames past the buffer arrive through 'data'
+                assert wait_for(lambda: len(got) == 501 - nframes, 10)
+        nl.run(sock.destroy)
+    finally:
+        srv.shutdown()

@@ -81,8 +81,22 @@ HOST_EXTS = {'_zkhost': 'zk_host_codec.cpp',     # Jute host codec
              '_zkloop': 'zk_loop.cpp'}           # epoll event loop
 
 
+FAST_SERVER = os.path.join(ROOT, 'zkmi', 'bin', 'zk_fastserver')
+
+
+def build_fastserver():
+    """The native benchmark server (csrc/host/zk_fastserver.cpp), a plain
+    executable: zkmi/server/fast.py runs it as a child process."""
+    src = os.path.join(HDIR, 'zk_fastserver.cpp')
+    os.makedirs(os.path.dirname(FAST_SERVER), exist_ok=True)
+    if _stale(FAST_SERVER, [src]):
+        _run(['g++', '-O3', '-std=c++17', '-Wall', '-Wextra', src, '-o',
+              FAST_SERVER])
+    return FAST_SERVER
+
+
 def build_host():
-    outs = []
+    outs = [build_fastserver()]
     inc = sysconfig.get_paths()['include']
     for name, src in HOST_EXTS.items():
         src = os.path.join(HDIR, src)

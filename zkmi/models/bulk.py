@@ -7,13 +7,21 @@ as ONE unit through the same connection, with the byte work on the GPU:
 
   submit   K10 encodes the N requests (xids = a contiguous range reserved on
            the connection, opcodes recorded in an HBM xid table) into one
-           framed byte stream; one D2H copy, one socket write.
-  collect  the connection's host framer routes every reply frame whose xid
-           falls in the range into the batch's RX buffer (notifications,
-           pings and ordinary requests keep flowing through the normal path,
-           ZooKeeper answers a session's requests in order).
-  finish   one H2D copy of the collected reply stream, K1 frame scan,
-           K2-K8 decode into SoA tensors (:class:`~zkmi.ops.batch.ReplyBatch`).
+           framed byte stream; one D2H copy into a pinned TX buffer, which
+           the native loop queues straight from that memory (write_from).
+  collect  the native loop's read path frames the inbound stream itself and
+           copies every reply frame whose xid falls in the range into a
+           pinned RX buffer (Transport.capture, csrc/host/zk_loop.cpp): no
+           reply of the batch becomes a Python object.  Notifications,
+           pings and ordinary requests keep flowing through the normal path
+           (ZooKeeper answers a session's requests in order).
+  finish   one H2D copy of the pinned RX buffer, K1 frame scan, K2-K8 decode
+           into SoA tensors (:class:`~zkmi.ops.batch.ReplyBatch`); a CUDA
+           event marks completion, readers wait on it.
+
+Fallbacks: on the asyncio loop, or when the replies outgrow the RX buffer,
+the connection routes reply frames to :meth:`BulkBatch.add` one by one (the
+frames captured so far are kept).
 
 Without a GPU (CPU-only hosts, the CPU test suite) the same object encodes
 and decodes with the host codec (:mod:`zkmi.codec`), so the API works
@@ -50,14 +58,23 @@ class BulkResult(object):
     to the per-request dicts the interactive API produces.  On the host path
     the packets are decoded directly."""
 
-    def __init__(self, n, replies=None, buf=None, packets=None, device=None):
+    def __init__(self, n, replies=None, buf=None, packets=None, device=None,
+                 event=None):
         self.n = n
         self.replies = replies
         self.buf = buf
         self.device = device
         self._packets = packets
+        self.event = event
+
+    def wait(self):
+        """Block until the GPU decode finished (no-op on the host path)."""
+        if self.event is not None:
+            self.event.synchronize()
+        return self
 
     def packets(self):
+        self.wait()
         if self._packets is None:
             from ..ops import batch as B
             self._packets = B.replies_to_packets(self.buf, self.replies,
@@ -66,12 +83,14 @@ class BulkResult(object):
 
     def errors(self):
         """Per-request error names ('OK', 'NO_NODE', ...)."""
+        self.wait()
         if self.replies is not None and self._packets is None:
             errs = self.replies.err[:self.n].cpu().tolist()
             return [consts.ERR_LOOKUP.get(e, e) for e in errs]
         return [p.get('err') for p in self.packets()]
 
     def ok_count(self):
+        self.wait()
         if self.replies is not None:
             r = self.replies
             return int(((r.err[:self.n] == 0) & (r.status[:self.n] == 0))
@@ -83,10 +102,23 @@ class BulkBatch(object):
     """N requests (dicts as :func:`zkmi.jute.encode_request` takes them,
     without xids) submitted, collected and decoded as one unit."""
 
-    def __init__(self, pkts, device=None):
-        self.pkts = list(pkts)
-        self.n = len(self.pkts)
+    # reply bytes reserved per request in the pinned RX buffer (a GET_DATA
+    # of 100 bytes is 192); bigger replies overflow into the per-frame path
+    RX_PER_REQ = 224
+
+    def __init__(self, pkts, device=None, reqs=None):
+        """``pkts``: request dicts; or ``reqs`` = a device
+        :class:`~zkmi.ops.batch.RequestBatch` already packed on the GPU
+        (xids are assigned at submit), then ``pkts`` is None."""
+        self.pkts = list(pkts) if pkts is not None else None
+        self.reqs = reqs
+        self.n = reqs.n if reqs is not None else len(self.pkts)
         self.device = _gpu_device(device)
+        if reqs is not None and self.device is None:
+            raise ValueError('a device request batch needs a GPU')
+        self.capturing = False
+        self.tx_pin = None
+        self.rx_pin = None
         self.x0 = 0
         self.rx = bytearray()
         self.got = 0
@@ -98,12 +130,52 @@ class BulkBatch(object):
 
     # -- encode ---------------------------------------------------------------
 
+    @classmethod
+    def gets(cls, paths, device=None):
+        """GET_DATA of every path (strings, or a device ``(arena u8, off
+        i64, len i32)`` triple of path bytes) packed straight into a device
+        request batch (no per-request dict)."""
+        dev = _gpu_device(device)
+        if dev is None:
+            return cls([{'opcode': 'GET_DATA', 'path': p, 'watch': False}
+                        for p in paths], False)
+        import numpy as np
+        import torch
+        from ..ops import batch as B
+        if isinstance(paths, tuple):
+            arena, off, ln = paths
+            n = off.numel()
+        else:
+            enc = [p.encode('utf-8') for p in paths]
+            n = len(enc)
+            lens = np.fromiter((len(e) for e in enc), np.int32, n)
+            offs = np.zeros(n, np.int64)
+            if n > 1:
+                np.cumsum(lens[:-1], out=offs[1:])
+            blob = b''.join(enc) or b'\0'
+            arena = torch.frombuffer(bytearray(blob), dtype=torch.uint8) \
+                .to(dev)
+            off = torch.from_numpy(offs).to(dev)
+            ln = torch.from_numpy(lens).to(dev)
+        z32 = torch.zeros(n, dtype=torch.int32, device=dev)
+        z64 = torch.zeros(n, dtype=torch.int64, device=dev)
+        op = torch.full((n,), consts.OP_CODES['GET_DATA'], dtype=torch.int32,
+                        device=dev)
+        rb = B.RequestBatch(n, op, z32, z32, off, ln, z64, z32, z32, arena,
+                            arena, torch.zeros(1, dtype=torch.int64,
+                                               device=dev),
+                            torch.zeros(1, dtype=torch.int32, device=dev),
+                            torch.zeros(16, dtype=torch.uint8, device=dev))
+        return cls(None, dev, reqs=rb)
+
     def encode(self, x0):
         """Assign xids ``x0 .. x0+n-1`` and return the framed request
-        stream (bytes) for the socket."""
+        stream for the socket: bytes, or on the GPU path ``(addr, n)`` of
+        the pinned TX buffer holding it."""
         self.x0 = x0
-        for i, p in enumerate(self.pkts):
-            p['xid'] = x0 + i
+        if self.pkts is not None:
+            for i, p in enumerate(self.pkts):
+                p['xid'] = x0 + i
         if self.device is None:
             self.xid_map = {}
             out = []
@@ -114,15 +186,44 @@ class BulkBatch(object):
         import torch
         from ..ops import batch as B
         with torch.cuda.device(self.device):
-            rb = B.pack_requests(self.pkts, self.device)
+            if self.reqs is not None:
+                rb = self.reqs
+                rb.xid = torch.arange(x0, x0 + self.n, dtype=torch.int32,
+                                      device=self.device)
+            else:
+                rb = B.pack_requests(self.pkts, self.device)
             bits = max(12, (max(self.n, 1) - 1).bit_length() + 1)
             self.xt = B.XidTable(bits=bits, device=self.device)
             tx, _, total, err = B.encode_requests(rb, self.xt)
-            ntx = int(total.item())
-            if int(err.item()) != 0:
+            te = torch.cat([total, err.to(torch.int64)]).cpu().tolist()
+            ntx = te[0]
+            if te[1] != 0:
                 raise ZKProtocolError('BAD_ARGUMENTS',
                                       'bulk request encode failed')
-            return bytes(tx[:ntx].cpu().numpy().tobytes())
+            self.tx_pin = torch.empty(max(ntx, 1), dtype=torch.uint8,
+                                      pin_memory=True)
+            self.tx_pin[:ntx].copy_(tx[:ntx])
+            return (self.tx_pin.data_ptr(), ntx)
+
+    def rx_buffer(self):
+        """(addr, size) of the pinned RX buffer the transport captures the
+        batch's reply frames into."""
+        import torch
+        size = self.n * self.RX_PER_REQ + (1 << 16)
+        self.rx_pin = torch.empty(size, dtype=torch.uint8, pin_memory=True)
+        return self.rx_pin.data_ptr(), size
+
+    def captured(self, status, nbytes, got):
+        """The transport's capture ended.  ``status`` 0: all replies are in
+        the RX buffer.  Otherwise the batch falls back to per-frame
+        collection, keeping what was captured."""
+        self.capturing = False
+        if status == 0:
+            return True
+        self.rx = bytearray(self.rx_pin[:nbytes].numpy().tobytes())
+        self.got = got
+        self.rx_pin = None
+        return False
 
     # -- collect --------------------------------------------------------------
 
@@ -138,7 +239,9 @@ class BulkBatch(object):
 
     # -- decode ---------------------------------------------------------------
 
-    def finish(self):
+    def finish(self, nbytes=None):
+        """Decode the collected replies.  ``nbytes``: the replies are the
+        first ``nbytes`` of the pinned RX buffer (capture path)."""
         if self.device is None:
             pk = []
             data = bytes(self.rx)
@@ -151,13 +254,24 @@ class BulkBatch(object):
         import torch
         from ..ops import batch as B
         with torch.cuda.device(self.device):
-            host = torch.from_numpy(np.frombuffer(bytes(self.rx) or b'\0',
-                                                  np.uint8).copy())
-            buf = host.pin_memory().to(self.device, non_blocking=True)
-            ft = B.frame_scan(buf, len(self.rx), cap=max(self.n, 1))
+            if nbytes is not None:
+                host = self.rx_pin[:max(nbytes, 1)]
+            else:
+                nbytes = len(self.rx)
+                host = torch.from_numpy(np.frombuffer(
+                    bytes(self.rx) or b'\0', np.uint8).copy()).pin_memory()
+            buf = host.to(self.device, non_blocking=True)
+            ft = B.frame_scan(buf, nbytes, cap=max(self.n, 1))
             rep = B.decode_replies(buf, ft, self.xt)
-            torch.cuda.current_stream().synchronize()
-        return BulkResult(self.n, replies=rep, buf=buf, device=self.device)
+            ev = torch.cuda.Event()
+            ev.record()
+        # the pinned buffers stay referenced by the result until the copy
+        # the event covers has run
+        res = BulkResult(self.n, replies=rep, buf=buf, device=self.device,
+                         event=ev)
+        res._hold = (host, self.tx_pin)
+        self.rx_pin = self.tx_pin = None
+        return res
 
     def elapsed_ms(self):
         return (time.perf_counter() - self.t_submit) * 1e3

@@ -515,10 +515,32 @@ class Client(FSM):
         self._dispatch(go)
 
     def bulk_get(self, paths, cb):
-        """:meth:`bulk` of GET_DATA for every path."""
-        if not isinstance(paths, (list, tuple)):
+        """:meth:`bulk` of GET_DATA for every path: ``paths`` is a list of
+        strings, or (GPU) a device ``(arena, off, len)`` triple of path
+        bytes (uint8 / int64 / int32 tensors), packed straight into the
+        request batch without per-request Python objects."""
+        from .bulk import BulkBatch
+        _check_func(cb)
+        if isinstance(paths, tuple) and len(paths) == 3 and \
+                hasattr(paths[0], 'device'):
+            batch = BulkBatch.gets(paths, self.bulk_device)
+        elif isinstance(paths, (list, tuple)):
+            for p in paths:
+                _check_str(p, 'path')
+            batch = BulkBatch.gets(list(paths), self.bulk_device)
+        else:
             raise TypeError('paths ([string]) is required')
-        self.bulk([{'opcode': 'GET_DATA', 'path': p} for p in paths], cb)
+
+        def go():
+            conn = self.currentConnection()
+            if conn is None or not conn.isInState('connected'):
+                self._not_connected(cb)
+                return
+            try:
+                conn.bulk_submit(batch, cb)
+            except Exception as e:
+                self.loop.call_soon(cb, e)
+        self._dispatch(go)
 
     def watcher(self, path):
         _check_str(path, 'path')

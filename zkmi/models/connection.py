@@ -71,6 +71,7 @@ class ZKConnectionFSM(FSM):
         self.xid_map = {}
         self.xid = 0
         self.bulks = []                 # in-flight BulkBatch (models/bulk.py)
+        self.bulk_frames_py = 0         # bulk replies routed one by one
         self.reqs = {}
         self.socket = None
         self.session = None
@@ -310,8 +311,13 @@ class ZKConnectionFSM(FSM):
             self.last_error = err
             S.gotoState('closed')
 
+        def on_bulk_done():
+            if len(self.reqs) < 1 and not self.bulks:
+                send_close_session()
+
         S.on(self, '_rx', on_rx)
         S.on(self, '_rxerr', on_error)
+        S.on(self, '_bulkdone', on_bulk_done)
         S.on(self.socket, 'error', on_error)
         S.on(self.socket, 'end', lambda: S.gotoState('closed'))
         S.on(self.socket, 'close', lambda: S.gotoState('closed'))
@@ -408,13 +414,52 @@ class ZKConnectionFSM(FSM):
         self.xid = (x0 + n) & 0x7fffffff
         wire = batch.encode(x0)
         self.bulks.append(batch)
-        self.log.trace({'xid0': x0, 'n': n, 'bytes': len(wire)},
-                       'sent bulk batch')
-        self.socket.write(wire)
+        if batch.device is not None and self.socket.can_capture() and \
+                not any(b.capturing for b in self.bulks):
+            # the native loop routes the batch's replies into pinned memory
+            addr, size = batch.rx_buffer()
+            batch.capturing = True
+            self.socket.capture(
+                x0, n, addr, size, self.config.max_packet,
+                lambda st, nb, got, last, b=batch:
+                    self._bulk_captured(b, st, nb, got, last),
+                self.decoder.take_pending())
+        if isinstance(wire, tuple):
+            self.log.trace({'xid0': x0, 'n': n, 'bytes': wire[1]},
+                           'sent bulk batch')
+            self.socket.write_from(*wire)
+        else:
+            self.log.trace({'xid0': x0, 'n': n, 'bytes': len(wire)},
+                           'sent bulk batch')
+            self.socket.write(wire)
+
+    def _bulk_captured(self, b, status, nbytes, got, last_off):
+        """The transport's capture of ``b`` ended (loop thread)."""
+        if b not in self.bulks:
+            return
+        if not b.captured(status, nbytes, got):
+            return              # per-frame collection goes on (_bulk_rx)
+        # one 'packet' for the batch: the last reply's zxid keeps the
+        # session's lastZxid and expiry current
+        hdr = bytes(b.rx_pin[last_off + 4:last_off + 16].numpy().tobytes())
+        self.emit('packet', {'xid': int.from_bytes(hdr[:4], 'big',
+                                                   signed=True),
+                             'opcode': 'BULK',
+                             'zxid': int.from_bytes(hdr[4:12], 'big',
+                                                    signed=True)})
+        self.bulks.remove(b)
+        try:
+            res = b.finish(nbytes)
+        except Exception as e:                  # decode failure -> caller
+            b.cb(e)
+        else:
+            b.cb(None, res)
+        self.emit('_bulkdone')
 
     def _bulk_rx(self, xid, body):
         for b in self.bulks:
             if b.owns(xid):
+                self.bulk_frames_py += 1
                 # header zxid keeps the session's lastZxid / expiry current
                 self.emit('packet', {'xid': xid, 'opcode': 'BULK',
                                      'zxid': int.from_bytes(body[4:12], 'big',

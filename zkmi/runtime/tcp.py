@@ -143,6 +143,43 @@ class TcpSocket(EventEmitter):
             return False
         return True
 
+    # -- GPU bulk path (native loop only) -------------------------------------
+
+    def can_capture(self):
+        """True when the transport can route a reply xid range into a
+        buffer itself (the native loop's Transport.capture)."""
+        return (self.transport is not None and not self.closed and
+                not self._paused and hasattr(self.transport, 'capture'))
+
+    def capture(self, x0, n, addr, size, max_packet, done, prefix=b''):
+        """Copy the reply frames with xid in [x0, x0+n) into ``size``
+        bytes at ``addr`` (a pinned host buffer) inside the loop's read
+        path; ``done(status, nbytes, nframes, last_off)`` ends it (0 all
+        frames, 1 buffer full, 2 bad frame length, 3 cancelled; the frames
+        not captured go to 'data' as usual)."""
+        self.transport.capture(x0, n, addr, size, max_packet, done, prefix)
+
+    def capture_cancel(self):
+        if self.transport is not None and hasattr(self.transport,
+                                                  'capture_cancel'):
+            self.transport.capture_cancel()
+
+    def write_from(self, addr, n):
+        """Queue ``n`` bytes at ``addr`` (raw memory, e.g. a pinned host
+        buffer the GPU encoder filled) without a bytes object."""
+        if self.closed or self.ended or self.transport is None or \
+                self.transport.is_closing():
+            return False
+        f = getattr(self.transport, 'write_from', None)
+        if f is None:
+            import ctypes
+            return self.write(ctypes.string_at(addr, n))
+        self.bytes_out += n
+        try:
+            return f(addr, n)
+        except (OSError, RuntimeError):
+            return False
+
     def end(self, data=None):
         """Half-close after writing ``data`` (Node ``socket.end``)."""
         if data:

@@ -71,6 +71,13 @@ class ZKDecoder(object):
     def pending(self):
         return len(self.buf)
 
+    def take_pending(self):
+        """Hand the buffered partial frame to another framer (the native
+        transport's bulk capture) and forget it."""
+        b = bytes(self.buf)
+        self.buf = bytearray()
+        return b
+
 
 class ZKEncoder(object):
     """Outbound framing; records ``xid -> opcode`` for the decoder

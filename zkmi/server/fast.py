@@ -24,10 +24,14 @@ class FastZKServer(object):
         if not available():
             raise RuntimeError('zk_fastserver not built '
                                '(tools/build_native.py)')
+        # a sanitizer runtime preloaded into the caller (tools/
+        # sanitize_host.sh) is not for this uninstrumented program
+        env = {k: v for k, v in os.environ.items() if k != 'LD_PRELOAD'}
         self.p = subprocess.Popen(
             [BINARY, '--port', str(port), '--preload', str(preload),
              '--data-bytes', str(data_bytes), '--fanout', str(fanout)],
-            stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True)
+            stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True,
+            env=env)
         f = self.p.stdout.readline().split()
         if len(f) != 2 or f[0] != 'PORT':
             self.p.kill()

@@ -238,6 +238,12 @@ def main():
                     help='GET_DATA requests per GPU per step')
     ap.add_argument('--nodes', type=int, default=1_000_000)
     ap.add_argument('--data-bytes', type=int, default=100)
+    ap.add_argument('--data-dist', default=None,
+                    help='uniform:LO-HI: leaf data lengths uniform in LO..HI '
+                         'bytes instead of --data-bytes (variable frames)')
+    ap.add_argument('--name-pad', default=None,
+                    help='LO-HI: leaf names padded by a uniform LO..HI '
+                         'characters (variable path lengths)')
     ap.add_argument('--no-rtt', action='store_true',
                     help='skip the interactive RTT and bulk-TCP runs')
     ap.add_argument('--bulk-batch', type=int, default=1 << 20,
@@ -293,6 +299,14 @@ def main():
     cdev = dev if backend == 'nccl' else torch.device('cpu')
 
     from zkmi.bench import synthetic as S
+    dd = npad = None
+    if a.data_dist:
+        kind, _, rng = a.data_dist.partition(':')
+        if kind != 'uniform':
+            raise SystemExit('--data-dist: only uniform:LO-HI')
+        dd = tuple(int(x) for x in rng.split('-'))
+    if a.name_pad:
+        npad = tuple(int(x) for x in a.name_pad.split('-'))
     if a.workload == 'get' and a.sharded:
         from zkmi.parallel.sharded import ShardedGetPipeline
         # every rank holds the same layout and data; its index covers only
@@ -303,7 +317,8 @@ def main():
                                   coll_device=cdev)
         per_step = a.batch
     elif a.workload == 'get':
-        tree = S.GpuTree(a.nodes, a.data_bytes, device=dev, seed=rank)
+        tree = S.GpuTree(a.nodes, a.data_bytes, device=dev, seed=rank,
+                         data_dist=dd, name_pad=npad)
         pipe = S.GetPipeline(tree, a.batch, seed=rank, streams=a.streams)
         per_step = a.batch
     elif a.workload == 'watch':
@@ -390,9 +405,11 @@ def main():
             'dtype': 'uint8',
             'data': 'synthetic',
             'config': {
-                'model': 'zk-%s%s %dk-znode tree, %dB data' % (
+                'model': 'zk-%s%s %dk-znode tree, %s data%s' % (
                     a.workload, ' sharded' if a.sharded else '',
-                    a.nodes // 1000, a.data_bytes),
+                    a.nodes // 1000,
+                    ('%d-%dB' % dd) if dd else '%dB' % a.data_bytes,
+                    (', names +%d-%d chars' % npad) if npad else ''),
                 'global_batch': per_step * world,
                 'seq_len': 1,
                 'parallelism': 'dp%d' % world,

@@ -1,0 +1,806 @@
+// torch.ops.zkmi — the HIP batch codec (csrc/kernels, libzkmi_hip.so) as a
+// PyTorch-ROCm operator library.
+//
+// Every op takes tensors, checks dtype / device / contiguity / length
+// before a pointer reaches a kernel (a wrong tensor raises; it never
+// corrupts memory), runs on the caller's current HIP stream and raises
+// on a launch error.  The kernels' launchers are the extern "C" functions
+// of libzkmi_hip.so; the batch descriptors they take (ZkReqBatch, ZkTree,
+// ...) are assembled here from tensor lists in the field order of
+// csrc/kernels/zk_batch.h and tree.hip.  Mutated arguments are marked
+// (a!) in the schemas.
+#include <ATen/ATen.h>
+#include <c10/hip/HIPStream.h>
+#include <torch/library.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../kernels/zk_batch.h"
+
+extern "C" {
+struct ZkTree {
+  int64_t* ht;
+  int64_t mask;
+  int64_t* node_path_off;
+  int32_t* node_path_len;
+  int64_t* node_parent;
+  uint8_t* path_arena;
+  int64_t path_cap;
+  int64_t slab_cap;
+  int64_t* counters;
+  ZkNodeStore store;
+  int64_t* free_list;
+  int64_t free_cap;
+  int32_t* cver;
+  int32_t* nchild;
+  int64_t* pzxid;
+  int32_t* dirty;
+  int64_t* dirty_list;
+  int64_t* node_pw;
+};
+struct ZkSessionTable {
+  int64_t* sid;
+  uint8_t* passwd;
+  int32_t* timeout;
+  int32_t* state;
+  int64_t* next;
+  int64_t cap;
+};
+
+int64_t zk_scan_workspace(int64_t n);
+int zk_scan_set_mode(int mode);
+int zk_scan_excl_i64(const int64_t*, int64_t*, int64_t, int64_t*, int64_t*,
+                     hipStream_t);
+int zk_scan_excl_i32(const int32_t*, int64_t*, int64_t, int64_t*, int64_t*,
+                     hipStream_t);
+int zk_encode_requests2(const ZkReqBatch*, int64_t, int64_t*, int64_t*,
+                        int64_t*, int64_t*, uint8_t*, int64_t, int64_t*,
+                        int64_t, int32_t*, int32_t, hipStream_t);
+int zk_encode_set_watches(const int64_t*, const int32_t*, const uint8_t*,
+                          int64_t, int64_t, int64_t, int64_t, int64_t*,
+                          int64_t*, int64_t*, int64_t*, uint8_t*, int64_t,
+                          int32_t*, hipStream_t);
+int zk_encode_connect_requests(const int32_t*, const int64_t*, const int32_t*,
+                               const int64_t*, const int64_t*, const int32_t*,
+                               const uint8_t*, int64_t, int64_t*, int64_t*,
+                               int64_t*, int64_t*, uint8_t*, hipStream_t);
+int zk_encode_responses2(const ZkRespBatch*, const ZkNodeStore*,
+                         const int64_t*, int64_t, int64_t*, int64_t*,
+                         int64_t*, int64_t*, uint8_t*, int64_t, int32_t*,
+                         int32_t, int32_t, hipStream_t);
+int64_t zk_frame_scan_workspace(int64_t n);
+int zk_frame_scan3(const uint8_t*, const int64_t*, int64_t, int64_t,
+                   uint8_t*, int64_t, int64_t*, int32_t*, int64_t, int64_t*,
+                   int32_t, hipStream_t);
+int zk_frame_scan_stats(const uint8_t*, int64_t, int32_t, uint32_t*,
+                        hipStream_t);
+int zk_frame_scan_dbg(int64_t* host, int64_t tiles);
+int zk_decode_replies(const uint8_t*, const int64_t*, const int32_t*,
+                      const int64_t*, int64_t, const int64_t*, int64_t,
+                      const ZkReplyOut*, hipStream_t);
+int zk_expand_strings(const uint8_t*, const int64_t*, const int32_t*,
+                      const int64_t*, int64_t, int64_t*, int32_t*,
+                      hipStream_t);
+int zk_expand_acl(const uint8_t*, const int64_t*, const int32_t*,
+                  const int64_t*, int64_t, int32_t*, int64_t*, int32_t*,
+                  int64_t*, int32_t*, hipStream_t);
+int zk_decode_requests(const uint8_t*, const int64_t*, const int32_t*,
+                       const int64_t*, int64_t, const ZkReqOut*, hipStream_t);
+int zk_decode_connect_responses(const uint8_t*, const int64_t*,
+                                const int32_t*, int64_t, int32_t*, int32_t*,
+                                int64_t*, int64_t*, int32_t*, int32_t*,
+                                hipStream_t);
+int zk_tree_fill(const ZkTree*, int64_t, int64_t, const int32_t*, int64_t,
+                 hipStream_t);
+int zk_tree_build(const ZkTree*, int64_t, int64_t, hipStream_t);
+int zk_tree_serve(const ZkTree*, const uint8_t*, const ZkReqOut*,
+                  const int64_t*, int64_t, int32_t*, int32_t*, int32_t*,
+                  int64_t*, int64_t*, int64_t*, int32_t*, int64_t*, int64_t*,
+                  int64_t*, int64_t, int64_t, hipStream_t);
+int zk_tree_expire(const ZkTree*, int64_t, int64_t, unsigned long long*,
+                   hipStream_t);
+int zk_bench_gen_get(int64_t, uint64_t, int64_t, int64_t, int32_t,
+                     const int64_t*, int64_t*, int32_t*, int64_t*, int32_t*,
+                     hipStream_t);
+int zk_bench_check_get(int64_t, const int32_t*, const int32_t*,
+                       const int32_t*, const int32_t*, const int64_t*,
+                       const int32_t*, const int64_t*, const int32_t*,
+                       const int32_t*, unsigned long long*, hipStream_t);
+int zk_bench_check_notif(int64_t, int64_t, const uint64_t*, int64_t, int64_t,
+                         const int64_t*, const int32_t*, const uint8_t*,
+                         const uint8_t*, const int32_t*, const int32_t*,
+                         const int32_t*, const int32_t*, const int32_t*,
+                         const int64_t*, const int32_t*, unsigned long long*,
+                         hipStream_t);
+int64_t zk_route_workspace(int64_t n, int32_t world);
+int zk_route_requests(int64_t, int32_t, const int64_t*, const int32_t*,
+                      const uint8_t*, const int64_t*, const int32_t*,
+                      int32_t*, int64_t*, int32_t*, int64_t*, int32_t*,
+                      int64_t*, int64_t*, hipStream_t);
+int zk_session_connect(const uint8_t*, const int64_t*, const int32_t*,
+                       const int64_t*, int64_t, const ZkSessionTable*,
+                       int64_t, uint64_t, int32_t, int32_t, const int64_t*,
+                       uint8_t*, int64_t*, int32_t*, hipStream_t);
+int zk_session_close(const ZkSessionTable*, const int64_t*, int64_t,
+                     hipStream_t);
+}
+
+namespace {
+
+using at::Tensor;
+using c10::ScalarType;
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void hip_ok(int rc, const char* what) {
+  TORCH_CHECK(rc == 0, "zkmi: ", what, " failed (hip error ", rc, ")");
+}
+
+const char* dtname(ScalarType t) { return c10::toString(t); }
+
+// A device tensor of `dt`, contiguous, with at least `min_numel` elements,
+// on the same device as `ref` (when given).
+template <typename T>
+T* P(const Tensor& t, ScalarType dt, int64_t min_numel, const char* name,
+     const Tensor* ref = nullptr) {
+  TORCH_CHECK(t.defined(), "zkmi: ", name, " is undefined");
+  TORCH_CHECK(t.is_cuda(), "zkmi: ", name, " must be a GPU tensor, got ",
+              t.device());
+  TORCH_CHECK(t.scalar_type() == dt, "zkmi: ", name, " must be ",
+              dtname(dt), ", got ", dtname(t.scalar_type()));
+  TORCH_CHECK(t.is_contiguous(), "zkmi: ", name, " must be contiguous");
+  TORCH_CHECK(t.numel() >= min_numel, "zkmi: ", name, " has ", t.numel(),
+              " elements, needs ", min_numel);
+  if (ref != nullptr)
+    TORCH_CHECK(t.device() == ref->device(), "zkmi: ", name, " is on ",
+                t.device(), ", expected ", ref->device());
+  return reinterpret_cast<T*>(t.data_ptr());
+}
+
+template <typename T>
+T* Popt(const c10::optional<Tensor>& t, ScalarType dt, int64_t min_numel,
+        const char* name, const Tensor* ref = nullptr) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  return P<T>(*t, dt, min_numel, name, ref);
+}
+
+#define U8 ScalarType::Byte
+#define I32 ScalarType::Int
+#define I64 ScalarType::Long
+
+void need(const std::vector<Tensor>& v, size_t k, const char* what) {
+  TORCH_CHECK(v.size() == k, "zkmi: ", what, " needs ", k, " tensors, got ",
+              v.size());
+}
+
+// -- descriptor assembly ---------------------------------------------------
+
+// [opcode, xid, arg, path_off, path_len, data_off, data_len, acl_id,
+//  path_arena, data_arena, acl_off, acl_len, acl_arena], n records
+ZkReqBatch req_batch(const std::vector<Tensor>& b, int64_t n) {
+  need(b, 13, "request batch");
+  const Tensor* r = &b[0];
+  ZkReqBatch s;
+  s.opcode = P<int32_t>(b[0], I32, n, "batch.opcode", r);
+  s.xid = P<int32_t>(b[1], I32, n, "batch.xid", r);
+  s.arg = P<int32_t>(b[2], I32, n, "batch.arg", r);
+  s.path_off = P<int64_t>(b[3], I64, n, "batch.path_off", r);
+  s.path_len = P<int32_t>(b[4], I32, n, "batch.path_len", r);
+  s.data_off = P<int64_t>(b[5], I64, n, "batch.data_off", r);
+  s.data_len = P<int32_t>(b[6], I32, n, "batch.data_len", r);
+  s.acl_id = P<int32_t>(b[7], I32, n, "batch.acl_id", r);
+  s.path_arena = P<uint8_t>(b[8], U8, 1, "batch.path_arena", r);
+  s.data_arena = P<uint8_t>(b[9], U8, 1, "batch.data_arena", r);
+  s.acl_off = P<int64_t>(b[10], I64, 1, "batch.acl_off", r);
+  s.acl_len = P<int32_t>(b[11], I32, 1, "batch.acl_len", r);
+  s.acl_arena = P<uint8_t>(b[12], U8, 1, "batch.acl_arena", r);
+  return s;
+}
+
+// [slab, slot_off, data_len, slot_cap]
+ZkNodeStore node_store(const std::vector<Tensor>& v, size_t at,
+                       const Tensor* r) {
+  ZkNodeStore s;
+  const int64_t cap = v[at + 1].numel();
+  s.slab = P<uint8_t>(v[at], U8, 1, "store.slab", r);
+  s.slot_off = P<int64_t>(v[at + 1], I64, 1, "store.slot_off", r);
+  s.data_len = P<int32_t>(v[at + 2], I32, cap, "store.data_len", r);
+  s.slot_cap = P<int32_t>(v[at + 3], I32, cap, "store.slot_cap", r);
+  s.cap = cap;
+  return s;
+}
+
+// [ht, node_path_off, node_path_len, node_parent, path_arena, counters,
+//  slab, slot_off, data_len, slot_cap, free_list, cver, nchild, pzxid,
+//  dirty, dirty_list, node_pw]; sizes give mask, caps
+ZkTree tree(const std::vector<Tensor>& v) {
+  need(v, 17, "tree");
+  const Tensor* r = &v[0];
+  ZkTree t;
+  const int64_t hw = v[0].numel() / 2;          // {key, val} entries
+  TORCH_CHECK(hw > 0 && (hw & (hw - 1)) == 0,
+              "zkmi: tree.ht must hold a power of two of 2-word entries");
+  const int64_t cap = v[7].numel();
+  t.ht = P<int64_t>(v[0], I64, 2, "tree.ht", r);
+  t.mask = hw - 1;
+  t.node_path_off = P<int64_t>(v[1], I64, cap, "tree.node_path_off", r);
+  t.node_path_len = P<int32_t>(v[2], I32, cap, "tree.node_path_len", r);
+  t.node_parent = P<int64_t>(v[3], I64, cap, "tree.node_parent", r);
+  t.path_arena = P<uint8_t>(v[4], U8, 1, "tree.path_arena", r);
+  t.path_cap = v[4].numel();
+  t.counters = P<int64_t>(v[5], I64, 9, "tree.counters", r);
+  t.store = node_store(v, 6, r);
+  t.slab_cap = v[6].numel();
+  t.free_list = P<int64_t>(v[10], I64, 1, "tree.free_list", r);
+  t.free_cap = v[10].numel();
+  t.cver = P<int32_t>(v[11], I32, cap, "tree.cver", r);
+  t.nchild = P<int32_t>(v[12], I32, cap, "tree.nchild", r);
+  t.pzxid = P<int64_t>(v[13], I64, cap, "tree.pzxid", r);
+  t.dirty = P<int32_t>(v[14], I32, cap, "tree.dirty", r);
+  t.dirty_list = P<int64_t>(v[15], I64, cap, "tree.dirty_list", r);
+  t.node_pw = P<int64_t>(v[16], I64, cap, "tree.node_pw", r);
+  return t;
+}
+
+// [xid, err, opcode, status, zxid, stat64 [6, cap], stat32 [5, cap],
+//  pay_off, pay_len, aux0, aux1]
+ZkReplyOut reply_out(const std::vector<Tensor>& v, int64_t cap,
+                     const Tensor* r) {
+  need(v, 11, "reply table");
+  ZkReplyOut o;
+  o.xid = P<int32_t>(v[0], I32, cap, "reply.xid", r);
+  o.err = P<int32_t>(v[1], I32, cap, "reply.err", r);
+  o.opcode = P<int32_t>(v[2], I32, cap, "reply.opcode", r);
+  o.status = P<int32_t>(v[3], I32, cap, "reply.status", r);
+  o.zxid = P<int64_t>(v[4], I64, cap, "reply.zxid", r);
+  TORCH_CHECK(v[5].dim() == 2 && v[5].size(0) == 6 && v[5].size(1) == cap,
+              "zkmi: reply.stat64 must be [6, ", cap, "]");
+  TORCH_CHECK(v[6].dim() == 2 && v[6].size(0) == 5 && v[6].size(1) == cap,
+              "zkmi: reply.stat32 must be [5, ", cap, "]");
+  o.stat64 = P<int64_t>(v[5], I64, 6 * cap, "reply.stat64", r);
+  o.stat32 = P<int32_t>(v[6], I32, 5 * cap, "reply.stat32", r);
+  o.pay_off = P<int64_t>(v[7], I64, cap, "reply.pay_off", r);
+  o.pay_len = P<int32_t>(v[8], I32, cap, "reply.pay_len", r);
+  o.aux0 = P<int32_t>(v[9], I32, cap, "reply.aux0", r);
+  o.aux1 = P<int32_t>(v[10], I32, cap, "reply.aux1", r);
+  o.cap = cap;
+  return o;
+}
+
+// [xid, opcode, status, path_off, path_len, data_off, data_len, arg,
+//  vec_off, vec_count, rel_zxid]
+ZkReqOut req_out(const std::vector<Tensor>& v, int64_t cap, const Tensor* r) {
+  need(v, 11, "request table");
+  ZkReqOut o;
+  o.xid = P<int32_t>(v[0], I32, cap, "req.xid", r);
+  o.opcode = P<int32_t>(v[1], I32, cap, "req.opcode", r);
+  o.status = P<int32_t>(v[2], I32, cap, "req.status", r);
+  o.path_off = P<int64_t>(v[3], I64, cap, "req.path_off", r);
+  o.path_len = P<int32_t>(v[4], I32, cap, "req.path_len", r);
+  o.data_off = P<int64_t>(v[5], I64, cap, "req.data_off", r);
+  o.data_len = P<int32_t>(v[6], I32, cap, "req.data_len", r);
+  o.arg = P<int32_t>(v[7], I32, cap, "req.arg", r);
+  o.vec_off = P<int64_t>(v[8], I64, cap, "req.vec_off", r);
+  o.vec_count = P<int32_t>(v[9], I32, cap, "req.vec_count", r);
+  o.rel_zxid = P<int64_t>(v[10], I64, cap, "req.rel_zxid", r);
+  o.cap = cap;
+  return o;
+}
+
+// [opcode, xid, err, node, zxid, path_off, path_len, path_arena, aux]
+ZkRespBatch resp_batch(const std::vector<Tensor>& v,
+                       const c10::optional<Tensor>& slot, int64_t cap,
+                       const Tensor* r) {
+  need(v, 9, "response batch");
+  ZkRespBatch b;
+  b.opcode = P<int32_t>(v[0], I32, cap, "resp.opcode", r);
+  b.xid = P<int32_t>(v[1], I32, cap, "resp.xid", r);
+  b.err = P<int32_t>(v[2], I32, cap, "resp.err", r);
+  b.node = P<int64_t>(v[3], I64, cap, "resp.node", r);
+  b.zxid = P<int64_t>(v[4], I64, cap, "resp.zxid", r);
+  b.path_off = P<int64_t>(v[5], I64, cap, "resp.path_off", r);
+  b.path_len = P<int32_t>(v[6], I32, cap, "resp.path_len", r);
+  b.path_arena = P<uint8_t>(v[7], U8, 1, "resp.path_arena", r);
+  b.aux = P<int32_t>(v[8], I32, cap, "resp.aux", r);
+  b.slot = Popt<int64_t>(slot, I64, cap, "resp.slot", r);
+  return b;
+}
+
+// [sid, passwd, timeout, state, next]
+ZkSessionTable session_table(const std::vector<Tensor>& v) {
+  need(v, 5, "session table");
+  const Tensor* r = &v[0];
+  const int64_t cap = v[0].numel();
+  ZkSessionTable s;
+  s.sid = P<int64_t>(v[0], I64, cap, "sessions.sid", r);
+  s.passwd = P<uint8_t>(v[1], U8, 16 * cap, "sessions.passwd", r);
+  s.timeout = P<int32_t>(v[2], I32, cap, "sessions.timeout", r);
+  s.state = P<int32_t>(v[3], I32, cap, "sessions.state", r);
+  s.next = P<int64_t>(v[4], I64, 1, "sessions.next", r);
+  s.cap = cap;
+  return s;
+}
+
+// -- ops ---------------------------------------------------------------------
+
+int64_t scan_workspace(int64_t n) { return zk_scan_workspace(n); }
+int64_t scan_set_mode(int64_t m) { return zk_scan_set_mode((int)m); }
+
+void scan_excl(const Tensor& x, const Tensor& base, const Tensor& total,
+               const Tensor& ws) {
+  const int64_t n = x.numel();
+  auto b = P<int64_t>(base, I64, std::max<int64_t>(n, 1), "base", &x);
+  auto t = P<int64_t>(total, I64, 1, "total", &x);
+  auto w = P<int64_t>(ws, I64, zk_scan_workspace(std::max<int64_t>(n, 1)),
+                      "ws", &x);
+  if (x.scalar_type() == I32)
+    hip_ok(zk_scan_excl_i32(P<int32_t>(x, I32, n, "x"), b, n, t, w,
+                            cur_stream()), "scan_excl");
+  else
+    hip_ok(zk_scan_excl_i64(P<int64_t>(x, I64, n, "x"), b, n, t, w,
+                            cur_stream()), "scan_excl");
+}
+
+void encode_requests(const std::vector<Tensor>& batch, int64_t n,
+                     const Tensor& sizes, const Tensor& rec_off,
+                     const Tensor& total, const Tensor& ws, const Tensor& out,
+                     const c10::optional<Tensor>& xid_tab, int64_t xid_mask,
+                     const Tensor& err, bool terminate) {
+  ZkReqBatch b = req_batch(batch, n);
+  const Tensor* r = &batch[0];
+  const int64_t m = std::max<int64_t>(n, 1);
+  int64_t* tab = Popt<int64_t>(xid_tab, I64, xid_mask + 1, "xid_tab", r);
+  hip_ok(zk_encode_requests2(
+             &b, n, P<int64_t>(sizes, I64, m, "sizes", r),
+             P<int64_t>(rec_off, I64, m, "rec_off", r),
+             P<int64_t>(total, I64, 1, "total", r),
+             P<int64_t>(ws, I64, zk_scan_workspace(m), "ws", r),
+             P<uint8_t>(out, U8, 1, "out", r), out.numel(), tab, xid_mask,
+             P<int32_t>(err, I32, 1, "err", r), terminate ? 1 : 0,
+             cur_stream()),
+         "encode_requests");
+}
+
+void encode_set_watches(const Tensor& poff, const Tensor& plen,
+                        const Tensor& arena, int64_t n, int64_t c0,
+                        int64_t c1, int64_t rel_zxid, const Tensor& sizes,
+                        const Tensor& off, const Tensor& total,
+                        const Tensor& ws, const Tensor& out,
+                        const Tensor& err) {
+  const int64_t m = std::max<int64_t>(n, 1);
+  TORCH_CHECK(c0 >= 0 && c1 >= 0 && c0 + c1 <= n, "zkmi: bad vector split");
+  hip_ok(zk_encode_set_watches(
+             P<int64_t>(poff, I64, m, "poff"),
+             P<int32_t>(plen, I32, m, "plen", &poff),
+             P<uint8_t>(arena, U8, 1, "arena", &poff), n, c0, c1, rel_zxid,
+             P<int64_t>(sizes, I64, m, "sizes", &poff),
+             P<int64_t>(off, I64, m, "off", &poff),
+             P<int64_t>(total, I64, 1, "total", &poff),
+             P<int64_t>(ws, I64, zk_scan_workspace(m), "ws", &poff),
+             P<uint8_t>(out, U8, 1, "out", &poff), out.numel(),
+             P<int32_t>(err, I32, 1, "err", &poff), cur_stream()),
+         "encode_set_watches");
+}
+
+void encode_connect_requests(const Tensor& proto, const Tensor& zxid,
+                             const Tensor& tmo, const Tensor& sid,
+                             const Tensor& pwo, const Tensor& pwl,
+                             const Tensor& arena, int64_t n,
+                             const Tensor& sizes, const Tensor& off,
+                             const Tensor& total, const Tensor& ws,
+                             const Tensor& out) {
+  const int64_t m = std::max<int64_t>(n, 1);
+  const Tensor* r = &proto;
+  // frame + 28 fixed bytes + password per record
+  TORCH_CHECK(out.numel() >= n * 32 + arena.numel() || n == 0,
+              "zkmi: connect request out buffer too small");
+  hip_ok(zk_encode_connect_requests(
+             P<int32_t>(proto, I32, m, "proto"),
+             P<int64_t>(zxid, I64, m, "zxid", r),
+             P<int32_t>(tmo, I32, m, "timeout", r),
+             P<int64_t>(sid, I64, m, "sid", r),
+             P<int64_t>(pwo, I64, m, "passwd_off", r),
+             P<int32_t>(pwl, I32, m, "passwd_len", r),
+             P<uint8_t>(arena, U8, 1, "arena", r), n,
+             P<int64_t>(sizes, I64, m, "sizes", r),
+             P<int64_t>(off, I64, m, "off", r),
+             P<int64_t>(total, I64, 1, "total", r),
+             P<int64_t>(ws, I64, zk_scan_workspace(m), "ws", r),
+             P<uint8_t>(out, U8, 1, "out", r), cur_stream()),
+         "encode_connect_requests");
+}
+
+void encode_responses(const std::vector<Tensor>& resp,
+                      const c10::optional<Tensor>& slot,
+                      const std::vector<Tensor>& store, const Tensor& n_dev,
+                      int64_t ncap, const Tensor& sizes, const Tensor& rec_off,
+                      const Tensor& total, const Tensor& ws, const Tensor& out,
+                      const Tensor& err, bool presized, bool terminate) {
+  need(store, 4, "node store");
+  const Tensor* r = &resp[0];
+  ZkRespBatch b = resp_batch(resp, slot, ncap, r);
+  ZkNodeStore s = node_store(store, 0, r);
+  const int64_t m = std::max<int64_t>(ncap, 1);
+  hip_ok(zk_encode_responses2(
+             &b, &s, P<int64_t>(n_dev, I64, 1, "count", r), ncap,
+             P<int64_t>(sizes, I64, m, "sizes", r),
+             P<int64_t>(rec_off, I64, m, "rec_off", r),
+             P<int64_t>(total, I64, 1, "total", r),
+             P<int64_t>(ws, I64, zk_scan_workspace(m), "ws", r),
+             P<uint8_t>(out, U8, 1, "out", r), out.numel(),
+             P<int32_t>(err, I32, 1, "err", r), presized ? 1 : 0,
+             terminate ? 1 : 0, cur_stream()),
+         "encode_responses");
+}
+
+int64_t frame_scan_workspace(int64_t n) { return zk_frame_scan_workspace(n); }
+
+void frame_scan(const Tensor& buf, const c10::optional<Tensor>& n_dev,
+                int64_t n_cap, int64_t max_packet, const Tensor& ws,
+                const Tensor& foff, const Tensor& flen, const Tensor& result,
+                int64_t window) {
+  TORCH_CHECK(n_cap >= 0 && n_cap <= buf.numel(),
+              "zkmi: frame_scan length ", n_cap, " past the buffer (",
+              buf.numel(), " bytes)");
+  TORCH_CHECK(ws.numel() >= zk_frame_scan_workspace(n_cap),
+              "zkmi: frame_scan workspace too small");
+  const int64_t cap = foff.numel();
+  hip_ok(zk_frame_scan3(
+             P<uint8_t>(buf, U8, 1, "buf"),
+             Popt<int64_t>(n_dev, I64, 1, "n", &buf), n_cap, max_packet,
+             P<uint8_t>(ws, U8, 1, "ws", &buf), ws.numel(),
+             P<int64_t>(foff, I64, 1, "frame_off", &buf),
+             P<int32_t>(flen, I32, cap, "frame_len", &buf), cap,
+             P<int64_t>(result, I64, 4, "result", &buf), (int32_t)window,
+             cur_stream()),
+         "frame_scan");
+}
+
+std::vector<int64_t> frame_scan_stats(const Tensor& ws, int64_t n_cap,
+                                      int64_t window) {
+  uint32_t o[3] = {0, 0, 0};
+  hip_ok(zk_frame_scan_stats(P<uint8_t>(ws, U8, 1, "ws"), n_cap,
+                             (int32_t)window, o, cur_stream()),
+         "frame_scan_stats");
+  return {o[0], o[1], o[2]};
+}
+
+// Per-tile timing records of the last K1 run built with ZKMI_FS_DBG
+// (tools/diag/k1_dbg.py): [tiles, 8] int64 on the host.
+Tensor frame_scan_dbg(int64_t tiles) {
+  Tensor out = at::zeros({tiles, 8}, at::kLong);
+  hip_ok(zk_frame_scan_dbg(out.data_ptr<int64_t>(), tiles), "frame_scan_dbg");
+  return out;
+}
+
+void decode_replies(const Tensor& buf, const Tensor& foff, const Tensor& flen,
+                    const Tensor& n_dev, const Tensor& xid_tab,
+                    int64_t xid_mask, const std::vector<Tensor>& out) {
+  const int64_t cap = foff.numel();
+  ZkReplyOut o = reply_out(out, cap, &buf);
+  hip_ok(zk_decode_replies(
+             P<uint8_t>(buf, U8, 1, "buf"),
+             P<int64_t>(foff, I64, cap, "frame_off", &buf),
+             P<int32_t>(flen, I32, cap, "frame_len", &buf),
+             P<int64_t>(n_dev, I64, 1, "count", &buf), cap,
+             P<int64_t>(xid_tab, I64, xid_mask + 1, "xid_tab", &buf),
+             xid_mask, &o, cur_stream()),
+         "decode_replies");
+}
+
+void expand_strings(const Tensor& buf, const Tensor& region,
+                    const Tensor& count, const Tensor& base,
+                    const Tensor& soff, const Tensor& slen) {
+  const int64_t n = region.numel();
+  hip_ok(zk_expand_strings(
+             P<uint8_t>(buf, U8, 1, "buf"),
+             P<int64_t>(region, I64, n, "region", &buf),
+             P<int32_t>(count, I32, n, "count", &buf),
+             P<int64_t>(base, I64, n, "base", &buf), n,
+             P<int64_t>(soff, I64, 1, "str_off", &buf),
+             P<int32_t>(slen, I32, soff.numel(), "str_len", &buf),
+             cur_stream()),
+         "expand_strings");
+}
+
+void expand_acl(const Tensor& buf, const Tensor& region, const Tensor& count,
+                const Tensor& base, const Tensor& perms, const Tensor& so,
+                const Tensor& sl, const Tensor& io, const Tensor& il) {
+  const int64_t n = region.numel();
+  const int64_t m = perms.numel();
+  hip_ok(zk_expand_acl(
+             P<uint8_t>(buf, U8, 1, "buf"),
+             P<int64_t>(region, I64, n, "region", &buf),
+             P<int32_t>(count, I32, n, "count", &buf),
+             P<int64_t>(base, I64, n, "base", &buf), n,
+             P<int32_t>(perms, I32, 1, "perms", &buf),
+             P<int64_t>(so, I64, m, "scheme_off", &buf),
+             P<int32_t>(sl, I32, m, "scheme_len", &buf),
+             P<int64_t>(io, I64, m, "id_off", &buf),
+             P<int32_t>(il, I32, m, "id_len", &buf), cur_stream()),
+         "expand_acl");
+}
+
+void decode_requests(const Tensor& buf, const Tensor& foff,
+                     const Tensor& flen, const Tensor& n_dev,
+                     const std::vector<Tensor>& out) {
+  const int64_t cap = foff.numel();
+  ZkReqOut o = req_out(out, cap, &buf);
+  hip_ok(zk_decode_requests(
+             P<uint8_t>(buf, U8, 1, "buf"),
+             P<int64_t>(foff, I64, cap, "frame_off", &buf),
+             P<int32_t>(flen, I32, cap, "frame_len", &buf),
+             P<int64_t>(n_dev, I64, 1, "count", &buf), cap, &o,
+             cur_stream()),
+         "decode_requests");
+}
+
+void decode_connect_responses(const Tensor& buf, const Tensor& foff,
+                              const Tensor& flen, int64_t n,
+                              const Tensor& proto, const Tensor& tmo,
+                              const Tensor& sid, const Tensor& pw_off,
+                              const Tensor& pw_len, const Tensor& status) {
+  const int64_t m = std::max<int64_t>(n, 1);
+  hip_ok(zk_decode_connect_responses(
+             P<uint8_t>(buf, U8, 1, "buf"),
+             P<int64_t>(foff, I64, n, "frame_off", &buf),
+             P<int32_t>(flen, I32, n, "frame_len", &buf), n,
+             P<int32_t>(proto, I32, m, "proto", &buf),
+             P<int32_t>(tmo, I32, m, "timeout", &buf),
+             P<int64_t>(sid, I64, m, "sid", &buf),
+             P<int64_t>(pw_off, I64, m, "passwd_off", &buf),
+             P<int32_t>(pw_len, I32, m, "passwd_len", &buf),
+             P<int32_t>(status, I32, m, "status", &buf), cur_stream()),
+         "decode_connect_responses");
+}
+
+void tree_fill(const std::vector<Tensor>& t, int64_t n0, int64_t n,
+               const Tensor& nkids, int64_t now_ms) {
+  ZkTree s = tree(t);
+  TORCH_CHECK(n0 >= 0 && n <= s.store.cap, "zkmi: tree_fill range");
+  hip_ok(zk_tree_fill(&s, n0, n, P<int32_t>(nkids, I32, n, "nkids", &t[0]),
+                      now_ms, cur_stream()),
+         "tree_fill");
+}
+
+void tree_build(const std::vector<Tensor>& t, int64_t n0, int64_t n) {
+  ZkTree s = tree(t);
+  TORCH_CHECK(n0 >= 0 && n <= s.store.cap, "zkmi: tree_build range");
+  hip_ok(zk_tree_build(&s, n0, n, cur_stream()), "tree_build");
+}
+
+// r = [op, xid, err, node, zxid, path_off, path_len, slot, sizes, bsum]
+void tree_serve(const std::vector<Tensor>& t, const Tensor& rx,
+                const std::vector<Tensor>& q, const Tensor& n_dev,
+                int64_t ncap, const std::vector<Tensor>& r, int64_t session,
+                int64_t now_ms) {
+  ZkTree s = tree(t);
+  const Tensor* d = &t[0];
+  ZkReqOut qo = req_out(q, ncap, d);
+  need(r, 10, "serve outputs");
+  const int64_t nb = (ncap + 255) / 256;
+  hip_ok(zk_tree_serve(
+             &s, P<uint8_t>(rx, U8, 1, "rx", d), &qo,
+             P<int64_t>(n_dev, I64, 1, "count", d), ncap,
+             P<int32_t>(r[0], I32, ncap, "r.opcode", d),
+             P<int32_t>(r[1], I32, ncap, "r.xid", d),
+             P<int32_t>(r[2], I32, ncap, "r.err", d),
+             P<int64_t>(r[3], I64, ncap, "r.node", d),
+             P<int64_t>(r[4], I64, ncap, "r.zxid", d),
+             P<int64_t>(r[5], I64, ncap, "r.path_off", d),
+             P<int32_t>(r[6], I32, ncap, "r.path_len", d),
+             P<int64_t>(r[7], I64, ncap, "r.slot", d),
+             P<int64_t>(r[8], I64, ncap, "r.sizes", d),
+             P<int64_t>(r[9], I64, nb, "r.block_sums", d), session, now_ms,
+             cur_stream()),
+         "tree_serve");
+}
+
+void tree_expire(const std::vector<Tensor>& t, int64_t session, int64_t ncap,
+                 const Tensor& removed) {
+  ZkTree s = tree(t);
+  TORCH_CHECK(ncap <= s.store.cap, "zkmi: tree_expire range");
+  hip_ok(zk_tree_expire(&s, session, ncap,
+                        reinterpret_cast<unsigned long long*>(P<int64_t>(
+                            removed, I64, 1, "removed", &t[0])),
+                        cur_stream()),
+         "tree_expire");
+}
+
+void bench_gen_get(int64_t n, int64_t seed, int64_t leaf0, int64_t nleaves,
+                   int64_t xid_base, const Tensor& node_pw, const Tensor& idx,
+                   const Tensor& xid, const Tensor& poff, const Tensor& plen) {
+  TORCH_CHECK(leaf0 >= 0 && leaf0 + nleaves <= node_pw.numel(),
+              "zkmi: bench_gen_get leaf range");
+  hip_ok(zk_bench_gen_get(n, (uint64_t)seed, leaf0, nleaves,
+                          (int32_t)xid_base,
+                          P<int64_t>(node_pw, I64, 1, "node_pw"),
+                          P<int64_t>(idx, I64, n, "idx", &node_pw),
+                          P<int32_t>(xid, I32, n, "xid", &node_pw),
+                          P<int64_t>(poff, I64, n, "path_off", &node_pw),
+                          P<int32_t>(plen, I32, n, "path_len", &node_pw),
+                          cur_stream()),
+         "bench_gen_get");
+}
+
+void bench_check_get(int64_t n, const std::vector<Tensor>& reply,
+                     const Tensor& idx, const Tensor& xid,
+                     const Tensor& data_len, const Tensor& acc) {
+  const int64_t cap = reply[0].numel();
+  TORCH_CHECK(n <= cap, "zkmi: bench_check_get n past the reply table");
+  ZkReplyOut o = reply_out(reply, cap, &idx);
+  hip_ok(zk_bench_check_get(
+             n, o.status, o.err, o.opcode, o.xid, o.stat64, o.pay_len,
+             P<int64_t>(idx, I64, n, "idx"),
+             P<int32_t>(xid, I32, n, "xid", &idx),
+             P<int32_t>(data_len, I32, 1, "data_len", &idx),
+             reinterpret_cast<unsigned long long*>(
+                 P<int64_t>(acc, I64, 1, "acc", &idx)),
+             cur_stream()),
+         "bench_check_get");
+}
+
+void bench_check_notif(int64_t total, int64_t n_per, const Tensor& seeds,
+                       int64_t leaf0, int64_t nleaves,
+                       const Tensor& node_path_off,
+                       const Tensor& node_path_len, const Tensor& path_arena,
+                       const Tensor& rx, const std::vector<Tensor>& reply,
+                       const Tensor& acc) {
+  const int64_t cap = reply[0].numel();
+  TORCH_CHECK(total <= cap, "zkmi: bench_check_notif past the reply table");
+  TORCH_CHECK(n_per > 0 && seeds.numel() * n_per >= total,
+              "zkmi: bench_check_notif seeds");
+  ZkReplyOut o = reply_out(reply, cap, &rx);
+  hip_ok(zk_bench_check_notif(
+             total, n_per,
+             reinterpret_cast<const uint64_t*>(
+                 P<int64_t>(seeds, I64, 1, "seeds", &rx)),
+             leaf0, nleaves,
+             P<int64_t>(node_path_off, I64, leaf0 + nleaves,
+                        "node_path_off", &rx),
+             P<int32_t>(node_path_len, I32, leaf0 + nleaves,
+                        "node_path_len", &rx),
+             P<uint8_t>(path_arena, U8, 1, "path_arena", &rx),
+             P<uint8_t>(rx, U8, 1, "rx"), o.status, o.err, o.opcode, o.aux0,
+             o.aux1, o.pay_off, o.pay_len,
+             reinterpret_cast<unsigned long long*>(
+                 P<int64_t>(acc, I64, 1, "acc", &rx)),
+             cur_stream()),
+         "bench_check_notif");
+}
+
+int64_t route_workspace(int64_t n, int64_t world) {
+  return zk_route_workspace(n, (int32_t)world);
+}
+
+void route_requests(int64_t n, int64_t world, const Tensor& poff,
+                    const Tensor& plen, const Tensor& arena,
+                    const Tensor& idx, const Tensor& xid, const Tensor& owner,
+                    const Tensor& idx_s, const Tensor& xid_s,
+                    const Tensor& poff_s, const Tensor& plen_s,
+                    const Tensor& counts, const Tensor& ws) {
+  TORCH_CHECK(world >= 1 && world <= 64, "zkmi: route world 1..64");
+  const Tensor* r = &poff;
+  hip_ok(zk_route_requests(
+             n, (int32_t)world, P<int64_t>(poff, I64, n, "path_off"),
+             P<int32_t>(plen, I32, n, "path_len", r),
+             P<uint8_t>(arena, U8, 1, "arena", r),
+             P<int64_t>(idx, I64, n, "idx", r),
+             P<int32_t>(xid, I32, n, "xid", r),
+             P<int32_t>(owner, I32, n, "owner", r),
+             P<int64_t>(idx_s, I64, n, "idx_s", r),
+             P<int32_t>(xid_s, I32, n, "xid_s", r),
+             P<int64_t>(poff_s, I64, n, "path_off_s", r),
+             P<int32_t>(plen_s, I32, n, "path_len_s", r),
+             P<int64_t>(counts, I64, world, "counts", r),
+             P<int64_t>(ws, I64, zk_route_workspace(n, (int32_t)world),
+                        "ws", r),
+             cur_stream()),
+         "route_requests");
+}
+
+void session_connect(const Tensor& buf, const Tensor& foff,
+                     const Tensor& flen, const Tensor& n_dev, int64_t ncap,
+                     const std::vector<Tensor>& tab, int64_t server_id,
+                     int64_t secret, int64_t min_to, int64_t max_to,
+                     const Tensor& zxid_now, const Tensor& out,
+                     const Tensor& resp_sid, const Tensor& outcome) {
+  ZkSessionTable s = session_table(tab);
+  const Tensor* r = &buf;
+  hip_ok(zk_session_connect(
+             P<uint8_t>(buf, U8, 1, "buf"),
+             P<int64_t>(foff, I64, ncap, "frame_off", r),
+             P<int32_t>(flen, I32, ncap, "frame_len", r),
+             P<int64_t>(n_dev, I64, 1, "count", r), ncap, &s, server_id,
+             (uint64_t)secret, (int32_t)min_to, (int32_t)max_to,
+             P<int64_t>(zxid_now, I64, 1, "zxid_now", r),
+             P<uint8_t>(out, U8, 41 * ncap, "out", r),
+             P<int64_t>(resp_sid, I64, ncap, "resp_sid", r),
+             P<int32_t>(outcome, I32, ncap, "outcome", r), cur_stream()),
+         "session_connect");
+}
+
+void session_close(const std::vector<Tensor>& tab, const Tensor& sids) {
+  ZkSessionTable s = session_table(tab);
+  hip_ok(zk_session_close(&s, P<int64_t>(sids, I64, 0, "sids", &tab[0]),
+                          sids.numel(), cur_stream()),
+         "session_close");
+}
+
+}  // namespace
+
+TORCH_LIBRARY(zkmi, m) {
+  m.def("scan_workspace(int n) -> int", &scan_workspace);
+  m.def("scan_set_mode(int mode) -> int", &scan_set_mode);
+  m.def("scan_excl(Tensor x, Tensor(a!) base, Tensor(b!) total, "
+        "Tensor(c!) ws) -> ()", &scan_excl);
+  m.def("encode_requests(Tensor[] batch, int n, Tensor(a!) sizes, "
+        "Tensor(b!) rec_off, Tensor(c!) total, Tensor(d!) ws, "
+        "Tensor(e!) out, Tensor(f!)? xid_tab, int xid_mask, Tensor(g!) err, "
+        "bool terminate) -> ()", &encode_requests);
+  m.def("encode_set_watches(Tensor poff, Tensor plen, Tensor arena, int n, "
+        "int c0, int c1, int rel_zxid, Tensor(a!) sizes, Tensor(b!) off, "
+        "Tensor(c!) total, Tensor(d!) ws, Tensor(e!) out, Tensor(f!) err) "
+        "-> ()", &encode_set_watches);
+  m.def("encode_connect_requests(Tensor proto, Tensor zxid, Tensor timeout, "
+        "Tensor sid, Tensor passwd_off, Tensor passwd_len, Tensor arena, "
+        "int n, Tensor(a!) sizes, Tensor(b!) off, Tensor(c!) total, "
+        "Tensor(d!) ws, Tensor(e!) out) -> ()", &encode_connect_requests);
+  m.def("encode_responses(Tensor[] resp, Tensor? slot, Tensor[] store, "
+        "Tensor count, int ncap, Tensor(a!) sizes, Tensor(b!) rec_off, "
+        "Tensor(c!) total, Tensor(d!) ws, Tensor(e!) out, Tensor(f!) err, "
+        "bool presized, bool terminate) -> ()", &encode_responses);
+  m.def("frame_scan_workspace(int n) -> int", &frame_scan_workspace);
+  m.def("frame_scan(Tensor buf, Tensor? n, int n_cap, int max_packet, "
+        "Tensor(a!) ws, Tensor(b!) frame_off, Tensor(c!) frame_len, "
+        "Tensor(d!) result, int window) -> ()", &frame_scan);
+  m.def("frame_scan_stats(Tensor ws, int n_cap, int window) -> int[]",
+        &frame_scan_stats);
+  m.def("frame_scan_dbg(int tiles) -> Tensor", &frame_scan_dbg);
+  m.def("decode_replies(Tensor buf, Tensor frame_off, Tensor frame_len, "
+        "Tensor count, Tensor xid_tab, int xid_mask, Tensor(a!)[] out) -> ()",
+        &decode_replies);
+  m.def("expand_strings(Tensor buf, Tensor region, Tensor count, "
+        "Tensor base, Tensor(a!) str_off, Tensor(b!) str_len) -> ()",
+        &expand_strings);
+  m.def("expand_acl(Tensor buf, Tensor region, Tensor count, Tensor base, "
+        "Tensor(a!) perms, Tensor(b!) scheme_off, Tensor(c!) scheme_len, "
+        "Tensor(d!) id_off, Tensor(e!) id_len) -> ()", &expand_acl);
+  m.def("decode_requests(Tensor buf, Tensor frame_off, Tensor frame_len, "
+        "Tensor count, Tensor(a!)[] out) -> ()", &decode_requests);
+  m.def("decode_connect_responses(Tensor buf, Tensor frame_off, "
+        "Tensor frame_len, int n, Tensor(a!) proto, Tensor(b!) timeout, "
+        "Tensor(c!) sid, Tensor(d!) passwd_off, Tensor(e!) passwd_len, "
+        "Tensor(f!) status) -> ()", &decode_connect_responses);
+  m.def("tree_fill(Tensor(a!)[] tree, int n0, int n, Tensor nkids, "
+        "int now_ms) -> ()", &tree_fill);
+  m.def("tree_build(Tensor(a!)[] tree, int n0, int n) -> ()", &tree_build);
+  m.def("tree_serve(Tensor(a!)[] tree, Tensor rx, Tensor[] requests, "
+        "Tensor count, int ncap, Tensor(b!)[] out, int session, int now_ms) "
+        "-> ()", &tree_serve);
+  m.def("tree_expire(Tensor(a!)[] tree, int session, int ncap, "
+        "Tensor(b!) removed) -> ()", &tree_expire);
+  m.def("bench_gen_get(int n, int seed, int leaf0, int nleaves, "
+        "int xid_base, Tensor node_pw, Tensor(a!) idx, Tensor(b!) xid, "
+        "Tensor(c!) path_off, Tensor(d!) path_len) -> ()", &bench_gen_get);
+  m.def("bench_check_get(int n, Tensor[] reply, Tensor idx, Tensor xid, "
+        "Tensor data_len, Tensor(a!) acc) -> ()", &bench_check_get);
+  m.def("bench_check_notif(int total, int n_per, Tensor seeds, int leaf0, "
+        "int nleaves, Tensor node_path_off, Tensor node_path_len, "
+        "Tensor path_arena, Tensor rx, Tensor[] reply, Tensor(a!) acc) -> ()",
+        &bench_check_notif);
+  m.def("route_workspace(int n, int world) -> int", &route_workspace);
+  m.def("route_requests(int n, int world, Tensor path_off, Tensor path_len, "
+        "Tensor arena, Tensor idx, Tensor xid, Tensor(a!) owner, "
+        "Tensor(b!) idx_s, Tensor(c!) xid_s, Tensor(d!) path_off_s, "
+        "Tensor(e!) path_len_s, Tensor(f!) counts, Tensor(g!) ws) -> ()",
+        &route_requests);
+  m.def("session_connect(Tensor buf, Tensor frame_off, Tensor frame_len, "
+        "Tensor count, int ncap, Tensor(a!)[] table, int server_id, "
+        "int secret, int min_to, int max_to, Tensor zxid_now, Tensor(b!) out, "
+        "Tensor(c!) resp_sid, Tensor(d!) outcome) -> ()", &session_connect);
+  m.def("session_close(Tensor(a!)[] table, Tensor sids) -> ()",
+        &session_close);
+}

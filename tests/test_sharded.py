@@ -23,16 +23,13 @@ def test_router_matches_host_hash(gpu):
     pipe.step()
     from zkmi.ops import _lib
     L = _lib.lib()
-    P = _lib.ptr
     for W in (3, 8):
-        pipe.rws = torch.empty(L.zk_route_workspace(5000, W),
+        pipe.rws = torch.empty(L.route_workspace(5000, W),
                                dtype=torch.int64, device=gpu)
         cnt = torch.empty(W, dtype=torch.int64, device=gpu)
-        _lib.check(L.zk_route_requests(
-            5000, W, P(pipe.poff), P(pipe.plen), P(tree.path_arena),
-            P(pipe.idx), P(pipe.xid), P(pipe.owner), P(pipe.idx_s),
-            P(pipe.xid_s), P(pipe.poff_s), P(pipe.plen_s), P(cnt),
-            P(pipe.rws), _lib.stream_ptr()), 'route')
+        L.route_requests(5000, W, pipe.poff, pipe.plen, tree.path_arena,
+                         pipe.idx, pipe.xid, pipe.owner, pipe.idx_s,
+                         pipe.xid_s, pipe.poff_s, pipe.plen_s, cnt, pipe.rws)
         arena = tree.path_arena.cpu().numpy().tobytes()
         po, pl = pipe.poff.cpu().tolist(), pipe.plen.cpu().tolist()
         want = path_owner([arena[o:o + n] for o, n in zip(po, pl)], W)

@@ -67,6 +67,37 @@ def build_hip(jobs=4):
     return HIP_SO
 
 
+TORCH_SO = os.path.join(ROOT, 'zkmi', 'ops', 'libzkmi_torch.so')
+TDIR = os.path.join(ROOT, 'csrc', 'torch')
+
+
+def build_torch_ops():
+    """``zkmi/ops/libzkmi_torch.so``: the TORCH_LIBRARY(zkmi, ...) operator
+    library (csrc/torch/zkmi_ops.cpp) over libzkmi_hip.so, loaded with
+    ``torch.ops.load_library`` (torch.ops.zkmi.*).  Built with the host
+    compiler against torch's headers; the kernels stay in libzkmi_hip.so
+    (found through the rpath)."""
+    import torch
+    src = os.path.join(TDIR, 'zkmi_ops.cpp')
+    deps = [src, os.path.join(KDIR, 'zk_batch.h'), HIP_SO]
+    if not _stale(TORCH_SO, deps):
+        return TORCH_SO
+    tdir = os.path.dirname(torch.__file__)
+    inc = [os.path.join(tdir, 'include'),
+           os.path.join(tdir, 'include', 'torch', 'csrc', 'api', 'include'),
+           '/opt/rocm/include']
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    _run(['g++', '-O2', '-fPIC', '-shared', '-std=c++17', '-Wall',
+          '-Wno-unused-function', '-D__HIP_PLATFORM_AMD__=1', '-DUSE_ROCM=1',
+          '-D_GLIBCXX_USE_CXX11_ABI=%d' % abi] +
+         ['-I' + i for i in inc] +
+         [src, '-o', TORCH_SO, '-L' + os.path.join(tdir, 'lib'),
+          '-L' + os.path.dirname(HIP_SO), '-lzkmi_hip', '-lc10', '-lc10_hip',
+          '-ltorch_cpu', '-Wl,-rpath,$ORIGIN',
+          '-Wl,-rpath,' + os.path.join(tdir, 'lib')])
+    return TORCH_SO
+
+
 def host_so_path():
     return _ext_path('_zkhost')
 
@@ -172,6 +203,7 @@ def main():
         return
     if not a.host_only:
         print(build_hip(a.j))
+        print(build_torch_ops())
     if not a.hip_only:
         print(build_host())
 

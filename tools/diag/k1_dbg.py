@@ -1,7 +1,6 @@
 """Per-tile timing of fs_tile (ZKMI_FS_DBG=1): survivor walk, wait for the
 tile before's exit, join walk; for the benchmark's request and reply
 streams."""
-import ctypes
 import os
 import sys
 
@@ -19,10 +18,7 @@ from zkmi.bench import synthetic as S  # noqa: E402
 def dump(name, scanner, nbytes):
     torch.cuda.synchronize()
     tiles = (scanner.last_cap + 4095) // 4096
-    a = np.zeros(tiles * 8, np.int64)
-    _lib.check(_lib.lib().zk_frame_scan_dbg(
-        a.ctypes.data_as(ctypes.c_void_p), tiles), 'dbg')
-    a = a.reshape(tiles, 8)
+    a = _lib.lib().frame_scan_dbg(tiles).numpy()
     nt = (nbytes + 4095) // 4096
     a = a[:nt]
     t0 = a[:, 0].min()

@@ -1,6 +1,5 @@
 """Diagnostic: run the GET pipeline's server half step by step and check
 the serve kernel's reply descriptors on the host before the reply encode."""
-import ctypes
 import os
 import sys
 import time
@@ -38,15 +37,10 @@ def main():
     r = srv.resp
     r.count = ft.count
     r.slot.fill_(-7)
-    q = rt.struct()
-    _lib.check(L.zk_tree_serve(
-        ctypes.byref(tree.struct), _lib.ptr(tx), ctypes.byref(q),
-        _lib.ptr(ft.count), srv.cap_frames, _lib.ptr(r.opcode),
-        _lib.ptr(r.xid), _lib.ptr(r.err), _lib.ptr(r.node),
-        _lib.ptr(r.zxid), _lib.ptr(r.path_off), _lib.ptr(r.path_len),
-        _lib.ptr(r.slot), _lib.ptr(srv.presized[0]),
-        _lib.ptr(srv.presized[1]), 0, int(time.time() * 1000),
-        _lib.stream_ptr()), 'serve')
+    L.tree_serve(tree.tensors, tx, rt.tensors(), ft.count, srv.cap_frames,
+                 [r.opcode, r.xid, r.err, r.node, r.zxid, r.path_off,
+                  r.path_len, r.slot, srv.presized[0], srv.presized[1]],
+                 0, int(time.time() * 1000))
     torch.cuda.synchronize()
     print('serve ok', flush=True)
     err = r.err[:n].cpu()

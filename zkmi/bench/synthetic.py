@@ -22,7 +22,6 @@ sync-free and no byte past a stream's end is walked.
 version CAS and ACL encode (BASELINE config 3).
 """
 
-import ctypes
 import os
 import time
 
@@ -75,6 +74,12 @@ def path_owner(paths, world):
     return out
 
 
+def _i64(u):
+    """A 64-bit unsigned seed as the signed int a torch op schema takes."""
+    u &= (1 << 64) - 1
+    return u - (1 << 64) if u >= (1 << 63) else u
+
+
 def slot_bytes(data_cap):
     """Bytes of one wire-format node slot (zk_batch.h ZkNodeStore)."""
     return _lib.SLOT_DATA + ((data_cap + 15) & ~15) + 4
@@ -86,7 +91,8 @@ class GpuTree(object):
     ``czxid == v + 1``."""
 
     def __init__(self, n_nodes=1_000_000, data_bytes=100, fanout=1000,
-                 device=None, spare=0.25, seed=0, shard=None, ctime_ms=None):
+                 device=None, spare=0.25, seed=0, shard=None, ctime_ms=None,
+                 data_dist=None, name_pad=None):
         dev = torch.device(device) if device is not None else \
             torch.device('cuda', torch.cuda.current_device())
         self.device = dev
@@ -95,8 +101,16 @@ class GpuTree(object):
         # node order: 0 = /bench, 1..ndirs = dirs, then leaves
         paths = ['/bench'] + ['/bench/d%06d' % d for d in range(ndirs)]
         leaf0 = len(paths)
-        paths += ['/bench/d%06d/n%09d' % (i // fanout, i)
-                  for i in range(n_nodes)]
+        # name_pad = (lo, hi): leaf names padded with a uniform lo..hi
+        # characters (variable path lengths)
+        rng = np.random.default_rng(seed + 17)
+        if name_pad is not None:
+            pad = rng.integers(name_pad[0], name_pad[1] + 1, n_nodes)
+            paths += ['/bench/d%06d/n%09d%s' % (i // fanout, i, 'p' * pad[i])
+                      for i in range(n_nodes)]
+        else:
+            paths += ['/bench/d%06d/n%09d' % (i // fanout, i)
+                      for i in range(n_nodes)]
         nst = len(paths)
         parents = np.empty(nst, np.int64)
         parents[0] = -1
@@ -105,6 +119,12 @@ class GpuTree(object):
         self.n_static = nst
         self.leaf0 = leaf0
         self.n_leaves = n_nodes
+        # data_dist = (lo, hi): leaf data lengths uniform in lo..hi bytes
+        # (variable payloads); data_bytes is then the largest
+        if data_dist is not None:
+            leaf_dl = rng.integers(data_dist[0], data_dist[1] + 1,
+                                   n_nodes).astype(np.int32)
+            data_bytes = int(data_dist[1])
         self.data_bytes = data_bytes
         cap = int(nst * (1 + spare)) + 1024
         self.cap = cap
@@ -141,7 +161,10 @@ class GpuTree(object):
                                   device=dev, generator=g)
         self.slot_off = torch.arange(cap, dtype=I64, device=dev) * sb
         self.data_len = torch.zeros(cap, dtype=I32, device=dev)
-        self.data_len[leaf0:nst] = data_bytes
+        if data_dist is not None:
+            self.data_len[leaf0:nst] = torch.from_numpy(leaf_dl).to(dev)
+        else:
+            self.data_len[leaf0:nst] = data_bytes
         self.slot_cap = torch.full((cap,), dcap, dtype=I32, device=dev)
         nkids = np.zeros(nst, np.int32)
         nkids[0] = ndirs
@@ -164,12 +187,16 @@ class GpuTree(object):
         self.dirty = torch.zeros(cap, dtype=I32, device=dev)
         self.dirty_list = torch.empty(cap, dtype=I64, device=dev)
         self.hcap = hcap
-        self._struct = self._make_struct(hcap - 1)
-        sp = _lib.stream_ptr()
+        # the tree / node-store descriptor lists torch.ops.zkmi takes
+        # (csrc/torch/zkmi_ops.cpp tree() / node_store() field order)
+        self.store = [self.slab, self.slot_off, self.data_len,
+                      self.slot_cap]
+        self._tensors = [self.ht, self.node_path_off, self.node_path_len,
+                         self.node_parent, self.path_arena, self.counters] + \
+            self.store + [self.free_list, self.cver, self.nchild, self.pzxid,
+                          self.dirty, self.dirty_list, self.node_pw]
         now = int(time.time() * 1000) if ctime_ms is None else ctime_ms
-        _lib.check(L.zk_tree_fill(ctypes.byref(self._struct), 0, nst,
-                                  _lib.ptr(nk), now, sp),
-                   'zk_tree_fill')
+        L.tree_fill(self._tensors, 0, nst, nk, now)
         # shard = (rank, world): this replica indexes only the leaves whose
         # path hashes to `rank` (zkmi/parallel/sharded.py routes every read
         # there); the rest stay in the layout, unreachable by lookup
@@ -178,30 +205,13 @@ class GpuTree(object):
             own = path_owner(enc[leaf0:], shard[1])
             gone = np.nonzero(own != shard[0])[0] + leaf0
             self.node_parent[torch.from_numpy(gone).to(dev)] = NODE_FREE
-        _lib.check(L.zk_tree_build(ctypes.byref(self._struct), 0, nst, sp),
-                   'zk_tree_build')
+        L.tree_build(self._tensors, 0, nst)
         torch.cuda.synchronize(dev)
 
-    def _make_struct(self, mask):
-        st = _lib.ZkNodeStore(self.slab.data_ptr(), self.slot_off.data_ptr(),
-                              self.data_len.data_ptr(),
-                              self.slot_cap.data_ptr(), self.cap)
-        self.store = st
-        return _lib.ZkTree(self.ht.data_ptr(), mask,
-                           self.node_path_off.data_ptr(),
-                           self.node_path_len.data_ptr(),
-                           self.node_parent.data_ptr(),
-                           self.path_arena.data_ptr(), self.path_cap,
-                           self.slab_cap, self.counters.data_ptr(), st,
-                           self.free_list.data_ptr(), self.cap,
-                           self.cver.data_ptr(), self.nchild.data_ptr(),
-                           self.pzxid.data_ptr(), self.dirty.data_ptr(),
-                           self.dirty_list.data_ptr(),
-                           self.node_pw.data_ptr())
-
     @property
-    def struct(self):
-        return self._struct
+    def tensors(self):
+        """The descriptor list of the tree for torch.ops.zkmi."""
+        return self._tensors
 
     def expire(self, session, removed=None):
         """Delete every ephemeral node owned by ``session`` (server side of
@@ -209,9 +219,7 @@ class GpuTree(object):
         number of nodes removed."""
         if removed is None:
             removed = torch.zeros(1, dtype=I64, device=self.device)
-        _lib.check(_lib.lib().zk_tree_expire(
-            ctypes.byref(self._struct), session, self.cap, _lib.ptr(removed),
-            _lib.stream_ptr()), 'zk_tree_expire')
+        _lib.lib().tree_expire(self._tensors, session, self.cap, removed)
         return removed
 
     def rehash(self):
@@ -221,10 +229,7 @@ class GpuTree(object):
         n = int(self.counters[_lib.TC_NODES].item())
         self.ht.zero_()
         self.ht.view(-1, _lib.HT_WORDS)[:, 1] = -3
-        _lib.check(_lib.lib().zk_tree_build(ctypes.byref(self._struct), 0,
-                                            min(n, self.cap),
-                                            _lib.stream_ptr()),
-                   'zk_tree_build')
+        _lib.lib().tree_build(self._tensors, 0, min(n, self.cap))
 
     def find_host(self, path):
         """Node index of ``path`` (host scan of the path table; tests)."""
@@ -290,16 +295,12 @@ class GpuServer(object):
         rt = B.decode_requests(rx, ft, out=self.rt)
         r = self.resp
         r.count = ft.count
-        q = rt.struct()
-        _lib.check(L.zk_tree_serve(
-            ctypes.byref(self.tree.struct), _lib.ptr(rx), ctypes.byref(q),
-            _lib.ptr(ft.count), self.cap_frames, _lib.ptr(r.opcode),
-            _lib.ptr(r.xid), _lib.ptr(r.err), _lib.ptr(r.node),
-            _lib.ptr(r.zxid), _lib.ptr(r.path_off), _lib.ptr(r.path_len),
-            _lib.ptr(r.slot), _lib.ptr(self.presized[0]),
-            _lib.ptr(self.presized[1]),
-            session, int(time.time() * 1000), _lib.stream_ptr()),
-            'zk_tree_serve')
+        L.tree_serve(self.tree.tensors, rx, rt.tensors(), ft.count,
+                     self.cap_frames,
+                     [r.opcode, r.xid, r.err, r.node, r.zxid, r.path_off,
+                      r.path_len, r.slot, self.presized[0],
+                      self.presized[1]],
+                     session, int(time.time() * 1000))
         out, rec_off, total, err = B.encode_responses(
             r, self.tree.store, self.out.numel(), out=self.out,
             presized=self.presized, terminate=terminate)
@@ -393,14 +394,10 @@ class GetPipeline(object):
         t = self.tree
         n = self.batch
         L = _lib.lib()
-        sp = _lib.stream_ptr()
         seed = (self.seed * 0x9E3779B97F4A7C15 + self.step_no) & (2**64 - 1)
         self.step_no += 1
-        _lib.check(L.zk_bench_gen_get(
-            n, seed, t.leaf0, t.n_leaves, self.xid_base,
-            _lib.ptr(t.node_pw), _lib.ptr(self.idx), _lib.ptr(self.xid),
-            _lib.ptr(self.poff), _lib.ptr(self.plen), sp),
-            'zk_bench_gen_get')
+        L.bench_gen_get(n, _i64(seed), t.leaf0, t.n_leaves, self.xid_base,
+                        t.node_pw, self.idx, self.xid, self.poff, self.plen)
         xid = self.xid
         self.xid_base = (self.xid_base + n) & 0x7fffffff
         rb = B.RequestBatch(n, self.opcode, xid, self.arg, self.poff,
@@ -416,11 +413,7 @@ class GetPipeline(object):
         self.last = (self.idx, rep, rx, ft)
         if not validate:
             return
-        _lib.check(L.zk_bench_check_get(
-            n, _lib.ptr(rep.status), _lib.ptr(rep.err), _lib.ptr(rep.opcode),
-            _lib.ptr(rep.xid), _lib.ptr(rep.stat64[0]), _lib.ptr(rep.pay_len),
-            _lib.ptr(self.idx), _lib.ptr(xid), _lib.ptr(t.data_len),
-            _lib.ptr(acc), sp), 'zk_bench_check_get')
+        L.bench_check_get(n, rep.tensors(), self.idx, xid, t.data_len, acc)
 
 
 def _arena(strings, dev):
@@ -654,10 +647,8 @@ class GpuSessionTable(object):
         self.state = torch.zeros(cap, dtype=I32, device=dev)
         self.next = torch.zeros(1, dtype=I64, device=dev)
         self.allocated = 0              # host mirror of `next`
-        self._st = _lib.ZkSessionTable(
-            self.sid.data_ptr(), self.passwd.data_ptr(),
-            self.timeout.data_ptr(), self.state.data_ptr(),
-            self.next.data_ptr(), cap)
+        self._tensors = [self.sid, self.passwd, self.timeout, self.state,
+                         self.next]
         self.scanner = B.FrameScanner(64, dev, window=256)
         self.resp = torch.empty(64 * _lib.CR_RESP_BYTES, dtype=U8, device=dev)
         self.resp_sid = torch.empty(64, dtype=I64, device=dev)
@@ -672,21 +663,17 @@ class GpuSessionTable(object):
         bookkeeping of the allocation counter).  Returns (response stream
         [41 * frames], bound session ids, outcome codes)."""
         ft = self.scanner.scan(rx, nbytes)
-        _lib.check(_lib.lib().zk_session_connect(
-            _lib.ptr(rx), _lib.ptr(ft.off), _lib.ptr(ft.length),
-            _lib.ptr(ft.count), 64, ctypes.byref(self._st), self.server_id,
-            self.secret, self.MIN_TO, self.MAX_TO,
-            _lib.ptr(self.tree.counters[_lib.TC_ZXID:]), _lib.ptr(self.resp),
-            _lib.ptr(self.resp_sid), _lib.ptr(self.outcome),
-            _lib.stream_ptr()), 'zk_session_connect')
+        _lib.lib().session_connect(
+            rx, ft.off, ft.length, ft.count, 64, self._tensors,
+            self.server_id, _i64(self.secret), self.MIN_TO, self.MAX_TO,
+            self.tree.counters[_lib.TC_ZXID:], self.resp, self.resp_sid,
+            self.outcome)
         self.allocated += n_new
         return self.resp, self.resp_sid, self.outcome
 
     def close(self, sids):
         """Expire / close sessions (device int64 tensor of ids)."""
-        _lib.check(_lib.lib().zk_session_close(
-            ctypes.byref(self._st), _lib.ptr(sids), sids.numel(),
-            _lib.stream_ptr()), 'zk_session_close')
+        _lib.lib().session_close(self._tensors, sids)
 
 
 class StormPipeline(object):
@@ -752,7 +739,7 @@ class StormPipeline(object):
         self.last_zxid = torch.zeros(1, dtype=I64, device=dev)
         self.hs_ok = torch.ones(1, dtype=torch.bool, device=dev)
         self.cr_tx = torch.empty(256, dtype=U8, device=dev)
-        self.cr_ws = torch.empty(_lib.lib().zk_scan_workspace(2),
+        self.cr_ws = torch.empty(_lib.lib().scan_workspace(2),
                                  dtype=I64, device=dev)
         self.rscan = B.FrameScanner(4, dev, window=256)
         # K9 encode arguments per handshake shape (m requests, pwl bytes)
@@ -797,12 +784,8 @@ class StormPipeline(object):
             arena = self.zero_pw
         proto, tmo, pwo, pwlt, sizes, off, total = self.cr_args[(m, pwl)]
         zx = self.last_zxid.expand(m).contiguous()
-        _lib.check(L.zk_encode_connect_requests(
-            _lib.ptr(proto), _lib.ptr(zx), _lib.ptr(tmo), _lib.ptr(sid),
-            _lib.ptr(pwo), _lib.ptr(pwlt), _lib.ptr(arena), m,
-            _lib.ptr(sizes), _lib.ptr(off), _lib.ptr(total),
-            _lib.ptr(self.cr_ws), _lib.ptr(self.cr_tx), _lib.stream_ptr()),
-            'zk_encode_connect_requests')
+        L.encode_connect_requests(proto, zx, tmo, sid, pwo, pwlt, arena, m,
+                                  sizes, off, total, self.cr_ws, self.cr_tx)
         nbytes = m * (32 + pwl)
         resp, bound, outcome = self.sessions.connect(
             self.cr_tx[:nbytes], nbytes, 0 if resume else 1)
@@ -985,14 +968,10 @@ class WatchPipeline(object):
         t = self.tree
         n = self.n
         L = _lib.lib()
-        sp = _lib.stream_ptr()
         seeds = [self._seed(r) for r in range(self.world)]
         self.step_no += 1
-        _lib.check(L.zk_bench_gen_get(
-            n, seeds[self.rank], t.leaf0, t.n_leaves, 0,
-            _lib.ptr(t.node_pw), _lib.ptr(self.idx), _lib.ptr(self.xid),
-            _lib.ptr(self.poff), _lib.ptr(self.plen), sp),
-            'zk_bench_gen_get')
+        L.bench_gen_get(n, _i64(seeds[self.rank]), t.leaf0, t.n_leaves, 0,
+                        t.node_pw, self.idx, self.xid, self.poff, self.plen)
         _, _, total, err = B.encode_responses(self.resp, t.store,
                                               self.tx.numel(), out=self.tx)
         rx, nrx = self._gather(total)
@@ -1007,13 +986,9 @@ class WatchPipeline(object):
         self.seeds.copy_(torch.tensor(
             [s - (1 << 64) if s >= (1 << 63) else s for s in seeds],
             dtype=I64))
-        _lib.check(L.zk_bench_check_notif(
-            self.world * n, n, _lib.ptr(self.seeds), t.leaf0, t.n_leaves,
-            _lib.ptr(t.node_path_off), _lib.ptr(t.node_path_len),
-            _lib.ptr(t.path_arena), _lib.ptr(rx), _lib.ptr(rep.status),
-            _lib.ptr(rep.err), _lib.ptr(rep.opcode), _lib.ptr(rep.aux0),
-            _lib.ptr(rep.aux1), _lib.ptr(rep.pay_off), _lib.ptr(rep.pay_len),
-            _lib.ptr(acc), sp), 'zk_bench_check_notif')
+        L.bench_check_notif(self.world * n, n, self.seeds, t.leaf0,
+                            t.n_leaves, t.node_path_off, t.node_path_len,
+                            t.path_arena, rx, rep.tensors(), acc)
         return acc
 
     def diagnose(self):

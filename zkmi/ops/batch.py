@@ -21,7 +21,6 @@ import torch
 from .. import consts
 from .. import jute
 from . import _lib
-from ._lib import ptr, check, stream_ptr
 
 SENTINEL_XID = -(1 << 63)          # xid table entry that matches no xid
 I64 = torch.int64
@@ -72,11 +71,12 @@ class RequestBatch:
     acl_len: torch.Tensor
     acl_arena: torch.Tensor
 
-    def struct(self):
-        return _lib.ZkReqBatch(*[t.data_ptr() for t in (
-            self.opcode, self.xid, self.arg, self.path_off, self.path_len,
-            self.data_off, self.data_len, self.acl_id, self.path_arena,
-            self.data_arena, self.acl_off, self.acl_len, self.acl_arena)])
+    def tensors(self):
+        """The descriptor list torch.ops.zkmi takes (zk_batch.h order)."""
+        return [self.opcode, self.xid, self.arg, self.path_off,
+                self.path_len, self.data_off, self.data_len, self.acl_id,
+                self.path_arena, self.data_arena, self.acl_off, self.acl_len,
+                self.acl_arena]
 
 
 def _acl_bytes(acl):
@@ -171,7 +171,7 @@ def encode_requests(batch, xid_table=None, out=None, stream=None,
     sizes = torch.empty(max(n, 1), dtype=I64, device=dev)
     rec_off = torch.empty(max(n, 1), dtype=I64, device=dev)
     total, err = _total_err(dev)
-    ws = torch.empty(L.zk_scan_workspace(max(n, 1)), dtype=I64, device=dev)
+    ws = torch.empty(L.scan_workspace(max(n, 1)), dtype=I64, device=dev)
     if out is None:
         # Upper bound: 4+8 header, 4+path, 4+data, acl, 8 ints.
         ub = int(n * 40 + batch.path_arena.numel() + batch.data_arena.numel()
@@ -179,19 +179,17 @@ def encode_requests(batch, xid_table=None, out=None, stream=None,
         out = torch.empty(max(ub, 16), dtype=U8, device=dev)
     tab = xid_table.tab if xid_table is not None else None
     mask = xid_table.mask if xid_table is not None else 0
-    s = batch.struct()
-    check(L.zk_encode_requests2(ctypes_ref(s), n, ptr(sizes), ptr(rec_off),
-                                ptr(total), ptr(ws), ptr(out), out.numel(),
-                                ptr(tab), mask, ptr(err),
-                                1 if terminate else 0, stream_ptr(stream)),
-          'zk_encode_requests')
-    batch._keep = (s, sizes, ws, err)
+    with _on(stream):
+        L.encode_requests(batch.tensors(), n, sizes, rec_off, total, ws, out,
+                          tab, mask, err, bool(terminate))
     return out, rec_off[:n], total, err
 
 
-def ctypes_ref(s):
-    import ctypes
-    return ctypes.byref(s)
+def _on(stream):
+    """Context running the ops on ``stream`` (None: the current one)."""
+    import contextlib
+    return torch.cuda.stream(stream) if stream is not None else \
+        contextlib.nullcontext()
 
 
 def encode_set_watches(rel_zxid, data_paths, exist_paths, child_paths,
@@ -216,16 +214,14 @@ def encode_set_watches(rel_zxid, data_paths, exist_paths, child_paths,
     sizes = torch.empty(max(n, 1), dtype=I64, device=dev)
     off = torch.zeros(max(n, 1), dtype=I64, device=dev)
     total = torch.zeros(1, dtype=I64, device=dev)
-    ws = torch.empty(L.zk_scan_workspace(max(n, 1)), dtype=I64, device=dev)
+    ws = torch.empty(L.scan_workspace(max(n, 1)), dtype=I64, device=dev)
     cap = 64 + len(arena) + 4 * n
     out = torch.empty(cap, dtype=U8, device=dev)
     err = torch.zeros(1, dtype=I32, device=dev)
-    check(L.zk_encode_set_watches(ptr(t_poff), ptr(t_plen), ptr(t_ar), n,
-                                  len(data_paths), len(exist_paths),
-                                  rel_zxid, ptr(sizes), ptr(off), ptr(total),
-                                  ptr(ws), ptr(out), cap, ptr(err),
-                                  stream_ptr(stream)),
-          'zk_encode_set_watches')
+    with _on(stream):
+        L.encode_set_watches(t_poff, t_plen, t_ar, n, len(data_paths),
+                             len(exist_paths), rel_zxid, sizes, off, total,
+                             ws, out, err)
     frame_len = 32 + len(arena) + 4 * n
     return out[:frame_len]
 
@@ -258,14 +254,13 @@ def encode_connect_requests(reqs, device=None, stream=None):
     sizes = torch.empty(max(n, 1), dtype=I64, device=dev)
     off = torch.empty(max(n, 1), dtype=I64, device=dev)
     total = torch.zeros(1, dtype=I64, device=dev)
-    ws = torch.empty(L.zk_scan_workspace(max(n, 1)), dtype=I64, device=dev)
+    ws = torch.empty(L.scan_workspace(max(n, 1)), dtype=I64, device=dev)
     size = n * 32 + len(arena)           # frame len + 28 fixed + passwd
     cap = size + 16
     out = torch.empty(cap, dtype=U8, device=dev)
-    check(L.zk_encode_connect_requests(
-        ptr(proto), ptr(zx), ptr(tmo), ptr(sid), ptr(t_pwo), ptr(t_pwl),
-        ptr(t_ar), n, ptr(sizes), ptr(off), ptr(total), ptr(ws), ptr(out),
-        stream_ptr(stream)), 'zk_encode_connect_requests')
+    with _on(stream):
+        L.encode_connect_requests(proto, zx, tmo, sid, t_pwo, t_pwl, t_ar, n,
+                                  sizes, off, total, ws, out)
     return out[:size]
 
 
@@ -277,11 +272,11 @@ def decode_connect_responses(buf, frames, n, stream=None):
     e = lambda dt: torch.empty(max(n, 1), dtype=dt, device=dev)  # noqa
     o = {'protocolVersion': e(I32), 'timeOut': e(I32), 'sessionId': e(I64),
          'passwd_off': e(I64), 'passwd_len': e(I32), 'status': e(I32)}
-    check(L.zk_decode_connect_responses(
-        ptr(buf), ptr(frames.off), ptr(frames.length), n,
-        ptr(o['protocolVersion']), ptr(o['timeOut']), ptr(o['sessionId']),
-        ptr(o['passwd_off']), ptr(o['passwd_len']), ptr(o['status']),
-        stream_ptr(stream)), 'zk_decode_connect_responses')
+    with _on(stream):
+        L.decode_connect_responses(
+            buf, frames.off, frames.length, n, o['protocolVersion'],
+            o['timeOut'], o['sessionId'], o['passwd_off'], o['passwd_len'],
+            o['status'])
     return {k: v[:n] for k, v in o.items()}
 
 
@@ -361,28 +356,23 @@ class FrameScanner:
         n_dev, ncap = _scan_len(buf, n)
         if ncap > self.ws_for:
             cover = max(ncap, 2 * self.ws_for)
-            wsb = L.zk_frame_scan_workspace(cover)
+            wsb = L.frame_scan_workspace(cover)
             self.ws = torch.empty(max(wsb, 256), dtype=U8,
                                   device=buf.device)
             self.ws_for = cover
         t = self.table
-        check(L.zk_frame_scan3(ptr(buf), ptr(n_dev), ncap, self.max_packet,
-                               ptr(self.ws), self.ws.numel(), ptr(t.off),
-                               ptr(t.length), self.cap, ptr(t.result),
-                               int(self.window), stream_ptr(stream)),
-              'zk_frame_scan')
+        with _on(stream):
+            L.frame_scan(buf, n_dev, ncap, self.max_packet, self.ws, t.off,
+                         t.length, t.result, int(self.window))
         self.last_cap = ncap
         return t
 
     def chain_stats(self, stream=None):
         """K1 one-pass chain counters of the last scan (host sync): tiles
         without a speculated entry, tiles re-walked, repair rounds."""
-        import ctypes
-        L = _lib.lib()
-        out = (ctypes.c_uint32 * 3)()
-        check(L.zk_frame_scan_stats(ptr(self.ws), self.last_cap,
-                                    int(self.window), ctypes.byref(out),
-                                    stream_ptr(stream)), 'frame_scan_stats')
+        with _on(stream):
+            out = _lib.lib().frame_scan_stats(self.ws, self.last_cap,
+                                              int(self.window))
         return {'no_spec': out[0], 'rewalked': out[1], 'rounds': out[2]}
 
 
@@ -403,16 +393,15 @@ def frame_scan(buf, n=None, max_packet=consts.MAX_PACKET, cap=None,
     dev = buf.device
     if cap is None:
         cap = max(ncap // 4, 1)
-    wsb = L.zk_frame_scan_workspace(ncap)
+    wsb = L.frame_scan_workspace(ncap)
     if workspace is None or workspace.numel() < wsb:
         workspace = torch.empty(max(wsb, 256), dtype=U8, device=dev)
     off = torch.empty(cap, dtype=I64, device=dev)
     ln = torch.empty(cap, dtype=I32, device=dev)
     res = torch.empty(4, dtype=I64, device=dev)     # zeroed by the kernels
-    check(L.zk_frame_scan3(ptr(buf), ptr(n_dev), ncap, max_packet,
-                           ptr(workspace), workspace.numel(), ptr(off),
-                           ptr(ln), cap, ptr(res), int(window),
-                           stream_ptr(stream)), 'zk_frame_scan')
+    with _on(stream):
+        L.frame_scan(buf, n_dev, ncap, max_packet, workspace, off, ln, res,
+                     int(window))
     return FrameTable(off, ln, res)
 
 
@@ -439,11 +428,11 @@ class ReplyBatch:
     aux1: torch.Tensor
     count: torch.Tensor      # device int64 [1]
 
-    def struct(self):
-        return _lib.ZkReplyOut(*[t.data_ptr() for t in (
-            self.xid, self.err, self.opcode, self.status, self.zxid,
-            self.stat64, self.stat32, self.pay_off, self.pay_len, self.aux0,
-            self.aux1)], self.xid.numel())
+    def tensors(self):
+        """The reply table list torch.ops.zkmi takes (ZkReplyOut order)."""
+        return [self.xid, self.err, self.opcode, self.status, self.zxid,
+                self.stat64, self.stat32, self.pay_off, self.pay_len,
+                self.aux0, self.aux1]
 
 
 def alloc_replies(cap, device):
@@ -470,11 +459,9 @@ def decode_replies(buf, frames, xid_table, out=None, stream=None):
     if out is None:
         out = alloc_replies(cap, buf.device)
     out.count = frames.count
-    s = out.struct()
-    check(L.zk_decode_replies(ptr(buf), ptr(frames.off), ptr(frames.length),
-                              ptr(frames.count), cap, ptr(xid_table.tab),
-                              xid_table.mask, ctypes_ref(s),
-                              stream_ptr(stream)), 'zk_decode_replies')
+    with _on(stream):
+        L.decode_replies(buf, frames.off, frames.length, frames.count,
+                         xid_table.tab, xid_table.mask, out.tensors())
     return out
 
 
@@ -487,12 +474,11 @@ def exclusive_scan(x, stream=None):
     dev = x.device
     base = torch.empty(max(n, 1), dtype=I64, device=dev)
     total = torch.zeros(1, dtype=I64, device=dev)
-    ws = torch.empty(L.zk_scan_workspace(max(n, 1)), dtype=I64, device=dev)
-    fn = L.zk_scan_excl_i32 if x.dtype == torch.int32 else L.zk_scan_excl_i64
+    ws = torch.empty(L.scan_workspace(max(n, 1)), dtype=I64, device=dev)
     if x.dtype not in (torch.int32, torch.int64):
         raise TypeError('exclusive_scan: int32 or int64 input')
-    check(fn(ptr(x), ptr(base), n, ptr(total), ptr(ws), stream_ptr(stream)),
-          'zk_scan_excl')
+    with _on(stream):
+        L.scan_excl(x, base, total, ws)
     return base[:n], total
 
 
@@ -502,9 +488,9 @@ def _scan_i32(counts, stream=None):
     dev = counts.device
     base = torch.empty(max(n, 1), dtype=I64, device=dev)
     total = torch.zeros(1, dtype=I64, device=dev)
-    ws = torch.empty(L.zk_scan_workspace(max(n, 1)), dtype=I64, device=dev)
-    check(L.zk_scan_excl_i32(ptr(counts), ptr(base), n, ptr(total), ptr(ws),
-                             stream_ptr(stream)), 'zk_scan_excl_i32')
+    ws = torch.empty(L.scan_workspace(max(n, 1)), dtype=I64, device=dev)
+    with _on(stream):
+        L.scan_excl(counts, base, total, ws)
     return base, total
 
 
@@ -516,9 +502,8 @@ def expand_strings(buf, region, count, stream=None):
     m = int(total.item())
     soff = torch.empty(max(m, 1), dtype=I64, device=buf.device)
     slen = torch.empty(max(m, 1), dtype=I32, device=buf.device)
-    check(L.zk_expand_strings(ptr(buf), ptr(region), ptr(count), ptr(base),
-                              n, ptr(soff), ptr(slen), stream_ptr(stream)),
-          'zk_expand_strings')
+    with _on(stream):
+        L.expand_strings(buf, region, count, base[:n], soff, slen)
     return base[:n], soff[:m], slen[:m]
 
 
@@ -534,9 +519,8 @@ def expand_acl(buf, region, count, stream=None):
     sl = torch.empty(max(m, 1), dtype=I32, device=dev)
     io = torch.empty(max(m, 1), dtype=I64, device=dev)
     il = torch.empty(max(m, 1), dtype=I32, device=dev)
-    check(L.zk_expand_acl(ptr(buf), ptr(region), ptr(count), ptr(base), n,
-                          ptr(perms), ptr(so), ptr(sl), ptr(io), ptr(il),
-                          stream_ptr(stream)), 'zk_expand_acl')
+    with _on(stream):
+        L.expand_acl(buf, region, count, base[:n], perms, so, sl, io, il)
     return base[:n], perms[:m], so[:m], sl[:m], io[:m], il[:m]
 
 
@@ -559,11 +543,11 @@ class RequestTable:
     rel_zxid: torch.Tensor
     count: torch.Tensor
 
-    def struct(self):
-        return _lib.ZkReqOut(*[t.data_ptr() for t in (
-            self.xid, self.opcode, self.status, self.path_off,
-            self.path_len, self.data_off, self.data_len, self.arg,
-            self.vec_off, self.vec_count, self.rel_zxid)], self.xid.numel())
+    def tensors(self):
+        """The request table list torch.ops.zkmi takes (ZkReqOut order)."""
+        return [self.xid, self.opcode, self.status, self.path_off,
+                self.path_len, self.data_off, self.data_len, self.arg,
+                self.vec_off, self.vec_count, self.rel_zxid]
 
 
 def alloc_request_table(cap, device):
@@ -580,10 +564,9 @@ def decode_requests(buf, frames, out=None, stream=None):
     if out is None:
         out = alloc_request_table(cap, buf.device)
     out.count = frames.count
-    s = out.struct()
-    check(L.zk_decode_requests(ptr(buf), ptr(frames.off), ptr(frames.length),
-                               ptr(frames.count), cap, ctypes_ref(s),
-                               stream_ptr(stream)), 'zk_decode_requests')
+    with _on(stream):
+        L.decode_requests(buf, frames.off, frames.length, frames.count,
+                          out.tensors())
     return out
 
 
@@ -601,11 +584,11 @@ class ResponseBatch:
     count: torch.Tensor
     slot: torch.Tensor = None   # slot offsets (from the tree lookup) or None
 
-    def struct(self):
-        return _lib.ZkRespBatch(*[t.data_ptr() for t in (
-            self.opcode, self.xid, self.err, self.node, self.zxid,
-            self.path_off, self.path_len, self.path_arena, self.aux)],
-            self.slot.data_ptr() if self.slot is not None else None)
+    def tensors(self):
+        """The reply descriptor list torch.ops.zkmi takes (ZkRespBatch
+        order; ``slot`` goes separately, it is optional)."""
+        return [self.opcode, self.xid, self.err, self.node, self.zxid,
+                self.path_off, self.path_len, self.path_arena, self.aux]
 
 
 def response_workspace(cap, device):
@@ -613,12 +596,14 @@ def response_workspace(cap, device):
     :func:`encode_responses` (zk_tree_serve writes both)."""
     L = _lib.lib()
     return (torch.empty(cap, dtype=I64, device=device),
-            torch.empty(L.zk_scan_workspace(cap), dtype=I64, device=device))
+            torch.empty(L.scan_workspace(cap), dtype=I64, device=device))
 
 
-def encode_responses(resp, store_struct, out_cap, out=None, stream=None,
+def encode_responses(resp, store, out_cap, out=None, stream=None,
                      presized=None, terminate=False):
     """K13: server-mode reply encode -> (bytes, rec_off, total, err).
+    ``store``: the node store's tensors [slab, slot_off, data_len,
+    slot_cap] (:attr:`zkmi.bench.synthetic.GpuTree.store`).
     ``presized``: the (sizes, workspace) pair of :func:`response_workspace`
     already filled by the producer; the sizes pass is then skipped."""
     L = _lib.lib()
@@ -628,19 +613,15 @@ def encode_responses(resp, store_struct, out_cap, out=None, stream=None,
         sizes, ws = presized
     else:
         sizes = torch.empty(cap, dtype=I64, device=dev)
-        ws = torch.empty(L.zk_scan_workspace(cap), dtype=I64, device=dev)
+        ws = torch.empty(L.scan_workspace(cap), dtype=I64, device=dev)
     rec_off = torch.empty(cap, dtype=I64, device=dev)
     total, err = _total_err(dev)
     if out is None:
         out = torch.empty(out_cap, dtype=U8, device=dev)
-    s = resp.struct()
-    check(L.zk_encode_responses2(ctypes_ref(s), ctypes_ref(store_struct),
-                                 ptr(resp.count), cap, ptr(sizes),
-                                 ptr(rec_off), ptr(total), ptr(ws), ptr(out),
-                                 out.numel(), ptr(err),
-                                 1 if presized is not None else 0,
-                                 1 if terminate else 0, stream_ptr(stream)),
-          'zk_encode_responses')
+    with _on(stream):
+        L.encode_responses(resp.tensors(), resp.slot, list(store), resp.count,
+                           cap, sizes, rec_off, total, ws, out, err,
+                           presized is not None, bool(terminate))
     return out, rec_off, total, err
 
 

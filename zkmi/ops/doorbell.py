@@ -37,17 +37,24 @@ _SIGS = {
 }
 
 _live = weakref.WeakSet()
+_L = None
 
 
 def _lib_db():
-    L = _lib.lib()
-    if not getattr(L, '_zk_db_bound', False):
+    """The doorbell's control functions in libzkmi_hip.so.  Unlike the
+    batch codec (torch.ops.zkmi) they move no tensors: an opaque handle to
+    host-coherent slot memory and per-record host buffers, so they are
+    bound directly."""
+    global _L
+    if _L is None:
+        _lib.lib()                    # torch + the op library (and HIP) first
+        L = ctypes.CDLL(_lib.HIP_LIB_PATH)
         for name, (res, args) in _SIGS.items():
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args
-        L._zk_db_bound = True
-    return L
+        _L = L
+    return _L
 
 
 @atexit.register

@@ -33,6 +33,7 @@ import torch.distributed as dist
 from .. import consts
 from ..ops import _lib
 from ..ops import batch as B
+from ..bench.synthetic import _i64
 
 I64, I32, U8 = torch.int64, torch.int32, torch.uint8
 
@@ -65,7 +66,7 @@ class ShardedGetPipeline(object):
         self.owner = e32()
         self.counts = torch.empty(W, dtype=I64, device=dev)
         L = _lib.lib()
-        self.rws = torch.empty(L.zk_route_workspace(n, W), dtype=I64,
+        self.rws = torch.empty(L.route_workspace(n, W), dtype=I64,
                                device=dev)
         self.opcode = torch.full((n,), consts.OP_CODES['GET_DATA'],
                                  dtype=I32, device=dev)
@@ -126,23 +127,17 @@ class ShardedGetPipeline(object):
         n = self.batch
         W = self.world
         L = _lib.lib()
-        sp = _lib.stream_ptr()
         if validate and acc is None:
             acc = torch.zeros(1, dtype=I64, device=self.dev)
         seed = ((self.rank + 1) * 0x9E3779B97F4A7C15 + self.seed * 7919 +
                 self.step_no) & (2**64 - 1)
         self.step_no += 1
-        _lib.check(L.zk_bench_gen_get(
-            n, seed, t.leaf0, t.n_leaves, self.xid_base,
-            _lib.ptr(t.node_pw), _lib.ptr(self.idx), _lib.ptr(self.xid),
-            _lib.ptr(self.poff), _lib.ptr(self.plen), sp), 'zk_bench_gen_get')
+        L.bench_gen_get(n, _i64(seed), t.leaf0, t.n_leaves, self.xid_base,
+                        t.node_pw, self.idx, self.xid, self.poff, self.plen)
         self.xid_base = (self.xid_base + n) & 0x7fffffff
-        P = _lib.ptr
-        _lib.check(L.zk_route_requests(
-            n, W, P(self.poff), P(self.plen), P(t.path_arena), P(self.idx),
-            P(self.xid), P(self.owner), P(self.idx_s), P(self.xid_s),
-            P(self.poff_s), P(self.plen_s), P(self.counts), P(self.rws), sp),
-            'zk_route_requests')
+        L.route_requests(n, W, self.poff, self.plen, t.path_arena, self.idx,
+                         self.xid, self.owner, self.idx_s, self.xid_s,
+                         self.poff_s, self.plen_s, self.counts, self.rws)
         rb = B.RequestBatch(n, self.opcode, self.xid_s, self.zero32,
                             self.poff_s, self.plen_s, self.zero64,
                             self.zero32, self.zero32, t.path_arena, t.slab,
@@ -187,8 +182,6 @@ class ShardedGetPipeline(object):
         self.last = (rep, crx, ft)
         if not validate:
             return None
-        _lib.check(L.zk_bench_check_get(
-            n, P(rep.status), P(rep.err), P(rep.opcode), P(rep.xid),
-            P(rep.stat64[0]), P(rep.pay_len), P(self.idx_s), P(self.xid_s),
-            P(t.data_len), P(acc), sp), 'zk_bench_check_get')
+        L.bench_check_get(n, rep.tensors(), self.idx_s, self.xid_s,
+                          t.data_len, acc)
         return acc

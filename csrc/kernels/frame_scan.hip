@@ -20,14 +20,24 @@
 //               one walker — the survivor — is left;
 //            2. the survivor walks to the tile end, recording its frame
 //               starts (LDS, one hop = one LDS round trip);
-//            3. the survivor's exit is published as the tile's speculated
-//               exit X[t]; X[t-1] (a one-step wait: that tile's wave started
-//               earlier and does the same work) is this tile's entry;
+//            3. every exit a walker took into the next tile's window is
+//               published as one of that tile's entry candidates (a bit
+//               map); the true chain's exit is always among them when
+//               frames are <= W.  The tile takes the candidates of the tile
+//               before (a one-step wait: that wave started earlier and does
+//               the same work) and walks each in LDS: a garbage chain of
+//               the tile before, read on here, dies on a bad length within
+//               a few hops; the first candidate whose chain survives the
+//               tile is the entry.  (Round 2 first published only the last
+//               surviving walker's exit: on structured replies of a few
+//               hundred bytes a slow garbage crawler outlived the true
+//               chain in ~20 % of the tiles, and every such tile cost a
+//               serial repair.)
 //            4. from the entry, a short walk (usually 1-5 frames) until the
 //               chain meets the survivor's recorded path (merge-walk against
 //               the sorted list), the tile end or a terminal.
 //            The entry is exact unless a frame longer than the window ends
-//            in the tile before or that tile's survivor was not its chain.
+//            in the tile before or two candidates' chains both survive.
 //  fs_link   one workgroup checks every link in parallel (tile k's entry
 //            must be tile k-1's exit), re-walks the tiles after a broken
 //            link from the exact exit (serial, rare: frames longer than the
@@ -105,11 +115,13 @@ ZK_DEV int32_t lds_be32(const uint8_t* sb, int32_t p) {
   return (int32_t)bswap32(__builtin_amdgcn_alignbyte(hi, lo, p & 3));
 }
 
-// ---- LDS layout of fs_tile<W> (5.1 KiB per wave) ----------------------------
+// ---- LDS layout of fs_tile<W> (5.4 KiB per wave) ----------------------------
 // tile [FT_STAGE] | claimed bits [FT_S/32] | survivor bits [FT_S/32] |
-// compaction scratch [64] (uint16)
+// compaction scratch [64] (uint16) | exit candidate bits [FT_XW]
 constexpr int FT_BITS = FT_S / 32;         // uint32 words per position map
-constexpr int FT_LDS = FT_STAGE + 2 * FT_BITS * 4 + 64 * 2;
+constexpr int FT_XW = 2048 / 32;           // exit candidates: the next tile's
+                                           // window positions (W <= 2048)
+constexpr int FT_LDS = FT_STAGE + 2 * FT_BITS * 4 + 64 * 2 + FT_XW * 4;
 
 // One hop from tile-relative p (< FT_S).  Returns 0 and q (in-tile
 // successor), 1 for a terminal (the chain ends in the tile), or 2 and the
@@ -191,6 +203,37 @@ ZK_DEV void ft_record(uint16_t* L, int32_t& m, uint32_t& ent, int32_t c,
   if ((m & 63) == 0) L[m - 64 + lane] = (uint16_t)ent;
 }
 
+// Mark a walker's exit x (offset into the next tile) as an entry candidate
+// of that tile; exits past the window cannot be the chain's (frames <= W).
+ZK_DEV bool ft_mark_exit(uint32_t* xbits, int32_t x, int W) {
+  if (x < 0 || x >= W) return false;
+  __hip_atomic_fetch_or(&xbits[x >> 5], 1u << (x & 31), __ATOMIC_RELAXED,
+                        __HIP_MEMORY_SCOPE_WAVEFRONT);
+  return true;
+}
+
+// Does the chain from tile-relative e survive this tile?  It walks (wave-
+// uniform, in LDS) until it leaves the tile or the stream (yes), meets the
+// survivor's path (yes unless the survivor ends on a bad length) or hits a
+// bad length (no).  A partial frame at the stream end counts as surviving
+// (it is the carry).
+ZK_DEV bool ft_alive(const uint8_t* sb, const uint32_t* sbits, int32_t e,
+                     int32_t nrel, int32_t maxp, int32_t m, int64_t send,
+                     int64_t n, int64_t ts) {
+  int32_t c = e;
+  for (;;) {
+    if (c >= FT_S || ts + c >= n) return true;
+    if (m > 0 && ((sbits[c >> 5] >> (c & 31)) & 1u))
+      return !((send & TERM) && (send & TBAD));
+    if (c + 4 > nrel) return true;
+    const int32_t len = __builtin_amdgcn_readfirstlane(lds_be32(sb, c));
+    if (len < 0 || len > maxp) return false;
+    const int32_t nx = c + 4 + len;
+    if (nx > nrel) return true;
+    c = nx;
+  }
+}
+
 template <int W>
 __global__ __launch_bounds__(256) void fs_tile(
     const uint8_t* __restrict__ buf, const int64_t* __restrict__ n_dev,
@@ -200,6 +243,7 @@ __global__ __launch_bounds__(256) void fs_tile(
     int64_t* __restrict__ rec_meta, int32_t* __restrict__ rcount,
     int64_t ntiles_cap, int64_t* __restrict__ dbg) {
   constexpr int K = W / 64;                 // window entries per lane
+  constexpr int XW = W / 32;                // candidate words used
   static_assert(W % 64 == 0 && K >= 1 && K <= 32, "window");
   // one tile per wave; a block's waves work independently (no barriers),
   // each in its own LDS slice
@@ -211,6 +255,7 @@ __global__ __launch_bounds__(256) void fs_tile(
   uint32_t* claimed = (uint32_t*)(smem + FT_STAGE);
   uint32_t* sbits = claimed + FT_BITS;       // survivor frame starts
   uint16_t* scratch = (uint16_t*)(sbits + FT_BITS);
+  uint32_t* xbits = (uint32_t*)(scratch + 64);    // exits into the next tile
   const int lane = threadIdx.x & 63;
   const int64_t n = stream_len(n_dev, n_cap);
   const int64_t ntiles = (n + FT_S - 1) / FT_S;
@@ -255,6 +300,7 @@ __global__ __launch_bounds__(256) void fs_tile(
     // window positions start claimed (each by its own walker)
     for (int k = lane; k < 2 * FT_BITS; k += 64)
       claimed[k] = k < W / 32 ? 0xFFFFFFFFu : 0u;
+    if (lane < FT_XW) xbits[lane] = 0u;
 #pragma unroll
     for (int j = 0; j < PER; ++j) *(uint4*)(sb + 16 * (lane + 64 * j)) = v[j];
     if (lane == 0) *(uint4*)(sb + FT_S) = pad;
@@ -265,8 +311,10 @@ __global__ __launch_bounds__(256) void fs_tile(
   // claims its landing position with one fetch-or; landing on a claimed
   // position means merging into that chain, so it stops.  A round is two
   // LDS round trips (length words, claim) for all K walkers at once.
-  // `lastx` remembers the latest tile exit taken (round << 16 | x): the
-  // speculated exit when no single survivor is left.
+  // Every walker that leaves the tile marks its exit in `xbits` when it
+  // lands inside the next tile's window: the candidate entries of the
+  // next tile.  With frames <= W the true chain's exit is always one of
+  // them (whichever walker carries the true chain leaves the tile there).
   int32_t p[K];
   uint32_t act = 0;
 #pragma unroll
@@ -274,6 +322,8 @@ __global__ __launch_bounds__(256) void fs_tile(
     p[k] = lane + 64 * k;
     act |= 1u << k;
   }
+  // `lastx` = (round << 16 | x) of the latest in-window exit the frontier
+  // took: the preferred candidate when the survivor does not leave
   uint32_t lastx = 0;
   int round = 1;
   int32_t live = W;
@@ -291,9 +341,8 @@ __global__ __launch_bounds__(256) void fs_tile(
       if (code[k] == 0 && ft_claim(claimed, q[k])) {
         p[k] = q[k];
       } else {
-        if (code[k] == 2)
-          lastx = max(lastx, ((uint32_t)round << 16) |
-                                 (uint32_t)min(q[k] - FT_S, 0xFFFF));
+        if (code[k] == 2 && ft_mark_exit(xbits, q[k] - FT_S, W))
+          lastx = max(lastx, ((uint32_t)round << 16) | (uint32_t)(q[k] - FT_S));
         act &= ~(1u << k);
       }
     }
@@ -333,9 +382,8 @@ __global__ __launch_bounds__(256) void fs_tile(
       if (code == 0 && ft_claim(claimed, q)) {
         mp = q;
       } else {
-        if (code == 2)
-          lastx = max(lastx, ((uint32_t)round << 16) |
-                                 (uint32_t)min(q - FT_S, 0xFFFF));
+        if (code == 2 && ft_mark_exit(xbits, q - FT_S, W))
+          lastx = max(lastx, ((uint32_t)round << 16) | (uint32_t)(q - FT_S));
         ma = false;
       }
     }
@@ -367,6 +415,7 @@ __global__ __launch_bounds__(256) void fs_tile(
       ft_record(L, m, ent, c, lane);
       if (nx >= FT_S) {
         send = ts + nx;
+        if (lane == 0) ft_mark_exit(xbits, nx - FT_S, W);
         break;
       }
       c = nx;
@@ -380,19 +429,45 @@ __global__ __launch_bounds__(256) void fs_tile(
                             __HIP_MEMORY_SCOPE_WAVEFRONT);
     }
   }
-  // speculated exit: the survivor's, else the latest exit the frontier took
-  int64_t cx = -1;
-  if (sm && !(send & TERM)) {
-    cx = send;
+  // ---- 3. publish this tile's exit candidates; take the tile before's -----
+  // preferred candidate: the survivor's exit, else the latest in-window
+  // exit of the frontier (-1: none)
+  int32_t px = -1;
+  if (sm && !(send & TERM) && send - tend < W) {
+    px = (int32_t)(send - tend);
   } else {
     uint32_t lx = lastx;
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1)
       lx = max(lx, (uint32_t)__shfl_xor((int)lx, d, 64));
-    if (lx != 0 && (lx & 0xFFFF) != 0xFFFF) cx = tend + (lx & 0xFFFF);
+    if (lx != 0) px = (int32_t)(lx & 0xFFFF);
   }
-  // ---- 3. publish X[t], take X[t-1] as the entry -------------------------
-  if (lane == 0) lb_store(&lbw[2 * t], (uint64_t)(cx + 2));   // 0 = not yet
+  // Candidates go out packed in ONE 64-bit word (a relaxed agent-scope
+  // store, like the single exit before: no fence, no L2 write-back on this
+  // multi-XCD part): bit 63 = ready, five 12-bit slots of offset + 1
+  // (0 = empty), slot 0 the preferred one, then up to four other in-window
+  // exits in offset order.
+  __builtin_amdgcn_wave_barrier();
+  uint64_t word = (uint64_t)1 << 63;
+  if (px >= 0) word |= (uint64_t)(px + 1);
+  {
+    uint32_t xw = lane < XW ? xbits[lane] : 0u;
+    if (px >= 0 && lane == (px >> 5)) xw &= ~(1u << (px & 31));
+    uint64_t any = __ballot(xw != 0);
+    int slot = 1;
+    while (any && slot < 5) {
+      const int wl = (int)__builtin_ctzll(any);
+      uint32_t bits = (uint32_t)__builtin_amdgcn_readlane((int)xw, wl);
+      while (bits && slot < 5) {
+        const int bit = (int)__builtin_ctz(bits);
+        bits &= bits - 1;
+        word |= (uint64_t)(wl * 32 + bit + 1) << (12 * slot);
+        ++slot;
+      }
+      any &= any - 1;
+    }
+  }
+  if (lane == 0) lb_store(&lbw[2 * t], word);    // 0 = not yet
   const int64_t t_1 = dbg ? wall_clock64() : 0;
   int64_t E = 0;
   bool none = false;
@@ -407,10 +482,7 @@ __global__ __launch_bounds__(256) void fs_tile(
     for (;;) {
       x = lb_load(&lbw[2 * (t - 1)]);
       if (x != 0) break;
-      if (wall_clock64() - t_w > FT_WAIT_TICKS) {
-        x = 1;                              // give up: no speculated entry
-        break;
-      }
+      if (wall_clock64() - t_w > FT_WAIT_TICKS) break;   // no speculation
       switch (nap) {                        // s_sleep takes an immediate
         case 0: __builtin_amdgcn_s_sleep(2); break;
         case 1: __builtin_amdgcn_s_sleep(4); break;
@@ -420,7 +492,27 @@ __global__ __launch_bounds__(256) void fs_tile(
       }
       ++nap;
     }
-    E = (int64_t)x - 2;
+    // Pick the entry among the candidates (the tile before's exits that
+    // land here).  A wrong one is a garbage chain of the tile before; read
+    // on in THIS tile it almost always dies on a bad length within a few
+    // hops, while the true chain lives on.  So the preferred candidate is
+    // walked first (LDS only, no recording) and taken if its chain
+    // survives the tile — meeting the survivor's path counts as surviving
+    // when the survivor does — else the next candidate, and so on.
+    E = -1;
+    int64_t first = -1;
+    for (int slot = 0; slot < 5; ++slot) {
+      const int32_t v = (int32_t)((x >> (12 * slot)) & 0xFFF);
+      if (v == 0) continue;
+      const int32_t e = v - 1;
+      if (ts + e >= n) continue;
+      if (first < 0) first = ts + e;
+      if (ft_alive(sb, sbits, e, nrel, maxp32, m, send, n, ts)) {
+        E = ts + e;
+        break;
+      }
+    }
+    if (E < 0) E = first;        // no live candidate: the first one
     none = E < 0;
   }
   const int64_t t_2 = dbg ? wall_clock64() : 0;
@@ -436,14 +528,20 @@ __global__ __launch_bounds__(256) void fs_tile(
       if (c >= n) { w.exit = n; break; }    // the stream ends cleanly
       const int32_t crel = (int32_t)(c - ts);
       if (m > 0 && ((sbits[crel >> 5] >> (crel & 31)) & 1u)) {
-        // joined: the rest is the survivor's list from this start on
-        const uint32_t wd = sbits[lane];
-        const int32_t below =
-            lane < (crel >> 5)
-                ? __popc(wd)
-                : (lane == (crel >> 5) ? __popc(wd & ((1u << (crel & 31)) - 1u))
-                                       : 0);
-        int32_t s = below;
+        // joined: the rest is the survivor's list from this start on; its
+        // index is the number of survivor starts below crel (the map has
+        // FT_BITS = 2 x 64 words, two per lane)
+        static_assert(FT_BITS == 2 * 64, "two map words per lane");
+        const int32_t cw = crel >> 5;
+        int32_t s = 0;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int32_t wi = lane + 64 * h;
+          const uint32_t wd = sbits[wi];
+          s += wi < cw ? __popc(wd)
+                       : (wi == cw ? __popc(wd & ((1u << (crel & 31)) - 1u))
+                                   : 0);
+        }
 #pragma unroll
         for (int d = 32; d >= 1; d >>= 1) s += __shfl_xor(s, d, 64);
         w.js = s;
@@ -576,7 +674,9 @@ __global__ __launch_bounds__(FL_T) void fs_link(
   for (;;) {
     // leftmost terminal, and leftmost broken link at or after `from`
     int64_t fb = INF, fterm = INF;
-    for (int64_t k = tid; k < ntiles; k += FL_T) {
+    // links before `from` hold (repaired), so terminals before from - 1
+    // were found in an earlier round: only the rest is scanned again
+    for (int64_t k = from - 1 + tid; k < ntiles; k += FL_T) {
       const int64_t mk = ld_agent(&rec_meta[k]);
       if (m_term(mk)) {
         fterm = min(fterm, k);

@@ -733,3 +733,25 @@ def test_gpu_watch_pipeline_two_ranks_gloo(gpu):
     assert all(p.exitcode == 0 for p in procs)
     got = dict(q.get(timeout=5) for _ in range(2))
     assert got == {0: 6000, 1: 6000}
+
+
+def test_gpu_get_pipeline_variable_sizes(gpu):
+    """GET over variable data (0..1024 bytes) and path lengths: every reply
+    checked on the device, and K1's frames of the reply stream equal the
+    host framer's.  (Structured reply bytes keep garbage chains alive deep
+    into K1's tiles; a join past the first 2 KiB of a tile once took the
+    wrong survivor index.)"""
+    from zkmi.bench.synthetic import GpuTree, GetPipeline
+    tree = GpuTree(100_000, 0, fanout=1000, device=gpu, data_dist=(0, 1024),
+                   name_pad=(0, 16))
+    pipe = GetPipeline(tree, 1 << 16)
+    for _ in range(3):
+        assert int(pipe.step().item()) == 1 << 16
+    idx, rep, rx, ft = pipe.last
+    n = 1 << 16
+    ro = pipe.server.last_rec_off[:n].cpu().numpy()
+    end = int(ro[-1]) + 4 + int(rep.pay_len[n - 1].item()) + 16 + 4 + 68
+    frames, cons, bad = jute.scan_frames(
+        bytes(rx[:end].cpu().numpy().tobytes()))
+    assert bad < 0 and cons == end and len(frames) == n
+    assert ft.off[:n].cpu().numpy().tolist() == [o for o, _ in frames]

@@ -652,16 +652,129 @@ ZK_DEV FcWalk fc_walk(const uint8_t* __restrict__ buf, int64_t n,
   return r;
 }
 
+// fs_link's parallel repair pass (all threads of the block call it).
+// Lists the broken links in order, groups them into runs of consecutive
+// tiles, and re-walks the runs in rounds, one wave per run: a run's wave
+// walks from the exit before its head until a link holds, a terminal, or
+// the next run's head.  Each tile is written by one wave per round.  An
+// exit that lies before the tile (-1 of a tile with no entry, a terminal's
+// position) is no entry: that run waits (the serial pass afterwards
+// settles whatever is left).  At most FL_ROUNDS rounds.
+constexpr int FL_ROUNDS = 8;
+ZK_DEV void fs_link_parallel(
+    const uint8_t* __restrict__ buf, int64_t n, int64_t ntiles, int64_t maxp,
+    const int64_t* __restrict__ sx, const uint16_t* __restrict__ list,
+    const int32_t* __restrict__ rcount, uint16_t* pre, int64_t* rec_entry,
+    int64_t* rec_exit, int64_t* rec_meta, int32_t* hbuf, int32_t* blist,
+    int64_t* red, int64_t* s_nh, uint8_t* win, uint64_t* stats) {
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int64_t INF = INT64_MAX;
+  // 1. broken links k (1 <= k < ntiles, tile k-1 not a terminal), in order
+  const int64_t pch = (ntiles + FL_T - 1) / FL_T;
+  const int64_t c0 = min((int64_t)tid * pch, ntiles);
+  const int64_t c1 = min(c0 + pch, ntiles);
+  int64_t nb = 0;
+  for (int64_t k = max(c0, (int64_t)1); k < c1; ++k) {
+    if (m_term(ld_agent(&rec_meta[k - 1]))) continue;
+    const int64_t e = ld_agent(&rec_entry[k]);
+    nb += e < 0 || e != ld_agent(&rec_exit[k - 1]);
+  }
+  int64_t nb_tot;
+  int64_t ob = block_excl_scan(nb, red, &nb_tot);
+  for (int64_t k = max(c0, (int64_t)1); k < c1; ++k) {
+    if (m_term(ld_agent(&rec_meta[k - 1]))) continue;
+    const int64_t e = ld_agent(&rec_entry[k]);
+    if (e < 0 || e != ld_agent(&rec_exit[k - 1])) blist[ob++] = (int32_t)k;
+  }
+  __threadfence_block();
+  __syncthreads();
+  // 2. run heads: broken links whose predecessor link is not broken
+  int32_t* hcur = hbuf;
+  int32_t* hnxt = blist;
+  {
+    const int64_t per = (nb_tot + FL_T - 1) / FL_T;
+    const int64_t q0 = min((int64_t)tid * per, nb_tot);
+    const int64_t q1 = min(q0 + per, nb_tot);
+    int64_t nh = 0;
+    for (int64_t i = q0; i < q1; ++i)
+      nh += i == 0 || blist[i - 1] != blist[i] - 1;
+    int64_t nh_tot;
+    int64_t oh = block_excl_scan(nh, red, &nh_tot);
+    for (int64_t i = q0; i < q1; ++i)
+      if (i == 0 || blist[i - 1] != blist[i] - 1) hcur[oh++] = blist[i];
+    if (tid == 0) *s_nh = nh_tot;
+  }
+  __threadfence_block();
+  __syncthreads();
+  uint8_t* mywin = win + (size_t)wv * (FC_WIN + 16);
+  uint32_t walked = 0;
+  for (int round = 0; round < FL_ROUNDS; ++round) {
+    const int64_t nh = *s_nh;
+    if (nh <= 0) break;
+    for (int64_t j = wv; j < nh; j += FL_T / 64) {
+      const int64_t h = hcur[j];
+      const int64_t hnext = j + 1 < nh ? (int64_t)hcur[j + 1] : INF;
+      int64_t k = h;
+      while (k >= 1 && k < ntiles && k < hnext) {
+        const int64_t E = ld_agent(&rec_exit[k - 1]);
+        if (E < k * FT_S) break;             // no entry yet
+        const int32_t m0 = __builtin_amdgcn_readfirstlane(rcount[k]);
+        const FcWalk w = fc_walk(buf, n, maxp, k * FT_S, E,
+                                 list + k * FT_LMAX, m0, sx[k], mywin,
+                                 pre + k * FT_LMAX, lane);
+        ++walked;
+        if (lane == 0) {
+          st_agent(&rec_entry[k], E);
+          st_agent(&rec_exit[k], w.exit);
+          st_agent(&rec_meta[k], fc_meta(w));
+        }
+        if (w.term) break;
+        ++k;
+        if (k < ntiles && ld_agent(&rec_entry[k]) == w.exit) break;
+      }
+    }
+    __threadfence();
+    __syncthreads();
+    // heads whose link is still broken (an earlier run moved their exit)
+    const int64_t per = (nh + FL_T - 1) / FL_T;
+    const int64_t q0 = min((int64_t)tid * per, nh);
+    const int64_t q1 = min(q0 + per, nh);
+    int64_t nl = 0;
+    for (int64_t i = q0; i < q1; ++i) {
+      const int64_t h = hcur[i];
+      nl += !m_term(ld_agent(&rec_meta[h - 1])) &&
+            ld_agent(&rec_entry[h]) != ld_agent(&rec_exit[h - 1]);
+    }
+    int64_t nn;
+    int64_t on = block_excl_scan(nl, red, &nn);
+    for (int64_t i = q0; i < q1; ++i) {
+      const int64_t h = hcur[i];
+      if (!m_term(ld_agent(&rec_meta[h - 1])) &&
+          ld_agent(&rec_entry[h]) != ld_agent(&rec_exit[h - 1]))
+        hnxt[on++] = (int32_t)h;
+    }
+    __threadfence_block();
+    __syncthreads();
+    if (tid == 0) *s_nh = nn;
+    int32_t* tmp = hcur;
+    hcur = hnxt;
+    hnxt = tmp;
+    __syncthreads();
+  }
+  if (lane == 0 && walked) fc_stat(stats, 2, walked);
+}
+
 __global__ __launch_bounds__(FL_T) void fs_link(
     const uint8_t* __restrict__ buf, const int64_t* __restrict__ n_dev,
     int64_t n_cap, int64_t maxp, const int64_t* __restrict__ sx,
     const uint16_t* __restrict__ list, const int32_t* __restrict__ rcount,
     uint16_t* pre, int64_t* rec_entry, int64_t* rec_exit, int64_t* rec_meta,
     int64_t* __restrict__ base, int64_t cap, int64_t* __restrict__ result,
-    uint64_t* stats) {
-  __shared__ __attribute__((aligned(16))) uint8_t win[FC_WIN + 16];
+    uint64_t* stats, int32_t* __restrict__ blist) {
+  __shared__ __attribute__((aligned(16)))
+      uint8_t win[(FL_T / 64) * (FC_WIN + 16)];      // one per wave
   __shared__ int64_t red[2 * (FL_T / 64) + 2];
-  __shared__ int64_t s_next;
+  __shared__ int64_t s_next, s_nh;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int64_t n = stream_len(n_dev, n_cap);
   const int64_t ntiles = (n + FT_S - 1) / FT_S;
@@ -671,6 +784,7 @@ __global__ __launch_bounds__(FL_T) void fs_link(
   }
   const int64_t INF = INT64_MAX;
   int64_t from = 1, ft = INF;
+  bool accel = true;
   for (;;) {
     // leftmost terminal, and leftmost broken link at or after `from`
     int64_t fb = INF, fterm = INF;
@@ -701,6 +815,20 @@ __global__ __launch_bounds__(FL_T) void fs_link(
     if (fb == INF || fb > fterm) {          // every live link holds
       ft = fterm;
       break;
+    }
+    if (accel) {
+      // The first broken link: before the serial repairs, re-walk every
+      // RUN of broken links in parallel (one wave per run) — usually all
+      // of them.  A garbage entry of the tile before typically merges into
+      // the true chain inside the tile, so a repair rarely moves a tile's
+      // exit and the runs are independent.  Best effort only: the serial
+      // loop re-checks every link afterwards and repairs what is left.
+      accel = false;
+      fs_link_parallel(buf, n, ntiles, maxp, sx, list, rcount, pre,
+                       rec_entry, rec_exit, rec_meta, (int32_t*)base, blist,
+                       red, &s_nh, win, stats);
+      __syncthreads();
+      continue;
     }
     // repair: re-walk tiles from fb while their links stay broken
     if (wv == 0) {
@@ -789,7 +917,7 @@ __global__ __launch_bounds__(256) void fs_rows(
 struct FsPlan {
   int64_t tiles;
   size_t off_list, off_pre, off_sx, off_lbw, off_rent, off_rexit, off_rmeta,
-      off_rcnt, off_base, total;
+      off_rcnt, off_base, off_blist, total;
 };
 
 static FsPlan fs_plan(int64_t n) {
@@ -807,6 +935,7 @@ static FsPlan fs_plan(int64_t n) {
   p.off_rmeta = take((size_t)tiles * 8);
   p.off_rcnt = take((size_t)tiles * 4);
   p.off_base = take((size_t)tiles * 8);
+  p.off_blist = take((size_t)tiles * 4);
   p.total = o;
   return p;
 }
@@ -880,6 +1009,7 @@ int zk_frame_scan3(const uint8_t* buf, const int64_t* n_dev, int64_t n_cap,
   int64_t* rmeta = (int64_t*)(ws + p.off_rmeta);
   int32_t* rcnt = (int32_t*)(ws + p.off_rcnt);
   int64_t* base = (int64_t*)(ws + p.off_base);
+  int32_t* blist = (int32_t*)(ws + p.off_blist);
   // X flags, the tile counter and the stats start at zero
   if (hipMemsetAsync(lbw, 0, (size_t)(2 * tiles + 4) * 8, st) != hipSuccess)
     return -4;
@@ -906,7 +1036,7 @@ int zk_frame_scan3(const uint8_t* buf, const int64_t* n_dev, int64_t n_cap,
   ZK_LAUNCH_CHECK();
   fs_link<<<1, FL_T, 0, st>>>(buf, n_dev, n_cap, maxp, sx, list, rcnt, pre,
                               rent, rexit, rmeta, base, cap, result,
-                              lbw + 2 * tiles);
+                              lbw + 2 * tiles, blist);
   ZK_LAUNCH_CHECK();
   fs_rows<<<(unsigned)((tiles + 3) / 4), 256, 0, st>>>(
       buf, n_dev, n_cap, list, pre, rmeta, base, foff, flen, cap);

@@ -9,7 +9,9 @@ encode on the same 1M-znode tree), ``--workload storm`` configs[4]
 (EPHEMERAL|SEQUENTIAL create storm with per-step session expiry) and
 ``--workload watch`` the watch fan-out of configs[3] (every rank's
 notifications all-gathered over RCCL and decoded by every rank; the value
-counts node-wide deliveries).
+counts node-wide deliveries).  ``--workload chain`` pipelines
+create -> set -> get -> delete of each path inside ONE batch (in-batch
+ordering of the GPU server, 4 ordered passes).
 One step = one batch
 of ``--batch`` GET_DATA requests per GPU pushed through the full ZooKeeper
 wire path on the GPU (see zkmi/bench/synthetic.py): client request encode
@@ -257,7 +259,7 @@ def main():
                          'streams than GPU_MAX_HW_QUEUES allows were '
                          'unstable)')
     ap.add_argument('--workload', choices=('get', 'mix', 'storm', 'watch',
-                                           'ensemble'),
+                                           'ensemble', 'chain'),
                     default='get')
     ap.add_argument('--sharded', action='store_true',
                     help='get: one tree sharded by path hash over the '
@@ -330,10 +332,17 @@ def main():
         # room for the write working set next to the 1M static nodes: the
         # mix keeps 3 generations of batch/3 nodes, the storm up to 3
         # batches (the expiring session's two, the new session's first)
-        spare = (a.batch * (1 if a.workload == 'mix' else 3) + 8192) / a.nodes
+        spare = (a.batch * (1 if a.workload in ('mix', 'chain') else 3) +
+                 8192) / a.nodes
+        # chain: the set and get of every chain reply from a snapshot
+        scratch = (a.batch // 2 + 64) * (80 + ((a.data_bytes + 15) & ~15)) \
+            if a.workload == 'chain' else 0
         tree = S.GpuTree(a.nodes, a.data_bytes, device=dev, seed=rank,
-                         spare=spare + 0.05)
-        if a.workload == 'mix':
+                         spare=spare + 0.05, scratch=scratch)
+        if a.workload == 'chain':
+            pipe = S.ChainPipeline(tree, a.batch, a.data_bytes, seed=rank)
+            per_step = pipe.n
+        elif a.workload == 'mix':
             pipe = S.MixPipeline(tree, a.batch, a.data_bytes, seed=rank)
             per_step = pipe.n
         else:

@@ -30,9 +30,12 @@
 // serve and expire kernels keep every thread alive to the end (out-of-range
 // threads carry a no-op).
 //
-// Requests are applied concurrently within a batch; conflicting operations
-// on the same path inside ONE batch are unordered (the benchmark generators
-// never emit them).  Version CAS is an atomicCAS on the slot's big-endian
+// Requests are applied concurrently within a batch, except that requests
+// on ONE path are applied in batch (xid) order when any of them writes:
+// tree_order_* rank every request by the number of earlier same-path
+// requests of the batch and the serve kernel runs in passes of equal rank
+// (ZooKeeper applies a session's requests in order; requests on different
+// paths commute).  Version CAS is an atomicCAS on the slot's big-endian
 // version word, so exactly one of several same-version SET_DATAs wins (the
 // others get BAD_VERSION), matching ZooKeeper's conditional set.  Every
 // write request is assigned a zxid, failed ones included (ZooKeeper logs an
@@ -72,6 +75,9 @@ enum : int {
   TC_DONE = 8, TC_N = 9
 };
 constexpr int64_t NODE_FREE = -2;
+
+// ordered serve: rank byte = min(rank, ORD_RANK) | ORD_SNAP
+constexpr int32_t ORD_RANK = 0x7f, ORD_SNAP = 0x80;
 
 ZK_DEV int64_t slot_bytes(int32_t data_cap) {
   return ZK_SLOT_DATA + (((int64_t)data_cap + 15) & ~(int64_t)15) + 4;
@@ -225,7 +231,10 @@ ZK_DEV int64_t tree_find(const ZkTree& t, const uint8_t* p, int32_t n) {
 }
 
 // Insert node `v` (path already in the arena).  Returns the existing node if
-// the path is present (NODE_EXISTS), else v.
+// the path is present (NODE_EXISTS), else v; TREE_INSERT_TIMEOUT when a
+// concurrent claimer of the same key never published its value (the caller
+// answers SYSTEMERROR rather than probing on and indexing the path twice).
+constexpr int64_t TREE_INSERT_TIMEOUT = -4;
 ZK_DEV int64_t tree_insert(const ZkTree& t, int64_t v, const uint8_t* p,
                            int32_t n) {
   const int64_t key = (int64_t)(path_hash(p, n) | 1ull);
@@ -245,6 +254,7 @@ ZK_DEV int64_t tree_insert(const ZkTree& t, int64_t v, const uint8_t* p,
       for (int spin = 0; spin < 1000000 && w == -3; ++spin)
         w = __hip_atomic_load(ht_val(t, s), __ATOMIC_RELAXED,
                               __HIP_MEMORY_SCOPE_AGENT);
+      if (w == -3) return TREE_INSERT_TIMEOUT;
       if (w >= 0 && path_is(t, val_node(w), p, n)) return val_node(w);
       if (w == -2 &&                      // tombstone of the same key: reuse
           atomicCAS((unsigned long long*)ht_val(t, s), (unsigned long long)-2,
@@ -415,7 +425,9 @@ ZK_DEV int32_t do_create(const ZkTree& t, Lane& L, const uint8_t* data,
   // batch contract; every field it could read is in bounds), and the next
   // launch sees everything.  A __threadfence here is an XCD-L2 writeback
   // per wave (MI355X_MICROARCH.md: ~3.5 us each) and cost milliseconds.
-  if (tree_insert(t, v, pd, npl) != v) return ERR_NODE_EXISTS;
+  const int64_t ins = tree_insert(t, v, pd, npl);
+  if (ins == TREE_INSERT_TIMEOUT) return ERR_SYSTEM;
+  if (ins != v) return ERR_NODE_EXISTS;
   if (par >= 0) parent_touch(t, par, 1, !seq, L.zx);
   L.par = par;
   L.node = v;
@@ -437,15 +449,25 @@ __global__ __launch_bounds__(TR_T) void tree_serve_k(
     int64_t* __restrict__ r_node, int64_t* __restrict__ r_zxid,
     int64_t* __restrict__ r_path_off, int32_t* __restrict__ r_path_len,
     int64_t* __restrict__ r_slot, int64_t* __restrict__ r_sizes,
-    int64_t* __restrict__ r_bsum, int64_t session, int64_t now_ms) {
+    int64_t* __restrict__ r_bsum, int64_t session, int64_t now_ms,
+    const uint8_t* __restrict__ rank, int32_t pass, int32_t last_pass,
+    int64_t snap_base, int64_t snap_cap, int64_t* __restrict__ snap_top) {
   const uint32_t blk = xcd_remap(blockIdx.x, gridDim.x);
   const int64_t i = (int64_t)blk * TR_T + threadIdx.x;
-  const bool live = i < ncap && i < *n_dev;
-  const bool ok_req = live && q.status[i] == ST_OK;
+  const bool in_batch = i < ncap && i < *n_dev;
+  // ordered passes: this launch serves the requests of rank `pass`; the
+  // last pass also answers any of a higher rank, refused (SYSTEMERROR: more
+  // same-path requests than passes).  rank bit 7: a later request of the
+  // batch writes this path, so the reply's slot is snapshotted.
+  const int32_t rb = rank != nullptr && in_batch ? (int32_t)rank[i] : 0;
+  const int32_t rk = rb & ORD_RANK;
+  const bool live = in_batch && (rk == pass || (last_pass && rk > pass));
+  const bool refused = live && rk > pass;
+  const bool ok_req = live && !refused && q.status[i] == ST_OK;
   const ZkNodeStore& s = t.store;
   Lane L;
   L.op = live ? q.opcode[i] : OP_PING;
-  L.err = live && !ok_req ? ERR_BAD_ARGUMENTS : ERR_OK;
+  L.err = refused ? ERR_SYSTEM : (live && !ok_req ? ERR_BAD_ARGUMENTS : ERR_OK);
   L.node = -1;
   L.slot = -1;
   L.dlen = 0;
@@ -584,6 +606,26 @@ __global__ __launch_bounds__(TR_T) void tree_serve_k(
         L.err = ERR_UNIMPLEMENTED;
     }
   }
+  // ---- ordered snapshot: a reply that reads the node's slot (stat, data)
+  // while a later pass of this batch writes the node reads a private copy
+  // in the slab's scratch tail, taken now (wave-aggregated claim)
+  if (rank != nullptr) {
+    const bool snap = (rb & ORD_SNAP) && live && L.err == ERR_OK &&
+                      (L.op == OP_GET_DATA || L.op == OP_EXISTS ||
+                       L.op == OP_SET_DATA);
+    const int64_t dl = snap && L.op == OP_GET_DATA ? L.dlen : 0;
+    const int64_t sb = snap ? slot_bytes((int32_t)dl) : 0;
+    const int64_t so = wave_bytes(snap_top, sb);
+    if (snap) {
+      if (so + sb <= snap_cap) {
+        copy_bytes(s.slab + snap_base + so, s.slab + L.slot,
+                   (int32_t)(ZK_SLOT_DATA + dl));
+        L.slot = snap_base + so;
+      } else {
+        L.err = ERR_SYSTEM;              // scratch full (counted by caller)
+      }
+    }
+  }
   // ---- phase C: wave-aggregated frees and dirty parents -----------------
   if (create && L.err != ERR_OK && v >= 0) freed = v;  // return the claim
   // (A read-only block could skip these claims, but guarding them with a
@@ -598,8 +640,12 @@ __global__ __launch_bounds__(TR_T) void tree_serve_k(
       const bool mk = L.err == ERR_OK && L.op == OP_CREATE;
       sz = served_reply_size(L.op, L.err, get ? L.dlen : 0,
                              mk ? t.node_path_len[L.node] : 0);
+      r_sizes[i] = sz;
+    } else if (in_batch && rk < pass) {
+      sz = r_sizes[i];                  // served by an earlier pass
+    } else if (!in_batch && i < ncap) {
+      r_sizes[i] = 0;
     }
-    if (i < ncap) r_sizes[i] = sz;
     int64_t tot;
     block_excl_scan(sz, sm, &tot);
     if (threadIdx.x == 0) r_bsum[blk] = tot;
@@ -611,6 +657,107 @@ __global__ __launch_bounds__(TR_T) void tree_serve_k(
   r_node[i] = L.op == OP_DELETE ? -1 : L.node;
   r_zxid[i] = L.zx;
   if (r_slot != nullptr) r_slot[i] = L.op == OP_DELETE ? -1 : L.slot;
+}
+
+// ---- in-batch ordering (tree_order_*) ---------------------------------------
+// Requests on one path are ordered when a request of the batch writes the
+// path: rank[i] = number of earlier requests of the batch on i's path (0 for
+// paths only read).  A scratch hash table groups the batch's requests by
+// path hash (a 64-bit collision merges two groups: extra ordering, never
+// less); multi-request write groups get a member list, and each member
+// counts the members before it.  ws layout (OrderWs): key, cnt, wr, fill,
+// base, members, eidx, top / maxrank.
+struct OrderWs {
+  int64_t* key;      // [mask + 1]
+  int32_t* cnt;      // [mask + 1] requests on the path
+  int32_t* wr;       // [mask + 1] a request writes it
+  int32_t* fill;     // [mask + 1] member-list fill
+  int64_t* base;     // [mask + 1] member-list base
+  int32_t* members;  // [ncap]
+  int64_t* eidx;     // [ncap] request -> entry (-1: no path)
+  int64_t* ctr;      // [4] member-list top, max rank, scratch top, 0
+  int64_t mask;
+};
+
+ZK_DEV bool ord_has_path(int32_t op) {
+  return op == OP_CREATE || op == OP_DELETE || op == OP_SET_DATA ||
+         op == OP_GET_DATA || op == OP_EXISTS || op == OP_GET_CHILDREN ||
+         op == OP_GET_CHILDREN2 || op == OP_GET_ACL || op == OP_SYNC;
+}
+
+ZK_DEV bool ord_writes(int32_t op) {
+  return op == OP_CREATE || op == OP_DELETE || op == OP_SET_DATA;
+}
+
+__global__ __launch_bounds__(TR_T) void ord_insert_k(
+    const uint8_t* __restrict__ rx, ZkReqOut q,
+    const int64_t* __restrict__ n_dev, int64_t ncap, OrderWs w) {
+  const int64_t i = (int64_t)blockIdx.x * TR_T + threadIdx.x;
+  if (i >= ncap) return;
+  int64_t e = -1;
+  // SEQUENTIAL creates name a fresh node each: they conflict with nothing
+  // on the requested prefix
+  if (i < *n_dev && q.status[i] == ST_OK && ord_has_path(q.opcode[i]) &&
+      !(q.opcode[i] == OP_CREATE && (q.arg[i] & CF_SEQUENTIAL))) {
+    const int32_t op = q.opcode[i];
+    const int64_t key =
+        (int64_t)(path_hash(rx + q.path_off[i], q.path_len[i]) | 1ull);
+    int64_t sl = key & w.mask;
+    for (int64_t probe = 0; probe <= w.mask; ++probe) {
+      const int64_t k = (int64_t)atomicCAS((unsigned long long*)&w.key[sl],
+                                           0ull, (unsigned long long)key);
+      if (k == 0 || k == key) { e = sl; break; }
+      sl = (sl + 1) & w.mask;
+    }
+    if (e >= 0) {
+      atomicAdd(&w.cnt[e], 1);
+      if (ord_writes(op)) atomicOr(&w.wr[e], 1);
+    }
+  }
+  w.eidx[i] = e;
+}
+
+// member-list bases of the write groups with more than one request (one
+// atomic per wave on the list top)
+__global__ __launch_bounds__(TR_T) void ord_base_k(OrderWs w) {
+  const int64_t e = (int64_t)blockIdx.x * TR_T + threadIdx.x;
+  const bool grp = e <= w.mask && w.key[e] != 0 && w.wr[e] && w.cnt[e] > 1;
+  const int64_t b = wave_bytes(&w.ctr[0], grp ? w.cnt[e] : 0);
+  if (grp) w.base[e] = b;
+}
+
+ZK_DEV bool ord_grouped(const OrderWs& w, int64_t e) {
+  return e >= 0 && w.wr[e] && w.cnt[e] > 1;
+}
+
+__global__ __launch_bounds__(TR_T) void ord_fill_k(int64_t ncap, OrderWs w) {
+  const int64_t i = (int64_t)blockIdx.x * TR_T + threadIdx.x;
+  if (i >= ncap) return;
+  const int64_t e = w.eidx[i];
+  if (!ord_grouped(w, e)) return;
+  const int32_t pos = atomicAdd(&w.fill[e], 1);
+  w.members[w.base[e] + pos] = (int32_t)i;
+}
+
+__global__ __launch_bounds__(TR_T) void ord_rank_k(int64_t ncap, ZkReqOut q,
+                                                   OrderWs w,
+                                                   uint8_t* __restrict__ rank) {
+  const int64_t i = (int64_t)blockIdx.x * TR_T + threadIdx.x;
+  if (i >= ncap) return;
+  const int64_t e = w.eidx[i];
+  int32_t r = 0;
+  bool later_write = false;
+  if (ord_grouped(w, e)) {
+    const int32_t* m = w.members + w.base[e];
+    const int32_t c = w.cnt[e];
+    for (int32_t k = 0; k < c; ++k) {
+      const int32_t j = m[k];
+      r += j < (int32_t)i;
+      later_write |= j > (int32_t)i && ord_writes(q.opcode[j]);
+    }
+    atomicMax((unsigned long long*)&w.ctr[1], (unsigned long long)r);
+  }
+  rank[i] = (uint8_t)(min(r, ORD_RANK) | (later_write ? ORD_SNAP : 0));
 }
 
 // After a serve / expire launch, one kernel (grid-stride over a bounded
@@ -627,7 +774,8 @@ constexpr int FIN_BLOCKS = 64;   // <= 64 sign-offs on one counter word
 
 __global__ __launch_bounds__(TR_T) void tree_finish_k(ZkTree t,
                                                      const int64_t* n_dev,
-                                                     int64_t bump_zxid) {
+                                                     int64_t bump_zxid,
+                                                     int32_t publish) {
   __shared__ int last;
   int64_t* c = t.counters;
   const int64_t nd = c[TC_DIRTY];
@@ -649,8 +797,10 @@ __global__ __launch_bounds__(TR_T) void tree_finish_k(ZkTree t,
   __syncthreads();
   if (!last || threadIdx.x != 0) return;
   __threadfence();
-  if (c[TC_FREE_HEAD] > c[TC_FREE_PUB]) c[TC_FREE_HEAD] = c[TC_FREE_PUB];
-  c[TC_FREE_PUB] = c[TC_FREE_TAIL];
+  if (publish) {
+    if (c[TC_FREE_HEAD] > c[TC_FREE_PUB]) c[TC_FREE_HEAD] = c[TC_FREE_PUB];
+    c[TC_FREE_PUB] = c[TC_FREE_TAIL];
+  }
   c[TC_DIRTY] = 0;
   c[TC_ZXID] += n_dev != nullptr ? *n_dev : bump_zxid;
   c[TC_DONE] = 0;
@@ -708,11 +858,13 @@ int zk_tree_build(const ZkTree* t, int64_t n0, int64_t n, hipStream_t st) {
 }
 
 static int finish_launch(const ZkTree* t, int64_t ncap, const int64_t* n_dev,
-                         int64_t bump_zxid, hipStream_t st) {
+                         int64_t bump_zxid, hipStream_t st,
+                         int32_t publish = 1) {
   // the dirty list holds at most one parent per request
   const int64_t nb = min((ncap + zk::TR_T - 1) / zk::TR_T,
                          (int64_t)zk::FIN_BLOCKS);
-  zk::tree_finish_k<<<(unsigned)nb, zk::TR_T, 0, st>>>(*t, n_dev, bump_zxid);
+  zk::tree_finish_k<<<(unsigned)nb, zk::TR_T, 0, st>>>(*t, n_dev, bump_zxid,
+                                                      publish);
   ZK_LAUNCH_CHECK();
   return 0;
 }
@@ -730,10 +882,95 @@ int zk_tree_serve(const ZkTree* t, const uint8_t* rx, const ZkReqOut* q,
   zk::tree_serve_k<<<(unsigned)((ncap + zk::TR_T - 1) / zk::TR_T), zk::TR_T,
                      0, st>>>(*t, rx, *q, n_dev, ncap, r_op, r_xid, r_err,
                               r_node, r_zxid, r_path_off, r_path_len, r_slot,
-                              r_sizes, r_bsum, session, now_ms);
+                              r_sizes, r_bsum, session, now_ms, nullptr, 0, 1,
+                              0, 0, nullptr);
   ZK_LAUNCH_CHECK();
   // at most one dirty parent per request
   return finish_launch(t, ncap, n_dev, 0, st);
+}
+
+// Bytes of the ordering workspace for up to ncap requests.
+int64_t zk_tree_order_workspace(int64_t ncap) {
+  int64_t h = 1024;
+  while (h < 2 * ncap) h <<= 1;
+  return h * (8 + 4 + 4 + 4 + 8) + ncap * (4 + 8 + 1) + 64;
+}
+
+// zk_tree_serve with the batch applied in path order: rank every request
+// (tree_order_*), then `passes` serve launches of increasing rank (each
+// followed by the parent fix-up and free-node publish; the batch's zxids are
+// consumed by the last).  A request of rank >= passes is answered
+// SYSTEMERROR and counted in ws's max rank (the caller can read it and use
+// more passes).  The launches do not depend on the ranks: no host read.
+int zk_tree_serve_ordered(const ZkTree* t, const uint8_t* rx, const ZkReqOut* q,
+                          const int64_t* n_dev, int64_t ncap, int32_t* r_op,
+                          int32_t* r_xid, int32_t* r_err, int64_t* r_node,
+                          int64_t* r_zxid, int64_t* r_path_off,
+                          int32_t* r_path_len, int64_t* r_slot,
+                          int64_t* r_sizes, int64_t* r_bsum, int64_t session,
+                          int64_t now_ms, uint8_t* ws, int64_t ws_bytes,
+                          int32_t passes, int64_t snap_base, int64_t snap_cap,
+                          hipStream_t st) {
+  if (ncap <= 0) return 0;
+  if ((r_sizes == nullptr) != (r_bsum == nullptr)) return -1;
+  if (passes < 1 || passes > zk::ORD_RANK) return -1;
+  if (snap_base < 0 || snap_cap < 0 || (snap_base & 15)) return -1;
+  if (ws_bytes < zk_tree_order_workspace(ncap)) return -1;
+  int64_t h = 1024;
+  while (h < 2 * ncap) h <<= 1;
+  zk::OrderWs w;
+  uint8_t* p = ws;
+  w.key = (int64_t*)p; p += h * 8;
+  w.base = (int64_t*)p; p += h * 8;
+  w.cnt = (int32_t*)p; p += h * 4;
+  w.wr = (int32_t*)p; p += h * 4;
+  w.fill = (int32_t*)p; p += h * 4;
+  w.eidx = (int64_t*)p; p += ncap * 8;
+  w.members = (int32_t*)p; p += ncap * 4;
+  uint8_t* rank = p; p += ncap;
+  p = (uint8_t*)(((uintptr_t)p + 15) & ~(uintptr_t)15);
+  w.ctr = (int64_t*)p;
+  w.mask = h - 1;
+  // key, the contiguous cnt / wr / fill and the counters start at 0 (base
+  // and members are written before they are read)
+  if (hipMemsetAsync(w.key, 0, (size_t)h * 8, st) != hipSuccess ||
+      hipMemsetAsync(w.cnt, 0, (size_t)h * 12, st) != hipSuccess ||
+      hipMemsetAsync(w.ctr, 0, 32, st) != hipSuccess)
+    return -4;
+  const unsigned nb = (unsigned)((ncap + zk::TR_T - 1) / zk::TR_T);
+  zk::ord_insert_k<<<nb, zk::TR_T, 0, st>>>(rx, *q, n_dev, ncap, w);
+  ZK_LAUNCH_CHECK();
+  zk::ord_base_k<<<(unsigned)((h + zk::TR_T - 1) / zk::TR_T), zk::TR_T, 0,
+                   st>>>(w);
+  ZK_LAUNCH_CHECK();
+  zk::ord_fill_k<<<nb, zk::TR_T, 0, st>>>(ncap, w);
+  ZK_LAUNCH_CHECK();
+  zk::ord_rank_k<<<nb, zk::TR_T, 0, st>>>(ncap, *q, w, rank);
+  ZK_LAUNCH_CHECK();
+  for (int32_t pass = 0; pass < passes; ++pass) {
+    const int32_t last = pass == passes - 1;
+    zk::tree_serve_k<<<nb, zk::TR_T, 0, st>>>(
+        *t, rx, *q, n_dev, ncap, r_op, r_xid, r_err, r_node, r_zxid,
+        r_path_off, r_path_len, r_slot, r_sizes, r_bsum, session, now_ms,
+        rank, pass, last, snap_base, snap_cap, &w.ctr[2]);
+    ZK_LAUNCH_CHECK();
+    // nodes freed by a pass are recycled from the next batch on: a reply of
+    // this batch may still name them
+    const int rc = finish_launch(t, ncap, last ? n_dev : nullptr, 0, st,
+                                 last);
+    if (rc) return rc;
+  }
+  return 0;
+}
+
+// Byte offset in the ordering workspace of {max rank, scratch bytes used}
+// of the last ordered serve (int64 each; read them after the stream).
+int64_t zk_tree_order_stats_offset(int64_t ncap) {
+  int64_t h = 1024;
+  while (h < 2 * ncap) h <<= 1;
+  int64_t off = h * 28 + ncap * 13;
+  off = (off + 15) & ~(int64_t)15;
+  return off + 8;
 }
 
 int zk_tree_expire(const ZkTree* t, int64_t session, int64_t ncap,

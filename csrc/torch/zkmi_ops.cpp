@@ -99,6 +99,14 @@ int zk_tree_serve(const ZkTree*, const uint8_t*, const ZkReqOut*,
                   const int64_t*, int64_t, int32_t*, int32_t*, int32_t*,
                   int64_t*, int64_t*, int64_t*, int32_t*, int64_t*, int64_t*,
                   int64_t*, int64_t, int64_t, hipStream_t);
+int zk_tree_serve_ordered(const ZkTree*, const uint8_t*, const ZkReqOut*,
+                          const int64_t*, int64_t, int32_t*, int32_t*,
+                          int32_t*, int64_t*, int64_t*, int64_t*, int32_t*,
+                          int64_t*, int64_t*, int64_t*, int64_t, int64_t,
+                          uint8_t*, int64_t, int32_t, int64_t, int64_t,
+                          hipStream_t);
+int64_t zk_tree_order_workspace(int64_t);
+int64_t zk_tree_order_stats_offset(int64_t);
 int zk_tree_expire(const ZkTree*, int64_t, int64_t, unsigned long long*,
                    hipStream_t);
 int zk_bench_gen_get(int64_t, uint64_t, int64_t, int64_t, int32_t,
@@ -598,6 +606,64 @@ void tree_serve(const std::vector<Tensor>& t, const Tensor& rx,
          "tree_serve");
 }
 
+int64_t tree_order_workspace(int64_t n) {
+  TORCH_CHECK(n >= 0, "zkmi: tree_order_workspace n");
+  return zk_tree_order_workspace(n);
+}
+
+int64_t tree_order_stats_offset(int64_t n) {
+  TORCH_CHECK(n >= 0, "zkmi: tree_order_stats_offset n");
+  return zk_tree_order_stats_offset(n);
+}
+
+// tree_serve with same-path requests applied in batch order over `passes`
+// launches.  `scratch` (optional) is the slab's tail past the tree's view of
+// it (t[6] = slab[:cap]); snapshot replies are written there and named by
+// their offset from the slab start, so the encoder must be given the whole
+// slab.
+void tree_serve_ordered(const std::vector<Tensor>& t, const Tensor& rx,
+                        const std::vector<Tensor>& q, const Tensor& n_dev,
+                        int64_t ncap, const std::vector<Tensor>& r,
+                        int64_t session, int64_t now_ms, const Tensor& ws,
+                        int64_t passes, const c10::optional<Tensor>& scratch) {
+  ZkTree s = tree(t);
+  const Tensor* d = &t[0];
+  ZkReqOut qo = req_out(q, ncap, d);
+  need(r, 10, "serve outputs");
+  TORCH_CHECK(passes >= 1 && passes <= 127, "zkmi: passes in 1..127");
+  const int64_t need_ws = zk_tree_order_workspace(ncap);
+  uint8_t* w = P<uint8_t>(ws, U8, need_ws, "order workspace", d);
+  int64_t snap_base = 0, snap_cap = 0;
+  if (scratch.has_value() && scratch->defined()) {
+    const Tensor& sc = *scratch;
+    P<uint8_t>(sc, U8, 0, "scratch", d);
+    TORCH_CHECK(sc.storage().is_alias_of(t[6].storage()),
+                "zkmi: scratch must be a view of the tree's slab");
+    snap_base = (int64_t)((const uint8_t*)sc.data_ptr() -
+                          (const uint8_t*)t[6].data_ptr());
+    TORCH_CHECK(snap_base >= s.slab_cap && snap_base % 16 == 0,
+                "zkmi: scratch must start 16-aligned past the tree's slab");
+    snap_cap = sc.numel();
+  }
+  const int64_t nb = (ncap + 255) / 256;
+  hip_ok(zk_tree_serve_ordered(
+             &s, P<uint8_t>(rx, U8, 1, "rx", d), &qo,
+             P<int64_t>(n_dev, I64, 1, "count", d), ncap,
+             P<int32_t>(r[0], I32, ncap, "r.opcode", d),
+             P<int32_t>(r[1], I32, ncap, "r.xid", d),
+             P<int32_t>(r[2], I32, ncap, "r.err", d),
+             P<int64_t>(r[3], I64, ncap, "r.node", d),
+             P<int64_t>(r[4], I64, ncap, "r.zxid", d),
+             P<int64_t>(r[5], I64, ncap, "r.path_off", d),
+             P<int32_t>(r[6], I32, ncap, "r.path_len", d),
+             P<int64_t>(r[7], I64, ncap, "r.slot", d),
+             P<int64_t>(r[8], I64, ncap, "r.sizes", d),
+             P<int64_t>(r[9], I64, nb, "r.block_sums", d), session, now_ms,
+             w, ws.numel(), (int32_t)passes, snap_base, snap_cap,
+             cur_stream()),
+         "tree_serve_ordered");
+}
+
 void tree_expire(const std::vector<Tensor>& t, int64_t session, int64_t ncap,
                  const Tensor& removed) {
   ZkTree s = tree(t);
@@ -780,6 +846,12 @@ TORCH_LIBRARY(zkmi, m) {
   m.def("tree_serve(Tensor(a!)[] tree, Tensor rx, Tensor[] requests, "
         "Tensor count, int ncap, Tensor(b!)[] out, int session, int now_ms) "
         "-> ()", &tree_serve);
+  m.def("tree_order_workspace(int n) -> int", &tree_order_workspace);
+  m.def("tree_order_stats_offset(int n) -> int", &tree_order_stats_offset);
+  m.def("tree_serve_ordered(Tensor(a!)[] tree, Tensor rx, Tensor[] requests, "
+        "Tensor count, int ncap, Tensor(b!)[] out, int session, int now_ms, "
+        "Tensor(c!) ws, int passes, Tensor? scratch) -> ()",
+        &tree_serve_ordered);
   m.def("tree_expire(Tensor(a!)[] tree, int session, int ncap, "
         "Tensor(b!) removed) -> ()", &tree_expire);
   m.def("bench_gen_get(int n, int seed, int leaf0, int nleaves, "

@@ -92,7 +92,7 @@ class GpuTree(object):
 
     def __init__(self, n_nodes=1_000_000, data_bytes=100, fanout=1000,
                  device=None, spare=0.25, seed=0, shard=None, ctime_ms=None,
-                 data_dist=None, name_pad=None):
+                 data_dist=None, name_pad=None, scratch=0):
         dev = torch.device(device) if device is not None else \
             torch.device('cuda', torch.cuda.current_device())
         self.device = dev
@@ -157,8 +157,14 @@ class GpuTree(object):
         assert cap < (1 << 31) and self.slab_cap < (1 << 35), 'tree too big'
         g = torch.Generator(device=dev)
         g.manual_seed(seed)
-        self.slab = torch.randint(0, 256, (self.slab_cap,), dtype=U8,
-                                  device=dev, generator=g)
+        # scratch: bytes past the tree's slab for the snapshots of ordered
+        # serving (GpuServer.serve(ordered=True)); the tree's descriptor
+        # sees slab[:slab_cap], the reply encoder the whole allocation
+        scratch = (int(scratch) + 15) & ~15
+        self.slab_all = torch.randint(0, 256, (self.slab_cap + scratch,),
+                                      dtype=U8, device=dev, generator=g)
+        self.slab = self.slab_all[:self.slab_cap]
+        self.scratch = self.slab_all[self.slab_cap:] if scratch else None
         self.slot_off = torch.arange(cap, dtype=I64, device=dev) * sb
         self.data_len = torch.zeros(cap, dtype=I32, device=dev)
         if data_dist is not None:
@@ -189,11 +195,12 @@ class GpuTree(object):
         self.hcap = hcap
         # the tree / node-store descriptor lists torch.ops.zkmi takes
         # (csrc/torch/zkmi_ops.cpp tree() / node_store() field order)
-        self.store = [self.slab, self.slot_off, self.data_len,
+        self.store = [self.slab_all, self.slot_off, self.data_len,
                       self.slot_cap]
         self._tensors = [self.ht, self.node_path_off, self.node_path_len,
-                         self.node_parent, self.path_arena, self.counters] + \
-            self.store + [self.free_list, self.cver, self.nchild, self.pzxid,
+                         self.node_parent, self.path_arena, self.counters,
+                         self.slab, self.slot_off, self.data_len,
+                         self.slot_cap] + [self.free_list, self.cver, self.nchild, self.pzxid,
                           self.dirty, self.dirty_list, self.node_pw]
         now = int(time.time() * 1000) if ctime_ms is None else ctime_ms
         L.tree_fill(self._tensors, 0, nst, nk, now)
@@ -283,29 +290,53 @@ class GpuServer(object):
         self.out = torch.empty(out_cap, dtype=U8, device=dev)
         self.cap_frames = cap_frames
         self.scanner = B.FrameScanner(cap_frames, dev, window=window)
+        self.ows = None                   # ordered-serve workspace (lazy)
 
-    def serve(self, rx, n, session=0, terminate=False):
+    def serve(self, rx, n, session=0, terminate=False, ordered=False,
+              passes=4):
         """Serve the request stream ``rx[:n]`` for ``session`` (the owner of
         any EPHEMERAL node it creates).  ``n`` is a host length or the
         request encoder's device total (no host read).  Returns the reply
         stream buffer, its device total, the encoder error flag and the
-        request frame table."""
+        request frame table.
+
+        ``ordered``: requests on one path are applied in stream order when
+        one of them writes it (``passes`` launches; a path with more than
+        ``passes`` requests in the batch has the excess answered
+        SYSTEMERROR, see :meth:`order_stats`).  Reads and sets followed by
+        a write to their path snapshot their reply into the tree's
+        ``scratch``.  Without it requests of a batch are concurrent."""
         L = _lib.lib()
         ft = self.scanner.scan(rx, n)
         rt = B.decode_requests(rx, ft, out=self.rt)
         r = self.resp
         r.count = ft.count
-        L.tree_serve(self.tree.tensors, rx, rt.tensors(), ft.count,
-                     self.cap_frames,
-                     [r.opcode, r.xid, r.err, r.node, r.zxid, r.path_off,
-                      r.path_len, r.slot, self.presized[0],
-                      self.presized[1]],
-                     session, int(time.time() * 1000))
+        out = [r.opcode, r.xid, r.err, r.node, r.zxid, r.path_off,
+               r.path_len, r.slot, self.presized[0], self.presized[1]]
+        now = int(time.time() * 1000)
+        if ordered:
+            if self.ows is None:
+                self.ows = torch.empty(
+                    L.tree_order_workspace(self.cap_frames), dtype=U8,
+                    device=self.tree.device)
+            L.tree_serve_ordered(self.tree.tensors, rx, rt.tensors(),
+                                 ft.count, self.cap_frames, out, session,
+                                 now, self.ows, passes, self.tree.scratch)
+        else:
+            L.tree_serve(self.tree.tensors, rx, rt.tensors(), ft.count,
+                         self.cap_frames, out, session, now)
         out, rec_off, total, err = B.encode_responses(
             r, self.tree.store, self.out.numel(), out=self.out,
             presized=self.presized, terminate=terminate)
         self.last_rec_off = rec_off         # reply frame starts (R2 splits)
         return out, total, err, ft
+
+    def order_stats(self):
+        """(largest same-path rank, scratch bytes used) of the last ordered
+        serve (host read).  A rank >= the passes used means refusals."""
+        o = _lib.lib().tree_order_stats_offset(self.cap_frames)
+        v = self.ows[o:o + 16].cpu().view(torch.int64).tolist()
+        return v[0], v[1]
 
 
 class GetPipeline(object):
@@ -474,6 +505,7 @@ class _Driver(object):
         self.rscanner = None
         self.xid_base = 0
         self.iota = torch.arange(batch, dtype=I32, device=dev)
+        self.passes = 0          # > 0: ordered serving in that many passes
 
     def xids(self, n):
         x = (self.iota[:n] + self.xid_base) & 0x7fffffff
@@ -509,7 +541,9 @@ class _Driver(object):
         (``ZKMI_SYNC_STREAMS=1`` reads them back instead, for A/B)."""
         tx, _, total, _ = B.encode_requests(rb, self.xt, out=self.tx)
         rx, rtotal, _, _ = self.server.serve(tx, _len(total),
-                                             session=session)
+                                             session=session,
+                                             ordered=self.passes > 0,
+                                             passes=max(self.passes, 1))
         if self.rscanner is None:
             self.rscanner = B.FrameScanner(self.batch, self.dev,
                                            window=self.rwindow)
@@ -622,6 +656,96 @@ class MixPipeline(object):
         return {'wrong_err': dict(zip(e.cpu().tolist(), c.cpu().tolist())),
                 'status_bad': int((rep.status[:n] != 0).sum().item()),
                 'counters': self.tree.counters.cpu().tolist()}
+
+
+class ChainPipeline(object):
+    """In-batch ordering workload: every step sends, for each of ``m`` paths
+    ``/chain/dDDDD/cKKKKKKKKK``, the chain CREATE (``data_bytes // 2``
+    bytes) -> SET_DATA (version 0, ``data_bytes``) -> GET_DATA -> DELETE
+    (version 1) back to back in one batch, as one session pipelining them
+    would.  The server must apply each chain in order (ordered serving, 4
+    passes): every reply is checked on the device — all OK, the set and the
+    get see version 1, and the get returns the set's data length.  Nodes
+    are recycled through the free ring (each step deletes what it created).
+    """
+
+    def __init__(self, tree, batch, data_bytes=100, ndirs=1024, seed=0):
+        m = max(batch // 4, 1)
+        self.m = m
+        self.n = n = 4 * m
+        dev = tree.device
+        self.tree = tree
+        self.data_bytes = data_bytes
+        need = 2 * m * (80 + ((data_bytes + 15) & ~15))
+        if tree.scratch is None or tree.scratch.numel() < need:
+            raise ValueError('ChainPipeline needs GpuTree(scratch >= %d)'
+                             % need)
+        paths = ['/chain/d%05d/c%09d' % (k % ndirs, k) for k in range(m)]
+        maxp = max(len(p) for p in paths)
+        self.drv = _Driver(tree, n, maxp, data_bytes, seed)
+        self.drv.passes = 4
+        self.path_arena, poff, plen = _arena(paths, dev)
+        g = torch.Generator(device=dev)
+        g.manual_seed(seed + 11)
+        nblk = 1024
+        self.data_arena = torch.randint(0, 256, (nblk * data_bytes + 16,),
+                                        dtype=U8, device=dev, generator=g)
+        self.acl_arena, self.acl_off, self.acl_len = _acl_table(MIX_ACLS, dev)
+        ops = consts.OP_CODES
+
+        def il(a, b, c, d):      # interleave per path: [a0 b0 c0 d0 a1 ...]
+            return torch.stack([a, b, c, d], 1).reshape(-1)
+        k = torch.arange(m, dtype=I64, device=dev)
+        full = lambda v, dt: torch.full((m,), v, dtype=dt, device=dev)  # noqa
+        self.opcode = il(full(ops['CREATE'], I32), full(ops['SET_DATA'], I32),
+                         full(ops['GET_DATA'], I32), full(ops['DELETE'], I32))
+        self.arg = il(full(0, I32), full(0, I32), full(0, I32), full(1, I32))
+        self.path_off = il(poff, poff, poff, poff)
+        self.path_len = il(plen, plen, plen, plen)
+        self.data_off = il((k % nblk) * data_bytes,
+                           ((k + 7) % nblk) * data_bytes, full(0, I64),
+                           full(0, I64))
+        self.data_len = il(full(data_bytes // 2, I32), full(data_bytes, I32),
+                           full(0, I32), full(0, I32))
+        self.acl_id = il((k % 2).to(I32), full(0, I32), full(0, I32),
+                         full(0, I32))
+        self.is_set = self.opcode == ops['SET_DATA']
+        self.is_get = self.opcode == ops['GET_DATA']
+        self.drv.create_dirs(
+            [['/chain'], ['/chain/d%05d' % d for d in range(ndirs)]],
+            (self.acl_arena, self.acl_off, self.acl_len))
+        self.last = None
+
+    def step(self, validate=True, acc=None):
+        n = self.n
+        d = self.drv
+        rb = B.RequestBatch(n, self.opcode, d.xids(n), self.arg,
+                            self.path_off, self.path_len, self.data_off,
+                            self.data_len, self.acl_id, self.path_arena,
+                            self.data_arena, self.acl_off, self.acl_len,
+                            self.acl_arena)
+        rep, _ = d.run(rb)
+        self.last = (rb, rep)
+        if not validate:
+            return None
+        ver1 = rep.stat32[0, :n] == 1
+        ok = ((rep.status[:n] == 0) & (rep.err[:n] == 0) &
+              (rep.xid[:n] == rb.xid) & (rep.opcode[:n] == rb.opcode) &
+              (~(self.is_set | self.is_get) | ver1) &
+              (~self.is_get | ((rep.stat32[3, :n] == self.data_bytes) &
+                               (rep.pay_len[:n] == self.data_bytes))))
+        if acc is None:
+            return ok.sum()
+        acc += ok.sum()
+        return acc
+
+    def diagnose(self):
+        rb, rep = self.last
+        n = rb.n
+        bad = rep.err[:n] != 0
+        e, c = torch.unique(rep.err[:n][bad], return_counts=True)
+        return {'wrong_err': dict(zip(e.cpu().tolist(), c.cpu().tolist())),
+                'order_stats': self.drv.server.order_stats()}
 
 
 class GpuSessionTable(object):

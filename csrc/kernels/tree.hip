@@ -664,19 +664,24 @@ __global__ __launch_bounds__(TR_T) void tree_serve_k(
 // path: rank[i] = number of earlier requests of the batch on i's path (0 for
 // paths only read).  A scratch hash table groups the batch's requests by
 // path hash (a 64-bit collision merges two groups: extra ordering, never
-// less); multi-request write groups get a member list, and each member
-// counts the members before it.  ws layout (OrderWs): key, cnt, wr, fill,
-// base, members, eidx, top / maxrank.
+// less); write groups of more than one request get a member list (offsets
+// from a block scan of the group sizes: no shared counter), and each member
+// counts the members before it.  No kernel here puts more than one atomic
+// per block on a shared word (a single word sustains ~88 returning atomics
+// per us, MI355X_MICROARCH.md).
+constexpr int64_t ORD_MAX_GROUP = 1 << 16;   // larger write groups: refused
+
 struct OrderWs {
-  int64_t* key;      // [mask + 1]
-  int32_t* cnt;      // [mask + 1] requests on the path
-  int32_t* wr;       // [mask + 1] a request writes it
-  int32_t* fill;     // [mask + 1] member-list fill
-  int64_t* base;     // [mask + 1] member-list base
+  int64_t* ctr;      // [4] -, max rank, scratch top, -
+  int64_t* key;      // [h] path hash | 1
+  int64_t* cw;       // [h] requests (low 32 bits) | writers (high 32)
+  int32_t* fill;     // [h] member-list fill
+  int32_t* lastw;    // [h] 1 + index of the group's last writer
+  int32_t* base;     // [h] member-list offset within its block of entries
+  int64_t* bsum;     // [h / TR_T] block totals, then exclusive offsets
+  int64_t* eidx;     // [ncap] request -> entry (-1: not ordered)
   int32_t* members;  // [ncap]
-  int64_t* eidx;     // [ncap] request -> entry (-1: no path)
-  int64_t* ctr;      // [4] member-list top, max rank, scratch top, 0
-  int64_t mask;
+  int64_t mask;      // h - 1
 };
 
 ZK_DEV bool ord_has_path(int32_t op) {
@@ -687,6 +692,11 @@ ZK_DEV bool ord_has_path(int32_t op) {
 
 ZK_DEV bool ord_writes(int32_t op) {
   return op == OP_CREATE || op == OP_DELETE || op == OP_SET_DATA;
+}
+
+// a write group of more than one request
+ZK_DEV bool ord_grouped(int64_t cw) {
+  return (cw >> 32) != 0 && (int32_t)cw > 1;
 }
 
 __global__ __launch_bounds__(TR_T) void ord_insert_k(
@@ -710,54 +720,88 @@ __global__ __launch_bounds__(TR_T) void ord_insert_k(
       sl = (sl + 1) & w.mask;
     }
     if (e >= 0) {
-      atomicAdd(&w.cnt[e], 1);
-      if (ord_writes(op)) atomicOr(&w.wr[e], 1);
+      const bool wr = ord_writes(op);
+      atomicAdd((unsigned long long*)&w.cw[e], 1ull + (wr ? 1ull << 32 : 0));
+      if (wr) atomicMax(&w.lastw[e], (int32_t)i + 1);
     }
   }
   w.eidx[i] = e;
 }
 
-// member-list bases of the write groups with more than one request (one
-// atomic per wave on the list top)
+// member-list offsets: a block scan of the group sizes per TR_T entries
 __global__ __launch_bounds__(TR_T) void ord_base_k(OrderWs w) {
-  const int64_t e = (int64_t)blockIdx.x * TR_T + threadIdx.x;
-  const bool grp = e <= w.mask && w.key[e] != 0 && w.wr[e] && w.cnt[e] > 1;
-  const int64_t b = wave_bytes(&w.ctr[0], grp ? w.cnt[e] : 0);
-  if (grp) w.base[e] = b;
+  __shared__ int64_t sm[TR_T / 64 + 1];
+  const int64_t e = (int64_t)blockIdx.x * TR_T + threadIdx.x;  // h % TR_T == 0
+  const int64_t cw = w.cw[e];
+  const int64_t c = ord_grouped(cw) ? (int64_t)(int32_t)cw : 0;
+  int64_t tot;
+  const int64_t x = block_excl_scan(c, sm, &tot);
+  if (c) w.base[e] = (int32_t)x;
+  if (threadIdx.x == 0) w.bsum[blockIdx.x] = tot;
 }
 
-ZK_DEV bool ord_grouped(const OrderWs& w, int64_t e) {
-  return e >= 0 && w.wr[e] && w.cnt[e] > 1;
+// exclusive scan of the block totals in place (one block)
+constexpr int ORD_SCAN_T = 1024;
+__global__ __launch_bounds__(ORD_SCAN_T) void ord_bscan_k(int64_t* bsum,
+                                                          int64_t nbh) {
+  __shared__ int64_t sm[ORD_SCAN_T / 64 + 1];
+  const int64_t per = (nbh + ORD_SCAN_T - 1) / ORD_SCAN_T;
+  const int64_t b0 = (int64_t)threadIdx.x * per;
+  const int64_t b1 = min(b0 + per, nbh);
+  int64_t sum = 0;
+  for (int64_t k = b0; k < b1; ++k) sum += bsum[k];
+  int64_t tot;
+  int64_t x = block_excl_scan(sum, sm, &tot);
+  for (int64_t k = b0; k < b1; ++k) {
+    const int64_t v = bsum[k];
+    bsum[k] = x;
+    x += v;
+  }
+}
+
+ZK_DEV int32_t* ord_list(const OrderWs& w, int64_t e) {
+  return w.members + w.bsum[e / TR_T] + w.base[e];
 }
 
 __global__ __launch_bounds__(TR_T) void ord_fill_k(int64_t ncap, OrderWs w) {
   const int64_t i = (int64_t)blockIdx.x * TR_T + threadIdx.x;
   if (i >= ncap) return;
   const int64_t e = w.eidx[i];
-  if (!ord_grouped(w, e)) return;
+  if (e < 0 || !ord_grouped(w.cw[e])) return;
   const int32_t pos = atomicAdd(&w.fill[e], 1);
-  w.members[w.base[e] + pos] = (int32_t)i;
+  ord_list(w, e)[pos] = (int32_t)i;
 }
 
-__global__ __launch_bounds__(TR_T) void ord_rank_k(int64_t ncap, ZkReqOut q,
-                                                   OrderWs w,
+__global__ __launch_bounds__(TR_T) void ord_rank_k(int64_t ncap, OrderWs w,
                                                    uint8_t* __restrict__ rank) {
+  __shared__ int32_t smx[TR_T / 64];
   const int64_t i = (int64_t)blockIdx.x * TR_T + threadIdx.x;
-  if (i >= ncap) return;
-  const int64_t e = w.eidx[i];
+  const int64_t e = i < ncap ? w.eidx[i] : -1;
+  const int64_t cw = e >= 0 ? w.cw[e] : 0;
   int32_t r = 0;
   bool later_write = false;
-  if (ord_grouped(w, e)) {
-    const int32_t* m = w.members + w.base[e];
-    const int32_t c = w.cnt[e];
-    for (int32_t k = 0; k < c; ++k) {
-      const int32_t j = m[k];
-      r += j < (int32_t)i;
-      later_write |= j > (int32_t)i && ord_writes(q.opcode[j]);
+  if (ord_grouped(cw)) {
+    const int32_t c = (int32_t)cw;
+    later_write = w.lastw[e] > (int32_t)i + 1;
+    if (c > ORD_MAX_GROUP) {
+      r = ORD_RANK;                               // refused wholesale
+    } else {
+      const int32_t* m = ord_list(w, e);
+      for (int32_t k = 0; k < c && r < ORD_RANK; ++k) r += m[k] < (int32_t)i;
     }
-    atomicMax((unsigned long long*)&w.ctr[1], (unsigned long long)r);
   }
-  rank[i] = (uint8_t)(min(r, ORD_RANK) | (later_write ? ORD_SNAP : 0));
+  if (i < ncap) rank[i] = (uint8_t)(r | (later_write ? ORD_SNAP : 0));
+  // the batch's largest rank: one atomic per block
+  int32_t mx = r;
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) mx = max(mx, __shfl_xor(mx, d, 64));
+  if ((threadIdx.x & 63) == 0) smx[threadIdx.x >> 6] = mx;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int k = 1; k < TR_T / 64; ++k) mx = max(mx, smx[k]);
+    if (mx > 0) atomicMax((unsigned long long*)&w.ctr[1],
+                          (unsigned long long)mx);
+  }
 }
 
 // After a serve / expire launch, one kernel (grid-stride over a bounded
@@ -889,19 +933,56 @@ int zk_tree_serve(const ZkTree* t, const uint8_t* rx, const ZkReqOut* q,
   return finish_launch(t, ncap, n_dev, 0, st);
 }
 
-// Bytes of the ordering workspace for up to ncap requests.
-int64_t zk_tree_order_workspace(int64_t ncap) {
+// Ordering workspace layout for up to ncap requests: the zeroed prefix
+// (counters, key, cw, fill, lastw), then base, bsum, eidx, members, rank.
+static int64_t order_hcap(int64_t ncap) {
   int64_t h = 1024;
   while (h < 2 * ncap) h <<= 1;
-  return h * (8 + 4 + 4 + 4 + 8) + ncap * (4 + 8 + 1) + 64;
+  return h;
+}
+
+static int64_t order_layout(int64_t ncap, uint8_t* ws, zk::OrderWs* w,
+                            uint8_t** rank, int64_t* zeroed) {
+  const int64_t h = order_hcap(ncap);
+  int64_t o = 32;
+  if (w != nullptr) {
+    w->ctr = (int64_t*)ws;
+    w->key = (int64_t*)(ws + o);
+  }
+  o += h * 8;
+  if (w != nullptr) w->cw = (int64_t*)(ws + o);
+  o += h * 8;
+  if (w != nullptr) w->fill = (int32_t*)(ws + o);
+  o += h * 4;
+  if (w != nullptr) w->lastw = (int32_t*)(ws + o);
+  o += h * 4;
+  if (zeroed != nullptr) *zeroed = o;
+  if (w != nullptr) w->base = (int32_t*)(ws + o);
+  o += h * 4;
+  if (w != nullptr) w->bsum = (int64_t*)(ws + o);
+  o += (h / zk::TR_T) * 8;
+  if (w != nullptr) w->eidx = (int64_t*)(ws + o);
+  o += ncap * 8;
+  if (w != nullptr) w->members = (int32_t*)(ws + o);
+  o += ncap * 4;
+  if (rank != nullptr) *rank = ws + o;
+  o += ncap;
+  if (w != nullptr) w->mask = h - 1;
+  return o;
+}
+
+// Bytes of the ordering workspace for up to ncap requests.
+int64_t zk_tree_order_workspace(int64_t ncap) {
+  return order_layout(ncap, nullptr, nullptr, nullptr, nullptr);
 }
 
 // zk_tree_serve with the batch applied in path order: rank every request
 // (tree_order_*), then `passes` serve launches of increasing rank (each
-// followed by the parent fix-up and free-node publish; the batch's zxids are
-// consumed by the last).  A request of rank >= passes is answered
-// SYSTEMERROR and counted in ws's max rank (the caller can read it and use
-// more passes).  The launches do not depend on the ranks: no host read.
+// followed by the parent fix-up; the free nodes are published and the
+// batch's zxids consumed by the last).  A request of rank >= passes is
+// answered SYSTEMERROR and shows in the max rank (zk_tree_order_stats_offset;
+// the caller can read it and use more passes).  The launches do not depend
+// on the ranks: no host read.
 int zk_tree_serve_ordered(const ZkTree* t, const uint8_t* rx, const ZkReqOut* q,
                           const int64_t* n_dev, int64_t ncap, int32_t* r_op,
                           int32_t* r_xid, int32_t* r_err, int64_t* r_node,
@@ -912,40 +993,28 @@ int zk_tree_serve_ordered(const ZkTree* t, const uint8_t* rx, const ZkReqOut* q,
                           int32_t passes, int64_t snap_base, int64_t snap_cap,
                           hipStream_t st) {
   if (ncap <= 0) return 0;
+  if (ncap >= (int64_t)1 << 31) return -1;
   if ((r_sizes == nullptr) != (r_bsum == nullptr)) return -1;
   if (passes < 1 || passes > zk::ORD_RANK) return -1;
   if (snap_base < 0 || snap_cap < 0 || (snap_base & 15)) return -1;
   if (ws_bytes < zk_tree_order_workspace(ncap)) return -1;
-  int64_t h = 1024;
-  while (h < 2 * ncap) h <<= 1;
+  if (((uintptr_t)ws & 15) != 0) return -1;
   zk::OrderWs w;
-  uint8_t* p = ws;
-  w.key = (int64_t*)p; p += h * 8;
-  w.base = (int64_t*)p; p += h * 8;
-  w.cnt = (int32_t*)p; p += h * 4;
-  w.wr = (int32_t*)p; p += h * 4;
-  w.fill = (int32_t*)p; p += h * 4;
-  w.eidx = (int64_t*)p; p += ncap * 8;
-  w.members = (int32_t*)p; p += ncap * 4;
-  uint8_t* rank = p; p += ncap;
-  p = (uint8_t*)(((uintptr_t)p + 15) & ~(uintptr_t)15);
-  w.ctr = (int64_t*)p;
-  w.mask = h - 1;
-  // key, the contiguous cnt / wr / fill and the counters start at 0 (base
-  // and members are written before they are read)
-  if (hipMemsetAsync(w.key, 0, (size_t)h * 8, st) != hipSuccess ||
-      hipMemsetAsync(w.cnt, 0, (size_t)h * 12, st) != hipSuccess ||
-      hipMemsetAsync(w.ctr, 0, 32, st) != hipSuccess)
-    return -4;
+  uint8_t* rank = nullptr;
+  int64_t zeroed = 0;
+  order_layout(ncap, ws, &w, &rank, &zeroed);
+  const int64_t h = w.mask + 1;
+  if (hipMemsetAsync(ws, 0, (size_t)zeroed, st) != hipSuccess) return -4;
   const unsigned nb = (unsigned)((ncap + zk::TR_T - 1) / zk::TR_T);
   zk::ord_insert_k<<<nb, zk::TR_T, 0, st>>>(rx, *q, n_dev, ncap, w);
   ZK_LAUNCH_CHECK();
-  zk::ord_base_k<<<(unsigned)((h + zk::TR_T - 1) / zk::TR_T), zk::TR_T, 0,
-                   st>>>(w);
+  zk::ord_base_k<<<(unsigned)(h / zk::TR_T), zk::TR_T, 0, st>>>(w);
+  ZK_LAUNCH_CHECK();
+  zk::ord_bscan_k<<<1, zk::ORD_SCAN_T, 0, st>>>(w.bsum, h / zk::TR_T);
   ZK_LAUNCH_CHECK();
   zk::ord_fill_k<<<nb, zk::TR_T, 0, st>>>(ncap, w);
   ZK_LAUNCH_CHECK();
-  zk::ord_rank_k<<<nb, zk::TR_T, 0, st>>>(ncap, *q, w, rank);
+  zk::ord_rank_k<<<nb, zk::TR_T, 0, st>>>(ncap, w, rank);
   ZK_LAUNCH_CHECK();
   for (int32_t pass = 0; pass < passes; ++pass) {
     const int32_t last = pass == passes - 1;
@@ -966,11 +1035,8 @@ int zk_tree_serve_ordered(const ZkTree* t, const uint8_t* rx, const ZkReqOut* q,
 // Byte offset in the ordering workspace of {max rank, scratch bytes used}
 // of the last ordered serve (int64 each; read them after the stream).
 int64_t zk_tree_order_stats_offset(int64_t ncap) {
-  int64_t h = 1024;
-  while (h < 2 * ncap) h <<= 1;
-  int64_t off = h * 28 + ncap * 13;
-  off = (off + 15) & ~(int64_t)15;
-  return off + 8;
+  (void)ncap;
+  return 8;
 }
 
 int zk_tree_expire(const ZkTree* t, int64_t session, int64_t ncap,

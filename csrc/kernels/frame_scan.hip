@@ -4,7 +4,7 @@
 // i32-BE length chain one frame at a time and memmoves the remainder per
 // packet (O(bytes x packets)).  The chain is inherently
 // sequential; we make it parallel without speculation errors, over 4 KiB
-// tiles, in three launches:
+// tiles, in four launches:
 //
 //  fs_tile   ONE WAVE per tile (4 per workgroup, independent, no barriers).
 //            The tile is staged into the wave's LDS once; everything else
@@ -20,29 +20,38 @@
 //               one walker — the survivor — is left;
 //            2. the survivor walks to the tile end, recording its frame
 //               starts (LDS, one hop = one LDS round trip);
-//            3. every exit a walker took into the next tile's window is
-//               published as one of that tile's entry candidates (a bit
-//               map); the true chain's exit is always among them when
-//               frames are <= W.  The tile takes the candidates of the tile
-//               before (a one-step wait: that wave started earlier and does
-//               the same work) and walks each in LDS: a garbage chain of
-//               the tile before, read on here, dies on a bad length within
-//               a few hops; the first candidate whose chain survives the
-//               tile is the entry.  (Round 2 first published only the last
-//               surviving walker's exit: on structured replies of a few
-//               hundred bytes a slow garbage crawler outlived the true
-//               chain in ~20 % of the tiles, and every such tile cost a
-//               serial repair.)
+//            3. every exit a walker took into the next tile's window is a
+//               candidate entry of that tile; the preferred one (the
+//               survivor's exit) and up to four others go out in ONE packed
+//               64-bit word (ready bit + five 12-bit offsets, a relaxed
+//               agent-scope store: no release fence, which costs an L2
+//               writeback per wave on a multi-XCD part).  The true chain's
+//               exit is among the in-window exits when frames are <= W.
+//               The tile takes the word of the tile before (a one-step wait:
+//               that wave started earlier and does the same work) and walks
+//               each candidate in LDS: a garbage chain of the tile before,
+//               read on here, dies on a bad length within a few hops; the
+//               first candidate whose chain survives the tile is the entry.
+//               (Round 2 first published only the last surviving walker's
+//               exit: on structured replies of a few hundred bytes a slow
+//               garbage crawler outlived the true chain in ~20 % of the
+//               tiles, and every such tile cost a serial repair.)
 //            4. from the entry, a short walk (usually 1-5 frames) until the
 //               chain meets the survivor's recorded path (merge-walk against
 //               the sorted list), the tile end or a terminal.
 //            The entry is exact unless a frame longer than the window ends
 //            in the tile before or two candidates' chains both survive.
-//  fs_link   one workgroup checks every link in parallel (tile k's entry
-//            must be tile k-1's exit), re-walks the tiles after a broken
-//            link from the exact exit (serial, rare: frames longer than the
-//            window), then scans the counts up to the first terminal: row
-//            bases and result[0..3].
+//  fs_check  one thread per tile (a grid): is tile k's entry tile k-1's
+//            exit, is the tile terminal; frame counts scanned per block of
+//            256 tiles.  The leftmost broken link / terminal go to fs_link
+//            as one atomic per block.
+//  fs_link   one workgroup.  No broken link before the first terminal (the
+//            usual case): scan the block totals, done.  Otherwise repair:
+//            every run of broken links is re-walked in parallel from the
+//            exact exit (one wave per run, bounded rounds), then the links
+//            are re-checked and what is left is repaired serially; then
+//            the counts are scanned up to the first terminal: row bases and
+//            result[0..3].
 //  fs_rows   one wave per tile writes its (body offset, length) rows.
 //
 // The stream length is read ON THE DEVICE (n = min(*n_dev, n_cap), e.g. an
@@ -764,13 +773,72 @@ ZK_DEV void fs_link_parallel(
   if (lane == 0 && walked) fc_stat(stats, 2, walked);
 }
 
+// fs_check: every link and terminal checked in parallel (one thread per
+// tile, a grid over the tiles) and the frame counts scanned per block of
+// FK_T tiles: base[k] = count before tile k within its block, bsum[b] = the
+// block's total.  The leftmost broken link and terminal reach fs_link as
+// (ntiles - k) maxima in mins[0..1] (zeroed with the X flags; one atomic
+// per block).  Round 2's fs_link did this in one workgroup, ~25 dependent
+// round trips per thread on a 100 MB stream (60 us per scan).
+constexpr int FK_T = 256;
+__global__ __launch_bounds__(FK_T) void fs_check(
+    const int64_t* __restrict__ n_dev, int64_t n_cap,
+    const int64_t* __restrict__ rec_entry, const int64_t* __restrict__ rec_exit,
+    const int64_t* __restrict__ rec_meta, int64_t* __restrict__ base,
+    int64_t* __restrict__ bsum, uint64_t* __restrict__ mins) {
+  __shared__ int64_t sm[FK_T / 64 + 1];
+  __shared__ int64_t smin[2 * (FK_T / 64)];
+  const int64_t n = stream_len(n_dev, n_cap);
+  const int64_t ntiles = (n + FT_S - 1) / FT_S;
+  const int64_t k = (int64_t)blockIdx.x * FK_T + threadIdx.x;
+  if ((int64_t)blockIdx.x * FK_T >= ntiles) return;       // block-uniform
+  const int64_t INF = INT64_MAX;
+  int64_t cnt = 0, fb = INF, fterm = INF;
+  if (k < ntiles) {
+    // written by fs_tile (an earlier launch): plain loads, issued together
+    const int64_t mk = rec_meta[k];
+    const bool nxt = k + 1 < ntiles;
+    const int64_t e = nxt ? rec_entry[k + 1] : 0;
+    const int64_t x = rec_exit[k];
+    cnt = m_cnt(mk);
+    if (m_term(mk)) fterm = k;
+    else if (nxt && (e < 0 || e != x)) fb = k + 1;
+  }
+  int64_t tot;
+  const int64_t ex = block_excl_scan(cnt, sm, &tot);
+  if (k < ntiles) base[k] = ex;
+  for (int d = 32; d >= 1; d >>= 1) {
+    fb = min(fb, (int64_t)__shfl_xor(fb, d, 64));
+    fterm = min(fterm, (int64_t)__shfl_xor(fterm, d, 64));
+  }
+  const int wv = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    smin[wv] = fb;
+    smin[FK_T / 64 + wv] = fterm;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int j = 1; j < FK_T / 64; ++j) {
+      fb = min(fb, smin[j]);
+      fterm = min(fterm, smin[FK_T / 64 + j]);
+    }
+    bsum[blockIdx.x] = tot;
+    if (fb != INF) atomicMax((unsigned long long*)&mins[0],
+                             (unsigned long long)(ntiles - fb));
+    if (fterm != INF) atomicMax((unsigned long long*)&mins[1],
+                                (unsigned long long)(ntiles - fterm));
+  }
+}
+
 __global__ __launch_bounds__(FL_T) void fs_link(
     const uint8_t* __restrict__ buf, const int64_t* __restrict__ n_dev,
     int64_t n_cap, int64_t maxp, const int64_t* __restrict__ sx,
     const uint16_t* __restrict__ list, const int32_t* __restrict__ rcount,
     uint16_t* pre, int64_t* rec_entry, int64_t* rec_exit, int64_t* rec_meta,
     int64_t* __restrict__ base, int64_t cap, int64_t* __restrict__ result,
-    uint64_t* stats, int32_t* __restrict__ blist) {
+    uint64_t* stats, int32_t* __restrict__ blist,
+    int64_t* __restrict__ bsum, const uint64_t* __restrict__ mins,
+    int64_t* __restrict__ lastk) {
   __shared__ __attribute__((aligned(16)))
       uint8_t win[(FL_T / 64) * (FC_WIN + 16)];      // one per wave
   __shared__ int64_t red[2 * (FL_T / 64) + 2];
@@ -780,9 +848,50 @@ __global__ __launch_bounds__(FL_T) void fs_link(
   const int64_t ntiles = (n + FT_S - 1) / FT_S;
   if (ntiles == 0) {
     if (tid < 4) result[tid] = 0;
+    if (tid == 0) *lastk = -1;
     return;
   }
   const int64_t INF = INT64_MAX;
+  {
+    // fast path: fs_check found no broken link before the first terminal;
+    // the row bases are bsum's block offsets + fs_check's in-block bases
+    const uint64_t mb = mins[0], mt = mins[1];
+    const int64_t fb0 = mb ? ntiles - (int64_t)mb : INF;
+    const int64_t ft0 = mt ? ntiles - (int64_t)mt : INF;
+    if (fb0 == INF || fb0 > ft0) {
+      const int64_t last = ft0 == INF ? ntiles - 1 : ft0;
+      const int64_t nbl = last / FK_T + 1;
+      const int64_t per = (nbl + FL_T - 1) / FL_T;
+      const int64_t b0 = (int64_t)tid * per;
+      const int64_t b1 = min(b0 + per, nbl);
+      int64_t sum = 0;
+      for (int64_t b = b0; b < b1; ++b) sum += bsum[b];
+      int64_t tot;
+      int64_t run = block_excl_scan(sum, red, &tot);
+      const int64_t blast = last / FK_T;
+      for (int64_t b = b0; b < b1; ++b) {
+        const int64_t v = bsum[b];
+        bsum[b] = run;
+        if (b == blast) {
+          // frames up to `last` (tiles after it in its block are dead)
+          const int64_t ml = rec_meta[last];
+          const int64_t total = run + base[last] + m_cnt(ml);
+          *lastk = last;
+          result[0] = total;
+          result[3] = total > cap ? 1 : 0;
+          if (ft0 == INF) {
+            result[1] = n;
+            result[2] = 0;
+          } else {
+            result[1] = rec_exit[ft0];
+            result[2] = m_bad(ml) ? 1 : 0;
+          }
+        }
+        run += v;
+      }
+      return;
+    }
+  }
   int64_t from = 1, ft = INF;
   bool accel = true;
   for (;;) {
@@ -873,7 +982,10 @@ __global__ __launch_bounds__(FL_T) void fs_link(
     run += m_cnt(ld_agent(&rec_meta[k]));
   }
   for (int64_t k = last + 1 + tid; k < ntiles; k += FL_T) base[k] = -1;
+  // absolute bases: fs_rows adds a zero block offset
+  for (int64_t b = tid; b <= last / FK_T; b += FL_T) bsum[b] = 0;
   if (tid == 0) {
+    *lastk = last;
     result[0] = tot;
     result[3] = tot > cap ? 1 : 0;
     if (ft == INF) {
@@ -891,25 +1003,32 @@ __global__ __launch_bounds__(256) void fs_rows(
     const uint8_t* __restrict__ buf, const int64_t* __restrict__ n_dev,
     int64_t n_cap, const uint16_t* __restrict__ list,
     const uint16_t* __restrict__ pre, const int64_t* __restrict__ rec_meta,
-    const int64_t* __restrict__ base, int64_t* __restrict__ foff,
+    const int64_t* __restrict__ rec_exit,
+    const int64_t* __restrict__ base, const int64_t* __restrict__ bsum,
+    const int64_t* __restrict__ lastk, int64_t* __restrict__ foff,
     int32_t* __restrict__ flen, int64_t cap) {
   const int lane = threadIdx.x & 63;
   const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int64_t n = stream_len(n_dev, n_cap);
-  if (t * FT_S >= n) return;
-  const int64_t b = base[t];
-  if (b < 0) return;
+  if (t * FT_S >= n || t > *lastk) return;
+  const int64_t b = bsum[t / FK_T] + base[t];
   const int64_t m = rec_meta[t];
+  const int64_t x = rec_exit[t];
   const int32_t cnt = m_cnt(m), np = m_np(m), js = m_js(m);
   const int64_t ts = t * FT_S;
   const uint16_t* P = pre + t * FT_LMAX;
   const uint16_t* R = list + t * FT_LMAX + (js < 0 ? 0 : js);
+  // a frame ends where the next one of the chain starts, the tile's last
+  // at the tile's exit (the next tile's first frame, or the stop offset of
+  // a terminal tile): lengths come from the recorded starts, no stream read
   for (int32_t k = lane; k < cnt; k += 64) {
     const int64_t p = ts + (k < np ? P[k] : R[k - np]);
+    const int32_t k1 = k + 1;
+    const int64_t q = k1 < cnt ? ts + (k1 < np ? P[k1] : R[k1 - np]) : x;
     const int64_t idx = b + k;
     if (idx < cap) {
       foff[idx] = p + 4;
-      flen[idx] = ld_be32(buf + p);
+      flen[idx] = (int32_t)(q - p - 4);
     }
   }
 }
@@ -917,7 +1036,7 @@ __global__ __launch_bounds__(256) void fs_rows(
 struct FsPlan {
   int64_t tiles;
   size_t off_list, off_pre, off_sx, off_lbw, off_rent, off_rexit, off_rmeta,
-      off_rcnt, off_base, off_blist, total;
+      off_rcnt, off_base, off_blist, off_bsum, total;
 };
 
 static FsPlan fs_plan(int64_t n) {
@@ -929,13 +1048,15 @@ static FsPlan fs_plan(int64_t n) {
   p.off_list = take((size_t)tiles * FT_LMAX * 2);
   p.off_pre = take((size_t)tiles * FT_LMAX * 2);
   p.off_sx = take((size_t)tiles * 8);
-  p.off_lbw = take((size_t)(2 * tiles + 4) * 8);
+  // X flags (2 per tile), 4 stats words, fs_check's 2 minima, last tile
+  p.off_lbw = take((size_t)(2 * tiles + 7) * 8);
   p.off_rent = take((size_t)tiles * 8);
   p.off_rexit = take((size_t)tiles * 8);
   p.off_rmeta = take((size_t)tiles * 8);
   p.off_rcnt = take((size_t)tiles * 4);
   p.off_base = take((size_t)tiles * 8);
   p.off_blist = take((size_t)tiles * 4);
+  p.off_bsum = take((size_t)(tiles / FK_T + 1) * 8);
   p.total = o;
   return p;
 }
@@ -1010,8 +1131,11 @@ int zk_frame_scan3(const uint8_t* buf, const int64_t* n_dev, int64_t n_cap,
   int32_t* rcnt = (int32_t*)(ws + p.off_rcnt);
   int64_t* base = (int64_t*)(ws + p.off_base);
   int32_t* blist = (int32_t*)(ws + p.off_blist);
-  // X flags, the tile counter and the stats start at zero
-  if (hipMemsetAsync(lbw, 0, (size_t)(2 * tiles + 4) * 8, st) != hipSuccess)
+  int64_t* bsum = (int64_t*)(ws + p.off_bsum);
+  uint64_t* mins = lbw + 2 * tiles + 4;
+  int64_t* lastk = (int64_t*)(lbw + 2 * tiles + 6);
+  // X flags, the stats and fs_check's minima start at zero
+  if (hipMemsetAsync(lbw, 0, (size_t)(2 * tiles + 6) * 8, st) != hipSuccess)
     return -4;
   int64_t* dbg = fs_dbg_buf(tiles);
   // ZKMI_FS_TPB: tiles (waves) per block, 1..4 (A/B)
@@ -1034,12 +1158,16 @@ int zk_frame_scan3(const uint8_t* buf, const int64_t* n_dev, int64_t n_cap,
   }
 #undef ZK_FS_TILE
   ZK_LAUNCH_CHECK();
+  fs_check<<<(unsigned)((tiles + FK_T - 1) / FK_T), FK_T, 0, st>>>(
+      n_dev, n_cap, rent, rexit, rmeta, base, bsum, mins);
+  ZK_LAUNCH_CHECK();
   fs_link<<<1, FL_T, 0, st>>>(buf, n_dev, n_cap, maxp, sx, list, rcnt, pre,
                               rent, rexit, rmeta, base, cap, result,
-                              lbw + 2 * tiles, blist);
+                              lbw + 2 * tiles, blist, bsum, mins, lastk);
   ZK_LAUNCH_CHECK();
   fs_rows<<<(unsigned)((tiles + 3) / 4), 256, 0, st>>>(
-      buf, n_dev, n_cap, list, pre, rmeta, base, foff, flen, cap);
+      buf, n_dev, n_cap, list, pre, rmeta, rexit, base, bsum, lastk, foff,
+      flen, cap);
   ZK_LAUNCH_CHECK();
   return 0;
 }

@@ -804,27 +804,28 @@ __global__ __launch_bounds__(TR_T) void ord_rank_k(int64_t ncap, OrderWs w,
   }
 }
 
-// After a serve / expire launch, one kernel (grid-stride over a bounded
-// grid):
+// After a serve / expire launch, one kernel:
 //  1. rewrite the wire-format Stat words of every dirty parent from the
 //     shadows;
-//  2. the last block to finish publishes: make the nodes freed by the launch
-//     poppable, clamp a head that overshot the previously published tail,
-//     reset the dirty list and consume the launch's zxids (`*n_dev` for a
-//     batch of requests, 1 for a session expiry, which is one closeSession
-//     txn).  Every block reads the dirty count before it signs off on
-//     TC_DONE, so the reset cannot race a reader.
-constexpr int FIN_BLOCKS = 64;   // <= 64 sign-offs on one counter word
+//  2. then (thread 0, after a barrier) publish: make the nodes freed by the
+//     launch poppable, clamp a head that overshot the previously published
+//     tail, reset the dirty list and consume the launch's zxids (`*n_dev`
+//     for a batch of requests, 1 for a session expiry, which is one
+//     closeSession txn).  TC_DONE is no longer used.
+constexpr int FIN_T = 1024;
 
-__global__ __launch_bounds__(TR_T) void tree_finish_k(ZkTree t,
-                                                     const int64_t* n_dev,
-                                                     int64_t bump_zxid,
-                                                     int32_t publish) {
-  __shared__ int last;
+// One workgroup: the dirty list holds the distinct parents a batch touched
+// (a few thousand at most in practice), and a single block needs no
+// cross-block sign-off — the grid version's atomic sign-off counter took
+// 15-60 us per launch on a read-only GET batch, and two streams finishing
+// at once could interleave on it.
+__global__ __launch_bounds__(FIN_T) void tree_finish_k(ZkTree t,
+                                                      const int64_t* n_dev,
+                                                      int64_t bump_zxid,
+                                                      int32_t publish) {
   int64_t* c = t.counters;
   const int64_t nd = c[TC_DIRTY];
-  for (int64_t k = (int64_t)blockIdx.x * TR_T + threadIdx.x; k < nd;
-       k += (int64_t)gridDim.x * TR_T) {
+  for (int64_t k = threadIdx.x; k < nd; k += FIN_T) {
     const int64_t p = t.dirty_list[k];
     uint8_t* slot = t.store.slab + t.store.slot_off[p];
     st_be32(slot + 36, t.cver[p]);
@@ -832,22 +833,14 @@ __global__ __launch_bounds__(TR_T) void tree_finish_k(ZkTree t,
     st_be64(slot + 60, t.pzxid[p]);
     t.dirty[p] = 0;
   }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __threadfence();
-    last = atomicAdd((unsigned long long*)&c[TC_DONE], 1ull) ==
-           (unsigned long long)gridDim.x - 1;
-  }
-  __syncthreads();
-  if (!last || threadIdx.x != 0) return;
-  __threadfence();
+  __syncthreads();                 // every thread has read TC_DIRTY
+  if (threadIdx.x != 0) return;
   if (publish) {
     if (c[TC_FREE_HEAD] > c[TC_FREE_PUB]) c[TC_FREE_HEAD] = c[TC_FREE_PUB];
     c[TC_FREE_PUB] = c[TC_FREE_TAIL];
   }
   c[TC_DIRTY] = 0;
   c[TC_ZXID] += n_dev != nullptr ? *n_dev : bump_zxid;
-  c[TC_DONE] = 0;
 }
 
 // Session expiry: remove every ephemeral node owned by `session`
@@ -904,11 +897,8 @@ int zk_tree_build(const ZkTree* t, int64_t n0, int64_t n, hipStream_t st) {
 static int finish_launch(const ZkTree* t, int64_t ncap, const int64_t* n_dev,
                          int64_t bump_zxid, hipStream_t st,
                          int32_t publish = 1) {
-  // the dirty list holds at most one parent per request
-  const int64_t nb = min((ncap + zk::TR_T - 1) / zk::TR_T,
-                         (int64_t)zk::FIN_BLOCKS);
-  zk::tree_finish_k<<<(unsigned)nb, zk::TR_T, 0, st>>>(*t, n_dev, bump_zxid,
-                                                      publish);
+  (void)ncap;
+  zk::tree_finish_k<<<1, zk::FIN_T, 0, st>>>(*t, n_dev, bump_zxid, publish);
   ZK_LAUNCH_CHECK();
   return 0;
 }

@@ -439,6 +439,24 @@ def test_gpu_get_pipeline_two_connections(gpu):
     assert [p.batch for p in pipe.subs] == [4097, 4096]
 
 
+def test_gpu_get_pipeline_staggered_streams(gpu):
+    """bench's default: the second connection runs half a step (2 phases)
+    behind the first; each step() issues one step of work per connection
+    and the lagging connection's checks land one call later."""
+    from zkmi.bench.synthetic import GetPipeline
+    tree = _small_tree(gpu, 20000, 37)
+    pipe = GetPipeline(tree, 8193, streams=2, stagger=True)
+    acc = torch.zeros(1, dtype=torch.int64, device=gpu)
+    pipe.step(acc=acc)
+    assert int(acc.item()) == 4097              # connection 1 not checked yet
+    for _ in range(3):
+        pipe.step(acc=acc)
+    assert int(acc.item()) == 4 * 4097 + 3 * 4096
+    acc.zero_()
+    pipe.step(acc=acc)
+    assert int(acc.item()) == 8193              # steady state: a full step
+
+
 def test_gpu_tree_mutations(gpu):
     """SET_DATA version CAS, CREATE (parent must exist, NODE_EXISTS),
     DELETE through the GPU server, checked reply by reply."""

@@ -306,9 +306,19 @@ class GpuServer(object):
         SYSTEMERROR, see :meth:`order_stats`).  Reads and sets followed by
         a write to their path snapshot their reply into the tree's
         ``scratch``.  Without it requests of a batch are concurrent."""
+        for _ in self.serve_steps(rx, n, session, terminate, ordered, passes):
+            pass
+        return self.result
+
+    def serve_steps(self, rx, n, session=0, terminate=False, ordered=False,
+                    passes=4):
+        """:meth:`serve` as a generator yielding once, between the request
+        decode and the tree; the return tuple lands in ``self.result`` (a
+        pipelined caller interleaves another connection's work there)."""
         L = _lib.lib()
         ft = self.scanner.scan(rx, n)
         rt = B.decode_requests(rx, ft, out=self.rt)
+        yield
         r = self.resp
         r.count = ft.count
         out = [r.opcode, r.xid, r.err, r.node, r.zxid, r.path_off,
@@ -329,7 +339,7 @@ class GpuServer(object):
             r, self.tree.store, self.out.numel(), out=self.out,
             presized=self.presized, terminate=terminate)
         self.last_rec_off = rec_off         # reply frame starts (R2 splits)
-        return out, total, err, ft
+        self.result = (out, total, err, ft)
 
     def order_stats(self):
         """(largest same-path rank, scratch bytes used) of the last ordered
@@ -342,7 +352,9 @@ class GpuServer(object):
 class GetPipeline(object):
     """Batched get() over the synthetic tree (BASELINE config 2)."""
 
-    def __init__(self, tree, batch, seed=0, streams=1):
+    PHASES = 4          # client encode | server decode | tree + encode | client
+
+    def __init__(self, tree, batch, seed=0, streams=1, stagger=False):
         self.tree = tree
         self.batch = batch
         dev = tree.device
@@ -350,15 +362,23 @@ class GetPipeline(object):
         self.subs = []
         if streams > 1:
             # `streams` independent pipelined connections, each with its own
-            # HIP stream, buffers and xid table, sharing the tree.  Their
-            # phases are issued round-robin (see step), so one connection's
-            # latency-bound kernels (frame-scan walks, composition, scans)
-            # and host read-backs overlap another's bandwidth-bound ones.
+            # HIP stream, buffers and xid table, sharing the (read-only)
+            # tree.  Their phases are issued round-robin (see step), so one
+            # connection's latency-bound kernels (frame-scan walks, scans)
+            # overlap another's bandwidth-bound ones.  `stagger`: connection
+            # k runs k * PHASES / streams phases behind connection 0 (the
+            # steady state of pipelined connections), so the frame scans of
+            # one meet the encoders and tree of another instead of their own
+            # copies; a step still issues PHASES phases of every connection,
+            # and a connection's reply check lands in the step() call that
+            # runs its last phase.
             per = [batch // streams + (1 if k < batch % streams else 0)
                    for k in range(streams)]
             self.subs = [GetPipeline(tree, m, seed=seed * streams + k)
                          for k, m in enumerate(per)]
             self.streams = [torch.cuda.Stream(dev) for _ in per]
+            self.stagger = stagger
+            self._gens = None
             self.last = None
             return
         self.xt = B.XidTable(bits=max(20, (batch - 1).bit_length() + 1),
@@ -403,6 +423,21 @@ class GetPipeline(object):
                 pass
             return acc if validate else None
         cur = torch.cuda.current_stream(self.dev)
+        if self.stagger:
+            for s in self.streams:
+                s.wait_stream(cur)
+            self._validate, self._acc = validate, acc
+            if self._gens is None:
+                ns = len(self.subs)
+                self._gens = [p._forever(self, k * self.PHASES // ns)
+                              for k, p in enumerate(self.subs)]
+            for _ in range(self.PHASES):
+                for s, g in zip(self.streams, self._gens):
+                    with torch.cuda.stream(s):
+                        next(g)
+            for s in self.streams:
+                cur.wait_stream(s)
+            return acc if validate else None
         live = []
         for p, s in zip(self.subs, self.streams):
             s.wait_stream(cur)
@@ -418,10 +453,22 @@ class GetPipeline(object):
             cur.wait_stream(s)
         return acc if validate else None
 
-    def _phases(self, validate, acc):
+    def _forever(self, parent, lag):
+        """Phases of step after step, one per next(), starting ``lag`` idle
+        phases late; the validation flag and counter are the parent's at
+        the time of the check."""
+        for _ in range(lag):
+            yield
+        while True:
+            for _ in self._phases(None, None, parent):
+                yield           # after each of the first PHASES - 1 phases
+            yield               # after the last
+
+    def _phases(self, validate, acc, parent=None):
         """The step as a generator on the caller's current stream, yielding
-        between client encode, server and client decode (a multi-stream
-        step interleaves the connections' phases)."""
+        between its PHASES phases (client encode, server frame scan and
+        decode, tree and reply encode, client decode and check); a
+        multi-stream step interleaves the connections' phases."""
         t = self.tree
         n = self.batch
         L = _lib.lib()
@@ -437,11 +484,18 @@ class GetPipeline(object):
                             self.acl_len, self.acl_arena)
         tx, rec_off, total, err = B.encode_requests(rb, self.xt, out=self.tx)
         yield
-        rx, rtotal, rerr, _ = self.server.serve(tx, _len(total))
+        srv = self.server.serve_steps(tx, _len(total))
+        next(srv)
+        yield
+        for _ in srv:
+            pass
+        rx, rtotal, rerr, _ = self.server.result
         yield
         ft = self.rscanner.scan(rx, _len(rtotal))
         rep = B.decode_replies(rx, ft, self.xt, out=self.reply)
         self.last = (self.idx, rep, rx, ft)
+        if parent is not None:
+            validate, acc = parent._validate, parent._acc
         if not validate:
             return
         L.bench_check_get(n, rep.tensors(), self.idx, xid, t.data_len, acc)

@@ -409,25 +409,41 @@ __global__ __launch_bounds__(256) void fs_tile(
     const int sl = (int)__builtin_ctzll(sm);
     int32_t c = __builtin_amdgcn_readlane(mp, sl);
     uint32_t ent = 0;
-    for (;;) {
-      if (c >= nrel) {                       // reached the stream end
-        send = TERM | (ts + c);
-        break;
+    // The hot loop of the scan (one hop per frame of the tile, serial):
+    // kept to a few scalar compares per hop — one unsigned test covers a
+    // negative or oversize length, one bound (min(tile end, stream end))
+    // both ways out, and the frame start goes into lane m & 63 of `ent`
+    // (a compare and a select).  The rare exits are classified on the way
+    // out.
+    // (The round-2 loop spent ~45 instructions per hop on mixed VALU/SALU
+    // tests; at ~7 waves per SIMD that issue cost, not the LDS latency,
+    // set the ~300 ns per hop measured with ZKMI_FS_DBG.)
+    const int32_t lim = min((int32_t)FT_S, nrel);
+    if (c >= nrel) {
+      send = TERM | (ts + c);                // reached the stream end
+    } else {
+      for (;;) {
+        const int32_t len = __builtin_amdgcn_readfirstlane(lds_be32(sb, c));
+        const int32_t nx = c + 4 + len;
+        if ((uint32_t)len > (uint32_t)maxp32 || nx > nrel) {
+          const bool bad = (c + 4 <= nrel) && ((len < 0) | (len > maxp32));
+          send = TERM | (bad ? TBAD : 0) | (ts + c);
+          break;
+        }
+        ent = lane == (m & 63) ? (uint32_t)c : ent;
+        ++m;
+        if ((m & 63) == 0) L[m - 64 + lane] = (uint16_t)ent;
+        if (nx >= lim) {
+          if (nx >= FT_S) {
+            send = ts + nx;
+            if (lane == 0) ft_mark_exit(xbits, nx - FT_S, W);
+          } else {
+            send = TERM | (ts + nx);         // the stream ends at nx
+          }
+          break;
+        }
+        c = nx;
       }
-      const int32_t len = __builtin_amdgcn_readfirstlane(lds_be32(sb, c));
-      const int32_t nx = c + 4 + len;
-      if ((c + 4 > nrel) | (len < 0) | (len > maxp32) | (nx > nrel)) {
-        const bool bad = (c + 4 <= nrel) && ((len < 0) | (len > maxp32));
-        send = TERM | (bad ? TBAD : 0) | (ts + c);
-        break;
-      }
-      ft_record(L, m, ent, c, lane);
-      if (nx >= FT_S) {
-        send = ts + nx;
-        if (lane == 0) ft_mark_exit(xbits, nx - FT_S, W);
-        break;
-      }
-      c = nx;
     }
     if (lane < (m & 63)) L[(m & ~63) + lane] = (uint16_t)ent;
     // survivor bit map for the join walk, from the list just stored (each

@@ -258,6 +258,11 @@ def main():
                          'with the other\'s bandwidth-bound ones, more '
                          'streams than GPU_MAX_HW_QUEUES allows were '
                          'unstable)')
+    ap.add_argument('--no-graph', action='store_true',
+                    help='get: time eager steps instead of replays of one '
+                         'step captured as a HIP graph after the warmup '
+                         '(every replay draws a new batch from a '
+                         'device-resident seed; ~2%% faster than eager)')
     ap.add_argument('--stagger', action='store_true',
                     help='get: offset the pipelined connections by half a '
                          'step (measured no faster than lockstep, 0.80 vs 0.79 ms)')
@@ -356,6 +361,13 @@ def main():
     ok_total = torch.zeros(1, dtype=torch.int64, device=dev)
     for _ in range(a.warmup):
         pipe.step(acc=ok_total)
+    run = lambda: pipe.step(acc=ok_total)            # noqa: E731
+    a.graph = not a.no_graph and hasattr(pipe, 'capture')
+    if a.graph:
+        g = pipe.capture(ok_total)
+        run = g.replay
+        for _ in range(2):
+            run()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -363,7 +375,7 @@ def main():
     ok_total.zero_()
     t0 = time.perf_counter()
     for _ in range(a.steps):
-        pipe.step(acc=ok_total)
+        run()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -416,6 +428,7 @@ def main():
             'scaling': 'weak',
             'vs_baseline': value / REF_PKTS_PER_S,
             'dtype': 'uint8',
+            'hip_graph': bool(a.graph),
             'data': 'synthetic',
             'config': {
                 'model': 'zk-%s%s %dk-znode tree, %s data%s' % (

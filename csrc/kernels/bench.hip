@@ -23,9 +23,17 @@ __global__ __launch_bounds__(BG_T) void bench_gen_get(
     int64_t n, uint64_t seed, int64_t leaf0, int64_t nleaves,
     int32_t xid_base, const int64_t* __restrict__ node_pw,
     int64_t* __restrict__ idx, int32_t* __restrict__ xid,
-    int64_t* __restrict__ path_off, int32_t* __restrict__ path_len) {
+    int64_t* __restrict__ path_off, int32_t* __restrict__ path_len,
+    const int64_t* __restrict__ state) {
   const int64_t i = (int64_t)blockIdx.x * BG_T + threadIdx.x;
   if (i >= n) return;
+  if (state != nullptr) {
+    // device-resident {seed, step} (a captured graph replays new batches):
+    // the step's seed and xids derive from the step counter
+    const uint64_t st = (uint64_t)state[1];
+    seed = (uint64_t)state[0] * 0x9E3779B97F4A7C15ull + st;
+    xid_base = (int32_t)((st * (uint64_t)n) & 0x7fffffffu);
+  }
   const uint64_t r = splitmix64(seed ^ (uint64_t)i * 0xD1B54A32D192ED03ull);
   // multiply-shift range reduction (bias < 2^-32 for 1M leaves)
   const int64_t v = leaf0 + (int64_t)(((r >> 32) * (uint64_t)nleaves) >> 32);
@@ -128,11 +136,11 @@ int zk_bench_check_notif(int64_t total, int64_t n_per, const uint64_t* seeds,
 int zk_bench_gen_get(int64_t n, uint64_t seed, int64_t leaf0, int64_t nleaves,
                      int32_t xid_base, const int64_t* node_pw, int64_t* idx,
                      int32_t* xid, int64_t* path_off, int32_t* path_len,
-                     hipStream_t st) {
+                     const int64_t* state, hipStream_t st) {
   if (n <= 0) return 0;
   zk::bench_gen_get<<<(unsigned)((n + zk::BG_T - 1) / zk::BG_T), zk::BG_T, 0,
                       st>>>(n, seed, leaf0, nleaves, xid_base, node_pw, idx,
-                            xid, path_off, path_len);
+                            xid, path_off, path_len, state);
   ZK_LAUNCH_CHECK();
   return 0;
 }

@@ -111,7 +111,7 @@ int zk_tree_expire(const ZkTree*, int64_t, int64_t, unsigned long long*,
                    hipStream_t);
 int zk_bench_gen_get(int64_t, uint64_t, int64_t, int64_t, int32_t,
                      const int64_t*, int64_t*, int32_t*, int64_t*, int32_t*,
-                     hipStream_t);
+                     const int64_t*, hipStream_t);
 int zk_bench_check_get(int64_t, const int32_t*, const int32_t*,
                        const int32_t*, const int32_t*, const int64_t*,
                        const int32_t*, const int64_t*, const int32_t*,
@@ -677,9 +677,11 @@ void tree_expire(const std::vector<Tensor>& t, int64_t session, int64_t ncap,
 
 void bench_gen_get(int64_t n, int64_t seed, int64_t leaf0, int64_t nleaves,
                    int64_t xid_base, const Tensor& node_pw, const Tensor& idx,
-                   const Tensor& xid, const Tensor& poff, const Tensor& plen) {
+                   const Tensor& xid, const Tensor& poff, const Tensor& plen,
+                   const c10::optional<Tensor>& state) {
   TORCH_CHECK(leaf0 >= 0 && leaf0 + nleaves <= node_pw.numel(),
               "zkmi: bench_gen_get leaf range");
+  TORCH_CHECK(nleaves > 0, "zkmi: bench_gen_get needs leaves");
   hip_ok(zk_bench_gen_get(n, (uint64_t)seed, leaf0, nleaves,
                           (int32_t)xid_base,
                           P<int64_t>(node_pw, I64, 1, "node_pw"),
@@ -687,6 +689,7 @@ void bench_gen_get(int64_t n, int64_t seed, int64_t leaf0, int64_t nleaves,
                           P<int32_t>(xid, I32, n, "xid", &node_pw),
                           P<int64_t>(poff, I64, n, "path_off", &node_pw),
                           P<int32_t>(plen, I32, n, "path_len", &node_pw),
+                          Popt<int64_t>(state, I64, 2, "state", &node_pw),
                           cur_stream()),
          "bench_gen_get");
 }
@@ -856,7 +859,8 @@ TORCH_LIBRARY(zkmi, m) {
         "Tensor(b!) removed) -> ()", &tree_expire);
   m.def("bench_gen_get(int n, int seed, int leaf0, int nleaves, "
         "int xid_base, Tensor node_pw, Tensor(a!) idx, Tensor(b!) xid, "
-        "Tensor(c!) path_off, Tensor(d!) path_len) -> ()", &bench_gen_get);
+        "Tensor(c!) path_off, Tensor(d!) path_len, Tensor? state=None) "
+        "-> ()", &bench_gen_get);
   m.def("bench_check_get(int n, Tensor[] reply, Tensor idx, Tensor xid, "
         "Tensor data_len, Tensor(a!) acc) -> ()", &bench_check_get);
   m.def("bench_check_notif(int total, int n_per, Tensor seeds, int leaf0, "

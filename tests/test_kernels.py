@@ -439,6 +439,26 @@ def test_gpu_get_pipeline_two_connections(gpu):
     assert [p.batch for p in pipe.subs] == [4097, 4096]
 
 
+def test_gpu_get_pipeline_graph_replay(gpu):
+    """bench --graph: one step captured as a HIP graph; every replay draws
+    a NEW batch (device-resident seed) and checks all its replies."""
+    from zkmi.bench.synthetic import GetPipeline
+    tree = _small_tree(gpu, 20000, 37)
+    pipe = GetPipeline(tree, 8193, streams=2)
+    acc = torch.zeros(1, dtype=torch.int64, device=gpu)
+    pipe.step(acc=acc)
+    acc.zero_()
+    g = pipe.capture(acc)
+    seen = []
+    for _ in range(3):
+        g.replay()
+        torch.cuda.synchronize()
+        seen.append(pipe.subs[0].idx[:64].clone())
+    assert int(acc.item()) == 3 * 8193
+    assert not torch.equal(seen[0], seen[1])
+    assert not torch.equal(seen[1], seen[2])
+
+
 def test_gpu_get_pipeline_staggered_streams(gpu):
     """bench's default: the second connection runs half a step (2 phases)
     behind the first; each step() issues one step of work per connection

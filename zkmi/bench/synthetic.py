@@ -410,6 +410,30 @@ class GetPipeline(object):
         self.xid = torch.empty(n, dtype=I32, device=dev)
         self.poff = torch.empty(n, dtype=I64, device=dev)
         self.plen = torch.empty(n, dtype=I32, device=dev)
+        self.gstate = None      # device {seed, step} (see capture)
+
+    def _device_seed(self):
+        """Draw each step's requests from a device-resident {seed, step}
+        pair advanced on the device, so a captured graph replays NEW
+        batches (a host seed would be frozen into the graph)."""
+        for p in self.subs or [self]:
+            if p.gstate is None:
+                p.gstate = torch.tensor([p.seed, p.step_no], dtype=I64,
+                                        device=self.dev)
+
+    def capture(self, acc):
+        """Capture one step (validated into ``acc``, which every replay adds
+        to) as a HIP graph: a step's ~50 launches over two streams replay
+        with one host call.  Run at least one eager step first (buffers
+        are sized then).  Returns the graph; ``graph.replay()`` is a step.
+        """
+        self._device_seed()
+        torch.cuda.synchronize(self.dev)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self.step(acc=acc)
+        self.graph = g
+        return g
 
     def step(self, validate=True, acc=None):
         """One batch.  With ``validate`` the number of correct replies is
@@ -475,7 +499,10 @@ class GetPipeline(object):
         seed = (self.seed * 0x9E3779B97F4A7C15 + self.step_no) & (2**64 - 1)
         self.step_no += 1
         L.bench_gen_get(n, _i64(seed), t.leaf0, t.n_leaves, self.xid_base,
-                        t.node_pw, self.idx, self.xid, self.poff, self.plen)
+                        t.node_pw, self.idx, self.xid, self.poff, self.plen,
+                        self.gstate)
+        if self.gstate is not None:
+            self.gstate[1:].add_(1)         # next step (on the device)
         xid = self.xid
         self.xid_base = (self.xid_base + n) & 0x7fffffff
         rb = B.RequestBatch(n, self.opcode, xid, self.arg, self.poff,

@@ -358,7 +358,9 @@ def main():
             pipe = S.StormPipeline(tree, a.batch, seed=rank)
             per_step = pipe.n
 
-    ok_total = torch.zeros(1, dtype=torch.int64, device=dev)
+    # 64 counter slots (the fused GET check spreads its per-block atomics
+    # over them); the other checks add into slot 0
+    ok_total = torch.zeros(64, dtype=torch.int64, device=dev)
     for _ in range(a.warmup):
         pipe.step(acc=ok_total)
     run = lambda: pipe.step(acc=ok_total)            # noqa: E731
@@ -383,7 +385,7 @@ def main():
     elapsed = time.perf_counter() - t0
 
     el = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
-    ok = ok_total.to(cdev)
+    ok = ok_total.sum().view(1).to(cdev)
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
         dist.all_reduce(ok, op=dist.ReduceOp.SUM)   # R4: node-level counters

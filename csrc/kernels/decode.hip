@@ -13,6 +13,7 @@
 // expanded by a second pass after a scan of the per-frame counts.
 #include "zk_common.h"
 #include "zk_batch.h"
+#include "zk_reqparse.h"
 
 namespace zk {
 
@@ -55,40 +56,33 @@ ZK_DEV bool read_stat(const uint8_t* p, const ZkReplyOut& o, int64_t i) {
   return true;
 }
 
-// Walk `count` ustrings starting at p; returns bytes consumed or -1.
-ZK_DEV int64_t skip_strings(const uint8_t* p, int64_t avail, int32_t count) {
-  int64_t k = 0;
-  for (int32_t j = 0; j < count; ++j) {
-    if (k + 4 > avail) return -1;
-    int32_t l = ld_be32(p + k);
-    if (l < 0) l = 0;
-    k += 4 + l;
-    if (k > avail) return -1;
-  }
-  return k;
-}
 
-// ACL vector entries: perms i32, scheme ustring, id ustring.
-ZK_DEV int64_t skip_acl(const uint8_t* p, int64_t avail, int32_t count) {
-  int64_t k = 0;
-  for (int32_t j = 0; j < count; ++j) {
-    if (k + 4 > avail) return -1;
-    k += 4;
-    int64_t s = skip_strings(p + k, avail - k, 2);
-    if (s < 0) return -1;
-    k += s;
-  }
-  return k;
-}
+// Optional fused check of GET_DATA replies against the requests that were
+// sent (the benchmark's validation, otherwise a separate pass over the SoA
+// it just wrote): reply i must be a clean GET_DATA success for request i —
+// same xid, the node's czxid (idx + 1) and data length.  Counts go to
+// acc[block % slots] (one atomic per block, spread over the slots so the
+// blocks of a launch do not queue on one word).
+struct ZkGetCheck {
+  const int64_t* idx;
+  const int32_t* xid;
+  const int32_t* data_len;
+  unsigned long long* acc;
+  int32_t slots;
+};
 
+template <bool CHECK>
 __global__ __launch_bounds__(DEC_T) void decode_replies_k(
     const uint8_t* __restrict__ buf, const int64_t* __restrict__ foff,
     const int32_t* __restrict__ flen, const int64_t* __restrict__ n_dev,
     int64_t ncap, const int64_t* __restrict__ xid_tab, int64_t xid_mask,
-    ZkReplyOut o) {
+    ZkReplyOut o, ZkGetCheck chk) {
   const uint32_t nwg = gridDim.x;
   const int64_t i = (int64_t)xcd_remap(blockIdx.x, nwg) * DEC_T + threadIdx.x;
-  if (i >= ncap || i >= *n_dev) return;
+  const bool live = i < ncap && i < *n_dev;
+  if (!CHECK && !live) return;
+  int64_t good = 0;
+  if (live) {
   const uint8_t* p = buf + foff[i];
   const int64_t L = flen[i];
   int32_t status = ST_OK;
@@ -210,6 +204,20 @@ __global__ __launch_bounds__(DEC_T) void decode_replies_k(
   o.pay_len[i] = plen;
   o.aux0[i] = a0;
   o.aux1[i] = a1;
+  if (CHECK && status == ST_OK && err == ERR_OK && op == OP_GET_DATA) {
+    const int64_t v = chk.idx[i];
+    good = xid == chk.xid[i] && o.stat64[i] == v + 1 &&
+           plen == chk.data_len[v];
+  }
+  }  // live
+  if (CHECK) {
+    __shared__ int64_t sm[DEC_T / 64 + 1];
+    int64_t tot;
+    block_excl_scan(good, sm, &tot);
+    if (threadIdx.x == 0 && tot)
+      atomicAdd(&chk.acc[blockIdx.x % (uint32_t)chk.slots],
+                (unsigned long long)tot);
+  }
 }
 
 // Expand string vectors: region (offset of first string) + count per row ->
@@ -268,95 +276,18 @@ __global__ __launch_bounds__(DEC_T) void decode_requests_k(
   const uint32_t nwg = gridDim.x;
   const int64_t i = (int64_t)xcd_remap(blockIdx.x, nwg) * DEC_T + threadIdx.x;
   if (i >= ncap || i >= *n_dev) return;
-  const int64_t base = foff[i];
-  const uint8_t* p = buf + base;
-  const int64_t L = flen[i];
-  int32_t status = ST_OK, xid = 0, op = OP_UNKNOWN, arg = 0;
-  int64_t poff = -1, doff = -1, voff = -1, rel = 0;
-  int32_t pl = 0, dl = 0, vc = 0;
-  if (L < 8) {
-    status = ST_BAD_DECODE;
-  } else {
-    xid = ld_be32(p);
-    op = ld_be32(p + 4);
-    int64_t k = 8;
-    auto get_str = [&](int64_t& off, int32_t& len) -> bool {
-      if (k + 4 > L) return false;
-      int32_t l = ld_be32(p + k);
-      if (l < 0) l = 0;
-      if (k + 4 + l > L) return false;
-      off = base + k + 4;
-      len = l;
-      k += 4 + l;
-      return true;
-    };
-    auto get_i32 = [&](int32_t& v) -> bool {
-      if (k + 4 > L) return false;
-      v = ld_be32(p + k);
-      k += 4;
-      return true;
-    };
-    bool ok = true;
-    switch (op) {
-      case OP_GET_DATA: case OP_EXISTS: case OP_GET_CHILDREN:
-      case OP_GET_CHILDREN2:
-        ok = get_str(poff, pl) && k + 1 <= L;
-        if (ok) { arg = p[k]; ok = (arg == 0 || arg == 1); ++k; }
-        break;
-      case OP_CREATE: {
-        ok = get_str(poff, pl) && get_str(doff, dl) && get_i32(vc);
-        if (!ok) break;
-        if (vc < 0) vc = 0;
-        voff = base + k;
-        const int64_t s = skip_acl(p + k, L - k, vc);
-        ok = s >= 0;
-        if (ok) { k += s; ok = get_i32(arg); }
-        break;
-      }
-      case OP_DELETE:
-        ok = get_str(poff, pl) && get_i32(arg);
-        break;
-      case OP_SET_DATA:
-        ok = get_str(poff, pl) && get_str(doff, dl) && get_i32(arg);
-        break;
-      case OP_GET_ACL: case OP_SYNC:
-        ok = get_str(poff, pl);
-        break;
-      case OP_SET_WATCHES: {
-        if (k + 8 > L) { ok = false; break; }
-        rel = ld_be64(p + k);
-        k += 8;
-        voff = base + k;
-        for (int g = 0; g < 3 && ok; ++g) {
-          int32_t c;
-          ok = get_i32(c);
-          if (!ok) break;
-          c = max(c, 0);
-          const int64_t s = skip_strings(p + k, L - k, c);
-          ok = s >= 0;
-          k += s;
-          vc += c;
-        }
-        break;
-      }
-      case OP_PING: case OP_CLOSE_SESSION:
-        break;
-      default:
-        status = ST_BAD_OPCODE;
-    }
-    if (!ok) status = ST_BAD_DECODE;
-  }
-  o.xid[i] = xid;
-  o.opcode[i] = op;
-  o.status[i] = status;
-  o.path_off[i] = poff;
-  o.path_len[i] = pl;
-  o.data_off[i] = doff;
-  o.data_len[i] = dl;
-  o.arg[i] = arg;
-  o.vec_off[i] = voff;
-  o.vec_count[i] = vc;
-  o.rel_zxid[i] = rel;
+  const ReqFields f = parse_request(buf, foff[i], flen[i]);
+  o.xid[i] = f.xid;
+  o.opcode[i] = f.op;
+  o.status[i] = f.status;
+  o.path_off[i] = f.poff;
+  o.path_len[i] = f.pl;
+  o.data_off[i] = f.doff;
+  o.data_len[i] = f.dl;
+  o.arg[i] = f.arg;
+  o.vec_off[i] = f.voff;
+  o.vec_count[i] = f.vc;
+  o.rel_zxid[i] = f.rel;
 }
 
 // ---------------------------------------------------------------- K9
@@ -403,8 +334,28 @@ int zk_decode_replies(const uint8_t* buf, const int64_t* foff,
                       const int64_t* xid_tab, int64_t xid_mask,
                       const ZkReplyOut* o, hipStream_t st) {
   if (ncap <= 0) return 0;
-  zk::decode_replies_k<<<zk::nblk(ncap), zk::DEC_T, 0, st>>>(
-      buf, foff, flen, n_dev, ncap, xid_tab, xid_mask, *o);
+  zk::decode_replies_k<false><<<zk::nblk(ncap), zk::DEC_T, 0, st>>>(
+      buf, foff, flen, n_dev, ncap, xid_tab, xid_mask, *o,
+      zk::ZkGetCheck{nullptr, nullptr, nullptr, nullptr, 1});
+  ZK_LAUNCH_CHECK();
+  return 0;
+}
+
+// zk_decode_replies + the fused GET_DATA check (ZkGetCheck): idx / xid are
+// the requests sent (ncap of them), data_len the tree's per-node lengths,
+// acc `slots` (1..64) int64 counters the caller sums.
+int zk_decode_replies_check(const uint8_t* buf, const int64_t* foff,
+                            const int32_t* flen, const int64_t* n_dev,
+                            int64_t ncap, const int64_t* xid_tab,
+                            int64_t xid_mask, const ZkReplyOut* o,
+                            const int64_t* idx, const int32_t* xid,
+                            const int32_t* data_len, unsigned long long* acc,
+                            int32_t slots, hipStream_t st) {
+  if (ncap <= 0) return 0;
+  if (slots < 1 || slots > 64) return (int)hipErrorInvalidValue;
+  zk::decode_replies_k<true><<<zk::nblk(ncap), zk::DEC_T, 0, st>>>(
+      buf, foff, flen, n_dev, ncap, xid_tab, xid_mask, *o,
+      zk::ZkGetCheck{idx, xid, data_len, acc, slots});
   ZK_LAUNCH_CHECK();
   return 0;
 }

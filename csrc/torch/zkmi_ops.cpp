@@ -80,6 +80,11 @@ int zk_frame_scan_dbg(int64_t* host, int64_t tiles);
 int zk_decode_replies(const uint8_t*, const int64_t*, const int32_t*,
                       const int64_t*, int64_t, const int64_t*, int64_t,
                       const ZkReplyOut*, hipStream_t);
+int zk_decode_replies_check(const uint8_t*, const int64_t*, const int32_t*,
+                            const int64_t*, int64_t, const int64_t*, int64_t,
+                            const ZkReplyOut*, const int64_t*, const int32_t*,
+                            const int32_t*, unsigned long long*, int32_t,
+                            hipStream_t);
 int zk_expand_strings(const uint8_t*, const int64_t*, const int32_t*,
                       const int64_t*, int64_t, int64_t*, int32_t*,
                       hipStream_t);
@@ -99,6 +104,11 @@ int zk_tree_serve(const ZkTree*, const uint8_t*, const ZkReqOut*,
                   const int64_t*, int64_t, int32_t*, int32_t*, int32_t*,
                   int64_t*, int64_t*, int64_t*, int32_t*, int64_t*, int64_t*,
                   int64_t*, int64_t, int64_t, hipStream_t);
+int zk_tree_serve_frames(const ZkTree*, const uint8_t*, const int64_t*,
+                         const int32_t*, const int64_t*, int64_t, int32_t*,
+                         int32_t*, int32_t*, int64_t*, int64_t*, int64_t*,
+                         int32_t*, int64_t*, int64_t*, int64_t*, int64_t,
+                         int64_t, hipStream_t);
 int zk_tree_serve_ordered(const ZkTree*, const uint8_t*, const ZkReqOut*,
                           const int64_t*, int64_t, int32_t*, int32_t*,
                           int32_t*, int64_t*, int64_t*, int64_t*, int32_t*,
@@ -498,6 +508,34 @@ void decode_replies(const Tensor& buf, const Tensor& foff, const Tensor& flen,
          "decode_replies");
 }
 
+// decode_replies + the fused GET_DATA check (bench validation): request i
+// was (idx[i], xid[i]); counts of good replies go to acc (1..64 slots,
+// summed by the caller).
+void decode_replies_check(const Tensor& buf, const Tensor& foff,
+                          const Tensor& flen, const Tensor& n_dev,
+                          const Tensor& xid_tab, int64_t xid_mask,
+                          const std::vector<Tensor>& out, const Tensor& idx,
+                          const Tensor& xid, const Tensor& data_len,
+                          const Tensor& acc) {
+  const int64_t cap = foff.numel();
+  ZkReplyOut o = reply_out(out, cap, &buf);
+  const int32_t slots = (int32_t)std::min<int64_t>(acc.numel(), 64);
+  TORCH_CHECK(slots >= 1, "zkmi: decode_replies_check needs an acc slot");
+  hip_ok(zk_decode_replies_check(
+             P<uint8_t>(buf, U8, 1, "buf"),
+             P<int64_t>(foff, I64, cap, "frame_off", &buf),
+             P<int32_t>(flen, I32, cap, "frame_len", &buf),
+             P<int64_t>(n_dev, I64, 1, "count", &buf), cap,
+             P<int64_t>(xid_tab, I64, xid_mask + 1, "xid_tab", &buf),
+             xid_mask, &o, P<int64_t>(idx, I64, cap, "idx", &buf),
+             P<int32_t>(xid, I32, cap, "xid", &buf),
+             P<int32_t>(data_len, I32, 1, "data_len", &buf),
+             reinterpret_cast<unsigned long long*>(
+                 P<int64_t>(acc, I64, slots, "acc", &buf)),
+             slots, cur_stream()),
+         "decode_replies_check");
+}
+
 void expand_strings(const Tensor& buf, const Tensor& region,
                     const Tensor& count, const Tensor& base,
                     const Tensor& soff, const Tensor& slen) {
@@ -604,6 +642,36 @@ void tree_serve(const std::vector<Tensor>& t, const Tensor& rx,
              P<int64_t>(r[9], I64, nb, "r.block_sums", d), session, now_ms,
              cur_stream()),
          "tree_serve");
+}
+
+// tree_serve from K1's frame table: each lane parses its request frame in
+// registers (no K12 decode pass).
+void tree_serve_frames(const std::vector<Tensor>& t, const Tensor& rx,
+                       const Tensor& foff, const Tensor& flen,
+                       const Tensor& n_dev, int64_t ncap,
+                       const std::vector<Tensor>& r, int64_t session,
+                       int64_t now_ms) {
+  ZkTree s = tree(t);
+  const Tensor* d = &t[0];
+  need(r, 10, "serve outputs");
+  const int64_t nb = (ncap + 255) / 256;
+  hip_ok(zk_tree_serve_frames(
+             &s, P<uint8_t>(rx, U8, 1, "rx", d),
+             P<int64_t>(foff, I64, ncap, "frame_off", d),
+             P<int32_t>(flen, I32, ncap, "frame_len", d),
+             P<int64_t>(n_dev, I64, 1, "count", d), ncap,
+             P<int32_t>(r[0], I32, ncap, "r.opcode", d),
+             P<int32_t>(r[1], I32, ncap, "r.xid", d),
+             P<int32_t>(r[2], I32, ncap, "r.err", d),
+             P<int64_t>(r[3], I64, ncap, "r.node", d),
+             P<int64_t>(r[4], I64, ncap, "r.zxid", d),
+             P<int64_t>(r[5], I64, ncap, "r.path_off", d),
+             P<int32_t>(r[6], I32, ncap, "r.path_len", d),
+             P<int64_t>(r[7], I64, ncap, "r.slot", d),
+             P<int64_t>(r[8], I64, ncap, "r.sizes", d),
+             P<int64_t>(r[9], I64, nb, "r.block_sums", d), session, now_ms,
+             cur_stream()),
+         "tree_serve_frames");
 }
 
 int64_t tree_order_workspace(int64_t n) {
@@ -831,6 +899,10 @@ TORCH_LIBRARY(zkmi, m) {
   m.def("decode_replies(Tensor buf, Tensor frame_off, Tensor frame_len, "
         "Tensor count, Tensor xid_tab, int xid_mask, Tensor(a!)[] out) -> ()",
         &decode_replies);
+  m.def("decode_replies_check(Tensor buf, Tensor frame_off, Tensor frame_len, "
+        "Tensor count, Tensor xid_tab, int xid_mask, Tensor(a!)[] out, "
+        "Tensor idx, Tensor xid, Tensor data_len, Tensor(b!) acc) -> ()",
+        &decode_replies_check);
   m.def("expand_strings(Tensor buf, Tensor region, Tensor count, "
         "Tensor base, Tensor(a!) str_off, Tensor(b!) str_len) -> ()",
         &expand_strings);
@@ -849,6 +921,9 @@ TORCH_LIBRARY(zkmi, m) {
   m.def("tree_serve(Tensor(a!)[] tree, Tensor rx, Tensor[] requests, "
         "Tensor count, int ncap, Tensor(b!)[] out, int session, int now_ms) "
         "-> ()", &tree_serve);
+  m.def("tree_serve_frames(Tensor(a!)[] tree, Tensor rx, Tensor frame_off, "
+        "Tensor frame_len, Tensor count, int ncap, Tensor(b!)[] out, "
+        "int session, int now_ms) -> ()", &tree_serve_frames);
   m.def("tree_order_workspace(int n) -> int", &tree_order_workspace);
   m.def("tree_order_stats_offset(int n) -> int", &tree_order_stats_offset);
   m.def("tree_serve_ordered(Tensor(a!)[] tree, Tensor rx, Tensor[] requests, "

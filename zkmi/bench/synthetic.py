@@ -317,7 +317,9 @@ class GpuServer(object):
         pipelined caller interleaves another connection's work there)."""
         L = _lib.lib()
         ft = self.scanner.scan(rx, n)
-        rt = B.decode_requests(rx, ft, out=self.rt)
+        # ordered serving ranks the batch from K12's request table; the
+        # plain serve parses each frame in registers instead
+        rt = B.decode_requests(rx, ft, out=self.rt) if ordered else None
         yield
         r = self.resp
         r.count = ft.count
@@ -333,8 +335,8 @@ class GpuServer(object):
                                  ft.count, self.cap_frames, out, session,
                                  now, self.ows, passes, self.tree.scratch)
         else:
-            L.tree_serve(self.tree.tensors, rx, rt.tensors(), ft.count,
-                         self.cap_frames, out, session, now)
+            L.tree_serve_frames(self.tree.tensors, rx, ft.off, ft.length,
+                                ft.count, self.cap_frames, out, session, now)
         out, rec_off, total, err = B.encode_responses(
             r, self.tree.store, self.out.numel(), out=self.out,
             presized=self.presized, terminate=terminate)
@@ -519,13 +521,12 @@ class GetPipeline(object):
         rx, rtotal, rerr, _ = self.server.result
         yield
         ft = self.rscanner.scan(rx, _len(rtotal))
-        rep = B.decode_replies(rx, ft, self.xt, out=self.reply)
-        self.last = (self.idx, rep, rx, ft)
         if parent is not None:
             validate, acc = parent._validate, parent._acc
-        if not validate:
-            return
-        L.bench_check_get(n, rep.tensors(), self.idx, xid, t.data_len, acc)
+        # the reply check rides in the decode kernel (acc: 1..64 slots)
+        chk = (self.idx, xid, t.data_len, acc) if validate else None
+        rep = B.decode_replies(rx, ft, self.xt, out=self.reply, check=chk)
+        self.last = (self.idx, rep, rx, ft)
 
 
 def _arena(strings, dev):
@@ -726,7 +727,7 @@ class MixPipeline(object):
               (~self.is_set_ok[:n] | (rep.stat32[0, :n] == 1)))
         if acc is None:
             return ok.sum()
-        acc += ok.sum()
+        acc[:1] += ok.sum()
         return acc
 
     def diagnose(self):
@@ -817,7 +818,7 @@ class ChainPipeline(object):
                                (rep.pay_len[:n] == self.data_bytes))))
         if acc is None:
             return ok.sum()
-        acc += ok.sum()
+        acc[:1] += ok.sum()
         return acc
 
     def diagnose(self):
@@ -1065,7 +1066,7 @@ class StormPipeline(object):
         good = torch.where(self.hs_ok[0] & expire_ok, good, 0)
         if acc is None:
             return good
-        acc += good
+        acc[:1] += good
         return acc
 
     def diagnose(self):

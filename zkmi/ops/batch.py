@@ -452,16 +452,29 @@ def alloc_replies(cap, device):
         None)
 
 
-def decode_replies(buf, frames, xid_table, out=None, stream=None):
-    """K2-K8: decode every frame of ``frames`` as a reply."""
+def decode_replies(buf, frames, xid_table, out=None, stream=None,
+                   check=None):
+    """K2-K8: decode every frame of ``frames`` as a reply.
+
+    ``check = (idx, xid, data_len, acc)``: also count, in the same kernel,
+    the replies that are clean GET_DATA successes for the requests sent
+    (request i = node idx[i] with xid[i]; czxid idx + 1 and the node's data
+    length) into ``acc`` (int64, 1..64 slots the caller sums)."""
     L = _lib.lib()
     cap = frames.off.numel()
     if out is None:
         out = alloc_replies(cap, buf.device)
     out.count = frames.count
     with _on(stream):
-        L.decode_replies(buf, frames.off, frames.length, frames.count,
-                         xid_table.tab, xid_table.mask, out.tensors())
+        if check is None:
+            L.decode_replies(buf, frames.off, frames.length, frames.count,
+                             xid_table.tab, xid_table.mask, out.tensors())
+        else:
+            idx, xid, data_len, acc = check
+            L.decode_replies_check(buf, frames.off, frames.length,
+                                   frames.count, xid_table.tab,
+                                   xid_table.mask, out.tensors(), idx, xid,
+                                   data_len, acc)
     return out
 
 

@@ -82,6 +82,7 @@ constexpr int64_t TBAD = (int64_t)1 << 60;
 constexpr int64_t FC_MAXP = (int64_t)1 << 24;
 constexpr int FC_WIN = 1024;               // fs_link's staged walk window
 constexpr int FL_T = 1024;                 // fs_link threads
+constexpr int FL_U = 8;                    // fs_link loads per batch
 // Bound of fs_tile's wait for the tile before (100 MHz ticks, 2 ms): normal
 // waits are tens of microseconds; past the bound the tile takes no
 // speculated entry and fs_link re-walks it from the exact one.
@@ -691,26 +692,22 @@ ZK_DEV void fs_link_parallel(
     const int64_t* __restrict__ sx, const uint16_t* __restrict__ list,
     const int32_t* __restrict__ rcount, uint16_t* pre, int64_t* rec_entry,
     int64_t* rec_exit, int64_t* rec_meta, int32_t* hbuf, int32_t* blist,
-    int64_t* red, int64_t* s_nh, uint8_t* win, uint64_t* stats) {
+    int64_t* red, int64_t* s_nh, uint8_t* win, uint64_t* stats,
+    const uint8_t* __restrict__ bflag) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int64_t INF = INT64_MAX;
   // 1. broken links k (1 <= k < ntiles, tile k-1 not a terminal), in order
   const int64_t pch = (ntiles + FL_T - 1) / FL_T;
   const int64_t c0 = min((int64_t)tid * pch, ntiles);
   const int64_t c1 = min(c0 + pch, ntiles);
+  // (fs_check's per-link flags: this pass runs before any repair, so they
+  // are current; contiguous bytes, no dependent loads)
   int64_t nb = 0;
-  for (int64_t k = max(c0, (int64_t)1); k < c1; ++k) {
-    if (m_term(ld_agent(&rec_meta[k - 1]))) continue;
-    const int64_t e = ld_agent(&rec_entry[k]);
-    nb += e < 0 || e != ld_agent(&rec_exit[k - 1]);
-  }
+  for (int64_t k = max(c0, (int64_t)1); k < c1; ++k) nb += bflag[k];
   int64_t nb_tot;
   int64_t ob = block_excl_scan(nb, red, &nb_tot);
-  for (int64_t k = max(c0, (int64_t)1); k < c1; ++k) {
-    if (m_term(ld_agent(&rec_meta[k - 1]))) continue;
-    const int64_t e = ld_agent(&rec_entry[k]);
-    if (e < 0 || e != ld_agent(&rec_exit[k - 1])) blist[ob++] = (int32_t)k;
-  }
+  for (int64_t k = max(c0, (int64_t)1); k < c1; ++k)
+    if (bflag[k]) blist[ob++] = (int32_t)k;
   __threadfence_block();
   __syncthreads();
   // 2. run heads: broken links whose predecessor link is not broken
@@ -801,7 +798,8 @@ __global__ __launch_bounds__(FK_T) void fs_check(
     const int64_t* __restrict__ n_dev, int64_t n_cap,
     const int64_t* __restrict__ rec_entry, const int64_t* __restrict__ rec_exit,
     const int64_t* __restrict__ rec_meta, int64_t* __restrict__ base,
-    int64_t* __restrict__ bsum, uint64_t* __restrict__ mins) {
+    int64_t* __restrict__ bsum, uint64_t* __restrict__ mins,
+    uint8_t* __restrict__ bflag) {
   __shared__ int64_t sm[FK_T / 64 + 1];
   __shared__ int64_t smin[2 * (FK_T / 64)];
   const int64_t n = stream_len(n_dev, n_cap);
@@ -819,6 +817,9 @@ __global__ __launch_bounds__(FK_T) void fs_check(
     cnt = m_cnt(mk);
     if (m_term(mk)) fterm = k;
     else if (nxt && (e < 0 || e != x)) fb = k + 1;
+    // bflag[k + 1]: link k + 1 broken (fs_link's repair lists read it)
+    if (nxt) bflag[k + 1] = fb != INF;
+    if (k == 0) bflag[0] = 0;
   }
   int64_t tot;
   const int64_t ex = block_excl_scan(cnt, sm, &tot);
@@ -854,7 +855,7 @@ __global__ __launch_bounds__(FL_T) void fs_link(
     int64_t* __restrict__ base, int64_t cap, int64_t* __restrict__ result,
     uint64_t* stats, int32_t* __restrict__ blist,
     int64_t* __restrict__ bsum, const uint64_t* __restrict__ mins,
-    int64_t* __restrict__ lastk) {
+    int64_t* __restrict__ lastk, const uint8_t* __restrict__ bflag) {
   __shared__ __attribute__((aligned(16)))
       uint8_t win[(FL_T / 64) * (FC_WIN + 16)];      // one per wave
   __shared__ int64_t red[2 * (FL_T / 64) + 2];
@@ -909,20 +910,42 @@ __global__ __launch_bounds__(FL_T) void fs_link(
     }
   }
   int64_t from = 1, ft = INF;
-  bool accel = true;
+  bool accel = true, first = true;
+  const uint64_t mb0 = mins[0], mt0 = mins[1];
   for (;;) {
     // leftmost terminal, and leftmost broken link at or after `from`
     int64_t fb = INF, fterm = INF;
+    if (first) {
+      // fs_check's answer (every thread read the same minima)
+      first = false;
+      fb = mb0 ? ntiles - (int64_t)mb0 : INF;
+      fterm = mt0 ? ntiles - (int64_t)mt0 : INF;
+    } else {
     // links before `from` hold (repaired), so terminals before from - 1
-    // were found in an earlier round: only the rest is scanned again
-    for (int64_t k = from - 1 + tid; k < ntiles; k += FL_T) {
-      const int64_t mk = ld_agent(&rec_meta[k]);
-      if (m_term(mk)) {
-        fterm = min(fterm, k);
-      } else if (k + 1 < ntiles && k + 1 >= from) {
-        const int64_t e = ld_agent(&rec_entry[k + 1]);
-        if (e < 0 || e != ld_agent(&rec_exit[k])) fb = min(fb, k + 1);
+    // were found in an earlier round: only the rest is scanned again.
+    // Loads in batches of FL_U tiles per thread (all issued before any is
+    // used: one round trip per batch, not two per tile)
+    for (int64_t k0 = from - 1 + tid; k0 < ntiles; k0 += FL_U * FL_T) {
+      int64_t mk[FL_U], e[FL_U], x[FL_U];
+#pragma unroll
+      for (int u = 0; u < FL_U; ++u) {
+        const int64_t k = k0 + (int64_t)u * FL_T;
+        const bool in = k < ntiles, nx = k + 1 < ntiles;
+        mk[u] = in ? ld_agent(&rec_meta[k]) : 0;
+        e[u] = nx ? ld_agent(&rec_entry[k + 1]) : 0;
+        x[u] = in ? ld_agent(&rec_exit[k]) : 0;
       }
+#pragma unroll
+      for (int u = 0; u < FL_U; ++u) {
+        const int64_t k = k0 + (int64_t)u * FL_T;
+        if (k >= ntiles) break;
+        if (m_term(mk[u])) {
+          fterm = min(fterm, k);
+        } else if (k + 1 < ntiles && k + 1 >= from) {
+          if (e[u] < 0 || e[u] != x[u]) fb = min(fb, k + 1);
+        }
+      }
+    }
     }
     for (int d = 32; d >= 1; d >>= 1) {
       fb = min(fb, (int64_t)__shfl_xor(fb, d, 64));
@@ -951,7 +974,7 @@ __global__ __launch_bounds__(FL_T) void fs_link(
       accel = false;
       fs_link_parallel(buf, n, ntiles, maxp, sx, list, rcount, pre,
                        rec_entry, rec_exit, rec_meta, (int32_t*)base, blist,
-                       red, &s_nh, win, stats);
+                       red, &s_nh, win, stats, bflag);
       __syncthreads();
       continue;
     }
@@ -990,12 +1013,26 @@ __global__ __launch_bounds__(FL_T) void fs_link(
   const int64_t k0 = (int64_t)tid * per;
   const int64_t k1 = min(k0 + per, last + 1);
   int64_t sum = 0;
-  for (int64_t k = k0; k < k1; ++k) sum += m_cnt(ld_agent(&rec_meta[k]));
+  for (int64_t kb = k0; kb < k1; kb += FL_U) {
+    int64_t v[FL_U];
+#pragma unroll
+    for (int u = 0; u < FL_U; ++u)
+      v[u] = kb + u < k1 ? ld_agent(&rec_meta[kb + u]) : 0;
+#pragma unroll
+    for (int u = 0; u < FL_U; ++u) sum += m_cnt(v[u]);
+  }
   int64_t tot;
   int64_t run = block_excl_scan(sum, red, &tot);
-  for (int64_t k = k0; k < k1; ++k) {
-    base[k] = run;
-    run += m_cnt(ld_agent(&rec_meta[k]));
+  for (int64_t kb = k0; kb < k1; kb += FL_U) {
+    int64_t v[FL_U];
+#pragma unroll
+    for (int u = 0; u < FL_U; ++u)
+      v[u] = kb + u < k1 ? ld_agent(&rec_meta[kb + u]) : 0;
+#pragma unroll
+    for (int u = 0; u < FL_U; ++u) {
+      if (kb + u < k1) base[kb + u] = run;
+      run += m_cnt(v[u]);
+    }
   }
   for (int64_t k = last + 1 + tid; k < ntiles; k += FL_T) base[k] = -1;
   // absolute bases: fs_rows adds a zero block offset
@@ -1052,7 +1089,7 @@ __global__ __launch_bounds__(256) void fs_rows(
 struct FsPlan {
   int64_t tiles;
   size_t off_list, off_pre, off_sx, off_lbw, off_rent, off_rexit, off_rmeta,
-      off_rcnt, off_base, off_blist, off_bsum, total;
+      off_rcnt, off_base, off_blist, off_bsum, off_bflag, total;
 };
 
 static FsPlan fs_plan(int64_t n) {
@@ -1073,6 +1110,7 @@ static FsPlan fs_plan(int64_t n) {
   p.off_base = take((size_t)tiles * 8);
   p.off_blist = take((size_t)tiles * 4);
   p.off_bsum = take((size_t)(tiles / FK_T + 1) * 8);
+  p.off_bflag = take((size_t)tiles + 1);
   p.total = o;
   return p;
 }
@@ -1148,6 +1186,7 @@ int zk_frame_scan3(const uint8_t* buf, const int64_t* n_dev, int64_t n_cap,
   int64_t* base = (int64_t*)(ws + p.off_base);
   int32_t* blist = (int32_t*)(ws + p.off_blist);
   int64_t* bsum = (int64_t*)(ws + p.off_bsum);
+  uint8_t* bflag = ws + p.off_bflag;
   uint64_t* mins = lbw + 2 * tiles + 4;
   int64_t* lastk = (int64_t*)(lbw + 2 * tiles + 6);
   // X flags, the stats and fs_check's minima start at zero
@@ -1175,11 +1214,12 @@ int zk_frame_scan3(const uint8_t* buf, const int64_t* n_dev, int64_t n_cap,
 #undef ZK_FS_TILE
   ZK_LAUNCH_CHECK();
   fs_check<<<(unsigned)((tiles + FK_T - 1) / FK_T), FK_T, 0, st>>>(
-      n_dev, n_cap, rent, rexit, rmeta, base, bsum, mins);
+      n_dev, n_cap, rent, rexit, rmeta, base, bsum, mins, bflag);
   ZK_LAUNCH_CHECK();
   fs_link<<<1, FL_T, 0, st>>>(buf, n_dev, n_cap, maxp, sx, list, rcnt, pre,
                               rent, rexit, rmeta, base, cap, result,
-                              lbw + 2 * tiles, blist, bsum, mins, lastk);
+                              lbw + 2 * tiles, blist, bsum, mins, lastk,
+                              bflag);
   ZK_LAUNCH_CHECK();
   fs_rows<<<(unsigned)((tiles + 3) / 4), 256, 0, st>>>(
       buf, n_dev, n_cap, list, pre, rmeta, rexit, base, bsum, lastk, foff,

@@ -219,6 +219,18 @@ struct LSink {
   }
   ZK_DEV void bytes(const uint8_t* s, int64_t n) {
     int64_t i = 0;
+    // 128-byte batches: eight 16-byte loads in flight before the first
+    // LDS write (one round trip per 128 bytes instead of per 16 — large
+    // payloads, e.g. KiB GET_DATA replies, were latency-bound here)
+    for (; i + 128 <= n; i += 128) {
+      uint4 v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) __builtin_memcpy(&v[j], s + i + 16 * j, 16);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        put4(v[j].x); put4(v[j].y); put4(v[j].z); put4(v[j].w);
+      }
+    }
     for (; i + 16 <= n; i += 16) {
       uint4 v; __builtin_memcpy(&v, s + i, 16);
       put4(v.x); put4(v.y); put4(v.z); put4(v.w);

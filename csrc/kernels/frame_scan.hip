@@ -136,12 +136,17 @@ constexpr int FT_LDS = FT_STAGE + 2 * FT_BITS * 4 + 64 * 2 + FT_XW * 4;
 // One hop from tile-relative p (< FT_S).  Returns 0 and q (in-tile
 // successor), 1 for a terminal (the chain ends in the tile), or 2 and the
 // exit x (tile end + x) when the frame leaves the tile.
+// `minb`: the frontier's plausibility floor on a frame body (the smallest
+// ZooKeeper body is 8 bytes: a ping's xid + type).  Speculative walkers
+// reading a shorter length die at once instead of crawling 4 bytes a hop
+// through zero header fields; exactness is untouched (a real frame that
+// short only costs its tile the speculated entry, fs_link repairs it).
 ZK_DEV int ft_hop(const uint8_t* sb, int32_t p, int32_t nrel, int32_t maxp,
-                  int32_t& q) {
+                  int32_t minb, int32_t& q) {
   if (p >= nrel) return 1;                 // the stream ended before p
   const int32_t len = lds_be32(sb, p);
   const int32_t nx = p + 4 + len;
-  if ((p + 4 > nrel) | (len < 0) | (len > maxp) | (nx > nrel)) return 1;
+  if ((p + 4 > nrel) | (len < minb) | (len > maxp) | (nx > nrel)) return 1;
   q = nx;
   return nx >= FT_S ? 2 : 0;
 }
@@ -251,7 +256,7 @@ __global__ __launch_bounds__(256) void fs_tile(
     uint16_t* __restrict__ pre, int64_t* __restrict__ sx, uint64_t* lbw,
     int64_t* __restrict__ rec_entry, int64_t* __restrict__ rec_exit,
     int64_t* __restrict__ rec_meta, int32_t* __restrict__ rcount,
-    int64_t ntiles_cap, int64_t* __restrict__ dbg) {
+    int64_t ntiles_cap, int64_t* __restrict__ dbg, int32_t minb) {
   constexpr int K = W / 64;                 // window entries per lane
   constexpr int XW = W / 32;                // candidate words used
   static_assert(W % 64 == 0 && K >= 1 && K <= 32, "window");
@@ -343,7 +348,7 @@ __global__ __launch_bounds__(256) void fs_tile(
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       q[k] = 0;
-      code[k] = (act >> k) & 1 ? ft_hop(sb, p[k], nrel, maxp32, q[k]) : 1;
+      code[k] = (act >> k) & 1 ? ft_hop(sb, p[k], nrel, maxp32, minb, q[k]) : 1;
     }
 #pragma unroll
     for (int k = 0; k < K; ++k) {
@@ -387,7 +392,7 @@ __global__ __launch_bounds__(256) void fs_tile(
   }
   while (live > 1) {
     int32_t q = 0;
-    const int code = ma ? ft_hop(sb, mp, nrel, maxp32, q) : 1;
+    const int code = ma ? ft_hop(sb, mp, nrel, maxp32, minb, q) : 1;
     if (ma) {
       if (code == 0 && ft_claim(claimed, q)) {
         mp = q;
@@ -1115,6 +1120,18 @@ static FsPlan fs_plan(int64_t n) {
   return p;
 }
 
+// ZKMI_FS_MINB: the frontier's minimum plausible body length (default 8;
+// 0 = any length, the round-2 behaviour; A/B only)
+static int32_t fs_minb() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("ZKMI_FS_MINB");
+    v = e ? atoi(e) : 8;
+    if (v < 0) v = 0;
+  }
+  return v;
+}
+
 static int fs_window(int32_t window) {
   return window <= 256 ? 256 : window <= 512 ? 512
        : window <= 1024 ? 1024 : 2048;
@@ -1204,7 +1221,7 @@ int zk_frame_scan3(const uint8_t* buf, const int64_t* n_dev, int64_t n_cap,
 #define ZK_FS_TILE(WW)                                                       \
   fs_tile<WW><<<tblocks, 64 * tpb, FT_LDS * tpb, st>>>(                      \
       buf, n_dev, n_cap, maxp, list, pre, sx, lbw, rent, rexit, rmeta, rcnt, \
-      tiles, dbg)
+      tiles, dbg, fs_minb())
   switch (W) {
     case 256: ZK_FS_TILE(256); break;
     case 512: ZK_FS_TILE(512); break;

@@ -18,7 +18,8 @@ def plan(n):
     tiles = (n + FT_S - 1) // FT_S if n > 0 else 1
     o = 0
     offs = {}
-    for name, b in (('list', tiles * FT_LMAX * 2), ('pre', tiles * FT_LMAX * 2),
+    for name, b in (('list', tiles * FT_LMAX * 2),
+                    ('pre', tiles * FT_LMAX * 2),
                     ('sx', tiles * 8), ('lbw', (2 * tiles + 4) * 8),
                     ('rent', tiles * 8), ('rexit', tiles * 8),
                     ('rmeta', tiles * 8), ('rcnt', tiles * 4),

@@ -4,9 +4,13 @@ set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
-  tests/test_kernels.py tests/test_torch_ops.py tests/test_sharded.py -m gpu > gpurun_out/r2n_tests.log 2>&1 || { tail -40 gpurun_out/r2n_tests.log; exit 1; }
+  tests/test_kernels.py tests/test_torch_ops.py tests/test_sharded.py -m gpu \
+  > gpurun_out/r2n_tests.log 2>&1 \
+  || { tail -40 gpurun_out/r2n_tests.log; exit 1; }
 tail -2 gpurun_out/r2n_tests.log
 for v in "--graph" "" "--graph" ""; do
-timeout -k 10 240 python bench.py --steps 30 --warmup 5 --no-rtt $v > gpurun_out/r2n_get.json 2> gpurun_out/r2n_get.err || { tail -20 gpurun_out/r2n_get.err; exit 1; }
+timeout -k 10 240 python bench.py --steps 30 --warmup 5 --no-rtt $v \
+  > gpurun_out/r2n_get.json 2> gpurun_out/r2n_get.err \
+  || { tail -20 gpurun_out/r2n_get.err; exit 1; }
 echo "[$v]"; cut -c90-220 gpurun_out/r2n_get.json
 done

@@ -200,8 +200,9 @@ class GpuTree(object):
         self._tensors = [self.ht, self.node_path_off, self.node_path_len,
                          self.node_parent, self.path_arena, self.counters,
                          self.slab, self.slot_off, self.data_len,
-                         self.slot_cap] + [self.free_list, self.cver, self.nchild, self.pzxid,
-                          self.dirty, self.dirty_list, self.node_pw]
+                         self.slot_cap, self.free_list, self.cver,
+                         self.nchild, self.pzxid, self.dirty,
+                         self.dirty_list, self.node_pw]
         now = int(time.time() * 1000) if ctime_ms is None else ctime_ms
         L.tree_fill(self._tensors, 0, nst, nk, now)
         # shard = (rank, world): this replica indexes only the leaves whose
@@ -354,7 +355,8 @@ class GpuServer(object):
 class GetPipeline(object):
     """Batched get() over the synthetic tree (BASELINE config 2)."""
 
-    PHASES = 4          # client encode | server decode | tree + encode | client
+    # client encode | server decode | tree + encode | client decode
+    PHASES = 4
 
     def __init__(self, tree, batch, seed=0, streams=1, stagger=False):
         self.tree = tree
@@ -432,7 +434,9 @@ class GetPipeline(object):
         self._device_seed()
         torch.cuda.synchronize(self.dev)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        # thread-local: another thread's HIP calls (a process group's
+        # watchdog) do not invalidate this capture
+        with torch.cuda.graph(g, capture_error_mode='thread_local'):
             self.step(acc=acc)
         self.graph = g
         return g

@@ -130,12 +130,16 @@ def test_bulk_fails_on_connection_loss(zk):
     try:
         _populate(c, 5)
         zk.set_mode('hang')
+        # the server stops reading first, so the batch is still in flight
+        # when the connection drops (else it could be answered in time)
+        zk.pause_reads()
         b = Box()
         c.bulk_get(['/bulk/n%04d' % i for i in range(5)], b)
         zk.drop_connections()
         err = b.wait(20)[0]
         assert err is not None
     finally:
+        zk.resume_reads()
         zk.set_mode('normal')
         wait_for(lambda: c.isConnected(), 10)
         c.close_sync(10)

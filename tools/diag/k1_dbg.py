@@ -42,7 +42,10 @@ def dump(name, scanner, nbytes):
 
 def main():
     dev = torch.device('cuda', 0)
-    tree = S.GpuTree(1_000_000, 100, device=dev)
+    # K1DBG_DIST=lo-hi: variable payloads (uniform lo..hi bytes)
+    dist = os.environ.get('K1DBG_DIST')
+    dd = tuple(int(x) for x in dist.split('-')) if dist else None
+    tree = S.GpuTree(1_000_000, 100, device=dev, data_dist=dd)
     pipe = S.GetPipeline(tree, 1 << 19)
     for _ in range(2):
         pipe.step()

@@ -69,6 +69,8 @@ struct ZkGetCheck {
   const int32_t* data_len;
   unsigned long long* acc;
   int32_t slots;
+  int64_t* tick;   // optional: tick[1] += 1 once per launch (a captured
+                   // graph's step counter, see bench_gen_get's state)
 };
 
 template <bool CHECK>
@@ -211,6 +213,8 @@ __global__ __launch_bounds__(DEC_T) void decode_replies_k(
   }
   }  // live
   if (CHECK) {
+    if (chk.tick != nullptr && blockIdx.x == 0 && threadIdx.x == 0)
+      chk.tick[1] += 1;
     __shared__ int64_t sm[DEC_T / 64 + 1];
     int64_t tot;
     block_excl_scan(good, sm, &tot);
@@ -336,7 +340,7 @@ int zk_decode_replies(const uint8_t* buf, const int64_t* foff,
   if (ncap <= 0) return 0;
   zk::decode_replies_k<false><<<zk::nblk(ncap), zk::DEC_T, 0, st>>>(
       buf, foff, flen, n_dev, ncap, xid_tab, xid_mask, *o,
-      zk::ZkGetCheck{nullptr, nullptr, nullptr, nullptr, 1});
+      zk::ZkGetCheck{nullptr, nullptr, nullptr, nullptr, 1, nullptr});
   ZK_LAUNCH_CHECK();
   return 0;
 }
@@ -350,12 +354,12 @@ int zk_decode_replies_check(const uint8_t* buf, const int64_t* foff,
                             int64_t xid_mask, const ZkReplyOut* o,
                             const int64_t* idx, const int32_t* xid,
                             const int32_t* data_len, unsigned long long* acc,
-                            int32_t slots, hipStream_t st) {
+                            int32_t slots, int64_t* tick, hipStream_t st) {
   if (ncap <= 0) return 0;
   if (slots < 1 || slots > 64) return (int)hipErrorInvalidValue;
   zk::decode_replies_k<true><<<zk::nblk(ncap), zk::DEC_T, 0, st>>>(
       buf, foff, flen, n_dev, ncap, xid_tab, xid_mask, *o,
-      zk::ZkGetCheck{idx, xid, data_len, acc, slots});
+      zk::ZkGetCheck{idx, xid, data_len, acc, slots, tick});
   ZK_LAUNCH_CHECK();
   return 0;
 }

@@ -84,7 +84,7 @@ int zk_decode_replies_check(const uint8_t*, const int64_t*, const int32_t*,
                             const int64_t*, int64_t, const int64_t*, int64_t,
                             const ZkReplyOut*, const int64_t*, const int32_t*,
                             const int32_t*, unsigned long long*, int32_t,
-                            hipStream_t);
+                            int64_t*, hipStream_t);
 int zk_expand_strings(const uint8_t*, const int64_t*, const int32_t*,
                       const int64_t*, int64_t, int64_t*, int32_t*,
                       hipStream_t);
@@ -516,7 +516,8 @@ void decode_replies_check(const Tensor& buf, const Tensor& foff,
                           const Tensor& xid_tab, int64_t xid_mask,
                           const std::vector<Tensor>& out, const Tensor& idx,
                           const Tensor& xid, const Tensor& data_len,
-                          const Tensor& acc) {
+                          const Tensor& acc,
+                          const c10::optional<Tensor>& tick) {
   const int64_t cap = foff.numel();
   ZkReplyOut o = reply_out(out, cap, &buf);
   const int32_t slots = (int32_t)std::min<int64_t>(acc.numel(), 64);
@@ -532,7 +533,7 @@ void decode_replies_check(const Tensor& buf, const Tensor& foff,
              P<int32_t>(data_len, I32, 1, "data_len", &buf),
              reinterpret_cast<unsigned long long*>(
                  P<int64_t>(acc, I64, slots, "acc", &buf)),
-             slots, cur_stream()),
+             slots, Popt<int64_t>(tick, I64, 2, "tick", &buf), cur_stream()),
          "decode_replies_check");
 }
 
@@ -901,7 +902,8 @@ TORCH_LIBRARY(zkmi, m) {
         &decode_replies);
   m.def("decode_replies_check(Tensor buf, Tensor frame_off, Tensor frame_len, "
         "Tensor count, Tensor xid_tab, int xid_mask, Tensor(a!)[] out, "
-        "Tensor idx, Tensor xid, Tensor data_len, Tensor(b!) acc) -> ()",
+        "Tensor idx, Tensor xid, Tensor data_len, Tensor(b!) acc, "
+        "Tensor(c!)? tick=None) -> ()",
         &decode_replies_check);
   m.def("expand_strings(Tensor buf, Tensor region, Tensor count, "
         "Tensor base, Tensor(a!) str_off, Tensor(b!) str_len) -> ()",

@@ -1,0 +1,14 @@
+#!/bin/bash
+# step counter advanced in the checking decode: tests + bench
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
+  tests/test_kernels.py tests/test_ordering.py tests/test_sharded.py -m gpu \
+  > gpurun_out/r2z_tests.log 2>&1 || { tail -40 gpurun_out/r2z_tests.log; exit 1; }
+tail -2 gpurun_out/r2z_tests.log
+for v in "" "" "--data-bytes 512"; do
+timeout -k 10 240 python bench.py --steps 30 --warmup 5 --no-rtt $v \
+  > gpurun_out/r2z_get.json 2> gpurun_out/r2z_get.err || { tail -20 gpurun_out/r2z_get.err; exit 1; }
+echo "[$v]"; cut -c90-200 gpurun_out/r2z_get.json
+done

@@ -507,8 +507,6 @@ class GetPipeline(object):
         L.bench_gen_get(n, _i64(seed), t.leaf0, t.n_leaves, self.xid_base,
                         t.node_pw, self.idx, self.xid, self.poff, self.plen,
                         self.gstate)
-        if self.gstate is not None:
-            self.gstate[1:].add_(1)         # next step (on the device)
         xid = self.xid
         self.xid_base = (self.xid_base + n) & 0x7fffffff
         rb = B.RequestBatch(n, self.opcode, xid, self.arg, self.poff,
@@ -529,7 +527,12 @@ class GetPipeline(object):
             validate, acc = parent._validate, parent._acc
         # the reply check rides in the decode kernel (acc: 1..64 slots)
         chk = (self.idx, xid, t.data_len, acc) if validate else None
-        rep = B.decode_replies(rx, ft, self.xt, out=self.reply, check=chk)
+        # the device step counter advances in the checking decode (one
+        # launch less per step), else on its own
+        rep = B.decode_replies(rx, ft, self.xt, out=self.reply, check=chk,
+                               tick=self.gstate if validate else None)
+        if self.gstate is not None and not validate:
+            self.gstate[1:].add_(1)
         self.last = (self.idx, rep, rx, ft)
 
 

@@ -453,13 +453,15 @@ def alloc_replies(cap, device):
 
 
 def decode_replies(buf, frames, xid_table, out=None, stream=None,
-                   check=None):
+                   check=None, tick=None):
     """K2-K8: decode every frame of ``frames`` as a reply.
 
     ``check = (idx, xid, data_len, acc)``: also count, in the same kernel,
     the replies that are clean GET_DATA successes for the requests sent
     (request i = node idx[i] with xid[i]; czxid idx + 1 and the node's data
-    length) into ``acc`` (int64, 1..64 slots the caller sums)."""
+    length) into ``acc`` (int64, 1..64 slots the caller sums).  ``tick``
+    (int64 [2], with ``check``): ``tick[1]`` advances by one in the same
+    kernel (the device step counter of a captured pipeline)."""
     L = _lib.lib()
     cap = frames.off.numel()
     if out is None:
@@ -474,7 +476,7 @@ def decode_replies(buf, frames, xid_table, out=None, stream=None,
             L.decode_replies_check(buf, frames.off, frames.length,
                                    frames.count, xid_table.tab,
                                    xid_table.mask, out.tensors(), idx, xid,
-                                   data_len, acc)
+                                   data_len, acc, tick)
     return out
 
 

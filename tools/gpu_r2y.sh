@@ -8,7 +8,9 @@ timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method threa
   > gpurun_out/r2y_tests.log 2>&1 || { tail -40 gpurun_out/r2y_tests.log; exit 1; }
 tail -2 gpurun_out/r2y_tests.log
 for v in "" "" "--data-bytes 512"; do
-timeout -k 10 240 python bench.py --steps 30 --warmup 5 --no-rtt $v \
-  > gpurun_out/r2y_get.json 2> gpurun_out/r2y_get.err || { tail -20 gpurun_out/r2y_get.err; exit 1; }
+timeout -k 10 240 python bench.py --steps 30 --warmup 5 --no-rtt \
+  $v \
+  > gpurun_out/r2y_get.json 2> gpurun_out/r2y_get.err \
+  || { tail -20 gpurun_out/r2y_get.err; exit 1; }
 echo "[$v]"; cut -c90-200 gpurun_out/r2y_get.json
 done

@@ -859,7 +859,7 @@ __global__ __launch_bounds__(FL_T) void fs_link(
     uint16_t* pre, int64_t* rec_entry, int64_t* rec_exit, int64_t* rec_meta,
     int64_t* __restrict__ base, int64_t cap, int64_t* __restrict__ result,
     uint64_t* stats, int32_t* __restrict__ blist,
-    int64_t* __restrict__ bsum, const uint64_t* __restrict__ mins,
+    int64_t* __restrict__ bsum, uint64_t* __restrict__ mins,
     int64_t* __restrict__ lastk, const uint8_t* __restrict__ bflag) {
   __shared__ __attribute__((aligned(16)))
       uint8_t win[(FL_T / 64) * (FC_WIN + 16)];      // one per wave
@@ -874,10 +874,18 @@ __global__ __launch_bounds__(FL_T) void fs_link(
     return;
   }
   const int64_t INF = INT64_MAX;
+  // fs_check's minima, read by every thread, then cleared for the next
+  // scan of this workspace
+  const uint64_t mb0 = mins[0], mt0 = mins[1];
+  __syncthreads();
+  if (tid == 0) {
+    mins[0] = 0;
+    mins[1] = 0;
+  }
   {
     // fast path: fs_check found no broken link before the first terminal;
     // the row bases are bsum's block offsets + fs_check's in-block bases
-    const uint64_t mb = mins[0], mt = mins[1];
+    const uint64_t mb = mb0, mt = mt0;
     const int64_t fb0 = mb ? ntiles - (int64_t)mb : INF;
     const int64_t ft0 = mt ? ntiles - (int64_t)mt : INF;
     if (fb0 == INF || fb0 > ft0) {
@@ -916,7 +924,6 @@ __global__ __launch_bounds__(FL_T) void fs_link(
   }
   int64_t from = 1, ft = INF;
   bool accel = true, first = true;
-  const uint64_t mb0 = mins[0], mt0 = mins[1];
   for (;;) {
     // leftmost terminal, and leftmost broken link at or after `from`
     int64_t fb = INF, fterm = INF;
@@ -1064,11 +1071,18 @@ __global__ __launch_bounds__(256) void fs_rows(
     const int64_t* __restrict__ rec_exit,
     const int64_t* __restrict__ base, const int64_t* __restrict__ bsum,
     const int64_t* __restrict__ lastk, int64_t* __restrict__ foff,
-    int32_t* __restrict__ flen, int64_t cap) {
+    int32_t* __restrict__ flen, int64_t cap, uint64_t* __restrict__ lbw) {
   const int lane = threadIdx.x & 63;
   const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int64_t n = stream_len(n_dev, n_cap);
-  if (t * FT_S >= n || t > *lastk) return;
+  if (t * FT_S >= n) return;
+  // the scan is over for this tile: clear its candidate flags, so the next
+  // scan of this workspace needs no memset (zk_frame_scan4 clean=1)
+  if (lane == 0) {
+    lbw[2 * t] = 0;
+    lbw[2 * t + 1] = 0;
+  }
+  if (t > *lastk) return;
   const int64_t b = bsum[t / FK_T] + base[t];
   const int64_t m = rec_meta[t];
   const int64_t x = rec_exit[t];
@@ -1182,10 +1196,14 @@ int64_t zk_frame_scan_workspace(int64_t n) {
 // performance hint: the smallest one covering the stream's usual frame
 // size makes the scan cheapest.  maxp must be <= 16 MiB (the protocol's
 // frame limit).
-int zk_frame_scan3(const uint8_t* buf, const int64_t* n_dev, int64_t n_cap,
+// clean != 0: the workspace's flags were left cleared by the previous scan
+// of it over the same n_cap (fs_rows / fs_link clear what they used), so
+// the memset is skipped.  A stale flag could only cost speed, never
+// correctness (fs_check / fs_link verify every speculated entry).
+int zk_frame_scan4(const uint8_t* buf, const int64_t* n_dev, int64_t n_cap,
                    int64_t maxp, uint8_t* ws, int64_t ws_bytes, int64_t* foff,
                    int32_t* flen, int64_t cap, int64_t* result, int32_t window,
-                   hipStream_t st) {
+                   int32_t clean, hipStream_t st) {
   using namespace zk;
   const int W = fs_window(window);
   if (maxp > FC_MAXP || maxp < 0) return -3;
@@ -1207,7 +1225,8 @@ int zk_frame_scan3(const uint8_t* buf, const int64_t* n_dev, int64_t n_cap,
   uint64_t* mins = lbw + 2 * tiles + 4;
   int64_t* lastk = (int64_t*)(lbw + 2 * tiles + 6);
   // X flags, the stats and fs_check's minima start at zero
-  if (hipMemsetAsync(lbw, 0, (size_t)(2 * tiles + 6) * 8, st) != hipSuccess)
+  if (!clean &&
+      hipMemsetAsync(lbw, 0, (size_t)(2 * tiles + 6) * 8, st) != hipSuccess)
     return -4;
   int64_t* dbg = fs_dbg_buf(tiles);
   // ZKMI_FS_TPB: tiles (waves) per block, 1..4 (A/B)
@@ -1240,9 +1259,17 @@ int zk_frame_scan3(const uint8_t* buf, const int64_t* n_dev, int64_t n_cap,
   ZK_LAUNCH_CHECK();
   fs_rows<<<(unsigned)((tiles + 3) / 4), 256, 0, st>>>(
       buf, n_dev, n_cap, list, pre, rmeta, rexit, base, bsum, lastk, foff,
-      flen, cap);
+      flen, cap, lbw);
   ZK_LAUNCH_CHECK();
   return 0;
+}
+
+int zk_frame_scan3(const uint8_t* buf, const int64_t* n_dev, int64_t n_cap,
+                   int64_t maxp, uint8_t* ws, int64_t ws_bytes, int64_t* foff,
+                   int32_t* flen, int64_t cap, int64_t* result, int32_t window,
+                   hipStream_t st) {
+  return zk_frame_scan4(buf, n_dev, n_cap, maxp, ws, ws_bytes, foff, flen, cap,
+                        result, window, 0, st);
 }
 
 // Chain statistics of the last scan of workspace `ws` over a buffer of
@@ -1258,6 +1285,12 @@ int zk_frame_scan_stats(const uint8_t* ws, int64_t n_cap, int32_t window,
     if (hipMemcpyAsync(out3 + k, lbw + 2 * p.tiles + 1 + k, 4,
                        hipMemcpyDeviceToHost, st) != hipSuccess)
       return -1;
+  if (hipStreamSynchronize(st) != hipSuccess) return -1;
+  // counters since the last read (scans of a clean workspace skip the
+  // memset that used to reset them)
+  if (hipMemsetAsync((void*)(lbw + 2 * p.tiles + 1), 0, 3 * 8, st) !=
+      hipSuccess)
+    return -1;
   return hipStreamSynchronize(st) == hipSuccess ? 0 : -1;
 }
 

@@ -71,9 +71,9 @@ int zk_encode_responses2(const ZkRespBatch*, const ZkNodeStore*,
                          int64_t*, int64_t*, uint8_t*, int64_t, int32_t*,
                          int32_t, int32_t, hipStream_t);
 int64_t zk_frame_scan_workspace(int64_t n);
-int zk_frame_scan3(const uint8_t*, const int64_t*, int64_t, int64_t,
+int zk_frame_scan4(const uint8_t*, const int64_t*, int64_t, int64_t,
                    uint8_t*, int64_t, int64_t*, int32_t*, int64_t, int64_t*,
-                   int32_t, hipStream_t);
+                   int32_t, int32_t, hipStream_t);
 int zk_frame_scan_stats(const uint8_t*, int64_t, int32_t, uint32_t*,
                         hipStream_t);
 int zk_frame_scan_dbg(int64_t* host, int64_t tiles);
@@ -458,21 +458,21 @@ int64_t frame_scan_workspace(int64_t n) { return zk_frame_scan_workspace(n); }
 void frame_scan(const Tensor& buf, const c10::optional<Tensor>& n_dev,
                 int64_t n_cap, int64_t max_packet, const Tensor& ws,
                 const Tensor& foff, const Tensor& flen, const Tensor& result,
-                int64_t window) {
+                int64_t window, bool clean) {
   TORCH_CHECK(n_cap >= 0 && n_cap <= buf.numel(),
               "zkmi: frame_scan length ", n_cap, " past the buffer (",
               buf.numel(), " bytes)");
   TORCH_CHECK(ws.numel() >= zk_frame_scan_workspace(n_cap),
               "zkmi: frame_scan workspace too small");
   const int64_t cap = foff.numel();
-  hip_ok(zk_frame_scan3(
+  hip_ok(zk_frame_scan4(
              P<uint8_t>(buf, U8, 1, "buf"),
              Popt<int64_t>(n_dev, I64, 1, "n", &buf), n_cap, max_packet,
              P<uint8_t>(ws, U8, 1, "ws", &buf), ws.numel(),
              P<int64_t>(foff, I64, 1, "frame_off", &buf),
              P<int32_t>(flen, I32, cap, "frame_len", &buf), cap,
              P<int64_t>(result, I64, 4, "result", &buf), (int32_t)window,
-             cur_stream()),
+             clean ? 1 : 0, cur_stream()),
          "frame_scan");
 }
 
@@ -893,7 +893,8 @@ TORCH_LIBRARY(zkmi, m) {
   m.def("frame_scan_workspace(int n) -> int", &frame_scan_workspace);
   m.def("frame_scan(Tensor buf, Tensor? n, int n_cap, int max_packet, "
         "Tensor(a!) ws, Tensor(b!) frame_off, Tensor(c!) frame_len, "
-        "Tensor(d!) result, int window) -> ()", &frame_scan);
+        "Tensor(d!) result, int window, bool clean=False) -> ()",
+        &frame_scan);
   m.def("frame_scan_stats(Tensor ws, int n_cap, int window) -> int[]",
         &frame_scan_stats);
   m.def("frame_scan_dbg(int tiles) -> Tensor", &frame_scan_dbg);

@@ -181,6 +181,41 @@ def test_frame_scan_device_length_garbage_tail(gpu, window, maxbody, n):
     assert res['frames'] == len(want) and res['consumed'] == wc
 
 
+@pytest.mark.parametrize('window', [256, 1024])
+def test_frame_scanner_clean_reuse_many_streams(gpu, window):
+    """A FrameScanner reused over one capacity skips the workspace memset
+    (the previous scan cleared its flags): many different streams in a row
+    — short and long frames (repairs), BAD_LENGTH, carries, cut lengths —
+    must each match the oracle exactly."""
+    from zkmi.ops import batch as B
+    r = synth.rng(4242 + window)
+    cap = 1 << 20
+    sc = B.FrameScanner(cap // 4, gpu, window=window)
+    buf = torch.randint(0, 256, (cap,), dtype=torch.uint8, device=gpu)
+    n_dev = torch.zeros(1, dtype=torch.int64, device=gpu)
+    for it in range(12):
+        maxbody = r.choice([16, 200, 900, 6000, 30000])
+        s = _frames_stream(r, r.randint(1, 4000 if maxbody < 1000 else 40),
+                           maxbody)
+        if it % 3 == 1:
+            s += b'\xff\xff\xff\xf0' + b'junk'        # BAD_LENGTH
+        elif it % 3 == 2:
+            s += jute.frame(b'z' * 70)[:-9]             # carry
+        s = s[:cap]
+        buf[:len(s)] = _dev_bytes(s, gpu)
+        n = len(s) if it % 4 else max(len(s) - r.randint(1, 64), 0)
+        n_dev.fill_(n)
+        ft = sc.scan(buf, n_dev)
+        res = ft.host_result()
+        frames, consumed, bad_at = jute.scan_frames(s[:n])
+        assert res['frames'] == len(frames), it
+        assert res['consumed'] == consumed, it
+        assert bool(res['bad']) == (bad_at >= 0), it
+        got = list(zip(ft.off[:len(frames)].cpu().tolist(),
+                       ft.length[:len(frames)].cpu().tolist()))
+        assert got == frames, it
+
+
 def test_frame_scan_device_length_bad_frame(gpu):
     from zkmi.ops import batch as B
     r = synth.rng(77)

@@ -348,6 +348,7 @@ class FrameScanner:
                                 torch.empty(4, dtype=I64, device=device))
         self.ws = torch.empty(0, dtype=U8, device=device)
         self.ws_for = -1            # stream length the workspace covers
+        self.clean_for = -1         # n_cap whose flags the last scan cleared
 
     def scan(self, buf, n, stream=None):
         """Frame ``buf[:n]``; ``n`` may be a device int64 length (see
@@ -360,10 +361,15 @@ class FrameScanner:
             self.ws = torch.empty(max(wsb, 256), dtype=U8,
                                   device=buf.device)
             self.ws_for = cover
+            self.clean_for = -1
         t = self.table
+        # a scan leaves its workspace's flags cleared for the next scan over
+        # the same capacity (the layout depends on it): no memset then
         with _on(stream):
             L.frame_scan(buf, n_dev, ncap, self.max_packet, self.ws, t.off,
-                         t.length, t.result, int(self.window))
+                         t.length, t.result, int(self.window),
+                         ncap == self.clean_for)
+        self.clean_for = ncap
         self.last_cap = ncap
         return t
 

@@ -54,23 +54,31 @@ ZK_DEV int64_t req_body_size(const ZkReqBatch& b, int64_t i, bool* ok) {
 // block sums (zk_scan_small_i64), and the write kernel adds its block base
 // to a block scan of the sizes.  Three launches where a separate device-wide
 // scan made five.
+// A malformed request is flagged per block (bbad, a plain store every
+// launch) and req_write's block 0 folds the flags into err, so err needs no
+// zeroing launch before the encode.
 __global__ __launch_bounds__(ENC_T) void req_sizes(ZkReqBatch b, int64_t n,
                                                   int64_t* __restrict__ sizes,
-                                                  int32_t* __restrict__ err,
+                                                  int64_t* __restrict__ bbad,
                                                   int64_t* __restrict__ bsum) {
   __shared__ int64_t sm[ENC_T / 64 + 1];
   const int64_t i = (int64_t)blockIdx.x * ENC_T + threadIdx.x;
   int64_t sz = 0;
+  bool bad = false;
   if (i < n) {
     bool ok;
     const int64_t s = req_body_size(b, i, &ok);
     sz = ok ? 4 + s : 0;
     sizes[i] = sz;
-    if (!ok) atomicOr(err, 1);
+    bad = !ok;
   }
   int64_t tot;
   block_excl_scan(sz, sm, &tot);
-  if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
+  const int any = __syncthreads_or(bad);
+  if (threadIdx.x == 0) {
+    bsum[blockIdx.x] = tot;
+    bbad[blockIdx.x] = any ? 1 : 0;
+  }
 }
 
 // ---------------------------------------------------------------- K11
@@ -463,11 +471,10 @@ __global__ __launch_bounds__(ENC_T) void resp_write(
   const int64_t n = min(*n_dev, ncap);
   const int64_t r0 = (int64_t)blockIdx.x * ENC_T;
   put_terminator(term, total, out, cap);
+  // err written whole by one thread (no zeroing launch before the encode)
+  if (blockIdx.x == 0 && threadIdx.x == 0) *err = *total > cap ? 2 : 0;
   if (r0 >= n) return;
-  if (*total > cap) {
-    if (r0 == 0 && threadIdx.x == 0) atomicOr(err, 2);
-    return;
-  }
+  if (*total > cap) return;
   const int64_t r1 = min(r0 + ENC_T, n);
   block_offsets(r0, r1, sizes, bbase, rec_off, E);
   staged_emit(r0, r1, E.off, E.sz, out, lw, [&](auto& k, int64_t i) {
@@ -555,16 +562,21 @@ __global__ __launch_bounds__(ENC_T) void req_write(
     const int64_t* __restrict__ bbase, int64_t* __restrict__ rec_off,
     const int64_t* __restrict__ total, uint8_t* __restrict__ out, int64_t cap,
     int64_t* __restrict__ xid_tab, int64_t xid_mask,
-    int32_t* __restrict__ err, int32_t term) {
+    int32_t* __restrict__ err, int32_t term,
+    const int64_t* __restrict__ bbad, int64_t nb) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lw[];
   __shared__ EncLocal E;
   const int64_t r0 = (int64_t)blockIdx.x * ENC_T;
   put_terminator(term, total, out, cap);
-  if (r0 >= n) return;
-  if (*total > cap) {                       // capacity guard (whole batch)
-    if (r0 == 0 && threadIdx.x == 0) atomicOr(err, 2);
-    return;
+  if (blockIdx.x == 0) {
+    // err, written whole (1: a malformed request, 2: over capacity)
+    int64_t e = 0;
+    for (int64_t k = threadIdx.x; k < nb; k += ENC_T) e |= bbad[k];
+    const int any = __syncthreads_or(e != 0);
+    if (threadIdx.x == 0) *err = (any ? 1 : 0) | (*total > cap ? 2 : 0);
   }
+  if (r0 >= n) return;
+  if (*total > cap) return;                 // capacity guard (whole batch)
   const int64_t r1 = min(r0 + ENC_T, n);
   block_offsets(r0, r1, sizes, bbase, rec_off, E);
   staged_emit(r0, r1, E.off, E.sz, out, lw, [&](auto& k, int64_t i) {
@@ -622,19 +634,21 @@ int zk_encode_requests2(const ZkReqBatch* b, int64_t n, int64_t* sizes,
                         hipStream_t st) {
   if (n <= 0) {
     int rc = hipMemsetAsync(total, 0, 8, st);
+    if (!rc) rc = hipMemsetAsync(err, 0, 4, st);
     if (!rc && terminate && out_cap >= 4) rc = hipMemsetAsync(out, 0xFF, 4, st);
     return rc;
   }
   const unsigned nb = zk::nblk(n);
-  int64_t* bsum = scan_ws;                 // zk_scan_workspace(n) >= 2 nb
+  int64_t* bsum = scan_ws;                 // zk_scan_workspace(n) >= 3 nb
   int64_t* bbase = scan_ws + nb;
-  zk::req_sizes<<<nb, zk::ENC_T, 0, st>>>(*b, n, sizes, err, bsum);
+  int64_t* bbad = scan_ws + 2 * nb;
+  zk::req_sizes<<<nb, zk::ENC_T, 0, st>>>(*b, n, sizes, bbad, bsum);
   ZK_LAUNCH_CHECK();
   int rc = zk_scan_small_i64(bsum, bbase, nb, total, st);
   if (rc) return rc;
   zk::req_write<<<nb, zk::ENC_T, zk::STAGE_BYTES, st>>>(
       *b, n, sizes, bbase, rec_off, total, out, out_cap, xid_tab, xid_mask,
-      err, terminate);
+      err, terminate, bbad, (int64_t)nb);
   ZK_LAUNCH_CHECK();
   return 0;
 }
@@ -695,6 +709,7 @@ int zk_encode_responses2(const ZkRespBatch* r, const ZkNodeStore* s,
                          int32_t presized, int32_t terminate, hipStream_t st) {
   if (ncap <= 0) {
     int rc = hipMemsetAsync(total, 0, 8, st);
+    if (!rc) rc = hipMemsetAsync(err, 0, 4, st);
     if (!rc && terminate && out_cap >= 4) rc = hipMemsetAsync(out, 0xFF, 4, st);
     return rc;
   }

@@ -352,7 +352,8 @@ extern "C" {
 // Also covers the encoders' per-256-record block sums and bases
 // (2 * ceil(n / 256)).
 int64_t zk_scan_workspace(int64_t n) {
-  const int64_t enc = 2 * ((n + 255) / 256) + 2;
+  // the encoders: block sums, block bases, per-block flags (+2)
+  const int64_t enc = 3 * ((n + 255) / 256) + 2;
   int64_t w = 0;
   while (n > zk::SCAN_E) {
     const int64_t nb = (n + zk::MS_WAVE_E - 1) / zk::MS_WAVE_E;

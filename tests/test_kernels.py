@@ -64,6 +64,27 @@ def test_encode_set_watches_matches_oracle(gpu):
     assert bytes(got0.cpu().numpy().tobytes()) == want0
 
 
+def test_encode_requests_error_word(gpu):
+    """K10's err is written whole by the encode (no zero fill before it):
+    0 clean, 1 an unknown opcode, 2 over capacity — and a clean encode
+    after a failed one reads 0 again from a reused buffer."""
+    from zkmi.ops import batch as B
+    pk = [{'xid': i, 'opcode': 'GET_DATA', 'path': '/a/%d' % i,
+           'watch': False} for i in range(3000)]
+    rb = B.pack_requests(pk, gpu)
+    _, _, total, err = B.encode_requests(rb)
+    assert int(err.item()) == 0
+    small = torch.empty(64, dtype=torch.uint8, device=gpu)
+    _, _, total, err = B.encode_requests(rb, out=small)
+    assert int(err.item()) & 2
+    rb.opcode[1000] = 12345                      # no such opcode
+    _, _, total, err = B.encode_requests(rb)
+    assert int(err.item()) == 1
+    rb.opcode[1000] = 4
+    _, _, total, err = B.encode_requests(rb)
+    assert int(err.item()) == 0
+
+
 def _frames_stream(r, n, maxbody):
     parts = []
     for _ in range(n):

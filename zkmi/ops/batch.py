@@ -148,10 +148,10 @@ def pack_requests(pkts, device=None):
 
 
 def _total_err(dev):
-    """The encoders' (total, err) device scalars.  ``total`` is always
-    written by the launcher (scan or memset); ``err`` is OR-ed into, so it
-    starts at zero — one fill for both."""
-    z = torch.zeros(2, dtype=I64, device=dev)
+    """The encoders' (total, err) device scalars.  Both are written whole
+    by the encode (scan / writer's block 0, or a memset for an empty
+    batch), so no fill launch precedes it."""
+    z = torch.empty(2, dtype=I64, device=dev)
     return z[0:1], z[1:2].view(I32)[0:1]
 
 

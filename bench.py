@@ -31,7 +31,10 @@ whole-node aggregate (sum over ranks of ops / max-rank time) is reported.
 round trip over loopback TCP to the fake server running as its own process
 (``python -m zkmi.server``, started before the GPU is touched), with the
 client on the native epoll loop; reported for honesty about where the GPU
-helps.
+helps.  ``p50_get_rtt_us_evloop`` is the same round trip
+through the callback API on the client's event loop (one get issued from
+the previous one's callback), the way the single-threaded reference runs
+``get(path, cb)``.
 """
 
 import argparse
@@ -133,6 +136,47 @@ def measure_rtt(port, n=2000):
         c.call_sync('get', '/rtt')
         lat.append((time.perf_counter() - t) * 1e6)
     c.close_sync(10)
+    lat.sort()
+    return statistics.median(lat), lat[int(0.99 * len(lat))]
+
+
+def measure_rtt_async(port, n=2000, warm=200):
+    """get() round trips the way the reference measures them: the callback
+    API on the client's event loop, each reply's callback issuing the next
+    get (node-zkstream is single-threaded; there is no cross-thread wake in
+    its get(path, cb)).  ``measure_rtt`` adds a caller-thread hop per call
+    (``call_sync``) and is reported next to it."""
+    import threading
+    from zkmi import Client
+    c = Client(address='127.0.0.1', port=port)
+    c.wait_connected(10)
+    c.call_sync('create', '/rtt_a', b'x' * 100, {})
+    lat = []
+    done = threading.Event()
+    st = {'k': 0, 't': 0.0, 'err': None}
+
+    def issue():
+        st['t'] = time.perf_counter()
+        c.get('/rtt_a', on_reply)
+
+    def on_reply(err, data=None, stat=None):
+        now = time.perf_counter()
+        if err is not None:
+            st['err'] = err
+            done.set()
+            return
+        st['k'] += 1
+        if st['k'] > warm:
+            lat.append((now - st['t']) * 1e6)
+        if st['k'] >= n + warm:
+            done.set()
+            return
+        issue()
+    c.loop.call_soon(issue)
+    ok = done.wait(120)
+    c.close_sync(10)
+    if not ok or st['err'] is not None or not lat:
+        raise RuntimeError('async RTT run failed: %r' % (st['err'],))
     lat.sort()
     return statistics.median(lat), lat[int(0.99 * len(lat))]
 
@@ -407,6 +451,7 @@ def main():
     value = ops / elapsed
 
     rtt50 = rtt99 = py50 = py99 = bulk_ops = bulk_ms = None
+    ev50 = ev99 = None
     if rtt_srv is not None:
         try:
             py50, py99 = measure_rtt(rtt_srv[1])
@@ -416,6 +461,7 @@ def main():
     if fast_srv is not None:
         try:
             rtt50, rtt99 = measure_rtt(fast_srv.port)
+            ev50, ev99 = measure_rtt_async(fast_srv.port)
             bulk_ops, bulk_ms = measure_bulk_tcp(
                 fast_srv.port, a.nodes, a.bulk_batch, 3, dev)
         finally:
@@ -455,6 +501,12 @@ def main():
             'rtt_note': 'one blocking Client.get over loopback TCP to the '
                         'native server (zk_fastserver); *_fakezk: to the '
                         'Python fake server',
+            'p50_get_rtt_us_evloop': ev50,
+            'p99_get_rtt_us_evloop': ev99,
+            'rtt_evloop_note': 'get(path, cb) chained on the client event '
+                               'loop (each callback issues the next get), '
+                               'as node-zkstream runs it: no caller-thread '
+                               'hop; same native server',
             'p50_get_rtt_us_fakezk': py50,
             'p99_get_rtt_us_fakezk': py99,
             'bulk_tcp_ops_s': bulk_ops,

@@ -14,7 +14,9 @@ on the loop thread.  ``*_sync`` helpers block the calling thread for a
 result (they must not be called from the loop thread itself).
 """
 
+import os
 import threading
+import time
 
 from .. import consts
 from ..config import ClientConfig
@@ -27,6 +29,15 @@ from ..utils.log import create_logger
 from ..utils.metrics import create_collector, METRIC_ZK_EVENT_COUNTER
 from .connection import ZKConnectionFSM
 from .connection_set import ConnectionSet, StaticResolver
+
+# call_sync's poll window before it sleeps on the reply lock, seconds
+# (ZKMI_SYNC_SPIN_US).  Default 100 us on hosts with >= 16 CPUs: on a GPU
+# box the blocking get() RTT went 37-44 -> 20 us (tools/gpu_r3k.sh; a
+# 30 us window is shorter than the round trip and does nothing); off on
+# small hosts, where the poller competes with the loop thread for the GIL.
+_SYNC_SPIN_S = float(os.environ.get(
+    'ZKMI_SYNC_SPIN_US',
+    '100' if (os.cpu_count() or 1) >= 16 else '0')) / 1e6
 from .session import ZKSession
 
 
@@ -566,7 +577,17 @@ class Client(FSM):
             box['res'] = res
             done.release()
         getattr(self, method)(*args, cb)
-        if not done.acquire(timeout=timeout):
+        got = False
+        if _SYNC_SPIN_S > 0:
+            # a short poll before sleeping on the lock: the reply usually
+            # lands within tens of us, and a sleeping thread's wake-up costs
+            # about that much again (ZKMI_SYNC_SPIN_US)
+            t_end = time.perf_counter() + _SYNC_SPIN_S
+            while not got and time.perf_counter() < t_end:
+                got = done.acquire(False)
+                if not got:
+                    time.sleep(0)
+        if not got and not done.acquire(timeout=timeout):
             raise TimeoutError('%s%r timed out' % (method, args))
         if box['err'] is not None:
             raise box['err']

@@ -428,27 +428,27 @@ __global__ __launch_bounds__(256) void fs_tile(
     if (c >= nrel) {
       send = TERM | (ts + c);                // reached the stream end
     } else {
+      int32_t len, nx;
+      bool ok;
       for (;;) {
-        const int32_t len = __builtin_amdgcn_readfirstlane(lds_be32(sb, c));
-        const int32_t nx = c + 4 + len;
-        if ((uint32_t)len > (uint32_t)maxp32 || nx > nrel) {
-          const bool bad = (c + 4 <= nrel) && ((len < 0) | (len > maxp32));
-          send = TERM | (bad ? TBAD : 0) | (ts + c);
-          break;
-        }
+        len = __builtin_amdgcn_readfirstlane(lds_be32(sb, c));
+        nx = c + 4 + len;
+        ok = (uint32_t)len <= (uint32_t)maxp32 && nx <= nrel;
+        if (!ok) break;                      // one exit test per hop
         ent = lane == (m & 63) ? (uint32_t)c : ent;
         ++m;
         if ((m & 63) == 0) L[m - 64 + lane] = (uint16_t)ent;
-        if (nx >= lim) {
-          if (nx >= FT_S) {
-            send = ts + nx;
-            if (lane == 0) ft_mark_exit(xbits, nx - FT_S, W);
-          } else {
-            send = TERM | (ts + nx);         // the stream ends at nx
-          }
-          break;
-        }
+        if (nx >= lim) break;
         c = nx;
+      }
+      if (!ok) {
+        const bool bad = (c + 4 <= nrel) && ((len < 0) | (len > maxp32));
+        send = TERM | (bad ? TBAD : 0) | (ts + c);
+      } else if (nx >= FT_S) {
+        send = ts + nx;
+        if (lane == 0) ft_mark_exit(xbits, nx - FT_S, W);
+      } else {
+        send = TERM | (ts + nx);             // the stream ends at nx
       }
     }
     if (lane < (m & 63)) L[(m & ~63) + lane] = (uint16_t)ent;

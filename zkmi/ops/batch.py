@@ -374,8 +374,10 @@ class FrameScanner:
         return t
 
     def chain_stats(self, stream=None):
-        """K1 one-pass chain counters of the last scan (host sync): tiles
-        without a speculated entry, tiles re-walked, repair rounds."""
+        """K1 chain counters (host sync) accumulated over this scanner's
+        scans since the previous call (a reused workspace skips the memset
+        that used to reset them per scan): tiles without a speculated
+        entry, tiles re-walked, repair rounds."""
         with _on(stream):
             out = _lib.lib().frame_scan_stats(self.ws, self.last_cap,
                                               int(self.window))

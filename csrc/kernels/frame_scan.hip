@@ -558,7 +558,11 @@ __global__ __launch_bounds__(256) void fs_tile(
       if (c >= tend) { w.exit = c; break; }
       if (c >= n) { w.exit = n; break; }    // the stream ends cleanly
       const int32_t crel = (int32_t)(c - ts);
-      if (m > 0 && ((sbits[crel >> 5] >> (crel & 31)) & 1u)) {
+      // both LDS reads of the hop issued together (the survivor map word
+      // and the length word); the map is all zero when m == 0
+      const uint32_t smw = sbits[crel >> 5];
+      const int32_t lraw = lds_be32(sb, crel);
+      if ((smw >> (crel & 31)) & 1u) {
         // joined: the rest is the survivor's list from this start on; its
         // index is the number of survivor starts below crel (the map has
         // FT_BITS = 2 x 64 words, two per lane)
@@ -578,9 +582,9 @@ __global__ __launch_bounds__(256) void fs_tile(
         w.js = s;
         break;
       }
-      const int32_t len = __builtin_amdgcn_readfirstlane(lds_be32(sb, crel));
+      const int32_t len = __builtin_amdgcn_readfirstlane(lraw);
       const int32_t nx = crel + 4 + len;
-      if ((crel + 4 > nrel) | (len < 0) | (len > maxp32) | (nx > nrel)) {
+      if ((uint32_t)len > (uint32_t)maxp32 || nx > nrel) {
         w.exit = c;
         w.term = true;
         w.bad = (crel + 4 <= nrel) && ((len < 0) | (len > maxp32));

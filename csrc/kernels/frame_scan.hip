@@ -235,14 +235,18 @@ ZK_DEV bool ft_mark_exit(uint32_t* xbits, int32_t x, int W) {
 ZK_DEV bool ft_alive(const uint8_t* sb, const uint32_t* sbits, int32_t e,
                      int32_t nrel, int32_t maxp, int32_t m, int64_t send,
                      int64_t n, int64_t ts) {
+  (void)m;                       // the map is empty when m == 0
   int32_t c = e;
   for (;;) {
     if (c >= FT_S || ts + c >= n) return true;
-    if (m > 0 && ((sbits[c >> 5] >> (c & 31)) & 1u))
-      return !((send & TERM) && (send & TBAD));
+    // the survivor-map word and the length word, read together (the map
+    // is all zero when m == 0)
+    const uint32_t smw = sbits[c >> 5];
+    const int32_t lraw = lds_be32(sb, c);
+    if ((smw >> (c & 31)) & 1u) return !((send & TERM) && (send & TBAD));
     if (c + 4 > nrel) return true;
-    const int32_t len = __builtin_amdgcn_readfirstlane(lds_be32(sb, c));
-    if (len < 0 || len > maxp) return false;
+    const int32_t len = __builtin_amdgcn_readfirstlane(lraw);
+    if ((uint32_t)len > (uint32_t)maxp) return false;
     const int32_t nx = c + 4 + len;
     if (nx > nrel) return true;
     c = nx;

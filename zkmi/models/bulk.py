@@ -23,6 +23,14 @@ Fallbacks: on the asyncio loop, or when the replies outgrow the RX buffer,
 the connection routes reply frames to :meth:`BulkBatch.add` one by one (the
 frames captured so far are kept).
 
+Loop stall: ``encode`` (one D2H copy of the encoded stream) and ``finish``
+(one H2D copy, then a wait on the decode) run on the connection's loop
+thread, so every FSM on that loop (pings, expiry timers, watch delivery)
+waits for them.  For a 1M-request batch that is a few milliseconds, well
+under the ping interval (max(T/8, 2 s)); keep batches around 1M requests
+or fewer, or run huge batches on a client of their own so only its loop
+stalls.
+
 Without a GPU (CPU-only hosts, the CPU test suite) the same object encodes
 and decodes with the host codec (:mod:`zkmi.codec`), so the API works
 everywhere; on a GPU box the HIP path is the one that runs.

@@ -189,3 +189,62 @@ def test_loop_run_from_threads():
     for t in ts:
         t.join()
     assert sorted(out) == [(True, i) for i in range(8)]
+
+
+class _ManualLoop(object):
+    """A loop whose clock only moves when the test advances it."""
+
+    def __init__(self):
+        self.now = 0.0
+        self.timers = []
+
+    def time_ms(self):
+        return self.now
+
+    def call_later(self, ms, fn):
+        loop = self
+
+        class _H(object):
+            cancelled = False
+
+            def cancel(self):
+                self.cancelled = True
+                loop.timers.remove(entry)
+        entry = [self.now + ms, fn, _H()]
+        self.timers.append(entry)
+        return entry[2]
+
+    def advance(self, ms):
+        end = self.now + ms
+        while True:
+            due = [t for t in self.timers if t[0] <= end]
+            if not due:
+                break
+            t = min(due, key=lambda e: e[0])
+            self.timers.remove(t)
+            self.now = t[0]
+            t[1]()
+        self.now = end
+
+
+def test_expiry_timer_rearms_on_shorter_timeout():
+    """A reattach that negotiates a shorter session timeout must move the
+    expiry earlier (lib/zk-session.js:99-108 clears and re-sets the timer on
+    every reset); a reset with the same timeout pushes the deadline out."""
+    from zkmi.models.session import ExpiryTimer
+    loop = _ManualLoop()
+    fired = []
+    t = ExpiryTimer(loop)
+    t.on('timeout', lambda: fired.append(loop.time_ms()))
+    t.reset(30000)
+    loop.advance(1000)
+    t.reset(4000)              # deadline 5000, not the old 30000
+    loop.advance(10000)
+    assert fired == [5000]
+    t.reset(4000)              # at 11000: deadline 15000
+    loop.advance(2000)
+    t.reset(4000)              # at 13000: deadline pushed to 17000
+    loop.advance(3000)
+    assert fired == [5000]
+    loop.advance(1000)
+    assert fired == [5000, 17000]

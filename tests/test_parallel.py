@@ -93,6 +93,28 @@ def _scn_batched_get(rank, world, c, g, dist, wait_for, owner_of, zport):
     assert g.stats['batched_get_requested'] == 12
 
 
+def _scn_batched_get_timeout(rank, world, c, g, dist, wait_for, owner_of,
+                             zport):
+    """A rank whose session never answers: its reads fail with
+    OPERATION_TIMEOUT on every rank, and the collective still completes (no
+    rank is left blocked in the second all-gather)."""
+    if rank == 0:
+        for i in range(8):
+            c.call_sync('create', '/bt%d' % i, b'v%d' % i, {})
+    dist.barrier()
+    paths = ['/bt%d' % i for i in range(8)]
+    owners = set(owner_of(p, world) for p in paths)
+    assert owners == set(range(world))       # both ranks own some paths
+    if rank == 1:
+        c.get = lambda path, cb: None          # replies never come
+    res = g.batched_get(paths, timeout=0.5)
+    for p, r in zip(paths, res):
+        if owner_of(p, world) == 1:
+            assert getattr(r, 'code', None) == 'OPERATION_TIMEOUT', (p, r)
+        else:
+            assert r[0] == ('v' + p[3:]).encode(), (p, r)
+
+
 def _scn_watch_fanout(rank, world, c, g, dist, wait_for, owner_of, zport):
     path = '/fan'
     if rank == 0:
@@ -166,7 +188,7 @@ def _missing(c, p):
 # -- tests --------------------------------------------------------------------
 
 @pytest.mark.parametrize('scenario', ['metrics', 'batched_get',
-                                      'watch_fanout'])
+                                      'batched_get_timeout', 'watch_fanout'])
 def test_group_collectives(scenario):
     _run(scenario)
 

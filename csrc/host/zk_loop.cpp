@@ -494,8 +494,11 @@ int32_t be32(const char* p) {
   return (int32_t)ntohl(v);
 }
 
+void deliver(Transport* t, const char* p, size_t n);
+
 // End the capture: done(status, nbytes, nframes, last_off), then the bytes
-// after the last parsed frame go to Python.
+// after the last parsed frame go on (to a capture done() started, or to
+// Python).
 void capture_end(Transport* t, int status) {
   Capture& c = *t->cap;
   c.on = false;
@@ -512,7 +515,11 @@ void capture_end(Transport* t, int status) {
     Py_XDECREF(r);
     Py_DECREF(cb);
   }
-  if (!t->closed) deliver_raw(t, rest.data(), rest.size());
+  // The done callback may have started the next capture (a bulk callback
+  // chaining the next batch): the leftover bytes then belong to it, so
+  // they go through deliver(), which frames them into a capture that is on
+  // and passes them to Python raw otherwise.
+  if (!t->closed && !rest.empty()) deliver(t, rest.data(), rest.size());
 }
 
 void deliver(Transport* t, const char* p, size_t n) {
@@ -998,8 +1005,10 @@ PyObject* Loop_run(Loop* L, PyObject*) {
       // thread polls instead of sleeping, so the reply to a request it just
       // wrote (or the next call_soon) is picked up without a wake-up from
       // an idle core (tens of us per hop on the GPU boxes).  Idle loops
-      // still block: the window only follows activity.
+      // still block: the window only follows activity (a timer firing is
+      // not activity), and time spent spinning comes off the wait.
       const double t_end = L->last_active + loop_spin_ms();
+      const double spin_start = mono_ms();
       for (;;) {
         n = epoll_wait(L->epfd, evs.data(), (int)evs.size(), 0);
         if (n != 0) break;
@@ -1007,7 +1016,7 @@ PyObject* Loop_run(Loop* L, PyObject*) {
         if (now >= t_end) {
           int rest = timeout;
           if (rest > 0) {
-            const double waited = now - (t_end - loop_spin_ms());
+            const double waited = now - spin_start;
             rest = std::max(0, rest - (int)waited);
           }
           n = epoll_wait(L->epfd, evs.data(), (int)evs.size(), rest);

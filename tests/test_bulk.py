@@ -116,6 +116,11 @@ def test_bulk_not_connected_and_bad_args(zk):
                lambda *a: None)
     with pytest.raises(TypeError):
         c.bulk_get('/a', lambda *a: None)
+    import torch
+    with pytest.raises(ValueError):       # device paths on the host codec
+        c.bulk_get((torch.zeros(2, dtype=torch.uint8),
+                    torch.zeros(1, dtype=torch.int64),
+                    torch.ones(1, dtype=torch.int32)), lambda *a: None)
     c.wait_connected(10)
     c.close_sync(10)
     b = Box()

@@ -263,3 +263,82 @@ def test_transport_capture_routes_xid_range(nl):
         nl.run(sock.destroy)
     finally:
         srv.shutdown()
+
+
+def test_chained_capture_takes_leftover_bytes(nl):
+    """A capture whose done callback starts the next capture (a bulk
+    callback chaining the next batch) hands the bytes after its last frame
+    to that capture: with both batches' replies in one read, the second
+    capture still gets all of its frames and Python none."""
+    import ctypes
+    from zkmi import jute
+    from zkmi.runtime.tcp import TcpSocket
+    from zkmi.streams import ZKDecoder
+    srv = FakeZKServer()
+    for k in range(100):
+        srv.cli_create('/q%03d' % k, b'w' * (k % 50))
+    try:
+        sock = TcpSocket(nl)
+        dec = ZKDecoder()
+        got = []
+        sock.on('data', lambda d: got.extend(dec.feed(d)[0]))
+        up = threading.Event()
+        sock.on('connect', up.set)
+        nl.run(lambda: sock.connect('127.0.0.1', srv.port))
+        assert up.wait(5)
+        nl.run(lambda: sock.write(jute.frame(jute.encode_connect_request({
+            'protocolVersion': 0, 'lastZxidSeen': 0, 'timeOut': 30000,
+            'sessionId': 0, 'passwd': b'\0' * 8}))))
+        assert wait_for(lambda: len(got) == 1, 5)
+        got.clear()
+        bufs = [ctypes.create_string_buffer(1 << 16) for _ in range(2)]
+        done = []
+
+        def second(*a):
+            done.append(('b',) + a)
+
+        def first(*a):
+            done.append(('a',) + a)
+            sock.capture(300, 50, ctypes.addressof(bufs[1]), 1 << 16,
+                         1 << 24, second, b'')
+
+        nl.run(lambda: sock.capture(200, 50, ctypes.addressof(bufs[0]),
+                                    1 << 16, 1 << 24, first, b''))
+        reqs = b''.join(jute.frame(jute.encode_request({
+            'xid': x0 + k, 'opcode': 'GET_DATA', 'watch': False,
+            'path': '/q%03d' % (k + (50 if x0 == 300 else 0))}))
+            for x0 in (200, 300) for k in range(50))
+        nl.run(lambda: sock.write(reqs))
+        assert wait_for(lambda: len(done) == 2, 10), done
+        assert [d[:2] for d in done] == [('a', 0), ('b', 0)]
+        assert done[0][3] == 50 and done[1][3] == 50
+        assert got == []
+        nl.run(sock.destroy)
+    finally:
+        srv.shutdown()
+
+
+def test_busy_poll_does_not_spin_between_timers():
+    """With the busy-poll window on, a loop whose only events are timers
+    blocks between them (the window follows socket activity only)."""
+    import subprocess
+    import sys
+    code = r'''
+import resource, time
+from zkmi.runtime import nloop
+lp = nloop.NativeLoop('spin-check')
+for k in range(1, 5):
+    lp.call_later(200 * k, lambda: None)
+time.sleep(0.1)
+r0 = resource.getrusage(resource.RUSAGE_SELF)
+time.sleep(0.9)
+r1 = resource.getrusage(resource.RUSAGE_SELF)
+lp.stop()
+print((r1.ru_utime + r1.ru_stime) - (r0.ru_utime + r0.ru_stime))
+'''
+    env = dict(os.environ, ZKMI_LOOP_SPIN_US='50')
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, '-c', code], cwd=root, env=env,
+                         stdout=subprocess.PIPE, text=True, timeout=60)
+    cpu = float(out.stdout.strip().splitlines()[-1])
+    assert cpu < 0.15, 'loop burnt %.2f s of CPU in 0.9 s of timers' % cpu

@@ -9,7 +9,11 @@
 
 Usage: ``python tools/build_native.py [--hip-only|--host-only|--sanitize]
 [-j N]``.
-Objects are cached under ``build/`` by source mtime.
+Objects are cached under ``build/``.  Every artefact is stamped with the
+hash of the sources and flags it was built from (``zkmi/ops/_srchash.py``)
+and rebuilt whenever that differs from the tree's hash — never by file age,
+so prebuilt binaries from another tree are never reused.  The kernel library
+embeds its hash (``zkmi_hip_src_hash``), which the loader checks.
 """
 
 import argparse
@@ -20,11 +24,13 @@ import sys
 import sysconfig
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from zkmi.ops import _srchash as SH  # noqa: E402
 KDIR = os.path.join(ROOT, 'csrc', 'kernels')
 HDIR = os.path.join(ROOT, 'csrc', 'host')
 BDIR = os.path.join(ROOT, 'build')
 HIP_SO = os.path.join(ROOT, 'zkmi', 'ops', 'libzkmi_hip.so')
-ARCH = os.environ.get('ZKMI_OFFLOAD_ARCH', 'gfx950')
+ARCH = SH.ARCH
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 
 
@@ -37,11 +43,16 @@ def _run(cmd):
     return r.stdout
 
 
-def _stale(out, deps):
-    if not os.path.exists(out):
-        return True
-    t = os.path.getmtime(out)
-    return any(os.path.getmtime(d) > t for d in deps)
+def _stale(out, deps, extra=''):
+    """(rebuild needed, hash): ``out`` is missing or its stamp is not the
+    hash of ``deps`` + ``extra``."""
+    h = SH.files_hash(deps, extra)
+    return (not os.path.exists(out) or SH.read_stamp(out) != h), h
+
+
+def _stamped(out, h):
+    SH.write_stamp(out, h)
+    return out
 
 
 def build_hip(jobs=4):
@@ -49,21 +60,30 @@ def build_hip(jobs=4):
     srcs = sorted(f for f in os.listdir(KDIR) if f.endswith('.hip'))
     hdrs = [os.path.join(KDIR, f) for f in os.listdir(KDIR)
             if f.endswith('.h')]
-    flags = ['--offload-arch=' + ARCH, '-O3', '-fPIC', '-std=c++17',
-             '-Wno-unused-result', '-Wno-unused-value', '-munsafe-fp-atomics']
+    flags = SH.HIP_FLAGS
     objs = []
     todo = []
     for s in srcs:
         src = os.path.join(KDIR, s)
         obj = os.path.join(BDIR, s.replace('.hip', '.o'))
         objs.append(obj)
-        if _stale(obj, [src] + hdrs):
-            todo.append([HIPCC] + flags + ['-c', src, '-o', obj])
+        stale, h = _stale(obj, [src] + hdrs, ' '.join(flags))
+        if stale:
+            todo.append((obj, h, [HIPCC] + flags + ['-c', src, '-o', obj]))
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
-        list(ex.map(_run, todo))
-    if todo or _stale(HIP_SO, objs):
+        list(ex.map(lambda t: (_run(t[2]), _stamped(t[0], t[1])), todo))
+    full = SH.hip_hash()
+    if todo or SH.read_stamp(HIP_SO) != full or not os.path.exists(HIP_SO):
+        # the library carries the hash of the sources it was built from
+        stamp_src = os.path.join(BDIR, 'zkmi_stamp.cpp')
+        with open(stamp_src, 'w') as f:
+            f.write('extern "C" const char *zkmi_hip_src_hash(void) '
+                    '{ return "%s"; }\n' % full)
+        stamp_obj = os.path.join(BDIR, 'zkmi_stamp.o')
+        _run(['g++', '-O2', '-fPIC', '-c', stamp_src, '-o', stamp_obj])
         _run([HIPCC, '--offload-arch=' + ARCH, '-shared', '-fPIC', '-o',
-              HIP_SO] + objs)
+              HIP_SO] + objs + [stamp_obj])
+        _stamped(HIP_SO, full)
     return HIP_SO
 
 
@@ -79,8 +99,9 @@ def build_torch_ops():
     (found through the rpath)."""
     import torch
     src = os.path.join(TDIR, 'zkmi_ops.cpp')
-    deps = [src, os.path.join(KDIR, 'zk_batch.h'), HIP_SO]
-    if not _stale(TORCH_SO, deps):
+    deps = [src, os.path.join(KDIR, 'zk_batch.h')]
+    stale, h = _stale(TORCH_SO, deps, torch.__version__)
+    if not stale:
         return TORCH_SO
     tdir = os.path.dirname(torch.__file__)
     inc = [os.path.join(tdir, 'include'),
@@ -95,7 +116,7 @@ def build_torch_ops():
           '-L' + os.path.dirname(HIP_SO), '-lzkmi_hip', '-lc10', '-lc10_hip',
           '-ltorch_cpu', '-Wl,-rpath,$ORIGIN',
           '-Wl,-rpath,' + os.path.join(tdir, 'lib')])
-    return TORCH_SO
+    return _stamped(TORCH_SO, h)
 
 
 def host_so_path():
@@ -120,9 +141,11 @@ def build_fastserver():
     executable: zkmi/server/fast.py runs it as a child process."""
     src = os.path.join(HDIR, 'zk_fastserver.cpp')
     os.makedirs(os.path.dirname(FAST_SERVER), exist_ok=True)
-    if _stale(FAST_SERVER, [src]):
+    stale, h = _stale(FAST_SERVER, [src])
+    if stale:
         _run(['g++', '-O3', '-std=c++17', '-Wall', '-Wextra', src, '-o',
-              FAST_SERVER])
+              FAST_SERVER, '-lpthread'])
+        _stamped(FAST_SERVER, h)
     return FAST_SERVER
 
 
@@ -132,11 +155,13 @@ def build_host():
     for name, src in HOST_EXTS.items():
         src = os.path.join(HDIR, src)
         out = _ext_path(name)
-        if _stale(out, [src]):
+        stale, h = _stale(out, [src])
+        if stale:
             _run(['g++', '-O3', '-fPIC', '-shared', '-std=c++17', '-Wall',
                   '-Wextra', '-Wno-missing-field-initializers',
                   '-Wno-cast-function-type', '-fno-strict-aliasing',
                   '-I' + inc, src, '-o', out])
+            _stamped(out, h)
         outs.append(out)
     return outs
 
@@ -157,11 +182,13 @@ def build_host_sanitized():
     for name, src in HOST_EXTS.items():
         src = os.path.join(HDIR, src)
         out = os.path.join(SANITIZE_DIR, name + suffix)
-        if _stale(out, [src]):
+        stale, h = _stale(out, [src], 'asan')
+        if stale:
             _run(['g++', '-O1', '-g', '-fPIC', '-shared', '-std=c++17',
                   '-Wall', '-fno-strict-aliasing', '-fno-omit-frame-pointer',
                   '-fsanitize=address,undefined', '-fno-sanitize-recover=all',
                   '-I' + inc, src, '-o', out])
+            _stamped(out, h)
         outs.append(out)
     return outs
 
@@ -178,10 +205,12 @@ def build_loop_tsan():
     suffix = sysconfig.get_config_var('EXT_SUFFIX') or '.so'
     src = os.path.join(HDIR, HOST_EXTS['_zkloop'])
     out = os.path.join(TSAN_DIR, '_zkloop' + suffix)
-    if _stale(out, [src]):
+    stale, h = _stale(out, [src], 'tsan')
+    if stale:
         inc = sysconfig.get_paths()['include']
         _run(['g++', '-O1', '-g', '-fPIC', '-shared', '-std=c++17', '-Wall',
               '-fsanitize=thread', '-I' + inc, src, '-o', out])
+        _stamped(out, h)
     return out
 
 

@@ -534,6 +534,10 @@ class Client(FSM):
         _check_func(cb)
         if isinstance(paths, tuple) and len(paths) == 3 and \
                 hasattr(paths[0], 'device'):
+            from .bulk import _gpu_device
+            if _gpu_device(self.bulk_device) is None:
+                raise ValueError('bulk_get: a device (arena, off, len) '
+                                 'triple needs a GPU bulk device')
             batch = BulkBatch.gets(paths, self.bulk_device)
         elif isinstance(paths, (list, tuple)):
             for p in paths:

@@ -9,9 +9,12 @@ contiguity and lengths of its tensors before a pointer reaches a kernel,
 runs on the current HIP stream and raises on a launch error.
 
 On a machine with a GPU a missing library is an error (:func:`lib`
-raises); there is no silent CPU fallback for the batch codec.
+raises); there is no silent CPU fallback for the batch codec.  So is a
+kernel library built from other sources than this tree's
+(``zkmi/ops/_srchash.py``): its embedded source hash must match.
 """
 
+import ctypes
 import os
 
 import torch
@@ -48,6 +51,7 @@ def lib():
             raise RuntimeError(
                 'zkmi operator library not built: run `python tools/'
                 'build_native.py` (or __graft_entry__.build())')
+        check_build()
         torch.ops.load_library(LIB_PATH)
         _ops = torch.ops.zkmi
         # ZKMI_SCAN=shfl selects the shuffle scan engine instead of the
@@ -55,6 +59,30 @@ def lib():
         _ops.scan_set_mode(SCAN_SHFL if os.environ.get('ZKMI_SCAN') ==
                            'shfl' else SCAN_MFMA)
     return _ops
+
+
+def built_hash():
+    """The source hash embedded in ``libzkmi_hip.so`` (None if absent)."""
+    try:
+        f = ctypes.CDLL(HIP_LIB_PATH).zkmi_hip_src_hash
+    except (OSError, AttributeError):
+        return None
+    f.restype = ctypes.c_char_p
+    return f().decode()
+
+
+def check_build():
+    """Raise unless the kernel library was compiled from this tree's kernel
+    sources and flags (``ZKMI_ALLOW_STALE_BUILD=1`` skips the check for
+    A/B runs that swap libraries on purpose)."""
+    from . import _srchash
+    if os.environ.get('ZKMI_ALLOW_STALE_BUILD') == '1':
+        return
+    want, got = _srchash.hip_hash(), built_hash()
+    if got != want:
+        raise RuntimeError(
+            'zkmi/ops/libzkmi_hip.so was built from other sources (hash %s, '
+            'tree %s): run `python tools/build_native.py`' % (got, want))
 
 
 def set_scan_mode(mode):

@@ -367,7 +367,10 @@ class EnsembleWorkload(object):
         this rank received."""
         got = 0
         t_end = time.monotonic() + timeout
-        flag = torch.zeros(1, dtype=torch.int64, device=self.coll)
+        # [not done, timed out], all-reduced with MAX: every rank stops
+        # together, and a rank's timeout makes every rank raise (none is
+        # left waiting in the next collective)
+        flag = torch.zeros(2, dtype=torch.int64, device=self.coll)
         while True:
             with self._lk:
                 batch = self.pending[:KMAX]
@@ -375,13 +378,16 @@ class EnsembleWorkload(object):
             for src, path, data, stat in self.fan.exchange(batch):
                 self.seen[(path, data)] += 1
                 got += 1
-            flag.fill_(1 if got >= want else 0)
+            flag[0] = 0 if got >= want else 1
+            flag[1] = 1 if time.monotonic() > t_end else 0
             if self.world > 1:
-                dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.group)
-            if int(flag.item()):
+                dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=self.group)
+            busy, late = flag.tolist()
+            if not busy:
                 return got
-            if time.monotonic() > t_end:
-                raise RuntimeError('fan-out: %d of %d events after %.0f s'
+            if late:
+                raise RuntimeError('fan-out: %d of %d events after %.0f s '
+                                   '(on this rank or another)'
                                    % (got, want, timeout))
             time.sleep(0.002)
 

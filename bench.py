@@ -22,11 +22,25 @@ node payloads, uniformly random node per request.
 
 Each GPU serves its batch over ``--streams`` (default 2) pipelined
 connections, each on its own HIP stream with its own buffers and xid table;
-a step makes no device-to-host read (terminated streams, frame-scanned over
-host-known length bounds), so the connections' kernels overlap.
+a step makes no device-to-host read (K1 reads every stream's length from
+the device byte count its encoder produced), so the connections' kernels
+overlap.
 
-One process per GPU (torchrun); per-GPU work is fixed (weak scaling).  The
-whole-node aggregate (sum over ranks of ops / max-rank time) is reported.
+GET scale-out (the headline at every N): ONE tree sharded by path hash over
+the ranks, every read routed to the rank that owns its path (R2,
+zkmi/parallel/sharded.py): per connection and step, two equal-split
+``all_to_all_single`` over RCCL/xGMI (the request slots out, the reply
+slots back) — the bytes really cross the GPUs.  With one GPU there is one
+shard and nothing to route; the step is the local pipeline, HIP-graph
+captured.  For N > 1 the same run also times ``--replica`` (every rank
+serves its own full replica, no collective in the step) and reports it as
+``replica_value``; ``--replica`` makes that the headline instead.
+
+One process per GPU: ``--gpus N`` without a torchrun environment starts the
+N rank processes itself (before anything touches the GPU); under torchrun
+the ranks come from the environment.  Per-GPU work is fixed (weak
+scaling).  The whole-node aggregate (sum over ranks of ops / max-rank time)
+is reported.
 ``p50_get_rtt_us`` is the interactive path: one blocking ``Client.get``
 round trip over loopback TCP to the fake server running as its own process
 (``python -m zkmi.server``, started before the GPU is touched), with the
@@ -324,12 +338,13 @@ def main():
     ap.add_argument('--workload', choices=('get', 'mix', 'storm', 'watch',
                                            'ensemble', 'chain'),
                     default='get')
-    ap.add_argument('--sharded', action='store_true',
-                    help='get: one tree sharded by path hash over the '
-                         'ranks; every read is routed to its owner rank '
-                         'with all_to_all over RCCL/xGMI (R2, '
-                         'zkmi/parallel/sharded.py) instead of served by '
-                         'the local replica')
+    ap.add_argument('--replica', action='store_true',
+                    help='get: every rank serves its own full replica of the '
+                         'tree (no collective in the step) instead of the '
+                         'path-hash-sharded tree with R2 routing over '
+                         'RCCL/xGMI (the default)')
+    ap.add_argument('--no-compare', action='store_true',
+                    help='get, N > 1: skip the replica comparison run')
     ap.add_argument('--paths', type=int, default=512,
                     help='ensemble: watched znodes (one owner rank each)')
     ap.add_argument('--writes', type=int, default=128,
@@ -339,8 +354,121 @@ def main():
                          'is on and makes that step\'s writes during the '
                          'outage (replayed through SET_WATCHES)')
     a = ap.parse_args()
+    if a.gpus > 1 and 'WORLD_SIZE' not in os.environ:
+        return launch(a)
+    # a rank that fails (tests inject one with ZKMI_BENCH_FAIL_RANK) ends
+    # the whole launch; the other ranks are stopped by the launcher
+    fail = os.environ.get('ZKMI_BENCH_FAIL_RANK')
+    if fail is not None and fail == os.environ.get('RANK', '0'):
+        raise SystemExit('rank %s: injected failure' % fail)
     if a.workload == 'ensemble':
         return run_ensemble(a)
+    return run_rank(a)
+
+
+def _free_port():
+    import socket
+    so = socket.socket()
+    so.bind(('127.0.0.1', 0))
+    port = so.getsockname()[1]
+    so.close()
+    return port
+
+
+def launch(a):
+    """``--gpus N`` outside torchrun: start the N rank processes (one per
+    GPU, RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in their environment,
+    rendezvous on 127.0.0.1) and exit with the first failure's code.  This
+    process never touches the GPU (counting devices does not initialise
+    it)."""
+    n = a.gpus
+    backend = os.environ.get('ZKMI_BENCH_BACKEND', 'nccl')
+    ndev = torch.cuda.device_count()
+    if backend == 'nccl' and ndev < n and not (ndev == 0 and
+                                               a.workload == 'ensemble'):
+        raise SystemExit('--gpus %d: %d GPU(s) visible (RCCL needs one per '
+                         'rank; ZKMI_BENCH_BACKEND=gloo shares them)'
+                         % (n, ndev))
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r),
+                   WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK='0', MASTER_ADDR='127.0.0.1',
+                   MASTER_PORT=str(port))
+        procs.append(subprocess.Popen(
+            [sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+            env=env, cwd=ROOT))
+    rc = 0
+    live = list(procs)
+    while live:
+        time.sleep(0.2)
+        for p in list(live):
+            c = p.poll()
+            if c is None:
+                continue
+            live.remove(p)
+            if c != 0 and rc == 0:
+                rc = c
+                for q in live:             # the others would wait forever
+                    q.terminate()
+    for p in procs:
+        try:
+            p.wait(30)
+        except subprocess.TimeoutExpired:
+            p.kill()
+    if rc:
+        raise SystemExit(rc if rc > 0 else 128 - rc)
+    return 0
+
+
+def _time_steps(pipe, a, world, dev):
+    """Warm up, optionally capture one step as a HIP graph, then time
+    ``a.steps`` steps between barriers + device syncs.  Returns (seconds
+    on this rank, correct replies counted on the device, graph used)."""
+    ok_total = torch.zeros(64, dtype=torch.int64, device=dev)
+    for _ in range(a.warmup):
+        pipe.step(acc=ok_total)
+    run = lambda: pipe.step(acc=ok_total)            # noqa: E731
+    graph = not a.no_graph and hasattr(pipe, 'capture') and \
+        getattr(pipe, 'capturable', True)
+    if graph:
+        try:
+            g = pipe.capture(ok_total)
+            run = g.replay
+            for _ in range(2):
+                run()
+        except RuntimeError as e:              # keep the run: eager steps
+            print('graph capture failed, timing eager steps: %s' % e,
+                  file=sys.stderr)
+            graph = False
+            run = lambda: pipe.step(acc=ok_total)    # noqa: E731
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ok_total.zero_()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        run()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    return time.perf_counter() - t0, ok_total, graph
+
+
+def _reduce(elapsed, ok_total, world, cdev):
+    """(max seconds over ranks, correct replies summed over ranks) — R4."""
+    el = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
+    ok = ok_total.sum().view(1).to(cdev)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        dist.all_reduce(ok, op=dist.ReduceOp.SUM)
+    return el.item(), int(ok.item())
+
+
+def run_rank(a):
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
@@ -372,20 +500,24 @@ def main():
         dd = tuple(int(x) for x in rng.split('-'))
     if a.name_pad:
         npad = tuple(int(x) for x in a.name_pad.split('-'))
-    if a.workload == 'get' and a.sharded:
+    sharded = a.workload == 'get' and not a.replica
+
+    def make_get(replica):
+        if replica:
+            tree = S.GpuTree(a.nodes, a.data_bytes, device=dev, seed=rank,
+                             data_dist=dd, name_pad=npad)
+            return S.GetPipeline(tree, a.batch, seed=rank, streams=a.streams,
+                                 stagger=a.stagger)
         from zkmi.parallel.sharded import ShardedGetPipeline
-        # every rank holds the same layout and data; its index covers only
-        # the leaves whose path hashes to it
+        # every rank holds the same layout and data (seed 0); its index
+        # covers only the leaves whose path hashes to it
         tree = S.GpuTree(a.nodes, a.data_bytes, device=dev, seed=0,
-                         shard=(rank, world))
-        pipe = ShardedGetPipeline(tree, a.batch, seed=rank,
-                                  coll_device=cdev)
-        per_step = a.batch
-    elif a.workload == 'get':
-        tree = S.GpuTree(a.nodes, a.data_bytes, device=dev, seed=rank,
-                         data_dist=dd, name_pad=npad)
-        pipe = S.GetPipeline(tree, a.batch, seed=rank, streams=a.streams,
-                             stagger=a.stagger)
+                         data_dist=dd, name_pad=npad, shard=(rank, world))
+        return ShardedGetPipeline(tree, a.batch, seed=rank, coll_device=cdev,
+                                  streams=a.streams)
+
+    if a.workload == 'get':
+        pipe = make_get(not sharded)
         per_step = a.batch
     elif a.workload == 'watch':
         tree = S.GpuTree(a.nodes, a.data_bytes, device=dev, seed=rank)
@@ -413,52 +545,45 @@ def main():
             pipe = S.StormPipeline(tree, a.batch, seed=rank)
             per_step = pipe.n
 
+    ops = per_step * a.steps * world
+
+    def checked(pipe, elapsed, ok_total):
+        elapsed, ok = _reduce(elapsed, ok_total, world, cdev)
+        if ok != ops:
+            if hasattr(pipe, 'diagnose'):
+                print('diagnose:', pipe.diagnose(), file=sys.stderr)
+            raise SystemExit('validation failed: %d of %d replies wrong'
+                             % (ops - ok, ops))
+        return elapsed
+
     # 64 counter slots (the fused GET check spreads its per-block atomics
     # over them); the other checks add into slot 0
-    ok_total = torch.zeros(64, dtype=torch.int64, device=dev)
-    for _ in range(a.warmup):
-        pipe.step(acc=ok_total)
-    run = lambda: pipe.step(acc=ok_total)            # noqa: E731
-    a.graph = not a.no_graph and hasattr(pipe, 'capture')
-    if a.graph:
-        try:
-            g = pipe.capture(ok_total)
-            run = g.replay
-            for _ in range(2):
-                run()
-        except RuntimeError as e:              # keep the run: eager steps
-            print('graph capture failed, timing eager steps: %s' % e,
-                  file=sys.stderr)
-            a.graph = False
-            run = lambda: pipe.step(acc=ok_total)    # noqa: E731
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    ok_total.zero_()
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        run()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-
-    el = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
-    ok = ok_total.sum().view(1).to(cdev)
-    if world > 1:
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
-        dist.all_reduce(ok, op=dist.ReduceOp.SUM)   # R4: node-level counters
-    elapsed = el.item()
-    ops = per_step * a.steps * world
-    ok = int(ok.item())
-    if ok != ops:
-        if hasattr(pipe, 'diagnose'):
-            print('diagnose:', pipe.diagnose(), file=sys.stderr)
-        raise SystemExit('validation failed: %d of %d replies wrong'
-                         % (ops - ok, ops))
+    elapsed, ok_total, a.graph = _time_steps(pipe, a, world, dev)
+    elapsed = checked(pipe, elapsed, ok_total)
     value = ops / elapsed
+    r2 = None
+    if sharded:
+        st = pipe.stats
+        r2 = {'bytes_sent_per_rank_step': st['bytes_sent'] / max(st['steps'],
+                                                                 1),
+              'wire_bytes_sent_per_rank_step':
+                  st['wire_bytes_sent'] / max(st['steps'], 1),
+              'remote_requests': st['remote_reqs'],
+              'overflow_segments': st['overflow_segments'],
+              'slot_bytes': {'request': st['req_slot_bytes'],
+                             'reply': st['rep_slot_bytes']}}
+    replica = None
+    if sharded and world > 1 and not a.no_compare:
+        # the same batch served by per-rank full replicas (no collective in
+        # the step): what the sharding's xGMI traffic costs
+        del pipe
+        torch.cuda.empty_cache()
+        rp = make_get(True)
+        rel, rok, rgraph = _time_steps(rp, a, world, dev)
+        rel = checked(rp, rel, rok)
+        replica = {'value': ops / rel, 'ms_per_step': rel / a.steps * 1e3,
+                   'hip_graph': bool(rgraph)}
+        del rp
 
     rtt50 = rtt99 = py50 = py99 = bulk_ops = bulk_ms = None
     ev50 = ev99 = None
@@ -496,16 +621,25 @@ def main():
             'hip_graph': bool(a.graph),
             'data': 'synthetic',
             'config': {
-                'model': 'zk-%s%s %dk-znode tree, %s data%s' % (
-                    a.workload, ' sharded' if a.sharded else '',
+                'model': 'zk-%s %dk-znode tree, %s data%s' % (
+                    a.workload,
                     a.nodes // 1000,
                     ('%d-%dB' % dd) if dd else '%dB' % a.data_bytes,
                     (', names +%d-%d chars' % npad) if npad else ''),
                 'global_batch': per_step * world,
                 'seq_len': 1,
-                'parallelism': 'dp%d' % world,
+                'parallelism': ('r2shard%d' % world) if sharded and
+                               world > 1 else 'dp%d' % world,
             },
-            'r2_bytes_sent': getattr(pipe, 'stats', {}).get('bytes_sent'),
+            'get_mode': ('sharded: one tree, path-hash shards over %d '
+                         'ranks, reads routed with all_to_all over '
+                         'RCCL/xGMI' % world if world > 1 else
+                         'one shard (nothing to route), local pipeline')
+                        if sharded else
+                        ('replica per rank' if a.workload == 'get' else None),
+            'r2': r2,
+            'replica_value': replica['value'] if replica else None,
+            'replica_ms_per_step': replica['ms_per_step'] if replica else None,
             'p50_get_rtt_us': rtt50,
             'p99_get_rtt_us': rtt99,
             'rtt_note': 'one blocking Client.get over loopback TCP to the '

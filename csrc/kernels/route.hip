@@ -98,6 +98,119 @@ __global__ __launch_bounds__(RT_T) void route_counts_k(
   counts[w] = b1 - b0;
 }
 
+// ---------------------------------------------------------------------------
+// Fixed-capacity per-peer segments (the sync-free R2 exchange).
+//
+// all_to_all_single with equal splits needs no host-side split sizes, so a
+// step never reads the device back: every rank sends each peer one slot of
+// `slot_cap` bytes = a 16-byte header {payload bytes, records} (int64 x2)
+// and the payload.  seg_pack_k cuts a framed stream whose records are
+// grouped by destination (counts[w] consecutive records each) into the
+// slots; seg_unpack_k concatenates the received slots' payloads back into
+// one contiguous stream (source rank order) with its device length and the
+// per-source record counts.  A segment that does not fit its slot is sent
+// empty and counted in stats[0] (the receiving check then fails loudly).
+
+constexpr int SG_T = 256;
+constexpr int64_t SEG_HDR = 16;
+
+// Copy n bytes s -> d with the nt threads of a team (this thread is t):
+// 16-byte stores aligned on the destination, 16-byte loads at any address
+// (gfx950 unaligned mode); the ragged head and tail go byte by byte, so a
+// team writes exactly its own bytes and neighbouring spans never race.
+ZK_DEV void team_copy(uint8_t* __restrict__ d, const uint8_t* __restrict__ s,
+                      int64_t n, int64_t t, int64_t nt) {
+  if (n <= 0) return;
+  int64_t head = (16 - (int64_t)((uintptr_t)d & 15)) & 15;
+  if (head > n) head = n;
+  if (t < head) d[t] = s[t];
+  const int64_t body = (n - head) >> 4;
+  uint8_t* db = d + head;
+  const uint8_t* sb = s + head;
+  for (int64_t k = t; k < body; k += nt) {
+    uint4 v;
+    __builtin_memcpy(&v, sb + 16 * k, 16);
+    *reinterpret_cast<uint4*>(db + 16 * k) = v;
+  }
+  const int64_t t0 = head + 16 * body;
+  if (t < n - t0) d[t0 + t] = s[t0 + t];
+}
+
+__global__ __launch_bounds__(SG_T) void seg_pack_k(
+    const uint8_t* __restrict__ src, int64_t src_cap,
+    const int64_t* __restrict__ rec_off, const int64_t* __restrict__ nrec_dev,
+    int64_t nrec_cap, const int64_t* __restrict__ total,
+    const int64_t* __restrict__ counts, int32_t world, int32_t self,
+    int64_t slot_cap, uint8_t* __restrict__ out,
+    unsigned long long* __restrict__ stats) {
+  const int32_t w = blockIdx.y;
+  int64_t f = 0;
+  for (int32_t k = 0; k < w; ++k) f += counts[k];
+  const int64_t c = counts[w];
+  int64_t nrec = nrec_cap;
+  if (nrec_dev != nullptr && *nrec_dev < nrec) nrec = *nrec_dev;
+  const int64_t tot = *total;
+  const int64_t s0 = f < nrec ? rec_off[f] : tot;
+  const int64_t e0 = f + c < nrec ? rec_off[f + c] : tot;
+  const int64_t bytes = e0 - s0;
+  const bool ok = c >= 0 && f >= 0 && f + c <= nrec && s0 >= 0 &&
+                  bytes >= 0 && e0 <= src_cap && bytes <= slot_cap - SEG_HDR;
+  uint8_t* slot = out + (int64_t)w * slot_cap;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    const int64_t h[2] = {ok ? bytes : 0, ok ? c : 0};
+    __builtin_memcpy(slot, h, 16);
+    if (!ok) atomicAdd(&stats[0], 1ull);
+    else if (w != self) {
+      atomicAdd(&stats[1], (unsigned long long)bytes);
+      atomicAdd(&stats[2], (unsigned long long)c);
+    }
+  }
+  if (!ok) return;
+  team_copy(slot + SEG_HDR, src + s0, bytes,
+            (int64_t)blockIdx.x * SG_T + threadIdx.x,
+            (int64_t)gridDim.x * SG_T);
+}
+
+ZK_DEV void seg_hdr(const uint8_t* in, int32_t k, int64_t slot_cap,
+                    int64_t* bytes, int64_t* recs) {
+  int64_t h[2];
+  __builtin_memcpy(h, in + (int64_t)k * slot_cap, 16);
+  *bytes = h[0] < 0 ? 0 : (h[0] > slot_cap - SEG_HDR ? slot_cap - SEG_HDR
+                                                      : h[0]);
+  *recs = h[1] < 0 ? 0 : h[1];
+}
+
+__global__ __launch_bounds__(SG_T) void seg_unpack_k(
+    const uint8_t* __restrict__ in, int32_t world, int32_t self,
+    int64_t slot_cap, uint8_t* __restrict__ out,
+    int64_t* __restrict__ total_out, int64_t* __restrict__ counts_out,
+    unsigned long long* __restrict__ stats) {
+  const int32_t w = blockIdx.y;
+  int64_t pre = 0, mine = 0, all = 0, peers = 0;
+  for (int32_t k = 0; k < world; ++k) {
+    int64_t b, r;
+    seg_hdr(in, k, slot_cap, &b, &r);
+    if (k < w) pre += b;
+    if (k == w) mine = b;
+    if (k != self) peers += b;
+    all += b;
+  }
+  if (blockIdx.x == 0 && w == 0) {
+    if (threadIdx.x == 0) {
+      *total_out = all;
+      if (stats != nullptr) atomicAdd(&stats[0], (unsigned long long)peers);
+    }
+    if (threadIdx.x < world) {
+      int64_t b, r;
+      seg_hdr(in, threadIdx.x, slot_cap, &b, &r);
+      counts_out[threadIdx.x] = r;
+    }
+  }
+  team_copy(out + pre, in + (int64_t)w * slot_cap + SEG_HDR, mine,
+            (int64_t)blockIdx.x * SG_T + threadIdx.x,
+            (int64_t)gridDim.x * SG_T);
+}
+
 }  // namespace zk
 
 extern "C" {
@@ -141,6 +254,48 @@ int zk_route_requests(int64_t n, int32_t world, const int64_t* poff,
   zk::route_scatter_k<<<(unsigned)nblk, zk::RT_T, 0, st>>>(
       n, world, owner, base, idx, xid, poff, plen, idx_s, xid_s, poff_s,
       plen_s);
+  ZK_LAUNCH_CHECK();
+  return 0;
+}
+
+// Team size per segment: enough blocks to stream a full slot, at most 512.
+static unsigned seg_blocks(int64_t slot_cap) {
+  int64_t b = (slot_cap + 16 * zk::SG_T - 1) / (16 * zk::SG_T);
+  return (unsigned)(b < 1 ? 1 : (b > 512 ? 512 : b));
+}
+
+// Pack the framed stream src (records at rec_off, nrec = min(*nrec_dev,
+// nrec_cap) of them, *total bytes) into `world` slots of slot_cap bytes:
+// slot w gets records [sum(counts[:w]), +counts[w]).  stats (uint64 [3]):
+// += segments that did not fit, payload bytes and records for peers.
+int zk_seg_pack(const uint8_t* src, int64_t src_cap, const int64_t* rec_off,
+                const int64_t* nrec_dev, int64_t nrec_cap,
+                const int64_t* total, const int64_t* counts, int32_t world,
+                int32_t self, int64_t slot_cap, uint8_t* out,
+                unsigned long long* stats, hipStream_t st) {
+  if (world < 1 || world > zk::RT_MAXW || slot_cap < 32 || (slot_cap & 15))
+    return (int)hipErrorInvalidValue;
+  dim3 grid(seg_blocks(slot_cap), (unsigned)world);
+  zk::seg_pack_k<<<grid, zk::SG_T, 0, st>>>(
+      src, src_cap, rec_off, nrec_dev, nrec_cap, total, counts, world, self,
+      slot_cap, out, stats);
+  ZK_LAUNCH_CHECK();
+  return 0;
+}
+
+// Concatenate the payloads of `world` received slots into out (source rank
+// order); *total_out = its length, counts_out[w] = records from rank w,
+// stats[0] (optional) += payload bytes from the other ranks.  out must hold
+// world * (slot_cap - 16) bytes.
+int zk_seg_unpack(const uint8_t* in, int32_t world, int32_t self,
+                  int64_t slot_cap, uint8_t* out, int64_t* total_out,
+                  int64_t* counts_out, unsigned long long* stats,
+                  hipStream_t st) {
+  if (world < 1 || world > zk::RT_MAXW || slot_cap < 32 || (slot_cap & 15))
+    return (int)hipErrorInvalidValue;
+  dim3 grid(seg_blocks(slot_cap), (unsigned)world);
+  zk::seg_unpack_k<<<grid, zk::SG_T, 0, st>>>(in, world, self, slot_cap, out,
+                                               total_out, counts_out, stats);
   ZK_LAUNCH_CHECK();
   return 0;
 }

@@ -64,6 +64,10 @@ struct ZkTree {
   int32_t* dirty;              // [cap] parent-on-dirty-list flag
   int64_t* dirty_list;         // [cap]
   int64_t* node_pw;            // [cap] path word: offset << 24 | length
+  // watch table (null wt_key: the tree keeps no watches), see wt_* below
+  int64_t* wt_key;             // [wt_hmask + 1] path hash | 1, 0 = empty
+  unsigned long long* wt_mask; // [2 * (wt_hmask + 1)] data / child masks
+  int64_t wt_hmask;
 };
 }
 
@@ -290,6 +294,66 @@ ZK_DEV bool tree_erase(const ZkTree& t, int64_t v, const uint8_t* p,
   return false;
 }
 
+// ---- watches (one-shot, per watcher slot) ---------------------------------
+// A path-keyed table beside the tree (lib/zk-session.js:482-526 describes
+// the server semantics the client relies on): key = path
+// hash | 1 (0 = empty, linear probing, entries are never removed), two
+// 64-bit masks per entry — the data watches (GET_DATA / EXISTS with
+// watch=1; an EXISTS on a missing path is ZooKeeper's "exist" watch, kept
+// in the same set like the server's dataWatches) and the child watches —
+// one bit per watcher slot (<= 64 sessions of the server).  Firing is an
+// atomic exchange with 0: one-shot, and each watcher of a path is notified
+// exactly once even when several writes of a batch hit the path (the first
+// takes the mask).  Paths are keyed, not nodes, so a watch on a missing
+// path waits for its creation.
+enum : int { WK_DATA = 0, WK_CHILD = 1 };
+// notification types (lib/zk-consts.js NOTIFICATION_TYPE)
+enum : int32_t { NT_CREATED = 1, NT_DELETED = 2, NT_DATA_CHANGED = 3,
+                 NT_CHILDREN_CHANGED = 4 };
+constexpr int WT_REC = 5;    // per request: m_path, m_path_child, m_parent,
+                             // path word of the node, of its parent
+
+ZK_DEV int64_t wt_slot(const ZkTree& t, uint64_t key, bool insert) {
+  int64_t s = (int64_t)key & t.wt_hmask;
+  for (int64_t probe = 0; probe <= t.wt_hmask; ++probe) {
+    int64_t k = __hip_atomic_load(&t.wt_key[s], __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT);
+    if (k == (int64_t)key) return s;
+    if (k == 0) {
+      if (!insert) return -1;
+      k = (int64_t)atomicCAS((unsigned long long*)&t.wt_key[s], 0ull,
+                             (unsigned long long)key);
+      if (k == 0 || k == (int64_t)key) return s;
+    }
+    s = (s + 1) & t.wt_hmask;
+  }
+  return -1;                                      // table full
+}
+
+ZK_DEV void wt_arm(const ZkTree& t, const uint8_t* p, int32_t n, int kind,
+                   int32_t wslot) {
+  if (t.wt_key == nullptr || wslot < 0 || wslot > 63) return;
+  const int64_t s = wt_slot(t, path_hash(p, n) | 1ull, true);
+  if (s >= 0) atomicOr(&t.wt_mask[2 * s + kind], 1ull << wslot);
+}
+
+ZK_DEV uint64_t wt_fire(const ZkTree& t, const uint8_t* p, int32_t n,
+                        int kind) {
+  if (t.wt_key == nullptr) return 0;
+  const int64_t s = wt_slot(t, path_hash(p, n) | 1ull, false);
+  if (s < 0) return 0;
+  unsigned long long* m = &t.wt_mask[2 * s + kind];
+  if (__hip_atomic_load(m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
+    return 0;
+  return atomicExch(m, 0ull);
+}
+
+// Node v's path from its path word.
+ZK_DEV const uint8_t* node_path(const ZkTree& t, int64_t pw) {
+  return t.path_arena + (pw >> 24);
+}
+ZK_DEV int32_t pw_len(int64_t pw) { return (int32_t)(pw & 0xFFFFFF); }
+
 ZK_DEV void fill_stat(uint8_t* st, int64_t cz, int64_t mz, int64_t ct,
                       int64_t mt, int32_t ver, int32_t cver, int32_t aver,
                       int64_t owner, int32_t dlen, int32_t nkids, int64_t pz) {
@@ -457,7 +521,8 @@ __global__ __launch_bounds__(TR_T) void tree_serve_k(
     int64_t* __restrict__ r_slot, int64_t* __restrict__ r_sizes,
     int64_t* __restrict__ r_bsum, int64_t session, int64_t now_ms,
     const uint8_t* __restrict__ rank, int32_t pass, int32_t last_pass,
-    int64_t snap_base, int64_t snap_cap, int64_t* __restrict__ snap_top) {
+    int64_t snap_base, int64_t snap_cap, int64_t* __restrict__ snap_top,
+    int32_t wslot, int64_t* __restrict__ fired) {
   const uint32_t blk = xcd_remap(blockIdx.x, gridDim.x);
   const int64_t i = (int64_t)blk * TR_T + threadIdx.x;
   const bool in_batch = i < ncap && i < *n_dev;
@@ -624,8 +689,44 @@ __global__ __launch_bounds__(TR_T) void tree_serve_k(
       }
       case OP_SYNC: case OP_PING:
         break;
+      case OP_SET_WATCHES:
+        // header-only reply; the catch-up (notifications for what changed
+        // after relZxid, re-registration of the rest) is zk_watch_resume
+        break;
       default:
         L.err = ERR_UNIMPLEMENTED;
+    }
+  }
+  // ---- watches: reads with watch=1 arm (this session's slot), successful
+  // writes fire (lib/zk-session.js:558-574 is the client side of the
+  // trigger table; the server rules are SURVEY Appendix D)
+  if (t.wt_key != nullptr && ok_req) {
+    const bool wflag = rq.arg == 1;
+    if (L.op == OP_GET_DATA && wflag && L.err == ERR_OK) {
+      wt_arm(t, L.path, L.pl, WK_DATA, wslot);
+    } else if (L.op == OP_EXISTS && wflag &&
+               (L.err == ERR_OK || L.err == ERR_NO_NODE)) {
+      wt_arm(t, L.path, L.pl, WK_DATA, wslot);
+    } else if (L.err == ERR_OK && (L.op == OP_SET_DATA ||
+                                   L.op == OP_CREATE ||
+                                   L.op == OP_DELETE)) {
+      const int64_t node = L.op == OP_DELETE ? freed : L.node;
+      const int64_t pw = t.node_pw[node];
+      const int64_t ppw = L.par >= 0 ? t.node_pw[L.par] : 0;
+      const uint8_t* np = node_path(t, pw);
+      const int32_t nl = pw_len(pw);
+      uint64_t m0 = wt_fire(t, np, nl, WK_DATA), m1 = 0, m2 = 0;
+      if (L.op == OP_DELETE) m1 = wt_fire(t, np, nl, WK_CHILD) & ~m0;
+      if (L.op != OP_SET_DATA && L.par >= 0)
+        m2 = wt_fire(t, node_path(t, ppw), pw_len(ppw), WK_CHILD);
+      if (fired != nullptr) {
+        int64_t* f = fired + (int64_t)WT_REC * i;
+        f[0] = (int64_t)m0;
+        f[1] = (int64_t)m1;
+        f[2] = (int64_t)m2;
+        f[3] = pw;
+        f[4] = ppw;
+      }
     }
   }
   // ---- ordered snapshot: a reply that reads the node's slot (stat, data)
@@ -893,6 +994,176 @@ __global__ __launch_bounds__(TR_T) void tree_expire_k(
   block_ticket((int64_t*)removed, hit);
 }
 
+// ---- watch event expansion ------------------------------------------------
+// Notifications of a served batch, in request order (ZooKeeper delivers a
+// session's notifications in zxid order; write i of a batch has zxid base +
+// i + 1): request i contributes one event per watcher bit of the masks it
+// fired — m_path (type by op), m_path_child (NodeDeleted, a watcher holding
+// both a data and a child watch on a deleted path is told once), m_parent
+// (NodeChildrenChanged on the parent).  Three launches: counts + block
+// sums, one-block scan of the sums, write.
+ZK_DEV bool wt_live(const int32_t* r_op, const int32_t* r_err, int64_t i) {
+  const int32_t op = r_op[i];
+  return r_err[i] == ERR_OK &&
+         (op == OP_SET_DATA || op == OP_CREATE || op == OP_DELETE);
+}
+
+ZK_DEV int64_t wt_count(const int32_t* r_op, const int32_t* r_err,
+                        const int64_t* fired, int64_t i, bool in) {
+  if (!in || !wt_live(r_op, r_err, i)) return 0;
+  const int64_t* f = fired + (int64_t)WT_REC * i;
+  return __popcll((uint64_t)f[0]) + __popcll((uint64_t)f[1]) +
+         __popcll((uint64_t)f[2]);
+}
+
+__global__ __launch_bounds__(TR_T) void wt_count_k(
+    const int32_t* __restrict__ r_op, const int32_t* __restrict__ r_err,
+    const int64_t* __restrict__ n_dev, int64_t ncap,
+    const int64_t* __restrict__ fired, int64_t* __restrict__ bsum) {
+  __shared__ int64_t sm[TR_T / 64 + 1];
+  const int64_t i = (int64_t)blockIdx.x * TR_T + threadIdx.x;
+  const bool in = i < ncap && i < *n_dev;
+  int64_t tot;
+  block_excl_scan(wt_count(r_op, r_err, fired, i, in), sm, &tot);
+  if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
+}
+
+ZK_DEV void wt_emit(uint64_t m, int32_t type, int64_t pw, int64_t& o,
+                    int64_t cap, int32_t* ev_slot, int32_t* ev_type,
+                    int64_t* ev_poff, int32_t* ev_plen) {
+  while (m) {
+    const int b = __builtin_ctzll(m);
+    m &= m - 1;
+    if (o < cap) {
+      ev_slot[o] = b;
+      ev_type[o] = type;
+      ev_poff[o] = pw >> 24;
+      ev_plen[o] = pw_len(pw);
+    }
+    ++o;
+  }
+}
+
+__global__ __launch_bounds__(TR_T) void wt_expand_k(
+    const int32_t* __restrict__ r_op, const int32_t* __restrict__ r_err,
+    const int64_t* __restrict__ n_dev, int64_t ncap,
+    const int64_t* __restrict__ fired, const int64_t* __restrict__ bsum,
+    int64_t nb, int64_t cap, int32_t* __restrict__ ev_slot,
+    int32_t* __restrict__ ev_type, int64_t* __restrict__ ev_poff,
+    int32_t* __restrict__ ev_plen, int64_t* __restrict__ ev_total) {
+  __shared__ int64_t sm[TR_T / 64 + 1];
+  const int64_t i = (int64_t)blockIdx.x * TR_T + threadIdx.x;
+  const bool in = i < ncap && i < *n_dev;
+  const int64_t c = wt_count(r_op, r_err, fired, i, in);
+  int64_t tot;
+  int64_t o = bsum[blockIdx.x] + block_excl_scan(c, sm, &tot);
+  if (blockIdx.x == nb - 1 && threadIdx.x == 0)
+    *ev_total = bsum[blockIdx.x] + tot;
+  if (c == 0) return;
+  const int64_t* f = fired + (int64_t)WT_REC * i;
+  const int32_t op = r_op[i];
+  const int32_t t0 = op == OP_SET_DATA ? NT_DATA_CHANGED
+                   : op == OP_CREATE ? NT_CREATED : NT_DELETED;
+  wt_emit((uint64_t)f[0], t0, f[3], o, cap, ev_slot, ev_type, ev_poff,
+          ev_plen);
+  wt_emit((uint64_t)f[1], NT_DELETED, f[3], o, cap, ev_slot, ev_type,
+          ev_poff, ev_plen);
+  wt_emit((uint64_t)f[2], NT_CHILDREN_CHANGED, f[4], o, cap, ev_slot,
+          ev_type, ev_poff, ev_plen);
+}
+
+// ---- SET_WATCHES catch-up (one workgroup) ---------------------------------
+// A resumed session re-sends its watches with relZxid = the last zxid it saw
+// (lib/zk-session.js:421-471, lib/zk-buffer.js:255-273).  For every path
+// (SURVEY Appendix D): data watch — node gone: NodeDeleted, mzxid > rel:
+// NodeDataChanged, else re-armed; exist watch — node there: NodeCreated,
+// else re-armed; child watch — node gone: NodeDeleted, pzxid > rel:
+// NodeChildrenChanged, else re-armed.  Events name the request's path
+// bytes (offsets into rx), in request order (data, exist, child lists).
+constexpr int WR_T = 1024;
+
+__global__ __launch_bounds__(WR_T) void wt_resume_k(
+    ZkTree t, const uint8_t* __restrict__ rx,
+    const int64_t* __restrict__ foff, const int32_t* __restrict__ flen,
+    const int64_t* __restrict__ n_dev, int64_t ncap, int32_t wslot,
+    int64_t* __restrict__ ent, int64_t ent_cap, int64_t cap,
+    int32_t* __restrict__ ev_type, int64_t* __restrict__ ev_poff,
+    int32_t* __restrict__ ev_plen, int64_t* __restrict__ out) {
+  __shared__ int64_t sm[WR_T / 64 + 1];
+  __shared__ int64_t s_n, s_rel;
+  int64_t o = 0, rearmed = 0;
+  const int64_t nfr = min(*n_dev, ncap);
+  for (int64_t fr = 0; fr < nfr; ++fr) {
+    // thread 0 lists the frame's paths (kind << 62 | off << 24 | len);
+    // a frame that is not a well-formed SET_WATCHES lists none
+    if (threadIdx.x == 0) {
+      const ReqFields rq = parse_request(rx, foff[fr], flen[fr]);
+      int64_t m = 0;
+      if (rq.status == ST_OK && rq.op == OP_SET_WATCHES) {
+        int64_t k = rq.voff;
+        for (int g = 0; g < 3; ++g) {
+          const int32_t c = max(ld_be32(rx + k), 0);
+          k += 4;
+          for (int32_t j = 0; j < c; ++j) {
+            const int32_t l = max(ld_be32(rx + k), 0);
+            if (m < ent_cap)
+              ent[m] = ((int64_t)g << 62) | ((k + 4) << 24) | l;
+            ++m;
+            k += 4 + l;
+          }
+        }
+      }
+      s_n = min(m, ent_cap);
+      s_rel = rq.rel;
+    }
+    __syncthreads();
+    const int64_t n = s_n, rel = s_rel;
+    for (int64_t b = 0; b < n; b += WR_T) {
+      const int64_t j = b + threadIdx.x;
+      int32_t type = 0;
+      int64_t po = 0;
+      int32_t pl = 0;
+      if (j < n) {
+        const int64_t e = ent[j];
+        const int g = (int)((uint64_t)e >> 62);
+        po = (e >> 24) & ((1ll << 38) - 1);
+        pl = (int32_t)(e & 0xFFFFFF);
+        const uint8_t* p = rx + po;
+        const Found f = tree_lookup(t, p, pl);
+        if (g == 0) {                              // data watch
+          if (f.node < 0) type = NT_DELETED;
+          else if (ld_be64(t.store.slab + f.slot + 8) > rel)
+            type = NT_DATA_CHANGED;
+        } else if (g == 1) {                       // exist watch
+          if (f.node >= 0) type = NT_CREATED;
+        } else {                                   // child watch
+          if (f.node < 0) type = NT_DELETED;
+          else if (t.pzxid[f.node] > rel) type = NT_CHILDREN_CHANGED;
+        }
+        if (type == 0) {
+          wt_arm(t, p, pl, g == 2 ? WK_CHILD : WK_DATA, wslot);
+          ++rearmed;
+        }
+      }
+      int64_t tot;
+      const int64_t x = o + block_excl_scan(type != 0 ? 1 : 0, sm, &tot);
+      if (type != 0 && x < cap) {
+        ev_type[x] = type;
+        ev_poff[x] = po;
+        ev_plen[x] = pl;
+      }
+      o += tot;
+    }
+    __syncthreads();
+  }
+  int64_t tot;
+  block_excl_scan(rearmed, sm, &tot);
+  if (threadIdx.x == 0) {
+    out[0] = o;                  // events
+    out[1] = tot;                // watches re-armed
+  }
+}
+
 }  // namespace zk
 
 extern "C" {
@@ -939,7 +1210,7 @@ int zk_tree_serve(const ZkTree* t, const uint8_t* rx, const ZkReqOut* q,
                             zk::TR_T, 0, st>>>(
       *t, rx, *q, nullptr, nullptr, n_dev, ncap, r_op, r_xid, r_err, r_node,
       r_zxid, r_path_off, r_path_len, r_slot, r_sizes, r_bsum, session,
-      now_ms, nullptr, 0, 1, 0, 0, nullptr);
+      now_ms, nullptr, 0, 1, 0, 0, nullptr, -1, nullptr);
   ZK_LAUNCH_CHECK();
   // at most one dirty parent per request
   return finish_launch(t, ncap, n_dev, 0, st);
@@ -947,6 +1218,9 @@ int zk_tree_serve(const ZkTree* t, const uint8_t* rx, const ZkReqOut* q,
 
 // zk_tree_serve straight from K1's frame table (foff / flen, *n_dev
 // frames): every lane parses its request in registers (no K12 pass).
+// wslot: this session's watcher slot (-1: its reads arm no watch); fired
+// (may be null; [ncap * 5]): per successful write, the watcher masks it
+// fired and the paths (zk_watch_events expands them).
 int zk_tree_serve_frames(const ZkTree* t, const uint8_t* rx,
                          const int64_t* foff, const int32_t* flen,
                          const int64_t* n_dev, int64_t ncap, int32_t* r_op,
@@ -954,7 +1228,8 @@ int zk_tree_serve_frames(const ZkTree* t, const uint8_t* rx,
                          int64_t* r_zxid, int64_t* r_path_off,
                          int32_t* r_path_len, int64_t* r_slot,
                          int64_t* r_sizes, int64_t* r_bsum, int64_t session,
-                         int64_t now_ms, hipStream_t st) {
+                         int64_t now_ms, int32_t wslot, int64_t* fired,
+                         hipStream_t st) {
   if (ncap <= 0) return 0;
   if ((r_sizes == nullptr) != (r_bsum == nullptr)) return -1;
   ZkReqOut none{};
@@ -962,7 +1237,7 @@ int zk_tree_serve_frames(const ZkTree* t, const uint8_t* rx,
                            zk::TR_T, 0, st>>>(
       *t, rx, none, foff, flen, n_dev, ncap, r_op, r_xid, r_err, r_node,
       r_zxid, r_path_off, r_path_len, r_slot, r_sizes, r_bsum, session,
-      now_ms, nullptr, 0, 1, 0, 0, nullptr);
+      now_ms, nullptr, 0, 1, 0, 0, nullptr, wslot, fired);
   ZK_LAUNCH_CHECK();
   return finish_launch(t, ncap, n_dev, 0, st);
 }
@@ -1025,7 +1300,7 @@ int zk_tree_serve_ordered(const ZkTree* t, const uint8_t* rx, const ZkReqOut* q,
                           int64_t* r_sizes, int64_t* r_bsum, int64_t session,
                           int64_t now_ms, uint8_t* ws, int64_t ws_bytes,
                           int32_t passes, int64_t snap_base, int64_t snap_cap,
-                          hipStream_t st) {
+                          int32_t wslot, int64_t* fired, hipStream_t st) {
   if (ncap <= 0) return 0;
   if (ncap >= (int64_t)1 << 31) return -1;
   if ((r_sizes == nullptr) != (r_bsum == nullptr)) return -1;
@@ -1055,7 +1330,7 @@ int zk_tree_serve_ordered(const ZkTree* t, const uint8_t* rx, const ZkReqOut* q,
     zk::tree_serve_k<false><<<nb, zk::TR_T, 0, st>>>(
         *t, rx, *q, nullptr, nullptr, n_dev, ncap, r_op, r_xid, r_err, r_node, r_zxid,
         r_path_off, r_path_len, r_slot, r_sizes, r_bsum, session, now_ms,
-        rank, pass, last, snap_base, snap_cap, &w.ctr[2]);
+        rank, pass, last, snap_base, snap_cap, &w.ctr[2], wslot, fired);
     ZK_LAUNCH_CHECK();
     // nodes freed by a pass are recycled from the next batch on: a reply of
     // this batch may still name them
@@ -1080,6 +1355,47 @@ int zk_tree_expire(const ZkTree* t, int64_t session, int64_t ncap,
                       0, st>>>(*t, session, ncap, removed);
   ZK_LAUNCH_CHECK();
   return finish_launch(t, ncap, nullptr, 1, st);
+}
+
+// Expand the watch masks a served batch fired (tree_serve's `fired`) into
+// notification events in request order: ev_slot (watcher slot), ev_type,
+// ev_poff / ev_plen (path in the tree's path arena); *ev_total = events
+// (only the first `cap` are written).  bsum: ceil(ncap / 256) int64.
+int zk_watch_events(const int32_t* r_op, const int32_t* r_err,
+                    const int64_t* n_dev, int64_t ncap, const int64_t* fired,
+                    int64_t* bsum, int64_t cap, int32_t* ev_slot,
+                    int32_t* ev_type, int64_t* ev_poff, int32_t* ev_plen,
+                    int64_t* ev_total, hipStream_t st) {
+  if (ncap <= 0) return hipMemsetAsync(ev_total, 0, 8, st);
+  const int64_t nb = (ncap + zk::TR_T - 1) / zk::TR_T;
+  zk::wt_count_k<<<(unsigned)nb, zk::TR_T, 0, st>>>(r_op, r_err, n_dev, ncap,
+                                                    fired, bsum);
+  ZK_LAUNCH_CHECK();
+  zk::ord_bscan_k<<<1, zk::ORD_SCAN_T, 0, st>>>(bsum, nb);
+  ZK_LAUNCH_CHECK();
+  zk::wt_expand_k<<<(unsigned)nb, zk::TR_T, 0, st>>>(
+      r_op, r_err, n_dev, ncap, fired, bsum, nb, cap, ev_slot, ev_type,
+      ev_poff, ev_plen, ev_total);
+  ZK_LAUNCH_CHECK();
+  return 0;
+}
+
+// SET_WATCHES catch-up for the frames (foff / flen, *n_dev of them) of a
+// resumed session with watcher slot wslot: events (ev_type, ev_poff /
+// ev_plen into rx) for what changed after each frame's relZxid, the other
+// watches re-armed.  out[0] = events, out[1] = re-armed watches.  ent:
+// scratch for ent_cap paths.
+int zk_watch_resume(const ZkTree* t, const uint8_t* rx, const int64_t* foff,
+                    const int32_t* flen, const int64_t* n_dev, int64_t ncap,
+                    int32_t wslot, int64_t* ent, int64_t ent_cap, int64_t cap,
+                    int32_t* ev_type, int64_t* ev_poff, int32_t* ev_plen,
+                    int64_t* out, hipStream_t st) {
+  if (t->wt_key == nullptr) return -1;
+  zk::wt_resume_k<<<1, zk::WR_T, 0, st>>>(*t, rx, foff, flen, n_dev, ncap,
+                                           wslot, ent, ent_cap, cap, ev_type,
+                                           ev_poff, ev_plen, out);
+  ZK_LAUNCH_CHECK();
+  return 0;
 }
 
 }  // extern "C"

@@ -39,6 +39,9 @@ struct ZkTree {
   int32_t* dirty;
   int64_t* dirty_list;
   int64_t* node_pw;
+  int64_t* wt_key;
+  unsigned long long* wt_mask;
+  int64_t wt_hmask;
 };
 struct ZkSessionTable {
   int64_t* sid;
@@ -108,13 +111,20 @@ int zk_tree_serve_frames(const ZkTree*, const uint8_t*, const int64_t*,
                          const int32_t*, const int64_t*, int64_t, int32_t*,
                          int32_t*, int32_t*, int64_t*, int64_t*, int64_t*,
                          int32_t*, int64_t*, int64_t*, int64_t*, int64_t,
-                         int64_t, hipStream_t);
+                         int64_t, int32_t, int64_t*, hipStream_t);
 int zk_tree_serve_ordered(const ZkTree*, const uint8_t*, const ZkReqOut*,
                           const int64_t*, int64_t, int32_t*, int32_t*,
                           int32_t*, int64_t*, int64_t*, int64_t*, int32_t*,
                           int64_t*, int64_t*, int64_t*, int64_t, int64_t,
                           uint8_t*, int64_t, int32_t, int64_t, int64_t,
-                          hipStream_t);
+                          int32_t, int64_t*, hipStream_t);
+int zk_watch_events(const int32_t*, const int32_t*, const int64_t*, int64_t,
+                    const int64_t*, int64_t*, int64_t, int32_t*, int32_t*,
+                    int64_t*, int32_t*, int64_t*, hipStream_t);
+int zk_watch_resume(const ZkTree*, const uint8_t*, const int64_t*,
+                    const int32_t*, const int64_t*, int64_t, int32_t,
+                    int64_t*, int64_t, int64_t, int32_t*, int64_t*, int32_t*,
+                    int64_t*, hipStream_t);
 int64_t zk_tree_order_workspace(int64_t);
 int64_t zk_tree_order_stats_offset(int64_t);
 int zk_tree_expire(const ZkTree*, int64_t, int64_t, unsigned long long*,
@@ -137,6 +147,11 @@ int zk_route_requests(int64_t, int32_t, const int64_t*, const int32_t*,
                       const uint8_t*, const int64_t*, const int32_t*,
                       int32_t*, int64_t*, int32_t*, int64_t*, int32_t*,
                       int64_t*, int64_t*, hipStream_t);
+int zk_seg_pack(const uint8_t*, int64_t, const int64_t*, const int64_t*,
+                int64_t, const int64_t*, const int64_t*, int32_t, int32_t,
+                int64_t, uint8_t*, unsigned long long*, hipStream_t);
+int zk_seg_unpack(const uint8_t*, int32_t, int32_t, int64_t, uint8_t*,
+                  int64_t*, int64_t*, unsigned long long*, hipStream_t);
 int zk_session_connect(const uint8_t*, const int64_t*, const int32_t*,
                        const int64_t*, int64_t, const ZkSessionTable*,
                        int64_t, uint64_t, int32_t, int32_t, const int64_t*,
@@ -233,8 +248,13 @@ ZkNodeStore node_store(const std::vector<Tensor>& v, size_t at,
 // [ht, node_path_off, node_path_len, node_parent, path_arena, counters,
 //  slab, slot_off, data_len, slot_cap, free_list, cver, nchild, pzxid,
 //  dirty, dirty_list, node_pw]; sizes give mask, caps
+// [ht, node_path_off, node_path_len, node_parent, path_arena, counters,
+//  slab, slot_off, data_len, slot_cap, free_list, cver, nchild, pzxid,
+//  dirty, dirty_list, node_pw] + optionally [wt_key, wt_mask] (watches)
 ZkTree tree(const std::vector<Tensor>& v) {
-  need(v, 17, "tree");
+  TORCH_CHECK(v.size() == 17 || v.size() == 19,
+              "zkmi: tree needs 17 tensors (19 with a watch table), got ",
+              v.size());
   const Tensor* r = &v[0];
   ZkTree t;
   const int64_t hw = v[0].numel() / 2;          // {key, val} entries
@@ -259,6 +279,18 @@ ZkTree tree(const std::vector<Tensor>& v) {
   t.dirty = P<int32_t>(v[14], I32, cap, "tree.dirty", r);
   t.dirty_list = P<int64_t>(v[15], I64, cap, "tree.dirty_list", r);
   t.node_pw = P<int64_t>(v[16], I64, cap, "tree.node_pw", r);
+  t.wt_key = nullptr;
+  t.wt_mask = nullptr;
+  t.wt_hmask = 0;
+  if (v.size() == 19) {
+    const int64_t h = v[17].numel();
+    TORCH_CHECK(h > 0 && (h & (h - 1)) == 0,
+                "zkmi: tree.wt_key must hold a power of two of entries");
+    t.wt_key = P<int64_t>(v[17], I64, h, "tree.wt_key", r);
+    t.wt_mask = reinterpret_cast<unsigned long long*>(
+        P<int64_t>(v[18], I64, 2 * h, "tree.wt_mask", r));
+    t.wt_hmask = h - 1;
+  }
   return t;
 }
 
@@ -651,10 +683,12 @@ void tree_serve_frames(const std::vector<Tensor>& t, const Tensor& rx,
                        const Tensor& foff, const Tensor& flen,
                        const Tensor& n_dev, int64_t ncap,
                        const std::vector<Tensor>& r, int64_t session,
-                       int64_t now_ms) {
+                       int64_t now_ms, int64_t wslot,
+                       const c10::optional<Tensor>& fired) {
   ZkTree s = tree(t);
   const Tensor* d = &t[0];
   need(r, 10, "serve outputs");
+  TORCH_CHECK(wslot >= -1 && wslot < 64, "zkmi: watcher slot -1..63");
   const int64_t nb = (ncap + 255) / 256;
   hip_ok(zk_tree_serve_frames(
              &s, P<uint8_t>(rx, U8, 1, "rx", d),
@@ -671,6 +705,7 @@ void tree_serve_frames(const std::vector<Tensor>& t, const Tensor& rx,
              P<int64_t>(r[7], I64, ncap, "r.slot", d),
              P<int64_t>(r[8], I64, ncap, "r.sizes", d),
              P<int64_t>(r[9], I64, nb, "r.block_sums", d), session, now_ms,
+             (int32_t)wslot, Popt<int64_t>(fired, I64, 5 * ncap, "fired", d),
              cur_stream()),
          "tree_serve_frames");
 }
@@ -694,7 +729,9 @@ void tree_serve_ordered(const std::vector<Tensor>& t, const Tensor& rx,
                         const std::vector<Tensor>& q, const Tensor& n_dev,
                         int64_t ncap, const std::vector<Tensor>& r,
                         int64_t session, int64_t now_ms, const Tensor& ws,
-                        int64_t passes, const c10::optional<Tensor>& scratch) {
+                        int64_t passes, const c10::optional<Tensor>& scratch,
+                        int64_t wslot, const c10::optional<Tensor>& fired) {
+  TORCH_CHECK(wslot >= -1 && wslot < 64, "zkmi: watcher slot -1..63");
   ZkTree s = tree(t);
   const Tensor* d = &t[0];
   ZkReqOut qo = req_out(q, ncap, d);
@@ -729,8 +766,53 @@ void tree_serve_ordered(const std::vector<Tensor>& t, const Tensor& rx,
              P<int64_t>(r[8], I64, ncap, "r.sizes", d),
              P<int64_t>(r[9], I64, nb, "r.block_sums", d), session, now_ms,
              w, ws.numel(), (int32_t)passes, snap_base, snap_cap,
+             (int32_t)wslot, Popt<int64_t>(fired, I64, 5 * ncap, "fired", d),
              cur_stream()),
          "tree_serve_ordered");
+}
+
+void watch_events(const Tensor& r_op, const Tensor& r_err, const Tensor& n_dev,
+                  int64_t ncap, const Tensor& fired, const Tensor& bsum,
+                  const Tensor& ev_slot, const Tensor& ev_type,
+                  const Tensor& ev_poff, const Tensor& ev_plen,
+                  const Tensor& ev_total) {
+  const Tensor* d = &r_op;
+  const int64_t cap = ev_slot.numel();
+  hip_ok(zk_watch_events(
+             P<int32_t>(r_op, I32, ncap, "r.opcode"),
+             P<int32_t>(r_err, I32, ncap, "r.err", d),
+             P<int64_t>(n_dev, I64, 1, "count", d), ncap,
+             P<int64_t>(fired, I64, 5 * ncap, "fired", d),
+             P<int64_t>(bsum, I64, (ncap + 255) / 256, "bsum", d), cap,
+             P<int32_t>(ev_slot, I32, cap, "ev_slot", d),
+             P<int32_t>(ev_type, I32, cap, "ev_type", d),
+             P<int64_t>(ev_poff, I64, cap, "ev_path_off", d),
+             P<int32_t>(ev_plen, I32, cap, "ev_path_len", d),
+             P<int64_t>(ev_total, I64, 1, "ev_total", d), cur_stream()),
+         "watch_events");
+}
+
+void watch_resume(const std::vector<Tensor>& t, const Tensor& rx,
+                  const Tensor& foff, const Tensor& flen, const Tensor& n_dev,
+                  int64_t ncap, int64_t wslot, const Tensor& ent,
+                  const Tensor& ev_type, const Tensor& ev_poff,
+                  const Tensor& ev_plen, const Tensor& out) {
+  ZkTree s = tree(t);
+  TORCH_CHECK(s.wt_key != nullptr, "zkmi: watch_resume needs a watch table");
+  TORCH_CHECK(wslot >= 0 && wslot < 64, "zkmi: watcher slot 0..63");
+  const Tensor* d = &t[0];
+  const int64_t cap = ev_type.numel();
+  hip_ok(zk_watch_resume(
+             &s, P<uint8_t>(rx, U8, 1, "rx", d),
+             P<int64_t>(foff, I64, ncap, "frame_off", d),
+             P<int32_t>(flen, I32, ncap, "frame_len", d),
+             P<int64_t>(n_dev, I64, 1, "count", d), ncap, (int32_t)wslot,
+             P<int64_t>(ent, I64, 1, "ent", d), ent.numel(), cap,
+             P<int32_t>(ev_type, I32, cap, "ev_type", d),
+             P<int64_t>(ev_poff, I64, cap, "ev_path_off", d),
+             P<int32_t>(ev_plen, I32, cap, "ev_path_len", d),
+             P<int64_t>(out, I64, 2, "out", d), cur_stream()),
+         "watch_resume");
 }
 
 void tree_expire(const std::vector<Tensor>& t, int64_t session, int64_t ncap,
@@ -839,6 +921,50 @@ void route_requests(int64_t n, int64_t world, const Tensor& poff,
          "route_requests");
 }
 
+void seg_pack(const Tensor& src, const Tensor& rec_off,
+              const c10::optional<Tensor>& nrec, int64_t nrec_cap,
+              const Tensor& total, const Tensor& counts, int64_t world,
+              int64_t self, int64_t slot_cap, const Tensor& out,
+              const Tensor& stats) {
+  TORCH_CHECK(world >= 1 && world <= 64, "zkmi: seg_pack world 1..64");
+  TORCH_CHECK(self >= 0 && self < world, "zkmi: seg_pack self rank");
+  TORCH_CHECK(slot_cap >= 32 && slot_cap % 16 == 0,
+              "zkmi: seg_pack slot_cap must be a multiple of 16, >= 32");
+  TORCH_CHECK(nrec_cap >= 0, "zkmi: seg_pack nrec_cap");
+  const Tensor* r = &src;
+  hip_ok(zk_seg_pack(P<uint8_t>(src, U8, 1, "src"), src.numel(),
+                     P<int64_t>(rec_off, I64, std::max<int64_t>(nrec_cap, 1),
+                                "rec_off", r),
+                     Popt<int64_t>(nrec, I64, 1, "nrec", r), nrec_cap,
+                     P<int64_t>(total, I64, 1, "total", r),
+                     P<int64_t>(counts, I64, world, "counts", r),
+                     (int32_t)world, (int32_t)self, slot_cap,
+                     P<uint8_t>(out, U8, world * slot_cap, "out", r),
+                     reinterpret_cast<unsigned long long*>(
+                         P<int64_t>(stats, I64, 3, "stats", r)),
+                     cur_stream()),
+         "seg_pack");
+}
+
+void seg_unpack(const Tensor& inp, int64_t world, int64_t self,
+                int64_t slot_cap, const Tensor& out, const Tensor& total,
+                const Tensor& counts, const c10::optional<Tensor>& stats) {
+  TORCH_CHECK(world >= 1 && world <= 64, "zkmi: seg_unpack world 1..64");
+  TORCH_CHECK(self >= 0 && self < world, "zkmi: seg_unpack self rank");
+  TORCH_CHECK(slot_cap >= 32 && slot_cap % 16 == 0,
+              "zkmi: seg_unpack slot_cap must be a multiple of 16, >= 32");
+  const Tensor* r = &inp;
+  hip_ok(zk_seg_unpack(P<uint8_t>(inp, U8, world * slot_cap, "in"),
+                       (int32_t)world, (int32_t)self, slot_cap,
+                       P<uint8_t>(out, U8, world * (slot_cap - 16), "out", r),
+                       P<int64_t>(total, I64, 1, "total", r),
+                       P<int64_t>(counts, I64, world, "counts", r),
+                       reinterpret_cast<unsigned long long*>(
+                           Popt<int64_t>(stats, I64, 1, "stats", r)),
+                       cur_stream()),
+         "seg_unpack");
+}
+
 void session_connect(const Tensor& buf, const Tensor& foff,
                      const Tensor& flen, const Tensor& n_dev, int64_t ncap,
                      const std::vector<Tensor>& tab, int64_t server_id,
@@ -926,13 +1052,22 @@ TORCH_LIBRARY(zkmi, m) {
         "-> ()", &tree_serve);
   m.def("tree_serve_frames(Tensor(a!)[] tree, Tensor rx, Tensor frame_off, "
         "Tensor frame_len, Tensor count, int ncap, Tensor(b!)[] out, "
-        "int session, int now_ms) -> ()", &tree_serve_frames);
+        "int session, int now_ms, int wslot=-1, Tensor(c!)? fired=None) "
+        "-> ()", &tree_serve_frames);
   m.def("tree_order_workspace(int n) -> int", &tree_order_workspace);
   m.def("tree_order_stats_offset(int n) -> int", &tree_order_stats_offset);
   m.def("tree_serve_ordered(Tensor(a!)[] tree, Tensor rx, Tensor[] requests, "
         "Tensor count, int ncap, Tensor(b!)[] out, int session, int now_ms, "
-        "Tensor(c!) ws, int passes, Tensor? scratch) -> ()",
-        &tree_serve_ordered);
+        "Tensor(c!) ws, int passes, Tensor? scratch, int wslot=-1, "
+        "Tensor(d!)? fired=None) -> ()", &tree_serve_ordered);
+  m.def("watch_events(Tensor r_op, Tensor r_err, Tensor count, int ncap, "
+        "Tensor fired, Tensor(a!) bsum, Tensor(b!) ev_slot, "
+        "Tensor(c!) ev_type, Tensor(d!) ev_path_off, Tensor(e!) ev_path_len, "
+        "Tensor(f!) ev_total) -> ()", &watch_events);
+  m.def("watch_resume(Tensor(a!)[] tree, Tensor rx, Tensor frame_off, "
+        "Tensor frame_len, Tensor count, int ncap, int wslot, "
+        "Tensor(b!) ent, Tensor(c!) ev_type, Tensor(d!) ev_path_off, "
+        "Tensor(e!) ev_path_len, Tensor(f!) out) -> ()", &watch_resume);
   m.def("tree_expire(Tensor(a!)[] tree, int session, int ncap, "
         "Tensor(b!) removed) -> ()", &tree_expire);
   m.def("bench_gen_get(int n, int seed, int leaf0, int nleaves, "
@@ -951,6 +1086,12 @@ TORCH_LIBRARY(zkmi, m) {
         "Tensor(b!) idx_s, Tensor(c!) xid_s, Tensor(d!) path_off_s, "
         "Tensor(e!) path_len_s, Tensor(f!) counts, Tensor(g!) ws) -> ()",
         &route_requests);
+  m.def("seg_pack(Tensor src, Tensor rec_off, Tensor? nrec, int nrec_cap, "
+        "Tensor total, Tensor counts, int world, int self, int slot_cap, "
+        "Tensor(a!) out, Tensor(b!) stats) -> ()", &seg_pack);
+  m.def("seg_unpack(Tensor inp, int world, int self, int slot_cap, "
+        "Tensor(a!) out, Tensor(b!) total, Tensor(c!) counts, "
+        "Tensor(d!)? stats=None) -> ()", &seg_unpack);
   m.def("session_connect(Tensor buf, Tensor frame_off, Tensor frame_len, "
         "Tensor count, int ncap, Tensor(a!)[] table, int server_id, "
         "int secret, int min_to, int max_to, Tensor zxid_now, Tensor(b!) out, "

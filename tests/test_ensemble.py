@@ -70,7 +70,7 @@ def _run(world, steps):
     return res
 
 
-@pytest.mark.parametrize('world', [2, 4])
+@pytest.mark.parametrize('world', [2, 4, 8])
 def test_ensemble_failover_replay_fanout(world):
     steps = 4                               # failovers at steps 1 and 3
     res = _run(world, steps)

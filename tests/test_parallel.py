@@ -204,3 +204,12 @@ def test_watch_fanout_uses_one_server_watch():
     zk = _run('watch_fanout')
     sids = zk.db.watch_log.get('/fan', set())
     assert len(sids) == 1, sids
+
+
+@pytest.mark.parametrize('scenario', ['metrics', 'watch_fanout',
+                                      'session_failover'])
+def test_group_eight_ranks(scenario):
+    """The node layer at world 8 (gloo): R4 metrics all-reduce, R1 watch
+    fan-out from one owner rank to seven, R3 session credential broadcast
+    and adoption."""
+    _run(scenario, world=8)

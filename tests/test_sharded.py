@@ -21,32 +21,99 @@ def test_router_matches_host_hash(gpu):
     tree = GpuTree(20000, 37, fanout=100, device=gpu, seed=0)
     pipe = ShardedGetPipeline(tree, 5000)
     pipe.step()
+    c = pipe.subs[0]
     from zkmi.ops import _lib
     L = _lib.lib()
+    i64 = lambda: torch.empty(5000, dtype=torch.int64, device=gpu)  # noqa
+    i32 = lambda: torch.empty(5000, dtype=torch.int32, device=gpu)  # noqa
+    owner, idx_s, xid_s, poff_s, plen_s = i32(), i64(), i32(), i64(), i32()
     for W in (3, 8):
-        pipe.rws = torch.empty(L.route_workspace(5000, W),
-                               dtype=torch.int64, device=gpu)
+        rws = torch.empty(L.route_workspace(5000, W), dtype=torch.int64,
+                          device=gpu)
         cnt = torch.empty(W, dtype=torch.int64, device=gpu)
-        L.route_requests(5000, W, pipe.poff, pipe.plen, tree.path_arena,
-                         pipe.idx, pipe.xid, pipe.owner, pipe.idx_s,
-                         pipe.xid_s, pipe.poff_s, pipe.plen_s, cnt, pipe.rws)
+        L.route_requests(5000, W, c.poff, c.plen, tree.path_arena, c.idx,
+                         c.xid, owner, idx_s, xid_s, poff_s, plen_s, cnt,
+                         rws)
         arena = tree.path_arena.cpu().numpy().tobytes()
-        po, pl = pipe.poff.cpu().tolist(), pipe.plen.cpu().tolist()
+        po, pl = c.poff.cpu().tolist(), c.plen.cpu().tolist()
         want = path_owner([arena[o:o + n] for o, n in zip(po, pl)], W)
-        assert pipe.owner.cpu().numpy().tolist() == want.tolist()
+        assert owner.cpu().numpy().tolist() == want.tolist()
         order = np.argsort(want, kind='stable')
-        assert pipe.idx_s.cpu().numpy().tolist() == \
-            pipe.idx.cpu().numpy()[order].tolist()
+        assert idx_s.cpu().numpy().tolist() == \
+            c.idx.cpu().numpy()[order].tolist()
         assert cnt.cpu().tolist() == np.bincount(want, minlength=W).tolist()
+
+
+def test_seg_pack_unpack_roundtrip(gpu):
+    """seg_pack cuts a framed stream into per-destination slots with
+    {bytes, records} headers (any byte alignment, empty segments, an
+    overflowing segment sent empty and counted); seg_unpack concatenates
+    slots back with the device length and per-source counts."""
+    from zkmi.ops import _lib
+    L = _lib.lib()
+    rng = np.random.default_rng(3)
+    W = 5
+    counts = [7, 0, 13, 1, 30]
+    sizes = rng.integers(1, 60, sum(counts))
+    stream = rng.integers(0, 256, int(sizes.sum()), dtype=np.uint8)
+    rec_off = np.zeros(len(sizes), np.int64)
+    rec_off[1:] = np.cumsum(sizes)[:-1]
+    dev = gpu
+    src = torch.from_numpy(np.concatenate([stream, np.zeros(64, np.uint8)]))\
+        .to(dev)
+    ro = torch.from_numpy(rec_off).to(dev)
+    total = torch.tensor([len(stream)], dtype=torch.int64, device=dev)
+    cnt = torch.tensor(counts, dtype=torch.int64, device=dev)
+    segs = []
+    f = 0
+    for c in counts:
+        a = rec_off[f] if f < len(sizes) else len(stream)
+        b = rec_off[f + c] if f + c < len(sizes) else len(stream)
+        segs.append(bytes(stream[a:b]))
+        f += c
+    # slot payload capacity 16 * 40 bytes: segment 4 (30 records) overflows
+    slot = 16 + 16 * 40
+    assert len(segs[4]) > slot - 16 and max(map(len, segs[:4])) <= slot - 16
+    out = torch.full((W * slot,), 0xEE, dtype=torch.uint8, device=dev)
+    st = torch.zeros(3, dtype=torch.int64, device=dev)
+    L.seg_pack(src, ro, None, len(sizes), total, cnt, W, 2, slot, out, st)
+    ob = out.cpu().numpy().tobytes()
+    for w in range(W):
+        hb, hr = np.frombuffer(ob[w * slot:w * slot + 16], np.int64)
+        if w == 4:
+            assert (hb, hr) == (0, 0)
+        else:
+            assert (hb, hr) == (len(segs[w]), counts[w])
+            assert ob[w * slot + 16:w * slot + 16 + hb] == segs[w]
+    sent = sum(len(segs[w]) for w in range(4) if w != 2)
+    assert st.cpu().tolist() == [1, sent, sum(counts[:4]) - counts[2]]
+    # unpack: a shifted copy so the destination offsets are unaligned
+    back = torch.zeros(W * (slot - 16) + 64, dtype=torch.uint8, device=dev)
+    tot = torch.zeros(1, dtype=torch.int64, device=dev)
+    rc = torch.zeros(W, dtype=torch.int64, device=dev)
+    rs = torch.zeros(1, dtype=torch.int64, device=dev)
+    L.seg_unpack(out, W, 1, slot, back, tot, rc, rs)
+    want = b''.join(segs[:4])
+    assert tot.item() == len(want)
+    assert back[:len(want)].cpu().numpy().tobytes() == want
+    assert rc.cpu().tolist() == counts[:4] + [0]
+    assert rs.item() == len(want) - len(segs[1])
 
 
 def test_sharded_get_one_rank(gpu):
     from zkmi.bench.synthetic import GpuTree
     from zkmi.parallel.sharded import ShardedGetPipeline
     tree = GpuTree(20000, 37, fanout=100, device=gpu, seed=0, shard=(0, 1))
-    pipe = ShardedGetPipeline(tree, 4096)
-    for _ in range(3):
-        assert int(pipe.step().item()) == 4096
+    for streams in (1, 2):
+        pipe = ShardedGetPipeline(tree, 4096, streams=streams)
+        for _ in range(3):
+            assert int(pipe.step().item()) == 4096
+        acc = torch.zeros(1, dtype=torch.int64, device=gpu)
+        g = pipe.capture(acc)
+        acc.zero_()
+        for _ in range(3):
+            g.replay()
+        assert int(acc.item()) == 3 * 4096
 
 
 def _mask_zxid(stream):
@@ -59,7 +126,7 @@ def _mask_zxid(stream):
             for o, n in frames]
 
 
-def _rank(rank, world, port, q):
+def _rank(rank, world, port, q, streams):
     import os
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
@@ -72,31 +139,31 @@ def _rank(rank, world, port, q):
         n = 3000
         tree = GpuTree(20000, 37, fanout=100, device=dev, seed=0,
                        shard=(rank, world), ctime_ms=1 << 40)
-        pipe = ShardedGetPipeline(tree, n, seed=5, coll_device='cpu')
+        pipe = ShardedGetPipeline(tree, n, seed=5, coll_device='cpu',
+                                  streams=streams)
         oks = [int(pipe.step().item()) for _ in range(3)]
+        c = pipe.subs[-1]
         rep, crx, ft = pipe.last
-        got = bytes(crx.cpu().numpy().tobytes())
+        got = bytes(crx[:int(c.ncrx.item())].cpu().numpy().tobytes())
         # the same (routed-order) requests served by an unsharded replica
         full = GpuTree(20000, 37, fanout=100, device=dev, seed=0,
                        ctime_ms=1 << 40)
-        srv = GpuServer(full, n, n * 300)
-        rb = B.RequestBatch(n, pipe.opcode, pipe.xid_s, pipe.zero32,
-                            pipe.poff_s, pipe.plen_s, pipe.zero64,
-                            pipe.zero32, pipe.zero32, tree.path_arena,
-                            tree.slab, pipe.acl_off, pipe.acl_len,
-                            pipe.acl_arena)
+        srv = GpuServer(full, c.n, c.n * 300)
+        rb = B.RequestBatch(c.n, c.opcode, c.xid_s, c.zero32, c.poff_s,
+                            c.plen_s, c.zero64, c.zero32, c.zero32,
+                            tree.path_arena, tree.slab, c.acl_off,
+                            c.acl_len, c.acl_arena)
         tx, _, total, _ = B.encode_requests(rb, B.XidTable(bits=14,
                                                            device=dev))
         out, rtotal, _, _ = srv.serve(tx, total)
         want = bytes(out[:int(rtotal.item())].cpu().numpy().tobytes())
         q.put((rank, oks, _mask_zxid(got) == _mask_zxid(want), len(got),
-               dict(pipe.stats)))
+               pipe.stats))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize('world', [2, 3])
-def test_sharded_get_multi_rank_gloo(gpu, world):
+def _run_world(world, streams):
     import torch.multiprocessing as mp
     s = socket.socket()
     s.bind(('127.0.0.1', 0))
@@ -104,20 +171,34 @@ def test_sharded_get_multi_rank_gloo(gpu, world):
     s.close()
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
-    procs = [ctx.Process(target=_rank, args=(r, world, port, q))
+    procs = [ctx.Process(target=_rank, args=(r, world, port, q, streams))
              for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
-        p.join(180)
+        p.join(240)
     assert all(p.exitcode == 0 for p in procs)
     res = {}
     for _ in range(world):
         r = q.get(timeout=5)
         res[r[0]] = r[1:]
+    n = 3000
     for rank, (oks, same, nbytes, st) in res.items():
-        assert oks == [3000] * 3, (rank, oks)
-        assert same and nbytes > 3000 * 100, rank
+        assert oks == [n] * 3, (rank, oks)
+        assert same and nbytes > (n // streams) * 100, rank
+        assert st['overflow_segments'] == 0
         # most reads are remote: bytes really moved between the ranks
-        assert st['remote_reqs'] > 3 * 3000 * (world - 1) / world * 0.8
+        assert st['remote_reqs'] > 3 * n * (world - 1) / world * 0.8
         assert st['bytes_sent'] > 0 and st['bytes_recv'] > 0
+        assert st['wire_bytes_sent'] >= st['bytes_sent']
+
+
+@pytest.mark.parametrize('world,streams', [(2, 1), (3, 2)])
+def test_sharded_get_multi_rank_gloo(gpu, world, streams):
+    _run_world(world, streams)
+
+
+def test_sharded_get_eight_ranks_gloo(gpu):
+    """The 8-rank rehearsal: eight ranks share the one GPU (gloo
+    collectives), two pipelined connections each."""
+    _run_world(8, 2)

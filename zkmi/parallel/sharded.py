@@ -4,28 +4,41 @@ by path hash, and every read travels to the rank that owns its path.
 The reference pipelines all of a client's requests over its one
 connection, keyed by xid (``lib/connection-fsm.js:384-408``).  On a node of
 ``world`` GPU sessions one step of :class:`ShardedGetPipeline`
-on rank ``r`` is:
+on rank ``r`` is, per pipelined connection:
 
-  client  draw ``batch`` GET_DATA requests over the whole tree;
-          route them (csrc/kernels/route.hip): owner = FNV-1a(path) % world,
-          stable split by owner; K10 encode -> one byte segment per owner
-  R2      exchange (bytes, requests) per rank pair — ``all_to_all_single``
-          of a [world, 2] int64 tensor, the one size exchange — then
-          ``all_to_all_single`` of the encoded request bytes (RCCL over xGMI
-          with ``nccl``)
-  server  K1 + K12 over the received stream (every rank's requests for my
-          shard, in rank order), lookup in my shard, K13 encode
-  R2      reply sizes per source rank from the reply frame offsets, one
-          ``all_to_all_single`` of them, one of the reply bytes back
-  client  K1 + K2-K4 over the replies (they come back owner by owner, in
-          the order the router sent them) and the on-device check
+  client  draw ``batch`` GET_DATA requests over the whole tree; route them
+          (csrc/kernels/route.hip): owner = FNV-1a(path) % world, stable
+          split by owner; K10 encode -> one byte segment per owner;
+          ``seg_pack`` cuts the stream into one fixed-capacity slot per
+          owner ({bytes, records} header + payload)
+  R2      ``all_to_all_single`` of the slots with EQUAL splits (RCCL over
+          xGMI with ``nccl``): no size exchange, no host split list
+  server  ``seg_unpack`` concatenates the received payloads (source rank
+          order) with their device length; K1 + K12 over that stream,
+          lookup in my shard, K13 encode; ``seg_pack`` cuts the reply
+          stream back into one slot per source rank (the per-source record
+          counts came with the request headers)
+  R2      ``all_to_all_single`` of the reply slots
+  client  ``seg_unpack``, K1 + K2-K4 over the replies (they come back owner
+          by owner, in the order the router sent them) and the on-device
+          check of every reply
 
-Host reads per step: the size table after the request-size exchange and
-the reply-size table (two small D2H copies; ``all_to_all_single`` takes its
-splits on the host).  Each rank's :class:`~zkmi.bench.synthetic.GpuTree`
-indexes only its shard (``shard=(rank, world)``): a read that reached the
-wrong rank would answer NO_NODE and fail the check.
+A step makes **no device-to-host read**: every length the kernels need
+travels in the slot headers, so with RCCL the whole step (collectives
+included) is stream-ordered device work.  Slots are sized for the expected
+share of a uniform hash plus a wide margin (``n/W + 6 sqrt(n/W) + 64``
+records); a segment that would not fit is sent empty and counted, so the
+reply check fails loudly instead of reading past a slot.  With one rank
+there is nothing to route: the step is the local GET pipeline (no router,
+no slots) and is HIP-graph captured.
+
+Each rank's :class:`~zkmi.bench.synthetic.GpuTree` indexes only its shard
+(``shard=(rank, world)``): a read that reached the wrong rank would answer
+NO_NODE and fail the check.  ``coll_device='cpu'`` runs the all-to-alls on
+host tensors (a gloo rehearsal on ranks that share one GPU).
 """
+
+import math
 
 import torch
 import torch.distributed as dist
@@ -37,11 +50,33 @@ from ..bench.synthetic import _i64
 
 I64, I32, U8 = torch.int64, torch.int32, torch.uint8
 
+SEG_HDR = 16
+
+
+def _r16(x):
+    return (int(x) + 15) & ~15
+
+
+def slot_records(n, world):
+    """Records one per-peer slot holds: the uniform share plus 6 standard
+    deviations and a constant margin (a hash split of ``n`` requests over
+    ``world`` owners overflowing it is a < 1e-9 event)."""
+    if world == 1:
+        return n
+    m = n / world
+    return int(math.ceil(m + 6 * math.sqrt(m) + 64))
+
 
 class ShardedGetPipeline(object):
+    """Sharded GET over ``streams`` pipelined connections per rank (their
+    phases interleaved on separate HIP streams, as in
+    :class:`~zkmi.bench.synthetic.GetPipeline`)."""
 
-    def __init__(self, tree, batch, seed=0, group=None, coll_device=None):
-        from ..bench.synthetic import GpuServer
+    # client | R2 out | server decode | tree + encode | R2 back | client
+    PHASES = 6
+
+    def __init__(self, tree, batch, seed=0, group=None, coll_device=None,
+                 streams=1):
         on = dist.is_available() and dist.is_initialized()
         self.group = group
         self.world = W = dist.get_world_size(group) if on else 1
@@ -50,24 +85,143 @@ class ShardedGetPipeline(object):
             raise ValueError('tree shard %r on rank %d of %d'
                              % (tree.shard, self.rank, W))
         self.tree = tree
-        self.batch = n = batch
+        self.batch = batch
         self.dev = dev = tree.device
         self.coll = torch.device(coll_device) if coll_device else dev
         self.seed = seed
+        # device counters: requests [overflow, bytes to peers, records to
+        # peers], replies [overflow, bytes to peers, -], received [bytes]
+        self.req_stats = torch.zeros(3, dtype=I64, device=dev)
+        self.rep_stats = torch.zeros(3, dtype=I64, device=dev)
+        self.recv_stats = torch.zeros(1, dtype=I64, device=dev)
+        self.steps = 0
+        self.subs = []
+        if streams > 1:
+            per = [batch // streams + (1 if k < batch % streams else 0)
+                   for k in range(streams)]
+            self.subs = [_Conn(self, m, seed * streams + k)
+                         for k, m in enumerate(per)]
+            self.streams = [torch.cuda.Stream(dev) for _ in per]
+        else:
+            self.subs = [_Conn(self, batch, seed)]
+            self.streams = None
+        self.last = None
+
+    # -- collectives ----------------------------------------------------------
+
+    def a2a(self, out, inp):
+        """Equal-split ``all_to_all_single`` on the collective device
+        (device tensors with RCCL; host staging for a gloo rehearsal)."""
+        if self.coll == self.dev:
+            dist.all_to_all_single(out, inp, group=self.group)
+            return out
+        o = torch.empty(out.shape, dtype=out.dtype, device=self.coll)
+        dist.all_to_all_single(o, inp.to(self.coll), group=self.group)
+        out.copy_(o)
+        return out
+
+    @property
+    def capturable(self):
+        """One rank: the whole step is device work on our streams.  With
+        RCCL the collectives are stream-ordered too, but their capture into
+        a HIP graph is not exercised here, so multi-rank steps run eager."""
+        return self.world == 1
+
+    def capture(self, acc):
+        if not self.capturable:
+            raise RuntimeError('multi-rank sharded steps run eager')
+        for c in self.subs:
+            c.device_seed()
+        torch.cuda.synchronize(self.dev)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, capture_error_mode='thread_local'):
+            self.step(acc=acc)
+        self.graph = g
+        return g
+
+    # -- one step -------------------------------------------------------------
+
+    def step(self, validate=True, acc=None):
+        if validate and acc is None:
+            acc = torch.zeros(1, dtype=I64, device=self.dev)
+        self.steps += 1
+        if self.streams is None:
+            for _ in self.subs[0].phases(validate, acc):
+                pass
+            self.last = self.subs[0].last
+            return acc if validate else None
+        cur = torch.cuda.current_stream(self.dev)
+        live = []
+        for c, s in zip(self.subs, self.streams):
+            s.wait_stream(cur)
+            live.append((s, c.phases(validate, acc)))
+        # round-robin: every rank issues the connections' collectives in the
+        # same order (a requirement of RCCL / gloo), and one connection's
+        # kernels overlap the other's all-to-all
+        while live:
+            nxt = []
+            for s, g in live:
+                with torch.cuda.stream(s):
+                    if next(g, StopIteration) is not StopIteration:
+                        nxt.append((s, g))
+            live = nxt
+        for s in self.streams:
+            cur.wait_stream(s)
+        self.last = self.subs[-1].last
+        return acc if validate else None
+
+    # -- reporting ------------------------------------------------------------
+
+    @property
+    def stats(self):
+        """Host view of the R2 counters (one device read; call after the
+        timed steps): payload bytes sent to / received from the other
+        ranks, requests served remotely, overflowing segments, and the
+        bytes every all-to-all moves between ranks (slots, padding
+        included)."""
+        rq = self.req_stats.cpu().tolist()
+        rp = self.rep_stats.cpu().tolist()
+        rv = self.recv_stats.cpu().tolist()
+        W = self.world
+        wire = sum((W - 1) * (c.req_slot + c.rep_slot) for c in self.subs) \
+            * self.steps if W > 1 else 0
+        return {'bytes_sent': rq[1] + rp[1], 'bytes_recv': rv[0],
+                'remote_reqs': rq[2], 'overflow_segments': rq[0] + rp[0],
+                'wire_bytes_sent': wire, 'steps': self.steps,
+                'req_slot_bytes': [c.req_slot for c in self.subs],
+                'rep_slot_bytes': [c.rep_slot for c in self.subs]}
+
+
+class _Conn(object):
+    """One pipelined connection of a :class:`ShardedGetPipeline`: its own
+    request / reply buffers, xid table, GPU server and slots."""
+
+    def __init__(self, pipe, n, seed):
+        from ..bench.synthetic import GpuServer
+        self.p = pipe
+        t = pipe.tree
+        W = pipe.world
+        dev = pipe.dev
+        self.n = n
+        self.seed = seed
         self.step_no = 0
         self.xid_base = 0
+        self.gstate = None
         self.xt = B.XidTable(bits=max(20, (n - 1).bit_length() + 1),
                              device=dev)
         e64 = lambda: torch.empty(n, dtype=I64, device=dev)   # noqa: E731
         e32 = lambda: torch.empty(n, dtype=I32, device=dev)   # noqa: E731
         self.idx, self.xid, self.poff, self.plen = e64(), e32(), e64(), e32()
-        self.idx_s, self.xid_s, self.poff_s, self.plen_s = (e64(), e32(),
-                                                            e64(), e32())
-        self.owner = e32()
-        self.counts = torch.empty(W, dtype=I64, device=dev)
-        L = _lib.lib()
-        self.rws = torch.empty(L.route_workspace(n, W), dtype=I64,
-                               device=dev)
+        if W > 1:
+            self.idx_s, self.xid_s, self.poff_s, self.plen_s = (
+                e64(), e32(), e64(), e32())
+            self.owner = e32()
+            self.counts = torch.empty(W, dtype=I64, device=dev)
+            self.rws = torch.empty(_lib.lib().route_workspace(n, W),
+                                   dtype=I64, device=dev)
+        else:
+            self.idx_s, self.xid_s, self.poff_s, self.plen_s = (
+                self.idx, self.xid, self.poff, self.plen)
         self.opcode = torch.full((n,), consts.OP_CODES['GET_DATA'],
                                  dtype=I32, device=dev)
         self.zero32 = torch.zeros(n, dtype=I32, device=dev)
@@ -75,113 +229,110 @@ class ShardedGetPipeline(object):
         self.acl_off = torch.zeros(1, dtype=I64, device=dev)
         self.acl_len = torch.zeros(1, dtype=I32, device=dev)
         self.acl_arena = torch.zeros(16, dtype=U8, device=dev)
-        self.maxpath = int(tree.node_path_len.max().item())
-        self.req_max = 17 + self.maxpath
-        self.rep_max = 4 + 16 + 4 + max(tree.data_bytes, 128) + 68
+        maxpath = int(t.node_path_len.max().item())
+        maxdata = int(t.data_len.max().item())
+        self.req_max = 17 + maxpath
+        self.rep_max = 4 + 16 + 4 + maxdata + 68
         self.tx = torch.empty(n * self.req_max + 64, dtype=U8, device=dev)
-        self._server_cap = 0
-        self._mk_server(n + n // 4 + 1024)
+        k = slot_records(n, W)
+        self.slot_recs = k
+        cap = W * k                      # requests this rank can receive
+        self.req_slot = _r16(SEG_HDR + k * self.req_max)
+        self.rep_slot = _r16(SEG_HDR + k * self.rep_max)
+        self.server = GpuServer(t, cap, cap * self.rep_max + 64,
+                                window=B.frame_window(self.req_max))
+        # the replies to this connection's own n requests come back
         self.rscanner = B.FrameScanner(n, dev,
                                        window=B.frame_window(self.rep_max))
         self.reply = B.alloc_replies(n, dev)
-        self.crx = torch.empty(n * self.rep_max + 64, dtype=U8, device=dev)
-        self.GpuServer = GpuServer
-        self.stats = {'bytes_sent': 0, 'bytes_recv': 0, 'remote_reqs': 0}
+        if W > 1:
+            u8 = lambda m: torch.empty(m, dtype=U8, device=dev)  # noqa: E731
+            self.sq, self.rq = u8(W * self.req_slot), u8(W * self.req_slot)
+            self.sp, self.rp = u8(W * self.rep_slot), u8(W * self.rep_slot)
+            self.rxq = u8(W * (self.req_slot - SEG_HDR) + 64)
+            self.crx = u8(W * (self.rep_slot - SEG_HDR) + 64)
+            self.nrx = torch.zeros(1, dtype=I64, device=dev)
+            self.ncrx = torch.zeros(1, dtype=I64, device=dev)
+            self.src_counts = torch.zeros(W, dtype=I64, device=dev)
+            self.back_counts = torch.zeros(W, dtype=I64, device=dev)
         self.last = None
 
-    def _mk_server(self, cap):
-        from ..bench.synthetic import GpuServer
-        self._server_cap = cap
-        self.server = GpuServer(self.tree, cap, cap * self.rep_max + 64,
-                                window=B.frame_window(self.req_max))
-        self.rxq = torch.empty(cap * self.req_max + 64, dtype=U8,
-                               device=self.dev)
+    def base_seed(self):
+        """Per-rank, per-connection request seed (bench.hip draws step s
+        from base * golden + s)."""
+        return self.seed + 1000003 * (self.p.rank + 1)
 
-    # -- collectives ----------------------------------------------------------
+    def device_seed(self):
+        """Draw the requests from a device {seed, step} pair advanced on
+        the device, so a captured graph replays new batches."""
+        if self.gstate is None:
+            self.gstate = torch.tensor([self.base_seed(), self.step_no],
+                                       dtype=I64, device=self.p.dev)
 
-    def _a2a(self, out, inp, out_splits, in_splits):
-        """``all_to_all_single`` on the collective device (device tensors
-        with RCCL; host staging for a gloo rehearsal)."""
-        if self.coll == self.dev:
-            dist.all_to_all_single(out, inp, out_splits, in_splits,
-                                   group=self.group)
-            return out
-        o = torch.empty(out.shape, dtype=out.dtype, device=self.coll)
-        dist.all_to_all_single(o, inp.to(self.coll), out_splits, in_splits,
-                               group=self.group)
-        out.copy_(o)
-        return out
-
-    @staticmethod
-    def _seg_bytes(rec_off, total, counts):
-        """Bytes of each owner's contiguous run of records: offsets of the
-        runs' first records (the stream total closes the last run)."""
-        ext = torch.cat([rec_off, total.view(1)])
-        ends = torch.cumsum(counts, 0)
-        return ext[ends] - ext[ends - counts]
-
-    # -- one step -------------------------------------------------------------
-
-    def step(self, validate=True, acc=None):
-        t = self.tree
-        n = self.batch
-        W = self.world
+    def phases(self, validate, acc):
+        """One step of this connection as a generator, yielding between the
+        PHASES phases (the parent interleaves connections there)."""
+        p = self.p
+        t = p.tree
+        n = self.n
+        W = p.world
         L = _lib.lib()
-        if validate and acc is None:
-            acc = torch.zeros(1, dtype=I64, device=self.dev)
-        seed = ((self.rank + 1) * 0x9E3779B97F4A7C15 + self.seed * 7919 +
-                self.step_no) & (2**64 - 1)
+        seed = (self.base_seed() * 0x9E3779B97F4A7C15 + self.step_no) \
+            & (2**64 - 1)
         self.step_no += 1
         L.bench_gen_get(n, _i64(seed), t.leaf0, t.n_leaves, self.xid_base,
-                        t.node_pw, self.idx, self.xid, self.poff, self.plen)
+                        t.node_pw, self.idx, self.xid, self.poff, self.plen,
+                        self.gstate)
         self.xid_base = (self.xid_base + n) & 0x7fffffff
-        L.route_requests(n, W, self.poff, self.plen, t.path_arena, self.idx,
-                         self.xid, self.owner, self.idx_s, self.xid_s,
-                         self.poff_s, self.plen_s, self.counts, self.rws)
+        if W > 1:
+            L.route_requests(n, W, self.poff, self.plen, t.path_arena,
+                             self.idx, self.xid, self.owner, self.idx_s,
+                             self.xid_s, self.poff_s, self.plen_s,
+                             self.counts, self.rws)
         rb = B.RequestBatch(n, self.opcode, self.xid_s, self.zero32,
                             self.poff_s, self.plen_s, self.zero64,
                             self.zero32, self.zero32, t.path_arena, t.slab,
                             self.acl_off, self.acl_len, self.acl_arena)
         tx, rec_off, total, _ = B.encode_requests(rb, self.xt, out=self.tx)
-        if W == 1:
-            m = n
+        if W > 1:
+            L.seg_pack(tx, rec_off, None, n, total, self.counts, W, p.rank,
+                       self.req_slot, self.sq, p.req_stats)
+        yield
+        if W > 1:
+            p.a2a(self.rq, self.sq)
+        yield
+        if W > 1:
+            L.seg_unpack(self.rq, W, p.rank, self.req_slot, self.rxq,
+                         self.nrx, self.src_counts, None)
+            rxq, nrx = self.rxq, self.nrx
+        else:
             rxq, nrx = tx, total
+        srv = self.server.serve_steps(rxq, nrx)
+        next(srv)
+        yield
+        for _ in srv:
+            pass
+        rout, rtotal, _, ft = self.server.result
+        if W > 1:
+            # replies in request order = source rank order; the source
+            # counts came with the request slots' headers
+            L.seg_pack(rout, self.server.last_rec_off, ft.count,
+                       self.server.cap_frames, rtotal, self.src_counts, W,
+                       p.rank, self.rep_slot, self.sp, p.rep_stats)
+        yield
+        if W > 1:
+            p.a2a(self.rp, self.sp)
+        yield
+        if W > 1:
+            L.seg_unpack(self.rp, W, p.rank, self.rep_slot, self.crx,
+                         self.ncrx, self.back_counts, p.recv_stats)
+            crx, ncrx = self.crx, self.ncrx
         else:
-            # the size exchange: (bytes, requests) for every rank pair
-            send = torch.stack([self._seg_bytes(rec_off, total, self.counts),
-                                self.counts], 1).contiguous()
-            recv = torch.empty_like(send)
-            self._a2a(recv, send, None, None)
-            sz = torch.cat([send, recv]).cpu().tolist()      # host read 1
-            sbytes = [r[0] for r in sz[:W]]
-            rbytes = [r[0] for r in sz[W:]]
-            rcounts = [r[1] for r in sz[W:]]
-            m = sum(rcounts)
-            nrx = sum(rbytes)
-            if m > self._server_cap:
-                self._mk_server(m + m // 4)
-            rxq = self._a2a(self.rxq[:nrx], tx[:sum(sbytes)], rbytes, sbytes)
-            self.stats['bytes_sent'] += sum(sbytes) - sbytes[self.rank]
-            self.stats['bytes_recv'] += nrx - rbytes[self.rank]
-            self.stats['remote_reqs'] += m - rcounts[self.rank]
-        rout, rtotal, _, _ = self.server.serve(rxq, nrx)
-        if W == 1:
             crx, ncrx = rout, rtotal
-        else:
-            rc = torch.tensor(rcounts, dtype=I64, device=self.dev)
-            rep_bytes = self._seg_bytes(self.server.last_rec_off[:m], rtotal,
-                                        rc)
-            back = torch.empty_like(rep_bytes)
-            self._a2a(back, rep_bytes, None, None)
-            sz = torch.cat([rep_bytes, back]).cpu().tolist()  # host read 2
-            out_b, in_b = sz[:W], sz[W:]
-            ncrx = sum(in_b)
-            crx = self._a2a(self.crx[:ncrx], rout[:sum(out_b)], in_b, out_b)
-        ft = self.rscanner.scan(crx, ncrx)
-        rep = B.decode_replies(crx, ft, self.xt, out=self.reply)
-        self.last = (rep, crx, ft)
-        if not validate:
-            return None
-        L.bench_check_get(n, rep.tensors(), self.idx_s, self.xid_s,
-                          t.data_len, acc)
-        return acc
+        cft = self.rscanner.scan(crx, ncrx)
+        chk = (self.idx_s, self.xid_s, t.data_len, acc) if validate else None
+        rep = B.decode_replies(crx, cft, self.xt, out=self.reply, check=chk,
+                               tick=self.gstate if validate else None)
+        if self.gstate is not None and not validate:
+            self.gstate[1:].add_(1)
+        self.last = (rep, crx, cft)

@@ -7,9 +7,10 @@ synthetic tree with the Jute-decode HIP kernels on each MI355X.
 ``--workload mix`` is configs[2] (create/set/delete with version CAS and ACL
 encode on the same 1M-znode tree), ``--workload storm`` configs[4]
 (EPHEMERAL|SEQUENTIAL create storm with per-step session expiry) and
-``--workload watch`` the watch fan-out of configs[3] (every rank's
-notifications all-gathered over RCCL and decoded by every rank; the value
-counts node-wide deliveries).  ``--workload chain`` pipelines
+``--workload watch`` the watch fan-out of configs[3] driven by real writes
+(each rank's GPU server arms GET_DATA watches and fires them on SET_DATA;
+the notifications of every rank are all-gathered over RCCL and decoded by
+every rank; the value counts node-wide deliveries).  ``--workload chain`` pipelines
 create -> set -> get -> delete of each path inside ONE batch (in-batch
 ordering of the GPU server, 4 ordered passes).
 One step = one batch
@@ -520,10 +521,13 @@ def run_rank(a):
         pipe = make_get(not sharded)
         per_step = a.batch
     elif a.workload == 'watch':
-        tree = S.GpuTree(a.nodes, a.data_bytes, device=dev, seed=rank)
+        tree = S.GpuTree(a.nodes, a.data_bytes, device=dev, seed=rank,
+                         watch_cap=2 * a.batch)
         pipe = S.WatchPipeline(tree, a.batch, seed=rank,
                                coll_device=cdev if world > 1 else None)
-        per_step = a.batch * world      # notifications decoded per rank
+        # write-triggered notifications decoded per rank (every rank's
+        # writes reach every rank); a batch watches distinct nodes
+        per_step = pipe.n * world
     else:
         # room for the write working set next to the 1M static nodes: the
         # mix keeps 3 generations of batch/3 nodes, the storm up to 3

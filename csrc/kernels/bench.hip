@@ -77,9 +77,12 @@ __global__ __launch_bounds__(BG_T) void bench_check_get(
 // record i belongs to producer rank i / n_per, index i % n_per, drawn with
 // seeds[rank] exactly as bench_gen_get draws it.  OK = clean decode,
 // NOTIFICATION, err OK, type NodeDataChanged, state SyncConnected and the
-// path bytes equal to the node's path.
+// path bytes equal to the node's path.  With `want` (int64 [total]) record
+// i must name node want[i] instead (the write-triggered workload: the
+// nodes a writer set, in write order).
 __global__ __launch_bounds__(BG_T) void bench_check_notif(
     int64_t total, int64_t n_per, const uint64_t* __restrict__ seeds,
+    const int64_t* __restrict__ want,
     int64_t leaf0, int64_t nleaves, const int64_t* __restrict__ node_path_off,
     const int32_t* __restrict__ node_path_len,
     const uint8_t* __restrict__ path_arena, const uint8_t* __restrict__ rx,
@@ -91,11 +94,18 @@ __global__ __launch_bounds__(BG_T) void bench_check_notif(
   int64_t good = 0;
   for (int64_t i = (int64_t)blockIdx.x * BG_T + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * BG_T) {
-    const int64_t r = i / n_per, j = i - r * n_per;
-    const uint64_t h = splitmix64(seeds[r] ^ (uint64_t)j * 0xD1B54A32D192ED03ull);
-    const int64_t v = leaf0 + (int64_t)(((h >> 32) * (uint64_t)nleaves) >> 32);
-    const int32_t pl = node_path_len[v];
-    bool g = status[i] == 0 && err[i] == 0 && opcode[i] == OP_NOTIFICATION &&
+    int64_t v;
+    if (want != nullptr) {
+      v = want[i];
+    } else {
+      const int64_t r = i / n_per, j = i - r * n_per;
+      const uint64_t h =
+          splitmix64(seeds[r] ^ (uint64_t)j * 0xD1B54A32D192ED03ull);
+      v = leaf0 + (int64_t)(((h >> 32) * (uint64_t)nleaves) >> 32);
+    }
+    const bool inr = v >= leaf0 && v < leaf0 + nleaves;
+    const int32_t pl = inr ? node_path_len[v] : -1;
+    bool g = inr && status[i] == 0 && err[i] == 0 && opcode[i] == OP_NOTIFICATION &&
              aux0[i] == 3 && aux1[i] == 3 && pay_len[i] == pl;
     if (g) {
       const uint8_t* a = rx + pay_off[i];
@@ -114,7 +124,7 @@ __global__ __launch_bounds__(BG_T) void bench_check_notif(
 extern "C" {
 
 int zk_bench_check_notif(int64_t total, int64_t n_per, const uint64_t* seeds,
-                         int64_t leaf0, int64_t nleaves,
+                         const int64_t* want, int64_t leaf0, int64_t nleaves,
                          const int64_t* node_path_off,
                          const int32_t* node_path_len,
                          const uint8_t* path_arena, const uint8_t* rx,
@@ -127,7 +137,7 @@ int zk_bench_check_notif(int64_t total, int64_t n_per, const uint64_t* seeds,
   const int64_t nb = min((total + zk::BG_T - 1) / zk::BG_T,
                          (int64_t)zk::BG_CHECK_BLOCKS);
   zk::bench_check_notif<<<(unsigned)nb, zk::BG_T, 0, st>>>(
-      total, n_per, seeds, leaf0, nleaves, node_path_off, node_path_len,
+      total, n_per, seeds, want, leaf0, nleaves, node_path_off, node_path_len,
       path_arena, rx, status, err, opcode, aux0, aux1, pay_off, pay_len, ok);
   ZK_LAUNCH_CHECK();
   return 0;

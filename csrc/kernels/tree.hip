@@ -1057,8 +1057,11 @@ __global__ __launch_bounds__(TR_T) void wt_expand_k(
   const int64_t c = wt_count(r_op, r_err, fired, i, in);
   int64_t tot;
   int64_t o = bsum[blockIdx.x] + block_excl_scan(c, sm, &tot);
-  if (blockIdx.x == nb - 1 && threadIdx.x == 0)
-    *ev_total = bsum[blockIdx.x] + tot;
+  if (blockIdx.x == nb - 1 && threadIdx.x == 0) {
+    const int64_t all = bsum[blockIdx.x] + tot;
+    ev_total[0] = min(all, cap);     // events written (the encoder's count)
+    ev_total[1] = all;               // events fired (> [0]: overflow)
+  }
   if (c == 0) return;
   const int64_t* f = fired + (int64_t)WT_REC * i;
   const int32_t op = r_op[i];
@@ -1159,8 +1162,9 @@ __global__ __launch_bounds__(WR_T) void wt_resume_k(
   int64_t tot;
   block_excl_scan(rearmed, sm, &tot);
   if (threadIdx.x == 0) {
-    out[0] = o;                  // events
+    out[0] = min(o, cap);        // events written
     out[1] = tot;                // watches re-armed
+    out[2] = o;                  // events (> out[0]: overflow)
   }
 }
 
@@ -1359,14 +1363,15 @@ int zk_tree_expire(const ZkTree* t, int64_t session, int64_t ncap,
 
 // Expand the watch masks a served batch fired (tree_serve's `fired`) into
 // notification events in request order: ev_slot (watcher slot), ev_type,
-// ev_poff / ev_plen (path in the tree's path arena); *ev_total = events
-// (only the first `cap` are written).  bsum: ceil(ncap / 256) int64.
+// ev_poff / ev_plen (path in the tree's path arena); ev_total[0] = events
+// written (at most `cap`), ev_total[1] = events fired.  bsum: ceil(ncap /
+// 256) int64.
 int zk_watch_events(const int32_t* r_op, const int32_t* r_err,
                     const int64_t* n_dev, int64_t ncap, const int64_t* fired,
                     int64_t* bsum, int64_t cap, int32_t* ev_slot,
                     int32_t* ev_type, int64_t* ev_poff, int32_t* ev_plen,
                     int64_t* ev_total, hipStream_t st) {
-  if (ncap <= 0) return hipMemsetAsync(ev_total, 0, 8, st);
+  if (ncap <= 0) return hipMemsetAsync(ev_total, 0, 16, st);
   const int64_t nb = (ncap + zk::TR_T - 1) / zk::TR_T;
   zk::wt_count_k<<<(unsigned)nb, zk::TR_T, 0, st>>>(r_op, r_err, n_dev, ncap,
                                                     fired, bsum);
@@ -1383,8 +1388,8 @@ int zk_watch_events(const int32_t* r_op, const int32_t* r_err,
 // SET_WATCHES catch-up for the frames (foff / flen, *n_dev of them) of a
 // resumed session with watcher slot wslot: events (ev_type, ev_poff /
 // ev_plen into rx) for what changed after each frame's relZxid, the other
-// watches re-armed.  out[0] = events, out[1] = re-armed watches.  ent:
-// scratch for ent_cap paths.
+// watches re-armed.  out[0] = events written (<= cap), out[1] = re-armed
+// watches, out[2] = events.  ent: scratch for ent_cap paths.
 int zk_watch_resume(const ZkTree* t, const uint8_t* rx, const int64_t* foff,
                     const int32_t* flen, const int64_t* n_dev, int64_t ncap,
                     int32_t wslot, int64_t* ent, int64_t ent_cap, int64_t cap,

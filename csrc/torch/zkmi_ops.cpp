@@ -136,7 +136,8 @@ int zk_bench_check_get(int64_t, const int32_t*, const int32_t*,
                        const int32_t*, const int32_t*, const int64_t*,
                        const int32_t*, const int64_t*, const int32_t*,
                        const int32_t*, unsigned long long*, hipStream_t);
-int zk_bench_check_notif(int64_t, int64_t, const uint64_t*, int64_t, int64_t,
+int zk_bench_check_notif(int64_t, int64_t, const uint64_t*, const int64_t*,
+                         int64_t, int64_t,
                          const int64_t*, const int32_t*, const uint8_t*,
                          const uint8_t*, const int32_t*, const int32_t*,
                          const int32_t*, const int32_t*, const int32_t*,
@@ -788,7 +789,7 @@ void watch_events(const Tensor& r_op, const Tensor& r_err, const Tensor& n_dev,
              P<int32_t>(ev_type, I32, cap, "ev_type", d),
              P<int64_t>(ev_poff, I64, cap, "ev_path_off", d),
              P<int32_t>(ev_plen, I32, cap, "ev_path_len", d),
-             P<int64_t>(ev_total, I64, 1, "ev_total", d), cur_stream()),
+             P<int64_t>(ev_total, I64, 2, "ev_total", d), cur_stream()),
          "watch_events");
 }
 
@@ -811,7 +812,7 @@ void watch_resume(const std::vector<Tensor>& t, const Tensor& rx,
              P<int32_t>(ev_type, I32, cap, "ev_type", d),
              P<int64_t>(ev_poff, I64, cap, "ev_path_off", d),
              P<int32_t>(ev_plen, I32, cap, "ev_path_len", d),
-             P<int64_t>(out, I64, 2, "out", d), cur_stream()),
+             P<int64_t>(out, I64, 3, "out", d), cur_stream()),
          "watch_resume");
 }
 
@@ -867,17 +868,18 @@ void bench_check_notif(int64_t total, int64_t n_per, const Tensor& seeds,
                        const Tensor& node_path_off,
                        const Tensor& node_path_len, const Tensor& path_arena,
                        const Tensor& rx, const std::vector<Tensor>& reply,
-                       const Tensor& acc) {
+                       const Tensor& acc, const c10::optional<Tensor>& want) {
   const int64_t cap = reply[0].numel();
   TORCH_CHECK(total <= cap, "zkmi: bench_check_notif past the reply table");
-  TORCH_CHECK(n_per > 0 && seeds.numel() * n_per >= total,
+  const bool have_want = want.has_value() && want->defined();
+  TORCH_CHECK(have_want || (n_per > 0 && seeds.numel() * n_per >= total),
               "zkmi: bench_check_notif seeds");
   ZkReplyOut o = reply_out(reply, cap, &rx);
   hip_ok(zk_bench_check_notif(
              total, n_per,
              reinterpret_cast<const uint64_t*>(
                  P<int64_t>(seeds, I64, 1, "seeds", &rx)),
-             leaf0, nleaves,
+             Popt<int64_t>(want, I64, total, "want", &rx), leaf0, nleaves,
              P<int64_t>(node_path_off, I64, leaf0 + nleaves,
                         "node_path_off", &rx),
              P<int32_t>(node_path_len, I32, leaf0 + nleaves,
@@ -1078,8 +1080,8 @@ TORCH_LIBRARY(zkmi, m) {
         "Tensor data_len, Tensor(a!) acc) -> ()", &bench_check_get);
   m.def("bench_check_notif(int total, int n_per, Tensor seeds, int leaf0, "
         "int nleaves, Tensor node_path_off, Tensor node_path_len, "
-        "Tensor path_arena, Tensor rx, Tensor[] reply, Tensor(a!) acc) -> ()",
-        &bench_check_notif);
+        "Tensor path_arena, Tensor rx, Tensor[] reply, Tensor(a!) acc, "
+        "Tensor? want=None) -> ()", &bench_check_notif);
   m.def("route_workspace(int n, int world) -> int", &route_workspace);
   m.def("route_requests(int n, int world, Tensor path_off, Tensor path_len, "
         "Tensor arena, Tensor idx, Tensor xid, Tensor(a!) owner, "

@@ -770,24 +770,37 @@ def test_gpu_session_handshake_k9_server(gpu):
 
 
 def test_gpu_watch_pipeline_single_rank(gpu):
-    """Notification fan-out data path on one rank: K13 notification encode,
-    K1 + K8 decode, device check; a few records against the Jute oracle."""
-    from zkmi.bench.synthetic import WatchPipeline
-    tree = _small_tree(gpu, 20000, 37)
+    """Write-triggered notification fan-out on one rank: GET_DATA watch=1
+    arms the server's watch table, SET_DATA of the same nodes fires one
+    NodeDataChanged each (K13), K1 + K8 decode and the device check; a few
+    records against the Jute oracle, and nothing fires twice."""
+    from zkmi.bench.synthetic import GpuTree, WatchPipeline
+    tree = GpuTree(20000, 37, fanout=100, device=gpu, seed=0,
+                   watch_cap=8192)
     pipe = WatchPipeline(tree, 5000)
     for _ in range(2):
         ok = pipe.step()
         assert int(ok.item()) == 5000
-    rep, rx, ft = pipe.last
+    rep, ft, idx = pipe.last
     assert ft.host_result()['frames'] == 5000
-    hb = bytes(rx[:4096].cpu().numpy().tobytes())
+    assert pipe.server.ev_total.cpu().tolist() == [5000, 5000]
+    hb = bytes(pipe.rx[:4096].cpu().numpy().tobytes())
     frames, _, _ = jute.scan_frames(hb)
-    for (o, ln) in frames[:20]:
+    arena = tree.path_arena.cpu().numpy().tobytes()
+    po = tree.node_path_off[idx[:20]].cpu().tolist()
+    pl = tree.node_path_len[idx[:20]].cpu().tolist()
+    for k, (o, ln) in enumerate(frames[:20]):
         pkt = jute.decode_response(hb[o:o + ln], {})
-        assert pkt['opcode'] == 'NOTIFICATION'
+        assert pkt['opcode'] == 'NOTIFICATION' and pkt['xid'] == -1
         assert pkt['type'] == 'DATA_CHANGED'
         assert pkt['state'] == 'SYNC_CONNECTED'
-        assert pkt['path'].startswith('/bench/d')
+        assert pkt['path'].encode() == arena[po[k]:po[k] + pl[k]]
+    # a write nobody watches any more fires nothing
+    from zkmi.ops import batch as B
+    rb = pipe._batch(pipe.ops_set, pipe.neg32, idx, pipe._xids(), True)
+    tx, _, total, _ = B.encode_requests(rb, pipe.xt, out=pipe.tx)
+    pipe.server.serve(tx, total, session=pipe.sid_wr, wslot=1)
+    assert pipe.server.ev_total.cpu().tolist() == [0, 0]
 
 
 def _watch_rank(rank, world, port, q):
@@ -798,7 +811,8 @@ def _watch_rank(rank, world, port, q):
     try:
         from zkmi.bench.synthetic import GpuTree, WatchPipeline
         dev = torch.device('cuda', 0)
-        tree = GpuTree(20000, 37, fanout=100, device=dev, seed=rank)
+        tree = GpuTree(20000, 37, fanout=100, device=dev, seed=rank,
+                       watch_cap=8192)
         pipe = WatchPipeline(tree, 3000, coll_device='cpu')
         ok = pipe.step()
         q.put((rank, int(ok.item())))

@@ -92,7 +92,7 @@ class GpuTree(object):
 
     def __init__(self, n_nodes=1_000_000, data_bytes=100, fanout=1000,
                  device=None, spare=0.25, seed=0, shard=None, ctime_ms=None,
-                 data_dist=None, name_pad=None, scratch=0):
+                 data_dist=None, name_pad=None, scratch=0, watch_cap=0):
         dev = torch.device(device) if device is not None else \
             torch.device('cuda', torch.cuda.current_device())
         self.device = dev
@@ -203,6 +203,15 @@ class GpuTree(object):
                          self.slot_cap, self.free_list, self.cver,
                          self.nchild, self.pzxid, self.dirty,
                          self.dirty_list, self.node_pw]
+        # watch table (watch_cap > 0): path-keyed one-shot watches of up to
+        # 64 watcher slots (csrc/kernels/tree.hip wt_*); every serve of a
+        # tree with one fires the watches its writes hit
+        self.watch = None
+        if watch_cap > 0:
+            wh = _next_pow2(2 * int(watch_cap))
+            self.watch = (torch.zeros(wh, dtype=I64, device=dev),
+                          torch.zeros(2 * wh, dtype=I64, device=dev))
+            self._tensors = self._tensors + list(self.watch)
         now = int(time.time() * 1000) if ctime_ms is None else ctime_ms
         L.tree_fill(self._tensors, 0, nst, nk, now)
         # shard = (rank, world): this replica indexes only the leaves whose
@@ -292,9 +301,91 @@ class GpuServer(object):
         self.cap_frames = cap_frames
         self.scanner = B.FrameScanner(cap_frames, dev, window=window)
         self.ows = None                   # ordered-serve workspace (lazy)
+        self.notif = None
+        if tree.watch is not None:
+            self._init_watch(cap_frames, dev)
+
+    # -- watches --------------------------------------------------------------
+
+    def _init_watch(self, cap, dev):
+        """Buffers of the watch events of one batch: the masks each write
+        fired (5 words per request), then per event the watcher slot,
+        notification type and path, and their K13 encode as xid -1
+        notification frames (``NOTIFICATION``, state SyncConnected)."""
+        ecap = 3 * cap + 64
+        self.ecap = ecap
+        self.fired = torch.zeros(5 * cap, dtype=I64, device=dev)
+        self.wbsum = torch.empty((cap + 255) // 256, dtype=I64, device=dev)
+        self.ev_slot = torch.empty(ecap, dtype=I32, device=dev)
+        self.ev_type = torch.empty(ecap, dtype=I32, device=dev)
+        self.ev_poff = torch.empty(ecap, dtype=I64, device=dev)
+        self.ev_plen = torch.empty(ecap, dtype=I32, device=dev)
+        # [events written (<= ecap), events fired]
+        self.ev_total = torch.zeros(2, dtype=I64, device=dev)
+        self.rs_out = torch.zeros(3, dtype=I64, device=dev)
+        # notification frame: 4 + 16 header + type + state + path
+        self.maxpath = int(self.tree.node_path_len.max().item()) + 16
+        self.notif_buf = torch.empty(ecap * (28 + 4 + self.maxpath) + 64,
+                                     dtype=U8, device=dev)
+        self._nresp = self._notif_batch(self.ev_poff, self.ev_plen,
+                                        self.tree.path_arena, self.ev_type,
+                                        self.ev_total[0:1], ecap, dev)
+
+    @staticmethod
+    def _notif_batch(poff, plen, arena, ntype, count, cap, dev):
+        """ResponseBatch of `cap` notification records (xid -1, zxid -1)."""
+        return B.ResponseBatch(
+            torch.full((cap,), consts.OP_CODES['NOTIFICATION'], dtype=I32,
+                       device=dev),
+            torch.full((cap,), consts.XID_NOTIFICATION, dtype=I32,
+                       device=dev),
+            torch.zeros(cap, dtype=I32, device=dev),
+            torch.full((cap,), -1, dtype=I64, device=dev),
+            torch.full((cap,), -1, dtype=I64, device=dev),
+            poff, plen, arena, ntype, count)
+
+    def _notify(self):
+        """Expand the fired masks of the last serve into events (request
+        order) and encode them: ``self.notif = (stream, bytes, slot per
+        frame, events)`` — the watchers' notification frames, all on the
+        device."""
+        L = _lib.lib()
+        r = self.resp
+        L.watch_events(r.opcode, r.err, r.count, self.cap_frames, self.fired,
+                       self.wbsum, self.ev_slot, self.ev_type, self.ev_poff,
+                       self.ev_plen, self.ev_total)
+        out, rec_off, total, _ = B.encode_responses(
+            self._nresp, self.tree.store, self.notif_buf.numel(),
+            out=self.notif_buf)
+        self.notif_rec_off = rec_off
+        self.notif = (out, total, self.ev_slot, self.ev_total[0:1])
+
+    def _resume(self, rx, ft, wslot):
+        """SET_WATCHES catch-up of the batch's SET_WATCHES frames for
+        watcher ``wslot`` (csrc/kernels/tree.hip wt_resume_k): events for
+        what changed after relZxid, encoded with the request bytes as path
+        arena; the other watches are re-armed."""
+        L = _lib.lib()
+        dev = self.tree.device
+        cap = self.ecap
+        ev_type = torch.empty(cap, dtype=I32, device=dev)
+        ev_poff = torch.empty(cap, dtype=I64, device=dev)
+        ev_plen = torch.empty(cap, dtype=I32, device=dev)
+        ent = torch.empty(cap, dtype=I64, device=dev)
+        L.watch_resume(self.tree.tensors, rx, ft.off, ft.length, ft.count,
+                       self.cap_frames, wslot, ent, ev_type, ev_poff, ev_plen,
+                       self.rs_out)
+        nb = self._notif_batch(ev_poff, ev_plen, rx, ev_type,
+                               self.rs_out[0:1], cap, dev)
+        # paths of a SET_WATCHES are bounded by its frame: ZooKeeper paths
+        buf = torch.empty(cap * 32 + int(rx.numel()) + 64, dtype=U8,
+                          device=dev)
+        out, _, total, _ = B.encode_responses(nb, self.tree.store,
+                                              buf.numel(), out=buf)
+        self.resume_notif = (out, total, self.rs_out)
 
     def serve(self, rx, n, session=0, terminate=False, ordered=False,
-              passes=4):
+              passes=4, wslot=-1, resume=False):
         """Serve the request stream ``rx[:n]`` for ``session`` (the owner of
         any EPHEMERAL node it creates).  ``n`` is a host length or the
         request encoder's device total (no host read).  Returns the reply
@@ -307,12 +398,13 @@ class GpuServer(object):
         SYSTEMERROR, see :meth:`order_stats`).  Reads and sets followed by
         a write to their path snapshot their reply into the tree's
         ``scratch``.  Without it requests of a batch are concurrent."""
-        for _ in self.serve_steps(rx, n, session, terminate, ordered, passes):
+        for _ in self.serve_steps(rx, n, session, terminate, ordered, passes,
+                                  wslot, resume):
             pass
         return self.result
 
     def serve_steps(self, rx, n, session=0, terminate=False, ordered=False,
-                    passes=4):
+                    passes=4, wslot=-1, resume=False):
         """:meth:`serve` as a generator yielding once, between the request
         decode and the tree; the return tuple lands in ``self.result`` (a
         pipelined caller interleaves another connection's work there)."""
@@ -334,15 +426,25 @@ class GpuServer(object):
                     device=self.tree.device)
             L.tree_serve_ordered(self.tree.tensors, rx, rt.tensors(),
                                  ft.count, self.cap_frames, out, session,
-                                 now, self.ows, passes, self.tree.scratch)
+                                 now, self.ows, passes, self.tree.scratch,
+                                 wslot, self.fired if self.tree.watch
+                                 is not None else None)
         else:
             L.tree_serve_frames(self.tree.tensors, rx, ft.off, ft.length,
-                                ft.count, self.cap_frames, out, session, now)
+                                ft.count, self.cap_frames, out, session, now,
+                                wslot, self.fired if self.tree.watch
+                                is not None else None)
         out, rec_off, total, err = B.encode_responses(
             r, self.tree.store, self.out.numel(), out=self.out,
             presized=self.presized, terminate=terminate)
         self.last_rec_off = rec_off         # reply frame starts (R2 splits)
         self.result = (out, total, err, ft)
+        if self.tree.watch is not None:
+            self._notify()
+            if resume:
+                if wslot < 0:
+                    raise ValueError('resume needs the watcher slot')
+                self._resume(rx, ft, wslot)
 
     def order_stats(self):
         """(largest same-path rank, scratch bytes used) of the last ordered
@@ -1092,120 +1194,211 @@ class StormPipeline(object):
 
 
 class WatchPipeline(object):
-    """Watch fan-out across the node (BASELINE config 4's data path, R1 at
-    scale): every rank fires ``batch`` NodeDataChanged notifications for
-    random nodes of its tree, encodes them as wire records on the GPU (K13,
-    xid -1), and the streams of all ranks are all-gathered over RCCL
-    (``torch.distributed``, backend ``nccl`` = RCCL over xGMI); every rank
-    then frame-scans and decodes ALL ranks' notifications (K1 + K8) and
-    checks each one on the device (producer rank, node path, type, state).
+    """Watch fan-out across the node driven by real writes (BASELINE config
+    4's data path, R1 at scale).  Every rank's GPU server keeps a watch
+    table (:class:`GpuTree` ``watch_cap``); one step on rank ``r``:
 
-    One step moves ``world * batch`` notifications into every rank, i.e.
-    ``world**2 * batch`` deliveries node-wide.  ``coll_device='cpu'`` runs
-    the collective on host tensors (gloo rehearsal)."""
+      arm     the watcher session (slot 0) sends ``batch`` GET_DATA with
+              watch=1 for distinct nodes (K10 -> K1 -> lookup + arm -> K13
+              -> K1 + K2-K4, every reply checked on the device)
+      write   the writer session (slot 1) SET_DATAs the same nodes; each
+              write fires its node's watch (lib/zk-session.js:558-574): the
+              server expands the fired masks and K13-encodes one
+              NodeDataChanged notification frame (xid -1) per node, in
+              write order; the writes' replies are checked too
+      R1      the notification streams of all ranks travel in equal-size
+              slots ({bytes, frames} header + frames) through one
+              ``all_gather_into_tensor`` (RCCL over xGMI with ``nccl``);
+              every rank concatenates them (``seg_unpack``), K1 + K8
+              decodes ALL ranks' notifications and checks each on the
+              device: NodeDataChanged, SyncConnected, and the path of the
+              node that rank's writer set at that position
+
+    One step delivers ``world * batch`` notifications to every rank:
+    ``world**2 * batch`` deliveries node-wide (:attr:`per_step`).
+    ``coll_device='cpu'`` runs the all-gather on host tensors (gloo
+    rehearsal).  A step makes no device-to-host read."""
 
     def __init__(self, tree, batch, seed=0, group=None, coll_device=None):
         import torch.distributed as dist
+        if tree.watch is None:
+            raise ValueError('WatchPipeline needs GpuTree(watch_cap=...)')
         self.dist = dist
         self.group = group
         on = dist.is_available() and dist.is_initialized()
-        self.world = dist.get_world_size(group) if on else 1
+        self.world = W = dist.get_world_size(group) if on else 1
         self.rank = dist.get_rank(group) if on else 0
         self.tree = tree
-        self.n = batch
+        # distinct nodes per step: at most the tree's leaves
+        self.n = n = min(batch, tree.n_leaves)
         dev = tree.device
         self.dev = dev
         self.coll_device = torch.device(coll_device) if coll_device else dev
-        n = batch
-        self.idx = torch.empty(n, dtype=I64, device=dev)
-        self.xid = torch.empty(n, dtype=I32, device=dev)
-        self.poff = torch.empty(n, dtype=I64, device=dev)
-        self.plen = torch.empty(n, dtype=I32, device=dev)
-        self.resp = B.ResponseBatch(
-            torch.zeros(n, dtype=I32, device=dev),            # NOTIFICATION
-            torch.full((n,), consts.XID_NOTIFICATION, dtype=I32, device=dev),
-            torch.zeros(n, dtype=I32, device=dev),
-            torch.full((n,), -1, dtype=I64, device=dev),
-            torch.full((n,), -1, dtype=I64, device=dev),      # zxid -1
-            self.poff, self.plen, tree.path_arena,
-            torch.full((n,), consts.NOTIFICATION_TYPE['DATA_CHANGED'],
-                       dtype=I32, device=dev),
-            torch.tensor([n], dtype=I64, device=dev))
+        self.per_step = W * W * n
         maxpath = int(tree.node_path_len.max().item())
-        self.rec_max = 16 + 4 + 4 + 4 + maxpath + 4
-        self.tx = torch.empty(n * self.rec_max + 64, dtype=U8, device=dev)
-        self.rx = torch.empty(self.world * self.tx.numel(), dtype=U8,
+        self.data_bytes = min(tree.data_bytes, 128)
+        self.j = torch.arange(n, dtype=I64, device=dev)
+        self.jw = torch.arange(W * n, dtype=I64, device=dev) % n
+        self.rank_of = torch.arange(W * n, dtype=I64, device=dev) // n
+        self.xid_iota = torch.arange(n, dtype=I32, device=dev)
+        self.xid_base = 0
+        self.ops_get = torch.full((n,), consts.OP_CODES['GET_DATA'],
+                                  dtype=I32, device=dev)
+        self.ops_set = torch.full((n,), consts.OP_CODES['SET_DATA'],
+                                  dtype=I32, device=dev)
+        self.one32 = torch.ones(n, dtype=I32, device=dev)
+        self.neg32 = torch.full((n,), -1, dtype=I32, device=dev)
+        self.zero32 = torch.zeros(n, dtype=I32, device=dev)
+        self.zero64 = torch.zeros(n, dtype=I64, device=dev)
+        g = torch.Generator(device=dev)
+        g.manual_seed(seed + 23)
+        self.data_arena = torch.randint(0, 256, (n * self.data_bytes + 16,),
+                                        dtype=U8, device=dev, generator=g)
+        self.data_off = self.j * self.data_bytes
+        self.data_len = torch.full((n,), self.data_bytes, dtype=I32,
+                                   device=dev)
+        self.acl_off = torch.zeros(1, dtype=I64, device=dev)
+        self.acl_len = torch.zeros(1, dtype=I32, device=dev)
+        self.acl_arena = torch.zeros(16, dtype=U8, device=dev)
+        self.tx = torch.empty(n * (33 + maxpath + self.data_bytes) + 64,
+                              dtype=U8, device=dev)
+        self.xt = B.XidTable(bits=max(12, (n - 1).bit_length() + 1),
+                             device=dev)
+        rep_max = 4 + 16 + 4 + max(tree.data_bytes, 128) + 68
+        self.server = GpuServer(tree, n, n * rep_max + 64,
+                                window=B.frame_window(33 + maxpath +
+                                                      self.data_bytes))
+        self.rscan = B.FrameScanner(n, dev, window=B.frame_window(rep_max))
+        self.reply = B.alloc_replies(n, dev)
+        # R1 slots: one notification stream per rank
+        rec = 4 + 16 + 4 + 4 + 4 + maxpath
+        self.rec_max = rec
+        self.slot = (16 + n * rec + 15) & ~15
+        self.send = torch.empty(self.slot, dtype=U8, device=dev)
+        self.big = torch.empty(W * self.slot, dtype=U8, device=dev)
+        self.rx = torch.empty(W * (self.slot - 16) + 64, dtype=U8,
                               device=dev)
-        self.xt = B.XidTable(bits=10, device=dev)
-        self.reply = B.alloc_replies(self.world * n, dev)
-        self.seeds = torch.empty(self.world, dtype=I64, device=dev)
+        self.nrx = torch.zeros(1, dtype=I64, device=dev)
+        self.src_counts = torch.zeros(W, dtype=I64, device=dev)
+        self.pstats = torch.zeros(3, dtype=I64, device=dev)
+        self.nscan = B.FrameScanner(W * n, dev, window=B.frame_window(rec))
+        self.nreply = B.alloc_replies(W * n, dev)
+        self.nxt = B.XidTable(bits=10, device=dev)
+        self.sid_w = (2 << 56) | (self.rank + 1)
+        self.sid_wr = (3 << 56) | (self.rank + 1)
         self.seed = seed
         self.step_no = 0
         self.last = None
+        self.stats = {'armed': 0, 'written': 0, 'notified': 0}
 
-    def _seed(self, rank):
-        return ((rank * 0x9E3779B97F4A7C15 + self.step_no) & (2**64 - 1))
+    def _affine(self, rank, step):
+        """(a, b) of the distinct nodes rank ``rank`` watches and writes at
+        ``step``: node leaf0 + (a * j + b) % n_leaves, a coprime with
+        n_leaves (a permutation, so the batch's nodes are distinct)."""
+        import math
+        nl = self.tree.n_leaves
+        h = (rank + 1) * 0x9E3779B97F4A7C15 + (step + 1) * 0xBF58476D1CE4E5B9 \
+            + self.seed * 0x94D049BB133111EB
+        h &= (1 << 62) - 1
+        a = (h % max(nl - 1, 1)) + 1
+        while math.gcd(a, nl) != 1:
+            a += 1
+        b = (h >> 20) % nl
+        return a, b
 
-    def _gather(self, total):
-        """All-gather the ranks' encoded streams into ``self.rx``; returns
-        the gathered byte count (contiguous, rank order)."""
-        dist, W, cd = self.dist, self.world, self.coll_device
-        if W == 1:
-            return self.tx, int(total.item())
-        sz = torch.empty(W, dtype=I64, device=cd)
-        dist.all_gather_into_tensor(sz, total.to(cd), group=self.group)
-        sizes = sz.tolist()
-        mx = max(sizes)
-        if cd == self.dev:
-            dist.all_gather_into_tensor(self.rx[:W * mx], self.tx[:mx],
-                                        group=self.group)
-            big = self.rx
+    def _batch(self, ops, arg, idx, xid, data):
+        t = self.tree
+        poff = t.node_path_off[idx]
+        plen = t.node_path_len[idx]
+        if data:
+            doff, dlen = self.data_off, self.data_len
         else:
-            big = torch.empty(W * mx, dtype=U8, device=cd)
-            dist.all_gather_into_tensor(big, self.tx[:mx].to(cd),
-                                        group=self.group)
-        if all(s == mx for s in sizes):
-            if big is not self.rx:
-                self.rx[:W * mx].copy_(big)
-            return self.rx, W * mx
-        # uneven streams: close the gaps (rank order is kept)
-        out = torch.empty(sum(sizes), dtype=U8, device=self.dev)
-        o = 0
-        for r, s in enumerate(sizes):
-            out[o:o + s].copy_(big[r * mx:r * mx + s])
-            o += s
-        self.rx[:o].copy_(out)
-        return self.rx, o
+            doff, dlen = self.zero64, self.zero32
+        return B.RequestBatch(self.n, ops, xid, arg, poff, plen, doff, dlen,
+                              self.zero32, t.path_arena, self.data_arena,
+                              self.acl_off, self.acl_len, self.acl_arena)
+
+    def _xids(self):
+        x = (self.xid_iota + self.xid_base) & 0x7fffffff
+        self.xid_base = (self.xid_base + self.n) & 0x7fffffff
+        return x
+
+    def _roundtrip(self, rb, session, wslot, check=None):
+        tx, _, total, _ = B.encode_requests(rb, self.xt, out=self.tx)
+        out, rtotal, _, _ = self.server.serve(tx, total, session=session,
+                                              wslot=wslot)
+        ft = self.rscan.scan(out, rtotal)
+        return B.decode_replies(out, ft, self.xt, out=self.reply,
+                                check=check)
 
     def step(self, validate=True, acc=None):
         t = self.tree
         n = self.n
+        W = self.world
         L = _lib.lib()
-        seeds = [self._seed(r) for r in range(self.world)]
-        self.step_no += 1
-        L.bench_gen_get(n, _i64(seeds[self.rank]), t.leaf0, t.n_leaves, 0,
-                        t.node_pw, self.idx, self.xid, self.poff, self.plen)
-        _, _, total, err = B.encode_responses(self.resp, t.store,
-                                              self.tx.numel(), out=self.tx)
-        rx, nrx = self._gather(total)
-        ft = B.frame_scan(rx, nrx, cap=self.world * n,
-                          window=B.frame_window(self.rec_max))
-        rep = B.decode_replies(rx, ft, self.xt, out=self.reply)
-        self.last = (rep, rx, ft)
-        if not validate:
-            return None
         if acc is None:
             acc = torch.zeros(1, dtype=I64, device=self.dev)
-        self.seeds.copy_(torch.tensor(
-            [s - (1 << 64) if s >= (1 << 63) else s for s in seeds],
-            dtype=I64))
-        L.bench_check_notif(self.world * n, n, self.seeds, t.leaf0,
-                            t.n_leaves, t.node_path_off, t.node_path_len,
-                            t.path_arena, rx, rep.tensors(), acc)
+        nl = t.n_leaves
+        a, b = self._affine(self.rank, self.step_no)
+        idx = t.leaf0 + (self.j * a + b) % nl
+        # arm: GET_DATA watch=1 from the watcher session (slot 0)
+        xid = self._xids()
+        arm = acc.new_zeros(1)
+        self._roundtrip(self._batch(self.ops_get, self.one32, idx, xid,
+                                    False), self.sid_w, 0,
+                        check=(idx, xid, t.data_len, arm))
+        # write: SET_DATA of the same nodes from the writer (slot 1)
+        rep = self._roundtrip(self._batch(self.ops_set, self.neg32, idx,
+                                          self._xids(), True),
+                              self.sid_wr, 1)
+        wrote = ((rep.status[:n] == 0) & (rep.err[:n] == 0)).sum()
+        # R1: every rank's notification stream to every rank
+        nbuf, ntotal, _, ncount = self.server.notif
+        L.seg_pack(nbuf, self.server.notif_rec_off, ncount,
+                   self.server.ecap, ntotal, ncount, 1, 0, self.slot,
+                   self.send, self.pstats)
+        if W > 1:
+            if self.coll_device == self.dev:
+                self.dist.all_gather_into_tensor(self.big, self.send,
+                                                 group=self.group)
+            else:
+                o = torch.empty(self.big.shape, dtype=U8,
+                                device=self.coll_device)
+                self.dist.all_gather_into_tensor(
+                    o, self.send.to(self.coll_device), group=self.group)
+                self.big.copy_(o)
+            big = self.big
+        else:
+            big = self.send
+        L.seg_unpack(big, W, self.rank, self.slot, self.rx, self.nrx,
+                     self.src_counts, None)
+        ft = self.nscan.scan(self.rx, self.nrx)
+        nrep = B.decode_replies(self.rx, ft, self.nxt, out=self.nreply)
+        self.step_no += 1
+        self.last = (nrep, ft, idx)
+        if not validate:
+            return None
+        # the nodes every rank's writer set, in write order
+        want = torch.empty(W * n, dtype=I64, device=self.dev)
+        for r in range(W):
+            ar, br = self._affine(r, self.step_no - 1)
+            want[r * n:(r + 1) * n] = t.leaf0 + (self.j * ar + br) % nl
+        good = torch.zeros(1, dtype=I64, device=self.dev)
+        L.bench_check_notif(W * n, n, self.zero64[:1], t.leaf0, nl,
+                            t.node_path_off, t.node_path_len, t.path_arena,
+                            self.rx, nrep.tensors(), good, want)
+        # a step counts only if every arm and write answered OK
+        ok = (arm[0] == n) & (wrote == n) & (ft.count[0] == W * n)
+        acc[:1] += torch.where(ok, good, torch.zeros_like(good))
+        self.stats['armed'] += n
+        self.stats['written'] += n
+        self.stats['notified'] += W * n
         return acc
 
     def diagnose(self):
-        rep, rx, ft = self.last
+        nrep, ft, idx = self.last
         return {'frames': ft.host_result(),
-                'status_bad': int((rep.status != 0).sum().item()),
-                'opcodes': torch.unique(rep.opcode).cpu().tolist()}
+                'status_bad': int((nrep.status != 0).sum().item()),
+                'opcodes': torch.unique(nrep.opcode).cpu().tolist(),
+                'events': self.server.ev_total.cpu().tolist(),
+                'overflow': self.pstats.cpu().tolist()}

@@ -12,7 +12,9 @@ encode on the same 1M-znode tree), ``--workload storm`` configs[4]
 the notifications of every rank are all-gathered over RCCL and decoded by
 every rank; the value counts node-wide deliveries).  ``--workload chain`` pipelines
 create -> set -> get -> delete of each path inside ONE batch (in-batch
-ordering of the GPU server, 4 ordered passes).
+ordering of the GPU server, 4 ordered passes); ``--workload nest`` does
+createWithEmptyParents-style depth-3 creates, the parent's EXISTS and the
+bottom-up deletes in one batch (parent / child order).
 One step = one batch
 of ``--batch`` GET_DATA requests per GPU pushed through the full ZooKeeper
 wire path on the GPU (see zkmi/bench/synthetic.py): client request encode
@@ -337,7 +339,7 @@ def main():
                          'step (measured no faster than lockstep, 0.80 vs '
                          '0.79 ms)')
     ap.add_argument('--workload', choices=('get', 'mix', 'storm', 'watch',
-                                           'ensemble', 'chain'),
+                                           'ensemble', 'chain', 'nest'),
                     default='get')
     ap.add_argument('--replica', action='store_true',
                     help='get: every rank serves its own full replica of the '
@@ -532,15 +534,19 @@ def run_rank(a):
         # room for the write working set next to the 1M static nodes: the
         # mix keeps 3 generations of batch/3 nodes, the storm up to 3
         # batches (the expiring session's two, the new session's first)
-        spare = (a.batch * (1 if a.workload in ('mix', 'chain') else 3) +
-                 8192) / a.nodes
-        # chain: the set and get of every chain reply from a snapshot
+        spare = (a.batch * (1 if a.workload in ('mix', 'chain', 'nest')
+                            else 3) + 8192) / a.nodes
+        # chain: the set and get of every chain reply from a snapshot; nest:
+        # the parents' EXISTS
         scratch = (a.batch // 2 + 64) * (80 + ((a.data_bytes + 15) & ~15)) \
-            if a.workload == 'chain' else 0
+            if a.workload in ('chain', 'nest') else 0
         tree = S.GpuTree(a.nodes, a.data_bytes, device=dev, seed=rank,
                          spare=spare + 0.05, scratch=scratch)
         if a.workload == 'chain':
             pipe = S.ChainPipeline(tree, a.batch, a.data_bytes, seed=rank)
+            per_step = pipe.n
+        elif a.workload == 'nest':
+            pipe = S.NestPipeline(tree, a.batch, seed=rank)
             per_step = pipe.n
         elif a.workload == 'mix':
             pipe = S.MixPipeline(tree, a.batch, a.data_bytes, seed=rank)

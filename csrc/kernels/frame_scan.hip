@@ -45,12 +45,14 @@
 //            exit, is the tile terminal; frame counts scanned per block of
 //            256 tiles.  The leftmost broken link / terminal go to fs_link
 //            as one atomic per block.
-//  fs_link   one workgroup.  No broken link before the first terminal (the
-//            usual case): scan the block totals, done.  Otherwise repair:
-//            every run of broken links is re-walked in parallel from the
-//            exact exit (one wave per run, bounded rounds), then the links
-//            are re-checked and what is left is repaired serially; then
-//            the counts are scanned up to the first terminal: row bases and
+//  fs_link   No broken link before the first terminal (the usual case):
+//            one workgroup scans the block totals, done.  Otherwise repair
+//            over a grid of 32 workgroups, in rounds to a fix-point: every
+//            broken link is re-walked in parallel (one wave per link) from
+//            the exit before it; what the rounds leave (chains of exits
+//            that each depend on the previous repair) is finished serially,
+//            tiles covered whole by one frame filled in one step; then the
+//            counts are scanned up to the first terminal: row bases and
 //            result[0..3].
 //  fs_rows   one wave per tile writes its (body offset, length) rows.
 //
@@ -260,7 +262,8 @@ __global__ __launch_bounds__(256) void fs_tile(
     uint16_t* __restrict__ pre, int64_t* __restrict__ sx, uint64_t* lbw,
     int64_t* __restrict__ rec_entry, int64_t* __restrict__ rec_exit,
     int64_t* __restrict__ rec_meta, int32_t* __restrict__ rcount,
-    int64_t ntiles_cap, int64_t* __restrict__ dbg, int32_t minb) {
+    int64_t ntiles_cap, int64_t* __restrict__ dbg, int32_t minb,
+    int32_t nospec) {
   constexpr int K = W / 64;                 // window entries per lane
   constexpr int XW = W / 32;                // candidate words used
   static_assert(W % 64 == 0 && K >= 1 && K <= 32, "window");
@@ -506,7 +509,11 @@ __global__ __launch_bounds__(256) void fs_tile(
   const int64_t t_1 = dbg ? wall_clock64() : 0;
   int64_t E = 0;
   bool none = false;
-  if (t > 0) {
+  if (t > 0 && nospec) {
+    // (tests: every tile but the first without a speculated entry, the
+    // worst case of the link repair)
+    none = true;
+  } else if (t > 0) {
     // Tile t-1 is running or done.  Poll with exponential back-off: these
     // loads bypass the caches, and thousands of waves polling every few
     // hundred cycles flood the fabric (it tripled every tile's staging
@@ -604,8 +611,13 @@ __global__ __launch_bounds__(256) void fs_tile(
       w.cnt = np + (m - w.js);
       fc_join_end(w, send, n);
     }
-  } else if (lane == 0) {
-    fc_stat(stats, 1, 1);
+  } else {
+    // no speculated entry: the exit recorded is the survivor's (the likely
+    // one), so fs_link's grid repair of the NEXT tile can start from it in
+    // the same round as this tile's own repair (a run of such tiles settles
+    // in one round, not one tile per round)
+    if (sm) fc_join_end(w, send, n);
+    if (lane == 0) fc_stat(stats, 1, 1);
   }
   if (lane == 0) {
     sx[t] = send;
@@ -691,112 +703,144 @@ ZK_DEV FcWalk fc_walk(const uint8_t* __restrict__ buf, int64_t n,
   return r;
 }
 
-// fs_link's parallel repair pass (all threads of the block call it).
-// Lists the broken links in order, groups them into runs of consecutive
-// tiles, and re-walks the runs in rounds, one wave per run: a run's wave
-// walks from the exit before its head until a link holds, a terminal, or
-// the next run's head.  Each tile is written by one wave per round.  An
-// exit that lies before the tile (-1 of a tile with no entry, a terminal's
-// position) is no entry: that run waits (the serial pass afterwards
-// settles whatever is left).  At most FL_ROUNDS rounds.
-constexpr int FL_ROUNDS = 8;
-ZK_DEV void fs_link_parallel(
-    const uint8_t* __restrict__ buf, int64_t n, int64_t ntiles, int64_t maxp,
-    const int64_t* __restrict__ sx, const uint16_t* __restrict__ list,
-    const int32_t* __restrict__ rcount, uint16_t* pre, int64_t* rec_entry,
-    int64_t* rec_exit, int64_t* rec_meta, int32_t* hbuf, int32_t* blist,
-    int64_t* red, int64_t* s_nh, uint8_t* win, uint64_t* stats,
-    const uint8_t* __restrict__ bflag) {
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int64_t INF = INT64_MAX;
-  // 1. broken links k (1 <= k < ntiles, tile k-1 not a terminal), in order
-  const int64_t pch = (ntiles + FL_T - 1) / FL_T;
-  const int64_t c0 = min((int64_t)tid * pch, ntiles);
-  const int64_t c1 = min(c0 + pch, ntiles);
-  // (fs_check's per-link flags: this pass runs before any repair, so they
-  // are current; contiguous bytes, no dependent loads)
-  int64_t nb = 0;
-  for (int64_t k = max(c0, (int64_t)1); k < c1; ++k) nb += bflag[k];
-  int64_t nb_tot;
-  int64_t ob = block_excl_scan(nb, red, &nb_tot);
-  for (int64_t k = max(c0, (int64_t)1); k < c1; ++k)
-    if (bflag[k]) blist[ob++] = (int32_t)k;
-  __threadfence_block();
+// fs_link's grid: FL_B workgroups.  The usual scan (no broken link before
+// the first terminal) is block 0 alone: the others return at once.  A
+// repair runs in rounds over the whole grid (a fix-point): each round lists
+// the broken links before the current first terminal and re-walks every
+// one of them in parallel, one wave per link, from the exit of the tile
+// before as it stands.  A link holds once its entry equals the exit before
+// it; a tile whose speculated entry was missing or wrong but whose survivor
+// is the true chain (the usual repair: a frontier wait that timed out, a
+// garbage candidate that survived its tile) re-walks to the same exit, so
+// one round settles any number of such tiles at once — where the serial
+// repair paid one tile after the other (the round-2 storm stream: 50 ms).
+// What a round cannot settle is a chain of exits that each depend on the
+// previous repair (frames longer than the window crossing tile after tile):
+// after FL_GROUNDS rounds block 0 finishes those serially, skipping the
+// tiles a long frame covers in one step.
+constexpr int FL_B = 32;                   // fs_link workgroups
+constexpr int FL_GROUNDS = 6;              // grid repair rounds
+constexpr uint64_t FL_BAR_TICKS = 50000000;   // 0.5 s: barrier abandoned
+// grid words after lbw's stats (uint64): [0] barrier arrivals, [1] barrier
+// generation, [2] abort, then per round r [3 + 2r] first terminal (ntiles -
+// k, max), [4 + 2r] broken links listed
+constexpr int FL_GW = 3 + 2 * FL_GROUNDS;
+
+// Grid barrier over fs_link's FL_B workgroups (they are co-resident: 32
+// blocks on a 256-CU part, and nothing they wait for needs a CU they hold).
+// Every wait is bounded: past FL_BAR_TICKS the grid is told to abort and
+// block 0 falls back to the serial repair.  Returns false on abort.
+ZK_DEV bool fl_sync(unsigned long long* g) {
+  __shared__ int s_ok;
   __syncthreads();
-  // 2. run heads: broken links whose predecessor link is not broken
-  int32_t* hcur = hbuf;
-  int32_t* hnxt = blist;
-  {
-    const int64_t per = (nb_tot + FL_T - 1) / FL_T;
-    const int64_t q0 = min((int64_t)tid * per, nb_tot);
-    const int64_t q1 = min(q0 + per, nb_tot);
-    int64_t nh = 0;
-    for (int64_t i = q0; i < q1; ++i)
-      nh += i == 0 || blist[i - 1] != blist[i] - 1;
-    int64_t nh_tot;
-    int64_t oh = block_excl_scan(nh, red, &nh_tot);
-    for (int64_t i = q0; i < q1; ++i)
-      if (i == 0 || blist[i - 1] != blist[i] - 1) hcur[oh++] = blist[i];
-    if (tid == 0) *s_nh = nh_tot;
-  }
-  __threadfence_block();
-  __syncthreads();
-  uint8_t* mywin = win + (size_t)wv * (FC_WIN + 16);
-  uint32_t walked = 0;
-  for (int round = 0; round < FL_ROUNDS; ++round) {
-    const int64_t nh = *s_nh;
-    if (nh <= 0) break;
-    for (int64_t j = wv; j < nh; j += FL_T / 64) {
-      const int64_t h = hcur[j];
-      const int64_t hnext = j + 1 < nh ? (int64_t)hcur[j + 1] : INF;
-      int64_t k = h;
-      while (k >= 1 && k < ntiles && k < hnext) {
-        const int64_t E = ld_agent(&rec_exit[k - 1]);
-        if (E < k * FT_S) break;             // no entry yet
-        const int32_t m0 = __builtin_amdgcn_readfirstlane(rcount[k]);
-        const FcWalk w = fc_walk(buf, n, maxp, k * FT_S, E,
-                                 list + k * FT_LMAX, m0, sx[k], mywin,
-                                 pre + k * FT_LMAX, lane);
-        ++walked;
-        if (lane == 0) {
-          st_agent(&rec_entry[k], E);
-          st_agent(&rec_exit[k], w.exit);
-          st_agent(&rec_meta[k], fc_meta(w));
+  if (threadIdx.x == 0) {
+    int ok = 1;
+    __threadfence();
+    const unsigned long long gen =
+        __hip_atomic_load(&g[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long a =
+        __hip_atomic_fetch_add(&g[0], 1ull, __ATOMIC_ACQ_REL,
+                               __HIP_MEMORY_SCOPE_AGENT) + 1;
+    if (a == gridDim.x) {
+      __hip_atomic_store(&g[0], 0ull, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(&g[1], 1ull, __ATOMIC_RELEASE,
+                             __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      const uint64_t t0 = wall_clock64();
+      while (__hip_atomic_load(&g[1], __ATOMIC_ACQUIRE,
+                               __HIP_MEMORY_SCOPE_AGENT) == gen) {
+        if (__hip_atomic_load(&g[2], __ATOMIC_RELAXED,
+                              __HIP_MEMORY_SCOPE_AGENT)) {
+          ok = 0;
+          break;
         }
-        if (w.term) break;
-        ++k;
-        if (k < ntiles && ld_agent(&rec_entry[k]) == w.exit) break;
+        if (wall_clock64() - t0 > FL_BAR_TICKS) {
+          __hip_atomic_store(&g[2], 1ull, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+          ok = 0;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(8);
       }
     }
     __threadfence();
-    __syncthreads();
-    // heads whose link is still broken (an earlier run moved their exit)
-    const int64_t per = (nh + FL_T - 1) / FL_T;
-    const int64_t q0 = min((int64_t)tid * per, nh);
-    const int64_t q1 = min(q0 + per, nh);
-    int64_t nl = 0;
-    for (int64_t i = q0; i < q1; ++i) {
-      const int64_t h = hcur[i];
-      nl += !m_term(ld_agent(&rec_meta[h - 1])) &&
-            ld_agent(&rec_entry[h]) != ld_agent(&rec_exit[h - 1]);
+    if (__hip_atomic_load(&g[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+      ok = 0;
+    s_ok = ok;
+  }
+  __syncthreads();
+  return s_ok != 0;
+}
+
+// One grid repair round (every thread of every block calls it).  Returns
+// false when no link was broken (the fix-point is reached) or on abort.
+ZK_DEV bool fl_round(const uint8_t* __restrict__ buf, int64_t n,
+                     int64_t ntiles, int64_t maxp,
+                     const int64_t* __restrict__ sx,
+                     const uint16_t* __restrict__ list,
+                     const int32_t* __restrict__ rcount, uint16_t* pre,
+                     int64_t* rec_entry, int64_t* rec_exit, int64_t* rec_meta,
+                     int32_t* blist, unsigned long long* g, int r,
+                     int64_t* red, uint8_t* win, uint64_t* stats) {
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int64_t INF = INT64_MAX;
+  const int64_t nth = (int64_t)gridDim.x * FL_T;
+  const int64_t gt = (int64_t)blockIdx.x * FL_T + tid;
+  // A. the first terminal as the records stand
+  int64_t ft = INF;
+  for (int64_t k = gt; k < ntiles; k += nth)
+    if (m_term(ld_agent(&rec_meta[k]))) { ft = k; break; }
+  for (int d = 32; d >= 1; d >>= 1)
+    ft = min(ft, (int64_t)__shfl_xor(ft, d, 64));
+  if (lane == 0 && ft != INF)
+    atomicMax(&g[3 + 2 * r], (unsigned long long)(ntiles - ft));
+  if (!fl_sync(g)) return false;
+  const unsigned long long mt = __hip_atomic_load(
+      &g[3 + 2 * r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int64_t ftr = mt ? ntiles - (int64_t)mt : ntiles - 1;
+  // B. list the broken links k <= ftr (tile k-1 is not a terminal there)
+  int64_t nb = 0;
+  const int64_t per = (ftr + nth - 1) / nth;
+  const int64_t k0 = 1 + gt * per, k1 = min(k0 + per, ftr + 1);
+  for (int64_t k = k0; k < k1; ++k)
+    nb += ld_agent(&rec_entry[k]) != ld_agent(&rec_exit[k - 1]);
+  int64_t tot;
+  const int64_t o = block_excl_scan(nb, red, &tot);
+  __shared__ unsigned long long s_base;
+  if (tid == 0)
+    s_base = tot ? atomicAdd(&g[4 + 2 * r], (unsigned long long)tot) : 0;
+  __syncthreads();
+  int64_t w = (int64_t)s_base + o;
+  for (int64_t k = k0; k < k1; ++k)
+    if (ld_agent(&rec_entry[k]) != ld_agent(&rec_exit[k - 1]))
+      blist[w++] = (int32_t)k;
+  if (!fl_sync(g)) return false;
+  const int64_t nbr = (int64_t)__hip_atomic_load(
+      &g[4 + 2 * r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (nbr == 0) return false;
+  // C. every listed link re-walked by one wave, from the exit before it
+  uint8_t* mywin = win + (size_t)wv * (FC_WIN + 16);
+  const int64_t nwv = (int64_t)gridDim.x * (FL_T / 64);
+  uint32_t walked = 0;
+  for (int64_t j = (int64_t)blockIdx.x * (FL_T / 64) + wv; j < nbr;
+       j += nwv) {
+    const int64_t k = blist[j];
+    const int64_t E = ld_agent(&rec_exit[k - 1]);
+    if (E < k * FT_S) continue;               // no exact entry yet
+    const int32_t m0 = __builtin_amdgcn_readfirstlane(rcount[k]);
+    const FcWalk fw = fc_walk(buf, n, maxp, k * FT_S, E, list + k * FT_LMAX,
+                              m0, sx[k], mywin, pre + k * FT_LMAX, lane);
+    ++walked;
+    if (lane == 0) {
+      st_agent(&rec_entry[k], E);
+      st_agent(&rec_exit[k], fw.exit);
+      st_agent(&rec_meta[k], fc_meta(fw));
     }
-    int64_t nn;
-    int64_t on = block_excl_scan(nl, red, &nn);
-    for (int64_t i = q0; i < q1; ++i) {
-      const int64_t h = hcur[i];
-      if (!m_term(ld_agent(&rec_meta[h - 1])) &&
-          ld_agent(&rec_entry[h]) != ld_agent(&rec_exit[h - 1]))
-        hnxt[on++] = (int32_t)h;
-    }
-    __threadfence_block();
-    __syncthreads();
-    if (tid == 0) *s_nh = nn;
-    int32_t* tmp = hcur;
-    hcur = hnxt;
-    hnxt = tmp;
-    __syncthreads();
   }
   if (lane == 0 && walked) fc_stat(stats, 2, walked);
+  if (blockIdx.x == 0 && tid == 0) fc_stat(stats, 3, 1);
+  return fl_sync(g);
 }
 
 // fs_check: every link and terminal checked in parallel (one thread per
@@ -811,8 +855,7 @@ __global__ __launch_bounds__(FK_T) void fs_check(
     const int64_t* __restrict__ n_dev, int64_t n_cap,
     const int64_t* __restrict__ rec_entry, const int64_t* __restrict__ rec_exit,
     const int64_t* __restrict__ rec_meta, int64_t* __restrict__ base,
-    int64_t* __restrict__ bsum, uint64_t* __restrict__ mins,
-    uint8_t* __restrict__ bflag) {
+    int64_t* __restrict__ bsum, uint64_t* __restrict__ mins) {
   __shared__ int64_t sm[FK_T / 64 + 1];
   __shared__ int64_t smin[2 * (FK_T / 64)];
   const int64_t n = stream_len(n_dev, n_cap);
@@ -830,9 +873,6 @@ __global__ __launch_bounds__(FK_T) void fs_check(
     cnt = m_cnt(mk);
     if (m_term(mk)) fterm = k;
     else if (nxt && (e < 0 || e != x)) fb = k + 1;
-    // bflag[k + 1]: link k + 1 broken (fs_link's repair lists read it)
-    if (nxt) bflag[k + 1] = fb != INF;
-    if (k == 0) bflag[0] = 0;
   }
   int64_t tot;
   const int64_t ex = block_excl_scan(cnt, sm, &tot);
@@ -868,84 +908,90 @@ __global__ __launch_bounds__(FL_T) void fs_link(
     int64_t* __restrict__ base, int64_t cap, int64_t* __restrict__ result,
     uint64_t* stats, int32_t* __restrict__ blist,
     int64_t* __restrict__ bsum, uint64_t* __restrict__ mins,
-    int64_t* __restrict__ lastk, const uint8_t* __restrict__ bflag) {
+    int64_t* __restrict__ lastk, unsigned long long* __restrict__ g) {
   __shared__ __attribute__((aligned(16)))
       uint8_t win[(FL_T / 64) * (FC_WIN + 16)];      // one per wave
   __shared__ int64_t red[2 * (FL_T / 64) + 2];
-  __shared__ int64_t s_next, s_nh;
+  __shared__ int64_t s_next;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int64_t n = stream_len(n_dev, n_cap);
   const int64_t ntiles = (n + FT_S - 1) / FT_S;
   if (ntiles == 0) {
-    if (tid < 4) result[tid] = 0;
-    if (tid == 0) *lastk = -1;
+    if (blockIdx.x == 0) {
+      if (tid < 4) result[tid] = 0;
+      if (tid == 0) *lastk = -1;
+    }
     return;
   }
   const int64_t INF = INT64_MAX;
-  // fs_check's minima, read by every thread, then cleared for the next
-  // scan of this workspace
+  // fs_check's minima, read by every thread of every block; block 0
+  // clears them for the next scan of this workspace once every block has
+  // read them (on the fast path only block 0 goes on, so at once)
   const uint64_t mb0 = mins[0], mt0 = mins[1];
-  __syncthreads();
-  if (tid == 0) {
+  const int64_t fb0 = mb0 ? ntiles - (int64_t)mb0 : INF;
+  const int64_t ft0 = mt0 ? ntiles - (int64_t)mt0 : INF;
+  const bool fast = fb0 == INF || fb0 > ft0;
+  if (fast) {
+    // no broken link before the first terminal: the row bases are bsum's
+    // block offsets + fs_check's in-block bases
+    if (blockIdx.x != 0) return;
+    __syncthreads();
+    if (tid == 0) {
+      mins[0] = 0;
+      mins[1] = 0;
+    }
+    const int64_t last = ft0 == INF ? ntiles - 1 : ft0;
+    const int64_t nbl = last / FK_T + 1;
+    const int64_t per = (nbl + FL_T - 1) / FL_T;
+    const int64_t b0 = (int64_t)tid * per;
+    const int64_t b1 = min(b0 + per, nbl);
+    int64_t sum = 0;
+    for (int64_t b = b0; b < b1; ++b) sum += bsum[b];
+    int64_t tot;
+    int64_t run = block_excl_scan(sum, red, &tot);
+    const int64_t blast = last / FK_T;
+    for (int64_t b = b0; b < b1; ++b) {
+      const int64_t v = bsum[b];
+      bsum[b] = run;
+      if (b == blast) {
+        // frames up to `last` (tiles after it in its block are dead)
+        const int64_t ml = rec_meta[last];
+        const int64_t total = run + base[last] + m_cnt(ml);
+        *lastk = last;
+        result[0] = total;
+        result[3] = total > cap ? 1 : 0;
+        if (ft0 == INF) {
+          result[1] = n;
+          result[2] = 0;
+        } else {
+          result[1] = rec_exit[ft0];
+          result[2] = m_bad(ml) ? 1 : 0;
+        }
+      }
+      run += v;
+    }
+    return;
+  }
+  // ---- repair: grid rounds to a fix-point ---------------------------------
+  bool grid_ok = fl_sync(g);                // every block has read the minima
+  if (blockIdx.x == 0 && tid == 0) {
     mins[0] = 0;
     mins[1] = 0;
   }
-  {
-    // fast path: fs_check found no broken link before the first terminal;
-    // the row bases are bsum's block offsets + fs_check's in-block bases
-    const uint64_t mb = mb0, mt = mt0;
-    const int64_t fb0 = mb ? ntiles - (int64_t)mb : INF;
-    const int64_t ft0 = mt ? ntiles - (int64_t)mt : INF;
-    if (fb0 == INF || fb0 > ft0) {
-      const int64_t last = ft0 == INF ? ntiles - 1 : ft0;
-      const int64_t nbl = last / FK_T + 1;
-      const int64_t per = (nbl + FL_T - 1) / FL_T;
-      const int64_t b0 = (int64_t)tid * per;
-      const int64_t b1 = min(b0 + per, nbl);
-      int64_t sum = 0;
-      for (int64_t b = b0; b < b1; ++b) sum += bsum[b];
-      int64_t tot;
-      int64_t run = block_excl_scan(sum, red, &tot);
-      const int64_t blast = last / FK_T;
-      for (int64_t b = b0; b < b1; ++b) {
-        const int64_t v = bsum[b];
-        bsum[b] = run;
-        if (b == blast) {
-          // frames up to `last` (tiles after it in its block are dead)
-          const int64_t ml = rec_meta[last];
-          const int64_t total = run + base[last] + m_cnt(ml);
-          *lastk = last;
-          result[0] = total;
-          result[3] = total > cap ? 1 : 0;
-          if (ft0 == INF) {
-            result[1] = n;
-            result[2] = 0;
-          } else {
-            result[1] = rec_exit[ft0];
-            result[2] = m_bad(ml) ? 1 : 0;
-          }
-        }
-        run += v;
-      }
-      return;
-    }
-  }
+  for (int r = 0; r < FL_GROUNDS && grid_ok; ++r)
+    grid_ok = fl_round(buf, n, ntiles, maxp, sx, list, rcount, pre,
+                       rec_entry, rec_exit, rec_meta, blist, g, r, red, win,
+                       stats);
+  if (blockIdx.x != 0) return;
+  // ---- block 0: whatever is left, serially; then the count scan -----------
   int64_t from = 1, ft = INF;
-  bool accel = true, first = true;
   for (;;) {
-    // leftmost terminal, and leftmost broken link at or after `from`
-    int64_t fb = INF, fterm = INF;
-    if (first) {
-      // fs_check's answer (every thread read the same minima)
-      first = false;
-      fb = mb0 ? ntiles - (int64_t)mb0 : INF;
-      fterm = mt0 ? ntiles - (int64_t)mt0 : INF;
-    } else {
-    // links before `from` hold (repaired), so terminals before from - 1
-    // were found in an earlier round: only the rest is scanned again.
+    // leftmost terminal, and leftmost broken link at or after `from`.
     // Loads in batches of FL_U tiles per thread (all issued before any is
     // used: one round trip per batch, not two per tile)
-    for (int64_t k0 = from - 1 + tid; k0 < ntiles; k0 += FL_U * FL_T) {
+    int64_t fb = INF, fterm = INF;
+    for (int64_t k0 = max(from - 1, (int64_t)0) + tid; k0 < ntiles;
+         k0 += FL_U * FL_T) {
       int64_t mk[FL_U], e[FL_U], x[FL_U];
 #pragma unroll
       for (int u = 0; u < FL_U; ++u) {
@@ -966,7 +1012,6 @@ __global__ __launch_bounds__(FL_T) void fs_link(
         }
       }
     }
-    }
     for (int d = 32; d >= 1; d >>= 1) {
       fb = min(fb, (int64_t)__shfl_xor(fb, d, 64));
       fterm = min(fterm, (int64_t)__shfl_xor(fterm, d, 64));
@@ -980,30 +1025,34 @@ __global__ __launch_bounds__(FL_T) void fs_link(
       fterm = min(fterm, red[FL_T / 64 + j]);
     }
     __syncthreads();
+    // terminals before from - 1 were found in an earlier pass of this loop
+    // (links before `from` hold)
     if (fb == INF || fb > fterm) {          // every live link holds
       ft = fterm;
       break;
     }
-    if (accel) {
-      // The first broken link: before the serial repairs, re-walk every
-      // RUN of broken links in parallel (one wave per run) — usually all
-      // of them.  A garbage entry of the tile before typically merges into
-      // the true chain inside the tile, so a repair rarely moves a tile's
-      // exit and the runs are independent.  Best effort only: the serial
-      // loop re-checks every link afterwards and repairs what is left.
-      accel = false;
-      fs_link_parallel(buf, n, ntiles, maxp, sx, list, rcount, pre,
-                       rec_entry, rec_exit, rec_meta, (int32_t*)base, blist,
-                       red, &s_nh, win, stats, bflag);
-      __syncthreads();
-      continue;
-    }
-    // repair: re-walk tiles from fb while their links stay broken
+    // repair: re-walk tiles from fb while their links stay broken; the
+    // tiles a frame covers whole (its exit lies past them) hold no frame
+    // start: they are filled in one step, not walked
     if (wv == 0) {
       int64_t k = fb;
       uint32_t walked = 0;
       for (;;) {
         const int64_t E = ld_agent(&rec_exit[k - 1]);
+        const int64_t kx = E / FT_S;          // the tile the entry lies in
+        if (kx > k) {
+          const int64_t kend = min(kx, ntiles);
+          const FcWalk cov{E, 0, 0, -1, false, false};
+          for (int64_t c = k + lane; c < kend; c += 64) {
+            st_agent(&rec_entry[c], E);
+            st_agent(&rec_exit[c], E);
+            st_agent(&rec_meta[c], fc_meta(cov));
+          }
+          k = kend;
+          if (k >= ntiles) break;
+          if (ld_agent(&rec_entry[k]) == E) break;     // link k holds
+          continue;
+        }
         const int32_t m0 = __builtin_amdgcn_readfirstlane(rcount[k]);
         const FcWalk w = fc_walk(buf, n, maxp, k * FT_S, E,
                                  list + k * FT_LMAX, m0, sx[k], win,
@@ -1027,6 +1076,8 @@ __global__ __launch_bounds__(FL_T) void fs_link(
     __syncthreads();
     from = s_next;
   }
+  // the grid words back to zero for the next scan of this workspace
+  if (tid < FL_GW && tid != 1) g[tid] = 0;
   // exclusive scan of the counts of tiles 0..ft; tiles after ft are dead
   const int64_t last = ft == INF ? ntiles - 1 : ft;
   const int64_t per = (last + 1 + FL_T - 1) / FL_T;
@@ -1116,7 +1167,7 @@ __global__ __launch_bounds__(256) void fs_rows(
 struct FsPlan {
   int64_t tiles;
   size_t off_list, off_pre, off_sx, off_lbw, off_rent, off_rexit, off_rmeta,
-      off_rcnt, off_base, off_blist, off_bsum, off_bflag, total;
+      off_rcnt, off_base, off_blist, off_bsum, total;
 };
 
 static FsPlan fs_plan(int64_t n) {
@@ -1128,8 +1179,9 @@ static FsPlan fs_plan(int64_t n) {
   p.off_list = take((size_t)tiles * FT_LMAX * 2);
   p.off_pre = take((size_t)tiles * FT_LMAX * 2);
   p.off_sx = take((size_t)tiles * 8);
-  // X flags (2 per tile), 4 stats words, fs_check's 2 minima, last tile
-  p.off_lbw = take((size_t)(2 * tiles + 7) * 8);
+  // X flags (2 per tile), 4 stats words, fs_check's 2 minima, last tile,
+  // a pad word, fs_link's grid words
+  p.off_lbw = take((size_t)(2 * tiles + 8 + FL_GW) * 8);
   p.off_rent = take((size_t)tiles * 8);
   p.off_rexit = take((size_t)tiles * 8);
   p.off_rmeta = take((size_t)tiles * 8);
@@ -1137,7 +1189,6 @@ static FsPlan fs_plan(int64_t n) {
   p.off_base = take((size_t)tiles * 8);
   p.off_blist = take((size_t)tiles * 4);
   p.off_bsum = take((size_t)(tiles / FK_T + 1) * 8);
-  p.off_bflag = take((size_t)tiles + 1);
   p.total = o;
   return p;
 }
@@ -1208,10 +1259,11 @@ int64_t zk_frame_scan_workspace(int64_t n) {
 // of it over the same n_cap (fs_rows / fs_link clear what they used), so
 // the memset is skipped.  A stale flag could only cost speed, never
 // correctness (fs_check / fs_link verify every speculated entry).
-int zk_frame_scan4(const uint8_t* buf, const int64_t* n_dev, int64_t n_cap,
+// flags bit 0: no speculated tile entries (tests of the link repair).
+int zk_frame_scan5(const uint8_t* buf, const int64_t* n_dev, int64_t n_cap,
                    int64_t maxp, uint8_t* ws, int64_t ws_bytes, int64_t* foff,
                    int32_t* flen, int64_t cap, int64_t* result, int32_t window,
-                   int32_t clean, hipStream_t st) {
+                   int32_t clean, int32_t flags, hipStream_t st) {
   using namespace zk;
   const int W = fs_window(window);
   if (maxp > FC_MAXP || maxp < 0) return -3;
@@ -1229,12 +1281,14 @@ int zk_frame_scan4(const uint8_t* buf, const int64_t* n_dev, int64_t n_cap,
   int64_t* base = (int64_t*)(ws + p.off_base);
   int32_t* blist = (int32_t*)(ws + p.off_blist);
   int64_t* bsum = (int64_t*)(ws + p.off_bsum);
-  uint8_t* bflag = ws + p.off_bflag;
   uint64_t* mins = lbw + 2 * tiles + 4;
   int64_t* lastk = (int64_t*)(lbw + 2 * tiles + 6);
-  // X flags, the stats and fs_check's minima start at zero
+  unsigned long long* grid = (unsigned long long*)(lbw + 2 * tiles + 8);
+  // X flags, the stats, fs_check's minima and fs_link's grid words start
+  // at zero
   if (!clean &&
-      hipMemsetAsync(lbw, 0, (size_t)(2 * tiles + 6) * 8, st) != hipSuccess)
+      hipMemsetAsync(lbw, 0, (size_t)(2 * tiles + 8 + FL_GW) * 8, st) !=
+          hipSuccess)
     return -4;
   int64_t* dbg = fs_dbg_buf(tiles);
   // ZKMI_FS_TPB: tiles (waves) per block, 1..4 (A/B)
@@ -1248,7 +1302,7 @@ int zk_frame_scan4(const uint8_t* buf, const int64_t* n_dev, int64_t n_cap,
 #define ZK_FS_TILE(WW)                                                       \
   fs_tile<WW><<<tblocks, 64 * tpb, FT_LDS * tpb, st>>>(                      \
       buf, n_dev, n_cap, maxp, list, pre, sx, lbw, rent, rexit, rmeta, rcnt, \
-      tiles, dbg, fs_minb())
+      tiles, dbg, fs_minb(), flags & 1)
   switch (W) {
     case 256: ZK_FS_TILE(256); break;
     case 512: ZK_FS_TILE(512); break;
@@ -1258,18 +1312,26 @@ int zk_frame_scan4(const uint8_t* buf, const int64_t* n_dev, int64_t n_cap,
 #undef ZK_FS_TILE
   ZK_LAUNCH_CHECK();
   fs_check<<<(unsigned)((tiles + FK_T - 1) / FK_T), FK_T, 0, st>>>(
-      n_dev, n_cap, rent, rexit, rmeta, base, bsum, mins, bflag);
+      n_dev, n_cap, rent, rexit, rmeta, base, bsum, mins);
   ZK_LAUNCH_CHECK();
-  fs_link<<<1, FL_T, 0, st>>>(buf, n_dev, n_cap, maxp, sx, list, rcnt, pre,
-                              rent, rexit, rmeta, base, cap, result,
-                              lbw + 2 * tiles, blist, bsum, mins, lastk,
-                              bflag);
+  fs_link<<<FL_B, FL_T, 0, st>>>(buf, n_dev, n_cap, maxp, sx, list, rcnt,
+                                 pre, rent, rexit, rmeta, base, cap, result,
+                                 lbw + 2 * tiles, blist, bsum, mins, lastk,
+                                 grid);
   ZK_LAUNCH_CHECK();
   fs_rows<<<(unsigned)((tiles + 3) / 4), 256, 0, st>>>(
       buf, n_dev, n_cap, list, pre, rmeta, rexit, base, bsum, lastk, foff,
       flen, cap, lbw);
   ZK_LAUNCH_CHECK();
   return 0;
+}
+
+int zk_frame_scan4(const uint8_t* buf, const int64_t* n_dev, int64_t n_cap,
+                   int64_t maxp, uint8_t* ws, int64_t ws_bytes, int64_t* foff,
+                   int32_t* flen, int64_t cap, int64_t* result, int32_t window,
+                   int32_t clean, hipStream_t st) {
+  return zk_frame_scan5(buf, n_dev, n_cap, maxp, ws, ws_bytes, foff, flen,
+                        cap, result, window, clean, 0, st);
 }
 
 int zk_frame_scan3(const uint8_t* buf, const int64_t* n_dev, int64_t n_cap,

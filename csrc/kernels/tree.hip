@@ -64,6 +64,7 @@ struct ZkTree {
   int32_t* dirty;              // [cap] parent-on-dirty-list flag
   int64_t* dirty_list;         // [cap]
   int64_t* node_pw;            // [cap] path word: offset << 24 | length
+  int32_t* node_path_cap;      // [cap] bytes of the node's path storage
   // watch table (null wt_key: the tree keeps no watches), see wt_* below
   int64_t* wt_key;             // [wt_hmask + 1] path hash | 1, 0 = empty
   unsigned long long* wt_mask; // [2 * (wt_hmask + 1)] data / child masks
@@ -589,19 +590,25 @@ __global__ __launch_bounds__(TR_T) void tree_serve_k(
     const bool fresh = create && v < 0;
     const int64_t nv = block_ticket(&t.counters[TC_NODES], fresh);
     if (fresh && nv < s.cap) v = nv;
-    // storage: reuse the recycled node's when it fits
-    const bool new_path = v >= 0 && (fresh || npl > t.node_path_len[v]);
+    // storage: reuse the recycled node's when it fits (path storage comes
+    // in 16-byte multiples and keeps its capacity, so nodes recycled across
+    // paths of a few lengths stop allocating: the arena is bounded by the
+    // node count, not by the number of creates)
+    const bool new_path = v >= 0 && (fresh || npl > t.node_path_cap[v]);
     const bool new_slot = v >= 0 && (fresh || cap > s.slot_cap[v]);
+    const int32_t pcap = (npl + 15) & ~15;
     const int64_t po = wave_bytes(&t.counters[TC_PATH_TOP],
-                                  new_path ? npl : 0);
+                                  new_path ? pcap : 0);
     const int64_t sb = new_slot ? slot_bytes(cap) : 0;
     const int64_t so = wave_bytes(&t.counters[TC_SLAB_TOP], sb);
     if (new_path) {
-      if (po + npl <= t.path_cap) {
+      if (po + pcap <= t.path_cap) {
         t.node_path_off[v] = po;
         t.node_path_len[v] = npl;
+        t.node_path_cap[v] = pcap;
       } else {
         t.node_path_len[v] = 0;                     // storage-less free node
+        t.node_path_cap[v] = 0;
       }
     }
     if (new_slot) {
@@ -612,7 +619,7 @@ __global__ __launch_bounds__(TR_T) void tree_serve_k(
         s.slot_cap[v] = -1;
       }
     }
-    if (v >= 0 && ((new_path && po + npl > t.path_cap) ||
+    if (v >= 0 && ((new_path && po + pcap > t.path_cap) ||
                    (new_slot && so + sb > t.slab_cap))) {
       L.err = ERR_SYSTEM;                           // arena full
     }
@@ -783,27 +790,39 @@ __global__ __launch_bounds__(TR_T) void tree_serve_k(
 }
 
 // ---- in-batch ordering (tree_order_*) ---------------------------------------
-// Requests on one path are ordered when a request of the batch writes the
-// path: rank[i] = number of earlier requests of the batch on i's path (0 for
-// paths only read).  A scratch hash table groups the batch's requests by
+// ZooKeeper applies a session's pipelined requests in order.  Two requests
+// of a batch conflict when they touch the same path and one writes it, or
+// when one creates / deletes a CHILD of the path the other operates on (the
+// child write changes the parent's cversion / numChildren / pzxid and needs
+// the parent to exist; a parent delete needs it gone):
+//   * every request with a path joins its own path's group as an A member;
+//   * a CREATE / DELETE also joins its parent's group as a C member (a
+//     SEQUENTIAL create only that one: its own name is fresh).
+// Edges inside a group (the later request runs in a later pass): A-A when
+// the group has an A writer, A-C and C-A always, C-C never (children of one
+// parent commute).  rank[i] = the longest chain of edges ending at i,
+// computed by relaxation (`passes` + 1 rounds; a rank >= passes is refused
+// with SYSTEMERROR, as before).  A scratch hash table groups the batch by
 // path hash (a 64-bit collision merges two groups: extra ordering, never
-// less); write groups of more than one request get a member list (offsets
-// from a block scan of the group sizes: no shared counter), and each member
-// counts the members before it.  No kernel here puts more than one atomic
-// per block on a shared word (a single word sustains ~88 returning atomics
-// per us, MI355X_MICROARCH.md).
-constexpr int64_t ORD_MAX_GROUP = 1 << 16;   // larger write groups: refused
+// less); only ordered groups get member lists (offsets from a block scan of
+// the group sizes: no shared counter).  No kernel here puts more than one
+// atomic per block on a shared word, except the per-group counters (a
+// single word sustains ~88 returning atomics per us, MI355X_MICROARCH.md).
+constexpr int64_t ORD_MAX_GROUP = 1 << 16;   // larger ordered groups: refused
+constexpr int ORD_F = 21;                     // bits per packed group count
+constexpr int64_t ORD_FM = (1ll << ORD_F) - 1;
 
 struct OrderWs {
   int64_t* ctr;      // [4] -, max rank, scratch top, -
   int64_t* key;      // [h] path hash | 1
-  int64_t* cw;       // [h] requests (low 32 bits) | writers (high 32)
+  int64_t* cnt;      // [h] A | A writers << 21 | C << 42
   int32_t* fill;     // [h] member-list fill
-  int32_t* lastw;    // [h] 1 + index of the group's last writer
+  int32_t* lastw;    // [h] 1 + index of the group's last writer (A or C)
   int32_t* base;     // [h] member-list offset within its block of entries
   int64_t* bsum;     // [h / TR_T] block totals, then exclusive offsets
-  int64_t* eidx;     // [ncap] request -> entry (-1: not ordered)
-  int32_t* members;  // [ncap]
+  int64_t* eidx;     // [2 ncap] request -> own (A) entry, parent (C) entry
+  int32_t* members;  // [2 ncap] request << 1 | (1 = C member)
+  int32_t* rnk;      // [ncap] relaxed ranks
   int64_t mask;      // h - 1
 };
 
@@ -817,9 +836,26 @@ ZK_DEV bool ord_writes(int32_t op) {
   return op == OP_CREATE || op == OP_DELETE || op == OP_SET_DATA;
 }
 
-// a write group of more than one request
-ZK_DEV bool ord_grouped(int64_t cw) {
-  return (cw >> 32) != 0 && (int32_t)cw > 1;
+ZK_DEV int64_t ord_na(int64_t c) { return c & ORD_FM; }
+ZK_DEV int64_t ord_naw(int64_t c) { return (c >> ORD_F) & ORD_FM; }
+ZK_DEV int64_t ord_nc(int64_t c) { return (c >> (2 * ORD_F)) & ORD_FM; }
+ZK_DEV int64_t ord_size(int64_t c) { return ord_na(c) + ord_nc(c); }
+
+// a group with at least one edge
+ZK_DEV bool ord_grouped(int64_t c) {
+  return (ord_naw(c) >= 1 && ord_na(c) >= 2) ||
+         (ord_na(c) >= 1 && ord_nc(c) >= 1);
+}
+
+ZK_DEV int64_t ord_entry(const OrderWs& w, int64_t key) {
+  int64_t sl = key & w.mask;
+  for (int64_t probe = 0; probe <= w.mask; ++probe) {
+    const int64_t k = (int64_t)atomicCAS((unsigned long long*)&w.key[sl],
+                                         0ull, (unsigned long long)key);
+    if (k == 0 || k == key) return sl;
+    sl = (sl + 1) & w.mask;
+  }
+  return -1;
 }
 
 __global__ __launch_bounds__(TR_T) void ord_insert_k(
@@ -827,36 +863,44 @@ __global__ __launch_bounds__(TR_T) void ord_insert_k(
     const int64_t* __restrict__ n_dev, int64_t ncap, OrderWs w) {
   const int64_t i = (int64_t)blockIdx.x * TR_T + threadIdx.x;
   if (i >= ncap) return;
-  int64_t e = -1;
-  // SEQUENTIAL creates name a fresh node each: they conflict with nothing
-  // on the requested prefix
-  if (i < *n_dev && q.status[i] == ST_OK && ord_has_path(q.opcode[i]) &&
-      !(q.opcode[i] == OP_CREATE && (q.arg[i] & CF_SEQUENTIAL))) {
+  int64_t ea = -1, ec = -1;
+  if (i < *n_dev && q.status[i] == ST_OK && ord_has_path(q.opcode[i])) {
     const int32_t op = q.opcode[i];
-    const int64_t key =
-        (int64_t)(path_hash(rx + q.path_off[i], q.path_len[i]) | 1ull);
-    int64_t sl = key & w.mask;
-    for (int64_t probe = 0; probe <= w.mask; ++probe) {
-      const int64_t k = (int64_t)atomicCAS((unsigned long long*)&w.key[sl],
-                                           0ull, (unsigned long long)key);
-      if (k == 0 || k == key) { e = sl; break; }
-      sl = (sl + 1) & w.mask;
+    const uint8_t* p = rx + q.path_off[i];
+    const int32_t pl = q.path_len[i];
+    const bool wr = ord_writes(op);
+    const bool seq = op == OP_CREATE && (q.arg[i] & CF_SEQUENTIAL);
+    if (!seq) {
+      ea = ord_entry(w, (int64_t)(path_hash(p, pl) | 1ull));
+      if (ea >= 0) {
+        atomicAdd((unsigned long long*)&w.cnt[ea],
+                  1ull + (wr ? 1ull << ORD_F : 0ull));
+        if (wr) atomicMax(&w.lastw[ea], (int32_t)i + 1);
+      }
     }
-    if (e >= 0) {
-      const bool wr = ord_writes(op);
-      atomicAdd((unsigned long long*)&w.cw[e], 1ull + (wr ? 1ull << 32 : 0));
-      if (wr) atomicMax(&w.lastw[e], (int32_t)i + 1);
+    if (op == OP_CREATE || op == OP_DELETE) {
+      int32_t cut = pl - 1;
+      while (cut > 0 && p[cut] != '/') --cut;
+      if (cut > 0) {                   // the root's children: no group
+        ec = ord_entry(w, (int64_t)(path_hash(p, cut) | 1ull));
+        if (ec >= 0) {
+          atomicAdd((unsigned long long*)&w.cnt[ec], 1ull << (2 * ORD_F));
+          atomicMax(&w.lastw[ec], (int32_t)i + 1);
+        }
+      }
     }
   }
-  w.eidx[i] = e;
+  w.eidx[2 * i] = ea;
+  w.eidx[2 * i + 1] = ec;
 }
 
-// member-list offsets: a block scan of the group sizes per TR_T entries
+// member-list offsets: a block scan of the ordered groups' sizes per TR_T
+// entries
 __global__ __launch_bounds__(TR_T) void ord_base_k(OrderWs w) {
   __shared__ int64_t sm[TR_T / 64 + 1];
   const int64_t e = (int64_t)blockIdx.x * TR_T + threadIdx.x;  // h % TR_T == 0
-  const int64_t cw = w.cw[e];
-  const int64_t c = ord_grouped(cw) ? (int64_t)(int32_t)cw : 0;
+  const int64_t cw = w.cnt[e];
+  const int64_t c = ord_grouped(cw) ? ord_size(cw) : 0;
   int64_t tot;
   const int64_t x = block_excl_scan(c, sm, &tot);
   if (c) w.base[e] = (int32_t)x;
@@ -889,31 +933,68 @@ ZK_DEV int32_t* ord_list(const OrderWs& w, int64_t e) {
 __global__ __launch_bounds__(TR_T) void ord_fill_k(int64_t ncap, OrderWs w) {
   const int64_t i = (int64_t)blockIdx.x * TR_T + threadIdx.x;
   if (i >= ncap) return;
-  const int64_t e = w.eidx[i];
-  if (e < 0 || !ord_grouped(w.cw[e])) return;
-  const int32_t pos = atomicAdd(&w.fill[e], 1);
-  ord_list(w, e)[pos] = (int32_t)i;
+  w.rnk[i] = 0;
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int64_t e = w.eidx[2 * i + c];
+    if (e < 0 || !ord_grouped(w.cnt[e])) continue;
+    const int32_t pos = atomicAdd(&w.fill[e], 1);
+    ord_list(w, e)[pos] = ((int32_t)i << 1) | c;
+  }
+}
+
+// One relaxation round: rank[i] = 1 + the largest rank of an earlier
+// request it has an edge to (in place: a rank never exceeds its chain).
+__global__ __launch_bounds__(TR_T) void ord_relax_k(int64_t ncap, OrderWs w) {
+  const int64_t i = (int64_t)blockIdx.x * TR_T + threadIdx.x;
+  if (i >= ncap) return;
+  int32_t r = 0;
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int64_t e = w.eidx[2 * i + c];
+    if (e < 0) continue;
+    const int64_t cw = w.cnt[e];
+    if (!ord_grouped(cw)) continue;
+    const int64_t sz = ord_size(cw);
+    if (sz > ORD_MAX_GROUP) { r = ORD_RANK; break; }   // refused wholesale
+    const bool aw = ord_naw(cw) >= 1;
+    const int32_t* m = ord_list(w, e);
+    // earlier A members with an edge to i form a chain among themselves
+    // (A-A edges need an A writer, and then every A pair has one), earlier
+    // C members do not: their count + 1 is a lower bound of the rank that
+    // makes a one-path group exact in the first round
+    int32_t na = 0, anyc = 0;
+    for (int64_t k = 0; k < sz; ++k) {
+      const int32_t x = m[k];
+      const int32_t j = x >> 1;
+      if (j >= (int32_t)i) continue;
+      const bool jc = x & 1;
+      const bool edge = c == 0 ? (jc || aw) : !jc;
+      if (!edge) continue;
+      r = max(r, w.rnk[j] + 1);
+      if (jc) anyc = 1;
+      else ++na;
+    }
+    r = max(r, (c == 0 && aw ? na : min(na, 1)) + anyc);
+  }
+  w.rnk[i] = min(r, (int32_t)ORD_RANK);
 }
 
 __global__ __launch_bounds__(TR_T) void ord_rank_k(int64_t ncap, OrderWs w,
                                                    uint8_t* __restrict__ rank) {
   __shared__ int32_t smx[TR_T / 64];
   const int64_t i = (int64_t)blockIdx.x * TR_T + threadIdx.x;
-  const int64_t e = i < ncap ? w.eidx[i] : -1;
-  const int64_t cw = e >= 0 ? w.cw[e] : 0;
   int32_t r = 0;
   bool later_write = false;
-  if (ord_grouped(cw)) {
-    const int32_t c = (int32_t)cw;
-    later_write = w.lastw[e] > (int32_t)i + 1;
-    if (c > ORD_MAX_GROUP) {
-      r = ORD_RANK;                               // refused wholesale
-    } else {
-      const int32_t* m = ord_list(w, e);
-      for (int32_t k = 0; k < c && r < ORD_RANK; ++k) r += m[k] < (int32_t)i;
-    }
+  if (i < ncap) {
+    r = w.rnk[i];
+    // a read of the path whose own group is written later in the batch (by
+    // a writer of the path or a child create / delete) snapshots its reply
+    const int64_t e = w.eidx[2 * i];
+    later_write = e >= 0 && ord_grouped(w.cnt[e]) &&
+                  w.lastw[e] > (int32_t)i + 1;
+    rank[i] = (uint8_t)(r | (later_write ? ORD_SNAP : 0));
   }
-  if (i < ncap) rank[i] = (uint8_t)(r | (later_write ? ORD_SNAP : 0));
   // the batch's largest rank: one atomic per block
   int32_t mx = r;
 #pragma unroll
@@ -1263,7 +1344,7 @@ static int64_t order_layout(int64_t ncap, uint8_t* ws, zk::OrderWs* w,
     w->key = (int64_t*)(ws + o);
   }
   o += h * 8;
-  if (w != nullptr) w->cw = (int64_t*)(ws + o);
+  if (w != nullptr) w->cnt = (int64_t*)(ws + o);
   o += h * 8;
   if (w != nullptr) w->fill = (int32_t*)(ws + o);
   o += h * 4;
@@ -1275,8 +1356,10 @@ static int64_t order_layout(int64_t ncap, uint8_t* ws, zk::OrderWs* w,
   if (w != nullptr) w->bsum = (int64_t*)(ws + o);
   o += (h / zk::TR_T) * 8;
   if (w != nullptr) w->eidx = (int64_t*)(ws + o);
-  o += ncap * 8;
+  o += 2 * ncap * 8;
   if (w != nullptr) w->members = (int32_t*)(ws + o);
+  o += 2 * ncap * 4;
+  if (w != nullptr) w->rnk = (int32_t*)(ws + o);
   o += ncap * 4;
   if (rank != nullptr) *rank = ws + o;
   o += ncap;
@@ -1306,7 +1389,7 @@ int zk_tree_serve_ordered(const ZkTree* t, const uint8_t* rx, const ZkReqOut* q,
                           int32_t passes, int64_t snap_base, int64_t snap_cap,
                           int32_t wslot, int64_t* fired, hipStream_t st) {
   if (ncap <= 0) return 0;
-  if (ncap >= (int64_t)1 << 31) return -1;
+  if (ncap > zk::ORD_FM) return -1;          // packed group counts
   if ((r_sizes == nullptr) != (r_bsum == nullptr)) return -1;
   if (passes < 1 || passes > zk::ORD_RANK) return -1;
   if (snap_base < 0 || snap_cap < 0 || (snap_base & 15)) return -1;
@@ -1327,6 +1410,12 @@ int zk_tree_serve_ordered(const ZkTree* t, const uint8_t* rx, const ZkReqOut* q,
   ZK_LAUNCH_CHECK();
   zk::ord_fill_k<<<nb, zk::TR_T, 0, st>>>(ncap, w);
   ZK_LAUNCH_CHECK();
+  // ranks of chains up to `passes` long are exact after passes + 1 rounds
+  // (a longer chain ends at rank >= passes: refused either way)
+  for (int32_t r = 0; r <= passes; ++r) {
+    zk::ord_relax_k<<<nb, zk::TR_T, 0, st>>>(ncap, w);
+    ZK_LAUNCH_CHECK();
+  }
   zk::ord_rank_k<<<nb, zk::TR_T, 0, st>>>(ncap, w, rank);
   ZK_LAUNCH_CHECK();
   for (int32_t pass = 0; pass < passes; ++pass) {

@@ -39,6 +39,7 @@ struct ZkTree {
   int32_t* dirty;
   int64_t* dirty_list;
   int64_t* node_pw;
+  int32_t* node_path_cap;
   int64_t* wt_key;
   unsigned long long* wt_mask;
   int64_t wt_hmask;
@@ -74,9 +75,9 @@ int zk_encode_responses2(const ZkRespBatch*, const ZkNodeStore*,
                          int64_t*, int64_t*, uint8_t*, int64_t, int32_t*,
                          int32_t, int32_t, hipStream_t);
 int64_t zk_frame_scan_workspace(int64_t n);
-int zk_frame_scan4(const uint8_t*, const int64_t*, int64_t, int64_t,
+int zk_frame_scan5(const uint8_t*, const int64_t*, int64_t, int64_t,
                    uint8_t*, int64_t, int64_t*, int32_t*, int64_t, int64_t*,
-                   int32_t, int32_t, hipStream_t);
+                   int32_t, int32_t, int32_t, hipStream_t);
 int zk_frame_scan_stats(const uint8_t*, int64_t, int32_t, uint32_t*,
                         hipStream_t);
 int zk_frame_scan_dbg(int64_t* host, int64_t tiles);
@@ -251,10 +252,11 @@ ZkNodeStore node_store(const std::vector<Tensor>& v, size_t at,
 //  dirty, dirty_list, node_pw]; sizes give mask, caps
 // [ht, node_path_off, node_path_len, node_parent, path_arena, counters,
 //  slab, slot_off, data_len, slot_cap, free_list, cver, nchild, pzxid,
-//  dirty, dirty_list, node_pw] + optionally [wt_key, wt_mask] (watches)
+//  dirty, dirty_list, node_pw, node_path_cap] + optionally [wt_key,
+//  wt_mask] (watches)
 ZkTree tree(const std::vector<Tensor>& v) {
-  TORCH_CHECK(v.size() == 17 || v.size() == 19,
-              "zkmi: tree needs 17 tensors (19 with a watch table), got ",
+  TORCH_CHECK(v.size() == 18 || v.size() == 20,
+              "zkmi: tree needs 18 tensors (20 with a watch table), got ",
               v.size());
   const Tensor* r = &v[0];
   ZkTree t;
@@ -280,16 +282,17 @@ ZkTree tree(const std::vector<Tensor>& v) {
   t.dirty = P<int32_t>(v[14], I32, cap, "tree.dirty", r);
   t.dirty_list = P<int64_t>(v[15], I64, cap, "tree.dirty_list", r);
   t.node_pw = P<int64_t>(v[16], I64, cap, "tree.node_pw", r);
+  t.node_path_cap = P<int32_t>(v[17], I32, cap, "tree.node_path_cap", r);
   t.wt_key = nullptr;
   t.wt_mask = nullptr;
   t.wt_hmask = 0;
-  if (v.size() == 19) {
-    const int64_t h = v[17].numel();
+  if (v.size() == 20) {
+    const int64_t h = v[18].numel();
     TORCH_CHECK(h > 0 && (h & (h - 1)) == 0,
                 "zkmi: tree.wt_key must hold a power of two of entries");
-    t.wt_key = P<int64_t>(v[17], I64, h, "tree.wt_key", r);
+    t.wt_key = P<int64_t>(v[18], I64, h, "tree.wt_key", r);
     t.wt_mask = reinterpret_cast<unsigned long long*>(
-        P<int64_t>(v[18], I64, 2 * h, "tree.wt_mask", r));
+        P<int64_t>(v[19], I64, 2 * h, "tree.wt_mask", r));
     t.wt_hmask = h - 1;
   }
   return t;
@@ -491,21 +494,21 @@ int64_t frame_scan_workspace(int64_t n) { return zk_frame_scan_workspace(n); }
 void frame_scan(const Tensor& buf, const c10::optional<Tensor>& n_dev,
                 int64_t n_cap, int64_t max_packet, const Tensor& ws,
                 const Tensor& foff, const Tensor& flen, const Tensor& result,
-                int64_t window, bool clean) {
+                int64_t window, bool clean, int64_t flags) {
   TORCH_CHECK(n_cap >= 0 && n_cap <= buf.numel(),
               "zkmi: frame_scan length ", n_cap, " past the buffer (",
               buf.numel(), " bytes)");
   TORCH_CHECK(ws.numel() >= zk_frame_scan_workspace(n_cap),
               "zkmi: frame_scan workspace too small");
   const int64_t cap = foff.numel();
-  hip_ok(zk_frame_scan4(
+  hip_ok(zk_frame_scan5(
              P<uint8_t>(buf, U8, 1, "buf"),
              Popt<int64_t>(n_dev, I64, 1, "n", &buf), n_cap, max_packet,
              P<uint8_t>(ws, U8, 1, "ws", &buf), ws.numel(),
              P<int64_t>(foff, I64, 1, "frame_off", &buf),
              P<int32_t>(flen, I32, cap, "frame_len", &buf), cap,
              P<int64_t>(result, I64, 4, "result", &buf), (int32_t)window,
-             clean ? 1 : 0, cur_stream()),
+             clean ? 1 : 0, (int32_t)flags, cur_stream()),
          "frame_scan");
 }
 
@@ -1021,7 +1024,7 @@ TORCH_LIBRARY(zkmi, m) {
   m.def("frame_scan_workspace(int n) -> int", &frame_scan_workspace);
   m.def("frame_scan(Tensor buf, Tensor? n, int n_cap, int max_packet, "
         "Tensor(a!) ws, Tensor(b!) frame_off, Tensor(c!) frame_len, "
-        "Tensor(d!) result, int window, bool clean=False) -> ()",
+        "Tensor(d!) result, int window, bool clean=False, int flags=0) -> ()",
         &frame_scan);
   m.def("frame_scan_stats(Tensor ws, int n_cap, int window) -> int[]",
         &frame_scan_stats);

@@ -242,3 +242,95 @@ def test_chain_pipeline_steps():
             hw = int(tree.counters[_lib.TC_NODES].item())
     assert int(tree.counters[_lib.TC_NODES].item()) == hw
     assert pipe.drv.server.order_stats()[0] == 3
+
+
+def _key_tree(rep):
+    """_key plus the parent-visible Stat fields (children count and
+    cversion): what a batch mixing a node's and its children's writes must
+    get right."""
+    k = list(_key(rep))
+    st = rep.get('stat') if rep['err'] == 'OK' else None
+    if st is not None:
+        k += [st.numChildren, st.cversion]
+    return tuple(k)
+
+
+@pytest.mark.gpu
+def test_ordered_parent_child_batch_matches_sequential_server():
+    """createWithEmptyParents in ONE batch (lib/client.js:412-481,
+    test/basic.test.js:317-611): depth-3 creates, the parents' Stat read
+    between the children's writes, a child created before its parent, a
+    parent delete refused while it has a child — every reply as the
+    sequential server gives it (a create and its parent's create conflict;
+    a parent's Stat read conflicts with its children's writes)."""
+    from zkmi.bench.synthetic import GpuTree, GpuServer
+    dev = torch.device('cuda', 0)
+    tree = GpuTree(1000, 16, fanout=100, device=dev, spare=0.5,
+                   scratch=1 << 20)
+    srv = GpuServer(tree, 256, 1 << 18)
+    db = _mirror(tree, [])
+    A = jute.DEFAULT_ACL
+    d = '/bench/d000000'
+    x, y, z = d + '/x', d + '/x/y', d + '/x/y/z'
+
+    def c(p, data=b'', flags=()):
+        return {'opcode': 'CREATE', 'path': p, 'data': data, 'acl': A,
+                'flags': list(flags)}
+
+    def ex(p):
+        return {'opcode': 'EXISTS', 'path': p, 'watch': False}
+
+    def get(p):
+        return {'opcode': 'GET_DATA', 'path': p, 'watch': False}
+
+    def rm(p, v=-1):
+        return {'opcode': 'DELETE', 'path': p, 'version': v}
+
+    batches = [
+        # child before its parent: NO_NODE, then the chain in order
+        [c(y, b'early'), ex(x), c(x, b'null'), c(y, b'null'), c(z, b'leaf'),
+         ex(x), get(y), ex(d + '/x/y/z'), c(z, b'again'), rm(y),
+         c(x + '/s-', b'', ['SEQUENTIAL']), ex(x)],
+        # tear down bottom-up with the parents' Stat read in between
+        [ex(y), rm(z), ex(y), rm(y), ex(x), get(x), rm(x + '/s-0000000001'),
+         rm(x), ex(x), get(y)],
+        # the same path rebuilt and re-deleted in one batch
+        [c(x, b'1'), c(y, b'2'), rm(y), ex(x), rm(x), c(x, b'3'), ex(x),
+         get(x)],
+    ]
+    xid = 0
+    for bno, pk in enumerate(batches):
+        for p in pk:
+            p['xid'] = xid
+            xid += 1
+        want = [_key_tree(db.handle(dict(p), None)) for p in pk]
+        got = [_key_tree(r) for r in _serve(srv, pk, dev, ordered=True,
+                                            passes=16)]
+        assert srv.order_stats()[0] < 16
+        assert got == want, 'batch %d: first mismatch at %d: %r vs %r' % (
+            bno, *next((i, a, b) for i, (a, b) in enumerate(zip(got, want))
+                       if a != b))
+
+
+@pytest.mark.gpu
+def test_nest_pipeline_steps():
+    """bench --workload nest: depth-3 creates, the parent's EXISTS and the
+    bottom-up deletes of every tree in one batch, checked on the device."""
+    from zkmi.bench.synthetic import GpuTree, NestPipeline
+    from zkmi.ops import _lib
+    dev = torch.device('cuda', 0)
+    tree = GpuTree(20000, 37, fanout=100, device=dev, spare=1.0,
+                   scratch=1 << 22)
+    pipe = NestPipeline(tree, 7 * 1024, ndirs=64)
+    hw = top = None
+    for s in range(12):
+        ok = pipe.step()
+        assert int(ok.item()) == pipe.n, pipe.diagnose()
+        if s == 1:
+            hw = int(tree.counters[_lib.TC_NODES].item())
+            top = int(tree.counters[_lib.TC_PATH_TOP].item())
+    assert int(tree.counters[_lib.TC_NODES].item()) == hw
+    # recycled nodes reuse their path storage across the three path
+    # lengths: the path arena does not grow step after step
+    assert int(tree.counters[_lib.TC_PATH_TOP].item()) == top
+    assert pipe.drv.server.order_stats()[0] == 5

@@ -133,8 +133,9 @@ class GpuTree(object):
         poff = np.zeros(nst, np.int64)
         np.cumsum(plen[:-1], out=poff[1:])
         arena = b''.join(enc)
-        # every spare node may need a fresh path (up to 64 bytes each)
-        self.path_cap = len(arena) + (cap - nst) * 64 + (1 << 16)
+        # every spare node may need a fresh path (up to 64 bytes each, in
+        # 16-byte multiples)
+        self.path_cap = len(arena) + (cap - nst) * 80 + (1 << 16)
         self.path_arena = torch.zeros(self.path_cap, dtype=U8, device=dev)
         self.path_arena[:len(arena)] = torch.frombuffer(
             bytearray(arena), dtype=U8).to(dev)
@@ -142,6 +143,9 @@ class GpuTree(object):
         self.node_path_len = torch.zeros(cap, dtype=I32, device=dev)
         self.node_path_off[:nst] = torch.from_numpy(poff).to(dev)
         self.node_path_len[:nst] = torch.from_numpy(plen).to(dev)
+        # bytes of each node's path storage (the static paths are packed)
+        self.node_path_cap = torch.zeros(cap, dtype=I32, device=dev)
+        self.node_path_cap[:nst] = self.node_path_len[:nst]
         # path word (offset << 24 | length) the hash lookups verify against
         self.node_pw = torch.zeros(cap, dtype=I64, device=dev)
         self.node_pw[:nst] = torch.from_numpy(
@@ -202,7 +206,7 @@ class GpuTree(object):
                          self.slab, self.slot_off, self.data_len,
                          self.slot_cap, self.free_list, self.cver,
                          self.nchild, self.pzxid, self.dirty,
-                         self.dirty_list, self.node_pw]
+                         self.dirty_list, self.node_pw, self.node_path_cap]
         # watch table (watch_cap > 0): path-keyed one-shot watches of up to
         # 64 watcher slots (csrc/kernels/tree.hip wt_*); every serve of a
         # tree with one fires the watches its writes hit
@@ -925,6 +929,96 @@ class ChainPipeline(object):
               (~(self.is_set | self.is_get) | ver1) &
               (~self.is_get | ((rep.stat32[3, :n] == self.data_bytes) &
                                (rep.pay_len[:n] == self.data_bytes))))
+        if acc is None:
+            return ok.sum()
+        acc[:1] += ok.sum()
+        return acc
+
+    def diagnose(self):
+        rb, rep = self.last
+        n = rb.n
+        bad = rep.err[:n] != 0
+        e, c = torch.unique(rep.err[:n][bad], return_counts=True)
+        return {'wrong_err': dict(zip(e.cpu().tolist(), c.cpu().tolist())),
+                'order_stats': self.drv.server.order_stats()}
+
+
+class NestPipeline(object):
+    """createWithEmptyParents in one batch (lib/client.js:412-481): every
+    step sends, for each of ``m`` trees ``/nest/dDDDD/pKKKKKKKKK``, the
+    depth-3 chain CREATE p -> CREATE p/c -> CREATE p/c/g -> EXISTS p ->
+    DELETE p/c/g -> DELETE p/c -> DELETE p (7 requests) back to back in ONE
+    batch, as one session pipelining them would.  The creates depend on
+    their parents, the EXISTS on its children's writes and the deletes on
+    their children being gone: the ordered GPU server must honour
+    parent / child order (passes by the longest conflict chain, 6 here).
+    Every reply is checked on the device: all OK, and the parent's EXISTS
+    sees exactly one child (numChildren 1, cversion 1).  The tree is left
+    as it was (every step deletes what it created)."""
+
+    PER = 7
+
+    def __init__(self, tree, batch, ndirs=1024, seed=0):
+        m = max(batch // self.PER, 1)
+        self.m = m
+        self.n = n = self.PER * m
+        dev = tree.device
+        self.tree = tree
+        need = 2 * m * (80 + 16)
+        if tree.scratch is None or tree.scratch.numel() < need:
+            raise ValueError('NestPipeline needs GpuTree(scratch >= %d)'
+                             % need)
+        base = ['/nest/d%05d/p%09d' % (k % ndirs, k) for k in range(m)]
+        paths = [b + sfx for b in base for sfx in ('', '/c', '/c/g')]
+        maxp = max(len(p) for p in paths)
+        self.drv = _Driver(tree, n, maxp, 16, seed)
+        self.drv.passes = 8
+        self.path_arena, poff, plen = _arena(paths, dev)
+        poff = poff.view(m, 3)
+        plen = plen.view(m, 3)
+        self.data_arena = torch.full((16,), 0x6e, dtype=U8, device=dev)
+        self.acl_arena, self.acl_off, self.acl_len = _acl_table(MIX_ACLS[:1],
+                                                                dev)
+        ops = consts.OP_CODES
+        col = lambda *c: torch.stack(c, 1).reshape(-1)     # noqa: E731
+        full = lambda v, dt: torch.full((m,), v, dtype=dt, device=dev)  # noqa
+        self.opcode = col(*(full(ops[o], I32) for o in (
+            'CREATE', 'CREATE', 'CREATE', 'EXISTS', 'DELETE', 'DELETE',
+            'DELETE')))
+        # path per request: p, c, g, p, g, c, p
+        self.path_off = col(poff[:, 0], poff[:, 1], poff[:, 2], poff[:, 0],
+                            poff[:, 2], poff[:, 1], poff[:, 0])
+        self.path_len = col(plen[:, 0], plen[:, 1], plen[:, 2], plen[:, 0],
+                            plen[:, 2], plen[:, 1], plen[:, 0])
+        self.arg = col(full(0, I32), full(0, I32), full(0, I32),
+                       full(0, I32), full(-1, I32), full(-1, I32),
+                       full(-1, I32))
+        self.data_off = torch.zeros(n, dtype=I64, device=dev)
+        self.data_len = col(full(4, I32), full(4, I32), full(4, I32),
+                            *(full(0, I32) for _ in range(4)))
+        self.acl_id = torch.zeros(n, dtype=I32, device=dev)
+        self.is_exists = self.opcode == ops['EXISTS']
+        self.drv.create_dirs(
+            [['/nest'], ['/nest/d%05d' % d for d in range(ndirs)]],
+            (self.acl_arena, self.acl_off, self.acl_len))
+        self.last = None
+
+    def step(self, validate=True, acc=None):
+        n = self.n
+        d = self.drv
+        rb = B.RequestBatch(n, self.opcode, d.xids(n), self.arg,
+                            self.path_off, self.path_len, self.data_off,
+                            self.data_len, self.acl_id, self.path_arena,
+                            self.data_arena, self.acl_off, self.acl_len,
+                            self.acl_arena)
+        rep, _ = d.run(rb)
+        self.last = (rb, rep)
+        if not validate:
+            return None
+        one_child = (rep.stat32[4, :n] == 1) & (rep.stat32[1, :n] == 1)
+        ok = ((rep.status[:n] == 0) & (rep.err[:n] == 0) &
+              (rep.xid[:n] == rb.xid) & (rep.opcode[:n] == rb.opcode) &
+              (~self.is_exists | one_child))
         if acc is None:
             return ok.sum()
         acc[:1] += ok.sum()

@@ -96,17 +96,25 @@ def start_fast_server(nodes, data_bytes):
     return fast.FastZKServer(preload=nodes, data_bytes=data_bytes)
 
 
-def measure_bulk_tcp(port, nodes, batch, iters, dev):
+def measure_bulk_tcp(port, nodes, batch, iters, dev, conns=1):
     """``Client.bulk_get`` over loopback TCP to the native server: every
-    batch is ``batch`` GET_DATA of random existing nodes, device-resident
-    paths -> K10 -> pinned TX -> socket -> server -> native-loop capture
-    into pinned RX -> K1 + K2-K8 on the GPU; every reply checked OK.
-    Returns (ops/s, ms per batch)."""
+    batch is ``batch`` GET_DATA of random existing nodes split over
+    ``conns`` sessions (one connection and one event loop each, all
+    submitted at once), device-resident paths -> K10 -> pinned TX ->
+    socket -> server -> native-loop capture into pinned RX -> K1 + K2-K8 on
+    the GPU; every reply checked OK.  Returns (ops/s, ms per batch, phase
+    ms): the mean over sessions of encode (K10 + D2H, on the loop thread),
+    wire + server (sent -> last reply captured), finish (H2D + decode
+    enqueued) and decode (the device finishing it)."""
     import threading
     import numpy as np
     from zkmi import Client
-    c = Client(address='127.0.0.1', port=port, device=dev)
-    c.wait_connected(10)
+    from zkmi.runtime.loop import new_loop
+    loops = [new_loop() for _ in range(conns)]
+    cs = [Client({'address': '127.0.0.1', 'port': port, 'device': dev,
+                  'loop': lp}) for lp in loops]
+    for c in cs:
+        c.wait_connected(10)
     i = np.arange(nodes)
     paths = np.char.add(np.char.add('/bench/d', np.char.zfill(
         (i // 1000).astype(str), 6)), np.char.add('/n', np.char.zfill(
@@ -114,30 +122,50 @@ def measure_bulk_tcp(port, nodes, batch, iters, dev):
     blob = ''.join(paths.tolist()).encode()
     plen = len(paths[0])
     arena = torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(dev)
-    ln = torch.full((batch,), plen, dtype=torch.int32, device=dev)
+    per = batch // conns
+    ln = torch.full((per,), plen, dtype=torch.int32, device=dev)
+    phases = []
 
     def one(seed):
         g = torch.Generator(device=dev)
         g.manual_seed(seed)
-        idx = torch.randint(0, nodes, (batch,), device=dev, generator=g)
-        box, ev = [], threading.Event()
-        c.bulk_get((arena, idx * plen, ln),
-                   lambda err, res=None: (box.append((err, res)), ev.set()))
-        if not ev.wait(120):
-            raise SystemExit('bulk_get timed out')
-        err, res = box[0]
-        if err is not None:
-            raise SystemExit('bulk_get failed: %r' % (err,))
-        if res.ok_count() != batch:
-            raise SystemExit('bulk_get: %d of %d replies OK'
-                             % (res.ok_count(), batch))
+        idx = torch.randint(0, nodes, (per * conns,), device=dev, generator=g)
+        boxes = [[] for _ in cs]
+        evs = [threading.Event() for _ in cs]
+        for k, c in enumerate(cs):
+            c.bulk_get((arena, idx[k * per:(k + 1) * per] * plen, ln),
+                       lambda err, res=None, k=k: (boxes[k].append((err, res)),
+                                                   evs[k].set()))
+        for k, ev in enumerate(evs):
+            if not ev.wait(120):
+                raise SystemExit('bulk_get timed out')
+            err, res = boxes[k][0]
+            if err is not None:
+                raise SystemExit('bulk_get failed: %r' % (err,))
+            if res.ok_count() != per:
+                raise SystemExit('bulk_get: %d of %d replies OK'
+                                 % (res.ok_count(), per))
+            t_done = time.perf_counter()
+            p = res.phases
+            if p:
+                phases.append((p['encoded'] - p['submit'],
+                               p['captured'] - p['sent'],
+                               p['finished'] - p['captured'],
+                               t_done - p['finished']))
     one(0)                                   # warm-up (allocations)
+    phases.clear()
     t0 = time.perf_counter()
     for k in range(iters):
         one(k + 1)
     el = time.perf_counter() - t0
-    c.close_sync(10)
-    return batch * iters / el, el / iters * 1e3
+    for c in cs:
+        c.close_sync(10)
+    ph = None
+    if phases:
+        m = np.mean(np.array(phases), axis=0) * 1e3
+        ph = {'encode_ms': m[0], 'wire_server_ms': m[1], 'finish_ms': m[2],
+              'decode_wait_ms': m[3]}
+    return per * conns * iters / el, el / iters * 1e3, ph
 
 
 def _create_quiet(c, path):
@@ -322,6 +350,11 @@ def main():
     ap.add_argument('--bulk-batch', type=int, default=1 << 20,
                     help='requests per Client.bulk_get batch of the '
                          'bulk-TCP measurement')
+    ap.add_argument('--bulk-conns', type=int, default=8,
+                    help='sessions (connections, one event loop each) the '
+                         'k-connection bulk-TCP measurement splits a batch '
+                         'over (the native server serves each on its own '
+                         'worker thread)')
     ap.add_argument('--streams', type=int, default=2,
                     help='get: pipelined connections per GPU, one HIP '
                          'stream each (the batch is split between them; 2 '
@@ -595,7 +628,8 @@ def run_rank(a):
                    'hip_graph': bool(rgraph)}
         del rp
 
-    rtt50 = rtt99 = py50 = py99 = bulk_ops = bulk_ms = None
+    rtt50 = rtt99 = py50 = py99 = bulk_ops = bulk_ms = bulk_ph = None
+    bulk_k = (None, None, None)
     ev50 = ev99 = None
     if rtt_srv is not None:
         try:
@@ -607,8 +641,10 @@ def run_rank(a):
         try:
             rtt50, rtt99 = measure_rtt(fast_srv.port)
             ev50, ev99 = measure_rtt_async(fast_srv.port)
-            bulk_ops, bulk_ms = measure_bulk_tcp(
-                fast_srv.port, a.nodes, a.bulk_batch, 3, dev)
+            bulk_ops, bulk_ms, bulk_ph = measure_bulk_tcp(
+                fast_srv.port, a.nodes, a.bulk_batch, 3, dev, 1)
+            bulk_k = measure_bulk_tcp(fast_srv.port, a.nodes, a.bulk_batch,
+                                      3, dev, a.bulk_conns)
         finally:
             fast_srv.shutdown()
     elif rtt_srv is not None:
@@ -665,10 +701,17 @@ def run_rank(a):
             'p99_get_rtt_us_fakezk': py99,
             'bulk_tcp_ops_s': bulk_ops,
             'bulk_tcp_ms_per_batch': bulk_ms,
+            'bulk_tcp_phases_ms': bulk_ph,
+            'bulk_tcp_conns': a.bulk_conns,
+            'bulk_tcp_ops_s_kconn': bulk_k[0],
+            'bulk_tcp_ms_per_batch_kconn': bulk_k[1],
+            'bulk_tcp_phases_ms_kconn': bulk_k[2],
             'bulk_tcp_note': 'Client.bulk_get of %d random nodes per batch '
                              'over loopback TCP to the native server: GPU '
                              'encode/decode, pinned TX/RX, replies captured '
-                             'by the native loop' % a.bulk_batch,
+                             'by the native loop; *_kconn: the batch split '
+                             'over bulk_tcp_conns sessions at once' %
+                             a.bulk_batch,
             'batch_latency_ms': elapsed / a.steps * 1e3,
             'baseline_note': 'vs_baseline = value / 0.51M pkts/s, the '
                              'reference ZKDecodeStream frame+decode on one '

@@ -4,7 +4,7 @@
 // Appendix-D contract (watches, ensembles, fault hooks) in Python; at tens
 // of thousands of requests per second it, not the client, would be what a
 // pipelined client benchmark measures.  This server speaks the same wire
-// protocol from one epoll thread: handshake (new and resumed sessions),
+// protocol from a pool of epoll threads: handshake (new and resumed sessions),
 // PING, GET_DATA, EXISTS, SET_DATA (version CAS), CREATE (persistent,
 // EPHEMERAL, SEQUENTIAL), DELETE, SYNC, GET_CHILDREN(2), CLOSE_SESSION.  No
 // watches (requests with watch=1 are served, the watch is not kept), no
@@ -14,8 +14,16 @@
 // the burst are served in order (ZooKeeper answers a session's requests in
 // order) and their replies appended to one output buffer.
 //
+// Threads: the main thread accepts and hands each connection to one of
+// --threads workers (round robin; each worker runs its own epoll set), so
+// k client connections are served by up to k cores.  The tree is shared
+// under a reader/writer lock taken once per burst: a burst of reads (GET,
+// EXISTS, children, SYNC, PING) shares it, a burst holding any write or
+// the handshake takes it alone.  (Round 2's single epoll thread served
+// ~1.4 M GETs/s — the bound of the bulk TCP benchmark.)
+//
 // Usage: zk_fastserver [--port P] [--preload N] [--data-bytes B]
-//                      [--fanout F]
+//                      [--fanout F] [--threads T]
 // --preload creates /bench, /bench/dDDDDDD and N leaves
 // /bench/dDDDDDD/nNNNNNNNNN with B bytes of data each (the layout of
 // zkmi/bench/synthetic.py GpuTree).  Prints "PORT <n>" once listening and
@@ -34,10 +42,16 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <sys/eventfd.h>
+
+#include <atomic>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <set>
+#include <shared_mutex>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -121,6 +135,7 @@ struct Wr {
 };
 
 struct Server {
+  std::shared_mutex mu;          // the tree and the session table
   std::unordered_map<std::string, std::unique_ptr<Node>> nodes;
   std::unordered_map<int64_t, std::string> sessions;    // sid -> passwd
   int64_t zxid = 1;
@@ -385,18 +400,159 @@ bool flush_out(Conn& c) {
   return true;
 }
 
+bool is_write(int32_t op) {
+  return op == OP_CREATE || op == OP_DELETE || op == OP_SET_DATA ||
+         op == OP_CLOSE_SESSION;
+}
+
+// One worker: its own epoll set over the connections the acceptor handed
+// it (through `pending` + the eventfd).
+struct Worker {
+  Server* S = nullptr;
+  int ep = -1, efd = -1;
+  std::mutex mu;
+  std::vector<int> pending;
+  std::map<int, std::unique_ptr<Conn>> conns;
+  std::string key;
+  std::vector<char> rbuf = std::vector<char>(1 << 20);
+
+  void add(int fd) {
+    {
+      std::lock_guard<std::mutex> g(mu);
+      pending.push_back(fd);
+    }
+    uint64_t one = 1;
+    (void)!write(efd, &one, 8);
+  }
+
+  void drop(int fd) {
+    epoll_ctl(ep, EPOLL_CTL_DEL, fd, nullptr);
+    close(fd);
+    conns.erase(fd);
+  }
+
+  // Serve every complete frame of the connection's input (one lock per
+  // burst: shared for reads only, exclusive otherwise).
+  bool serve_burst(Conn& c) {
+    bool writes = !c.hs;
+    for (size_t o = c.in_off; !writes && c.in.size() - o >= 8;) {
+      uint32_t l, opw;
+      memcpy(&l, c.in.data() + o, 4);
+      const int32_t len = (int32_t)ntohl(l);
+      if (len < 0 || len > MAX_PACKET) break;
+      if (c.in.size() - o < 4 + (size_t)len) break;
+      if (len >= 8) {
+        memcpy(&opw, c.in.data() + o + 8, 4);
+        writes = is_write((int32_t)ntohl(opw));
+      }
+      o += 4 + (size_t)len;
+    }
+    std::unique_lock<std::shared_mutex> ex(S->mu, std::defer_lock);
+    std::shared_lock<std::shared_mutex> sh(S->mu, std::defer_lock);
+    if (writes) ex.lock(); else sh.lock();
+    bool dead = false;
+    while (!c.closing && c.in.size() - c.in_off >= 4) {
+      uint32_t l;
+      memcpy(&l, c.in.data() + c.in_off, 4);
+      const int32_t len = (int32_t)ntohl(l);
+      if (len < 0 || len > MAX_PACKET) { dead = true; break; }
+      if (c.in.size() - c.in_off < 4 + (size_t)len) break;
+      const uint8_t* b = (const uint8_t*)c.in.data() + c.in_off + 4;
+      if (!c.hs) {
+        if (!writes) break;            // (cannot happen: !hs => exclusive)
+        c.sid = S->handshake(b, len, &c.out);
+        c.hs = true;
+        if (c.sid == 0) c.closing = true;
+      } else if (!writes && len >= 8) {
+        uint32_t opw;
+        memcpy(&opw, b + 4, 4);
+        if (is_write((int32_t)ntohl(opw))) break;   // next burst, exclusive
+        if (!S->serve(b, len, c.sid, &c.out, &key)) c.closing = true;
+      } else if (!S->serve(b, len, c.sid, &c.out, &key)) {
+        c.closing = true;
+      }
+      c.in_off += 4 + (size_t)len;
+    }
+    return !dead;
+  }
+
+  void run() {
+    epoll_event evs[64];
+    for (;;) {
+      int ne = epoll_wait(ep, evs, 64, -1);
+      if (ne < 0 && errno == EINTR) continue;
+      for (int k = 0; k < ne; ++k) {
+        const int fd = evs[k].data.fd;
+        if (fd == efd) {
+          uint64_t v;
+          (void)!read(efd, &v, 8);
+          std::vector<int> fds;
+          {
+            std::lock_guard<std::mutex> g(mu);
+            fds.swap(pending);
+          }
+          for (int c : fds) {
+            auto cn = std::make_unique<Conn>();
+            cn->fd = c;
+            conns[c] = std::move(cn);
+            epoll_event e{};
+            e.events = EPOLLIN | EPOLLRDHUP;
+            e.data.fd = c;
+            epoll_ctl(ep, EPOLL_CTL_ADD, c, &e);
+          }
+          continue;
+        }
+        auto it = conns.find(fd);
+        if (it == conns.end()) continue;
+        Conn& c = *it->second;
+        bool dead = false;
+        if (evs[k].events & (EPOLLIN | EPOLLRDHUP | EPOLLHUP | EPOLLERR)) {
+          for (;;) {
+            ssize_t m = recv(fd, rbuf.data(), rbuf.size(), MSG_DONTWAIT);
+            if (m > 0) { c.in.append(rbuf.data(), (size_t)m); continue; }
+            if (m == 0) { dead = true; break; }
+            if (errno == EINTR) continue;
+            if (errno != EAGAIN && errno != EWOULDBLOCK) dead = true;
+            break;
+          }
+          // a read burst may end at a write frame: serve until no frame
+          // is left or a partial one
+          for (int guard = 0; guard < 1 << 20; ++guard) {
+            const size_t before = c.in_off;
+            if (!serve_burst(c)) { dead = true; break; }
+            if (c.in_off == before || c.closing) break;
+          }
+          if (c.in_off == c.in.size()) { c.in.clear(); c.in_off = 0; }
+          else if (c.in_off > (1u << 20)) { c.in.erase(0, c.in_off); c.in_off = 0; }
+        }
+        if (!flush_out(c)) dead = true;
+        if (!dead && c.closing && c.out.empty()) dead = true;
+        if (dead) { drop(fd); continue; }
+        epoll_event e{};
+        e.events = EPOLLIN | EPOLLRDHUP | (c.out.empty() ? 0 : EPOLLOUT);
+        e.data.fd = fd;
+        epoll_ctl(ep, EPOLL_CTL_MOD, fd, &e);
+      }
+    }
+  }
+};
+
 }  // namespace
 
 int main(int argc, char** argv) {
   int port = 0;
   int64_t pre = 0;
   int32_t dbytes = 100, fanout = 1000;
+  unsigned hw = std::thread::hardware_concurrency();
+  int nthreads = (int)(hw == 0 ? 4 : (hw < 16 ? hw : 16));
   for (int i = 1; i + 1 < argc; i += 2) {
     if (!strcmp(argv[i], "--port")) port = atoi(argv[i + 1]);
     else if (!strcmp(argv[i], "--preload")) pre = atoll(argv[i + 1]);
     else if (!strcmp(argv[i], "--data-bytes")) dbytes = atoi(argv[i + 1]);
     else if (!strcmp(argv[i], "--fanout")) fanout = atoi(argv[i + 1]);
+    else if (!strcmp(argv[i], "--threads")) nthreads = atoi(argv[i + 1]);
   }
+  if (nthreads < 1) nthreads = 1;
   Server S;
   if (pre > 0) preload(S, pre, dbytes, fanout);
   else { S.make("/", "", 0, 0); S.make("/zookeeper", "", 0, 0); }
@@ -414,6 +570,23 @@ int main(int argc, char** argv) {
   }
   socklen_t al = sizeof a;
   getsockname(ls, (sockaddr*)&a, &al);
+
+  std::vector<std::unique_ptr<Worker>> workers;
+  for (int t = 0; t < nthreads; ++t) {
+    auto w = std::make_unique<Worker>();
+    w->S = &S;
+    w->ep = epoll_create1(0);
+    w->efd = eventfd(0, EFD_NONBLOCK);
+    epoll_event e{};
+    e.events = EPOLLIN;
+    e.data.fd = w->efd;
+    epoll_ctl(w->ep, EPOLL_CTL_ADD, w->efd, &e);
+    workers.push_back(std::move(w));
+  }
+  for (auto& w : workers) {
+    Worker* wp = w.get();
+    std::thread([wp] { wp->run(); }).detach();
+  }
   printf("PORT %d\n", ntohs(a.sin_port));
   fflush(stdout);
 
@@ -424,80 +597,24 @@ int main(int argc, char** argv) {
   epoll_ctl(ep, EPOLL_CTL_ADD, ls, &ev);
   ev.data.fd = 0;                              // stdin EOF = shut down
   epoll_ctl(ep, EPOLL_CTL_ADD, 0, &ev);
-  std::map<int, std::unique_ptr<Conn>> conns;
-  std::string key;
-  std::vector<char> rbuf(1 << 20);
-  epoll_event evs[64];
-  auto drop = [&](int fd) {
-    epoll_ctl(ep, EPOLL_CTL_DEL, fd, nullptr);
-    close(fd);
-    conns.erase(fd);
-  };
+  epoll_event evs[8];
+  unsigned rr = 0;
   for (;;) {
-    int ne = epoll_wait(ep, evs, 64, -1);
+    int ne = epoll_wait(ep, evs, 8, -1);
     if (ne < 0 && errno == EINTR) continue;
     for (int k = 0; k < ne; ++k) {
       const int fd = evs[k].data.fd;
       if (fd == 0) {
         char tmp[256];
-        if (read(0, tmp, sizeof tmp) <= 0) return 0;
+        if (read(0, tmp, sizeof tmp) <= 0) _exit(0);
         continue;
       }
-      if (fd == ls) {
-        for (;;) {
-          int c = accept4(ls, nullptr, nullptr, SOCK_NONBLOCK);
-          if (c < 0) break;
-          setsockopt(c, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
-          auto cn = std::make_unique<Conn>();
-          cn->fd = c;
-          conns[c] = std::move(cn);
-          epoll_event e{};
-          e.events = EPOLLIN | EPOLLRDHUP;
-          e.data.fd = c;
-          epoll_ctl(ep, EPOLL_CTL_ADD, c, &e);
-        }
-        continue;
+      for (;;) {
+        int c = accept4(ls, nullptr, nullptr, SOCK_NONBLOCK);
+        if (c < 0) break;
+        setsockopt(c, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+        workers[rr++ % workers.size()]->add(c);
       }
-      auto it = conns.find(fd);
-      if (it == conns.end()) continue;
-      Conn& c = *it->second;
-      bool dead = false;
-      if (evs[k].events & (EPOLLIN | EPOLLRDHUP | EPOLLHUP | EPOLLERR)) {
-        for (;;) {
-          ssize_t m = recv(fd, rbuf.data(), rbuf.size(), MSG_DONTWAIT);
-          if (m > 0) { c.in.append(rbuf.data(), (size_t)m); continue; }
-          if (m == 0) { dead = true; break; }
-          if (errno == EINTR) continue;
-          if (errno != EAGAIN && errno != EWOULDBLOCK) dead = true;
-          break;
-        }
-        // serve every complete frame of the burst
-        while (!c.closing && c.in.size() - c.in_off >= 4) {
-          uint32_t l;
-          memcpy(&l, c.in.data() + c.in_off, 4);
-          const int32_t len = (int32_t)ntohl(l);
-          if (len < 0 || len > MAX_PACKET) { dead = true; break; }
-          if (c.in.size() - c.in_off < 4 + (size_t)len) break;
-          const uint8_t* b = (const uint8_t*)c.in.data() + c.in_off + 4;
-          if (!c.hs) {
-            c.sid = S.handshake(b, len, &c.out);
-            c.hs = true;
-            if (c.sid == 0) c.closing = true;
-          } else if (!S.serve(b, len, c.sid, &c.out, &key)) {
-            c.closing = true;
-          }
-          c.in_off += 4 + (size_t)len;
-        }
-        if (c.in_off == c.in.size()) { c.in.clear(); c.in_off = 0; }
-        else if (c.in_off > (1u << 20)) { c.in.erase(0, c.in_off); c.in_off = 0; }
-      }
-      if (!flush_out(c)) dead = true;
-      if (!dead && c.closing && c.out.empty()) dead = true;
-      if (dead) { drop(fd); continue; }
-      epoll_event e{};
-      e.events = EPOLLIN | EPOLLRDHUP | (c.out.empty() ? 0 : EPOLLOUT);
-      e.data.fd = fd;
-      epoll_ctl(ep, EPOLL_CTL_MOD, fd, &e);
     }
   }
 }

@@ -65,6 +65,7 @@ struct ZkTree {
   int64_t* dirty_list;         // [cap]
   int64_t* node_pw;            // [cap] path word: offset << 24 | length
   int32_t* node_path_cap;      // [cap] bytes of the node's path storage
+  uint8_t* node_line;          // [cap * 64] lookup line, see LN_* below
   // watch table (null wt_key: the tree keeps no watches), see wt_* below
   int64_t* wt_key;             // [wt_hmask + 1] path hash | 1, 0 = empty
   unsigned long long* wt_mask; // [2 * (wt_hmask + 1)] data / child masks
@@ -186,10 +187,40 @@ ZK_DEV int64_t* ht_val(const ZkTree& t, int64_t s) { return &t.ht[2 * s + 1]; }
 ZK_DEV int64_t pw_pack(int64_t off, int32_t len) {
   return (off << 24) | (int64_t)(uint32_t)len;
 }
-ZK_DEV bool path_is(const ZkTree& t, int64_t v, const uint8_t* p, int32_t n) {
+// Node lookup line (64 bytes, one cache line per node): path length, data
+// length and the path's first LN_PATH bytes.  A hash hit verifies the path
+// and gets a GET reply's data length from this one line — the hash entry
+// and the line are a lookup's only random reads (round 2 read the path
+// word, the path bytes in the arena and data_len[]: four).  Longer paths
+// compare their tail in the arena.
+constexpr int LN_BYTES = 64, LN_PATH = 56;
+
+ZK_DEV void line_set(const ZkTree& t, int64_t v, const uint8_t* p, int32_t n,
+                     int32_t dl) {
+  uint8_t* ln = t.node_line + v * LN_BYTES;
+  __builtin_memcpy(ln, &n, 4);
+  __builtin_memcpy(ln + 4, &dl, 4);
+  copy_bytes(ln + 8, p, n < LN_PATH ? n : LN_PATH);
+}
+
+ZK_DEV void line_set_dlen(const ZkTree& t, int64_t v, int32_t dl) {
+  __builtin_memcpy(t.node_line + v * LN_BYTES + 4, &dl, 4);
+}
+
+// Is node v's path p[0, n)?  *dl gets its data length (from the same line).
+ZK_DEV bool path_is(const ZkTree& t, int64_t v, const uint8_t* p, int32_t n,
+                    int32_t* dl = nullptr) {
+  const uint8_t* ln = t.node_line + v * LN_BYTES;
+  int32_t hd[2];
+  __builtin_memcpy(hd, ln, 8);
+  if (dl != nullptr) *dl = hd[1];
+  if (hd[0] != n) return false;
+  const int32_t head = n < LN_PATH ? n : LN_PATH;
+  if (!bytes_eq(ln + 8, p, head)) return false;
+  if (n <= LN_PATH) return true;
   const int64_t pw = t.node_pw[v];
-  return (int32_t)(pw & 0xFFFFFF) == n &&
-         bytes_eq(t.path_arena + (pw >> 24), p, n);
+  return bytes_eq(t.path_arena + (pw >> 24) + LN_PATH, p + LN_PATH,
+                  n - LN_PATH);
 }
 
 // A hash val holds the node index (low 32 bits) and its slot offset / 16
@@ -224,8 +255,9 @@ ZK_DEV Found tree_lookup(const ZkTree& t, const uint8_t* p, int32_t n) {
     if (k == 0) break;
     if (k == key && v >= 0) {
       const int64_t node = val_node(v);
-      const int32_t dl = DLEN ? t.store.data_len[node] : 0;
-      if (path_is(t, node, p, n)) return Found{node, val_slot(v), dl};
+      int32_t dl = 0;
+      if (path_is(t, node, p, n, DLEN ? &dl : nullptr))
+        return Found{node, val_slot(v), dl};
     }
     s = (s + 1) & t.mask;
   }
@@ -405,6 +437,7 @@ __global__ __launch_bounds__(TR_T) void tree_fill_k(ZkTree t, int64_t n0,
             nkids[v], v + 1);
   st_be32(slot + 68, 0);
   st_be32(slot + ZK_SLOT_LEN, dl > 0 ? dl : -1);
+  line_set(t, v, t.path_arena + t.node_path_off[v], t.node_path_len[v], dl);
   t.cver[v] = nkids[v];
   t.nchild[v] = nkids[v];
   t.pzxid[v] = v + 1;
@@ -481,6 +514,7 @@ ZK_DEV int32_t do_create(const ZkTree& t, Lane& L, const uint8_t* data,
   copy_bytes(slot + ZK_SLOT_DATA, data, dl);
   t.node_path_len[v] = npl;
   s.data_len[v] = dl;
+  line_set(t, v, pd, npl, dl);
   t.cver[v] = 0;
   t.nchild[v] = 0;
   t.pzxid[v] = L.zx;
@@ -659,6 +693,7 @@ __global__ __launch_bounds__(TR_T) void tree_serve_k(
         copy_bytes(slot + ZK_SLOT_DATA, rx + rq.doff, L.dl);
         st_be32(slot + ZK_SLOT_LEN, L.dl > 0 ? L.dl : -1);
         s.data_len[node] = L.dl;
+        line_set_dlen(t, node, L.dl);
         st_be64(slot + 8, L.zx);                      // mzxid
         st_be64(slot + 24, now_ms);                   // mtime
         st_be32(slot + 52, L.dl);                     // dataLength

@@ -40,6 +40,7 @@ struct ZkTree {
   int64_t* dirty_list;
   int64_t* node_pw;
   int32_t* node_path_cap;
+  uint8_t* node_line;
   int64_t* wt_key;
   unsigned long long* wt_mask;
   int64_t wt_hmask;
@@ -252,11 +253,11 @@ ZkNodeStore node_store(const std::vector<Tensor>& v, size_t at,
 //  dirty, dirty_list, node_pw]; sizes give mask, caps
 // [ht, node_path_off, node_path_len, node_parent, path_arena, counters,
 //  slab, slot_off, data_len, slot_cap, free_list, cver, nchild, pzxid,
-//  dirty, dirty_list, node_pw, node_path_cap] + optionally [wt_key,
-//  wt_mask] (watches)
+//  dirty, dirty_list, node_pw, node_path_cap, node_line] + optionally
+//  [wt_key, wt_mask] (watches)
 ZkTree tree(const std::vector<Tensor>& v) {
-  TORCH_CHECK(v.size() == 18 || v.size() == 20,
-              "zkmi: tree needs 18 tensors (20 with a watch table), got ",
+  TORCH_CHECK(v.size() == 19 || v.size() == 21,
+              "zkmi: tree needs 19 tensors (21 with a watch table), got ",
               v.size());
   const Tensor* r = &v[0];
   ZkTree t;
@@ -283,16 +284,19 @@ ZkTree tree(const std::vector<Tensor>& v) {
   t.dirty_list = P<int64_t>(v[15], I64, cap, "tree.dirty_list", r);
   t.node_pw = P<int64_t>(v[16], I64, cap, "tree.node_pw", r);
   t.node_path_cap = P<int32_t>(v[17], I32, cap, "tree.node_path_cap", r);
+  t.node_line = P<uint8_t>(v[18], U8, 64 * cap, "tree.node_line", r);
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(t.node_line) & 63) == 0,
+              "zkmi: tree.node_line must be 64-byte aligned");
   t.wt_key = nullptr;
   t.wt_mask = nullptr;
   t.wt_hmask = 0;
-  if (v.size() == 20) {
-    const int64_t h = v[18].numel();
+  if (v.size() == 21) {
+    const int64_t h = v[19].numel();
     TORCH_CHECK(h > 0 && (h & (h - 1)) == 0,
                 "zkmi: tree.wt_key must hold a power of two of entries");
-    t.wt_key = P<int64_t>(v[18], I64, h, "tree.wt_key", r);
+    t.wt_key = P<int64_t>(v[19], I64, h, "tree.wt_key", r);
     t.wt_mask = reinterpret_cast<unsigned long long*>(
-        P<int64_t>(v[19], I64, 2 * h, "tree.wt_mask", r));
+        P<int64_t>(v[20], I64, 2 * h, "tree.wt_mask", r));
     t.wt_hmask = h - 1;
   }
   return t;

@@ -1,0 +1,44 @@
+"""Diagnostic: the reply stream of the storm workload's FIRST step (the
+one whose link repair ran long) — K1 chain statistics, the repair time,
+and a prefix of the stream saved for offline analysis."""
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), '..', '..'))
+from zkmi.bench import synthetic as S  # noqa: E402
+from zkmi.ops import batch as B  # noqa: E402
+
+dev = torch.device('cuda', 0)
+batch = 1 << 20
+tree = S.GpuTree(1_000_000, 100, device=dev, seed=0,
+                 spare=(batch * 3 + 8192) / 1e6 + 0.05)
+pipe = S.StormPipeline(tree, batch, seed=0)
+d = pipe.drv
+rb, rep = pipe.last
+# re-scan the reply stream of that first step from the server's buffer
+out, total, _, _ = d.server.result
+n = int(total.item())
+print('reply stream bytes', n, 'frames', int(rep.count.item()), flush=True)
+for nospec in (False, True):
+    sc = B.FrameScanner(batch + 16, dev, window=d.rwindow)
+    sc.scan(out, n, nospec=nospec)
+    torch.cuda.synchronize()
+    sc.chain_stats()
+    t0 = time.perf_counter()
+    ft = sc.scan(out, n, nospec=nospec)
+    torch.cuda.synchronize()
+    el = (time.perf_counter() - t0) * 1e3
+    print('nospec', nospec, 'window', d.rwindow, 'scan ms', round(el, 3),
+          ft.host_result(), sc.chain_stats(), flush=True)
+raw = out[:min(n, 8 << 20)].cpu().numpy()
+os.makedirs('gpurun_out', exist_ok=True)
+np.save('gpurun_out/storm_first_reply.npy', raw)
+ft = d.rscanner.table
+off = ft.off[:200].cpu().numpy()
+print('first frame bodies', off[:10].tolist(),
+      'lens', ft.length[:10].cpu().tolist())
+print(bytes(raw[:160]).hex())

@@ -146,6 +146,9 @@ class GpuTree(object):
         # bytes of each node's path storage (the static paths are packed)
         self.node_path_cap = torch.zeros(cap, dtype=I32, device=dev)
         self.node_path_cap[:nst] = self.node_path_len[:nst]
+        # per-node lookup line: path and data length + the path's first 56
+        # bytes (csrc/kernels/tree.hip LN_*), written by tree_fill / create
+        self.node_line = torch.zeros(cap * 64, dtype=U8, device=dev)
         # path word (offset << 24 | length) the hash lookups verify against
         self.node_pw = torch.zeros(cap, dtype=I64, device=dev)
         self.node_pw[:nst] = torch.from_numpy(
@@ -206,7 +209,8 @@ class GpuTree(object):
                          self.slab, self.slot_off, self.data_len,
                          self.slot_cap, self.free_list, self.cver,
                          self.nchild, self.pzxid, self.dirty,
-                         self.dirty_list, self.node_pw, self.node_path_cap]
+                         self.dirty_list, self.node_pw, self.node_path_cap,
+                         self.node_line]
         # watch table (watch_cap > 0): path-keyed one-shot watches of up to
         # 64 watcher slots (csrc/kernels/tree.hip wt_*); every serve of a
         # tree with one fires the watches its writes hit

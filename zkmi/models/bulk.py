@@ -69,6 +69,7 @@ class BulkResult(object):
     def __init__(self, n, replies=None, buf=None, packets=None, device=None,
                  event=None):
         self.n = n
+        self.phases = {}
         self.replies = replies
         self.buf = buf
         self.device = device
@@ -132,6 +133,11 @@ class BulkBatch(object):
         self.got = 0
         self.cb = None
         self.t_submit = None
+        # phase clock (perf_counter): submit, encoded (K10 + D2H into the
+        # pinned TX buffer done), sent (queued on the transport), captured
+        # (every reply in the pinned RX buffer), finished (H2D + decode
+        # enqueued); BulkResult.phases reports them
+        self.t = {}
         self.done = False
         self.xid_map = None
         self.xt = None
@@ -211,6 +217,7 @@ class BulkBatch(object):
             self.tx_pin = torch.empty(max(ntx, 1), dtype=torch.uint8,
                                       pin_memory=True)
             self.tx_pin[:ntx].copy_(tx[:ntx])
+            self.t['encoded'] = time.perf_counter()
             return (self.tx_pin.data_ptr(), ntx)
 
     def rx_buffer(self):
@@ -226,6 +233,7 @@ class BulkBatch(object):
         the RX buffer.  Otherwise the batch falls back to per-frame
         collection, keeping what was captured."""
         self.capturing = False
+        self.t['captured'] = time.perf_counter()
         if status == 0:
             return True
         self.rx = bytearray(self.rx_pin[:nbytes].numpy().tobytes())
@@ -277,6 +285,8 @@ class BulkBatch(object):
         # the event covers has run
         res = BulkResult(self.n, replies=rep, buf=buf, device=self.device,
                          event=ev)
+        self.t['finished'] = time.perf_counter()
+        res.phases = dict(self.t, submit=self.t_submit)
         res._hold = (host, self.tx_pin)
         self.rx_pin = self.tx_pin = None
         return res

@@ -432,6 +432,7 @@ class ZKConnectionFSM(FSM):
             self.log.trace({'xid0': x0, 'n': n, 'bytes': len(wire)},
                            'sent bulk batch')
             self.socket.write(wire)
+        batch.t['sent'] = time.perf_counter()
 
     def _bulk_captured(self, b, status, nbytes, got, last_off):
         """The transport's capture of ``b`` ended (loop thread)."""

@@ -296,6 +296,9 @@ class EnsembleWorkload(object):
             codec_device=str(codec_device) if codec_device else None)
         self.connects = 0
         self._lk = threading.Lock()
+        # signalled by every event an owner's watcher emits: the fan-out
+        # waits on it instead of polling on a timer
+        self._ev = threading.Condition(self._lk)
         self._connected = threading.Event()
 
         def on_connect():
@@ -328,7 +331,7 @@ class EnsembleWorkload(object):
             self.client.watcher(p).on(
                 'dataChanged', lambda d, s, p=p: self._on_event(p, d, s))
         self.expected.update((p, b'init') for p in self.paths)
-        self._deliver_until(len(self.paths))
+        self._deliver_until(len(self.paths), mine=len(self.mine))
 
     # -- plumbing -------------------------------------------------------------
 
@@ -360,21 +363,30 @@ class EnsembleWorkload(object):
     def _on_event(self, path, data, stat):
         with self._lk:
             self.pending.append((path, data, stat))
+            self._ev.notify_all()
 
-    def _deliver_until(self, want, timeout=60.0):
+    def _deliver_until(self, want, timeout=60.0, mine=None):
         """Tick the fan-out until every rank has received ``want`` events
         (collective; the stop decision is all-reduced).  Returns the number
-        this rank received."""
+        this rank received.  ``mine``: the events this rank's watchers will
+        emit — each round first waits (on the event condition, no polling)
+        until they are all pending or a tick (5 ms) passes, so a step is
+        usually ONE exchange."""
         got = 0
         t_end = time.monotonic() + timeout
         # [not done, timed out], all-reduced with MAX: every rank stops
         # together, and a rank's timeout makes every rank raise (none is
         # left waiting in the next collective)
         flag = torch.zeros(2, dtype=torch.int64, device=self.coll)
+        sent = 0
         while True:
             with self._lk:
+                if mine is not None:
+                    self._ev.wait_for(
+                        lambda: sent + len(self.pending) >= mine, 0.005)
                 batch = self.pending[:KMAX]
                 del self.pending[:KMAX]
+            sent += len(batch)
             for src, path, data, stat in self.fan.exchange(batch):
                 self.seen[(path, data)] += 1
                 got += 1
@@ -389,7 +401,6 @@ class EnsembleWorkload(object):
                 raise RuntimeError('fan-out: %d of %d events after %.0f s '
                                    '(on this rank or another)'
                                    % (got, want, timeout))
-            time.sleep(0.002)
 
     def _choose(self, s):
         rng = np.random.default_rng(self.seed * 1000003 + s)
@@ -441,7 +452,8 @@ class EnsembleWorkload(object):
             mine = chosen[self.rank::self.world]
             self._set_all(mine, data)
         self._barrier()
-        return self._deliver_until(len(chosen))
+        mine = sum(1 for p in chosen if owner_of(p, self.world) == self.rank)
+        return self._deliver_until(len(chosen), mine=mine)
 
     def _set_all(self, paths, data):
         if not paths:

@@ -1,7 +1,8 @@
 """The native benchmark server (``csrc/host/zk_fastserver.cpp``) as a child
 process: the ZooKeeper wire protocol's data plane (handshake, ping, get,
-exists, set, create, delete, sync, children) from one epoll thread, so a
-pipelined client benchmark measures the client, not a Python server.  The
+exists, set, create, delete, sync, children) from a pool of epoll threads
+(one connection per worker, round robin), so a pipelined client benchmark
+measures the client, not a Python server.  The
 full contract (watches, ensembles, fault hooks) stays with
 :class:`~zkmi.server.fakezk.FakeZKServer`."""
 
@@ -20,7 +21,8 @@ class FastZKServer(object):
     """``FastZKServer(preload=N, data_bytes=B)`` starts the server with the
     synthetic ``/bench`` tree of N leaves (GpuTree's layout)."""
 
-    def __init__(self, preload=0, data_bytes=100, fanout=1000, port=0):
+    def __init__(self, preload=0, data_bytes=100, fanout=1000, port=0,
+                 threads=None):
         if not available():
             raise RuntimeError('zk_fastserver not built '
                                '(tools/build_native.py)')
@@ -29,7 +31,8 @@ class FastZKServer(object):
         env = {k: v for k, v in os.environ.items() if k != 'LD_PRELOAD'}
         self.p = subprocess.Popen(
             [BINARY, '--port', str(port), '--preload', str(preload),
-             '--data-bytes', str(data_bytes), '--fanout', str(fanout)],
+             '--data-bytes', str(data_bytes), '--fanout', str(fanout)] +
+            (['--threads', str(threads)] if threads else []),
             stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True,
             env=env)
         f = self.p.stdout.readline().split()

@@ -83,6 +83,7 @@ constexpr int64_t TERM = (int64_t)1 << 62;
 constexpr int64_t TBAD = (int64_t)1 << 60;
 constexpr int64_t FC_MAXP = (int64_t)1 << 24;
 constexpr int FC_WIN = 1024;               // fs_link's staged walk window
+constexpr int FC_TAILWIN = 8192;           // the serial tail's (one wave)
 constexpr int FL_T = 1024;                 // fs_link threads
 constexpr int FL_U = 8;                    // fs_link loads per batch
 // Bound of fs_tile's wait for the tile before (100 MHz ticks, 2 ms): normal
@@ -263,7 +264,9 @@ __global__ __launch_bounds__(256) void fs_tile(
     int64_t* __restrict__ rec_entry, int64_t* __restrict__ rec_exit,
     int64_t* __restrict__ rec_meta, int32_t* __restrict__ rcount,
     int64_t ntiles_cap, int64_t* __restrict__ dbg, int32_t minb,
-    int32_t nospec) {
+    int32_t tflags) {
+  const bool nospec = tflags & 1;
+  const int32_t misspec = tflags >> 8;
   constexpr int K = W / 64;                 // window entries per lane
   constexpr int XW = W / 32;                // candidate words used
   static_assert(W % 64 == 0 && K >= 1 && K <= 32, "window");
@@ -555,6 +558,9 @@ __global__ __launch_bounds__(256) void fs_tile(
       }
     }
     if (E < 0) E = first;        // no live candidate: the first one
+    // (tests: every misspec-th tile takes a garbage entry one byte past the
+    // chosen one, the link repair's adversary)
+    if (misspec > 0 && t % misspec == 1 && E >= 0 && E + 1 < n) ++E;
     none = E < 0;
   }
   const int64_t t_2 = dbg ? wall_clock64() : 0;
@@ -640,24 +646,35 @@ __global__ __launch_bounds__(256) void fs_tile(
 
 // ---- fs_link ---------------------------------------------------------------
 
-// Stage [wb, wb + FC_WIN) (zero past n) into the wave's window.
+// Stage [wb, wb + WIN) (zero past n) into the wave's window: all WIN/1024
+// 16-byte loads of a lane issued before the first LDS write.
+template <int WIN>
 ZK_DEV void fc_stage(const uint8_t* __restrict__ buf, int64_t n, int64_t wb,
                      uint8_t* win, int lane) {
-  const int64_t g = wb + 16 * lane;
-  uint4 v = make_uint4(0, 0, 0, 0);
-  if (g + 16 <= n) {
-    __builtin_memcpy(&v, buf + g, 16);
-  } else if (g < n) {
-    uint8_t* b = (uint8_t*)&v;
-    for (int k = 0; k < 16; ++k) b[k] = g + k < n ? buf[g + k] : 0;
+  constexpr int PER = WIN / 1024;
+  uint4 v[PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int64_t g = wb + 16 * (lane + 64 * j);
+    v[j] = make_uint4(0, 0, 0, 0);
+    if (g + 16 <= n) {
+      __builtin_memcpy(&v[j], buf + g, 16);
+    } else if (g < n) {
+      uint8_t* b = (uint8_t*)&v[j];
+      for (int k = 0; k < 16; ++k) b[k] = g + k < n ? buf[g + k] : 0;
+    }
   }
-  *(uint4*)(win + 16 * lane) = v;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) *(uint4*)(win + 16 * (lane + 64 * j)) = v[j];
   __builtin_amdgcn_wave_barrier();
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_wave_barrier();
 }
 
-// fs_tile's join walk from global memory (a repair from the exact entry E).
+// fs_tile's join walk from global memory (a repair from the exact entry E),
+// through a WIN-byte LDS window (the grid rounds: 1 KiB per wave; block
+// 0's serial tail: 8 KiB, a whole tile in one staging).
+template <int WIN = FC_WIN>
 ZK_DEV FcWalk fc_walk(const uint8_t* __restrict__ buf, int64_t n,
                       int64_t maxp, int64_t ts, int64_t E, const uint16_t* L,
                       int32_t m0, int64_t send, uint8_t* win, uint16_t* pre,
@@ -665,7 +682,7 @@ ZK_DEV FcWalk fc_walk(const uint8_t* __restrict__ buf, int64_t n,
   FcWalk r{E, 0, 0, -1, false, false};
   const int64_t tend = ts + FT_S;
   int64_t c = E;
-  int64_t wb = -(int64_t)FC_WIN;
+  int64_t wb = -(int64_t)WIN;
   int32_t lb = 0;
   uint32_t lv = lane < m0 ? (uint32_t)L[lane] : 0xFFFFFFFFu;
   int32_t np = 0;
@@ -679,9 +696,9 @@ ZK_DEV FcWalk fc_walk(const uint8_t* __restrict__ buf, int64_t n,
       if (j >= 0) { r.js = j; break; }
     }
     if (c + 4 > n) { r.exit = c; r.term = true; break; }
-    if (c < wb || c + 8 > wb + FC_WIN) {
+    if (c < wb || c + 8 > wb + WIN) {
       wb = c & ~(int64_t)15;
-      fc_stage(buf, n, wb, win, lane);
+      fc_stage<WIN>(buf, n, wb, win, lane);
     }
     const int32_t len =
         __builtin_amdgcn_readfirstlane(lds_be32(win, (int32_t)(c - wb)));
@@ -724,7 +741,12 @@ constexpr uint64_t FL_BAR_TICKS = 50000000;   // 0.5 s: barrier abandoned
 // grid words after lbw's stats (uint64): [0] barrier arrivals, [1] barrier
 // generation, [2] abort, then per round r [3 + 2r] first terminal (ntiles -
 // k, max), [4 + 2r] broken links listed
-constexpr int FL_GW = 3 + 2 * FL_GROUNDS;
+constexpr int FL_NB = 3 + 2 * FL_GROUNDS;     // broken links fs_check saw
+constexpr int FL_GW = FL_NB + 1;
+// At most this many broken links: block 0 repairs them alone from fs_check's
+// list (fl_worklist: no grid barrier, no pass over every tile — a reply
+// stream usually has a handful of broken links or none).
+constexpr unsigned long long FL_SMALL = 64;
 
 // Grid barrier over fs_link's FL_B workgroups (they are co-resident: 32
 // blocks on a 256-CU part, and nothing they wait for needs a CU they hold).
@@ -773,6 +795,30 @@ ZK_DEV bool fl_sync(unsigned long long* g) {
   return s_ok != 0;
 }
 
+// Is a repair walk of tile k (new exit x) written?  Always when the link
+// before k holds (its entry E is then exact, or at least as good as the
+// records get).  When that link is itself broken, E is suspect: a garbage
+// exit of tile k-1 (say a frame-length read from an xid, megabytes ahead)
+// walked on would break the link after k where it holds, that link's walk
+// would break the next, and a wave of garbage would cross the stream one
+// tile per round, with the true repair one round behind it (the first storm
+// reply stream: 1413 tiles re-walked over 71 rounds).  So a suspect walk
+// that changes the exit is not written while link k+1 holds; link k stays
+// broken and is walked again once the tile before has settled.  The
+// leftmost broken link always has an exact entry, so every round settles
+// at least it.  A walk from an E that tile k-1 has since replaced is stale
+// and not written either.
+ZK_DEV bool fl_accept(const int64_t* rec_entry, const int64_t* rec_exit,
+                      int64_t ntiles, int64_t k, int64_t E, int64_t x) {
+  if (ld_agent(&rec_exit[k - 1]) != E) return false;
+  if (k < 2) return true;
+  const bool suspect = ld_agent(&rec_entry[k - 1]) != ld_agent(&rec_exit[k - 2]);
+  if (!suspect) return true;
+  const int64_t ox = ld_agent(&rec_exit[k]);
+  if (x == ox || k + 1 >= ntiles) return true;
+  return ld_agent(&rec_entry[k + 1]) != ox;
+}
+
 // One grid repair round (every thread of every block calls it).  Returns
 // false when no link was broken (the fix-point is reached) or on abort.
 ZK_DEV bool fl_round(const uint8_t* __restrict__ buf, int64_t n,
@@ -785,8 +831,10 @@ ZK_DEV bool fl_round(const uint8_t* __restrict__ buf, int64_t n,
                      int64_t* red, uint8_t* win, uint64_t* stats) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int64_t INF = INT64_MAX;
-  const int64_t nth = (int64_t)gridDim.x * FL_T;
-  const int64_t gt = (int64_t)blockIdx.x * FL_T + tid;
+  const int64_t nblk = gridDim.x;
+  const int64_t bid = blockIdx.x;
+  const int64_t nth = nblk * FL_T;
+  const int64_t gt = bid * FL_T + tid;
   // A. the first terminal as the records stand
   int64_t ft = INF;
   for (int64_t k = gt; k < ntiles; k += nth)
@@ -821,10 +869,9 @@ ZK_DEV bool fl_round(const uint8_t* __restrict__ buf, int64_t n,
   if (nbr == 0) return false;
   // C. every listed link re-walked by one wave, from the exit before it
   uint8_t* mywin = win + (size_t)wv * (FC_WIN + 16);
-  const int64_t nwv = (int64_t)gridDim.x * (FL_T / 64);
+  const int64_t nwv = nblk * (FL_T / 64);
   uint32_t walked = 0;
-  for (int64_t j = (int64_t)blockIdx.x * (FL_T / 64) + wv; j < nbr;
-       j += nwv) {
+  for (int64_t j = bid * (FL_T / 64) + wv; j < nbr; j += nwv) {
     const int64_t k = blist[j];
     const int64_t E = ld_agent(&rec_exit[k - 1]);
     if (E < k * FT_S) continue;               // no exact entry yet
@@ -832,14 +879,14 @@ ZK_DEV bool fl_round(const uint8_t* __restrict__ buf, int64_t n,
     const FcWalk fw = fc_walk(buf, n, maxp, k * FT_S, E, list + k * FT_LMAX,
                               m0, sx[k], mywin, pre + k * FT_LMAX, lane);
     ++walked;
-    if (lane == 0) {
+    if (lane == 0 && fl_accept(rec_entry, rec_exit, ntiles, k, E, fw.exit)) {
       st_agent(&rec_entry[k], E);
       st_agent(&rec_exit[k], fw.exit);
       st_agent(&rec_meta[k], fc_meta(fw));
     }
   }
   if (lane == 0 && walked) fc_stat(stats, 2, walked);
-  if (blockIdx.x == 0 && tid == 0) fc_stat(stats, 3, 1);
+  if (bid == 0 && tid == 0) fc_stat(stats, 3, 1);
   return fl_sync(g);
 }
 
@@ -855,7 +902,8 @@ __global__ __launch_bounds__(FK_T) void fs_check(
     const int64_t* __restrict__ n_dev, int64_t n_cap,
     const int64_t* __restrict__ rec_entry, const int64_t* __restrict__ rec_exit,
     const int64_t* __restrict__ rec_meta, int64_t* __restrict__ base,
-    int64_t* __restrict__ bsum, uint64_t* __restrict__ mins) {
+    int64_t* __restrict__ bsum, uint64_t* __restrict__ mins,
+    unsigned long long* __restrict__ nbroken, int32_t* __restrict__ blist) {
   __shared__ int64_t sm[FK_T / 64 + 1];
   __shared__ int64_t smin[2 * (FK_T / 64)];
   const int64_t n = stream_len(n_dev, n_cap);
@@ -873,6 +921,19 @@ __global__ __launch_bounds__(FK_T) void fs_check(
     cnt = m_cnt(mk);
     if (m_term(mk)) fterm = k;
     else if (nxt && (e < 0 || e != x)) fb = k + 1;
+  }
+  // broken links, counted and listed (fs_link picks its repair by the
+  // count; a small repair starts from the list)
+  const uint64_t bm = __ballot(fb != INF);
+  if (bm) {
+    const int lane = threadIdx.x & 63;
+    unsigned long long b0 = 0;
+    if (lane == 0) b0 = atomicAdd(nbroken, (unsigned long long)__popcll(bm));
+    b0 = __shfl(b0, 0, 64);
+    if (fb != INF) {
+      const uint64_t below = lane ? (bm & ((~0ull) >> (64 - lane))) : 0ull;
+      blist[b0 + __popcll(below)] = (int32_t)fb;
+    }
   }
   int64_t tot;
   const int64_t ex = block_excl_scan(cnt, sm, &tot);
@@ -900,6 +961,215 @@ __global__ __launch_bounds__(FK_T) void fs_check(
   }
 }
 
+// Row bases once every link up to the first terminal ft (INF: none) holds:
+// bsum[b] (block b's count total, fs_check's or re-counted) becomes block
+// b's exclusive offset; base[k] stays the in-block one; result[0..3] and
+// the last tile.  Block 0 alone.
+ZK_DEV void fl_bases(int64_t n, int64_t ntiles, int64_t ft,
+                     const int64_t* rec_exit, const int64_t* rec_meta,
+                     const int64_t* base, int64_t* bsum, int64_t cap,
+                     int64_t* result, int64_t* lastk, int64_t* red) {
+  const int tid = threadIdx.x;
+  const int64_t INF = INT64_MAX;
+  const int64_t last = ft == INF ? ntiles - 1 : ft;
+  const int64_t nbl = last / FK_T + 1;
+  const int64_t per = (nbl + FL_T - 1) / FL_T;
+  const int64_t b0 = (int64_t)tid * per;
+  const int64_t b1 = min(b0 + per, nbl);
+  int64_t sum = 0;
+  for (int64_t b = b0; b < b1; ++b) sum += ld_agent(&bsum[b]);
+  int64_t tot;
+  int64_t run = block_excl_scan(sum, red, &tot);
+  const int64_t blast = last / FK_T;
+  for (int64_t b = b0; b < b1; ++b) {
+    const int64_t v = ld_agent(&bsum[b]);
+    bsum[b] = run;
+    if (b == blast) {
+      // frames up to `last` (tiles after it in its block are dead)
+      const int64_t ml = ld_agent(&rec_meta[last]);
+      const int64_t total = run + ld_agent(&base[last]) + m_cnt(ml);
+      *lastk = last;
+      result[0] = total;
+      result[3] = total > cap ? 1 : 0;
+      if (ft == INF) {
+        result[1] = n;
+        result[2] = 0;
+      } else {
+        result[1] = ld_agent(&rec_exit[ft]);
+        result[2] = m_bad(ml) ? 1 : 0;
+      }
+    }
+    run += v;
+  }
+}
+
+// The small repair: block 0 alone, a worklist instead of rounds over the
+// whole tile array (a 550 MB reply stream has 134K tiles: one workgroup
+// scanning them for broken links costs ~30 us a pass, a grid barrier a few
+// us; a small repair needs neither).  fs_check listed the broken links;
+// each round re-walks the listed ones in parallel (one wave per link, from
+// the exit before it as it stands), then checks the link after every tile
+// it re-wrote — a link only breaks when a tile next to it is re-written,
+// and a walked tile's own link is checked by its walked predecessor — and
+// lists the broken ones (deduplicated in an LDS hash set) for the next
+// round.  An empty list is the fix-point.  Only the count blocks holding a
+// re-written tile are re-counted.  Returns false (nothing lost: the serial
+// tail finishes from the records as they stand) when the list outgrows
+// LDS or the rounds run out.
+constexpr int FL_WL = 1024;                // worklist entries per round
+constexpr int FL_HS = 2048;                // its dedup hash set
+constexpr int FL_WR = 48;                  // rounds before the serial tail
+constexpr int FL_DB = 8192;                // count blocks tracked (2M tiles)
+
+ZK_DEV bool fl_worklist(const uint8_t* __restrict__ buf, int64_t n,
+                        int64_t ntiles, int64_t maxp,
+                        const int64_t* __restrict__ sx,
+                        const uint16_t* __restrict__ list,
+                        const int32_t* __restrict__ rcount, uint16_t* pre,
+                        int64_t* rec_entry, int64_t* rec_exit,
+                        int64_t* rec_meta, int64_t* base, int64_t* bsum,
+                        const int32_t* __restrict__ blist, int nb0,
+                        int64_t ft0, uint8_t* win, uint64_t* stats,
+                        int64_t* ft_out) {
+  __shared__ int32_t wl[2][FL_WL];
+  __shared__ int32_t wk[FL_WL];
+  __shared__ uint32_t hs[FL_HS];
+  __shared__ uint32_t dirty[FL_DB / 32];
+  __shared__ int s_n[3];          // next list, walked, overflow
+  __shared__ int s_cur;
+  __shared__ unsigned long long s_term;       // leftmost new terminal
+  __shared__ int s_healed;                    // fs_check's first one gone
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int64_t INF = INT64_MAX;
+  for (int i = tid; i < FL_DB / 32; i += FL_T) dirty[i] = 0;
+  for (int i = tid; i < nb0; i += FL_T) wl[0][i] = blist[i];
+  if (tid == 0) {
+    s_term = (unsigned long long)INF;
+    s_healed = 0;
+    s_n[2] = 0;
+    s_cur = nb0;
+  }
+  uint8_t* mywin = win + (size_t)wv * (FC_WIN + 16);
+  int cur = 0, rounds = 0;
+  uint32_t walked = 0;
+  __syncthreads();
+  int ncur = s_cur;
+  while (ncur > 0) {
+    if (rounds == FL_WR) break;
+    ++rounds;
+    const int nxt = cur ^ 1;
+    for (int i = tid; i < FL_HS; i += FL_T) hs[i] = 0;
+    if (tid == 0) {
+      s_n[0] = 0;
+      s_n[1] = 0;
+    }
+    __syncthreads();
+    // one lane lists link k for the next round (once)
+    auto push = [&](int64_t k) {
+      const uint32_t key = (uint32_t)k + 1;
+      uint32_t h = (key * 2654435761u) >> (32 - 11);
+      for (;;) {
+        const uint32_t old = atomicCAS(&hs[h], 0u, key);
+        if (old == 0) break;
+        if (old == key) return;
+        h = (h + 1) & (FL_HS - 1);
+      }
+      const int i = atomicAdd(&s_n[0], 1);
+      if (i < FL_WL) wl[nxt][i] = (int32_t)k;
+      else s_n[2] = 1;
+    };
+    // re-walk the listed links
+    for (int j = wv; j < ncur; j += FL_T / 64) {
+      const int64_t k = wl[cur][j];
+      const int64_t E = ld_agent(&rec_exit[k - 1]);
+      if (E < k * FT_S || m_term(ld_agent(&rec_meta[k - 1]))) continue;
+      if (ld_agent(&rec_entry[k]) == E) continue;       // holds by now
+      const int32_t m0 = __builtin_amdgcn_readfirstlane(rcount[k]);
+      const FcWalk fw = fc_walk(buf, n, maxp, k * FT_S, E,
+                                list + k * FT_LMAX, m0, sx[k], mywin,
+                                pre + k * FT_LMAX, lane);
+      ++walked;
+      if (lane == 0) {
+        if (fl_accept(rec_entry, rec_exit, ntiles, k, E, fw.exit)) {
+          st_agent(&rec_entry[k], E);
+          st_agent(&rec_exit[k], fw.exit);
+          st_agent(&rec_meta[k], fc_meta(fw));
+          const int64_t b = k / FK_T;
+          atomicOr(&dirty[b >> 5], 1u << (b & 31));
+          if (fw.term) atomicMin(&s_term, (unsigned long long)k);
+          else if (k == ft0) s_healed = 1;
+          wk[atomicAdd(&s_n[1], 1)] = (int32_t)k;
+        } else {
+          push(k);
+        }
+      }
+    }
+    __syncthreads();
+    // the link after every re-written tile
+    const int nw = s_n[1];
+    for (int j = tid; j < nw; j += FL_T) {
+      const int64_t k = wk[j];
+      if (k + 1 >= ntiles || m_term(ld_agent(&rec_meta[k]))) continue;
+      if (ld_agent(&rec_entry[k + 1]) != ld_agent(&rec_exit[k])) push(k + 1);
+    }
+    __syncthreads();
+    if (tid == 0) s_cur = s_n[2] ? -1 : s_n[0];
+    __syncthreads();
+    ncur = s_cur;
+    cur = nxt;
+    __syncthreads();
+    if (ncur < 0) break;
+  }
+  if (lane == 0 && walked) fc_stat(stats, 2, walked);
+  if (tid == 0 && rounds) fc_stat(stats, 3, rounds);
+  if (ncur != 0) return false;
+  // the first terminal: fs_check's, unless a re-walk made an earlier one or
+  // healed it (then looked up again; rare)
+  int64_t ft = min(ft0, (int64_t)s_term);
+  const bool stale = s_healed ||
+      (s_term != (unsigned long long)INF &&
+       !m_term(ld_agent(&rec_meta[(int64_t)s_term])));
+  if (stale) {
+    int64_t f = INF;
+    for (int64_t k = tid; k < ntiles; k += FL_T)
+      if (m_term(ld_agent(&rec_meta[k]))) { f = k; break; }
+    for (int d = 32; d >= 1; d >>= 1) f = min(f, (int64_t)__shfl_xor(f, d, 64));
+    __shared__ int64_t s_f[FL_T / 64];
+    if (lane == 0) s_f[wv] = f;
+    __syncthreads();
+    ft = INF;
+    for (int j = 0; j < FL_T / 64; ++j) ft = min(ft, s_f[j]);
+  }
+  // re-count the blocks holding a re-written tile: one wave per block,
+  // four tiles per lane
+  const int64_t nbl = (ntiles + FK_T - 1) / FK_T;
+  for (int64_t b = wv; b < nbl; b += FL_T / 64) {
+    if (!((dirty[b >> 5] >> (b & 31)) & 1u)) continue;
+    const int64_t k0 = b * FK_T + 4 * lane;
+    int64_t c[4], s = 0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      c[u] = k0 + u < ntiles ? m_cnt(ld_agent(&rec_meta[k0 + u])) : 0;
+      s += c[u];
+    }
+    int64_t inc = s;
+    for (int d = 1; d < 64; d <<= 1) {
+      const int64_t v = __shfl_up(inc, d, 64);
+      if (lane >= d) inc += v;
+    }
+    int64_t run = inc - s;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (k0 + u < ntiles) st_agent(&base[k0 + u], run);
+      run += c[u];
+    }
+    if (lane == 63) st_agent(&bsum[b], inc);
+  }
+  __syncthreads();
+  *ft_out = ft;
+  return true;
+}
+
 __global__ __launch_bounds__(FL_T) void fs_link(
     const uint8_t* __restrict__ buf, const int64_t* __restrict__ n_dev,
     int64_t n_cap, int64_t maxp, const int64_t* __restrict__ sx,
@@ -911,6 +1181,8 @@ __global__ __launch_bounds__(FL_T) void fs_link(
     int64_t* __restrict__ lastk, unsigned long long* __restrict__ g) {
   __shared__ __attribute__((aligned(16)))
       uint8_t win[(FL_T / 64) * (FC_WIN + 16)];      // one per wave
+  static_assert(FC_TAILWIN <= (FL_T / 64) * (FC_WIN + 16),
+                "the serial tail's window is the waves' windows together");
   __shared__ int64_t red[2 * (FL_T / 64) + 2];
   __shared__ int64_t s_next;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -928,55 +1200,55 @@ __global__ __launch_bounds__(FL_T) void fs_link(
   // clears them for the next scan of this workspace once every block has
   // read them (on the fast path only block 0 goes on, so at once)
   const uint64_t mb0 = mins[0], mt0 = mins[1];
+  const unsigned long long nb0 = g[FL_NB];
   const int64_t fb0 = mb0 ? ntiles - (int64_t)mb0 : INF;
   const int64_t ft0 = mt0 ? ntiles - (int64_t)mt0 : INF;
   const bool fast = fb0 == INF || fb0 > ft0;
+  // a small repair (a handful of broken links, the usual one) is block 0's
+  // worklist; the grid takes part only in a large one (every block decides
+  // alike: block 0 clears the words it read only after the grid's first
+  // barrier, or — without the grid — in a way that reads as "not grid")
+  const bool small = !fast && nb0 <= FL_SMALL &&
+                     (ntiles + FK_T - 1) / FK_T <= FL_DB;
+  const bool grid = !fast && !small;
+  if (!grid && blockIdx.x != 0) return;
   if (fast) {
     // no broken link before the first terminal: the row bases are bsum's
     // block offsets + fs_check's in-block bases
-    if (blockIdx.x != 0) return;
+    __syncthreads();
+    if (tid == 0) {
+      mins[0] = 0;
+      mins[1] = 0;
+      g[FL_NB] = 0;
+    }
+    fl_bases(n, ntiles, ft0, rec_exit, rec_meta, base, bsum, cap, result,
+             lastk, red);
+    return;
+  }
+  bool grid_ok = true;
+  if (small) {
     __syncthreads();
     if (tid == 0) {
       mins[0] = 0;
       mins[1] = 0;
     }
-    const int64_t last = ft0 == INF ? ntiles - 1 : ft0;
-    const int64_t nbl = last / FK_T + 1;
-    const int64_t per = (nbl + FL_T - 1) / FL_T;
-    const int64_t b0 = (int64_t)tid * per;
-    const int64_t b1 = min(b0 + per, nbl);
-    int64_t sum = 0;
-    for (int64_t b = b0; b < b1; ++b) sum += bsum[b];
-    int64_t tot;
-    int64_t run = block_excl_scan(sum, red, &tot);
-    const int64_t blast = last / FK_T;
-    for (int64_t b = b0; b < b1; ++b) {
-      const int64_t v = bsum[b];
-      bsum[b] = run;
-      if (b == blast) {
-        // frames up to `last` (tiles after it in its block are dead)
-        const int64_t ml = rec_meta[last];
-        const int64_t total = run + base[last] + m_cnt(ml);
-        *lastk = last;
-        result[0] = total;
-        result[3] = total > cap ? 1 : 0;
-        if (ft0 == INF) {
-          result[1] = n;
-          result[2] = 0;
-        } else {
-          result[1] = rec_exit[ft0];
-          result[2] = m_bad(ml) ? 1 : 0;
-        }
-      }
-      run += v;
+    int64_t ft;
+    if (fl_worklist(buf, n, ntiles, maxp, sx, list, rcount, pre, rec_entry,
+                    rec_exit, rec_meta, base, bsum, blist, (int)nb0, ft0, win,
+                    stats, &ft)) {
+      if (tid == 0) g[FL_NB] = 0;
+      fl_bases(n, ntiles, ft, rec_exit, rec_meta, base, bsum, cap, result,
+               lastk, red);
+      return;
     }
-    return;
-  }
-  // ---- repair: grid rounds to a fix-point ---------------------------------
-  bool grid_ok = fl_sync(g);                // every block has read the minima
-  if (blockIdx.x == 0 && tid == 0) {
-    mins[0] = 0;
-    mins[1] = 0;
+    grid_ok = false;          // not settled: block 0's serial tail finishes
+  } else {
+    // ---- repair: rounds to a fix-point over the grid ---------------------
+    grid_ok = fl_sync(g);                    // every block read the minima
+    if (blockIdx.x == 0 && tid == 0) {
+      mins[0] = 0;
+      mins[1] = 0;
+    }
   }
   for (int r = 0; r < FL_GROUNDS && grid_ok; ++r)
     grid_ok = fl_round(buf, n, ntiles, maxp, sx, list, rcount, pre,
@@ -1054,9 +1326,9 @@ __global__ __launch_bounds__(FL_T) void fs_link(
           continue;
         }
         const int32_t m0 = __builtin_amdgcn_readfirstlane(rcount[k]);
-        const FcWalk w = fc_walk(buf, n, maxp, k * FT_S, E,
-                                 list + k * FT_LMAX, m0, sx[k], win,
-                                 pre + k * FT_LMAX, lane);
+        const FcWalk w = fc_walk<FC_TAILWIN>(buf, n, maxp, k * FT_S, E,
+                                             list + k * FT_LMAX, m0, sx[k],
+                                             win, pre + k * FT_LMAX, lane);
         ++walked;
         if (lane == 0) {
           st_agent(&rec_entry[k], E);
@@ -1259,7 +1531,8 @@ int64_t zk_frame_scan_workspace(int64_t n) {
 // of it over the same n_cap (fs_rows / fs_link clear what they used), so
 // the memset is skipped.  A stale flag could only cost speed, never
 // correctness (fs_check / fs_link verify every speculated entry).
-// flags bit 0: no speculated tile entries (tests of the link repair).
+// flags (tests of the link repair): bit 0 no speculated tile entries; bits
+// 8..23 P > 0: every P-th tile (t % P == 1) takes a garbage entry.
 int zk_frame_scan5(const uint8_t* buf, const int64_t* n_dev, int64_t n_cap,
                    int64_t maxp, uint8_t* ws, int64_t ws_bytes, int64_t* foff,
                    int32_t* flen, int64_t cap, int64_t* result, int32_t window,
@@ -1302,7 +1575,7 @@ int zk_frame_scan5(const uint8_t* buf, const int64_t* n_dev, int64_t n_cap,
 #define ZK_FS_TILE(WW)                                                       \
   fs_tile<WW><<<tblocks, 64 * tpb, FT_LDS * tpb, st>>>(                      \
       buf, n_dev, n_cap, maxp, list, pre, sx, lbw, rent, rexit, rmeta, rcnt, \
-      tiles, dbg, fs_minb(), flags & 1)
+      tiles, dbg, fs_minb(), flags)
   switch (W) {
     case 256: ZK_FS_TILE(256); break;
     case 512: ZK_FS_TILE(512); break;
@@ -1312,7 +1585,7 @@ int zk_frame_scan5(const uint8_t* buf, const int64_t* n_dev, int64_t n_cap,
 #undef ZK_FS_TILE
   ZK_LAUNCH_CHECK();
   fs_check<<<(unsigned)((tiles + FK_T - 1) / FK_T), FK_T, 0, st>>>(
-      n_dev, n_cap, rent, rexit, rmeta, base, bsum, mins);
+      n_dev, n_cap, rent, rexit, rmeta, base, bsum, mins, grid + FL_NB, blist);
   ZK_LAUNCH_CHECK();
   fs_link<<<FL_B, FL_T, 0, st>>>(buf, n_dev, n_cap, maxp, sx, list, rcnt,
                                  pre, rent, rexit, rmeta, base, cap, result,

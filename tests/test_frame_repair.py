@@ -8,7 +8,11 @@ bounded in time.
 * frames longer than the entry window whose payloads are made of
   plausible length words (garbage chains that never die): the serial tail
   skips the tiles a frame covers whole;
-* variable reply-sized frames (the 0-1024 B GET workload's reply stream).
+* variable reply-sized frames (the 0-1024 B GET workload's reply stream);
+* garbage entries forced into every P-th tile (``misspec``) of a stream
+  whose garbage chains jump megabytes ahead (create replies: an xid or a
+  zxid read as a length): the repair must not carry a garbage exit from
+  tile to tile (the first storm reply stream: 1413 tiles over 71 rounds).
 
 Reference framer: lib/zk-streams.js:47-64 (one frame at a time)."""
 
@@ -39,18 +43,18 @@ def _stream(rng, lens, payload='random'):
     return buf, starts
 
 
-def _scan_timed(buf, nframes, window, nospec=False, reps=3):
+def _scan_timed(buf, nframes, window, nospec=False, reps=3, misspec=0):
     dev = torch.device('cuda', 0)
     d = torch.from_numpy(buf).to(dev)
     sc = B.FrameScanner(nframes + 16, dev, window=window)
-    sc.scan(d, len(buf), nospec=nospec)               # warm
+    sc.scan(d, len(buf), nospec=nospec, misspec=misspec)      # warm
     torch.cuda.synchronize()
     best = None
     for _ in range(reps):
         t0 = torch.cuda.Event(enable_timing=True)
         t1 = torch.cuda.Event(enable_timing=True)
         t0.record()
-        ft = sc.scan(d, len(buf), nospec=nospec)
+        ft = sc.scan(d, len(buf), nospec=nospec, misspec=misspec)
         t1.record()
         torch.cuda.synchronize()
         ms = t0.elapsed_time(t1)
@@ -103,4 +107,58 @@ def test_variable_reply_frames_exact(gpu):
         lens = rng.integers(lo, hi + 1, 40000)
         buf, starts = _stream(rng, lens)
         r, off, ms, st = _scan_timed(buf, len(lens), win, reps=1)
+        _check(r, off, buf, starts)
+
+
+def _create_replies(n, xid0=0x300401, zxid0=0x3f4a2c):
+    """The storm workload's CREATE replies: 50-byte frames {len 46, xid,
+    zxid, err 0, path length 26, '/storm/dNNNNN/e-NNNNNNNNNN'}."""
+    i = np.arange(n, dtype=np.int64)
+    rec = np.zeros((n, 50), np.uint8)
+
+    def be(col, v, w):
+        for b in range(w):
+            rec[:, col + b] = (v >> (8 * (w - 1 - b))) & 0xff
+    be(0, np.full(n, 46), 4)
+    be(4, xid0 + i, 4)
+    be(8, zxid0 + i, 8)
+    be(20, np.full(n, 26), 4)
+    paths = np.frombuffer(b''.join(b'/storm/d%05d/e-%010d' % (k % 100, k)
+                                   for k in range(n)), np.uint8)
+    rec[:, 24:] = paths.reshape(n, 26)
+    return rec.reshape(-1), np.arange(n, dtype=np.int64) * 50
+
+
+@pytest.mark.parametrize('period', [97, 1])
+def test_garbage_entries_do_not_propagate(gpu, period):
+    """Every period-th tile (period 1: every tile) enters on a garbage chain.
+    Few broken links are block 0's worklist, every tile the grid's rounds;
+    either way each broken link settles in a round or two (a garbage exit
+    walked on would cost one round per tile it crosses)."""
+    n = 1 << 20
+    buf, starts = _create_replies(n)
+    _, _, base_ms, _ = _scan_timed(buf, n, 256)
+    r, off, ms, st = _scan_timed(buf, n, 256, misspec=period)
+    _check(r, off, buf, starts)
+    tiles = (len(buf) + 4095) // 4096
+    broken = (tiles - 1) // period
+    scans = 4                                  # warm + 3 timed
+    assert st['rounds'] <= scans * 6, st
+    assert st['rewalked'] <= scans * (3 * broken + 8), st
+    assert ms < max(6 * base_ms, 1.5), (ms, base_ms)
+
+
+def test_garbage_entries_variable_and_long_frames(gpu):
+    rng = np.random.default_rng(8)
+    lens = rng.integers(88, 1113, 40000)
+    buf, starts = _stream(rng, lens)
+    for period in (3, 50):
+        r, off, ms, st = _scan_timed(buf, len(lens), 2048, reps=1,
+                                     misspec=period)
+        _check(r, off, buf, starts)
+    lens = rng.integers(2000, 9001, 3000)
+    buf, starts = _stream(rng, lens, payload='plausible')
+    for period in (2, 7):
+        r, off, ms, st = _scan_timed(buf, len(lens), 256, reps=1,
+                                     misspec=period)
         _check(r, off, buf, starts)

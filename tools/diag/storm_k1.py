@@ -16,8 +16,19 @@ dev = torch.device('cuda', 0)
 batch = 1 << 20
 tree = S.GpuTree(1_000_000, 100, device=dev, seed=0,
                  spare=(batch * 3 + 8192) / 1e6 + 0.05)
+t0 = time.perf_counter()
 pipe = S.StormPipeline(tree, batch, seed=0)
+torch.cuda.synchronize()
+print('init s', round(time.perf_counter() - t0, 3))
 d = pipe.drv
+# chain counters of the scans run so far (create_dirs + the first step)
+print('reply scanner', d.rscanner.chain_stats(), 'request scanner',
+      d.server.scanner.chain_stats(), flush=True)
+for k in range(3):
+    pipe.step(validate=False)
+    torch.cuda.synchronize()
+    print('step', k, 'reply scanner', d.rscanner.chain_stats(),
+          'request scanner', d.server.scanner.chain_stats(), flush=True)
 rb, rep = pipe.last
 # re-scan the reply stream of that first step from the server's buffer
 out, total, _, _ = d.server.result

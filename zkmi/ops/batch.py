@@ -350,11 +350,12 @@ class FrameScanner:
         self.ws_for = -1            # stream length the workspace covers
         self.clean_for = -1         # n_cap whose flags the last scan cleared
 
-    def scan(self, buf, n, stream=None, nospec=False):
+    def scan(self, buf, n, stream=None, nospec=False, misspec=0):
         """Frame ``buf[:n]``; ``n`` may be a device int64 length (see
         :func:`frame_scan`) — then nothing is read back to the host.
         ``nospec`` (tests): no tile takes a speculated entry, every link
-        goes through the repair."""
+        goes through the repair; ``misspec`` = P > 0 (tests): every P-th
+        tile takes a garbage entry (one byte past the speculated one)."""
         L = _lib.lib()
         n_dev, ncap = _scan_len(buf, n)
         if ncap > self.ws_for:
@@ -370,7 +371,8 @@ class FrameScanner:
         with _on(stream):
             L.frame_scan(buf, n_dev, ncap, self.max_packet, self.ws, t.off,
                          t.length, t.result, int(self.window),
-                         ncap == self.clean_for, 1 if nospec else 0)
+                         ncap == self.clean_for,
+                         (1 if nospec else 0) | (int(misspec) << 8))
         self.clean_for = ncap
         self.last_cap = ncap
         return t

@@ -60,7 +60,10 @@ ZK_DEV bool read_stat(const uint8_t* p, const ZkReplyOut& o, int64_t i) {
 // Optional fused check of GET_DATA replies against the requests that were
 // sent (the benchmark's validation, otherwise a separate pass over the SoA
 // it just wrote): reply i must be a clean GET_DATA success for request i —
-// same xid, the node's czxid (idx + 1) and data length.  Counts go to
+// same xid, the node's czxid (idx + 1) and data length; with `slab` also
+// the payload BYTES of one reply in 16 (which ones rotates with the step
+// counter), compared against the node's slot in the tree's slab — a
+// corrupted copy that keeps the length fails the check.  Counts go to
 // acc[block % slots] (one atomic per block, spread over the slots so the
 // blocks of a launch do not queue on one word).
 struct ZkGetCheck {
@@ -71,7 +74,30 @@ struct ZkGetCheck {
   int32_t slots;
   int64_t* tick;   // optional: tick[1] += 1 once per launch (a captured
                    // graph's step counter, see bench_gen_get's state)
+  const uint8_t* slab;        // optional: the payload sample's reference
+  const int64_t* slot_off;
 };
+constexpr int CHK_SAMPLE = 16;
+
+// n bytes at a (any alignment, readable up to 3 bytes past a + n: a reply's
+// data is followed by its Stat) equal n bytes at b (4-byte aligned)?
+// Aligned dword loads funnel-shifted into place, then the tail bytes.
+ZK_DEV bool bytes_equal(const uint8_t* a, const uint8_t* b, int32_t n) {
+  const uintptr_t ua = (uintptr_t)a;
+  const uint32_t* wa = (const uint32_t*)(ua & ~(uintptr_t)3);
+  const uint32_t* wb = (const uint32_t*)b;
+  const uint32_t sh = (uint32_t)(ua & 3);
+  const int32_t nw = n >> 2;
+  uint32_t diff = 0;
+  uint32_t lo = wa[0];
+  for (int32_t k = 0; k < nw; ++k) {
+    const uint32_t hi = wa[k + 1];
+    diff |= __builtin_amdgcn_alignbyte(hi, lo, sh) ^ wb[k];
+    lo = hi;
+  }
+  for (int32_t j = nw * 4; j < n; ++j) diff |= (uint32_t)(a[j] ^ b[j]);
+  return diff == 0;
+}
 
 template <bool CHECK>
 __global__ __launch_bounds__(DEC_T) void decode_replies_k(
@@ -84,6 +110,8 @@ __global__ __launch_bounds__(DEC_T) void decode_replies_k(
   const bool live = i < ncap && i < *n_dev;
   if (!CHECK && !live) return;
   int64_t good = 0;
+  // the payload sample of this step (read before block 0 advances tick)
+  const int64_t salt = CHECK && chk.tick != nullptr ? chk.tick[1] : 0;
   if (live) {
   const uint8_t* p = buf + foff[i];
   const int64_t L = flen[i];
@@ -210,6 +238,10 @@ __global__ __launch_bounds__(DEC_T) void decode_replies_k(
     const int64_t v = chk.idx[i];
     good = xid == chk.xid[i] && o.stat64[i] == v + 1 &&
            plen == chk.data_len[v];
+    if (good && chk.slab != nullptr &&
+        ((i + salt) & (CHK_SAMPLE - 1)) == 0)
+      good = bytes_equal(buf + poff, chk.slab + chk.slot_off[v] + ZK_SLOT_DATA,
+                         plen);
   }
   }  // live
   if (CHECK) {
@@ -340,26 +372,33 @@ int zk_decode_replies(const uint8_t* buf, const int64_t* foff,
   if (ncap <= 0) return 0;
   zk::decode_replies_k<false><<<zk::nblk(ncap), zk::DEC_T, 0, st>>>(
       buf, foff, flen, n_dev, ncap, xid_tab, xid_mask, *o,
-      zk::ZkGetCheck{nullptr, nullptr, nullptr, nullptr, 1, nullptr});
+      zk::ZkGetCheck{nullptr, nullptr, nullptr, nullptr, 1, nullptr, nullptr,
+                     nullptr});
   ZK_LAUNCH_CHECK();
   return 0;
 }
 
 // zk_decode_replies + the fused GET_DATA check (ZkGetCheck): idx / xid are
 // the requests sent (ncap of them), data_len the tree's per-node lengths,
-// acc `slots` (1..64) int64 counters the caller sums.
-int zk_decode_replies_check(const uint8_t* buf, const int64_t* foff,
-                            const int32_t* flen, const int64_t* n_dev,
-                            int64_t ncap, const int64_t* xid_tab,
-                            int64_t xid_mask, const ZkReplyOut* o,
-                            const int64_t* idx, const int32_t* xid,
-                            const int32_t* data_len, unsigned long long* acc,
-                            int32_t slots, int64_t* tick, hipStream_t st) {
+// acc `slots` (1..64) int64 counters the caller sums; slab / slot_off
+// (optional, both or neither): the tree's node slots, for the sampled
+// payload comparison.
+int zk_decode_replies_check2(const uint8_t* buf, const int64_t* foff,
+                             const int32_t* flen, const int64_t* n_dev,
+                             int64_t ncap, const int64_t* xid_tab,
+                             int64_t xid_mask, const ZkReplyOut* o,
+                             const int64_t* idx, const int32_t* xid,
+                             const int32_t* data_len, unsigned long long* acc,
+                             int32_t slots, int64_t* tick,
+                             const uint8_t* slab, const int64_t* slot_off,
+                             hipStream_t st) {
   if (ncap <= 0) return 0;
   if (slots < 1 || slots > 64) return (int)hipErrorInvalidValue;
+  if ((slab == nullptr) != (slot_off == nullptr))
+    return (int)hipErrorInvalidValue;
   zk::decode_replies_k<true><<<zk::nblk(ncap), zk::DEC_T, 0, st>>>(
       buf, foff, flen, n_dev, ncap, xid_tab, xid_mask, *o,
-      zk::ZkGetCheck{idx, xid, data_len, acc, slots, tick});
+      zk::ZkGetCheck{idx, xid, data_len, acc, slots, tick, slab, slot_off});
   ZK_LAUNCH_CHECK();
   return 0;
 }

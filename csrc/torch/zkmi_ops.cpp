@@ -85,11 +85,12 @@ int zk_frame_scan_dbg(int64_t* host, int64_t tiles);
 int zk_decode_replies(const uint8_t*, const int64_t*, const int32_t*,
                       const int64_t*, int64_t, const int64_t*, int64_t,
                       const ZkReplyOut*, hipStream_t);
-int zk_decode_replies_check(const uint8_t*, const int64_t*, const int32_t*,
-                            const int64_t*, int64_t, const int64_t*, int64_t,
-                            const ZkReplyOut*, const int64_t*, const int32_t*,
-                            const int32_t*, unsigned long long*, int32_t,
-                            int64_t*, hipStream_t);
+int zk_decode_replies_check2(const uint8_t*, const int64_t*, const int32_t*,
+                             const int64_t*, int64_t, const int64_t*, int64_t,
+                             const ZkReplyOut*, const int64_t*, const int32_t*,
+                             const int32_t*, unsigned long long*, int32_t,
+                             int64_t*, const uint8_t*, const int64_t*,
+                             hipStream_t);
 int zk_expand_strings(const uint8_t*, const int64_t*, const int32_t*,
                       const int64_t*, int64_t, int64_t*, int32_t*,
                       hipStream_t);
@@ -550,19 +551,28 @@ void decode_replies(const Tensor& buf, const Tensor& foff, const Tensor& flen,
 
 // decode_replies + the fused GET_DATA check (bench validation): request i
 // was (idx[i], xid[i]); counts of good replies go to acc (1..64 slots,
-// summed by the caller).
+// summed by the caller).  slab + slot_off (the tree's node slots): one
+// reply in 16 also has its payload bytes compared with its node's.
 void decode_replies_check(const Tensor& buf, const Tensor& foff,
                           const Tensor& flen, const Tensor& n_dev,
                           const Tensor& xid_tab, int64_t xid_mask,
                           const std::vector<Tensor>& out, const Tensor& idx,
                           const Tensor& xid, const Tensor& data_len,
                           const Tensor& acc,
-                          const c10::optional<Tensor>& tick) {
+                          const c10::optional<Tensor>& tick,
+                          const c10::optional<Tensor>& slab,
+                          const c10::optional<Tensor>& slot_off) {
   const int64_t cap = foff.numel();
   ZkReplyOut o = reply_out(out, cap, &buf);
   const int32_t slots = (int32_t)std::min<int64_t>(acc.numel(), 64);
   TORCH_CHECK(slots >= 1, "zkmi: decode_replies_check needs an acc slot");
-  hip_ok(zk_decode_replies_check(
+  TORCH_CHECK(slab.has_value() == slot_off.has_value(),
+              "zkmi: decode_replies_check: slab and slot_off go together");
+  // every slot_off entry the sampled idx can reach lies in data_len's range
+  if (slot_off.has_value())
+    TORCH_CHECK(slot_off->numel() >= data_len.numel(),
+                "zkmi: decode_replies_check: slot_off shorter than data_len");
+  hip_ok(zk_decode_replies_check2(
              P<uint8_t>(buf, U8, 1, "buf"),
              P<int64_t>(foff, I64, cap, "frame_off", &buf),
              P<int32_t>(flen, I32, cap, "frame_len", &buf),
@@ -573,7 +583,9 @@ void decode_replies_check(const Tensor& buf, const Tensor& foff,
              P<int32_t>(data_len, I32, 1, "data_len", &buf),
              reinterpret_cast<unsigned long long*>(
                  P<int64_t>(acc, I64, slots, "acc", &buf)),
-             slots, Popt<int64_t>(tick, I64, 2, "tick", &buf), cur_stream()),
+             slots, Popt<int64_t>(tick, I64, 2, "tick", &buf),
+             Popt<uint8_t>(slab, U8, 1, "slab", &buf),
+             Popt<int64_t>(slot_off, I64, 1, "slot_off", &buf), cur_stream()),
          "decode_replies_check");
 }
 
@@ -1039,7 +1051,8 @@ TORCH_LIBRARY(zkmi, m) {
   m.def("decode_replies_check(Tensor buf, Tensor frame_off, Tensor frame_len, "
         "Tensor count, Tensor xid_tab, int xid_mask, Tensor(a!)[] out, "
         "Tensor idx, Tensor xid, Tensor data_len, Tensor(b!) acc, "
-        "Tensor(c!)? tick=None) -> ()",
+        "Tensor(c!)? tick=None, Tensor? slab=None, Tensor? slot_off=None) "
+        "-> ()",
         &decode_replies_check);
   m.def("expand_strings(Tensor buf, Tensor region, Tensor count, "
         "Tensor base, Tensor(a!) str_off, Tensor(b!) str_len) -> ()",

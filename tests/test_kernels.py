@@ -480,6 +480,39 @@ def test_gpu_get_pipeline_end_to_end(gpu):
         assert bytes(hb[po[k]:po[k] + 37].tobytes()) == data
 
 
+def test_gpu_get_check_samples_payload_bytes(gpu):
+    """The fused GET check compares the payload bytes of one reply in 16
+    with its node's slot: a reply stream whose every payload has one byte
+    flipped keeps its lengths, and fails exactly the sampled replies."""
+    from zkmi.bench.synthetic import GetPipeline
+    from zkmi.ops import batch as B
+    tree = _small_tree(gpu, 20000, 37)
+    n = 8192
+    pipe = GetPipeline(tree, n)
+    pipe.step()
+    idx, rep, rx, ft = pipe.last
+
+    def check(buf, tick=None):
+        acc = torch.zeros(1, dtype=torch.int64, device=gpu)
+        B.decode_replies(buf, ft, pipe.xt, check=(idx, pipe.xid,
+                                                  tree.data_len, acc,
+                                                  tree.slab_all,
+                                                  tree.slot_off), tick=tick)
+        return int(acc.item())
+    assert check(rx) == n
+    bad = rx.clone()
+    po = rep.pay_off[:n]
+    bad[po + 5] ^= 0x5A
+    assert check(bad) == n - (n + 15) // 16
+    # the sample rotates with the step counter: salt 3 -> i % 16 == 13
+    tick = torch.tensor([0, 3], dtype=torch.int64, device=gpu)
+    assert check(bad, tick) == n - len(range(13, n, 16))
+    # the flipped byte of an unsampled reply goes unnoticed, by design
+    one = rx.clone()
+    one[po[1] + 5] ^= 0x5A
+    assert check(one) == n
+
+
 def test_gpu_get_pipeline_two_connections(gpu):
     """The bench's default shape: the batch split over two pipelined
     connections (own HIP streams, buffers, xid tables), no host read-back

@@ -24,11 +24,36 @@ d = pipe.drv
 # chain counters of the scans run so far (create_dirs + the first step)
 print('reply scanner', d.rscanner.chain_stats(), 'request scanner',
       d.server.scanner.chain_stats(), flush=True)
+def rescan(out, n, sc, tag):
+    if hasattr(sc, 'last_cap'):
+        sc.chain_stats()
+    t0 = time.perf_counter()
+    ft = sc.scan(out, n)
+    torch.cuda.synchronize()
+    el = (time.perf_counter() - t0) * 1e3
+    print(tag, 'scan ms', round(el, 3), ft.host_result(), sc.chain_stats(),
+          flush=True)
+
+
 for k in range(3):
     pipe.step(validate=False)
     torch.cuda.synchronize()
     print('step', k, 'reply scanner', d.rscanner.chain_stats(),
           'request scanner', d.server.scanner.chain_stats(), flush=True)
+    out, total, _, _ = d.server.result
+    n = int(total.item())
+    if k == 0:
+        keep = out[:n].clone()
+        np.savez_compressed('gpurun_out/storm_step0_reply.npz',
+                            raw=keep.cpu().numpy())
+        # the same stream again: the pipeline's own scanner (reused
+        # workspace), a fresh one, and the pipeline's scanner once more
+        rescan(out, n, d.rscanner, 'step0 again, pipeline scanner')
+        rescan(keep, n, B.FrameScanner(batch + 16, dev, window=d.rwindow),
+               'step0 copy, fresh scanner')
+        rescan(out, n, d.rscanner, 'step0 third, pipeline scanner')
+        print('pipeline scanner window', d.rwindow, 'cap', d.rscanner.cap,
+              'ws_for', d.rscanner.ws_for, 'buf numel', out.numel(), flush=True)
 rb, rep = pipe.last
 # re-scan the reply stream of that first step from the server's buffer
 out, total, _, _ = d.server.result

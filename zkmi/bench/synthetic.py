@@ -636,7 +636,8 @@ class GetPipeline(object):
         if parent is not None:
             validate, acc = parent._validate, parent._acc
         # the reply check rides in the decode kernel (acc: 1..64 slots)
-        chk = (self.idx, xid, t.data_len, acc) if validate else None
+        chk = (self.idx, xid, t.data_len, acc, t.slab_all,
+               t.slot_off) if validate else None
         # the device step counter advances in the checking decode (one
         # launch less per step), else on its own
         rep = B.decode_replies(rx, ft, self.xt, out=self.reply, check=chk,

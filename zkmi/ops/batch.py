@@ -468,10 +468,12 @@ def decode_replies(buf, frames, xid_table, out=None, stream=None,
                    check=None, tick=None):
     """K2-K8: decode every frame of ``frames`` as a reply.
 
-    ``check = (idx, xid, data_len, acc)``: also count, in the same kernel,
-    the replies that are clean GET_DATA successes for the requests sent
-    (request i = node idx[i] with xid[i]; czxid idx + 1 and the node's data
-    length) into ``acc`` (int64, 1..64 slots the caller sums).  ``tick``
+    ``check = (idx, xid, data_len, acc[, slab, slot_off])``: also count, in
+    the same kernel, the replies that are clean GET_DATA successes for the
+    requests sent (request i = node idx[i] with xid[i]; czxid idx + 1 and
+    the node's data length) into ``acc`` (int64, 1..64 slots the caller
+    sums); with the tree's ``slab`` / ``slot_off`` one reply in 16 (rotating
+    with ``tick``) must also carry its node's payload bytes.  ``tick``
     (int64 [2], with ``check``): ``tick[1]`` advances by one in the same
     kernel (the device step counter of a captured pipeline)."""
     L = _lib.lib()
@@ -484,11 +486,12 @@ def decode_replies(buf, frames, xid_table, out=None, stream=None,
             L.decode_replies(buf, frames.off, frames.length, frames.count,
                              xid_table.tab, xid_table.mask, out.tensors())
         else:
-            idx, xid, data_len, acc = check
+            idx, xid, data_len, acc = check[:4]
+            slab, slot_off = check[4:6] if len(check) > 4 else (None, None)
             L.decode_replies_check(buf, frames.off, frames.length,
                                    frames.count, xid_table.tab,
                                    xid_table.mask, out.tensors(), idx, xid,
-                                   data_len, acc, tick)
+                                   data_len, acc, tick, slab, slot_off)
     return out
 
 

@@ -330,7 +330,8 @@ class _Conn(object):
         else:
             crx, ncrx = rout, rtotal
         cft = self.rscanner.scan(crx, ncrx)
-        chk = (self.idx_s, self.xid_s, t.data_len, acc) if validate else None
+        chk = (self.idx_s, self.xid_s, t.data_len, acc, t.slab_all,
+               t.slot_off) if validate else None
         rep = B.decode_replies(crx, cft, self.xt, out=self.reply, check=chk,
                                tick=self.gstate if validate else None)
         if self.gstate is not None and not validate:

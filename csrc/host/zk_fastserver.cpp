@@ -1,14 +1,34 @@
 // zk_fastserver — a native ZooKeeper wire server for client benchmarks.
 //
 // The in-process fake server (zkmi/server/fakezk.py) implements the whole
-// Appendix-D contract (watches, ensembles, fault hooks) in Python; at tens
-// of thousands of requests per second it, not the client, would be what a
-// pipelined client benchmark measures.  This server speaks the same wire
-// protocol from a pool of epoll threads: handshake (new and resumed sessions),
-// PING, GET_DATA, EXISTS, SET_DATA (version CAS), CREATE (persistent,
-// EPHEMERAL, SEQUENTIAL), DELETE, SYNC, GET_CHILDREN(2), CLOSE_SESSION.  No
-// watches (requests with watch=1 are served, the watch is not kept), no
-// ACL checks, no expiry: a data-plane server for throughput and RTT runs.
+// Appendix-D contract in Python; at tens of thousands of requests per second
+// it, not the client, would be what a pipelined client benchmark measures.
+// This server speaks the same wire protocol from a pool of epoll threads:
+// handshake (new and resumed sessions), PING, GET_DATA, EXISTS, SET_DATA
+// (version CAS), CREATE (persistent, EPHEMERAL, SEQUENTIAL), DELETE, SYNC,
+// GET_CHILDREN(2), CLOSE_SESSION, and watches: GET_DATA / EXISTS /
+// GET_CHILDREN(2) with watch=1 arm one-shot watches, writes fire
+// NODE_CREATED / NODE_DELETED / NODE_DATA_CHANGED / NODE_CHILDREN_CHANGED
+// notifications (xid -1) with fakezk.py's trigger table, SET_WATCHES
+// re-arms them and catches up on changes after relZxid (SURVEY Appendix D;
+// reference client side: lib/zk-session.js:558-574, :421-471).  A
+// session's watches live with its connection (as on a real ZooKeeper
+// server: a client that moves re-arms them with SET_WATCHES).  No ACL
+// checks, no expiry.
+//
+// --members M: M listening ports sharing one tree and session table (the
+// 3-server ensemble of test/multi-node.test.js, BASELINE config 4); stdin
+// then carries fakezk's ensemble fault commands, one per line, each
+// answered by one line:
+//   outage <i> [<path>=<hexdata> ...]  close member i's connections and its
+//                                      port, then apply the sets (firing
+//                                      watches); answers "OK <zxid>"
+//   start <i>                          listen on member i's port again
+//
+// Notifications to a connection served by another worker go through that
+// connection's note buffer (its own mutex) and the worker's eventfd; every
+// burst drains the notes before serving, so a notification always precedes
+// the reply to any request served after the write that fired it.
 //
 // Every readable burst is answered with one send(): all complete frames of
 // the burst are served in order (ZooKeeper answers a session's requests in
@@ -23,11 +43,11 @@
 // ~1.4 M GETs/s — the bound of the bulk TCP benchmark.)
 //
 // Usage: zk_fastserver [--port P] [--preload N] [--data-bytes B]
-//                      [--fanout F] [--threads T]
+//                      [--fanout F] [--threads T] [--members M]
 // --preload creates /bench, /bench/dDDDDDD and N leaves
 // /bench/dDDDDDD/nNNNNNNNNN with B bytes of data each (the layout of
-// zkmi/bench/synthetic.py GpuTree).  Prints "PORT <n>" once listening and
-// exits when stdin reaches EOF.
+// zkmi/bench/synthetic.py GpuTree).  Prints "PORT <n>" (M = 1) or
+// "PORTS <p1> ... <pM>" once listening and exits when stdin reaches EOF.
 #include <arpa/inet.h>
 #include <errno.h>
 #include <fcntl.h>
@@ -62,6 +82,10 @@ enum : int32_t {
   OP_SET_DATA = 5, OP_GET_ACL = 6, OP_GET_CHILDREN = 8, OP_SYNC = 9,
   OP_PING = 11, OP_GET_CHILDREN2 = 12, OP_SET_WATCHES = 101,
   OP_CLOSE_SESSION = -11
+};
+enum : int32_t {           // notification types, state SyncConnected
+  EV_CREATED = 1, EV_DELETED = 2, EV_DATA_CHANGED = 3,
+  EV_CHILDREN_CHANGED = 4, ST_SYNC_CONNECTED = 3
 };
 enum : int32_t {
   E_OK = 0, E_MARSHALLING = -5, E_UNIMPLEMENTED = -6, E_BAD_ARGUMENTS = -8,
@@ -134,6 +158,21 @@ struct Wr {
   }
 };
 
+struct Worker;
+
+struct Conn {
+  int fd;
+  int member = 0;
+  bool hs = false;
+  bool closing = false;
+  int64_t sid = 0;
+  std::string in, out;
+  size_t in_off = 0, out_off = 0;
+  Worker* w = nullptr;
+  std::mutex nmu;        // notes: notifications from other workers' writes
+  std::string notes;
+};
+
 struct Server {
   std::shared_mutex mu;          // the tree and the session table
   std::unordered_map<std::string, std::unique_ptr<Node>> nodes;
@@ -141,6 +180,18 @@ struct Server {
   int64_t zxid = 1;
   int64_t next_sid = 1;
   uint64_t pw_state = 0x9E3779B97F4A7C15ull;
+  // watches (under wmu; readers arm them under the shared tree lock):
+  // path -> watching sessions, data (also exist watches of missing nodes,
+  // as fakezk.py keeps them) and child; the session's connection route;
+  // the (table, path) pairs a session armed, to drop them with its
+  // connection
+  std::mutex wmu;
+  std::unordered_map<std::string, std::set<int64_t>> wdata, wchild;
+  std::unordered_map<int64_t, Conn*> route;
+  std::unordered_map<int64_t, std::set<std::pair<int, std::string>>> armed;
+  std::atomic<uint64_t> n_notes{0};
+  // members: connections per member (under mu, exclusive to change)
+  std::vector<std::set<Conn*>> mconns;
 
   Node* find(const std::string& p) {
     auto it = nodes.find(p);
@@ -184,12 +235,105 @@ struct Server {
     return s;
   }
 
-  // One request frame body -> one reply appended to `o`.  Returns false
+  // -- watches (callers hold wmu) --------------------------------------------
+  void arm(int table, const std::string& path, int64_t sid) {
+    (table == 0 ? wdata : wchild)[path].insert(sid);
+    armed[sid].emplace(table, path);
+  }
+  // A notification frame for `sid`'s connection: `self` (the connection
+  // being served) gets it in its output now, ahead of the reply being
+  // built; another connection through its notes and its worker.
+  void notify(int64_t sid, int32_t type, const std::string& path, Conn* self);
+  // Fire and clear table[path]'s watches; returns the sessions notified.
+  std::set<int64_t> trigger(int table, const std::string& path, int32_t type,
+                            Conn* self, const std::set<int64_t>* skip) {
+    auto& tab = table == 0 ? wdata : wchild;
+    auto it = tab.find(path);
+    std::set<int64_t> fired;
+    if (it == tab.end()) return fired;
+    std::set<int64_t> sids;
+    sids.swap(it->second);
+    tab.erase(it);
+    for (int64_t sid : sids) {
+      auto a = armed.find(sid);
+      if (a != armed.end()) a->second.erase({table, path});
+      if (skip != nullptr && skip->count(sid)) continue;
+      notify(sid, type, path, self);
+      fired.insert(sid);
+    }
+    return fired;
+  }
+  // A session's connection is gone: its watches go with it.
+  void drop_watches(int64_t sid) {
+    auto a = armed.find(sid);
+    if (a == armed.end()) return;
+    for (const auto& tp : a->second) {
+      auto& tab = tp.first == 0 ? wdata : wchild;
+      auto it = tab.find(tp.second);
+      if (it == tab.end()) continue;
+      it->second.erase(sid);
+      if (it->second.empty()) tab.erase(it);
+    }
+    armed.erase(a);
+  }
+
+  // -- writes (exclusive tree lock; they take wmu to fire) -------------------
+  int32_t set_data(const std::string& p, const uint8_t* d, int32_t dl,
+                   int32_t ver, Conn* self, Node** out) {
+    Node* nd = find(p);
+    if (nd == nullptr) return E_NO_NODE;
+    if (ver != -1 && ver != nd->st.version) return E_BAD_VERSION;
+    nd->data.assign((const char*)d, dl);
+    nd->st.version++;
+    nd->st.mzxid = ++zxid;
+    nd->st.mtime = now_ms();
+    nd->st.dlen = dl;
+    {
+      std::lock_guard<std::mutex> g(wmu);
+      trigger(0, p, EV_DATA_CHANGED, self, nullptr);
+    }
+    *out = nd;
+    return E_OK;
+  }
+
+  // SET_WATCHES (relZxid, data, exist, child path lists): re-arm, and fire
+  // at once what changed after relZxid (fakezk.py set_watches).
+  void set_watches(Rd& r, int64_t sid, Conn* self) {
+    const int64_t rel = r.i64();
+    std::lock_guard<std::mutex> g(wmu);
+    for (int list = 0; list < 3 && r.ok; ++list) {
+      const int32_t cnt = r.i32();
+      for (int32_t k = 0; k < cnt && r.ok; ++k) {
+        const uint8_t* s; int32_t l;
+        if (!r.buf(&s, &l)) break;
+        const std::string path((const char*)s, l);
+        Node* nd = find(path);
+        if (list == 0) {
+          if (nd == nullptr) notify(sid, EV_DELETED, path, self);
+          else if (nd->st.mzxid > rel) notify(sid, EV_DATA_CHANGED, path, self);
+          else arm(0, path, sid);
+        } else if (list == 1) {
+          if (nd != nullptr) notify(sid, EV_CREATED, path, self);
+          else arm(0, path, sid);
+        } else {
+          if (nd == nullptr) notify(sid, EV_DELETED, path, self);
+          else if (nd->st.pzxid > rel)
+            notify(sid, EV_CHILDREN_CHANGED, path, self);
+          else arm(1, path, sid);
+        }
+      }
+    }
+  }
+
+  // One request frame body -> one reply appended to c->out.  Returns false
   // when the connection must close after this reply (CLOSE_SESSION).
-  bool serve(const uint8_t* b, int32_t n, int64_t sid, std::string* o,
-             std::string* key) {
+  bool serve(const uint8_t* b, int32_t n, Conn* c, std::string* key) {
+    const int64_t sid = c->sid;
+    std::string* o = &c->out;
     Rd r{b, b + n};
     const int32_t xid = r.i32(), op = r.i32();
+    // a SET_WATCHES catch-up notifies this connection before its reply
+    if (op == OP_SET_WATCHES && r.ok) set_watches(r, sid, c);
     Wr w{o};
     const size_t at = o->size();
     w.i32(0);                      // frame length, patched below
@@ -214,7 +358,14 @@ struct Server {
         case OP_CLOSE_SESSION: keep = false; break;
         case OP_GET_DATA: case OP_EXISTS: {
           if (!path()) { err = E_MARSHALLING; break; }
+          const bool watch = r.boolean();
           Node* nd = find(*key);
+          // EXISTS arms on a missing node too (an exist watch); GET_DATA
+          // only on a node it returns
+          if (watch && (nd != nullptr || op == OP_EXISTS)) {
+            std::lock_guard<std::mutex> g(wmu);
+            arm(0, *key, sid);
+          }
           if (nd == nullptr) { err = E_NO_NODE; break; }
           if (op == OP_GET_DATA) w.buf(nd->data.data(), nd->data.size());
           w.stat(nd->st);
@@ -222,8 +373,13 @@ struct Server {
         }
         case OP_GET_CHILDREN: case OP_GET_CHILDREN2: {
           if (!path()) { err = E_MARSHALLING; break; }
+          const bool watch = r.boolean();
           Node* nd = find(*key);
           if (nd == nullptr) { err = E_NO_NODE; break; }
+          if (watch) {
+            std::lock_guard<std::mutex> g(wmu);
+            arm(1, *key, sid);
+          }
           w.i32((int32_t)nd->kids.size());
           for (const auto& k : nd->kids) {
             w.i32((int32_t)k.size());
@@ -242,15 +398,21 @@ struct Server {
           const uint8_t* d; int32_t dl;
           if (!path() || !r.buf(&d, &dl)) { err = E_MARSHALLING; break; }
           const int32_t ver = r.i32();
-          Node* nd = find(*key);
-          if (nd == nullptr) { err = E_NO_NODE; break; }
-          if (ver != -1 && ver != nd->st.version) { err = E_BAD_VERSION; break; }
-          nd->data.assign((const char*)d, dl);
-          nd->st.version++;
-          nd->st.mzxid = ++zxid;
-          nd->st.mtime = now_ms();
-          nd->st.dlen = dl;
-          w.stat(nd->st);
+          Node* nd = nullptr;
+          // (a notification to this connection lands before the reply:
+          // the reply frame is moved after it)
+          const size_t mark = o->size();
+          err = set_data(*key, d, dl, ver, c, &nd);
+          if (err == E_OK) {
+            if (o->size() != mark) {
+              std::string note = o->substr(mark);
+              o->resize(mark);
+              o->insert(at, note);
+              return finish(o, at + note.size(), zat + note.size(),
+                            eat + note.size(), E_OK, &nd->st, keep);
+            }
+            w.stat(nd->st);
+          }
           break;
         }
         case OP_CREATE: {
@@ -267,7 +429,8 @@ struct Server {
               (key->size() > 1 && key->back() == '/' && !(flags & 2))) {
             err = E_BAD_ARGUMENTS; break;
           }
-          Node* par = find(parent_of(*key));
+          const std::string ppath = parent_of(*key);
+          Node* par = find(ppath);
           if (par == nullptr) { err = E_NO_NODE; break; }
           if (par->st.eph != 0) { err = E_NO_CHILDREN_FOR_EPHEMERALS; break; }
           if (flags & 2) {
@@ -277,8 +440,22 @@ struct Server {
           }
           if (find(*key) != nullptr) { err = E_NODE_EXISTS; break; }
           make(*key, (const char*)d, dl, (flags & 1) ? sid : 0);
+          std::string note;
+          {
+            std::lock_guard<std::mutex> g(wmu);
+            const size_t mark = o->size();
+            trigger(0, *key, EV_CREATED, c, nullptr);
+            trigger(1, ppath, EV_CHILDREN_CHANGED, c, nullptr);
+            note = o->substr(mark);
+            o->resize(mark);
+          }
           w.i32((int32_t)key->size());
           o->append(*key);
+          if (!note.empty()) {
+            o->insert(at, note);
+            return finish(o, at + note.size(), zat + note.size(),
+                          eat + note.size(), E_OK, nullptr, keep);
+          }
           break;
         }
         case OP_DELETE: {
@@ -289,7 +466,8 @@ struct Server {
           if (ver != -1 && ver != nd->st.version) { err = E_BAD_VERSION; break; }
           if (!nd->kids.empty()) { err = E_NOT_EMPTY; break; }
           const int64_t z = ++zxid;
-          Node* par = find(parent_of(*key));
+          const std::string ppath = parent_of(*key);
+          Node* par = find(ppath);
           if (par != nullptr) {
             par->kids.erase(key->substr(key->rfind('/') + 1));
             par->st.nkids = (int32_t)par->kids.size();
@@ -297,14 +475,37 @@ struct Server {
             par->st.pzxid = z;
           }
           nodes.erase(*key);
+          std::string note;
+          {
+            std::lock_guard<std::mutex> g(wmu);
+            const size_t mark = o->size();
+            const std::set<int64_t> done =
+                trigger(0, *key, EV_DELETED, c, nullptr);
+            trigger(1, *key, EV_DELETED, c, &done);
+            trigger(1, ppath, EV_CHILDREN_CHANGED, c, nullptr);
+            note = o->substr(mark);
+            o->resize(mark);
+          }
+          if (!note.empty()) {
+            o->insert(at, note);
+            return finish(o, at + note.size(), zat + note.size(),
+                          eat + note.size(), E_OK, nullptr, keep);
+          }
           break;
         }
         default: err = E_UNIMPLEMENTED;
       }
     }
+    return finish(o, at, zat, eat, err, nullptr, keep);
+  }
+
+  // Patch a reply frame's header (the zxid after the request, err, length);
+  // `st` (SET_DATA behind a notification): the Stat still to append.
+  bool finish(std::string* o, size_t at, size_t zat, size_t eat, int32_t err,
+              const Stat* st, bool keep) {
     if (err != E_OK) o->resize(eat + 4);          // header only
-    // the header zxid is the one after this request
-    int64_t z = zxid;
+    else if (st != nullptr) Wr{o}.stat(*st);
+    const int64_t z = zxid;
     uint32_t hi = htonl((uint32_t)(z >> 32)), lo = htonl((uint32_t)z);
     memcpy(&(*o)[zat], &hi, 4);
     memcpy(&(*o)[zat + 4], &lo, 4);
@@ -316,8 +517,9 @@ struct Server {
   }
 
   // ConnectRequest body -> ConnectResponse frame; the bound session (0 =
-  // expired answer).
-  int64_t handshake(const uint8_t* b, int32_t n, std::string* o) {
+  // expired answer).  Exclusive tree lock.
+  int64_t handshake(const uint8_t* b, int32_t n, Conn* c) {
+    std::string* o = &c->out;
     Rd r{b, b + n};
     r.i32();
     r.i64();
@@ -341,7 +543,15 @@ struct Server {
         sid = 0; to = 0; pass.assign(16, '\0');
       }
     }
-    if (sid != 0) to = to < 4000 ? 4000 : (to > 40000 ? 40000 : to);
+    if (sid != 0) {
+      to = to < 4000 ? 4000 : (to > 40000 ? 40000 : to);
+      std::lock_guard<std::mutex> g(wmu);
+      auto it = route.find(sid);
+      // a session moving here from a live connection leaves its watches
+      // there (the client re-arms them with SET_WATCHES)
+      if (it != route.end() && it->second != c) drop_watches(sid);
+      route[sid] = c;
+    }
     Wr w{o};
     w.i32(4 + 4 + 8 + 4 + 16 + 1);
     w.i32(0);
@@ -352,15 +562,20 @@ struct Server {
     o->push_back('\0');
     return sid;
   }
-};
 
-struct Conn {
-  int fd;
-  bool hs = false;
-  bool closing = false;
-  int64_t sid = 0;
-  std::string in, out;
-  size_t in_off = 0, out_off = 0;
+  // Connection c is closing (its worker, or an outage): unroute its session
+  // and drop the watches that lived on it.  Caller holds mu exclusively.
+  void detach(Conn* c) {
+    if (c->member >= 0 && c->member < (int)mconns.size())
+      mconns[c->member].erase(c);
+    if (c->sid == 0) return;
+    std::lock_guard<std::mutex> g(wmu);
+    auto it = route.find(c->sid);
+    if (it != route.end() && it->second == c) {
+      route.erase(it);
+      drop_watches(c->sid);
+    }
+  }
 };
 
 void preload(Server& S, int64_t n, int32_t dbytes, int32_t fanout) {
@@ -400,35 +615,61 @@ bool flush_out(Conn& c) {
   return true;
 }
 
+// Requests that take the tree lock exclusively.  Reads with watch=1 and
+// SET_WATCHES only touch the watch tables (their own mutex).
 bool is_write(int32_t op) {
   return op == OP_CREATE || op == OP_DELETE || op == OP_SET_DATA ||
          op == OP_CLOSE_SESSION;
 }
 
 // One worker: its own epoll set over the connections the acceptor handed
-// it (through `pending` + the eventfd).
+// it (through `pending` + the eventfd), and the connections other workers'
+// notifications woke (`woken`).
 struct Worker {
   Server* S = nullptr;
   int ep = -1, efd = -1;
   std::mutex mu;
-  std::vector<int> pending;
+  std::vector<std::pair<int, int>> pending;     // (fd, member)
+  std::vector<int> woken;
   std::map<int, std::unique_ptr<Conn>> conns;
   std::string key;
   std::vector<char> rbuf = std::vector<char>(1 << 20);
 
-  void add(int fd) {
+  void add(int fd, int member) {
     {
       std::lock_guard<std::mutex> g(mu);
-      pending.push_back(fd);
+      pending.emplace_back(fd, member);
+    }
+    uint64_t one = 1;
+    (void)!write(efd, &one, 8);
+  }
+
+  void wake(int fd) {
+    {
+      std::lock_guard<std::mutex> g(mu);
+      woken.push_back(fd);
     }
     uint64_t one = 1;
     (void)!write(efd, &one, 8);
   }
 
   void drop(int fd) {
+    auto it = conns.find(fd);
+    if (it != conns.end()) {
+      std::unique_lock<std::shared_mutex> ex(S->mu);
+      S->detach(it->second.get());
+    }
     epoll_ctl(ep, EPOLL_CTL_DEL, fd, nullptr);
     close(fd);
     conns.erase(fd);
+  }
+
+  static void drain_notes(Conn& c) {
+    std::lock_guard<std::mutex> g(c.nmu);
+    if (!c.notes.empty()) {
+      c.out.append(c.notes);
+      c.notes.clear();
+    }
   }
 
   // Serve every complete frame of the connection's input (one lock per
@@ -450,6 +691,8 @@ struct Worker {
     std::unique_lock<std::shared_mutex> ex(S->mu, std::defer_lock);
     std::shared_lock<std::shared_mutex> sh(S->mu, std::defer_lock);
     if (writes) ex.lock(); else sh.lock();
+    // notifications of writes before this burst go out ahead of its replies
+    drain_notes(c);
     bool dead = false;
     while (!c.closing && c.in.size() - c.in_off >= 4) {
       uint32_t l;
@@ -460,20 +703,27 @@ struct Worker {
       const uint8_t* b = (const uint8_t*)c.in.data() + c.in_off + 4;
       if (!c.hs) {
         if (!writes) break;            // (cannot happen: !hs => exclusive)
-        c.sid = S->handshake(b, len, &c.out);
+        c.sid = S->handshake(b, len, &c);
         c.hs = true;
         if (c.sid == 0) c.closing = true;
       } else if (!writes && len >= 8) {
         uint32_t opw;
         memcpy(&opw, b + 4, 4);
         if (is_write((int32_t)ntohl(opw))) break;   // next burst, exclusive
-        if (!S->serve(b, len, c.sid, &c.out, &key)) c.closing = true;
-      } else if (!S->serve(b, len, c.sid, &c.out, &key)) {
+        if (!S->serve(b, len, &c, &key)) c.closing = true;
+      } else if (!S->serve(b, len, &c, &key)) {
         c.closing = true;
       }
       c.in_off += 4 + (size_t)len;
     }
     return !dead;
+  }
+
+  void rearm(int fd, Conn& c) {
+    epoll_event e{};
+    e.events = EPOLLIN | EPOLLRDHUP | (c.out.empty() ? 0u : (uint32_t)EPOLLOUT);
+    e.data.fd = fd;
+    epoll_ctl(ep, EPOLL_CTL_MOD, fd, &e);
   }
 
   void run() {
@@ -486,19 +736,36 @@ struct Worker {
         if (fd == efd) {
           uint64_t v;
           (void)!read(efd, &v, 8);
-          std::vector<int> fds;
+          std::vector<std::pair<int, int>> fds;
+          std::vector<int> wk;
           {
             std::lock_guard<std::mutex> g(mu);
             fds.swap(pending);
+            wk.swap(woken);
           }
-          for (int c : fds) {
+          for (const auto& fm : fds) {
             auto cn = std::make_unique<Conn>();
-            cn->fd = c;
-            conns[c] = std::move(cn);
+            cn->fd = fm.first;
+            cn->member = fm.second;
+            cn->w = this;
+            {
+              std::unique_lock<std::shared_mutex> ex(S->mu);
+              if (fm.second < (int)S->mconns.size())
+                S->mconns[fm.second].insert(cn.get());
+            }
+            conns[fm.first] = std::move(cn);
             epoll_event e{};
             e.events = EPOLLIN | EPOLLRDHUP;
-            e.data.fd = c;
-            epoll_ctl(ep, EPOLL_CTL_ADD, c, &e);
+            e.data.fd = fm.first;
+            epoll_ctl(ep, EPOLL_CTL_ADD, fm.first, &e);
+          }
+          for (int f : wk) {
+            auto it = conns.find(f);
+            if (it == conns.end()) continue;
+            Conn& c = *it->second;
+            drain_notes(c);
+            if (!flush_out(c)) { drop(f); continue; }
+            rearm(f, c);
           }
           continue;
         }
@@ -525,22 +792,141 @@ struct Worker {
           if (c.in_off == c.in.size()) { c.in.clear(); c.in_off = 0; }
           else if (c.in_off > (1u << 20)) { c.in.erase(0, c.in_off); c.in_off = 0; }
         }
+        drain_notes(c);
         if (!flush_out(c)) dead = true;
         if (!dead && c.closing && c.out.empty()) dead = true;
         if (dead) { drop(fd); continue; }
-        epoll_event e{};
-        e.events = EPOLLIN | EPOLLRDHUP | (c.out.empty() ? 0 : EPOLLOUT);
-        e.data.fd = fd;
-        epoll_ctl(ep, EPOLL_CTL_MOD, fd, &e);
+        rearm(fd, c);
       }
     }
   }
 };
 
+void Server::notify(int64_t sid, int32_t type, const std::string& path,
+                    Conn* self) {
+  auto it = route.find(sid);
+  if (it == route.end()) return;
+  Conn* c = it->second;
+  std::string f;
+  Wr w{&f};
+  w.i32(4 + 8 + 4 + 4 + 4 + 4 + (int32_t)path.size());
+  w.i32(-1);                       // xid: notification
+  w.i64(-1);
+  w.i32(E_OK);
+  w.i32(type);
+  w.i32(ST_SYNC_CONNECTED);
+  w.i32((int32_t)path.size());
+  f.append(path);
+  n_notes.fetch_add(1, std::memory_order_relaxed);
+  if (c == self) {
+    c->out.append(f);
+    return;
+  }
+  {
+    std::lock_guard<std::mutex> g(c->nmu);
+    c->notes.append(f);
+  }
+  c->w->wake(c->fd);
+}
+
+// -- members and the fault channel (main thread) ------------------------------
+
+struct Member {
+  int port = 0;
+  int ls = -1;
+};
+
+int listen_on(int port) {
+  int ls = socket(AF_INET, SOCK_STREAM | SOCK_NONBLOCK, 0);
+  int one = 1;
+  setsockopt(ls, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
+  sockaddr_in a{};
+  a.sin_family = AF_INET;
+  a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+  a.sin_port = htons((uint16_t)port);
+  if (bind(ls, (sockaddr*)&a, sizeof a) != 0 || listen(ls, 128) != 0) {
+    close(ls);
+    return -1;
+  }
+  return ls;
+}
+
+int port_of(int ls) {
+  sockaddr_in a{};
+  socklen_t al = sizeof a;
+  getsockname(ls, (sockaddr*)&a, &al);
+  return ntohs(a.sin_port);
+}
+
+int hexval(char ch) {
+  if (ch >= '0' && ch <= '9') return ch - '0';
+  if (ch >= 'a' && ch <= 'f') return ch - 'a' + 10;
+  if (ch >= 'A' && ch <= 'F') return ch - 'A' + 10;
+  return -1;
+}
+
+// One fault command line -> its answer line.
+std::string command(Server& S, std::vector<Member>& mem, int ep,
+                    const std::string& line) {
+  std::vector<std::string> f;
+  size_t i = 0;
+  while (i < line.size()) {
+    while (i < line.size() && (line[i] == ' ' || line[i] == '\t')) ++i;
+    size_t j = i;
+    while (j < line.size() && line[j] != ' ' && line[j] != '\t') ++j;
+    if (j > i) f.push_back(line.substr(i, j - i));
+    i = j;
+  }
+  if (f.empty()) return "ERR empty";
+  if (f.size() < 2) return "ERR missing member";
+  const int m = atoi(f[1].c_str());
+  if (m < 0 || m >= (int)mem.size()) return "ERR no such member";
+  if (f[0] == "outage") {
+    std::unique_lock<std::shared_mutex> ex(S.mu);
+    if (mem[m].ls >= 0) {
+      epoll_ctl(ep, EPOLL_CTL_DEL, mem[m].ls, nullptr);
+      close(mem[m].ls);
+      mem[m].ls = -1;
+    }
+    // the member's connections end (their workers see the hang-up and
+    // free them); their sessions stay, their watches go
+    std::vector<Conn*> cs(S.mconns[m].begin(), S.mconns[m].end());
+    for (Conn* c : cs) {
+      shutdown(c->fd, SHUT_RDWR);
+      S.detach(c);
+    }
+    for (size_t k = 2; k < f.size(); ++k) {
+      const size_t eq = f[k].find('=');
+      if (eq == std::string::npos) return "ERR bad set";
+      const std::string path = f[k].substr(0, eq), hex = f[k].substr(eq + 1);
+      std::string d;
+      for (size_t h = 0; h + 1 < hex.size(); h += 2)
+        d.push_back((char)(hexval(hex[h]) * 16 + hexval(hex[h + 1])));
+      Node* nd = nullptr;
+      const int32_t err = S.set_data(path, (const uint8_t*)d.data(),
+                                     (int32_t)d.size(), -1, nullptr, &nd);
+      if (err != E_OK) return "ERR set " + path;
+    }
+    return "OK " + std::to_string((long long)S.zxid);
+  }
+  if (f[0] == "start") {
+    if (mem[m].ls < 0) {
+      mem[m].ls = listen_on(mem[m].port);
+      if (mem[m].ls < 0) return "ERR listen";
+      epoll_event ev{};
+      ev.events = EPOLLIN;
+      ev.data.u64 = 1000 + (uint64_t)m;
+      epoll_ctl(ep, EPOLL_CTL_ADD, mem[m].ls, &ev);
+    }
+    return "OK " + std::to_string(mem[m].port);
+  }
+  return "ERR unknown command " + f[0];
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
-  int port = 0;
+  int port = 0, members = 1;
   int64_t pre = 0;
   int32_t dbytes = 100, fanout = 1000;
   unsigned hw = std::thread::hardware_concurrency();
@@ -551,25 +937,29 @@ int main(int argc, char** argv) {
     else if (!strcmp(argv[i], "--data-bytes")) dbytes = atoi(argv[i + 1]);
     else if (!strcmp(argv[i], "--fanout")) fanout = atoi(argv[i + 1]);
     else if (!strcmp(argv[i], "--threads")) nthreads = atoi(argv[i + 1]);
+    else if (!strcmp(argv[i], "--members")) members = atoi(argv[i + 1]);
   }
   if (nthreads < 1) nthreads = 1;
+  if (members < 1) members = 1;
   Server S;
+  S.mconns.resize(members);
   if (pre > 0) preload(S, pre, dbytes, fanout);
   else { S.make("/", "", 0, 0); S.make("/zookeeper", "", 0, 0); }
 
-  int ls = socket(AF_INET, SOCK_STREAM | SOCK_NONBLOCK, 0);
-  int one = 1;
-  setsockopt(ls, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
-  sockaddr_in a{};
-  a.sin_family = AF_INET;
-  a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
-  a.sin_port = htons((uint16_t)port);
-  if (bind(ls, (sockaddr*)&a, sizeof a) != 0 || listen(ls, 128) != 0) {
-    perror("zk_fastserver: bind/listen");
-    return 1;
+  int ep = epoll_create1(0);
+  std::vector<Member> mem(members);
+  for (int m = 0; m < members; ++m) {
+    mem[m].ls = listen_on(m == 0 ? port : 0);
+    if (mem[m].ls < 0) {
+      perror("zk_fastserver: bind/listen");
+      return 1;
+    }
+    mem[m].port = port_of(mem[m].ls);
+    epoll_event ev{};
+    ev.events = EPOLLIN;
+    ev.data.u64 = 1000 + (uint64_t)m;
+    epoll_ctl(ep, EPOLL_CTL_ADD, mem[m].ls, &ev);
   }
-  socklen_t al = sizeof a;
-  getsockname(ls, (sockaddr*)&a, &al);
 
   std::vector<std::unique_ptr<Worker>> workers;
   for (int t = 0; t < nthreads; ++t) {
@@ -587,33 +977,50 @@ int main(int argc, char** argv) {
     Worker* wp = w.get();
     std::thread([wp] { wp->run(); }).detach();
   }
-  printf("PORT %d\n", ntohs(a.sin_port));
+  if (members == 1) {
+    printf("PORT %d\n", mem[0].port);
+  } else {
+    printf("PORTS");
+    for (const auto& m : mem) printf(" %d", m.port);
+    printf("\n");
+  }
   fflush(stdout);
 
-  int ep = epoll_create1(0);
   epoll_event ev{};
   ev.events = EPOLLIN;
-  ev.data.fd = ls;
-  epoll_ctl(ep, EPOLL_CTL_ADD, ls, &ev);
-  ev.data.fd = 0;                              // stdin EOF = shut down
+  ev.data.u64 = 0;                             // stdin: commands; EOF = exit
   epoll_ctl(ep, EPOLL_CTL_ADD, 0, &ev);
   epoll_event evs[8];
   unsigned rr = 0;
+  std::string cmd;
+  const int one = 1;
   for (;;) {
     int ne = epoll_wait(ep, evs, 8, -1);
     if (ne < 0 && errno == EINTR) continue;
     for (int k = 0; k < ne; ++k) {
-      const int fd = evs[k].data.fd;
-      if (fd == 0) {
-        char tmp[256];
-        if (read(0, tmp, sizeof tmp) <= 0) _exit(0);
+      const uint64_t tag = evs[k].data.u64;
+      if (tag == 0) {
+        char tmp[4096];
+        const ssize_t m = read(0, tmp, sizeof tmp);
+        if (m <= 0) _exit(0);
+        cmd.append(tmp, (size_t)m);
+        size_t nl;
+        while ((nl = cmd.find('\n')) != std::string::npos) {
+          const std::string line = cmd.substr(0, nl);
+          cmd.erase(0, nl + 1);
+          const std::string ans = command(S, mem, ep, line);
+          printf("%s\n", ans.c_str());
+          fflush(stdout);
+        }
         continue;
       }
+      const int m = (int)(tag - 1000);
+      if (m < 0 || m >= members || mem[m].ls < 0) continue;
       for (;;) {
-        int c = accept4(ls, nullptr, nullptr, SOCK_NONBLOCK);
+        int c = accept4(mem[m].ls, nullptr, nullptr, SOCK_NONBLOCK);
         if (c < 0) break;
         setsockopt(c, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
-        workers[rr++ % workers.size()]->add(c);
+        workers[rr++ % workers.size()]->add(c, m);
       }
     }
   }

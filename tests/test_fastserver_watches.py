@@ -1,0 +1,269 @@
+"""Watches and ensemble members of the native server (csrc/host/
+zk_fastserver.cpp): the trigger table, SET_WATCHES catch-up and member
+outages, checked against the fake server's database (zkmi/server/fakezk.py,
+SURVEY Appendix D) applied one request at a time, over raw wire sessions.
+
+Reference: lib/zk-session.js:558-574 (trigger table, client side), :421-471
+(watch resume with SET_WATCHES), test/multi-node.test.js:233-350 (member
+failover)."""
+
+import socket
+
+import pytest
+
+from zkmi import consts
+from zkmi import jute
+from zkmi.server import fast
+
+pytestmark = pytest.mark.skipif(not fast.available(),
+                                reason='zk_fastserver not built')
+
+FANOUT = 100
+NLEAF = 300
+
+
+def leaf(i):
+    return '/bench/d%06d/n%09d' % (i // FANOUT, i)
+
+
+class Raw(object):
+    """One wire session: blocking calls; notifications collected in order."""
+
+    def __init__(self, port, sid=0, passwd=b'\0' * 16):
+        self.s = socket.create_connection(('127.0.0.1', port), timeout=10)
+        self.buf = b''
+        self.notes = []
+        self.xid = 1
+        self.s.sendall(jute.frame(jute.encode_connect_request(
+            {'timeOut': 30000, 'sessionId': sid, 'passwd': passwd})))
+        rep = jute.decode_connect_response(self._frame())
+        self.sid, self.passwd = rep['sessionId'], rep['passwd']
+
+    def _frame(self):
+        while True:
+            if len(self.buf) >= 4:
+                n = int.from_bytes(self.buf[:4], 'big')
+                if len(self.buf) >= 4 + n:
+                    body = self.buf[4:4 + n]
+                    self.buf = self.buf[4 + n:]
+                    return body
+            chunk = self.s.recv(1 << 16)
+            if not chunk:
+                raise ConnectionError('closed')
+            self.buf += chunk
+
+    def call(self, pkt):
+        if pkt['opcode'] == 'SET_WATCHES':
+            xid = consts.XID_SET_WATCHES
+        elif pkt['opcode'] == 'PING':
+            xid = consts.XID_PING
+        else:
+            xid = self.xid
+            self.xid += 1
+        pkt = dict(pkt, xid=xid)
+        self.s.sendall(jute.frame(jute.encode_request(pkt)))
+        while True:
+            rep = jute.decode_response(self._frame(), {xid: pkt['opcode']})
+            if rep['xid'] == consts.XID_NOTIFICATION:
+                assert rep['state'] == 'SYNC_CONNECTED'
+                self.notes.append((rep['type'], rep['path']))
+                continue
+            assert rep['xid'] == xid
+            return rep
+
+    def sync(self):
+        """A ping round trip: every notification of writes before it is in."""
+        self.call({'opcode': 'PING'})
+
+    def close(self):
+        self.s.close()
+
+
+class _Handle(object):
+    def cancel(self):
+        pass
+
+
+class _Loop(object):
+    def call_later(self, ms, fn, *a):
+        return _Handle()
+
+    def time_ms(self):
+        return 0
+
+
+class _Conn(object):
+    def __init__(self):
+        self.got = []
+
+    def send_notification(self, evtype, path):
+        self.got.append((evtype, path))
+
+
+class Mirror(object):
+    """The native server and the fake database side by side."""
+
+    def __init__(self, members=1):
+        from zkmi.server.fakezk import ZKDatabase
+        self.srv = fast.FastZKServer(preload=NLEAF, data_bytes=8,
+                                     fanout=FANOUT, members=members)
+        self.db = ZKDatabase(_Loop())
+        w = ZKDatabase._world()
+        self.db.create('/bench', b'', [w], [], None)
+        for d in range((NLEAF + FANOUT - 1) // FANOUT):
+            self.db.create('/bench/d%06d' % d, b'', [w], [], None)
+        for i in range(NLEAF):
+            self.db.create(leaf(i), b'x', [w], [], None)
+        self.raw, self.conns, self.sids = {}, {}, {}
+        for slot in range(3):
+            self.raw[slot] = Raw(self.srv.ports[0])
+            s = self.db.new_session(30000)
+            s.conn = self.conns[slot] = _Conn()
+            self.sids[slot] = s.sid
+
+    def batch(self, slot, pkts):
+        errs = []
+        for p in pkts:
+            rep = self.raw[slot].call(p)
+            want = self.db.handle(dict(p, xid=0, acl=p.get('acl', [])),
+                                  self.sids[slot])
+            assert rep['err'] == want['err'], (p, rep['err'], want['err'])
+            errs.append(rep['err'])
+        return errs
+
+    def check(self):
+        for slot in range(3):
+            self.raw[slot].sync()
+            assert self.raw[slot].notes == self.conns[slot].got, slot
+
+    def close(self):
+        for r in self.raw.values():
+            r.close()
+        self.srv.shutdown()
+
+
+def _get(p, w=True):
+    return {'opcode': 'GET_DATA', 'path': p, 'watch': w}
+
+
+def _exists(p, w=True):
+    return {'opcode': 'EXISTS', 'path': p, 'watch': w}
+
+
+def _kids(p, w=True):
+    return {'opcode': 'GET_CHILDREN2', 'path': p, 'watch': w}
+
+
+def _set(p, v=-1, data=b'new'):
+    return {'opcode': 'SET_DATA', 'path': p, 'data': data, 'version': v}
+
+
+def _create(p):
+    return {'opcode': 'CREATE', 'path': p, 'data': b'c',
+            'acl': [{'perms': ['READ', 'WRITE', 'CREATE', 'DELETE', 'ADMIN'],
+                     'id': {'scheme': 'world', 'id': 'anyone'}}],
+            'flags': []}
+
+
+def _delete(p, v=-1):
+    return {'opcode': 'DELETE', 'path': p, 'version': v}
+
+
+def test_trigger_rules_match_fake_server():
+    m = Mirror()
+    try:
+        d0 = '/bench/d000000'
+        m.batch(0, [_get(leaf(k)) for k in range(10)] +
+                [_exists(d0 + '/new%d' % k) for k in range(5)] +
+                [_exists(leaf(k)) for k in range(10, 15)] +
+                [_get(d0 + '/miss'), _get(leaf(40), False), _kids(d0)])
+        m.batch(2, [_get(leaf(k)) for k in range(5, 10)] +
+                [_get(leaf(k)) for k in range(20, 25)] + [_kids(leaf(21))])
+        m.check()
+        assert not any(r.notes for r in m.raw.values())
+        m.batch(1, [_set(leaf(k)) for k in range(10)] +
+                [_create(d0 + '/new%d' % k) for k in range(3)] +
+                [_delete(leaf(k)) for k in range(10, 13)] +
+                [_delete(leaf(20)), _set(leaf(0)), _create(d0 + '/miss'),
+                 _set(leaf(40)), _set(leaf(21), 7), _delete(leaf(22), 5),
+                 _delete(leaf(21))])
+        m.check()
+        # re-arm after a fire; a session's own write fires its own watch
+        # (the notification ahead of the write's reply)
+        m.batch(0, [_get(leaf(0)), _exists(d0 + '/new3')])
+        m.batch(0, [_set(leaf(0))])
+        assert m.raw[0].notes[-1] == ('DATA_CHANGED', leaf(0))
+        m.batch(1, [_get(leaf(30)), _create(d0 + '/new3'),
+                    _delete(d0 + '/new3'), _set(leaf(30))])
+        m.check()
+        assert len(m.raw[0].notes) > 10 and len(m.raw[2].notes) > 5
+    finally:
+        m.close()
+
+
+def test_set_watches_catch_up_matches_fake_server():
+    m = Mirror()
+    try:
+        d0 = '/bench/d000000'
+        m.batch(1, [_create(d0 + '/late')])
+        rel = m.raw[1].call({'opcode': 'EXISTS', 'path': d0,
+                             'watch': False})['zxid']
+        rel_db = m.db.zxid
+        m.batch(1, [_set(leaf(1)), _delete(leaf(2)), _create(d0 + '/born')])
+        data = [leaf(1), leaf(2), leaf(3)]
+        exist = [d0 + '/born', d0 + '/never', d0 + '/late']
+        child = [leaf(2), d0]
+        ev = {'dataChanged': data, 'createdOrDestroyed': exist,
+              'childrenChanged': child}
+        rep = m.raw[0].call({'opcode': 'SET_WATCHES', 'relZxid': rel,
+                             'events': ev})
+        assert rep['err'] == 'OK'
+        m.db.set_watches(rel_db, ev, m.sids[0])
+        m.check()
+        assert [t for t, _ in m.raw[0].notes] == [
+            'DATA_CHANGED', 'DELETED', 'CREATED', 'CREATED', 'DELETED',
+            'CHILDREN_CHANGED']
+        # the re-armed ones fire on the next writes
+        m.batch(1, [_set(leaf(3)), _create(d0 + '/never')])
+        m.check()
+        assert m.raw[0].notes[-2:] == [('DATA_CHANGED', leaf(3)),
+                                       ('CREATED', d0 + '/never')]
+    finally:
+        m.close()
+
+
+def test_member_outage_and_resume():
+    """A session on member 0 watches two nodes; member 0 goes down while
+    one of them is written; the session resumes on member 1, SET_WATCHES
+    replays the change and re-arms the other watch; member 0 comes back."""
+    srv = fast.FastZKServer(preload=NLEAF, data_bytes=8, fanout=FANOUT,
+                            members=3)
+    try:
+        assert len(srv.ports) == 3
+        a = Raw(srv.ports[0])
+        w = Raw(srv.ports[2])
+        for k in (1, 2):
+            assert a.call(_get(leaf(k)))['err'] == 'OK'
+        rel = a.call(_get(leaf(3), False))['zxid']
+        z = srv.outage(0, [(leaf(1), b'during')])
+        assert z > rel
+        with pytest.raises((ConnectionError, OSError)):
+            a.sync()
+        with pytest.raises(OSError):
+            socket.create_connection(('127.0.0.1', srv.ports[0]), timeout=2)
+        b = Raw(srv.ports[1], a.sid, a.passwd)
+        assert b.sid == a.sid
+        b.call({'opcode': 'SET_WATCHES', 'relZxid': rel,
+                'events': {'dataChanged': [leaf(1), leaf(2)]}})
+        assert b.notes == [('DATA_CHANGED', leaf(1))]
+        assert b.call(_get(leaf(1)))['data'] == b'during'
+        w.call(_set(leaf(2)))
+        b.sync()
+        assert b.notes[-1] == ('DATA_CHANGED', leaf(2))
+        assert srv.start(0) == srv.ports[0]
+        c = Raw(srv.ports[0])
+        c.sync()
+        for r in (b, c, w):
+            r.close()
+    finally:
+        srv.shutdown()

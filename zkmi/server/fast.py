@@ -1,9 +1,11 @@
 """The native benchmark server (``csrc/host/zk_fastserver.cpp``) as a child
-process: the ZooKeeper wire protocol's data plane (handshake, ping, get,
-exists, set, create, delete, sync, children) from a pool of epoll threads
-(one connection per worker, round robin), so a pipelined client benchmark
-measures the client, not a Python server.  The
-full contract (watches, ensembles, fault hooks) stays with
+process: the ZooKeeper wire protocol (handshake, ping, get, exists, set,
+create, delete, sync, children, watches and SET_WATCHES) from a pool of
+epoll threads (one connection per worker, round robin), so a pipelined
+client benchmark measures the client, not a Python server.  ``members=M``
+serves M ports over one tree with fakezk's ensemble fault commands
+(:meth:`FastZKServer.outage`, :meth:`FastZKServer.start`).  ACLs, expiry and
+the connection-level fault modes stay with
 :class:`~zkmi.server.fakezk.FakeZKServer`."""
 
 import os
@@ -22,7 +24,7 @@ class FastZKServer(object):
     synthetic ``/bench`` tree of N leaves (GpuTree's layout)."""
 
     def __init__(self, preload=0, data_bytes=100, fanout=1000, port=0,
-                 threads=None):
+                 threads=None, members=1):
         if not available():
             raise RuntimeError('zk_fastserver not built '
                                '(tools/build_native.py)')
@@ -32,21 +34,42 @@ class FastZKServer(object):
         self.p = subprocess.Popen(
             [BINARY, '--port', str(port), '--preload', str(preload),
              '--data-bytes', str(data_bytes), '--fanout', str(fanout)] +
-            (['--threads', str(threads)] if threads else []),
+            (['--threads', str(threads)] if threads else []) +
+            (['--members', str(members)] if members > 1 else []),
             stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True,
             env=env)
         f = self.p.stdout.readline().split()
-        if len(f) != 2 or f[0] != 'PORT':
+        if len(f) < 2 or f[0] not in ('PORT', 'PORTS'):
             self.p.kill()
             raise RuntimeError('zk_fastserver did not start: %r' % f)
-        self.port = int(f[1])
+        self.ports = [int(x) for x in f[1:]]
+        self.port = self.ports[0]
+
+    def _cmd(self, line):
+        self.p.stdin.write(line + '\n')
+        self.p.stdin.flush()
+        ans = self.p.stdout.readline().split(None, 1)
+        if not ans or ans[0] != 'OK':
+            raise RuntimeError('zk_fastserver command %r: %r' % (line, ans))
+        return ans[1].strip() if len(ans) > 1 else ''
+
+    def outage(self, i, sets=()):
+        """Member ``i`` down (its connections and port close; sessions
+        stay, their watches go), then ``sets`` = [(path, data)] applied,
+        firing watches.  Returns the zxid after them."""
+        return int(self._cmd('outage %d %s' % (i, ' '.join(
+            '%s=%s' % (p, d.hex()) for p, d in sets))))
+
+    def start(self, i):
+        """Member ``i`` listens on its port again; returns the port."""
+        return int(self._cmd('start %d' % i))
 
     @property
     def address(self):
         return {'address': '127.0.0.1', 'port': self.port}
 
     def servers(self):
-        return [self.address]
+        return [{'address': '127.0.0.1', 'port': p} for p in self.ports]
 
     def shutdown(self):
         try:

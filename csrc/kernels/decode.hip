@@ -79,24 +79,36 @@ struct ZkGetCheck {
 };
 constexpr int CHK_SAMPLE = 16;
 
-// n bytes at a (any alignment, readable up to 3 bytes past a + n: a reply's
-// data is followed by its Stat) equal n bytes at b (4-byte aligned)?
-// Aligned dword loads funnel-shifted into place, then the tail bytes.
-ZK_DEV bool bytes_equal(const uint8_t* a, const uint8_t* b, int32_t n) {
-  const uintptr_t ua = (uintptr_t)a;
-  const uint32_t* wa = (const uint32_t*)(ua & ~(uintptr_t)3);
-  const uint32_t* wb = (const uint32_t*)b;
-  const uint32_t sh = (uint32_t)(ua & 3);
-  const int32_t nw = n >> 2;
+// Wave-cooperative byte comparison: do n bytes at a (any alignment;
+// readable up to 19 bytes past a + n — a reply's data is followed by its
+// 68-byte Stat) equal n bytes at b (4-byte aligned; a node slot, padded
+// past its data capacity)?  Lane l compares bytes [16 l, 16 l + 16) of
+// every 1 KiB: aligned dword loads funnel-shifted into place.  All lanes of
+// the wave call it with the same arguments.
+ZK_DEV bool wave_bytes_equal(const uint8_t* a, const uint8_t* b, int32_t n,
+                             int lane) {
   uint32_t diff = 0;
-  uint32_t lo = wa[0];
-  for (int32_t k = 0; k < nw; ++k) {
-    const uint32_t hi = wa[k + 1];
-    diff |= __builtin_amdgcn_alignbyte(hi, lo, sh) ^ wb[k];
-    lo = hi;
+  for (int32_t o = 16 * lane; o < n; o += 1024) {
+    const uintptr_t ua = (uintptr_t)(a + o);
+    const uint32_t* wa = (const uint32_t*)(ua & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)(ua & 3);
+    const uint32_t* wb = (const uint32_t*)(b + o);
+    uint32_t va[5], vb[4];
+#pragma unroll
+    for (int q = 0; q < 5; ++q) va[q] = wa[q];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) vb[q] = wb[q];
+    const int32_t rem = n - o;                 // bytes of this chunk in n
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int32_t keep = rem - 4 * q;        // bytes of dword q in n
+      const uint32_t mask = keep >= 4 ? 0xFFFFFFFFu
+                          : keep <= 0 ? 0u : (1u << (8 * keep)) - 1u;
+      diff |= (__builtin_amdgcn_alignbyte(va[q + 1], va[q], sh) ^ vb[q]) &
+              mask;
+    }
   }
-  for (int32_t j = nw * 4; j < n; ++j) diff |= (uint32_t)(a[j] ^ b[j]);
-  return diff == 0;
+  return __ballot(diff != 0) == 0;
 }
 
 template <bool CHECK>
@@ -112,6 +124,9 @@ __global__ __launch_bounds__(DEC_T) void decode_replies_k(
   int64_t good = 0;
   // the payload sample of this step (read before block 0 advances tick)
   const int64_t salt = CHECK && chk.tick != nullptr ? chk.tick[1] : 0;
+  bool samp = false;                 // this reply's payload is compared
+  int64_t s_off = 0, s_node = 0;
+  int32_t s_len = 0;
   if (live) {
   const uint8_t* p = buf + foff[i];
   const int64_t L = flen[i];
@@ -238,13 +253,27 @@ __global__ __launch_bounds__(DEC_T) void decode_replies_k(
     const int64_t v = chk.idx[i];
     good = xid == chk.xid[i] && o.stat64[i] == v + 1 &&
            plen == chk.data_len[v];
-    if (good && chk.slab != nullptr &&
-        ((i + salt) & (CHK_SAMPLE - 1)) == 0)
-      good = bytes_equal(buf + poff, chk.slab + chk.slot_off[v] + ZK_SLOT_DATA,
-                         plen);
+    samp = good && chk.slab != nullptr && plen > 0 &&
+           ((i + salt) & (CHK_SAMPLE - 1)) == 0;
+    s_off = poff;
+    s_node = v;
+    s_len = plen;
   }
   }  // live
   if (CHECK) {
+    // the sampled payloads, one at a time by the whole wave
+    uint64_t pend = __ballot(samp);
+    const int lane = threadIdx.x & 63;
+    while (pend) {
+      const int l = (int)__builtin_ctzll(pend);
+      pend &= pend - 1;
+      const int64_t po = __shfl(s_off, l, 64);
+      const int64_t vn = __shfl(s_node, l, 64);
+      const int32_t pl = __shfl(s_len, l, 64);
+      const bool eq = wave_bytes_equal(
+          buf + po, chk.slab + chk.slot_off[vn] + ZK_SLOT_DATA, pl, lane);
+      if (lane == l && !eq) good = 0;
+    }
     if (chk.tick != nullptr && blockIdx.x == 0 && threadIdx.x == 0)
       chk.tick[1] += 1;
     __shared__ int64_t sm[DEC_T / 64 + 1];

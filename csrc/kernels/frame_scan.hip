@@ -46,14 +46,18 @@
 //            256 tiles.  The leftmost broken link / terminal go to fs_link
 //            as one atomic per block.
 //  fs_link   No broken link before the first terminal (the usual case):
-//            one workgroup scans the block totals, done.  Otherwise repair
-//            over a grid of 32 workgroups, in rounds to a fix-point: every
-//            broken link is re-walked in parallel (one wave per link) from
-//            the exit before it; what the rounds leave (chains of exits
-//            that each depend on the previous repair) is finished serially,
-//            tiles covered whole by one frame filled in one step; then the
-//            counts are scanned up to the first terminal: row bases and
-//            result[0..3].
+//            one workgroup scans the block totals, done.  A few broken
+//            links (<= 64): chased — from each, forward while the next link
+//            stays broken, the exact entry of a tile looked up among the
+//            candidates fs_tile walked (their exits are its entry -> exit
+//            map), so a run of tiles costs a few instructions each; the
+//            looked-up tiles are then re-walked in parallel over the grid
+//            of 64 workgroups for their frame lists.  Many broken links: a
+//            fix-point in grid rounds (every broken link re-walked in
+//            parallel from the exit before it).  Whatever neither settles
+//            is finished serially, tiles covered whole by one frame filled
+//            in one step; then the counts are scanned up to the first
+//            terminal: row bases and result[0..3].
 //  fs_rows   one wave per tile writes its (body offset, length) rows.
 //
 // The stream length is read ON THE DEVICE (n = min(*n_dev, n_cap), e.g. an
@@ -82,9 +86,11 @@ constexpr int FT_STAGE = FT_S + 16;        // staged bytes (+ length overhang)
 constexpr int64_t TERM = (int64_t)1 << 62;
 constexpr int64_t TBAD = (int64_t)1 << 60;
 constexpr int64_t FC_MAXP = (int64_t)1 << 24;
-constexpr int FC_WIN = 1024;               // fs_link's staged walk window
+constexpr int FC_WIN = 4096;               // fs_link's staged walk window
 constexpr int FC_TAILWIN = 8192;           // the serial tail's (one wave)
-constexpr int FL_T = 1024;                 // fs_link threads
+// fs_link threads (512: 256 VGPRs a lane — with 1024 the chase and the walk
+// inlined together spilled to scratch, 0.64 us a looked-up tile)
+constexpr int FL_T = 512;
 constexpr int FL_U = 8;                    // fs_link loads per batch
 // Bound of fs_tile's wait for the tile before (100 MHz ticks, 2 ms): normal
 // waits are tens of microseconds; past the bound the tile takes no
@@ -112,9 +118,9 @@ ZK_DEV void st_agent(int64_t* p, int64_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Chain statistics after the X flags: [1] tiles without a speculated
-// entry, [2] tiles re-walked by fs_link, [3] fs_link repair rounds
-// (zk_frame_scan_stats reads them).
+// Chain statistics after the X flags: [0] tiles fs_link's chases looked up,
+// [1] tiles without a speculated entry, [2] tiles re-walked by fs_link, [3]
+// fs_link repair rounds (zk_frame_scan_stats reads them).
 ZK_DEV void fc_stat(uint64_t* stats, int k, uint32_t v) {
   __hip_atomic_fetch_add((uint32_t*)&stats[k], v, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
@@ -182,6 +188,10 @@ ZK_DEV int32_t m_np(int64_t m) { return (int32_t)((m >> 11) & 0x7FF); }
 ZK_DEV int32_t m_js(int64_t m) { return (int32_t)((m >> 22) & 0x7FF) - 1; }
 ZK_DEV bool m_term(int64_t m) { return (m >> 33) & 1; }
 ZK_DEV bool m_bad(int64_t m) { return (m >> 34) & 1; }
+// a tile whose exact entry, exit and frame count fs_link's chase looked up:
+// its recorded frame starts are still the old entry's, so fs_rows walks it
+constexpr int64_t M_STALE = (int64_t)1 << 35;
+ZK_DEV bool m_stale(int64_t m) { return (m >> 35) & 1; }
 
 // Resolve the survivor's end code `send` into the walk result's exit.
 ZK_DEV void fc_join_end(FcWalk& r, int64_t send, int64_t n) {
@@ -230,28 +240,59 @@ ZK_DEV bool ft_mark_exit(uint32_t* xbits, int32_t x, int W) {
   return true;
 }
 
-// Does the chain from tile-relative e survive this tile?  It walks (wave-
-// uniform, in LDS) until it leaves the tile or the stream (yes), meets the
-// survivor's path (yes unless the survivor ends on a bad length) or hits a
-// bad length (no).  A partial frame at the stream end counts as surviving
-// (it is the carry).
-ZK_DEV bool ft_alive(const uint8_t* sb, const uint32_t* sbits, int32_t e,
-                     int32_t nrel, int32_t maxp, int32_t m, int64_t send,
-                     int64_t n, int64_t ts) {
-  (void)m;                       // the map is empty when m == 0
+// The chain from tile-relative candidate entry e, walked in LDS (wave-
+// uniform): does it survive this tile, and where does it leave it?
+// Returns the absolute exit (>= the tile end) when it leaves the tile, or
+// meets the survivor's path and the survivor leaves (its exit `send`),
+// packed with the number of frames the chain starts in this tile
+// (cx_exit / cx_cnt); FC_DEAD when it hits a bad length or meets a
+// survivor that ends on one; FC_LIVE when it survives without a known exit
+// (it reaches the stream end, or meets a survivor that ends there).
+// fs_link's chase takes these as the tile's entry -> (exit, count) map.
+constexpr int64_t FC_DEAD = -1;
+constexpr int64_t FC_LIVE = -2;
+constexpr int CX_SHIFT = 48;
+ZK_DEV int64_t cx_exit(int64_t v) {
+  return v < 0 ? v : v & (((int64_t)1 << CX_SHIFT) - 1);
+}
+ZK_DEV int32_t cx_cnt(int64_t v) { return v < 0 ? 0 : (int32_t)(v >> CX_SHIFT); }
+
+ZK_DEV int64_t ft_cand(const uint8_t* sb, const uint32_t* sbits, int32_t e,
+                       int32_t nrel, int32_t maxp, int64_t send, int64_t n,
+                       int64_t ts, int32_t m, int lane) {
   int32_t c = e;
+  int32_t hops = 0;
   for (;;) {
-    if (c >= FT_S || ts + c >= n) return true;
+    if (c >= FT_S) return (ts + c) | ((int64_t)hops << CX_SHIFT);
+    if (ts + c >= n) return FC_LIVE;
     // the survivor-map word and the length word, read together (the map
-    // is all zero when m == 0)
+    // is all zero without a survivor)
     const uint32_t smw = sbits[c >> 5];
     const int32_t lraw = lds_be32(sb, c);
-    if ((smw >> (c & 31)) & 1u) return !((send & TERM) && (send & TBAD));
-    if (c + 4 > nrel) return true;
+    if ((smw >> (c & 31)) & 1u) {
+      if (send & TERM) return (send & TBAD) ? FC_DEAD : FC_LIVE;
+      // joined: the survivor's frames from its start at c on (their index
+      // is the number of survivor starts below c; two map words a lane)
+      const int32_t cw = c >> 5;
+      int32_t below = 0;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int32_t wi = lane + 64 * h;
+        const uint32_t wd = sbits[wi];
+        below += wi < cw ? __popc(wd)
+                         : (wi == cw ? __popc(wd & ((1u << (c & 31)) - 1u))
+                                     : 0);
+      }
+#pragma unroll
+      for (int d = 32; d >= 1; d >>= 1) below += __shfl_xor(below, d, 64);
+      return send | ((int64_t)(hops + m - below) << CX_SHIFT);
+    }
+    if (c + 4 > nrel) return FC_LIVE;
     const int32_t len = __builtin_amdgcn_readfirstlane(lraw);
-    if ((uint32_t)len > (uint32_t)maxp) return false;
+    if ((uint32_t)len > (uint32_t)maxp) return FC_DEAD;
     const int32_t nx = c + 4 + len;
-    if (nx > nrel) return true;
+    if (nx > nrel) return FC_LIVE;
+    ++hops;
     c = nx;
   }
 }
@@ -264,7 +305,7 @@ __global__ __launch_bounds__(256) void fs_tile(
     int64_t* __restrict__ rec_entry, int64_t* __restrict__ rec_exit,
     int64_t* __restrict__ rec_meta, int32_t* __restrict__ rcount,
     int64_t ntiles_cap, int64_t* __restrict__ dbg, int32_t minb,
-    int32_t tflags) {
+    int32_t tflags, int64_t* __restrict__ cx) {
   const bool nospec = tflags & 1;
   const int32_t misspec = tflags >> 8;
   constexpr int K = W / 64;                 // window entries per lane
@@ -514,8 +555,9 @@ __global__ __launch_bounds__(256) void fs_tile(
   bool none = false;
   if (t > 0 && nospec) {
     // (tests: every tile but the first without a speculated entry, the
-    // worst case of the link repair)
+    // worst case of the link repair; no candidate exits either)
     none = true;
+    if (lane < 5) cx[5 * t + lane] = FC_DEAD;
   } else if (t > 0) {
     // Tile t-1 is running or done.  Poll with exponential back-off: these
     // loads bypass the caches, and thousands of waves polling every few
@@ -540,22 +582,27 @@ __global__ __launch_bounds__(256) void fs_tile(
     // Pick the entry among the candidates (the tile before's exits that
     // land here).  A wrong one is a garbage chain of the tile before; read
     // on in THIS tile it almost always dies on a bad length within a few
-    // hops, while the true chain lives on.  So the preferred candidate is
-    // walked first (LDS only, no recording) and taken if its chain
-    // survives the tile — meeting the survivor's path counts as surviving
-    // when the survivor does — else the next candidate, and so on.
+    // hops, while the true chain lives on.  Every candidate is walked (LDS
+    // only, no recording) to where it leaves the tile — meeting the
+    // survivor's path counts as leaving with the survivor — and the first
+    // that survives is the entry.  The exits of all of them go to `cx`:
+    // where two chains both survive tile after tile (a phantom chain: in
+    // the storm's create replies, zxids 0x2Exxxx make the bytes 10 past
+    // each frame start read as the frame length 46), the tile cannot tell
+    // which is true, and fs_link's chase follows the exact one through
+    // this map instead of re-walking every tile.
     E = -1;
     int64_t first = -1;
     for (int slot = 0; slot < 5; ++slot) {
       const int32_t v = (int32_t)((x >> (12 * slot)) & 0xFFF);
-      if (v == 0) continue;
-      const int32_t e = v - 1;
-      if (ts + e >= n) continue;
-      if (first < 0) first = ts + e;
-      if (ft_alive(sb, sbits, e, nrel, maxp32, m, send, n, ts)) {
-        E = ts + e;
-        break;
+      int64_t xe = FC_DEAD;
+      if (v != 0 && ts + (v - 1) < n) {
+        const int32_t e = v - 1;
+        if (first < 0) first = ts + e;
+        xe = ft_cand(sb, sbits, e, nrel, maxp32, send, n, ts, m, lane);
+        if (E < 0 && xe != FC_DEAD) E = ts + e;
       }
+      if (lane == 0) cx[5 * t + slot] = xe;
     }
     if (E < 0) E = first;        // no live candidate: the first one
     // (tests: every misspec-th tile takes a garbage entry one byte past the
@@ -672,8 +719,8 @@ ZK_DEV void fc_stage(const uint8_t* __restrict__ buf, int64_t n, int64_t wb,
 }
 
 // fs_tile's join walk from global memory (a repair from the exact entry E),
-// through a WIN-byte LDS window (the grid rounds: 1 KiB per wave; block
-// 0's serial tail: 8 KiB, a whole tile in one staging).
+// through a WIN-byte LDS window (4 KiB per wave: a tile in one staging;
+// block 0's serial tail: 8 KiB).
 template <int WIN = FC_WIN>
 ZK_DEV FcWalk fc_walk(const uint8_t* __restrict__ buf, int64_t n,
                       int64_t maxp, int64_t ts, int64_t E, const uint16_t* L,
@@ -735,20 +782,21 @@ ZK_DEV FcWalk fc_walk(const uint8_t* __restrict__ buf, int64_t n,
 // previous repair (frames longer than the window crossing tile after tile):
 // after FL_GROUNDS rounds block 0 finishes those serially, skipping the
 // tiles a long frame covers in one step.
-constexpr int FL_B = 32;                   // fs_link workgroups
+constexpr int FL_B = 64;                   // fs_link workgroups
 constexpr int FL_GROUNDS = 6;              // grid repair rounds
 constexpr uint64_t FL_BAR_TICKS = 50000000;   // 0.5 s: barrier abandoned
 // grid words after lbw's stats (uint64): [0] barrier arrivals, [1] barrier
-// generation, [2] abort, then per round r [3 + 2r] first terminal (ntiles -
-// k, max), [4 + 2r] broken links listed
+// generation, [2] abort, then per round r [4 + 2r] broken links listed (the
+// chase repair, which runs no rounds, uses [3] settled and [5] / [6] its
+// grid check's first broken link / terminal)
 constexpr int FL_NB = 3 + 2 * FL_GROUNDS;     // broken links fs_check saw
 constexpr int FL_GW = FL_NB + 1;
-// At most this many broken links: block 0 repairs them alone from fs_check's
-// list (fl_worklist: no grid barrier, no pass over every tile — a reply
-// stream usually has a handful of broken links or none).
-constexpr unsigned long long FL_SMALL = 64;
+// At most this many broken links: chased from fs_check's list (fl_chase; a
+// reply stream usually has a handful of broken links or none); more (every
+// tile without a speculated entry) go to the grid rounds.
+constexpr unsigned long long FL_SMALL = 1024;
 
-// Grid barrier over fs_link's FL_B workgroups (they are co-resident: 32
+// Grid barrier over fs_link's FL_B workgroups (they are co-resident: 64
 // blocks on a 256-CU part, and nothing they wait for needs a CU they hold).
 // Every wait is bounded: past FL_BAR_TICKS the grid is told to abort and
 // block 0 falls back to the serial repair.  Returns false on abort.
@@ -807,7 +855,8 @@ ZK_DEV bool fl_sync(unsigned long long* g) {
 // broken and is walked again once the tile before has settled.  The
 // leftmost broken link always has an exact entry, so every round settles
 // at least it.  A walk from an E that tile k-1 has since replaced is stale
-// and not written either.
+// and not written either.  (A refused walk has overwritten the tile's
+// recorded frame starts all the same: its caller clears the entry.)
 ZK_DEV bool fl_accept(const int64_t* rec_entry, const int64_t* rec_exit,
                       int64_t ntiles, int64_t k, int64_t E, int64_t x) {
   if (ld_agent(&rec_exit[k - 1]) != E) return false;
@@ -835,24 +884,21 @@ ZK_DEV bool fl_round(const uint8_t* __restrict__ buf, int64_t n,
   const int64_t bid = blockIdx.x;
   const int64_t nth = nblk * FL_T;
   const int64_t gt = bid * FL_T + tid;
-  // A. the first terminal as the records stand
-  int64_t ft = INF;
-  for (int64_t k = gt; k < ntiles; k += nth)
-    if (m_term(ld_agent(&rec_meta[k]))) { ft = k; break; }
-  for (int d = 32; d >= 1; d >>= 1)
-    ft = min(ft, (int64_t)__shfl_xor(ft, d, 64));
-  if (lane == 0 && ft != INF)
-    atomicMax(&g[3 + 2 * r], (unsigned long long)(ntiles - ft));
-  if (!fl_sync(g)) return false;
-  const unsigned long long mt = __hip_atomic_load(
-      &g[3 + 2 * r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const int64_t ftr = mt ? ntiles - (int64_t)mt : ntiles - 1;
-  // B. list the broken links k <= ftr (tile k-1 is not a terminal there)
+  // B. list the broken links (after a tile that is not a terminal).  Every
+  // one, not only those before the first terminal: a terminal may be a
+  // speculation's (a garbage entry that died) that this very round fixes,
+  // and stopping the list there made a stream with many such tiles take a
+  // round per terminal (26 ms a 0-1024 B reply stream at a 1 KiB window).
+  // Past a real bad frame the walks are wasted, and the serial tail's
+  // first terminal bounds what counts.
   int64_t nb = 0;
-  const int64_t per = (ftr + nth - 1) / nth;
-  const int64_t k0 = 1 + gt * per, k1 = min(k0 + per, ftr + 1);
-  for (int64_t k = k0; k < k1; ++k)
-    nb += ld_agent(&rec_entry[k]) != ld_agent(&rec_exit[k - 1]);
+  const int64_t per = (ntiles - 1 + nth - 1) / nth;
+  const int64_t k0 = 1 + gt * per, k1 = min(k0 + per, ntiles);
+  auto broken = [&](int64_t k) {
+    return ld_agent(&rec_entry[k]) != ld_agent(&rec_exit[k - 1]) &&
+           !m_term(ld_agent(&rec_meta[k - 1]));
+  };
+  for (int64_t k = k0; k < k1; ++k) nb += broken(k);
   int64_t tot;
   const int64_t o = block_excl_scan(nb, red, &tot);
   __shared__ unsigned long long s_base;
@@ -861,8 +907,7 @@ ZK_DEV bool fl_round(const uint8_t* __restrict__ buf, int64_t n,
   __syncthreads();
   int64_t w = (int64_t)s_base + o;
   for (int64_t k = k0; k < k1; ++k)
-    if (ld_agent(&rec_entry[k]) != ld_agent(&rec_exit[k - 1]))
-      blist[w++] = (int32_t)k;
+    if (broken(k)) blist[w++] = (int32_t)k;
   if (!fl_sync(g)) return false;
   const int64_t nbr = (int64_t)__hip_atomic_load(
       &g[4 + 2 * r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -879,10 +924,18 @@ ZK_DEV bool fl_round(const uint8_t* __restrict__ buf, int64_t n,
     const FcWalk fw = fc_walk(buf, n, maxp, k * FT_S, E, list + k * FT_LMAX,
                               m0, sx[k], mywin, pre + k * FT_LMAX, lane);
     ++walked;
-    if (lane == 0 && fl_accept(rec_entry, rec_exit, ntiles, k, E, fw.exit)) {
-      st_agent(&rec_entry[k], E);
-      st_agent(&rec_exit[k], fw.exit);
-      st_agent(&rec_meta[k], fc_meta(fw));
+    if (lane == 0) {
+      if (fl_accept(rec_entry, rec_exit, ntiles, k, E, fw.exit)) {
+        st_agent(&rec_entry[k], E);
+        st_agent(&rec_exit[k], fw.exit);
+        st_agent(&rec_meta[k], fc_meta(fw));
+      } else {
+        // the walk overwrote the tile's frame starts (pre) while its
+        // record keeps the old entry: no entry, so the link stays broken
+        // and the tile is walked again (its exit, which the refusal
+        // protects, is kept)
+        st_agent(&rec_entry[k], -1);
+      }
     }
   }
   if (lane == 0 && walked) fc_stat(stats, 2, walked);
@@ -1003,52 +1056,322 @@ ZK_DEV void fl_bases(int64_t n, int64_t ntiles, int64_t ft,
   }
 }
 
-// The small repair: block 0 alone, a worklist instead of rounds over the
-// whole tile array (a 550 MB reply stream has 134K tiles: one workgroup
-// scanning them for broken links costs ~30 us a pass, a grid barrier a few
-// us; a small repair needs neither).  fs_check listed the broken links;
-// each round re-walks the listed ones in parallel (one wave per link, from
-// the exit before it as it stands), then checks the link after every tile
-// it re-wrote — a link only breaks when a tile next to it is re-written,
-// and a walked tile's own link is checked by its walked predecessor — and
-// lists the broken ones (deduplicated in an LDS hash set) for the next
-// round.  An empty list is the fix-point.  Only the count blocks holding a
-// re-written tile are re-counted.  Returns false (nothing lost: the serial
-// tail finishes from the records as they stand) when the list outgrows
-// LDS or the rounds run out.
-constexpr int FL_WL = 1024;                // worklist entries per round
-constexpr int FL_HS = 2048;                // its dedup hash set
+// The small repair (a handful of broken links, the usual kind): CHASES.
+// fs_check listed the broken links.  A chase starts at one with the exact
+// entry (the exit before it) and runs forward while the link after the
+// tile it settled is still broken.  Most tiles of a run need no walk:
+// their exact entry is one of the candidate entries fs_tile walked, whose
+// exit and frame count `cx` already holds (fs_tile's entry -> exit map),
+// so the chase only looks it up — a wave loads the candidate words and
+// exits of 64 tiles at once and resolves them with a 6-step parallel
+// prefix over the tiles' slot maps.  A tile whose entry is not a candidate
+// (a frame longer than the window) is walked; tiles a long frame covers
+// whole are filled in one step.  Looked-up tiles are marked stale: fs_rows
+// walks their frame starts, in parallel with every other tile.  (Round 3
+// first re-walked every tile of a run one after the other: on the storm's
+// phantom-chain replies, 650 tiles in 18 ms; then looked them up one tile
+// at a time, ~0.3 us each.)
+// Chases of different runs run in parallel (one wave each) in rounds: a
+// round's chases, then a check of every run's first and last link (another
+// run may have moved an exit), the broken ones (deduplicated in an LDS
+// hash set) chased next round.  Only the count blocks holding a re-written
+// tile are re-counted.  When the lists outgrow LDS or the rounds run out,
+// block 0's serial tail finishes from the records as they stand.
+constexpr int FL_WL = 1024;                // chases per round
+constexpr int FL_HS = 2048;                // their dedup hash set
 constexpr int FL_WR = 48;                  // rounds before the serial tail
 constexpr int FL_DB = 8192;                // count blocks tracked (2M tiles)
+static_assert(FL_SMALL <= FL_WL, "fs_check's list fits the first round");
 
-ZK_DEV bool fl_worklist(const uint8_t* __restrict__ buf, int64_t n,
-                        int64_t ntiles, int64_t maxp,
-                        const int64_t* __restrict__ sx,
-                        const uint16_t* __restrict__ list,
-                        const int32_t* __restrict__ rcount, uint16_t* pre,
-                        int64_t* rec_entry, int64_t* rec_exit,
-                        int64_t* rec_meta, int64_t* base, int64_t* bsum,
-                        const int32_t* __restrict__ blist, int nb0,
-                        int64_t ft0, uint8_t* win, uint64_t* stats,
-                        int64_t* ft_out) {
-  __shared__ int32_t wl[2][FL_WL];
-  __shared__ int32_t wk[FL_WL];
-  __shared__ uint32_t hs[FL_HS];
-  __shared__ uint32_t dirty[FL_DB / 32];
-  __shared__ int s_n[3];          // next list, walked, overflow
-  __shared__ int s_cur;
-  __shared__ unsigned long long s_term;       // leftmost new terminal
-  __shared__ int s_healed;                    // fs_check's first one gone
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int64_t INF = INT64_MAX;
-  for (int i = tid; i < FL_DB / 32; i += FL_T) dirty[i] = 0;
-  for (int i = tid; i < nb0; i += FL_T) wl[0][i] = blist[i];
-  if (tid == 0) {
-    s_term = (unsigned long long)INF;
-    s_healed = 0;
-    s_n[2] = 0;
-    s_cur = nb0;
+struct FlChase {
+  uint32_t* dirty;                // count blocks holding re-written tiles
+  int* overflow;
+  uint64_t* stats;
+  int64_t* clk;                   // ZKMI_FS_DBG: the exact chase's span
+};
+
+ZK_DEV void fl_dirty(FlChase& ch, int64_t t) {
+  const int64_t b = t / FK_T;
+  atomicOr(&ch.dirty[b >> 5], 1u << (b & 31));
+}
+
+ZK_DEV int live_count(const int64_t* c5) {
+  int live = 0;
+#pragma unroll
+  for (int j = 0; j < 5; ++j) live += c5[j] != FC_DEAD;
+  return live;
+}
+
+ZK_DEV int64_t rfl64(int64_t v) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+  const uint32_t hi =
+      (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)v >> 32));
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
+ZK_DEV uint64_t readlane64(uint64_t v, int l) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+  const uint32_t hi =
+      (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// One chase (one wave) from broken link k0.  Returns the last tile it
+// wrote (-1: none), `term` when that tile ends the chain.
+// `exact`: k0 is the round's leftmost broken link, so its entry (the exit
+// before it) is exact and so is everything the chase derives.  It stops at
+// a link that holds only where the tile after is unambiguous (one live
+// candidate): a run of tiles where two chains both survive (a phantom
+// chain) can hold links that are consistent and wrong, and only a chase
+// from an exact entry can tell — it goes through the whole run.
+// Otherwise (another broken link of the round, entry not known exact) the
+// chase writes nothing that would break a link that holds (fl_accept's
+// rule: a phantom's exit must not run over a true segment); it stops there
+// and the link waits for a later round.
+ZK_DEV int64_t fl_chase_run(const uint8_t* __restrict__ buf, int64_t n,
+                            int64_t ntiles, int64_t maxp,
+                            const int64_t* __restrict__ sx,
+                            const uint16_t* __restrict__ list,
+                            const int32_t* __restrict__ rcount, uint16_t* pre,
+                            int64_t* rec_entry, int64_t* rec_exit,
+                            int64_t* rec_meta, const uint64_t* lbw,
+                            const int64_t* cx,
+                            uint8_t* mywin, FlChase& ch, int64_t k0,
+                            bool exact, bool& term, uint32_t& walked) {
+  const int lane = threadIdx.x & 63;
+  term = false;
+  // everything that steers the chase is wave-uniform; saying so keeps its
+  // control flow scalar (else the compiler runs the batch loop below as
+  // divergent code under exec masks: ~850 cycles a tile)
+  k0 = rfl64(k0);
+  exact = __builtin_amdgcn_readfirstlane((int)exact) != 0;
+  int64_t k = k0;
+  int64_t E = rfl64(ld_agent(&rec_exit[k - 1]));
+  if (E < k * FT_S ||
+      __builtin_amdgcn_readfirstlane(m_term(ld_agent(&rec_meta[k - 1]))))
+    return -1;
+  if (!exact && rfl64(ld_agent(&rec_entry[k])) == E) return -1;  // holds
+  bool first = true;             // tile k0's own link is the broken one
+  for (;;) {
+    if (E >= (k + 1) * FT_S) {
+      // a frame covers tiles k .. kx-1 whole: no frame starts there.  (Only
+      // from an exact entry: a garbage exit megabytes ahead would wipe out
+      // every tile it claims to cover.)
+      if (!exact) return k - 1;
+      const int64_t kend = min(E / FT_S, ntiles);
+      const FcWalk cov{E, 0, 0, -1, false, false};
+      for (int64_t c = k + lane; c < kend; c += 64) {
+        st_agent(&rec_entry[c], E);
+        st_agent(&rec_exit[c], E);
+        st_agent(&rec_meta[c], fc_meta(cov));
+        fl_dirty(ch, c);
+      }
+      if (kend >= ntiles) return kend - 1;
+      k = kend;
+      first = false;
+      continue;
+    }
+    // ---- a batch of 64 tiles, lane i = tile k+i ------------------------
+    // Each lane loads its tile's candidate word (written by the tile
+    // before), the five candidate exits, its entry and exit and the next
+    // tile's entry, and turns them into a transition table over its five
+    // candidate slots: the slot of the next tile that each exit enters
+    // (next lane's word), whether the link into this tile holds with that
+    // slot's entry, whether taking it would break a holding link, whether
+    // two candidates survive.  The serial walk over the batch is then a
+    // few scalar instructions a tile.  (Round 3 first resolved each tile
+    // from the raw words: ~150 dependent instructions, 0.6 us a tile.)
+    const int64_t tl = k + lane;
+    const int64_t ts_l = tl * FT_S;
+    uint64_t wd = 0;
+    int64_t en = INT64_MIN, ent = INT64_MIN, ox = INT64_MIN + 1;
+    int64_t c5[5];               // candidate exits
+    int32_t n5[5];               // and their frame counts
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+      c5[j] = FC_DEAD;
+      n5[j] = 0;
+    }
+    if (tl < ntiles) {
+      wd = lb_load(&lbw[2 * (tl - 1)]);
+#pragma unroll
+      for (int j = 0; j < 5; ++j) {
+        const int64_t v = cx[5 * tl + j];
+        c5[j] = cx_exit(v);
+        n5[j] = cx_cnt(v);
+      }
+      ent = ld_agent(&rec_entry[tl]);
+      ox = ld_agent(&rec_exit[tl]);
+    }
+    if (tl + 1 < ntiles) en = ld_agent(&rec_entry[tl + 1]);
+    // the next tile's slots
+    const uint32_t wn_lo = (uint32_t)__shfl_down((int)(uint32_t)wd, 1, 64);
+    const uint32_t wn_hi =
+        (uint32_t)__shfl_down((int)(uint32_t)(wd >> 32), 1, 64);
+    const uint64_t wn = ((uint64_t)wn_hi << 32) | wn_lo;
+    const int64_t tend_l = ts_l + FT_S;
+    const bool next_holds = tl + 1 < ntiles && en == ox;
+    // lane i's map M over the state of its tile — the entry slot 0..4, or
+    // 5 stopped (an earlier tile ended the run), 6 walk (the entry is the
+    // exit before, not among the candidates), 7 leave (the entry lies
+    // past the tile or the batch) — to the state of the tile after it.
+    // Tile i stops the run (maps to 5) when its link already holds with
+    // that entry (an exact chase goes on through ambiguous tiles), when a
+    // non-exact chase would break a holding link, or when the exit is not
+    // known (the tile is walked).
+    const bool amb = live_count(c5) >= 2;
+    const bool head = first && lane == 0;   // k0: its link is the broken one
+    uint32_t M = (5u << 15) | (5u << 18) | (5u << 21);
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+      const uint32_t oj = (uint32_t)((wd >> (12 * j)) & 0xFFF);  // off + 1
+      const int64_t xj = c5[j];
+      uint32_t nx = 5;                      // (no looked-up exit: stops)
+      if (tl < ntiles && oj != 0 && xj >= tend_l) {
+        if (xj >= tend_l + FT_S || lane == 63 || tl + 1 >= ntiles) {
+          nx = 7;
+        } else {
+          const uint32_t want = (uint32_t)(xj - tend_l) + 1;
+          nx = 6;
+#pragma unroll
+          for (int q = 4; q >= 0; --q)
+            if ((uint32_t)((wn >> (12 * q)) & 0xFFF) == want) nx = q;
+        }
+        const bool holds = ent == ts_l + (int64_t)oj - 1;
+        if (!head && holds && !(exact && amb)) nx = 5;
+        if (!exact && xj != ox && next_holds) nx = 5;
+      }
+      M |= nx << (3 * j);
+    }
+    // the state of the batch's first tile
+    uint32_t j0 = 6;
+    {
+      const uint64_t w0 = readlane64(wd, 0);
+      const uint32_t want = (uint32_t)(E - k * FT_S) + 1;
+#pragma unroll
+      for (int q = 4; q >= 0; --q)
+        if ((uint32_t)((w0 >> (12 * q)) & 0xFFF) == want) j0 = q;
+    }
+    // prefix composition over the lanes (Hillis-Steele, 6 steps): T_i =
+    // M_i o ... o M_0; the state of tile i is T_{i-1}(j0)
+    uint32_t T = M;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t U = (uint32_t)__shfl_up((int)T, d, 64);
+      if (lane >= d) {
+        uint32_t C = 0;
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+          C |= ((T >> (3 * ((U >> (3 * q)) & 7))) & 7) << (3 * q);
+        T = C;
+      }
+    }
+    const uint32_t Tp = (uint32_t)__shfl_up((int)T, 1, 64);
+    const uint32_t st = lane == 0 ? j0 : (Tp >> (3 * j0)) & 7;
+    // looked up: a tile whose state is an entry slot and whose map does not
+    // stop there
+    const bool mine = tl < ntiles && st < 5 && ((M >> (3 * st)) & 7) != 5;
+    const uint64_t looked = __ballot(mine);
+    // the run of looked-up tiles is a prefix of the batch
+    const int f = looked == ~0ull ? 64 : (int)__builtin_ctzll(~looked);
+    if (f > 0) {
+      if (lane == 0) fc_stat(ch.stats, 0, (uint32_t)f);
+      if (lane < f) {
+        // exact entry, exit and frame count; the frame starts themselves
+        // are walked by fs_rows (a stale tile)
+        const uint32_t oj = (uint32_t)((wd >> (12 * st)) & 0xFFF);
+        const int64_t xj = st == 0 ? c5[0] : st == 1 ? c5[1]
+                           : st == 2 ? c5[2] : st == 3 ? c5[3] : c5[4];
+        const int32_t nj = st == 0 ? n5[0] : st == 1 ? n5[1]
+                           : st == 2 ? n5[2] : st == 3 ? n5[3] : n5[4];
+        st_agent(&rec_entry[tl], ts_l + (int64_t)oj - 1);
+        st_agent(&rec_exit[tl], xj);
+        st_agent(&rec_meta[tl], M_STALE | nj);
+        fl_dirty(ch, tl);
+      }
+      first = false;
+    }
+    if (k + f >= ntiles) return ntiles - 1;
+    // what ends the run at tile k+f: its state
+    const uint32_t sf = (uint32_t)__builtin_amdgcn_readlane((int)st, f & 63);
+    if (f < 64 && sf < 5) {
+      // its map stops there: the link holds, a refusal, or no known exit
+      const uint32_t oj = (uint32_t)((readlane64(wd, f) >> (12 * sf)) & 0xFFF);
+      const int64_t xs = (int64_t)readlane64(
+          (uint64_t)(sf == 0 ? c5[0] : sf == 1 ? c5[1] : sf == 2 ? c5[2]
+                     : sf == 3 ? c5[3] : c5[4]), f);
+      if (xs >= (k + f + 1) * FT_S) return k + f - 1;   // link / refusal
+      E = (k + f) * FT_S + (int64_t)oj - 1;              // walked below
+    } else {
+      // 6 / 7 (or the batch done): the entry is the exit before it
+      const int l = f - 1;
+      const uint32_t sl =
+          (uint32_t)__builtin_amdgcn_readlane((int)st, l < 0 ? 0 : l);
+      if (l >= 0)
+        E = (int64_t)readlane64(
+            (uint64_t)(sl == 0 ? c5[0] : sl == 1 ? c5[1] : sl == 2 ? c5[2]
+                       : sl == 3 ? c5[3] : c5[4]), l);
+    }
+    k += f;
+    if (f == 64 || sf == 7) continue;          // next batch / covered
+
+    // stop == 2: tile k (entry E) is walked
+    {
+      const int64_t t = k;
+      if (t >= ntiles) return t - 1;
+      if (E >= (t + 1) * FT_S) continue;          // covered: to the top
+      if (!first && rfl64(ld_agent(&rec_entry[t])) == E && !exact)
+        return t - 1;
+      const int64_t ts = t * FT_S;
+      const int64_t oldx = rfl64(ld_agent(&rec_exit[t]));
+      const bool nh = t + 1 < ntiles &&
+                      rfl64(ld_agent(&rec_entry[t + 1])) == oldx;
+      const int32_t m0 = __builtin_amdgcn_readfirstlane(rcount[t]);
+      const FcWalk fw = fc_walk(buf, n, maxp, ts, E, list + t * FT_LMAX, m0,
+                                sx[t], mywin, pre + t * FT_LMAX, lane);
+      ++walked;
+      if (!exact && rfl64(fw.exit) != oldx && nh) {
+        // refused, but the walk overwrote the tile's frame starts: no
+        // entry, so its link stays broken (see fl_round)
+        if (lane == 0) st_agent(&rec_entry[t], -1);
+        return t - 1;
+      }
+      if (lane == 0) {
+        st_agent(&rec_entry[t], E);
+        st_agent(&rec_exit[t], fw.exit);
+        st_agent(&rec_meta[t], fc_meta(fw));
+        fl_dirty(ch, t);
+      }
+      first = false;
+      if (__builtin_amdgcn_readfirstlane(fw.term)) { term = true; return t; }
+      if (t + 1 >= ntiles) return t;
+      // an exact chase stops where the next link holds and the tile after
+      // has one live candidate; the next batch checks that
+      E = rfl64(fw.exit);
+      k = t + 1;
+    }
   }
+}
+
+// Block 0: chase rounds to a fix-point of the links.  Returns false when it
+// gave up (the serial tail takes over).
+ZK_DEV bool fl_chase(const uint8_t* __restrict__ buf, int64_t n,
+                     int64_t ntiles, int64_t maxp,
+                     const int64_t* __restrict__ sx,
+                     const uint16_t* __restrict__ list,
+                     const int32_t* __restrict__ rcount, uint16_t* pre,
+                     int64_t* rec_entry, int64_t* rec_exit, int64_t* rec_meta,
+                     const uint64_t* lbw, const int64_t* cx, int32_t* blist,
+                     int nb0, uint8_t* win, uint64_t* stats, FlChase& ch) {
+  __shared__ int32_t wl[2][FL_WL];
+  __shared__ int32_t wk[FL_WL];              // run ends (+ 1; 0: none)
+  __shared__ uint32_t hs[FL_HS];
+  __shared__ int s_n;
+  __shared__ int s_cur;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  // fs_check's list to LDS
+  for (int i = tid; i < nb0; i += FL_T) wl[0][i] = blist[i];
+  if (tid == 0) s_cur = nb0;
   uint8_t* mywin = win + (size_t)wv * (FC_WIN + 16);
   int cur = 0, rounds = 0;
   uint32_t walked = 0;
@@ -1059,10 +1382,7 @@ ZK_DEV bool fl_worklist(const uint8_t* __restrict__ buf, int64_t n,
     ++rounds;
     const int nxt = cur ^ 1;
     for (int i = tid; i < FL_HS; i += FL_T) hs[i] = 0;
-    if (tid == 0) {
-      s_n[0] = 0;
-      s_n[1] = 0;
-    }
+    if (tid == 0) s_n = 0;
     __syncthreads();
     // one lane lists link k for the next round (once)
     auto push = [&](int64_t k) {
@@ -1074,46 +1394,43 @@ ZK_DEV bool fl_worklist(const uint8_t* __restrict__ buf, int64_t n,
         if (old == key) return;
         h = (h + 1) & (FL_HS - 1);
       }
-      const int i = atomicAdd(&s_n[0], 1);
+      const int i = atomicAdd(&s_n, 1);
       if (i < FL_WL) wl[nxt][i] = (int32_t)k;
-      else s_n[2] = 1;
+      else *ch.overflow = 1;
     };
-    // re-walk the listed links
+    // the round's leftmost broken link: its entry is exact
+    int32_t lo = INT32_MAX;
+    for (int j = lane; j < ncur; j += 64) lo = min(lo, wl[cur][j]);
+    for (int d = 32; d >= 1; d >>= 1) lo = min(lo, __shfl_xor(lo, d, 64));
     for (int j = wv; j < ncur; j += FL_T / 64) {
-      const int64_t k = wl[cur][j];
-      const int64_t E = ld_agent(&rec_exit[k - 1]);
-      if (E < k * FT_S || m_term(ld_agent(&rec_meta[k - 1]))) continue;
-      if (ld_agent(&rec_entry[k]) == E) continue;       // holds by now
-      const int32_t m0 = __builtin_amdgcn_readfirstlane(rcount[k]);
-      const FcWalk fw = fc_walk(buf, n, maxp, k * FT_S, E,
-                                list + k * FT_LMAX, m0, sx[k], mywin,
-                                pre + k * FT_LMAX, lane);
-      ++walked;
-      if (lane == 0) {
-        if (fl_accept(rec_entry, rec_exit, ntiles, k, E, fw.exit)) {
-          st_agent(&rec_entry[k], E);
-          st_agent(&rec_exit[k], fw.exit);
-          st_agent(&rec_meta[k], fc_meta(fw));
-          const int64_t b = k / FK_T;
-          atomicOr(&dirty[b >> 5], 1u << (b & 31));
-          if (fw.term) atomicMin(&s_term, (unsigned long long)k);
-          else if (k == ft0) s_healed = 1;
-          wk[atomicAdd(&s_n[1], 1)] = (int32_t)k;
-        } else {
-          push(k);
-        }
-      }
+      bool term;
+      const bool ex = wl[cur][j] == lo;
+      if (ex && ch.clk && lane == 0) ch.clk[6] = wall_clock64();
+      const int64_t kend = fl_chase_run(buf, n, ntiles, maxp, sx, list,
+                                        rcount, pre, rec_entry, rec_exit,
+                                        rec_meta, lbw, cx, mywin,
+                                        ch, wl[cur][j], wl[cur][j] == lo,
+                                        term, walked);
+      if (ex && ch.clk && lane == 0) ch.clk[7] = wall_clock64();
+      if (lane == 0)
+        wk[j] = kend < 0 ? 0 : (int32_t)(kend + 1) | (term ? (1 << 30) : 0);
     }
     __syncthreads();
-    // the link after every re-written tile
-    const int nw = s_n[1];
-    for (int j = tid; j < nw; j += FL_T) {
-      const int64_t k = wk[j];
-      if (k + 1 >= ntiles || m_term(ld_agent(&rec_meta[k]))) continue;
-      if (ld_agent(&rec_entry[k + 1]) != ld_agent(&rec_exit[k])) push(k + 1);
+    // every run's first and last link, as the records stand now
+    for (int j = tid; j < ncur; j += FL_T) {
+      const int64_t k0 = wl[cur][j];
+      if (ld_agent(&rec_entry[k0]) != ld_agent(&rec_exit[k0 - 1]) &&
+          !m_term(ld_agent(&rec_meta[k0 - 1])))
+        push(k0);
+      const int32_t e = wk[j];
+      if (e == 0 || (e & (1 << 30))) continue;
+      const int64_t kend = (e & ((1 << 30) - 1)) - 1;
+      if (kend + 1 < ntiles &&
+          ld_agent(&rec_entry[kend + 1]) != ld_agent(&rec_exit[kend]))
+        push(kend + 1);
     }
     __syncthreads();
-    if (tid == 0) s_cur = s_n[2] ? -1 : s_n[0];
+    if (tid == 0) s_cur = *ch.overflow ? -1 : s_n;
     __syncthreads();
     ncur = s_cur;
     cur = nxt;
@@ -1122,29 +1439,18 @@ ZK_DEV bool fl_worklist(const uint8_t* __restrict__ buf, int64_t n,
   }
   if (lane == 0 && walked) fc_stat(stats, 2, walked);
   if (tid == 0 && rounds) fc_stat(stats, 3, rounds);
-  if (ncur != 0) return false;
-  // the first terminal: fs_check's, unless a re-walk made an earlier one or
-  // healed it (then looked up again; rare)
-  int64_t ft = min(ft0, (int64_t)s_term);
-  const bool stale = s_healed ||
-      (s_term != (unsigned long long)INF &&
-       !m_term(ld_agent(&rec_meta[(int64_t)s_term])));
-  if (stale) {
-    int64_t f = INF;
-    for (int64_t k = tid; k < ntiles; k += FL_T)
-      if (m_term(ld_agent(&rec_meta[k]))) { f = k; break; }
-    for (int d = 32; d >= 1; d >>= 1) f = min(f, (int64_t)__shfl_xor(f, d, 64));
-    __shared__ int64_t s_f[FL_T / 64];
-    if (lane == 0) s_f[wv] = f;
-    __syncthreads();
-    ft = INF;
-    for (int j = 0; j < FL_T / 64; ++j) ft = min(ft, s_f[j]);
-  }
-  // re-count the blocks holding a re-written tile: one wave per block,
-  // four tiles per lane
+  return ncur == 0 && !*ch.overflow;
+}
+
+// After the chases and the grid's check of every link (block 0): re-count
+// the count blocks holding a re-written tile, one wave per block, four
+// tiles per lane.
+ZK_DEV void fl_chase_recount(int64_t ntiles, const int64_t* rec_meta,
+                             int64_t* base, int64_t* bsum, FlChase& ch) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t nbl = (ntiles + FK_T - 1) / FK_T;
   for (int64_t b = wv; b < nbl; b += FL_T / 64) {
-    if (!((dirty[b >> 5] >> (b & 31)) & 1u)) continue;
+    if (!((ch.dirty[b >> 5] >> (b & 31)) & 1u)) continue;
     const int64_t k0 = b * FK_T + 4 * lane;
     int64_t c[4], s = 0;
 #pragma unroll
@@ -1166,8 +1472,6 @@ ZK_DEV bool fl_worklist(const uint8_t* __restrict__ buf, int64_t n,
     if (lane == 63) st_agent(&bsum[b], inc);
   }
   __syncthreads();
-  *ft_out = ft;
-  return true;
 }
 
 __global__ __launch_bounds__(FL_T) void fs_link(
@@ -1178,7 +1482,9 @@ __global__ __launch_bounds__(FL_T) void fs_link(
     int64_t* __restrict__ base, int64_t cap, int64_t* __restrict__ result,
     uint64_t* stats, int32_t* __restrict__ blist,
     int64_t* __restrict__ bsum, uint64_t* __restrict__ mins,
-    int64_t* __restrict__ lastk, unsigned long long* __restrict__ g) {
+    int64_t* __restrict__ lastk, unsigned long long* __restrict__ g,
+    const uint64_t* lbw, const int64_t* __restrict__ cx,
+    int64_t* __restrict__ ldbg) {
   __shared__ __attribute__((aligned(16)))
       uint8_t win[(FL_T / 64) * (FC_WIN + 16)];      // one per wave
   static_assert(FC_TAILWIN <= (FL_T / 64) * (FC_WIN + 16),
@@ -1204,14 +1510,13 @@ __global__ __launch_bounds__(FL_T) void fs_link(
   const int64_t fb0 = mb0 ? ntiles - (int64_t)mb0 : INF;
   const int64_t ft0 = mt0 ? ntiles - (int64_t)mt0 : INF;
   const bool fast = fb0 == INF || fb0 > ft0;
-  // a small repair (a handful of broken links, the usual one) is block 0's
-  // worklist; the grid takes part only in a large one (every block decides
-  // alike: block 0 clears the words it read only after the grid's first
-  // barrier, or — without the grid — in a way that reads as "not grid")
+  // a small repair (a handful of broken links, the usual kind) is chased
+  // (fl_chase), a large one repaired in grid rounds; the whole grid takes
+  // part in either (every block decides alike: block 0 clears the words it
+  // read only after the grid's first barrier)
   const bool small = !fast && nb0 <= FL_SMALL &&
                      (ntiles + FK_T - 1) / FK_T <= FL_DB;
-  const bool grid = !fast && !small;
-  if (!grid && blockIdx.x != 0) return;
+  if (fast && blockIdx.x != 0) return;
   if (fast) {
     // no broken link before the first terminal: the row bases are bsum's
     // block offsets + fs_check's in-block bases
@@ -1227,18 +1532,80 @@ __global__ __launch_bounds__(FL_T) void fs_link(
   }
   bool grid_ok = true;
   if (small) {
-    __syncthreads();
-    if (tid == 0) {
+    // ---- chases: block 0; then every link checked over the grid ---------
+    __shared__ uint32_t dirty[FL_DB / 32];
+    __shared__ int s_ovf;
+    FlChase ch{dirty, &s_ovf, stats, ldbg};
+    unsigned long long* cw = &g[3];       // 1: the chases settled
+    const bool clk = ldbg != nullptr && blockIdx.x == 0 && tid == 0;
+    if (clk) ldbg[0] = wall_clock64();
+    if (blockIdx.x == 0) {
+      for (int i = tid; i < FL_DB / 32; i += FL_T) dirty[i] = 0;
+      if (tid == 0) s_ovf = 0;
+      __syncthreads();
+      const bool ok = fl_chase(buf, n, ntiles, maxp, sx, list, rcount, pre,
+                               rec_entry, rec_exit, rec_meta, lbw, cx, blist,
+                               (int)nb0, win, stats, ch);
+      if (tid == 0)
+        __hip_atomic_store(cw, ok ? 1ull : 0ull, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      if (clk) ldbg[1] = wall_clock64();
+    }
+    bool synced = fl_sync(g);        // (block 0 cleared nothing yet)
+    if (clk) ldbg[2] = wall_clock64();
+    if (blockIdx.x == 0 && tid == 0) {
       mins[0] = 0;
       mins[1] = 0;
     }
-    int64_t ft;
-    if (fl_worklist(buf, n, ntiles, maxp, sx, list, rcount, pre, rec_entry,
-                    rec_exit, rec_meta, base, bsum, blist, (int)nb0, ft0, win,
-                    stats, &ft)) {
+    const bool settled =
+        __hip_atomic_load(cw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+    // every link and the first terminal, checked over the grid (a chase
+    // only vouches for the links it saw): [5] / [6] = ntiles - the first
+    // broken link / terminal, maxima
+    if (synced) {
+      const int64_t nth = (int64_t)gridDim.x * FL_T;
+      int64_t fb = INF, fterm = INF;
+      for (int64_t k = (int64_t)blockIdx.x * FL_T + tid; k < ntiles;
+           k += nth) {
+        const int64_t mk = ld_agent(&rec_meta[k]);
+        if (m_term(mk)) {
+          fterm = min(fterm, k);
+        } else if (k + 1 < ntiles &&
+                   ld_agent(&rec_entry[k + 1]) != ld_agent(&rec_exit[k])) {
+          fb = min(fb, k + 1);
+        }
+      }
+      for (int d = 32; d >= 1; d >>= 1) {
+        fb = min(fb, (int64_t)__shfl_xor(fb, d, 64));
+        fterm = min(fterm, (int64_t)__shfl_xor(fterm, d, 64));
+      }
+      if (lane == 0 && fb != INF)
+        atomicMax(&g[5], (unsigned long long)(ntiles - fb));
+      if (lane == 0 && fterm != INF)
+        atomicMax(&g[6], (unsigned long long)(ntiles - fterm));
+    }
+    synced = synced && fl_sync(g);
+    if (clk) ldbg[3] = wall_clock64();
+    if (blockIdx.x != 0) return;
+    const unsigned long long gb = __hip_atomic_load(
+        &g[5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long gt = __hip_atomic_load(
+        &g[6], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int64_t fbv = gb ? ntiles - (int64_t)gb : INF;
+    const int64_t ftv = gt ? ntiles - (int64_t)gt : INF;
+    __syncthreads();
+    if (tid == 0) {
+      g[2] = 0;
+      g[3] = 0;
+      g[5] = 0;
+      g[6] = 0;
+    }
+    if (settled && synced && (fbv == INF || fbv > ftv)) {
+      fl_chase_recount(ntiles, rec_meta, base, bsum, ch);
       if (tid == 0) g[FL_NB] = 0;
-      fl_bases(n, ntiles, ft, rec_exit, rec_meta, base, bsum, cap, result,
+      fl_bases(n, ntiles, ftv, rec_exit, rec_meta, base, bsum, cap, result,
                lastk, red);
+      if (clk) ldbg[4] = wall_clock64();
       return;
     }
     grid_ok = false;          // not settled: block 0's serial tail finishes
@@ -1394,17 +1761,25 @@ __global__ __launch_bounds__(FL_T) void fs_link(
   }
 }
 
-// (body offset, length) rows: one wave per tile, 4 tiles per block.
+// (body offset, length) rows: one wave per tile, 4 tiles per block.  A
+// stale tile (its exact entry, exit and count looked up by fs_link's chase)
+// has no recorded frame starts for that entry: its wave stages the tile in
+// LDS and walks them first.
 __global__ __launch_bounds__(256) void fs_rows(
     const uint8_t* __restrict__ buf, const int64_t* __restrict__ n_dev,
     int64_t n_cap, const uint16_t* __restrict__ list,
     const uint16_t* __restrict__ pre, const int64_t* __restrict__ rec_meta,
+    const int64_t* __restrict__ rec_entry,
     const int64_t* __restrict__ rec_exit,
     const int64_t* __restrict__ base, const int64_t* __restrict__ bsum,
     const int64_t* __restrict__ lastk, int64_t* __restrict__ foff,
     int32_t* __restrict__ flen, int64_t cap, uint64_t* __restrict__ lbw) {
+  // (only the staged tile: 16 KiB a block keeps fs_rows at full occupancy;
+  // a frame-start array beside it cost the var-size GET 3x in fs_rows)
+  __shared__ __attribute__((aligned(16))) uint8_t stage[4][FT_STAGE];
   const int lane = threadIdx.x & 63;
-  const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int64_t t = (int64_t)blockIdx.x * 4 + wv;
   const int64_t n = stream_len(n_dev, n_cap);
   if (t * FT_S >= n) return;
   // the scan is over for this tile: clear its candidate flags, so the next
@@ -1421,6 +1796,41 @@ __global__ __launch_bounds__(256) void fs_rows(
   const int64_t ts = t * FT_S;
   const uint16_t* P = pre + t * FT_LMAX;
   const uint16_t* R = list + t * FT_LMAX + (js < 0 ? 0 : js);
+  if (m_stale(m)) {
+    uint8_t* sb = stage[wv];
+    fc_stage<FT_S>(buf, n, ts, sb, lane);
+    if (lane == 0) {
+      uint8_t* pb = sb + FT_S;
+      for (int k = 0; k < 16; ++k)
+        pb[k] = ts + FT_S + k < n ? buf[ts + FT_S + k] : 0;
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    // the walk keeps 64 starts in the lanes (lane k & 63 holds start k)
+    // and writes their rows every 64 frames
+    int32_t c = __builtin_amdgcn_readfirstlane((int32_t)(rec_entry[t] - ts));
+    int32_t ent = 0;
+    for (int32_t k = 0; k < cnt; ++k) {
+      ent = lane == (k & 63) ? c : ent;
+      const int32_t len = __builtin_amdgcn_readfirstlane(lds_be32(sb, c));
+      c += 4 + len;
+      if ((k & 63) == 63 || k == cnt - 1) {
+        const int32_t last = k & 63;
+        const int32_t nxt = __shfl_down(ent, 1, 64);
+        if (lane <= last) {
+          const int64_t p = ts + ent;
+          const int64_t q = lane < last ? ts + nxt
+                                        : (k == cnt - 1 ? x : ts + c);
+          const int64_t idx = b + (k & ~63) + lane;
+          if (idx < cap) {
+            foff[idx] = p + 4;
+            flen[idx] = (int32_t)(q - p - 4);
+          }
+        }
+      }
+    }
+    return;
+  }
   // a frame ends where the next one of the chain starts, the tile's last
   // at the tile's exit (the next tile's first frame, or the stop offset of
   // a terminal tile): lengths come from the recorded starts, no stream read
@@ -1439,7 +1849,7 @@ __global__ __launch_bounds__(256) void fs_rows(
 struct FsPlan {
   int64_t tiles;
   size_t off_list, off_pre, off_sx, off_lbw, off_rent, off_rexit, off_rmeta,
-      off_rcnt, off_base, off_blist, off_bsum, total;
+      off_rcnt, off_base, off_blist, off_bsum, off_cx, total;
 };
 
 static FsPlan fs_plan(int64_t n) {
@@ -1461,6 +1871,7 @@ static FsPlan fs_plan(int64_t n) {
   p.off_base = take((size_t)tiles * 8);
   p.off_blist = take((size_t)tiles * 4);
   p.off_bsum = take((size_t)(tiles / FK_T + 1) * 8);
+  p.off_cx = take((size_t)tiles * 5 * 8);   // candidate exits (fs_tile)
   p.total = o;
   return p;
 }
@@ -1493,7 +1904,8 @@ static int64_t* fs_dbg_buf(int64_t tiles) {
   if (!on) return nullptr;
   if (tiles > g_dbg_tiles) {
     if (g_dbg) (void)hipFree(g_dbg);
-    if (hipMalloc(&g_dbg, tiles * 8 * 8) != hipSuccess) return nullptr;
+    // a row per tile (fs_tile) + one for fs_link's phase clock
+    if (hipMalloc(&g_dbg, (tiles + 1) * 8 * 8) != hipSuccess) return nullptr;
     g_dbg_tiles = tiles;
   }
   return g_dbg;
@@ -1554,6 +1966,7 @@ int zk_frame_scan5(const uint8_t* buf, const int64_t* n_dev, int64_t n_cap,
   int64_t* base = (int64_t*)(ws + p.off_base);
   int32_t* blist = (int32_t*)(ws + p.off_blist);
   int64_t* bsum = (int64_t*)(ws + p.off_bsum);
+  int64_t* cx = (int64_t*)(ws + p.off_cx);
   uint64_t* mins = lbw + 2 * tiles + 4;
   int64_t* lastk = (int64_t*)(lbw + 2 * tiles + 6);
   unsigned long long* grid = (unsigned long long*)(lbw + 2 * tiles + 8);
@@ -1575,7 +1988,7 @@ int zk_frame_scan5(const uint8_t* buf, const int64_t* n_dev, int64_t n_cap,
 #define ZK_FS_TILE(WW)                                                       \
   fs_tile<WW><<<tblocks, 64 * tpb, FT_LDS * tpb, st>>>(                      \
       buf, n_dev, n_cap, maxp, list, pre, sx, lbw, rent, rexit, rmeta, rcnt, \
-      tiles, dbg, fs_minb(), flags)
+      tiles, dbg, fs_minb(), flags, cx)
   switch (W) {
     case 256: ZK_FS_TILE(256); break;
     case 512: ZK_FS_TILE(512); break;
@@ -1590,11 +2003,11 @@ int zk_frame_scan5(const uint8_t* buf, const int64_t* n_dev, int64_t n_cap,
   fs_link<<<FL_B, FL_T, 0, st>>>(buf, n_dev, n_cap, maxp, sx, list, rcnt,
                                  pre, rent, rexit, rmeta, base, cap, result,
                                  lbw + 2 * tiles, blist, bsum, mins, lastk,
-                                 grid);
+                                 grid, lbw, cx, dbg ? dbg + 8 * tiles : nullptr);
   ZK_LAUNCH_CHECK();
   fs_rows<<<(unsigned)((tiles + 3) / 4), 256, 0, st>>>(
-      buf, n_dev, n_cap, list, pre, rmeta, rexit, base, bsum, lastk, foff,
-      flen, cap, lbw);
+      buf, n_dev, n_cap, list, pre, rmeta, rent, rexit, base, bsum, lastk,
+      foff, flen, cap, lbw);
   ZK_LAUNCH_CHECK();
   return 0;
 }
@@ -1618,27 +2031,32 @@ int zk_frame_scan3(const uint8_t* buf, const int64_t* n_dev, int64_t n_cap,
 // Chain statistics of the last scan of workspace `ws` over a buffer of
 // n_cap bytes, into out3 (host): tiles without a speculated entry, tiles
 // re-walked, repair rounds.
+// out4: tiles without a speculated entry, tiles re-walked, repair rounds,
+// tiles a chase looked up
 int zk_frame_scan_stats(const uint8_t* ws, int64_t n_cap, int32_t window,
-                        uint32_t* out3, hipStream_t st) {
+                        uint32_t* out4, hipStream_t st) {
   using namespace zk;
   (void)window;
   FsPlan p = fs_plan(n_cap);
   const uint64_t* lbw = (const uint64_t*)(ws + p.off_lbw);
-  for (int k = 0; k < 3; ++k)
-    if (hipMemcpyAsync(out3 + k, lbw + 2 * p.tiles + 1 + k, 4,
+  for (int k = 0; k < 4; ++k)
+    if (hipMemcpyAsync(out4 + k, lbw + 2 * p.tiles + (k + 1) % 4, 4,
                        hipMemcpyDeviceToHost, st) != hipSuccess)
       return -1;
   if (hipStreamSynchronize(st) != hipSuccess) return -1;
   // counters since the last read (scans of a clean workspace skip the
   // memset that used to reset them)
-  if (hipMemsetAsync((void*)(lbw + 2 * p.tiles + 1), 0, 3 * 8, st) !=
+  if (hipMemsetAsync((void*)(lbw + 2 * p.tiles), 0, 4 * 8, st) !=
       hipSuccess)
     return -1;
   return hipStreamSynchronize(st) == hipSuccess ? 0 : -1;
 }
 
+// rows = tiles + 1: the last row is fs_link's phase clock of a chase repair
+// (start, chases done, barrier, links checked, end; [6] / [7] the exact
+// chase's start and end)
 int zk_frame_scan_dbg(int64_t* host, int64_t tiles) {
-  if (!zk::g_dbg || tiles > zk::g_dbg_tiles) return -1;
+  if (!zk::g_dbg || tiles > zk::g_dbg_tiles + 1) return -1;
   return hipMemcpy(host, zk::g_dbg, tiles * 8 * 8, hipMemcpyDeviceToHost) ==
                  hipSuccess ? 0 : -1;
 }

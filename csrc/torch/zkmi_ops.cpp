@@ -519,11 +519,11 @@ void frame_scan(const Tensor& buf, const c10::optional<Tensor>& n_dev,
 
 std::vector<int64_t> frame_scan_stats(const Tensor& ws, int64_t n_cap,
                                       int64_t window) {
-  uint32_t o[3] = {0, 0, 0};
+  uint32_t o[4] = {0, 0, 0, 0};
   hip_ok(zk_frame_scan_stats(P<uint8_t>(ws, U8, 1, "ws"), n_cap,
                              (int32_t)window, o, cur_stream()),
          "frame_scan_stats");
-  return {o[0], o[1], o[2]};
+  return {o[0], o[1], o[2], o[3]};
 }
 
 // Per-tile timing records of the last K1 run built with ZKMI_FS_DBG

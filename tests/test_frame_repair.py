@@ -162,3 +162,47 @@ def test_garbage_entries_variable_and_long_frames(gpu):
         r, off, ms, st = _scan_timed(buf, len(lens), 256, reps=1,
                                      misspec=period)
         _check(r, off, buf, starts)
+
+
+def test_phantom_chain_region_is_chased_not_walked(gpu):
+    """Create replies whose zxids run through 0x2Exxxx: the bytes 10 past
+    every frame start then read as the frame length 46, a phantom chain
+    parallel to the true one over ~800 tiles.  No tile can tell the two
+    apart; fs_link's chase follows the exact one through fs_tile's candidate
+    exit map and the grid re-walks the tiles in parallel.  (The storm's
+    first reply stream: 18 ms of tile-after-tile repair before.)"""
+    n = 1 << 20
+    clean, starts = _create_replies(n, zxid0=0x500000)
+    _, _, base_ms, _ = _scan_timed(clean, n, 256)
+    buf, starts = _create_replies(n, zxid0=0x2E0000 - 500000)
+    r, off, ms, st = _scan_timed(buf, n, 256)
+    _check(r, off, buf, starts)
+    assert st['looked_up'] >= 4 * 700, st      # the region, looked up
+    assert st['rounds'] <= 4 * 4, st           # in a round or two per scan
+    assert ms < max(3 * base_ms, 0.6), (ms, base_ms)
+
+
+def test_get_replies_exact_below_the_largest_frame(gpu, monkeypatch):
+    """0-1024 B GET replies scanned at a 512 B window (half the largest
+    frame): most tiles lose their speculated entry and go through the grid
+    rounds and the serial tail.  Every frame table must still equal the
+    host framing — a refused repair walk once left a tile's frame starts
+    overwritten under its old record (3 frames in 20M)."""
+    monkeypatch.setenv('ZKMI_FS_WINDOW_MAX', '512')
+    from zkmi.bench import synthetic as S
+    tree = S.GpuTree(200_000, 100, device=gpu, seed=0, data_dist=(0, 1024))
+    pipe = S.GetPipeline(tree, 1 << 16, seed=1)
+    assert pipe.rwindow == 512
+    for _ in range(4):
+        acc = pipe.step()
+        idx, rep, rx, ft = pipe.last
+        r = ft.host_result()
+        b = rx[:r['consumed']].cpu().numpy().tobytes()
+        want = []
+        p = 0
+        while p + 4 <= len(b):
+            want.append(p + 4)
+            p += 4 + int.from_bytes(b[p:p + 4], 'big')
+        got = ft.off[:r['frames']].cpu().numpy()
+        assert np.array_equal(got, np.asarray(want, np.int64))
+        assert int(acc.item()) == 1 << 16

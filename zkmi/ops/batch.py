@@ -14,6 +14,7 @@ K10 :func:`encode_requests`; K11 :func:`encode_set_watches`; K12
 """
 
 from dataclasses import dataclass
+import os
 
 import numpy as np
 import torch
@@ -305,11 +306,14 @@ FS_WINDOWS = (256, 512, 1024, 2048)
 
 def frame_window(max_frame):
     """The smallest K1 entry window covering frames of ``max_frame`` bytes
-    (length prefix included); larger frames stay exact, only slower."""
+    (length prefix included); larger frames stay exact, only slower.
+    ``ZKMI_FS_WINDOW_MAX`` caps it (A/B of a window below the largest
+    frame: the rare tile entered past the window is repaired)."""
+    cap = int(os.environ.get('ZKMI_FS_WINDOW_MAX', FS_WINDOWS[-1]))
     for w in FS_WINDOWS:
         if max_frame <= w:
-            return w
-    return FS_WINDOWS[-1]
+            return min(w, max(cap, FS_WINDOWS[0]))
+    return min(FS_WINDOWS[-1], max(cap, FS_WINDOWS[0]))
 
 
 def _scan_len(buf, n):
@@ -381,11 +385,13 @@ class FrameScanner:
         """K1 chain counters (host sync) accumulated over this scanner's
         scans since the previous call (a reused workspace skips the memset
         that used to reset them per scan): tiles without a speculated
-        entry, tiles re-walked, repair rounds."""
+        entry, tiles re-walked, repair rounds, tiles fs_link's chases
+        looked up in fs_tile's candidate exits."""
         with _on(stream):
             out = _lib.lib().frame_scan_stats(self.ws, self.last_cap,
                                               int(self.window))
-        return {'no_spec': out[0], 'rewalked': out[1], 'rounds': out[2]}
+        return {'no_spec': out[0], 'rewalked': out[1], 'rounds': out[2],
+                'looked_up': out[3]}
 
 
 def frame_scan(buf, n=None, max_packet=consts.MAX_PACKET, cap=None,

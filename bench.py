@@ -265,6 +265,7 @@ def run_ensemble(a):
     try:
         wl = E.EnsembleWorkload(ctl, n_paths=a.paths, writes=a.writes,
                                 failover_every=a.failover_every,
+                                max_versions=a.warmup + a.steps + 2,
                                 codec_device=dev)
         for _ in range(a.warmup):
             wl.step()
@@ -321,6 +322,7 @@ def run_ensemble(a):
             'ops_note': 'watch-event deliveries over the node (every event '
                         'reaches every rank exactly once, checked)',
             'failovers': int(fo // world),
+            'step_ms_rank0': [round(x, 2) for x in wl.step_ms],
             'watches_rearmed_by_set_watches': int(rep),
             'events_decoded_on_gpu': int(dg),
             'events_decoded_on_host': int(dh),
@@ -381,9 +383,9 @@ def main():
                          'RCCL/xGMI (the default)')
     ap.add_argument('--no-compare', action='store_true',
                     help='get, N > 1: skip the replica comparison run')
-    ap.add_argument('--paths', type=int, default=512,
+    ap.add_argument('--paths', type=int, default=65536,
                     help='ensemble: watched znodes (one owner rank each)')
-    ap.add_argument('--writes', type=int, default=128,
+    ap.add_argument('--writes', type=int, default=4096,
                     help='ensemble: znodes set per step')
     ap.add_argument('--failover-every', type=int, default=4,
                     help='ensemble: every k-th step kills the member rank 0 '

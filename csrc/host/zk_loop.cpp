@@ -173,6 +173,19 @@ struct Capture {
 };
 enum { CAP_DONE = 0, CAP_FULL = 1, CAP_BAD = 2, CAP_CANCEL = 3 };
 
+// Notification sink (Transport.note_sink): while on, the read path frames
+// the inbound stream itself and keeps every NOTIFICATION frame (xid -1),
+// length prefix included, in `buf` instead of handing it to Python; the
+// node-wide watch fan-out (zkmi/parallel/fanout.py) takes them in bulk
+// (take_notes) and forwards the raw bytes.  Other frames go on to Python
+// whole.  All access holds the GIL (the loop thread calls into Python).
+struct NoteSink {
+  bool on = false;
+  int64_t max_packet = 0;
+  std::string buf;
+  int64_t frames = 0;
+};
+
 struct Transport {
   Watched w;
   PyObject* protocol;
@@ -183,6 +196,7 @@ struct Transport {
   bool closing, closed;
   PyObject* peer;        // (host, port) tuple
   Capture* cap;
+  NoteSink* ns;
 };
 
 struct Server {
@@ -362,6 +376,7 @@ Transport* new_transport(Loop* L, int fd) {
   t->eof_pending = t->wr_shut = t->closing = t->closed = false;
   t->peer = nullptr;
   t->cap = new Capture();
+  t->ns = new NoteSink();
   return t;
 }
 
@@ -370,6 +385,7 @@ void Transport_dealloc(Transport* t) {
   delete t->wbuf;
   Py_XDECREF(t->cap->done);
   delete t->cap;
+  delete t->ns;
   Py_XDECREF(t->protocol);
   Py_XDECREF(t->on_fail);
   Py_XDECREF(t->peer);
@@ -524,7 +540,8 @@ void capture_end(Transport* t, int status) {
 
 void deliver(Transport* t, const char* p, size_t n) {
   Capture& c = *t->cap;
-  if (!c.on) { deliver_raw(t, p, n); return; }
+  NoteSink& ns = *t->ns;
+  if (!c.on && !ns.on) { deliver_raw(t, p, n); return; }
   std::string buf;
   const char* s = p;
   size_t len = n;
@@ -534,26 +551,42 @@ void deliver(Transport* t, const char* p, size_t n) {
     s = buf.data();
     len = buf.size();
   }
-  std::string pass;               // frames that are not the batch's
+  std::string pass;               // frames that are neither
+  int64_t nn = 0;
   size_t i = 0;
   int status = -1;
-  while (len - i >= 4 && c.got < c.n) {
+  const int64_t maxp = c.on ? c.max_packet : ns.max_packet;
+  while (len - i >= 4) {
+    if (c.on && c.got >= c.n) break;      // (capture_end re-delivers the rest)
     const int32_t fl = be32(s + i);
-    if (fl < 0 || fl > c.max_packet) { status = CAP_BAD; break; }
+    if (fl < 0 || fl > maxp) {
+      if (c.on) {
+        status = CAP_BAD;
+      } else {
+        // the sink alone: Python's framer sees the bad length and reports it
+        pass.append(s + i, len - i);
+        i = len;
+      }
+      break;
+    }
     if (len - i < 4 + (size_t)fl) break;
-    const int64_t xid = fl >= 4 ? be32(s + i + 4) : -1;
-    if (fl >= 16 && xid >= c.x0 && xid < c.x0 + c.n) {
+    const int64_t xid = fl >= 4 ? be32(s + i + 4) : -2;
+    if (c.on && fl >= 16 && xid >= c.x0 && xid < c.x0 + c.n) {
       if (c.len + 4 + (size_t)fl > c.size) { status = CAP_FULL; break; }
       memcpy(c.dst + c.len, s + i, 4 + (size_t)fl);
       c.last_off = c.len;
       c.len += 4 + (size_t)fl;
       ++c.got;
+    } else if (ns.on && fl >= 16 && xid == -1) {
+      ns.buf.append(s + i, 4 + (size_t)fl);
+      ++nn;
     } else {
       pass.append(s + i, 4 + (size_t)fl);
     }
     i += 4 + (size_t)fl;
   }
-  if (status < 0 && c.got >= c.n) status = CAP_DONE;
+  ns.frames += nn;
+  if (status < 0 && c.on && c.got >= c.n) status = CAP_DONE;
   c.carry.assign(s + i, len - i);
   deliver_raw(t, pass.data(), pass.size());
   if (status >= 0 && c.on && !t->closed) capture_end(t, status);
@@ -693,13 +726,57 @@ PyObject* Transport_capture(Transport* t, PyObject* args) {
   c.dst = (uint8_t*)(uintptr_t)addr;
   c.size = (size_t)size;
   c.len = c.last_off = 0;
-  c.carry.clear();
+  // with the sink on the native framer already holds the partial frame
+  // (Python's holds none); else the caller's framer hands it over below
+  if (!t->ns->on) c.carry.clear();
   Py_INCREF(done);
   c.done = done;
   std::string head((const char*)pre.buf, (size_t)pre.len);
   PyBuffer_Release(&pre);
   if (!head.empty()) deliver(t, head.data(), head.size());
   Py_RETURN_NONE;
+}
+
+// note_sink(on, max_packet, prefix): route NOTIFICATION frames into the
+// sink (see NoteSink).  `prefix` = a partial frame the caller's framer
+// holds, parsed first.  Turning it off hands a partial frame the native
+// framer holds back to Python.
+PyObject* Transport_note_sink(Transport* t, PyObject* args) {
+  int on;
+  long long maxp;
+  Py_buffer pre;
+  if (!PyArg_ParseTuple(args, "pLy*", &on, &maxp, &pre)) return nullptr;
+  NoteSink& ns = *t->ns;
+  std::string head((const char*)pre.buf, (size_t)pre.len);
+  PyBuffer_Release(&pre);
+  if (on) {
+    const bool was = ns.on;
+    ns.on = true;
+    ns.max_packet = maxp;
+    if (!was && !t->cap->on) t->cap->carry.clear();
+    if (!head.empty() && !t->closed) deliver(t, head.data(), head.size());
+  } else if (ns.on) {
+    ns.on = false;
+    if (!t->cap->on && !t->cap->carry.empty()) {
+      std::string rest;
+      rest.swap(t->cap->carry);
+      deliver_raw(t, rest.data(), rest.size());
+    }
+  }
+  Py_RETURN_NONE;
+}
+
+// take_notes() -> (bytes, frames): the notification frames the sink kept
+// since the last call.
+PyObject* Transport_take_notes(Transport* t, PyObject*) {
+  NoteSink& ns = *t->ns;
+  PyObject* b = PyBytes_FromStringAndSize(ns.buf.data(),
+                                          (Py_ssize_t)ns.buf.size());
+  if (b == nullptr) return nullptr;
+  const long long nf = ns.frames;
+  ns.buf.clear();
+  ns.frames = 0;
+  return Py_BuildValue("(NL)", b, nf);
 }
 
 // capture_cancel(): end an active capture (done gets CAP_CANCEL).
@@ -818,6 +895,10 @@ PyMethodDef Transport_methods[] = {
      "route an xid range of reply frames into a buffer"},
     {"capture_cancel", (PyCFunction)Transport_capture_cancel, METH_NOARGS,
      "end the active capture"},
+    {"note_sink", (PyCFunction)Transport_note_sink, METH_VARARGS,
+     "keep NOTIFICATION frames natively"},
+    {"take_notes", (PyCFunction)Transport_take_notes, METH_NOARGS,
+     "the kept NOTIFICATION frames (bytes, count)"},
     {nullptr, nullptr, 0, nullptr}};
 
 PyGetSetDef Transport_getset[] = {

@@ -2,9 +2,10 @@
 a 3-member ensemble, one session per rank, member failover with watch
 replay through SET_WATCHES, every event fanned out to every rank.
 
-CPU: gloo, world 2 and 4, host decode of the fanned-out wire frames.  GPU:
-one rank with the live connection's K9 / K11 records and the fan-out's K1 +
-K2-K8 decode on the device."""
+CPU: gloo, world 2, 4 and 8, host decode of the fanned-out wire frames,
+against the native 3-member ensemble server.  GPU: one rank with the live
+connection's K9 / K11 records, the bulk re-arm on the GPU and the fan-out's
+K1 + K2-K8 decode and (path, version) count on the device."""
 
 import os
 import socket
@@ -81,7 +82,8 @@ def test_ensemble_failover_replay_fanout(world):
         assert bad is None, (rank, bad)
         assert got == [12] * steps, (rank, got)
         assert fo == 2 and replayed == 24
-        assert st['decoded_host'] == 48 + 12 * steps
+        # a notification + its re-arm reply per event
+        assert st['decoded_host'] == 2 * (48 + 12 * steps)
         rearmed += rea
     # the killed members' sessions resumed their watches (SET_WATCHES)
     assert rearmed > 0
@@ -102,7 +104,7 @@ def test_ensemble_gpu_codec_and_fanout_decode():
         for _ in range(4):
             assert wl.step() == 10
         assert wl.verify() is None
-        assert wl.fan.stats['decoded_gpu'] == 40 + 40
+        assert wl.fan.stats['decoded_gpu'] == 2 * (40 + 40)
         assert wl.rearmed() == 40 * 2        # one resume per failover
         from zkmi.models import gpucodec
         calls = gpucodec.for_device(dev).calls

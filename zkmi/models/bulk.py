@@ -145,13 +145,15 @@ class BulkBatch(object):
     # -- encode ---------------------------------------------------------------
 
     @classmethod
-    def gets(cls, paths, device=None):
+    def gets(cls, paths, device=None, watch=False):
         """GET_DATA of every path (strings, or a device ``(arena u8, off
         i64, len i32)`` triple of path bytes) packed straight into a device
-        request batch (no per-request dict)."""
+        request batch (no per-request dict).  ``watch``: each read arms a
+        data watch (the re-arm of a bulk watch, see
+        :meth:`~zkmi.models.client.Client.watch_bulk`)."""
         dev = _gpu_device(device)
         if dev is None:
-            return cls([{'opcode': 'GET_DATA', 'path': p, 'watch': False}
+            return cls([{'opcode': 'GET_DATA', 'path': p, 'watch': watch}
                         for p in paths], False)
         import numpy as np
         import torch
@@ -175,7 +177,8 @@ class BulkBatch(object):
         z64 = torch.zeros(n, dtype=torch.int64, device=dev)
         op = torch.full((n,), consts.OP_CODES['GET_DATA'], dtype=torch.int32,
                         device=dev)
-        rb = B.RequestBatch(n, op, z32, z32, off, ln, z64, z32, z32, arena,
+        arg = torch.ones(n, dtype=torch.int32, device=dev) if watch else z32
+        rb = B.RequestBatch(n, op, z32, arg, off, ln, z64, z32, z32, arena,
                             arena, torch.zeros(1, dtype=torch.int64,
                                                device=dev),
                             torch.zeros(1, dtype=torch.int32, device=dev),
@@ -265,7 +268,9 @@ class BulkBatch(object):
                                              consts.MAX_PACKET)
             for (o, ln) in frames:
                 pk.append(codec.decode_response(data[o:o + ln], self.xid_map))
-            return BulkResult(self.n, packets=pk)
+            res = BulkResult(self.n, packets=pk)
+            res.raw = data              # (the reply frames as received)
+            return res
         import numpy as np
         import torch
         from ..ops import batch as B
@@ -285,6 +290,8 @@ class BulkBatch(object):
         # the event covers has run
         res = BulkResult(self.n, replies=rep, buf=buf, device=self.device,
                          event=ev)
+        res.frames = ft                 # (the reply frames' offsets)
+        res.nbytes = nbytes
         self.t['finished'] = time.perf_counter()
         res.phases = dict(self.t, submit=self.t_submit)
         res._hold = (host, self.tx_pin)

@@ -130,6 +130,9 @@ class Client(FSM):
         self.tracer = o.get('tracer')
         # bulk codec device: None = the current GPU if any, False = host
         self.bulk_device = o.get('device')
+        # bulk watches (watch_bulk): connections keep notification frames
+        self.note_capture = False
+        self.note_conns = set()
         self._resume_cred = o.get('session')
         # listeners attached before the FSM starts: a JS caller attaching
         # in the constructor's tick sees every event; on a loop thread that
@@ -525,11 +528,13 @@ class Client(FSM):
                 self.loop.call_soon(cb, e)
         self._dispatch(go)
 
-    def bulk_get(self, paths, cb):
+    def bulk_get(self, paths, cb, watch=False):
         """:meth:`bulk` of GET_DATA for every path: ``paths`` is a list of
         strings, or (GPU) a device ``(arena, off, len)`` triple of path
         bytes (uint8 / int64 / int32 tensors), packed straight into the
-        request batch without per-request Python objects."""
+        request batch without per-request Python objects.  ``watch``: each
+        read arms a data watch whose notification goes to the bulk watch
+        sink (:meth:`watch_bulk`), not to a :meth:`watcher`."""
         from .bulk import BulkBatch
         _check_func(cb)
         if isinstance(paths, tuple) and len(paths) == 3 and \
@@ -538,11 +543,11 @@ class Client(FSM):
             if _gpu_device(self.bulk_device) is None:
                 raise ValueError('bulk_get: a device (arena, off, len) '
                                  'triple needs a GPU bulk device')
-            batch = BulkBatch.gets(paths, self.bulk_device)
+            batch = BulkBatch.gets(paths, self.bulk_device, watch=watch)
         elif isinstance(paths, (list, tuple)):
             for p in paths:
                 _check_str(p, 'path')
-            batch = BulkBatch.gets(list(paths), self.bulk_device)
+            batch = BulkBatch.gets(list(paths), self.bulk_device, watch=watch)
         else:
             raise TypeError('paths ([string]) is required')
 
@@ -560,6 +565,44 @@ class Client(FSM):
     def watcher(self, path):
         _check_str(path, 'path')
         return self.loop.run(lambda: self.getSession().watcher(path))
+
+    # -- bulk watches (the node-wide fan-out, zkmi/parallel/fanout.py) --------
+
+    def watch_bulk(self, paths):
+        """Data watches on ``paths`` kept in bulk, for the node-wide fan-out:
+        from now on every connection keeps NOTIFICATION frames in its
+        transport (the native loop's note sink; no Python object per event)
+        for :meth:`take_notes`, and a session that moves re-arms these paths
+        with SET_WATCHES at its last zxid like any watcher's.  Arm them with
+        ``bulk_get(paths, cb, watch=True)``.  Not in the reference, whose
+        watchers handle each notification on the event loop
+        (lib/zk-session.js:853-854)."""
+        for p in paths:
+            _check_str(p, 'path')
+
+        def go():
+            self.note_capture = True
+            self.getSession().bulk_watches.update(paths)
+            conn = self.currentConnection()
+            if conn is not None:
+                conn.start_note_capture()
+        self.loop.run(go)
+
+    def take_notes(self):
+        """(bytes, frames): the NOTIFICATION frames every connection of this
+        client kept since the last call, in arrival order per connection
+        (length prefixes included)."""
+        def go():
+            parts, n = [], 0
+            for c in list(self.note_conns):
+                b, k = c.take_notes()
+                if k:
+                    parts.append(b)
+                    n += k
+                if c.isInState('closed') or c.isInState('error'):
+                    self.note_conns.discard(c)
+            return b''.join(parts), n
+        return self.loop.run(go)
 
     # -- blocking helpers -----------------------------------------------------
 

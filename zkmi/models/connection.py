@@ -71,6 +71,11 @@ class ZKConnectionFSM(FSM):
         self.xid_map = {}
         self.xid = 0
         self.bulks = []                 # in-flight BulkBatch (models/bulk.py)
+        # bulk watch notifications (Client.watch_bulk): kept by the native
+        # transport (note sink), or here on the asyncio loop
+        self.note_native = False
+        self.notes = None
+        self.notes_left = (b'', 0)
         self.bulk_frames_py = 0         # bulk replies routed one by one
         self.reqs = {}
         self.socket = None
@@ -161,6 +166,8 @@ class ZKConnectionFSM(FSM):
         if not self.wanted:
             S.gotoState('closed')
             return
+        if getattr(self.client, 'note_capture', False):
+            self.start_note_capture()
 
         def on_rx(body, more):
             if more > 0:
@@ -240,6 +247,13 @@ class ZKConnectionFSM(FSM):
                 xid = int.from_bytes(body[0:4], 'big', signed=True)
                 if xid >= 0 and self._bulk_rx(xid, body):
                     return
+            if self.notes is not None and len(body) >= 16 and \
+                    body[0:4] == b'\xff\xff\xff\xff':
+                # bulk watch notification (no native note sink)
+                self.notes += len(body).to_bytes(4, 'big')
+                self.notes += body
+                self.notes_n += 1
+                return
             try:
                 pkt = self._decode_reply(body)
             except ZKProtocolError as e:
@@ -346,6 +360,9 @@ class ZKConnectionFSM(FSM):
 
     def state_closed(self, S):
         self.encoder = None
+        if self.socket is not None and self.note_native:
+            # the notifications the transport kept outlive it
+            self.notes_left = self.socket.take_notes()
         if self.socket is not None:
             self.socket.destroy()
         self.socket = None
@@ -392,6 +409,40 @@ class ZKConnectionFSM(FSM):
                        'sent request to server')
         self.socket.write(self.encoder.request(pkt))
         return req
+
+    # -- bulk watch notifications (Client.watch_bulk) ------------------------
+
+    def start_note_capture(self):
+        """Keep this connection's NOTIFICATION frames for
+        :meth:`take_notes` (loop thread): in the native transport (its read
+        path frames the stream and keeps them; the partial frame Python's
+        framer holds is handed over), else in :attr:`notes`."""
+        if self.note_native or self.notes is not None:
+            return
+        sock = self.socket
+        if sock is not None and sock.can_sink_notes():
+            pre = self.decoder.take_pending() if self.decoder else b''
+            sock.note_sink(True, self.config.max_packet, pre)
+            self.note_native = True
+        else:
+            self.notes = bytearray()
+            self.notes_n = 0
+        self.client.note_conns.add(self)
+
+    def take_notes(self):
+        """(bytes, frames) kept since the last call."""
+        if self.note_native:
+            sock = self.socket
+            if sock is None:
+                left, self.notes_left = self.notes_left, (b'', 0)
+                return left
+            return sock.take_notes()
+        if not self.notes:
+            return b'', 0
+        b, n = bytes(self.notes), self.notes_n
+        self.notes = bytearray()
+        self.notes_n = 0
+        return b, n
 
     # -- bulk (GPU-coded, pipelined) batches ----------------------------------
 

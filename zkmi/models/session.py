@@ -85,6 +85,9 @@ class ZKSession(FSM):
         self.config = config
         self.last_attach = 0
         self.last_zxid = 0
+        # paths with bulk data watches (Client.watch_bulk): re-armed on a
+        # move like the watchers' (their notifications go to the fan-out)
+        self.bulk_watches = set()
         self.rearmed = 0            # watches re-armed by SET_WATCHES resumes
         self.session_id = 0
         self.passwd = b'\0' * 8
@@ -357,6 +360,9 @@ class ZKSession(FSM):
                     raise AssertionError('unknown event: ' + e)
                 count += 1
                 all_evts.append(ev)
+        for path in sorted(self.bulk_watches):
+            events['dataChanged'].append(path)
+            count += 1
         if count < 1:
             return
         zxid = self.last_zxid

@@ -12,31 +12,26 @@ Reference behaviour this reproduces at node scale:
 * watch fan-out — one server watch per path, its events delivered to every
   listener (``lib/zk-session.js:853-854``), here to every rank of the node.
 
-Per rank: a :class:`~zkmi.Client` on the ensemble (rank ``r`` prefers
-member ``r % n``), with ``ClientConfig.codec_device`` set on a GPU so its
-(re)connects run K9 (ConnectRequest / ConnectResponse) and its watch resume
-K11 (SET_WATCHES) on the device (:mod:`zkmi.models.gpucodec`).  Each path
-has one owner rank (``crc32(path) % world``) that holds the only server
-watch on it; owners forward the events their watchers emit with
-:class:`WireFanout` (R1).
-
-:class:`WireFanout` ships events as the ZooKeeper wire frames the owner's
-session received — a NOTIFICATION frame (xid -1, type, state, path) and the
-re-arm's GET_DATA reply (data + Stat) — so the node-wide stream is decoded
-by the same kernels as a connection's RX stream: one size exchange, one
-padded ``all_gather_into_tensor`` on the collective device (GPU tensors
-over RCCL/xGMI with ``nccl``), then K1 frame scan + K2-K8 reply decode on
-the GPU of every rank and one device-to-host copy of the decoded table.
-Without a GPU (gloo rehearsal on CPU) the gathered frames are decoded by
-the host codec instead.
+The ensemble is the native server with ``--members 3`` (one tree, three
+ports, fakezk's fault commands; ``csrc/host/zk_fastserver.cpp``) in a child
+process started before anything touches the GPU.  Per rank: a
+:class:`~zkmi.Client` on the ensemble (rank ``r`` prefers member ``r % n``)
+whose (re)connects run K9 and its watch resume K11 on the GPU
+(``ClientConfig.codec_device``).  Each path has one owner rank
+(``owner_of``) holding the only server watch on it, as a bulk watch
+(:meth:`~zkmi.Client.watch_bulk`): the native loop keeps the notification
+frames, the owner re-arms them with ONE bulk GET_DATA(watch) per tick (K10
+encode on the GPU, replies captured in pinned memory, K1 + K2-K8 decode),
+and forwards the raw notification + reply frames with
+:class:`~zkmi.parallel.fanout.FrameFanout` (R1).  Every rank decodes the
+node's stream on its GPU and counts each (path, version) event in HBM; no
+event becomes a Python object on the way.  Writes go out as bulk SET_DATA
+batches.  Without a GPU (the gloo rehearsal on CPU) the same flow runs on
+the host codec.
 """
 
-import collections
-import subprocess
-import sys
 import threading
 import time
-import zlib
 
 import numpy as np
 import torch
@@ -44,171 +39,29 @@ import torch.distributed as dist
 
 from .. import codec
 from .. import consts
-from .. import jute
+from .fanout import FrameFanout, XID_FWD, notification_frames, owner_of, \
+    path_ids
 
-KMAX = 1 << 16            # events one rank forwards per exchange
-_GET_DATA = consts.OP_CODES['GET_DATA']
+__all__ = ['EnsembleControl', 'EnsembleWorkload', 'owner_of']
 
-
-def owner_of(path, world):
-    return zlib.crc32(path.encode('utf-8')) % world
-
-
-class WireFanout(object):
-    """R1 over the node: every rank's watch events, as wire frames, to every
-    rank (collective: all ranks call :meth:`exchange` together)."""
-
-    def __init__(self, group=None, decode_device=None):
-        on = dist.is_available() and dist.is_initialized()
-        self.group = group
-        self.world = dist.get_world_size(group) if on else 1
-        self.rank = dist.get_rank(group) if on else 0
-        backend = dist.get_backend(group) if on else None
-        if decode_device is None and torch.cuda.is_available():
-            decode_device = torch.device('cuda', torch.cuda.current_device())
-        self.dev = torch.device(decode_device) if decode_device else None
-        # collective tensors live where the backend moves them: HBM for
-        # RCCL, host memory for gloo
-        self.coll = self.dev if backend in (None, 'nccl') and self.dev \
-            else torch.device('cpu')
-        self.stats = collections.Counter()
-        self.xt = None
-        if self.dev is not None and self.dev.type == 'cuda':
-            from ..ops import batch as B
-            self.B = B
-            bits = max(10, (self.world * KMAX - 1).bit_length())
-            self.xt = B.XidTable(bits=bits, device=self.dev)
-            x = torch.arange(self.world * KMAX, dtype=torch.int64,
-                             device=self.dev)
-            self.xt.tab[x & self.xt.mask] = (x << 32) | _GET_DATA
-
-    # -- encode (owner side) -------------------------------------------------
-
-    def encode(self, events):
-        """``events`` = [(path, data, Stat)] -> framed NOTIFICATION +
-        GET_DATA reply per event (xid = rank << 16 | k)."""
-        parts = []
-        base = self.rank << 16
-        for k, (path, data, stat) in enumerate(events):
-            parts.append(codec.frame(jute.encode_response({
-                'xid': consts.XID_NOTIFICATION, 'zxid': -1, 'err': 'OK',
-                'opcode': 'NOTIFICATION', 'type': 'DATA_CHANGED',
-                'state': 'SYNC_CONNECTED', 'path': path})))
-            parts.append(codec.frame(jute.encode_response({
-                'xid': base | k, 'zxid': stat.mzxid, 'err': 'OK',
-                'opcode': 'GET_DATA', 'data': data, 'stat': stat})))
-        return b''.join(parts)
-
-    # -- the collective -------------------------------------------------------
-
-    def exchange(self, events):
-        """Send this rank's ``events`` (at most :data:`KMAX`), receive every
-        rank's: returns [(src_rank, path, data, Stat)] in rank order."""
-        if len(events) > KMAX:
-            raise ValueError('at most %d events per exchange' % KMAX)
-        payload = self.encode(events)
-        W = self.world
-        if W == 1:
-            sizes = [len(payload)]
-            rx = None
-        else:
-            # the one size exchange (a single host read of W sizes)
-            n = torch.tensor([len(payload)], dtype=torch.int64,
-                             device=self.coll)
-            st = torch.empty(W, dtype=torch.int64, device=self.coll)
-            dist.all_gather_into_tensor(st, n, group=self.group)
-            sizes = st.cpu().tolist()
-            mx = max(max(sizes), 1)
-            buf = torch.zeros(mx, dtype=torch.uint8, device=self.coll)
-            if payload:
-                buf[:len(payload)].copy_(torch.frombuffer(
-                    bytearray(payload), dtype=torch.uint8))
-            rx = torch.empty(W * mx, dtype=torch.uint8, device=self.coll)
-            dist.all_gather_into_tensor(rx, buf, group=self.group)
-        self.stats['exchanges'] += 1
-        self.stats['bytes'] += sum(sizes)
-        if self.xt is not None:
-            return self._decode_gpu(payload, rx, sizes)
-        return self._decode_host(payload, rx, sizes)
-
-    def _segments(self, payload, rx, sizes):
-        mx = max(max(sizes), 1)
-        if rx is None:
-            return [torch.frombuffer(bytearray(payload or b'\0'),
-                                     dtype=torch.uint8)[:len(payload)]]
-        return [rx[r * mx:r * mx + s] for r, s in enumerate(sizes) if s]
-
-    def _decode_gpu(self, payload, rx, sizes):
-        B = self.B
-        dev = self.dev
-        total = sum(sizes)
-        if total == 0:
-            return []
-        segs = self._segments(payload, rx, sizes)
-        # close the padding gaps on the device (rank order kept)
-        stream = torch.cat([s.to(dev, non_blocking=True) for s in segs])
-        ft = B.frame_scan(stream, total, cap=total // 32 + 1,
-                          window=B.frame_window(512))
-        rep = B.decode_replies(stream, ft, self.xt)
-        cap = ft.off.numel()
-        cols = torch.cat([
-            ft.result.to(torch.int64),
-            rep.xid.to(torch.int64), rep.opcode.to(torch.int64),
-            rep.status.to(torch.int64), rep.err.to(torch.int64),
-            rep.pay_off, rep.pay_len.to(torch.int64),
-            rep.aux0.to(torch.int64), rep.aux1.to(torch.int64),
-            rep.stat64.reshape(-1), rep.stat32.to(torch.int64).reshape(-1)])
-        host = cols.cpu().numpy()                   # one D2H for the table
-        hb = stream.cpu().numpy().tobytes()        # one for the bytes
-        nfr, bad = int(host[0]), int(host[2])
-        if bad or int(host[3]):
-            raise RuntimeError('fan-out stream: bad frame')
-        c = host[4:]
-        xid, op, st, err, po, pl, a0, a1 = (c[k * cap:(k + 1) * cap]
-                                            for k in range(8))
-        s64 = c[8 * cap:14 * cap].reshape(6, cap)
-        s32 = c[14 * cap:19 * cap].reshape(5, cap)
-        out = []
-        notif = consts.OP_CODES['NOTIFICATION']
-        for i in range(0, nfr, 2):
-            j = i + 1
-            if j >= nfr or op[i] != notif or op[j] != _GET_DATA or \
-                    st[i] or st[j] or err[i] or err[j]:
-                raise RuntimeError('fan-out stream: unpaired frame %d' % i)
-            path = hb[po[i]:po[i] + pl[i]].decode('utf-8')
-            data = hb[po[j]:po[j] + pl[j]]
-            stat = jute.Stat(int(s64[0, j]), int(s64[1, j]), int(s64[2, j]),
-                             int(s64[3, j]), int(s32[0, j]), int(s32[1, j]),
-                             int(s32[2, j]), int(s64[4, j]), int(s32[3, j]),
-                             int(s32[4, j]), int(s64[5, j]))
-            out.append((int(xid[j]) >> 16, path, data, stat))
-        self.stats['decoded_gpu'] += len(out)
-        return out
-
-    def _decode_host(self, payload, rx, sizes):
-        out = []
-        for seg in self._segments(payload, rx, sizes):
-            raw = bytes(seg.numpy().tobytes()) if seg.numel() else b''
-            frames, _, bad = codec.scan_frames(raw, 0, len(raw),
-                                               consts.MAX_PACKET)
-            if bad >= 0:
-                raise RuntimeError('fan-out stream: bad frame')
-            bodies = [raw[o:o + n] for o, n in frames]
-            for i in range(0, len(bodies), 2):
-                nb, rb = bodies[i], bodies[i + 1]
-                xid = int.from_bytes(rb[0:4], 'big', signed=True)
-                n = codec.decode_response(nb, {})
-                r = codec.decode_response(rb, {xid: 'GET_DATA'})
-                out.append((xid >> 16, n['path'], r['data'], r['stat']))
-        self.stats['decoded_host'] += len(out)
-        return out
+_DIGITS = 5                      # paths are /ens/pNNNNN
 
 
 class EnsembleControl(object):
-    """The fake ensemble as a child process (``python -m zkmi.server
-    --ensemble N``), driven over its stdin fault-command channel."""
+    """The ensemble as a child process — the native server with ``n``
+    members (``zkmi.server.fast``), or with ``native=False`` the Python
+    fake ensemble (``python -m zkmi.server --ensemble N``) — driven over its
+    stdin fault-command channel: :meth:`outage`, :meth:`start`."""
 
-    def __init__(self, n=3, tick_ms=250):
+    def __init__(self, n=3, tick_ms=250, native=True):
+        from ..server import fast
+        self.native = native and fast.available()
+        if self.native:
+            self.srv = fast.FastZKServer(members=n)
+            self.ports = list(self.srv.ports)
+            return
+        import subprocess
+        import sys
         self.p = subprocess.Popen(
             [sys.executable, '-m', 'zkmi.server', '--ensemble', str(n),
              '--tick-ms', str(tick_ms)],
@@ -228,13 +81,23 @@ class EnsembleControl(object):
         return ans[1].strip() if len(ans) > 1 else ''
 
     def outage(self, i, sets):
+        """Member ``i`` down, then ``sets`` = [(path, data)] applied while
+        its sessions are detached; returns the zxid after them."""
+        if self.native:
+            return self.srv.outage(i, sets)
         return int(self._cmd('outage %d %s' % (i, ' '.join(
             '%s=%s' % (p, d.hex()) for p, d in sets))))
 
     def start(self, i):
-        self._cmd('start %d' % i)
+        if self.native:
+            self.srv.start(i)
+        else:
+            self._cmd('start %d' % i)
 
     def close(self):
+        if self.native:
+            self.srv.shutdown()
+            return
         try:
             self.p.stdin.close()
             self.p.wait(10)
@@ -251,25 +114,37 @@ def _bcast_ints(vals, n, src, device):
     return t.cpu().tolist()
 
 
+def _patch_xids(raw):
+    """Host path: reply frames with their xids set to XID_FWD."""
+    b = bytearray(raw)
+    frames, _, _ = codec.scan_frames(bytes(b), 0, len(b), consts.MAX_PACKET)
+    x = XID_FWD.to_bytes(4, 'big')
+    for o, _ in frames:
+        b[o:o + 4] = x
+    return bytes(b)
+
+
 class EnsembleWorkload(object):
     """Collective: every rank constructs it and calls :meth:`step` together.
 
-    ``n_paths`` znodes ``/ens/pNNNNN``; a step sets ``writes`` of them
-    (each exactly once, new data ``s<step>``) and ticks the fan-out until
-    every rank received every resulting event.  Every ``failover_every``-th
-    step the writes are made by the ensemble itself while the member rank 0
-    is on is down (:meth:`EnsembleControl.outage`): rank 0's session (and
-    any other session on that member) fails over, resumes its watches with
+    ``n_paths`` znodes ``/ens/pNNNNN``; a step sets ``writes`` of them (each
+    exactly once) and ticks the fan-out until every rank received every
+    resulting event.  Every ``failover_every``-th step the writes are made
+    by the ensemble itself while the member rank 0 is on is down
+    (:meth:`EnsembleControl.outage`): rank 0's session (and any other
+    session on that member) fails over, resumes its watches with
     SET_WATCHES and the server replays the missed changes, which the owners
-    forward like any other event.  :meth:`verify` checks that every rank saw
-    every event (initial arm, live and replayed) exactly once.
+    forward like any other event.  Each event is identified by (path,
+    version); :meth:`verify` checks that every rank saw every one (initial
+    arm, live and replayed) exactly once.  ``max_versions`` bounds the
+    writes per path the check can count.
 
-    ``ctl`` is the :class:`EnsembleControl` on rank 0 (None elsewhere);
-    the member ports are broadcast from rank 0."""
+    ``ctl`` is the :class:`EnsembleControl` on rank 0 (None elsewhere); the
+    member ports are broadcast from rank 0."""
 
     def __init__(self, ctl=None, n_members=3, n_paths=256, writes=64,
                  failover_every=4, session_timeout=8000, codec_device=None,
-                 group=None, seed=0, coll_device=None):
+                 group=None, seed=0, coll_device=None, max_versions=64):
         from ..models.client import Client
         from ..config import ClientConfig, RecoveryPolicy
         on = dist.is_available() and dist.is_initialized()
@@ -289,16 +164,18 @@ class EnsembleWorkload(object):
         me = self.rank % n
         servers = [{'address': '127.0.0.1', 'port': ports[(me + k) % n]}
                    for k in range(n)]
+        # (a member that went down is retried after 5 ms, not the 50-100
+        # ms of an interactive client: the failover is the measured step)
         cfg = ClientConfig(
             ping_floor_ms=500, ping_timeout_floor_ms=2000,
-            connect_policy=RecoveryPolicy(1000, 3, 50, 400),
-            default_policy=RecoveryPolicy(1000, 3, 100, 800),
+            connect_policy=RecoveryPolicy(1000, 3, 5, 100),
+            default_policy=RecoveryPolicy(1000, 3, 5, 100),
             codec_device=str(codec_device) if codec_device else None)
+        self.dev = torch.device(codec_device) if codec_device else None
+        if self.dev is not None and self.dev.type != 'cuda':
+            self.dev = None
         self.connects = 0
         self._lk = threading.Lock()
-        # signalled by every event an owner's watcher emits: the fan-out
-        # waits on it instead of polling on a timer
-        self._ev = threading.Condition(self._lk)
         self._connected = threading.Event()
 
         def on_connect():
@@ -308,17 +185,24 @@ class EnsembleWorkload(object):
         self.client = Client({'servers': servers,
                               'sessionTimeout': session_timeout,
                               'config': cfg,
+                              'device': self.dev if self.dev else False,
                               'listeners': [('connect', on_connect)]})
         self.client.wait_connected(20)
         self.paths = ['/ens/p%05d' % k for k in range(n_paths)]
         self.writes = min(writes, n_paths)
         self.failover_every = failover_every
         self.seed = seed
-        self.fan = WireFanout(group, decode_device=codec_device)
-        self.pending = []
-        self.seen = collections.Counter()
-        self.expected = set()
+        self.fan = FrameFanout(group, device=self.dev)
+        # (path, version) events: expected and seen, per rank
+        self.vmax = max_versions
+        self.version = np.zeros(n_paths, np.int64)      # last write's
+        self.expected = np.zeros(n_paths * self.vmax, np.int32)
+        dev = self.dev if self.dev is not None else torch.device('cpu')
+        self.seen = torch.zeros(n_paths * self.vmax, dtype=torch.int32,
+                                device=dev)
+        self.bad_frames = torch.zeros(1, dtype=torch.int64, device=dev)
         self.replayed = set()
+        self.step_ms = []
         self.step_no = 0
         self.failovers = 0
         self.down = None
@@ -327,11 +211,12 @@ class EnsembleWorkload(object):
         self._barrier()
         self.mine = [p for p in self.paths
                      if owner_of(p, self.world) == self.rank]
-        for p in self.mine:
-            self.client.watcher(p).on(
-                'dataChanged', lambda d, s, p=p: self._on_event(p, d, s))
-        self.expected.update((p, b'init') for p in self.paths)
-        self._deliver_until(len(self.paths), mine=len(self.mine))
+        self.client.watch_bulk(self.mine)
+        self.expected[np.arange(n_paths) * self.vmax] = 1
+        # the initial values go out like every later event: a notification
+        # (type -1: none) + the reply of the read that armed the watch
+        notes = notification_frames(self.mine)
+        self._deliver_until(len(self.paths), initial=(notes, self.mine))
 
     # -- plumbing -------------------------------------------------------------
 
@@ -339,57 +224,126 @@ class EnsembleWorkload(object):
         if self.world > 1:
             dist.barrier(group=self.group)
 
+    def _bulk(self, call, *args, timeout=60.0, **kw):
+        done = threading.Event()
+        box = {}
+
+        def cb(err, res=None):
+            box['err'], box['res'] = err, res
+            done.set()
+        call(*args, cb, **kw)
+        if not done.wait(timeout):
+            raise RuntimeError('bulk batch timed out')
+        if box['err'] is not None:
+            raise box['err']
+        return box['res']
+
     def _create_tree(self):
         c = self.client
         c.call_sync('create', '/ens', b'', {})
-        left = [len(self.paths)]
-        done = threading.Event()
-        errs = []
+        acl = [{'perms': ['READ', 'WRITE', 'CREATE', 'DELETE', 'ADMIN'],
+                'id': {'scheme': 'world', 'id': 'anyone'}}]
+        res = self._bulk(c.bulk, [{'opcode': 'CREATE', 'path': p,
+                                   'data': b'init', 'acl': acl}
+                                  for p in self.paths])
+        bad = [e for e in res.errors() if e != 'OK']
+        if bad:
+            raise RuntimeError('ensemble tree create failed: %r' % bad[:3])
 
-        def cb(err, *_):
-            if err is not None:
-                errs.append(err)
-            left[0] -= 1
-            if left[0] == 0:
-                done.set()
+    def _rearm(self, notes, k):
+        """The owner side of one tick: the ``k`` notification frames in
+        ``notes`` re-armed with one bulk GET_DATA(watch); returns the
+        forwardable stream [notifications][replies] and its frame count."""
+        if k == 0:
+            return b'', 0
+        if self.dev is None:
+            frames, _, _ = codec.scan_frames(notes, 0, len(notes),
+                                             consts.MAX_PACKET)
+            paths = [codec.decode_response(notes[o:o + ln], {})['path']
+                     for o, ln in frames]
+            res = self._bulk(self.client.bulk_get, paths, watch=True)
+            return notes + _patch_xids(res.raw), 2 * k
+        from ..ops import batch as B
+        nd = torch.frombuffer(bytearray(notes), dtype=torch.uint8) \
+            .to(self.dev, non_blocking=True)
+        ft = B.frame_scan(nd, len(notes), cap=k, window=B.frame_window(512))
+        rep = B.decode_replies(nd, ft, self.fan.xt)
+        triple = (nd, rep.pay_off[:k], rep.pay_len[:k])
+        res = self._bulk(self.client.bulk_get, triple, watch=True)
+        return torch.cat([nd, self.fan.forward_replies(res)]), 2 * k
 
-        def go():
-            for p in self.paths:
-                c.create(p, b'init', {}, cb)
-        c.loop.run(go)
-        if not done.wait(60) or errs:
-            raise RuntimeError('ensemble tree create failed: %r' % errs[:3])
+    def _initial(self, notes, paths):
+        res = self._bulk(self.client.bulk_get, list(paths), watch=True)
+        if self.dev is None:
+            return notes + _patch_xids(res.raw), 2 * len(paths)
+        nd = torch.frombuffer(bytearray(notes or b'\0'),
+                              dtype=torch.uint8)[:len(notes)].to(self.dev)
+        return torch.cat([nd, self.fan.forward_replies(res)]), 2 * len(paths)
 
-    def _on_event(self, path, data, stat):
-        with self._lk:
-            self.pending.append((path, data, stat))
-            self._ev.notify_all()
+    def _count(self, g):
+        """Count the gathered events into ``seen``; returns how many."""
+        nev = sum(g.frames) // 2
+        if nev == 0:
+            return 0
+        if self.dev is None:
+            pk = self.fan.decode(g)
+            base = 0
+            for f in g.frames:
+                m = f // 2
+                for i in range(m):
+                    nt, rp = pk[base + i], pk[base + m + i]
+                    pid = int(nt['path'][-_DIGITS:])
+                    ok = (nt['opcode'] == 'NOTIFICATION' and
+                          rp['opcode'] == 'GET_DATA' and rp['err'] == 'OK')
+                    if not ok:
+                        self.bad_frames += 1
+                        continue
+                    v = min(rp['stat'].version, self.vmax - 1)
+                    self.seen[pid * self.vmax + v] += 1
+                base += f
+            return nev
+        ft, rep = self.fan.decode(g)
+        nidx, ridx = FrameFanout.pair_index(g.frames, self.dev)
+        pid = path_ids(g.buf, rep.pay_off[nidx], rep.pay_len[nidx], _DIGITS)
+        ver = rep.stat32[0][ridx].to(torch.int64).clamp(0, self.vmax - 1)
+        ok = (rep.opcode[nidx] == consts.OP_CODES['NOTIFICATION']) & \
+             (rep.opcode[ridx] == consts.OP_CODES['GET_DATA']) & \
+             (rep.status[ridx] == 0) & (rep.err[ridx] == 0) & \
+             (rep.status[nidx] == 0)
+        key = (pid.clamp(0, len(self.paths) - 1) * self.vmax + ver)[ok]
+        self.seen.index_put_((key,), torch.ones_like(key, dtype=torch.int32),
+                             accumulate=True)
+        self.bad_frames += (~ok).sum()
+        return nev
 
-    def _deliver_until(self, want, timeout=60.0, mine=None):
+    def _deliver_until(self, want, timeout=60.0, mine=None, initial=None):
         """Tick the fan-out until every rank has received ``want`` events
-        (collective; the stop decision is all-reduced).  Returns the number
-        this rank received.  ``mine``: the events this rank's watchers will
-        emit — each round first waits (on the event condition, no polling)
-        until they are all pending or a tick (5 ms) passes, so a step is
-        usually ONE exchange."""
+        (collective; the stop decision is all-reduced).  ``mine``: the
+        events this rank's notifications will bring — each tick first polls
+        the transports' kept notifications until they are all in or a tick
+        (5 ms) passes, so a step is usually ONE exchange."""
         got = 0
         t_end = time.monotonic() + timeout
         # [not done, timed out], all-reduced with MAX: every rank stops
-        # together, and a rank's timeout makes every rank raise (none is
-        # left waiting in the next collective)
+        # together, and a rank's timeout makes every rank raise
         flag = torch.zeros(2, dtype=torch.int64, device=self.coll)
-        sent = 0
+        have = 0
         while True:
-            with self._lk:
+            if initial is not None:
+                stream, nf = self._initial(*initial)
+                initial = None
+            else:
+                notes, k = self.client.take_notes()
                 if mine is not None:
-                    self._ev.wait_for(
-                        lambda: sent + len(self.pending) >= mine, 0.005)
-                batch = self.pending[:KMAX]
-                del self.pending[:KMAX]
-            sent += len(batch)
-            for src, path, data, stat in self.fan.exchange(batch):
-                self.seen[(path, data)] += 1
-                got += 1
+                    t_tick = time.monotonic() + 0.005
+                    while have + k < mine and time.monotonic() < t_tick:
+                        time.sleep(0.0002)
+                        more, k2 = self.client.take_notes()
+                        notes += more
+                        k += k2
+                have += k
+                stream, nf = self._rearm(notes, k)
+            got += self._count(self.fan.gather(stream, nf))
             flag[0] = 0 if got >= want else 1
             flag[1] = 1 if time.monotonic() > t_end else 0
             if self.world > 1:
@@ -404,9 +358,8 @@ class EnsembleWorkload(object):
 
     def _choose(self, s):
         rng = np.random.default_rng(self.seed * 1000003 + s)
-        return [self.paths[k] for k in rng.choice(len(self.paths),
-                                                  self.writes,
-                                                  replace=False)]
+        return [int(k) for k in rng.choice(len(self.paths), self.writes,
+                                           replace=False)]
 
     def _member(self):
         def go():
@@ -419,11 +372,22 @@ class EnsembleWorkload(object):
 
     def step(self):
         """One step (collective); returns the events this rank received."""
+        t0 = time.perf_counter()
+        try:
+            return self._step()
+        finally:
+            self.step_ms.append((time.perf_counter() - t0) * 1e3)
+
+    def _step(self):
         s = self.step_no
         self.step_no += 1
         data = b's%d' % s
         chosen = self._choose(s)
-        self.expected.update((p, data) for p in chosen)
+        for k in chosen:
+            self.version[k] += 1
+            v = min(int(self.version[k]), self.vmax - 1)
+            self.expected[k * self.vmax + v] += 1
+        cp = [self.paths[k] for k in chosen]
         fail = self.failover_every and (s % self.failover_every ==
                                         self.failover_every - 1)
         if fail:
@@ -435,11 +399,11 @@ class EnsembleWorkload(object):
                 m = mine_m
                 if self.down is not None:
                     self.ctl.start(self.down)       # the last victim is back
-                self.ctl.outage(m, [(p, data) for p in chosen])
+                self.ctl.outage(m, [(p, data) for p in cp])
                 self.down = m
             m = _bcast_ints([m] if m is not None else None, 1, 0,
                             self.coll)[0]
-            self.replayed.update((p, data) for p in chosen)
+            self.replayed.update((p, data) for p in cp)
             self.failovers += 1
             # every session on the killed member reconnects and replays
             if mine_m == m:
@@ -447,49 +411,40 @@ class EnsembleWorkload(object):
                 while self.connects <= before:
                     if time.monotonic() > t_end:
                         raise RuntimeError('rank %d: no failover' % self.rank)
-                    time.sleep(0.005)
+                    time.sleep(0.002)
         else:
-            mine = chosen[self.rank::self.world]
-            self._set_all(mine, data)
+            mine = cp[self.rank::self.world]
+            if mine:
+                res = self._bulk(self.client.bulk, [
+                    {'opcode': 'SET_DATA', 'path': p, 'data': data,
+                     'version': -1} for p in mine])
+                bad = [e for e in res.errors() if e != 'OK']
+                if bad:
+                    raise RuntimeError('set failed: %r' % bad[:3])
         self._barrier()
-        mine = sum(1 for p in chosen if owner_of(p, self.world) == self.rank)
-        return self._deliver_until(len(chosen), mine=mine)
-
-    def _set_all(self, paths, data):
-        if not paths:
-            return
-        c = self.client
-        left = [len(paths)]
-        done = threading.Event()
-        errs = []
-
-        def cb(err, *_):
-            if err is not None:
-                errs.append(err)
-            left[0] -= 1
-            if left[0] == 0:
-                done.set()
-
-        def go():
-            for p in paths:
-                c.set(p, data, -1, cb)
-        c.loop.run(go)
-        if not done.wait(30) or errs:
-            raise RuntimeError('set failed: %r' % errs[:3])
+        mine = sum(1 for p in cp if owner_of(p, self.world) == self.rank)
+        return self._deliver_until(len(cp), mine=mine)
 
     def rearmed(self):
         """Watches this rank's session re-armed through SET_WATCHES."""
         return self.client.loop.run(lambda: self.client.getSession().rearmed)
 
     def verify(self):
-        """Every expected (path, data) seen exactly once on this rank, and
-        nothing else.  Returns a problem description or None."""
-        extra = [k for k in self.seen if k not in self.expected]
-        dup = [k for k, v in self.seen.items() if v != 1]
-        miss = [k for k in self.expected if self.seen.get(k, 0) == 0]
-        if extra or dup or miss:
-            return {'missing': miss[:5], 'dup': dup[:5], 'extra': extra[:5],
-                    'n_missing': len(miss), 'n_dup': len(dup)}
+        """Every expected (path, version) event seen exactly once on this
+        rank, and nothing else.  Returns a problem description or None."""
+        seen = self.seen.cpu().numpy()
+        bad = int(self.bad_frames.item())
+        miss = np.nonzero((self.expected > 0) & (seen == 0))[0]
+        dup = np.nonzero(seen > 1)[0]
+        extra = np.nonzero((self.expected == 0) & (seen > 0))[0]
+        if len(miss) or len(dup) or len(extra) or bad:
+            def name(i):
+                return (self.paths[i // self.vmax], int(i % self.vmax))
+            return {'missing': [name(i) for i in miss[:5]],
+                    'dup': [name(i) for i in dup[:5]],
+                    'extra': [name(i) for i in extra[:5]],
+                    'n_missing': len(miss), 'n_dup': len(dup),
+                    'bad_frames': bad}
         return None
 
     def close(self):

@@ -159,6 +159,25 @@ class TcpSocket(EventEmitter):
         not captured go to 'data' as usual)."""
         self.transport.capture(x0, n, addr, size, max_packet, done, prefix)
 
+    def can_sink_notes(self):
+        """True when the transport can keep NOTIFICATION frames itself (the
+        native loop's Transport.note_sink)."""
+        return (self.transport is not None and not self.closed and
+                hasattr(self.transport, 'note_sink'))
+
+    def note_sink(self, on, max_packet, prefix=b''):
+        """Keep (``on``) every NOTIFICATION frame in the transport instead of
+        emitting it; :meth:`take_notes` drains them."""
+        self.transport.note_sink(on, max_packet, prefix)
+
+    def take_notes(self):
+        """(bytes, frames): the NOTIFICATION frames kept since the last
+        call, length prefixes included."""
+        t = self.transport
+        if t is None or not hasattr(t, 'take_notes'):
+            return b'', 0
+        return t.take_notes()
+
     def capture_cancel(self):
         if self.transport is not None and hasattr(self.transport,
                                                   'capture_cancel'):

@@ -269,6 +269,7 @@ def run_ensemble(a):
                                 codec_device=dev)
         for _ in range(a.warmup):
             wl.step()
+        wl.phase_ms.clear()
         if world > 1:
             dist.barrier()
         if dev is not None:
@@ -323,6 +324,8 @@ def run_ensemble(a):
                         'reaches every rank exactly once, checked)',
             'failovers': int(fo // world),
             'step_ms_rank0': [round(x, 2) for x in wl.step_ms],
+            'phase_ms_rank0': {k: round(v, 2)
+                               for k, v in wl.phase_ms.items()},
             'watches_rearmed_by_set_watches': int(rep),
             'events_decoded_on_gpu': int(dg),
             'events_decoded_on_host': int(dh),

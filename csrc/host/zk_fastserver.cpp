@@ -74,6 +74,7 @@
 #include <string>
 #include <thread>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 namespace {
@@ -110,11 +111,17 @@ struct Stat {
 };
 
 // Watching sessions (one-shot): usually none or one, so a short vector.
+// SET_WATCHES lists at least this long look their paths up on SW_THREADS
+// threads
+constexpr size_t SW_PAR_MIN = 8192;
+constexpr size_t SW_THREADS = 8;
+
 struct Watchers {
   std::vector<int64_t> s;
-  void add(int64_t sid) {
-    for (int64_t x : s) if (x == sid) return;
+  bool add(int64_t sid) {
+    for (int64_t x : s) if (x == sid) return false;
     s.push_back(sid);
+    return true;
   }
   bool drop(int64_t sid) {
     for (size_t i = 0; i < s.size(); ++i)
@@ -204,6 +211,13 @@ struct Server {
   // session's connection route
   std::mutex wmu;
   std::unordered_map<std::string, Watchers> ew;
+  // what each session armed (the index drop_watches walks instead of the
+  // tree): nodes it data-/child-watches, missing paths it exist-watches
+  struct SessW {
+    std::unordered_set<Node*> d, c;
+    std::unordered_set<std::string> e;
+  };
+  std::unordered_map<int64_t, SessW> sw;
   std::unordered_map<int64_t, Conn*> route;
   std::atomic<uint64_t> n_notes{0};
   // members: connections per member (under mu, exclusive to change)
@@ -254,22 +268,38 @@ struct Server {
   // -- watches (callers hold wmu) --------------------------------------------
   // table 0: data watch (of the node, or an exist watch of a missing path);
   // table 1: child watch of the node
-  void arm(int table, const std::string& path, Node* nd, int64_t sid) {
-    if (table == 1) nd->cw.add(sid);
-    else if (nd != nullptr) nd->dw.add(sid);
-    else ew[path].add(sid);
+  // table 2 (internal): the exist watches of a missing path
+  void arm(int table, const std::string& path, Node* nd, int64_t sid,
+           SessW* ss = nullptr) {
+    if (table == 1) {
+      if (nd->cw.add(sid)) (ss ? *ss : sw[sid]).c.insert(nd);
+    } else if (nd != nullptr) {
+      if (nd->dw.add(sid)) (ss ? *ss : sw[sid]).d.insert(nd);
+    } else if (ew[path].add(sid)) {
+      (ss ? *ss : sw[sid]).e.insert(path);
+    }
+  }
+  void unlist(int64_t sid, int table, Node* nd, const std::string& path) {
+    auto it = sw.find(sid);
+    if (it == sw.end()) return;
+    if (table == 0) it->second.d.erase(nd);
+    else if (table == 1) it->second.c.erase(nd);
+    else it->second.e.erase(path);
   }
   // A notification frame for `sid`'s connection: `self` (the connection
   // being served) gets it in its output now, ahead of the reply being
   // built; another connection through its notes and its worker.
   void notify(int64_t sid, int32_t type, const std::string& path, Conn* self);
-  // Fire and clear a watcher list; returns the sessions notified.
+  // Fire and clear a watcher list (`table`, `nd`: which one, for the
+  // sessions' index); returns the sessions notified.
   std::vector<int64_t> fire(Watchers& w, const std::string& path, int32_t type,
-                            Conn* self, const std::vector<int64_t>* skip) {
+                            Conn* self, const std::vector<int64_t>* skip,
+                            int table, Node* nd) {
     std::vector<int64_t> sids;
     sids.swap(w.s);
     std::vector<int64_t> fired;
     for (int64_t sid : sids) {
+      unlist(sid, table, nd, path);
       if (skip != nullptr &&
           std::find(skip->begin(), skip->end(), sid) != skip->end())
         continue;
@@ -278,18 +308,20 @@ struct Server {
     }
     return fired;
   }
-  // A session's connection is gone: its watches go with it (a pass over
-  // the tree — a disconnect, not a request, pays it).
+  // A session's connection is gone: its watches go with it (through the
+  // session's index: O(its watches), not a pass over the tree).
   void drop_watches(int64_t sid) {
-    for (auto& kv : nodes) {
-      kv.second->dw.drop(sid);
-      kv.second->cw.drop(sid);
+    auto it = sw.find(sid);
+    if (it == sw.end()) return;
+    for (Node* nd : it->second.d) nd->dw.drop(sid);
+    for (Node* nd : it->second.c) nd->cw.drop(sid);
+    for (const std::string& p : it->second.e) {
+      auto e = ew.find(p);
+      if (e == ew.end()) continue;
+      e->second.drop(sid);
+      if (e->second.s.empty()) ew.erase(e);
     }
-    for (auto it = ew.begin(); it != ew.end();) {
-      it->second.drop(sid);
-      if (it->second.s.empty()) it = ew.erase(it);
-      else ++it;
-    }
+    sw.erase(it);
   }
 
   // -- writes (exclusive tree lock; they take wmu to fire) -------------------
@@ -305,37 +337,72 @@ struct Server {
     nd->st.dlen = dl;
     if (!nd->dw.s.empty()) {
       std::lock_guard<std::mutex> g(wmu);
-      fire(nd->dw, p, EV_DATA_CHANGED, self, nullptr);
+      fire(nd->dw, p, EV_DATA_CHANGED, self, nullptr, 0, nd);
     }
     *out = nd;
     return E_OK;
   }
 
   // SET_WATCHES (relZxid, data, exist, child path lists): re-arm, and fire
-  // at once what changed after relZxid (fakezk.py set_watches).
+  // at once what changed after relZxid (fakezk.py set_watches).  A resume
+  // carries every watch of the session (tens of thousands for the bulk
+  // watches of the node-wide fan-out): the tree lookups — the cost, one
+  // hash probe and its cache misses per path — run on several threads
+  // (the tree cannot change: the caller holds the shared tree lock), then
+  // the watches are armed or fired in list order under wmu.
   void set_watches(Rd& r, int64_t sid, Conn* self) {
     const int64_t rel = r.i64();
-    std::lock_guard<std::mutex> g(wmu);
+    struct Ent { int list; const char* s; int32_t l; };
+    std::vector<Ent> es;
     for (int list = 0; list < 3 && r.ok; ++list) {
       const int32_t cnt = r.i32();
-      for (int32_t k = 0; k < cnt && r.ok; ++k) {
+      if (!r.ok || cnt < 0) break;
+      es.reserve(es.size() + (size_t)cnt);
+      for (int32_t k = 0; k < cnt; ++k) {
         const uint8_t* s; int32_t l;
         if (!r.buf(&s, &l)) break;
-        const std::string path((const char*)s, l);
-        Node* nd = find(path);
-        if (list == 0) {
-          if (nd == nullptr) notify(sid, EV_DELETED, path, self);
-          else if (nd->st.mzxid > rel) notify(sid, EV_DATA_CHANGED, path, self);
-          else arm(0, path, nd, sid);
-        } else if (list == 1) {
-          if (nd != nullptr) notify(sid, EV_CREATED, path, self);
-          else arm(0, path, nullptr, sid);
-        } else {
-          if (nd == nullptr) notify(sid, EV_DELETED, path, self);
-          else if (nd->st.pzxid > rel)
-            notify(sid, EV_CHILDREN_CHANGED, path, self);
-          else arm(1, path, nd, sid);
-        }
+        es.push_back({list, (const char*)s, l});
+      }
+    }
+    const size_t n = es.size();
+    std::vector<Node*> nds(n);
+    auto look = [&](size_t a, size_t b) {
+      std::string p;
+      for (size_t i = a; i < b; ++i) {
+        p.assign(es[i].s, (size_t)es[i].l);
+        nds[i] = find(p);
+      }
+    };
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    const size_t T = n >= SW_PAR_MIN ? std::min<size_t>(SW_THREADS, hw) : 1;
+    if (T > 1) {
+      std::vector<std::thread> th;
+      for (size_t t = 1; t < T; ++t)
+        th.emplace_back(look, n * t / T, n * (t + 1) / T);
+      look(0, n / T);
+      for (auto& t : th) t.join();
+    } else {
+      look(0, n);
+    }
+    std::lock_guard<std::mutex> g(wmu);
+    SessW& ss = sw[sid];
+    ss.d.reserve(ss.d.size() + n);
+    std::string path;
+    for (size_t i = 0; i < n; ++i) {
+      Node* nd = nds[i];
+      path.assign(es[i].s, (size_t)es[i].l);
+      if (es[i].list == 0) {
+        if (nd == nullptr) notify(sid, EV_DELETED, path, self);
+        else if (nd->st.mzxid > rel) notify(sid, EV_DATA_CHANGED, path, self);
+        else arm(0, path, nd, sid, &ss);
+      } else if (es[i].list == 1) {
+        if (nd != nullptr) notify(sid, EV_CREATED, path, self);
+        else arm(0, path, nullptr, sid, &ss);
+      } else {
+        if (nd == nullptr) notify(sid, EV_DELETED, path, self);
+        else if (nd->st.pzxid > rel)
+          notify(sid, EV_CHILDREN_CHANGED, path, self);
+        else arm(1, path, nd, sid, &ss);
       }
     }
   }
@@ -461,10 +528,10 @@ struct Server {
             const size_t mark = o->size();
             auto it = ew.find(*key);
             if (it != ew.end()) {
-              fire(it->second, *key, EV_CREATED, c, nullptr);
+              fire(it->second, *key, EV_CREATED, c, nullptr, 2, nullptr);
               ew.erase(it);
             }
-            fire(par->cw, ppath, EV_CHILDREN_CHANGED, c, nullptr);
+            fire(par->cw, ppath, EV_CHILDREN_CHANGED, c, nullptr, 1, par);
             note = o->substr(mark);
             o->resize(mark);
           }
@@ -498,10 +565,10 @@ struct Server {
             std::lock_guard<std::mutex> g(wmu);
             const size_t mark = o->size();
             const std::vector<int64_t> done =
-                fire(nd->dw, *key, EV_DELETED, c, nullptr);
-            fire(nd->cw, *key, EV_DELETED, c, &done);
+                fire(nd->dw, *key, EV_DELETED, c, nullptr, 0, nd);
+            fire(nd->cw, *key, EV_DELETED, c, &done, 1, nd);
             if (par != nullptr)
-              fire(par->cw, ppath, EV_CHILDREN_CHANGED, c, nullptr);
+              fire(par->cw, ppath, EV_CHILDREN_CHANGED, c, nullptr, 1, par);
             note = o->substr(mark);
             o->resize(mark);
           }

@@ -40,7 +40,7 @@ def _worker(rank, world, mport, steps, errq, outq):
             got = [wl.step() for _ in range(steps)]
             bad = wl.verify()
             outq.put((rank, bad, got, wl.failovers, wl.rearmed(),
-                      len(wl.replayed), dict(wl.fan.stats)))
+                      wl.replayed, dict(wl.fan.stats)))
             dist.barrier()
             wl.close()
         finally:

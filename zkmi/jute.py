@@ -242,11 +242,59 @@ class JuteWriter(object):
 
     def write_string_vector(self, v):
         self.write_int(len(v))
+        if isinstance(v, PackedStrings):
+            self.buf += v.blob
+            return
         for s in v:
             self.write_ustring(s)
 
     def getvalue(self):
         return bytes(self.buf)
+
+
+class PackedStrings(object):
+    """A jute string vector kept encoded: ``n`` entries, ``blob`` their
+    length-prefixed UTF-8 bytes (the vector without its count).  For a large
+    vector re-sent unchanged — the bulk watches every SET_WATCHES resume
+    carries — so a resume copies bytes instead of encoding each path again.
+    ``a + b`` concatenates (either side may be a list of strings)."""
+
+    __slots__ = ('n', 'blob')
+
+    def __init__(self, n=0, blob=b''):
+        self.n = n
+        self.blob = blob
+
+    @classmethod
+    def of(cls, strings):
+        if isinstance(strings, PackedStrings):
+            return strings
+        enc = [s.encode('utf-8') for s in strings]
+        return cls(len(enc), b''.join(len(e).to_bytes(4, 'big') + e
+                                      for e in enc))
+
+    def __add__(self, other):
+        o = PackedStrings.of(other)
+        return PackedStrings(self.n + o.n, self.blob + o.blob)
+
+    def __radd__(self, other):
+        return PackedStrings.of(other) + self
+
+    def __len__(self):
+        return self.n
+
+    def __iter__(self):
+        b, k = self.blob, 0
+        for _ in range(self.n):
+            ln = int.from_bytes(b[k:k + 4], 'big')
+            yield b[k + 4:k + 4 + ln].decode('utf-8')
+            k += 4 + ln
+
+
+def packed_events(events):
+    """True when a SET_WATCHES ``events`` dict holds a :class:`PackedStrings`
+    (encode it with this module's :func:`encode_request`)."""
+    return any(isinstance(v, PackedStrings) for v in events.values())
 
 
 def perms_to_mask(perms):

@@ -151,10 +151,26 @@ class BulkBatch(object):
         request batch (no per-request dict).  ``watch``: each read arms a
         data watch (the re-arm of a bulk watch, see
         :meth:`~zkmi.models.client.Client.watch_bulk`)."""
+        return cls._uniform('GET_DATA', paths, device, 1 if watch else 0)
+
+    @classmethod
+    def sets(cls, paths, data, device=None, version=-1):
+        """SET_DATA of ``data`` (one bytes value for every path) at
+        ``version`` to every path, packed like :meth:`gets`."""
+        return cls._uniform('SET_DATA', paths, device, version,
+                            bytes(data or b''))
+
+    @classmethod
+    def _uniform(cls, opcode, paths, device, arg, data=None):
+        """One opcode over many paths (the arg and data shared): packed on
+        the device with array ops, or as dicts on the host path."""
         dev = _gpu_device(device)
         if dev is None:
-            return cls([{'opcode': 'GET_DATA', 'path': p, 'watch': watch}
-                        for p in paths], False)
+            if opcode == 'GET_DATA':
+                return cls([{'opcode': opcode, 'path': p,
+                             'watch': bool(arg)} for p in paths], False)
+            return cls([{'opcode': opcode, 'path': p, 'data': data,
+                         'version': arg} for p in paths], False)
         import numpy as np
         import torch
         from ..ops import batch as B
@@ -175,12 +191,19 @@ class BulkBatch(object):
             ln = torch.from_numpy(lens).to(dev)
         z32 = torch.zeros(n, dtype=torch.int32, device=dev)
         z64 = torch.zeros(n, dtype=torch.int64, device=dev)
-        op = torch.full((n,), consts.OP_CODES['GET_DATA'], dtype=torch.int32,
+        op = torch.full((n,), consts.OP_CODES[opcode], dtype=torch.int32,
                         device=dev)
-        arg = torch.ones(n, dtype=torch.int32, device=dev) if watch else z32
-        rb = B.RequestBatch(n, op, z32, arg, off, ln, z64, z32, z32, arena,
-                            arena, torch.zeros(1, dtype=torch.int64,
-                                               device=dev),
+        a = torch.full((n,), arg, dtype=torch.int32, device=dev) \
+            if arg else z32
+        if data:
+            darena = torch.frombuffer(bytearray(data), dtype=torch.uint8) \
+                .to(dev)
+            dlen = torch.full((n,), len(data), dtype=torch.int32, device=dev)
+        else:
+            darena, dlen = arena, z32
+        rb = B.RequestBatch(n, op, z32, a, off, ln, z64, dlen, z32, arena,
+                            darena, torch.zeros(1, dtype=torch.int64,
+                                                device=dev),
                             torch.zeros(1, dtype=torch.int32, device=dev),
                             torch.zeros(16, dtype=torch.uint8, device=dev))
         return cls(None, dev, reqs=rb)

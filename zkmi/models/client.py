@@ -550,7 +550,9 @@ class Client(FSM):
             batch = BulkBatch.gets(list(paths), self.bulk_device, watch=watch)
         else:
             raise TypeError('paths ([string]) is required')
+        self._submit_bulk(batch, cb)
 
+    def _submit_bulk(self, batch, cb):
         def go():
             conn = self.currentConnection()
             if conn is None or not conn.isInState('connected'):
@@ -561,6 +563,29 @@ class Client(FSM):
             except Exception as e:
                 self.loop.call_soon(cb, e)
         self._dispatch(go)
+
+    def bulk_set(self, paths, data, cb, version=-1):
+        """:meth:`bulk` of SET_DATA of one ``data`` value at ``version`` to
+        every path (strings, or a device ``(arena, off, len)`` triple),
+        packed like :meth:`bulk_get` without per-request Python objects."""
+        from .bulk import BulkBatch
+        _check_func(cb)
+        if not isinstance(data, (bytes, bytearray)):
+            raise TypeError('data (bytes) is required')
+        if isinstance(paths, tuple) and len(paths) == 3 and \
+                hasattr(paths[0], 'device'):
+            from .bulk import _gpu_device
+            if _gpu_device(self.bulk_device) is None:
+                raise ValueError('bulk_set: a device (arena, off, len) '
+                                 'triple needs a GPU bulk device')
+        elif isinstance(paths, (list, tuple)):
+            for p in paths:
+                _check_str(p, 'path')
+            paths = list(paths)
+        else:
+            raise TypeError('paths ([string]) is required')
+        batch = BulkBatch.sets(paths, data, self.bulk_device, version)
+        self._submit_bulk(batch, cb)
 
     def watcher(self, path):
         _check_str(path, 'path')
@@ -582,7 +607,7 @@ class Client(FSM):
 
         def go():
             self.note_capture = True
-            self.getSession().bulk_watches.update(paths)
+            self.getSession().add_bulk_watches(paths)
             conn = self.currentConnection()
             if conn is not None:
                 conn.start_note_capture()

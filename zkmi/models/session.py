@@ -18,6 +18,7 @@ import re
 import threading
 import time
 
+from .. import jute
 from ..runtime.emitter import EventEmitter
 from ..runtime.fsm import FSM
 from ..utils.metrics import METRIC_ZK_NOTIFICATION_COUNTER
@@ -88,6 +89,8 @@ class ZKSession(FSM):
         # paths with bulk data watches (Client.watch_bulk): re-armed on a
         # move like the watchers' (their notifications go to the fan-out)
         self.bulk_watches = set()
+        self._bulk_packed = None    # bulk_watches as an encoded vector
+                                    # (in the order they were added)
         self.rearmed = 0            # watches re-armed by SET_WATCHES resumes
         self.session_id = 0
         self.passwd = b'\0' * 8
@@ -360,9 +363,9 @@ class ZKSession(FSM):
                     raise AssertionError('unknown event: ' + e)
                 count += 1
                 all_evts.append(ev)
-        for path in sorted(self.bulk_watches):
-            events['dataChanged'].append(path)
-            count += 1
+        if self.bulk_watches:
+            events['dataChanged'] = events['dataChanged'] + self._bulk_packed
+            count += self._bulk_packed.n
         if count < 1:
             return
         zxid = self.last_zxid
@@ -380,6 +383,16 @@ class ZKSession(FSM):
             for ev in all_evts:
                 ev.resume()
         self.conn.setWatches(events, zxid, done)
+
+    def add_bulk_watches(self, paths):
+        """Paths watched in bulk (:meth:`~zkmi.models.client.Client.
+        watch_bulk`): every resume re-arms them with the session's other
+        watches."""
+        new = [p for p in dict.fromkeys(paths) if p not in self.bulk_watches]
+        if not new:
+            return
+        self.bulk_watches.update(new)
+        self._bulk_packed = (self._bulk_packed or jute.PackedStrings()) + new
 
     def watcher(self, path):
         w = self.watchers.get(path)

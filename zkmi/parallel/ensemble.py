@@ -30,6 +30,7 @@ batches.  Without a GPU (the gloo rehearsal on CPU) the same flow runs on
 the host codec.
 """
 
+import collections
 import threading
 import time
 
@@ -201,16 +202,19 @@ class EnsembleWorkload(object):
         self.seen = torch.zeros(n_paths * self.vmax, dtype=torch.int32,
                                 device=dev)
         self.bad_frames = torch.zeros(1, dtype=torch.int64, device=dev)
-        self.replayed = set()
+        self.replayed = 0                 # writes made during outages
         self.step_ms = []
+        self.phase_ms = collections.Counter()     # where a step's time goes
         self.step_no = 0
         self.failovers = 0
         self.down = None
         if self.rank == 0:
             self._create_tree()
         self._barrier()
-        self.mine = [p for p in self.paths
-                     if owner_of(p, self.world) == self.rank]
+        self.owner = np.array([owner_of(p, self.world) for p in self.paths],
+                              np.int32)
+        self.mine = [p for p, o in zip(self.paths, self.owner)
+                     if o == self.rank]
         self.client.watch_bulk(self.mine)
         self.expected[np.arange(n_paths) * self.vmax] = 1
         # the initial values go out like every later event: a notification
@@ -269,7 +273,15 @@ class EnsembleWorkload(object):
         ft = B.frame_scan(nd, len(notes), cap=k, window=B.frame_window(512))
         rep = B.decode_replies(nd, ft, self.fan.xt)
         triple = (nd, rep.pay_off[:k], rep.pay_len[:k])
+        t0 = time.perf_counter()
         res = self._bulk(self.client.bulk_get, triple, watch=True)
+        ph = self.phase_ms
+        ph['rearm_bulk_get'] += (time.perf_counter() - t0) * 1e3
+        t = getattr(res, 'phases', None) or {}
+        if t.get('submit') and 'finished' in t:
+            ph['rb_encode'] += (t['encoded'] - t['submit']) * 1e3
+            ph['rb_wire'] += (t['captured'] - t['encoded']) * 1e3
+            ph['rb_finish'] += (t['finished'] - t['captured']) * 1e3
         return torch.cat([nd, self.fan.forward_replies(res)]), 2 * k
 
     def _initial(self, notes, paths):
@@ -328,7 +340,9 @@ class EnsembleWorkload(object):
         # together, and a rank's timeout makes every rank raise
         flag = torch.zeros(2, dtype=torch.int64, device=self.coll)
         have = 0
+        ph = self.phase_ms
         while True:
+            t0 = time.perf_counter()
             if initial is not None:
                 stream, nf = self._initial(*initial)
                 initial = None
@@ -342,8 +356,18 @@ class EnsembleWorkload(object):
                         notes += more
                         k += k2
                 have += k
+                t1 = time.perf_counter()
+                ph['notes_wait'] += (t1 - t0) * 1e3
+                t0 = t1
                 stream, nf = self._rearm(notes, k)
-            got += self._count(self.fan.gather(stream, nf))
+            t1 = time.perf_counter()
+            ph['rearm'] += (t1 - t0) * 1e3
+            g = self.fan.gather(stream, nf)
+            t2 = time.perf_counter()
+            ph['gather'] += (t2 - t1) * 1e3
+            got += self._count(g)
+            ph['count'] += (time.perf_counter() - t2) * 1e3
+            ph['ticks'] += 1
             flag[0] = 0 if got >= want else 1
             flag[1] = 1 if time.monotonic() > t_end else 0
             if self.world > 1:
@@ -358,8 +382,7 @@ class EnsembleWorkload(object):
 
     def _choose(self, s):
         rng = np.random.default_rng(self.seed * 1000003 + s)
-        return [int(k) for k in rng.choice(len(self.paths), self.writes,
-                                           replace=False)]
+        return rng.choice(len(self.paths), self.writes, replace=False)
 
     def _member(self):
         def go():
@@ -383,11 +406,11 @@ class EnsembleWorkload(object):
         self.step_no += 1
         data = b's%d' % s
         chosen = self._choose(s)
-        for k in chosen:
-            self.version[k] += 1
-            v = min(int(self.version[k]), self.vmax - 1)
-            self.expected[k * self.vmax + v] += 1
+        self.version[chosen] += 1
+        v = np.minimum(self.version[chosen], self.vmax - 1)
+        np.add.at(self.expected, chosen * self.vmax + v, 1)
         cp = [self.paths[k] for k in chosen]
+        t0 = time.perf_counter()
         fail = self.failover_every and (s % self.failover_every ==
                                         self.failover_every - 1)
         if fail:
@@ -397,32 +420,37 @@ class EnsembleWorkload(object):
             m = None
             if self.rank == 0:
                 m = mine_m
+                t1 = time.perf_counter()
                 if self.down is not None:
                     self.ctl.start(self.down)       # the last victim is back
                 self.ctl.outage(m, [(p, data) for p in cp])
                 self.down = m
+                self.phase_ms['fo_outage'] += (time.perf_counter() - t1) * 1e3
             m = _bcast_ints([m] if m is not None else None, 1, 0,
                             self.coll)[0]
-            self.replayed.update((p, data) for p in cp)
+            self.replayed += len(cp)
             self.failovers += 1
             # every session on the killed member reconnects and replays
             if mine_m == m:
+                t1 = time.perf_counter()
                 t_end = time.monotonic() + 30
                 while self.connects <= before:
                     if time.monotonic() > t_end:
                         raise RuntimeError('rank %d: no failover' % self.rank)
-                    time.sleep(0.002)
+                    time.sleep(0.0002)
+                self.phase_ms['fo_reconnect'] += \
+                    (time.perf_counter() - t1) * 1e3
         else:
             mine = cp[self.rank::self.world]
             if mine:
-                res = self._bulk(self.client.bulk, [
-                    {'opcode': 'SET_DATA', 'path': p, 'data': data,
-                     'version': -1} for p in mine])
+                res = self._bulk(self.client.bulk_set, mine, data)
                 bad = [e for e in res.errors() if e != 'OK']
                 if bad:
                     raise RuntimeError('set failed: %r' % bad[:3])
+        self.phase_ms['failover' if fail else 'write'] += \
+            (time.perf_counter() - t0) * 1e3
         self._barrier()
-        mine = sum(1 for p in cp if owner_of(p, self.world) == self.rank)
+        mine = int((self.owner[chosen] == self.rank).sum())
         return self._deliver_until(len(cp), mine=mine)
 
     def rearmed(self):

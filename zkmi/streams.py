@@ -21,6 +21,7 @@ oracle otherwise.  Batched GPU framing/decoding lives in :mod:`zkmi.ops`.
 
 from . import consts
 from . import codec
+from . import jute
 from .errors import ZKProtocolError
 
 
@@ -102,7 +103,11 @@ class ZKEncoder(object):
         xid = pkt['xid']
         if not isinstance(xid, int):
             raise TypeError('xid must be an int')
-        if self.gpu is not None and pkt['opcode'] == 'SET_WATCHES':
+        if pkt['opcode'] == 'SET_WATCHES' and \
+                jute.packed_events(pkt['events']):
+            # the bulk watches' vector is already encoded: a byte copy
+            out = jute.frame(jute.encode_request(pkt))
+        elif self.gpu is not None and pkt['opcode'] == 'SET_WATCHES':
             out = self.gpu.set_watches(pkt)
         else:
             out = codec.frame(codec.encode_request(pkt))

@@ -132,6 +132,32 @@ def _scn_watch_fanout(rank, world, c, g, dist, wait_for, owner_of, zport):
     assert seen == [b'a', b'b'], seen
 
 
+def _scn_watch_kinds(rank, world, c, g, dist, wait_for, owner_of, zport):
+    """Every event kind crosses the fan-out as wire frames (NOTIFICATION +
+    the forwarded GET_CHILDREN2 / EXISTS reply) and arrives with its
+    values on every rank."""
+    path = '/wk'
+    if rank == 0:
+        c.call_sync('create', path, b'p', {})
+    dist.barrier()
+    kids, gone = [], []
+    g.watcher(path).on('childrenChanged', lambda ch, st: kids.append(
+        (sorted(ch), st.numChildren))).on('deleted', lambda: gone.append(1))
+    _tick_until(g, dist, lambda: len(kids) >= 1)
+    assert kids == [([], 0)], kids
+    dist.barrier()
+    if rank == 0:
+        c.call_sync('create', path + '/c1', b'', {})
+    _tick_until(g, dist, lambda: len(kids) >= 2)
+    assert kids[-1] == (['c1'], 1), kids
+    dist.barrier()
+    if rank == 0:
+        c.call_sync('delete', path + '/c1', -1)
+        c.call_sync('delete', path, -1)
+    _tick_until(g, dist, lambda: len(gone) >= 1)
+    assert g.fan.stats['decoded_host'] >= 2 * len(kids)
+
+
 def _tick_until(g, dist, cond, rounds=200):
     """tick() is a collective: every rank must call it the same number of
     times, so the stop decision is all-reduced."""
@@ -195,6 +221,10 @@ def test_group_collectives(scenario):
 
 def test_session_failover_between_ranks():
     _run('session_failover')
+
+
+def test_watch_kinds_cross_the_frame_fanout():
+    _run('watch_kinds')
 
 
 def test_watch_fanout_uses_one_server_watch():

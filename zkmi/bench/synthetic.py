@@ -1307,8 +1307,10 @@ class WatchPipeline(object):
               write order; the writes' replies are checked too
       R1      the notification streams of all ranks travel in equal-size
               slots ({bytes, frames} header + frames) through one
-              ``all_gather_into_tensor`` (RCCL over xGMI with ``nccl``);
-              every rank concatenates them (``seg_unpack``), K1 + K8
+              ``all_gather_into_tensor`` (RCCL over xGMI with ``nccl``;
+              :meth:`~zkmi.parallel.fanout.FrameFanout.gather_slots`, the
+              one R1 path's sync-free transport); every rank concatenates
+              them (``seg_unpack``), K1 + K8
               decodes ALL ranks' notifications and checks each on the
               device: NodeDataChanged, SyncConnected, and the path of the
               node that rank's writer set at that position
@@ -1373,13 +1375,10 @@ class WatchPipeline(object):
         rec = 4 + 16 + 4 + 4 + 4 + maxpath
         self.rec_max = rec
         self.slot = (16 + n * rec + 15) & ~15
-        self.send = torch.empty(self.slot, dtype=U8, device=dev)
-        self.big = torch.empty(W * self.slot, dtype=U8, device=dev)
-        self.rx = torch.empty(W * (self.slot - 16) + 64, dtype=U8,
-                              device=dev)
-        self.nrx = torch.zeros(1, dtype=I64, device=dev)
-        self.src_counts = torch.zeros(W, dtype=I64, device=dev)
-        self.pstats = torch.zeros(3, dtype=I64, device=dev)
+        from ..parallel.fanout import FrameFanout
+        self.fan = FrameFanout(group, device=dev,
+                               coll_device=self.coll_device)
+        self.pstats = None
         self.nscan = B.FrameScanner(W * n, dev, window=B.frame_window(rec))
         self.nreply = B.alloc_replies(W * n, dev)
         self.nxt = B.XidTable(bits=10, device=dev)
@@ -1451,26 +1450,12 @@ class WatchPipeline(object):
                                           self._xids(), True),
                               self.sid_wr, 1)
         wrote = ((rep.status[:n] == 0) & (rep.err[:n] == 0)).sum()
-        # R1: every rank's notification stream to every rank
+        # R1: every rank's notification stream to every rank (FrameFanout's
+        # fixed-slot transport: no host read in the step)
         nbuf, ntotal, _, ncount = self.server.notif
-        L.seg_pack(nbuf, self.server.notif_rec_off, ncount,
-                   self.server.ecap, ntotal, ncount, 1, 0, self.slot,
-                   self.send, self.pstats)
-        if W > 1:
-            if self.coll_device == self.dev:
-                self.dist.all_gather_into_tensor(self.big, self.send,
-                                                 group=self.group)
-            else:
-                o = torch.empty(self.big.shape, dtype=U8,
-                                device=self.coll_device)
-                self.dist.all_gather_into_tensor(
-                    o, self.send.to(self.coll_device), group=self.group)
-                self.big.copy_(o)
-            big = self.big
-        else:
-            big = self.send
-        L.seg_unpack(big, W, self.rank, self.slot, self.rx, self.nrx,
-                     self.src_counts, None)
+        self.rx, self.nrx, self.src_counts, self.pstats = \
+            self.fan.gather_slots(nbuf, self.server.notif_rec_off, ncount,
+                                  self.server.ecap, ntotal, self.slot)
         ft = self.nscan.scan(self.rx, self.nrx)
         nrep = B.decode_replies(self.rx, ft, self.nxt, out=self.nreply)
         self.step_no += 1

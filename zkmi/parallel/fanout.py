@@ -38,7 +38,10 @@ from .. import consts
 from .. import jute
 
 XID_FWD = 0x7ffffff0          # the forwarded replies' xid (-> GET_DATA)
-_GET_DATA = consts.OP_CODES['GET_DATA']
+XID_FWD_KIDS = 0x7ffffff1     # (-> GET_CHILDREN2)
+XID_FWD_STAT = 0x7ffffff2     # (-> EXISTS)
+FWD_XIDS = {XID_FWD: 'GET_DATA', XID_FWD_KIDS: 'GET_CHILDREN2',
+            XID_FWD_STAT: 'EXISTS'}
 
 
 def owner_of(path, world):
@@ -61,7 +64,7 @@ class Gathered(object):
 class FrameFanout(object):
     """Collective: every rank calls :meth:`gather` together."""
 
-    def __init__(self, group=None, device=None):
+    def __init__(self, group=None, device=None, coll_device=None):
         on = dist.is_available() and dist.is_initialized()
         self.group = group
         self.world = dist.get_world_size(group) if on else 1
@@ -76,13 +79,18 @@ class FrameFanout(object):
         # RCCL, host memory for gloo
         self.coll = self.dev if backend in (None, 'nccl') and self.dev \
             else torch.device('cpu')
+        if coll_device is not None:
+            self.coll = torch.device(coll_device)
         self.stats = collections.Counter()
         self.xt = None
+        self._slots = {}
         if self.dev is not None:
             from ..ops import batch as B
             self.B = B
             self.xt = B.XidTable(bits=12, device=self.dev)
-            self.xt.tab[XID_FWD & self.xt.mask] = (XID_FWD << 32) | _GET_DATA
+            for x, op in FWD_XIDS.items():
+                self.xt.tab[x & self.xt.mask] = \
+                    (x << 32) | consts.OP_CODES[op]
             self._x4 = torch.tensor(list(XID_FWD.to_bytes(4, 'big')),
                                     dtype=torch.uint8, device=self.dev)
 
@@ -121,6 +129,49 @@ class FrameFanout(object):
         self.stats['bytes'] += sum(sizes)
         return Gathered(body, sizes, frames)
 
+    def gather_slots(self, buf, rec_off, count, cap, total, slot):
+        """The fixed-slot transport: no host read, so a step can be
+        graph-captured.  This rank's framed stream (``buf``, ``total`` bytes,
+        ``count`` records starting at ``rec_off``, at most ``cap``; all
+        device tensors) is cut into one ``slot``-byte segment ({bytes,
+        records} header + frames, ``seg_pack``), every rank's segment is
+        all-gathered, and the payloads are concatenated on the device in
+        rank order (``seg_unpack``).  Returns ``(rx, nrx, src_counts,
+        overflow)``: the stream, its device length, the records per source
+        rank and the pack stats (``overflow[0]``: a stream that did not fit
+        its slot went empty).  Buffers are kept per slot size."""
+        from ..ops import _lib
+        L = _lib.lib()
+        W = self.world
+        dev = buf.device
+        st = self._slots.get(slot)
+        if st is None:
+            u8 = torch.uint8
+            st = self._slots[slot] = {
+                'send': torch.empty(slot, dtype=u8, device=dev),
+                'big': torch.empty(W * slot, dtype=u8, device=dev),
+                'rx': torch.empty(W * (slot - 16) + 64, dtype=u8, device=dev),
+                'nrx': torch.zeros(1, dtype=torch.int64, device=dev),
+                'src': torch.zeros(W, dtype=torch.int64, device=dev),
+                'pstats': torch.zeros(3, dtype=torch.int64, device=dev)}
+        L.seg_pack(buf, rec_off, count, cap, total, count, 1, 0, slot,
+                   st['send'], st['pstats'])
+        big = st['send']
+        if W > 1:
+            big = st['big']
+            if self.coll == dev:
+                dist.all_gather_into_tensor(big, st['send'], group=self.group)
+            else:
+                o = torch.empty(big.shape, dtype=torch.uint8,
+                                device=self.coll)
+                dist.all_gather_into_tensor(o, st['send'].to(self.coll),
+                                            group=self.group)
+                big.copy_(o)
+        L.seg_unpack(big, W, self.rank, slot, st['rx'], st['nrx'], st['src'],
+                     None)
+        self.stats['slot_exchanges'] += 1
+        return st['rx'], st['nrx'], st['src'], st['pstats']
+
     # -- helpers for the owner side -------------------------------------------
 
     def forward_replies(self, res):
@@ -145,7 +196,7 @@ class FrameFanout(object):
                                                consts.MAX_PACKET)
             if bad >= 0:
                 raise RuntimeError('fan-out stream: bad frame')
-            xmap = {XID_FWD: 'GET_DATA'}
+            xmap = dict(FWD_XIDS)
             self.stats['decoded_host'] += len(frames)
             return [codec.decode_response(raw[o:o + ln], xmap)
                     for o, ln in frames]
@@ -156,6 +207,17 @@ class FrameFanout(object):
         rep = B.decode_replies(g.buf, ft, self.xt)
         self.stats['decoded_gpu'] += nf
         return ft, rep
+
+    def decode_packets(self, g):
+        """The gathered stream as packet dicts (:func:`zkmi.jute.
+        decode_response`'s), for listeners that take Python values: decoded
+        on the GPU (K1 + K2-K8) when there is one, else by the host codec."""
+        if self.dev is None:
+            return self.decode(g)
+        if g.total == 0:
+            return []
+        ft, rep = self.decode(g)
+        return self.B.replies_to_packets(g.buf, rep, n=sum(g.frames))
 
     @staticmethod
     def pair_index(frames, device):

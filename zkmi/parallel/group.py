@@ -11,7 +11,11 @@ group adds:
      owner, ``crc32(path) % world``) holds the real server watch; every
      other rank receives the owner's events (with the re-fetched data and
      Stat, so nobody re-reads).  8 sessions watching one hot path cost the
-     ensemble 1 watch instead of 8.
+     ensemble 1 watch instead of 8.  The events travel as ZooKeeper wire
+     frames — a NOTIFICATION and the reply of the owner's re-fetch — through
+     :class:`~zkmi.parallel.fanout.FrameFanout`, the one R1 path (the bulk
+     watches of config 4 and the GPU server's watch pipeline use it too),
+     and every rank decodes the gathered stream (K1 + K2-K8 on its GPU).
   R2 :meth:`SessionGroup.batched_get` — request batching: ranks pool their
      reads, duplicates are dropped, each unique path is fetched once by one
      rank over its own session, results are exchanged.
@@ -29,12 +33,12 @@ per-event collectives.  Payloads are Jute-encoded records.
 
 import collections
 import threading
-import zlib
 
 import torch
 import torch.distributed as dist
 
 from .. import jute
+from .fanout import FWD_XIDS, FrameFanout, owner_of
 from ..utils.metrics import METRIC_ZK_EVENT_COUNTER, \
     METRIC_ZK_NOTIFICATION_COUNTER
 
@@ -45,11 +49,12 @@ METRIC_SCHEMA = (
      for e in ('created', 'deleted', 'dataChanged', 'childrenChanged')])
 
 _KINDS = ('created', 'deleted', 'dataChanged', 'childrenChanged')
-
-
-def owner_of(path, world):
-    """Deterministic owner rank of a path (same on every rank)."""
-    return zlib.crc32(path.encode('utf-8')) % world
+# event kind <-> (notification type, the forwarded reply's opcode)
+_NOTE_TYPE = {'created': 'CREATED', 'deleted': 'DELETED',
+              'dataChanged': 'DATA_CHANGED',
+              'childrenChanged': 'CHILDREN_CHANGED'}
+_KIND_OF = {v: k for k, v in _NOTE_TYPE.items()}
+_FWD_OF = {op: x for x, op in FWD_XIDS.items()}
 
 
 class SessionGroup(object):
@@ -71,6 +76,11 @@ class SessionGroup(object):
         self._lock = threading.Lock()
         self._watchers = {}
         self.stats = collections.Counter()
+        # R1: frames decoded on this rank's GPU when the collectives run
+        # there, by the host codec otherwise
+        self.fan = FrameFanout(group, device=self.device
+                               if self.device.type == 'cuda' else None,
+                               coll_device=self.device)
 
     # -- low level: variable-size all-gather of byte strings --------------
 
@@ -245,19 +255,28 @@ class SessionGroup(object):
         return w
 
     def _publish(self, kind, path, args):
-        w = jute.JuteWriter()
-        w.write_int(_KINDS.index(kind))
-        w.write_ustring(path)
+        """An owner's watcher event as two wire frames: the NOTIFICATION
+        and the reply the watcher's re-fetch got (GET_DATA for dataChanged,
+        GET_CHILDREN2 for childrenChanged, EXISTS for created; an EXISTS
+        NO_NODE for deleted), its xid the forwarding xid of that opcode."""
+        note = jute.encode_response({
+            'xid': -1, 'zxid': -1, 'err': 'OK', 'opcode': 'NOTIFICATION',
+            'type': _NOTE_TYPE[kind], 'state': 'SYNC_CONNECTED',
+            'path': path})
         if kind == 'dataChanged':
-            w.write_buffer(args[0])
-            w.write_stat(args[1])
+            rep = {'opcode': 'GET_DATA', 'data': args[0], 'stat': args[1]}
         elif kind == 'childrenChanged':
-            w.write_string_vector(args[0])
-            w.write_stat(args[1])
+            rep = {'opcode': 'GET_CHILDREN2', 'children': args[0],
+                   'stat': args[1]}
         elif kind == 'created':
-            w.write_stat(args[0])
+            rep = {'opcode': 'EXISTS', 'stat': args[0]}
+        else:
+            rep = {'opcode': 'EXISTS', 'err': 'NO_NODE'}
+        rep['xid'] = _FWD_OF[rep['opcode']]
+        rep['zxid'] = -1
         with self._lock:
-            self._pending.append(w.getvalue())
+            self._pending.append(jute.frame(note) +
+                                 jute.frame(jute.encode_response(rep)))
 
     def tick(self):
         """Collective: exchange every rank's pending watch events and deliver
@@ -266,29 +285,24 @@ class SessionGroup(object):
         with self._lock:
             batch = list(self._pending)
             self._pending.clear()
-        w = jute.JuteWriter()
-        w.write_int(len(batch))
-        for rec in batch:
-            w.write_buffer(rec)
+        g = self.fan.gather(b''.join(batch), 2 * len(batch))
+        pk = self.fan.decode_packets(g)
         n = 0
-        for blob in self._allgather_bytes(w.getvalue()):
-            r = jute.JuteReader(blob)
-            for _ in range(r.read_int()):
-                rr = jute.JuteReader(r.read_buffer())
-                kind = _KINDS[rr.read_int()]
-                path = rr.read_ustring()
-                if kind == 'dataChanged':
-                    args = (rr.read_buffer(), rr.read_stat())
-                elif kind == 'childrenChanged':
-                    args = (rr.read_string_vector(), rr.read_stat())
-                elif kind == 'created':
-                    args = (rr.read_stat(),)
-                else:
-                    args = ()
-                dw = self._watchers.get(path)
-                if dw is not None:
-                    dw._deliver(kind, args)
-                    n += 1
+        for i in range(0, len(pk), 2):
+            note, rep = pk[i], pk[i + 1]
+            kind = _KIND_OF[note['type']]
+            if kind == 'dataChanged':
+                args = (rep['data'], rep['stat'])
+            elif kind == 'childrenChanged':
+                args = (rep['children'], rep['stat'])
+            elif kind == 'created':
+                args = (rep['stat'],)
+            else:
+                args = ()
+            dw = self._watchers.get(note['path'])
+            if dw is not None:
+                dw._deliver(kind, args)
+                n += 1
         self.stats['events_delivered'] += n
         return n
 

@@ -463,6 +463,75 @@ def test_encode_responses_matches_oracle(gpu):
     assert got == b''.join(want)
 
 
+@pytest.mark.parametrize('dist,mix', [(None, False), ((0, 300), False),
+                                      ((0, 300), True)])
+def test_encode_responses_serve_mix_matches_oracle(gpu, dist, mix):
+    """K13 on the serve path's usual replies (GET_DATA / Stat / header-only,
+    errors among them) against jute.encode_response: fixed and variable
+    data lengths, a terminated stream (four 0xFF bytes right after it,
+    nothing written past the last 16-byte chunk), and with ``mix`` a CREATE
+    in every third block.  Round 3 measured a gather variant of the writer
+    (each aligned 16-byte chunk built from its record's slot) 2.4x slower
+    than the LDS-staged one (README, Measured and rejected)."""
+    from zkmi.bench.synthetic import GpuTree
+    from zkmi.ops import batch as B
+    tree = GpuTree(5000, 100, fanout=100, device=gpu, spare=0.25,
+                   data_dist=dist)
+    r = synth.rng(22)
+    n = 256 * 9 + 77
+    ops, errs, nodes, zx, paths = [], [], [], [], []
+    for i in range(n):
+        op = r.choice(['GET_DATA', 'GET_DATA', 'GET_DATA', 'EXISTS',
+                       'SET_DATA', 'DELETE'])
+        if mix and (i // 256) % 3 == 1 and i % 256 == 100:
+            op = 'CREATE'
+        ops.append(op)
+        errs.append(0 if r.random() < 0.85 else -101)
+        nodes.append(r.randrange(tree.leaf0, tree.n_static))
+        zx.append(r.randint(0, 2**40))
+        paths.append(synth.rand_path(r))
+    parena = b''.join(p.encode() for p in paths)
+    poff = np.cumsum([0] + [len(p.encode()) for p in paths[:-1]])
+    T = lambda a, dt: torch.tensor(a, dtype=dt, device=gpu)  # noqa: E731
+    resp = B.ResponseBatch(
+        T([consts.OP_CODES[o] for o in ops], torch.int32),
+        T(list(range(n)), torch.int32), T(errs, torch.int32),
+        T(nodes, torch.int64), T(zx, torch.int64),
+        T(poff.tolist(), torch.int64),
+        T([len(p.encode()) for p in paths], torch.int32),
+        _dev_bytes(parena, gpu), T([1] * n, torch.int32), T([n], torch.int64))
+    slots = {}
+    want = []
+    for i in range(n):
+        nd = nodes[i]
+        if nd not in slots:
+            slots[nd] = tree.node_slot_host(nd)
+        data, st = slots[nd]
+        rep = {'xid': i, 'zxid': zx[i], 'err': errs[i], 'opcode': ops[i],
+               'stat': st, 'path': paths[i], 'data': data}
+        want.append(jute.frame(jute.encode_response(rep)))
+    want = b''.join(want)
+    cap = 1 << 22
+    out = torch.full((cap,), 0xAB, dtype=torch.uint8, device=gpu)
+    out, rec_off, total, err = B.encode_responses(resp, tree.store, cap,
+                                                  out=out, terminate=True)
+    torch.cuda.synchronize()
+    assert err.item() == 0
+    t = int(total.item())
+    assert t == len(want)
+    hb = bytes(out[:t + 64].cpu().numpy().tobytes())
+    assert hb[:t] == want
+    assert hb[t:t + 4] == b'\xff' * 4
+    end = (t + 4 + 15) & ~15
+    assert hb[end:] == b'\xab' * (t + 64 - end)
+    # record offsets: where each frame starts
+    starts, o = [], 0
+    while o < t:
+        starts.append(o)
+        o += 4 + int.from_bytes(want[o:o + 4], 'big')
+    assert rec_off[:n].cpu().tolist() == starts
+
+
 def test_gpu_get_pipeline_end_to_end(gpu):
     from zkmi.bench.synthetic import GetPipeline
     tree = _small_tree(gpu, 20000, 37)

@@ -45,7 +45,8 @@ def main():
     # K1DBG_DIST=lo-hi: variable payloads (uniform lo..hi bytes)
     dist = os.environ.get('K1DBG_DIST')
     dd = tuple(int(x) for x in dist.split('-')) if dist else None
-    tree = S.GpuTree(1_000_000, 100, device=dev, data_dist=dd)
+    data = int(os.environ.get('K1DBG_DATA', '100'))
+    tree = S.GpuTree(1_000_000, data, device=dev, data_dist=dd)
     pipe = S.GetPipeline(tree, 1 << 19)
     for _ in range(2):
         pipe.step()

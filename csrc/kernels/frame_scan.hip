@@ -297,7 +297,98 @@ ZK_DEV int64_t ft_cand(const uint8_t* sb, const uint32_t* sbits, int32_t e,
   }
 }
 
+// Frontier passes past the window (fs_tile<W, true>, streams whose frames
+// may be longer than the window): when a frame longer than the window
+// covers [0, W) of a tile, every walker starts inside its body and dies
+// (body bytes read as lengths are implausible), so no survivor is left.
+// The frontier then runs again from [base, base + W) for base = W, 2W, ...
+// until a walker survives: the chain resumes after that frame.  Positions
+// the dead walkers claimed keep their meaning (a chain through one dies
+// too).  Kept out of the usual path (its own function, only instantiated
+// for LONG): a loop around the main frontier cost the GET step 9 %.
 template <int W>
+ZK_DEV void ft_frontier_passes(const uint8_t* sb, uint32_t* claimed,
+                               uint32_t* xbits, uint16_t* scratch,
+                               int32_t nrel, int32_t maxp32, int32_t minb,
+                               int lane, uint32_t& lastx, int& round,
+                               int32_t& mp, bool& ma) {
+  constexpr int K = W / 64;
+  for (int32_t base = W; base < FT_S && base < nrel && __ballot(ma) == 0;
+       base += W) {
+    for (int k = lane; k < W / 32; k += 64)
+      claimed[base / 32 + k] = 0xFFFFFFFFu;
+    __builtin_amdgcn_wave_barrier();
+    int32_t p[K];
+    uint32_t act = 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      p[k] = base + lane + 64 * k;
+      act |= 1u << k;
+    }
+    int32_t live = W;
+    while (live > 64) {
+      int32_t q[K];
+      int code[K];
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        q[k] = 0;
+        code[k] = (act >> k) & 1 ? ft_hop(sb, p[k], nrel, maxp32, minb, q[k])
+                                 : 1;
+      }
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        if (!((act >> k) & 1)) continue;
+        if (code[k] == 0 && ft_claim(claimed, q[k])) {
+          p[k] = q[k];
+        } else {
+          if (code[k] == 2 && ft_mark_exit(xbits, q[k] - FT_S, W))
+            lastx = max(lastx, ((uint32_t)round << 16) |
+                                   (uint32_t)(q[k] - FT_S));
+          act &= ~(1u << k);
+        }
+      }
+      ++round;
+      int c = __popc(act);
+#pragma unroll
+      for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d, 64);
+      live = c;
+    }
+    {
+      const uint32_t mine = __popc(act);
+      uint32_t incl = mine;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += y;
+      }
+      uint32_t o = incl - mine;
+#pragma unroll
+      for (int k = 0; k < K; ++k)
+        if ((act >> k) & 1) scratch[o++] = (uint16_t)p[k];
+      __builtin_amdgcn_wave_barrier();
+      ma = lane < live;
+      mp = ma ? (int32_t)scratch[lane] : 0;
+      __builtin_amdgcn_wave_barrier();
+    }
+    while (live > 1) {
+      int32_t q = 0;
+      const int code = ma ? ft_hop(sb, mp, nrel, maxp32, minb, q) : 1;
+      if (ma) {
+        if (code == 0 && ft_claim(claimed, q)) {
+          mp = q;
+        } else {
+          if (code == 2 && ft_mark_exit(xbits, q - FT_S, W))
+            lastx = max(lastx, ((uint32_t)round << 16) | (uint32_t)(q - FT_S));
+          ma = false;
+        }
+      }
+      ++round;
+      live = __popcll(__ballot(ma));
+    }
+  }
+}
+
+template <int W, bool LONG>
 __global__ __launch_bounds__(256) void fs_tile(
     const uint8_t* __restrict__ buf, const int64_t* __restrict__ n_dev,
     int64_t n_cap, int64_t maxp, uint16_t* __restrict__ list,
@@ -456,6 +547,10 @@ __global__ __launch_bounds__(256) void fs_tile(
     ++round;
     live = __popcll(__ballot(ma));
   }
+  if constexpr (LONG) {
+    ft_frontier_passes<W>(sb, claimed, xbits, scratch, nrel, maxp32, minb,
+                          lane, lastx, round, mp, ma);
+  }
   const int64_t t_f = dbg ? wall_clock64() : 0;
   // ---- 2. the survivor walks to the tile end ------------------------------
   int64_t send = -1;
@@ -515,7 +610,10 @@ __global__ __launch_bounds__(256) void fs_tile(
   // preferred candidate: the survivor's exit, else the latest in-window
   // exit of the frontier (-1: none)
   int32_t px = -1;
-  if (sm && !(send & TERM) && send - tend < W) {
+  // (LONG: the survivor's exit may lie past the window — after a frame
+  // longer than the window the chain resumes there, and the next tile's
+  // frontier passes find it)
+  if (sm && !(send & TERM) && send - tend < (LONG ? FT_S - 1 : W)) {
     px = (int32_t)(send - tend);
   } else {
     uint32_t lx = lastx;
@@ -1888,7 +1986,16 @@ static int32_t fs_minb() {
   return v;
 }
 
+// scan flag: frames may be longer than the window (fs_tile's frontier
+// passes past the window, and survivor exits past it as candidates)
+constexpr int32_t FS_LONG = 2;
+
+// `window` values with this bit: FS_LONG (zkmi.ops.batch.frame_window sets
+// it when the window is below the stream's largest frame)
+constexpr int32_t FS_WIN_LONG = 1 << 16;
+
 static int fs_window(int32_t window) {
+  window &= FS_WIN_LONG - 1;
   return window <= 256 ? 256 : window <= 512 ? 512
        : window <= 1024 ? 1024 : 2048;
 }
@@ -1943,14 +2050,17 @@ int64_t zk_frame_scan_workspace(int64_t n) {
 // of it over the same n_cap (fs_rows / fs_link clear what they used), so
 // the memset is skipped.  A stale flag could only cost speed, never
 // correctness (fs_check / fs_link verify every speculated entry).
-// flags (tests of the link repair): bit 0 no speculated tile entries; bits
-// 8..23 P > 0: every P-th tile (t % P == 1) takes a garbage entry.
+// flags: bit 1 (FS_LONG) frames may be longer than the window (a window
+// below the stream's largest frame: fs_tile's frontier passes); tests of
+// the link repair: bit 0 no speculated tile entries; bits 8..23 P > 0:
+// every P-th tile (t % P == 1) takes a garbage entry.
 int zk_frame_scan5(const uint8_t* buf, const int64_t* n_dev, int64_t n_cap,
                    int64_t maxp, uint8_t* ws, int64_t ws_bytes, int64_t* foff,
                    int32_t* flen, int64_t cap, int64_t* result, int32_t window,
                    int32_t clean, int32_t flags, hipStream_t st) {
   using namespace zk;
   const int W = fs_window(window);
+  if (window & FS_WIN_LONG) flags |= FS_LONG;
   if (maxp > FC_MAXP || maxp < 0) return -3;
   FsPlan p = fs_plan(n_cap);
   if ((int64_t)p.total > ws_bytes) return -1;
@@ -1985,15 +2095,24 @@ int zk_frame_scan5(const uint8_t* buf, const int64_t* n_dev, int64_t n_cap,
     if (tpb < 1 || tpb > 4) tpb = 4;
   }
   const unsigned tblocks = (unsigned)((tiles + tpb - 1) / tpb);
-#define ZK_FS_TILE(WW)                                                       \
-  fs_tile<WW><<<tblocks, 64 * tpb, FT_LDS * tpb, st>>>(                      \
+#define ZK_FS_TILE(WW, LL)                                                   \
+  fs_tile<WW, LL><<<tblocks, 64 * tpb, FT_LDS * tpb, st>>>(                  \
       buf, n_dev, n_cap, maxp, list, pre, sx, lbw, rent, rexit, rmeta, rcnt, \
       tiles, dbg, fs_minb(), flags, cx)
-  switch (W) {
-    case 256: ZK_FS_TILE(256); break;
-    case 512: ZK_FS_TILE(512); break;
-    case 1024: ZK_FS_TILE(1024); break;
-    default: ZK_FS_TILE(2048); break;
+  if (flags & FS_LONG) {
+    switch (W) {
+      case 256: ZK_FS_TILE(256, true); break;
+      case 512: ZK_FS_TILE(512, true); break;
+      case 1024: ZK_FS_TILE(1024, true); break;
+      default: ZK_FS_TILE(2048, true); break;
+    }
+  } else {
+    switch (W) {
+      case 256: ZK_FS_TILE(256, false); break;
+      case 512: ZK_FS_TILE(512, false); break;
+      case 1024: ZK_FS_TILE(1024, false); break;
+      default: ZK_FS_TILE(2048, false); break;
+    }
   }
 #undef ZK_FS_TILE
   ZK_LAUNCH_CHECK();

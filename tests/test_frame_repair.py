@@ -184,15 +184,17 @@ def test_phantom_chain_region_is_chased_not_walked(gpu):
 
 def test_get_replies_exact_below_the_largest_frame(gpu, monkeypatch):
     """0-1024 B GET replies scanned at a 512 B window (half the largest
-    frame): most tiles lose their speculated entry and go through the grid
-    rounds and the serial tail.  Every frame table must still equal the
-    host framing — a refused repair walk once left a tile's frame starts
+    frame, long-frame mode: frontier passes past the window, survivor exits
+    past it as entries; the tiles still broken go through the grid rounds
+    and the serial tail).  Every frame table must still equal the host
+    framing — a refused repair walk once left a tile's frame starts
     overwritten under its old record (3 frames in 20M)."""
     monkeypatch.setenv('ZKMI_FS_WINDOW_MAX', '512')
     from zkmi.bench import synthetic as S
     tree = S.GpuTree(200_000, 100, device=gpu, seed=0, data_dist=(0, 1024))
     pipe = S.GetPipeline(tree, 1 << 16, seed=1)
-    assert pipe.rwindow == 512
+    from zkmi.ops import batch as B
+    assert pipe.rwindow == 512 | B.FS_WIN_LONG
     for _ in range(4):
         acc = pipe.step()
         idx, rep, rx, ft = pipe.last

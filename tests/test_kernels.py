@@ -94,8 +94,9 @@ def _frames_stream(r, n, maxbody):
 
 
 # K1 entry windows: frames longer than the window take the slow path and
-# must stay exact (the 600 / 5000 / 40000-byte cases at window 256)
-WINDOWS = [256, 1024, 2048]
+# must stay exact (the 600 / 5000 / 40000-byte cases at window 256), also
+# in long-frame mode (bit 16: zkmi.ops.batch.FS_WIN_LONG)
+WINDOWS = [256, 1024, 2048, 256 | 1 << 16, 1024 | 1 << 16]
 
 
 @pytest.mark.parametrize('window', WINDOWS)

@@ -73,7 +73,14 @@ def build_hip(jobs=4):
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         list(ex.map(lambda t: (_run(t[2]), _stamped(t[0], t[1])), todo))
     full = SH.hip_hash()
-    if todo or SH.read_stamp(HIP_SO) != full or not os.path.exists(HIP_SO):
+
+    def embedded():
+        # the hash string the library itself carries (a library copied over
+        # the built one keeps a matching stamp file but not this)
+        with open(HIP_SO, 'rb') as f:
+            return full.encode() in f.read()
+    if todo or SH.read_stamp(HIP_SO) != full or not os.path.exists(HIP_SO) \
+            or not embedded():
         # the library carries the hash of the sources it was built from
         stamp_src = os.path.join(BDIR, 'zkmi_stamp.cpp')
         with open(stamp_src, 'w') as f:

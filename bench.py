@@ -10,11 +10,11 @@ encode on the same 1M-znode tree), ``--workload storm`` configs[4]
 ``--workload watch`` the watch fan-out of configs[3] driven by real writes
 (each rank's GPU server arms GET_DATA watches and fires them on SET_DATA;
 the notifications of every rank are all-gathered over RCCL and decoded by
-every rank; the value counts node-wide deliveries).  ``--workload chain`` pipelines
-create -> set -> get -> delete of each path inside ONE batch (in-batch
-ordering of the GPU server, 4 ordered passes); ``--workload nest`` does
-createWithEmptyParents-style depth-3 creates, the parent's EXISTS and the
-bottom-up deletes in one batch (parent / child order).
+every rank; the value counts node-wide deliveries).  ``--workload chain``
+pipelines create -> set -> get -> delete of each path inside ONE batch
+(in-batch ordering of the GPU server, 4 ordered passes); ``--workload nest``
+does createWithEmptyParents-style depth-3 creates, the parent's EXISTS and
+the bottom-up deletes in one batch (parent / child order).
 One step = one batch
 of ``--batch`` GET_DATA requests per GPU pushed through the full ZooKeeper
 wire path on the GPU (see zkmi/bench/synthetic.py): client request encode

@@ -10,7 +10,6 @@ Reference: lib/zk-session.js:558-574 (trigger table, client side),
 :986-1005 (arming requests), lib/zk-buffer.js:364-370 (notification)."""
 
 import pytest
-import torch
 
 from zkmi import jute
 from zkmi.ops import batch as B

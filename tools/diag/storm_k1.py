@@ -53,7 +53,8 @@ for k in range(3):
                'step0 copy, fresh scanner')
         rescan(out, n, d.rscanner, 'step0 third, pipeline scanner')
         print('pipeline scanner window', d.rwindow, 'cap', d.rscanner.cap,
-              'ws_for', d.rscanner.ws_for, 'buf numel', out.numel(), flush=True)
+              'ws_for', d.rscanner.ws_for, 'buf numel', out.numel(),
+              flush=True)
 rb, rep = pipe.last
 # re-scan the reply stream of that first step from the server's buffer
 out, total, _, _ = d.server.result

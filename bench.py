@@ -236,6 +236,46 @@ def measure_rtt_async(port, n=2000, warm=200):
     return statistics.median(lat), lat[int(0.99 * len(lat))]
 
 
+def measure_pipelined(port, n=200000, window=256):
+    """Interactive get(path, cb) throughput: ``window`` requests in flight
+    on the client's event loop, each reply's callback issuing the next —
+    the per-request API (no bulk batch), so every reply goes through the
+    connection's completion path one at a time."""
+    import threading
+    from zkmi import Client
+    c = Client(address='127.0.0.1', port=port)
+    c.wait_connected(10)
+    _create_quiet(c, '/rtt_p')
+    done = threading.Event()
+    st = {'sent': 0, 'got': 0, 'err': None}
+
+    def on_reply(err, data=None, stat=None):
+        if err is not None:
+            st['err'] = err
+            done.set()
+            return
+        st['got'] += 1
+        if st['got'] >= n:
+            done.set()
+            return
+        if st['sent'] < n:
+            st['sent'] += 1
+            c.get('/rtt_p', on_reply)
+
+    def start():
+        for _ in range(min(window, n)):
+            st['sent'] += 1
+            c.get('/rtt_p', on_reply)
+    t0 = time.perf_counter()
+    c.loop.call_soon(start)
+    ok = done.wait(300)
+    el = time.perf_counter() - t0
+    c.close_sync(10)
+    if not ok or st['err'] is not None:
+        raise RuntimeError('pipelined run failed: %r' % (st['err'],))
+    return n / el
+
+
 def run_ensemble(a):
     """BASELINE config 4 (zkmi/parallel/ensemble.py): 3-server ensemble,
     one session per rank, member failover with watch replay, every event
@@ -635,7 +675,7 @@ def run_rank(a):
 
     rtt50 = rtt99 = py50 = py99 = bulk_ops = bulk_ms = bulk_ph = None
     bulk_k = (None, None, None)
-    ev50 = ev99 = None
+    ev50 = ev99 = pipe_ops = None
     if rtt_srv is not None:
         try:
             py50, py99 = measure_rtt(rtt_srv[1])
@@ -646,6 +686,7 @@ def run_rank(a):
         try:
             rtt50, rtt99 = measure_rtt(fast_srv.port)
             ev50, ev99 = measure_rtt_async(fast_srv.port)
+            pipe_ops = measure_pipelined(fast_srv.port)
             bulk_ops, bulk_ms, bulk_ph = measure_bulk_tcp(
                 fast_srv.port, a.nodes, a.bulk_batch, 3, dev, 1)
             bulk_k = measure_bulk_tcp(fast_srv.port, a.nodes, a.bulk_batch,
@@ -702,6 +743,12 @@ def run_rank(a):
                                'loop (each callback issues the next get), '
                                'as node-zkstream runs it: no caller-thread '
                                'hop; same native server',
+            'pipelined_get_ops_s': pipe_ops,
+            'pipelined_note': 'get(path, cb) with 256 in flight on one '
+                              'connection (each callback issues the next): '
+                              'the per-request API through the native '
+                              'completion path (reply router + coalesced '
+                              'writes in the native loop)',
             'p50_get_rtt_us_fakezk': py50,
             'p99_get_rtt_us_fakezk': py99,
             'bulk_tcp_ops_s': bulk_ops,

@@ -191,11 +191,12 @@ bool set_steal(PyObject* d, PyObject* k, PyObject* v) {
   return true;
 }
 
-PyObject* decode_response(PyObject*, PyObject* args) {
-  Py_buffer view;
-  PyObject* xmap;
-  if (!PyArg_ParseTuple(args, "y*O", &view, &xmap)) return nullptr;
-  Reader r{(const uint8_t*)view.buf, 0, view.len};
+// One reply body -> dict (new reference), or nullptr with the error set.
+// Also reached from the native loop's reply router through the module's
+// `_C_decode_reply` capsule, on bytes still in its receive buffer.
+PyObject* decode_reply_raw(const uint8_t* body, Py_ssize_t len,
+                           PyObject* xmap) {
+  Reader r{body, 0, len};
   PyObject* d = nullptr;
   int32_t xid, err;
   int64_t zxid;
@@ -261,13 +262,20 @@ PyObject* decode_response(PyObject*, PyObject* args) {
     if (!ok) goto fail;
   }
   Py_DECREF(op);
-  PyBuffer_Release(&view);
   return d;
 fail:
   Py_XDECREF(op);
   Py_XDECREF(d);
-  PyBuffer_Release(&view);
   return nullptr;
+}
+
+PyObject* decode_response(PyObject*, PyObject* args) {
+  Py_buffer view;
+  PyObject* xmap;
+  if (!PyArg_ParseTuple(args, "y*O", &view, &xmap)) return nullptr;
+  PyObject* d = decode_reply_raw((const uint8_t*)view.buf, view.len, xmap);
+  PyBuffer_Release(&view);
+  return d;
 }
 
 // -- writer -------------------------------------------------------------------
@@ -381,27 +389,32 @@ long as_long(PyObject* o, long dflt) {
   return PyLong_AsLong(o);
 }
 
-PyObject* encode_request(PyObject*, PyObject* arg) {
-  PyObject* d = arg;
+// Encode one request dict, appending it to `out` (with its 4-byte length
+// prefix when `framed`).  False with the error set on a bad packet (`out`
+// is then left as it was).  Also reached from the native loop's request
+// path through the module's `_C_encode_request` capsule.
+bool encode_request_into(PyObject* d, std::string* out, bool framed) {
   if (!PyDict_Check(d)) {
     PyErr_SetString(PyExc_TypeError, "packet must be a dict");
-    return nullptr;
+    return false;
   }
   PyObject* opo = get(d, N.opcode);
   PyObject* xo = get(d, N.xid);
   if (!opo || !xo) {
     if (!PyErr_Occurred()) PyErr_SetString(PyExc_KeyError, "opcode/xid");
-    return nullptr;
+    return false;
   }
   const char* op = PyUnicode_AsUTF8(opo);
-  if (!op) return nullptr;
+  if (!op) return false;
   int32_t code;
   if (!code_of(g_ops, op, &code)) {
     PyErr_Format(PyExc_ValueError, "Unsupported opcode %s", op);
-    return nullptr;
+    return false;
   }
+  const size_t base = out->size();
   Writer w;
-  w.s.reserve(64);
+  w.s.swap(*out);
+  if (framed) w.i32(0);                  // length, patched below
   w.i32((int32_t)PyLong_AsLong(xo));
   w.i32(code);
   bool ok = true;
@@ -444,13 +457,26 @@ PyObject* encode_request(PyObject*, PyObject* arg) {
       break;
     default:
       PyErr_Format(PyExc_ValueError, "Unsupported opcode %s", op);
-      return nullptr;
+      ok = false;
   }
+  w.s.swap(*out);
   if (!ok || PyErr_Occurred()) {
     if (!PyErr_Occurred()) PyErr_SetString(PyExc_KeyError, "packet field");
-    return nullptr;
+    out->resize(base);
+    return false;
   }
-  return PyBytes_FromStringAndSize(w.s.data(), (Py_ssize_t)w.s.size());
+  if (framed) {
+    const uint32_t n = __builtin_bswap32((uint32_t)(out->size() - base - 4));
+    memcpy(&(*out)[base], &n, 4);
+  }
+  return true;
+}
+
+PyObject* encode_request(PyObject*, PyObject* arg) {
+  std::string s;
+  s.reserve(64);
+  if (!encode_request_into(arg, &s, false)) return nullptr;
+  return PyBytes_FromStringAndSize(s.data(), (Py_ssize_t)s.size());
 }
 
 PyObject* frame(PyObject*, PyObject* arg) {
@@ -537,5 +563,22 @@ PyMODINIT_FUNC PyInit__zkhost(void) {
   intern(g_perms); intern(g_flags);
   g_decode_err = PyExc_ValueError;
   Py_INCREF(g_decode_err);
-  return PyModule_Create(&mod);
+  PyObject* m = PyModule_Create(&mod);
+  if (m == nullptr) return nullptr;
+  // C entry point for the native loop (csrc/host/zk_loop.cpp, Router)
+  PyObject* cap = PyCapsule_New((void*)&decode_reply_raw,
+                                "zkmi._zkhost.decode_reply_raw", nullptr);
+  if (cap == nullptr || PyModule_AddObject(m, "_C_decode_reply", cap) < 0) {
+    Py_XDECREF(cap);
+    Py_DECREF(m);
+    return nullptr;
+  }
+  PyObject* cap2 = PyCapsule_New((void*)&encode_request_into,
+                                 "zkmi._zkhost.encode_request_into", nullptr);
+  if (cap2 == nullptr || PyModule_AddObject(m, "_C_encode_request", cap2) < 0) {
+    Py_XDECREF(cap2);
+    Py_DECREF(m);
+    return nullptr;
+  }
+  return m;
 }

@@ -81,6 +81,15 @@ double loop_spin_ms() {
   return v;
 }
 
+// ZKMI_LOOP_CORK=0 sends every write at once (A/B switch for queue_write).
+bool loop_cork() {
+  static const bool v = [] {
+    const char* e = getenv("ZKMI_LOOP_CORK");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
 PyObject* os_error(int err) {
   return PyObject_CallFunction(PyExc_OSError, "is", err, strerror(err));
 }
@@ -186,6 +195,43 @@ struct NoteSink {
   int64_t frames = 0;
 };
 
+// Reply router (Transport.route): the completion path of the interactive
+// API.  While on, the read path frames the inbound stream itself and, for
+// every reply whose xid is an outstanding request in `reqs` (the
+// connection's dict xid -> ZKRequest), decodes it with the host codec
+// (zk_host_codec.cpp, straight from the receive buffer), removes the xid
+// from `reqs` and `xmap` (the xid -> opcode map) and settles the request:
+// an OK reply goes to the request's (on_reply, on_error) pair directly
+// (ZKRequest.then), anything else to `on_other(req, pkt)`.  Frames it does
+// not own (notifications, pings, SET_WATCHES, bulk replies without a
+// capture, unknown xids, undecodable bodies) go to Python in stream order.
+// Routed replies update `max_zxid` and `last_rx` here; the session reads
+// them when it needs them (lastZxidSeen, expiry) instead of per reply.
+typedef PyObject* (*DecodeFn)(const uint8_t*, Py_ssize_t, PyObject*);
+typedef bool (*EncodeFn)(PyObject*, std::string*, bool);
+struct Router {
+  bool on = false;
+  bool give_back = false;    // turned off mid-dispatch: carry goes to Python
+  int64_t max_packet = 0;
+  PyObject* reqs = nullptr;
+  PyObject* xmap = nullptr;
+  PyObject* on_other = nullptr;
+  DecodeFn decode = nullptr;
+  EncodeFn encode = nullptr;     // Transport.request (optional)
+  int64_t max_zxid = 0;
+  double last_rx = 0;
+  int64_t routed = 0;
+};
+
+// One unit of an inbound read, in stream order: bytes for Python, or a
+// routed (request, reply) pair.
+struct RxItem {
+  PyObject* req;             // nullptr: `bytes` holds frames for Python
+  PyObject* pkt;
+  int32_t err;
+  std::string bytes;
+};
+
 struct Transport {
   Watched w;
   PyObject* protocol;
@@ -197,6 +243,9 @@ struct Transport {
   PyObject* peer;        // (host, port) tuple
   Capture* cap;
   NoteSink* ns;
+  Router* rt;
+  int dispatching;       // >0 while deliver() hands a read's items out
+  bool queued;           // on the loop's dirty list (a coalesced write)
 };
 
 struct Server {
@@ -225,6 +274,7 @@ struct Loop {
   std::vector<Handle*>* timers;                  // min-heap by (when, seq)
   std::unordered_map<uint64_t, Watched*>* regs;  // strong refs
   double last_active;                            // mono_ms of the last event
+  std::vector<Transport*>* dirty;                // writes to flush this turn
 };
 
 bool on_loop_thread(Loop* L) {
@@ -377,6 +427,9 @@ Transport* new_transport(Loop* L, int fd) {
   t->peer = nullptr;
   t->cap = new Capture();
   t->ns = new NoteSink();
+  t->rt = new Router();
+  t->dispatching = 0;
+  t->queued = false;
   return t;
 }
 
@@ -386,6 +439,10 @@ void Transport_dealloc(Transport* t) {
   Py_XDECREF(t->cap->done);
   delete t->cap;
   delete t->ns;
+  Py_XDECREF(t->rt->reqs);
+  Py_XDECREF(t->rt->xmap);
+  Py_XDECREF(t->rt->on_other);
+  delete t->rt;
   Py_XDECREF(t->protocol);
   Py_XDECREF(t->on_fail);
   Py_XDECREF(t->peer);
@@ -415,6 +472,7 @@ void finish(Transport* t, PyObject* exc) {
   t->cap->dst = nullptr;
   t->cap->carry.clear();
   Py_CLEAR(t->cap->done);
+  t->rt->on = false;
   Py_INCREF(t);
   drop_watch(&t->w);
   if (t->connected && t->protocol != nullptr)
@@ -510,6 +568,12 @@ int32_t be32(const char* p) {
   return (int32_t)ntohl(v);
 }
 
+uint64_t be64(const char* p) {
+  uint64_t v;
+  memcpy(&v, p, 8);
+  return __builtin_bswap64(v);
+}
+
 void deliver(Transport* t, const char* p, size_t n);
 
 // End the capture: done(status, nbytes, nframes, last_off), then the bytes
@@ -538,10 +602,74 @@ void capture_end(Transport* t, int status) {
   if (!t->closed && !rest.empty()) deliver(t, rest.data(), rest.size());
 }
 
+// The router's part of a frame (see Router): decode and unlink a reply
+// whose xid is outstanding; false leaves the frame to Python.  Calls no
+// Python code (dict lookups on int keys, the C decoder).
+bool route_frame(Router& rt, const char* f, int32_t fl, int64_t xid,
+                 RxItem& it) {
+  PyObject* k = PyLong_FromLongLong(xid);
+  if (k == nullptr) { PyErr_Clear(); return false; }
+  PyObject* req = PyDict_GetItemWithError(rt.reqs, k);     // borrowed
+  if (req == nullptr) {
+    PyErr_Clear();
+    Py_DECREF(k);
+    return false;
+  }
+  PyObject* pkt = rt.decode((const uint8_t*)f + 4, fl, rt.xmap);
+  if (pkt == nullptr) {
+    // Python's path raises the same decode error on the same bytes
+    PyErr_Clear();
+    Py_DECREF(k);
+    return false;
+  }
+  Py_INCREF(req);
+  if (PyDict_DelItem(rt.reqs, k) != 0) PyErr_Clear();
+  if (PyDict_DelItem(rt.xmap, k) != 0) PyErr_Clear();
+  Py_DECREF(k);
+  const int64_t zxid = (int64_t)be64(f + 8);
+  if (zxid > rt.max_zxid) rt.max_zxid = zxid;
+  ++rt.routed;
+  it.req = req;
+  it.pkt = pkt;
+  it.err = be32(f + 16);
+  return true;
+}
+
+// Settle one routed request: (on_reply, on_error) = req.fast, called
+// directly for an OK reply when nothing else listens on the request;
+// otherwise on_other(req, pkt) (error replies, listener-style requests).
+void settle_routed(Transport* t, RxItem& it) {
+  Loop* L = t->w.loop;
+  PyObject* r = nullptr;
+  bool direct = false;
+  if (it.err == 0) {
+    PyObject* fast = PyObject_GetAttrString(it.req, "fast");
+    PyObject* lst = fast ? PyObject_GetAttrString(it.req, "_listeners")
+                         : nullptr;
+    if (fast && lst && PyTuple_Check(fast) && PyTuple_GET_SIZE(fast) == 2 &&
+        PyDict_Check(lst) && PyDict_GET_SIZE(lst) == 0) {
+      direct = true;
+      r = PyObject_CallOneArg(PyTuple_GET_ITEM(fast, 0), it.pkt);
+    }
+    if (!fast || !lst) PyErr_Clear();
+    Py_XDECREF(fast);
+    Py_XDECREF(lst);
+  }
+  if (!direct) {
+    PyObject* cb = t->rt->on_other;
+    if (cb != nullptr) r = PyObject_CallFunctionObjArgs(cb, it.req, it.pkt,
+                                                       nullptr);
+    else r = Py_NewRef(Py_None);
+  }
+  if (r == nullptr) report_exception(L);
+  Py_XDECREF(r);
+}
+
 void deliver(Transport* t, const char* p, size_t n) {
   Capture& c = *t->cap;
   NoteSink& ns = *t->ns;
-  if (!c.on && !ns.on) { deliver_raw(t, p, n); return; }
+  Router& rt = *t->rt;
+  if (!c.on && !ns.on && !rt.on) { deliver_raw(t, p, n); return; }
   std::string buf;
   const char* s = p;
   size_t len = n;
@@ -551,11 +679,13 @@ void deliver(Transport* t, const char* p, size_t n) {
     s = buf.data();
     len = buf.size();
   }
-  std::string pass;               // frames that are neither
+  std::vector<RxItem> items;      // in stream order
+  std::string pass;               // frames for Python since the last item
   int64_t nn = 0;
   size_t i = 0;
   int status = -1;
-  const int64_t maxp = c.on ? c.max_packet : ns.max_packet;
+  const int64_t maxp = c.on ? c.max_packet
+                            : ns.on ? ns.max_packet : rt.max_packet;
   while (len - i >= 4) {
     if (c.on && c.got >= c.n) break;      // (capture_end re-delivers the rest)
     const int32_t fl = be32(s + i);
@@ -563,7 +693,7 @@ void deliver(Transport* t, const char* p, size_t n) {
       if (c.on) {
         status = CAP_BAD;
       } else {
-        // the sink alone: Python's framer sees the bad length and reports it
+        // no capture: Python's framer sees the bad length and reports it
         pass.append(s + i, len - i);
         i = len;
       }
@@ -580,15 +710,54 @@ void deliver(Transport* t, const char* p, size_t n) {
     } else if (ns.on && fl >= 16 && xid == -1) {
       ns.buf.append(s + i, 4 + (size_t)fl);
       ++nn;
+    } else if (rt.on && fl >= 16 && xid >= 0) {
+      RxItem one;
+      one.req = one.pkt = nullptr;
+      if (route_frame(rt, s + i, fl, xid, one)) {
+        if (!pass.empty()) {
+          RxItem b;
+          b.req = b.pkt = nullptr;
+          b.err = 0;
+          b.bytes.swap(pass);
+          items.push_back(std::move(b));
+        }
+        items.push_back(std::move(one));
+      } else {
+        pass.append(s + i, 4 + (size_t)fl);
+      }
     } else {
       pass.append(s + i, 4 + (size_t)fl);
     }
     i += 4 + (size_t)fl;
   }
   ns.frames += nn;
+  if (rt.on && i > 0) rt.last_rx = mono_ms();
   if (status < 0 && c.on && c.got >= c.n) status = CAP_DONE;
   c.carry.assign(s + i, len - i);
+  // Hand the read out in order.  Callbacks may close the transport, turn
+  // the router off or start a capture: routed replies are settled anyway
+  // (they arrived and were unlinked), bytes go to Python while it is open.
+  ++t->dispatching;
+  for (size_t j = 0; j < items.size(); ++j) {
+    RxItem& it = items[j];
+    if (it.req == nullptr) {
+      deliver_raw(t, it.bytes.data(), it.bytes.size());
+    } else {
+      settle_routed(t, it);
+      Py_CLEAR(it.req);
+      Py_CLEAR(it.pkt);
+    }
+  }
   deliver_raw(t, pass.data(), pass.size());
+  --t->dispatching;
+  if (t->dispatching == 0 && rt.give_back) {
+    rt.give_back = false;
+    if (!c.on && !ns.on && !rt.on && !c.carry.empty() && !t->closed) {
+      std::string rest;
+      rest.swap(c.carry);
+      deliver_raw(t, rest.data(), rest.size());
+    }
+  }
   if (status >= 0 && c.on && !t->closed) capture_end(t, status);
 }
 
@@ -647,6 +816,57 @@ void transport_event(Transport* t, uint32_t ev) {
   Py_DECREF(t);
 }
 
+// Writes made on the loop thread are coalesced: the bytes wait in wbuf and
+// the transport goes on the loop's dirty list, flushed once at the end of
+// the loop turn (flush_dirty), so a burst of pipelined requests issued from
+// one batch of reply callbacks leaves in one send() instead of one per
+// request.  A write from another thread, or one that leaves more than
+// kCorkMax unsent, is sent at once.
+constexpr size_t kCorkMax = 256 * 1024;
+
+PyObject* queue_write(Transport* t) {
+  if (!t->connected) Py_RETURN_TRUE;
+  Loop* L = t->w.loop;
+  if (loop_cork() && on_loop_thread(L) &&
+      t->wbuf->size() - t->woff < kCorkMax) {
+    if (!t->queued) {
+      t->queued = true;
+      Py_INCREF(t);
+      L->dirty->push_back(t);
+    }
+    Py_RETURN_TRUE;
+  }
+  int err = flush(t);
+  if (err) {
+    // report from the loop, never from inside the caller's stack
+    PyObject* e = PyLong_FromLong(err);
+    defer_method(L, (PyObject*)t, "_fatal", e);
+    Py_XDECREF(e);
+    t->closing = true;
+    Py_RETURN_FALSE;
+  }
+  refresh(t);
+  Py_RETURN_TRUE;
+}
+
+// Send what the loop turn's writes queued (see queue_write).
+void flush_dirty(Loop* L) {
+  if (L->dirty->empty()) return;
+  std::vector<Transport*> ts;
+  ts.swap(*L->dirty);
+  for (Transport* t : ts) {
+    t->queued = false;
+    if (!t->closed && t->connected) {
+      int err = flush(t);
+      if (err) fatal(t, err);
+      else if (!t->closed && t->closing && t->woff == t->wbuf->size())
+        finish(t, nullptr);
+      else refresh(t);
+    }
+    Py_DECREF(t);
+  }
+}
+
 PyObject* Transport_write(Transport* t, PyObject* arg) {
   Py_buffer v;
   if (PyObject_GetBuffer(arg, &v, PyBUF_SIMPLE) != 0) return nullptr;
@@ -656,19 +876,7 @@ PyObject* Transport_write(Transport* t, PyObject* arg) {
   }
   t->wbuf->append((const char*)v.buf, (size_t)v.len);
   PyBuffer_Release(&v);
-  if (t->connected) {
-    int err = flush(t);
-    if (err) {
-      // report from the loop, never from inside the caller's stack
-      PyObject* e = PyLong_FromLong(err);
-      defer_method(t->w.loop, (PyObject*)t, "_fatal", e);
-      Py_XDECREF(e);
-      t->closing = true;
-      Py_RETURN_FALSE;
-    }
-    refresh(t);
-  }
-  Py_RETURN_TRUE;
+  return queue_write(t);
 }
 
 // write_from(addr, n): queue n bytes read from raw memory (a pinned host
@@ -684,18 +892,7 @@ PyObject* Transport_write_from(Transport* t, PyObject* args) {
   if (t->closed || t->closing || t->wr_shut || t->eof_pending)
     Py_RETURN_FALSE;
   t->wbuf->append((const char*)(uintptr_t)addr, (size_t)n);
-  if (t->connected) {
-    int err = flush(t);
-    if (err) {
-      PyObject* e = PyLong_FromLong(err);
-      defer_method(t->w.loop, (PyObject*)t, "_fatal", e);
-      Py_XDECREF(e);
-      t->closing = true;
-      Py_RETURN_FALSE;
-    }
-    refresh(t);
-  }
-  Py_RETURN_TRUE;
+  return queue_write(t);
 }
 
 // capture(x0, n, addr, size, max_packet, done, prefix): see Capture.  The
@@ -728,7 +925,7 @@ PyObject* Transport_capture(Transport* t, PyObject* args) {
   c.len = c.last_off = 0;
   // with the sink on the native framer already holds the partial frame
   // (Python's holds none); else the caller's framer hands it over below
-  if (!t->ns->on) c.carry.clear();
+  if (!t->ns->on && !t->rt->on) c.carry.clear();
   Py_INCREF(done);
   c.done = done;
   std::string head((const char*)pre.buf, (size_t)pre.len);
@@ -753,17 +950,111 @@ PyObject* Transport_note_sink(Transport* t, PyObject* args) {
     const bool was = ns.on;
     ns.on = true;
     ns.max_packet = maxp;
-    if (!was && !t->cap->on) t->cap->carry.clear();
+    if (!was && !t->cap->on && !t->rt->on) t->cap->carry.clear();
     if (!head.empty() && !t->closed) deliver(t, head.data(), head.size());
   } else if (ns.on) {
     ns.on = false;
-    if (!t->cap->on && !t->cap->carry.empty()) {
+    if (t->dispatching > 0) {
+      t->rt->give_back = true;
+    } else if (!t->cap->on && !t->rt->on && !t->cap->carry.empty()) {
       std::string rest;
       rest.swap(t->cap->carry);
       deliver_raw(t, rest.data(), rest.size());
     }
   }
   Py_RETURN_NONE;
+}
+
+// route(on, reqs, xid_map, on_other, decoder, max_packet, prefix): see
+// Router.  `decoder` is the host codec's `_C_decode_reply` capsule;
+// `prefix` = a partial frame the caller's framer holds, parsed first.
+// Turning it off hands a partial frame the native framer holds back to
+// Python (after the read being dispatched, when called from a callback).
+PyObject* Transport_route(Transport* t, PyObject* args) {
+  int on;
+  PyObject *reqs, *xmap, *other, *cap;
+  PyObject* ecap = Py_None;
+  long long maxp;
+  Py_buffer pre;
+  if (!PyArg_ParseTuple(args, "pOOOOLy*|O", &on, &reqs, &xmap, &other, &cap,
+                        &maxp, &pre, &ecap))
+    return nullptr;
+  std::string head((const char*)pre.buf, (size_t)pre.len);
+  PyBuffer_Release(&pre);
+  Router& rt = *t->rt;
+  if (!on) {
+    if (!rt.on) Py_RETURN_NONE;
+    rt.on = false;
+    if (t->dispatching > 0) {
+      rt.give_back = true;
+    } else if (!t->cap->on && !t->ns->on && !t->cap->carry.empty()) {
+      std::string rest;
+      rest.swap(t->cap->carry);
+      deliver_raw(t, rest.data(), rest.size());
+    }
+    Py_RETURN_NONE;
+  }
+  if (!PyDict_Check(reqs) || !PyDict_Check(xmap) || !PyCallable_Check(other)) {
+    PyErr_SetString(PyExc_TypeError, "route: reqs/xid_map dicts, callable");
+    return nullptr;
+  }
+  void* fn = PyCapsule_GetPointer(cap, "zkmi._zkhost.decode_reply_raw");
+  if (fn == nullptr) return nullptr;
+  void* efn = nullptr;
+  if (ecap != Py_None) {
+    efn = PyCapsule_GetPointer(ecap, "zkmi._zkhost.encode_request_into");
+    if (efn == nullptr) return nullptr;
+  }
+  if (t->closed) Py_RETURN_NONE;
+  const bool was = rt.on;
+  Py_INCREF(reqs);
+  Py_XSETREF(rt.reqs, reqs);
+  Py_INCREF(xmap);
+  Py_XSETREF(rt.xmap, xmap);
+  Py_INCREF(other);
+  Py_XSETREF(rt.on_other, other);
+  rt.decode = (DecodeFn)fn;
+  rt.encode = (EncodeFn)efn;
+  rt.max_packet = maxp;
+  rt.on = true;
+  rt.give_back = false;
+  if (!was && !t->cap->on && !t->ns->on) t->cap->carry.clear();
+  if (!head.empty()) deliver(t, head.data(), head.size());
+  Py_RETURN_NONE;
+}
+
+// request(pkt, req): the send half of the completion path.  pkt is a
+// request dict with its xid set; it is encoded by the host codec straight
+// into the write buffer, and req (the ZKRequest its reply settles) and its
+// opcode are entered in the router's reqs / xid_map under that xid.  True
+// when queued; None when the router is off (or has no encoder; the caller
+// sends it its own way); False on a closing transport; raises on a packet
+// the codec refuses.
+PyObject* Transport_request(Transport* t, PyObject* args) {
+  PyObject *pkt, *req;
+  if (!PyArg_ParseTuple(args, "O!O", &PyDict_Type, &pkt, &req)) return nullptr;
+  Router& rt = *t->rt;
+  if (!rt.on || rt.encode == nullptr) Py_RETURN_NONE;   // caller's path
+  if (t->closed || t->closing || t->wr_shut || t->eof_pending)
+    Py_RETURN_FALSE;
+  PyObject* xo = PyDict_GetItemString(pkt, "xid");           // borrowed
+  PyObject* op = PyDict_GetItemString(pkt, "opcode");
+  if (xo == nullptr || op == nullptr) {
+    PyErr_SetString(PyExc_KeyError, "request: xid/opcode");
+    return nullptr;
+  }
+  if (!rt.encode(pkt, t->wbuf, true)) return nullptr;
+  if (PyDict_SetItem(rt.reqs, xo, req) != 0 ||
+      PyDict_SetItem(rt.xmap, xo, op) != 0)
+    return nullptr;
+  return queue_write(t);
+}
+
+// route_state() -> (max_zxid, last_rx_ms, routed): what the router saw.
+PyObject* Transport_route_state(Transport* t, PyObject*) {
+  const Router& rt = *t->rt;
+  return Py_BuildValue("(LdL)", (long long)rt.max_zxid, rt.last_rx,
+                       (long long)rt.routed);
 }
 
 // take_notes() -> (bytes, frames): the notification frames the sink kept
@@ -897,6 +1188,12 @@ PyMethodDef Transport_methods[] = {
      "end the active capture"},
     {"note_sink", (PyCFunction)Transport_note_sink, METH_VARARGS,
      "keep NOTIFICATION frames natively"},
+    {"route", (PyCFunction)Transport_route, METH_VARARGS,
+     "settle outstanding requests' replies natively"},
+    {"request", (PyCFunction)Transport_request, METH_VARARGS,
+     "encode a request into the write buffer and register its reply"},
+    {"route_state", (PyCFunction)Transport_route_state, METH_NOARGS,
+     "(max_zxid, last_rx_ms, routed) of the reply router"},
     {"take_notes", (PyCFunction)Transport_take_notes, METH_NOARGS,
      "the kept NOTIFICATION frames (bytes, count)"},
     {nullptr, nullptr, 0, nullptr}};
@@ -1012,10 +1309,16 @@ PyObject* Loop_new(PyTypeObject* type, PyObject* args, PyObject*) {
   L->last_active = 0;
   L->timers = new std::vector<Handle*>();
   L->regs = new std::unordered_map<uint64_t, Watched*>();
+  L->dirty = new std::vector<Transport*>();
   return (PyObject*)L;
 }
 
 void clear_all(Loop* L) {
+  for (Transport* t : *L->dirty) {
+    t->queued = false;
+    Py_DECREF(t);
+  }
+  L->dirty->clear();
   for (Handle* h : *L->ready) Py_DECREF(h);
   L->ready->clear();
   for (Handle* h : *L->timers) Py_DECREF(h);
@@ -1035,6 +1338,7 @@ void Loop_dealloc(Loop* L) {
   delete L->ready;
   delete L->timers;
   delete L->regs;
+  delete L->dirty;
   if (L->epfd >= 0) close(L->epfd);
   if (L->evfd >= 0) close(L->evfd);
   Py_XDECREF(L->on_exception);
@@ -1064,6 +1368,7 @@ PyObject* Loop_run(Loop* L, PyObject*) {
   std::vector<epoll_event> evs(256);
   std::vector<Handle*> due;
   while (!L->stopping) {
+    flush_dirty(L);
     int timeout = -1;
     if (!L->ready->empty()) {
       timeout = 0;
@@ -1149,6 +1454,7 @@ PyObject* Loop_run(Loop* L, PyObject*) {
       Py_DECREF(h);
     }
   }
+  flush_dirty(L);           // what the last turn wrote still leaves
   clear_all(L);
   L->running = false;
   Py_RETURN_NONE;

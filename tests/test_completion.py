@@ -1,0 +1,174 @@
+"""The native completion path of the interactive API (CPU): the native
+loop's reply router (``Transport.route``, csrc/host/zk_loop.cpp) settles
+replies to outstanding requests without Python framing/decoding, and
+``Transport.request`` encodes requests straight into the write buffer.
+
+Parity targets: the reply routing of ``lib/connection-fsm.js:213-229`` and
+``:384-408`` (every reply settles its request, in stream order with the
+notifications around it), ``lib/zk-session.js:227-238`` (every packet
+advances lastZxid and the expiry timer)."""
+
+import threading
+
+import pytest
+
+from zkmi.errors import ZKError
+from zkmi.server import FakeZKServer
+from zkmi.runtime import nloop
+
+from zkhelpers import Box, client, wait_for
+
+pytestmark = pytest.mark.skipif(not nloop.available(),
+                                reason='native loop not built')
+
+
+@pytest.fixture
+def zk():
+    s = FakeZKServer(tick_ms=250)
+    yield s
+    s.shutdown()
+
+
+@pytest.fixture
+def zkc(zk):
+    c = client(zk.servers())
+    c.wait_connected(10)
+    yield c
+    c.close_sync(10)
+
+
+def _conn(c):
+    return c.loop.run(lambda: c.getSession().getConnection())
+
+
+def _routed(c):
+    conn = _conn(c)
+    return c.loop.run(lambda: conn.socket.transport.route_state()[2])
+
+
+def test_router_settles_replies(zkc):
+    conn = _conn(zkc)
+    assert conn.routing
+    before = _routed(zkc)
+    assert zkc.call_sync('create', '/r', b'abc', {}) == '/r'
+    data, stat = zkc.call_sync('get', '/r')
+    assert data == b'abc' and stat.dataLength == 3
+    assert _routed(zkc) >= before + 2
+    # nothing left behind in the connection's tables
+    assert zkc.loop.run(lambda: (len(conn.reqs), len(conn.xid_map))) == (0, 0)
+
+
+def test_error_replies_and_pipelined_mix(zkc):
+    zkc.call_sync('create', '/m', b'', {})
+    for i in range(0, 200, 2):
+        zkc.call_sync('create', '/m/n%d' % i, b'%d' % i, {})
+    n = 200
+    got = {}
+    done = threading.Event()
+
+    def issue():
+        for i in range(n):
+            def cb(err, data=None, stat=None, i=i):
+                got[i] = (err, data)
+                if len(got) == n:
+                    done.set()
+            zkc.get('/m/n%d' % i, cb)
+    zkc.loop.call_soon(issue)
+    assert done.wait(20)
+    for i in range(n):
+        err, data = got[i]
+        if i % 2 == 0:
+            assert err is None and data == b'%d' % i
+        else:
+            assert isinstance(err, ZKError) and err.code == 'NO_NODE'
+
+
+def test_last_zxid_and_liveness_follow_routed_replies(zkc):
+    sess = zkc.loop.run(zkc.getSession)
+    z0 = zkc.loop.run(lambda: sess.last_zxid)
+    zkc.call_sync('create', '/z', b'', {})
+    zkc.call_sync('set', '/z', b'x', -1)
+    st = zkc.call_sync('stat', '/z')
+    z1 = zkc.loop.run(lambda: sess.last_zxid)
+    assert z1 >= st.mzxid > z0
+    assert zkc.loop.run(lambda: sess.credentials()['lastZxid']) == z1
+
+    # the routed replies alone keep the session alive: forget the Python
+    # side's last packet and ask again
+    def probe():
+        sess.last_pkt = None
+        return sess.isAlive()
+    assert zkc.loop.run(probe)
+
+
+def test_notification_order_around_routed_replies(zk, zkc):
+    """A watch event and the replies around it reach the client in stream
+    order: the notification goes through Python's path, the replies through
+    the router, and neither overtakes the other."""
+    zkc.call_sync('create', '/w', b'0', {})
+    order = []
+    fired = Box()
+
+    w = zkc.watcher('/w')
+    w.on('dataChanged', lambda d, s: (order.append(('data', d)), fired(d)))
+    assert wait_for(lambda: ('data', b'0') in order, 10)
+    done = threading.Event()
+
+    def go():
+        zkc.set('/w', b'1', -1, lambda err, *a: order.append(('set', err)))
+        zkc.get('/w', lambda err, d=None, s=None: (order.append(('get', d)),
+                                                     done.set()))
+    zkc.loop.call_soon(go)
+    assert done.wait(10)
+    assert wait_for(lambda: ('data', b'1') in order, 10)
+    i_set = order.index(('set', None))
+    i_get = order.index(('get', b'1'))
+    assert i_set < i_get
+
+
+def test_large_reply_split_across_reads(zkc):
+    blob = bytes(range(256)) * 4096           # 1 MiB: many recv() calls
+    zkc.call_sync('create', '/big', blob, {})
+    before = _routed(zkc)
+    data, stat = zkc.call_sync('get', '/big')
+    assert data == blob and stat.dataLength == len(blob)
+    assert _routed(zkc) == before + 1
+
+
+def test_router_off_while_paused_falls_back(zkc):
+    """pause_reading holds the stream: the router steps aside, requests go
+    the Python way and settle when reading resumes."""
+    conn = _conn(zkc)
+    sock = conn.socket
+    res = Box()
+
+    def go():
+        sock.pause_reading()
+        zkc.create('/p', b'x', {}, lambda err, *a: res(err, *a))
+    zkc.loop.run(go)
+    assert not res.ev.wait(0.5)
+    zkc.loop.run(sock.resume_reading)
+    err, path = res.wait(10)
+    assert err is None and path == '/p'
+    assert zkc.call_sync('get', '/p')[0] == b'x'
+
+
+def test_close_with_routed_requests_in_flight(zk):
+    c = client(zk.servers())
+    c.wait_connected(10)
+    n = 100
+    got = []
+    done = threading.Event()
+
+    def go():
+        for i in range(n):
+            c.stat('/nope%d' % i, lambda err, *a: (got.append(err),
+                                                       len(got) == n and
+                                                       done.set()))
+        c.close()
+    c.loop.call_soon(go)
+    assert done.wait(20)
+    # every request settles exactly once: a reply (NO_NODE) or a
+    # connection error, never both and never neither
+    assert len(got) == n
+    assert all(e is not None for e in got)

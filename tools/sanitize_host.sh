@@ -12,7 +12,7 @@ export ZKMI_HOST_CODEC_PATH="$SO"
 export ZKMI_NATIVE_LOOP_PATH="$LOOP_SO"
 python -m pytest -q -x -p no:cacheprovider tests/test_host_codec.py \
   tests/test_proto.py tests/test_fuzz_codec.py tests/test_native_loop.py \
-  tests/test_basic.py "$@"
+  tests/test_basic.py tests/test_completion.py "$@"
 
 # ThreadSanitizer over the threaded host code (the native event loop): the
 # loop, client and fault-injection suites
@@ -21,4 +21,4 @@ LD_PRELOAD="$(gcc -print-file-name=libtsan.so)" \
 TSAN_OPTIONS="halt_on_error=1 report_signal_unsafe=0" \
 ZKMI_HOST_CODEC_PATH= ZKMI_NATIVE_LOOP_PATH="$TSAN_SO" \
   python -m pytest -q -x -p no:cacheprovider tests/test_native_loop.py \
-  tests/test_basic.py tests/test_nasty.py "$@"
+  tests/test_basic.py tests/test_nasty.py tests/test_completion.py "$@"

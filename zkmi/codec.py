@@ -24,6 +24,10 @@ decode_request = jute.decode_request
 encode_response = jute.encode_response
 scan_frames = jute.scan_frames
 frame = jute.frame
+# C entry point of the native reply decoder (a capsule the native loop's
+# reply router calls); None without the native codec
+DECODE_REPLY_C = None
+ENCODE_REQUEST_C = None
 
 def _load_native():
     """The in-tree extension, or the one at ``ZKMI_HOST_CODEC_PATH`` (the
@@ -51,4 +55,6 @@ if os.environ.get('ZKMI_HOST_CODEC', 'native') != 'python':
         decode_response = _zkhost.decode_response
         scan_frames = _zkhost.scan_frames
         frame = _zkhost.frame
+        DECODE_REPLY_C = _zkhost._C_decode_reply
+        ENCODE_REQUEST_C = _zkhost._C_encode_request
         IMPL = 'native'

@@ -348,13 +348,24 @@ class Client(FSM):
         self.loop.call_soon(cb, ZKNotConnectedError())
 
     def _request(self, pkt, cb, on_reply):
-        def go():
+        if self.loop.in_loop():
+            self._issue(pkt, cb, on_reply)
+        else:
+            self.loop.call_soon(self._issue, pkt, cb, on_reply)
+
+    def _issue(self, pkt, cb, on_reply):
+        # currentConnection() with the state checks inlined: this runs once
+        # per data-API request
+        sess = self.session
+        if self._fsm_state != 'normal' or sess is None or \
+                sess._fsm_state != 'attached':
             conn = self.currentConnection()
-            if conn is None or not conn.isInState('connected'):
-                self._not_connected(cb)
-                return
-            conn.request(pkt).then(on_reply, lambda err, *_: cb(err))
-        self._dispatch(go)
+        else:
+            conn = sess.conn
+        if conn is None or conn._fsm_state != 'connected':
+            self._not_connected(cb)
+            return
+        conn.request(pkt).then(on_reply, lambda err, *_: cb(err))
 
     def ping(self, cb):
         _check_func(cb)

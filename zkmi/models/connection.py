@@ -77,6 +77,7 @@ class ZKConnectionFSM(FSM):
         self.notes = None
         self.notes_left = (b'', 0)
         self.bulk_frames_py = 0         # bulk replies routed one by one
+        self.routing = False            # native reply router on (_route)
         self.reqs = {}
         self.socket = None
         self.session = None
@@ -287,9 +288,11 @@ class ZKConnectionFSM(FSM):
         S.on(self, 'closeAsserted', lambda: S.gotoState('closing'))
         S.on(self, 'destroyAsserted', lambda: S.gotoState('closed'))
         S.on(self, 'pingTimeout', on_ping_timeout)
+        self._route(True)
         S.immediate(lambda: self.emit('connect'))
 
     def state_closing(self, S):
+        self._route(False)
         box = {'xid': None}
 
         def send_close_session():
@@ -342,6 +345,7 @@ class ZKConnectionFSM(FSM):
             send_close_session()
 
     def state_error(self, S):
+        self._route(False)
         err = self.last_error
         self.log.warn(err if isinstance(err, BaseException) else {},
                       'error communicating with ZK')
@@ -359,6 +363,7 @@ class ZKConnectionFSM(FSM):
             self.emit('error', err)
 
     def state_closed(self, S):
+        self._route(False)
         self.encoder = None
         if self.socket is not None and self.note_native:
             # the notifications the transport kept outlive it
@@ -376,6 +381,61 @@ class ZKConnectionFSM(FSM):
                 req.settle('error', err)
             self._fail_bulks(err)
         S.immediate(later)
+
+    # -- native completion path ----------------------------------------------
+
+    def _route(self, on):
+        """Settle replies to outstanding requests in the native transport
+        (``Transport.route``, csrc/host/zk_loop.cpp): it frames the stream,
+        decodes each reply whose xid is in :attr:`reqs` with the host codec,
+        unlinks it from :attr:`reqs` and :attr:`xid_map` and calls the
+        request's ``then`` pair — the per-reply work of ``on_rx`` /
+        ``_decode_reply`` / ``processReply`` without a Python frame in
+        between (``lib/connection-fsm.js:213-229``, ``:384-408``).  Every
+        other frame still comes through ``on_rx`` in stream order.  Off while
+        a tracer or trace logging wants each reply, on the asyncio loop and
+        outside ``connected``."""
+        sock = self.socket
+        if not on:
+            if self.routing:
+                self.routing = False
+                if sock is not None and sock.transport is not None:
+                    z, rx, _ = sock.transport.route_state()
+                    sock.transport.route(False, None, None, None, None, 0,
+                                         b'')
+                    if self.session is not None:
+                        self.session.fold_routed(z, rx)
+            return
+        if self.routing or sock is None or not sock.can_route() or \
+                self.tracer is not None or self.log.enabled('trace') or \
+                codec.DECODE_REPLY_C is None or self.decoder is None or \
+                self.decoder.dead:
+            return
+        sock.transport.route(True, self.reqs, self.xid_map,
+                             self._routed_other, codec.DECODE_REPLY_C,
+                             self.config.max_packet,
+                             self.decoder.take_pending(),
+                             codec.ENCODE_REQUEST_C)
+        self.routing = True
+
+    def route_state(self):
+        """(max zxid, loop ms of the last frame) the router settled."""
+        sock = self.socket
+        if not self.routing or sock is None or sock.transport is None:
+            return 0, 0.0
+        z, rx, _ = sock.transport.route_state()
+        return z, rx
+
+    def _routed_other(self, req, pkt):
+        """A routed reply the transport does not hand straight to the
+        request's ``then`` pair: an error reply, or a listener-style
+        request (processReply's delivery, the entry already unlinked)."""
+        if pkt['err'] == 'OK':
+            req.settle('reply', pkt)
+            return
+        code = pkt['err']
+        req.settle('error', ZKError(code, consts.ERR_TEXT.get(code, str(code))),
+                   pkt)
 
     # -- requests -------------------------------------------------------------
 
@@ -402,8 +462,14 @@ class ZKConnectionFSM(FSM):
         if not self.isInState('connected'):
             raise Exception('Client must be connected to send requests')
         req = ZKRequest(pkt)
-        xid = self.nextXid()
+        xid = self.xid
+        self.xid = (xid + 1) & 0x7fffffff
         pkt['xid'] = xid
+        if self.routing and pkt['opcode'] != 'SET_WATCHES' and \
+                self.socket.transport.request(pkt, req):
+            # encoded into the write buffer, entered in reqs / xid_map by
+            # the native transport; the router settles the reply
+            return req
         self.reqs[xid] = req      # removed by processReply / the fail paths
         self.log.trace({'xid': xid, 'opcode': pkt['opcode']},
                        'sent request to server')

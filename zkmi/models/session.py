@@ -33,6 +33,10 @@ class ExpiryTimer(EventEmitter):
         self.deadline = None
         self.timeout_ms = None
         self._h = None
+        # () -> ms (loop clock) of the last reply the connection's native
+        # router settled, or None: those replies reset the timer lazily,
+        # here, instead of one reset() each
+        self.probe = None
 
     def reset(self, timeout_ms):
         now = self.loop.time_ms()
@@ -52,6 +56,10 @@ class ExpiryTimer(EventEmitter):
         self._h = None
         if self.deadline is None:
             return
+        if self.probe is not None:
+            last = self.probe()
+            if last is not None and last + self.timeout_ms > self.deadline:
+                self.deadline = last + self.timeout_ms
         rem = self.deadline - self.loop.time_ms()
         if rem > 0.5:
             self._h = self.loop.call_later(rem, self._fire)
@@ -85,7 +93,8 @@ class ZKSession(FSM):
         self.collector = collector
         self.config = config
         self.last_attach = 0
-        self.last_zxid = 0
+        self._last_zxid = 0
+        self.expiry.probe = self._routed_last_rx
         # paths with bulk data watches (Client.watch_bulk): re-armed on a
         # move like the watchers' (their notifications go to the fan-out)
         self.bulk_watches = set()
@@ -104,9 +113,55 @@ class ZKSession(FSM):
         return self.isInState('attaching') or self.isInState('reattaching')
 
     def isAlive(self):
-        if self.last_pkt is None:
+        last = self.last_pkt
+        rx = self._routed_last_rx()
+        if rx is not None and (last is None or rx / 1e3 > last):
+            last = rx / 1e3
+        if last is None:
             return False
-        return (time.monotonic() - self.last_pkt) * 1000.0 < self.timeout
+        return (time.monotonic() - last) * 1000.0 < self.timeout
+
+    # -- replies settled by the connection's native router ------------------
+    # (ZKConnectionFSM.route_state): they carry zxids and keep the session
+    # alive like the packets on_packet sees, but are folded in only when
+    # read (lastZxidSeen, expiry, isAlive), or when the router stops.
+
+    def _routed(self):
+        for c in (self.conn, self.old_conn):
+            if c is not None and c.routing:
+                yield c.route_state()
+
+    def _routed_last_rx(self):
+        last = None
+        for _, rx in self._routed():
+            if rx > 0 and (last is None or rx > last):
+                last = rx
+        return last
+
+    @property
+    def last_zxid(self):
+        z = self._last_zxid
+        for rz, _ in self._routed():
+            if rz > z:
+                z = rz
+        return z
+
+    @last_zxid.setter
+    def last_zxid(self, z):
+        self._last_zxid = z
+
+    def fold_routed(self, zxid, last_rx_ms):
+        """A connection's router stopped: keep what it saw."""
+        if zxid > self._last_zxid:
+            self._last_zxid = zxid
+        if last_rx_ms > 0:
+            t = last_rx_ms / 1e3
+            if self.last_pkt is None or t > self.last_pkt:
+                self.last_pkt = t
+            ex = self.expiry
+            if ex.deadline is not None and ex.timeout_ms is not None and \
+                    last_rx_ms + ex.timeout_ms > ex.deadline:
+                ex.deadline = last_rx_ms + ex.timeout_ms
 
     def attachAndSendCR(self, conn):
         if not self.isInState('detached') and not self.isInState('attached'):
@@ -218,8 +273,8 @@ class ZKSession(FSM):
             self.resetExpiryTimer()
             if pkt['opcode'] != 'NOTIFICATION':
                 z = pkt['zxid']
-                if z > self.last_zxid:
-                    self.last_zxid = z
+                if z > self._last_zxid:
+                    self._last_zxid = z
                 return
             self.processNotification(pkt)
         S.on(conn, 'packet', on_packet)

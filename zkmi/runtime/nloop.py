@@ -85,7 +85,7 @@ class NativeLoop(object):
     # -- scheduling ---------------------------------------------------------
 
     def in_loop(self):
-        return threading.current_thread() is self._thread
+        return self._n.in_loop()
 
     def time_ms(self):
         return self._n.time_ms()

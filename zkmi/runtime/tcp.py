@@ -159,6 +159,12 @@ class TcpSocket(EventEmitter):
         not captured go to 'data' as usual)."""
         self.transport.capture(x0, n, addr, size, max_packet, done, prefix)
 
+    def can_route(self):
+        """True when the transport can settle replies itself (the native
+        loop's Transport.route)."""
+        return (self.transport is not None and not self.closed and
+                not self._paused and hasattr(self.transport, 'route'))
+
     def can_sink_notes(self):
         """True when the transport can keep NOTIFICATION frames itself (the
         native loop's Transport.note_sink)."""
@@ -226,6 +232,11 @@ class TcpSocket(EventEmitter):
         """Stop delivering ``data`` events (the reference test #46 unpipes
         the socket, ``test/basic.test.js:1374``)."""
         self._paused = True
+        t = self.transport
+        if t is not None and hasattr(t, 'route'):
+            # held means held: the native reply router stops settling (its
+            # partial frame comes back through data_received, held here)
+            t.route(False, None, None, None, None, 0, b'')
 
     def resume_reading(self):
         self._paused = False

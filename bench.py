@@ -557,6 +557,11 @@ def run_rank(a):
     rtt_srv = start_rtt_server() if rank == 0 and not a.no_rtt else None
     fast_srv = start_fast_server(a.nodes, a.data_bytes) \
         if rank == 0 and not a.no_rtt and a.workload == 'get' else None
+    ev_idle = (None, None)
+    if fast_srv is not None:
+        # the same event-loop round trip before this process touches the
+        # GPU, next to the one measured after the timed steps
+        ev_idle = measure_rtt_async(fast_srv.port)
     # One rank per GPU over RCCL ("nccl").  ZKMI_BENCH_BACKEND=gloo (host
     # collectives, ranks may share a GPU) exists only to rehearse the
     # multi-rank path on a one-GPU box.
@@ -749,6 +754,8 @@ def run_rank(a):
                               'the per-request API through the native '
                               'completion path (reply router + coalesced '
                               'writes in the native loop)',
+            'p50_get_rtt_us_evloop_pre_gpu': ev_idle[0],
+            'p99_get_rtt_us_evloop_pre_gpu': ev_idle[1],
             'p50_get_rtt_us_fakezk': py50,
             'p99_get_rtt_us_fakezk': py99,
             'bulk_tcp_ops_s': bulk_ops,

@@ -18,8 +18,16 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--n', type=int, default=20000)
     ap.add_argument('--window', type=int, default=256)
+    ap.add_argument('--nodes', type=int, default=1000,
+                    help='znodes preloaded in the native server')
+    ap.add_argument('--torch-gpu', action='store_true',
+                    help='start the server, then initialise the GPU in this '
+                         'process first (as bench.py does)')
     a = ap.parse_args()
-    srv = bench.start_fast_server(1000, 100)
+    srv = bench.start_fast_server(a.nodes, 100)
+    if a.torch_gpu:
+        import torch
+        torch.ones(1, device='cuda').sum().item()
     if srv is None:
         raise SystemExit('native server not built')
     try:
@@ -33,7 +41,10 @@ def main():
                       'blocking_p50_us': round(b50, 2),
                       'blocking_p99_us': round(b99, 2),
                       'pipelined_get_ops_s': round(ops),
-                      'window': a.window}))
+                      'window': a.window, 'nodes': a.nodes,
+                      'torch_gpu': a.torch_gpu,
+                      'cork': os.environ.get('ZKMI_LOOP_CORK', '1'),
+                      'route': os.environ.get('ZKMI_ROUTE', '1')}))
 
 
 if __name__ == '__main__':

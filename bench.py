@@ -529,6 +529,9 @@ def _time_steps(pipe, a, world, dev):
         dist.barrier()
     torch.cuda.synchronize()
     ok_total.zero_()
+    # (per-connection graphs do not wait on this stream: the zeroing must
+    # land before the first replay)
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         run()

@@ -15,5 +15,6 @@ for i in 1 2 3; do
   done
 done
 timeout -k 10 200 python tools/rtt_cpu.py --n 20000 --nodes 1000000 >> $OUT 2>&1 || exit $?
-timeout -k 10 200 python tools/rtt_cpu.py --n 20000 --nodes 1000000 --torch-gpu >> $OUT 2>&1 || exit $?
+timeout -k 10 200 python tools/rtt_cpu.py --n 20000 --nodes 1000000 \
+  --torch-gpu >> $OUT 2>&1 || exit $?
 cat $OUT

@@ -440,8 +440,8 @@ class ZKConnectionFSM(FSM):
             req.settle('reply', pkt)
             return
         code = pkt['err']
-        req.settle('error', ZKError(code, consts.ERR_TEXT.get(code, str(code))),
-                   pkt)
+        err = ZKError(code, consts.ERR_TEXT.get(code, str(code)))
+        req.settle('error', err, pkt)
 
     # -- requests -------------------------------------------------------------
 

@@ -1976,6 +1976,19 @@ static FsPlan fs_plan(int64_t n) {
 
 // ZKMI_FS_MINB: the frontier's minimum plausible body length (default 8;
 // 0 = any length, the round-2 behaviour; A/B only)
+// fs_link's grid (ZKMI_FL_B, 1..FL_B, default 16): every block must find a
+// CU slot before the launch ends, also on the usual path where block 0
+// alone works, so a smaller grid waits less behind another stream's kernel.
+static unsigned fl_blocks() {
+  static int b = -1;
+  if (b < 0) {
+    const char* e = getenv("ZKMI_FL_B");
+    b = e ? atoi(e) : 16;
+    if (b < 1 || b > FL_B) b = FL_B;
+  }
+  return (unsigned)b;
+}
+
 static int32_t fs_minb() {
   static int v = -1;
   if (v < 0) {
@@ -2119,7 +2132,7 @@ int zk_frame_scan5(const uint8_t* buf, const int64_t* n_dev, int64_t n_cap,
   fs_check<<<(unsigned)((tiles + FK_T - 1) / FK_T), FK_T, 0, st>>>(
       n_dev, n_cap, rent, rexit, rmeta, base, bsum, mins, grid + FL_NB, blist);
   ZK_LAUNCH_CHECK();
-  fs_link<<<FL_B, FL_T, 0, st>>>(buf, n_dev, n_cap, maxp, sx, list, rcnt,
+  fs_link<<<fl_blocks(), FL_T, 0, st>>>(buf, n_dev, n_cap, maxp, sx, list, rcnt,
                                  pre, rent, rexit, rmeta, base, cap, result,
                                  lbw + 2 * tiles, blist, bsum, mins, lastk,
                                  grid, lbw, cx, dbg ? dbg + 8 * tiles : nullptr);

@@ -79,13 +79,28 @@ constexpr int SB_T = 1024;
 constexpr int SB_V = 8;
 constexpr int64_t SCAN_ONE_MAX = 1 << 16;       // use it up to this n
 
-template <typename T>
-__global__ __launch_bounds__(SB_T) void scan_one_block(
+// A one-workgroup scan sits on its stream's critical path, and with two
+// connections in flight it waits for a CU with room for the whole
+// workgroup behind the other stream's kernel: up to 2048 values (the
+// encoders' block sums of a 512K-record batch) a 256-thread workgroup
+// scans them in one chunk (ZKMI_SB_SMALL=0: always 1024 threads).
+constexpr int SB_T_SMALL = 256;
+static bool sb_small() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("ZKMI_SB_SMALL");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v == 1;
+}
+
+template <typename T, int NT = SB_T>
+__global__ __launch_bounds__(NT) void scan_one_block(
     const T* __restrict__ in, int64_t n, int64_t* __restrict__ out,
     int64_t* __restrict__ total) {
-  __shared__ int64_t sm[SB_T / 64 + 1];
+  __shared__ int64_t sm[NT / 64 + 1];
   int64_t carry = 0;
-  for (int64_t c0 = 0; c0 < n; c0 += (int64_t)SB_T * SB_V) {   // uniform
+  for (int64_t c0 = 0; c0 < n; c0 += (int64_t)NT * SB_V) {   // uniform
     // thread t owns values c0 + t*V .. +V-1 (its own run: the scan order)
     const int64_t b = c0 + (int64_t)threadIdx.x * SB_V;
     int64_t v[SB_V];
@@ -105,6 +120,15 @@ __global__ __launch_bounds__(SB_T) void scan_one_block(
     carry += tot;
   }
   if (total != nullptr && threadIdx.x == 0) *total = carry;
+}
+
+template <typename T>
+static void launch_one_block(const T* in, int64_t n, int64_t* out,
+                             int64_t* total, hipStream_t st) {
+  if (sb_small() && n <= (int64_t)SB_T_SMALL * SB_V)
+    scan_one_block<T, SB_T_SMALL><<<1, SB_T_SMALL, 0, st>>>(in, n, out, total);
+  else
+    scan_one_block<T><<<1, SB_T, 0, st>>>(in, n, out, total);
 }
 
 // ---------------------------------------------------------------------------
@@ -327,7 +351,7 @@ static int scan_rec(const T* in, int64_t* out, int64_t n, int64_t* total,
     return 0;
   }
   if (n <= SCAN_ONE_MAX) {
-    scan_one_block<T><<<1, SB_T, 0, st>>>(in, n, out, total);
+    launch_one_block<T>(in, n, out, total, st);
     ZK_LAUNCH_CHECK();
     return 0;
   }
@@ -371,7 +395,7 @@ int zk_scan_small_i64(const int64_t* in, int64_t* out, int64_t n,
     if (total) return hipMemsetAsync(total, 0, sizeof(int64_t), st);
     return 0;
   }
-  zk::scan_one_block<int64_t><<<1, zk::SB_T, 0, st>>>(in, n, out, total);
+  zk::launch_one_block<int64_t>(in, n, out, total, st);
   ZK_LAUNCH_CHECK();
   return 0;
 }

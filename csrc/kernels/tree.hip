@@ -1058,13 +1058,14 @@ constexpr int FIN_T = 1024;
 // cross-block sign-off — the grid version's atomic sign-off counter took
 // 15-60 us per launch on a read-only GET batch, and two streams finishing
 // at once could interleave on it.
-__global__ __launch_bounds__(FIN_T) void tree_finish_k(ZkTree t,
-                                                      const int64_t* n_dev,
-                                                      int64_t bump_zxid,
-                                                      int32_t publish) {
+template <int NT = FIN_T>
+__global__ __launch_bounds__(NT) void tree_finish_k(ZkTree t,
+                                                   const int64_t* n_dev,
+                                                   int64_t bump_zxid,
+                                                   int32_t publish) {
   int64_t* c = t.counters;
   const int64_t nd = c[TC_DIRTY];
-  for (int64_t k = threadIdx.x; k < nd; k += FIN_T) {
+  for (int64_t k = threadIdx.x; k < nd; k += NT) {
     const int64_t p = t.dirty_list[k];
     uint8_t* slot = t.store.slab + t.store.slot_off[p];
     st_be32(slot + 36, t.cver[p]);
@@ -1311,7 +1312,17 @@ static int finish_launch(const ZkTree* t, int64_t ncap, const int64_t* n_dev,
                          int64_t bump_zxid, hipStream_t st,
                          int32_t publish = 1) {
   (void)ncap;
-  zk::tree_finish_k<<<1, zk::FIN_T, 0, st>>>(*t, n_dev, bump_zxid, publish);
+  // (ZKMI_FIN_T=1024: the round-3 workgroup; 256 finds a CU sooner behind
+  // another stream's kernel, and the dirty list is a few thousand entries)
+  static int fin = -1;
+  if (fin < 0) {
+    const char* e = getenv("ZKMI_FIN_T");
+    fin = (e && atoi(e) == 1024) ? 1024 : 256;
+  }
+  if (fin == 1024)
+    zk::tree_finish_k<1024><<<1, 1024, 0, st>>>(*t, n_dev, bump_zxid, publish);
+  else
+    zk::tree_finish_k<256><<<1, 256, 0, st>>>(*t, n_dev, bump_zxid, publish);
   ZK_LAUNCH_CHECK();
   return 0;
 }

@@ -1,20 +1,33 @@
 #!/bin/bash
-# A/B an environment switch on the GET bench: AB_VAR=<name> (values 1 and
-# 0), alternated ROUNDS times (default 3); BENCH_ARGS passed through.
-# Output: gpurun_out/ab_<name>.log (one JSON line per run, tagged).
+# A/B environment settings on a bench workload, alternated ROUNDS times
+# (default 3) so box drift hits every setting alike.
+#   AB_VAR=<name> AB_VALUES="1 0"     one variable over values, or
+#   AB_SETS="A=1,B=2 -"               whole settings ("-" = the defaults)
+# BENCH_ARGS is passed through.  Output: gpurun_out/ab_<tag>.log, one line
+# per run (setting, ms per step, ops/s).
 set -o pipefail
 mkdir -p gpurun_out
-OUT=gpurun_out/ab_${AB_VAR}.log
+if [ -n "$AB_SETS" ]; then
+  SETS="$AB_SETS"; TAG=${AB_TAG:-sets}
+else
+  SETS=""
+  for v in ${AB_VALUES:-1 0}; do SETS="$SETS $AB_VAR=$v"; done
+  TAG=$AB_VAR
+fi
+OUT=gpurun_out/ab_${TAG}.log
 : > $OUT
 for i in $(seq ${ROUNDS:-3}); do
-  for v in 1 0; do
-    env $AB_VAR=$v timeout -k 10 300 python bench.py --no-rtt ${BENCH_ARGS:-} \
+  for set in $SETS; do
+    envs=""
+    [ "$set" != "-" ] && envs=$(echo "$set" | tr ',' ' ')
+    env $envs timeout -k 10 300 python bench.py --no-rtt ${BENCH_ARGS:-} \
       > gpurun_out/ab_run.log 2>&1 || { tail -20 gpurun_out/ab_run.log; exit 1; }
-    python - "$AB_VAR=$v" gpurun_out/ab_run.log >> $OUT <<'PY'
+    python - "$set" gpurun_out/ab_run.log >> $OUT <<'PY'
 import json, sys
 line = [l for l in open(sys.argv[2]) if l.startswith('{')][-1]
 d = json.loads(line)
-print(sys.argv[1], '%.4f ms' % d['ms_per_step'], '%.3f G ops/s' % (d['value'] / 1e9))
+print(sys.argv[1], '%.4f ms' % d['ms_per_step'],
+      '%.3f G ops/s' % (d['value'] / 1e9))
 PY
   done
 done

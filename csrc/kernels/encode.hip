@@ -415,14 +415,14 @@ ZK_DEV void stage_out(const uint32_t* lw, int64_t a0, int64_t B0, int64_t B1,
 template <class F>
 ZK_DEV void staged_emit(int64_t r0, int64_t r1, const int64_t* off,
                         const int64_t* sizes, uint8_t* __restrict__ out,
-                        uint32_t* lw, F emit) {
+                        uint32_t* lw, F emit, int64_t stage = STAGE_BYTES) {
   int64_t rs = r0;
   while (rs < r1) {                              // block-uniform
     const int64_t B0 = off[rs - r0];
     const int64_t a0 = B0 & ~(int64_t)15;
     const int64_t i = rs + threadIdx.x;
     const bool fits = i < r1 &&
-                      off[i - r0] + sizes[i - r0] - a0 + 16 <= STAGE_BYTES;
+                      off[i - r0] + sizes[i - r0] - a0 + 16 <= stage;
     const int k = __syncthreads_count(fits);
     if (k == 0) {
       if (threadIdx.x == 0) {
@@ -465,7 +465,7 @@ __global__ __launch_bounds__(ENC_T) void resp_write(
     int64_t ncap, const int64_t* __restrict__ sizes,
     const int64_t* __restrict__ bbase, int64_t* __restrict__ rec_off,
     const int64_t* __restrict__ total, uint8_t* __restrict__ out, int64_t cap,
-    int32_t* __restrict__ err, int32_t term) {
+    int32_t* __restrict__ err, int32_t term, int64_t stage) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lw[];
   __shared__ EncLocal E;
   const int64_t n = min(*n_dev, ncap);
@@ -479,7 +479,7 @@ __global__ __launch_bounds__(ENC_T) void resp_write(
   block_offsets(r0, r1, sizes, bbase, rec_off, E);
   staged_emit(r0, r1, E.off, E.sz, out, lw, [&](auto& k, int64_t i) {
     emit_response(k, r, s, i, E.sz[i - r0] - 4);
-  });
+  }, stage);
 }
 
 // ---------------------------------------------------------------- K10 write
@@ -723,9 +723,19 @@ int zk_encode_responses2(const ZkRespBatch* r, const ZkNodeStore* s,
   }
   int rc = zk_scan_small_i64(bsum, bbase, nb, total, st);
   if (rc) return rc;
-  zk::resp_write<<<nb, zk::ENC_T, zk::STAGE_BYTES, st>>>(
+  // reply image per workgroup (ZKMI_RESP_STAGE_KB, 8..56; A/B): larger
+  // images stage longer runs of big replies, smaller ones keep more
+  // workgroups per CU
+  static int64_t stage = -1;
+  if (stage < 0) {
+    const char* e = getenv("ZKMI_RESP_STAGE_KB");
+    int kb = e ? atoi(e) : (int)(zk::STAGE_BYTES / 1024);
+    if (kb < 8 || kb > 56) kb = (int)(zk::STAGE_BYTES / 1024);
+    stage = (int64_t)kb * 1024;
+  }
+  zk::resp_write<<<nb, zk::ENC_T, (size_t)stage, st>>>(
       *r, *s, n_dev, ncap, sizes, bbase, rec_off, total, out, out_cap, err,
-      terminate);
+      terminate, stage);
   ZK_LAUNCH_CHECK();
   return 0;
 }

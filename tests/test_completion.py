@@ -172,3 +172,69 @@ def test_close_with_routed_requests_in_flight(zk):
     # connection error, never both and never neither
     assert len(got) == n
     assert all(e is not None for e in got)
+
+
+def test_direct_requests_from_many_threads(zkc):
+    """call_sync from several threads at once sends from each caller's
+    thread (request_direct) while the loop thread issues its own requests:
+    every xid stays unique and every reply reaches its caller."""
+    conn = _conn(zkc)
+    zkc.call_sync('create', '/t', b'', {})
+    for k in range(8):
+        zkc.call_sync('create', '/t/%d' % k, b'v%d' % k, {})
+    errors = []
+    loop_done = threading.Event()
+    got = []
+
+    def loop_side():
+        def cb(err, data=None, stat=None):
+            got.append((err, data))
+            if len(got) == 400:
+                loop_done.set()
+        for i in range(400):
+            zkc.get('/t/%d' % (i % 8), cb)
+
+    def worker(k):
+        try:
+            for i in range(200):
+                data, stat = zkc.call_sync('get', '/t/%d' % k)
+                assert data == b'v%d' % k
+            try:
+                zkc.call_sync('get', '/t/missing%d' % k)
+                errors.append('no error for a missing node')
+            except ZKError as e:
+                assert e.code == 'NO_NODE'
+        except Exception as e:          # reported below
+            errors.append(repr(e))
+    ths = [threading.Thread(target=worker, args=(k,)) for k in range(8)]
+    zkc.loop.call_soon(loop_side)
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join(60)
+    assert loop_done.wait(20)
+    assert not errors, errors
+    assert all(e is None and d is not None and d.startswith(b'v')
+               for e, d in got)
+    assert zkc.loop.run(lambda: (len(conn.reqs), len(conn.xid_map))) == (0, 0)
+
+
+def test_direct_falls_back_when_router_off(zkc):
+    """With the router off (a paused socket) a blocking call hops to the
+    loop thread as before and still completes once reading resumes."""
+    conn = _conn(zkc)
+    sock = conn.socket
+    zkc.loop.run(sock.pause_reading)
+    res = Box()
+
+    def call():
+        try:
+            res(zkc.call_sync('create', '/fb', b'x', {}, timeout=10))
+        except Exception as e:          # reported by the assert below
+            res(e)
+    th = threading.Thread(target=call)
+    th.start()
+    assert not res.ev.wait(0.3)
+    zkc.loop.run(sock.resume_reading)
+    th.join(10)
+    assert res.wait(10)[0] == '/fb'

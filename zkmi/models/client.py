@@ -35,6 +35,9 @@ from .connection_set import ConnectionSet, StaticResolver
 # box the blocking get() RTT went 37-44 -> 20 us (tools/gpu_r3k.sh; a
 # 30 us window is shorter than the round trip and does nothing); off on
 # small hosts, where the poller competes with the loop thread for the GIL.
+# ZKMI_DIRECT=0: requests made off the loop thread always hop to it first
+# (ZKConnectionFSM.request_direct is the default when the router is on)
+_DIRECT = os.environ.get('ZKMI_DIRECT', '1') != '0'
 _SYNC_SPIN_S = float(os.environ.get(
     'ZKMI_SYNC_SPIN_US',
     '100' if (os.cpu_count() or 1) >= 16 else '0')) / 1e6
@@ -350,8 +353,18 @@ class Client(FSM):
     def _request(self, pkt, cb, on_reply):
         if self.loop.in_loop():
             self._issue(pkt, cb, on_reply)
-        else:
-            self.loop.call_soon(self._issue, pkt, cb, on_reply)
+            return
+        if _DIRECT:
+            # another thread: send from here when the live connection's
+            # native router will settle the reply (request_direct)
+            sess = self.session
+            conn = sess.conn if sess is not None and \
+                self._fsm_state == 'normal' and \
+                sess._fsm_state == 'attached' else None
+            if conn is not None and conn.request_direct(
+                    pkt, on_reply, lambda err, *_: cb(err)):
+                return
+        self.loop.call_soon(self._issue, pkt, cb, on_reply)
 
     def _issue(self, pkt, cb, on_reply):
         # currentConnection() with the state checks inlined: this runs once

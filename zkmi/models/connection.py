@@ -16,6 +16,7 @@ ZooKeeper replies are not self-describing (SURVEY §7.4 hard part 1).
 """
 
 import os
+import threading
 import time
 
 from .. import consts
@@ -75,6 +76,8 @@ class ZKConnectionFSM(FSM):
         self.gpu = None
         self.xid_map = {}
         self.xid = 0
+        # xids are also taken off the loop thread (request_direct)
+        self.xid_lock = threading.Lock()
         self.bulks = []                 # in-flight BulkBatch (models/bulk.py)
         # bulk watch notifications (Client.watch_bulk): kept by the native
         # transport (note sink), or here on the asyncio loop
@@ -112,8 +115,9 @@ class ZKConnectionFSM(FSM):
         self.emit('destroyAsserted')
 
     def nextXid(self):
-        x = self.xid
-        self.xid = (self.xid + 1) & 0x7fffffff
+        with self.xid_lock:
+            x = self.xid
+            self.xid = (x + 1) & 0x7fffffff
         return x
 
     # -- inbound plumbing -----------------------------------------------------
@@ -468,8 +472,9 @@ class ZKConnectionFSM(FSM):
         if not self.isInState('connected'):
             raise Exception('Client must be connected to send requests')
         req = ZKRequest(pkt)
-        xid = self.xid
-        self.xid = (xid + 1) & 0x7fffffff
+        with self.xid_lock:
+            xid = self.xid
+            self.xid = (xid + 1) & 0x7fffffff
         pkt['xid'] = xid
         if self.routing and pkt['opcode'] != 'SET_WATCHES' and \
                 self.socket.transport.request(pkt, req):
@@ -481,6 +486,38 @@ class ZKConnectionFSM(FSM):
                        'sent request to server')
         self.socket.write(self.encoder.request(pkt))
         return req
+
+    def request_direct(self, pkt, on_reply, on_error):
+        """:meth:`request` from a thread other than the loop's (the
+        blocking helpers): the request is encoded and sent from the calling
+        thread, the reply settled by the native router on the loop thread —
+        one cross-thread hand-off instead of two.  The (reply, error) pair is
+        attached before the request leaves, so a reply cannot beat it.
+        Returns False (nothing sent) when the router is not on; the caller
+        then goes through the loop."""
+        if not self.routing or self._fsm_state != 'connected' or \
+                pkt['opcode'] == 'SET_WATCHES':
+            return False
+        sock = self.socket
+        t = sock.transport if sock is not None else None
+        if t is None:
+            return False
+        req = ZKRequest(pkt)
+        req.fast = (on_reply, on_error)
+        with self.xid_lock:
+            xid = self.xid
+            self.xid = (xid + 1) & 0x7fffffff
+        pkt['xid'] = xid
+        r = t.request(pkt, req)
+        if r is None:
+            return False        # router went off meanwhile (xid skipped)
+        if not r:
+            # the transport is closing: the request fails as the loop
+            # path's would once the connection reports the loss
+            self.fsm_loop.call_soon(
+                on_error, ZKProtocolError('CONNECTION_LOSS',
+                                          'Connection closed.'))
+        return True
 
     # -- bulk watch notifications (Client.watch_bulk) ------------------------
 
@@ -531,10 +568,11 @@ class ZKConnectionFSM(FSM):
             # nothing to send: no xids, no encode, an empty result
             self.fsm_loop.call_soon(lambda: cb(None, batch.finish()))
             return
-        x0 = self.xid
-        if x0 + n > 0x7fffffff:
-            x0 = 0
-        self.xid = (x0 + n) & 0x7fffffff
+        with self.xid_lock:
+            x0 = self.xid
+            if x0 + n > 0x7fffffff:
+                x0 = 0
+            self.xid = (x0 + n) & 0x7fffffff
         wire = batch.encode(x0)
         self.bulks.append(batch)
         if batch.device is not None and self.socket.can_capture() and \

@@ -732,8 +732,10 @@ def run_rank(a):
                                world > 1 else 'dp%d' % world,
             },
             'get_mode': ('sharded: one tree, path-hash shards over %d '
-                         'ranks, reads routed with all_to_all over '
-                         'RCCL/xGMI' % world if world > 1 else
+                         'ranks, reads routed with all_to_all over %s' % (
+                             world, 'RCCL/xGMI' if backend == 'nccl' else
+                             '%s (rehearsal, ranks may share a GPU)'
+                             % backend) if world > 1 else
                          'one shard (nothing to route), local pipeline')
                         if sharded else
                         ('replica per rank' if a.workload == 'get' else None),

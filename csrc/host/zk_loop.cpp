@@ -216,6 +216,7 @@ struct Router {
   PyObject* reqs = nullptr;
   PyObject* xmap = nullptr;
   PyObject* on_other = nullptr;
+  PyObject* on_note = nullptr;   // NOTIFICATION frames, decoded (optional)
   DecodeFn decode = nullptr;
   EncodeFn encode = nullptr;     // Transport.request (optional)
   int64_t max_zxid = 0;
@@ -226,7 +227,8 @@ struct Router {
 // One unit of an inbound read, in stream order: bytes for Python, or a
 // routed (request, reply) pair.
 struct RxItem {
-  PyObject* req;             // nullptr: `bytes` holds frames for Python
+  PyObject* req;             // nullptr: `bytes` holds frames for Python,
+                             // or (with pkt) a decoded notification
   PyObject* pkt;
   int32_t err;
   std::string bytes;
@@ -442,6 +444,7 @@ void Transport_dealloc(Transport* t) {
   Py_XDECREF(t->rt->reqs);
   Py_XDECREF(t->rt->xmap);
   Py_XDECREF(t->rt->on_other);
+  Py_XDECREF(t->rt->on_note);
   delete t->rt;
   Py_XDECREF(t->protocol);
   Py_XDECREF(t->on_fail);
@@ -710,6 +713,26 @@ void deliver(Transport* t, const char* p, size_t n) {
     } else if (ns.on && fl >= 16 && xid == -1) {
       ns.buf.append(s + i, 4 + (size_t)fl);
       ++nn;
+    } else if (rt.on && rt.on_note != nullptr && fl >= 16 && xid == -1) {
+      // a watch event: decoded here, handed to on_note in stream order
+      PyObject* pkt = rt.decode((const uint8_t*)s + i + 4, fl, rt.xmap);
+      if (pkt == nullptr) {
+        PyErr_Clear();                 // Python's path reports it
+        pass.append(s + i, 4 + (size_t)fl);
+      } else {
+        if (!pass.empty()) {
+          RxItem b;
+          b.req = b.pkt = nullptr;
+          b.err = 0;
+          b.bytes.swap(pass);
+          items.push_back(std::move(b));
+        }
+        RxItem nt;
+        nt.req = nullptr;
+        nt.pkt = pkt;
+        nt.err = 0;
+        items.push_back(std::move(nt));
+      }
     } else if (rt.on && fl >= 16 && xid >= 0) {
       RxItem one;
       one.req = one.pkt = nullptr;
@@ -740,7 +763,17 @@ void deliver(Transport* t, const char* p, size_t n) {
   ++t->dispatching;
   for (size_t j = 0; j < items.size(); ++j) {
     RxItem& it = items[j];
-    if (it.req == nullptr) {
+    if (it.req == nullptr && it.pkt != nullptr) {
+      PyObject* cb = rt.on_note;
+      if (cb != nullptr && !t->closed) {
+        Py_INCREF(cb);
+        PyObject* r = PyObject_CallOneArg(cb, it.pkt);
+        if (r == nullptr) report_exception(t->w.loop);
+        Py_XDECREF(r);
+        Py_DECREF(cb);
+      }
+      Py_CLEAR(it.pkt);
+    } else if (it.req == nullptr) {
       deliver_raw(t, it.bytes.data(), it.bytes.size());
     } else {
       settle_routed(t, it);
@@ -965,8 +998,9 @@ PyObject* Transport_note_sink(Transport* t, PyObject* args) {
   Py_RETURN_NONE;
 }
 
-// route(on, reqs, xid_map, on_other, decoder, max_packet, prefix): see
-// Router.  `decoder` is the host codec's `_C_decode_reply` capsule;
+// route(on, reqs, xid_map, on_other, decoder, max_packet, prefix
+//       [, encoder, on_note]): see Router; on_note(pkt) takes the decoded
+// NOTIFICATION frames (without it they go to Python as bytes).  `decoder` is the host codec's `_C_decode_reply` capsule;
 // `prefix` = a partial frame the caller's framer holds, parsed first.
 // Turning it off hands a partial frame the native framer holds back to
 // Python (after the read being dispatched, when called from a callback).
@@ -974,10 +1008,11 @@ PyObject* Transport_route(Transport* t, PyObject* args) {
   int on;
   PyObject *reqs, *xmap, *other, *cap;
   PyObject* ecap = Py_None;
+  PyObject* note = Py_None;
   long long maxp;
   Py_buffer pre;
-  if (!PyArg_ParseTuple(args, "pOOOOLy*|O", &on, &reqs, &xmap, &other, &cap,
-                        &maxp, &pre, &ecap))
+  if (!PyArg_ParseTuple(args, "pOOOOLy*|OO", &on, &reqs, &xmap, &other, &cap,
+                        &maxp, &pre, &ecap, &note))
     return nullptr;
   std::string head((const char*)pre.buf, (size_t)pre.len);
   PyBuffer_Release(&pre);
@@ -1013,6 +1048,12 @@ PyObject* Transport_route(Transport* t, PyObject* args) {
   Py_XSETREF(rt.xmap, xmap);
   Py_INCREF(other);
   Py_XSETREF(rt.on_other, other);
+  if (note != Py_None && PyCallable_Check(note)) {
+    Py_INCREF(note);
+    Py_XSETREF(rt.on_note, note);
+  } else {
+    Py_CLEAR(rt.on_note);
+  }
   rt.decode = (DecodeFn)fn;
   rt.encode = (EncodeFn)efn;
   rt.max_packet = maxp;

@@ -118,12 +118,18 @@ def test_notification_order_around_routed_replies(zk, zkc):
         zkc.set('/w', b'1', -1, lambda err, *a: order.append(('set', err)))
         zkc.get('/w', lambda err, d=None, s=None: (order.append(('get', d)),
                                                      done.set()))
+    conn = _conn(zkc)
+    framed0 = zkc.loop.run(lambda: conn.decoder.frames_in)
     zkc.loop.call_soon(go)
     assert done.wait(10)
     assert wait_for(lambda: ('data', b'1') in order, 10)
     i_set = order.index(('set', None))
     i_get = order.index(('get', b'1'))
     assert i_set < i_get
+    # the notification and the replies (the watcher's re-arm included,
+    # four frames at least) were framed and decoded natively: Python's
+    # framer saw at most a ping reply (xid -2) that landed in between
+    assert zkc.loop.run(lambda: conn.decoder.frames_in) - framed0 <= 1
 
 
 def test_large_reply_split_across_reads(zkc):

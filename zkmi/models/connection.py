@@ -425,7 +425,9 @@ class ZKConnectionFSM(FSM):
                              self._routed_other, codec.DECODE_REPLY_C,
                              self.config.max_packet,
                              self.decoder.take_pending(),
-                             codec.ENCODE_REQUEST_C)
+                             codec.ENCODE_REQUEST_C,
+                             self._routed_note if self.notes is None
+                             else None)
         self.routing = True
 
     def route_state(self):
@@ -435,6 +437,11 @@ class ZKConnectionFSM(FSM):
             return 0, 0.0
         z, rx, _ = sock.transport.route_state()
         return z, rx
+
+    def _routed_note(self, pkt):
+        """A NOTIFICATION the router decoded: to the session, as on_rx
+        hands it over (lib/zk-session.js:227-238)."""
+        self.emit('packet', pkt)
 
     def _routed_other(self, req, pkt):
         """A routed reply the transport does not hand straight to the

@@ -1000,8 +1000,10 @@ PyObject* Transport_note_sink(Transport* t, PyObject* args) {
 
 // route(on, reqs, xid_map, on_other, decoder, max_packet, prefix
 //       [, encoder, on_note]): see Router; on_note(pkt) takes the decoded
-// NOTIFICATION frames (without it they go to Python as bytes).  `decoder` is the host codec's `_C_decode_reply` capsule;
-// `prefix` = a partial frame the caller's framer holds, parsed first.
+// NOTIFICATION frames (without it they go to Python as bytes).  `decoder`
+// is the host codec's `_C_decode_reply` capsule (`encoder`: its
+// `_C_encode_request`, for Transport.request); `prefix` = a partial frame
+// the caller's framer holds, parsed first.
 // Turning it off hands a partial frame the native framer holds back to
 // Python (after the read being dispatched, when called from a callback).
 PyObject* Transport_route(Transport* t, PyObject* args) {

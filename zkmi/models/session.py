@@ -74,10 +74,18 @@ class ExpiryTimer(EventEmitter):
             self._h = None
 
 
+_CAMEL = {}
+
+
 def _camel(evt_type):
-    """``DATA_CHANGED`` -> ``dataChanged`` (``zk-session.js:401``)."""
-    return re.sub(r'_[a-z]', lambda m: m.group(0)[1].upper(),
-                  evt_type.lower())
+    """``DATA_CHANGED`` -> ``dataChanged`` (``zk-session.js:401``);
+    memoised (one lookup per notification)."""
+    c = _CAMEL.get(evt_type)
+    if c is None:
+        c = _CAMEL[evt_type] = re.sub(r'_[a-z]',
+                                      lambda m: m.group(0)[1].upper(),
+                                      evt_type.lower())
+    return c
 
 
 class ZKSession(FSM):

@@ -744,9 +744,10 @@ def run_rank(a):
             'replica_ms_per_step': replica['ms_per_step'] if replica else None,
             'p50_get_rtt_us': rtt50,
             'p99_get_rtt_us': rtt99,
-            'rtt_note': 'one blocking Client.get over loopback TCP to the '
-                        'native server (zk_fastserver); *_fakezk: to the '
-                        'Python fake server',
+            'rtt_note': 'one blocking Client.call_sync(get) over loopback '
+                        'TCP to the native server (zk_fastserver), sent '
+                        'from the calling thread and settled by the native '
+                        'reply router; *_fakezk: to the Python fake server',
             'p50_get_rtt_us_evloop': ev50,
             'p99_get_rtt_us_evloop': ev99,
             'rtt_evloop_note': 'get(path, cb) chained on the client event '

@@ -24,7 +24,8 @@ def main():
     import torch
     dev = torch.device('cuda', 0)
     try:
-        one = bench.measure_bulk_tcp(srv.port, a.nodes, a.batch, a.iters, dev, 1)
+        one = bench.measure_bulk_tcp(srv.port, a.nodes, a.batch, a.iters,
+                                     dev, 1)
         k = bench.measure_bulk_tcp(srv.port, a.nodes, a.batch, a.iters, dev, 8)
     finally:
         srv.shutdown()

@@ -188,12 +188,51 @@ enum { CAP_DONE = 0, CAP_FULL = 1, CAP_BAD = 2, CAP_CANCEL = 3 };
 // node-wide watch fan-out (zkmi/parallel/fanout.py) takes them in bulk
 // (take_notes) and forwards the raw bytes.  Other frames go on to Python
 // whole.  All access holds the GIL (the loop thread calls into Python).
+// With `watchers` (the session's dict path -> ZKWatcher) non-empty, an
+// event on a watcher()'s path goes on to Python as well (the session's
+// watchers must keep firing) and stays in the sink only when its path is
+// also in `bulk` (the session's bulk watch set).
 struct NoteSink {
   bool on = false;
   int64_t max_packet = 0;
   std::string buf;
   int64_t frames = 0;
+  PyObject* watchers = nullptr;
+  PyObject* bulk = nullptr;
 };
+
+int32_t be32(const char* p);
+
+// Sink a NOTIFICATION frame (body b, fl bytes): keeps it when it belongs to
+// the sink; returns true when Python should also get it (see NoteSink).
+bool note_take(NoteSink& ns, const char* frame, int32_t fl) {
+  bool keep = true, to_py = false;
+  if (ns.watchers != nullptr && PyDict_GET_SIZE(ns.watchers) > 0 &&
+      fl >= 16 + 12) {
+    // body: xid i32, zxid i64, err i32, type i32, state i32, path ustring
+    const char* b = frame + 4;
+    const int32_t pl = be32(b + 24);
+    if (pl >= 0 && 28 + (int64_t)pl <= fl) {
+      PyObject* key = PyUnicode_DecodeUTF8(b + 28, pl, "replace");
+      if (key == nullptr) {
+        PyErr_Clear();
+      } else {
+        const int w = PyDict_Contains(ns.watchers, key);
+        if (w > 0) {
+          to_py = true;
+          keep = ns.bulk != nullptr && PySet_Contains(ns.bulk, key) > 0;
+        }
+        PyErr_Clear();
+        Py_DECREF(key);
+      }
+    }
+  }
+  if (keep) {
+    ns.buf.append(frame, 4 + (size_t)fl);
+    ++ns.frames;
+  }
+  return to_py;
+}
 
 // Reply router (Transport.route): the completion path of the interactive
 // API.  While on, the read path frames the inbound stream itself and, for
@@ -440,6 +479,8 @@ void Transport_dealloc(Transport* t) {
   delete t->wbuf;
   Py_XDECREF(t->cap->done);
   delete t->cap;
+  Py_XDECREF(t->ns->watchers);
+  Py_XDECREF(t->ns->bulk);
   delete t->ns;
   Py_XDECREF(t->rt->reqs);
   Py_XDECREF(t->rt->xmap);
@@ -684,7 +725,6 @@ void deliver(Transport* t, const char* p, size_t n) {
   }
   std::vector<RxItem> items;      // in stream order
   std::string pass;               // frames for Python since the last item
-  int64_t nn = 0;
   size_t i = 0;
   int status = -1;
   const int64_t maxp = c.on ? c.max_packet
@@ -710,9 +750,8 @@ void deliver(Transport* t, const char* p, size_t n) {
       c.last_off = c.len;
       c.len += 4 + (size_t)fl;
       ++c.got;
-    } else if (ns.on && fl >= 16 && xid == -1) {
-      ns.buf.append(s + i, 4 + (size_t)fl);
-      ++nn;
+    } else if (ns.on && fl >= 16 && xid == -1 && !note_take(ns, s + i, fl)) {
+      // kept by the sink only
     } else if (rt.on && rt.on_note != nullptr && fl >= 16 && xid == -1) {
       // a watch event: decoded here, handed to on_note in stream order
       PyObject* pkt = rt.decode((const uint8_t*)s + i + 4, fl, rt.xmap);
@@ -753,7 +792,6 @@ void deliver(Transport* t, const char* p, size_t n) {
     }
     i += 4 + (size_t)fl;
   }
-  ns.frames += nn;
   if (rt.on && i > 0) rt.last_rx = mono_ms();
   if (status < 0 && c.on && c.got >= c.n) status = CAP_DONE;
   c.carry.assign(s + i, len - i);
@@ -975,8 +1013,22 @@ PyObject* Transport_note_sink(Transport* t, PyObject* args) {
   int on;
   long long maxp;
   Py_buffer pre;
-  if (!PyArg_ParseTuple(args, "pLy*", &on, &maxp, &pre)) return nullptr;
+  PyObject *watchers = Py_None, *bulk = Py_None;
+  if (!PyArg_ParseTuple(args, "pLy*|OO", &on, &maxp, &pre, &watchers, &bulk))
+    return nullptr;
   NoteSink& ns = *t->ns;
+  if (watchers != Py_None && !PyDict_Check(watchers)) {
+    PyBuffer_Release(&pre);
+    PyErr_SetString(PyExc_TypeError, "note_sink: watchers must be a dict");
+    return nullptr;
+  }
+  if (bulk != Py_None && !PyAnySet_Check(bulk)) {
+    PyBuffer_Release(&pre);
+    PyErr_SetString(PyExc_TypeError, "note_sink: bulk must be a set");
+    return nullptr;
+  }
+  Py_XSETREF(ns.watchers, watchers == Py_None ? nullptr : Py_NewRef(watchers));
+  Py_XSETREF(ns.bulk, bulk == Py_None ? nullptr : Py_NewRef(bulk));
   std::string head((const char*)pre.buf, (size_t)pre.len);
   PyBuffer_Release(&pre);
   if (on) {
@@ -1090,7 +1142,15 @@ PyObject* Transport_request(Transport* t, PyObject* args) {
   if (PyDict_SetItem(rt.reqs, xo, req) != 0 ||
       PyDict_SetItem(rt.xmap, xo, op) != 0)
     return nullptr;
-  return queue_write(t);
+  PyObject* r = queue_write(t);
+  if (r == Py_False) {
+    // the send failed and the transport is closing: the caller fails this
+    // request itself (False), so it must not stay registered — the closed
+    // connection would fail it a second time
+    if (PyDict_DelItem(rt.reqs, xo) != 0) PyErr_Clear();
+    if (PyDict_DelItem(rt.xmap, xo) != 0) PyErr_Clear();
+  }
+  return r;
 }
 
 // route_state() -> (max_zxid, last_rx_ms, routed): what the router saw.

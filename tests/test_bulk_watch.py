@@ -170,3 +170,45 @@ def test_bulk_watch_notes_and_failover_replay(kind, monkeypatch):
         finally:
             lp.stop()
             srv.shutdown()
+
+
+@pytest.mark.skipif(not fast.available(), reason='zk_fastserver not built')
+@pytest.mark.parametrize('kind', _loops())
+def test_watchers_keep_firing_with_bulk_watches(kind, monkeypatch):
+    """With the note sink on, events for a watcher()'s path still reach the
+    watcher (and stay out of the sink unless the path is also a bulk
+    watch); bulk paths go to the sink only (the sink swallowed
+    every notification of the connection)."""
+    monkeypatch.setenv('ZKMI_LOOP', kind)
+    srv = fast.FastZKServer(members=1)
+    lp = L.new_loop('bulk-watch-mixed-' + kind)
+    c = Client({'servers': [{'address': '127.0.0.1', 'port': srv.ports[0]}],
+                'sessionTimeout': 8000, 'device': False, 'loop': lp})
+    try:
+        c.wait_connected(20)
+        c.call_sync('create', '/mx', b'', {})
+        for p in ('/mx/w', '/mx/b', '/mx/both'):
+            c.call_sync('create', p, b'0', {})
+        seen = {'/mx/w': [], '/mx/both': []}
+        for p in seen:
+            c.watcher(p).on('dataChanged',
+                            lambda d, s, p=p: seen[p].append(d))
+        _wait(lambda: all(v == [b'0'] for v in seen.values()), 'arming')
+        c.watch_bulk(['/mx/b', '/mx/both'])
+        _bulk(c.bulk_get, ['/mx/b', '/mx/both'], watch=True)
+        notes = _Notes(c)
+        for p in ('/mx/w', '/mx/b', '/mx/both'):
+            c.call_sync('set', p, b'1', -1)
+        # the sink: the bulk paths only
+        assert sorted(notes.until(2)) == ['/mx/b', '/mx/both']
+        # the watchers: fired and re-armed with the new data
+        _wait(lambda: seen['/mx/w'][-1:] == [b'1'], 'the watcher event')
+        _wait(lambda: seen['/mx/both'][-1:] == [b'1'], 'the shared event')
+        raw, k = c.take_notes()
+        assert k == 0
+    finally:
+        try:
+            c.close_sync(10)
+        finally:
+            lp.stop()
+            srv.shutdown()

@@ -244,3 +244,73 @@ def test_direct_falls_back_when_router_off(zkc):
     zkc.loop.run(sock.resume_reading)
     th.join(10)
     assert res.wait(10)[0] == '/fb'
+
+
+@pytest.fixture
+def pzkc(zk):
+    """A client on a loop of its own: holding its loop thread (the tests
+    below do, to order events) leaves the fake server's loop running."""
+    from zkmi.runtime import loop as L
+    lp = L.new_loop('completion-private')
+    c = client(zk.servers(), loop=lp)
+    c.wait_connected(10)
+    yield c
+    try:
+        c.close_sync(10)
+    finally:
+        lp.stop()
+
+
+def test_failed_direct_send_settles_once(pzkc):
+    """A direct send that fails (the socket is already shut for writing)
+    settles its request exactly once: the transport unregisters it, so the
+    connection's later failure does not fail it a second time (ADVICE r3:
+    a second callback released call_sync's lock twice and aborted the
+    connection's cleanup)."""
+    import os
+    import socket
+    conn = _conn(pzkc)
+    fd = pzkc.loop.run(lambda: conn.socket.transport.get_extra_info('fd'))
+    gate = threading.Event()
+    pzkc.loop.call_soon(gate.wait, 10)          # hold the loop thread
+    s = socket.socket(fileno=os.dup(fd))    # closing the dup leaves fd
+    try:
+        s.shutdown(socket.SHUT_WR)
+    finally:
+        s.close()
+    calls = []
+    pzkc.get('/nope', lambda err, *a: calls.append(err))   # sent directly
+    gate.set()
+    assert wait_for(lambda: len(calls) >= 1, 10)
+    import time
+    time.sleep(0.5)             # the connection's failure has run by now
+    assert len(calls) == 1, calls
+    assert calls[0] is not None and calls[0].code == 'CONNECTION_LOSS'
+
+
+def test_direct_send_keeps_fifo_behind_queued_submissions(pzkc):
+    """A request sent from a thread must not overtake that thread's earlier
+    submissions still queued for the loop: a bulk_set queued
+    while the loop is busy, then a blocking get from the same thread, must
+    read the value the bulk_set wrote."""
+    pzkc.call_sync('create', '/fifo', b'old', {})
+    # a first bulk batch pays the bulk path's imports and setup (seconds
+    # under the sanitizers) before the loop is held
+    pzkc.call_sync('bulk_set', ['/fifo'], b'old')
+    gate = threading.Event()
+    pzkc.loop.call_soon(gate.wait, 10)          # the loop is busy
+    res = Box()
+    pzkc.bulk_set(['/fifo'], b'new', lambda err, r=None: res(err))
+    assert pzkc._hops >= 1
+    got = Box()
+
+    def reader():
+        got(pzkc.call_sync('get', '/fifo')[0])
+    th = threading.Thread(target=reader)
+    th.start()
+    import time
+    time.sleep(0.2)
+    gate.set()
+    th.join(10)
+    assert res.wait(10)[0] is None
+    assert got.wait(10)[0] == b'new'

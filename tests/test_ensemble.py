@@ -63,6 +63,8 @@ def _run(world, steps):
         msgs = []
         while not errq.empty():
             msgs.append('rank %d:\n%s' % errq.get())
+        while not outq.empty():
+            msgs.append('rank %d finished: %r' % (outq.get()[0],))
         raise AssertionError('\n'.join(msgs) or 'worker failed')
     res = {}
     while not outq.empty():
@@ -75,15 +77,19 @@ def _run(world, steps):
 def test_ensemble_failover_replay_fanout(world):
     steps = 4                               # failovers at steps 1 and 3
     res = _run(world, steps)
-    assert sorted(res) == list(range(world))
+    assert sorted(res) == list(range(world)), res
+    # on any failure, every rank's (bad, got, failovers, rearmed, replayed,
+    # fan-out stats) goes into the message
+    report = {r: dict(zip(('bad', 'got', 'fo', 'rearmed', 'replayed',
+                           'stats'), v)) for r, v in res.items()}
     rearmed = 0
     for rank, (bad, got, fo, rea, replayed, st) in res.items():
         # every event (initial arm, live, replayed) exactly once per rank
-        assert bad is None, (rank, bad)
-        assert got == [12] * steps, (rank, got)
-        assert fo == 2 and replayed == 24
+        assert bad is None, (rank, report)
+        assert got == [12] * steps, (rank, report)
+        assert fo == 2 and replayed == 24, (rank, report)
         # a notification + its re-arm reply per event
-        assert st['decoded_host'] == 2 * (48 + 12 * steps)
+        assert st['decoded_host'] == 2 * (48 + 12 * steps), (rank, report)
         rearmed += rea
     # the killed members' sessions resumed their watches (SET_WATCHES)
     assert rearmed > 0

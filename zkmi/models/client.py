@@ -130,6 +130,9 @@ class Client(FSM):
             else st
         self.config = o.get('config') or ClientConfig()
         self.loop = o.get('loop') or default_loop()
+        # submissions from other threads still queued for the loop (_hop)
+        self._hop_lock = threading.Lock()
+        self._hops = 0
         self.tracer = o.get('tracer')
         # bulk codec device: None = the current GPU if any, False = host
         self.bulk_device = o.get('device')
@@ -341,11 +344,28 @@ class Client(FSM):
 
     # -- data API ------------------------------------------------------------
 
-    def _dispatch(self, fn):
+    def _dispatch(self, fn, *args):
         if self.loop.in_loop():
-            fn()
+            fn(*args)
         else:
-            self.loop.call_soon(fn)
+            self._hop(fn, *args)
+
+    def _hop(self, fn, *args):
+        """Run ``fn(*args)`` on the loop thread, counted as a pending
+        submission: while one is queued, requests from other threads do not
+        go out directly (:meth:`_request`), so a later request never
+        overtakes an earlier one from the same thread on the wire (a
+        session's requests are FIFO, as on the reference's single loop)."""
+        with self._hop_lock:
+            self._hops += 1
+
+        def run():
+            try:
+                fn(*args)
+            finally:
+                with self._hop_lock:
+                    self._hops -= 1
+        self.loop.call_soon(run)
 
     def _not_connected(self, cb):
         self.loop.call_soon(cb, ZKNotConnectedError())
@@ -354,9 +374,10 @@ class Client(FSM):
         if self.loop.in_loop():
             self._issue(pkt, cb, on_reply)
             return
-        if _DIRECT:
+        if _DIRECT and self._hops == 0:
             # another thread: send from here when the live connection's
-            # native router will settle the reply (request_direct)
+            # native router will settle the reply (request_direct) and no
+            # earlier submission is still waiting for the loop
             sess = self.session
             conn = sess.conn if sess is not None and \
                 self._fsm_state == 'normal' and \
@@ -364,7 +385,7 @@ class Client(FSM):
             if conn is not None and conn.request_direct(
                     pkt, on_reply, lambda err, *_: cb(err)):
                 return
-        self.loop.call_soon(self._issue, pkt, cb, on_reply)
+        self._hop(self._issue, pkt, cb, on_reply)
 
     def _issue(self, pkt, cb, on_reply):
         # currentConnection() with the state checks inlined: this runs once
@@ -669,6 +690,8 @@ class Client(FSM):
         box = {}
 
         def cb(err=None, *res):
+            if 'err' in box:
+                return          # settled already (one callback per call)
             box['err'] = err
             box['res'] = res
             done.release()

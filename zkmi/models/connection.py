@@ -84,6 +84,7 @@ class ZKConnectionFSM(FSM):
         self.note_native = False
         self.notes = None
         self.notes_left = (b'', 0)
+        self.note_sess = None       # whose watchers the note sink spares
         self.bulk_frames_py = 0         # bulk replies routed one by one
         self.routing = False            # native reply router on (_route)
         self.reqs = {}
@@ -258,11 +259,8 @@ class ZKConnectionFSM(FSM):
                 if xid >= 0 and self._bulk_rx(xid, body):
                     return
             if self.notes is not None and len(body) >= 16 and \
-                    body[0:4] == b'\xff\xff\xff\xff':
-                # bulk watch notification (no native note sink)
-                self.notes += len(body).to_bytes(4, 'big')
-                self.notes += body
-                self.notes_n += 1
+                    body[0:4] == b'\xff\xff\xff\xff' and \
+                    not self._note_keep(body):
                 return
             try:
                 pkt = self._decode_reply(body)
@@ -536,14 +534,37 @@ class ZKConnectionFSM(FSM):
         if self.note_native or self.notes is not None:
             return
         sock = self.socket
+        sess = self.session or self.client.getSession()
+        self.note_sess = sess
         if sock is not None and sock.can_sink_notes():
             pre = self.decoder.take_pending() if self.decoder else b''
-            sock.note_sink(True, self.config.max_packet, pre)
+            sock.note_sink(True, self.config.max_packet, pre,
+                           sess.watchers if sess is not None else None,
+                           sess.bulk_watches if sess is not None else None)
             self.note_native = True
         else:
             self.notes = bytearray()
             self.notes_n = 0
         self.client.note_conns.add(self)
+
+    def _note_keep(self, body):
+        """Python twin of the native sink's filter (zk_loop.cpp note_take):
+        keep a NOTIFICATION body in :attr:`notes`; True when the session
+        should also get it (its path has a watcher())."""
+        sess = self.note_sess
+        keep, to_py = True, False
+        if sess is not None and sess.watchers and len(body) >= 28:
+            n = int.from_bytes(body[24:28], 'big', signed=True)
+            if 0 <= n <= len(body) - 28:
+                path = body[28:28 + n].decode('utf-8', 'replace')
+                if path in sess.watchers:
+                    to_py = True
+                    keep = path in sess.bulk_watches
+        if keep:
+            self.notes += len(body).to_bytes(4, 'big')
+            self.notes += body
+            self.notes_n += 1
+        return to_py
 
     def take_notes(self):
         """(bytes, frames) kept since the last call."""

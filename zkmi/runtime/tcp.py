@@ -171,10 +171,13 @@ class TcpSocket(EventEmitter):
         return (self.transport is not None and not self.closed and
                 hasattr(self.transport, 'note_sink'))
 
-    def note_sink(self, on, max_packet, prefix=b''):
+    def note_sink(self, on, max_packet, prefix=b'', watchers=None,
+                  bulk=None):
         """Keep (``on``) every NOTIFICATION frame in the transport instead of
-        emitting it; :meth:`take_notes` drains them."""
-        self.transport.note_sink(on, max_packet, prefix)
+        emitting it; :meth:`take_notes` drains them.  An event on a path of
+        ``watchers`` (the session's path -> ZKWatcher dict) is emitted too,
+        and kept only when its path is in ``bulk``."""
+        self.transport.note_sink(on, max_packet, prefix, watchers, bulk)
 
     def take_notes(self):
         """(bytes, frames): the NOTIFICATION frames kept since the last

@@ -12,7 +12,6 @@
 // coalesced.  Ragged vectors (children, ACL entries, SET_WATCHES paths) are
 // expanded by a second pass after a scan of the per-frame counts.
 #include "zk_common.h"
-#include "zk_batch.h"
 #include "zk_reqparse.h"
 
 namespace zk {

@@ -16,8 +16,6 @@
 //                    wave ballot per owner plus an LDS prefix over waves
 #include "zk_common.h"
 
-extern "C" int zk_scan_excl_i64(const int64_t* in, int64_t* out, int64_t n,
-                                int64_t* total, int64_t* ws, hipStream_t st);
 
 namespace zk {
 

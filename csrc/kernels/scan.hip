@@ -83,16 +83,8 @@ constexpr int64_t SCAN_ONE_MAX = 1 << 16;       // use it up to this n
 // connections in flight it waits for a CU with room for the whole
 // workgroup behind the other stream's kernel: up to 2048 values (the
 // encoders' block sums of a 512K-record batch) a 256-thread workgroup
-// scans them in one chunk (ZKMI_SB_SMALL=0: always 1024 threads).
+// scans them in one chunk.
 constexpr int SB_T_SMALL = 256;
-static bool sb_small() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("ZKMI_SB_SMALL");
-    v = (e && e[0] == '0') ? 0 : 1;
-  }
-  return v == 1;
-}
 
 template <typename T, int NT = SB_T>
 __global__ __launch_bounds__(NT) void scan_one_block(
@@ -125,7 +117,7 @@ __global__ __launch_bounds__(NT) void scan_one_block(
 template <typename T>
 static void launch_one_block(const T* in, int64_t n, int64_t* out,
                              int64_t* total, hipStream_t st) {
-  if (sb_small() && n <= (int64_t)SB_T_SMALL * SB_V)
+  if (n <= (int64_t)SB_T_SMALL * SB_V)
     scan_one_block<T, SB_T_SMALL><<<1, SB_T_SMALL, 0, st>>>(in, n, out, total);
   else
     scan_one_block<T><<<1, SB_T, 0, st>>>(in, n, out, total);

@@ -18,17 +18,6 @@
 // test/streams.test.js:24), so frame i lands at i * 41 with no scan.
 #include "zk_common.h"
 
-extern "C" {
-struct ZkSessionTable {
-  int64_t* sid;       // [cap]
-  uint8_t* passwd;    // [cap * 16]
-  int32_t* timeout;   // [cap]
-  int32_t* state;     // [cap] SS_*
-  int64_t* next;      // [1] allocation counter
-  int64_t cap;
-};
-}
-
 namespace zk {
 
 constexpr int SS_T = 256;

@@ -42,36 +42,6 @@
 // error txn for them).
 #include "zk_common.h"
 #include "zk_reqparse.h"
-#include "zk_batch.h"
-
-extern "C" {
-struct ZkTree {
-  int64_t* ht;                 // [2 * (mask + 1)] interleaved {key, val}
-  int64_t mask;
-  int64_t* node_path_off;
-  int32_t* node_path_len;
-  int64_t* node_parent;        // parent node index, -1 = root, -2 = free
-  uint8_t* path_arena;
-  int64_t path_cap;
-  int64_t slab_cap;
-  int64_t* counters;           // see TC_* below
-  ZkNodeStore store;
-  int64_t* free_list;          // ring of deleted node indices
-  int64_t free_cap;
-  int32_t* cver;               // [cap] host-endian cversion
-  int32_t* nchild;             // [cap] host-endian numChildren
-  int64_t* pzxid;              // [cap] host-endian pzxid
-  int32_t* dirty;              // [cap] parent-on-dirty-list flag
-  int64_t* dirty_list;         // [cap]
-  int64_t* node_pw;            // [cap] path word: offset << 24 | length
-  int32_t* node_path_cap;      // [cap] bytes of the node's path storage
-  uint8_t* node_line;          // [cap * 64] lookup line, see LN_* below
-  // watch table (null wt_key: the tree keeps no watches), see wt_* below
-  int64_t* wt_key;             // [wt_hmask + 1] path hash | 1, 0 = empty
-  unsigned long long* wt_mask; // [2 * (wt_hmask + 1)] data / child masks
-  int64_t wt_hmask;
-};
-}
 
 namespace zk {
 
@@ -1312,17 +1282,9 @@ static int finish_launch(const ZkTree* t, int64_t ncap, const int64_t* n_dev,
                          int64_t bump_zxid, hipStream_t st,
                          int32_t publish = 1) {
   (void)ncap;
-  // (ZKMI_FIN_T=1024: the round-3 workgroup; 256 finds a CU sooner behind
-  // another stream's kernel, and the dirty list is a few thousand entries)
-  static int fin = -1;
-  if (fin < 0) {
-    const char* e = getenv("ZKMI_FIN_T");
-    fin = (e && atoi(e) == 1024) ? 1024 : 256;
-  }
-  if (fin == 1024)
-    zk::tree_finish_k<1024><<<1, 1024, 0, st>>>(*t, n_dev, bump_zxid, publish);
-  else
-    zk::tree_finish_k<256><<<1, 256, 0, st>>>(*t, n_dev, bump_zxid, publish);
+  // (256 threads: the workgroup finds a CU sooner behind another stream's
+  // kernel than 1024 did, and the dirty list is a few thousand entries)
+  zk::tree_finish_k<256><<<1, 256, 0, st>>>(*t, n_dev, bump_zxid, publish);
   ZK_LAUNCH_CHECK();
   return 0;
 }

@@ -9,6 +9,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "zk_abi.h"
+
 #define ZK_DEV __device__ __forceinline__
 
 namespace zk {

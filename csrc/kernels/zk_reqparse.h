@@ -4,7 +4,6 @@
 // Reference: lib/zk-buffer.js:58-253 (request layouts).
 #pragma once
 #include "zk_common.h"
-#include "zk_batch.h"
 
 namespace zk {
 

@@ -17,152 +17,8 @@
 #include <string>
 #include <vector>
 
-#include "../kernels/zk_batch.h"
+#include "../kernels/zk_abi.h"
 
-extern "C" {
-struct ZkTree {
-  int64_t* ht;
-  int64_t mask;
-  int64_t* node_path_off;
-  int32_t* node_path_len;
-  int64_t* node_parent;
-  uint8_t* path_arena;
-  int64_t path_cap;
-  int64_t slab_cap;
-  int64_t* counters;
-  ZkNodeStore store;
-  int64_t* free_list;
-  int64_t free_cap;
-  int32_t* cver;
-  int32_t* nchild;
-  int64_t* pzxid;
-  int32_t* dirty;
-  int64_t* dirty_list;
-  int64_t* node_pw;
-  int32_t* node_path_cap;
-  uint8_t* node_line;
-  int64_t* wt_key;
-  unsigned long long* wt_mask;
-  int64_t wt_hmask;
-};
-struct ZkSessionTable {
-  int64_t* sid;
-  uint8_t* passwd;
-  int32_t* timeout;
-  int32_t* state;
-  int64_t* next;
-  int64_t cap;
-};
-
-int64_t zk_scan_workspace(int64_t n);
-int zk_scan_set_mode(int mode);
-int zk_scan_excl_i64(const int64_t*, int64_t*, int64_t, int64_t*, int64_t*,
-                     hipStream_t);
-int zk_scan_excl_i32(const int32_t*, int64_t*, int64_t, int64_t*, int64_t*,
-                     hipStream_t);
-int zk_encode_requests2(const ZkReqBatch*, int64_t, int64_t*, int64_t*,
-                        int64_t*, int64_t*, uint8_t*, int64_t, int64_t*,
-                        int64_t, int32_t*, int32_t, hipStream_t);
-int zk_encode_set_watches(const int64_t*, const int32_t*, const uint8_t*,
-                          int64_t, int64_t, int64_t, int64_t, int64_t*,
-                          int64_t*, int64_t*, int64_t*, uint8_t*, int64_t,
-                          int32_t*, hipStream_t);
-int zk_encode_connect_requests(const int32_t*, const int64_t*, const int32_t*,
-                               const int64_t*, const int64_t*, const int32_t*,
-                               const uint8_t*, int64_t, int64_t*, int64_t*,
-                               int64_t*, int64_t*, uint8_t*, hipStream_t);
-int zk_encode_responses2(const ZkRespBatch*, const ZkNodeStore*,
-                         const int64_t*, int64_t, int64_t*, int64_t*,
-                         int64_t*, int64_t*, uint8_t*, int64_t, int32_t*,
-                         int32_t, int32_t, hipStream_t);
-int64_t zk_frame_scan_workspace(int64_t n);
-int zk_frame_scan5(const uint8_t*, const int64_t*, int64_t, int64_t,
-                   uint8_t*, int64_t, int64_t*, int32_t*, int64_t, int64_t*,
-                   int32_t, int32_t, int32_t, hipStream_t);
-int zk_frame_scan_stats(const uint8_t*, int64_t, int32_t, uint32_t*,
-                        hipStream_t);
-int zk_frame_scan_dbg(int64_t* host, int64_t tiles);
-int zk_decode_replies(const uint8_t*, const int64_t*, const int32_t*,
-                      const int64_t*, int64_t, const int64_t*, int64_t,
-                      const ZkReplyOut*, hipStream_t);
-int zk_decode_replies_check2(const uint8_t*, const int64_t*, const int32_t*,
-                             const int64_t*, int64_t, const int64_t*, int64_t,
-                             const ZkReplyOut*, const int64_t*, const int32_t*,
-                             const int32_t*, unsigned long long*, int32_t,
-                             int64_t*, const uint8_t*, const int64_t*,
-                             hipStream_t);
-int zk_expand_strings(const uint8_t*, const int64_t*, const int32_t*,
-                      const int64_t*, int64_t, int64_t*, int32_t*,
-                      hipStream_t);
-int zk_expand_acl(const uint8_t*, const int64_t*, const int32_t*,
-                  const int64_t*, int64_t, int32_t*, int64_t*, int32_t*,
-                  int64_t*, int32_t*, hipStream_t);
-int zk_decode_requests(const uint8_t*, const int64_t*, const int32_t*,
-                       const int64_t*, int64_t, const ZkReqOut*, hipStream_t);
-int zk_decode_connect_responses(const uint8_t*, const int64_t*,
-                                const int32_t*, int64_t, int32_t*, int32_t*,
-                                int64_t*, int64_t*, int32_t*, int32_t*,
-                                hipStream_t);
-int zk_tree_fill(const ZkTree*, int64_t, int64_t, const int32_t*, int64_t,
-                 hipStream_t);
-int zk_tree_build(const ZkTree*, int64_t, int64_t, hipStream_t);
-int zk_tree_serve(const ZkTree*, const uint8_t*, const ZkReqOut*,
-                  const int64_t*, int64_t, int32_t*, int32_t*, int32_t*,
-                  int64_t*, int64_t*, int64_t*, int32_t*, int64_t*, int64_t*,
-                  int64_t*, int64_t, int64_t, hipStream_t);
-int zk_tree_serve_frames(const ZkTree*, const uint8_t*, const int64_t*,
-                         const int32_t*, const int64_t*, int64_t, int32_t*,
-                         int32_t*, int32_t*, int64_t*, int64_t*, int64_t*,
-                         int32_t*, int64_t*, int64_t*, int64_t*, int64_t,
-                         int64_t, int32_t, int64_t*, hipStream_t);
-int zk_tree_serve_ordered(const ZkTree*, const uint8_t*, const ZkReqOut*,
-                          const int64_t*, int64_t, int32_t*, int32_t*,
-                          int32_t*, int64_t*, int64_t*, int64_t*, int32_t*,
-                          int64_t*, int64_t*, int64_t*, int64_t, int64_t,
-                          uint8_t*, int64_t, int32_t, int64_t, int64_t,
-                          int32_t, int64_t*, hipStream_t);
-int zk_watch_events(const int32_t*, const int32_t*, const int64_t*, int64_t,
-                    const int64_t*, int64_t*, int64_t, int32_t*, int32_t*,
-                    int64_t*, int32_t*, int64_t*, hipStream_t);
-int zk_watch_resume(const ZkTree*, const uint8_t*, const int64_t*,
-                    const int32_t*, const int64_t*, int64_t, int32_t,
-                    int64_t*, int64_t, int64_t, int32_t*, int64_t*, int32_t*,
-                    int64_t*, hipStream_t);
-int64_t zk_tree_order_workspace(int64_t);
-int64_t zk_tree_order_stats_offset(int64_t);
-int zk_tree_expire(const ZkTree*, int64_t, int64_t, unsigned long long*,
-                   hipStream_t);
-int zk_bench_gen_get(int64_t, uint64_t, int64_t, int64_t, int32_t,
-                     const int64_t*, int64_t*, int32_t*, int64_t*, int32_t*,
-                     const int64_t*, hipStream_t);
-int zk_bench_check_get(int64_t, const int32_t*, const int32_t*,
-                       const int32_t*, const int32_t*, const int64_t*,
-                       const int32_t*, const int64_t*, const int32_t*,
-                       const int32_t*, unsigned long long*, hipStream_t);
-int zk_bench_check_notif(int64_t, int64_t, const uint64_t*, const int64_t*,
-                         int64_t, int64_t,
-                         const int64_t*, const int32_t*, const uint8_t*,
-                         const uint8_t*, const int32_t*, const int32_t*,
-                         const int32_t*, const int32_t*, const int32_t*,
-                         const int64_t*, const int32_t*, unsigned long long*,
-                         hipStream_t);
-int64_t zk_route_workspace(int64_t n, int32_t world);
-int zk_route_requests(int64_t, int32_t, const int64_t*, const int32_t*,
-                      const uint8_t*, const int64_t*, const int32_t*,
-                      int32_t*, int64_t*, int32_t*, int64_t*, int32_t*,
-                      int64_t*, int64_t*, hipStream_t);
-int zk_seg_pack(const uint8_t*, int64_t, const int64_t*, const int64_t*,
-                int64_t, const int64_t*, const int64_t*, int32_t, int32_t,
-                int64_t, uint8_t*, unsigned long long*, hipStream_t);
-int zk_seg_unpack(const uint8_t*, int32_t, int32_t, int64_t, uint8_t*,
-                  int64_t*, int64_t*, unsigned long long*, hipStream_t);
-int zk_session_connect(const uint8_t*, const int64_t*, const int32_t*,
-                       const int64_t*, int64_t, const ZkSessionTable*,
-                       int64_t, uint64_t, int32_t, int32_t, const int64_t*,
-                       uint8_t*, int64_t*, int32_t*, hipStream_t);
-int zk_session_close(const ZkSessionTable*, const int64_t*, int64_t,
-                     hipStream_t);
-}
 
 namespace {
 

@@ -106,7 +106,7 @@ def build_torch_ops():
     (found through the rpath)."""
     import torch
     src = os.path.join(TDIR, 'zkmi_ops.cpp')
-    deps = [src, os.path.join(KDIR, 'zk_batch.h')]
+    deps = [src, os.path.join(KDIR, 'zk_abi.h')]
     stale, h = _stale(TORCH_SO, deps, torch.__version__)
     if not stale:
         return TORCH_SO

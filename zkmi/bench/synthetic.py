@@ -22,7 +22,6 @@ sync-free and no byte past a stream's end is walked.
 version CAS and ACL encode (BASELINE config 3).
 """
 
-import os
 import time
 
 import numpy as np
@@ -34,15 +33,9 @@ from ..ops import batch as B
 
 I64, I32, U8 = torch.int64, torch.int32, torch.uint8
 
-# ZKMI_SYNC_STREAMS=1: the pipelines read the stream lengths back to the
-# host instead of handing K1 the encoders' device totals (A/B runs)
-_SYNC_STREAMS = os.environ.get('ZKMI_SYNC_STREAMS') == '1'
-
-
 def _len(total):
-    """A stream length for K1: the encoder's device total, or (A/B) its
-    host value."""
-    return int(total.item()) if _SYNC_STREAMS else total
+    """A stream length for K1: the encoder's device total (no host read)."""
+    return total
 
 
 
@@ -737,8 +730,7 @@ class _Driver(object):
 
     def run(self, rb, session=0):
         """One batch through encode -> server -> decode.  Both streams are
-        scanned over their encoders' device totals: no device-to-host read
-        (``ZKMI_SYNC_STREAMS=1`` reads them back instead, for A/B)."""
+        scanned over their encoders' device totals: no device-to-host read."""
         tx, _, total, _ = B.encode_requests(rb, self.xt, out=self.tx)
         rx, rtotal, _, _ = self.server.serve(tx, _len(total),
                                              session=session,

@@ -23,7 +23,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, 'libzkmi_torch.so')
 HIP_LIB_PATH = os.path.join(_HERE, 'libzkmi_hip.so')
 
-# wire-format node slot layout (csrc/kernels/zk_batch.h)
+# wire-format node slot layout (csrc/kernels/zk_abi.h)
 SLOT_STAT = 0
 SLOT_LEN = 72
 SLOT_DATA = 76
@@ -54,10 +54,9 @@ def lib():
         check_build()
         torch.ops.load_library(LIB_PATH)
         _ops = torch.ops.zkmi
-        # ZKMI_SCAN=shfl selects the shuffle scan engine instead of the
-        # MFMA byte-plane one (csrc/kernels/scan.hip)
-        _ops.scan_set_mode(SCAN_SHFL if os.environ.get('ZKMI_SCAN') ==
-                           'shfl' else SCAN_MFMA)
+        # the MFMA byte-plane scan engine (csrc/kernels/scan.hip); the
+        # shuffle engine stays selectable (scan_set_mode) for the tests
+        _ops.scan_set_mode(SCAN_MFMA)
     return _ops
 
 

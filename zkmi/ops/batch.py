@@ -73,7 +73,7 @@ class RequestBatch:
     acl_arena: torch.Tensor
 
     def tensors(self):
-        """The descriptor list torch.ops.zkmi takes (zk_batch.h order)."""
+        """The descriptor list torch.ops.zkmi takes (zk_abi.h order)."""
         return [self.opcode, self.xid, self.arg, self.path_off,
                 self.path_len, self.data_off, self.data_len, self.acl_id,
                 self.path_arena, self.data_arena, self.acl_off, self.acl_len,

@@ -424,6 +424,11 @@ def main():
                          'tree (no collective in the step) instead of the '
                          'path-hash-sharded tree with R2 routing over '
                          'RCCL/xGMI (the default)')
+    ap.add_argument('--force-route', action='store_true',
+                    help='get, N = 1: run the multi-rank sharded step over a '
+                         'one-rank RCCL group (router, slots, '
+                         'all_to_all_single on HBM tensors, captured in the '
+                         'HIP graph) and compare it with the local pipeline')
     ap.add_argument('--no-compare', action='store_true',
                     help='get, N > 1: skip the replica comparison run')
     ap.add_argument('--paths', type=int, default=65536,
@@ -460,16 +465,9 @@ def launch(a):
     """``--gpus N`` outside torchrun: start the N rank processes (one per
     GPU, RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in their environment,
     rendezvous on 127.0.0.1) and exit with the first failure's code.  This
-    process never touches the GPU (counting devices does not initialise
-    it)."""
+    process never touches the GPU or asks how many there are: it trusts
+    --gpus, and a rank without a GPU fails loudly (and ends the launch)."""
     n = a.gpus
-    backend = os.environ.get('ZKMI_BENCH_BACKEND', 'nccl')
-    ndev = torch.cuda.device_count()
-    if backend == 'nccl' and ndev < n and not (ndev == 0 and
-                                               a.workload == 'ensemble'):
-        raise SystemExit('--gpus %d: %d GPU(s) visible (RCCL needs one per '
-                         'rank; ZKMI_BENCH_BACKEND=gloo shares them)'
-                         % (n, ndev))
     port = _free_port()
     procs = []
     for r in range(n):
@@ -578,6 +576,12 @@ def run_rank(a):
             dist.init_process_group('nccl', device_id=dev)
         else:
             dist.init_process_group(backend)
+    elif a.force_route and a.workload == 'get':
+        # a one-rank RCCL group: the multi-rank step's collectives run
+        # through RCCL on this GPU's HBM
+        dist.init_process_group(
+            'nccl', device_id=dev, rank=0, world_size=1,
+            init_method='tcp://127.0.0.1:%d' % _free_port())
     cdev = dev if backend == 'nccl' else torch.device('cpu')
 
     from zkmi.bench import synthetic as S
@@ -603,7 +607,8 @@ def run_rank(a):
         tree = S.GpuTree(a.nodes, a.data_bytes, device=dev, seed=0,
                          data_dist=dd, name_pad=npad, shard=(rank, world))
         return ShardedGetPipeline(tree, a.batch, seed=rank, coll_device=cdev,
-                                  streams=a.streams)
+                                  streams=a.streams,
+                                  force_route=a.force_route)
 
     if a.workload == 'get':
         pipe = make_get(not sharded)
@@ -638,7 +643,9 @@ def run_rank(a):
             pipe = S.MixPipeline(tree, a.batch, a.data_bytes, seed=rank)
             per_step = pipe.n
         else:
-            pipe = S.StormPipeline(tree, a.batch, seed=rank)
+            # across GPUs the sessions move between members (R3)
+            pipe = S.StormPipeline(tree, a.batch, seed=rank,
+                                   coll_device=cdev if world > 1 else None)
             per_step = pipe.n
 
     ops = per_step * a.steps * world
@@ -666,10 +673,11 @@ def run_rank(a):
                   st['wire_bytes_sent'] / max(st['steps'], 1),
               'remote_requests': st['remote_reqs'],
               'overflow_segments': st['overflow_segments'],
+              'xgmi_lower_bound_ms': st['xgmi_lower_bound_ms'],
               'slot_bytes': {'request': st['req_slot_bytes'],
                              'reply': st['rep_slot_bytes']}}
     replica = None
-    if sharded and world > 1 and not a.no_compare:
+    if sharded and (world > 1 or a.force_route) and not a.no_compare:
         # the same batch served by per-rank full replicas (no collective in
         # the step): what the sharding's xGMI traffic costs
         del pipe
@@ -736,10 +744,16 @@ def run_rank(a):
                              world, 'RCCL/xGMI' if backend == 'nccl' else
                              '%s (rehearsal, ranks may share a GPU)'
                              % backend) if world > 1 else
+                         'sharded step forced over a one-rank RCCL group: '
+                         'route -> seg_pack -> all_to_all_single (RCCL, HBM '
+                         'tensors) -> seg_unpack; replica_* = the local '
+                         'pipeline' if a.force_route else
                          'one shard (nothing to route), local pipeline')
                         if sharded else
                         ('replica per rank' if a.workload == 'get' else None),
             'r2': r2,
+            'workload_stats': dict(pipe.stats) if a.workload == 'storm'
+                              else None,
             'replica_value': replica['value'] if replica else None,
             'replica_ms_per_step': replica['ms_per_step'] if replica else None,
             'p50_get_rtt_us': rtt50,
@@ -785,7 +799,7 @@ def run_rank(a):
                           'tables; no floating-point compute',
         }
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

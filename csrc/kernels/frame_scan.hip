@@ -134,40 +134,10 @@ ZK_DEV int32_t lds_be32(const uint8_t* sb, int32_t p) {
   return (int32_t)bswap32(__builtin_amdgcn_alignbyte(hi, lo, p & 3));
 }
 
-// ---- LDS layout of fs_tile<W> (5.4 KiB per wave) ----------------------------
-// tile [FT_STAGE] | claimed bits [FT_S/32] | survivor bits [FT_S/32] |
-// compaction scratch [64] (uint16) | exit candidate bits [FT_XW]
+// ---- per-tile records shared with fs_check / fs_link / fs_rows -------------
 constexpr int FT_BITS = FT_S / 32;         // uint32 words per position map
 constexpr int FT_XW = 2048 / 32;           // exit candidates: the next tile's
                                            // window positions (W <= 2048)
-constexpr int FT_LDS = FT_STAGE + 2 * FT_BITS * 4 + 64 * 2 + FT_XW * 4;
-
-// One hop from tile-relative p (< FT_S).  Returns 0 and q (in-tile
-// successor), 1 for a terminal (the chain ends in the tile), or 2 and the
-// exit x (tile end + x) when the frame leaves the tile.
-// `minb`: the frontier's plausibility floor on a frame body (the smallest
-// ZooKeeper body is 8 bytes: a ping's xid + type).  Speculative walkers
-// reading a shorter length die at once instead of crawling 4 bytes a hop
-// through zero header fields; exactness is untouched (a real frame that
-// short only costs its tile the speculated entry, fs_link repairs it).
-ZK_DEV int ft_hop(const uint8_t* sb, int32_t p, int32_t nrel, int32_t maxp,
-                  int32_t minb, int32_t& q) {
-  if (p >= nrel) return 1;                 // the stream ended before p
-  const int32_t len = lds_be32(sb, p);
-  const int32_t nx = p + 4 + len;
-  if ((p + 4 > nrel) | (len < minb) | (len > maxp) | (nx > nrel)) return 1;
-  q = nx;
-  return nx >= FT_S ? 2 : 0;
-}
-
-// Claim position q in a bit map: true when this lane is the first (the
-// fetch-or's old bit was clear).  Lanes of one instruction hitting the same
-// word are serialised by the LDS unit, so exactly one of them wins.
-ZK_DEV bool ft_claim(uint32_t* bits, int32_t q) {
-  const uint32_t b = 1u << (q & 31);
-  return (__hip_atomic_fetch_or(&bits[q >> 5], b, __ATOMIC_RELAXED,
-                                __HIP_MEMORY_SCOPE_WAVEFRONT) & b) == 0;
-}
 
 // per-tile record: meta = cnt | np << 11 | (js + 1) << 22 | term << 33 |
 // bad << 34; entry = the entry used (-1: none, the tile before had no
@@ -231,15 +201,6 @@ ZK_DEV void ft_record(uint16_t* L, int32_t& m, uint32_t& ent, int32_t c,
   if ((m & 63) == 0) L[m - 64 + lane] = (uint16_t)ent;
 }
 
-// Mark a walker's exit x (offset into the next tile) as an entry candidate
-// of that tile; exits past the window cannot be the chain's (frames <= W).
-ZK_DEV bool ft_mark_exit(uint32_t* xbits, int32_t x, int W) {
-  if (x < 0 || x >= W) return false;
-  __hip_atomic_fetch_or(&xbits[x >> 5], 1u << (x & 31), __ATOMIC_RELAXED,
-                        __HIP_MEMORY_SCOPE_WAVEFRONT);
-  return true;
-}
-
 // The chain from tile-relative candidate entry e, walked in LDS (wave-
 // uniform): does it survive this tile, and where does it leave it?
 // Returns the absolute exit (>= the tile end) when it leaves the tile, or
@@ -249,6 +210,8 @@ ZK_DEV bool ft_mark_exit(uint32_t* xbits, int32_t x, int W) {
 // survivor that ends on one; FC_LIVE when it survives without a known exit
 // (it reaches the stream end, or meets a survivor that ends there).
 // fs_link's chase takes these as the tile's entry -> (exit, count) map.
+// (fs_tile answers most candidates from its chain map; this exact walk is
+// the fallback for chains the map leaves open.)
 constexpr int64_t FC_DEAD = -1;
 constexpr int64_t FC_LIVE = -2;
 constexpr int CX_SHIFT = 48;
@@ -297,98 +260,1062 @@ ZK_DEV int64_t ft_cand(const uint8_t* sb, const uint32_t* sbits, int32_t e,
   }
 }
 
-// Frontier passes past the window (fs_tile<W, true>, streams whose frames
-// may be longer than the window): when a frame longer than the window
-// covers [0, W) of a tile, every walker starts inside its body and dies
-// (body bytes read as lengths are implausible), so no survivor is left.
-// The frontier then runs again from [base, base + W) for base = W, 2W, ...
-// until a walker survives: the chain resumes after that frame.  Positions
-// the dead walkers claimed keep their meaning (a chain through one dies
-// too).  Kept out of the usual path (its own function, only instantiated
-// for LONG): a loop around the main frontier cost the GET step 9 %.
-template <int W>
-ZK_DEV void ft_frontier_passes(const uint8_t* sb, uint32_t* claimed,
-                               uint32_t* xbits, uint16_t* scratch,
-                               int32_t nrel, int32_t maxp32, int32_t minb,
-                               int lane, uint32_t& lastx, int& round,
-                               int32_t& mp, bool& ma) {
-  constexpr int K = W / 64;
-  for (int32_t base = W; base < FT_S && base < nrel && __ballot(ma) == 0;
-       base += W) {
-    for (int k = lane; k < W / 32; k += 64)
-      claimed[base / 32 + k] = 0xFFFFFFFFu;
+// ---- fs_tile: the tile's chain map, by pointer jumping ---------------------
+//
+// Every position p of the tile whose length word reads as a plausible frame
+// body (minb <= len < FT_LIMIT; in the entry window also any length up to
+// maxp) is a NODE.  A node's successor is the next frame start, p + 4 + len:
+// another node, or a ROOT where the chain ends inside the tile's view —
+//   EXIT   the chain leaves the tile (val = its last frame's start: the exit
+//          is that frame's end, read from the staged bytes);
+//   END    the stream ends exactly at the last frame's end (val = its start);
+//   PART   a frame (val) is cut by the stream end (its header or body);
+//   BAD    a frame (val) has a length < 0 or > maxp (BAD_LENGTH);
+//   SHORT  a frame (val) has a legal length below minb: the map does not
+//          follow it (an exact serial walk does, when the chain matters).
+// Pointer jumping (each round: node -> successor's successor, counts
+// added) takes every node to its root in log2(frames per tile) rounds, all
+// lanes busy: ~5 rounds on 192-byte frames, ~7 on 42-byte ones, where the
+// round-3 kernel walked ~20 / ~90 dependent LDS hops on one lane after a
+// merging frontier.  Lane l holds nodes l, l + 64, ... in registers (their
+// positions and words), and every phase issues all of its LDS reads before
+// it waits.  The map then answers, in O(1) each, what the tile chain logic
+// needs: the exits of the window entries (the next tile's candidate
+// entries), the survival / exit / frame count of the tile before's
+// candidates (fs_link's candidate exit map), and the frame starts of the
+// chosen entry's chain (slot index = count - the node's count to the root;
+// a side branch landing on the chain is caught by the successor check and
+// sent to the serial walk).  What fs_check / fs_link / fs_rows read is
+// unchanged: entry, exit, count, frame-start lists and candidate exits.
+constexpr int FT_NMAX = 512;               // nodes a tile's map holds (GET
+                                           // streams: 240-340; more: the
+                                           // serial walks)
+constexpr int FT_SLOTS = 352;              // chain slots (frames >= 12 bytes)
+constexpr int32_t FT_LIMIT = FT_S;         // node lengths below this
+enum : uint32_t {
+  RK_NODE = 0, RK_EXIT = 1, RK_END = 2, RK_PART = 3, RK_BAD = 4, RK_SHORT = 5
+};
+// node word: kind (3 bits) | val (13 bits: successor node or a position) |
+// frame starts from the node to the root (16 bits)
+ZK_DEV uint32_t rk(uint32_t kind, uint32_t val, uint32_t cnt) {
+  return kind << 29 | val << 16 | cnt;
+}
+ZK_DEV uint32_t rk_kind(uint32_t w) { return w >> 29; }
+ZK_DEV uint32_t rk_val(uint32_t w) { return (w >> 16) & 0x1FFF; }
+ZK_DEV uint32_t rk_cnt(uint32_t w) { return w & 0xFFFF; }
+
+// LDS layout per wave (7.6 KiB: 20 waves a CU): staged tile | node masks
+// of the 64 position blocks | nodes before each block | node words | R:
+// node positions while the map is built, then the chain slots (or the
+// serial walks' survivor bits) and the exit candidate bits
+constexpr int FT_SLOT_B = 704;             // >= FT_SLOTS * 2, >= FT_BITS * 4
+constexpr int FT_O_BLK = FT_STAGE;         // uint64 [64]
+constexpr int FT_O_BASE = FT_O_BLK + 64 * 8;   // uint16 [64]
+constexpr int FT_O_PK = FT_O_BASE + 64 * 2;
+constexpr int FT_O_R = FT_O_PK + FT_NMAX * 4;
+constexpr int FT_R_B = FT_NMAX * 2 > FT_SLOT_B + FT_XW * 4
+                           ? FT_NMAX * 2 : FT_SLOT_B + FT_XW * 4;
+constexpr int FT_O_XB = FT_O_R + FT_SLOT_B;
+constexpr int FT_LDS = FT_O_R + FT_R_B;
+static_assert(FT_SLOT_B >= FT_SLOTS * 2 && FT_SLOT_B >= FT_BITS * 4, "slots");
+static_assert(FT_STAGE % 16 == 0 && FT_LDS % 16 == 0, "LDS alignment");
+
+// Big-endian i32 at byte p from the two aligned dwords around it.
+ZK_DEV int32_t be32_of(uint32_t lo, uint32_t hi, int32_t p) {
+  return (int32_t)bswap32(__builtin_amdgcn_alignbyte(hi, lo, p & 3));
+}
+
+// The node map of a tile: a mask of nodes per 64-position block and the
+// nodes before each block (node indices follow positions).
+struct FtBlk {
+  const uint64_t* mask;
+  const uint16_t* base;
+};
+
+// Is tile position q (< FT_S) a node; its index if so.
+ZK_DEV bool ft_node(const FtBlk& blk, int32_t q, int32_t& idx) {
+  const uint64_t m = blk.mask[q >> 6];
+  const int32_t b = blk.base[q >> 6];
+  const uint64_t bit = 1ull << (q & 63);
+  idx = b + __popcll(m & (bit - 1));
+  return (m & bit) != 0;
+}
+
+// The root word of a chain continuing at NON-node position q (< FT_S) whose
+// length word reads len, after `before` frame starts.
+ZK_DEV uint32_t ft_classify(int32_t q, int32_t len, int32_t nrel,
+                            int32_t maxp, int32_t minb, uint32_t before) {
+  if (q + 4 > nrel) return rk(RK_PART, q, before);
+  if ((uint32_t)len > (uint32_t)maxp) return rk(RK_BAD, q, before);
+  const int32_t nx = q + 4 + len;
+  if (nx > nrel) return rk(RK_PART, q, before);
+  if (len < minb) return rk(RK_SHORT, q, before);
+  // a legal length >= FT_LIMIT (not a node): the frame leaves the tile
+  if (nx >= FT_S) return rk(RK_EXIT, q, before + 1);
+  return nx == nrel ? rk(RK_END, q, before + 1) : rk(RK_SHORT, q, before);
+}
+
+// Root word of the chain entering at tile position e (wave-uniform; e <
+// nrel, the map built).
+ZK_DEV uint32_t ft_root_at(const uint8_t* sb, const FtBlk& blk,
+                           const uint32_t* pk, int32_t e, int32_t nrel,
+                           int32_t maxp, int32_t minb) {
+  int32_t j;
+  if (ft_node(blk, e, j)) return pk[j];
+  return ft_classify(e, lds_be32(sb, e), nrel, maxp, minb, 0);
+}
+
+// End of the frame starting at tile position p (its length word staged).
+ZK_DEV int32_t ft_next(const uint8_t* sb, int32_t p) {
+  return p + 4 + lds_be32(sb, p);
+}
+
+// The candidate-exit value (ft_cand's) of a chain with root word w.
+ZK_DEV int64_t ft_cx(const uint8_t* sb, uint32_t w, int64_t ts) {
+  switch (rk_kind(w)) {
+    case RK_EXIT:
+      return (ts + ft_next(sb, (int32_t)rk_val(w))) |
+             ((int64_t)rk_cnt(w) << CX_SHIFT);
+    case RK_BAD: return FC_DEAD;
+    default: return FC_LIVE;                 // END / PART
+  }
+}
+
+// The survivor end code (sx) of a chain with root word w.
+ZK_DEV int64_t ft_send(const uint8_t* sb, uint32_t w, int64_t ts) {
+  const int32_t v = (int32_t)rk_val(w);
+  switch (rk_kind(w)) {
+    case RK_EXIT: return ts + ft_next(sb, v);
+    case RK_END: return TERM | (ts + ft_next(sb, v));
+    case RK_BAD: return TERM | TBAD | (ts + v);
+    default: return TERM | (ts + v);         // PART
+  }
+}
+
+// This lane's nodes i = lane + 64 k: positions (-1: none) and words.
+template <int NK>
+struct FtNodes {
+  int32_t p[NK];
+  uint32_t w[NK];
+};
+
+// Successors of this lane's nodes, then pointer jumping until every node's
+// word is its root's (kind, val) with the frame count from it.  Returns the
+// jumping rounds.
+template <int NK>
+ZK_DEV int ft_build(FtNodes<NK>& me, const uint8_t* sb, const FtBlk& blk,
+                    uint32_t* pk, const uint16_t* pos, int32_t N,
+                    int32_t nrel, int32_t maxp, int32_t minb, int lane) {
+#pragma unroll
+  for (int k = 0; k < NK; ++k) {
+    const int32_t i = lane + 64 * k;
+    const int32_t p = pos[i < N ? i : 0];
+    me.p[k] = i < N ? p : -1;
+  }
+  uint32_t a[NK], b[NK];
+#pragma unroll
+  for (int k = 0; k < NK; ++k) {
+    const int32_t q = me.p[k] < 0 ? 0 : me.p[k] & ~3;
+    a[k] = *(const uint32_t*)(sb + q);
+    b[k] = *(const uint32_t*)(sb + q + 4);
+  }
+  int32_t nx[NK];
+  uint64_t bm[NK];
+  uint32_t bb[NK], c[NK], d[NK];
+#pragma unroll
+  for (int k = 0; k < NK; ++k) {
+    const int32_t p = me.p[k] < 0 ? 0 : me.p[k];
+    nx[k] = p + 4 + be32_of(a[k], b[k], p);
+    const int32_t q = nx[k] < FT_S ? nx[k] : 0;
+    bm[k] = blk.mask[q >> 6];
+    bb[k] = blk.base[q >> 6];
+    c[k] = *(const uint32_t*)(sb + (q & ~3));
+    d[k] = *(const uint32_t*)(sb + (q & ~3) + 4);
+  }
+#pragma unroll
+  for (int k = 0; k < NK; ++k) {
+    const int32_t p = me.p[k];
+    const int32_t q = nx[k];
+    uint32_t r;
+    if (q > nrel) {
+      r = rk(RK_PART, p, 0);
+    } else if (q >= FT_S) {
+      r = rk(RK_EXIT, p, 1);
+    } else if (q == nrel) {
+      r = rk(RK_END, p, 1);
+    } else {
+      const uint64_t bit = 1ull << (q & 63);
+      if (bm[k] & bit)
+        r = rk(RK_NODE, bb[k] + __popcll(bm[k] & (bit - 1)), 1);
+      else
+        r = ft_classify(q, be32_of(c[k], d[k], q), nrel, maxp, minb, 1);
+    }
+    me.w[k] = r;
+    if (p >= 0) pk[lane + 64 * k] = r;
+  }
+  __builtin_amdgcn_wave_barrier();
+  int rounds = 0;
+  for (;;) {
+    uint32_t q[NK];
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+      const bool go = me.p[k] >= 0 && rk_kind(me.w[k]) == RK_NODE;
+      q[k] = pk[go ? rk_val(me.w[k]) : 0];
+    }
+    bool more = false;
+    uint32_t nw[NK];
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+      nw[k] = me.w[k];
+      if (me.p[k] >= 0 && rk_kind(me.w[k]) == RK_NODE) {
+        nw[k] = (q[k] & 0xFFFF0000u) | (rk_cnt(me.w[k]) + rk_cnt(q[k]));
+        more |= rk_kind(q[k]) == RK_NODE;
+      }
+    }
+    // every read of the round is issued before its first write (the
+    // wave's LDS operations complete in order)
     __builtin_amdgcn_wave_barrier();
-    int32_t p[K];
-    uint32_t act = 0;
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
-      p[k] = base + lane + 64 * k;
-      act |= 1u << k;
+    for (int k = 0; k < NK; ++k) {
+      if (nw[k] != me.w[k]) pk[lane + 64 * k] = nw[k];
+      me.w[k] = nw[k];
     }
-    int32_t live = W;
-    while (live > 64) {
-      int32_t q[K];
-      int code[K];
+    __builtin_amdgcn_wave_barrier();
+    ++rounds;
+    if (!__ballot(more)) break;
+  }
+  return rounds;
+}
+
+// The window entries' exits into xbits (this tile's candidate entries of
+// the next one) and the preferred chain: the window entry with the longest
+// chain, else (LONG) the first node whose chain leaves the tile.  Returns
+// its position (-1: none) and its exit past the tile end in `sx`.
+template <int W, bool LONG, int NK>
+ZK_DEV int32_t ft_cands(const FtNodes<NK>& me, const uint8_t* sb,
+                        uint32_t* xbits, int32_t& sx) {
+  uint32_t a[NK], b[NK];
 #pragma unroll
-      for (int k = 0; k < K; ++k) {
-        q[k] = 0;
-        code[k] = (act >> k) & 1 ? ft_hop(sb, p[k], nrel, maxp32, minb, q[k])
-                                 : 1;
+  for (int k = 0; k < NK; ++k) {
+    const bool ex = rk_kind(me.w[k]) == RK_EXIT && me.p[k] >= 0 &&
+                    (LONG || me.p[k] < W);
+    const int32_t v = ex ? (int32_t)rk_val(me.w[k]) : 0;
+    a[k] = *(const uint32_t*)(sb + (v & ~3));
+    b[k] = *(const uint32_t*)(sb + (v & ~3) + 4);
+  }
+  // keys: (count, -position) above the exit, so the max carries its exit
+  uint64_t best = 0, first = 0;
+#pragma unroll
+  for (int k = 0; k < NK; ++k) {
+    const int32_t p = me.p[k];
+    if (p < 0 || rk_kind(me.w[k]) != RK_EXIT || (!LONG && p >= W)) continue;
+    const int32_t v = (int32_t)rk_val(me.w[k]);
+    const uint32_t x = (uint32_t)(v + 4 + be32_of(a[k], b[k], v) - FT_S);
+    if (p < W) {
+      if (x < (uint32_t)W)
+        __hip_atomic_fetch_or(&xbits[x >> 5], 1u << (x & 31),
+                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+      const uint64_t key = (uint64_t)(rk_cnt(me.w[k]) << 16 |
+                                      (uint32_t)(0xFFFF - p)) << 32 | x;
+      best = best > key ? best : key;
+    } else if (LONG) {
+      const uint64_t key = (uint64_t)(0xFFFF - p) << 32 | x;
+      first = first > key ? first : key;
+    }
+  }
+#pragma unroll
+  for (int s = 32; s >= 1; s >>= 1) {
+    const uint64_t o = (uint64_t)__shfl_xor((long long)best, s, 64);
+    best = best > o ? best : o;
+    if (LONG) {
+      const uint64_t f = (uint64_t)__shfl_xor((long long)first, s, 64);
+      first = first > f ? first : f;
+    }
+  }
+  const uint64_t k = best ? best : (LONG ? first : 0);
+  if (!k) return -1;
+  sx = (int32_t)(uint32_t)k;
+  return 0xFFFF - (int32_t)((k >> 32) & 0xFFFF);
+}
+
+// The frame starts of the chain entering at tile position e with root word
+// w into the wave's slots (slot k = the k-th start): every node of that
+// root with count c <= D at or after e lands in slot D - c; the successor
+// check over the slots rejects a side branch sharing the root and count.
+// Returns D, or -1 when the chain needs the exact serial walk.
+template <int NK>
+ZK_DEV int32_t ft_chain(const FtNodes<NK>& me, const uint8_t* sb,
+                        const FtBlk& blk, uint16_t* slot, int32_t e,
+                        uint32_t w, int lane) {
+  const uint32_t kind = rk_kind(w);
+  const int32_t D = (int32_t)rk_cnt(w);
+  if (kind == RK_SHORT || kind == RK_BAD || D > FT_SLOTS) return -1;
+  if (D == 0) return 0;
+  const uint32_t root = w >> 16;
+  int32_t hits = 0;
+#pragma unroll
+  for (int k = 0; k < NK; ++k) {
+    const int32_t c = (int32_t)rk_cnt(me.w[k]);
+    const int32_t p = me.p[k];
+    const bool on = p >= e && (me.w[k] >> 16) == root && c >= 1 && c <= D;
+    if (on) slot[D - c] = (uint16_t)p;
+    hits += __popcll(__ballot(on));
+  }
+  __builtin_amdgcn_wave_barrier();
+  // the chain's nodes: its D frame starts, less the last one when that
+  // frame (a long one) is not a node
+  int32_t want = D;
+  if (lane == 0) {
+    slot[0] = (uint16_t)e;
+    if (kind == RK_EXIT || kind == RK_END) slot[D - 1] = (uint16_t)rk_val(w);
+  }
+  if (kind == RK_EXIT || kind == RK_END) {
+    int32_t j;
+    if (!ft_node(blk, (int32_t)rk_val(w), j)) --want;
+  }
+  __builtin_amdgcn_wave_barrier();
+  // as many hits as chain nodes: no side branch shares the root and a
+  // count, every slot holds the chain's start
+  if (hits == want) return D;
+  bool ok = true;
+  for (int32_t k = lane; k < D; k += 64) {
+    const int32_t p = slot[k];
+    const int32_t nx = ft_next(sb, p);
+    if (k + 1 < D) {
+      ok &= nx == (int32_t)slot[k + 1];
+    } else if (kind == RK_PART) {
+      ok &= nx == (int32_t)rk_val(w);
+    }
+  }
+  return __ballot(!ok) ? -1 : D;
+}
+
+// What fs_tile's steps 2-5 need from the kernel.
+struct FtCtx {
+  const uint8_t* buf;
+  uint16_t* list;
+  uint16_t* pre;
+  int64_t* sx;
+  uint64_t* lbw;
+  int64_t* rec_entry;
+  int64_t* rec_exit;
+  int64_t* rec_meta;
+  int32_t* rcount;
+  int64_t* dbg;
+  int64_t* cx;
+  uint64_t* stats;
+  uint8_t* sb;
+  FtBlk blk;
+  uint32_t* pk;
+  uint16_t* pos;
+  uint16_t* slot;
+  uint32_t* sbits;
+  uint32_t* xbits;
+  int64_t n, t, ts, tend, t_0, t_s, t_d;
+  int32_t nrel, maxp32, minb, N, misspec;
+  bool nospec;
+  int lane;
+};
+
+template <int W, bool LONG, int NK>
+ZK_DEV void fs_tile_rest(const FtCtx& cx_, bool mapped) {
+  const FtCtx& C = cx_;
+  const int lane = C.lane;
+  const uint8_t* sb = C.sb;
+  const int64_t n = C.n, t = C.t, ts = C.ts, tend = C.tend;
+  const int32_t nrel = C.nrel, maxp32 = C.maxp32, minb = C.minb;
+  constexpr int XW = W / 32;                // candidate words used
+  FtNodes<NK> me;
+  int rounds = 0;
+  if (mapped)
+    rounds = ft_build<NK>(me, sb, C.blk, C.pk, C.pos, C.N, nrel, maxp32, minb,
+                          lane);
+  // the positions are in registers now: R becomes the slots / bits
+  for (int k = lane; k < FT_R_B / 4; k += 64) C.sbits[k] = 0u;
+  __builtin_amdgcn_wave_barrier();
+  const int64_t t_f = C.dbg ? wall_clock64() : 0;
+
+  // ---- 3. the window entries' exits: this tile's candidates for the next -
+  int32_t px = -1, sp = -1;
+  if (mapped) {
+    int32_t x = -1;
+    sp = ft_cands<W, LONG, NK>(me, sb, C.xbits, x);
+    if (sp >= 0 && x >= 0 && x < (LONG ? FT_S - 1 : W)) px = x;
+  }
+  // Candidates go out packed in ONE 64-bit word (a relaxed agent-scope
+  // store: no fence, no L2 write-back on this multi-XCD part): bit 63 =
+  // ready, five 12-bit slots of offset + 1 (0 = empty), slot 0 the preferred
+  // one, then up to four other in-window exits in offset order.
+  __builtin_amdgcn_wave_barrier();
+  uint64_t word = (uint64_t)1 << 63;
+  if (px >= 0) word |= (uint64_t)(px + 1);
+  {
+    uint32_t xw = lane < XW ? C.xbits[lane] : 0u;
+    if (px >= 0 && px < W && lane == (px >> 5)) xw &= ~(1u << (px & 31));
+    uint64_t any = __ballot(xw != 0);
+    int nsl = 1;
+    if (px < 0 && any) {
+      // no preferred exit: the first in-window one
+      const int wl = (int)__builtin_ctzll(any);
+      const uint32_t bits = (uint32_t)__builtin_amdgcn_readlane((int)xw, wl);
+      const int x0 = wl * 32 + (int)__builtin_ctz(bits);
+      word |= (uint64_t)(x0 + 1);
+      if (lane == wl) xw &= ~(1u << (x0 & 31));
+      any = __ballot(xw != 0);
+    }
+    while (any && nsl < 5) {
+      const int wl = (int)__builtin_ctzll(any);
+      uint32_t bits = (uint32_t)__builtin_amdgcn_readlane((int)xw, wl);
+      while (bits && nsl < 5) {
+        const int bit = (int)__builtin_ctz(bits);
+        bits &= bits - 1;
+        word |= (uint64_t)(wl * 32 + bit + 1) << (12 * nsl);
+        ++nsl;
       }
+      any &= any - 1;
+    }
+  }
+  if (lane == 0) lb_store(&C.lbw[2 * t], word);    // 0 = not yet
+  const int64_t t_1 = C.dbg ? wall_clock64() : 0;
+
+  // ---- 4. the entry: the tile before's candidates, checked in the map ----
+  int64_t E = 0;
+  bool none = false;
+  uint32_t wE = 0;               // the entry's root word, when wE_ok
+  bool wE_ok = false;
+  if (t > 0 && C.nospec) {
+    // (tests: every tile but the first without a speculated entry, the
+    // worst case of the link repair; no candidate exits either)
+    none = true;
+    if (lane < 5) C.cx[5 * t + lane] = FC_DEAD;
+  } else if (t > 0) {
+    // Tile t-1 is running or done.  Poll with exponential back-off: these
+    // loads bypass the caches, and thousands of waves polling every few
+    // hundred cycles flood the fabric.
+    uint64_t x;
+    int nap = 0;
+    const uint64_t t_w = wall_clock64();
+    for (;;) {
+      x = lb_load(&C.lbw[2 * (t - 1)]);
+      if (x != 0) break;
+      if (wall_clock64() - t_w > FT_WAIT_TICKS) break;   // no speculation
+      // the tile before usually publishes within a microsecond: short
+      // naps first (128 cycles), then back off
+      if (nap < 16) __builtin_amdgcn_s_sleep(2);
+      else if (nap < 32) __builtin_amdgcn_s_sleep(8);
+      else __builtin_amdgcn_s_sleep(32);
+      ++nap;
+    }
+    // The first candidate whose chain survives this tile is the entry (a
+    // garbage exit of the tile before dies on a bad length here).  Every
+    // candidate's outcome goes to `cx`: where two chains both survive tile
+    // after tile (a phantom chain), fs_link's chase follows the exact one
+    // through this map instead of re-walking every tile.  Lane s checks
+    // candidate s in the map; chains the map leaves open are walked.
+    const int32_t v = lane < 5 ? (int32_t)((x >> (12 * lane)) & 0xFFF) : 0;
+    const bool has = v != 0 && ts + (v - 1) < n;
+    const int32_t e = v - 1;
+    uint32_t we = 0;
+    if (has && mapped) we = ft_root_at(sb, C.blk, C.pk, e, nrel, maxp32, minb);
+    const bool open = has && (!mapped || rk_kind(we) == RK_SHORT);
+    int64_t xe = has && !open ? ft_cx(sb, we, ts) : FC_DEAD;
+    for (uint64_t um = __ballot(open); um; um &= um - 1) {
+      const int l = (int)__builtin_ctzll(um);
+      const int32_t el = __builtin_amdgcn_readlane(e, l);
+      const int64_t r = ft_cand(sb, C.sbits, el, nrel, maxp32, -1, n, ts, 0,
+                                lane);
+      if (lane == l) xe = r;
+    }
+    if (lane < 5) C.cx[5 * t + lane] = xe;
+    const uint64_t hm = __ballot(has);
+    const uint64_t lm = __ballot(has && xe != FC_DEAD);
+    int64_t first = -1;
+    E = -1;
+    if (lm) {
+      const int l = (int)__builtin_ctzll(lm);
+      E = ts + __builtin_amdgcn_readlane(e, l);
+      wE = (uint32_t)__builtin_amdgcn_readlane((int)we, l);
+      wE_ok = mapped && !__builtin_amdgcn_readlane((int)open, l);
+    }
+    if (hm) first = ts + __builtin_amdgcn_readlane(e, (int)__builtin_ctzll(hm));
+    if (E < 0) E = first;        // no live candidate: the first one
+    // (tests: every misspec-th tile takes a garbage entry one byte past the
+    // chosen one, the link repair's adversary)
+    if (C.misspec > 0 && t % C.misspec == 1 && E >= 0 && E + 1 < n) {
+      ++E;
+      wE_ok = false;
+    }
+    none = E < 0;
+  }
+  const int64_t t_2 = C.dbg ? wall_clock64() : 0;
+
+  // ---- 5. the chain's frame starts ---------------------------------------
+  // The entry's chain when the map has it (the usual case: its starts are
+  // the tile's list, no walk); otherwise the preferred chain's starts are
+  // the survivor list (fs_link's repair joins it) and the entry is walked
+  // serially until it joins it, dies or leaves, as round 3 did.
+  uint16_t* L = C.list + t * FT_LMAX;
+  FcWalk wk{E, 0, 0, -1, false, false};
+  int64_t send = -1;
+  int32_t m = 0;
+  bool done = false;
+  const int32_t erel = (int32_t)(E - ts);
+  if (!none && erel >= nrel) {
+    // the entry is the stream's end
+    send = TERM | E;
+    fc_join_end(wk, send, n);
+    done = true;
+  } else if (!none && mapped) {
+    const uint32_t we = wE_ok ? wE
+                              : ft_root_at(sb, C.blk, C.pk, erel, nrel, maxp32,
+                                           minb);
+    const int32_t D = ft_chain<NK>(me, sb, C.blk, C.slot, erel, we, lane);
+    if (D >= 0) {
+      for (int32_t k = lane; k < D; k += 64) L[k] = C.slot[k];
+      m = D;
+      send = ft_send(sb, we, ts);
+      wk.cnt = D;
+      wk.js = D > 0 ? 0 : -1;
+      fc_join_end(wk, send, n);
+      done = true;
+    }
+  }
+  if (!done) {
+    // survivor list: the preferred chain's starts (when the map has them)
+    if (sp >= 0) {
+      const uint32_t ws = ft_root_at(sb, C.blk, C.pk, sp, nrel, maxp32, minb);
+      const int32_t D = ft_chain<NK>(me, sb, C.blk, C.slot, sp, ws, lane);
+      if (D > 0) {
+        for (int32_t k = lane; k < D; k += 64) L[k] = C.slot[k];
+        m = D;
+        send = ft_send(sb, ws, ts);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    // survivor bits from the list just stored (each lane rereads only what
+    // it wrote itself)
+    for (int k = lane; k < FT_SLOT_B / 4; k += 64) C.sbits[k] = 0u;
+    __builtin_amdgcn_wave_barrier();
+    for (int i = lane; i < m; i += 64) {
+      const int32_t q = L[i];
+      __hip_atomic_fetch_or(&C.sbits[q >> 5], 1u << (q & 31),
+                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (!none) {
+      // join: walk from the entry until the survivor's path
+      int64_t c = E;
+      uint16_t* P = C.pre + t * FT_LMAX;
+      int32_t np = 0;
+      uint32_t ent = 0;
+      for (;;) {
+        if (c >= tend) { wk.exit = c; break; }
+        if (c >= n) { wk.exit = n; break; }  // the stream ends cleanly
+        const int32_t crel = (int32_t)(c - ts);
+        const uint32_t smw = C.sbits[crel >> 5];
+        const int32_t lraw = lds_be32(sb, crel);
+        if ((smw >> (crel & 31)) & 1u) {
+          // joined: the rest is the survivor's list from this start on
+          static_assert(FT_BITS == 2 * 64, "two map words per lane");
+          const int32_t cw = crel >> 5;
+          int32_t s = 0;
 #pragma unroll
-      for (int k = 0; k < K; ++k) {
-        if (!((act >> k) & 1)) continue;
-        if (code[k] == 0 && ft_claim(claimed, q[k])) {
-          p[k] = q[k];
-        } else {
-          if (code[k] == 2 && ft_mark_exit(xbits, q[k] - FT_S, W))
-            lastx = max(lastx, ((uint32_t)round << 16) |
-                                   (uint32_t)(q[k] - FT_S));
-          act &= ~(1u << k);
+          for (int h = 0; h < 2; ++h) {
+            const int32_t wi = lane + 64 * h;
+            const uint32_t wd = C.sbits[wi];
+            s += wi < cw ? __popc(wd)
+                         : (wi == cw ? __popc(wd & ((1u << (crel & 31)) - 1u))
+                                     : 0);
+          }
+#pragma unroll
+          for (int d = 32; d >= 1; d >>= 1) s += __shfl_xor(s, d, 64);
+          wk.js = s;
+          break;
         }
-      }
-      ++round;
-      int c = __popc(act);
-#pragma unroll
-      for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d, 64);
-      live = c;
-    }
-    {
-      const uint32_t mine = __popc(act);
-      uint32_t incl = mine;
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(incl, d, 64);
-        if (lane >= d) incl += y;
-      }
-      uint32_t o = incl - mine;
-#pragma unroll
-      for (int k = 0; k < K; ++k)
-        if ((act >> k) & 1) scratch[o++] = (uint16_t)p[k];
-      __builtin_amdgcn_wave_barrier();
-      ma = lane < live;
-      mp = ma ? (int32_t)scratch[lane] : 0;
-      __builtin_amdgcn_wave_barrier();
-    }
-    while (live > 1) {
-      int32_t q = 0;
-      const int code = ma ? ft_hop(sb, mp, nrel, maxp32, minb, q) : 1;
-      if (ma) {
-        if (code == 0 && ft_claim(claimed, q)) {
-          mp = q;
-        } else {
-          if (code == 2 && ft_mark_exit(xbits, q - FT_S, W))
-            lastx = max(lastx, ((uint32_t)round << 16) | (uint32_t)(q - FT_S));
-          ma = false;
+        const int32_t len = __builtin_amdgcn_readfirstlane(lraw);
+        const int32_t nx = crel + 4 + len;
+        if ((uint32_t)len > (uint32_t)maxp32 || nx > nrel) {
+          wk.exit = c;
+          wk.term = true;
+          wk.bad = (crel + 4 <= nrel) && ((len < 0) | (len > maxp32));
+          break;
         }
+        ft_record(P, np, ent, crel, lane);
+        c = ts + nx;
       }
-      ++round;
-      live = __popcll(__ballot(ma));
+      if (lane < (np & 63)) P[(np & ~63) + lane] = (uint16_t)ent;
+      wk.np = np;
+      wk.cnt = np;
+      if (wk.js >= 0) {
+        wk.cnt = np + (m - wk.js);
+        fc_join_end(wk, send, n);
+      }
+    } else {
+      // no speculated entry: the exit recorded is the survivor's (the
+      // likely one), so fs_link's grid repair of the NEXT tile can start
+      // from it in the same round as this tile's own repair
+      if (m > 0) fc_join_end(wk, send, n);
+      if (lane == 0) fc_stat(C.stats, 1, 1);
+    }
+  }
+  if (lane == 0) {
+    C.sx[t] = send;
+    C.rcount[t] = m;
+    C.rec_entry[t] = none ? -1 : E;
+    C.rec_exit[t] = wk.exit;
+    C.rec_meta[t] = fc_meta(wk);
+    if (C.dbg) {
+      int64_t* d = C.dbg + 8 * t;
+      d[0] = C.t_0;
+      d[1] = t_1;
+      d[2] = t_2;
+      d[3] = wall_clock64();
+      d[4] = C.t_d;
+      d[5] = (int64_t)C.N | (int64_t)rounds << 16 | (int64_t)done << 24;
+      d[6] = C.t_s;
+      d[7] = t_f;
     }
   }
 }
 
-template <int W, bool LONG>
+// ---- tile groups: the map once, then the chain walked on ------------------
+// A group of G consecutive tiles is one wave's work (G > 1: streams whose
+// frames are large, so a tile holds few of them).  The group's first tile
+// gets the chain map as above; its preferred chain is then WALKED through
+// the group's other tiles (staged one after the other into the same LDS;
+// the next tile's bytes ride in registers while the walk runs), one
+// dependent LDS hop per frame: ~20 hops a tile on 192-byte frames, where a
+// map costs ~6 us of detection and jumping.  Only the group's first tile
+// speculates an entry; the others' entries are the walk's exits, recorded
+// as their only candidate (word + cx) so fs_link's chase sees the usual
+// maps.  After its walk the group publishes its last exit and takes the
+// group before's: the first tile's candidates are checked in a register
+// table of its window positions' roots, kept from the map.
+
+// Stage the 4 KiB tile at ts in registers (zero past n) / into LDS.
+struct FtTileRegs {
+  uint4 v[FT_S / 16 / 64];
+  uint4 pad;
+};
+ZK_DEV void ft_load(const uint8_t* __restrict__ buf, int64_t n, int64_t ts,
+                    int lane, FtTileRegs& r) {
+  constexpr int PER = FT_S / 16 / 64;
+  r.pad = make_uint4(0, 0, 0, 0);
+  if (ts + FT_STAGE <= n) {
+#pragma unroll
+    for (int j = 0; j < PER; ++j)
+      __builtin_memcpy(&r.v[j], buf + ts + 16 * (lane + 64 * j), 16);
+    if (lane == 0) __builtin_memcpy(&r.pad, buf + ts + FT_S, 16);
+  } else {
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      uint8_t* b = (uint8_t*)&r.v[j];
+      const int64_t g = ts + 16 * (lane + 64 * j);
+      for (int k = 0; k < 16; ++k) b[k] = g + k < n ? buf[g + k] : 0;
+    }
+    if (lane == 0) {
+      uint8_t* b = (uint8_t*)&r.pad;
+      for (int k = 0; k < 16; ++k)
+        b[k] = ts + FT_S + k < n ? buf[ts + FT_S + k] : 0;
+    }
+  }
+}
+ZK_DEV void ft_store(uint8_t* sb, const FtTileRegs& r, int lane) {
+  constexpr int PER = FT_S / 16 / 64;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) *(uint4*)(sb + 16 * (lane + 64 * j)) = r.v[j];
+  if (lane == 0) *(uint4*)(sb + FT_S) = r.pad;
+  __builtin_amdgcn_wave_barrier();
+}
+
+// The chain from tile-relative c through the staged tile (wave-uniform),
+// its frame starts into L; returns the end code (sx) and the count.
+ZK_DEV int64_t ft_walk(const uint8_t* sb, int32_t c, int32_t nrel,
+                       int32_t maxp32, int64_t ts, uint16_t* L, int32_t& mo,
+                       int lane) {
+  int32_t m = 0;
+  uint32_t ent = 0;
+  int64_t send;
+  // (the walk is wave-uniform: the position and the bounds in SGPRs keep
+  // a hop to one LDS read and a few scalar instructions)
+  c = __builtin_amdgcn_readfirstlane(c);
+  nrel = __builtin_amdgcn_readfirstlane(nrel);
+  const int32_t lim = min((int32_t)FT_S, nrel);
+  if (c >= nrel) {
+    send = TERM | (ts + c);
+  } else {
+    int32_t len, nx;
+    bool ok;
+    for (;;) {
+      len = __builtin_amdgcn_readfirstlane(lds_be32(sb, c));
+      nx = c + 4 + len;
+      ok = (uint32_t)len <= (uint32_t)maxp32 && nx <= nrel;
+      if (!ok) break;
+      ent = lane == (m & 63) ? (uint32_t)c : ent;
+      ++m;
+      if ((m & 63) == 0) L[m - 64 + lane] = (uint16_t)ent;
+      if (nx >= lim) break;
+      c = nx;
+    }
+    if (!ok) {
+      const bool bad = (c + 4 <= nrel) && ((len < 0) | (len > maxp32));
+      send = TERM | (bad ? TBAD : 0) | (ts + c);
+    } else if (nx >= FT_S) {
+      send = ts + nx;
+    } else {
+      send = TERM | (ts + nx);               // the stream ends at nx
+    }
+  }
+  if (lane < (m & 63)) L[(m & ~63) + lane] = (uint16_t)ent;
+  mo = m;
+  return send;
+}
+
+// The candidate-exit value of a walk that ended with code `send` after m
+// frame starts.
+ZK_DEV int64_t ft_cx_of(int64_t send, int32_t m) {
+  if (!(send & TERM)) return send | ((int64_t)m << CX_SHIFT);
+  return (send & TBAD) ? FC_DEAD : FC_LIVE;
+}
+
+// Element q (wave-uniform) of a list held 64 to a register.
+template <int SVN>
+ZK_DEV int32_t ft_sv_at(const uint32_t (&sv)[SVN], int32_t q) {
+  uint32_t v = 0;
+#pragma unroll
+  for (int i = 0; i < SVN; ++i)
+    if (i == (q >> 6)) v = sv[i];
+  return __builtin_amdgcn_readlane((int)v, q & 63);
+}
+
+template <int W, int NK, int G>
+ZK_DEV void fs_group_rest(const FtCtx& cx_) {
+  static_assert(G > 1 && W <= 512, "groups: small windows");
+  constexpr int WJ = W / 64;                // window positions per lane
+  const FtCtx& C = cx_;
+  const int lane = C.lane;
+  uint8_t* sb = C.sb;
+  const int64_t n = C.n, t0 = C.t, ts = C.ts;
+  const int32_t nrel = C.nrel, maxp32 = C.maxp32, minb = C.minb;
+  const int64_t ntiles = (n + FT_S - 1) / FT_S;
+  FtNodes<NK> me;
+  const int rounds = ft_build<NK>(me, sb, C.blk, C.pk, C.pos, C.N, nrel,
+                                  maxp32, minb, lane);
+  for (int k = lane; k < FT_R_B / 4; k += 64) C.sbits[k] = 0u;
+  __builtin_amdgcn_wave_barrier();
+  const int64_t t_f = C.dbg ? wall_clock64() : 0;
+
+  // ---- the first tile: its preferred chain (the survivor) and its window
+  // positions' roots, in registers for the entry check after the walk
+  int32_t x = -1;
+  const int32_t sp = ft_cands<W, false, NK>(me, sb, C.xbits, x);
+  uint32_t rw[WJ];
+  int64_t rx[WJ];
+#pragma unroll
+  for (int j = 0; j < WJ; ++j) {
+    const int32_t e = lane + 64 * j;
+    rw[j] = e < nrel ? ft_root_at(sb, C.blk, C.pk, e, nrel, maxp32, minb)
+                     : rk(RK_END, 0, 0);
+    rx[j] = e < nrel ? ft_cx(sb, rw[j], ts) : FC_LIVE;
+  }
+  int32_t m0 = 0;
+  int64_t send0 = -1;
+  uint32_t ws = 0;
+  uint16_t* L0 = C.list + t0 * FT_LMAX;
+  if (sp >= 0) {
+    ws = ft_root_at(sb, C.blk, C.pk, sp, nrel, maxp32, minb);
+    const int32_t D = ft_chain<NK>(me, sb, C.blk, C.slot, sp, ws, lane);
+    if (D >= 0) {
+      for (int32_t k = lane; k < D; k += 64) L0[k] = C.slot[k];
+      m0 = D;
+      send0 = ft_send(sb, ws, ts);
+    } else {
+      // (a side branch or a short frame on it: walked)
+      __builtin_amdgcn_wave_barrier();
+      send0 = ft_walk(sb, sp, nrel, maxp32, ts, L0, m0, lane);
+      for (int32_t k = lane; k < m0; k += 64) C.slot[k] = L0[k];
+      ws = 0;                  // (the slots hold the walk's starts)
+    }
+  }
+  // the survivor's starts stay in registers (R becomes the survivor bits
+  // if tile t0 has to come back)
+  constexpr int SVN = (FT_SLOTS + 63) / 64;
+  __builtin_amdgcn_wave_barrier();
+  uint32_t sv[SVN];
+#pragma unroll
+  for (int i = 0; i < SVN; ++i)
+    sv[i] = lane + 64 * i < m0 ? C.slot[lane + 64 * i] : 0u;
+  const int64_t t_1 = C.dbg ? wall_clock64() : 0;
+
+  // ---- the group's other tiles: the survivor's chain walked on -----------
+  int64_t send = send0;
+  int32_t kdone = 1;
+  FtTileRegs nxt;
+  if (G > 1 && t0 + 1 < ntiles) ft_load(C.buf, n, ts + FT_S, lane, nxt);
+  for (int k = 1; k < G; ++k) {
+    const int64_t tk = t0 + k;
+    if (tk >= ntiles) break;
+    const int64_t tsk = tk * FT_S;
+    const int64_t c = send;                 // the chain's entry into tk
+    const bool live = sp >= 0 && !(send & TERM) && c >= tsk &&
+                      c < tsk + FT_S;
+    if (!live) break;
+    ft_store(sb, nxt, lane);
+    if (k + 1 < G && tk + 1 < ntiles) ft_load(C.buf, n, tsk + FT_S, lane, nxt);
+    int32_t m;
+    const int32_t nrelk = (int32_t)min(n - tsk, (int64_t)1 << 30);
+    send = ft_walk(sb, (int32_t)(c - tsk), nrelk, maxp32, tsk,
+                   C.list + tk * FT_LMAX, m, lane);
+    FcWalk wk{c, m, 0, m > 0 ? 0 : -1, false, false};
+    fc_join_end(wk, send, n);
+    if (lane == 0) {
+      // the tile's one candidate entry: the walk's (for fs_link's chase)
+      lb_store(&C.lbw[2 * (tk - 1)],
+               (uint64_t)1 << 63 | (uint64_t)(c - tsk + 1));
+      C.cx[5 * tk] = ft_cx_of(send, m);
+      C.sx[tk] = send;
+      C.rcount[tk] = m;
+      C.rec_entry[tk] = c;
+      C.rec_exit[tk] = wk.exit;
+      C.rec_meta[tk] = fc_meta(wk);
+    }
+    if (lane >= 1 && lane < 5) C.cx[5 * tk + lane] = FC_DEAD;
+    kdone = k + 1;
+  }
+  // tiles the walk did not reach: no entry (fs_link re-walks them)
+  for (int k = kdone; k < G; ++k) {
+    const int64_t tk = t0 + k;
+    if (tk >= ntiles) break;
+    if (lane == 0) {
+      lb_store(&C.lbw[2 * (tk - 1)], (uint64_t)1 << 63);
+      C.sx[tk] = -1;
+      C.rcount[tk] = 0;
+      C.rec_entry[tk] = -1;
+      C.rec_exit[tk] = -1;
+      C.rec_meta[tk] = 0;
+    }
+    if (lane < 5) C.cx[5 * tk + lane] = FC_DEAD;
+  }
+  // the group's last exit: the next group's candidate
+  const int64_t tl = min(t0 + G, ntiles) - 1;
+  {
+    uint64_t word = (uint64_t)1 << 63;
+    const int64_t tle = (tl + 1) * FT_S;
+    if (kdone == (int32_t)(tl - t0 + 1) && sp >= 0 && !(send & TERM) &&
+        send >= tle && send < tle + W)
+      word |= (uint64_t)(send - tle + 1);
+    if (lane == 0) lb_store(&C.lbw[2 * tl], word);
+  }
+
+  // ---- the first tile's entry: the group before's exit -------------------
+  int64_t E = 0;
+  bool none = false;
+  uint32_t wE = 0;
+  bool known = false;          // wE / the candidate values from the table
+  bool staged = false;         // tile t0 back in LDS (the fallbacks)
+  auto restage = [&]() {
+    if (staged) return;
+    FtTileRegs r;
+    ft_load(C.buf, n, ts, lane, r);
+    ft_store(sb, r, lane);
+    // survivor bits from the survivor's starts
+    for (int k = lane; k < FT_SLOT_B / 4; k += 64) C.sbits[k] = 0u;
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int i = 0; i < SVN; ++i)
+      if (lane + 64 * i < m0)
+        __hip_atomic_fetch_or(&C.sbits[sv[i] >> 5], 1u << (sv[i] & 31),
+                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    __builtin_amdgcn_wave_barrier();
+    staged = true;
+  };
+  if (t0 > 0) {
+    uint64_t xw;
+    int nap = 0;
+    const uint64_t t_w = wall_clock64();
+    for (;;) {
+      xw = lb_load(&C.lbw[2 * (t0 - 1)]);
+      if (xw != 0) break;
+      if (wall_clock64() - t_w > FT_WAIT_TICKS) break;   // no speculation
+      if (nap < 16) __builtin_amdgcn_s_sleep(2);
+      else if (nap < 32) __builtin_amdgcn_s_sleep(8);
+      else __builtin_amdgcn_s_sleep(32);
+      ++nap;
+    }
+    // lane s: candidate s, looked up in the window table (the lane owning
+    // position e holds its root in register e / 64)
+    const int32_t v = lane < 5 ? (int32_t)((xw >> (12 * lane)) & 0xFFF) : 0;
+    const bool has = v != 0 && ts + (v - 1) < n;
+    const int32_t e = v - 1;
+    uint32_t we = 0;
+    int64_t xe = FC_DEAD;
+    bool open = false;
+    for (int s = 0; s < 5; ++s) {
+      const int32_t es = __builtin_amdgcn_readlane(e, s);
+      if (!__builtin_amdgcn_readlane((int)has, s)) continue;
+      if (es >= W) {
+        if (lane == s) open = true;
+        continue;
+      }
+      const int jj = es >> 6, ll = es & 63;
+      uint32_t wv = 0;
+      int64_t xv = 0;
+#pragma unroll
+      for (int j = 0; j < WJ; ++j)
+        if (j == jj) { wv = rw[j]; xv = rx[j]; }
+      const uint32_t wsv = (uint32_t)__builtin_amdgcn_readlane((int)wv, ll);
+      const int64_t xsv = (int64_t)(
+          (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)xv,
+                                                         ll) |
+          (uint64_t)(uint32_t)__builtin_amdgcn_readlane(
+              (int)(uint32_t)((uint64_t)xv >> 32), ll) << 32);
+      if (lane == s) {
+        we = wsv;
+        xe = xsv;
+        open = rk_kind(wsv) == RK_SHORT;
+      }
+    }
+    if (__ballot(open)) {
+      restage();
+      for (uint64_t um = __ballot(open); um; um &= um - 1) {
+        const int l = (int)__builtin_ctzll(um);
+        const int32_t el = __builtin_amdgcn_readlane(e, l);
+        const int64_t r = ft_cand(sb, C.sbits, el, nrel, maxp32, send0, n,
+                                  ts, m0, lane);
+        if (lane == l) xe = r;
+      }
+    }
+    if (lane < 5) C.cx[5 * t0 + lane] = xe;
+    const uint64_t hm = __ballot(has);
+    const uint64_t lm = __ballot(has && xe != FC_DEAD);
+    E = -1;
+    if (lm) {
+      const int l = (int)__builtin_ctzll(lm);
+      E = ts + __builtin_amdgcn_readlane(e, l);
+      wE = (uint32_t)__builtin_amdgcn_readlane((int)we, l);
+      known = !__builtin_amdgcn_readlane((int)open, l);
+    } else if (hm) {
+      E = ts + __builtin_amdgcn_readlane(e, (int)__builtin_ctzll(hm));
+    }
+    none = E < 0;
+  } else {
+    wE = rw[0];                 // lane 0's position 0
+    wE = (uint32_t)__builtin_amdgcn_readlane((int)wE, 0);
+    known = true;
+  }
+  const int64_t t_2 = C.dbg ? wall_clock64() : 0;
+
+  // ---- the first tile's records -------------------------------------------
+  FcWalk wk{E, 0, 0, -1, false, false};
+  const int32_t erel = (int32_t)(E - ts);
+  bool done = false;
+  if (!none && erel >= nrel) {
+    fc_join_end(wk, TERM | E, n);
+    done = true;
+  } else if (!none && known && ws != 0 && (wE >> 16) == (ws >> 16) &&
+             (int32_t)rk_cnt(wE) <= m0 && rk_cnt(wE) > 0 &&
+             ft_sv_at<SVN>(sv, m0 - (int32_t)rk_cnt(wE)) == erel) {
+    // the entry is on the survivor's chain: the rest is its list
+    wk.js = m0 - (int32_t)rk_cnt(wE);
+    wk.cnt = (int32_t)rk_cnt(wE);
+    fc_join_end(wk, send0, n);
+    done = true;
+  }
+  if (!done && !none) {
+    // join: walk from the entry (tile t0 back in LDS) until the survivor's
+    // path, as a single tile does
+    restage();
+    int64_t c = E;
+    uint16_t* P = C.pre + t0 * FT_LMAX;
+    int32_t np = 0;
+    uint32_t ent = 0;
+    const int64_t tend = ts + FT_S;
+    for (;;) {
+      if (c >= tend) { wk.exit = c; break; }
+      if (c >= n) { wk.exit = n; break; }
+      const int32_t crel = (int32_t)(c - ts);
+      const uint32_t smw = C.sbits[crel >> 5];
+      const int32_t lraw = lds_be32(sb, crel);
+      if ((smw >> (crel & 31)) & 1u) {
+        const int32_t cw = crel >> 5;
+        int32_t s = 0;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int32_t wi = lane + 64 * h;
+          const uint32_t wd = C.sbits[wi];
+          s += wi < cw ? __popc(wd)
+                       : (wi == cw ? __popc(wd & ((1u << (crel & 31)) - 1u))
+                                   : 0);
+        }
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) s += __shfl_xor(s, d, 64);
+        wk.js = s;
+        break;
+      }
+      const int32_t len = __builtin_amdgcn_readfirstlane(lraw);
+      const int32_t nx = crel + 4 + len;
+      if ((uint32_t)len > (uint32_t)maxp32 || nx > nrel) {
+        wk.exit = c;
+        wk.term = true;
+        wk.bad = (crel + 4 <= nrel) && ((len < 0) | (len > maxp32));
+        break;
+      }
+      ft_record(P, np, ent, crel, lane);
+      c = ts + nx;
+    }
+    if (lane < (np & 63)) P[(np & ~63) + lane] = (uint16_t)ent;
+    wk.np = np;
+    wk.cnt = np;
+    if (wk.js >= 0) {
+      wk.cnt = np + (m0 - wk.js);
+      fc_join_end(wk, send0, n);
+    }
+  } else if (none) {
+    if (m0 > 0) fc_join_end(wk, send0, n);
+    if (lane == 0) fc_stat(C.stats, 1, 1);
+  }
+  if (lane == 0) {
+    C.sx[t0] = send0;
+    C.rcount[t0] = m0;
+    C.rec_entry[t0] = none ? -1 : E;
+    C.rec_exit[t0] = wk.exit;
+    C.rec_meta[t0] = fc_meta(wk);
+    if (C.dbg) {
+      int64_t* d = C.dbg + 8 * t0;
+      d[0] = C.t_0;
+      d[1] = t_1;
+      d[2] = t_2;
+      d[3] = wall_clock64();
+      d[4] = C.t_d;
+      d[5] = (int64_t)C.N | (int64_t)rounds << 16 | (int64_t)done << 24;
+      d[6] = C.t_s;
+      d[7] = t_f;
+    }
+  }
+}
+
+// Tiles t0 + 1 .. of a group the map could not take (too many nodes):
+// no entry, no candidates (fs_link re-walks them).
+ZK_DEV void ft_group_none(const FtCtx& C, int G) {
+  const int64_t ntiles = (C.n + FT_S - 1) / FT_S;
+  for (int k = 1; k < G; ++k) {
+    const int64_t tk = C.t + k;
+    if (tk >= ntiles) break;
+    if (C.lane == 0) {
+      if (k >= 2) lb_store(&C.lbw[2 * (tk - 1)], (uint64_t)1 << 63);
+      C.sx[tk] = -1;
+      C.rcount[tk] = 0;
+      C.rec_entry[tk] = -1;
+      C.rec_exit[tk] = -1;
+      C.rec_meta[tk] = 0;
+    }
+    if (C.lane < 5) C.cx[5 * tk + C.lane] = FC_DEAD;
+    if (C.lane == 0 && (k == G - 1 || tk + 1 >= ntiles))
+      lb_store(&C.lbw[2 * tk], (uint64_t)1 << 63);
+  }
+}
+
+template <int W, bool LONG, int G>
 __global__ __launch_bounds__(256) void fs_tile(
     const uint8_t* __restrict__ buf, const int64_t* __restrict__ n_dev,
     int64_t n_cap, int64_t maxp, uint16_t* __restrict__ list,
@@ -397,40 +1324,36 @@ __global__ __launch_bounds__(256) void fs_tile(
     int64_t* __restrict__ rec_meta, int32_t* __restrict__ rcount,
     int64_t ntiles_cap, int64_t* __restrict__ dbg, int32_t minb,
     int32_t tflags, int64_t* __restrict__ cx) {
-  const bool nospec = tflags & 1;
-  const int32_t misspec = tflags >> 8;
-  constexpr int K = W / 64;                 // window entries per lane
-  constexpr int XW = W / 32;                // candidate words used
-  static_assert(W % 64 == 0 && K >= 1 && K <= 32, "window");
+  static_assert(W % 64 == 0 && W <= 2048, "window");
   // one tile per wave; a block's waves work independently (no barriers),
   // each in its own LDS slice
   extern __shared__ __attribute__((aligned(16))) uint8_t smem_all[];
-  uint8_t* smem = smem_all +
-                  __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) *
-                      FT_LDS;
-  uint8_t* sb = smem;
-  uint32_t* claimed = (uint32_t*)(smem + FT_STAGE);
-  uint32_t* sbits = claimed + FT_BITS;       // survivor frame starts
-  uint16_t* scratch = (uint16_t*)(sbits + FT_BITS);
-  uint32_t* xbits = (uint32_t*)(scratch + 64);    // exits into the next tile
+  const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  uint8_t* smem = smem_all + wv * FT_LDS;
+  FtCtx C;
+  C.sb = smem;
+  uint64_t* bmask = (uint64_t*)(smem + FT_O_BLK);
+  uint16_t* bbase = (uint16_t*)(smem + FT_O_BASE);
+  C.blk.mask = bmask;
+  C.blk.base = bbase;
+  C.pk = (uint32_t*)(smem + FT_O_PK);
+  C.pos = (uint16_t*)(smem + FT_O_R);
+  C.slot = (uint16_t*)(smem + FT_O_R);
+  C.sbits = (uint32_t*)(smem + FT_O_R);
+  C.xbits = (uint32_t*)(smem + FT_O_XB);
   const int lane = threadIdx.x & 63;
   const int64_t n = stream_len(n_dev, n_cap);
   const int64_t ntiles = (n + FT_S - 1) / FT_S;
-  uint64_t* stats = &lbw[2 * ntiles_cap];
-  // Tiles in workgroup order.  (An atomic ticket counter serialised every
-  // wave's start at ~12 ns per ticket — one device-scope atomic address —
-  // and paced the whole scan.)  The wait for the tile before (step 3) is
-  // bounded, so no dispatch order can deadlock it.
-  // (readfirstlane: the wave index is wave-uniform, and saying so keeps
-  // the tile's positions and the walks' control in SGPRs)
-  const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  const int64_t t = (int64_t)blockIdx.x * (blockDim.x >> 6) + wv;
+  // Tiles in workgroup order; the wait for the tile before is bounded, so
+  // no dispatch order can deadlock it.
+  const int64_t t = ((int64_t)blockIdx.x * (blockDim.x >> 6) + wv) * G;
   if (t >= ntiles) return;
-  const int64_t t_0 = dbg ? wall_clock64() : 0;
+  C.t_0 = dbg ? wall_clock64() : 0;
   const int64_t ts = t * FT_S;
   const int64_t tend = ts + FT_S;
   const int32_t nrel = (int32_t)min(n - ts, (int64_t)1 << 30);
   const int32_t maxp32 = (int32_t)maxp;
+  uint8_t* sb = C.sb;
 
   // ---- stage the tile (all loads issued before the first LDS write) ------
   {
@@ -454,338 +1377,91 @@ __global__ __launch_bounds__(256) void fs_tile(
         for (int k = 0; k < 16; ++k) b[k] = tend + k < n ? buf[tend + k] : 0;
       }
     }
-    // window positions start claimed (each by its own walker)
-    for (int k = lane; k < 2 * FT_BITS; k += 64)
-      claimed[k] = k < W / 32 ? 0xFFFFFFFFu : 0u;
-    if (lane < FT_XW) xbits[lane] = 0u;
 #pragma unroll
     for (int j = 0; j < PER; ++j) *(uint4*)(sb + 16 * (lane + 64 * j)) = v[j];
     if (lane == 0) *(uint4*)(sb + FT_S) = pad;
   }
-  const int64_t t_s = dbg ? (__builtin_amdgcn_s_waitcnt(0), wall_clock64()) : 0;
-  // ---- 1. merging frontier ------------------------------------------------
-  // Dense rounds: lane holds walkers e = lane + 64k.  A walker hops, then
-  // claims its landing position with one fetch-or; landing on a claimed
-  // position means merging into that chain, so it stops.  A round is two
-  // LDS round trips (length words, claim) for all K walkers at once.
-  // Every walker that leaves the tile marks its exit in `xbits` when it
-  // lands inside the next tile's window: the candidate entries of the
-  // next tile.  With frames <= W the true chain's exit is always one of
-  // them (whichever walker carries the true chain leaves the tile there).
-  int32_t p[K];
-  uint32_t act = 0;
-#pragma unroll
-  for (int k = 0; k < K; ++k) {
-    p[k] = lane + 64 * k;
-    act |= 1u << k;
-  }
-  // `lastx` = (round << 16 | x) of the latest in-window exit the frontier
-  // took: the preferred candidate when the survivor does not leave
-  uint32_t lastx = 0;
-  int round = 1;
-  int32_t live = W;
-  while (live > 64) {
-    int32_t q[K];
-    int code[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      q[k] = 0;
-      code[k] = (act >> k) & 1 ? ft_hop(sb, p[k], nrel, maxp32, minb, q[k]) : 1;
-    }
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      if (!((act >> k) & 1)) continue;
-      if (code[k] == 0 && ft_claim(claimed, q[k])) {
-        p[k] = q[k];
-      } else {
-        if (code[k] == 2 && ft_mark_exit(xbits, q[k] - FT_S, W))
-          lastx = max(lastx, ((uint32_t)round << 16) | (uint32_t)(q[k] - FT_S));
-        act &= ~(1u << k);
-      }
-    }
-    ++round;
-    int c = __popc(act);
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d, 64);
-    live = c;
-  }
-  // sparse rounds: one walker per lane
-  int32_t mp;
-  bool ma;
-  {
-    uint32_t cnt_before = 0;
-    {
-      const uint32_t mine = __popc(act);
-      uint32_t incl = mine;
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(incl, d, 64);
-        if (lane >= d) incl += y;
-      }
-      cnt_before = incl - mine;
-    }
-    uint32_t o = cnt_before;
-#pragma unroll
-    for (int k = 0; k < K; ++k)
-      if ((act >> k) & 1) scratch[o++] = (uint16_t)p[k];
-    __builtin_amdgcn_wave_barrier();
-    ma = lane < live;
-    mp = ma ? (int32_t)scratch[lane] : 0;
-  }
-  while (live > 1) {
-    int32_t q = 0;
-    const int code = ma ? ft_hop(sb, mp, nrel, maxp32, minb, q) : 1;
-    if (ma) {
-      if (code == 0 && ft_claim(claimed, q)) {
-        mp = q;
-      } else {
-        if (code == 2 && ft_mark_exit(xbits, q - FT_S, W))
-          lastx = max(lastx, ((uint32_t)round << 16) | (uint32_t)(q - FT_S));
-        ma = false;
-      }
-    }
-    ++round;
-    live = __popcll(__ballot(ma));
-  }
-  if constexpr (LONG) {
-    ft_frontier_passes<W>(sb, claimed, xbits, scratch, nrel, maxp32, minb,
-                          lane, lastx, round, mp, ma);
-  }
-  const int64_t t_f = dbg ? wall_clock64() : 0;
-  // ---- 2. the survivor walks to the tile end ------------------------------
-  int64_t send = -1;
-  int32_t m = 0;
-  uint16_t* L = list + t * FT_LMAX;
-  const uint64_t sm = __ballot(ma);
-  if (sm) {
-    const int sl = (int)__builtin_ctzll(sm);
-    int32_t c = __builtin_amdgcn_readlane(mp, sl);
-    uint32_t ent = 0;
-    // The hot loop of the scan (one hop per frame of the tile, serial):
-    // kept to a few scalar compares per hop — one unsigned test covers a
-    // negative or oversize length, one bound (min(tile end, stream end))
-    // both ways out, and the frame start goes into lane m & 63 of `ent`
-    // (a compare and a select).  The rare exits are classified on the way
-    // out.
-    // (The round-2 loop spent ~45 instructions per hop on mixed VALU/SALU
-    // tests; at ~7 waves per SIMD that issue cost, not the LDS latency,
-    // set the ~300 ns per hop measured with ZKMI_FS_DBG.)
-    const int32_t lim = min((int32_t)FT_S, nrel);
-    if (c >= nrel) {
-      send = TERM | (ts + c);                // reached the stream end
-    } else {
-      int32_t len, nx;
-      bool ok;
-      for (;;) {
-        len = __builtin_amdgcn_readfirstlane(lds_be32(sb, c));
-        nx = c + 4 + len;
-        ok = (uint32_t)len <= (uint32_t)maxp32 && nx <= nrel;
-        if (!ok) break;                      // one exit test per hop
-        ent = lane == (m & 63) ? (uint32_t)c : ent;
-        ++m;
-        if ((m & 63) == 0) L[m - 64 + lane] = (uint16_t)ent;
-        if (nx >= lim) break;
-        c = nx;
-      }
-      if (!ok) {
-        const bool bad = (c + 4 <= nrel) && ((len < 0) | (len > maxp32));
-        send = TERM | (bad ? TBAD : 0) | (ts + c);
-      } else if (nx >= FT_S) {
-        send = ts + nx;
-        if (lane == 0) ft_mark_exit(xbits, nx - FT_S, W);
-      } else {
-        send = TERM | (ts + nx);             // the stream ends at nx
-      }
-    }
-    if (lane < (m & 63)) L[(m & ~63) + lane] = (uint16_t)ent;
-    // survivor bit map for the join walk, from the list just stored (each
-    // lane rereads only the entries it wrote itself)
-    for (int i = lane; i < m; i += 64) {
-      const int32_t q = L[i];
-      __hip_atomic_fetch_or(&sbits[q >> 5], 1u << (q & 31), __ATOMIC_RELAXED,
-                            __HIP_MEMORY_SCOPE_WAVEFRONT);
-    }
-  }
-  // ---- 3. publish this tile's exit candidates; take the tile before's -----
-  // preferred candidate: the survivor's exit, else the latest in-window
-  // exit of the frontier (-1: none)
-  int32_t px = -1;
-  // (LONG: the survivor's exit may lie past the window — after a frame
-  // longer than the window the chain resumes there, and the next tile's
-  // frontier passes find it)
-  if (sm && !(send & TERM) && send - tend < (LONG ? FT_S - 1 : W)) {
-    px = (int32_t)(send - tend);
-  } else {
-    uint32_t lx = lastx;
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1)
-      lx = max(lx, (uint32_t)__shfl_xor((int)lx, d, 64));
-    if (lx != 0) px = (int32_t)(lx & 0xFFFF);
-  }
-  // Candidates go out packed in ONE 64-bit word (a relaxed agent-scope
-  // store, like the single exit before: no fence, no L2 write-back on this
-  // multi-XCD part): bit 63 = ready, five 12-bit slots of offset + 1
-  // (0 = empty), slot 0 the preferred one, then up to four other in-window
-  // exits in offset order.
   __builtin_amdgcn_wave_barrier();
-  uint64_t word = (uint64_t)1 << 63;
-  if (px >= 0) word |= (uint64_t)(px + 1);
+  C.t_s = dbg ? (__builtin_amdgcn_s_waitcnt(0), wall_clock64()) : 0;
+
+  // ---- 1. nodes: lane l tests positions 64l .. 64l + 63 ------------------
+  int32_t N;
   {
-    uint32_t xw = lane < XW ? xbits[lane] : 0u;
-    if (px >= 0 && lane == (px >> 5)) xw &= ~(1u << (px & 31));
-    uint64_t any = __ballot(xw != 0);
-    int slot = 1;
-    while (any && slot < 5) {
-      const int wl = (int)__builtin_ctzll(any);
-      uint32_t bits = (uint32_t)__builtin_amdgcn_readlane((int)xw, wl);
-      while (bits && slot < 5) {
-        const int bit = (int)__builtin_ctz(bits);
-        bits &= bits - 1;
-        word |= (uint64_t)(wl * 32 + bit + 1) << (12 * slot);
-        ++slot;
+    const int32_t P0 = lane * 64;
+    uint32_t d[17];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint4 q = *(const uint4*)(sb + P0 + 16 * j);
+      d[4 * j] = q.x; d[4 * j + 1] = q.y; d[4 * j + 2] = q.z;
+      d[4 * j + 3] = q.w;
+    }
+    d[16] = *(const uint32_t*)(sb + P0 + 64);
+    // minb <= len < FT_LIMIT; in the entry window any legal length (a
+    // frame there longer than the tile is still an entry's chain)
+    const uint32_t lim = P0 < W ? (uint32_t)(maxp32 - minb + 1)
+                                : (uint32_t)(FT_LIMIT - minb);
+    uint32_t lo = 0, hi = 0;
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+      const uint32_t v = (uint32_t)be32_of(d[j >> 2], d[(j >> 2) + 1], j);
+      lo |= ((v - (uint32_t)minb) < lim ? 1u : 0u) << j;
+    }
+#pragma unroll
+    for (int j = 32; j < 64; ++j) {
+      const uint32_t v = (uint32_t)be32_of(d[j >> 2], d[(j >> 2) + 1], j);
+      hi |= ((v - (uint32_t)minb) < lim ? 1u : 0u) << (j - 32);
+    }
+    uint64_t mask = (uint64_t)hi << 32 | lo;
+    // a node's length word lies inside the stream
+    const int32_t room = nrel - 4 - P0;      // last position with a header
+    if (room < 63) mask = room < 0 ? 0 : mask & ((2ull << room) - 1);
+    const uint32_t c = (uint32_t)__popcll(mask);
+    uint32_t incl = c;
+#pragma unroll
+    for (int s = 1; s < 64; s <<= 1) {
+      const uint32_t y = __shfl_up(incl, s, 64);
+      if (lane >= s) incl += y;
+    }
+    N = __builtin_amdgcn_readlane((int)incl, 63);
+    const uint32_t base = incl - c;
+    bmask[lane] = mask;
+    bbase[lane] = (uint16_t)base;
+    if (N <= FT_NMAX) {
+      uint32_t k = base;
+      uint64_t m = mask;
+      while (m) {
+        C.pos[k++] = (uint16_t)(P0 + __builtin_ctzll(m));
+        m &= m - 1;
       }
-      any &= any - 1;
     }
   }
-  if (lane == 0) lb_store(&lbw[2 * t], word);    // 0 = not yet
-  const int64_t t_1 = dbg ? wall_clock64() : 0;
-  int64_t E = 0;
-  bool none = false;
-  if (t > 0 && nospec) {
-    // (tests: every tile but the first without a speculated entry, the
-    // worst case of the link repair; no candidate exits either)
-    none = true;
-    if (lane < 5) cx[5 * t + lane] = FC_DEAD;
-  } else if (t > 0) {
-    // Tile t-1 is running or done.  Poll with exponential back-off: these
-    // loads bypass the caches, and thousands of waves polling every few
-    // hundred cycles flood the fabric (it tripled every tile's staging
-    // latency before the back-off).
-    uint64_t x;
-    int nap = 0;
-    const uint64_t t_w = wall_clock64();
-    for (;;) {
-      x = lb_load(&lbw[2 * (t - 1)]);
-      if (x != 0) break;
-      if (wall_clock64() - t_w > FT_WAIT_TICKS) break;   // no speculation
-      switch (nap) {                        // s_sleep takes an immediate
-        case 0: __builtin_amdgcn_s_sleep(2); break;
-        case 1: __builtin_amdgcn_s_sleep(4); break;
-        case 2: __builtin_amdgcn_s_sleep(8); break;
-        case 3: __builtin_amdgcn_s_sleep(16); break;
-        default: __builtin_amdgcn_s_sleep(32); break;
-      }
-      ++nap;
-    }
-    // Pick the entry among the candidates (the tile before's exits that
-    // land here).  A wrong one is a garbage chain of the tile before; read
-    // on in THIS tile it almost always dies on a bad length within a few
-    // hops, while the true chain lives on.  Every candidate is walked (LDS
-    // only, no recording) to where it leaves the tile — meeting the
-    // survivor's path counts as leaving with the survivor — and the first
-    // that survives is the entry.  The exits of all of them go to `cx`:
-    // where two chains both survive tile after tile (a phantom chain: in
-    // the storm's create replies, zxids 0x2Exxxx make the bytes 10 past
-    // each frame start read as the frame length 46), the tile cannot tell
-    // which is true, and fs_link's chase follows the exact one through
-    // this map instead of re-walking every tile.
-    E = -1;
-    int64_t first = -1;
-    for (int slot = 0; slot < 5; ++slot) {
-      const int32_t v = (int32_t)((x >> (12 * slot)) & 0xFFF);
-      int64_t xe = FC_DEAD;
-      if (v != 0 && ts + (v - 1) < n) {
-        const int32_t e = v - 1;
-        if (first < 0) first = ts + e;
-        xe = ft_cand(sb, sbits, e, nrel, maxp32, send, n, ts, m, lane);
-        if (E < 0 && xe != FC_DEAD) E = ts + e;
-      }
-      if (lane == 0) cx[5 * t + slot] = xe;
-    }
-    if (E < 0) E = first;        // no live candidate: the first one
-    // (tests: every misspec-th tile takes a garbage entry one byte past the
-    // chosen one, the link repair's adversary)
-    if (misspec > 0 && t % misspec == 1 && E >= 0 && E + 1 < n) ++E;
-    none = E < 0;
-  }
-  const int64_t t_2 = dbg ? wall_clock64() : 0;
-  // ---- 4. join: walk from the entry until the survivor's path -------------
-  FcWalk w{E, 0, 0, -1, false, false};
-  if (!none) {
-    int64_t c = E;
-    uint16_t* P = pre + t * FT_LMAX;
-    int32_t np = 0;
-    uint32_t ent = 0;
-    for (;;) {
-      if (c >= tend) { w.exit = c; break; }
-      if (c >= n) { w.exit = n; break; }    // the stream ends cleanly
-      const int32_t crel = (int32_t)(c - ts);
-      // both LDS reads of the hop issued together (the survivor map word
-      // and the length word); the map is all zero when m == 0
-      const uint32_t smw = sbits[crel >> 5];
-      const int32_t lraw = lds_be32(sb, crel);
-      if ((smw >> (crel & 31)) & 1u) {
-        // joined: the rest is the survivor's list from this start on; its
-        // index is the number of survivor starts below crel (the map has
-        // FT_BITS = 2 x 64 words, two per lane)
-        static_assert(FT_BITS == 2 * 64, "two map words per lane");
-        const int32_t cw = crel >> 5;
-        int32_t s = 0;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int32_t wi = lane + 64 * h;
-          const uint32_t wd = sbits[wi];
-          s += wi < cw ? __popc(wd)
-                       : (wi == cw ? __popc(wd & ((1u << (crel & 31)) - 1u))
-                                   : 0);
-        }
-#pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) s += __shfl_xor(s, d, 64);
-        w.js = s;
-        break;
-      }
-      const int32_t len = __builtin_amdgcn_readfirstlane(lraw);
-      const int32_t nx = crel + 4 + len;
-      if ((uint32_t)len > (uint32_t)maxp32 || nx > nrel) {
-        w.exit = c;
-        w.term = true;
-        w.bad = (crel + 4 <= nrel) && ((len < 0) | (len > maxp32));
-        break;
-      }
-      ft_record(P, np, ent, crel, lane);
-      c = ts + nx;
-    }
-    if (lane < (np & 63)) P[(np & ~63) + lane] = (uint16_t)ent;
-    w.np = np;
-    w.cnt = np;
-    if (w.js >= 0) {
-      w.cnt = np + (m - w.js);
-      fc_join_end(w, send, n);
+  __builtin_amdgcn_wave_barrier();
+  C.t_d = dbg ? wall_clock64() : 0;
+  C.buf = buf; C.list = list; C.pre = pre; C.sx = sx; C.lbw = lbw;
+  C.rec_entry = rec_entry; C.rec_exit = rec_exit; C.rec_meta = rec_meta;
+  C.rcount = rcount; C.dbg = dbg; C.cx = cx;
+  C.stats = &lbw[2 * ntiles_cap];
+  C.n = n; C.t = t; C.ts = ts; C.tend = tend;
+  C.nrel = nrel; C.maxp32 = maxp32; C.minb = minb; C.N = N;
+  C.nospec = tflags & 1;
+  C.misspec = tflags >> 8;
+  C.lane = lane;
+  // ---- 2-5, with this lane's share of the nodes in registers -------------
+  static_assert(FT_NMAX == 512, "node buckets");
+  if constexpr (G > 1) {
+    static_assert(!LONG, "groups: frames within the window");
+    if (N <= 128) fs_group_rest<W, 2, G>(C);
+    else if (N <= 256) fs_group_rest<W, 4, G>(C);
+    else if (N <= FT_NMAX) fs_group_rest<W, 8, G>(C);
+    else {
+      fs_tile_rest<W, LONG, 1>(C, false);
+      ft_group_none(C, G);
     }
   } else {
-    // no speculated entry: the exit recorded is the survivor's (the likely
-    // one), so fs_link's grid repair of the NEXT tile can start from it in
-    // the same round as this tile's own repair (a run of such tiles settles
-    // in one round, not one tile per round)
-    if (sm) fc_join_end(w, send, n);
-    if (lane == 0) fc_stat(stats, 1, 1);
-  }
-  if (lane == 0) {
-    sx[t] = send;
-    rcount[t] = m;
-    rec_entry[t] = none ? -1 : E;
-    rec_exit[t] = w.exit;
-    rec_meta[t] = fc_meta(w);
-    if (dbg) {
-      dbg[8 * t + 0] = t_0;
-      dbg[8 * t + 1] = t_1;
-      dbg[8 * t + 2] = t_2;
-      dbg[8 * t + 3] = wall_clock64();
-      dbg[8 * t + 4] = w.np;
-      dbg[8 * t + 5] = m;
-      dbg[8 * t + 6] = t_s;
-      dbg[8 * t + 7] = t_f;
-    }
+    if (N <= 128) fs_tile_rest<W, LONG, 2>(C, true);
+    else if (N <= 256) fs_tile_rest<W, LONG, 4>(C, true);
+    else if (N <= FT_NMAX) fs_tile_rest<W, LONG, 8>(C, true);
+    else fs_tile_rest<W, LONG, 1>(C, false);
   }
 }
 
@@ -1974,30 +2650,15 @@ static FsPlan fs_plan(int64_t n) {
   return p;
 }
 
-// ZKMI_FS_MINB: the frontier's minimum plausible body length (default 8;
-// 0 = any length, the round-2 behaviour; A/B only)
-// fs_link's grid (ZKMI_FL_B, 1..FL_B, default 16): every block must find a
-// CU slot before the launch ends, also on the usual path where block 0
-// alone works, so a smaller grid waits less behind another stream's kernel.
-static unsigned fl_blocks() {
-  static int b = -1;
-  if (b < 0) {
-    const char* e = getenv("ZKMI_FL_B");
-    b = e ? atoi(e) : 16;
-    if (b < 1 || b > FL_B) b = FL_B;
-  }
-  return (unsigned)b;
-}
+// fs_link's grid: every block must find a CU slot before the launch ends,
+// also on the usual path where block 0 alone works, so a small grid waits
+// less behind another stream's kernel.
+static unsigned fl_blocks() { return 16; }
 
-static int32_t fs_minb() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("ZKMI_FS_MINB");
-    v = e ? atoi(e) : 8;
-    if (v < 0) v = 0;
-  }
-  return v;
-}
+// The smallest plausible frame body of the tile map's nodes (the smallest
+// ZooKeeper body is 8 bytes: a ping's xid + type).  A real frame that short
+// is still framed exactly (the map sends its chain to the serial walk).
+static int32_t fs_minb() { return 8; }
 
 // scan flag: frames may be longer than the window (fs_tile's frontier
 // passes past the window, and survivor exits past it as candidates)
@@ -2100,19 +2761,31 @@ int zk_frame_scan5(const uint8_t* buf, const int64_t* n_dev, int64_t n_cap,
           hipSuccess)
     return -4;
   int64_t* dbg = fs_dbg_buf(tiles);
-  // ZKMI_FS_TPB: tiles (waves) per block, 1..4 (A/B)
-  static int tpb = -1;
-  if (tpb < 0) {
-    const char* e = getenv("ZKMI_FS_TPB");
-    tpb = e ? atoi(e) : 4;
-    if (tpb < 1 || tpb > 4) tpb = 4;
-  }
-  const unsigned tblocks = (unsigned)((tiles + tpb - 1) / tpb);
+  // tiles (waves) per block: two 12 KiB slices, 6 blocks a CU
+  constexpr int tpb = 2;
+  // tiles a wave: groups (the map once, the chain walked on) for streams
+  // of large frames within a small window; tests of the link repair and
+  // long-frame streams take single tiles
+  int G = ((flags >> 4) & 7) + 1;
+  if ((flags & (FS_LONG | 1 | 0xFFFF00)) || W > 512) G = 1;
+  G = G >= 4 ? 4 : G >= 2 ? 2 : 1;
+  const int64_t waves = (tiles + G - 1) / G;
+  const unsigned tblocks = (unsigned)((waves + tpb - 1) / tpb);
 #define ZK_FS_TILE(WW, LL)                                                   \
-  fs_tile<WW, LL><<<tblocks, 64 * tpb, FT_LDS * tpb, st>>>(                  \
+  fs_tile<WW, LL, 1><<<tblocks, 64 * tpb, FT_LDS * tpb, st>>>(               \
       buf, n_dev, n_cap, maxp, list, pre, sx, lbw, rent, rexit, rmeta, rcnt, \
       tiles, dbg, fs_minb(), flags, cx)
-  if (flags & FS_LONG) {
+#define ZK_FS_GROUP(WW, GG)                                                  \
+  fs_tile<WW, false, GG><<<tblocks, 64 * tpb, FT_LDS * tpb, st>>>(           \
+      buf, n_dev, n_cap, maxp, list, pre, sx, lbw, rent, rexit, rmeta, rcnt, \
+      tiles, dbg, fs_minb(), flags, cx)
+  if (G == 4) {
+    if (W == 256) ZK_FS_GROUP(256, 4);
+    else ZK_FS_GROUP(512, 4);
+  } else if (G == 2) {
+    if (W == 256) ZK_FS_GROUP(256, 2);
+    else ZK_FS_GROUP(512, 2);
+  } else if (flags & FS_LONG) {
     switch (W) {
       case 256: ZK_FS_TILE(256, true); break;
       case 512: ZK_FS_TILE(512, true); break;
@@ -2128,6 +2801,7 @@ int zk_frame_scan5(const uint8_t* buf, const int64_t* n_dev, int64_t n_cap,
     }
   }
 #undef ZK_FS_TILE
+#undef ZK_FS_GROUP
   ZK_LAUNCH_CHECK();
   fs_check<<<(unsigned)((tiles + FK_T - 1) / FK_T), FK_T, 0, st>>>(
       n_dev, n_cap, rent, rexit, rmeta, base, bsum, mins, grid + FL_NB, blist);

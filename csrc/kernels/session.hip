@@ -27,6 +27,17 @@ enum : int32_t { SS_FREE = 0, SS_ALIVE = 1, SS_CLOSED = 2 };
 enum : int32_t { SC_NEW = 0, SC_RESUMED = 1, SC_EXPIRED = 2, SC_REFUSED = 3,
                  SC_BAD = 4, SC_FULL = 5 };
 
+// The table slot of session id s (-1: not one this table can hold).
+ZK_DEV int64_t sess_slot(const ZkSessionTable& tab, int64_t s,
+                         int64_t server_id) {
+  const int64_t srv = (s >> 56) & 0x7f;
+  const int64_t idx = (s & 0x00ffffffffffffffll) - 1;
+  if (idx < 0) return -1;
+  if (tab.span == 0) return srv == server_id && idx < tab.cap ? idx : -1;
+  if (srv < 1 || idx >= tab.span || srv * tab.span > tab.cap) return -1;
+  return (srv - 1) * tab.span + idx;
+}
+
 ZK_DEV uint64_t mix64(uint64_t x) {
   x += 0x9E3779B97F4A7C15ull;
   x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -60,10 +71,11 @@ __global__ __launch_bounds__(SS_T) void session_connect_k(
     } else if (last > *zxid_now) {
       oc = SC_REFUSED;
     } else if (csid == 0) {
-      const int64_t idx = (int64_t)atomicAdd((unsigned long long*)tab.next,
+      const int64_t own = (int64_t)atomicAdd((unsigned long long*)tab.next,
                                              1ull);
-      if (idx < tab.cap) {
-        sid = (server_id << 56) | (idx + 1);
+      const int64_t idx = tab.span ? (server_id - 1) * tab.span + own : own;
+      if (own < (tab.span ? tab.span : tab.cap) && idx < tab.cap) {
+        sid = (server_id << 56) | (own + 1);
         to = min(max(want, min_to), max_to);
         pw0 = mix64((uint64_t)sid ^ secret);
         pw1 = mix64(pw0 ^ secret);
@@ -77,9 +89,10 @@ __global__ __launch_bounds__(SS_T) void session_connect_k(
         oc = SC_FULL;
       }
     } else {
-      const int64_t idx = (csid & 0x00ffffffffffffffll) - 1;
-      bool ok = (csid >> 56) == server_id && idx >= 0 && idx < tab.cap &&
-                idx < *tab.next && pwl == 16;
+      // (an ensemble member knows every member's sessions: the replicated
+      // table; the id equality below rejects a slot never filled)
+      const int64_t idx = sess_slot(tab, csid, server_id);
+      bool ok = idx >= 0 && pwl == 16;
       if (ok) ok = tab.sid[idx] == csid && tab.state[idx] == SS_ALIVE;
       if (ok) {
         uint64_t a, b, c, d;
@@ -118,13 +131,31 @@ __global__ __launch_bounds__(SS_T) void session_connect_k(
 // Close / expire sessions: the table entry dies, so a later resume with its
 // id gets the expired answer.  (The ephemerals go with zk_tree_expire.)
 __global__ __launch_bounds__(SS_T) void session_close_k(
-    ZkSessionTable tab, const int64_t* __restrict__ sids, int64_t n) {
+    ZkSessionTable tab, const int64_t* __restrict__ sids, int64_t n,
+    int64_t server_id) {
   const int64_t i = (int64_t)blockIdx.x * SS_T + threadIdx.x;
   if (i >= n) return;
   const int64_t s = sids[i];
-  const int64_t idx = (s & 0x00ffffffffffffffll) - 1;
-  if (idx >= 0 && idx < tab.cap && idx < *tab.next && tab.sid[idx] == s)
-    tab.state[idx] = SS_CLOSED;
+  const int64_t idx = sess_slot(tab, s, server_id);
+  if (idx >= 0 && tab.sid[idx] == s) tab.state[idx] = SS_CLOSED;
+}
+
+// Install replicated session records {sid, timeout, passwd[16]} (an
+// ensemble's other members' new sessions, R3): ALIVE at their slots.
+__global__ __launch_bounds__(SS_T) void session_install_k(
+    ZkSessionTable tab, const int64_t* __restrict__ rec, int64_t n,
+    int64_t server_id) {
+  const int64_t i = (int64_t)blockIdx.x * SS_T + threadIdx.x;
+  if (i >= n) return;
+  const int64_t* r = rec + 4 * i;
+  const int64_t s = r[0];
+  if (s == 0 || ((s >> 56) & 0x7f) == server_id) return;
+  const int64_t idx = sess_slot(tab, s, 0);
+  if (idx < 0) return;
+  tab.sid[idx] = s;
+  tab.timeout[idx] = (int32_t)r[1];
+  __builtin_memcpy(tab.passwd + idx * 16, &r[2], 16);
+  tab.state[idx] = SS_ALIVE;
 }
 
 }  // namespace zk
@@ -151,10 +182,21 @@ int zk_session_connect(const uint8_t* buf, const int64_t* foff,
 }
 
 int zk_session_close(const ZkSessionTable* tab, const int64_t* sids,
-                     int64_t n, hipStream_t st) {
+                     int64_t n, int64_t server_id, hipStream_t st) {
   if (n <= 0) return 0;
   zk::session_close_k<<<(unsigned)((n + zk::SS_T - 1) / zk::SS_T), zk::SS_T,
-                        0, st>>>(*tab, sids, n);
+                        0, st>>>(*tab, sids, n, server_id);
+  ZK_LAUNCH_CHECK();
+  return 0;
+}
+
+// rec: n records of 4 int64 {sid, timeout, passwd bytes 0-7, 8-15}
+int zk_session_install(const ZkSessionTable* tab, const int64_t* rec,
+                       int64_t n, int64_t server_id, hipStream_t st) {
+  if (n <= 0) return 0;
+  if (tab->span <= 0) return (int)hipErrorInvalidValue;
+  zk::session_install_k<<<(unsigned)((n + zk::SS_T - 1) / zk::SS_T),
+                          zk::SS_T, 0, st>>>(*tab, rec, n, server_id);
   ZK_LAUNCH_CHECK();
   return 0;
 }

@@ -134,6 +134,10 @@ struct ZkSessionTable {
   int32_t* state;     // [cap] SS_*
   int64_t* next;      // [1] allocation counter
   int64_t cap;
+  // 0: one server's table (slot = the id's index).  > 0: an ensemble's
+  // replicated table, `span` slots per member: the session with id
+  // (member << 56 | index + 1) lives at slot (member - 1) * span + index
+  int64_t span;
 };
 
 // ---- launchers (stream-ordered; return 0 or a hipError_t) ----------------
@@ -244,7 +248,9 @@ int zk_session_connect(const uint8_t*, const int64_t*, const int32_t*,
                        int64_t, uint64_t, int32_t, int32_t, const int64_t*,
                        uint8_t*, int64_t*, int32_t*, hipStream_t);
 int zk_session_close(const ZkSessionTable*, const int64_t*, int64_t,
-                     hipStream_t);
+                     int64_t, hipStream_t);
+int zk_session_install(const ZkSessionTable*, const int64_t*, int64_t,
+                       int64_t, hipStream_t);
 int zk_scan_small_i64(const int64_t*, int64_t*, int64_t, int64_t*,
                       hipStream_t);
 }  // extern "C"
@@ -256,7 +262,7 @@ static_assert(sizeof(ZkNodeStore) == 5 * 8, "ZkNodeStore layout");
 static_assert(sizeof(ZkRespBatch) == 10 * 8, "ZkRespBatch layout");
 static_assert(sizeof(ZkReplyOut) == 12 * 8, "ZkReplyOut layout");
 static_assert(sizeof(ZkReqOut) == 12 * 8, "ZkReqOut layout");
-static_assert(sizeof(ZkSessionTable) == 6 * 8, "ZkSessionTable layout");
+static_assert(sizeof(ZkSessionTable) == 7 * 8, "ZkSessionTable layout");
 static_assert(sizeof(ZkTree) == 27 * 8, "ZkTree layout");
 static_assert(offsetof(ZkTree, store) == 9 * 8, "ZkTree.store");
 static_assert(offsetof(ZkTree, free_list) == 14 * 8, "ZkTree.free_list");

@@ -224,7 +224,7 @@ ZkRespBatch resp_batch(const std::vector<Tensor>& v,
 }
 
 // [sid, passwd, timeout, state, next]
-ZkSessionTable session_table(const std::vector<Tensor>& v) {
+ZkSessionTable session_table(const std::vector<Tensor>& v, int64_t span) {
   need(v, 5, "session table");
   const Tensor* r = &v[0];
   const int64_t cap = v[0].numel();
@@ -235,6 +235,8 @@ ZkSessionTable session_table(const std::vector<Tensor>& v) {
   s.state = P<int32_t>(v[3], I32, cap, "sessions.state", r);
   s.next = P<int64_t>(v[4], I64, 1, "sessions.next", r);
   s.cap = cap;
+  TORCH_CHECK(span >= 0 && span <= cap, "zkmi: sessions.span out of range");
+  s.span = span;
   return s;
 }
 
@@ -847,8 +849,9 @@ void session_connect(const Tensor& buf, const Tensor& foff,
                      const std::vector<Tensor>& tab, int64_t server_id,
                      int64_t secret, int64_t min_to, int64_t max_to,
                      const Tensor& zxid_now, const Tensor& out,
-                     const Tensor& resp_sid, const Tensor& outcome) {
-  ZkSessionTable s = session_table(tab);
+                     const Tensor& resp_sid, const Tensor& outcome,
+                     int64_t span) {
+  ZkSessionTable s = session_table(tab, span);
   const Tensor* r = &buf;
   hip_ok(zk_session_connect(
              P<uint8_t>(buf, U8, 1, "buf"),
@@ -863,11 +866,21 @@ void session_connect(const Tensor& buf, const Tensor& foff,
          "session_connect");
 }
 
-void session_close(const std::vector<Tensor>& tab, const Tensor& sids) {
-  ZkSessionTable s = session_table(tab);
+void session_close(const std::vector<Tensor>& tab, const Tensor& sids,
+                   int64_t server_id, int64_t span) {
+  ZkSessionTable s = session_table(tab, span);
   hip_ok(zk_session_close(&s, P<int64_t>(sids, I64, 0, "sids", &tab[0]),
-                          sids.numel(), cur_stream()),
+                          sids.numel(), server_id, cur_stream()),
          "session_close");
+}
+
+void session_install(const std::vector<Tensor>& tab, const Tensor& rec,
+                     int64_t server_id, int64_t span) {
+  ZkSessionTable s = session_table(tab, span);
+  TORCH_CHECK(rec.numel() % 4 == 0, "zkmi: session records are 4 x int64");
+  hip_ok(zk_session_install(&s, P<int64_t>(rec, I64, 0, "records", &tab[0]),
+                            rec.numel() / 4, server_id, cur_stream()),
+         "session_install");
 }
 
 }  // namespace
@@ -973,7 +986,10 @@ TORCH_LIBRARY(zkmi, m) {
   m.def("session_connect(Tensor buf, Tensor frame_off, Tensor frame_len, "
         "Tensor count, int ncap, Tensor(a!)[] table, int server_id, "
         "int secret, int min_to, int max_to, Tensor zxid_now, Tensor(b!) out, "
-        "Tensor(c!) resp_sid, Tensor(d!) outcome) -> ()", &session_connect);
-  m.def("session_close(Tensor(a!)[] table, Tensor sids) -> ()",
-        &session_close);
+        "Tensor(c!) resp_sid, Tensor(d!) outcome, int span=0) -> ()",
+        &session_connect);
+  m.def("session_close(Tensor(a!)[] table, Tensor sids, int server_id=0, "
+        "int span=0) -> ()", &session_close);
+  m.def("session_install(Tensor(a!)[] table, Tensor records, int server_id, "
+        "int span) -> ()", &session_install);
 }

@@ -828,7 +828,8 @@ def test_gpu_storm_pipeline(gpu):
     # 13 steps: 7 sessions born, 6 resumed (5 next to a refused expired
     # one), 6 expired with exactly their two batches
     assert pipe.stats == {'born': 7, 'resumed': 6, 'expired': 6,
-                          'expired_resume_refused': 5}
+                          'expired_resume_refused': 5,
+                          'cross_rank_resumes': 0}
     assert bool(pipe.hs_ok.item())
 
 

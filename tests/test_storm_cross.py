@@ -1,0 +1,78 @@
+"""BASELINE config 5 across GPUs (zkmi/bench/synthetic.py StormPipeline
+with a process group): each rank's session is born on its own member,
+replicated to every member (R3 all-gather into the replicated session
+tables), resumed on the NEXT member (the ConnectRequests go there through
+an all-gather, the answers come back the same way) with the same id and
+password, its second batch created there; its first batch survives the
+move and both go at its expiry, which every member applies; the expired
+session's resume is refused on any member.  Everything is checked on the
+device (the pipeline's reply / handshake / removed-count checks).
+
+Runs world 2 and 3 with gloo on one GPU (ranks share it; RCCL needs one GPU
+per rank).  Reference: lib/zk-session.js:265-339 (reattach to another
+backend), test/multi-node.test.js:233-350 (the ephemeral survives the
+failover), test/nasty.test.js:40-103."""
+
+import socket
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _rank(rank, world, port, q, steps, n):
+    import os
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        from zkmi.bench.synthetic import GpuTree, StormPipeline
+        dev = torch.device('cuda', 0)
+        tree = GpuTree(20000, 37, fanout=100, device=dev, seed=rank,
+                       spare=1.5)
+        pipe = StormPipeline(tree, n, ndirs=64, coll_device='cpu')
+        oks = [int(pipe.step().item()) for _ in range(steps)]
+        # the replicated tables: every member knows every live session
+        sids = pipe.sessions.sid[pipe.sessions.state == 1].cpu().tolist()
+        q.put((rank, oks, dict(pipe.stats), bool(pipe.hs_ok.item()),
+               sorted({s >> 56 for s in sids})))
+    except BaseException as e:          # reported by the parent
+        q.put((rank, repr(e), None, None, None))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('world', [2, 3])
+def test_storm_sessions_move_between_members(gpu, world):
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    steps, n = 8, 2048
+    procs = [ctx.Process(target=_rank, args=(r, world, port, q, steps, n))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(240)
+    res = {}
+    for _ in range(world):
+        r = q.get(timeout=10)
+        res[r[0]] = r[1:]
+    assert all(p.exitcode == 0 for p in procs), res
+    for rank, (oks, st, hs_ok, members) in res.items():
+        assert oks == [n] * steps, (rank, oks)
+        assert hs_ok
+        # steps 1..8 after the birth in __init__: 4 resumes, all on the
+        # next member; 4 births; 4 generations expired (two batches each
+        # on every member), 3 expired resumes refused
+        assert st == {'born': 5, 'resumed': 4, 'expired': 4,
+                      'expired_resume_refused': 3,
+                      'cross_rank_resumes': 4}, (rank, st)
+        # every member's live sessions are in every member's table
+        assert members == list(range(1, world + 1)), (rank, members)

@@ -119,6 +119,7 @@ class GpuTree(object):
                                    n_nodes).astype(np.int32)
             data_bytes = int(data_dist[1])
         self.data_bytes = data_bytes
+        self.data_dist = data_dist
         cap = int(nst * (1 + spare)) + 1024
         self.cap = cap
         enc = [p.encode() for p in paths]
@@ -507,7 +508,10 @@ class GetPipeline(object):
         self.server = GpuServer(tree, n, n * (4 + 16 + 4 + dmax + 68) + 64,
                                 window=B.frame_window(17 + maxpath))
         self.rwindow = B.frame_window(4 + 16 + 4 + dmax + 68)
-        self.rscanner = B.FrameScanner(n, dev, window=self.rwindow)
+        lo, hi = tree.data_dist or (tree.data_bytes, tree.data_bytes)
+        self.rscanner = B.FrameScanner(n, dev, window=self.rwindow,
+                                       frame_hint=4 + 16 + 4 + 68 +
+                                       (lo + hi) // 2)
         self.reply = B.alloc_replies(n, dev)
         self.xid_base = 0
         self.last = None
@@ -673,6 +677,34 @@ MIX_ACLS = (
 )
 
 
+class _GraphCycle(object):
+    """HIP graphs replayed in turn (a workload whose steps rotate through a
+    few shapes: one captured graph per shape)."""
+
+    def __init__(self, graphs):
+        self.graphs = graphs
+        self.i = 0
+
+    def replay(self):
+        self.graphs[self.i].replay()
+        self.i = (self.i + 1) % len(self.graphs)
+
+
+def _capture_steps(pipe, acc, k=1):
+    """Capture ``k`` consecutive steps of ``pipe`` as HIP graphs (run one
+    eager step first: buffers are sized then).  A replay is a step."""
+    dev = pipe.tree.device
+    torch.cuda.synchronize(dev)
+    graphs = []
+    for _ in range(k):
+        g = torch.cuda.CUDAGraph()
+        # thread-local: another thread's HIP calls do not invalidate it
+        with torch.cuda.graph(g, capture_error_mode='thread_local'):
+            pipe.step(acc=acc)
+        graphs.append(g)
+    return graphs[0] if k == 1 else _GraphCycle(graphs)
+
+
 class _Driver(object):
     """Client half shared by the write pipelines: K10 encode of a request
     batch (xids recorded in the HBM xid table), the GPU server, then K1 +
@@ -696,13 +728,15 @@ class _Driver(object):
                                       + 68)
         self.reply = B.alloc_replies(batch, dev)
         self.rscanner = None
-        self.xid_base = 0
-        self.iota = torch.arange(batch, dtype=I32, device=dev)
+        # the session's next xid, on the device: a captured step replays
+        # with new xids
+        self.xid_dev = torch.zeros(1, dtype=I64, device=dev)
+        self.iota = torch.arange(batch, dtype=I64, device=dev)
         self.passes = 0          # > 0: ordered serving in that many passes
 
     def xids(self, n):
-        x = (self.iota[:n] + self.xid_base) & 0x7fffffff
-        self.xid_base = (self.xid_base + n) & 0x7fffffff
+        x = ((self.iota[:n] + self.xid_dev) & 0x7fffffff).to(I32)
+        self.xid_dev.add_(n)
         return x
 
     def create_dirs(self, levels, acl):
@@ -815,6 +849,11 @@ class MixPipeline(object):
         self.step(validate=False, n=m)
         self.step(validate=False, n=2 * m)
 
+    def capture(self, acc):
+        """Three HIP graphs, one per rotation of the generations (step s
+        creates s % 3, sets s - 1, deletes s - 2), replayed in turn."""
+        return _capture_steps(self, acc, 3)
+
     def _batch(self, n, r):
         d = self.drv
         return B.RequestBatch(n, self.opcode[:n], d.xids(n), self.arg[:n],
@@ -908,6 +947,10 @@ class ChainPipeline(object):
             (self.acl_arena, self.acl_off, self.acl_len))
         self.last = None
 
+    def capture(self, acc):
+        """One step as a HIP graph (every step has the same shape)."""
+        return _capture_steps(self, acc)
+
     def step(self, validate=True, acc=None):
         n = self.n
         d = self.drv
@@ -1000,6 +1043,10 @@ class NestPipeline(object):
             (self.acl_arena, self.acl_off, self.acl_len))
         self.last = None
 
+    def capture(self, acc):
+        """One step as a HIP graph (every step has the same shape)."""
+        return _capture_steps(self, acc)
+
     def step(self, validate=True, acc=None):
         n = self.n
         d = self.drv
@@ -1040,13 +1087,18 @@ class GpuSessionTable(object):
 
     MIN_TO, MAX_TO = 4000, 40000        # 2 and 20 ticks of 2 s
 
-    def __init__(self, tree, cap=1 << 16, server_id=1, secret=0x5A4B1D):
+    def __init__(self, tree, cap=1 << 16, server_id=1, secret=0x5A4B1D,
+                 members=1):
         dev = tree.device
         self.tree = tree
         self.dev = dev
         self.cap = cap
         self.server_id = server_id
         self.secret = secret
+        # an ensemble of `members` servers replicates its session table:
+        # member m's sessions live in slots (m - 1) * span ... (see
+        # session.hip); one server's table has no partition
+        self.span = cap // members if members > 1 else 0
         self.sid = torch.zeros(cap, dtype=I64, device=dev)
         self.passwd = torch.zeros(cap * 16, dtype=U8, device=dev)
         self.timeout = torch.zeros(cap, dtype=I32, device=dev)
@@ -1073,13 +1125,21 @@ class GpuSessionTable(object):
             rx, ft.off, ft.length, ft.count, 64, self._tensors,
             self.server_id, _i64(self.secret), self.MIN_TO, self.MAX_TO,
             self.tree.counters[_lib.TC_ZXID:], self.resp, self.resp_sid,
-            self.outcome)
+            self.outcome, self.span)
         self.allocated += n_new
         return self.resp, self.resp_sid, self.outcome
 
     def close(self, sids):
         """Expire / close sessions (device int64 tensor of ids)."""
-        _lib.lib().session_close(self._tensors, sids)
+        _lib.lib().session_close(self._tensors, sids, self.server_id,
+                                 self.span)
+
+    def install(self, records):
+        """Replicate other members' sessions into this table (device int64
+        [k, 4]: sid, timeout, password bytes 0-7 and 8-15; this member's own
+        records are skipped) — the receiving end of R3."""
+        _lib.lib().session_install(self._tensors, records, self.server_id,
+                                   self.span)
 
 
 class StormPipeline(object):
@@ -1108,18 +1168,53 @@ class StormPipeline(object):
     Every check (replies, handshake outcome, ids, password, removed count)
     runs on the device; a step makes no device-to-host read.  The hash
     index is rebuilt whenever the tombstones left by never-reused sequential
-    names would fill it."""
+    names would fill it.
+
+    Across GPUs (a process group of ``world`` > 1 ranks: the members of one
+    ensemble, each rank's GPU server a member) the session MOVES, as
+    ``lib/zk-session.js:265-339`` reattaches it to another backend and
+    ``test/multi-node.test.js:233-350`` checks that its ephemeral survives:
+    session k of rank r is born on member r, and its records {id, timeout,
+    password} go to every member (R3: one ``all_gather_into_tensor`` of
+    the step's new sessions, installed into each member's replicated
+    table).  At step 2k+1 rank r's client resumes it on member (r+1) %
+    world: its ConnectRequests travel there and the ConnectResponses back
+    through two small all-gathers, member r+1 answers RESUMED with the same
+    id and password, and the session's second batch is created on member
+    r+1.  Its first batch survives the move on member r; at its expiry
+    every member drops what the session created there (so each removes two
+    sessions' batches: its own session's first and its neighbour's second)
+    and closes it in its table, so the expired resume tried at the next
+    move is refused on any member."""
 
     TIMEOUT = 30000
+    HS_SLOT = 128            # handshake bytes a rank sends per all-gather
 
-    def __init__(self, tree, batch, ndirs=1024, data_bytes=16, seed=0):
+    def __init__(self, tree, batch, ndirs=1024, data_bytes=16, seed=0,
+                 group=None, coll_device=None):
+        import torch.distributed as dist
         dev = tree.device
         self.tree = tree
         self.dev = dev
         self.n = batch
         self.ndirs = ndirs
+        on = dist.is_available() and dist.is_initialized()
+        self.dist = dist
+        self.group = group
+        self.world = W = dist.get_world_size(group) if on else 1
+        self.rank = dist.get_rank(group) if on else 0
+        self.coll = torch.device(coll_device) if coll_device else dev
         self.drv = _Driver(tree, batch, 32, data_bytes, seed)
-        self.sessions = GpuSessionTable(tree)
+        self.sessions = GpuSessionTable(tree, server_id=self.rank + 1,
+                                        members=W)
+        if W > 1:
+            # this step's new sessions of every member ([W, 4] records),
+            # the generation before's (expired at the next birth), and the
+            # handshake slots
+            self.recs = torch.zeros(W, 4, dtype=I64, device=dev)
+            self.prev_recs = torch.zeros(W, 4, dtype=I64, device=dev)
+            self.hs_out = torch.zeros(self.HS_SLOT, dtype=U8, device=dev)
+            self.hs_all = torch.zeros(W * self.HS_SLOT, dtype=U8, device=dev)
         prefixes = ['/storm/d%05d/e-' % (k % ndirs) for k in range(batch)]
         self.path_arena, self.path_off, self.path_len = _arena(prefixes, dev)
         self.data_arena = torch.full((data_bytes + 16,), 0x5a, dtype=U8,
@@ -1165,7 +1260,7 @@ class StormPipeline(object):
         self.step_no = 0
         self.inserted = 0
         self.stats = {'born': 0, 'resumed': 0, 'expired': 0,
-                      'expired_resume_refused': 0}
+                      'expired_resume_refused': 0, 'cross_rank_resumes': 0}
         self.drv.create_dirs(
             [['/storm'], ['/storm/d%05d' % d for d in range(ndirs)]],
             (self.acl_arena, self.acl_off, self.acl_len))
@@ -1173,11 +1268,29 @@ class StormPipeline(object):
 
     # -- the client / server handshake, all on the device ---------------------
 
+    def _gather(self, out, inp):
+        """``all_gather_into_tensor`` on the collective device."""
+        if self.coll == self.dev:
+            self.dist.all_gather_into_tensor(out, inp, group=self.group)
+            return out
+        o = torch.empty(out.shape, dtype=out.dtype, device=self.coll)
+        self.dist.all_gather_into_tensor(o, inp.to(self.coll),
+                                         group=self.group)
+        out.copy_(o)
+        return out
+
+    def sid(self, member, k):
+        """Session id of member ``member``'s k-th session (every member
+        allocates one a birth step, so ids are known on every rank)."""
+        return ((member + 1) << 56) | (k + 1)
+
     def _handshake(self, resume):
         """K9 client encode -> K9 server handshake -> K9 client decode.
         Birth: one request (id 0, 8 zero password bytes as zkstream sends,
         lib/zk-session.js:59).  Resume: [current session, the session that
-        expired last step] with their ids and passwords."""
+        expired last step] with their ids and passwords — on the next
+        member when the ensemble spans GPUs (the frames go there and the
+        answers come back through all-gathers)."""
         L = _lib.lib()
         # the first session has no expired predecessor to try
         m = 2 if resume and self.k >= 1 else 1
@@ -1193,9 +1306,30 @@ class StormPipeline(object):
         L.encode_connect_requests(proto, zx, tmo, sid, pwo, pwlt, arena, m,
                                   sizes, off, total, self.cr_ws, self.cr_tx)
         nbytes = m * (32 + pwl)
+        rb = m * _lib.CR_RESP_BYTES
+        W = self.world
+        if resume and W > 1:
+            # to member r + 1: every rank's frames gathered, each serves
+            # the previous rank's, the answers gathered back
+            S = self.HS_SLOT
+            self.hs_out[:nbytes].copy_(self.cr_tx[:nbytes])
+            self._gather(self.hs_all, self.hs_out)
+            src = (self.rank - 1) % W
+            rx = self.hs_all[src * S:src * S + nbytes].clone()
+            resp, bound, outcome = self.sessions.connect(rx, nbytes, 0)
+            self.hs_out[:rb].copy_(resp[:rb])
+            self._gather(self.hs_all, self.hs_out)
+            dst = (self.rank + 1) % W
+            resp = self.hs_all[dst * S:dst * S + rb].clone()
+            ft = self.rscan.scan(resp, rb)
+            o = B.decode_connect_responses(resp, ft, m)
+            # (`outcome`: how this member answered the previous rank's
+            # client — every member checks the one it served, the client
+            # checks the answer it got)
+            self.stats['cross_rank_resumes'] += 1
+            return o, bound, outcome, resp
         resp, bound, outcome = self.sessions.connect(
             self.cr_tx[:nbytes], nbytes, 0 if resume else 1)
-        rb = m * _lib.CR_RESP_BYTES
         ft = self.rscan.scan(resp[:rb], rb)
         o = B.decode_connect_responses(resp, ft, m)
         return o, bound, outcome, resp
@@ -1236,8 +1370,19 @@ class StormPipeline(object):
             self.cred_sid[0:1].copy_(o['sessionId'][0:1])
             self.cred_pw[0:16].copy_(resp[24:40])
             self.stats['born'] += 1
+            if self.world > 1:
+                # R3: every member's new session to every member
+                self.prev_recs.copy_(self.recs)
+                mine = torch.cat([o['sessionId'][0:1],
+                                  o['timeOut'][0:1].to(I64),
+                                  resp[24:40].view(I64)])
+                self._gather(self.recs.view(-1), mine)
+                self.sessions.install(self.recs)
         self.hs_ok &= ok
-        cur = self.sessions.sid_of(self.k)
+        # the session this member serves now: its own new one, or after a
+        # move the previous member's
+        cur = self.sid((self.rank - (1 if resume else 0)) % self.world,
+                       self.k)
         rb = B.RequestBatch(n, self.opcode, self.drv.xids(n), self.arg,
                             self.path_off, self.path_len, self.data_off,
                             self.data_len, self.acl_id, self.path_arena,
@@ -1249,7 +1394,18 @@ class StormPipeline(object):
         torch.maximum(self.last_zxid, rep.zxid[:n].max().view(1),
                       out=self.last_zxid)
         expire_ok = True
-        if not resume and self.k >= 1:
+        if not resume and self.k >= 1 and self.world > 1:
+            # the generation before expires on every member: here its first
+            # batch (our session) and its second (the previous member's,
+            # which moved here); every member closes all of them
+            self.removed.zero_()
+            t.expire(self.sid(self.rank, self.k - 1), self.removed)
+            t.expire(self.sid((self.rank - 1) % self.world, self.k - 1),
+                     self.removed)
+            self.sessions.close(self.prev_recs[:, 0].contiguous())
+            self.stats['expired'] += 1
+            expire_ok = self.removed[0] == 2 * n
+        elif not resume and self.k >= 1:
             # the previous session expires: both of its batches go
             prev = self.sessions.sid_of(self.k - 1)
             self.removed.zero_()

@@ -355,9 +355,15 @@ class FrameScanner:
     instead of four allocations."""
 
     def __init__(self, cap, device, window=2048,
-                 max_packet=consts.MAX_PACKET):
+                 max_packet=consts.MAX_PACKET, frame_hint=None, group=None):
         self.cap = cap
         self.window = window
+        # the stream's usual frame size: >= 128 bytes within a small window
+        # lets a wave take a group of tiles (the chain map once, then the
+        # chain walked on; csrc/kernels/frame_scan.hip fs_group_rest)
+        if group is None:
+            group = 4 if frame_hint is not None and frame_hint >= 128 else 1
+        self.group = group
         self.max_packet = max_packet
         self.table = FrameTable(torch.empty(cap, dtype=I64, device=device),
                                 torch.empty(cap, dtype=I32, device=device),
@@ -388,7 +394,8 @@ class FrameScanner:
             L.frame_scan(buf, n_dev, ncap, self.max_packet, self.ws, t.off,
                          t.length, t.result, int(self.window),
                          ncap == self.clean_for,
-                         (1 if nospec else 0) | (int(misspec) << 8))
+                         (1 if nospec else 0) | (int(misspec) << 8) |
+                         ((self.group - 1) << 4))
         self.clean_for = ncap
         self.last_cap = ncap
         return t

@@ -166,9 +166,15 @@ class EnsembleWorkload(object):
         servers = [{'address': '127.0.0.1', 'port': ports[(me + k) % n]}
                    for k in range(n)]
         # (a member that went down is retried after 5 ms, not the 50-100
-        # ms of an interactive client: the failover is the measured step)
+        # ms of an interactive client: the failover is the measured step.
+        # A ping may wait up to 3/4 of the session timeout: a busy host
+        # that stalls the client's loop for a second or two must not fail
+        # a healthy connection over — that extra move would resume the
+        # session's watches at a lastZxid older than events it had already
+        # forwarded, and the member would replay them a second time.)
         cfg = ClientConfig(
-            ping_floor_ms=500, ping_timeout_floor_ms=2000,
+            ping_floor_ms=500,
+            ping_timeout_floor_ms=max(2000, session_timeout * 3 // 4),
             connect_policy=RecoveryPolicy(1000, 3, 5, 100),
             default_policy=RecoveryPolicy(1000, 3, 5, 100),
             codec_device=str(codec_device) if codec_device else None)

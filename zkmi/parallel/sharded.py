@@ -25,12 +25,16 @@ on rank ``r`` is, per pipelined connection:
 
 A step makes **no device-to-host read**: every length the kernels need
 travels in the slot headers, so with RCCL the whole step (collectives
-included) is stream-ordered device work.  Slots are sized for the expected
-share of a uniform hash plus a wide margin (``n/W + 6 sqrt(n/W) + 64``
-records); a segment that would not fit is sent empty and counted, so the
-reply check fails loudly instead of reading past a slot.  With one rank
-there is nothing to route: the step is the local GET pipeline (no router,
-no slots) and is HIP-graph captured.
+included) is stream-ordered device work, and it is captured as one HIP
+graph, RCCL collectives included (the step replays with one host call).
+Slots are sized for the expected share of a uniform hash plus a wide
+margin (``n/W + 6 sqrt(n/W) + 64`` records); a segment that would not
+fit is sent empty and counted, so the reply check fails loudly instead of
+reading past a slot.  With one rank there is nothing to route: the step
+is the local GET pipeline (no router, no slots), unless ``force_route``:
+then the W > 1 step runs as is over a one-rank RCCL group (route ->
+seg_pack -> all_to_all_single -> seg_unpack on HBM tensors), which
+executes and captures the multi-rank code path on one GPU.
 
 Each rank's :class:`~zkmi.bench.synthetic.GpuTree` indexes only its shard
 (``shard=(rank, world)``): a read that reached the wrong rank would answer
@@ -57,6 +61,20 @@ def _r16(x):
     return (int(x) + 15) & ~15
 
 
+# xGMI: 7 point-to-point links per MI355X, ~153 GB/s each, both directions
+# together (cdna guides): one direction of one link
+XGMI_LINK_GBS = 76.5
+
+
+def xgmi_lower_bound_ms(slot_bytes, world):
+    """A lower bound on one step's all-to-all time: every rank sends one
+    slot to each peer over that peer's own link, all links at once, so a
+    step's collectives need at least ``sum(slot bytes) / one link``."""
+    if world <= 1:
+        return 0.0
+    return sum(slot_bytes) / (XGMI_LINK_GBS * 1e9) * 1e3
+
+
 def slot_records(n, world):
     """Records one per-peer slot holds: the uniform share plus 6 standard
     deviations and a constant margin (a hash split of ``n`` requests over
@@ -76,11 +94,16 @@ class ShardedGetPipeline(object):
     PHASES = 6
 
     def __init__(self, tree, batch, seed=0, group=None, coll_device=None,
-                 streams=1):
+                 streams=1, force_route=False):
         on = dist.is_available() and dist.is_initialized()
         self.group = group
         self.world = W = dist.get_world_size(group) if on else 1
         self.rank = dist.get_rank(group) if on else 0
+        if force_route and not on:
+            raise ValueError('force_route needs a process group')
+        # the multi-rank step (router, slots, all-to-alls): always with
+        # more than one rank, and on one rank when forced
+        self.route = W > 1 or force_route
         if tree.shard is not None and tuple(tree.shard) != (self.rank, W):
             raise ValueError('tree shard %r on rank %d of %d'
                              % (tree.shard, self.rank, W))
@@ -122,14 +145,14 @@ class ShardedGetPipeline(object):
 
     @property
     def capturable(self):
-        """One rank: the whole step is device work on our streams.  With
-        RCCL the collectives are stream-ordered too, but their capture into
-        a HIP graph is not exercised here, so multi-rank steps run eager."""
-        return self.world == 1
+        """The whole step is device work on our streams when the
+        collectives run on the device (RCCL): it is captured with them.  A
+        gloo rehearsal stages through the host and runs eager."""
+        return not self.route or self.coll == self.dev
 
     def capture(self, acc):
         if not self.capturable:
-            raise RuntimeError('multi-rank sharded steps run eager')
+            raise RuntimeError('host-staged collectives run eager')
         for c in self.subs:
             c.device_seed()
         torch.cuda.synchronize(self.dev)
@@ -185,11 +208,13 @@ class ShardedGetPipeline(object):
         W = self.world
         wire = sum((W - 1) * (c.req_slot + c.rep_slot) for c in self.subs) \
             * self.steps if W > 1 else 0
+        slots = [b for c in self.subs for b in (c.req_slot, c.rep_slot)]
         return {'bytes_sent': rq[1] + rp[1], 'bytes_recv': rv[0],
                 'remote_reqs': rq[2], 'overflow_segments': rq[0] + rp[0],
                 'wire_bytes_sent': wire, 'steps': self.steps,
                 'req_slot_bytes': [c.req_slot for c in self.subs],
-                'rep_slot_bytes': [c.rep_slot for c in self.subs]}
+                'rep_slot_bytes': [c.rep_slot for c in self.subs],
+                'xgmi_lower_bound_ms': xgmi_lower_bound_ms(slots, W)}
 
 
 class _Conn(object):
@@ -212,7 +237,7 @@ class _Conn(object):
         e64 = lambda: torch.empty(n, dtype=I64, device=dev)   # noqa: E731
         e32 = lambda: torch.empty(n, dtype=I32, device=dev)   # noqa: E731
         self.idx, self.xid, self.poff, self.plen = e64(), e32(), e64(), e32()
-        if W > 1:
+        if pipe.route:
             self.idx_s, self.xid_s, self.poff_s, self.plen_s = (
                 e64(), e32(), e64(), e32())
             self.owner = e32()
@@ -242,10 +267,13 @@ class _Conn(object):
         self.server = GpuServer(t, cap, cap * self.rep_max + 64,
                                 window=B.frame_window(self.req_max))
         # the replies to this connection's own n requests come back
+        lo, hi = t.data_dist or (t.data_bytes, t.data_bytes)
         self.rscanner = B.FrameScanner(n, dev,
-                                       window=B.frame_window(self.rep_max))
+                                       window=B.frame_window(self.rep_max),
+                                       frame_hint=4 + 16 + 4 + 68 +
+                                       (lo + hi) // 2)
         self.reply = B.alloc_replies(n, dev)
-        if W > 1:
+        if pipe.route:
             u8 = lambda m: torch.empty(m, dtype=U8, device=dev)  # noqa: E731
             self.sq, self.rq = u8(W * self.req_slot), u8(W * self.req_slot)
             self.sp, self.rp = u8(W * self.rep_slot), u8(W * self.rep_slot)
@@ -284,7 +312,7 @@ class _Conn(object):
                         t.node_pw, self.idx, self.xid, self.poff, self.plen,
                         self.gstate)
         self.xid_base = (self.xid_base + n) & 0x7fffffff
-        if W > 1:
+        if p.route:
             L.route_requests(n, W, self.poff, self.plen, t.path_arena,
                              self.idx, self.xid, self.owner, self.idx_s,
                              self.xid_s, self.poff_s, self.plen_s,
@@ -294,14 +322,14 @@ class _Conn(object):
                             self.zero32, self.zero32, t.path_arena, t.slab,
                             self.acl_off, self.acl_len, self.acl_arena)
         tx, rec_off, total, _ = B.encode_requests(rb, self.xt, out=self.tx)
-        if W > 1:
+        if p.route:
             L.seg_pack(tx, rec_off, None, n, total, self.counts, W, p.rank,
                        self.req_slot, self.sq, p.req_stats)
         yield
-        if W > 1:
+        if p.route:
             p.a2a(self.rq, self.sq)
         yield
-        if W > 1:
+        if p.route:
             L.seg_unpack(self.rq, W, p.rank, self.req_slot, self.rxq,
                          self.nrx, self.src_counts, None)
             rxq, nrx = self.rxq, self.nrx
@@ -313,17 +341,17 @@ class _Conn(object):
         for _ in srv:
             pass
         rout, rtotal, _, ft = self.server.result
-        if W > 1:
+        if p.route:
             # replies in request order = source rank order; the source
             # counts came with the request slots' headers
             L.seg_pack(rout, self.server.last_rec_off, ft.count,
                        self.server.cap_frames, rtotal, self.src_counts, W,
                        p.rank, self.rep_slot, self.sp, p.rep_stats)
         yield
-        if W > 1:
+        if p.route:
             p.a2a(self.rp, self.sp)
         yield
-        if W > 1:
+        if p.route:
             L.seg_unpack(self.rp, W, p.rank, self.rep_slot, self.crx,
                          self.ncrx, self.back_counts, p.recv_stats)
             crx, ncrx = self.crx, self.ncrx

@@ -24,7 +24,15 @@
 //                                      port, then apply the sets (firing
 //                                      watches); answers "OK <zxid>"
 //   start <i>                          listen on member i's port again
+//   timing [reset]                     the wire clock below (any M)
 //
+// The wire clock (CLOCK_MONOTONIC ns, the clock of Python's perf_counter
+// on Linux, so a client can line its own stamps up with it): first / last
+// recv that returned bytes, first / last send that moved bytes, and the
+// sums of time in recv(), in serving frames (tree lock + replies), in
+// send() and with replies waiting for the socket to drain (EAGAIN until the
+// next send that moves bytes); bytes in / out and bursts served.  "timing"
+// answers "OK" and those 13 numbers, "timing reset" zeroes them.
 // Notifications to a connection served by another worker go through that
 // connection's note buffer (its own mutex) and the worker's eventfd; every
 // burst drains the notes before serving, so a notification always precedes
@@ -56,6 +64,7 @@
 #include <sys/epoll.h>
 #include <sys/socket.h>
 #include <sys/time.h>
+#include <time.h>
 #include <unistd.h>
 
 #include <cstdint>
@@ -95,6 +104,37 @@ enum : int32_t {
   E_NODE_EXISTS = -110, E_NOT_EMPTY = -111
 };
 constexpr int32_t MAX_PACKET = 16 * 1024 * 1024;
+
+int64_t mono_ns() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return (int64_t)ts.tv_sec * 1000000000 + ts.tv_nsec;
+}
+
+// The wire clock (header comment): all fields atomics, workers add to them
+struct WireClock {
+  enum { FIRST_RX, LAST_RX, FIRST_TX, LAST_TX, RECV, SERVE, SEND, BLOCKED,
+         RX_BYTES, TX_BYTES, BURSTS, SENDS, RECVS, N };
+  std::atomic<int64_t> v[N];
+  WireClock() { reset(); }
+  void reset() { for (auto& x : v) x.store(0, std::memory_order_relaxed); }
+  void add(int k, int64_t d) { v[k].fetch_add(d, std::memory_order_relaxed); }
+  void first(int k, int64_t t) {
+    int64_t z = 0;
+    v[k].compare_exchange_strong(z, t, std::memory_order_relaxed);
+  }
+  void last(int k, int64_t t) {
+    int64_t o = v[k].load(std::memory_order_relaxed);
+    while (o < t && !v[k].compare_exchange_weak(o, t,
+                                                std::memory_order_relaxed)) {}
+  }
+  std::string report() {
+    std::string r = "OK";
+    for (auto& x : v) r += " " + std::to_string((long long)x.load());
+    return r;
+  }
+};
+WireClock wclock;
 
 int64_t now_ms() {
   timeval tv;
@@ -193,6 +233,7 @@ struct Conn {
   int64_t sid = 0;
   std::string in, out;
   size_t in_off = 0, out_off = 0;
+  int64_t t_block = 0;   // replies waiting for the socket since (wire clock)
   Worker* w = nullptr;
   std::mutex nmu;        // notes: notifications from other workers' writes
   std::string notes;
@@ -689,14 +730,33 @@ void preload(Server& S, int64_t n, int32_t dbytes, int32_t fanout) {
 }
 
 bool flush_out(Conn& c) {
+  if (c.out_off >= c.out.size()) return true;
+  int64_t t = mono_ns();
+  if (c.t_block) { wclock.add(WireClock::BLOCKED, t - c.t_block); c.t_block = 0; }
+  bool ok = true;
   while (c.out_off < c.out.size()) {
     ssize_t k = send(c.fd, c.out.data() + c.out_off, c.out.size() - c.out_off,
                      MSG_NOSIGNAL | MSG_DONTWAIT);
-    if (k > 0) { c.out_off += (size_t)k; continue; }
-    if (k < 0 && errno == EINTR) continue;
-    if (k < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) return true;
-    return false;
+    const int64_t t1 = mono_ns();
+    wclock.add(WireClock::SEND, t1 - t);
+    wclock.add(WireClock::SENDS, 1);
+    if (k > 0) {
+      c.out_off += (size_t)k;
+      wclock.add(WireClock::TX_BYTES, k);
+      wclock.first(WireClock::FIRST_TX, t1);
+      wclock.last(WireClock::LAST_TX, t1);
+      t = t1;
+      continue;
+    }
+    if (k < 0 && errno == EINTR) { t = t1; continue; }
+    if (k < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) {
+      c.t_block = t1;
+      return true;
+    }
+    ok = false;
+    break;
   }
+  if (!ok) return false;
   c.out.clear();
   c.out_off = 0;
   return true;
@@ -861,9 +921,20 @@ struct Worker {
         Conn& c = *it->second;
         bool dead = false;
         if (evs[k].events & (EPOLLIN | EPOLLRDHUP | EPOLLHUP | EPOLLERR)) {
+          int64_t t = mono_ns();
           for (;;) {
             ssize_t m = recv(fd, rbuf.data(), rbuf.size(), MSG_DONTWAIT);
-            if (m > 0) { c.in.append(rbuf.data(), (size_t)m); continue; }
+            const int64_t t1 = mono_ns();
+            wclock.add(WireClock::RECV, t1 - t);
+            wclock.add(WireClock::RECVS, 1);
+            t = t1;
+            if (m > 0) {
+              c.in.append(rbuf.data(), (size_t)m);
+              wclock.add(WireClock::RX_BYTES, m);
+              wclock.first(WireClock::FIRST_RX, t1);
+              wclock.last(WireClock::LAST_RX, t1);
+              continue;
+            }
             if (m == 0) { dead = true; break; }
             if (errno == EINTR) continue;
             if (errno != EAGAIN && errno != EWOULDBLOCK) dead = true;
@@ -876,6 +947,9 @@ struct Worker {
             if (!serve_burst(c)) { dead = true; break; }
             if (c.in_off == before || c.closing) break;
           }
+          const int64_t t2 = mono_ns();
+          wclock.add(WireClock::SERVE, t2 - t);
+          wclock.add(WireClock::BURSTS, 1);
           if (c.in_off == c.in.size()) { c.in.clear(); c.in_off = 0; }
           else if (c.in_off > (1u << 20)) { c.in.erase(0, c.in_off); c.in_off = 0; }
         }
@@ -965,6 +1039,10 @@ std::string command(Server& S, std::vector<Member>& mem, int ep,
     i = j;
   }
   if (f.empty()) return "ERR empty";
+  if (f[0] == "timing") {
+    if (f.size() > 1 && f[1] == "reset") { wclock.reset(); return "OK"; }
+    return wclock.report();
+  }
   if (f.size() < 2) return "ERR missing member";
   const int m = atoi(f[1].c_str());
   if (m < 0 || m >= (int)mem.size()) return "ERR no such member";

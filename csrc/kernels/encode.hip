@@ -271,12 +271,28 @@ ZK_DEV uint32_t vword(const uint4* v, int k) {
 // GET_DATA replies with up to this much data are emitted from registers.
 constexpr int GET_REG_DATA = 128;
 
+// hole > 0 (a large GET_DATA reply, see staged_emit_holes): the [len | data]
+// bytes [pre, pre + hole) are left out; the waves copy them slot -> out.
 template <class K>
 ZK_DEV void emit_response(K& k, const ZkRespBatch& r, const ZkNodeStore& s,
-                          int64_t i, int64_t body) {
+                          int64_t i, int64_t body, int64_t pre = 0,
+                          int64_t hole = 0) {
   const int32_t xid = r.xid[i], err = r.err[i], op = r.opcode[i];
   const int64_t zxid = r.zxid[i];
   const int64_t nd = body - 16 - STAT_BYTES;          // GET: 4 + data length
+  if (hole > 0) {
+    const uint8_t* slot = s.slab + (r.slot ? r.slot[i]
+                                           : s.slot_off[r.node[i]]);
+    k.be32((int32_t)body);
+    k.be32(xid);
+    k.be64(zxid);
+    k.be32(err);
+    k.bytes(slot + ZK_SLOT_LEN, pre);
+    k.bytes(slot + ZK_SLOT_LEN + pre + hole, nd - pre - hole);
+    k.bytes(slot + ZK_SLOT_STAT, STAT_BYTES);
+    k.finish();
+    return;
+  }
   if (err == ERR_OK && op == OP_GET_DATA && nd <= 4 + GET_REG_DATA) {
     // Fast path: every load of the record is issued before the first
     // sink write (the generic copy below waits on each 16-byte load in
@@ -455,6 +471,148 @@ ZK_DEV void put_terminator(bool term, const int64_t* total, uint8_t* out,
   if (T + 4 <= cap) st_be32(out + T, -1);
 }
 
+// ---- K13: large GET_DATA replies --------------------------------------------
+// A reply's [len | data] bytes sit at out [q0, q0 + nd), q0 = off + 20.  When
+// their 16-byte aligned interior [h0, h1) holds at least BIG_HOLE bytes it
+// is a HOLE: left out of the block's LDS image and copied slot -> out by the
+// waves, one reply per wave-iteration (64 lanes x 16 bytes, stores
+// coalesced), instead of by the reply's own lane one dword at a time (one
+// lane per record left a wave as slow as its longest record and a 28 KiB
+// image held ~46 replies of ~600 B, so most of a block's lanes idled).  The
+// image keeps the rest of every record — headers, the data's unaligned head
+// and tail, Stats — in COMPACTED coordinates (out offset minus the holes
+// before it; holes are multiples of 16, so 16-byte vectors stay aligned),
+// and a run is streamed out segment by segment between its holes.
+constexpr int64_t BIG_HOLE = 256;
+
+struct EncHoles {
+  int64_t hb[ENC_T];        // (holes before record k, block-exclusive) << 9
+                            // | big records before it
+  int32_t hole[ENC_T];      // record k's hole bytes (0: none)
+  int16_t bl[ENC_T];        // the block's big records in order (-1: written
+                            // whole, not a hole)
+};
+
+ZK_DEV int64_t hole_h0(int64_t off) { return (off + 20 + 15) & ~(int64_t)15; }
+
+// Stream a run's compacted image out: segment k (0..K) runs between the
+// holes of the run's big records k-1 and k (j0: the run's first big record
+// in the block's list); image position y of segment k is out position
+// y + a0c + (hole bytes before it).  One thread per segment; the run's first
+// and last 16-byte chunks are shared with other runs / blocks (byte stores).
+ZK_DEV void stage_out_segs(const uint32_t* lw, int64_t a0c, int64_t B0,
+                           int64_t B1, int64_t yend, int64_t hb0, int64_t K,
+                           int64_t j0, const int64_t* off, const EncHoles& H,
+                           uint8_t* __restrict__ out) {
+  for (int64_t k = threadIdx.x; k <= K; k += blockDim.x) {
+    int64_t y0, y1, d;
+    if (k == 0) {
+      y0 = B0 - (a0c + hb0);
+      d = hb0;
+    } else {
+      const int li = H.bl[j0 + k - 1];
+      const int64_t hc = H.hb[li] >> 9;
+      y0 = hole_h0(off[li]) - hc - a0c;
+      d = hc + H.hole[li];
+    }
+    if (k == K) {
+      y1 = yend;
+    } else {
+      const int li = H.bl[j0 + k];
+      y1 = hole_h0(off[li]) - (H.hb[li] >> 9) - a0c;
+    }
+    for (int64_t y = y0 & ~(int64_t)15; y < y1; y += 16) {
+      const int64_t x = y + a0c + d;
+      const uint4 v = *(const uint4*)(lw + swz(y >> 2));
+      if (x >= B0 && x + 16 <= B1) {
+        *(uint4*)(out + x) = v;
+      } else {
+        const uint8_t* b = (const uint8_t*)&v;
+        for (int q = 0; q < 16; ++q)
+          if (x + q >= B0 && x + q < B1) out[x + q] = b[q];
+      }
+    }
+  }
+}
+
+// One hole, slot -> out, by a whole wave: 16 bytes a lane, the source read
+// as dwords and realigned (alignbyte) to the 16-byte aligned destination.
+// The source's last dword may reach 3 bytes past the data: inside the slot
+// (its data capacity is rounded up to 16, plus 4).
+ZK_DEV void copy_hole(const uint8_t* __restrict__ src, uint8_t* dst,
+                      int64_t n, int lane) {
+  const int sh = (int)((uintptr_t)src & 3);
+  const uint32_t* sa = (const uint32_t*)((uintptr_t)src & ~(uintptr_t)3);
+  for (int64_t x = (int64_t)lane * 16; x < n; x += 64 * 16) {
+    const uint32_t* p = sa + (x >> 2);
+    uint32_t w[5];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) w[j] = p[j];
+    w[4] = sh ? p[4] : 0u;
+    uint4 v;
+    v.x = __builtin_amdgcn_alignbyte(w[1], w[0], sh);
+    v.y = __builtin_amdgcn_alignbyte(w[2], w[1], sh);
+    v.z = __builtin_amdgcn_alignbyte(w[3], w[2], sh);
+    v.w = __builtin_amdgcn_alignbyte(w[4], w[3], sh);
+    *(uint4*)(dst + x) = v;
+  }
+}
+
+// staged_emit for replies with holes.  off / sizes: the block's EncLocal
+// tables; H: the holes (set up by resp_write).
+template <class F>
+ZK_DEV void staged_emit_holes(int64_t r0, int64_t r1, const int64_t* off,
+                              const int64_t* sizes, EncHoles& H,
+                              uint8_t* __restrict__ out, uint32_t* lw, F emit,
+                              int64_t stage) {
+  int64_t rs = r0;
+  while (rs < r1) {                              // block-uniform
+    const int64_t ls = rs - r0;
+    const int64_t B0 = off[ls];
+    const int64_t hb0 = H.hb[ls] >> 9;
+    const int64_t a0c = (B0 & ~(int64_t)15) - hb0;   // compacted image base
+    const int64_t i = rs + threadIdx.x;
+    const int64_t li = i - r0;
+    const bool fits = i < r1 && off[li] - (H.hb[li] >> 9) + sizes[li] -
+                                        H.hole[li] - a0c + 16 <= stage;
+    const int k = __syncthreads_count(fits);
+    if (k == 0) {
+      // one record larger than the image, compacted: written whole
+      if (threadIdx.x == 0) {
+        GSink g{out + B0};
+        emit(g, rs, 0, 0);
+        if (H.hole[ls]) H.bl[H.hb[ls] & 511] = -1;
+      }
+      rs += 1;
+      continue;
+    }
+    const int64_t re = rs + k;
+    const int64_t le = re - 1 - r0;
+    const int64_t B1 = off[le] + sizes[le];
+    const int64_t hbe = (H.hb[le] >> 9) + H.hole[le];    // holes to run end
+    const int64_t yend = B1 - hbe - a0c;
+    const int64_t nrow = ((yend + 3) >> 8) + 1;         // 64-dword rows
+    for (int64_t x = threadIdx.x; x < nrow * 16; x += blockDim.x)
+      ((uint4*)lw)[x] = make_uint4(0, 0, 0, 0);
+    __syncthreads();
+    if (i < re) {
+      LSink l(lw, off[li] - (H.hb[li] >> 9) - a0c);
+      const int64_t hl = H.hole[li];
+      emit(l, i, hl ? hole_h0(off[li]) - (off[li] + 20) : 0, hl);
+    }
+    __syncthreads();
+    const int64_t j0 = H.hb[ls] & 511;
+    const int64_t K = ((H.hb[le] & 511) + (H.hole[le] ? 1 : 0)) - j0;
+    if (K == 0) {
+      stage_out(lw, B0 & ~(int64_t)15, B0, B1, out);
+    } else {
+      stage_out_segs(lw, a0c, B0, B1, yend, hb0, K, j0, off, H, out);
+    }
+    __syncthreads();                             // image reused next run
+    rs = re;
+  }
+}
+
 __global__ __launch_bounds__(ENC_T) void resp_write(
     ZkRespBatch r, ZkNodeStore s, const int64_t* __restrict__ n_dev,
     int64_t ncap, const int64_t* __restrict__ sizes,
@@ -472,9 +630,46 @@ __global__ __launch_bounds__(ENC_T) void resp_write(
   if (*total > cap) return;
   const int64_t r1 = min(r0 + ENC_T, n);
   block_offsets(r0, r1, sizes, bbase, rec_off, E);
-  staged_emit(r0, r1, E.off, E.sz, out, lw, [&](auto& k, int64_t i) {
-    emit_response(k, r, s, i, E.sz[i - r0] - 4);
+  // the holes (large GET_DATA replies), their block scan and list
+  __shared__ EncHoles H;
+  {
+    const int64_t i = r0 + threadIdx.x;
+    int64_t hole = 0;
+    if (i < r1 && r.opcode[i] == OP_GET_DATA && r.err[i] == ERR_OK) {
+      const int64_t o = E.off[threadIdx.x];
+      const int64_t nd = E.sz[threadIdx.x] - 4 - 16 - STAT_BYTES;
+      const int64_t h0 = hole_h0(o);
+      const int64_t h1 = (o + 20 + nd) & ~(int64_t)15;
+      if (h1 - h0 >= BIG_HOLE) hole = h1 - h0;
+    }
+    int64_t tot;
+    const int64_t hb = block_excl_scan(hole * 512 + (hole ? 1 : 0), E.sm,
+                                       &tot);
+    H.hb[threadIdx.x] = hb;
+    H.hole[threadIdx.x] = (int32_t)hole;
+    if (hole) H.bl[hb & 511] = (int16_t)threadIdx.x;
+    __syncthreads();
+  }
+  staged_emit_holes(r0, r1, E.off, E.sz, H, out, lw,
+                    [&](auto& k, int64_t i, int64_t pre, int64_t hole) {
+    emit_response(k, r, s, i, E.sz[i - r0] - 4, pre, hole);
   }, stage);
+  __syncthreads();                 // (bl: records written whole)
+  // the holes, one reply per wave-iteration
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t lt = r1 - 1 - r0;
+  const int64_t nb = (H.hb[lt] & 511) + (H.hole[lt] ? 1 : 0);
+  for (int64_t j = wv; j < nb; j += ENC_T / 64) {
+    const int li = H.bl[j];
+    if (li < 0) continue;                 // written whole
+    const int64_t i = r0 + li;
+    const uint8_t* slot = s.slab + (r.slot ? r.slot[i]
+                                           : s.slot_off[r.node[i]]);
+    const int64_t o = E.off[li];
+    const int64_t h0 = hole_h0(o);
+    copy_hole(slot + ZK_SLOT_LEN + (h0 - (o + 20)), out + h0, H.hole[li],
+              lane);
+  }
 }
 
 // ---------------------------------------------------------------- K10 write

@@ -3,61 +3,51 @@
 // Reference: ZKDecodeStream._transform (lib/zk-streams.js:39-65) walks the
 // i32-BE length chain one frame at a time and memmoves the remainder per
 // packet (O(bytes x packets)).  The chain is inherently
-// sequential; we make it parallel without speculation errors, over 4 KiB
-// tiles, in four launches:
+// sequential; we make it parallel over 4 KiB tiles in three launches:
 //
-//  fs_tile   ONE WAVE per tile (4 per workgroup, independent, no barriers).
-//            The tile is staged into the wave's LDS once; everything else
-//            runs there:
-//            1. merging frontier: one walker per window entry e < W (the
-//               only places a chain can enter a tile when frames are <= W
-//               bytes); each round every live walker hops and claims the
-//               position it lands on in an owner table; a walker landing on
-//               a claimed position has the same future as the claimant and
-//               stops.  Garbage entries die on their first hop (random
-//               bytes read as a length are huge or negative), the true
-//               chain's entries merge within a hop, so after a few rounds
-//               one walker — the survivor — is left;
-//            2. the survivor walks to the tile end, recording its frame
-//               starts (LDS, one hop = one LDS round trip);
-//            3. every exit a walker took into the next tile's window is a
-//               candidate entry of that tile; the preferred one (the
-//               survivor's exit) and up to four others go out in ONE packed
+//  fs_tile   ONE WAVE per tile (or per group of G = 2 / 4 tiles on streams
+//            of large frames), two waves a workgroup, no barriers.  The tile
+//            is staged into the wave's LDS once; everything else runs there:
+//            1. nodes: every position whose i32-BE word is a plausible
+//               length (8 <= len < 4 KiB; any legal length inside the entry
+//               window) is a node, found 64 positions a lane;
+//            2. the chain map: each node's successor (p + 4 + len) is
+//               resolved by POINTER JUMPING over the node table in
+//               registers (log2(chain length) rounds, ~5-7 on GET streams),
+//               so every node knows where its chain leaves the tile, how
+//               many frames it takes and whether it dies (a garbage entry
+//               lands on a non-node within a hop or two);
+//            3. the tile's candidate entries for the next tile — the exits
+//               of the chains rooted in the window — go out in ONE packed
 //               64-bit word (ready bit + five 12-bit offsets, a relaxed
 //               agent-scope store: no release fence, which costs an L2
-//               writeback per wave on a multi-XCD part).  The true chain's
-//               exit is among the in-window exits when frames are <= W.
-//               The tile takes the word of the tile before (a one-step wait:
-//               that wave started earlier and does the same work) and walks
-//               each candidate in LDS: a garbage chain of the tile before,
-//               read on here, dies on a bad length within a few hops; the
-//               first candidate whose chain survives the tile is the entry.
-//               (Round 2 first published only the last surviving walker's
-//               exit: on structured replies of a few hundred bytes a slow
-//               garbage crawler outlived the true chain in ~20 % of the
-//               tiles, and every such tile cost a serial repair.)
-//            4. from the entry, a short walk (usually 1-5 frames) until the
-//               chain meets the survivor's recorded path (merge-walk against
-//               the sorted list), the tile end or a terminal.
-//            The entry is exact unless a frame longer than the window ends
-//            in the tile before or two candidates' chains both survive.
-//  fs_check  one thread per tile (a grid): is tile k's entry tile k-1's
-//            exit, is the tile terminal; frame counts scanned per block of
-//            256 tiles.  The leftmost broken link / terminal go to fs_link
-//            as one atomic per block.
-//  fs_link   No broken link before the first terminal (the usual case):
-//            one workgroup scans the block totals, done.  A few broken
-//            links (<= 64): chased — from each, forward while the next link
-//            stays broken, the exact entry of a tile looked up among the
-//            candidates fs_tile walked (their exits are its entry -> exit
-//            map), so a run of tiles costs a few instructions each; the
-//            looked-up tiles are then re-walked in parallel over the grid
-//            of 64 workgroups for their frame lists.  Many broken links: a
-//            fix-point in grid rounds (every broken link re-walked in
-//            parallel from the exit before it).  Whatever neither settles
-//            is finished serially, tiles covered whole by one frame filled
-//            in one step; then the counts are scanned up to the first
-//            terminal: row bases and result[0..3].
+//               writeback per wave on a multi-XCD part);
+//            4. the entry: the tile before's candidates, each looked up in
+//               the map (the first whose chain survives is the entry; every
+//               candidate's exit goes to `cx`, the entry -> exit map the
+//               repair chases through);
+//            5. the entry's chain read out of the map into the tile's list
+//               of frame starts (a chain the map left open — a short frame
+//               on it — is walked serially, as is a join onto the preferred
+//               chain);
+//            6. settle (ft_settle): the links between the wave's tiles, the
+//               link into its first tile (the wave before's exit, a
+//               non-transitive one-step wait) and the frame count into its
+//               count block's sum.
+//            A group maps its first tile and walks the chain on through the
+//            others (one LDS hop a frame), then checks its entry in a
+//            register table of the first tile's window roots.
+//  fs_link   Every link settled (the usual case): block 0 scans the count
+//            block sums into row bases, done.  Otherwise the full check over
+//            a grid of 16 workgroups (links, terminals, in-block counts)
+//            and the repair: a few broken links are chased — from each,
+//            forward while the next link stays broken, the exact entry of a
+//            tile looked up among the candidates fs_tile mapped (`cx`), so a
+//            run of tiles costs a few instructions each; many are re-walked
+//            in grid rounds to a fix-point.  Whatever neither settles is
+//            finished serially, tiles covered whole by one frame filled in
+//            one step; then the counts are scanned up to the first terminal:
+//            row bases and result[0..3].
 //  fs_rows   one wave per tile writes its (body offset, length) rows.
 //
 // The stream length is read ON THE DEVICE (n = min(*n_dev, n_cap), e.g. an
@@ -92,6 +82,21 @@ constexpr int FC_TAILWIN = 8192;           // the serial tail's (one wave)
 // inlined together spilled to scratch, 0.64 us a looked-up tile)
 constexpr int FL_T = 512;
 constexpr int FL_U = 8;                    // fs_link loads per batch
+// fs_link's grid repair rounds and its grid words (see fl_sync)
+constexpr int FL_GROUNDS = 6;
+constexpr int FL_NB = 3 + 2 * FL_GROUNDS;     // broken links the check saw
+constexpr int FL_GW = FL_NB + 1;
+// Count blocks: frame counts summed per FK_T tiles (one wave's worth)
+constexpr int FK_T = 64;
+// The workspace's words after the X flags (uint64, lbw + 2 * tiles): [0..3]
+// stats, [4..5] the check's minima, [6] the last live tile, [7] fs_tile's
+// bad-link count, [8, 8 + FL_GW) fs_link's grid words, then fs_tile's
+// count-block sums (one per FK_T tiles)
+constexpr int LW_MINS = 4, LW_LAST = 6, LW_BAD = 7, LW_GRID = 8;
+constexpr int LW_CSUM = LW_GRID + FL_GW;
+// *lastk with this bit: fs_tile settled every link (fs_rows counts the
+// frames before a tile within its count block itself)
+constexpr int64_t LK_CLEAN = (int64_t)1 << 62;
 // Bound of fs_tile's wait for the tile before (100 MHz ticks, 2 ms): normal
 // waits are tens of microseconds; past the bound the tile takes no
 // speculated entry and fs_link re-walks it from the exact one.
@@ -134,7 +139,7 @@ ZK_DEV int32_t lds_be32(const uint8_t* sb, int32_t p) {
   return (int32_t)bswap32(__builtin_amdgcn_alignbyte(hi, lo, p & 3));
 }
 
-// ---- per-tile records shared with fs_check / fs_link / fs_rows -------------
+// ---- per-tile records shared with fs_link / fs_rows ------------------------
 constexpr int FT_BITS = FT_S / 32;         // uint32 words per position map
 constexpr int FT_XW = 2048 / 32;           // exit candidates: the next tile's
                                            // window positions (W <= 2048)
@@ -285,7 +290,7 @@ ZK_DEV int64_t ft_cand(const uint8_t* sb, const uint32_t* sbits, int32_t e,
 // candidates (fs_link's candidate exit map), and the frame starts of the
 // chosen entry's chain (slot index = count - the node's count to the root;
 // a side branch landing on the chain is caught by the successor check and
-// sent to the serial walk).  What fs_check / fs_link / fs_rows read is
+// sent to the serial walk).  What fs_link / fs_rows read is
 // unchanged: entry, exit, count, frame-start lists and candidate exits.
 constexpr int FT_NMAX = 512;               // nodes a tile's map holds (GET
                                            // streams: 240-340; more: the
@@ -1315,6 +1320,59 @@ ZK_DEV void ft_group_none(const FtCtx& C, int G) {
   }
 }
 
+// ---- the links into the wave's tiles and their frame count ----------------
+// (What a separate check kernel used to do.)  Lane 0 checks the links between
+// the wave's own tiles from its records, publishes its last tile's exit (the
+// REC word lbw[2 tl + 1] = ready | exit + 1; the stream's last tile has no
+// successor and publishes none) and checks the link into its first tile
+// against the wave before's REC word: a one-step wait that is never
+// transitive (REC goes out before the wait).  The tiles' frame count goes to
+// their count block's sum, one atomic.  A broken link, a missing entry or a
+// terminal before the stream's last tile counts in `bad`: fs_link then runs
+// the full check and the repair; otherwise fs_link only turns the block
+// sums into row bases.  (A decoupled look-back of the counts themselves
+// would wait on a chain of inclusive prefixes that crosses the stream at
+// ~64 tiles a round when every tile is resident at once.)
+template <int G>
+ZK_DEV void ft_settle(const FtCtx& C, int64_t ntiles_cap) {
+  static_assert(FK_T % G == 0, "a wave's tiles share a count block");
+  if (C.lane != 0) return;
+  const int64_t ntiles = (C.n + FT_S - 1) / FT_S;
+  const int64_t t0 = C.t, tl = min(t0 + G, ntiles) - 1;
+  bool ok = true;
+  int64_t cnt = 0, xp = 0;
+  for (int64_t k = t0; k <= tl; ++k) {
+    const int64_t e = C.rec_entry[k], m = C.rec_meta[k];
+    if (e < 0 || (k > t0 && e != xp)) ok = false;
+    if (m_term(m) && k != ntiles - 1) ok = false;
+    cnt += m_cnt(m);
+    xp = C.rec_exit[k];
+  }
+  if (tl + 1 < ntiles)
+    lb_store(&C.lbw[2 * tl + 1], (uint64_t)1 << 63 | (uint64_t)(xp + 1));
+  if (t0 > 0 && ok) {
+    uint64_t w;
+    int nap = 0;
+    const uint64_t t_w = wall_clock64();
+    for (;;) {
+      w = lb_load(&C.lbw[2 * (t0 - 1) + 1]);
+      if (w != 0 || wall_clock64() - t_w > FT_WAIT_TICKS) break;
+      if (nap < 16) __builtin_amdgcn_s_sleep(2);
+      else __builtin_amdgcn_s_sleep(16);
+      ++nap;
+    }
+    if (w == 0 || (int64_t)(w & ~((uint64_t)1 << 63)) - 1 != C.rec_entry[t0])
+      ok = false;
+  }
+  uint64_t* tail = C.lbw + 2 * ntiles_cap;
+  if (cnt)
+    __hip_atomic_fetch_add(&tail[LW_CSUM + t0 / FK_T], (uint64_t)cnt,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (!ok)
+    __hip_atomic_fetch_add(&tail[LW_BAD], (uint64_t)1, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <int W, bool LONG, int G>
 __global__ __launch_bounds__(256) void fs_tile(
     const uint8_t* __restrict__ buf, const int64_t* __restrict__ n_dev,
@@ -1463,6 +1521,7 @@ __global__ __launch_bounds__(256) void fs_tile(
     else if (N <= FT_NMAX) fs_tile_rest<W, LONG, 8>(C, true);
     else fs_tile_rest<W, LONG, 1>(C, false);
   }
+  ft_settle<G>(C, ntiles_cap);
 }
 
 // ---- fs_link ---------------------------------------------------------------
@@ -1556,16 +1615,12 @@ ZK_DEV FcWalk fc_walk(const uint8_t* __restrict__ buf, int64_t n,
 // previous repair (frames longer than the window crossing tile after tile):
 // after FL_GROUNDS rounds block 0 finishes those serially, skipping the
 // tiles a long frame covers in one step.
-constexpr int FL_B = 64;                   // fs_link workgroups
-constexpr int FL_GROUNDS = 6;              // grid repair rounds
 constexpr uint64_t FL_BAR_TICKS = 50000000;   // 0.5 s: barrier abandoned
-// grid words after lbw's stats (uint64): [0] barrier arrivals, [1] barrier
+// grid words (LW_GRID, uint64): [0] barrier arrivals, [1] barrier
 // generation, [2] abort, then per round r [4 + 2r] broken links listed (the
 // chase repair, which runs no rounds, uses [3] settled and [5] / [6] its
-// grid check's first broken link / terminal)
-constexpr int FL_NB = 3 + 2 * FL_GROUNDS;     // broken links fs_check saw
-constexpr int FL_GW = FL_NB + 1;
-// At most this many broken links: chased from fs_check's list (fl_chase; a
+// grid check's first broken link / terminal); [FL_NB] the check's count
+// At most this many broken links: chased from the check's list (fl_chase; a
 // reply stream usually has a handful of broken links or none); more (every
 // tile without a speculated entry) go to the grid rounds.
 constexpr unsigned long long FL_SMALL = 1024;
@@ -1717,70 +1772,67 @@ ZK_DEV bool fl_round(const uint8_t* __restrict__ buf, int64_t n,
   return fl_sync(g);
 }
 
-// fs_check: every link and terminal checked in parallel (one thread per
-// tile, a grid over the tiles) and the frame counts scanned per block of
-// FK_T tiles: base[k] = count before tile k within its block, bsum[b] = the
-// block's total.  The leftmost broken link and terminal reach fs_link as
-// (ntiles - k) maxima in mins[0..1] (zeroed with the X flags; one atomic
-// per block).  Round 2's fs_link did this in one workgroup, ~25 dependent
-// round trips per thread on a 100 MB stream (60 us per scan).
-constexpr int FK_T = 256;
-__global__ __launch_bounds__(FK_T) void fs_check(
-    const int64_t* __restrict__ n_dev, int64_t n_cap,
-    const int64_t* __restrict__ rec_entry, const int64_t* __restrict__ rec_exit,
-    const int64_t* __restrict__ rec_meta, int64_t* __restrict__ base,
-    int64_t* __restrict__ bsum, uint64_t* __restrict__ mins,
-    unsigned long long* __restrict__ nbroken, int32_t* __restrict__ blist) {
-  __shared__ int64_t sm[FK_T / 64 + 1];
-  __shared__ int64_t smin[2 * (FK_T / 64)];
-  const int64_t n = stream_len(n_dev, n_cap);
-  const int64_t ntiles = (n + FT_S - 1) / FT_S;
-  const int64_t k = (int64_t)blockIdx.x * FK_T + threadIdx.x;
-  if ((int64_t)blockIdx.x * FK_T >= ntiles) return;       // block-uniform
+// The full check (fs_link, when fs_tile counted a bad link): every link and
+// terminal, one wave per count block of FK_T tiles over the grid, and the
+// frame counts scanned per block: base[k] = count before tile k within its
+// block, bsum[b] = the block's total.  The leftmost broken link and terminal
+// go to mins[0..1] as (ntiles - k) maxima, the broken links to blist (their
+// count in *nbroken).  Cross-block data: agent-scope stores (the blocks may
+// sit on different XCDs, each with its own L2).
+ZK_DEV void fl_check(int64_t ntiles, const int64_t* __restrict__ rec_entry,
+                     const int64_t* __restrict__ rec_exit,
+                     const int64_t* __restrict__ rec_meta, int64_t* base,
+                     int64_t* bsum, uint64_t* mins,
+                     unsigned long long* nbroken, int32_t* blist) {
+  const int lane = threadIdx.x & 63;
   const int64_t INF = INT64_MAX;
-  int64_t cnt = 0, fb = INF, fterm = INF;
-  if (k < ntiles) {
-    // written by fs_tile (an earlier launch): plain loads, issued together
-    const int64_t mk = rec_meta[k];
-    const bool nxt = k + 1 < ntiles;
-    const int64_t e = nxt ? rec_entry[k + 1] : 0;
-    const int64_t x = rec_exit[k];
-    cnt = m_cnt(mk);
-    if (m_term(mk)) fterm = k;
-    else if (nxt && (e < 0 || e != x)) fb = k + 1;
-  }
-  // broken links, counted and listed (fs_link picks its repair by the
-  // count; a small repair starts from the list)
-  const uint64_t bm = __ballot(fb != INF);
-  if (bm) {
-    const int lane = threadIdx.x & 63;
-    unsigned long long b0 = 0;
-    if (lane == 0) b0 = atomicAdd(nbroken, (unsigned long long)__popcll(bm));
-    b0 = __shfl(b0, 0, 64);
-    if (fb != INF) {
-      const uint64_t below = lane ? (bm & ((~0ull) >> (64 - lane))) : 0ull;
-      blist[b0 + __popcll(below)] = (int32_t)fb;
+  const int64_t nw = (int64_t)gridDim.x * (FL_T / 64);
+  const int64_t nbl = (ntiles + FK_T - 1) / FK_T;
+  int64_t fb = INF, fterm = INF;
+  for (int64_t b = (int64_t)blockIdx.x * (FL_T / 64) + (threadIdx.x >> 6);
+       b < nbl; b += nw) {
+    const int64_t k = b * FK_T + lane;
+    int64_t cnt = 0;
+    bool brk = false;
+    if (k < ntiles) {
+      // written by fs_tile (an earlier launch): plain loads, issued together
+      const int64_t mk = rec_meta[k];
+      const bool nxt = k + 1 < ntiles;
+      const int64_t e = nxt ? rec_entry[k + 1] : 0;
+      const int64_t x = rec_exit[k];
+      cnt = m_cnt(mk);
+      if (m_term(mk)) {
+        fterm = min(fterm, k);
+      } else if (nxt && (e < 0 || e != x)) {
+        brk = true;
+        fb = min(fb, k + 1);
+      }
     }
+    const uint64_t bm = __ballot(brk);
+    if (bm) {
+      unsigned long long b0 = 0;
+      if (lane == 0) b0 = atomicAdd(nbroken, (unsigned long long)__popcll(bm));
+      b0 = __shfl(b0, 0, 64);
+      if (brk) {
+        const uint64_t below = lane ? (bm & ((~0ull) >> (64 - lane))) : 0ull;
+        __hip_atomic_store(&blist[b0 + __popcll(below)], (int32_t)(k + 1),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    int64_t inc = cnt;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int64_t v = __shfl_up(inc, d, 64);
+      if (lane >= d) inc += v;
+    }
+    if (k < ntiles) st_agent(&base[k], inc - cnt);
+    if (lane == 63) st_agent(&bsum[b], inc);
   }
-  int64_t tot;
-  const int64_t ex = block_excl_scan(cnt, sm, &tot);
-  if (k < ntiles) base[k] = ex;
   for (int d = 32; d >= 1; d >>= 1) {
     fb = min(fb, (int64_t)__shfl_xor(fb, d, 64));
     fterm = min(fterm, (int64_t)__shfl_xor(fterm, d, 64));
   }
-  const int wv = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) {
-    smin[wv] = fb;
-    smin[FK_T / 64 + wv] = fterm;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    for (int j = 1; j < FK_T / 64; ++j) {
-      fb = min(fb, smin[j]);
-      fterm = min(fterm, smin[FK_T / 64 + j]);
-    }
-    bsum[blockIdx.x] = tot;
+  if (lane == 0) {
     if (fb != INF) atomicMax((unsigned long long*)&mins[0],
                              (unsigned long long)(ntiles - fb));
     if (fterm != INF) atomicMax((unsigned long long*)&mins[1],
@@ -1788,8 +1840,46 @@ __global__ __launch_bounds__(FK_T) void fs_check(
   }
 }
 
+// fs_tile settled every link (block 0): its count-block sums csum become the
+// blocks' exclusive offsets in bsum (csum back to zero for the next scan),
+// and result[0..3] / the last tile.  A terminal can only be the last tile.
+ZK_DEV void fl_bases_clean(int64_t n, int64_t ntiles, const int64_t* rec_exit,
+                           const int64_t* rec_meta, uint64_t* csum,
+                           int64_t* bsum, int64_t cap, int64_t* result,
+                           int64_t* lastk, int64_t* red) {
+  const int tid = threadIdx.x;
+  const int64_t nbl = (ntiles + FK_T - 1) / FK_T;
+  const int64_t per = (nbl + FL_T - 1) / FL_T;
+  const int64_t b0 = (int64_t)tid * per;
+  const int64_t b1 = min(b0 + per, nbl);
+  int64_t sum = 0;
+  for (int64_t b = b0; b < b1; ++b) sum += (int64_t)csum[b];
+  int64_t tot;
+  int64_t run = block_excl_scan(sum, red, &tot);
+  for (int64_t b = b0; b < b1; ++b) {
+    const int64_t v = (int64_t)csum[b];
+    csum[b] = 0;
+    bsum[b] = run;
+    run += v;
+  }
+  if (tid == 0) {
+    const int64_t last = ntiles - 1;
+    const int64_t ml = rec_meta[last];
+    *lastk = last | LK_CLEAN;
+    result[0] = tot;
+    result[3] = tot > cap ? 1 : 0;
+    if (!m_term(ml)) {
+      result[1] = n;
+      result[2] = 0;
+    } else {
+      result[1] = rec_exit[last];
+      result[2] = m_bad(ml) ? 1 : 0;
+    }
+  }
+}
+
 // Row bases once every link up to the first terminal ft (INF: none) holds:
-// bsum[b] (block b's count total, fs_check's or re-counted) becomes block
+// bsum[b] (block b's count total, the check's or re-counted) becomes block
 // b's exclusive offset; base[k] stays the in-block one; result[0..3] and
 // the last tile.  Block 0 alone.
 ZK_DEV void fl_bases(int64_t n, int64_t ntiles, int64_t ft,
@@ -1831,7 +1921,7 @@ ZK_DEV void fl_bases(int64_t n, int64_t ntiles, int64_t ft,
 }
 
 // The small repair (a handful of broken links, the usual kind): CHASES.
-// fs_check listed the broken links.  A chase starts at one with the exact
+// The check listed the broken links.  A chase starts at one with the exact
 // entry (the exit before it) and runs forward while the link after the
 // tile it settled is still broken.  Most tiles of a run need no walk:
 // their exact entry is one of the candidate entries fs_tile walked, whose
@@ -1855,7 +1945,7 @@ constexpr int FL_WL = 1024;                // chases per round
 constexpr int FL_HS = 2048;                // their dedup hash set
 constexpr int FL_WR = 48;                  // rounds before the serial tail
 constexpr int FL_DB = 8192;                // count blocks tracked (2M tiles)
-static_assert(FL_SMALL <= FL_WL, "fs_check's list fits the first round");
+static_assert(FL_SMALL <= FL_WL, "the check's list fits the first round");
 
 struct FlChase {
   uint32_t* dirty;                // count blocks holding re-written tiles
@@ -2143,8 +2233,10 @@ ZK_DEV bool fl_chase(const uint8_t* __restrict__ buf, int64_t n,
   __shared__ int s_n;
   __shared__ int s_cur;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  // fs_check's list to LDS
-  for (int i = tid; i < nb0; i += FL_T) wl[0][i] = blist[i];
+  // the check's list to LDS
+  for (int i = tid; i < nb0; i += FL_T)
+    wl[0][i] = __hip_atomic_load(&blist[i], __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
   if (tid == 0) s_cur = nb0;
   uint8_t* mywin = win + (size_t)wv * (FC_WIN + 16);
   int cur = 0, rounds = 0;
@@ -2217,32 +2309,23 @@ ZK_DEV bool fl_chase(const uint8_t* __restrict__ buf, int64_t n,
 }
 
 // After the chases and the grid's check of every link (block 0): re-count
-// the count blocks holding a re-written tile, one wave per block, four
-// tiles per lane.
+// the count blocks holding a re-written tile, one wave per block, a tile per
+// lane.
 ZK_DEV void fl_chase_recount(int64_t ntiles, const int64_t* rec_meta,
                              int64_t* base, int64_t* bsum, FlChase& ch) {
+  static_assert(FK_T == 64, "a count block is a wave");
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t nbl = (ntiles + FK_T - 1) / FK_T;
   for (int64_t b = wv; b < nbl; b += FL_T / 64) {
     if (!((ch.dirty[b >> 5] >> (b & 31)) & 1u)) continue;
-    const int64_t k0 = b * FK_T + 4 * lane;
-    int64_t c[4], s = 0;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      c[u] = k0 + u < ntiles ? m_cnt(ld_agent(&rec_meta[k0 + u])) : 0;
-      s += c[u];
-    }
-    int64_t inc = s;
+    const int64_t k = b * FK_T + lane;
+    const int64_t c = k < ntiles ? m_cnt(ld_agent(&rec_meta[k])) : 0;
+    int64_t inc = c;
     for (int d = 1; d < 64; d <<= 1) {
       const int64_t v = __shfl_up(inc, d, 64);
       if (lane >= d) inc += v;
     }
-    int64_t run = inc - s;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      if (k0 + u < ntiles) st_agent(&base[k0 + u], run);
-      run += c[u];
-    }
+    if (k < ntiles) st_agent(&base[k], inc - c);
     if (lane == 63) st_agent(&bsum[b], inc);
   }
   __syncthreads();
@@ -2255,8 +2338,8 @@ __global__ __launch_bounds__(FL_T) void fs_link(
     uint16_t* pre, int64_t* rec_entry, int64_t* rec_exit, int64_t* rec_meta,
     int64_t* __restrict__ base, int64_t cap, int64_t* __restrict__ result,
     uint64_t* stats, int32_t* __restrict__ blist,
-    int64_t* __restrict__ bsum, uint64_t* __restrict__ mins,
-    int64_t* __restrict__ lastk, unsigned long long* __restrict__ g,
+    int64_t* __restrict__ bsum, uint64_t* mins,
+    int64_t* __restrict__ lastk, unsigned long long* g,
     const uint64_t* lbw, const int64_t* __restrict__ cx,
     int64_t* __restrict__ ldbg) {
   __shared__ __attribute__((aligned(16)))
@@ -2276,35 +2359,52 @@ __global__ __launch_bounds__(FL_T) void fs_link(
     return;
   }
   const int64_t INF = INT64_MAX;
-  // fs_check's minima, read by every thread of every block; block 0
-  // clears them for the next scan of this workspace once every block has
-  // read them (on the fast path only block 0 goes on, so at once)
-  const uint64_t mb0 = mins[0], mt0 = mins[1];
-  const unsigned long long nb0 = g[FL_NB];
+  uint64_t* tail = mins - LW_MINS;
+  uint64_t* csum = tail + LW_CSUM;
+  // fs_tile settled every link (the usual case): block 0 turns its count
+  // sums into row bases, done
+  if (ld_agent((const int64_t*)&tail[LW_BAD]) == 0) {
+    if (blockIdx.x != 0) return;
+    fl_bases_clean(n, ntiles, rec_exit, rec_meta, csum, bsum, cap, result,
+                   lastk, red);
+    return;
+  }
+  // the full check over the grid; then the minima and the broken-link count,
+  // read by every thread of every block before block 0 clears them (and
+  // fs_tile's words) for the next scan of this workspace
+  if (blockIdx.x == 0)
+    for (int64_t b = tid; b < (ntiles + FK_T - 1) / FK_T; b += FL_T) csum[b] = 0;
+  fl_check(ntiles, rec_entry, rec_exit, rec_meta, base, bsum, mins, &g[FL_NB],
+           blist);
+  bool grid_ok = fl_sync(g);
+  const uint64_t mb0 = ld_agent((const int64_t*)&mins[0]);
+  const uint64_t mt0 = ld_agent((const int64_t*)&mins[1]);
+  const unsigned long long nb0 = __hip_atomic_load(
+      &g[FL_NB], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  grid_ok = grid_ok && fl_sync(g);
+  if (blockIdx.x == 0 && tid == 0) {
+    st_agent((int64_t*)&mins[0], 0);
+    st_agent((int64_t*)&mins[1], 0);
+    st_agent((int64_t*)&tail[LW_BAD], 0);
+    __hip_atomic_store(&g[FL_NB], 0ull, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
   const int64_t fb0 = mb0 ? ntiles - (int64_t)mb0 : INF;
   const int64_t ft0 = mt0 ? ntiles - (int64_t)mt0 : INF;
-  const bool fast = fb0 == INF || fb0 > ft0;
+  const bool fast = grid_ok && (fb0 == INF || fb0 > ft0);
   // a small repair (a handful of broken links, the usual kind) is chased
   // (fl_chase), a large one repaired in grid rounds; the whole grid takes
-  // part in either (every block decides alike: block 0 clears the words it
-  // read only after the grid's first barrier)
-  const bool small = !fast && nb0 <= FL_SMALL &&
+  // part in either (every block decides alike)
+  const bool small = grid_ok && !fast && nb0 <= FL_SMALL &&
                      (ntiles + FK_T - 1) / FK_T <= FL_DB;
   if (fast && blockIdx.x != 0) return;
   if (fast) {
     // no broken link before the first terminal: the row bases are bsum's
-    // block offsets + fs_check's in-block bases
-    __syncthreads();
-    if (tid == 0) {
-      mins[0] = 0;
-      mins[1] = 0;
-      g[FL_NB] = 0;
-    }
+    // block offsets + the check's in-block bases
     fl_bases(n, ntiles, ft0, rec_exit, rec_meta, base, bsum, cap, result,
              lastk, red);
     return;
   }
-  bool grid_ok = true;
   if (small) {
     // ---- chases: block 0; then every link checked over the grid ---------
     __shared__ uint32_t dirty[FL_DB / 32];
@@ -2325,12 +2425,8 @@ __global__ __launch_bounds__(FL_T) void fs_link(
                            __HIP_MEMORY_SCOPE_AGENT);
       if (clk) ldbg[1] = wall_clock64();
     }
-    bool synced = fl_sync(g);        // (block 0 cleared nothing yet)
+    bool synced = fl_sync(g);
     if (clk) ldbg[2] = wall_clock64();
-    if (blockIdx.x == 0 && tid == 0) {
-      mins[0] = 0;
-      mins[1] = 0;
-    }
     const bool settled =
         __hip_atomic_load(cw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
     // every link and the first terminal, checked over the grid (a chase
@@ -2376,20 +2472,12 @@ __global__ __launch_bounds__(FL_T) void fs_link(
     }
     if (settled && synced && (fbv == INF || fbv > ftv)) {
       fl_chase_recount(ntiles, rec_meta, base, bsum, ch);
-      if (tid == 0) g[FL_NB] = 0;
       fl_bases(n, ntiles, ftv, rec_exit, rec_meta, base, bsum, cap, result,
                lastk, red);
       if (clk) ldbg[4] = wall_clock64();
       return;
     }
     grid_ok = false;          // not settled: block 0's serial tail finishes
-  } else {
-    // ---- repair: rounds to a fix-point over the grid ---------------------
-    grid_ok = fl_sync(g);                    // every block read the minima
-    if (blockIdx.x == 0 && tid == 0) {
-      mins[0] = 0;
-      mins[1] = 0;
-    }
   }
   for (int r = 0; r < FL_GROUNDS && grid_ok; ++r)
     grid_ok = fl_round(buf, n, ntiles, maxp, sx, list, rcount, pre,
@@ -2562,8 +2650,22 @@ __global__ __launch_bounds__(256) void fs_rows(
     lbw[2 * t] = 0;
     lbw[2 * t + 1] = 0;
   }
-  if (t > *lastk) return;
-  const int64_t b = bsum[t / FK_T] + base[t];
+  const int64_t lk = *lastk;
+  const bool clean = lk >= 0 && (lk & LK_CLEAN);
+  if (t > (clean ? lk & ~LK_CLEAN : lk)) return;
+  int64_t b = bsum[t / FK_T];
+  if (clean) {
+    // fs_tile settled the links: the frames before this tile in its count
+    // block, from their records (one load a lane)
+    static_assert(FK_T == 64, "a count block is a wave");
+    const int64_t k = (t & ~(int64_t)(FK_T - 1)) + lane;
+    int64_t c = k < t ? m_cnt(rec_meta[k]) : 0;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d, 64);
+    b += c;
+  } else {
+    b += base[t];
+  }
   const int64_t m = rec_meta[t];
   const int64_t x = rec_exit[t];
   const int32_t cnt = m_cnt(m), np = m_np(m), js = m_js(m);
@@ -2635,9 +2737,8 @@ static FsPlan fs_plan(int64_t n) {
   p.off_list = take((size_t)tiles * FT_LMAX * 2);
   p.off_pre = take((size_t)tiles * FT_LMAX * 2);
   p.off_sx = take((size_t)tiles * 8);
-  // X flags (2 per tile), 4 stats words, fs_check's 2 minima, last tile,
-  // a pad word, fs_link's grid words
-  p.off_lbw = take((size_t)(2 * tiles + 8 + FL_GW) * 8);
+  // X flags (2 per tile), then the words LW_* name
+  p.off_lbw = take((size_t)(2 * tiles + LW_CSUM + tiles / FK_T + 1) * 8);
   p.off_rent = take((size_t)tiles * 8);
   p.off_rexit = take((size_t)tiles * 8);
   p.off_rmeta = take((size_t)tiles * 8);
@@ -2723,7 +2824,7 @@ int64_t zk_frame_scan_workspace(int64_t n) {
 // clean != 0: the workspace's flags were left cleared by the previous scan
 // of it over the same n_cap (fs_rows / fs_link clear what they used), so
 // the memset is skipped.  A stale flag could only cost speed, never
-// correctness (fs_check / fs_link verify every speculated entry).
+// correctness (fs_tile / fs_link check every speculated entry).
 // flags: bit 1 (FS_LONG) frames may be longer than the window (a window
 // below the stream's largest frame: fs_tile's frontier passes); tests of
 // the link repair: bit 0 no speculated tile entries; bits 8..23 P > 0:
@@ -2751,14 +2852,14 @@ int zk_frame_scan5(const uint8_t* buf, const int64_t* n_dev, int64_t n_cap,
   int32_t* blist = (int32_t*)(ws + p.off_blist);
   int64_t* bsum = (int64_t*)(ws + p.off_bsum);
   int64_t* cx = (int64_t*)(ws + p.off_cx);
-  uint64_t* mins = lbw + 2 * tiles + 4;
-  int64_t* lastk = (int64_t*)(lbw + 2 * tiles + 6);
-  unsigned long long* grid = (unsigned long long*)(lbw + 2 * tiles + 8);
-  // X flags, the stats, fs_check's minima and fs_link's grid words start
-  // at zero
+  uint64_t* mins = lbw + 2 * tiles + LW_MINS;
+  int64_t* lastk = (int64_t*)(lbw + 2 * tiles + LW_LAST);
+  unsigned long long* grid = (unsigned long long*)(lbw + 2 * tiles + LW_GRID);
+  // X flags, the stats, the check's minima, the bad-link count, fs_link's
+  // grid words and the count sums start at zero
   if (!clean &&
-      hipMemsetAsync(lbw, 0, (size_t)(2 * tiles + 8 + FL_GW) * 8, st) !=
-          hipSuccess)
+      hipMemsetAsync(lbw, 0, (size_t)(2 * tiles + LW_CSUM + tiles / FK_T + 1) *
+                                 8, st) != hipSuccess)
     return -4;
   int64_t* dbg = fs_dbg_buf(tiles);
   // tiles (waves) per block: two 12 KiB slices, 6 blocks a CU
@@ -2802,9 +2903,6 @@ int zk_frame_scan5(const uint8_t* buf, const int64_t* n_dev, int64_t n_cap,
   }
 #undef ZK_FS_TILE
 #undef ZK_FS_GROUP
-  ZK_LAUNCH_CHECK();
-  fs_check<<<(unsigned)((tiles + FK_T - 1) / FK_T), FK_T, 0, st>>>(
-      n_dev, n_cap, rent, rexit, rmeta, base, bsum, mins, grid + FL_NB, blist);
   ZK_LAUNCH_CHECK();
   fs_link<<<fl_blocks(), FL_T, 0, st>>>(buf, n_dev, n_cap, maxp, sx, list, rcnt,
                                  pre, rent, rexit, rmeta, base, cap, result,

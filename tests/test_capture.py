@@ -2,8 +2,10 @@
 per rotation, after the warmup and times replays): a replay draws new xids
 from the device-side xid counter and every reply is checked on the device,
 exactly as in eager steps.  The tree stays steady across replays (nodes
-recycled through the free ring).  Storm and watch steps stay eager (their
-session ids and expiry / node draws are host decisions per step)."""
+recycled through the free ring).  The watch workload captures a cycle of
+steps (its node sets are host draws per step).  Storm steps stay eager:
+the session a step serves and the one it expires are host scalars handed
+to the serve and expire kernels, and the hash rebuild is a host decision."""
 
 import pytest
 import torch
@@ -58,3 +60,16 @@ def test_nest_replays(gpu):
     tree = _tree(gpu, scratch=1 << 22)
     pipe = NestPipeline(tree, 7 * 1024, ndirs=64)
     assert _replays(pipe, gpu) == 6 * pipe.n
+
+
+def test_watch_replays_a_cycle(gpu):
+    """Arm, write-fired notifications and their decode + check, replayed:
+    every replay's notifications all arrive and check out (the watches
+    re-arm every step, so a cycle's node sets can repeat)."""
+    from zkmi.bench.synthetic import GpuTree, WatchPipeline
+    tree = GpuTree(20000, 37, fanout=100, device=gpu, seed=0,
+                   watch_cap=8192)
+    pipe = WatchPipeline(tree, 3000)
+    assert pipe.capturable
+    assert _replays(pipe, gpu, eager=2, replays=11) == 11 * pipe.n
+    assert int(pipe.step().item()) == pipe.n

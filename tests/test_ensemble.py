@@ -36,11 +36,19 @@ def _worker(rank, world, mport, steps, errq, outq):
         ctl = E.EnsembleControl(3) if rank == 0 else None
         try:
             wl = E.EnsembleWorkload(ctl, n_paths=48, writes=12,
-                                    failover_every=2, codec_device=None)
+                                    failover_every=2, codec_device=None,
+                                    trace=True)
             got = [wl.step() for _ in range(steps)]
             bad = wl.verify()
+            extra = None
+            if bad is not None:
+                # what to look at when an event arrives twice: this rank's
+                # resumes (relZxid, watches), forwards and receipts
+                extra = {'resumes': wl.client.loop.run(
+                    lambda: list(wl.client.getSession().resumes)),
+                    'trace': wl.trace}
             outq.put((rank, bad, got, wl.failovers, wl.rearmed(),
-                      wl.replayed, dict(wl.fan.stats)))
+                      wl.replayed, dict(wl.fan.stats), extra))
             dist.barrier()
             wl.close()
         finally:
@@ -81,9 +89,15 @@ def test_ensemble_failover_replay_fanout(world):
     # on any failure, every rank's (bad, got, failovers, rearmed, replayed,
     # fan-out stats) goes into the message
     report = {r: dict(zip(('bad', 'got', 'fo', 'rearmed', 'replayed',
-                           'stats'), v)) for r, v in res.items()}
+                           'stats', 'trace'), v)) for r, v in res.items()}
     rearmed = 0
-    for rank, (bad, got, fo, rea, replayed, st) in res.items():
+    for rank, (bad, got, fo, rea, replayed, st, _) in res.items():
+        if bad is not None:
+            d = os.path.join(ROOT, 'gpurun_out')
+            os.makedirs(d, exist_ok=True)
+            with open(os.path.join(d, 'ensemble_dup_w%d_%d.txt'
+                                   % (world, os.getpid())), 'w') as f:
+                f.write(repr(report))
         # every event (initial arm, live, replayed) exactly once per rank
         assert bad is None, (rank, report)
         assert got == [12] * steps, (rank, report)

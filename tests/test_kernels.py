@@ -465,13 +465,17 @@ def test_encode_responses_matches_oracle(gpu):
 
 
 @pytest.mark.parametrize('dist,mix', [(None, False), ((0, 300), False),
-                                      ((0, 300), True)])
+                                      ((0, 300), True), ((0, 2000), False),
+                                      ((0, 2000), True), ((300, 1024), False)])
 def test_encode_responses_serve_mix_matches_oracle(gpu, dist, mix):
     """K13 on the serve path's usual replies (GET_DATA / Stat / header-only,
     errors among them) against jute.encode_response: fixed and variable
     data lengths, a terminated stream (four 0xFF bytes right after it,
     nothing written past the last 16-byte chunk), and with ``mix`` a CREATE
-    in every third block.  Round 3 measured a gather variant of the writer
+    in every third block.  Payloads past ~300 bytes exercise the holes (the
+    16-byte aligned interiors the waves copy slot -> out, the image streamed
+    out segment by segment between them).  Round 3 measured a gather variant
+    of the writer
     (each aligned 16-byte chunk built from its record's slot) 2.4x slower
     than the LDS-staged one (README, Measured and rejected)."""
     from zkmi.bench.synthetic import GpuTree

@@ -1466,7 +1466,9 @@ class WatchPipeline(object):
     One step delivers ``world * batch`` notifications to every rank:
     ``world**2 * batch`` deliveries node-wide (:attr:`per_step`).
     ``coll_device='cpu'`` runs the all-gather on host tensors (gloo
-    rehearsal).  A step makes no device-to-host read."""
+    rehearsal).  A step makes no device-to-host read; on one GPU, or with
+    the all-gather on it, steps are captured as HIP graphs
+    (:meth:`capture`)."""
 
     def __init__(self, tree, batch, seed=0, group=None, coll_device=None):
         import torch.distributed as dist
@@ -1489,8 +1491,10 @@ class WatchPipeline(object):
         self.j = torch.arange(n, dtype=I64, device=dev)
         self.jw = torch.arange(W * n, dtype=I64, device=dev) % n
         self.rank_of = torch.arange(W * n, dtype=I64, device=dev) // n
-        self.xid_iota = torch.arange(n, dtype=I32, device=dev)
-        self.xid_base = 0
+        # the sessions' next xid, on the device: a captured step replays
+        # with new xids
+        self.xid_iota = torch.arange(n, dtype=I64, device=dev)
+        self.xid_dev = torch.zeros(1, dtype=I64, device=dev)
         self.ops_get = torch.full((n,), consts.OP_CODES['GET_DATA'],
                                   dtype=I32, device=dev)
         self.ops_set = torch.full((n,), consts.OP_CODES['SET_DATA'],
@@ -1565,9 +1569,22 @@ class WatchPipeline(object):
                               self.acl_off, self.acl_len, self.acl_arena)
 
     def _xids(self):
-        x = (self.xid_iota + self.xid_base) & 0x7fffffff
-        self.xid_base = (self.xid_base + self.n) & 0x7fffffff
+        x = ((self.xid_iota + self.xid_dev) & 0x7fffffff).to(I32)
+        self.xid_dev.add_(self.n)
         return x
+
+    @property
+    def capturable(self):
+        """The R1 all-gather is captured with the step when it runs on this
+        GPU (RCCL); a gloo rehearsal's host all-gather is not."""
+        return self.world == 1 or self.coll_device == self.dev
+
+    def capture(self, acc, cycle=8):
+        """``cycle`` HIP graphs, replayed in turn: a step's watched and
+        written nodes are an affine permutation the host picks per step
+        (:meth:`_affine`), so each graph holds one step of a cycle of
+        ``cycle`` node sets; xids come from a device counter."""
+        return _capture_steps(self, acc, cycle)
 
     def _roundtrip(self, rb, session, wslot, check=None):
         tx, _, total, _ = B.encode_requests(rb, self.xt, out=self.tx)

@@ -613,6 +613,7 @@ class ZKConnectionFSM(FSM):
                 lambda st, nb, got, last, b=batch:
                     self._bulk_captured(b, st, nb, got, last),
                 self.decoder.take_pending())
+        batch.t['send0'] = time.perf_counter()
         if isinstance(wire, tuple):
             self.log.trace({'xid0': x0, 'n': n, 'bytes': wire[1]},
                            'sent bulk batch')

@@ -109,6 +109,7 @@ class ZKSession(FSM):
         self._bulk_packed = None    # bulk_watches as an encoded vector
                                     # (in the order they were added)
         self.rearmed = 0            # watches re-armed by SET_WATCHES resumes
+        self.resumes = []           # (relZxid, watches) of each resume
         self.session_id = 0
         self.passwd = b'\0' * 8
         collector.counter(METRIC_ZK_NOTIFICATION_COUNTER,
@@ -434,6 +435,8 @@ class ZKSession(FSM):
         zxid = self.last_zxid
         self.log.info('re-arming %d node watchers at zxid %x', count, zxid)
         self.rearmed += count
+        if len(self.resumes) < 64:
+            self.resumes.append((zxid, count))
 
         def done(err):
             if err is not None:

@@ -28,6 +28,17 @@ node's stream on its GPU and counts each (path, version) event in HBM; no
 event becomes a Python object on the way.  Writes go out as bulk SET_DATA
 batches.  Without a GPU (the gloo rehearsal on CPU) the same flow runs on
 the host codec.
+
+Exactly once: a watch's catch-up can reach its owner twice.  When the
+client's connection set moves a session again while the first resume's
+SET_WATCHES is still unanswered (e.g. back to its preferred member as soon
+as that member restarts), the second SET_WATCHES carries the same relZxid
+— the catch-up notifications carry no zxid that could have advanced it —
+and the member replays the same changes.  A ZooKeeper client drops such a
+repeat because the fired watch is gone from its watch table; bulk watches
+stay armed on the client, so the owner drops it by version instead: the
+re-arm read of a change it already forwarded returns a version no newer
+than the one it forwarded (:meth:`EnsembleWorkload._rearm`).
 """
 
 import collections
@@ -40,6 +51,7 @@ import torch.distributed as dist
 
 from .. import codec
 from .. import consts
+from ..errors import ZKProtocolError
 from .fanout import FrameFanout, XID_FWD, notification_frames, owner_of, \
     path_ids
 
@@ -145,7 +157,8 @@ class EnsembleWorkload(object):
 
     def __init__(self, ctl=None, n_members=3, n_paths=256, writes=64,
                  failover_every=4, session_timeout=8000, codec_device=None,
-                 group=None, seed=0, coll_device=None, max_versions=64):
+                 group=None, seed=0, coll_device=None, max_versions=64,
+                 trace=False):
         from ..models.client import Client
         from ..config import ClientConfig, RecoveryPolicy
         on = dist.is_available() and dist.is_initialized()
@@ -208,10 +221,18 @@ class EnsembleWorkload(object):
         self.seen = torch.zeros(n_paths * self.vmax, dtype=torch.int32,
                                 device=dev)
         self.bad_frames = torch.zeros(1, dtype=torch.int64, device=dev)
+        # the newest version this rank forwarded per path it owns (-1: none)
+        # and the repeats it dropped (module docstring)
+        self.fwd_ver = np.full(n_paths, -1, np.int64)
+        self.fwd_ver_dev = torch.from_numpy(self.fwd_ver.copy()).to(
+            self.dev) if self.dev is not None else None
+        self.redelivered = 0
         self.replayed = 0                 # writes made during outages
         self.step_ms = []
         self.phase_ms = collections.Counter()     # where a step's time goes
         self.step_no = 0
+        # trace: (step, tick, paths this rank forwarded) per host-path tick
+        self.trace = [] if trace else None
         self.failovers = 0
         self.down = None
         if self.rank == 0:
@@ -234,19 +255,33 @@ class EnsembleWorkload(object):
         if self.world > 1:
             dist.barrier(group=self.group)
 
-    def _bulk(self, call, *args, timeout=60.0, **kw):
-        done = threading.Event()
-        box = {}
+    def _bulk(self, call, *args, timeout=60.0, retry=False, **kw):
+        """One bulk batch, blocking.  ``retry``: an idempotent batch (the
+        re-arming reads) that failed because the session was between
+        connections is sent again once it is connected (ZooKeeper fails a
+        request with CONNECTION_LOSS during a move; the caller retries)."""
+        for attempt in range(4 if retry else 1):
+            done = threading.Event()
+            box = {}
 
-        def cb(err, res=None):
-            box['err'], box['res'] = err, res
-            done.set()
-        call(*args, cb, **kw)
-        if not done.wait(timeout):
-            raise RuntimeError('bulk batch timed out')
-        if box['err'] is not None:
-            raise box['err']
-        return box['res']
+            def cb(err, res=None):
+                box['err'], box['res'] = err, res
+                done.set()
+            try:
+                call(*args, cb, **kw)
+            except ZKProtocolError as e:
+                box['err'] = e
+                done.set()
+            if not done.wait(timeout):
+                raise RuntimeError('bulk batch timed out')
+            err = box['err']
+            if err is None:
+                return box['res']
+            if not retry or attempt == 3 or \
+                    getattr(err, 'code', None) != 'CONNECTION_LOSS':
+                raise err
+            self.client.wait_connected(timeout)
+        raise AssertionError('unreachable')
 
     def _create_tree(self):
         c = self.client
@@ -271,8 +306,30 @@ class EnsembleWorkload(object):
                                              consts.MAX_PACKET)
             paths = [codec.decode_response(notes[o:o + ln], {})['path']
                      for o, ln in frames]
-            res = self._bulk(self.client.bulk_get, paths, watch=True)
-            return notes + _patch_xids(res.raw), 2 * k
+            res = self._bulk(self.client.bulk_get, paths, watch=True,
+                             retry=True)
+            raw = _patch_xids(res.raw)
+            rf, _, _ = codec.scan_frames(raw, 0, len(raw), consts.MAX_PACKET)
+            keep = []
+            for i, pk in enumerate(res.packets()):
+                st = pk.get('stat') if pk.get('err') == 'OK' else None
+                if st is not None:
+                    pid = int(paths[i][-_DIGITS:])
+                    if st.version <= self.fwd_ver[pid]:
+                        self.redelivered += 1         # forwarded already
+                        continue
+                    self.fwd_ver[pid] = st.version
+                keep.append(i)
+            if self.trace is not None:
+                self.trace.append(('fwd', self.step_no,
+                                   self.phase_ms['ticks'],
+                                   [paths[i] for i in keep]))
+            if len(keep) == k:
+                return notes + raw, 2 * k
+            return (b''.join(notes[frames[i][0] - 4:sum(frames[i])]
+                             for i in keep) +
+                    b''.join(raw[rf[i][0] - 4:sum(rf[i])] for i in keep),
+                    2 * len(keep))
         from ..ops import batch as B
         nd = torch.frombuffer(bytearray(notes), dtype=torch.uint8) \
             .to(self.dev, non_blocking=True)
@@ -280,7 +337,7 @@ class EnsembleWorkload(object):
         rep = B.decode_replies(nd, ft, self.fan.xt)
         triple = (nd, rep.pay_off[:k], rep.pay_len[:k])
         t0 = time.perf_counter()
-        res = self._bulk(self.client.bulk_get, triple, watch=True)
+        res = self._bulk(self.client.bulk_get, triple, watch=True, retry=True)
         ph = self.phase_ms
         ph['rearm_bulk_get'] += (time.perf_counter() - t0) * 1e3
         t = getattr(res, 'phases', None) or {}
@@ -288,10 +345,40 @@ class EnsembleWorkload(object):
             ph['rb_encode'] += (t['encoded'] - t['submit']) * 1e3
             ph['rb_wire'] += (t['captured'] - t['encoded']) * 1e3
             ph['rb_finish'] += (t['finished'] - t['captured']) * 1e3
-        return torch.cat([nd, self.fan.forward_replies(res)]), 2 * k
+        fwd = self.fan.forward_replies(res)
+        # the owner's dedup by version (module docstring), on the device
+        rr = res.replies
+        pid = path_ids(nd, rep.pay_off[:k], rep.pay_len[:k], _DIGITS) \
+            .clamp(0, len(self.paths) - 1)
+        ver = rr.stat32[0][:k].to(torch.int64)
+        ok = (rr.status[:k] == 0) & (rr.err[:k] == 0)
+        dup = ok & (ver <= self.fwd_ver_dev[pid])
+        self.fwd_ver_dev.scatter_reduce_(0, pid[ok], ver[ok], 'amax')
+        ndup = int(dup.sum().item())
+        if ndup == 0:
+            return torch.cat([nd, fwd]), 2 * k
+        self.redelivered += ndup
+        keep = (~dup).nonzero().squeeze(1)
+
+        def frames_of(buf, off, ln):
+            # the kept frames' bytes, length prefixes included
+            s0 = off[keep] - 4
+            n = ln[keep].to(torch.int64) + 4
+            base = torch.repeat_interleave(s0 - (torch.cumsum(n, 0) - n), n)
+            return buf[base + torch.arange(int(n.sum().item()),
+                                           device=buf.device)]
+        return (torch.cat([frames_of(nd, ft.off[:k], ft.length[:k]),
+                           frames_of(fwd, res.frames.off[:k],
+                                     res.frames.length[:k])]),
+                2 * (k - ndup))
 
     def _initial(self, notes, paths):
-        res = self._bulk(self.client.bulk_get, list(paths), watch=True)
+        res = self._bulk(self.client.bulk_get, list(paths), watch=True,
+                         retry=True)
+        for p in paths:                       # version 0 forwarded
+            self.fwd_ver[int(p[-_DIGITS:])] = 0
+        if self.fwd_ver_dev is not None:
+            self.fwd_ver_dev.copy_(torch.from_numpy(self.fwd_ver))
         if self.dev is None:
             return notes + _patch_xids(res.raw), 2 * len(paths)
         nd = torch.frombuffer(bytearray(notes or b'\0'),
@@ -306,11 +393,16 @@ class EnsembleWorkload(object):
         if self.dev is None:
             pk = self.fan.decode(g)
             base = 0
-            for f in g.frames:
+            for src, f in enumerate(g.frames):
                 m = f // 2
                 for i in range(m):
                     nt, rp = pk[base + i], pk[base + m + i]
                     pid = int(nt['path'][-_DIGITS:])
+                    if self.trace is not None:
+                        self.trace.append((
+                            'got', self.step_no, self.phase_ms['ticks'], src,
+                            pid, rp['stat'].version if rp.get('stat')
+                            else None))
                     ok = (nt['opcode'] == 'NOTIFICATION' and
                           rp['opcode'] == 'GET_DATA' and rp['err'] == 'OK')
                     if not ok:

@@ -64,6 +64,22 @@ class FastZKServer(object):
         """Member ``i`` listens on its port again; returns the port."""
         return int(self._cmd('start %d' % i))
 
+    CLOCK = ('first_rx', 'last_rx', 'first_tx', 'last_tx', 'recv_ns',
+             'serve_ns', 'send_ns', 'blocked_ns', 'rx_bytes', 'tx_bytes',
+             'bursts', 'sends', 'recvs')
+
+    def timing(self, reset=False):
+        """The server's wire clock since the last reset (CLOCK_MONOTONIC ns,
+        the clock of ``time.perf_counter``): first / last recv that returned
+        bytes and send that moved bytes; ns spent in recv(), serving frames,
+        send() and with replies blocked on a full socket; bytes, bursts,
+        send and recv calls.  ``reset=True`` zeroes it (returns None)."""
+        if reset:
+            self._cmd('timing reset')
+            return None
+        v = [int(x) for x in self._cmd('timing').split()]
+        return dict(zip(self.CLOCK, v))
+
     @property
     def address(self):
         return {'address': '127.0.0.1', 'port': self.port}

@@ -29,18 +29,18 @@
 //            5. the entry's chain read out of the map into the tile's list
 //               of frame starts (a chain the map left open — a short frame
 //               on it — is walked serially, as is a join onto the preferred
-//               chain);
-//            6. settle (ft_settle): the links between the wave's tiles, the
-//               link into its first tile (the wave before's exit, a
-//               non-transitive one-step wait) and the frame count into its
-//               count block's sum.
+//               chain).
 //            A group maps its first tile and walks the chain on through the
 //            others (one LDS hop a frame), then checks its entry in a
 //            register table of the first tile's window roots.
-//  fs_link   Every link settled (the usual case): block 0 scans the count
-//            block sums into row bases, done.  Otherwise the full check over
-//            a grid of 16 workgroups (links, terminals, in-block counts)
-//            and the repair: a few broken links are chased — from each,
+//  fs_link   The check over a grid of 16 workgroups (one wave per 64 tiles:
+//            is each tile's entry the exit of the tile before, the first
+//            terminal, the in-block frame counts; a launch of its own until
+//            round 4 — moving it into fs_tile cost the tiles' ends more than
+//            the launch), one grid barrier.  No broken link before the first
+//            terminal (the usual case): block 0 scans the block totals into
+//            row bases, done.  Otherwise the repair: a few broken links are
+//            chased — from each,
 //            forward while the next link stays broken, the exact entry of a
 //            tile looked up among the candidates fs_tile mapped (`cx`), so a
 //            run of tiles costs a few instructions each; many are re-walked
@@ -86,17 +86,13 @@ constexpr int FL_U = 8;                    // fs_link loads per batch
 constexpr int FL_GROUNDS = 6;
 constexpr int FL_NB = 3 + 2 * FL_GROUNDS;     // broken links the check saw
 constexpr int FL_GW = FL_NB + 1;
-// Count blocks: frame counts summed per FK_T tiles (one wave's worth)
+// Count blocks: frame counts scanned per FK_T tiles (one wave's worth)
 constexpr int FK_T = 64;
 // The workspace's words after the X flags (uint64, lbw + 2 * tiles): [0..3]
-// stats, [4..5] the check's minima, [6] the last live tile, [7] fs_tile's
-// bad-link count, [8, 8 + FL_GW) fs_link's grid words, then fs_tile's
-// count-block sums (one per FK_T tiles)
-constexpr int LW_MINS = 4, LW_LAST = 6, LW_BAD = 7, LW_GRID = 8;
-constexpr int LW_CSUM = LW_GRID + FL_GW;
-// *lastk with this bit: fs_tile settled every link (fs_rows counts the
-// frames before a tile within its count block itself)
-constexpr int64_t LK_CLEAN = (int64_t)1 << 62;
+// stats, [4..5] the check's minima, [6] the last live tile, [7] unused,
+// [8, 8 + FL_GW) fs_link's grid words
+constexpr int LW_MINS = 4, LW_LAST = 6, LW_GRID = 8;
+constexpr int LW_END = LW_GRID + FL_GW;
 // Bound of fs_tile's wait for the tile before (100 MHz ticks, 2 ms): normal
 // waits are tens of microseconds; past the bound the tile takes no
 // speculated entry and fs_link re-walks it from the exact one.
@@ -1320,59 +1316,6 @@ ZK_DEV void ft_group_none(const FtCtx& C, int G) {
   }
 }
 
-// ---- the links into the wave's tiles and their frame count ----------------
-// (What a separate check kernel used to do.)  Lane 0 checks the links between
-// the wave's own tiles from its records, publishes its last tile's exit (the
-// REC word lbw[2 tl + 1] = ready | exit + 1; the stream's last tile has no
-// successor and publishes none) and checks the link into its first tile
-// against the wave before's REC word: a one-step wait that is never
-// transitive (REC goes out before the wait).  The tiles' frame count goes to
-// their count block's sum, one atomic.  A broken link, a missing entry or a
-// terminal before the stream's last tile counts in `bad`: fs_link then runs
-// the full check and the repair; otherwise fs_link only turns the block
-// sums into row bases.  (A decoupled look-back of the counts themselves
-// would wait on a chain of inclusive prefixes that crosses the stream at
-// ~64 tiles a round when every tile is resident at once.)
-template <int G>
-ZK_DEV void ft_settle(const FtCtx& C, int64_t ntiles_cap) {
-  static_assert(FK_T % G == 0, "a wave's tiles share a count block");
-  if (C.lane != 0) return;
-  const int64_t ntiles = (C.n + FT_S - 1) / FT_S;
-  const int64_t t0 = C.t, tl = min(t0 + G, ntiles) - 1;
-  bool ok = true;
-  int64_t cnt = 0, xp = 0;
-  for (int64_t k = t0; k <= tl; ++k) {
-    const int64_t e = C.rec_entry[k], m = C.rec_meta[k];
-    if (e < 0 || (k > t0 && e != xp)) ok = false;
-    if (m_term(m) && k != ntiles - 1) ok = false;
-    cnt += m_cnt(m);
-    xp = C.rec_exit[k];
-  }
-  if (tl + 1 < ntiles)
-    lb_store(&C.lbw[2 * tl + 1], (uint64_t)1 << 63 | (uint64_t)(xp + 1));
-  if (t0 > 0 && ok) {
-    uint64_t w;
-    int nap = 0;
-    const uint64_t t_w = wall_clock64();
-    for (;;) {
-      w = lb_load(&C.lbw[2 * (t0 - 1) + 1]);
-      if (w != 0 || wall_clock64() - t_w > FT_WAIT_TICKS) break;
-      if (nap < 16) __builtin_amdgcn_s_sleep(2);
-      else __builtin_amdgcn_s_sleep(16);
-      ++nap;
-    }
-    if (w == 0 || (int64_t)(w & ~((uint64_t)1 << 63)) - 1 != C.rec_entry[t0])
-      ok = false;
-  }
-  uint64_t* tail = C.lbw + 2 * ntiles_cap;
-  if (cnt)
-    __hip_atomic_fetch_add(&tail[LW_CSUM + t0 / FK_T], (uint64_t)cnt,
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (!ok)
-    __hip_atomic_fetch_add(&tail[LW_BAD], (uint64_t)1, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-}
-
 template <int W, bool LONG, int G>
 __global__ __launch_bounds__(256) void fs_tile(
     const uint8_t* __restrict__ buf, const int64_t* __restrict__ n_dev,
@@ -1521,7 +1464,6 @@ __global__ __launch_bounds__(256) void fs_tile(
     else if (N <= FT_NMAX) fs_tile_rest<W, LONG, 8>(C, true);
     else fs_tile_rest<W, LONG, 1>(C, false);
   }
-  ft_settle<G>(C, ntiles_cap);
 }
 
 // ---- fs_link ---------------------------------------------------------------
@@ -1837,44 +1779,6 @@ ZK_DEV void fl_check(int64_t ntiles, const int64_t* __restrict__ rec_entry,
                              (unsigned long long)(ntiles - fb));
     if (fterm != INF) atomicMax((unsigned long long*)&mins[1],
                                 (unsigned long long)(ntiles - fterm));
-  }
-}
-
-// fs_tile settled every link (block 0): its count-block sums csum become the
-// blocks' exclusive offsets in bsum (csum back to zero for the next scan),
-// and result[0..3] / the last tile.  A terminal can only be the last tile.
-ZK_DEV void fl_bases_clean(int64_t n, int64_t ntiles, const int64_t* rec_exit,
-                           const int64_t* rec_meta, uint64_t* csum,
-                           int64_t* bsum, int64_t cap, int64_t* result,
-                           int64_t* lastk, int64_t* red) {
-  const int tid = threadIdx.x;
-  const int64_t nbl = (ntiles + FK_T - 1) / FK_T;
-  const int64_t per = (nbl + FL_T - 1) / FL_T;
-  const int64_t b0 = (int64_t)tid * per;
-  const int64_t b1 = min(b0 + per, nbl);
-  int64_t sum = 0;
-  for (int64_t b = b0; b < b1; ++b) sum += (int64_t)csum[b];
-  int64_t tot;
-  int64_t run = block_excl_scan(sum, red, &tot);
-  for (int64_t b = b0; b < b1; ++b) {
-    const int64_t v = (int64_t)csum[b];
-    csum[b] = 0;
-    bsum[b] = run;
-    run += v;
-  }
-  if (tid == 0) {
-    const int64_t last = ntiles - 1;
-    const int64_t ml = rec_meta[last];
-    *lastk = last | LK_CLEAN;
-    result[0] = tot;
-    result[3] = tot > cap ? 1 : 0;
-    if (!m_term(ml)) {
-      result[1] = n;
-      result[2] = 0;
-    } else {
-      result[1] = rec_exit[last];
-      result[2] = m_bad(ml) ? 1 : 0;
-    }
   }
 }
 
@@ -2359,21 +2263,10 @@ __global__ __launch_bounds__(FL_T) void fs_link(
     return;
   }
   const int64_t INF = INT64_MAX;
-  uint64_t* tail = mins - LW_MINS;
-  uint64_t* csum = tail + LW_CSUM;
-  // fs_tile settled every link (the usual case): block 0 turns its count
-  // sums into row bases, done
-  if (ld_agent((const int64_t*)&tail[LW_BAD]) == 0) {
-    if (blockIdx.x != 0) return;
-    fl_bases_clean(n, ntiles, rec_exit, rec_meta, csum, bsum, cap, result,
-                   lastk, red);
-    return;
-  }
-  // the full check over the grid; then the minima and the broken-link count,
-  // read by every thread of every block before block 0 clears them (and
-  // fs_tile's words) for the next scan of this workspace
-  if (blockIdx.x == 0)
-    for (int64_t b = tid; b < (ntiles + FK_T - 1) / FK_T; b += FL_T) csum[b] = 0;
+  // the check over the grid (links, terminals, in-block counts; a launch of
+  // its own until round 4); then the minima and the broken-link count, read
+  // by every block (fs_rows clears them for the next scan of this
+  // workspace, once every block of this launch is done with them)
   fl_check(ntiles, rec_entry, rec_exit, rec_meta, base, bsum, mins, &g[FL_NB],
            blist);
   bool grid_ok = fl_sync(g);
@@ -2381,14 +2274,6 @@ __global__ __launch_bounds__(FL_T) void fs_link(
   const uint64_t mt0 = ld_agent((const int64_t*)&mins[1]);
   const unsigned long long nb0 = __hip_atomic_load(
       &g[FL_NB], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  grid_ok = grid_ok && fl_sync(g);
-  if (blockIdx.x == 0 && tid == 0) {
-    st_agent((int64_t*)&mins[0], 0);
-    st_agent((int64_t*)&mins[1], 0);
-    st_agent((int64_t*)&tail[LW_BAD], 0);
-    __hip_atomic_store(&g[FL_NB], 0ull, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-  }
   const int64_t fb0 = mb0 ? ntiles - (int64_t)mb0 : INF;
   const int64_t ft0 = mt0 ? ntiles - (int64_t)mt0 : INF;
   const bool fast = grid_ok && (fb0 == INF || fb0 > ft0);
@@ -2635,7 +2520,8 @@ __global__ __launch_bounds__(256) void fs_rows(
     const int64_t* __restrict__ rec_exit,
     const int64_t* __restrict__ base, const int64_t* __restrict__ bsum,
     const int64_t* __restrict__ lastk, int64_t* __restrict__ foff,
-    int32_t* __restrict__ flen, int64_t cap, uint64_t* __restrict__ lbw) {
+    int32_t* __restrict__ flen, int64_t cap, uint64_t* __restrict__ lbw,
+    uint64_t* __restrict__ lbw_tail) {
   // (only the staged tile: 16 KiB a block keeps fs_rows at full occupancy;
   // a frame-start array beside it cost the var-size GET 3x in fs_rows)
   __shared__ __attribute__((aligned(16))) uint8_t stage[4][FT_STAGE];
@@ -2650,22 +2536,14 @@ __global__ __launch_bounds__(256) void fs_rows(
     lbw[2 * t] = 0;
     lbw[2 * t + 1] = 0;
   }
-  const int64_t lk = *lastk;
-  const bool clean = lk >= 0 && (lk & LK_CLEAN);
-  if (t > (clean ? lk & ~LK_CLEAN : lk)) return;
-  int64_t b = bsum[t / FK_T];
-  if (clean) {
-    // fs_tile settled the links: the frames before this tile in its count
-    // block, from their records (one load a lane)
-    static_assert(FK_T == 64, "a count block is a wave");
-    const int64_t k = (t & ~(int64_t)(FK_T - 1)) + lane;
-    int64_t c = k < t ? m_cnt(rec_meta[k]) : 0;
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d, 64);
-    b += c;
-  } else {
-    b += base[t];
+  if (t == 0 && lane == 0) {
+    // fs_link's minima and broken-link count, for the next scan
+    lbw_tail[LW_MINS] = 0;
+    lbw_tail[LW_MINS + 1] = 0;
+    lbw_tail[LW_GRID + FL_NB] = 0;
   }
+  if (t > *lastk) return;
+  const int64_t b = bsum[t / FK_T] + base[t];
   const int64_t m = rec_meta[t];
   const int64_t x = rec_exit[t];
   const int32_t cnt = m_cnt(m), np = m_np(m), js = m_js(m);
@@ -2738,7 +2616,7 @@ static FsPlan fs_plan(int64_t n) {
   p.off_pre = take((size_t)tiles * FT_LMAX * 2);
   p.off_sx = take((size_t)tiles * 8);
   // X flags (2 per tile), then the words LW_* name
-  p.off_lbw = take((size_t)(2 * tiles + LW_CSUM + tiles / FK_T + 1) * 8);
+  p.off_lbw = take((size_t)(2 * tiles + LW_END) * 8);
   p.off_rent = take((size_t)tiles * 8);
   p.off_rexit = take((size_t)tiles * 8);
   p.off_rmeta = take((size_t)tiles * 8);
@@ -2855,11 +2733,11 @@ int zk_frame_scan5(const uint8_t* buf, const int64_t* n_dev, int64_t n_cap,
   uint64_t* mins = lbw + 2 * tiles + LW_MINS;
   int64_t* lastk = (int64_t*)(lbw + 2 * tiles + LW_LAST);
   unsigned long long* grid = (unsigned long long*)(lbw + 2 * tiles + LW_GRID);
-  // X flags, the stats, the check's minima, the bad-link count, fs_link's
-  // grid words and the count sums start at zero
+  // X flags, the stats, the check's minima and fs_link's grid words start
+  // at zero
   if (!clean &&
-      hipMemsetAsync(lbw, 0, (size_t)(2 * tiles + LW_CSUM + tiles / FK_T + 1) *
-                                 8, st) != hipSuccess)
+      hipMemsetAsync(lbw, 0, (size_t)(2 * tiles + LW_END) * 8, st) !=
+          hipSuccess)
     return -4;
   int64_t* dbg = fs_dbg_buf(tiles);
   // tiles (waves) per block: two 12 KiB slices, 6 blocks a CU
@@ -2911,7 +2789,7 @@ int zk_frame_scan5(const uint8_t* buf, const int64_t* n_dev, int64_t n_cap,
   ZK_LAUNCH_CHECK();
   fs_rows<<<(unsigned)((tiles + 3) / 4), 256, 0, st>>>(
       buf, n_dev, n_cap, list, pre, rmeta, rent, rexit, base, bsum, lastk,
-      foff, flen, cap, lbw);
+      foff, flen, cap, lbw, lbw + 2 * tiles);
   ZK_LAUNCH_CHECK();
   return 0;
 }

@@ -80,7 +80,10 @@ def test_bulk_tcp_wire_split():
     # serve + socket time happen inside the server's span (one connection)
     assert sp['server_serve'] + sp['server_socket'] <= \
         sp['server_span'] + 1.0
+    # (medians over the attributed batches: their sum is near, not at, the
+    # median of the sums)
     assert abs(sp['client_send'] + sp['server_span'] +
-               sp['client_capture'] - sp['send_to_capture']) < 1e-6
+               sp['client_capture'] - sp['send_to_capture']) < \
+        0.05 * sp['send_to_capture'] + 0.01
     assert w['rx_bytes'] > 0 and w['tx_bytes'] > w['rx_bytes']
     assert w['first_rx'] <= w['last_tx']

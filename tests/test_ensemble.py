@@ -136,3 +136,56 @@ def test_ensemble_gpu_codec_and_fanout_decode():
         wl.close()
     finally:
         ctl.close()
+
+
+def _replayed_catch_up(wl, gpu):
+    """One watched path written once, then its catch-up notification
+    forwarded twice (what a second SET_WATCHES at the same relZxid brings
+    when the session moves again before the first one is answered): the
+    owner forwards the change once and drops the repeat."""
+    from zkmi.parallel.fanout import notification_frames
+    p = wl.mine[0]
+    wl.client.call_sync('set', p, b'changed', -1)
+    notes = notification_frames([p], evtype=3)         # NODE_DATA_CHANGED
+    first, nf1 = wl._rearm(notes, 1)
+    again, nf2 = wl._rearm(notes, 1)
+    assert nf1 == 2 and len(first) > 0
+    assert nf2 == 0 and len(again) == 0
+    assert wl.redelivered == 1
+    assert wl.fwd_ver[int(p[-5:])] == 1
+    # a later change of the same path goes through again
+    wl.client.call_sync('set', p, b'changed2', -1)
+    _, nf3 = wl._rearm(notes, 1)
+    assert nf3 == 2 and wl.fwd_ver[int(p[-5:])] == 2
+
+
+def test_ensemble_owner_drops_replayed_catch_up():
+    from zkmi.parallel import ensemble as E
+    ctl = E.EnsembleControl(3)
+    try:
+        wl = E.EnsembleWorkload(ctl, n_paths=8, writes=2, failover_every=0,
+                                codec_device=None)
+        try:
+            _replayed_catch_up(wl, None)
+        finally:
+            wl.close()
+    finally:
+        ctl.close()
+
+
+@pytest.mark.gpu
+def test_ensemble_owner_drops_replayed_catch_up_gpu():
+    """The same on the device path (K1 + K2-K8 decode of the notes, the
+    dedup's compaction of the forwarded frames on the GPU)."""
+    import torch
+    from zkmi.parallel import ensemble as E
+    ctl = E.EnsembleControl(3)
+    try:
+        wl = E.EnsembleWorkload(ctl, n_paths=8, writes=2, failover_every=0,
+                                codec_device=torch.device('cuda', 0))
+        try:
+            _replayed_catch_up(wl, True)
+        finally:
+            wl.close()
+    finally:
+        ctl.close()

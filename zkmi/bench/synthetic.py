@@ -679,22 +679,31 @@ MIX_ACLS = (
 
 class _GraphCycle(object):
     """HIP graphs replayed in turn (a workload whose steps rotate through a
-    few shapes: one captured graph per shape)."""
+    few shapes: one captured graph per shape).  ``counter``: the name of the
+    pipeline's host step counter; capturing advanced it without running a
+    step, so it is put back and then advanced by each replay — an eager step
+    after replays continues where they left the device state."""
 
-    def __init__(self, graphs):
+    def __init__(self, graphs, pipe=None, counter=None):
         self.graphs = graphs
         self.i = 0
+        self.pipe = pipe
+        self.counter = counter
 
     def replay(self):
         self.graphs[self.i].replay()
         self.i = (self.i + 1) % len(self.graphs)
+        if self.counter:
+            setattr(self.pipe, self.counter,
+                    getattr(self.pipe, self.counter) + 1)
 
 
-def _capture_steps(pipe, acc, k=1):
+def _capture_steps(pipe, acc, k=1, counter=None):
     """Capture ``k`` consecutive steps of ``pipe`` as HIP graphs (run one
     eager step first: buffers are sized then).  A replay is a step."""
     dev = pipe.tree.device
     torch.cuda.synchronize(dev)
+    s0 = getattr(pipe, counter) if counter else None
     graphs = []
     for _ in range(k):
         g = torch.cuda.CUDAGraph()
@@ -702,7 +711,11 @@ def _capture_steps(pipe, acc, k=1):
         with torch.cuda.graph(g, capture_error_mode='thread_local'):
             pipe.step(acc=acc)
         graphs.append(g)
-    return graphs[0] if k == 1 else _GraphCycle(graphs)
+    if counter:
+        setattr(pipe, counter, s0)
+    if k == 1 and not counter:
+        return graphs[0]
+    return _GraphCycle(graphs, pipe, counter)
 
 
 class _Driver(object):
@@ -852,7 +865,7 @@ class MixPipeline(object):
     def capture(self, acc):
         """Three HIP graphs, one per rotation of the generations (step s
         creates s % 3, sets s - 1, deletes s - 2), replayed in turn."""
-        return _capture_steps(self, acc, 3)
+        return _capture_steps(self, acc, 3, counter='s')
 
     def _batch(self, n, r):
         d = self.drv
@@ -1584,7 +1597,7 @@ class WatchPipeline(object):
         written nodes are an affine permutation the host picks per step
         (:meth:`_affine`), so each graph holds one step of a cycle of
         ``cycle`` node sets; xids come from a device counter."""
-        return _capture_steps(self, acc, cycle)
+        return _capture_steps(self, acc, cycle, counter='step_no')
 
     def _roundtrip(self, rb, session, wslot, check=None):
         tx, _, total, _ = B.encode_requests(rb, self.xt, out=self.tx)

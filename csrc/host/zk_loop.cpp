@@ -81,15 +81,6 @@ double loop_spin_ms() {
   return v;
 }
 
-// ZKMI_LOOP_CORK=0 sends every write at once (A/B switch for queue_write).
-bool loop_cork() {
-  static const bool v = [] {
-    const char* e = getenv("ZKMI_LOOP_CORK");
-    return !(e && e[0] == '0');
-  }();
-  return v;
-}
-
 PyObject* os_error(int err) {
   return PyObject_CallFunction(PyExc_OSError, "is", err, strerror(err));
 }
@@ -898,7 +889,7 @@ constexpr size_t kCorkMax = 256 * 1024;
 PyObject* queue_write(Transport* t) {
   if (!t->connected) Py_RETURN_TRUE;
   Loop* L = t->w.loop;
-  if (loop_cork() && on_loop_thread(L) &&
+  if (on_loop_thread(L) &&
       t->wbuf->size() - t->woff < kCorkMax) {
     if (!t->queued) {
       t->queued = true;

@@ -189,7 +189,8 @@ def test_get_replies_exact_below_the_largest_frame(gpu, monkeypatch):
     and the serial tail).  Every frame table must still equal the host
     framing — a refused repair walk once left a tile's frame starts
     overwritten under its old record (3 frames in 20M)."""
-    monkeypatch.setenv('ZKMI_FS_WINDOW_MAX', '512')
+    from zkmi.ops import batch as B
+    monkeypatch.setattr(B, 'FS_WINDOW_AUTO_MAX', 512)
     from zkmi.bench import synthetic as S
     tree = S.GpuTree(200_000, 100, device=gpu, seed=0, data_dist=(0, 1024))
     pipe = S.GetPipeline(tree, 1 << 16, seed=1)

@@ -25,14 +25,12 @@ def main():
     dev = torch.device('cuda', 0)
     try:
         one = bench.measure_bulk_tcp(srv.port, a.nodes, a.batch, a.iters,
-                                     dev, 1)
+                                     dev, 1, srv)
         k = bench.measure_bulk_tcp(srv.port, a.nodes, a.batch, a.iters, dev, 8)
     finally:
         srv.shutdown()
     print(json.dumps({'ops_s_1conn': round(one[0]), 'phases_1conn': one[2],
-                      'ops_s_8conn': round(k[0]),
-                      'route': os.environ.get('ZKMI_ROUTE', '1'),
-                      'cork': os.environ.get('ZKMI_LOOP_CORK', '1')},
+                      'ops_s_8conn': round(k[0])},
                      default=float))
 
 

@@ -42,9 +42,7 @@ def main():
                       'blocking_p99_us': round(b99, 2),
                       'pipelined_get_ops_s': round(ops),
                       'window': a.window, 'nodes': a.nodes,
-                      'torch_gpu': a.torch_gpu,
-                      'cork': os.environ.get('ZKMI_LOOP_CORK', '1'),
-                      'route': os.environ.get('ZKMI_ROUTE', '1')}))
+                      'torch_gpu': a.torch_gpu}))
 
 
 if __name__ == '__main__':

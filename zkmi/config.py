@@ -42,3 +42,12 @@ class ClientConfig(object):
     # the ConnectRequest (K9) and SET_WATCHES (K11) records and decode the
     # ConnectResponse (K9) of every (re)connect (models/gpucodec.py)
     codec_device: Optional[str] = None
+    # not in the reference: the native completion path (README).  Replies
+    # to outstanding requests settled in the native loop's read path
+    # (Transport.route); requests made off the loop thread encoded and sent
+    # from the calling thread (ZKConnectionFSM.request_direct); and how long
+    # call_sync polls for the reply before it sleeps (None: 100 us on hosts
+    # with >= 16 CPUs, else 0)
+    native_route: bool = True
+    direct_send: bool = True
+    sync_spin_us: Optional[float] = None

@@ -30,17 +30,12 @@ from ..utils.metrics import create_collector, METRIC_ZK_EVENT_COUNTER
 from .connection import ZKConnectionFSM
 from .connection_set import ConnectionSet, StaticResolver
 
-# call_sync's poll window before it sleeps on the reply lock, seconds
-# (ZKMI_SYNC_SPIN_US).  Default 100 us on hosts with >= 16 CPUs: on a GPU
-# box the blocking get() RTT went 37-44 -> 20 us (tools/gpu_r3k.sh; a
-# 30 us window is shorter than the round trip and does nothing); off on
-# small hosts, where the poller competes with the loop thread for the GIL.
-# ZKMI_DIRECT=0: requests made off the loop thread always hop to it first
-# (ZKConnectionFSM.request_direct is the default when the router is on)
-_DIRECT = os.environ.get('ZKMI_DIRECT', '1') != '0'
-_SYNC_SPIN_S = float(os.environ.get(
-    'ZKMI_SYNC_SPIN_US',
-    '100' if (os.cpu_count() or 1) >= 16 else '0')) / 1e6
+# call_sync's default poll window before it sleeps on the reply lock
+# (ClientConfig.sync_spin_us): 100 us on hosts with >= 16 CPUs — on a GPU
+# box the blocking get() RTT went 37-44 -> 20 us (a 30 us window is shorter
+# than the round trip and does nothing); off on small hosts, where the
+# poller competes with the loop thread for the GIL.
+_SYNC_SPIN_US_AUTO = 100.0 if (os.cpu_count() or 1) >= 16 else 0.0
 from .session import ZKSession
 
 
@@ -374,7 +369,7 @@ class Client(FSM):
         if self.loop.in_loop():
             self._issue(pkt, cb, on_reply)
             return
-        if _DIRECT and self._hops == 0:
+        if self.config.direct_send and self._hops == 0:
             # another thread: send from here when the live connection's
             # native router will settle the reply (request_direct) and no
             # earlier submission is still waiting for the loop
@@ -697,11 +692,13 @@ class Client(FSM):
             done.release()
         getattr(self, method)(*args, cb)
         got = False
-        if _SYNC_SPIN_S > 0:
+        spin = self.config.sync_spin_us
+        spin = (_SYNC_SPIN_US_AUTO if spin is None else spin) / 1e6
+        if spin > 0:
             # a short poll before sleeping on the lock: the reply usually
             # lands within tens of us, and a sleeping thread's wake-up costs
-            # about that much again (ZKMI_SYNC_SPIN_US)
-            t_end = time.perf_counter() + _SYNC_SPIN_S
+            # about that much again (ClientConfig.sync_spin_us)
+            t_end = time.perf_counter() + spin
             while not got and time.perf_counter() < t_end:
                 got = done.acquire(False)
                 if not got:

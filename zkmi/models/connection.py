@@ -15,7 +15,6 @@ table keyed by xid, and the xid->opcode map the reply decoder needs because
 ZooKeeper replies are not self-describing (SURVEY §7.4 hard part 1).
 """
 
-import os
 import threading
 import time
 
@@ -29,9 +28,6 @@ from ..runtime.tcp import TcpSocket
 from ..streams import ZKDecoder, ZKEncoder
 from . import gpucodec
 
-# ZKMI_ROUTE=0 keeps every reply on the Python path (A/B switch for the
-# native completion path, ZKConnectionFSM._route)
-_ROUTE = os.environ.get('ZKMI_ROUTE', '1') != '0'
 
 
 class ZKRequest(EventEmitter):
@@ -413,7 +409,7 @@ class ZKConnectionFSM(FSM):
                     if self.session is not None:
                         self.session.fold_routed(z, rx)
             return
-        if self.routing or not _ROUTE or sock is None or \
+        if self.routing or not self.config.native_route or sock is None or \
                 not sock.can_route() or \
                 self.tracer is not None or self.log.enabled('trace') or \
                 codec.DECODE_REPLY_C is None or self.decoder is None or \

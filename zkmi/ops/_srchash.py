@@ -17,7 +17,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(
     os.path.abspath(__file__))))
 KDIR = os.path.join(ROOT, 'csrc', 'kernels')
 
-ARCH = os.environ.get('ZKMI_OFFLOAD_ARCH', 'gfx950')
+ARCH = 'gfx950'                  # MI355X only
 HIP_FLAGS = ['--offload-arch=' + ARCH, '-O3', '-fPIC', '-std=c++17',
              '-Wno-unused-result', '-Wno-unused-value', '-munsafe-fp-atomics']
 

@@ -14,7 +14,6 @@ K10 :func:`encode_requests`; K11 :func:`encode_set_watches`; K12
 """
 
 from dataclasses import dataclass
-import os
 
 import numpy as np
 import torch
@@ -316,10 +315,11 @@ FS_WINDOW_AUTO_MAX = 1024
 def frame_window(max_frame):
     """The K1 entry window for a stream whose frames are at most
     ``max_frame`` bytes (length prefix included): the smallest window
-    covering them, up to 1 KiB; past that (or past ``ZKMI_FS_WINDOW_MAX``,
-    an A/B cap) the window is 1 KiB (the cap) in long-frame mode.  Frames
-    longer than the window are framed exactly either way."""
-    cap = int(os.environ.get('ZKMI_FS_WINDOW_MAX', FS_WINDOW_AUTO_MAX))
+    covering them, up to 1 KiB; past that (or past the module's
+    ``FS_WINDOW_AUTO_MAX``, which a test lowers) the window is the cap in
+    long-frame mode.  Frames longer than the window are framed exactly
+    either way."""
+    cap = FS_WINDOW_AUTO_MAX
     cap = min(max(cap, FS_WINDOWS[0]), FS_WINDOWS[-1])
     for w in FS_WINDOWS:
         if max_frame <= w and w <= cap:

@@ -4,7 +4,7 @@
 # this pool).
 set -eo pipefail
 cd "$(dirname "$0")/.."
-read -r SO LOOP_SO < <(python tools/build_native.py --sanitize | tail -1)
+read -r SO LOOP_SO _WATCH_SO < <(python tools/build_native.py --sanitize | tail -1)
 export LD_PRELOAD="$(gcc -print-file-name=libasan.so):$(gcc -print-file-name=libubsan.so)"
 export ASAN_OPTIONS=detect_leaks=0:abort_on_error=1
 export UBSAN_OPTIONS=halt_on_error=1:print_stacktrace=1

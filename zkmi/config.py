@@ -49,5 +49,8 @@ class ClientConfig(object):
     # call_sync polls for the reply before it sleeps (None: 100 us on hosts
     # with >= 16 CPUs, else 0)
     native_route: bool = True
+    # the session's watch events in the native engine (csrc/host/
+    # zk_watch.cpp) instead of one Python state machine per (path, event)
+    native_watch: bool = True
     direct_send: bool = True
     sync_spin_us: Optional[float] = None

@@ -469,10 +469,13 @@ class ZKConnectionFSM(FSM):
         err = ZKError(code, consts.ERR_TEXT.get(code, str(code)))
         req.settle('error', err, pkt)
 
-    def request(self, pkt):
+    def request(self, pkt, req=None):
+        """Send ``pkt``; returns the request (``req``: an object with the
+        ZKRequest surface the reply settles — the native watch engine's)."""
         if not self.isInState('connected'):
             raise Exception('Client must be connected to send requests')
-        req = ZKRequest(pkt)
+        if req is None:
+            req = ZKRequest(pkt)
         with self.xid_lock:
             xid = self.xid
             self.xid = (xid + 1) & 0x7fffffff

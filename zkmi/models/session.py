@@ -20,6 +20,11 @@ import time
 
 from .. import jute
 from ..runtime.emitter import EventEmitter
+
+try:
+    from .. import _zkwatch
+except ImportError:                      # not built: the Python FSMs
+    _zkwatch = None
 from ..runtime.fsm import FSM
 from ..utils.metrics import METRIC_ZK_NOTIFICATION_COUNTER
 
@@ -114,7 +119,19 @@ class ZKSession(FSM):
         self.passwd = b'\0' * 8
         collector.counter(METRIC_ZK_NOTIFICATION_COUNTER,
                           'Notifications received from ZooKeeper')
+        # the watch events: the native engine (one table, the Python side
+        # keeps only the listeners) or one ZKWatchEvent FSM per (path, event)
+        self.wt = None
+        if _zkwatch is not None and getattr(config, 'native_watch', True):
+            self.wt = _zkwatch.WatchTable(self._wt_emit, loop,
+                                          float(config.doublecheck_ms),
+                                          float(config.doublecheck_rand_ms))
         FSM.__init__(self, 'detached', loop)
+
+    def _fsm_enter(self, state):
+        FSM._fsm_enter(self, state)
+        if self.wt is not None:
+            self._wt_sync()
 
     # -- queries --------------------------------------------------------------
 
@@ -296,6 +313,8 @@ class ZKSession(FSM):
                     self.old_conn.destroy()
                     self.old_conn = None
                 self.resumeWatches()
+            if self.wt is not None:
+                self._wt_sync()          # (after the SET_WATCHES)
         S.on(conn, 'stateChanged', on_conn_state)
 
         def on_attach(newconn):
@@ -383,9 +402,30 @@ class ZKSession(FSM):
     # -- watches --------------------------------------------------------------
 
     def watchersDisconnected(self):
+        if self.wt is not None:
+            self.wt.disconnected()
         for w in list(self.watchers.values()):
             for ev in w.events():
                 ev.disconnected()
+
+    def _wt_emit(self, path, evt, *args):
+        """The native engine's user-visible events, to the path's
+        ZKWatcher listeners."""
+        w = self.watchers.get(path)
+        if w is not None:
+            EventEmitter.emit(w, evt, *args)
+
+    def _wt_sync(self):
+        """Tell the native engine whether watch requests can go out: the
+        session attached and its connection connected (the reference's
+        wait_session / wait_connected)."""
+        wt = self.wt
+        conn = self.conn
+        if self.isInState('attached') and conn is not None and \
+                conn.isInState('connected'):
+            wt.ready(conn)
+        else:
+            wt.unready()
 
     def processNotification(self, pkt):
         if pkt['state'] != 'SYNC_CONNECTED':
@@ -411,8 +451,9 @@ class ZKSession(FSM):
         for path, w in list(self.watchers.items()):
             cod = False
             for ev in w.events():
-                if not ev.isInState('resuming'):
-                    continue
+                if isinstance(ev, _NativeWatchEvent) or \
+                        not ev.isInState('resuming'):
+                    continue               # (the engine's: resume_lists)
                 e = ev.getEvent()
                 if e == 'createdOrDeleted':
                     if cod:
@@ -427,6 +468,13 @@ class ZKSession(FSM):
                     raise AssertionError('unknown event: ' + e)
                 count += 1
                 all_evts.append(ev)
+        batch = None
+        if self.wt is not None:
+            batch, dw, ew, cw = self.wt.resume_lists()
+            events['dataChanged'] += dw
+            events['createdOrDestroyed'] += ew
+            events['childrenChanged'] += cw
+            count += len(dw) + len(ew) + len(cw)
         if self.bulk_watches:
             events['dataChanged'] = events['dataChanged'] + self._bulk_packed
             count += self._bulk_packed.n
@@ -448,6 +496,8 @@ class ZKSession(FSM):
                 return
             for ev in all_evts:
                 ev.resume()
+            if batch is not None:
+                self.wt.resumed(batch)
         self.conn.setWatches(events, zxid, done)
 
     def add_bulk_watches(self, paths):
@@ -499,6 +549,10 @@ class ZKWatcher(EventEmitter):
         raise Exception('ZKWatcher does not support once() (use on)')
 
     def notify(self, evt):
+        wt = self.session.wt
+        if wt is not None and wt.has(self.path):
+            wt.notify(self.path, evt)
+            return
         types = self._NOTIFY.get(evt)
         if types is None:
             raise Exception('Unknown notification type: ' + evt)
@@ -547,12 +601,49 @@ class ZKWatcher(EventEmitter):
             evt = 'createdOrDeleted'
         if evt not in ('createdOrDeleted', 'dataChanged', 'childrenChanged'):
             return
+        wt = self.session.wt
+        if wt is not None:
+            if evt not in self.evts:
+                self.evts[evt] = _NativeWatchEvent(wt, self.path, evt)
+            wt.arm(self.path, evt)
+            return
         ev = self.evts.get(evt)
         if ev is None:
             ev = ZKWatchEvent(self.session, self.path, self, evt, self.log)
             self.evts[evt] = ev
         if ev.isInState('disarmed'):
             ev.arm()
+
+
+class _NativeWatchEvent(object):
+    """A watch event held by the native engine: the ZKWatchEvent queries
+    (state, history) read from its table."""
+
+    def __init__(self, wt, path, evt):
+        self.wt = wt
+        self.path = path
+        self.evt = evt
+
+    def getEvent(self):
+        return self.evt
+
+    def getState(self):
+        return self.wt.state(self.path, self.evt)
+
+    def isInState(self, st):
+        cur = self.getState() or ''
+        return cur == st or cur.startswith(st + '.')
+
+    @property
+    def fsm_history(self):
+        return self.wt.history(self.path, self.evt)
+
+    # (the session drives the engine as a whole: these are no-ops here)
+    def disconnected(self):
+        pass
+
+    def resume(self):
+        pass
 
 
 class ZKWatchEvent(FSM):

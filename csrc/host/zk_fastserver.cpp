@@ -31,8 +31,9 @@
 // recv that returned bytes, first / last send that moved bytes, and the
 // sums of time in recv(), in serving frames (tree lock + replies), in
 // send() and with replies waiting for the socket to drain (EAGAIN until the
-// next send that moves bytes); bytes in / out and bursts served.  "timing"
-// answers "OK" and those 13 numbers, "timing reset" zeroes them.
+// next send that moves bytes); bytes in / out, bursts served, send() and
+// recv() calls, bursts served in parallel and the time in them.  "timing"
+// answers "OK" and those 15 numbers, "timing reset" zeroes them.
 // Notifications to a connection served by another worker go through that
 // connection's note buffer (its own mutex) and the worker's eventfd; every
 // burst drains the notes before serving, so a notification always precedes
@@ -75,6 +76,8 @@
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -114,7 +117,7 @@ int64_t mono_ns() {
 // The wire clock (header comment): all fields atomics, workers add to them
 struct WireClock {
   enum { FIRST_RX, LAST_RX, FIRST_TX, LAST_TX, RECV, SERVE, SEND, BLOCKED,
-         RX_BYTES, TX_BYTES, BURSTS, SENDS, RECVS, N };
+         RX_BYTES, TX_BYTES, BURSTS, SENDS, RECVS, PAR_BURSTS, PAR_NS, N };
   std::atomic<int64_t> v[N];
   WireClock() { reset(); }
   void reset() { for (auto& x : v) x.store(0, std::memory_order_relaxed); }
@@ -225,6 +228,82 @@ struct Wr {
 
 struct Worker;
 
+// Helper threads that serve one connection's large read burst in parallel
+// (ServePool::run).  A single pipelined connection's batch of a million
+// GETs was served by its one worker thread, ~0.9 us a request, and nothing
+// was sent before all of it was served: the bulk TCP benchmark's bound
+// (the server's wire clock, `timing`).  Reads of a burst touch the tree
+// under the worker's shared lock only, so chunks of the burst are served
+// into separate buffers by several threads and appended in order.
+struct ServePool {
+  std::vector<std::thread> th;
+  std::mutex mu, run_mu;
+  std::condition_variable cv, done_cv;
+  std::function<void(int)> job;
+  int next = 0, total = 0, pending = 0;
+  uint64_t gen = 0;
+  bool stop = false;
+
+  explicit ServePool(int n) {
+    for (int i = 0; i < n; ++i) th.emplace_back([this] { loop(); });
+  }
+  ~ServePool() {
+    {
+      std::lock_guard<std::mutex> g(mu);
+      stop = true;
+    }
+    cv.notify_all();
+    for (auto& t : th) t.join();
+  }
+  int size() const { return (int)th.size(); }
+  // grab and run tasks of the current job until none is left
+  void work() {
+    for (;;) {
+      int k;
+      {
+        std::lock_guard<std::mutex> g(mu);
+        if (next >= total) return;
+        k = next++;
+      }
+      job(k);
+      std::lock_guard<std::mutex> g(mu);
+      if (--pending == 0) done_cv.notify_all();
+    }
+  }
+  void loop() {
+    uint64_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> g(mu);
+        cv.wait(g, [&] { return stop || gen != seen; });
+        if (stop) return;
+        seen = gen;
+      }
+      work();
+    }
+  }
+  // n tasks f(0..n-1), the caller working too; false (nothing ran) when
+  // another connection's burst holds the pool
+  bool run(int n, const std::function<void(int)>& f) {
+    std::unique_lock<std::mutex> r(run_mu, std::try_to_lock);
+    if (!r.owns_lock()) return false;
+    {
+      std::lock_guard<std::mutex> g(mu);
+      job = f;
+      next = 0;
+      total = n;
+      pending = n;
+      ++gen;
+    }
+    cv.notify_all();
+    work();
+    std::unique_lock<std::mutex> g(mu);
+    done_cv.wait(g, [&] { return pending == 0; });
+    job = nullptr;
+    return true;
+  }
+};
+
 struct Conn {
   int fd;
   int member = 0;
@@ -240,6 +319,7 @@ struct Conn {
 };
 
 struct Server {
+  ServePool* pool = nullptr;     // parallel read bursts (nullptr: serial)
   std::shared_mutex mu;          // the tree and the session table
   std::unordered_map<std::string, std::unique_ptr<Node>> nodes;
   std::unordered_map<int64_t, std::string> sessions;    // sid -> passwd
@@ -450,9 +530,10 @@ struct Server {
 
   // One request frame body -> one reply appended to c->out.  Returns false
   // when the connection must close after this reply (CLOSE_SESSION).
-  bool serve(const uint8_t* b, int32_t n, Conn* c, std::string* key) {
+  bool serve(const uint8_t* b, int32_t n, Conn* c, std::string* key,
+             std::string* out = nullptr) {
     const int64_t sid = c->sid;
-    std::string* o = &c->out;
+    std::string* o = out != nullptr ? out : &c->out;
     Rd r{b, b + n};
     const int32_t xid = r.i32(), op = r.i32();
     // a SET_WATCHES catch-up notifies this connection before its reply
@@ -840,6 +921,7 @@ struct Worker {
     if (writes) ex.lock(); else sh.lock();
     // notifications of writes before this burst go out ahead of its replies
     drain_notes(c);
+    if (!writes && S->pool != nullptr && serve_parallel(c)) return true;
     bool dead = false;
     while (!c.closing && c.in.size() - c.in_off >= 4) {
       uint32_t l;
@@ -864,6 +946,52 @@ struct Worker {
       c.in_off += 4 + (size_t)len;
     }
     return !dead;
+  }
+
+  // A read burst of plain reads (GET_DATA, EXISTS, children, SYNC, PING:
+  // nothing that notifies this connection) of at least PAR_MIN frames,
+  // served in chunks on the pool; the replies appended in request order.
+  // False: not such a burst (or the pool is busy): the serial path.
+  static constexpr size_t PAR_MIN = 8192;
+  std::vector<std::pair<uint32_t, uint32_t>> fr;   // (body offset, length)
+  bool serve_parallel(Conn& c) {
+    fr.clear();
+    size_t o = c.in_off;
+    while (c.in.size() - o >= 12) {
+      uint32_t l, opw;
+      memcpy(&l, c.in.data() + o, 4);
+      const int32_t len = (int32_t)ntohl(l);
+      if (len < 8 || len > MAX_PACKET) break;
+      if (c.in.size() - o < 4 + (size_t)len) break;
+      memcpy(&opw, c.in.data() + o + 8, 4);
+      const int32_t op = (int32_t)ntohl(opw);
+      if (op != OP_GET_DATA && op != OP_EXISTS && op != OP_GET_CHILDREN &&
+          op != OP_GET_CHILDREN2 && op != OP_SYNC && op != OP_PING)
+        break;
+      fr.emplace_back((uint32_t)(o + 4 - c.in_off), (uint32_t)len);
+      o += 4 + (size_t)len;
+    }
+    if (fr.size() < PAR_MIN) return false;
+    const int K = std::min<int>(S->pool->size() + 1,
+                                (int)(fr.size() / (PAR_MIN / 4)));
+    std::vector<std::string> outs(K);
+    const uint8_t* base = (const uint8_t*)c.in.data() + c.in_off;
+    const size_t nf = fr.size();
+    const int64_t tp = mono_ns();
+    const bool ran = S->pool->run(K, [&](int k) {
+      std::string key;
+      const size_t f0 = nf * k / K, f1 = nf * (k + 1) / K;
+      outs[k].reserve((f1 - f0) * 128);
+      for (size_t f = f0; f < f1; ++f)
+        S->serve(base + fr[f].first, (int32_t)fr[f].second, &c, &key,
+                 &outs[k]);
+    });
+    if (!ran) return false;
+    wclock.add(WireClock::PAR_BURSTS, 1);
+    wclock.add(WireClock::PAR_NS, mono_ns() - tp);
+    for (auto& x : outs) c.out.append(x);
+    c.in_off = o;
+    return true;
   }
 
   void rearm(int fd, Conn& c) {
@@ -1096,17 +1224,23 @@ int main(int argc, char** argv) {
   int32_t dbytes = 100, fanout = 1000;
   unsigned hw = std::thread::hardware_concurrency();
   int nthreads = (int)(hw == 0 ? 4 : (hw < 16 ? hw : 16));
+  int serve_threads = (int)(hw == 0 ? 0 : (hw < 8 ? hw - 1 : 7));
   for (int i = 1; i + 1 < argc; i += 2) {
     if (!strcmp(argv[i], "--port")) port = atoi(argv[i + 1]);
     else if (!strcmp(argv[i], "--preload")) pre = atoll(argv[i + 1]);
     else if (!strcmp(argv[i], "--data-bytes")) dbytes = atoi(argv[i + 1]);
     else if (!strcmp(argv[i], "--fanout")) fanout = atoi(argv[i + 1]);
     else if (!strcmp(argv[i], "--threads")) nthreads = atoi(argv[i + 1]);
+    else if (!strcmp(argv[i], "--serve-threads"))
+      serve_threads = atoi(argv[i + 1]);
     else if (!strcmp(argv[i], "--members")) members = atoi(argv[i + 1]);
   }
   if (nthreads < 1) nthreads = 1;
   if (members < 1) members = 1;
   Server S;
+  // helpers for a connection's large read bursts (--serve-threads; 0: off)
+  ServePool pool(serve_threads);
+  if (serve_threads > 0) S.pool = &pool;
   S.mconns.resize(members);
   if (pre > 0) preload(S, pre, dbytes, fanout);
   else { S.make("/", "", 0, 0); S.make("/zookeeper", "", 0, 0); }

@@ -267,3 +267,62 @@ def test_member_outage_and_resume():
             r.close()
     finally:
         srv.shutdown()
+
+
+def _read_burst(port, reqs, nreplies):
+    """One raw session: the whole request stream in one send, then every
+    reply frame (bytes, in order)."""
+    r = Raw(port)
+    r.s.sendall(reqs)
+    out = []
+    for _ in range(nreplies):
+        out.append(r._frame())
+    r.s.close()
+    return out
+
+
+def test_parallel_read_burst_matches_serial():
+    """A connection's large read burst (>= 8192 plain reads) is served in
+    chunks by the server's helper threads; its replies must be the serial
+    server's, byte for byte and in order: GET_DATA / EXISTS (some with
+    watch=1) / GET_CHILDREN2 / SYNC, present and missing nodes."""
+    ops = []
+    for i in range(12000):
+        k = i % 5
+        p = leaf(i % NLEAF) if i % 7 else '/bench/missing%d' % i
+        if k == 0:
+            ops.append({'opcode': 'GET_DATA', 'path': p, 'watch': i % 3 == 0})
+        elif k == 1:
+            ops.append({'opcode': 'EXISTS', 'path': p, 'watch': i % 4 == 0})
+        elif k == 2:
+            ops.append({'opcode': 'GET_CHILDREN2',
+                        'path': '/bench/d%06d' % (i % 3), 'watch': False})
+        elif k == 3:
+            ops.append({'opcode': 'SYNC', 'path': p})
+        else:
+            ops.append({'opcode': 'GET_DATA', 'path': p, 'watch': False})
+    reqs = b''.join(jute.frame(jute.encode_request(dict(o, xid=i + 1)))
+                    for i, o in enumerate(ops))
+    got = {}
+    for st in (0, 4):
+        srv = fast.FastZKServer(preload=NLEAF, data_bytes=24, fanout=FANOUT,
+                                serve_threads=st)
+        try:
+            got[st] = _read_burst(srv.port, reqs, len(ops))
+            w = srv.timing()
+        finally:
+            srv.shutdown()
+        assert (w['par_bursts'] > 0) == (st > 0), w
+    # (the two servers' preloads ran at different times: ctime / mtime)
+    xmap = {i + 1: o['opcode'] for i, o in enumerate(ops)}
+
+    def norm(body):
+        rep = jute.decode_response(body, xmap)
+        st = rep.get('stat')
+        if st is not None:
+            rep['stat'] = (st.czxid, st.mzxid, st.version, st.cversion,
+                           st.dataLength, st.numChildren, st.pzxid,
+                           st.ephemeralOwner)
+        return rep
+    assert len(got[0]) == len(got[4])
+    assert [norm(b) for b in got[0]] == [norm(b) for b in got[4]]

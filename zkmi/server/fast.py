@@ -24,7 +24,7 @@ class FastZKServer(object):
     synthetic ``/bench`` tree of N leaves (GpuTree's layout)."""
 
     def __init__(self, preload=0, data_bytes=100, fanout=1000, port=0,
-                 threads=None, members=1):
+                 threads=None, members=1, serve_threads=None):
         if not available():
             raise RuntimeError('zk_fastserver not built '
                                '(tools/build_native.py)')
@@ -35,6 +35,8 @@ class FastZKServer(object):
             [BINARY, '--port', str(port), '--preload', str(preload),
              '--data-bytes', str(data_bytes), '--fanout', str(fanout)] +
             (['--threads', str(threads)] if threads else []) +
+            (['--serve-threads', str(serve_threads)]
+             if serve_threads is not None else []) +
             (['--members', str(members)] if members > 1 else []),
             stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True,
             env=env)
@@ -66,7 +68,7 @@ class FastZKServer(object):
 
     CLOCK = ('first_rx', 'last_rx', 'first_tx', 'last_tx', 'recv_ns',
              'serve_ns', 'send_ns', 'blocked_ns', 'rx_bytes', 'tx_bytes',
-             'bursts', 'sends', 'recvs')
+             'bursts', 'sends', 'recvs', 'par_bursts', 'par_ns')
 
     def timing(self, reset=False):
         """The server's wire clock since the last reset (CLOCK_MONOTONIC ns,

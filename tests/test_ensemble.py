@@ -152,11 +152,15 @@ def _replayed_catch_up(wl, gpu):
     assert nf1 == 2 and len(first) > 0
     assert nf2 == 0 and len(again) == 0
     assert wl.redelivered == 1
-    assert wl.fwd_ver[int(p[-5:])] == 1
+
+    def fwd():
+        k = int(p[-5:])
+        return int(wl.fwd_ver_dev[k].item()) if gpu else int(wl.fwd_ver[k])
+    assert fwd() == 1
     # a later change of the same path goes through again
     wl.client.call_sync('set', p, b'changed2', -1)
     _, nf3 = wl._rearm(notes, 1)
-    assert nf3 == 2 and wl.fwd_ver[int(p[-5:])] == 2
+    assert nf3 == 2 and fwd() == 2
 
 
 def test_ensemble_owner_drops_replayed_catch_up():

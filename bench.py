@@ -884,6 +884,13 @@ def run_rank(a):
                           'tables; no floating-point compute',
         }
         print(json.dumps(line), flush=True)
+    # captured graphs hold the communicator's work: release them (and the
+    # pipelines holding them) before the group goes — destroying an RCCL
+    # group under a live graph waits forever in its shutdown
+    pipe = None
+    import gc
+    gc.collect()
+    torch.cuda.synchronize()
     if dist.is_initialized():
         dist.destroy_process_group()
 

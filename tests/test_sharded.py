@@ -219,6 +219,7 @@ def test_sharded_forced_route_rccl_captured(gpu, streams):
     s.close()
     dist.init_process_group('nccl', device_id=gpu, rank=0, world_size=1,
                             init_method='tcp://127.0.0.1:%d' % port)
+    g = pipe = None
     try:
         assert dist.get_backend() == 'nccl'
         tree = GpuTree(20000, 100, fanout=100, device=gpu, seed=0,
@@ -244,4 +245,11 @@ def test_sharded_forced_route_rccl_captured(gpu, streams):
         assert st['overflow_segments'] == 0
         assert st['xgmi_lower_bound_ms'] == 0.0
     finally:
+        # the graph holds the communicator's captured work: release it
+        # before the group goes (destroying the group under a live graph
+        # waits forever in the communicator's shutdown)
+        g = pipe = None
+        import gc
+        gc.collect()
+        torch.cuda.synchronize()
         dist.destroy_process_group()

@@ -1345,19 +1345,11 @@ __global__ __launch_bounds__(256) void fs_tile(
   const int lane = threadIdx.x & 63;
   const int64_t n = stream_len(n_dev, n_cap);
   const int64_t ntiles = (n + FT_S - 1) / FT_S;
-  // Tiles XCD by XCD: workgroups are dealt round-robin over the 8 XCDs
-  // (b and b + 8 share one), each XCD starting its own in order, so the
-  // tiles of one XCD's workgroups form one contiguous range and a tile's
-  // predecessor (whose candidate word it waits for) was started before it
-  // on the same XCD — only the first tile of each range waits on another
-  // XCD.  (In plain workgroup order a tile's predecessor sits on the next
-  // XCD over, which may start it later.)  The wait is bounded, so no
-  // dispatch order can deadlock it.
-  const int64_t nb = gridDim.x, b = blockIdx.x;
-  const int64_t per = nb / 8, rem = nb % 8, x = b % 8, kx = b / 8;
-  const int64_t lb = x < rem ? x * (per + 1) + kx
-                             : rem * (per + 1) + (x - rem) * per + kx;
-  const int64_t t = (lb * (blockDim.x >> 6) + wv) * G;
+  // (tiles in workgroup order: a tile's predecessor was dispatched before
+  // it.  An XCD-by-XCD mapping — each XCD a contiguous tile range — put
+  // the predecessor on the same L2 but started every range's tail later:
+  // reply stream 94 -> 103 us.)
+  const int64_t t = ((int64_t)blockIdx.x * (blockDim.x >> 6) + wv) * G;
   if (t >= ntiles) return;
   C.t_0 = dbg ? wall_clock64() : 0;
   const int64_t ts = t * FT_S;

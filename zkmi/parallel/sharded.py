@@ -119,12 +119,18 @@ class ShardedGetPipeline(object):
         self.recv_stats = torch.zeros(1, dtype=I64, device=dev)
         self.steps = 0
         self.subs = []
+        self.comm = None
         if streams > 1:
             per = [batch // streams + (1 if k < batch % streams else 0)
                    for k in range(streams)]
             self.subs = [_Conn(self, m, seed * streams + k)
                          for k, m in enumerate(per)]
             self.streams = [torch.cuda.Stream(dev) for _ in per]
+            # one stream issues every collective (the communicator runs
+            # them in order anyway): the connections' kernels overlap the
+            # all-to-alls, and a captured graph has one collective chain
+            if self.route and self.coll == dev:
+                self.comm = torch.cuda.Stream(dev)
         else:
             self.subs = [_Conn(self, batch, seed)]
             self.streams = None
@@ -136,7 +142,14 @@ class ShardedGetPipeline(object):
         """Equal-split ``all_to_all_single`` on the collective device
         (device tensors with RCCL; host staging for a gloo rehearsal)."""
         if self.coll == self.dev:
-            dist.all_to_all_single(out, inp, group=self.group)
+            if self.comm is None:
+                dist.all_to_all_single(out, inp, group=self.group)
+                return out
+            cur = torch.cuda.current_stream(self.dev)
+            self.comm.wait_stream(cur)
+            with torch.cuda.stream(self.comm):
+                dist.all_to_all_single(out, inp, group=self.group)
+            cur.wait_stream(self.comm)
             return out
         o = torch.empty(out.shape, dtype=out.dtype, device=self.coll)
         dist.all_to_all_single(o, inp.to(self.coll), group=self.group)

@@ -170,8 +170,18 @@ class ShardedGetPipeline(object):
             c.device_seed()
         torch.cuda.synchronize(self.dev)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, capture_error_mode='thread_local'):
-            self.step(acc=acc)
+        # Under capture the collectives go on the capture's origin stream:
+        # RCCL work issued from a forked stream of the capture faulted in
+        # hipStreamEndCapture (tools/microbench/fr_probe.py: --mode comm vs
+        # origin); the connections' own kernels still run on their streams.
+        origin = torch.cuda.Stream(self.dev)
+        comm, self.comm = self.comm, origin if self.comm is not None else None
+        try:
+            with torch.cuda.graph(g, stream=origin,
+                                  capture_error_mode='thread_local'):
+                self.step(acc=acc)
+        finally:
+            self.comm = comm
         self.graph = g
         return g
 

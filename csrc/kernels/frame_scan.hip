@@ -264,7 +264,8 @@ ZK_DEV int64_t ft_cand(const uint8_t* sb, const uint32_t* sbits, int32_t e,
 // ---- fs_tile: the tile's chain map, by pointer jumping ---------------------
 //
 // Every position p of the tile whose length word reads as a plausible frame
-// body (minb <= len < FT_LIMIT; in the entry window also any length up to
+// body (minb <= len <= W - 4, the window covering the stream's frames;
+// < FT_LIMIT in long-frame mode; in the entry window also any length up to
 // maxp) is a NODE.  A node's successor is the next frame start, p + 4 + len:
 // another node, or a ROOT where the chain ends inside the tile's view —
 //   EXIT   the chain leaves the tile (val = its last frame's start: the exit
@@ -1399,10 +1400,17 @@ __global__ __launch_bounds__(256) void fs_tile(
       d[4 * j + 3] = q.w;
     }
     d[16] = *(const uint32_t*)(sb + P0 + 64);
-    // minb <= len < FT_LIMIT; in the entry window any legal length (a
-    // frame there longer than the tile is still an entry's chain)
+    // minb <= len <= W - 4 past the entry window (the window covers the
+    // stream's frames: a longer length is a byte pattern, not a frame; the
+    // rare real one meets the map as a SHORT root and is walked exactly),
+    // len < FT_LIMIT in long-frame mode; in the entry window any legal
+    // length (a frame there longer than the tile is still an entry's
+    // chain).  (Length-like words inside frames — zxids in [2^27, 2^28)
+    // read 2048..4095 — took a create / set / delete reply tile past
+    // FT_NMAX nodes: no map, no speculation, a 200 ms serial repair.)
     const uint32_t lim = P0 < W ? (uint32_t)(maxp32 - minb + 1)
-                                : (uint32_t)(FT_LIMIT - minb);
+                         : LONG ? (uint32_t)(FT_LIMIT - minb)
+                                : (uint32_t)(W - 3 - minb);
     uint32_t lo = 0, hi = 0;
 #pragma unroll
     for (int j = 0; j < 32; ++j) {

@@ -43,8 +43,11 @@ def test_server_wire_clock():
         c.wait_connected(10)
         for _ in range(20):
             c.call_sync('get', '/bench/d000000/n000000001')
-        t1 = time.perf_counter()
+        # (the server stamps a send after send() returns: the client may
+        # have the reply before that; read the clock once it settled)
+        time.sleep(0.05)
         w = srv.timing()
+        t1 = time.perf_counter()
         c.close_sync(10)
         srv.timing(reset=True)
         z = srv.timing()

@@ -209,3 +209,25 @@ def test_get_replies_exact_below_the_largest_frame(gpu, monkeypatch):
         got = ft.off[:r['frames']].cpu().numpy()
         assert np.array_equal(got, np.asarray(want, np.int64))
         assert int(acc.item()) == 1 << 16
+
+
+def test_length_like_words_keep_the_map(gpu):
+    """Delete-reply-sized frames (16-byte bodies) whose zxid field reads as
+    a 2-4 KiB length (zxid in [2^27, 2^28): bytes 00 00 08..0f xx): past
+    the entry window such words are not nodes (the window covers the
+    stream's frames), so every tile keeps its map and its speculated entry.
+    Counting them took a tile past the map's 512 nodes — no speculation, a
+    serial repair of ~200 ms per 50 MB reply stream."""
+    rng = np.random.default_rng(5)
+    n = 200000
+    lens = np.full(n, 16, np.int64)
+    buf, starts = _stream(rng, lens)
+    zx = (1 << 27) + np.arange(n, dtype=np.int64) * 7
+    for k in range(8):                     # xid 4 bytes, then the zxid
+        buf[starts + 8 + k] = ((zx >> (8 * (7 - k))) & 0xff).astype(np.uint8)
+    for k in range(4):                     # err = 0
+        buf[starts + 16 + k] = 0
+    r, off, ms, st = _scan_timed(buf, n, 512)
+    _check(r, off, buf, starts)
+    assert st['no_spec'] == 0 and st['rewalked'] == 0, st
+    assert ms < 5.0, ms

@@ -101,6 +101,11 @@ def main():
     ap.add_argument('--data-dist', default=None)
     ap.add_argument('--batch', type=int, default=1 << 19)
     ap.add_argument('--reps', type=int, default=20)
+    ap.add_argument('--workload', default='get',
+                    help='get, or mix (create / set / delete replies)')
+    ap.add_argument('--zxid', type=lambda x: int(x, 0), default=None,
+                    help='the tree zxid the GET replies carry (their header '
+                         'bytes: length-like words for some ranges)')
     ap.add_argument('--group', type=int, default=None,
                     help='tiles a wave takes on the reply stream (1, 2, 4)')
     a = ap.parse_args()
@@ -110,17 +115,31 @@ def main():
         lo, hi = a.data_dist.split('-')
         dist = (int(lo), int(hi))
     tree = S.GpuTree(1_000_000, 100, device=dev, seed=0, data_dist=dist)
-    pipe = S.GetPipeline(tree, a.batch, seed=1)
-    for _ in range(2):
-        pipe.step()
+    if a.workload == 'mix':
+        tree = S.GpuTree(1_000_000, 100, device=dev, seed=0,
+                         spare=(2 * a.batch + 8192) / 1e6 + 0.05)
+    if a.zxid is not None:
+        tree.counters[_lib.TC_ZXID] = a.zxid
+    if a.workload == 'mix':
+        pipe = S.MixPipeline(tree, 2 * a.batch, 100, seed=1)
+        for _ in range(2):
+            pipe.step()
+        drv = pipe.drv
+        tx, srv, rwin = drv.tx, drv.server, drv.rwindow
+        rgroup = drv.rscanner.group
+    else:
+        pipe = S.GetPipeline(tree, a.batch, seed=1)
+        for _ in range(2):
+            pipe.step()
+        tx, srv, rwin = pipe.tx, pipe.server, pipe.rwindow
+        rgroup = pipe.rscanner.group
     torch.cuda.synchronize()
-    srv = pipe.server
     req_n = srv.scanner.table.result[1:2].clone()
     rx, rtotal = srv.result[0], srv.result[1]
-    ok = bench('request', pipe.tx, req_n, srv.window, a.reps)
-    group = pipe.rscanner.group if a.group is None else a.group
-    ok &= bench('reply', rx, rtotal.reshape(1)[:1].clone(), pipe.rwindow,
-                a.reps, group)
+    ok = bench('request', tx, req_n, srv.window, a.reps)
+    group = rgroup if a.group is None else a.group
+    ok &= bench('reply', rx, rtotal.reshape(1)[:1].clone(), rwin, a.reps,
+                group)
     print('ALL EXACT' if ok else 'MISMATCH', flush=True)
     sys.exit(0 if ok else 1)
 

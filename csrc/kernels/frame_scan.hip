@@ -540,6 +540,64 @@ ZK_DEV int32_t ft_cands(const FtNodes<NK>& me, const uint8_t* sb,
   return 0xFFFF - (int32_t)((k >> 32) & 0xFFFF);
 }
 
+// ft_cands for a tile without a map (more than FT_NMAX nodes: payloads of
+// small big-endian words, each a plausible length).  The window's first
+// 128 nodes are walked, one chain per lane and round, all lanes at once
+// (per-lane LDS hops); their exits and the preferred chain are chosen as
+// ft_cands chooses them.  Without this the tile published no candidate,
+// the next one had no speculated entry, and a run of such tiles became a
+// serial repair.
+template <int W>
+ZK_DEV int32_t ft_cands_walk(const uint8_t* sb, const FtBlk& blk,
+                             uint32_t* xbits, int32_t nrel, int32_t maxp,
+                             int32_t& sx, int lane) {
+  uint64_t best = 0;
+  for (int r = 0; r < 2; ++r) {
+    // this lane's window node: index lane + 64 r in position order
+    int32_t want = lane + 64 * r, p = -1;
+    for (int b = 0; b < W / 64 && p < 0; ++b) {
+      uint64_t m = blk.mask[b];
+      const int32_t c = __popcll(m);
+      if (want < c) {
+        for (int k = 0; k < want; ++k) m &= m - 1;
+        p = b * 64 + (int32_t)__builtin_ctzll(m);
+      } else {
+        want -= c;
+      }
+    }
+    if (!__ballot(p >= 0)) break;
+    int32_t c = p, cnt = 0, x = -1;
+    bool live = p >= 0;
+    while (live) {
+      if (c + 4 > nrel) break;
+      const int32_t len = lds_be32(sb, c);
+      if ((uint32_t)len > (uint32_t)maxp) break;
+      const int32_t nx = c + 4 + len;
+      if (nx > nrel) break;
+      ++cnt;
+      if (nx >= FT_S) { x = nx - FT_S; break; }
+      c = nx;
+    }
+    if (x >= 0) {
+      if (x < W)
+        __hip_atomic_fetch_or(&xbits[x >> 5], 1u << (x & 31),
+                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+      const uint64_t key = (uint64_t)((uint32_t)cnt << 16 |
+                                      (uint32_t)(0xFFFF - p)) << 32 |
+                           (uint32_t)x;
+      best = best > key ? best : key;
+    }
+  }
+#pragma unroll
+  for (int s = 32; s >= 1; s >>= 1) {
+    const uint64_t o = (uint64_t)__shfl_xor((long long)best, s, 64);
+    best = best > o ? best : o;
+  }
+  if (!best) return -1;
+  sx = (int32_t)(uint32_t)best;
+  return 0xFFFF - (int32_t)((best >> 32) & 0xFFFF);
+}
+
 // The frame starts of the chain entering at tile position e with root word
 // w into the wave's slots (slot k = the k-th start): every node of that
 // root with count c <= D at or after e lands in slot D - c; the successor
@@ -592,6 +650,10 @@ ZK_DEV int32_t ft_chain(const FtNodes<NK>& me, const uint8_t* sb,
   return __ballot(!ok) ? -1 : D;
 }
 
+ZK_DEV int64_t ft_walk(const uint8_t* sb, int32_t c, int32_t nrel,
+                       int32_t maxp32, int64_t ts, uint16_t* L, int32_t& mo,
+                       int lane);
+
 // What fs_tile's steps 2-5 need from the kernel.
 struct FtCtx {
   const uint8_t* buf;
@@ -620,7 +682,7 @@ struct FtCtx {
 };
 
 template <int W, bool LONG, int NK>
-ZK_DEV void fs_tile_rest(const FtCtx& cx_, bool mapped) {
+ZK_DEV int64_t fs_tile_rest(const FtCtx& cx_, bool mapped) {
   const FtCtx& C = cx_;
   const int lane = C.lane;
   const uint8_t* sb = C.sb;
@@ -639,9 +701,10 @@ ZK_DEV void fs_tile_rest(const FtCtx& cx_, bool mapped) {
 
   // ---- 3. the window entries' exits: this tile's candidates for the next -
   int32_t px = -1, sp = -1;
-  if (mapped) {
+  {
     int32_t x = -1;
-    sp = ft_cands<W, LONG, NK>(me, sb, C.xbits, x);
+    sp = mapped ? ft_cands<W, LONG, NK>(me, sb, C.xbits, x)
+                : ft_cands_walk<W>(sb, C.blk, C.xbits, nrel, maxp32, x, lane);
     if (sp >= 0 && x >= 0 && x < (LONG ? FT_S - 1 : W)) px = x;
   }
   // Candidates go out packed in ONE 64-bit word (a relaxed agent-scope
@@ -783,8 +846,9 @@ ZK_DEV void fs_tile_rest(const FtCtx& cx_, bool mapped) {
     }
   }
   if (!done) {
-    // survivor list: the preferred chain's starts (when the map has them)
-    if (sp >= 0) {
+    // survivor list: the preferred chain's starts (from the map, or
+    // walked when the tile has none)
+    if (sp >= 0 && mapped) {
       const uint32_t ws = ft_root_at(sb, C.blk, C.pk, sp, nrel, maxp32, minb);
       const int32_t D = ft_chain<NK>(me, sb, C.blk, C.slot, sp, ws, lane);
       if (D > 0) {
@@ -792,6 +856,10 @@ ZK_DEV void fs_tile_rest(const FtCtx& cx_, bool mapped) {
         m = D;
         send = ft_send(sb, ws, ts);
       }
+    } else if (sp >= 0) {
+      __builtin_amdgcn_wave_barrier();
+      send = ft_walk(sb, sp, nrel, maxp32, ts, L, m, lane);
+      if (m == 0) send = -1;
     }
     __builtin_amdgcn_wave_barrier();
     // survivor bits from the list just stored (each lane rereads only what
@@ -878,6 +946,7 @@ ZK_DEV void fs_tile_rest(const FtCtx& cx_, bool mapped) {
       d[7] = t_f;
     }
   }
+  return send;
 }
 
 // ---- tile groups: the map once, then the chain walked on ------------------
@@ -990,6 +1059,78 @@ ZK_DEV int32_t ft_sv_at(const uint32_t (&sv)[SVN], int32_t q) {
   return __builtin_amdgcn_readlane((int)v, q & 63);
 }
 
+// The group's other tiles: the chain leaving tile t0 (end code send0; alive:
+// the tile has one) walked on through them, each tile's records and its one
+// candidate entry written as it goes; then the group's last exit published
+// as the next group's candidate.  `nxt` holds tile t0 + 1, loaded by the
+// caller (its load overlaps the caller's work).
+template <int W, int G>
+ZK_DEV void ft_group_tail(const FtCtx& C, int64_t send0, bool alive,
+                          FtTileRegs& nxt) {
+  const int lane = C.lane;
+  uint8_t* sb = C.sb;
+  const int64_t n = C.n, t0 = C.t;
+  const int32_t maxp32 = C.maxp32;
+  const int64_t ntiles = (n + FT_S - 1) / FT_S;
+  // ---- the group's other tiles: the survivor's chain walked on -----------
+  int64_t send = send0;
+  int32_t kdone = 1;
+  for (int k = 1; k < G; ++k) {
+    const int64_t tk = t0 + k;
+    if (tk >= ntiles) break;
+    const int64_t tsk = tk * FT_S;
+    const int64_t c = send;                 // the chain's entry into tk
+    const bool live = alive && !(send & TERM) && c >= tsk &&
+                      c < tsk + FT_S;
+    if (!live) break;
+    ft_store(sb, nxt, lane);
+    if (k + 1 < G && tk + 1 < ntiles) ft_load(C.buf, n, tsk + FT_S, lane, nxt);
+    int32_t m;
+    const int32_t nrelk = (int32_t)min(n - tsk, (int64_t)1 << 30);
+    send = ft_walk(sb, (int32_t)(c - tsk), nrelk, maxp32, tsk,
+                   C.list + tk * FT_LMAX, m, lane);
+    FcWalk wk{c, m, 0, m > 0 ? 0 : -1, false, false};
+    fc_join_end(wk, send, n);
+    if (lane == 0) {
+      // the tile's one candidate entry: the walk's (for fs_link's chase)
+      lb_store(&C.lbw[2 * (tk - 1)],
+               (uint64_t)1 << 63 | (uint64_t)(c - tsk + 1));
+      C.cx[5 * tk] = ft_cx_of(send, m);
+      C.sx[tk] = send;
+      C.rcount[tk] = m;
+      C.rec_entry[tk] = c;
+      C.rec_exit[tk] = wk.exit;
+      C.rec_meta[tk] = fc_meta(wk);
+    }
+    if (lane >= 1 && lane < 5) C.cx[5 * tk + lane] = FC_DEAD;
+    kdone = k + 1;
+  }
+  // tiles the walk did not reach: no entry (fs_link re-walks them)
+  for (int k = kdone; k < G; ++k) {
+    const int64_t tk = t0 + k;
+    if (tk >= ntiles) break;
+    if (lane == 0) {
+      lb_store(&C.lbw[2 * (tk - 1)], (uint64_t)1 << 63);
+      C.sx[tk] = -1;
+      C.rcount[tk] = 0;
+      C.rec_entry[tk] = -1;
+      C.rec_exit[tk] = -1;
+      C.rec_meta[tk] = 0;
+    }
+    if (lane < 5) C.cx[5 * tk + lane] = FC_DEAD;
+  }
+  // the group's last exit: the next group's candidate
+  const int64_t tl = min(t0 + G, ntiles) - 1;
+  {
+    uint64_t word = (uint64_t)1 << 63;
+    const int64_t tle = (tl + 1) * FT_S;
+    if (kdone == (int32_t)(tl - t0 + 1) && alive && !(send & TERM) &&
+        send >= tle && send < tle + W)
+      word |= (uint64_t)(send - tle + 1);
+    if (lane == 0) lb_store(&C.lbw[2 * tl], word);
+  }
+}
+
 template <int W, int NK, int G>
 ZK_DEV void fs_group_rest(const FtCtx& cx_) {
   static_assert(G > 1 && W <= 512, "groups: small windows");
@@ -1049,65 +1190,9 @@ ZK_DEV void fs_group_rest(const FtCtx& cx_) {
     sv[i] = lane + 64 * i < m0 ? C.slot[lane + 64 * i] : 0u;
   const int64_t t_1 = C.dbg ? wall_clock64() : 0;
 
-  // ---- the group's other tiles: the survivor's chain walked on -----------
-  int64_t send = send0;
-  int32_t kdone = 1;
   FtTileRegs nxt;
   if (G > 1 && t0 + 1 < ntiles) ft_load(C.buf, n, ts + FT_S, lane, nxt);
-  for (int k = 1; k < G; ++k) {
-    const int64_t tk = t0 + k;
-    if (tk >= ntiles) break;
-    const int64_t tsk = tk * FT_S;
-    const int64_t c = send;                 // the chain's entry into tk
-    const bool live = sp >= 0 && !(send & TERM) && c >= tsk &&
-                      c < tsk + FT_S;
-    if (!live) break;
-    ft_store(sb, nxt, lane);
-    if (k + 1 < G && tk + 1 < ntiles) ft_load(C.buf, n, tsk + FT_S, lane, nxt);
-    int32_t m;
-    const int32_t nrelk = (int32_t)min(n - tsk, (int64_t)1 << 30);
-    send = ft_walk(sb, (int32_t)(c - tsk), nrelk, maxp32, tsk,
-                   C.list + tk * FT_LMAX, m, lane);
-    FcWalk wk{c, m, 0, m > 0 ? 0 : -1, false, false};
-    fc_join_end(wk, send, n);
-    if (lane == 0) {
-      // the tile's one candidate entry: the walk's (for fs_link's chase)
-      lb_store(&C.lbw[2 * (tk - 1)],
-               (uint64_t)1 << 63 | (uint64_t)(c - tsk + 1));
-      C.cx[5 * tk] = ft_cx_of(send, m);
-      C.sx[tk] = send;
-      C.rcount[tk] = m;
-      C.rec_entry[tk] = c;
-      C.rec_exit[tk] = wk.exit;
-      C.rec_meta[tk] = fc_meta(wk);
-    }
-    if (lane >= 1 && lane < 5) C.cx[5 * tk + lane] = FC_DEAD;
-    kdone = k + 1;
-  }
-  // tiles the walk did not reach: no entry (fs_link re-walks them)
-  for (int k = kdone; k < G; ++k) {
-    const int64_t tk = t0 + k;
-    if (tk >= ntiles) break;
-    if (lane == 0) {
-      lb_store(&C.lbw[2 * (tk - 1)], (uint64_t)1 << 63);
-      C.sx[tk] = -1;
-      C.rcount[tk] = 0;
-      C.rec_entry[tk] = -1;
-      C.rec_exit[tk] = -1;
-      C.rec_meta[tk] = 0;
-    }
-    if (lane < 5) C.cx[5 * tk + lane] = FC_DEAD;
-  }
-  // the group's last exit: the next group's candidate
-  const int64_t tl = min(t0 + G, ntiles) - 1;
-  {
-    uint64_t word = (uint64_t)1 << 63;
-    const int64_t tle = (tl + 1) * FT_S;
-    if (kdone == (int32_t)(tl - t0 + 1) && sp >= 0 && !(send & TERM) &&
-        send >= tle && send < tle + W)
-      word |= (uint64_t)(send - tle + 1);
-    if (lane == 0) lb_store(&C.lbw[2 * tl], word);
-  }
+  ft_group_tail<W, G>(C, send0, sp >= 0, nxt);
 
   // ---- the first tile's entry: the group before's exit -------------------
   int64_t E = 0;
@@ -1296,27 +1381,6 @@ ZK_DEV void fs_group_rest(const FtCtx& cx_) {
   }
 }
 
-// Tiles t0 + 1 .. of a group the map could not take (too many nodes):
-// no entry, no candidates (fs_link re-walks them).
-ZK_DEV void ft_group_none(const FtCtx& C, int G) {
-  const int64_t ntiles = (C.n + FT_S - 1) / FT_S;
-  for (int k = 1; k < G; ++k) {
-    const int64_t tk = C.t + k;
-    if (tk >= ntiles) break;
-    if (C.lane == 0) {
-      if (k >= 2) lb_store(&C.lbw[2 * (tk - 1)], (uint64_t)1 << 63);
-      C.sx[tk] = -1;
-      C.rcount[tk] = 0;
-      C.rec_entry[tk] = -1;
-      C.rec_exit[tk] = -1;
-      C.rec_meta[tk] = 0;
-    }
-    if (C.lane < 5) C.cx[5 * tk + C.lane] = FC_DEAD;
-    if (C.lane == 0 && (k == G - 1 || tk + 1 >= ntiles))
-      lb_store(&C.lbw[2 * tk], (uint64_t)1 << 63);
-  }
-}
-
 template <int W, bool LONG, int G>
 __global__ __launch_bounds__(256) void fs_tile(
     const uint8_t* __restrict__ buf, const int64_t* __restrict__ n_dev,
@@ -1465,8 +1529,12 @@ __global__ __launch_bounds__(256) void fs_tile(
     else if (N <= 256) fs_group_rest<W, 4, G>(C);
     else if (N <= FT_NMAX) fs_group_rest<W, 8, G>(C);
     else {
-      fs_tile_rest<W, LONG, 1>(C, false);
-      ft_group_none(C, G);
+      // no map for the first tile (its candidates walked lane by lane):
+      // its survivor's exit is walked on through the group as usual
+      const int64_t s0 = fs_tile_rest<W, LONG, 1>(C, false);
+      FtTileRegs nxt;
+      if (t + 1 < (n + FT_S - 1) / FT_S) ft_load(buf, n, ts + FT_S, lane, nxt);
+      ft_group_tail<W, G>(C, s0, s0 >= 0, nxt);
     }
   } else {
     if (N <= 128) fs_tile_rest<W, LONG, 2>(C, true);

@@ -445,6 +445,8 @@ def main():
                          'step captured as a HIP graph after the warmup '
                          '(every replay draws a new batch from a '
                          'device-resident seed; ~2%% faster than eager)')
+    ap.add_argument('--stream-priority', action='store_true',
+                    help='get: connection 0 on a high-priority stream')
     ap.add_argument('--stagger', action='store_true',
                     help='get: offset the pipelined connections by half a '
                          'step (measured no faster than lockstep, 0.80 vs '
@@ -661,7 +663,8 @@ def run_rank(a):
             tree = S.GpuTree(a.nodes, a.data_bytes, device=dev, seed=rank,
                              data_dist=dd, name_pad=npad)
             return S.GetPipeline(tree, a.batch, seed=rank, streams=a.streams,
-                                 stagger=a.stagger)
+                                 stagger=a.stagger,
+                                 priority=a.stream_priority)
         from zkmi.parallel.sharded import ShardedGetPipeline
         # every rank holds the same layout and data (seed 0); its index
         # covers only the leaves whose path hashes to it

@@ -462,7 +462,8 @@ class GetPipeline(object):
     # client encode | server decode | tree + encode | client decode
     PHASES = 4
 
-    def __init__(self, tree, batch, seed=0, streams=1, stagger=False):
+    def __init__(self, tree, batch, seed=0, streams=1, stagger=False,
+                 priority=False):
         self.tree = tree
         self.batch = batch
         dev = tree.device
@@ -484,7 +485,11 @@ class GetPipeline(object):
                    for k in range(streams)]
             self.subs = [GetPipeline(tree, m, seed=seed * streams + k)
                          for k, m in enumerate(per)]
-            self.streams = [torch.cuda.Stream(dev) for _ in per]
+            # priority: connection 0's stream is a high-priority one (its
+            # small kernels take the next free slots, the others fill in)
+            self.streams = [torch.cuda.Stream(
+                dev, priority=-1 if priority and k == 0 else 0)
+                for k in range(len(per))]
             self.stagger = stagger
             self._gens = None
             self.last = None

@@ -535,26 +535,41 @@ ZK_DEV void stage_out_segs(const uint32_t* lw, int64_t a0c, int64_t B0,
   }
 }
 
-// One hole, slot -> out, by a whole wave: 16 bytes a lane, the source read
-// as dwords and realigned (alignbyte) to the 16-byte aligned destination.
-// The source's last dword may reach 3 bytes past the data: inside the slot
-// (its data capacity is rounded up to 16, plus 4).
-ZK_DEV void copy_hole(const uint8_t* __restrict__ src, uint8_t* dst,
-                      int64_t n, int lane) {
+// One hole, slot -> out, by a 16-lane quarter of a wave: 16 bytes a lane per
+// chunk, four chunks (1 KiB a quarter) loaded before any is stored (one
+// dependent round trip per hole, not per chunk).  The source is read as
+// dwords and realigned (alignbyte) to the 16-byte aligned destination; its
+// last dword may reach 3 bytes past the data: inside the slot (its data
+// capacity is rounded up to 16, plus 4).
+ZK_DEV void copy_hole_q(const uint8_t* __restrict__ src, uint8_t* dst,
+                        int64_t n, int ql) {
+  constexpr int U = 4;
   const int sh = (int)((uintptr_t)src & 3);
   const uint32_t* sa = (const uint32_t*)((uintptr_t)src & ~(uintptr_t)3);
-  for (int64_t x = (int64_t)lane * 16; x < n; x += 64 * 16) {
-    const uint32_t* p = sa + (x >> 2);
-    uint32_t w[5];
+  for (int64_t x0 = (int64_t)ql * 16; x0 < n; x0 += 16 * 16 * U) {
+    uint32_t w[U][5];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) w[j] = p[j];
-    w[4] = sh ? p[4] : 0u;
-    uint4 v;
-    v.x = __builtin_amdgcn_alignbyte(w[1], w[0], sh);
-    v.y = __builtin_amdgcn_alignbyte(w[2], w[1], sh);
-    v.z = __builtin_amdgcn_alignbyte(w[3], w[2], sh);
-    v.w = __builtin_amdgcn_alignbyte(w[4], w[3], sh);
-    *(uint4*)(dst + x) = v;
+    for (int u = 0; u < U; ++u) {
+      const int64_t x = x0 + 16 * 16 * u;
+      if (x < n) {
+        const uint32_t* p = sa + (x >> 2);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) w[u][k] = p[k];
+        w[u][4] = sh ? p[4] : 0u;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t x = x0 + 16 * 16 * u;
+      if (x < n) {
+        uint4 v;
+        v.x = __builtin_amdgcn_alignbyte(w[u][1], w[u][0], sh);
+        v.y = __builtin_amdgcn_alignbyte(w[u][2], w[u][1], sh);
+        v.z = __builtin_amdgcn_alignbyte(w[u][3], w[u][2], sh);
+        v.w = __builtin_amdgcn_alignbyte(w[u][4], w[u][3], sh);
+        *(uint4*)(dst + x) = v;
+      }
+    }
   }
 }
 
@@ -655,20 +670,28 @@ __global__ __launch_bounds__(ENC_T) void resp_write(
     emit_response(k, r, s, i, E.sz[i - r0] - 4, pre, hole);
   }, stage);
   __syncthreads();                 // (bl: records written whole)
-  // the holes, one reply per wave-iteration
+  // the holes: four replies per wave-iteration, one per 16-lane quarter,
+  // each quarter's loads all issued before its stores
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t lt = r1 - 1 - r0;
   const int64_t nb = (H.hb[lt] & 511) + (H.hole[lt] ? 1 : 0);
-  for (int64_t j = wv; j < nb; j += ENC_T / 64) {
-    const int li = H.bl[j];
-    if (li < 0) continue;                 // written whole
-    const int64_t i = r0 + li;
-    const uint8_t* slot = s.slab + (r.slot ? r.slot[i]
-                                           : s.slot_off[r.node[i]]);
-    const int64_t o = E.off[li];
-    const int64_t h0 = hole_h0(o);
-    copy_hole(slot + ZK_SLOT_LEN + (h0 - (o + 20)), out + h0, H.hole[li],
-              lane);
+  for (int64_t j0 = 4 * wv; j0 < nb; j0 += 4 * (ENC_T / 64)) {
+    const int64_t j = j0 + (lane >> 4);
+    const int li = j < nb ? H.bl[j] : -1;          // -1: written whole
+    const uint8_t* src = nullptr;
+    uint8_t* dst = nullptr;
+    int64_t hn = 0;
+    if (li >= 0) {
+      const int64_t i = r0 + li;
+      const uint8_t* slot = s.slab + (r.slot ? r.slot[i]
+                                             : s.slot_off[r.node[i]]);
+      const int64_t o = E.off[li];
+      const int64_t h0 = hole_h0(o);
+      src = slot + ZK_SLOT_LEN + (h0 - (o + 20));
+      dst = out + h0;
+      hn = H.hole[li];
+    }
+    copy_hole_q(src, dst, hn, lane & 15);
   }
 }
 

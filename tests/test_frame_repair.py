@@ -234,7 +234,7 @@ def test_length_like_words_keep_the_map(gpu):
     assert ms < 5.0, ms
 
 
-@pytest.mark.parametrize('group', [1, 4])
+@pytest.mark.parametrize('group', [1, 4, 8])
 def test_dense_length_words_walk_the_candidates(gpu, group):
     """Frames within the window whose payloads are all plausible length
     words (a tile holds far more than the map's 512 nodes): the tile walks

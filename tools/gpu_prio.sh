@@ -14,3 +14,8 @@ import json; d=json.loads(open('$OUT/prio_${m}_$r.log').read().strip().split('\n
 print('%-5s %d %.4f ms/step sustained %.4f' % ('$m', $r, d['ms_per_step'], d['sustained']['ms_per_step']))"
   done
 done
+for g in 8 4; do
+  timeout -k 10 120 python tools/microbench/k1_bench.py --group $g > $OUT/k1g${g}.log 2>&1 || exit $?
+  echo "group $g: $(grep reply $OUT/k1g${g}.log)"
+done
+bash tools/gpu_varprof.sh

@@ -101,6 +101,9 @@ def main():
     ap.add_argument('--data-dist', default=None)
     ap.add_argument('--batch', type=int, default=1 << 19)
     ap.add_argument('--reps', type=int, default=20)
+    ap.add_argument('--win-max', type=int, default=None,
+                    help='batch.FS_WINDOW_AUTO_MAX for this run (the largest '
+                         'window chosen without long-frame mode)')
     ap.add_argument('--workload', default='get',
                     help='get, or mix (create / set / delete replies)')
     ap.add_argument('--zxid', type=lambda x: int(x, 0), default=None,
@@ -110,6 +113,8 @@ def main():
                     help='tiles a wave takes on the reply stream (1, 2, 4)')
     a = ap.parse_args()
     dev = torch.device('cuda', 0)
+    if a.win_max is not None:
+        B.FS_WINDOW_AUTO_MAX = a.win_max
     dist = None
     if a.data_dist:
         lo, hi = a.data_dist.split('-')

@@ -14,7 +14,7 @@ pass() {
   local name=$1; shift
   timeout -s KILL 120 rocprofv3 --kernel-trace --output-format csv \
     --pmc "$@" -d $OUT/$name -o pmc -- python3 $REPO/bench.py \
-    --workload $W --steps 3 --warmup 1 --no-rtt > $OUT/$name.log 2>&1
+    --workload $W --steps 3 --warmup 1 --no-rtt --no-sustain > $OUT/$name.log 2>&1
   local rc=$?
   echo "pass $name rc=$rc"
   return $rc

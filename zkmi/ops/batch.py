@@ -360,9 +360,11 @@ class FrameScanner:
         self.window = window
         # the stream's usual frame size: >= 128 bytes within a small window
         # lets a wave take a group of tiles (the chain map once, then the
-        # chain walked on; csrc/kernels/frame_scan.hip fs_group_rest)
+        # chain walked on; csrc/kernels/frame_scan.hip fs_group_rest).
+        # GET reply stream (192-byte frames): 8 tiles a wave 77.4 us, 4
+        # tiles 93.0 us (profiles/r4_k1_microbench.md)
         if group is None:
-            group = 4 if frame_hint is not None and frame_hint >= 128 else 1
+            group = 8 if frame_hint is not None and frame_hint >= 128 else 1
         self.group = group
         self.max_packet = max_packet
         self.table = FrameTable(torch.empty(cap, dtype=I64, device=device),

@@ -306,10 +306,13 @@ FS_WINDOWS = (256, 512, 1024, 2048)
 # again past the window when a long frame leaves no walker alive, and takes
 # survivor exits past the window as the next tile's entry
 FS_WIN_LONG = 1 << 16
-# the largest window chosen on its own: a 2 KiB window's frontier (32
-# walkers a lane) cost more than the long-frame passes over the 1-2 % of
-# tiles a longer frame covers (uniform 0-1024 B GET: 1.78 vs 1.94 ms a step)
-FS_WINDOW_AUTO_MAX = 1024
+# the largest window chosen on its own.  Round 3's frontier made a 2 KiB
+# window dear (32 walkers a lane) and capped it at 1 KiB; with the chain map
+# the window only widens the entry positions, and long-frame mode at 1 KiB
+# left a 0-1024 B GET reply stream (frames to 1116 B) without speculation
+# in hundreds of tiles: 750.7 us a scan at a 1 KiB cap, 244.2 us at 2 KiB
+# (profiles/r4_k1_microbench.md)
+FS_WINDOW_AUTO_MAX = 2048
 
 
 def frame_window(max_frame):

@@ -101,6 +101,8 @@ def main():
     ap.add_argument('--data-dist', default=None)
     ap.add_argument('--batch', type=int, default=1 << 19)
     ap.add_argument('--reps', type=int, default=20)
+    ap.add_argument('--req-group', type=int, default=1,
+                    help='tiles a wave takes on the request stream')
     ap.add_argument('--win-max', type=int, default=None,
                     help='batch.FS_WINDOW_AUTO_MAX for this run (the largest '
                          'window chosen without long-frame mode)')
@@ -141,7 +143,7 @@ def main():
     torch.cuda.synchronize()
     req_n = srv.scanner.table.result[1:2].clone()
     rx, rtotal = srv.result[0], srv.result[1]
-    ok = bench('request', tx, req_n, srv.window, a.reps)
+    ok = bench('request', tx, req_n, srv.window, a.reps, a.req_group)
     group = rgroup if a.group is None else a.group
     ok &= bench('reply', rx, rtotal.reshape(1)[:1].clone(), rwin, a.reps,
                 group)

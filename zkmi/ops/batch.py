@@ -411,6 +411,8 @@ class FrameScanner:
         that used to reset them per scan): tiles without a speculated
         entry, tiles re-walked, repair rounds, tiles fs_link's chases
         looked up in fs_tile's candidate exits."""
+        if getattr(self, 'last_cap', None) is None:      # no scan yet
+            return {'no_spec': 0, 'rewalked': 0, 'rounds': 0, 'looked_up': 0}
         with _on(stream):
             out = _lib.lib().frame_scan_stats(self.ws, self.last_cap,
                                               int(self.window))

@@ -35,7 +35,7 @@ for s in range(a.steps):
     torch.cuda.synchronize()
     ms = 1e3 * (time.perf_counter() - t0)
     st = pipe.nscan.chain_stats()
-    if st['no_spec'] or st['rewalked'] or ms > 10:
+    if s > 0 and (st['no_spec'] or st['rewalked'] or ms > 10):
         print('step %d %.2f ms %r window %d zxid %d' % (
             s, ms, st, pipe.nscan.window, int(tree.counters[1].item())),
             flush=True)

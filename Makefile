@@ -27,11 +27,12 @@ sanitize:                 ## host codec suites under ASan + UBSan
 bench:                    ## headline benchmark, 1 GPU
 	$(PY) bench.py
 
-bench-all:                ## get / mix / storm workloads + tests (needs a GPU)
-	bash tools/gpu_bench_all.sh
+bench-all:                ## gpu tests + get / mix / storm workloads (needs a GPU)
+	bash tools/gpu.sh tests bench=--no-rtt bench=--no-rtt,--workload,mix \
+	  bench=--no-rtt,--workload,storm
 
 prof:                     ## rocprofv3 kernel stats for the three workloads
-	PROF=prof bash tools/gpu_bench_all.sh
+	bash tools/gpu.sh prof=prof,get,mix,storm
 
 clean:
 	rm -rf build zkmi/ops/libzkmi_hip.so zkmi/_zkhost*.so

@@ -98,10 +98,27 @@ struct Handle {
   bool cancelled;
 };
 
+// Handle, Transport and Server are GC types: a timer's callback, or a
+// transport's protocol, usually refers back to the object that holds the
+// handle or transport (a connection, a session), and a closed client's
+// objects must be collectable.  Objects the loop still holds (queued
+// handles, registered transports) are kept alive by those references.
+int Handle_traverse(Handle* h, visitproc visit, void* arg) {
+  Py_VISIT(h->fn);
+  Py_VISIT(h->args);
+  return 0;
+}
+
+int Handle_clear(Handle* h) {
+  Py_CLEAR(h->fn);
+  Py_CLEAR(h->args);
+  return 0;
+}
+
 void Handle_dealloc(Handle* h) {
-  Py_XDECREF(h->fn);
-  Py_XDECREF(h->args);
-  Py_TYPE(h)->tp_free((PyObject*)h);
+  PyObject_GC_UnTrack(h);
+  Handle_clear(h);
+  PyObject_GC_Del(h);
 }
 
 PyObject* Handle_cancel(Handle* h, PyObject*) {
@@ -347,7 +364,7 @@ void invoke(Loop* L, PyObject* obj, const char* name, PyObject* arg) {
 }
 
 Handle* new_handle(PyObject* fn, PyObject* args) {
-  Handle* h = PyObject_New(Handle, &HandleType);
+  Handle* h = PyObject_GC_New(Handle, &HandleType);
   if (h == nullptr) return nullptr;
   Py_INCREF(fn);
   h->fn = fn;
@@ -357,6 +374,7 @@ Handle* new_handle(PyObject* fn, PyObject* args) {
   h->when = 0;
   h->seq = 0;
   h->cancelled = false;
+  PyObject_GC_Track((PyObject*)h);
   return h;
 }
 
@@ -443,7 +461,7 @@ PyTypeObject ServerType = {PyVarObject_HEAD_INIT(nullptr, 0)};
 PyTypeObject LoopType = {PyVarObject_HEAD_INIT(nullptr, 0)};
 
 Transport* new_transport(Loop* L, int fd) {
-  Transport* t = PyObject_New(Transport, &TransportType);
+  Transport* t = PyObject_GC_New(Transport, &TransportType);
   if (t == nullptr) return nullptr;
   t->w.kind = K_TRANSPORT;
   t->w.fd = fd;
@@ -462,26 +480,47 @@ Transport* new_transport(Loop* L, int fd) {
   t->rt = new Router();
   t->dispatching = 0;
   t->queued = false;
+  PyObject_GC_Track((PyObject*)t);
   return t;
 }
 
+int Transport_traverse(Transport* t, visitproc visit, void* arg) {
+  Py_VISIT(t->protocol);
+  Py_VISIT(t->on_fail);
+  Py_VISIT(t->peer);
+  Py_VISIT(t->cap->done);
+  Py_VISIT(t->ns->watchers);
+  Py_VISIT(t->ns->bulk);
+  Py_VISIT(t->rt->reqs);
+  Py_VISIT(t->rt->xmap);
+  Py_VISIT(t->rt->on_other);
+  Py_VISIT(t->rt->on_note);
+  return 0;
+}
+
+int Transport_clear(Transport* t) {
+  Py_CLEAR(t->protocol);
+  Py_CLEAR(t->on_fail);
+  Py_CLEAR(t->peer);
+  Py_CLEAR(t->cap->done);
+  Py_CLEAR(t->ns->watchers);
+  Py_CLEAR(t->ns->bulk);
+  Py_CLEAR(t->rt->reqs);
+  Py_CLEAR(t->rt->xmap);
+  Py_CLEAR(t->rt->on_other);
+  Py_CLEAR(t->rt->on_note);
+  return 0;
+}
+
 void Transport_dealloc(Transport* t) {
+  PyObject_GC_UnTrack(t);
   if (t->w.fd >= 0) close(t->w.fd);
+  Transport_clear(t);
   delete t->wbuf;
-  Py_XDECREF(t->cap->done);
   delete t->cap;
-  Py_XDECREF(t->ns->watchers);
-  Py_XDECREF(t->ns->bulk);
   delete t->ns;
-  Py_XDECREF(t->rt->reqs);
-  Py_XDECREF(t->rt->xmap);
-  Py_XDECREF(t->rt->on_other);
-  Py_XDECREF(t->rt->on_note);
   delete t->rt;
-  Py_XDECREF(t->protocol);
-  Py_XDECREF(t->on_fail);
-  Py_XDECREF(t->peer);
-  Py_TYPE(t)->tp_free((PyObject*)t);
+  PyObject_GC_Del(t);
 }
 
 uint32_t wanted(Transport* t) {
@@ -1301,10 +1340,21 @@ PyGetSetDef Transport_getset[] = {
 // Server
 // ---------------------------------------------------------------------------
 
+int Server_traverse(Server* s, visitproc visit, void* arg) {
+  Py_VISIT(s->factory);
+  return 0;
+}
+
+int Server_clear(Server* s) {
+  Py_CLEAR(s->factory);
+  return 0;
+}
+
 void Server_dealloc(Server* s) {
+  PyObject_GC_UnTrack(s);
   if (s->w.fd >= 0) close(s->w.fd);
-  Py_XDECREF(s->factory);
-  Py_TYPE(s)->tp_free((PyObject*)s);
+  Server_clear(s);
+  PyObject_GC_Del(s);
 }
 
 PyObject* peer_tuple(const sockaddr_storage& ss) {
@@ -1684,7 +1734,7 @@ PyObject* Loop_listen(Loop* L, PyObject* args) {
   sockaddr_storage bs;
   socklen_t bl = sizeof bs;
   getsockname(fd, (sockaddr*)&bs, &bl);
-  Server* s = PyObject_New(Server, &ServerType);
+  Server* s = PyObject_GC_New(Server, &ServerType);
   if (s == nullptr) { close(fd); return nullptr; }
   s->w.kind = K_SERVER;
   s->w.fd = fd;
@@ -1695,6 +1745,7 @@ PyObject* Loop_listen(Loop* L, PyObject* args) {
   s->factory = factory;
   s->port = bs.ss_family == AF_INET6 ? ntohs(((sockaddr_in6*)&bs)->sin6_port)
                                      : ntohs(((sockaddr_in*)&bs)->sin_port);
+  PyObject_GC_Track((PyObject*)s);
   if (add_watch(L, &s->w, EPOLLIN) != 0) {
     Py_DECREF(s);
     return PyErr_SetFromErrno(PyExc_OSError);
@@ -1733,21 +1784,27 @@ PyModuleDef mod = {PyModuleDef_HEAD_INIT, "_zkloop",
 PyMODINIT_FUNC PyInit__zkloop(void) {
   HandleType.tp_name = "_zkloop.Handle";
   HandleType.tp_basicsize = sizeof(Handle);
-  HandleType.tp_flags = Py_TPFLAGS_DEFAULT;
+  HandleType.tp_flags = Py_TPFLAGS_DEFAULT | Py_TPFLAGS_HAVE_GC;
+  HandleType.tp_traverse = (traverseproc)Handle_traverse;
+  HandleType.tp_clear = (inquiry)Handle_clear;
   HandleType.tp_dealloc = (destructor)Handle_dealloc;
   HandleType.tp_methods = Handle_methods;
   HandleType.tp_getset = Handle_getset;
 
   TransportType.tp_name = "_zkloop.Transport";
   TransportType.tp_basicsize = sizeof(Transport);
-  TransportType.tp_flags = Py_TPFLAGS_DEFAULT;
+  TransportType.tp_flags = Py_TPFLAGS_DEFAULT | Py_TPFLAGS_HAVE_GC;
+  TransportType.tp_traverse = (traverseproc)Transport_traverse;
+  TransportType.tp_clear = (inquiry)Transport_clear;
   TransportType.tp_dealloc = (destructor)Transport_dealloc;
   TransportType.tp_methods = Transport_methods;
   TransportType.tp_getset = Transport_getset;
 
   ServerType.tp_name = "_zkloop.Server";
   ServerType.tp_basicsize = sizeof(Server);
-  ServerType.tp_flags = Py_TPFLAGS_DEFAULT;
+  ServerType.tp_flags = Py_TPFLAGS_DEFAULT | Py_TPFLAGS_HAVE_GC;
+  ServerType.tp_traverse = (traverseproc)Server_traverse;
+  ServerType.tp_clear = (inquiry)Server_clear;
   ServerType.tp_dealloc = (destructor)Server_dealloc;
   ServerType.tp_methods = Server_methods;
   ServerType.tp_getset = Server_getset;

@@ -98,6 +98,7 @@ Entry* find(Table* t, PyObject* path) {
 }
 
 double now_ms(Table* t) {
+  if (t->loop == nullptr) return 0;
   PyObject* r = PyObject_CallMethod(t->loop, "time_ms", nullptr);
   if (r == nullptr) { PyErr_Clear(); return 0; }
   const double v = PyFloat_AsDouble(r);
@@ -124,8 +125,11 @@ bool send(Table* t, Entry* en, int k, bool dc) {
                                 dc ? "EXISTS" : KIND_OP[k], "path", en->path,
                                 "watch", dc ? Py_False : Py_True);
   if (pkt == nullptr) return false;
-  Req* q = PyObject_New(Req, &ReqType);
+  Req* q = PyObject_GC_New(Req, &ReqType);
   if (q == nullptr) { Py_DECREF(pkt); return false; }
+  q->t = nullptr;
+  q->path = nullptr;
+  q->listeners = nullptr;
   Py_INCREF(t);
   q->t = t;
   Py_INCREF(en->path);
@@ -135,6 +139,7 @@ bool send(Table* t, Entry* en, int k, bool dc) {
   q->dc = dc;
   q->listeners = PyDict_New();
   q->t_submit = 0;
+  PyObject_GC_Track((PyObject*)q);
   PyObject* r = q->listeners ? PyObject_CallMethod(t->conn, "request", "OO",
                                                    pkt, (PyObject*)q)
                              : nullptr;
@@ -170,11 +175,26 @@ void to_armed(Table* t, Ev& e) {
 
 // ---- Req ------------------------------------------------------------------
 
+// Req and Table are GC types: a request the connection still holds refers
+// to its table, the table to the connection (and to the session through
+// emit, a bound method), so they form cycles the collector must see.
+int Req_traverse(Req* q, visitproc visit, void* arg) {
+  Py_VISIT((PyObject*)q->t);
+  Py_VISIT(q->listeners);
+  return 0;
+}
+
+int Req_clear(Req* q) {
+  Py_CLEAR(q->t);
+  Py_CLEAR(q->listeners);
+  return 0;
+}
+
 void Req_dealloc(Req* q) {
-  Py_XDECREF(q->t);
-  Py_XDECREF(q->path);
-  Py_XDECREF(q->listeners);
-  PyObject_Free(q);
+  PyObject_GC_UnTrack(q);
+  Req_clear(q);
+  Py_CLEAR(q->path);
+  PyObject_GC_Del(q);
 }
 
 int64_t stat_zxid(PyObject* stat, int k) {
@@ -190,6 +210,7 @@ int64_t stat_zxid(PyObject* stat, int k) {
 PyObject* do_emit(Table* t, PyObject* path, PyObject* args_tail,
                   const char* evt) {
   // emit(path, evt, *args_tail)
+  if (t->emit == nullptr) Py_RETURN_NONE;          // closed
   PyObject* ev = PyUnicode_FromString(evt);
   const Py_ssize_t n = args_tail ? PyTuple_GET_SIZE(args_tail) : 0;
   PyObject* args = PyTuple_New(2 + n);
@@ -257,9 +278,17 @@ PyObject* Req_reply(Req* q, PyObject* pkt) {
   e.has_prev = true;
   PyObject* r = do_emit(t, q->path, tail, evt);
   Py_DECREF(tail);
+  // a listener that raised: its exception is held while the entry's own
+  // transitions (which call into Python) run, then handed on to the
+  // caller (the loop's errors, like the Python FSM path)
+  PyObject *et = nullptr, *ev = nullptr, *tb = nullptr;
+  if (r == nullptr) PyErr_Fetch(&et, &ev, &tb);
   if (e.gen == q->gen) to_armed(t, e);
   if (q->kind == K_CD) wake_wait_node(t, en);
-  if (r == nullptr) return nullptr;
+  if (r == nullptr) {
+    PyErr_Restore(et, ev, tb);
+    return nullptr;
+  }
   Py_DECREF(r);
   Py_RETURN_NONE;
 }
@@ -285,8 +314,13 @@ PyObject* Req_error(Req* q, PyObject* args) {
   if (code == "NO_NODE" && q->kind == K_CD) {
     // existence watches arm on a missing node
     PyObject* r = do_emit(t, q->path, nullptr, "deleted");
+    PyObject *et = nullptr, *ev = nullptr, *tb = nullptr;
+    if (r == nullptr) PyErr_Fetch(&et, &ev, &tb);
     if (e.gen == q->gen) to_armed(t, e);
-    if (r == nullptr) return nullptr;
+    if (r == nullptr) {
+      PyErr_Restore(et, ev, tb);
+      return nullptr;
+    }
     Py_DECREF(r);
     Py_RETURN_NONE;
   }
@@ -360,7 +394,33 @@ int kind_of(PyObject* o) {
   return -1;
 }
 
+int Table_traverse(Table* t, visitproc visit, void* arg) {
+  Py_VISIT(t->emit);
+  Py_VISIT(t->loop);
+  Py_VISIT(t->conn);
+  Py_VISIT(t->timer);
+  return 0;
+}
+
+void cancel_timer(Table* t) {
+  if (t->timer == nullptr) return;
+  PyObject* r = PyObject_CallMethod(t->timer, "cancel", nullptr);
+  if (r == nullptr) PyErr_Clear();
+  Py_XDECREF(r);
+  Py_CLEAR(t->timer);
+  t->timer_due = 0;
+}
+
+int Table_clear(Table* t) {
+  Py_CLEAR(t->emit);
+  Py_CLEAR(t->loop);
+  Py_CLEAR(t->conn);
+  Py_CLEAR(t->timer);
+  return 0;
+}
+
 void Table_dealloc(Table* t) {
+  PyObject_GC_UnTrack(t);
   if (t->map != nullptr)
     for (auto& kv : *t->map) {
       Py_XDECREF(kv.second->path);
@@ -368,10 +428,7 @@ void Table_dealloc(Table* t) {
     }
   delete t->map;
   delete t->rng;
-  Py_XDECREF(t->emit);
-  Py_XDECREF(t->loop);
-  Py_XDECREF(t->conn);
-  Py_XDECREF(t->timer);
+  Table_clear(t);
   Py_TYPE(t)->tp_free((PyObject*)t);
 }
 
@@ -380,18 +437,17 @@ int Table_init(Table* t, PyObject* args, PyObject*) {
   PyObject *emit, *loop;
   double dc, dcr;
   if (!PyArg_ParseTuple(args, "OOdd", &emit, &loop, &dc, &dcr)) return -1;
-  t->map = new std::unordered_map<std::string, Entry*>();
-  t->rng = new std::mt19937_64(std::random_device{}());
+  if (t->map == nullptr) t->map = new std::unordered_map<std::string, Entry*>();
+  if (t->rng == nullptr) t->rng = new std::mt19937_64(std::random_device{}());
   Py_INCREF(emit);
-  t->emit = emit;
+  Py_XSETREF(t->emit, emit);
   Py_INCREF(loop);
-  t->loop = loop;
-  t->conn = nullptr;
+  Py_XSETREF(t->loop, loop);
+  Py_CLEAR(t->conn);
   t->dc_ms = dc;
   t->dc_rand_ms = dcr;
   t->batch = 0;
-  t->timer = nullptr;
-  t->timer_due = 0;
+  cancel_timer(t);
   t->kick_pending = false;
   return 0;
 }
@@ -407,7 +463,7 @@ PyObject* Table_new(PyTypeObject* type, PyObject*, PyObject*) {
 }
 
 void schedule_kick(Table* t) {
-  if (t->kick_pending || t->conn == nullptr) return;
+  if (t->kick_pending || t->conn == nullptr || t->loop == nullptr) return;
   PyObject* cb = PyObject_GetAttrString((PyObject*)t, "_kick");
   if (cb == nullptr) { PyErr_Clear(); return; }
   PyObject* r = PyObject_CallMethod(t->loop, "call_soon", "O", cb);
@@ -431,6 +487,7 @@ PyObject* Table_kick(Table* t, PyObject*) {
 PyObject* Table_dc_tick(Table* t, PyObject*);
 
 void schedule_dc(Table* t, double due) {
+  if (t->loop == nullptr) return;                 // closed
   if (t->timer != nullptr && t->timer_due <= due) return;
   if (t->timer != nullptr) {
     PyObject* r = PyObject_CallMethod(t->timer, "cancel", nullptr);
@@ -623,6 +680,24 @@ PyObject* Table_contains_path(Table* t, PyObject* path) {
   return PyBool_FromLong(en != nullptr);
 }
 
+// close(): the session is closed or expired: no more timers, requests or
+// emits; every entry is dropped (its watchers are dead, README.md:47-51)
+PyObject* Table_close(Table* t, PyObject*) {
+  cancel_timer(t);
+  Py_CLEAR(t->conn);
+  if (t->map != nullptr) {
+    for (auto& kv : *t->map) {
+      Py_XDECREF(kv.second->path);
+      delete kv.second;
+    }
+    t->map->clear();
+  }
+  t->kick_pending = true;                 // nothing more is scheduled
+  Py_CLEAR(t->emit);
+  Py_CLEAR(t->loop);
+  Py_RETURN_NONE;
+}
+
 // counts() -> {state: n}: how many watch events are in each state
 PyObject* Table_counts(Table* t, PyObject*) {
   int64_t c[7] = {0};
@@ -650,6 +725,7 @@ PyMethodDef Table_methods[] = {
     {"history", (PyCFunction)Table_history, METH_VARARGS, ""},
     {"has", (PyCFunction)Table_contains_path, METH_O, "has(path)"},
     {"counts", (PyCFunction)Table_counts, METH_NOARGS, ""},
+    {"close", (PyCFunction)Table_close, METH_NOARGS, "close()"},
     {"_kick", (PyCFunction)Table_kick, METH_NOARGS, ""},
     {"_dc_tick", (PyCFunction)Table_dc_tick, METH_NOARGS, ""},
     {nullptr, nullptr, 0, nullptr}};
@@ -662,13 +738,17 @@ PyModuleDef module = {PyModuleDef_HEAD_INIT, "_zkwatch",
 PyMODINIT_FUNC PyInit__zkwatch() {
   ReqType.tp_name = "zkmi._zkwatch.WatchRequest";
   ReqType.tp_basicsize = sizeof(Req);
-  ReqType.tp_flags = Py_TPFLAGS_DEFAULT;
+  ReqType.tp_flags = Py_TPFLAGS_DEFAULT | Py_TPFLAGS_HAVE_GC;
+  ReqType.tp_traverse = (traverseproc)Req_traverse;
+  ReqType.tp_clear = (inquiry)Req_clear;
   ReqType.tp_dealloc = (destructor)Req_dealloc;
   ReqType.tp_methods = Req_methods;
   ReqType.tp_getset = Req_getset;
   TableType.tp_name = "zkmi._zkwatch.WatchTable";
   TableType.tp_basicsize = sizeof(Table);
-  TableType.tp_flags = Py_TPFLAGS_DEFAULT;
+  TableType.tp_flags = Py_TPFLAGS_DEFAULT | Py_TPFLAGS_HAVE_GC;
+  TableType.tp_traverse = (traverseproc)Table_traverse;
+  TableType.tp_clear = (inquiry)Table_clear;
   TableType.tp_new = Table_new;
   TableType.tp_init = (initproc)Table_init;
   TableType.tp_dealloc = (destructor)Table_dealloc;

@@ -37,17 +37,19 @@
 //            is each tile's entry the exit of the tile before, the first
 //            terminal, the in-block frame counts; a launch of its own until
 //            round 4 — moving it into fs_tile cost the tiles' ends more than
-//            the launch), one grid barrier.  No broken link before the first
-//            terminal (the usual case): block 0 scans the block totals into
-//            row bases, done.  Otherwise the repair: a few broken links are
-//            chased — from each,
-//            forward while the next link stays broken, the exact entry of a
-//            tile looked up among the candidates fs_tile mapped (`cx`), so a
-//            run of tiles costs a few instructions each; many are re-walked
-//            in grid rounds to a fix-point.  Whatever neither settles is
-//            finished serially, tiles covered whole by one frame filled in
-//            one step; then the counts are scanned up to the first terminal:
-//            row bases and result[0..3].
+//            the launch), then a ticket: the LAST block to finish its check
+//            goes on alone, no block waits for another (no grid barrier, so
+//            no co-residency is assumed).  No broken link before the first
+//            terminal (the usual case): it scans the block totals into row
+//            bases, done.  Otherwise the repair: a few broken links are
+//            chased in parallel waves — from each, forward while the next
+//            link stays broken, the exact entry of a tile looked up among
+//            the candidates fs_tile mapped (`cx`), so a run of tiles costs a
+//            few instructions each; many, or what the chases leave, by the
+//            tail: exact chases from the leftmost broken link, tiles whose
+//            entry is no candidate walked, tiles covered whole by one frame
+//            filled in one step; then the counts are scanned up to the first
+//            terminal: row bases and result[0..3].
 //  fs_rows   one wave per tile writes its (body offset, length) rows.
 //
 // The stream length is read ON THE DEVICE (n = min(*n_dev, n_cap), e.g. an
@@ -77,14 +79,12 @@ constexpr int64_t TERM = (int64_t)1 << 62;
 constexpr int64_t TBAD = (int64_t)1 << 60;
 constexpr int64_t FC_MAXP = (int64_t)1 << 24;
 constexpr int FC_WIN = 4096;               // fs_link's staged walk window
-constexpr int FC_TAILWIN = 8192;           // the serial tail's (one wave)
 // fs_link threads (512: 256 VGPRs a lane — with 1024 the chase and the walk
 // inlined together spilled to scratch, 0.64 us a looked-up tile)
 constexpr int FL_T = 512;
 constexpr int FL_U = 8;                    // fs_link loads per batch
-// fs_link's grid repair rounds and its grid words (see fl_sync)
-constexpr int FL_GROUNDS = 6;
-constexpr int FL_NB = 3 + 2 * FL_GROUNDS;     // broken links the check saw
+// fs_link's grid words (see fl_check's caller)
+constexpr int FL_NB = 1;                   // broken links the check saw
 constexpr int FL_GW = FL_NB + 1;
 // Count blocks: frame counts scanned per FK_T tiles (one wave's worth)
 constexpr int FK_T = 64;
@@ -1572,8 +1572,7 @@ ZK_DEV void fc_stage(const uint8_t* __restrict__ buf, int64_t n, int64_t wb,
 }
 
 // fs_tile's join walk from global memory (a repair from the exact entry E),
-// through a WIN-byte LDS window (4 KiB per wave: a tile in one staging;
-// block 0's serial tail: 8 KiB).
+// through a WIN-byte LDS window (4 KiB per wave: a tile in one staging).
 template <int WIN = FC_WIN>
 ZK_DEV FcWalk fc_walk(const uint8_t* __restrict__ buf, int64_t n,
                       int64_t maxp, int64_t ts, int64_t E, const uint16_t* L,
@@ -1620,177 +1619,25 @@ ZK_DEV FcWalk fc_walk(const uint8_t* __restrict__ buf, int64_t n,
   return r;
 }
 
-// fs_link's grid: FL_B workgroups.  The usual scan (no broken link before
-// the first terminal) is block 0 alone: the others return at once.  A
-// repair runs in rounds over the whole grid (a fix-point): each round lists
-// the broken links before the current first terminal and re-walks every
-// one of them in parallel, one wave per link, from the exit of the tile
-// before as it stands.  A link holds once its entry equals the exit before
-// it; a tile whose speculated entry was missing or wrong but whose survivor
-// is the true chain (the usual repair: a frontier wait that timed out, a
-// garbage candidate that survived its tile) re-walks to the same exit, so
-// one round settles any number of such tiles at once — where the serial
-// repair paid one tile after the other (the round-2 storm stream: 50 ms).
-// What a round cannot settle is a chain of exits that each depend on the
-// previous repair (frames longer than the window crossing tile after tile):
-// after FL_GROUNDS rounds block 0 finishes those serially, skipping the
-// tiles a long frame covers in one step.
-constexpr uint64_t FL_BAR_TICKS = 50000000;   // 0.5 s: barrier abandoned
-// grid words (LW_GRID, uint64): [0] barrier arrivals, [1] barrier
-// generation, [2] abort, then per round r [4 + 2r] broken links listed (the
-// chase repair, which runs no rounds, uses [3] settled and [5] / [6] its
-// grid check's first broken link / terminal); [FL_NB] the check's count
+// fs_link's grid: fl_blocks() workgroups check the links (fl_check), then
+// each takes a ticket; the LAST block to arrive reads the check's minima
+// and does the rest alone.  No block ever waits for another, so nothing
+// depends on the grid being co-resident: a spin barrier here (rounds 2-4)
+// waited for room beside the other connection's kernels (34 us in the
+// overlapped GET step against 12 us alone, one 175 ms step on the watch
+// stream).  The usual scan — no broken link before the first terminal —
+// is the bases scan.  A repair: a handful of broken links are chased in
+// parallel waves (fl_chase); more (every tile without a speculated entry,
+// a run of garbage entries) go to the tail, which chases from the leftmost
+// broken link with the exact entry — one wave looks a run of tiles up in
+// fs_tile's candidate exits 64 at a time, walking only the tiles whose
+// exact entry is not a candidate — until every live link holds.
+// Grid words (LW_GRID, uint64): [0] the ticket, [FL_NB] the check's count
+// of broken links (fs_rows clears it for the next scan).
 // At most this many broken links: chased from the check's list (fl_chase; a
-// reply stream usually has a handful of broken links or none); more (every
-// tile without a speculated entry) go to the grid rounds.
+// reply stream usually has a handful of broken links or none); more go to
+// the tail's exact chases.
 constexpr unsigned long long FL_SMALL = 1024;
-
-// Grid barrier over fs_link's FL_B workgroups (they are co-resident: 64
-// blocks on a 256-CU part, and nothing they wait for needs a CU they hold).
-// Every wait is bounded: past FL_BAR_TICKS the grid is told to abort and
-// block 0 falls back to the serial repair.  Returns false on abort.
-ZK_DEV bool fl_sync(unsigned long long* g) {
-  __shared__ int s_ok;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int ok = 1;
-    __threadfence();
-    const unsigned long long gen =
-        __hip_atomic_load(&g[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned long long a =
-        __hip_atomic_fetch_add(&g[0], 1ull, __ATOMIC_ACQ_REL,
-                               __HIP_MEMORY_SCOPE_AGENT) + 1;
-    if (a == gridDim.x) {
-      __hip_atomic_store(&g[0], 0ull, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_fetch_add(&g[1], 1ull, __ATOMIC_RELEASE,
-                             __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      const uint64_t t0 = wall_clock64();
-      while (__hip_atomic_load(&g[1], __ATOMIC_ACQUIRE,
-                               __HIP_MEMORY_SCOPE_AGENT) == gen) {
-        if (__hip_atomic_load(&g[2], __ATOMIC_RELAXED,
-                              __HIP_MEMORY_SCOPE_AGENT)) {
-          ok = 0;
-          break;
-        }
-        if (wall_clock64() - t0 > FL_BAR_TICKS) {
-          __hip_atomic_store(&g[2], 1ull, __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-          ok = 0;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(8);
-      }
-    }
-    __threadfence();
-    if (__hip_atomic_load(&g[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-      ok = 0;
-    s_ok = ok;
-  }
-  __syncthreads();
-  return s_ok != 0;
-}
-
-// Is a repair walk of tile k (new exit x) written?  Always when the link
-// before k holds (its entry E is then exact, or at least as good as the
-// records get).  When that link is itself broken, E is suspect: a garbage
-// exit of tile k-1 (say a frame-length read from an xid, megabytes ahead)
-// walked on would break the link after k where it holds, that link's walk
-// would break the next, and a wave of garbage would cross the stream one
-// tile per round, with the true repair one round behind it (the first storm
-// reply stream: 1413 tiles re-walked over 71 rounds).  So a suspect walk
-// that changes the exit is not written while link k+1 holds; link k stays
-// broken and is walked again once the tile before has settled.  The
-// leftmost broken link always has an exact entry, so every round settles
-// at least it.  A walk from an E that tile k-1 has since replaced is stale
-// and not written either.  (A refused walk has overwritten the tile's
-// recorded frame starts all the same: its caller clears the entry.)
-ZK_DEV bool fl_accept(const int64_t* rec_entry, const int64_t* rec_exit,
-                      int64_t ntiles, int64_t k, int64_t E, int64_t x) {
-  if (ld_agent(&rec_exit[k - 1]) != E) return false;
-  if (k < 2) return true;
-  const bool suspect = ld_agent(&rec_entry[k - 1]) != ld_agent(&rec_exit[k - 2]);
-  if (!suspect) return true;
-  const int64_t ox = ld_agent(&rec_exit[k]);
-  if (x == ox || k + 1 >= ntiles) return true;
-  return ld_agent(&rec_entry[k + 1]) != ox;
-}
-
-// One grid repair round (every thread of every block calls it).  Returns
-// false when no link was broken (the fix-point is reached) or on abort.
-ZK_DEV bool fl_round(const uint8_t* __restrict__ buf, int64_t n,
-                     int64_t ntiles, int64_t maxp,
-                     const int64_t* __restrict__ sx,
-                     const uint16_t* __restrict__ list,
-                     const int32_t* __restrict__ rcount, uint16_t* pre,
-                     int64_t* rec_entry, int64_t* rec_exit, int64_t* rec_meta,
-                     int32_t* blist, unsigned long long* g, int r,
-                     int64_t* red, uint8_t* win, uint64_t* stats) {
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int64_t INF = INT64_MAX;
-  const int64_t nblk = gridDim.x;
-  const int64_t bid = blockIdx.x;
-  const int64_t nth = nblk * FL_T;
-  const int64_t gt = bid * FL_T + tid;
-  // B. list the broken links (after a tile that is not a terminal).  Every
-  // one, not only those before the first terminal: a terminal may be a
-  // speculation's (a garbage entry that died) that this very round fixes,
-  // and stopping the list there made a stream with many such tiles take a
-  // round per terminal (26 ms a 0-1024 B reply stream at a 1 KiB window).
-  // Past a real bad frame the walks are wasted, and the serial tail's
-  // first terminal bounds what counts.
-  int64_t nb = 0;
-  const int64_t per = (ntiles - 1 + nth - 1) / nth;
-  const int64_t k0 = 1 + gt * per, k1 = min(k0 + per, ntiles);
-  auto broken = [&](int64_t k) {
-    return ld_agent(&rec_entry[k]) != ld_agent(&rec_exit[k - 1]) &&
-           !m_term(ld_agent(&rec_meta[k - 1]));
-  };
-  for (int64_t k = k0; k < k1; ++k) nb += broken(k);
-  int64_t tot;
-  const int64_t o = block_excl_scan(nb, red, &tot);
-  __shared__ unsigned long long s_base;
-  if (tid == 0)
-    s_base = tot ? atomicAdd(&g[4 + 2 * r], (unsigned long long)tot) : 0;
-  __syncthreads();
-  int64_t w = (int64_t)s_base + o;
-  for (int64_t k = k0; k < k1; ++k)
-    if (broken(k)) blist[w++] = (int32_t)k;
-  if (!fl_sync(g)) return false;
-  const int64_t nbr = (int64_t)__hip_atomic_load(
-      &g[4 + 2 * r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (nbr == 0) return false;
-  // C. every listed link re-walked by one wave, from the exit before it
-  uint8_t* mywin = win + (size_t)wv * (FC_WIN + 16);
-  const int64_t nwv = nblk * (FL_T / 64);
-  uint32_t walked = 0;
-  for (int64_t j = bid * (FL_T / 64) + wv; j < nbr; j += nwv) {
-    const int64_t k = blist[j];
-    const int64_t E = ld_agent(&rec_exit[k - 1]);
-    if (E < k * FT_S) continue;               // no exact entry yet
-    const int32_t m0 = __builtin_amdgcn_readfirstlane(rcount[k]);
-    const FcWalk fw = fc_walk(buf, n, maxp, k * FT_S, E, list + k * FT_LMAX,
-                              m0, sx[k], mywin, pre + k * FT_LMAX, lane);
-    ++walked;
-    if (lane == 0) {
-      if (fl_accept(rec_entry, rec_exit, ntiles, k, E, fw.exit)) {
-        st_agent(&rec_entry[k], E);
-        st_agent(&rec_exit[k], fw.exit);
-        st_agent(&rec_meta[k], fc_meta(fw));
-      } else {
-        // the walk overwrote the tile's frame starts (pre) while its
-        // record keeps the old entry: no entry, so the link stays broken
-        // and the tile is walked again (its exit, which the refusal
-        // protects, is kept)
-        st_agent(&rec_entry[k], -1);
-      }
-    }
-  }
-  if (lane == 0 && walked) fc_stat(stats, 2, walked);
-  if (bid == 0 && tid == 0) fc_stat(stats, 3, 1);
-  return fl_sync(g);
-}
 
 // The full check (fs_link, when fs_tile counted a bad link): every link and
 // terminal, one wave per count block of FK_T tiles over the grid, and the
@@ -1863,7 +1710,7 @@ ZK_DEV void fl_check(int64_t ntiles, const int64_t* __restrict__ rec_entry,
 // Row bases once every link up to the first terminal ft (INF: none) holds:
 // bsum[b] (block b's count total, the check's or re-counted) becomes block
 // b's exclusive offset; base[k] stays the in-block one; result[0..3] and
-// the last tile.  Block 0 alone.
+// the last tile.  fs_link's last block alone.
 ZK_DEV void fl_bases(int64_t n, int64_t ntiles, int64_t ft,
                      const int64_t* rec_exit, const int64_t* rec_meta,
                      const int64_t* base, int64_t* bsum, int64_t cap,
@@ -1922,10 +1769,11 @@ ZK_DEV void fl_bases(int64_t n, int64_t ntiles, int64_t ft,
 // run may have moved an exit), the broken ones (deduplicated in an LDS
 // hash set) chased next round.  Only the count blocks holding a re-written
 // tile are re-counted.  When the lists outgrow LDS or the rounds run out,
-// block 0's serial tail finishes from the records as they stand.
+// fs_link's tail (exact chases from the leftmost broken link) finishes from
+// the records as they stand.
 constexpr int FL_WL = 1024;                // chases per round
 constexpr int FL_HS = 2048;                // their dedup hash set
-constexpr int FL_WR = 48;                  // rounds before the serial tail
+constexpr int FL_WR = 48;                  // rounds before the tail
 constexpr int FL_DB = 8192;                // count blocks tracked (2M tiles)
 static_assert(FL_SMALL <= FL_WL, "the check's list fits the first round");
 
@@ -1938,7 +1786,8 @@ struct FlChase {
 
 ZK_DEV void fl_dirty(FlChase& ch, int64_t t) {
   const int64_t b = t / FK_T;
-  atomicOr(&ch.dirty[b >> 5], 1u << (b & 31));
+  // (past FL_DB count blocks only the tail chases, which re-counts all)
+  if (b < FL_DB) atomicOr(&ch.dirty[b >> 5], 1u << (b & 31));
 }
 
 ZK_DEV int live_count(const int64_t* c5) {
@@ -1971,9 +1820,10 @@ ZK_DEV uint64_t readlane64(uint64_t v, int l) {
 // chain) can hold links that are consistent and wrong, and only a chase
 // from an exact entry can tell — it goes through the whole run.
 // Otherwise (another broken link of the round, entry not known exact) the
-// chase writes nothing that would break a link that holds (fl_accept's
-// rule: a phantom's exit must not run over a true segment); it stops there
-// and the link waits for a later round.
+// chase writes nothing that would break a link that holds (a phantom's
+// exit must not run over a true segment: a garbage exit walked on would
+// break the link after it, and a wave of garbage would cross the stream one
+// tile per round); it stops there and the link waits for a later round.
 ZK_DEV int64_t fl_chase_run(const uint8_t* __restrict__ buf, int64_t n,
                             int64_t ntiles, int64_t maxp,
                             const int64_t* __restrict__ sx,
@@ -2177,8 +2027,9 @@ ZK_DEV int64_t fl_chase_run(const uint8_t* __restrict__ buf, int64_t n,
                                 sx[t], mywin, pre + t * FT_LMAX, lane);
       ++walked;
       if (!exact && rfl64(fw.exit) != oldx && nh) {
-        // refused, but the walk overwrote the tile's frame starts: no
-        // entry, so its link stays broken (see fl_round)
+        // refused, but the walk overwrote the tile's frame starts (pre)
+        // while its record keeps the old entry: no entry, so its link stays
+        // broken and the tile is walked again
         if (lane == 0) st_agent(&rec_entry[t], -1);
         return t - 1;
       }
@@ -2199,8 +2050,8 @@ ZK_DEV int64_t fl_chase_run(const uint8_t* __restrict__ buf, int64_t n,
   }
 }
 
-// Block 0: chase rounds to a fix-point of the links.  Returns false when it
-// gave up (the serial tail takes over).
+// fs_link's last block: chase rounds to a fix-point of the links.  Returns false when it
+// gave up (the tail takes over).
 ZK_DEV bool fl_chase(const uint8_t* __restrict__ buf, int64_t n,
                      int64_t ntiles, int64_t maxp,
                      const int64_t* __restrict__ sx,
@@ -2290,7 +2141,7 @@ ZK_DEV bool fl_chase(const uint8_t* __restrict__ buf, int64_t n,
   return ncur == 0 && !*ch.overflow;
 }
 
-// After the chases and the grid's check of every link (block 0): re-count
+// After the chases and the check of every link (the last block): re-count
 // the count blocks holding a re-written tile, one wave per block, a tile per
 // lane.
 ZK_DEV void fl_chase_recount(int64_t ntiles, const int64_t* rec_meta,
@@ -2313,6 +2164,55 @@ ZK_DEV void fl_chase_recount(int64_t ntiles, const int64_t* rec_meta,
   __syncthreads();
 }
 
+// The leftmost terminal, and the leftmost broken link at or after `from`
+// (INF: none), over the whole block.  Loads in batches of FL_U tiles a
+// thread, all issued before any is used (one round trip a batch).
+ZK_DEV void fl_links(int64_t from, int64_t ntiles,
+                     const int64_t* rec_entry, const int64_t* rec_exit,
+                     const int64_t* rec_meta, int64_t* red, int64_t& fb_out,
+                     int64_t& ft_out) {
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int64_t INF = INT64_MAX;
+  int64_t fb = INF, fterm = INF;
+  for (int64_t k0 = max(from - 1, (int64_t)0) + tid; k0 < ntiles;
+       k0 += FL_U * FL_T) {
+    int64_t mk[FL_U], e[FL_U], x[FL_U];
+#pragma unroll
+    for (int u = 0; u < FL_U; ++u) {
+      const int64_t k = k0 + (int64_t)u * FL_T;
+      const bool in = k < ntiles, nx = k + 1 < ntiles;
+      mk[u] = in ? ld_agent(&rec_meta[k]) : 0;
+      e[u] = nx ? ld_agent(&rec_entry[k + 1]) : 0;
+      x[u] = in ? ld_agent(&rec_exit[k]) : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < FL_U; ++u) {
+      const int64_t k = k0 + (int64_t)u * FL_T;
+      if (k >= ntiles) break;
+      if (m_term(mk[u])) {
+        fterm = min(fterm, k);
+      } else if (k + 1 < ntiles && k + 1 >= from) {
+        if (e[u] < 0 || e[u] != x[u]) fb = min(fb, k + 1);
+      }
+    }
+  }
+  for (int d = 32; d >= 1; d >>= 1) {
+    fb = min(fb, (int64_t)__shfl_xor(fb, d, 64));
+    fterm = min(fterm, (int64_t)__shfl_xor(fterm, d, 64));
+  }
+  if (lane == 0) { red[wv] = fb; red[FL_T / 64 + wv] = fterm; }
+  __syncthreads();
+  fb = INF;
+  fterm = INF;
+  for (int j = 0; j < FL_T / 64; ++j) {
+    fb = min(fb, red[j]);
+    fterm = min(fterm, red[FL_T / 64 + j]);
+  }
+  __syncthreads();
+  fb_out = fb;
+  ft_out = fterm;
+}
+
 __global__ __launch_bounds__(FL_T) void fs_link(
     const uint8_t* __restrict__ buf, const int64_t* __restrict__ n_dev,
     int64_t n_cap, int64_t maxp, const int64_t* __restrict__ sx,
@@ -2326,8 +2226,6 @@ __global__ __launch_bounds__(FL_T) void fs_link(
     int64_t* __restrict__ ldbg) {
   __shared__ __attribute__((aligned(16)))
       uint8_t win[(FL_T / 64) * (FC_WIN + 16)];      // one per wave
-  static_assert(FC_TAILWIN <= (FL_T / 64) * (FC_WIN + 16),
-                "the serial tail's window is the waves' windows together");
   __shared__ int64_t red[2 * (FL_T / 64) + 2];
   __shared__ int64_t s_next;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -2342,206 +2240,104 @@ __global__ __launch_bounds__(FL_T) void fs_link(
   }
   const int64_t INF = INT64_MAX;
   // the check over the grid (links, terminals, in-block counts; a launch of
-  // its own until round 4); then the minima and the broken-link count, read
-  // by every block (fs_rows clears them for the next scan of this
-  // workspace, once every block of this launch is done with them)
+  // its own until round 4), then a ticket: the last block to take one sees
+  // every block's check (each releases it before its ticket) and goes on
+  // alone; the others are done
   fl_check(ntiles, rec_entry, rec_exit, rec_meta, base, bsum, mins, &g[FL_NB],
            blist);
-  bool grid_ok = fl_sync(g);
+  __shared__ int s_last;
+  __syncthreads();
+  if (tid == 0) {
+    __threadfence();
+    const unsigned long long a = __hip_atomic_fetch_add(
+        &g[0], 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = a + 1 == gridDim.x;
+    // the ticket back to zero for the next scan of this workspace
+    if (last)
+      __hip_atomic_store(&g[0], 0ull, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    __threadfence();
+    s_last = last;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  // the minima and the broken-link count (fs_rows clears them for the next
+  // scan of this workspace)
   const uint64_t mb0 = ld_agent((const int64_t*)&mins[0]);
   const uint64_t mt0 = ld_agent((const int64_t*)&mins[1]);
   const unsigned long long nb0 = __hip_atomic_load(
       &g[FL_NB], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int64_t fb0 = mb0 ? ntiles - (int64_t)mb0 : INF;
   const int64_t ft0 = mt0 ? ntiles - (int64_t)mt0 : INF;
-  const bool fast = grid_ok && (fb0 == INF || fb0 > ft0);
-  // a small repair (a handful of broken links, the usual kind) is chased
-  // (fl_chase), a large one repaired in grid rounds; the whole grid takes
-  // part in either (every block decides alike)
-  const bool small = grid_ok && !fast && nb0 <= FL_SMALL &&
-                     (ntiles + FK_T - 1) / FK_T <= FL_DB;
-  if (fast && blockIdx.x != 0) return;
-  if (fast) {
+  if (fb0 == INF || fb0 > ft0) {
     // no broken link before the first terminal: the row bases are bsum's
     // block offsets + the check's in-block bases
     fl_bases(n, ntiles, ft0, rec_exit, rec_meta, base, bsum, cap, result,
              lastk, red);
     return;
   }
-  if (small) {
-    // ---- chases: block 0; then every link checked over the grid ---------
-    __shared__ uint32_t dirty[FL_DB / 32];
-    __shared__ int s_ovf;
-    FlChase ch{dirty, &s_ovf, stats, ldbg};
-    unsigned long long* cw = &g[3];       // 1: the chases settled
-    const bool clk = ldbg != nullptr && blockIdx.x == 0 && tid == 0;
+  __shared__ uint32_t dirty[FL_DB / 32];
+  __shared__ int s_ovf;
+  FlChase ch{dirty, &s_ovf, stats, ldbg};
+  for (int i = tid; i < FL_DB / 32; i += FL_T) dirty[i] = 0;
+  if (tid == 0) s_ovf = 0;
+  __syncthreads();
+  const bool clk = ldbg != nullptr && tid == 0;
+  if (nb0 <= FL_SMALL && (ntiles + FK_T - 1) / FK_T <= FL_DB) {
+    // ---- a handful of broken links: chases, then every link checked -----
     if (clk) ldbg[0] = wall_clock64();
-    if (blockIdx.x == 0) {
-      for (int i = tid; i < FL_DB / 32; i += FL_T) dirty[i] = 0;
-      if (tid == 0) s_ovf = 0;
-      __syncthreads();
-      const bool ok = fl_chase(buf, n, ntiles, maxp, sx, list, rcount, pre,
-                               rec_entry, rec_exit, rec_meta, lbw, cx, blist,
-                               (int)nb0, win, stats, ch);
-      if (tid == 0)
-        __hip_atomic_store(cw, ok ? 1ull : 0ull, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-      if (clk) ldbg[1] = wall_clock64();
-    }
-    bool synced = fl_sync(g);
-    if (clk) ldbg[2] = wall_clock64();
-    const bool settled =
-        __hip_atomic_load(cw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
-    // every link and the first terminal, checked over the grid (a chase
-    // only vouches for the links it saw): [5] / [6] = ntiles - the first
-    // broken link / terminal, maxima
-    if (synced) {
-      const int64_t nth = (int64_t)gridDim.x * FL_T;
-      int64_t fb = INF, fterm = INF;
-      for (int64_t k = (int64_t)blockIdx.x * FL_T + tid; k < ntiles;
-           k += nth) {
-        const int64_t mk = ld_agent(&rec_meta[k]);
-        if (m_term(mk)) {
-          fterm = min(fterm, k);
-        } else if (k + 1 < ntiles &&
-                   ld_agent(&rec_entry[k + 1]) != ld_agent(&rec_exit[k])) {
-          fb = min(fb, k + 1);
-        }
-      }
-      for (int d = 32; d >= 1; d >>= 1) {
-        fb = min(fb, (int64_t)__shfl_xor(fb, d, 64));
-        fterm = min(fterm, (int64_t)__shfl_xor(fterm, d, 64));
-      }
-      if (lane == 0 && fb != INF)
-        atomicMax(&g[5], (unsigned long long)(ntiles - fb));
-      if (lane == 0 && fterm != INF)
-        atomicMax(&g[6], (unsigned long long)(ntiles - fterm));
-    }
-    synced = synced && fl_sync(g);
+    const bool settled = fl_chase(buf, n, ntiles, maxp, sx, list, rcount, pre,
+                                  rec_entry, rec_exit, rec_meta, lbw, cx, blist,
+                                  (int)nb0, win, stats, ch);
+    if (clk) ldbg[1] = ldbg[2] = wall_clock64();
+    // a chase only vouches for the links it saw
+    int64_t fbv, ftv;
+    fl_links(1, ntiles, rec_entry, rec_exit, rec_meta, red, fbv, ftv);
     if (clk) ldbg[3] = wall_clock64();
-    if (blockIdx.x != 0) return;
-    const unsigned long long gb = __hip_atomic_load(
-        &g[5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned long long gt = __hip_atomic_load(
-        &g[6], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int64_t fbv = gb ? ntiles - (int64_t)gb : INF;
-    const int64_t ftv = gt ? ntiles - (int64_t)gt : INF;
-    __syncthreads();
-    if (tid == 0) {
-      g[2] = 0;
-      g[3] = 0;
-      g[5] = 0;
-      g[6] = 0;
-    }
-    if (settled && synced && (fbv == INF || fbv > ftv)) {
+    if (settled && (fbv == INF || fbv > ftv)) {
       fl_chase_recount(ntiles, rec_meta, base, bsum, ch);
       fl_bases(n, ntiles, ftv, rec_exit, rec_meta, base, bsum, cap, result,
                lastk, red);
       if (clk) ldbg[4] = wall_clock64();
       return;
     }
-    grid_ok = false;          // not settled: block 0's serial tail finishes
   }
-  for (int r = 0; r < FL_GROUNDS && grid_ok; ++r)
-    grid_ok = fl_round(buf, n, ntiles, maxp, sx, list, rcount, pre,
-                       rec_entry, rec_exit, rec_meta, blist, g, r, red, win,
-                       stats);
-  if (blockIdx.x != 0) return;
-  // ---- block 0: whatever is left, serially; then the count scan -----------
+  // ---- the tail: exact chases from the leftmost broken link, until every
+  // live link holds; then the count scan ------------------------------------
   int64_t from = 1, ft = INF;
   for (;;) {
-    // leftmost terminal, and leftmost broken link at or after `from`.
-    // Loads in batches of FL_U tiles per thread (all issued before any is
-    // used: one round trip per batch, not two per tile)
-    int64_t fb = INF, fterm = INF;
-    for (int64_t k0 = max(from - 1, (int64_t)0) + tid; k0 < ntiles;
-         k0 += FL_U * FL_T) {
-      int64_t mk[FL_U], e[FL_U], x[FL_U];
-#pragma unroll
-      for (int u = 0; u < FL_U; ++u) {
-        const int64_t k = k0 + (int64_t)u * FL_T;
-        const bool in = k < ntiles, nx = k + 1 < ntiles;
-        mk[u] = in ? ld_agent(&rec_meta[k]) : 0;
-        e[u] = nx ? ld_agent(&rec_entry[k + 1]) : 0;
-        x[u] = in ? ld_agent(&rec_exit[k]) : 0;
-      }
-#pragma unroll
-      for (int u = 0; u < FL_U; ++u) {
-        const int64_t k = k0 + (int64_t)u * FL_T;
-        if (k >= ntiles) break;
-        if (m_term(mk[u])) {
-          fterm = min(fterm, k);
-        } else if (k + 1 < ntiles && k + 1 >= from) {
-          if (e[u] < 0 || e[u] != x[u]) fb = min(fb, k + 1);
-        }
-      }
-    }
-    for (int d = 32; d >= 1; d >>= 1) {
-      fb = min(fb, (int64_t)__shfl_xor(fb, d, 64));
-      fterm = min(fterm, (int64_t)__shfl_xor(fterm, d, 64));
-    }
-    if (lane == 0) { red[wv] = fb; red[FL_T / 64 + wv] = fterm; }
-    __syncthreads();
-    fb = INF;
-    fterm = INF;
-    for (int j = 0; j < FL_T / 64; ++j) {
-      fb = min(fb, red[j]);
-      fterm = min(fterm, red[FL_T / 64 + j]);
-    }
-    __syncthreads();
+    int64_t fb, fterm;
+    fl_links(from, ntiles, rec_entry, rec_exit, rec_meta, red, fb, fterm);
     // terminals before from - 1 were found in an earlier pass of this loop
     // (links before `from` hold)
     if (fb == INF || fb > fterm) {          // every live link holds
       ft = fterm;
       break;
     }
-    // repair: re-walk tiles from fb while their links stay broken; the
-    // tiles a frame covers whole (its exit lies past them) hold no frame
-    // start: they are filled in one step, not walked
     if (wv == 0) {
-      int64_t k = fb;
+      // the leftmost broken link has the exact entry (the exit before it):
+      // the chase settles tile fb at least (looked up or walked)
+      bool term = false;
       uint32_t walked = 0;
-      for (;;) {
-        const int64_t E = ld_agent(&rec_exit[k - 1]);
-        const int64_t kx = E / FT_S;          // the tile the entry lies in
-        if (kx > k) {
-          const int64_t kend = min(kx, ntiles);
-          const FcWalk cov{E, 0, 0, -1, false, false};
-          for (int64_t c = k + lane; c < kend; c += 64) {
-            st_agent(&rec_entry[c], E);
-            st_agent(&rec_exit[c], E);
-            st_agent(&rec_meta[c], fc_meta(cov));
-          }
-          k = kend;
-          if (k >= ntiles) break;
-          if (ld_agent(&rec_entry[k]) == E) break;     // link k holds
-          continue;
-        }
-        const int32_t m0 = __builtin_amdgcn_readfirstlane(rcount[k]);
-        const FcWalk w = fc_walk<FC_TAILWIN>(buf, n, maxp, k * FT_S, E,
-                                             list + k * FT_LMAX, m0, sx[k],
-                                             win, pre + k * FT_LMAX, lane);
-        ++walked;
-        if (lane == 0) {
-          st_agent(&rec_entry[k], E);
-          st_agent(&rec_exit[k], w.exit);
-          st_agent(&rec_meta[k], fc_meta(w));
-        }
-        ++k;
-        if (w.term || k >= ntiles) break;
-        if (ld_agent(&rec_entry[k]) == w.exit) break;   // link k holds
-      }
+      const int64_t kend = fl_chase_run(buf, n, ntiles, maxp, sx, list, rcount,
+                                        pre, rec_entry, rec_exit, rec_meta, lbw,
+                                        cx, win, ch, fb, true, term, walked);
       if (lane == 0) {
-        s_next = k;
-        fc_stat(stats, 2, walked);
+        // (kend < fb: nothing written, which the records before fb rule out;
+        // the scan then stops before tile fb rather than loop)
+        s_next = kend < fb ? -fb : kend + 1;
+        if (walked) fc_stat(stats, 2, walked);
         fc_stat(stats, 3, 1);
       }
     }
     __syncthreads();
     from = s_next;
+    __syncthreads();
+    if (from < 0) {
+      ft = -from - 1;
+      break;
+    }
   }
-  // the grid words back to zero for the next scan of this workspace
-  if (tid < FL_GW && tid != 1) g[tid] = 0;
   // exclusive scan of the counts of tiles 0..ft; tiles after ft are dead
   const int64_t last = ft == INF ? ntiles - 1 : ft;
   const int64_t per = (last + 1 + FL_T - 1) / FL_T;
@@ -2579,9 +2375,13 @@ __global__ __launch_bounds__(FL_T) void fs_link(
     if (ft == INF) {
       result[1] = n;
       result[2] = 0;
-    } else {
+    } else if (m_term(ld_agent(&rec_meta[ft]))) {
       result[1] = ld_agent(&rec_exit[ft]);
       result[2] = m_bad(ld_agent(&rec_meta[ft])) ? 1 : 0;
+    } else {
+      // (the unreachable stop above: the carry starts at tile ft's exit)
+      result[1] = ld_agent(&rec_exit[ft]);
+      result[2] = 0;
     }
   }
 }
@@ -2707,9 +2507,7 @@ static FsPlan fs_plan(int64_t n) {
   return p;
 }
 
-// fs_link's grid: every block must find a CU slot before the launch ends,
-// also on the usual path where block 0 alone works, so a small grid waits
-// less behind another stream's kernel.
+// fs_link's grid: the check's workgroups (the last to finish goes on).
 static unsigned fl_blocks() { return 16; }
 
 // The smallest plausible frame body of the tile map's nodes (the smallest

@@ -74,7 +74,7 @@ __global__ __launch_bounds__(SS_T) void session_connect_k(
       const int64_t own = (int64_t)atomicAdd((unsigned long long*)tab.next,
                                              1ull);
       const int64_t idx = tab.span ? (server_id - 1) * tab.span + own : own;
-      if (own < (tab.span ? tab.span : tab.cap) && idx < tab.cap) {
+      if (own < (tab.span ? tab.span : tab.cap) && idx >= 0 && idx < tab.cap) {
         sid = (server_id << 56) | (own + 1);
         to = min(max(want, min_to), max_to);
         pw0 = mix64((uint64_t)sid ^ secret);

@@ -852,6 +852,10 @@ void session_connect(const Tensor& buf, const Tensor& foff,
                      const Tensor& resp_sid, const Tensor& outcome,
                      int64_t span) {
   ZkSessionTable s = session_table(tab, span);
+  // a member's slots are [(server_id - 1) * span, server_id * span)
+  TORCH_CHECK(server_id >= 1 && server_id < 128 &&
+                  (span == 0 || server_id * span <= s.cap),
+              "zkmi: session_connect server_id out of range for the span");
   const Tensor* r = &buf;
   hip_ok(zk_session_connect(
              P<uint8_t>(buf, U8, 1, "buf"),

@@ -142,7 +142,8 @@ def _replayed_catch_up(wl, gpu):
     """One watched path written once, then its catch-up notification
     forwarded twice (what a second SET_WATCHES at the same relZxid brings
     when the session moves again before the first one is answered): the
-    owner forwards the change once and drops the repeat."""
+    owner forwards the change once and drops the repeat — also when both
+    copies arrive in one re-arm batch."""
     from zkmi.parallel.fanout import notification_frames
     p = wl.mine[0]
     wl.client.call_sync('set', p, b'changed', -1)
@@ -161,6 +162,13 @@ def _replayed_catch_up(wl, gpu):
     wl.client.call_sync('set', p, b'changed2', -1)
     _, nf3 = wl._rearm(notes, 1)
     assert nf3 == 2 and fwd() == 2
+    # the replay in the same tick as the original: one batch holds the
+    # path twice; only the first copy is forwarded
+    wl.client.call_sync('set', p, b'changed3', -1)
+    both = notification_frames([p, p], evtype=3)
+    _, nf4 = wl._rearm(both, 2)
+    assert nf4 == 2 and fwd() == 3
+    assert wl.redelivered == 2
 
 
 def test_ensemble_owner_drops_replayed_catch_up():

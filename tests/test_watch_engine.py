@@ -127,3 +127,77 @@ def test_engine_thousands_of_watchers():
         w.close_sync(10)
     finally:
         srv.shutdown()
+
+
+def _raising_created(native):
+    """A data watch on a missing node waits for it (wait_node) behind the
+    implicit existence watch; a user 'created' listener that raises must
+    not leave the data watch stuck, and its exception reaches the loop's
+    errors (the Python FSMs pass it on the same way)."""
+    zk = FakeZKServer(tick_ms=250)
+    got = []
+    try:
+        c = client(zk.servers(), config=fast_config(native_watch=native))
+        w = client(zk.servers())
+        c.wait_connected(10)
+        w.wait_connected(10)
+        errs0 = len(c.loop.errors)
+
+        def boom(stat):
+            got.append('created')
+            raise RuntimeError('listener failed')
+        c.watcher('/n').on('dataChanged', lambda d, s: got.append(d))
+        c.watcher('/n').on('created', boom)
+        assert wait_for(lambda: c.loop.run(
+            lambda: c.getSession().wt.state('/n', 'dataChanged')
+            if native else 'wait_node') == 'wait_node', 5)
+        w.call_sync('create', '/n', b'x', {})
+        assert wait_for(lambda: b'x' in got, 5), got
+        errs = c.loop.run(lambda: c.loop.errors[errs0:])
+        c.loop.run(lambda: c.loop.errors.__delitem__(
+            slice(errs0, len(c.loop.errors))))
+        c.close_sync(10)
+        w.close_sync(10)
+        return got, [type(e).__name__ for e in errs]
+    finally:
+        zk.shutdown()
+
+
+def test_raising_listener_does_not_strand_wait_node():
+    """(The reference's EventEmitter would crash the process on the throw;
+    the Python FSMs leave the data watch in wait_node.  The engine keeps
+    going and hands the error to the loop.)"""
+    got, errs = _raising_created(True)
+    assert got == ['created', b'x']
+    assert errs == ['RuntimeError']
+
+
+def test_closed_session_is_collected():
+    """The table refers to the session (its emit) and the session to the
+    table: a GC type pair, so a closed client's session and its watch
+    engine are collected, and close() stops the doublecheck timer."""
+    import gc
+    import weakref
+    zk = FakeZKServer(tick_ms=250)
+    try:
+        c = client(zk.servers())
+        c.wait_connected(10)
+        c.call_sync('create', '/g', b'1', {})
+        seen = []
+        c.watcher('/g').on('dataChanged', lambda d, s: seen.append(d))
+        assert wait_for(lambda: seen == [b'1'], 5)
+        sess = c.getSession()
+        ref = weakref.ref(sess)
+        wt = sess.wt
+        assert c.loop.run(wt.counts)['armed'] == 1
+        c.close_sync(10)
+        assert c.loop.run(wt.counts)['armed'] == 0
+        del sess, wt
+        loop = c.loop
+        c = None
+        for _ in range(3):
+            loop.run(lambda: None)
+            gc.collect()
+        assert ref() is None, gc.get_referrers(ref())
+    finally:
+        zk.shutdown()

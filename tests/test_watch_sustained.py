@@ -1,0 +1,41 @@
+"""The watch workload over a long run: no step may stall.
+
+Round 4 saw single steps of the watch workload (BASELINE config 4's data
+path, :class:`zkmi.bench.synthetic.WatchPipeline`) take 60-175 ms against a
+2.7 ms median, at steps 80-100 and 180-200 from a fresh tree: one ``fs_link``
+on the R1 notification stream (57 MB, 13917 tiles, no repair) waited in its
+grid barrier.  fs_link now has no barrier (the last block to finish its
+check goes on alone), so every step of the run must stay near the median.
+
+Reference framer: lib/zk-streams.js:47-64."""
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def test_watch_steps_do_not_stall(gpu):
+    from zkmi.bench import synthetic as S
+    n = 1 << 20
+    tree = S.GpuTree(1000000, 100, device=gpu, seed=0, watch_cap=2 * n)
+    pipe = S.WatchPipeline(tree, n, seed=0)
+    acc = torch.zeros(64, dtype=torch.int64, device=gpu)
+    steps = 130
+    ev = [(torch.cuda.Event(enable_timing=True),
+           torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    pipe.nscan.chain_stats()
+    for s in range(steps):
+        ev[s][0].record()
+        pipe.step(acc=acc)
+        ev[s][1].record()
+    torch.cuda.synchronize()
+    ms = np.array([a.elapsed_time(b) for a, b in ev[2:]])
+    med = float(np.median(ms))
+    worst = int(np.argmax(ms)) + 2
+    print('watch steps: median %.3f ms, max %.3f ms (step %d)'
+          % (med, ms.max(), worst))
+    # every step delivered and checked every notification
+    assert int(acc.sum().item()) == steps * n
+    assert ms.max() < 2 * med, (ms.max(), med, worst)

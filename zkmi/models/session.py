@@ -390,6 +390,8 @@ class ZKSession(FSM):
             self.conn.destroy()
         self.conn = None
         self.expiry.cancel()
+        if self.wt is not None:
+            self.wt.close()       # its watches are dead: no more timers
         self.log.warn('ZK session expired')
 
     def state_closed(self, S):
@@ -397,6 +399,8 @@ class ZKSession(FSM):
             self.conn.destroy()
         self.conn = None
         self.expiry.cancel()
+        if self.wt is not None:
+            self.wt.close()
         self.log.info('ZK session closed')
 
     # -- watches --------------------------------------------------------------

@@ -318,7 +318,7 @@ FS_WINDOW_AUTO_MAX = 2048
 def frame_window(max_frame):
     """The K1 entry window for a stream whose frames are at most
     ``max_frame`` bytes (length prefix included): the smallest window
-    covering them, up to 1 KiB; past that (or past the module's
+    covering them, up to 2 KiB; past that (or past the module's
     ``FS_WINDOW_AUTO_MAX``, which a test lowers) the window is the cap in
     long-frame mode.  Frames longer than the window are framed exactly
     either way."""

@@ -127,6 +127,29 @@ def _bcast_ints(vals, n, src, device):
     return t.cpu().tolist()
 
 
+def _batch_prior_max(key, val):
+    """For each entry i: the largest ``val`` of the entries before it in the
+    batch with the same ``key`` (-1: none) — a segmented exclusive running
+    max on the device: a stable sort by key, then one cummax over
+    ``segment * 2**32 + val`` (segments ascend, so the max never crosses
+    into the next segment; val in [-1, 2**31))."""
+    n = key.numel()
+    if n == 0:
+        return val.clone()
+    ks, order = torch.sort(key, stable=True)
+    seg = torch.cumsum((ks[1:] != ks[:-1]).to(torch.int64), 0)
+    seg = torch.cat([seg.new_zeros(1), seg])
+    v = val[order] + 1                        # >= 0
+    run = torch.cummax(seg * (1 << 32) + v, 0).values - seg * (1 << 32)
+    prior = torch.cat([run.new_zeros(1), run[:-1]])
+    start = torch.cat([torch.ones(1, dtype=torch.bool, device=key.device),
+                       ks[1:] != ks[:-1]])
+    prior = torch.where(start, torch.zeros_like(prior), prior) - 1
+    out = torch.empty_like(prior)
+    out[order] = prior
+    return out
+
+
 def _patch_xids(raw):
     """Host path: reply frames with their xids set to XID_FWD."""
     b = bytearray(raw)
@@ -352,7 +375,11 @@ class EnsembleWorkload(object):
             .clamp(0, len(self.paths) - 1)
         ver = rr.stat32[0][:k].to(torch.int64)
         ok = (rr.status[:k] == 0) & (rr.err[:k] == 0)
-        dup = ok & (ver <= self.fwd_ver_dev[pid])
+        # a path twice in one batch (a replayed catch-up in the tick of the
+        # original): the later copy is a repeat of the earlier one, as the
+        # host path's entry-by-entry update sees it
+        seen = _batch_prior_max(pid, torch.where(ok, ver, -1))
+        dup = ok & (ver <= torch.maximum(self.fwd_ver_dev[pid], seen))
         self.fwd_ver_dev.scatter_reduce_(0, pid[ok], ver[ok], 'amax')
         ndup = int(dup.sum().item())
         if ndup == 0:

@@ -45,10 +45,11 @@ ZK_DEV int64_t req_body_size(const ZkReqBatch& b, int64_t i, bool* ok) {
 }
 
 // Offsets are reduce-then-scan fused into the producer and the consumer:
-// the sizes kernel also writes its block's sum, one workgroup scans the
-// block sums (zk_scan_small_i64), and the write kernel adds its block base
-// to a block scan of the sizes.  Three launches where a separate device-wide
-// scan made five.
+// the sizes kernel also writes its block's sum and the write kernel sums
+// the block sums before its own (sum_blocks) and adds a block scan of the
+// sizes.  Two launches where a separate device-wide scan made five (and a
+// one-workgroup scan of the block sums between them made three, until
+// round 5; it is still used past FUSED_SCAN_BLOCKS).
 // A malformed request is flagged per block (bbad, a plain store every
 // launch) and req_write's block 0 folds the flags into err, so err needs no
 // zeroing launch before the encode.
@@ -373,19 +374,63 @@ struct EncLocal {
   int64_t sm[ENC_T / 64 + 1];
 };
 
-// off = bbase[block] + block scan of sizes; also written to rec_off.
+// off = base + block scan of sizes; also written to rec_off.
 ZK_DEV void block_offsets(int64_t r0, int64_t r1,
-                          const int64_t* __restrict__ sizes,
-                          const int64_t* __restrict__ bbase,
+                          const int64_t* __restrict__ sizes, int64_t base,
                           int64_t* __restrict__ rec_off, EncLocal& E) {
   const int64_t i = r0 + threadIdx.x;
   const int64_t sz = i < r1 ? sizes[i] : 0;
   int64_t tot;
-  const int64_t o = bbase[blockIdx.x] + block_excl_scan(sz, E.sm, &tot);
+  const int64_t o = base + block_excl_scan(sz, E.sm, &tot);
   E.off[threadIdx.x] = o;
   E.sz[threadIdx.x] = sz;
   if (i < r1 && rec_off != nullptr) rec_off[i] = o;
   __syncthreads();
+}
+
+// The write pass's block base without a scan launch: the sizes pass wrote
+// every block's sum (bsum, complete: an earlier launch), so block b sums
+// bsum[0, b) itself — four independent L2 loads a thread per 1024 blocks,
+// one round trip at the usual batch sizes.  Past FUSED_SCAN_BLOCKS the sum
+// grows with the grid (quadratic traffic) and the host scans bsum first
+// (zk_scan_small_i64 -> bbase).  Also the grand total, for the block that
+// needs it (the last one: it writes *total, err and the terminator).
+constexpr int64_t FUSED_SCAN_BLOCKS = 4096;
+
+ZK_DEV int64_t sum_blocks(const int64_t* __restrict__ bsum, int64_t b,
+                          int64_t* sm) {
+  int64_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+  int64_t k = threadIdx.x;
+  for (; k + 3 * ENC_T < b; k += 4 * ENC_T) {
+    a0 += bsum[k];
+    a1 += bsum[k + ENC_T];
+    a2 += bsum[k + 2 * ENC_T];
+    a3 += bsum[k + 3 * ENC_T];
+  }
+  for (; k < b; k += ENC_T) a0 += bsum[k];
+  int64_t tot;
+  block_excl_scan(a0 + a1 + a2 + a3, sm, &tot);
+  return tot;
+}
+
+// This block's base (bbase, or fused: sum_blocks) and, in the last block,
+// the stream total (fused: computed and stored; else read).
+ZK_DEV int64_t block_base(const int64_t* __restrict__ bbase,
+                          const int64_t* __restrict__ bsum,
+                          int64_t* __restrict__ total, int64_t* sm,
+                          int64_t* T) {
+  const int64_t b = blockIdx.x;
+  if (bsum == nullptr) {
+    *T = *total;
+    return bbase[b];
+  }
+  const int64_t base = sum_blocks(bsum, b, sm);
+  *T = -1;                              // (known in the last block only)
+  if (b == (int64_t)gridDim.x - 1) {
+    *T = base + bsum[b];
+    if (threadIdx.x == 0) *total = *T;
+  }
+  return base;
 }
 
 ZK_DEV uint8_t lds_byte(const uint32_t* lw, int64_t b) {
@@ -464,10 +509,8 @@ ZK_DEV void staged_emit(int64_t r0, int64_t r1, const int64_t* off,
 // after the stream when they fit.  A frame scan run over a host-known upper
 // bound of the stream length then stops exactly at the stream end, so the
 // pipeline needs no device-to-host read of the length before scanning.
-ZK_DEV void put_terminator(bool term, const int64_t* total, uint8_t* out,
-                           int64_t cap) {
-  if (!term || blockIdx.x != 0 || threadIdx.x != 0) return;
-  const int64_t T = *total;
+ZK_DEV void put_terminator(bool term, int64_t T, uint8_t* out, int64_t cap) {
+  if (!term || T < 0 || threadIdx.x != 0) return;
   if (T + 4 <= cap) st_be32(out + T, -1);
 }
 
@@ -628,23 +671,33 @@ ZK_DEV void staged_emit_holes(int64_t r0, int64_t r1, const int64_t* off,
   }
 }
 
+// bsum != null: fused (block_base); every block checks its own span
+// against cap, the last one writes *total and err (2: over capacity, the
+// stream is then incomplete).
 __global__ __launch_bounds__(ENC_T) void resp_write(
     ZkRespBatch r, ZkNodeStore s, const int64_t* __restrict__ n_dev,
     int64_t ncap, const int64_t* __restrict__ sizes,
-    const int64_t* __restrict__ bbase, int64_t* __restrict__ rec_off,
-    const int64_t* __restrict__ total, uint8_t* __restrict__ out, int64_t cap,
-    int32_t* __restrict__ err, int32_t term, int64_t stage) {
+    const int64_t* __restrict__ bbase, const int64_t* __restrict__ bsum,
+    int64_t* __restrict__ rec_off, int64_t* __restrict__ total,
+    uint8_t* __restrict__ out, int64_t cap, int32_t* __restrict__ err,
+    int32_t term, int64_t stage) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lw[];
   __shared__ EncLocal E;
   const int64_t n = min(*n_dev, ncap);
   const int64_t r0 = (int64_t)blockIdx.x * ENC_T;
-  put_terminator(term, total, out, cap);
-  // err written whole by one thread (no zeroing launch before the encode)
-  if (blockIdx.x == 0 && threadIdx.x == 0) *err = *total > cap ? 2 : 0;
+  int64_t T;
+  const int64_t base = block_base(bbase, bsum, total, E.sm, &T);
+  const bool last = blockIdx.x == gridDim.x - 1;
+  if (bsum != nullptr ? last : blockIdx.x == 0) {
+    put_terminator(term, T, out, cap);
+    // err written whole by one thread (no zeroing launch before the encode)
+    if (threadIdx.x == 0) *err = T > cap ? 2 : 0;
+  }
   if (r0 >= n) return;
-  if (*total > cap) return;
+  if (T > cap) return;
   const int64_t r1 = min(r0 + ENC_T, n);
-  block_offsets(r0, r1, sizes, bbase, rec_off, E);
+  if (bsum != nullptr && base + bsum[blockIdx.x] > cap) return;
+  block_offsets(r0, r1, sizes, base, rec_off, E);
   // the holes (large GET_DATA replies), their block scan and list
   __shared__ EncHoles H;
   {
@@ -772,26 +825,30 @@ ZK_DEV void emit_request(K& k, const ZkReqBatch& b, int64_t i, int64_t body) {
 // size 0 (nothing written).
 __global__ __launch_bounds__(ENC_T) void req_write(
     ZkReqBatch b, int64_t n, const int64_t* __restrict__ sizes,
-    const int64_t* __restrict__ bbase, int64_t* __restrict__ rec_off,
-    const int64_t* __restrict__ total, uint8_t* __restrict__ out, int64_t cap,
-    int64_t* __restrict__ xid_tab, int64_t xid_mask,
-    int32_t* __restrict__ err, int32_t term,
+    const int64_t* __restrict__ bbase, const int64_t* __restrict__ bsum,
+    int64_t* __restrict__ rec_off, int64_t* __restrict__ total,
+    uint8_t* __restrict__ out, int64_t cap, int64_t* __restrict__ xid_tab,
+    int64_t xid_mask, int32_t* __restrict__ err, int32_t term,
     const int64_t* __restrict__ bbad, int64_t nb) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lw[];
   __shared__ EncLocal E;
   const int64_t r0 = (int64_t)blockIdx.x * ENC_T;
-  put_terminator(term, total, out, cap);
-  if (blockIdx.x == 0) {
+  int64_t T;
+  const int64_t base = block_base(bbase, bsum, total, E.sm, &T);
+  if (bsum != nullptr ? blockIdx.x == gridDim.x - 1 : blockIdx.x == 0) {
+    put_terminator(term, T, out, cap);
     // err, written whole (1: a malformed request, 2: over capacity)
     int64_t e = 0;
     for (int64_t k = threadIdx.x; k < nb; k += ENC_T) e |= bbad[k];
     const int any = __syncthreads_or(e != 0);
-    if (threadIdx.x == 0) *err = (any ? 1 : 0) | (*total > cap ? 2 : 0);
+    if (threadIdx.x == 0) *err = (any ? 1 : 0) | (T > cap ? 2 : 0);
   }
   if (r0 >= n) return;
-  if (*total > cap) return;                 // capacity guard (whole batch)
+  if (T > cap) return;                      // capacity guard (whole batch)
   const int64_t r1 = min(r0 + ENC_T, n);
-  block_offsets(r0, r1, sizes, bbase, rec_off, E);
+  // fused: each block's own span (the last block flags the batch)
+  if (bsum != nullptr && base + bsum[blockIdx.x] > cap) return;
+  block_offsets(r0, r1, sizes, base, rec_off, E);
   staged_emit(r0, r1, E.off, E.sz, out, lw, [&](auto& k, int64_t i) {
     const int64_t sz = E.sz[i - r0];
     if (sz > 0) emit_request(k, b, i, sz - 4);
@@ -857,11 +914,14 @@ int zk_encode_requests2(const ZkReqBatch* b, int64_t n, int64_t* sizes,
   int64_t* bbad = scan_ws + 2 * nb;
   zk::req_sizes<<<nb, zk::ENC_T, 0, st>>>(*b, n, sizes, bbad, bsum);
   ZK_LAUNCH_CHECK();
-  int rc = zk_scan_small_i64(bsum, bbase, nb, total, st);
-  if (rc) return rc;
+  const bool fused = nb <= zk::FUSED_SCAN_BLOCKS;
+  if (!fused) {
+    int rc = zk_scan_small_i64(bsum, bbase, nb, total, st);
+    if (rc) return rc;
+  }
   zk::req_write<<<nb, zk::ENC_T, zk::STAGE_BYTES, st>>>(
-      *b, n, sizes, bbase, rec_off, total, out, out_cap, xid_tab, xid_mask,
-      err, terminate, bbad, (int64_t)nb);
+      *b, n, sizes, bbase, fused ? bsum : nullptr, rec_off, total, out,
+      out_cap, xid_tab, xid_mask, err, terminate, bbad, (int64_t)nb);
   ZK_LAUNCH_CHECK();
   return 0;
 }
@@ -934,14 +994,17 @@ int zk_encode_responses2(const ZkRespBatch* r, const ZkNodeStore* s,
                                              bsum);
     ZK_LAUNCH_CHECK();
   }
-  int rc = zk_scan_small_i64(bsum, bbase, nb, total, st);
-  if (rc) return rc;
+  const bool fused = nb <= zk::FUSED_SCAN_BLOCKS;
+  if (!fused) {
+    int rc = zk_scan_small_i64(bsum, bbase, nb, total, st);
+    if (rc) return rc;
+  }
   // reply image per workgroup (a 56 KiB image gained 0.5 % on 0-1024 B
   // payloads and cost GET 2 %)
   const int64_t stage = zk::STAGE_BYTES;
   zk::resp_write<<<nb, zk::ENC_T, (size_t)stage, st>>>(
-      *r, *s, n_dev, ncap, sizes, bbase, rec_off, total, out, out_cap, err,
-      terminate, stage);
+      *r, *s, n_dev, ncap, sizes, bbase, fused ? bsum : nullptr, rec_off,
+      total, out, out_cap, err, terminate, stage);
   ZK_LAUNCH_CHECK();
   return 0;
 }

@@ -84,8 +84,9 @@ constexpr int FC_WIN = 4096;               // fs_link's staged walk window
 constexpr int FL_T = 512;
 constexpr int FL_U = 8;                    // fs_link loads per batch
 // fs_link's grid words (see fl_check's caller)
-constexpr int FL_NB = 1;                   // broken links the check saw
+constexpr int FL_NB = 2;                   // broken links the check saw
 constexpr int FL_GW = FL_NB + 1;
+constexpr int FL_LOC = 1024;               // a block's own broken links
 // Count blocks: frame counts scanned per FK_T tiles (one wave's worth)
 constexpr int FK_T = 64;
 // The workspace's words after the X flags (uint64, lbw + 2 * tiles): [0..3]
@@ -1632,12 +1633,87 @@ ZK_DEV FcWalk fc_walk(const uint8_t* __restrict__ buf, int64_t n,
 // broken link with the exact entry — one wave looks a run of tiles up in
 // fs_tile's candidate exits 64 at a time, walking only the tiles whose
 // exact entry is not a candidate — until every live link holds.
-// Grid words (LW_GRID, uint64): [0] the ticket, [FL_NB] the check's count
-// of broken links (fs_rows clears it for the next scan).
+// Before its ticket, a block re-walks the broken links its own check found
+// (one wave a link, from the exit before it as recorded; fl_accept's rule),
+// one parallel repair round over the whole grid without any barrier: a
+// tile whose speculated entry was missing or wrong but whose survivor is
+// the true chain (every tile of a `nospec` stream, a frontier wait that
+// timed out) re-walks to the same exit, so the round settles any number of
+// such tiles at once — the last block then only checks and re-counts.
+// Grid words (LW_GRID, uint64): [0] the ticket, [1] tiles the blocks
+// re-walked, [FL_NB] the check's count of broken links (fs_rows clears it
+// for the next scan).
 // At most this many broken links: chased from the check's list (fl_chase; a
 // reply stream usually has a handful of broken links or none); more go to
 // the tail's exact chases.
 constexpr unsigned long long FL_SMALL = 1024;
+
+ZK_DEV int64_t rfl64(int64_t v) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+  const uint32_t hi =
+      (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)v >> 32));
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
+// Is a repair walk of tile k (new exit x) written?  Always when the link
+// before k holds (its entry E is then exact, or at least as good as the
+// records get).  When that link is itself broken, E is suspect: a garbage
+// exit of tile k-1 (say a frame-length read from an xid, megabytes ahead)
+// walked on would break the link after k where it holds, that link's walk
+// would break the next, and a wave of garbage would cross the stream one
+// tile per round (the first storm reply stream: 1413 tiles re-walked over
+// 71 rounds).  So a suspect walk that changes the exit is not written while
+// link k+1 holds; link k stays broken for the last block's chases.  A walk
+// from an E that tile k-1 has since replaced (another wave re-walked it at
+// the same time) is stale and not written either.  (A refused walk has
+// overwritten the tile's recorded frame starts all the same: its caller
+// clears the entry.)
+ZK_DEV bool fl_accept(const int64_t* rec_entry, const int64_t* rec_exit,
+                      int64_t ntiles, int64_t k, int64_t E, int64_t x) {
+  if (ld_agent(&rec_exit[k - 1]) != E) return false;
+  if (k < 2) return true;
+  const bool suspect = ld_agent(&rec_entry[k - 1]) != ld_agent(&rec_exit[k - 2]);
+  if (!suspect) return true;
+  const int64_t ox = ld_agent(&rec_exit[k]);
+  if (x == ox || k + 1 >= ntiles) return true;
+  return ld_agent(&rec_entry[k + 1]) != ox;
+}
+
+// The block's repair round (see FL_LOC): its check's broken links, one wave
+// a link.  Returns the tiles this wave re-walked.
+ZK_DEV uint32_t fl_local_round(const uint8_t* __restrict__ buf, int64_t n,
+                               int64_t ntiles, int64_t maxp,
+                               const int64_t* __restrict__ sx,
+                               const uint16_t* __restrict__ list,
+                               const int32_t* __restrict__ rcount,
+                               uint16_t* pre, int64_t* rec_entry,
+                               int64_t* rec_exit, int64_t* rec_meta,
+                               const int32_t* lloc, int nloc, uint8_t* win) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint8_t* mywin = win + (size_t)wv * (FC_WIN + 16);
+  uint32_t walked = 0;
+  for (int j = wv; j < nloc; j += FL_T / 64) {
+    const int64_t k = lloc[j];
+    const int64_t E = rfl64(ld_agent(&rec_exit[k - 1]));
+    if (E < k * FT_S ||
+        __builtin_amdgcn_readfirstlane(m_term(ld_agent(&rec_meta[k - 1]))))
+      continue;                               // no usable entry yet
+    const int32_t m0 = __builtin_amdgcn_readfirstlane(rcount[k]);
+    const FcWalk fw = fc_walk(buf, n, maxp, k * FT_S, E, list + k * FT_LMAX,
+                              m0, sx[k], mywin, pre + k * FT_LMAX, lane);
+    ++walked;
+    if (lane == 0) {
+      if (fl_accept(rec_entry, rec_exit, ntiles, k, E, fw.exit)) {
+        st_agent(&rec_entry[k], E);
+        st_agent(&rec_exit[k], fw.exit);
+        st_agent(&rec_meta[k], fc_meta(fw));
+      } else {
+        st_agent(&rec_entry[k], -1);
+      }
+    }
+  }
+  return walked;
+}
 
 // The full check (fs_link, when fs_tile counted a bad link): every link and
 // terminal, one wave per count block of FK_T tiles over the grid, and the
@@ -1650,7 +1726,8 @@ ZK_DEV void fl_check(int64_t ntiles, const int64_t* __restrict__ rec_entry,
                      const int64_t* __restrict__ rec_exit,
                      const int64_t* __restrict__ rec_meta, int64_t* base,
                      int64_t* bsum, uint64_t* mins,
-                     unsigned long long* nbroken, int32_t* blist) {
+                     unsigned long long* nbroken, int32_t* blist,
+                     int32_t* lloc, int* lcnt) {
   const int lane = threadIdx.x & 63;
   const int64_t INF = INT64_MAX;
   const int64_t nw = (int64_t)gridDim.x * (FL_T / 64);
@@ -1680,10 +1757,15 @@ ZK_DEV void fl_check(int64_t ntiles, const int64_t* __restrict__ rec_entry,
       unsigned long long b0 = 0;
       if (lane == 0) b0 = atomicAdd(nbroken, (unsigned long long)__popcll(bm));
       b0 = __shfl(b0, 0, 64);
+      int l0 = 0;
+      if (lane == 0) l0 = atomicAdd(lcnt, __popcll(bm));
+      l0 = __shfl(l0, 0, 64);
       if (brk) {
         const uint64_t below = lane ? (bm & ((~0ull) >> (64 - lane))) : 0ull;
         __hip_atomic_store(&blist[b0 + __popcll(below)], (int32_t)(k + 1),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int li = l0 + __popcll(below);
+        if (li < FL_LOC) lloc[li] = (int32_t)(k + 1);
       }
     }
     int64_t inc = cnt;
@@ -1797,12 +1879,6 @@ ZK_DEV int live_count(const int64_t* c5) {
   return live;
 }
 
-ZK_DEV int64_t rfl64(int64_t v) {
-  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
-  const uint32_t hi =
-      (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)v >> 32));
-  return (int64_t)(((uint64_t)hi << 32) | lo);
-}
 
 ZK_DEV uint64_t readlane64(uint64_t v, int l) {
   const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
@@ -2164,6 +2240,61 @@ ZK_DEV void fl_chase_recount(int64_t ntiles, const int64_t* rec_meta,
   __syncthreads();
 }
 
+// Every live link holds up to the first terminal ft (INF: none): the
+// exclusive scan of the counts of tiles 0..ft as absolute row bases (bsum
+// zero: fs_rows adds no block offset), tiles after ft dead; result[0..3]
+// and the last tile.  The last block alone, after a repair.
+ZK_DEV void fl_count_scan(int64_t n, int64_t ntiles, int64_t ft,
+                          const int64_t* rec_exit, const int64_t* rec_meta,
+                          int64_t* base, int64_t* bsum, int64_t cap,
+                          int64_t* result, int64_t* lastk, int64_t* red) {
+  const int tid = threadIdx.x;
+  const int64_t INF = INT64_MAX;
+  const int64_t last = ft == INF ? ntiles - 1 : ft;
+  const int64_t per = (last + 1 + FL_T - 1) / FL_T;
+  const int64_t k0 = (int64_t)tid * per;
+  const int64_t k1 = min(k0 + per, last + 1);
+  int64_t sum = 0;
+  for (int64_t kb = k0; kb < k1; kb += FL_U) {
+    int64_t v[FL_U];
+#pragma unroll
+    for (int u = 0; u < FL_U; ++u)
+      v[u] = kb + u < k1 ? ld_agent(&rec_meta[kb + u]) : 0;
+#pragma unroll
+    for (int u = 0; u < FL_U; ++u) sum += m_cnt(v[u]);
+  }
+  int64_t tot;
+  int64_t run = block_excl_scan(sum, red, &tot);
+  for (int64_t kb = k0; kb < k1; kb += FL_U) {
+    int64_t v[FL_U];
+#pragma unroll
+    for (int u = 0; u < FL_U; ++u)
+      v[u] = kb + u < k1 ? ld_agent(&rec_meta[kb + u]) : 0;
+#pragma unroll
+    for (int u = 0; u < FL_U; ++u) {
+      if (kb + u < k1) base[kb + u] = run;
+      run += m_cnt(v[u]);
+    }
+  }
+  for (int64_t k = last + 1 + tid; k < ntiles; k += FL_T) base[k] = -1;
+  for (int64_t b = tid; b <= last / FK_T; b += FL_T) bsum[b] = 0;
+  if (tid == 0) {
+    *lastk = last;
+    result[0] = tot;
+    result[3] = tot > cap ? 1 : 0;
+    if (ft == INF) {
+      result[1] = n;
+      result[2] = 0;
+    } else {
+      // (a stop before a tile that is no terminal — unreachable, see the
+      // tail — leaves the carry at tile ft's exit)
+      const int64_t mf = ld_agent(&rec_meta[ft]);
+      result[1] = ld_agent(&rec_exit[ft]);
+      result[2] = m_term(mf) && m_bad(mf) ? 1 : 0;
+    }
+  }
+}
+
 // The leftmost terminal, and the leftmost broken link at or after `from`
 // (INF: none), over the whole block.  Loads in batches of FL_U tiles a
 // thread, all issued before any is used (one round trip a batch).
@@ -2240,11 +2371,26 @@ __global__ __launch_bounds__(FL_T) void fs_link(
   }
   const int64_t INF = INT64_MAX;
   // the check over the grid (links, terminals, in-block counts; a launch of
-  // its own until round 4), then a ticket: the last block to take one sees
-  // every block's check (each releases it before its ticket) and goes on
+  // its own until round 4), the block's repair round over the broken links
+  // it found, then a ticket: the last block to take one sees every block's
+  // check and repairs (each releases them before its ticket) and goes on
   // alone; the others are done
+  __shared__ int32_t lloc[FL_LOC];
+  __shared__ int s_lcnt;
+  if (tid == 0) s_lcnt = 0;
+  __syncthreads();
   fl_check(ntiles, rec_entry, rec_exit, rec_meta, base, bsum, mins, &g[FL_NB],
-           blist);
+           blist, lloc, &s_lcnt);
+  __syncthreads();
+  if (s_lcnt > 0) {
+    const uint32_t w = fl_local_round(buf, n, ntiles, maxp, sx, list, rcount,
+                                      pre, rec_entry, rec_exit, rec_meta, lloc,
+                                      min(s_lcnt, FL_LOC), win);
+    if (lane == 0 && w) {
+      fc_stat(stats, 2, w);
+      atomicAdd(&g[1], (unsigned long long)w);
+    }
+  }
   __shared__ int s_last;
   __syncthreads();
   if (tid == 0) {
@@ -2262,20 +2408,25 @@ __global__ __launch_bounds__(FL_T) void fs_link(
   __syncthreads();
   if (!s_last) return;
   // the minima and the broken-link count (fs_rows clears them for the next
-  // scan of this workspace)
+  // scan of this workspace), and the tiles the blocks' rounds re-walked
   const uint64_t mb0 = ld_agent((const int64_t*)&mins[0]);
   const uint64_t mt0 = ld_agent((const int64_t*)&mins[1]);
   const unsigned long long nb0 = __hip_atomic_load(
       &g[FL_NB], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned long long rew = __hip_atomic_load(
+      &g[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int64_t fb0 = mb0 ? ntiles - (int64_t)mb0 : INF;
   const int64_t ft0 = mt0 ? ntiles - (int64_t)mt0 : INF;
   if (fb0 == INF || fb0 > ft0) {
-    // no broken link before the first terminal: the row bases are bsum's
+    // no broken link before the first terminal (the blocks re-walked only
+    // links past it, whose counts no row uses): the row bases are bsum's
     // block offsets + the check's in-block bases
     fl_bases(n, ntiles, ft0, rec_exit, rec_meta, base, bsum, cap, result,
              lastk, red);
+    if (tid == 0 && rew) g[1] = 0;
     return;
   }
+  if (tid == 0) g[1] = 0;
   __shared__ uint32_t dirty[FL_DB / 32];
   __shared__ int s_ovf;
   FlChase ch{dirty, &s_ovf, stats, ldbg};
@@ -2283,7 +2434,19 @@ __global__ __launch_bounds__(FL_T) void fs_link(
   if (tid == 0) s_ovf = 0;
   __syncthreads();
   const bool clk = ldbg != nullptr && tid == 0;
-  if (nb0 <= FL_SMALL && (ntiles + FK_T - 1) / FK_T <= FL_DB) {
+  int64_t from = 1, ft = INF;
+  if (rew) {
+    // the blocks' round changed records: every link checked again; all
+    // holding, only the counts are scanned again
+    int64_t fbv, ftv;
+    fl_links(1, ntiles, rec_entry, rec_exit, rec_meta, red, fbv, ftv);
+    if (fbv == INF || fbv > ftv) {
+      fl_count_scan(n, ntiles, ftv, rec_exit, rec_meta, base, bsum, cap,
+                    result, lastk, red);
+      return;
+    }
+    from = fbv;
+  } else if (nb0 <= FL_SMALL && (ntiles + FK_T - 1) / FK_T <= FL_DB) {
     // ---- a handful of broken links: chases, then every link checked -----
     if (clk) ldbg[0] = wall_clock64();
     const bool settled = fl_chase(buf, n, ntiles, maxp, sx, list, rcount, pre,
@@ -2304,7 +2467,6 @@ __global__ __launch_bounds__(FL_T) void fs_link(
   }
   // ---- the tail: exact chases from the leftmost broken link, until every
   // live link holds; then the count scan ------------------------------------
-  int64_t from = 1, ft = INF;
   for (;;) {
     int64_t fb, fterm;
     fl_links(from, ntiles, rec_entry, rec_exit, rec_meta, red, fb, fterm);
@@ -2338,52 +2500,8 @@ __global__ __launch_bounds__(FL_T) void fs_link(
       break;
     }
   }
-  // exclusive scan of the counts of tiles 0..ft; tiles after ft are dead
-  const int64_t last = ft == INF ? ntiles - 1 : ft;
-  const int64_t per = (last + 1 + FL_T - 1) / FL_T;
-  const int64_t k0 = (int64_t)tid * per;
-  const int64_t k1 = min(k0 + per, last + 1);
-  int64_t sum = 0;
-  for (int64_t kb = k0; kb < k1; kb += FL_U) {
-    int64_t v[FL_U];
-#pragma unroll
-    for (int u = 0; u < FL_U; ++u)
-      v[u] = kb + u < k1 ? ld_agent(&rec_meta[kb + u]) : 0;
-#pragma unroll
-    for (int u = 0; u < FL_U; ++u) sum += m_cnt(v[u]);
-  }
-  int64_t tot;
-  int64_t run = block_excl_scan(sum, red, &tot);
-  for (int64_t kb = k0; kb < k1; kb += FL_U) {
-    int64_t v[FL_U];
-#pragma unroll
-    for (int u = 0; u < FL_U; ++u)
-      v[u] = kb + u < k1 ? ld_agent(&rec_meta[kb + u]) : 0;
-#pragma unroll
-    for (int u = 0; u < FL_U; ++u) {
-      if (kb + u < k1) base[kb + u] = run;
-      run += m_cnt(v[u]);
-    }
-  }
-  for (int64_t k = last + 1 + tid; k < ntiles; k += FL_T) base[k] = -1;
-  // absolute bases: fs_rows adds a zero block offset
-  for (int64_t b = tid; b <= last / FK_T; b += FL_T) bsum[b] = 0;
-  if (tid == 0) {
-    *lastk = last;
-    result[0] = tot;
-    result[3] = tot > cap ? 1 : 0;
-    if (ft == INF) {
-      result[1] = n;
-      result[2] = 0;
-    } else if (m_term(ld_agent(&rec_meta[ft]))) {
-      result[1] = ld_agent(&rec_exit[ft]);
-      result[2] = m_bad(ld_agent(&rec_meta[ft])) ? 1 : 0;
-    } else {
-      // (the unreachable stop above: the carry starts at tile ft's exit)
-      result[1] = ld_agent(&rec_exit[ft]);
-      result[2] = 0;
-    }
-  }
+  fl_count_scan(n, ntiles, ft, rec_exit, rec_meta, base, bsum, cap, result,
+                lastk, red);
 }
 
 // (body offset, length) rows: one wave per tile, 4 tiles per block.  A

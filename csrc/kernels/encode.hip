@@ -174,13 +174,19 @@ __global__ __launch_bounds__(ENC_T) void resp_sizes(ZkRespBatch r,
 // dword can be shared with a neighbour, and those are OR-ed into the
 // zero-initialised image (ds_or_b32), everything else is a plain ds_write.
 //
-// The image is bank-swizzled: dword w lives at swz(w), which XORs bits 2-5
-// with the 64-dword row number.  Lanes emit their records in lockstep, so
-// their k-th dwords sit one record apart; at 192-byte records (48 dwords)
-// that put 4 lanes on every bank (measured: 23.6 M conflict cycles per 1M
-// GET_DATA replies).  The XOR keeps each aligned 4-dword group together, so
-// the read-out still moves 16-byte vectors.
-ZK_DEV int64_t swz(int64_t w) { return w ^ (((w >> 6) & 15) << 2); }
+// The image is bank-swizzled: dword w lives at swz(w) = w ^ ((w >> 4) & 31),
+// a permutation inside each aligned 32-dword group.  Lanes emit their
+// records in lockstep, so their k-th dwords sit one record apart; ds_write_b32
+// banks are (dword mod 32) over 32-lane groups, and at 192-byte records (48
+// dwords) an unswizzled image put 16 lanes on a bank.  Any swizzle that
+// keeps aligned 4-dword groups together (rounds 1-4: bits 2-5 XORed with the
+// 64-dword row, 2.49 M conflict cycles a 512K-reply dispatch) leaves lanes
+// writing dword k of 4-aligned records on 8 banks, 4-way; this one moves
+// bits 0-1 too (conflict-free at 48 dwords; 2-3 way for odd record sizes),
+// so the read-out goes a dword a lane: 32 consecutive dwords of a group hit
+// 32 distinct banks, and a wave's 4-byte stores still cover 256 contiguous
+// bytes.
+ZK_DEV int64_t swz(int64_t w) { return w ^ ((w >> 4) & 31); }
 struct GSink {
   uint8_t* o;
   ZK_DEV void be32(int32_t v) { st_be32(o, v); o += 4; }
@@ -438,16 +444,16 @@ ZK_DEV uint8_t lds_byte(const uint32_t* lw, int64_t b) {
 }
 
 // Stream the block's LDS image [B0, B1) (image base a0 = B0 & ~15) out to
-// global memory: 16-byte aligned interior with dwordx4 stores, the <= 15
-// head / tail bytes with byte stores (they abut other blocks' spans).
+// global memory: the dword-aligned interior a dword a lane (see swz), the
+// <= 3 head / tail bytes with byte stores (they abut other blocks' spans).
 ZK_DEV void stage_out(const uint32_t* lw, int64_t a0, int64_t B0, int64_t B1,
                       uint8_t* __restrict__ out) {
-  const int64_t c0 = (B0 + 15) & ~(int64_t)15;
-  const int64_t c1 = B1 & ~(int64_t)15;
+  const int64_t c0 = (B0 + 3) & ~(int64_t)3;
+  const int64_t c1 = B1 & ~(int64_t)3;
   if (c0 < c1) {
-    for (int64_t x = c0 + (int64_t)threadIdx.x * 16; x < c1;
-         x += (int64_t)blockDim.x * 16)
-      *(uint4*)(out + x) = *(const uint4*)(lw + swz((x - a0) >> 2));
+    for (int64_t x = c0 + (int64_t)threadIdx.x * 4; x < c1;
+         x += (int64_t)blockDim.x * 4)
+      *(uint32_t*)(out + x) = lw[swz((x - a0) >> 2)];
     const int64_t hb = c0 - B0, tb = B1 - c1;
     if ((int64_t)threadIdx.x < hb) {
       const int64_t x = B0 + threadIdx.x;
@@ -566,7 +572,9 @@ ZK_DEV void stage_out_segs(const uint32_t* lw, int64_t a0c, int64_t B0,
     }
     for (int64_t y = y0 & ~(int64_t)15; y < y1; y += 16) {
       const int64_t x = y + a0c + d;
-      const uint4 v = *(const uint4*)(lw + swz(y >> 2));
+      const int64_t wy = y >> 2;
+      const uint4 v = make_uint4(lw[swz(wy)], lw[swz(wy + 1)],
+                                 lw[swz(wy + 2)], lw[swz(wy + 3)]);
       if (x >= B0 && x + 16 <= B1) {
         *(uint4*)(out + x) = v;
       } else {

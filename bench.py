@@ -690,12 +690,15 @@ def run_rank(a):
         # mix keeps 3 generations of batch/3 nodes, the storm up to 3
         # batches (the expiring session's two, the new session's first)
         spare = (a.batch * (1 if a.workload in ('mix', 'chain', 'nest')
-                            else 3) + 8192) / a.nodes
+                            else 3 * world) + 8192) / a.nodes
         # chain: the set and get of every chain reply from a snapshot; nest:
         # the parents' EXISTS
         scratch = (a.batch // 2 + 64) * (80 + ((a.data_bytes + 15) & ~15)) \
             if a.workload in ('chain', 'nest') else 0
-        tree = S.GpuTree(a.nodes, a.data_bytes, device=dev, seed=rank,
+        # the storm's members hold one replicated tree: the same tree on
+        # every rank (seed 0), every member applies every member's writes
+        tree = S.GpuTree(a.nodes, a.data_bytes, device=dev,
+                         seed=0 if a.workload == 'storm' else rank,
                          spare=spare + 0.05, scratch=scratch)
         if a.workload == 'chain':
             pipe = S.ChainPipeline(tree, a.batch, a.data_bytes, seed=rank)

@@ -1,17 +1,23 @@
 """BASELINE config 5 across GPUs (zkmi/bench/synthetic.py StormPipeline
-with a process group): each rank's session is born on its own member,
+with a process group): the members hold one replicated tree (every
+member applies every member's write batch, in rank order, so sequential
+names and zxids agree); each rank's session is born on its own member,
 replicated to every member (R3 all-gather into the replicated session
 tables), resumed on the NEXT member (the ConnectRequests go there through
 an all-gather, the answers come back the same way) with the same id and
 password, its second batch created there; its first batch survives the
 move and both go at its expiry, which every member applies; the expired
-session's resume is refused on any member.  Everything is checked on the
-device (the pipeline's reply / handshake / removed-count checks).
+session's resume is refused on any member.  After a move the client reads
+its first batch (written through member r) on member r+1: every node is
+there, owned by its session (write visibility across members).  Everything
+is checked on the device (the pipeline's reply / handshake / removed-count
+checks).
 
 Runs world 2 and 3 with gloo on one GPU (ranks share it; RCCL needs one GPU
 per rank).  Reference: lib/zk-session.js:265-339 (reattach to another
-backend), test/multi-node.test.js:233-350 (the ephemeral survives the
-failover), test/nasty.test.js:40-103."""
+backend), test/multi-node.test.js:107-165 (a write through one server is
+read on another), :233-350 (the ephemeral survives the failover),
+test/nasty.test.js:40-103."""
 
 import socket
 
@@ -29,16 +35,22 @@ def _rank(rank, world, port, q, steps, n):
     try:
         from zkmi.bench.synthetic import GpuTree, StormPipeline
         dev = torch.device('cuda', 0)
-        tree = GpuTree(20000, 37, fanout=100, device=dev, seed=rank,
+        # every member starts from the same tree (one replicated tree)
+        tree = GpuTree(20000, 37, fanout=100, device=dev, seed=0,
                        spare=1.5)
         pipe = StormPipeline(tree, n, ndirs=64, coll_device='cpu')
         oks = [int(pipe.step().item()) for _ in range(steps)]
+        # the last step moved the session to the next member: its first
+        # batch, written through this member, read there
+        found = int(pipe.cross_read().item())
         # the replicated tables: every member knows every live session
         sids = pipe.sessions.sid[pipe.sessions.state == 1].cpu().tolist()
+        # one tree: every member's zxid counter agrees
+        zx = int(tree.counters[1].item())
         q.put((rank, oks, dict(pipe.stats), bool(pipe.hs_ok.item()),
-               sorted({s >> 56 for s in sids})))
+               sorted({s >> 56 for s in sids}), found, zx))
     except BaseException as e:          # reported by the parent
-        q.put((rank, repr(e), None, None, None))
+        q.put((rank, repr(e), None, None, None, None, None))
         raise
     finally:
         dist.destroy_process_group()
@@ -53,7 +65,7 @@ def test_storm_sessions_move_between_members(gpu, world):
     s.close()
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
-    steps, n = 8, 2048
+    steps, n = 9, 2048
     procs = [ctx.Process(target=_rank, args=(r, world, port, q, steps, n))
              for r in range(world)]
     for p in procs:
@@ -65,14 +77,20 @@ def test_storm_sessions_move_between_members(gpu, world):
         r = q.get(timeout=10)
         res[r[0]] = r[1:]
     assert all(p.exitcode == 0 for p in procs), res
-    for rank, (oks, st, hs_ok, members) in res.items():
+    zxids = set()
+    for rank, (oks, st, hs_ok, members, found, zx) in res.items():
         assert oks == [n] * steps, (rank, oks)
         assert hs_ok
-        # steps 1..8 after the birth in __init__: 4 resumes, all on the
-        # next member; 4 births; 4 generations expired (two batches each
-        # on every member), 3 expired resumes refused
-        assert st == {'born': 5, 'resumed': 4, 'expired': 4,
-                      'expired_resume_refused': 3,
-                      'cross_rank_resumes': 4}, (rank, st)
+        # steps 1..9 after the birth in __init__: 5 resumes, all on the
+        # next member; 4 births; 4 generations expired (two batches of
+        # every member's session on every member), 4 expired resumes
+        # refused; every member applied every member's batches
+        assert st == {'born': 5, 'resumed': 5, 'expired': 4,
+                      'expired_resume_refused': 4, 'cross_rank_resumes': 5,
+                      'replicated_writes': (steps + 1) * world * n}, \
+            (rank, st)
         # every member's live sessions are in every member's table
         assert members == list(range(1, world + 1)), (rank, members)
+        assert found == n, (rank, found)
+        zxids.add(zx)
+    assert len(zxids) == 1, zxids

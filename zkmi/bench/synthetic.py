@@ -1203,7 +1203,22 @@ class StormPipeline(object):
     every member drops what the session created there (so each removes two
     sessions' batches: its own session's first and its neighbour's second)
     and closes it in its table, so the expired resume tried at the next
-    move is refused on any member."""
+    move is refused on any member.
+
+    The members hold ONE replicated tree (every rank builds the same tree,
+    seed 0, and applies every committed write): a step's write batches of
+    all members are all-gathered as encoded CREATE frames and every member
+    applies them in rank order — the step's commit order, the zxid order a
+    ZooKeeper leader imposes — so sequential names, zxids and ephemeral
+    owners come out the same on every member.  The member a client is
+    attached to answers it (its reply stream comes back through an
+    all-gather after a move).  A znode created through member r is then
+    readable and deletable on member r+1 (:meth:`cross_read`; the
+    reference's test/multi-node.test.js:107-165 write visibility and
+    :233-350 ephemeral-survives-failover), and an expiry removes the
+    session's nodes on every member.  The work of a write grows with the
+    members (each applies W batches a step): ``stats['replicated_writes']``
+    counts what this member applied."""
 
     TIMEOUT = 30000
     HS_SLOT = 128            # handshake bytes a rank sends per all-gather
@@ -1279,6 +1294,13 @@ class StormPipeline(object):
         self.inserted = 0
         self.stats = {'born': 0, 'resumed': 0, 'expired': 0,
                       'expired_resume_refused': 0, 'cross_rank_resumes': 0}
+        # replicated tree (see the class docs): the step's stream slots
+        self.req_bytes = None       # a batch's encoded bytes (constant)
+        self.rep_bytes = None
+        self.len_ok = torch.ones(1, dtype=torch.bool, device=dev)
+        if W > 1:
+            self.stats['replicated_writes'] = 0
+        self.first = None           # the current session's first batch
         self.drv.create_dirs(
             [['/storm'], ['/storm/d%05d' % d for d in range(ndirs)]],
             (self.acl_arena, self.acl_off, self.acl_len))
@@ -1406,9 +1428,17 @@ class StormPipeline(object):
                             self.data_len, self.acl_id, self.path_arena,
                             self.data_arena, self.acl_off, self.acl_len,
                             self.acl_arena)
-        rep, _ = self.drv.run(rb, session=cur)
+        if self.world > 1:
+            rep = self._replicated_run(rb, resume)
+        else:
+            rep, _ = self.drv.run(rb, session=cur)
         self.last = (rb, rep)
-        self.inserted += n
+        self.inserted += n * self.world
+        if not resume and self.world > 1:
+            # the new session's first batch: the created paths (offsets into
+            # the reply stream kept with them), for cross_read
+            self.first = (self.my_rx.clone(), rep.pay_off[:n].clone(),
+                          rep.pay_len[:n].clone())
         torch.maximum(self.last_zxid, rep.zxid[:n].max().view(1),
                       out=self.last_zxid)
         expire_ok = True
@@ -1416,13 +1446,15 @@ class StormPipeline(object):
             # the generation before expires on every member: here its first
             # batch (our session) and its second (the previous member's,
             # which moved here); every member closes all of them
+            # the generation before expires on every member, which holds
+            # all members' sessions' nodes (the replicated tree): each of
+            # them created two batches
             self.removed.zero_()
-            t.expire(self.sid(self.rank, self.k - 1), self.removed)
-            t.expire(self.sid((self.rank - 1) % self.world, self.k - 1),
-                     self.removed)
+            for m in range(self.world):
+                t.expire(self.sid(m, self.k - 1), self.removed)
             self.sessions.close(self.prev_recs[:, 0].contiguous())
             self.stats['expired'] += 1
-            expire_ok = self.removed[0] == 2 * n
+            expire_ok = self.removed[0] == 2 * n * self.world
         elif not resume and self.k >= 1:
             # the previous session expires: both of its batches go
             prev = self.sessions.sid_of(self.k - 1)
@@ -1437,11 +1469,119 @@ class StormPipeline(object):
         good = ((rep.status[:n] == 0) & (rep.err[:n] == 0) &
                 (rep.xid[:n] == rb.xid) &
                 (rep.pay_len[:n] == self.want_len)).sum()
-        good = torch.where(self.hs_ok[0] & expire_ok, good, 0)
+        good = torch.where(self.hs_ok[0] & self.len_ok[0] & expire_ok, good,
+                           0)
         if acc is None:
             return good
         acc[:1] += good
         return acc
+
+    # -- the replicated tree ----------------------------------------------------
+
+    def _stream_len(self, total, attr):
+        """The byte length of a batch's encoded stream: the same every step
+        (fixed-size records), read from the device once; later steps check
+        it on the device (len_ok)."""
+        v = getattr(self, attr)
+        if v is None:
+            v = int(total.item())
+            setattr(self, attr, v)
+            return v
+        self.len_ok &= total.view(-1)[0] == v
+        return v
+
+    def _replicated_run(self, rb, resume):
+        """Every member's batch applied on every member, in rank order; the
+        reply stream of the client this member answers goes back to it."""
+        d = self.drv
+        W, r, n = self.world, self.rank, self.n
+        tx, _, total, _ = B.encode_requests(rb, d.xt, out=d.tx)
+        S = self._stream_len(total, 'req_bytes')
+        if not hasattr(self, 'tx_all'):
+            self.tx_all = torch.empty(W * S, dtype=U8, device=self.dev)
+        self._gather(self.tx_all, tx[:S])
+        # the client this member answers: its own, or after a move the
+        # previous member's
+        ans = (r - 1) % W if resume else r
+        for m in range(W):
+            rx, rtotal, _, _ = d.server.serve(
+                self.tx_all[m * S:(m + 1) * S], S, session=self.sid(m, self.k),
+                ordered=d.passes > 0, passes=max(d.passes, 1))
+            if m == ans:
+                R = self._stream_len(rtotal, 'rep_bytes')
+                if not hasattr(self, 'rep_out'):
+                    self.rep_out = torch.empty(R + 64, dtype=U8,
+                                               device=self.dev)
+                    self.rep_all = torch.empty(W * R, dtype=U8,
+                                               device=self.dev)
+                    self.my_rx = torch.empty(R + 64, dtype=U8,
+                                             device=self.dev)
+                self.rep_out[:R].copy_(rx[:R])
+        self.stats['replicated_writes'] += W * n
+        R = self.rep_bytes
+        if resume:
+            # my answers come from the member my session moved to
+            self._gather(self.rep_all, self.rep_out[:R])
+            src = (r + 1) % W
+            self.my_rx[:R].copy_(self.rep_all[src * R:(src + 1) * R])
+        else:
+            self.my_rx[:R].copy_(self.rep_out[:R])
+        if d.rscanner is None:
+            d.rscanner = B.FrameScanner(self.n, self.dev, window=d.rwindow)
+        ft = d.rscanner.scan(self.my_rx, R)
+        return B.decode_replies(self.my_rx, ft, d.xt, out=d.reply)
+
+    def cross_read(self):
+        """Write visibility across members: this rank's client reads its
+        current session's FIRST batch (created through the member the
+        session was born on) with EXISTS at the NEXT member — the requests
+        go there and the replies come back through all-gathers.  Returns
+        the device count of nodes found with this session as their
+        ephemeral owner (every member calls it together)."""
+        if self.world < 2 or self.first is None:
+            raise RuntimeError('cross_read needs an ensemble across GPUs '
+                               'and a born session')
+        d = self.drv
+        W, r, n, dev = self.world, self.rank, self.n, self.dev
+        arena, poff, plen = self.first
+        z32 = torch.zeros(n, dtype=I32, device=dev)
+        rb = B.RequestBatch(n, torch.full((n,), consts.OP_CODES['EXISTS'],
+                                          dtype=I32, device=dev),
+                            d.xids(n), z32, poff, plen,
+                            torch.zeros(n, dtype=I64, device=dev), z32, z32,
+                            arena, arena, self.acl_off, self.acl_len,
+                            self.acl_arena)
+        tx, _, total, _ = B.encode_requests(rb, d.xt, out=d.tx)
+        S = int(total.item())
+        sizes = self._gather(torch.empty(W, dtype=I64, device=dev),
+                             torch.tensor([S], dtype=I64, device=dev)).cpu()
+        Smax = int(sizes.max())
+        buf = torch.zeros(Smax, dtype=U8, device=dev)
+        buf[:S].copy_(tx[:S])
+        allq = torch.empty(W * Smax, dtype=U8, device=dev)
+        self._gather(allq, buf)
+        # serve the previous rank's reads here (member r + 1 of its client)
+        src = (r - 1) % W
+        rx, rtotal, _, _ = d.server.serve(
+            allq[src * Smax:src * Smax + int(sizes[src])], int(sizes[src]),
+            session=self.sid(src, self.k))
+        R = int(rtotal.item())
+        ra = self._gather(torch.empty(W, dtype=I64, device=dev),
+                          torch.tensor([R], dtype=I64, device=dev)).cpu()
+        Rmax = int(ra.max())
+        out = torch.zeros(Rmax, dtype=U8, device=dev)
+        out[:R].copy_(rx[:R])
+        alla = torch.empty(W * Rmax, dtype=U8, device=dev)
+        self._gather(alla, out)
+        dst = (r + 1) % W
+        mine = alla[dst * Rmax:dst * Rmax + int(ra[dst])].clone()
+        sc = B.FrameScanner(n, dev, window=256)
+        ft = sc.scan(mine, int(ra[dst]))
+        rep = B.decode_replies(mine, ft, d.xt)
+        owner = self.sid(r, self.k)
+        found = ((rep.status[:n] == 0) & (rep.err[:n] == 0) &
+                 (rep.stat64[4][:n] == owner)).sum()
+        return found
 
     def diagnose(self):
         rb, rep = self.last

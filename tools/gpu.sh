@@ -12,6 +12,7 @@
 #   bench[=ARGS]        bench.py ARGS (default: the driver's config)
 #   prof=TAG[,WL...]    rocprofv3 --kernel-trace --stats of bench.py
 #                       --steps 5 for each workload WL (default get)
+#   profb=TAG,ARGS      rocprofv3 --kernel-trace --stats of bench.py ARGS
 #   pmc=WL              tools/pmc_passes.sh WL (one counter pass a run)
 #   sustain=WL[,STEPS[,CHUNK]]   tools/microbench/sustain_probe.py
 #   py=SCRIPT[,ARGS]    python -u SCRIPT ARGS
@@ -58,6 +59,11 @@ for step in "$@"; do
           || { rc=$?; break; }
       done
       [ $rc -eq 0 ] ;;
+    profb)
+      set -- $args
+      tag=$1; shift
+      (cd /tmp && run 300 $OUT/${n}_$tag.log rocprofv3 --kernel-trace --stats \
+        --output-format csv -d $OUT/$tag -o prof -- python3 $R/bench.py "$@") ;;
     pmc)
       run 600 $log bash $R/tools/pmc_passes.sh $args ;;
     sustain)

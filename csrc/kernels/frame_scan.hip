@@ -87,6 +87,8 @@ constexpr int FL_U = 8;                    // fs_link loads per batch
 constexpr int FL_NB = 2;                   // broken links the check saw
 constexpr int FL_GW = FL_NB + 1;
 constexpr int FL_LOC = 1024;               // a block's own broken links
+constexpr int FL_LOCAL_MIN = 64;           // ... walked by the block when
+                                           // it found more than this many
 // Count blocks: frame counts scanned per FK_T tiles (one wave's worth)
 constexpr int FK_T = 64;
 // The workspace's words after the X flags (uint64, lbw + 2 * tiles): [0..3]
@@ -2392,7 +2394,11 @@ __global__ __launch_bounds__(FL_T) void fs_link(
   fl_check(ntiles, rec_entry, rec_exit, rec_meta, base, bsum, mins, &g[FL_NB],
            blist, lloc, &s_lcnt);
   __syncthreads();
-  if (s_lcnt > 0) {
+  // (a handful of broken links — a frontier timeout, a garbage candidate,
+  // the ends of a phantom chain's region — are the last block's chases:
+  // an exact chase runs on through a region of consistent-but-wrong links
+  // that no per-link walk sees broken)
+  if (s_lcnt > FL_LOCAL_MIN) {
     const uint32_t w = fl_local_round(buf, n, ntiles, maxp, sx, list, rcount,
                                       pre, rec_entry, rec_exit, rec_meta, lloc,
                                       min(s_lcnt, FL_LOC), win);

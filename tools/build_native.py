@@ -138,7 +138,8 @@ def _ext_path(name):
 # CPython extensions built from csrc/host: module name -> source
 HOST_EXTS = {'_zkhost': 'zk_host_codec.cpp',     # Jute host codec
              '_zkloop': 'zk_loop.cpp',           # epoll event loop
-             '_zkwatch': 'zk_watch.cpp'}         # watch-event engine
+             '_zkwatch': 'zk_watch.cpp',         # watch-event engine
+             '_zkfsm': 'zk_fsm.cpp'}             # FSM runtime
 
 
 FAST_SERVER = os.path.join(ROOT, 'zkmi', 'bin', 'zk_fastserver')

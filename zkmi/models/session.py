@@ -128,8 +128,8 @@ class ZKSession(FSM):
                                           float(config.doublecheck_rand_ms))
         FSM.__init__(self, 'detached', loop)
 
-    def _fsm_enter(self, state):
-        FSM._fsm_enter(self, state)
+    def _fsm_entered(self, state):
+        # after every transition (the FSM runtime's hook)
         if self.wt is not None:
             self._wt_sync()
 

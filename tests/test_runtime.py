@@ -44,7 +44,21 @@ class Toy(FSM):
         S.on(self.ext, 'back', lambda: S.gotoState('a'))
 
 
-def test_fsm_semantics():
+@pytest.fixture(params=['native', 'python'])
+def fsm_runtime(request, monkeypatch):
+    """Both FSM runtimes: the native one (csrc/host/zk_fsm.cpp) and the
+    Python oracle (ZKMI_PY_FSM=1)."""
+    from zkmi.runtime import fsm
+    if request.param == 'native':
+        if fsm._zkfsm is None:
+            pytest.skip('native FSM runtime not built')
+        monkeypatch.delenv('ZKMI_PY_FSM', raising=False)
+    else:
+        monkeypatch.setenv('ZKMI_PY_FSM', '1')
+    return request.param
+
+
+def test_fsm_semantics(fsm_runtime):
     loop = default_loop()
     log = []
     changes = []
@@ -75,7 +89,7 @@ def test_fsm_semantics():
     assert t.getState() == 'a'
 
 
-def test_fsm_stale_handle_raises():
+def test_fsm_stale_handle_raises(fsm_runtime):
     loop = default_loop()
 
     class T(FSM):
@@ -89,6 +103,30 @@ def test_fsm_stale_handle_raises():
     loop.run(lambda: S.gotoState('y'))
     with pytest.raises(AssertionError):
         loop.run(lambda: S.gotoState('x'))
+
+
+def test_fsm_runtime_kind(fsm_runtime):
+    """The machine runs on the runtime asked for; the native core's
+    interval re-arms and its disposal cancels it."""
+    from zkmi.runtime import fsm
+    loop = default_loop()
+    ticks = []
+
+    class T(FSM):
+        def state_x(self, S):
+            S.interval(10, lambda: ticks.append(1))
+            S.on(self, 'stop', lambda: S.gotoState('y'))
+
+        def state_y(self, S):
+            pass
+    t = loop.run(lambda: T('x', loop))
+    kind = type(t._fsm_core).__name__
+    assert kind == ('Core' if fsm_runtime == 'native' else 'PyCore')
+    assert wait_for(lambda: len(ticks) >= 3, 5)
+    loop.run(lambda: t.emit('stop'))
+    n = len(ticks)
+    time.sleep(0.08)
+    assert len(ticks) == n and t.fsm_history == ['x', 'y']
 
 
 def test_emitter_semantics():

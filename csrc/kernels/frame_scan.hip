@@ -2356,6 +2356,51 @@ ZK_DEV void fl_links(int64_t from, int64_t ntiles,
   ft_out = fterm;
 }
 
+// Every broken link (after a tile that is no terminal) into blist, in tile
+// order, by the whole block; returns their count.  fb / ft: the leftmost
+// broken link and terminal (INF: none).
+ZK_DEV int64_t fl_list_broken(int64_t ntiles, const int64_t* rec_entry,
+                              const int64_t* rec_exit, const int64_t* rec_meta,
+                              int32_t* blist, int64_t* red, int64_t& fb_out,
+                              int64_t& ft_out) {
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int64_t INF = INT64_MAX;
+  const int64_t per = (ntiles + FL_T - 1) / FL_T;
+  const int64_t k0 = (int64_t)tid * per, k1 = min(k0 + per, ntiles);
+  auto broken = [&](int64_t k) {
+    return k >= 1 && !m_term(ld_agent(&rec_meta[k - 1])) &&
+           ld_agent(&rec_entry[k]) != ld_agent(&rec_exit[k - 1]);
+  };
+  int64_t cnt = 0, fb = INF, fterm = INF;
+  for (int64_t k = k0; k < k1; ++k) {
+    if (broken(k)) {
+      ++cnt;
+      fb = min(fb, k);
+    }
+    if (m_term(ld_agent(&rec_meta[k]))) fterm = min(fterm, k);
+  }
+  int64_t tot;
+  int64_t w = block_excl_scan(cnt, red, &tot);
+  for (int64_t k = k0; k < k1 && cnt > 0; ++k)
+    if (broken(k)) blist[w++] = (int32_t)k;
+  for (int d = 32; d >= 1; d >>= 1) {
+    fb = min(fb, (int64_t)__shfl_xor(fb, d, 64));
+    fterm = min(fterm, (int64_t)__shfl_xor(fterm, d, 64));
+  }
+  if (lane == 0) { red[wv] = fb; red[FL_T / 64 + wv] = fterm; }
+  __syncthreads();
+  fb = INF;
+  fterm = INF;
+  for (int j = 0; j < FL_T / 64; ++j) {
+    fb = min(fb, red[j]);
+    fterm = min(fterm, red[FL_T / 64 + j]);
+  }
+  __syncthreads();
+  fb_out = fb;
+  ft_out = fterm;
+  return tot;
+}
+
 __global__ __launch_bounds__(FL_T) void fs_link(
     const uint8_t* __restrict__ buf, const int64_t* __restrict__ n_dev,
     int64_t n_cap, int64_t maxp, const int64_t* __restrict__ sx,
@@ -2451,35 +2496,46 @@ __global__ __launch_bounds__(FL_T) void fs_link(
   __syncthreads();
   const bool clk = ldbg != nullptr && tid == 0;
   int64_t from = 1, ft = INF;
+  int64_t nb = (int64_t)nb0;
   if (rew) {
-    // the blocks' round changed records: every link checked again; all
-    // holding, only the counts are scanned again
+    // the blocks' round changed records: the links still broken listed
+    // again (blist, in tile order); none before the first terminal: only
+    // the counts are scanned again
     int64_t fbv, ftv;
-    fl_links(1, ntiles, rec_entry, rec_exit, rec_meta, red, fbv, ftv);
+    nb = fl_list_broken(ntiles, rec_entry, rec_exit, rec_meta, blist, red,
+                        fbv, ftv);
     if (fbv == INF || fbv > ftv) {
       fl_count_scan(n, ntiles, ftv, rec_exit, rec_meta, base, bsum, cap,
                     result, lastk, red);
       return;
     }
     from = fbv;
-  } else if (nb0 <= FL_SMALL && (ntiles + FK_T - 1) / FK_T <= FL_DB) {
+  }
+  if (nb <= (int64_t)FL_SMALL && (ntiles + FK_T - 1) / FK_T <= FL_DB) {
     // ---- a handful of broken links: chases, then every link checked -----
     if (clk) ldbg[0] = wall_clock64();
     const bool settled = fl_chase(buf, n, ntiles, maxp, sx, list, rcount, pre,
                                   rec_entry, rec_exit, rec_meta, lbw, cx, blist,
-                                  (int)nb0, win, stats, ch);
+                                  (int)nb, win, stats, ch);
     if (clk) ldbg[1] = ldbg[2] = wall_clock64();
     // a chase only vouches for the links it saw
     int64_t fbv, ftv;
     fl_links(1, ntiles, rec_entry, rec_exit, rec_meta, red, fbv, ftv);
     if (clk) ldbg[3] = wall_clock64();
     if (settled && (fbv == INF || fbv > ftv)) {
+      if (rew) {
+        // (tiles the blocks re-walked are not in the chases' dirty set)
+        fl_count_scan(n, ntiles, ftv, rec_exit, rec_meta, base, bsum, cap,
+                      result, lastk, red);
+        return;
+      }
       fl_chase_recount(ntiles, rec_meta, base, bsum, ch);
       fl_bases(n, ntiles, ftv, rec_exit, rec_meta, base, bsum, cap, result,
                lastk, red);
       if (clk) ldbg[4] = wall_clock64();
       return;
     }
+    from = 1;
   }
   // ---- the tail: exact chases from the leftmost broken link, until every
   // live link holds; then the count scan ------------------------------------

@@ -5,8 +5,8 @@
 #   tools/gpu.sh STEP [STEP ...]
 #
 # A step is NAME or NAME=ARGS; ARGS is one word, commas stand for spaces.
-#   tests[=ARGS]        pytest -m gpu (ARGS: more pytest args, e.g.
-#                       tests/test_frame_repair.py,-k,garbage)
+#   tests[=ARGS]        pytest -m gpu over tests/ (ARGS: what to run
+#                       instead, e.g. tests/test_frame_repair.py,-k,garbage)
 #   cpu                 pytest -m "not gpu"
 #   smoke               __graft_entry__.smoke()
 #   bench[=ARGS]        bench.py ARGS (default: the driver's config)
@@ -40,8 +40,8 @@ for step in "$@"; do
   log=$OUT/${n}_$name.log
   case $name in
     tests)
-      run 900 $log python -u -m pytest tests -x -q -m gpu --timeout 120 \
-        --timeout-method thread $args ;;
+      run 900 $log python -u -m pytest ${args:-tests} -x -q -m gpu \
+        --timeout 120 --timeout-method thread ;;
     cpu)
       run 600 $log python -m pytest tests -x -q -m "not gpu" $args ;;
     smoke)

@@ -755,6 +755,9 @@ def run_rank(a):
               'remote_requests': st['remote_reqs'],
               'overflow_segments': st['overflow_segments'],
               'xgmi_lower_bound_ms': st['xgmi_lower_bound_ms'],
+              'copy_bytes_per_step_max': st['copy_bytes_per_step_max'],
+              'local_bytes_through_collective':
+                  st['local_bytes_through_collective'],
               'slot_bytes': {'request': st['req_slot_bytes'],
                              'reply': st['rep_slot_bytes']}}
     replica = None

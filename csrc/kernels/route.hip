@@ -112,6 +112,20 @@ __global__ __launch_bounds__(RT_T) void route_counts_k(
 constexpr int SG_T = 256;
 constexpr int64_t SEG_HDR = 16;
 
+// Where the slot for / from rank w sits.  Without a separate self slot:
+// w * slot_cap in `base`.  With one (`self_slot`, the all-to-all skips the
+// local segment): the collective buffer holds the other ranks' slots in
+// rank order with a 16-byte stub for this rank (all_to_all_single needs one
+// chunk per rank; 16 bytes, not a slot, cross the collective), and the
+// local segment lives in self_slot — no copy of it through the collective.
+ZK_DEV uint8_t* slot_at(uint8_t* base, uint8_t* self_slot, int32_t w,
+                        int32_t self, int64_t slot_cap) {
+  if (self_slot == nullptr) return base + (int64_t)w * slot_cap;
+  if (w == self) return self_slot;
+  if (w < self) return base + (int64_t)w * slot_cap;
+  return base + (int64_t)(w - 1) * slot_cap + SEG_HDR;
+}
+
 // Copy n bytes s -> d with the nt threads of a team (this thread is t):
 // 16-byte stores aligned on the destination, 16-byte loads at any address
 // (gfx950 unaligned mode); the ragged head and tail go byte by byte, so a
@@ -140,7 +154,7 @@ __global__ __launch_bounds__(SG_T) void seg_pack_k(
     int64_t nrec_cap, const int64_t* __restrict__ total,
     const int64_t* __restrict__ counts, int32_t world, int32_t self,
     int64_t slot_cap, uint8_t* __restrict__ out,
-    unsigned long long* __restrict__ stats) {
+    unsigned long long* __restrict__ stats, uint8_t* __restrict__ self_out) {
   const int32_t w = blockIdx.y;
   int64_t f = 0;
   for (int32_t k = 0; k < w; ++k) f += counts[k];
@@ -153,7 +167,7 @@ __global__ __launch_bounds__(SG_T) void seg_pack_k(
   const int64_t bytes = e0 - s0;
   const bool ok = c >= 0 && f >= 0 && f + c <= nrec && s0 >= 0 &&
                   bytes >= 0 && e0 <= src_cap && bytes <= slot_cap - SEG_HDR;
-  uint8_t* slot = out + (int64_t)w * slot_cap;
+  uint8_t* slot = slot_at(out, self_out, w, self, slot_cap);
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     const int64_t h[2] = {ok ? bytes : 0, ok ? c : 0};
     __builtin_memcpy(slot, h, 16);
@@ -169,10 +183,10 @@ __global__ __launch_bounds__(SG_T) void seg_pack_k(
             (int64_t)gridDim.x * SG_T);
 }
 
-ZK_DEV void seg_hdr(const uint8_t* in, int32_t k, int64_t slot_cap,
-                    int64_t* bytes, int64_t* recs) {
+ZK_DEV void seg_hdr(const uint8_t* slot, int64_t slot_cap, int64_t* bytes,
+                    int64_t* recs) {
   int64_t h[2];
-  __builtin_memcpy(h, in + (int64_t)k * slot_cap, 16);
+  __builtin_memcpy(h, slot, 16);
   *bytes = h[0] < 0 ? 0 : (h[0] > slot_cap - SEG_HDR ? slot_cap - SEG_HDR
                                                       : h[0]);
   *recs = h[1] < 0 ? 0 : h[1];
@@ -182,12 +196,17 @@ __global__ __launch_bounds__(SG_T) void seg_unpack_k(
     const uint8_t* __restrict__ in, int32_t world, int32_t self,
     int64_t slot_cap, uint8_t* __restrict__ out,
     int64_t* __restrict__ total_out, int64_t* __restrict__ counts_out,
-    unsigned long long* __restrict__ stats) {
+    unsigned long long* __restrict__ stats,
+    const uint8_t* __restrict__ self_in) {
   const int32_t w = blockIdx.y;
+  auto slot = [&](int32_t k) {
+    return (const uint8_t*)slot_at((uint8_t*)in, (uint8_t*)self_in, k, self,
+                                   slot_cap);
+  };
   int64_t pre = 0, mine = 0, all = 0, peers = 0;
   for (int32_t k = 0; k < world; ++k) {
     int64_t b, r;
-    seg_hdr(in, k, slot_cap, &b, &r);
+    seg_hdr(slot(k), slot_cap, &b, &r);
     if (k < w) pre += b;
     if (k == w) mine = b;
     if (k != self) peers += b;
@@ -200,11 +219,11 @@ __global__ __launch_bounds__(SG_T) void seg_unpack_k(
     }
     if (threadIdx.x < world) {
       int64_t b, r;
-      seg_hdr(in, threadIdx.x, slot_cap, &b, &r);
+      seg_hdr(slot(threadIdx.x), slot_cap, &b, &r);
       counts_out[threadIdx.x] = r;
     }
   }
-  team_copy(out + pre, in + (int64_t)w * slot_cap + SEG_HDR, mine,
+  team_copy(out + pre, slot(w) + SEG_HDR, mine,
             (int64_t)blockIdx.x * SG_T + threadIdx.x,
             (int64_t)gridDim.x * SG_T);
 }
@@ -266,17 +285,19 @@ static unsigned seg_blocks(int64_t slot_cap) {
 // nrec_cap) of them, *total bytes) into `world` slots of slot_cap bytes:
 // slot w gets records [sum(counts[:w]), +counts[w]).  stats (uint64 [3]):
 // += segments that did not fit, payload bytes and records for peers.
+// self_out (may be null): this rank's own slot, apart from `out` (see
+// slot_at; `out` then holds (world - 1) slots + a 16-byte stub).
 int zk_seg_pack(const uint8_t* src, int64_t src_cap, const int64_t* rec_off,
                 const int64_t* nrec_dev, int64_t nrec_cap,
                 const int64_t* total, const int64_t* counts, int32_t world,
                 int32_t self, int64_t slot_cap, uint8_t* out,
-                unsigned long long* stats, hipStream_t st) {
+                unsigned long long* stats, uint8_t* self_out, hipStream_t st) {
   if (world < 1 || world > zk::RT_MAXW || slot_cap < 32 || (slot_cap & 15))
     return (int)hipErrorInvalidValue;
   dim3 grid(seg_blocks(slot_cap), (unsigned)world);
   zk::seg_pack_k<<<grid, zk::SG_T, 0, st>>>(
       src, src_cap, rec_off, nrec_dev, nrec_cap, total, counts, world, self,
-      slot_cap, out, stats);
+      slot_cap, out, stats, self_out);
   ZK_LAUNCH_CHECK();
   return 0;
 }
@@ -285,15 +306,17 @@ int zk_seg_pack(const uint8_t* src, int64_t src_cap, const int64_t* rec_off,
 // order); *total_out = its length, counts_out[w] = records from rank w,
 // stats[0] (optional) += payload bytes from the other ranks.  out must hold
 // world * (slot_cap - 16) bytes.
+// self_in (may be null): this rank's own slot, apart from `in` (slot_at).
 int zk_seg_unpack(const uint8_t* in, int32_t world, int32_t self,
                   int64_t slot_cap, uint8_t* out, int64_t* total_out,
                   int64_t* counts_out, unsigned long long* stats,
-                  hipStream_t st) {
+                  const uint8_t* self_in, hipStream_t st) {
   if (world < 1 || world > zk::RT_MAXW || slot_cap < 32 || (slot_cap & 15))
     return (int)hipErrorInvalidValue;
   dim3 grid(seg_blocks(slot_cap), (unsigned)world);
   zk::seg_unpack_k<<<grid, zk::SG_T, 0, st>>>(in, world, self, slot_cap, out,
-                                               total_out, counts_out, stats);
+                                               total_out, counts_out, stats,
+                                               self_in);
   ZK_LAUNCH_CHECK();
   return 0;
 }

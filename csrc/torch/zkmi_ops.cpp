@@ -804,7 +804,7 @@ void seg_pack(const Tensor& src, const Tensor& rec_off,
               const c10::optional<Tensor>& nrec, int64_t nrec_cap,
               const Tensor& total, const Tensor& counts, int64_t world,
               int64_t self, int64_t slot_cap, const Tensor& out,
-              const Tensor& stats) {
+              const Tensor& stats, const c10::optional<Tensor>& self_out) {
   TORCH_CHECK(world >= 1 && world <= 64, "zkmi: seg_pack world 1..64");
   TORCH_CHECK(self >= 0 && self < world, "zkmi: seg_pack self rank");
   TORCH_CHECK(slot_cap >= 32 && slot_cap % 16 == 0,
@@ -818,28 +818,35 @@ void seg_pack(const Tensor& src, const Tensor& rec_off,
                      P<int64_t>(total, I64, 1, "total", r),
                      P<int64_t>(counts, I64, world, "counts", r),
                      (int32_t)world, (int32_t)self, slot_cap,
-                     P<uint8_t>(out, U8, world * slot_cap, "out", r),
+                     P<uint8_t>(out, U8,
+                                self_out ? (world - 1) * slot_cap + 16
+                                         : world * slot_cap, "out", r),
                      reinterpret_cast<unsigned long long*>(
                          P<int64_t>(stats, I64, 3, "stats", r)),
+                     Popt<uint8_t>(self_out, U8, slot_cap, "self_out", r),
                      cur_stream()),
          "seg_pack");
 }
 
 void seg_unpack(const Tensor& inp, int64_t world, int64_t self,
                 int64_t slot_cap, const Tensor& out, const Tensor& total,
-                const Tensor& counts, const c10::optional<Tensor>& stats) {
+                const Tensor& counts, const c10::optional<Tensor>& stats,
+                const c10::optional<Tensor>& self_in) {
   TORCH_CHECK(world >= 1 && world <= 64, "zkmi: seg_unpack world 1..64");
   TORCH_CHECK(self >= 0 && self < world, "zkmi: seg_unpack self rank");
   TORCH_CHECK(slot_cap >= 32 && slot_cap % 16 == 0,
               "zkmi: seg_unpack slot_cap must be a multiple of 16, >= 32");
   const Tensor* r = &inp;
-  hip_ok(zk_seg_unpack(P<uint8_t>(inp, U8, world * slot_cap, "in"),
+  hip_ok(zk_seg_unpack(P<uint8_t>(inp, U8,
+                                 self_in ? (world - 1) * slot_cap + 16
+                                         : world * slot_cap, "in"),
                        (int32_t)world, (int32_t)self, slot_cap,
                        P<uint8_t>(out, U8, world * (slot_cap - 16), "out", r),
                        P<int64_t>(total, I64, 1, "total", r),
                        P<int64_t>(counts, I64, world, "counts", r),
                        reinterpret_cast<unsigned long long*>(
                            Popt<int64_t>(stats, I64, 1, "stats", r)),
+                       Popt<uint8_t>(self_in, U8, slot_cap, "self_in", r),
                        cur_stream()),
          "seg_unpack");
 }
@@ -983,10 +990,11 @@ TORCH_LIBRARY(zkmi, m) {
         &route_requests);
   m.def("seg_pack(Tensor src, Tensor rec_off, Tensor? nrec, int nrec_cap, "
         "Tensor total, Tensor counts, int world, int self, int slot_cap, "
-        "Tensor(a!) out, Tensor(b!) stats) -> ()", &seg_pack);
+        "Tensor(a!) out, Tensor(b!) stats, Tensor(c!)? self_out=None) -> ()",
+        &seg_pack);
   m.def("seg_unpack(Tensor inp, int world, int self, int slot_cap, "
         "Tensor(a!) out, Tensor(b!) total, Tensor(c!) counts, "
-        "Tensor(d!)? stats=None) -> ()", &seg_unpack);
+        "Tensor(d!)? stats=None, Tensor? self_in=None) -> ()", &seg_unpack);
   m.def("session_connect(Tensor buf, Tensor frame_off, Tensor frame_len, "
         "Tensor count, int ncap, Tensor(a!)[] table, int server_id, "
         "int secret, int min_to, int max_to, Tensor zxid_now, Tensor(b!) out, "

@@ -98,6 +98,35 @@ def test_seg_pack_unpack_roundtrip(gpu):
     assert back[:len(want)].cpu().numpy().tobytes() == want
     assert rc.cpu().tolist() == counts[:4] + [0]
     assert rs.item() == len(want) - len(segs[1])
+    # the local segment in a slot of its own (the all-to-all carries the
+    # peers' slots and a 16-byte stub for this rank): same segments, same
+    # concatenation
+    me = 2
+    coll = torch.full(((W - 1) * slot + 16,), 0xEE, dtype=torch.uint8,
+                      device=dev)
+    own = torch.full((slot,), 0xEE, dtype=torch.uint8, device=dev)
+    st2 = torch.zeros(3, dtype=torch.int64, device=dev)
+    L.seg_pack(src, ro, None, len(sizes), total, cnt, W, me, slot, coll, st2,
+               own)
+    cb, ob2 = coll.cpu().numpy().tobytes(), own.cpu().numpy().tobytes()
+
+    def at(w):
+        if w == me:
+            return ob2[:slot]
+        p0 = w * slot if w < me else (w - 1) * slot + 16
+        return cb[p0:p0 + slot]
+    for w in range(W):
+        hb, hr = np.frombuffer(at(w)[:16], np.int64)
+        if w == 4:
+            assert (hb, hr) == (0, 0)
+        else:
+            assert (hb, hr) == (len(segs[w]), counts[w])
+            assert at(w)[16:16 + hb] == segs[w]
+    assert st2.cpu().tolist() == st.cpu().tolist()
+    back2 = torch.zeros(W * (slot - 16) + 64, dtype=torch.uint8, device=dev)
+    L.seg_unpack(coll, W, me, slot, back2, tot, rc, None, own)
+    assert tot.item() == len(want)
+    assert back2[:len(want)].cpu().numpy().tobytes() == want
 
 
 def test_sharded_get_one_rank(gpu):

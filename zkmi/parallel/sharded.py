@@ -11,8 +11,10 @@ on rank ``r`` is, per pipelined connection:
           split by owner; K10 encode -> one byte segment per owner;
           ``seg_pack`` cuts the stream into one fixed-capacity slot per
           owner ({bytes, records} header + payload)
-  R2      ``all_to_all_single`` of the slots with EQUAL splits (RCCL over
-          xGMI with ``nccl``): no size exchange, no host split list
+  R2      ``all_to_all_single`` of the slots (RCCL over xGMI with
+          ``nccl``): fixed splits, no size exchange; the local segment
+          stays in a slot of its own and crosses no collective (a 16-byte
+          stub stands in for it)
   server  ``seg_unpack`` concatenates the received payloads (source rank
           order) with their device length; K1 + K12 over that stream,
           lookup in my shard, K13 encode; ``seg_pack`` cuts the reply
@@ -138,21 +140,29 @@ class ShardedGetPipeline(object):
 
     # -- collectives ----------------------------------------------------------
 
-    def a2a(self, out, inp):
-        """Equal-split ``all_to_all_single`` on the collective device
+    def splits(self, slot):
+        """The all-to-all's split sizes: a slot per peer, the 16-byte stub
+        for this rank (its segment stays local, see route.hip slot_at)."""
+        return [SEG_HDR if w == self.rank else slot
+                for w in range(self.world)]
+
+    def a2a(self, out, inp, slot):
+        """``all_to_all_single`` of the slots on the collective device
         (device tensors with RCCL; host staging for a gloo rehearsal)."""
+        sp = self.splits(slot)
         if self.coll == self.dev:
             if self.comm is None:
-                dist.all_to_all_single(out, inp, group=self.group)
+                dist.all_to_all_single(out, inp, sp, sp, group=self.group)
                 return out
             cur = torch.cuda.current_stream(self.dev)
             self.comm.wait_stream(cur)
             with torch.cuda.stream(self.comm):
-                dist.all_to_all_single(out, inp, group=self.group)
+                dist.all_to_all_single(out, inp, sp, sp, group=self.group)
             cur.wait_stream(self.comm)
             return out
         o = torch.empty(out.shape, dtype=out.dtype, device=self.coll)
-        dist.all_to_all_single(o, inp.to(self.coll), group=self.group)
+        dist.all_to_all_single(o, inp.to(self.coll), sp, sp,
+                               group=self.group)
         out.copy_(o)
         return out
 
@@ -231,13 +241,20 @@ class ShardedGetPipeline(object):
         W = self.world
         wire = sum((W - 1) * (c.req_slot + c.rep_slot) for c in self.subs) \
             * self.steps if W > 1 else 0
+        # bytes the step's kernels copy per connection: the segments into
+        # the slots (seg_pack) and out of them (seg_unpack), requests and
+        # replies; the all-to-all moves the peers' slots only
+        copied = sum(2 * (c.n * c.req_max + c.n * c.rep_max)
+                     for c in self.subs)
         slots = [b for c in self.subs for b in (c.req_slot, c.rep_slot)]
         return {'bytes_sent': rq[1] + rp[1], 'bytes_recv': rv[0],
                 'remote_reqs': rq[2], 'overflow_segments': rq[0] + rp[0],
                 'wire_bytes_sent': wire, 'steps': self.steps,
                 'req_slot_bytes': [c.req_slot for c in self.subs],
                 'rep_slot_bytes': [c.rep_slot for c in self.subs],
-                'xgmi_lower_bound_ms': xgmi_lower_bound_ms(slots, W)}
+                'xgmi_lower_bound_ms': xgmi_lower_bound_ms(slots, W),
+                'copy_bytes_per_step_max': copied,
+                'local_bytes_through_collective': 2 * SEG_HDR * len(self.subs)}
 
 
 class _Conn(object):
@@ -298,8 +315,13 @@ class _Conn(object):
         self.reply = B.alloc_replies(n, dev)
         if pipe.route:
             u8 = lambda m: torch.empty(m, dtype=U8, device=dev)  # noqa: E731
-            self.sq, self.rq = u8(W * self.req_slot), u8(W * self.req_slot)
-            self.sp, self.rp = u8(W * self.rep_slot), u8(W * self.rep_slot)
+            # the collective buffers: the peers' slots + this rank's stub;
+            # this rank's own slots apart
+            cq = (W - 1) * self.req_slot + SEG_HDR
+            cp = (W - 1) * self.rep_slot + SEG_HDR
+            self.sq, self.rq = u8(cq), u8(cq)
+            self.sp, self.rp = u8(cp), u8(cp)
+            self.sq_self, self.sp_self = u8(self.req_slot), u8(self.rep_slot)
             self.rxq = u8(W * (self.req_slot - SEG_HDR) + 64)
             self.crx = u8(W * (self.rep_slot - SEG_HDR) + 64)
             self.nrx = torch.zeros(1, dtype=I64, device=dev)
@@ -347,14 +369,14 @@ class _Conn(object):
         tx, rec_off, total, _ = B.encode_requests(rb, self.xt, out=self.tx)
         if p.route:
             L.seg_pack(tx, rec_off, None, n, total, self.counts, W, p.rank,
-                       self.req_slot, self.sq, p.req_stats)
+                       self.req_slot, self.sq, p.req_stats, self.sq_self)
         yield
         if p.route:
-            p.a2a(self.rq, self.sq)
+            p.a2a(self.rq, self.sq, self.req_slot)
         yield
         if p.route:
             L.seg_unpack(self.rq, W, p.rank, self.req_slot, self.rxq,
-                         self.nrx, self.src_counts, None)
+                         self.nrx, self.src_counts, None, self.sq_self)
             rxq, nrx = self.rxq, self.nrx
         else:
             rxq, nrx = tx, total
@@ -369,14 +391,16 @@ class _Conn(object):
             # counts came with the request slots' headers
             L.seg_pack(rout, self.server.last_rec_off, ft.count,
                        self.server.cap_frames, rtotal, self.src_counts, W,
-                       p.rank, self.rep_slot, self.sp, p.rep_stats)
+                       p.rank, self.rep_slot, self.sp, p.rep_stats,
+                       self.sp_self)
         yield
         if p.route:
-            p.a2a(self.rp, self.sp)
+            p.a2a(self.rp, self.sp, self.rep_slot)
         yield
         if p.route:
             L.seg_unpack(self.rp, W, p.rank, self.rep_slot, self.crx,
-                         self.ncrx, self.back_counts, p.recv_stats)
+                         self.ncrx, self.back_counts, p.recv_stats,
+                         self.sp_self)
             crx, ncrx = self.crx, self.ncrx
         else:
             crx, ncrx = rout, rtotal

@@ -87,6 +87,7 @@ constexpr int FL_U = 8;                    // fs_link loads per batch
 constexpr int FL_NB = 2;                   // broken links the check saw
 constexpr int FL_GW = FL_NB + 1;
 constexpr int FL_LOC = 1024;               // a block's own broken links
+constexpr int FL_BROUNDS = 8;             // the last block's repair rounds
 constexpr int FL_LOCAL_MIN = 64;           // ... walked by the block when
                                            // it found more than this many
 // Count blocks: frame counts scanned per FK_T tiles (one wave's worth)
@@ -2497,45 +2498,57 @@ __global__ __launch_bounds__(FL_T) void fs_link(
   const bool clk = ldbg != nullptr && tid == 0;
   int64_t from = 1, ft = INF;
   int64_t nb = (int64_t)nb0;
-  if (rew) {
-    // the blocks' round changed records: the links still broken listed
-    // again (blist, in tile order); none before the first terminal: only
-    // the counts are scanned again
-    int64_t fbv, ftv;
-    nb = fl_list_broken(ntiles, rec_entry, rec_exit, rec_meta, blist, red,
-                        fbv, ftv);
-    if (fbv == INF || fbv > ftv) {
-      fl_count_scan(n, ntiles, ftv, rec_exit, rec_meta, base, bsum, cap,
-                    result, lastk, red);
-      return;
-    }
-    from = fbv;
-  }
-  if (nb <= (int64_t)FL_SMALL && (ntiles + FK_T - 1) / FK_T <= FL_DB) {
-    // ---- a handful of broken links: chases, then every link checked -----
-    if (clk) ldbg[0] = wall_clock64();
-    const bool settled = fl_chase(buf, n, ntiles, maxp, sx, list, rcount, pre,
-                                  rec_entry, rec_exit, rec_meta, lbw, cx, blist,
-                                  (int)nb, win, stats, ch);
-    if (clk) ldbg[1] = ldbg[2] = wall_clock64();
-    // a chase only vouches for the links it saw
-    int64_t fbv, ftv;
-    fl_links(1, ntiles, rec_entry, rec_exit, rec_meta, red, fbv, ftv);
-    if (clk) ldbg[3] = wall_clock64();
-    if (settled && (fbv == INF || fbv > ftv)) {
-      if (rew) {
-        // (tiles the blocks re-walked are not in the chases' dirty set)
+  // repair rounds of this block: a handful of broken links are chased (the
+  // usual repair: one pass, then only the count blocks it touched are
+  // re-counted); many are re-walked in parallel, one wave a link (the
+  // blocks' round continued here); after each, the links still broken are
+  // listed again.  What the rounds leave goes to the tail.
+  bool changed = rew != 0;       // records changed beyond the chases' dirty
+  for (int round = 0; round < FL_BROUNDS; ++round) {
+    if (changed) {
+      int64_t fbv, ftv;
+      nb = fl_list_broken(ntiles, rec_entry, rec_exit, rec_meta, blist, red,
+                          fbv, ftv);
+      if (fbv == INF || fbv > ftv) {
         fl_count_scan(n, ntiles, ftv, rec_exit, rec_meta, base, bsum, cap,
                       result, lastk, red);
         return;
       }
-      fl_chase_recount(ntiles, rec_meta, base, bsum, ch);
-      fl_bases(n, ntiles, ftv, rec_exit, rec_meta, base, bsum, cap, result,
-               lastk, red);
-      if (clk) ldbg[4] = wall_clock64();
-      return;
     }
-    from = 1;
+    if (nb <= (int64_t)FL_SMALL && (ntiles + FK_T - 1) / FK_T <= FL_DB) {
+      // ---- a handful of broken links: chases, then every link checked ---
+      if (clk && round == 0) ldbg[0] = wall_clock64();
+      const bool settled = fl_chase(buf, n, ntiles, maxp, sx, list, rcount,
+                                    pre, rec_entry, rec_exit, rec_meta, lbw,
+                                    cx, blist, (int)nb, win, stats, ch);
+      if (clk && round == 0) ldbg[1] = ldbg[2] = wall_clock64();
+      // a chase only vouches for the links it saw
+      int64_t fbv, ftv;
+      fl_links(1, ntiles, rec_entry, rec_exit, rec_meta, red, fbv, ftv);
+      if (clk && round == 0) ldbg[3] = wall_clock64();
+      if (settled && (fbv == INF || fbv > ftv)) {
+        if (changed) {
+          // (tiles re-walked in rounds are not in the chases' dirty set)
+          fl_count_scan(n, ntiles, ftv, rec_exit, rec_meta, base, bsum, cap,
+                        result, lastk, red);
+          return;
+        }
+        fl_chase_recount(ntiles, rec_meta, base, bsum, ch);
+        fl_bases(n, ntiles, ftv, rec_exit, rec_meta, base, bsum, cap, result,
+                 lastk, red);
+        if (clk) ldbg[4] = wall_clock64();
+        return;
+      }
+      if (!settled) break;              // the lists outgrew LDS: the tail
+    } else {
+      const uint32_t w = fl_local_round(buf, n, ntiles, maxp, sx, list,
+                                        rcount, pre, rec_entry, rec_exit,
+                                        rec_meta, blist, (int)nb, win);
+      if (lane == 0 && w) fc_stat(stats, 2, w);
+      if (tid == 0) fc_stat(stats, 3, 1);
+      __syncthreads();
+    }
+    changed = true;
   }
   // ---- the tail: exact chases from the leftmost broken link, until every
   // live link holds; then the count scan ------------------------------------

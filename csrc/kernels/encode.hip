@@ -10,6 +10,8 @@
 // replies are not self-describing, zk-buffer.js:288-291).
 #include "zk_common.h"
 
+#include <stdlib.h>
+
 
 namespace zk {
 
@@ -185,7 +187,14 @@ __global__ __launch_bounds__(ENC_T) void resp_sizes(ZkRespBatch r,
 // bits 0-1 too (conflict-free at 48 dwords; 2-3 way for odd record sizes),
 // so the read-out assembles each 16-byte vector from four dword reads
 // (~2.4-way on those reads, against 4-way on every record write before).
-ZK_DEV int64_t swz(int64_t w) { return w ^ ((w >> 4) & 31); }
+// SW = 1: the rounds 1-4 swizzle (bits 2-5 XOR the 64-dword row: 4-dword
+// groups stay whole, the read-out moves 16-byte vectors; 4-way on the
+// record writes), kept for A/B (ZKMI_ENC_SWZ=1).
+template <int SW>
+ZK_DEV int64_t swz(int64_t w) {
+  if (SW == 1) return w ^ (((w >> 6) & 15) << 2);
+  return w ^ ((w >> 4) & 31);
+}
 struct GSink {
   uint8_t* o;
   ZK_DEV void be32(int32_t v) { st_be32(o, v); o += 4; }
@@ -196,6 +205,7 @@ struct GSink {
   ZK_DEV void finish() {}
 };
 
+template <int SW>
 struct LSink {
   uint32_t* w;
   int64_t widx;
@@ -206,8 +216,8 @@ struct LSink {
                                              nb((int)(rel & 3)), first(true) {}
   ZK_DEV void flush() {
     const uint32_t v = (uint32_t)acc;
-    if (first) { atomicOr(&w[swz(widx)], v); first = false; }
-    else w[swz(widx)] = v;
+    if (first) { atomicOr(&w[swz<SW>(widx)], v); first = false; }
+    else w[swz<SW>(widx)] = v;
     ++widx;
     acc >>= 32;
     nb -= 4;
@@ -251,7 +261,7 @@ struct LSink {
     for (; i < n; ++i) u8(s[i]);
   }
   ZK_DEV void finish() {
-    if (nb > 0) atomicOr(&w[swz(widx)], (uint32_t)acc);
+    if (nb > 0) atomicOr(&w[swz<SW>(widx)], (uint32_t)acc);
   }
 };
 
@@ -438,22 +448,26 @@ ZK_DEV int64_t block_base(const int64_t* __restrict__ bbase,
   return base;
 }
 
+template <int SW>
 ZK_DEV uint8_t lds_byte(const uint32_t* lw, int64_t b) {
-  return ((const uint8_t*)(lw + swz(b >> 2)))[b & 3];
+  return ((const uint8_t*)(lw + swz<SW>(b >> 2)))[b & 3];
 }
 
 // 16 image bytes at image byte y (16-aligned): four dword reads (the
 // swizzle scatters a 4-dword group over banks), one 16-byte vector.
+template <int SW>
 ZK_DEV uint4 lds_vec(const uint32_t* lw, int64_t y) {
   const int64_t w = y >> 2;
-  return make_uint4(lw[swz(w)], lw[swz(w + 1)], lw[swz(w + 2)],
-                    lw[swz(w + 3)]);
+  if (SW == 1) return *(const uint4*)(lw + swz<SW>(w));
+  return make_uint4(lw[swz<SW>(w)], lw[swz<SW>(w + 1)], lw[swz<SW>(w + 2)],
+                    lw[swz<SW>(w + 3)]);
 }
 
 // Stream the block's LDS image [B0, B1) (image base a0 = B0 & ~15) out to
 // global memory: the 16-byte aligned interior with dwordx4 stores (a dword
 // a lane — four times the store instructions — cost the GET step 4 %), the
 // <= 15 head / tail bytes with byte stores (they abut other blocks' spans).
+template <int SW>
 ZK_DEV void stage_out(const uint32_t* lw, int64_t a0, int64_t B0, int64_t B1,
                       uint8_t* __restrict__ out) {
   const int64_t c0 = (B0 + 15) & ~(int64_t)15;
@@ -461,18 +475,18 @@ ZK_DEV void stage_out(const uint32_t* lw, int64_t a0, int64_t B0, int64_t B1,
   if (c0 < c1) {
     for (int64_t x = c0 + (int64_t)threadIdx.x * 16; x < c1;
          x += (int64_t)blockDim.x * 16)
-      *(uint4*)(out + x) = lds_vec(lw, x - a0);
+      *(uint4*)(out + x) = lds_vec<SW>(lw, x - a0);
     const int64_t hb = c0 - B0, tb = B1 - c1;
     if ((int64_t)threadIdx.x < hb) {
       const int64_t x = B0 + threadIdx.x;
-      out[x] = lds_byte(lw, x - a0);
+      out[x] = lds_byte<SW>(lw, x - a0);
     } else if ((int64_t)threadIdx.x >= 16 && (int64_t)threadIdx.x < 16 + tb) {
       const int64_t x = c1 + threadIdx.x - 16;
-      out[x] = lds_byte(lw, x - a0);
+      out[x] = lds_byte<SW>(lw, x - a0);
     }
   } else {
     for (int64_t x = B0 + threadIdx.x; x < B1; x += blockDim.x)
-      out[x] = lds_byte(lw, x - a0);
+      out[x] = lds_byte<SW>(lw, x - a0);
   }
 }
 
@@ -482,7 +496,7 @@ ZK_DEV void stage_out(const uint32_t* lw, int64_t a0, int64_t B0, int64_t B1,
 // run, counted with one barrier); a single record larger than the image is
 // written straight to global memory.  off / sizes are the block's EncLocal
 // tables (index i - r0).
-template <class F>
+template <int SW, class F>
 ZK_DEV void staged_emit(int64_t r0, int64_t r1, const int64_t* off,
                         const int64_t* sizes, uint8_t* __restrict__ out,
                         uint32_t* lw, F emit, int64_t stage = STAGE_BYTES) {
@@ -509,11 +523,11 @@ ZK_DEV void staged_emit(int64_t r0, int64_t r1, const int64_t* off,
       ((uint4*)lw)[x] = make_uint4(0, 0, 0, 0);
     __syncthreads();
     if (i < re) {
-      LSink l(lw, off[i - r0] - a0);
+      LSink<SW> l(lw, off[i - r0] - a0);
       emit(l, i);
     }
     __syncthreads();
-    stage_out(lw, a0, B0, B1, out);
+    stage_out<SW>(lw, a0, B0, B1, out);
     __syncthreads();                             // image reused next run
     rs = re;
   }
@@ -557,6 +571,7 @@ ZK_DEV int64_t hole_h0(int64_t off) { return (off + 20 + 15) & ~(int64_t)15; }
 // in the block's list); image position y of segment k is out position
 // y + a0c + (hole bytes before it).  One thread per segment; the run's first
 // and last 16-byte chunks are shared with other runs / blocks (byte stores).
+template <int SW>
 ZK_DEV void stage_out_segs(const uint32_t* lw, int64_t a0c, int64_t B0,
                            int64_t B1, int64_t yend, int64_t hb0, int64_t K,
                            int64_t j0, const int64_t* off, const EncHoles& H,
@@ -580,7 +595,7 @@ ZK_DEV void stage_out_segs(const uint32_t* lw, int64_t a0c, int64_t B0,
     }
     for (int64_t y = y0 & ~(int64_t)15; y < y1; y += 16) {
       const int64_t x = y + a0c + d;
-      const uint4 v = lds_vec(lw, y);
+      const uint4 v = lds_vec<SW>(lw, y);
       if (x >= B0 && x + 16 <= B1) {
         *(uint4*)(out + x) = v;
       } else {
@@ -632,7 +647,7 @@ ZK_DEV void copy_hole_q(const uint8_t* __restrict__ src, uint8_t* dst,
 
 // staged_emit for replies with holes.  off / sizes: the block's EncLocal
 // tables; H: the holes (set up by resp_write).
-template <class F>
+template <int SW, class F>
 ZK_DEV void staged_emit_holes(int64_t r0, int64_t r1, const int64_t* off,
                               const int64_t* sizes, EncHoles& H,
                               uint8_t* __restrict__ out, uint32_t* lw, F emit,
@@ -668,7 +683,7 @@ ZK_DEV void staged_emit_holes(int64_t r0, int64_t r1, const int64_t* off,
       ((uint4*)lw)[x] = make_uint4(0, 0, 0, 0);
     __syncthreads();
     if (i < re) {
-      LSink l(lw, off[li] - (H.hb[li] >> 9) - a0c);
+      LSink<SW> l(lw, off[li] - (H.hb[li] >> 9) - a0c);
       const int64_t hl = H.hole[li];
       emit(l, i, hl ? hole_h0(off[li]) - (off[li] + 20) : 0, hl);
     }
@@ -676,9 +691,9 @@ ZK_DEV void staged_emit_holes(int64_t r0, int64_t r1, const int64_t* off,
     const int64_t j0 = H.hb[ls] & 511;
     const int64_t K = ((H.hb[le] & 511) + (H.hole[le] ? 1 : 0)) - j0;
     if (K == 0) {
-      stage_out(lw, B0 & ~(int64_t)15, B0, B1, out);
+      stage_out<SW>(lw, B0 & ~(int64_t)15, B0, B1, out);
     } else {
-      stage_out_segs(lw, a0c, B0, B1, yend, hb0, K, j0, off, H, out);
+      stage_out_segs<SW>(lw, a0c, B0, B1, yend, hb0, K, j0, off, H, out);
     }
     __syncthreads();                             // image reused next run
     rs = re;
@@ -688,6 +703,7 @@ ZK_DEV void staged_emit_holes(int64_t r0, int64_t r1, const int64_t* off,
 // bsum != null: fused (block_base); every block checks its own span
 // against cap, the last one writes *total and err (2: over capacity, the
 // stream is then incomplete).
+template <int SW>
 __global__ __launch_bounds__(ENC_T) void resp_write(
     ZkRespBatch r, ZkNodeStore s, const int64_t* __restrict__ n_dev,
     int64_t ncap, const int64_t* __restrict__ sizes,
@@ -732,7 +748,7 @@ __global__ __launch_bounds__(ENC_T) void resp_write(
     if (hole) H.bl[hb & 511] = (int16_t)threadIdx.x;
     __syncthreads();
   }
-  staged_emit_holes(r0, r1, E.off, E.sz, H, out, lw,
+  staged_emit_holes<SW>(r0, r1, E.off, E.sz, H, out, lw,
                     [&](auto& k, int64_t i, int64_t pre, int64_t hole) {
     emit_response(k, r, s, i, E.sz[i - r0] - 4, pre, hole);
   }, stage);
@@ -837,6 +853,7 @@ ZK_DEV void emit_request(K& k, const ZkReqBatch& b, int64_t i, int64_t body) {
 // the frame bytes as partial-line writes: WRITE_SIZE 254 MB for a 36 MB
 // GET_DATA stream).  Unknown opcodes were flagged by req_sizes and get
 // size 0 (nothing written).
+template <int SW>
 __global__ __launch_bounds__(ENC_T) void req_write(
     ZkReqBatch b, int64_t n, const int64_t* __restrict__ sizes,
     const int64_t* __restrict__ bbase, const int64_t* __restrict__ bsum,
@@ -863,7 +880,7 @@ __global__ __launch_bounds__(ENC_T) void req_write(
   // fused: each block's own span (the last block flags the batch)
   if (bsum != nullptr && base + bsum[blockIdx.x] > cap) return;
   block_offsets(r0, r1, sizes, base, rec_off, E);
-  staged_emit(r0, r1, E.off, E.sz, out, lw, [&](auto& k, int64_t i) {
+  staged_emit<SW>(r0, r1, E.off, E.sz, out, lw, [&](auto& k, int64_t i) {
     const int64_t sz = E.sz[i - r0];
     if (sz > 0) emit_request(k, b, i, sz - 4);
   });
@@ -906,6 +923,19 @@ static inline unsigned nblk(int64_t n) {
   return (unsigned)((n + ENC_T - 1) / ENC_T);
 }
 
+// A/B switches read once: ZKMI_ENC_SWZ=1 the rounds 1-4 image swizzle;
+// ZKMI_ENC_FUSED=0 the block sums scanned by a launch of their own.
+static int enc_swz() {
+  static int v = -1;
+  if (v < 0) { const char* e = getenv("ZKMI_ENC_SWZ"); v = e ? atoi(e) : 0; }
+  return v;
+}
+static bool enc_fused() {
+  static int v = -1;
+  if (v < 0) { const char* e = getenv("ZKMI_ENC_FUSED"); v = e ? atoi(e) : 1; }
+  return v != 0;
+}
+
 }  // namespace zk
 
 extern "C" {
@@ -928,14 +958,19 @@ int zk_encode_requests2(const ZkReqBatch* b, int64_t n, int64_t* sizes,
   int64_t* bbad = scan_ws + 2 * nb;
   zk::req_sizes<<<nb, zk::ENC_T, 0, st>>>(*b, n, sizes, bbad, bsum);
   ZK_LAUNCH_CHECK();
-  const bool fused = nb <= zk::FUSED_SCAN_BLOCKS;
+  const bool fused = nb <= zk::FUSED_SCAN_BLOCKS && zk::enc_fused();
   if (!fused) {
     int rc = zk_scan_small_i64(bsum, bbase, nb, total, st);
     if (rc) return rc;
   }
-  zk::req_write<<<nb, zk::ENC_T, zk::STAGE_BYTES, st>>>(
-      *b, n, sizes, bbase, fused ? bsum : nullptr, rec_off, total, out,
-      out_cap, xid_tab, xid_mask, err, terminate, bbad, (int64_t)nb);
+  if (zk::enc_swz() == 1)
+    zk::req_write<1><<<nb, zk::ENC_T, zk::STAGE_BYTES, st>>>(
+        *b, n, sizes, bbase, fused ? bsum : nullptr, rec_off, total, out,
+        out_cap, xid_tab, xid_mask, err, terminate, bbad, (int64_t)nb);
+  else
+    zk::req_write<0><<<nb, zk::ENC_T, zk::STAGE_BYTES, st>>>(
+        *b, n, sizes, bbase, fused ? bsum : nullptr, rec_off, total, out,
+        out_cap, xid_tab, xid_mask, err, terminate, bbad, (int64_t)nb);
   ZK_LAUNCH_CHECK();
   return 0;
 }
@@ -1008,7 +1043,7 @@ int zk_encode_responses2(const ZkRespBatch* r, const ZkNodeStore* s,
                                              bsum);
     ZK_LAUNCH_CHECK();
   }
-  const bool fused = nb <= zk::FUSED_SCAN_BLOCKS;
+  const bool fused = nb <= zk::FUSED_SCAN_BLOCKS && zk::enc_fused();
   if (!fused) {
     int rc = zk_scan_small_i64(bsum, bbase, nb, total, st);
     if (rc) return rc;
@@ -1016,9 +1051,14 @@ int zk_encode_responses2(const ZkRespBatch* r, const ZkNodeStore* s,
   // reply image per workgroup (a 56 KiB image gained 0.5 % on 0-1024 B
   // payloads and cost GET 2 %)
   const int64_t stage = zk::STAGE_BYTES;
-  zk::resp_write<<<nb, zk::ENC_T, (size_t)stage, st>>>(
-      *r, *s, n_dev, ncap, sizes, bbase, fused ? bsum : nullptr, rec_off,
-      total, out, out_cap, err, terminate, stage);
+  if (zk::enc_swz() == 1)
+    zk::resp_write<1><<<nb, zk::ENC_T, (size_t)stage, st>>>(
+        *r, *s, n_dev, ncap, sizes, bbase, fused ? bsum : nullptr, rec_off,
+        total, out, out_cap, err, terminate, stage);
+  else
+    zk::resp_write<0><<<nb, zk::ENC_T, (size_t)stage, st>>>(
+        *r, *s, n_dev, ncap, sizes, bbase, fused ? bsum : nullptr, rec_off,
+        total, out, out_cap, err, terminate, stage);
   ZK_LAUNCH_CHECK();
   return 0;
 }

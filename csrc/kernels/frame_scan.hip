@@ -1701,16 +1701,6 @@ ZK_DEV uint32_t fl_local_round(const uint8_t* __restrict__ buf, int64_t n,
     if (E < k * FT_S ||
         __builtin_amdgcn_readfirstlane(m_term(ld_agent(&rec_meta[k - 1]))))
       continue;                               // no usable entry yet
-    // A tile with a speculated entry of its own whose link is broken only
-    // because the tile before is (E suspect): the tile after a garbage
-    // entry, whose own entry is usually right.  It waits for the tile
-    // before to settle (walked from a garbage E it could only be refused by
-    // fl_accept, and a refused walk costs the tile its recorded entry).
-    // Tiles without an entry (-1) walk from whatever the tile before
-    // recorded: its survivor's exit, usually the true one.
-    if (k >= 2 && rfl64(ld_agent(&rec_entry[k])) >= 0 &&
-        rfl64(ld_agent(&rec_entry[k - 1])) != rfl64(ld_agent(&rec_exit[k - 2])))
-      continue;
     const int32_t m0 = __builtin_amdgcn_readfirstlane(rcount[k]);
     const FcWalk fw = fc_walk(buf, n, maxp, k * FT_S, E, list + k * FT_LMAX,
                               m0, sx[k], mywin, pre + k * FT_LMAX, lane);

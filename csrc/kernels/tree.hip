@@ -515,6 +515,10 @@ ZK_DEV int32_t do_create(const ZkTree& t, Lane& L, const uint8_t* data,
 // PARSE: the requests come as K1 frames (foff / flen) and each lane parses
 // its own in registers (zk_reqparse.h) instead of reading K12's SoA back —
 // one launch and a 30 MB write + read less per 512K-request batch.
+ZK_DEV void finish_body(const ZkTree& t, const int64_t* n_dev,
+                        int64_t bump_zxid, int32_t publish);
+ZK_DEV bool serve_last(unsigned* tickets);
+
 template <bool PARSE>
 __global__ __launch_bounds__(TR_T) void tree_serve_k(
     ZkTree t, const uint8_t* __restrict__ rx, ZkReqOut q,
@@ -527,7 +531,7 @@ __global__ __launch_bounds__(TR_T) void tree_serve_k(
     int64_t* __restrict__ r_bsum, int64_t session, int64_t now_ms,
     const uint8_t* __restrict__ rank, int32_t pass, int32_t last_pass,
     int64_t snap_base, int64_t snap_cap, int64_t* __restrict__ snap_top,
-    int32_t wslot, int64_t* __restrict__ fired) {
+    int32_t wslot, int64_t* __restrict__ fired, unsigned* tickets) {
   const uint32_t blk = xcd_remap(blockIdx.x, gridDim.x);
   const int64_t i = (int64_t)blk * TR_T + threadIdx.x;
   const bool in_batch = i < ncap && i < *n_dev;
@@ -785,6 +789,9 @@ __global__ __launch_bounds__(TR_T) void tree_serve_k(
     block_excl_scan(sz, sm, &tot);
     if (threadIdx.x == 0) r_bsum[blk] = tot;
   }
+  // the finish in the launch's last workgroup (no tree_finish_k launch)
+  if (tickets != nullptr && serve_last(tickets))
+    finish_body(t, n_dev, 0, 1);
   if (!live) return;
   r_op[i] = L.op;
   r_xid[i] = rq.xid;
@@ -1028,29 +1035,78 @@ constexpr int FIN_T = 1024;
 // cross-block sign-off — the grid version's atomic sign-off counter took
 // 15-60 us per launch on a read-only GET batch, and two streams finishing
 // at once could interleave on it.
+// The finish (see above) by the calling workgroup (blockDim.x threads):
+// tree_finish_k's launch, or the serve launch's last workgroup (serve_last).
+// The counters and parent shadows other workgroups updated are read with
+// agent-scope loads (this workgroup's L1 may hold older lines).
+ZK_DEV void finish_body(const ZkTree& t, const int64_t* n_dev,
+                        int64_t bump_zxid, int32_t publish) {
+  int64_t* c = t.counters;
+  const int64_t nd = __hip_atomic_load(&c[TC_DIRTY], __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+  for (int64_t k = threadIdx.x; k < nd; k += blockDim.x) {
+    const int64_t p = __hip_atomic_load(&t.dirty_list[k], __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_AGENT);
+    uint8_t* slot = t.store.slab + t.store.slot_off[p];
+    st_be32(slot + 36, __hip_atomic_load(&t.cver[p], __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT));
+    st_be32(slot + 56, __hip_atomic_load(&t.nchild[p], __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT));
+    st_be64(slot + 60, __hip_atomic_load(&t.pzxid[p], __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT));
+    t.dirty[p] = 0;
+  }
+  __syncthreads();                 // every thread has read TC_DIRTY
+  if (threadIdx.x != 0) return;
+  auto ld = [&](int k) {
+    return __hip_atomic_load(&c[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  if (publish) {
+    if (ld(TC_FREE_HEAD) > ld(TC_FREE_PUB)) c[TC_FREE_HEAD] = ld(TC_FREE_PUB);
+    c[TC_FREE_PUB] = ld(TC_FREE_TAIL);
+  }
+  c[TC_DIRTY] = 0;
+  c[TC_ZXID] = ld(TC_ZXID) + (n_dev != nullptr ? *n_dev : bump_zxid);
+}
+
 template <int NT = FIN_T>
 __global__ __launch_bounds__(NT) void tree_finish_k(ZkTree t,
                                                    const int64_t* n_dev,
                                                    int64_t bump_zxid,
                                                    int32_t publish) {
-  int64_t* c = t.counters;
-  const int64_t nd = c[TC_DIRTY];
-  for (int64_t k = threadIdx.x; k < nd; k += NT) {
-    const int64_t p = t.dirty_list[k];
-    uint8_t* slot = t.store.slab + t.store.slot_off[p];
-    st_be32(slot + 36, t.cver[p]);
-    st_be32(slot + 56, t.nchild[p]);
-    st_be64(slot + 60, t.pzxid[p]);
-    t.dirty[p] = 0;
+  finish_body(t, n_dev, bump_zxid, publish);
+}
+
+// Is this the serve launch's last workgroup to finish?  Tickets in groups
+// of 64 workgroups (tickets[1 + g]; the last of a group takes one of
+// tickets[0]), so no counter takes more than 64 atomics — one counter
+// for a whole grid (thousands of same-address atomics) took 15-60 us a
+// launch.  The counters are the caller's (one set per server: two
+// connections serving one tree at once keep apart) and are left zero.
+ZK_DEV bool serve_last(unsigned* tickets) {
+  __shared__ int s_last;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    const unsigned ng = (gridDim.x + 63) / 64;
+    const unsigned g = blockIdx.x / 64;
+    const unsigned gs = min(64u, gridDim.x - g * 64);
+    int last = 0;
+    if (atomicAdd(&tickets[1 + g], 1u) + 1 == gs) {
+      __hip_atomic_store(&tickets[1 + g], 0u, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+      __threadfence();
+      if (atomicAdd(&tickets[0], 1u) + 1 == ng) {
+        __hip_atomic_store(&tickets[0], 0u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        last = 1;
+      }
+    }
+    __threadfence();
+    s_last = last;
   }
-  __syncthreads();                 // every thread has read TC_DIRTY
-  if (threadIdx.x != 0) return;
-  if (publish) {
-    if (c[TC_FREE_HEAD] > c[TC_FREE_PUB]) c[TC_FREE_HEAD] = c[TC_FREE_PUB];
-    c[TC_FREE_PUB] = c[TC_FREE_TAIL];
-  }
-  c[TC_DIRTY] = 0;
-  c[TC_ZXID] += n_dev != nullptr ? *n_dev : bump_zxid;
+  __syncthreads();
+  return s_last != 0;
 }
 
 // Session expiry: remove every ephemeral node owned by `session`
@@ -1303,7 +1359,7 @@ int zk_tree_serve(const ZkTree* t, const uint8_t* rx, const ZkReqOut* q,
                             zk::TR_T, 0, st>>>(
       *t, rx, *q, nullptr, nullptr, n_dev, ncap, r_op, r_xid, r_err, r_node,
       r_zxid, r_path_off, r_path_len, r_slot, r_sizes, r_bsum, session,
-      now_ms, nullptr, 0, 1, 0, 0, nullptr, -1, nullptr);
+      now_ms, nullptr, 0, 1, 0, 0, nullptr, -1, nullptr, nullptr);
   ZK_LAUNCH_CHECK();
   // at most one dirty parent per request
   return finish_launch(t, ncap, n_dev, 0, st);
@@ -1311,9 +1367,17 @@ int zk_tree_serve(const ZkTree* t, const uint8_t* rx, const ZkReqOut* q,
 
 // zk_tree_serve straight from K1's frame table (foff / flen, *n_dev
 // frames): every lane parses its request in registers (no K12 pass).
+// tickets (may be null; zk_serve_tickets(ncap) zeroed uint32, kept per
+// server): the launch's last workgroup does the finish (serve_last), no
+// tree_finish_k launch.
 // wslot: this session's watcher slot (-1: its reads arm no watch); fired
 // (may be null; [ncap * 5]): per successful write, the watcher masks it
 // fired and the paths (zk_watch_events expands them).
+int64_t zk_serve_tickets(int64_t ncap) {
+  const int64_t nb = (ncap + zk::TR_T - 1) / zk::TR_T;
+  return 1 + (nb + 63) / 64;
+}
+
 int zk_tree_serve_frames(const ZkTree* t, const uint8_t* rx,
                          const int64_t* foff, const int32_t* flen,
                          const int64_t* n_dev, int64_t ncap, int32_t* r_op,
@@ -1322,7 +1386,7 @@ int zk_tree_serve_frames(const ZkTree* t, const uint8_t* rx,
                          int32_t* r_path_len, int64_t* r_slot,
                          int64_t* r_sizes, int64_t* r_bsum, int64_t session,
                          int64_t now_ms, int32_t wslot, int64_t* fired,
-                         hipStream_t st) {
+                         unsigned* tickets, hipStream_t st) {
   if (ncap <= 0) return 0;
   if ((r_sizes == nullptr) != (r_bsum == nullptr)) return -1;
   ZkReqOut none{};
@@ -1330,9 +1394,10 @@ int zk_tree_serve_frames(const ZkTree* t, const uint8_t* rx,
                            zk::TR_T, 0, st>>>(
       *t, rx, none, foff, flen, n_dev, ncap, r_op, r_xid, r_err, r_node,
       r_zxid, r_path_off, r_path_len, r_slot, r_sizes, r_bsum, session,
-      now_ms, nullptr, 0, 1, 0, 0, nullptr, wslot, fired);
+      now_ms, nullptr, 0, 1, 0, 0, nullptr, wslot, fired, tickets);
   ZK_LAUNCH_CHECK();
-  return finish_launch(t, ncap, n_dev, 0, st);
+  // tickets: the serve launch's last workgroup did the finish
+  return tickets != nullptr ? 0 : finish_launch(t, ncap, n_dev, 0, st);
 }
 
 // Ordering workspace layout for up to ncap requests: the zeroed prefix
@@ -1431,7 +1496,8 @@ int zk_tree_serve_ordered(const ZkTree* t, const uint8_t* rx, const ZkReqOut* q,
     zk::tree_serve_k<false><<<nb, zk::TR_T, 0, st>>>(
         *t, rx, *q, nullptr, nullptr, n_dev, ncap, r_op, r_xid, r_err, r_node, r_zxid,
         r_path_off, r_path_len, r_slot, r_sizes, r_bsum, session, now_ms,
-        rank, pass, last, snap_base, snap_cap, &w.ctr[2], wslot, fired);
+        rank, pass, last, snap_base, snap_cap, &w.ctr[2], wslot, fired,
+        nullptr);
     ZK_LAUNCH_CHECK();
     // nodes freed by a pass are recycled from the next batch on: a reply of
     // this batch may still name them

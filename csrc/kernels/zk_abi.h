@@ -197,11 +197,13 @@ int zk_tree_serve(const ZkTree*, const uint8_t*, const ZkReqOut*,
                   const int64_t*, int64_t, int32_t*, int32_t*, int32_t*,
                   int64_t*, int64_t*, int64_t*, int32_t*, int64_t*, int64_t*,
                   int64_t*, int64_t, int64_t, hipStream_t);
+int64_t zk_serve_tickets(int64_t);
 int zk_tree_serve_frames(const ZkTree*, const uint8_t*, const int64_t*,
                          const int32_t*, const int64_t*, int64_t, int32_t*,
                          int32_t*, int32_t*, int64_t*, int64_t*, int64_t*,
                          int32_t*, int64_t*, int64_t*, int64_t*, int64_t,
-                         int64_t, int32_t, int64_t*, hipStream_t);
+                         int64_t, int32_t, int64_t*, unsigned*,
+                         hipStream_t);
 int zk_tree_serve_ordered(const ZkTree*, const uint8_t*, const ZkReqOut*,
                           const int64_t*, int64_t, int32_t*, int32_t*,
                           int32_t*, int64_t*, int64_t*, int64_t*, int32_t*,

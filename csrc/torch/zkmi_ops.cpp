@@ -243,6 +243,7 @@ ZkSessionTable session_table(const std::vector<Tensor>& v, int64_t span) {
 // -- ops ---------------------------------------------------------------------
 
 int64_t scan_workspace(int64_t n) { return zk_scan_workspace(n); }
+int64_t serve_tickets(int64_t ncap) { return zk_serve_tickets(ncap); }
 int64_t scan_set_mode(int64_t m) { return zk_scan_set_mode((int)m); }
 
 void scan_excl(const Tensor& x, const Tensor& base, const Tensor& total,
@@ -562,7 +563,8 @@ void tree_serve_frames(const std::vector<Tensor>& t, const Tensor& rx,
                        const Tensor& n_dev, int64_t ncap,
                        const std::vector<Tensor>& r, int64_t session,
                        int64_t now_ms, int64_t wslot,
-                       const c10::optional<Tensor>& fired) {
+                       const c10::optional<Tensor>& fired,
+                       const c10::optional<Tensor>& tickets) {
   ZkTree s = tree(t);
   const Tensor* d = &t[0];
   need(r, 10, "serve outputs");
@@ -584,6 +586,8 @@ void tree_serve_frames(const std::vector<Tensor>& t, const Tensor& rx,
              P<int64_t>(r[8], I64, ncap, "r.sizes", d),
              P<int64_t>(r[9], I64, nb, "r.block_sums", d), session, now_ms,
              (int32_t)wslot, Popt<int64_t>(fired, I64, 5 * ncap, "fired", d),
+             reinterpret_cast<unsigned*>(Popt<int32_t>(
+                 tickets, I32, zk_serve_tickets(ncap), "tickets", d)),
              cur_stream()),
          "tree_serve_frames");
 }
@@ -954,8 +958,8 @@ TORCH_LIBRARY(zkmi, m) {
         "-> ()", &tree_serve);
   m.def("tree_serve_frames(Tensor(a!)[] tree, Tensor rx, Tensor frame_off, "
         "Tensor frame_len, Tensor count, int ncap, Tensor(b!)[] out, "
-        "int session, int now_ms, int wslot=-1, Tensor(c!)? fired=None) "
-        "-> ()", &tree_serve_frames);
+        "int session, int now_ms, int wslot=-1, Tensor(c!)? fired=None, "
+        "Tensor(d!)? tickets=None) -> ()", &tree_serve_frames);
   m.def("tree_order_workspace(int n) -> int", &tree_order_workspace);
   m.def("tree_order_stats_offset(int n) -> int", &tree_order_stats_offset);
   m.def("tree_serve_ordered(Tensor(a!)[] tree, Tensor rx, Tensor[] requests, "
@@ -983,6 +987,7 @@ TORCH_LIBRARY(zkmi, m) {
         "Tensor path_arena, Tensor rx, Tensor[] reply, Tensor(a!) acc, "
         "Tensor? want=None) -> ()", &bench_check_notif);
   m.def("route_workspace(int n, int world) -> int", &route_workspace);
+  m.def("serve_tickets(int ncap) -> int", &serve_tickets);
   m.def("route_requests(int n, int world, Tensor path_off, Tensor path_len, "
         "Tensor arena, Tensor idx, Tensor xid, Tensor(a!) owner, "
         "Tensor(b!) idx_s, Tensor(c!) xid_s, Tensor(d!) path_off_s, "

@@ -303,6 +303,10 @@ class GpuServer(object):
         self.cap_frames = cap_frames
         self.scanner = B.FrameScanner(cap_frames, dev, window=window)
         self.ows = None                   # ordered-serve workspace (lazy)
+        # the serve launch's sign-off counters (its last workgroup does the
+        # tree's finish: no separate launch); this server's own, zero
+        self.tickets = torch.zeros(_lib.lib().serve_tickets(cap_frames),
+                                   dtype=I32, device=dev)
         self.notif = None
         if tree.watch is not None:
             self._init_watch(cap_frames, dev)
@@ -435,7 +439,7 @@ class GpuServer(object):
             L.tree_serve_frames(self.tree.tensors, rx, ft.off, ft.length,
                                 ft.count, self.cap_frames, out, session, now,
                                 wslot, self.fired if self.tree.watch
-                                is not None else None)
+                                is not None else None, self.tickets)
         out, rec_off, total, err = B.encode_responses(
             r, self.tree.store, self.out.numel(), out=self.out,
             presized=self.presized, terminate=terminate)

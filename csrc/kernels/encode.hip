@@ -923,16 +923,23 @@ static inline unsigned nblk(int64_t n) {
   return (unsigned)((n + ENC_T - 1) / ENC_T);
 }
 
-// A/B switches read once: ZKMI_ENC_SWZ=1 the rounds 1-4 image swizzle;
-// ZKMI_ENC_FUSED=0 the block sums scanned by a launch of their own.
+// A/B switches, read once (profiles/r5_encoder_ab.md, GET step, 2 x 50
+// steps each): the image swizzle — 1 (default) keeps 4-dword groups whole
+// (4-way conflicts on the record writes, 16-byte read-out), 0 scatters
+// them (conflict-free writes, four dword reads per 16-byte vector): 0
+// removes the conflict cycles and costs the step 0.5 %, the dword reads
+// cost more LDS issue than the conflicts did; the block sums — a one-
+// workgroup scan launch (default) or every write block summing the sums
+// before its own (ZKMI_ENC_FUSED=1: one launch less, but 1.3 % slower: each
+// block's sum is a round trip before its first store).
 static int enc_swz() {
   static int v = -1;
-  if (v < 0) { const char* e = getenv("ZKMI_ENC_SWZ"); v = e ? atoi(e) : 0; }
+  if (v < 0) { const char* e = getenv("ZKMI_ENC_SWZ"); v = e ? atoi(e) : 1; }
   return v;
 }
 static bool enc_fused() {
   static int v = -1;
-  if (v < 0) { const char* e = getenv("ZKMI_ENC_FUSED"); v = e ? atoi(e) : 1; }
+  if (v < 0) { const char* e = getenv("ZKMI_ENC_FUSED"); v = e ? atoi(e) : 0; }
   return v != 0;
 }
 

@@ -93,10 +93,18 @@ constexpr int FL_LOCAL_MIN = 64;           // ... walked by the block when
 // Count blocks: frame counts scanned per FK_T tiles (one wave's worth)
 constexpr int FK_T = 64;
 // The workspace's words after the X flags (uint64, lbw + 2 * tiles): [0..3]
-// stats, [4..5] the check's minima, [6] the last live tile, [7] unused,
-// [8, 8 + FL_GW) fs_link's grid words
-constexpr int LW_MINS = 4, LW_LAST = 6, LW_GRID = 8;
-constexpr int LW_END = LW_GRID + FL_GW;
+// stats, [4..5] the check's minima, [6] the last live tile, [7] this scan's
+// tiles without a speculated entry (fs_tile counts, fs_rows clears),
+// [8, 8 + FL_GW) fs_link's grid words, [16, 32) its barrier words (the big
+// repair, see fs_link)
+constexpr int LW_MINS = 4, LW_LAST = 6, LW_NOSPEC = 7, LW_GRID = 8;
+constexpr int LW_BIG = 16;
+constexpr int LW_END = 32;
+static_assert(LW_GRID + FL_GW <= LW_BIG, "grid words");
+// The big repair (barrier rounds over the grid) when a scan has more tiles
+// without a speculated entry than this
+constexpr unsigned FL_BIG_NOSPEC = 256;
+constexpr int FL_GROUNDS = 6;              // its grid rounds
 // Bound of fs_tile's wait for the tile before (100 MHz ticks, 2 ms): normal
 // waits are tens of microseconds; past the bound the tile takes no
 // speculated entry and fs_link re-walks it from the exact one.
@@ -929,7 +937,7 @@ ZK_DEV int64_t fs_tile_rest(const FtCtx& cx_, bool mapped) {
       // likely one), so fs_link's grid repair of the NEXT tile can start
       // from it in the same round as this tile's own repair
       if (m > 0) fc_join_end(wk, send, n);
-      if (lane == 0) fc_stat(C.stats, 1, 1);
+      if (lane == 0) fc_stat(C.stats, 1, 1), fc_stat(C.stats, LW_NOSPEC, 1);
     }
   }
   if (lane == 0) {
@@ -1363,7 +1371,7 @@ ZK_DEV void fs_group_rest(const FtCtx& cx_) {
     }
   } else if (none) {
     if (m0 > 0) fc_join_end(wk, send0, n);
-    if (lane == 0) fc_stat(C.stats, 1, 1);
+    if (lane == 0) fc_stat(C.stats, 1, 1), fc_stat(C.stats, LW_NOSPEC, 1);
   }
   if (lane == 0) {
     C.sx[t0] = send0;
@@ -1717,6 +1725,141 @@ ZK_DEV uint32_t fl_local_round(const uint8_t* __restrict__ buf, int64_t n,
   }
   return walked;
 }
+
+// ---- the big repair ---------------------------------------------------------
+// A scan with hundreds of tiles without a speculated entry (adversarial
+// streams: every payload word a plausible length, tests that withhold
+// every entry) needs the grid's parallelism round after round, which no
+// single block has: there the grid keeps the barrier rounds of rounds 2-4.
+// The decision comes from fs_tile's count of this scan, known before
+// fs_link starts, so every block takes the same path and no ordinary scan
+// ever waits in a barrier.  Barrier words (LW_BIG, uint64): [0] arrivals,
+// [1] generation, [2] abort, [4 + 2r] the links round r listed.
+constexpr uint64_t FL_BAR_TICKS = 50000000;   // 0.5 s: barrier abandoned
+
+// Grid barrier over fs_link's workgroups (16: they find CUs beside
+// anything else that runs, and nothing they wait for needs a CU they hold).
+// Every wait is bounded: past FL_BAR_TICKS the grid is told to abort and
+// block 0 falls back to the serial repair.  Returns false on abort.
+ZK_DEV bool fl_sync(unsigned long long* g) {
+  __shared__ int s_ok;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int ok = 1;
+    __threadfence();
+    const unsigned long long gen =
+        __hip_atomic_load(&g[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long a =
+        __hip_atomic_fetch_add(&g[0], 1ull, __ATOMIC_ACQ_REL,
+                               __HIP_MEMORY_SCOPE_AGENT) + 1;
+    if (a == gridDim.x) {
+      __hip_atomic_store(&g[0], 0ull, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(&g[1], 1ull, __ATOMIC_RELEASE,
+                             __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      const uint64_t t0 = wall_clock64();
+      while (__hip_atomic_load(&g[1], __ATOMIC_ACQUIRE,
+                               __HIP_MEMORY_SCOPE_AGENT) == gen) {
+        if (__hip_atomic_load(&g[2], __ATOMIC_RELAXED,
+                              __HIP_MEMORY_SCOPE_AGENT)) {
+          ok = 0;
+          break;
+        }
+        if (wall_clock64() - t0 > FL_BAR_TICKS) {
+          __hip_atomic_store(&g[2], 1ull, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+          ok = 0;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(8);
+      }
+    }
+    __threadfence();
+    if (__hip_atomic_load(&g[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+      ok = 0;
+    s_ok = ok;
+  }
+  __syncthreads();
+  return s_ok != 0;
+}
+
+// One grid repair round (every thread of every block calls it).  Returns
+// false when no link was broken (the fix-point is reached) or on abort.
+ZK_DEV bool fl_round(const uint8_t* __restrict__ buf, int64_t n,
+                     int64_t ntiles, int64_t maxp,
+                     const int64_t* __restrict__ sx,
+                     const uint16_t* __restrict__ list,
+                     const int32_t* __restrict__ rcount, uint16_t* pre,
+                     int64_t* rec_entry, int64_t* rec_exit, int64_t* rec_meta,
+                     int32_t* blist, unsigned long long* g, int r,
+                     int64_t* red, uint8_t* win, uint64_t* stats) {
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int64_t INF = INT64_MAX;
+  const int64_t nblk = gridDim.x;
+  const int64_t bid = blockIdx.x;
+  const int64_t nth = nblk * FL_T;
+  const int64_t gt = bid * FL_T + tid;
+  // B. list the broken links (after a tile that is not a terminal).  Every
+  // one, not only those before the first terminal: a terminal may be a
+  // speculation's (a garbage entry that died) that this very round fixes,
+  // and stopping the list there made a stream with many such tiles take a
+  // round per terminal (26 ms a 0-1024 B reply stream at a 1 KiB window).
+  // Past a real bad frame the walks are wasted, and the serial tail's
+  // first terminal bounds what counts.
+  int64_t nb = 0;
+  const int64_t per = (ntiles - 1 + nth - 1) / nth;
+  const int64_t k0 = 1 + gt * per, k1 = min(k0 + per, ntiles);
+  auto broken = [&](int64_t k) {
+    return ld_agent(&rec_entry[k]) != ld_agent(&rec_exit[k - 1]) &&
+           !m_term(ld_agent(&rec_meta[k - 1]));
+  };
+  for (int64_t k = k0; k < k1; ++k) nb += broken(k);
+  int64_t tot;
+  const int64_t o = block_excl_scan(nb, red, &tot);
+  __shared__ unsigned long long s_base;
+  if (tid == 0)
+    s_base = tot ? atomicAdd(&g[4 + 2 * r], (unsigned long long)tot) : 0;
+  __syncthreads();
+  int64_t w = (int64_t)s_base + o;
+  for (int64_t k = k0; k < k1; ++k)
+    if (broken(k)) blist[w++] = (int32_t)k;
+  if (!fl_sync(g)) return false;
+  const int64_t nbr = (int64_t)__hip_atomic_load(
+      &g[4 + 2 * r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (nbr == 0) return false;
+  // C. every listed link re-walked by one wave, from the exit before it
+  uint8_t* mywin = win + (size_t)wv * (FC_WIN + 16);
+  const int64_t nwv = nblk * (FL_T / 64);
+  uint32_t walked = 0;
+  for (int64_t j = bid * (FL_T / 64) + wv; j < nbr; j += nwv) {
+    const int64_t k = blist[j];
+    const int64_t E = ld_agent(&rec_exit[k - 1]);
+    if (E < k * FT_S) continue;               // no exact entry yet
+    const int32_t m0 = __builtin_amdgcn_readfirstlane(rcount[k]);
+    const FcWalk fw = fc_walk(buf, n, maxp, k * FT_S, E, list + k * FT_LMAX,
+                              m0, sx[k], mywin, pre + k * FT_LMAX, lane);
+    ++walked;
+    if (lane == 0) {
+      if (fl_accept(rec_entry, rec_exit, ntiles, k, E, fw.exit)) {
+        st_agent(&rec_entry[k], E);
+        st_agent(&rec_exit[k], fw.exit);
+        st_agent(&rec_meta[k], fc_meta(fw));
+      } else {
+        // the walk overwrote the tile's frame starts (pre) while its
+        // record keeps the old entry: no entry, so the link stays broken
+        // and the tile is walked again (its exit, which the refusal
+        // protects, is kept)
+        st_agent(&rec_entry[k], -1);
+      }
+    }
+  }
+  if (lane == 0 && walked) fc_stat(stats, 2, walked);
+  if (bid == 0 && tid == 0) fc_stat(stats, 3, 1);
+  return fl_sync(g);
+}
+
+// The full check (fs_link, when fs_tile counted a bad link): every link and
 
 // The full check (fs_link, when fs_tile counted a bad link): every link and
 // terminal, one wave per count block of FK_T tiles over the grid, and the
@@ -2356,24 +2499,47 @@ ZK_DEV int64_t fl_list_broken(int64_t ntiles, const int64_t* rec_entry,
                               int64_t& ft_out) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int64_t INF = INT64_MAX;
+  // a thread's run of tiles, its loads in batches of FL_U (all issued
+  // before any is used) — this runs once per repair round
   const int64_t per = (ntiles + FL_T - 1) / FL_T;
   const int64_t k0 = (int64_t)tid * per, k1 = min(k0 + per, ntiles);
-  auto broken = [&](int64_t k) {
-    return k >= 1 && !m_term(ld_agent(&rec_meta[k - 1])) &&
-           ld_agent(&rec_entry[k]) != ld_agent(&rec_exit[k - 1]);
-  };
   int64_t cnt = 0, fb = INF, fterm = INF;
-  for (int64_t k = k0; k < k1; ++k) {
-    if (broken(k)) {
-      ++cnt;
-      fb = min(fb, k);
+  for (int pass = 0; pass < 2; ++pass) {
+    int64_t w = 0;
+    if (pass == 1) {
+      int64_t tot;
+      w = block_excl_scan(cnt, red, &tot);
+      red[2 * (FL_T / 64) + 1] = tot;       // (read after the loop)
+      if (cnt == 0) break;
     }
-    if (m_term(ld_agent(&rec_meta[k]))) fterm = min(fterm, k);
+    for (int64_t kb = k0; kb < k1; kb += FL_U) {
+      int64_t mp[FL_U], mk[FL_U], e[FL_U], x[FL_U];
+#pragma unroll
+      for (int u = 0; u < FL_U; ++u) {
+        const int64_t k = kb + u;
+        const bool in = k < k1;
+        mk[u] = in ? ld_agent(&rec_meta[k]) : 0;
+        mp[u] = in && k >= 1 ? ld_agent(&rec_meta[k - 1]) : 0;
+        e[u] = in ? ld_agent(&rec_entry[k]) : 0;
+        x[u] = in && k >= 1 ? ld_agent(&rec_exit[k - 1]) : 0;
+      }
+#pragma unroll
+      for (int u = 0; u < FL_U; ++u) {
+        const int64_t k = kb + u;
+        if (k >= k1) break;
+        const bool brk = k >= 1 && !m_term(mp[u]) && e[u] != x[u];
+        if (pass == 0) {
+          if (brk) { ++cnt; fb = min(fb, k); }
+          if (m_term(mk[u])) fterm = min(fterm, k);
+        } else if (brk) {
+          blist[w++] = (int32_t)k;
+        }
+      }
+    }
   }
-  int64_t tot;
-  int64_t w = block_excl_scan(cnt, red, &tot);
-  for (int64_t k = k0; k < k1 && cnt > 0; ++k)
-    if (broken(k)) blist[w++] = (int32_t)k;
+  __syncthreads();
+  const int64_t total = red[2 * (FL_T / 64) + 1];
+  __syncthreads();
   for (int d = 32; d >= 1; d >>= 1) {
     fb = min(fb, (int64_t)__shfl_xor(fb, d, 64));
     fterm = min(fterm, (int64_t)__shfl_xor(fterm, d, 64));
@@ -2389,7 +2555,7 @@ ZK_DEV int64_t fl_list_broken(int64_t ntiles, const int64_t* rec_entry,
   __syncthreads();
   fb_out = fb;
   ft_out = fterm;
-  return tot;
+  return total;
 }
 
 __global__ __launch_bounds__(FL_T) void fs_link(
@@ -2429,12 +2595,29 @@ __global__ __launch_bounds__(FL_T) void fs_link(
   __syncthreads();
   fl_check(ntiles, rec_entry, rec_exit, rec_meta, base, bsum, mins, &g[FL_NB],
            blist, lloc, &s_lcnt);
+  // the big repair (see FL_BIG_NOSPEC): barrier rounds over the grid, then
+  // block 0 goes on as the last block does
+  const bool big = (uint32_t)ld_agent((const int64_t*)&stats[LW_NOSPEC]) >
+                   FL_BIG_NOSPEC;
+  if (big) {
+    unsigned long long* gb = (unsigned long long*)(stats + LW_BIG);
+    bool ok = fl_sync(gb);
+    for (int r = 0; r < FL_GROUNDS && ok; ++r)
+      ok = fl_round(buf, n, ntiles, maxp, sx, list, rcount, pre, rec_entry,
+                    rec_exit, rec_meta, blist, gb, r, red, win, stats);
+    if (blockIdx.x != 0) return;
+    __syncthreads();
+    if (tid == 0) {
+      gb[2] = 0;
+      for (int r = 0; r < FL_GROUNDS; ++r) gb[4 + 2 * r] = 0;
+    }
+  }
   __syncthreads();
   // (a handful of broken links — a frontier timeout, a garbage candidate,
   // the ends of a phantom chain's region — are the last block's chases:
   // an exact chase runs on through a region of consistent-but-wrong links
   // that no per-link walk sees broken)
-  if (s_lcnt > FL_LOCAL_MIN) {
+  if (!big && s_lcnt > FL_LOCAL_MIN) {
     const uint32_t w = fl_local_round(buf, n, ntiles, maxp, sx, list, rcount,
                                       pre, rec_entry, rec_exit, rec_meta, lloc,
                                       min(s_lcnt, FL_LOC), win);
@@ -2445,7 +2628,9 @@ __global__ __launch_bounds__(FL_T) void fs_link(
   }
   __shared__ int s_last;
   __syncthreads();
-  if (tid == 0) {
+  if (big) {
+    if (tid == 0) s_last = 1;             // (block 0, after the rounds)
+  } else if (tid == 0) {
     __threadfence();
     const unsigned long long a = __hip_atomic_fetch_add(
         &g[0], 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
@@ -2469,7 +2654,7 @@ __global__ __launch_bounds__(FL_T) void fs_link(
       &g[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int64_t fb0 = mb0 ? ntiles - (int64_t)mb0 : INF;
   const int64_t ft0 = mt0 ? ntiles - (int64_t)mt0 : INF;
-  if (fb0 == INF || fb0 > ft0) {
+  if (!big && (fb0 == INF || fb0 > ft0)) {
     // no broken link before the first terminal (the blocks re-walked only
     // links past it, whose counts no row uses): the row bases are bsum's
     // block offsets + the check's in-block bases
@@ -2493,7 +2678,7 @@ __global__ __launch_bounds__(FL_T) void fs_link(
   // re-counted); many are re-walked in parallel, one wave a link (the
   // blocks' round continued here); after each, the links still broken are
   // listed again.  What the rounds leave goes to the tail.
-  bool changed = rew != 0;       // records changed beyond the chases' dirty
+  bool changed = rew != 0 || big;       // records changed beyond the chases' dirty
   for (int round = 0; round < FL_BROUNDS; ++round) {
     if (changed) {
       int64_t fbv, ftv;
@@ -2611,6 +2796,7 @@ __global__ __launch_bounds__(256) void fs_rows(
     // fs_link's minima and broken-link count, for the next scan
     lbw_tail[LW_MINS] = 0;
     lbw_tail[LW_MINS + 1] = 0;
+    lbw_tail[LW_NOSPEC] = 0;
     lbw_tail[LW_GRID + FL_NB] = 0;
   }
   if (t > *lastk) return;

@@ -2584,6 +2584,7 @@ __global__ __launch_bounds__(FL_T) void fs_link(
     return;
   }
   const int64_t INF = INT64_MAX;
+  const int64_t t_in = ldbg != nullptr ? wall_clock64() : 0;
   // the check over the grid (links, terminals, in-block counts; a launch of
   // its own until round 4), the block's repair round over the broken links
   // it found, then a ticket: the last block to take one sees every block's
@@ -2671,6 +2672,9 @@ __global__ __launch_bounds__(FL_T) void fs_link(
   if (tid == 0) s_ovf = 0;
   __syncthreads();
   const bool clk = ldbg != nullptr && tid == 0;
+  // (ZKMI_FS_DBG: [5] the last block's start, [4] the end | path << 56:
+  // 1 chases, 2 count scan after rounds, 3 tail)
+  if (clk) ldbg[5] = t_in;
   int64_t from = 1, ft = INF;
   int64_t nb = (int64_t)nb0;
   // repair rounds of this block: a handful of broken links are chased (the
@@ -2687,6 +2691,7 @@ __global__ __launch_bounds__(FL_T) void fs_link(
       if (fbv == INF || fbv > ftv) {
         fl_count_scan(n, ntiles, ftv, rec_exit, rec_meta, base, bsum, cap,
                       result, lastk, red);
+        if (clk) ldbg[4] = wall_clock64() | (2ll << 56);
         return;
       }
     }
@@ -2706,12 +2711,13 @@ __global__ __launch_bounds__(FL_T) void fs_link(
           // (tiles re-walked in rounds are not in the chases' dirty set)
           fl_count_scan(n, ntiles, ftv, rec_exit, rec_meta, base, bsum, cap,
                         result, lastk, red);
+          if (clk) ldbg[4] = wall_clock64() | (2ll << 56);
           return;
         }
         fl_chase_recount(ntiles, rec_meta, base, bsum, ch);
         fl_bases(n, ntiles, ftv, rec_exit, rec_meta, base, bsum, cap, result,
                  lastk, red);
-        if (clk) ldbg[4] = wall_clock64();
+        if (clk) ldbg[4] = wall_clock64() | (1ll << 56);
         return;
       }
       if (!settled) break;              // the lists outgrew LDS: the tail
@@ -2762,6 +2768,7 @@ __global__ __launch_bounds__(FL_T) void fs_link(
   }
   fl_count_scan(n, ntiles, ft, rec_exit, rec_meta, base, bsum, cap, result,
                 lastk, red);
+  if (clk) ldbg[4] = wall_clock64() | (3ll << 56);
 }
 
 // (body offset, length) rows: one wave per tile, 4 tiles per block.  A

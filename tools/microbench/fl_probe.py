@@ -64,11 +64,16 @@ def main():
         if os.environ.get('ZKMI_FS_DBG'):
             tiles = (len(buf) + 4095) // 4096
             dd = _lib.lib().frame_scan_dbg(tiles + 1).cpu().numpy()
-            c = dd.reshape(-1)[8 * tiles:8 * tiles + 8].astype(np.float64)
+            raw = dd.reshape(-1)[8 * tiles:8 * tiles + 8]
+            path = int(raw[4]) >> 56
+            c = raw.astype(np.float64)
+            c[4] = float(int(raw[4]) & ((1 << 56) - 1))
             us = lambda x, y: (c[y] - c[x]) / 100.0 if c[x] and c[y] \
                 else -1.0                                       # noqa: E731
-            line += ' fs_link: chases %.1f us, check %.1f us, recount %.1f' \
-                    ' us' % (us(0, 1), us(2, 3), us(3, 4))
+            line += (' fs_link: to chase %.1f us, chases %.1f us, check %.1f'
+                     ' us, chase->end %.1f us, total %.1f us, path %d' % (
+                         us(5, 0), us(0, 1), us(2, 3), us(3, 4), us(5, 4),
+                         path))
         print(line, flush=True)
     r = ft.host_result()
     off = ft.off[:r['frames']].cpu().numpy()

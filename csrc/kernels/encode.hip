@@ -700,6 +700,62 @@ ZK_DEV void staged_emit_holes(int64_t r0, int64_t r1, const int64_t* off,
   }
 }
 
+// Uniform GET_DATA replies (every record of the block a successful
+// GET_DATA of the same size S, S a multiple of 16, the block's span
+// 16-byte aligned — a read batch of equal-sized znodes): the block's span
+// is written straight from the slots, 16 bytes a lane per step, every
+// store of a wave 1 KiB contiguous, no LDS image.  A record is
+//   [0,4) S - 4 | [4,8) xid | [8,16) zxid | [16,20) err |
+//   [20, S - 68) the slot's [len | data] | [S - 68, S) the slot's Stat,
+// and S % 16 == 0 makes the data length a multiple of 4, so every dword of
+// a 16-byte piece is one aligned dword of the slot (or of the header).
+// Lanes take consecutive pieces: a wave reads a run of slots front to back.
+ZK_DEV uint32_t slot_dw(const uint8_t* slot, int64_t p, int64_t dl) {
+  // record byte p (>= 20, 4-aligned) of a reply of data length dl
+  const int64_t so = p < 24 + dl ? p - 20 + ZK_SLOT_LEN : p - 24 - dl;
+  return *(const uint32_t*)(slot + so);
+}
+
+ZK_DEV void emit_uniform(const ZkRespBatch& r, const ZkNodeStore& s,
+                         int64_t r0, int64_t nrec, int64_t S, int64_t B0,
+                         uint8_t* __restrict__ out) {
+  const int64_t dl = S - 4 - 16 - 4 - STAT_BYTES;
+  const int64_t pieces = nrec * (S >> 4);
+  constexpr int U = 4;                   // pieces in flight per lane
+  for (int64_t c0 = threadIdx.x; c0 < pieces; c0 += (int64_t)U * ENC_T) {
+    uint32_t v[U][4];
+    int64_t xo[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t c = c0 + (int64_t)u * ENC_T;
+      xo[u] = -1;
+      if (c >= pieces) continue;
+      const int64_t x = c << 4;
+      const int64_t k = x / S, b = x - k * S;
+      const int64_t i = r0 + k;
+      const uint8_t* slot = s.slab + (r.slot ? r.slot[i] : s.slot_off[r.node[i]]);
+      xo[u] = x;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int64_t p = b + 4 * q;
+        uint32_t w;
+        if (p == 0) w = bswap32((uint32_t)(S - 4));
+        else if (p == 4) w = bswap32((uint32_t)r.xid[i]);
+        else if (p == 8) w = bswap32((uint32_t)((uint64_t)r.zxid[i] >> 32));
+        else if (p == 12) w = bswap32((uint32_t)r.zxid[i]);
+        else if (p == 16) w = bswap32((uint32_t)r.err[i]);
+        else w = slot_dw(slot, p, dl);
+        v[u][q] = w;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (xo[u] >= 0)
+        *(uint4*)(out + B0 + xo[u]) = make_uint4(v[u][0], v[u][1], v[u][2],
+                                                 v[u][3]);
+  }
+}
+
 // bsum != null: fused (block_base); every block checks its own span
 // against cap, the last one writes *total and err (2: over capacity, the
 // stream is then incomplete).
@@ -710,7 +766,7 @@ __global__ __launch_bounds__(ENC_T) void resp_write(
     const int64_t* __restrict__ bbase, const int64_t* __restrict__ bsum,
     int64_t* __restrict__ rec_off, int64_t* __restrict__ total,
     uint8_t* __restrict__ out, int64_t cap, int32_t* __restrict__ err,
-    int32_t term, int64_t stage) {
+    int32_t term, int64_t stage, int32_t uniform) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lw[];
   __shared__ EncLocal E;
   const int64_t n = min(*n_dev, ncap);
@@ -728,6 +784,19 @@ __global__ __launch_bounds__(ENC_T) void resp_write(
   const int64_t r1 = min(r0 + ENC_T, n);
   if (bsum != nullptr && base + bsum[blockIdx.x] > cap) return;
   block_offsets(r0, r1, sizes, base, rec_off, E);
+  // uniform GET_DATA replies: straight from the slots (emit_uniform)
+  {
+    const int64_t i = r0 + threadIdx.x;
+    const int64_t S = E.sz[0];
+    const bool u = i >= r1 ||
+                   (r.opcode[i] == OP_GET_DATA && r.err[i] == ERR_OK &&
+                    E.sz[threadIdx.x] == S);
+    if (__syncthreads_and(u) && (S & 15) == 0 && (E.off[0] & 15) == 0 &&
+        uniform) {
+      emit_uniform(r, s, r0, r1 - r0, S, E.off[0], out);
+      return;
+    }
+  }
   // the holes (large GET_DATA replies), their block scan and list
   __shared__ EncHoles H;
   {
@@ -937,6 +1006,13 @@ static int enc_swz() {
   if (v < 0) { const char* e = getenv("ZKMI_ENC_SWZ"); v = e ? atoi(e) : 1; }
   return v;
 }
+// ZKMI_ENC_UNIFORM=0: uniform GET_DATA reply blocks through the LDS image
+// like any other (emit_uniform off)
+static int enc_uniform() {
+  static int v = -1;
+  if (v < 0) { const char* e = getenv("ZKMI_ENC_UNIFORM"); v = e ? atoi(e) : 1; }
+  return v;
+}
 static bool enc_fused() {
   static int v = -1;
   if (v < 0) { const char* e = getenv("ZKMI_ENC_FUSED"); v = e ? atoi(e) : 0; }
@@ -1061,11 +1137,11 @@ int zk_encode_responses2(const ZkRespBatch* r, const ZkNodeStore* s,
   if (zk::enc_swz() == 1)
     zk::resp_write<1><<<nb, zk::ENC_T, (size_t)stage, st>>>(
         *r, *s, n_dev, ncap, sizes, bbase, fused ? bsum : nullptr, rec_off,
-        total, out, out_cap, err, terminate, stage);
+        total, out, out_cap, err, terminate, stage, zk::enc_uniform());
   else
     zk::resp_write<0><<<nb, zk::ENC_T, (size_t)stage, st>>>(
         *r, *s, n_dev, ncap, sizes, bbase, fused ? bsum : nullptr, rec_off,
-        total, out, out_cap, err, terminate, stage);
+        total, out, out_cap, err, terminate, stage, zk::enc_uniform());
   ZK_LAUNCH_CHECK();
   return 0;
 }

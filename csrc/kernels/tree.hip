@@ -49,8 +49,15 @@ constexpr int TR_T = 256;
 enum : int {
   TC_NODES = 0, TC_ZXID = 1, TC_PATH_TOP = 2, TC_SLAB_TOP = 3,
   TC_FREE_HEAD = 4, TC_FREE_TAIL = 5, TC_FREE_PUB = 6, TC_DIRTY = 7,
-  TC_DONE = 8, TC_N = 9
+  TC_SESS = 8, TC_N = 9
 };
+// `session` argument value meaning "the session in counters[TC_SESS]": a
+// captured step whose session changes from replay to replay (the storm's
+// born / resumed / expired sessions) keeps it on the device
+constexpr int64_t SESS_DEV = -2;
+ZK_DEV int64_t sess_of(const ZkTree& t, int64_t session) {
+  return session == SESS_DEV ? t.counters[TC_SESS] : session;
+}
 constexpr int64_t NODE_FREE = -2;
 
 // ordered serve: rank byte = min(rank, ORD_RANK) | ORD_SNAP
@@ -532,6 +539,7 @@ __global__ __launch_bounds__(TR_T) void tree_serve_k(
     const uint8_t* __restrict__ rank, int32_t pass, int32_t last_pass,
     int64_t snap_base, int64_t snap_cap, int64_t* __restrict__ snap_top,
     int32_t wslot, int64_t* __restrict__ fired, unsigned* tickets) {
+  session = sess_of(t, session);
   const uint32_t blk = xcd_remap(blockIdx.x, gridDim.x);
   const int64_t i = (int64_t)blk * TR_T + threadIdx.x;
   const bool in_batch = i < ncap && i < *n_dev;
@@ -1027,7 +1035,7 @@ __global__ __launch_bounds__(TR_T) void ord_rank_k(int64_t ncap, OrderWs w,
 //     launch poppable, clamp a head that overshot the previously published
 //     tail, reset the dirty list and consume the launch's zxids (`*n_dev`
 //     for a batch of requests, 1 for a session expiry, which is one
-//     closeSession txn).  TC_DONE is no longer used.
+//     closeSession txn).
 constexpr int FIN_T = 1024;
 
 // One workgroup: the dirty list holds the distinct parents a batch touched
@@ -1116,6 +1124,7 @@ ZK_DEV bool serve_last(unsigned* tickets) {
 __global__ __launch_bounds__(TR_T) void tree_expire_k(
     ZkTree t, int64_t session, int64_t ncap,
     unsigned long long* __restrict__ removed) {
+  session = sess_of(t, session);
   const int64_t v = (int64_t)blockIdx.x * TR_T + threadIdx.x;
   const ZkNodeStore& s = t.store;
   bool hit = v < ncap && v < t.counters[TC_NODES] &&

@@ -837,6 +837,32 @@ def test_gpu_storm_pipeline(gpu):
     assert bool(pipe.hs_ok.item())
 
 
+def test_gpu_storm_pipeline_captured(gpu):
+    """The storm step replayed from HIP graphs: session ids come from the
+    device (TC_SESS), so every replay serves, expires and checks the NEXT
+    session; rehashes run between replays.  Then eager steps carry on from
+    the replayed state."""
+    from zkmi.bench.synthetic import StormPipeline
+    tree = _small_tree(gpu, 20000, 37, spare=1.5)
+    pipe = StormPipeline(tree, 8192, ndirs=64)
+    acc = torch.zeros(64, dtype=torch.int64, device=gpu)
+    g = pipe.capture(acc)
+    torch.cuda.synchronize()
+    acc.zero_()
+    for _ in range(14):                 # crosses rehashes
+        g.replay()
+    torch.cuda.synchronize()
+    assert int(acc.sum().item()) == 14 * 8192
+    for _ in range(2):
+        assert int(pipe.step().item()) == 8192
+    assert bool(pipe.hs_ok.item())
+    st = pipe.stats
+    assert st['born'] == (pipe.step_no + 1) // 2
+    assert st['resumed'] == pipe.step_no // 2
+    assert st['expired'] == st['born'] - 1
+    assert int(pipe.kdev.item()) == pipe.k
+
+
 def test_gpu_session_handshake_k9_server(gpu):
     """The GPU server's handshake against the oracle's records: new
     session, resume with the right password, wrong password and unknown id

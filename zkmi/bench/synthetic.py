@@ -1294,6 +1294,11 @@ class StormPipeline(object):
                 torch.empty(m, dtype=I64, device=dev),
                 torch.zeros(1, dtype=I64, device=dev))
         self.k = -1                       # index of the current session
+        # ... and on the device (a captured step replays with the next
+        # session's ids: serve / expire take them from the tree's TC_SESS)
+        self.kdev = torch.full((1,), -1, dtype=I64, device=dev)
+        self.sid0 = self.sessions.sid_of(0)
+        self._capturing = False
         self.step_no = 0
         self.inserted = 0
         self.stats = {'born': 0, 'resumed': 0, 'expired': 0,
@@ -1373,21 +1378,84 @@ class StormPipeline(object):
             self.stats['cross_rank_resumes'] += 1
             return o, bound, outcome, resp
         resp, bound, outcome = self.sessions.connect(
-            self.cr_tx[:nbytes], nbytes, 0 if resume else 1)
+            self.cr_tx[:nbytes], nbytes, 0)
         ft = self.rscan.scan(resp[:rb], rb)
         o = B.decode_connect_responses(resp, ft, m)
         return o, bound, outcome, resp
 
-    def step(self, validate=True, acc=None):
-        t = self.tree
-        n = self.n
-        dev = self.dev
+    @property
+    def capturable(self):
+        return self.world == 1
+
+    def capture(self, acc):
+        """Capture the steady state's two step shapes (a birth that expires
+        the session before, a resume that also tries the expired one) as
+        HIP graphs; ``replay()`` runs the next step.  Session ids live on
+        the device (``kdev`` -> the tree's TC_SESS word), so a replay serves,
+        expires and checks the next session; the host keeps only its
+        bookkeeping (counts, the rehash due every few hundred steps, run
+        eagerly between replays).  One member only: the ensemble's steps
+        gather over the process group."""
+        if self.world > 1:
+            raise RuntimeError('storm capture: one member only')
+        while self.step_no < 2 or self.step_no % 2:
+            self.step(acc=acc)
+        self._check_rehash(2)
+        torch.cuda.synchronize(self.dev)
+        keep = (self.step_no, self.k, self.inserted, dict(self.stats),
+                self.sessions.allocated)
+        graphs = []
+        self._capturing = True
+        try:
+            for _ in range(2):
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, capture_error_mode='thread_local'):
+                    self.step(acc=acc)
+                graphs.append(g)
+        finally:
+            self._capturing = False
+        (self.step_no, self.k, self.inserted, self.stats,
+         self.sessions.allocated) = keep
+        return _StormCycle(self, graphs)
+
+    def _check_rehash(self, steps=1):
+        """Rebuild the hash index now if the next ``steps`` steps' inserts
+        would fill it (tombstones of never-reused sequential names)."""
+        if (self.inserted + (steps + 1) * self.n * self.world) > \
+                0.6 * self.tree.hcap:
+            self.tree.rehash()
+            self.inserted = 0
+
+    def _advance(self):
+        """The host side of a step (eager and replayed alike): step and
+        session counters, stats, the rehash decision.  Returns resume."""
         s = self.step_no
         self.step_no += 1
         resume = s % 2 == 1
-        if (self.inserted + 2 * n) > 0.6 * t.hcap:
-            t.rehash()
-            self.inserted = 0
+        if not self._capturing:
+            self._check_rehash()
+        if resume:
+            self.stats['resumed'] += 1
+            self.stats['expired_resume_refused'] += int(self.k >= 1)
+        else:
+            self.k += 1
+            self.sessions.allocated += 1
+            self.stats['born'] += 1
+            if self.k >= 1:
+                self.stats['expired'] += 1
+        self.inserted += self.n * self.world
+        return resume
+
+    def step(self, validate=True, acc=None):
+        t = self.tree
+        n = self.n
+        resume = self._advance()
+        if not resume:
+            self.kdev.add_(1)
+        # this step's session on the device (one member: its own; the
+        # ensemble passes host ids, see _replicated_run)
+        sess_dev = t.counters[_lib.TC_SESS:_lib.TC_SESS + 1]
+        torch.add(self.kdev, self.sid0, out=sess_dev)
         o, bound, outcome, resp = self._handshake(resume)
         if resume:
             # current session back with the same id and password; the
@@ -1401,11 +1469,10 @@ class StormPipeline(object):
             if self.k >= 1:
                 ok &= (outcome[1] == _lib.SC_EXPIRED) & \
                     (o['sessionId'][1] == 0)
-            self.stats['resumed'] += 1
-            self.stats['expired_resume_refused'] += int(self.k >= 1)
         else:
-            self.k += 1
-            want = self.sessions.sid_of(self.sessions.allocated - 1)
+            # the id the server handed out: member r's k-th session
+            want = sess_dev[0] if self.world == 1 else \
+                self.sid(self.rank, self.k)
             ok = ((o['status'][0] == 0) & (outcome[0] == _lib.SC_NEW) &
                   (o['sessionId'][0] == want) & (bound[0] == want))
             # credentials: the new session becomes current, the old one prev
@@ -1413,7 +1480,6 @@ class StormPipeline(object):
             self.cred_pw[16:32].copy_(self.cred_pw[0:16])
             self.cred_sid[0:1].copy_(o['sessionId'][0:1])
             self.cred_pw[0:16].copy_(resp[24:40])
-            self.stats['born'] += 1
             if self.world > 1:
                 # R3: every member's new session to every member
                 self.prev_recs.copy_(self.recs)
@@ -1423,10 +1489,6 @@ class StormPipeline(object):
                 self._gather(self.recs.view(-1), mine)
                 self.sessions.install(self.recs)
         self.hs_ok &= ok
-        # the session this member serves now: its own new one, or after a
-        # move the previous member's
-        cur = self.sid((self.rank - (1 if resume else 0)) % self.world,
-                       self.k)
         rb = B.RequestBatch(n, self.opcode, self.drv.xids(n), self.arg,
                             self.path_off, self.path_len, self.data_off,
                             self.data_len, self.acl_id, self.path_arena,
@@ -1435,9 +1497,8 @@ class StormPipeline(object):
         if self.world > 1:
             rep = self._replicated_run(rb, resume)
         else:
-            rep, _ = self.drv.run(rb, session=cur)
+            rep, _ = self.drv.run(rb, session=_lib.SESS_DEV)
         self.last = (rb, rep)
-        self.inserted += n * self.world
         if not resume and self.world > 1:
             # the new session's first batch: the created paths (offsets into
             # the reply stream kept with them), for cross_read
@@ -1457,16 +1518,15 @@ class StormPipeline(object):
             for m in range(self.world):
                 t.expire(self.sid(m, self.k - 1), self.removed)
             self.sessions.close(self.prev_recs[:, 0].contiguous())
-            self.stats['expired'] += 1
             expire_ok = self.removed[0] == 2 * n * self.world
         elif not resume and self.k >= 1:
-            # the previous session expires: both of its batches go
-            prev = self.sessions.sid_of(self.k - 1)
+            # the previous session expires: both of its batches go (its id,
+            # the current one's less one, through TC_SESS)
+            sess_dev.sub_(1)
             self.removed.zero_()
-            t.expire(prev, self.removed)
-            self.prev_sid.fill_(prev)
+            t.expire(_lib.SESS_DEV, self.removed)
+            self.prev_sid.copy_(sess_dev)
             self.sessions.close(self.prev_sid)
-            self.stats['expired'] += 1
             expire_ok = self.removed[0] == 2 * n
         if not validate:
             return None
@@ -1600,6 +1660,19 @@ class StormPipeline(object):
                                    .sum().item()),
                 'stats': dict(self.stats),
                 'counters': self.tree.counters.cpu().tolist()}
+
+
+class _StormCycle(object):
+    """The storm's two captured step shapes replayed in turn, the host
+    bookkeeping of each step done first (see StormPipeline.capture)."""
+
+    def __init__(self, pipe, graphs):
+        self.pipe = pipe
+        self.graphs = graphs
+
+    def replay(self):
+        resume = self.pipe._advance()
+        self.graphs[1 if resume else 0].replay()
 
 
 class WatchPipeline(object):

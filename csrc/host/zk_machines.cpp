@@ -1,0 +1,831 @@
+// _zkmach — the client's state machines in C++: the ZooKeeper session
+// (lib/zk-session.js:38-375), the connection (lib/connection-fsm.js:27-351)
+// and the client lifecycle (lib/client.js:123-181).
+//
+// Not the mooremachine shape.  The reference (and zkmi's Python oracle,
+// zkmi/models/*.py under ZKMI_PY_FSM=1) writes each state as a function that
+// subscribes its own listeners on every emitter it cares about and tears
+// them down on exit — a subscribe / unsubscribe pair per emitter per
+// transition.  Here a machine is a table:
+//
+//   * one dispatch entry per event kind (Relay objects: each is subscribed
+//     ONCE to an emitter — a socket, a connection, the expiry timer — and
+//     carries its source), so a transition costs no listener churn;
+//   * the state x event switch decides, with the source checked against the
+//     machine's current peer (an event from a connection the session has
+//     moved away from is simply not for any state), and guards computed in
+//     C++ (a ConnectResponse's session id, the protocol version, the
+//     session's liveness);
+//   * entry actions are C++; what they do to the outside world (send a
+//     record, destroy a connection, log) goes through the owner's methods —
+//     the Python objects keep the API and listener surface only.
+//
+// Transitions requested while one runs are queued and applied in order;
+// `stateChanged` is emitted on the owner after each entry action, then the
+// owner's `_fsm_entered(state)` hook runs (the session's watch engine
+// ready / unready), as the FSM runtime (zk_fsm.cpp) does.  Once a state has
+// requested its transition, further events for it are dropped (the
+// runtime's used-handle rule).
+#include <Python.h>
+
+#include <cstdint>
+#include <ctime>
+#include <vector>
+
+namespace {
+
+// ---- small C-API helpers ----------------------------------------------------
+
+// owner.name(*args) with a borrowed-args format; nullptr on error
+PyObject* callm(PyObject* o, const char* name) {
+  return PyObject_CallMethod(o, name, nullptr);
+}
+
+bool is_none(PyObject* o) { return o == nullptr || o == Py_None; }
+
+// o.attr (new ref), nullptr + error cleared if missing
+PyObject* attr(PyObject* o, const char* name) {
+  PyObject* v = PyObject_GetAttrString(o, name);
+  if (v == nullptr) PyErr_Clear();
+  return v;
+}
+
+int64_t attr_i64(PyObject* o, const char* name) {
+  PyObject* v = attr(o, name);
+  if (v == nullptr) return 0;
+  const int64_t r = PyLong_Check(v) ? PyLong_AsLongLong(v) : 0;
+  if (PyErr_Occurred()) PyErr_Clear();
+  Py_DECREF(v);
+  return r;
+}
+
+int set_attr(PyObject* o, const char* name, PyObject* v) {
+  return PyObject_SetAttrString(o, name, v);
+}
+
+// pkt[key] (borrowed) from a dict packet
+PyObject* field(PyObject* pkt, const char* key) {
+  return PyDict_Check(pkt) ? PyDict_GetItemString(pkt, key) : nullptr;
+}
+
+int64_t field_i64(PyObject* pkt, const char* key) {
+  PyObject* v = field(pkt, key);
+  if (v == nullptr || !PyLong_Check(v)) return 0;
+  const int64_t r = PyLong_AsLongLong(v);
+  if (PyErr_Occurred()) { PyErr_Clear(); return 0; }
+  return r;
+}
+
+bool field_is(PyObject* pkt, const char* key, const char* want) {
+  PyObject* v = field(pkt, key);
+  if (v == nullptr || !PyUnicode_Check(v)) return false;
+  return PyUnicode_CompareWithASCIIString(v, want) == 0;
+}
+
+bool in_state(PyObject* o, const char* st) {
+  PyObject* r = PyObject_CallMethod(o, "isInState", "s", st);
+  if (r == nullptr) { PyErr_Clear(); return false; }
+  const bool b = PyObject_IsTrue(r) == 1;
+  Py_DECREF(r);
+  return b;
+}
+
+// Report an error raised by an owner call without stopping the machine (an
+// exception in a loop callback is reported the same way).
+void report() {
+  if (PyErr_Occurred()) PyErr_WriteUnraisable(nullptr);
+}
+
+void call_void(PyObject* o, const char* name) {
+  PyObject* r = callm(o, name);
+  if (r == nullptr) report();
+  Py_XDECREF(r);
+}
+
+// o.log.<level>(fmt, *args) — the owner's bunyan-shaped logger
+void logv(PyObject* owner, const char* level, PyObject* args) {
+  PyObject* log = attr(owner, "log");
+  if (log == nullptr) return;
+  PyObject* fn = attr(log, level);
+  Py_DECREF(log);
+  if (fn == nullptr) return;
+  PyObject* r = PyObject_CallObject(fn, args);
+  Py_DECREF(fn);
+  if (r == nullptr) report();
+  Py_XDECREF(r);
+}
+
+uint64_t u64(int64_t v) { return (uint64_t)v; }
+
+// conn.server[key] (new ref; None when missing) — a connection's backend
+PyObject* server_of(PyObject* conn, const char* key) {
+  if (conn == nullptr) return Py_NewRef(Py_None);
+  PyObject* sv = attr(conn, "server");
+  PyObject* v = sv != nullptr && PyDict_Check(sv)
+                    ? PyDict_GetItemString(sv, key) : nullptr;
+  Py_XINCREF(v);
+  Py_XDECREF(sv);
+  return v != nullptr ? v : Py_NewRef(Py_None);
+}
+
+// ---- machine base -----------------------------------------------------------
+
+struct Machine;
+
+using EnterFn = void (*)(Machine*, int);
+using EventFn = void (*)(Machine*, int, PyObject*, PyObject*);
+
+struct Spec {
+  const char* const* names;
+  int n;
+  EnterFn enter;
+  EventFn event;
+};
+
+// one subscription of a Relay to an emitter
+struct Sub {
+  PyObject* src;      // the emitter
+  PyObject* evt;      // event name (str)
+  PyObject* relay;
+};
+
+struct Machine {
+  PyObject_HEAD
+  const Spec* spec;
+  PyObject* owner;
+  PyObject* loop;
+  int state;                    // -1 before the first transition
+  std::vector<int>* queue;
+  std::vector<Sub>* subs;
+  std::vector<int>* history;
+  PyObject* entered;            // owner._fsm_entered or nullptr
+  bool busy;
+  bool pending;                 // the current state asked for a transition
+  int64_t transitions;
+  // per-kind scratch
+  PyObject* peer;               // connection: its socket
+  PyObject* ping_iv;            // connection: the ping interval's loop handle
+  PyObject* close_xid;          // connection: CLOSE_SESSION xid (closing)
+  int close_n;                  // client: teardown parts done
+};
+
+PyTypeObject MachineType = {PyVarObject_HEAD_INIT(nullptr, 0)};
+PyTypeObject RelayType = {PyVarObject_HEAD_INIT(nullptr, 0)};
+
+// A Relay is subscribed to one emitter event and hands it to its machine as
+// (kind, source, args).
+struct Relay {
+  PyObject_HEAD
+  Machine* m;                   // strong ref
+  PyObject* src;                // strong ref
+  int kind;
+};
+
+void request(Machine* m, int st);
+
+PyObject* Relay_call(Relay* r, PyObject* args, PyObject*) {
+  Machine* m = r->m;
+  if (m == nullptr || m->state < 0) Py_RETURN_NONE;
+  if (m->pending) Py_RETURN_NONE;     // the state already chose its exit
+  Py_INCREF(m);
+  m->spec->event(m, r->kind, r->src, args);
+  Py_DECREF(m);
+  if (PyErr_Occurred()) return nullptr;
+  Py_RETURN_NONE;
+}
+
+int Relay_traverse(Relay* r, visitproc visit, void* arg) {
+  Py_VISIT((PyObject*)r->m);
+  Py_VISIT(r->src);
+  return 0;
+}
+
+int Relay_clear(Relay* r) {
+  Py_CLEAR(r->m);
+  Py_CLEAR(r->src);
+  return 0;
+}
+
+void Relay_dealloc(Relay* r) {
+  PyObject_GC_UnTrack(r);
+  Relay_clear(r);
+  PyObject_GC_Del(r);
+}
+
+// Subscribe (src, evt) -> kind unless already subscribed.
+int subscribe(Machine* m, PyObject* src, const char* evt, int kind) {
+  for (auto& s : *m->subs)
+    if (s.src == src && PyUnicode_CompareWithASCIIString(s.evt, evt) == 0)
+      return 0;
+  Relay* r = PyObject_GC_New(Relay, &RelayType);
+  if (r == nullptr) return -1;
+  Py_INCREF(m);
+  r->m = m;
+  Py_INCREF(src);
+  r->src = src;
+  r->kind = kind;
+  PyObject_GC_Track((PyObject*)r);
+  PyObject* e = PyUnicode_FromString(evt);
+  PyObject* res = e ? PyObject_CallMethod(src, "on", "OO", e, (PyObject*)r)
+                    : nullptr;
+  if (res == nullptr) {
+    Py_XDECREF(e);
+    Py_DECREF(r);
+    return -1;
+  }
+  Py_DECREF(res);
+  Py_INCREF(src);
+  m->subs->push_back(Sub{src, e, (PyObject*)r});
+  return 0;
+}
+
+// Drop every subscription whose emitter is not in keep[0..nk).
+void unsubscribe_others(Machine* m, PyObject* const* keep, int nk) {
+  std::vector<Sub> drop;
+  std::vector<Sub> stay;
+  for (auto& s : *m->subs) {
+    bool k = false;
+    for (int i = 0; i < nk; ++i) k = k || (keep[i] != nullptr && keep[i] == s.src);
+    (k ? stay : drop).push_back(s);
+  }
+  m->subs->swap(stay);
+  for (auto& s : drop) {
+    PyObject* r = PyObject_CallMethod(s.src, "removeListener", "OO", s.evt,
+                                      s.relay);
+    if (r == nullptr) report();
+    Py_XDECREF(r);
+    Py_DECREF(s.src);
+    Py_DECREF(s.evt);
+    Py_DECREF(s.relay);
+  }
+}
+
+// Enter state `st`: entry action, stateChanged, the owner's hook.
+void enter(Machine* m, int st) {
+  m->state = st;
+  m->pending = false;
+  ++m->transitions;
+  if (m->history->size() > 64)
+    m->history->erase(m->history->begin(), m->history->begin() + 32);
+  m->history->push_back(st);
+  m->spec->enter(m, st);
+  if (PyErr_Occurred()) report();
+  PyObject* name = PyUnicode_FromString(m->spec->names[st]);
+  if (name == nullptr) { report(); return; }
+  PyObject* r = PyObject_CallMethod(m->owner, "emit", "sO", "stateChanged",
+                                    name);
+  if (r == nullptr) report();
+  Py_XDECREF(r);
+  if (m->entered != nullptr) {
+    r = PyObject_CallOneArg(m->entered, name);
+    if (r == nullptr) report();
+    Py_XDECREF(r);
+  }
+  Py_DECREF(name);
+}
+
+void request(Machine* m, int st) {
+  m->queue->push_back(st);
+  m->pending = true;
+  if (m->busy) return;
+  m->busy = true;
+  Py_INCREF(m);
+  while (!m->queue->empty()) {
+    const int nxt = m->queue->front();
+    m->queue->erase(m->queue->begin());
+    enter(m, nxt);
+  }
+  m->busy = false;
+  Py_DECREF(m);
+}
+
+// ---- the session ------------------------------------------------------------
+// lib/zk-session.js:38-375.  Peers: owner.conn (and owner.old_conn while a
+// move is in flight); the owner keeps them as attributes the rest of the
+// client reads.
+
+enum { S_DETACHED, S_ATTACHING, S_ATTACHED, S_REATTACHING, S_CLOSING,
+       S_EXPIRED, S_CLOSED, S_N };
+const char* const S_NAMES[] = {"detached", "attaching", "attached",
+                               "reattaching", "closing", "expired", "closed"};
+// event kinds: user / timer inputs, then a connection's
+enum { SE_ATTACH, SE_CLOSE, SE_EXPIRY, SE_LOST, SE_PACKET, SE_CSTATE };
+
+// the owner's peers as new references (None -> nullptr)
+PyObject* peer(Machine* m, const char* name) {
+  PyObject* c = attr(m->owner, name);
+  if (c == Py_None) { Py_DECREF(c); return nullptr; }
+  return c;
+}
+
+void sess_sync_subs(Machine* m) {
+  PyObject* c = peer(m, "conn");
+  PyObject* o = peer(m, "old_conn");
+  PyObject* exp = attr(m->owner, "expiry");
+  PyObject* keep[3] = {c, o, exp};
+  unsubscribe_others(m, keep, 3);
+  for (PyObject* x : {c, o}) {
+    if (x == nullptr) continue;
+    if (subscribe(m, x, "error", SE_LOST) < 0 ||
+        subscribe(m, x, "close", SE_LOST) < 0 ||
+        subscribe(m, x, "packet", SE_PACKET) < 0 ||
+        subscribe(m, x, "stateChanged", SE_CSTATE) < 0)
+      report();
+  }
+  Py_XDECREF(c);
+  Py_XDECREF(o);
+  Py_XDECREF(exp);
+}
+
+bool sess_alive(Machine* m) {
+  PyObject* r = callm(m->owner, "isAlive");
+  if (r == nullptr) { report(); return false; }
+  const bool b = PyObject_IsTrue(r) == 1;
+  Py_DECREF(r);
+  return b;
+}
+
+// drop the current connection (destroyed) and the expiry
+void sess_drop_conn(Machine* m) {
+  PyObject* c = peer(m, "conn");
+  if (c != nullptr) {
+    call_void(c, "destroy");
+    Py_DECREF(c);
+  }
+  set_attr(m->owner, "conn", Py_None);
+}
+
+void sess_send_cr(Machine* m, PyObject* conn) {
+  PyObject* cr = callm(m->owner, "_connect_request");
+  if (cr == nullptr) { report(); return; }
+  PyObject* r = PyObject_CallMethod(conn, "send", "O", cr);
+  Py_DECREF(cr);
+  if (r == nullptr) report();
+  Py_XDECREF(r);
+}
+
+// A ConnectResponse with a live session id: adopt timeout / id / password.
+void sess_adopt(Machine* m, PyObject* pkt) {
+  PyObject* to = field(pkt, "timeOut");
+  PyObject* sid = field(pkt, "sessionId");
+  PyObject* pw = field(pkt, "passwd");
+  if (to) set_attr(m->owner, "timeout", to);
+  if (sid) set_attr(m->owner, "session_id", sid);
+  if (pw) set_attr(m->owner, "passwd", pw);
+  call_void(m->owner, "resetExpiryTimer");
+}
+
+void sess_enter(Machine* m, int st) {
+  PyObject* ow = m->owner;
+  switch (st) {
+    case S_DETACHED:
+      sess_drop_conn(m);
+      call_void(ow, "watchersDisconnected");
+      break;
+    case S_ATTACHING: {
+      PyObject* c = peer(m, "conn");
+      if (c != nullptr) {
+        sess_sync_subs(m);
+        sess_send_cr(m, c);
+        Py_DECREF(c);
+      }
+      break;
+    }
+    case S_ATTACHED: {
+      PyObject* t = PyFloat_FromDouble((double)time(nullptr));
+      if (t) { set_attr(ow, "last_attach", t); Py_DECREF(t); }
+      break;
+    }
+    case S_REATTACHING: {
+      PyObject* o = peer(m, "old_conn");
+      PyObject* c = peer(m, "conn");
+      if (o == nullptr || c == nullptr) {
+        PyErr_SetString(PyExc_AssertionError, "reattaching requires oldConn");
+        Py_XDECREF(o);
+        Py_XDECREF(c);
+        return;
+      }
+      sess_sync_subs(m);
+      PyObject* args = Py_BuildValue(
+          "(sKNNNN)",
+          "attempting to move zookeeper session %016x from %s:%d to %s:%d",
+          (unsigned long long)u64(attr_i64(ow, "session_id")),
+          server_of(o, "address"),
+          server_of(o, "port"),
+          server_of(c, "address"),
+          server_of(c, "port"));
+      if (args != nullptr) { logv(ow, "debug", args); Py_DECREF(args); }
+      else report();
+      sess_send_cr(m, c);
+      Py_DECREF(o);
+      Py_DECREF(c);
+      break;
+    }
+    case S_CLOSING: {
+      PyObject* c = peer(m, "conn");
+      if (c != nullptr) { call_void(c, "close"); Py_DECREF(c); }
+      break;
+    }
+    case S_EXPIRED:
+    case S_CLOSED: {
+      sess_drop_conn(m);
+      PyObject* ex = attr(ow, "expiry");
+      if (ex) { call_void(ex, "cancel"); Py_DECREF(ex); }
+      PyObject* wt = attr(ow, "wt");
+      if (!is_none(wt)) call_void(wt, "close");
+      Py_XDECREF(wt);
+      PyObject* args = Py_BuildValue(
+          "(s)", st == S_EXPIRED ? "ZK session expired" : "ZK session closed");
+      if (args) { logv(ow, st == S_EXPIRED ? "warn" : "info", args); Py_DECREF(args); }
+      break;
+    }
+  }
+  sess_sync_subs(m);
+}
+
+// The move failed (the new connection refused, lost, or the session's
+// deadline passed while moving): back to the old connection if it still
+// serves, else detach or expire (lib/zk-session.js:298-320).
+void sess_revert(Machine* m) {
+  PyObject* ow = m->owner;
+  PyObject* o = peer(m, "old_conn");
+  PyObject* c = peer(m, "conn");
+  const bool alive = sess_alive(m);
+  if (alive && o != nullptr && in_state(o, "connected")) {
+    PyObject* args = Py_BuildValue(
+        "(sKNNNN)",
+        "reverted move of session %016x (on %s:%d) to new backend (%s:%d)",
+        (unsigned long long)u64(attr_i64(ow, "session_id")),
+        server_of(o, "address"),
+        server_of(o, "port"),
+        server_of(c, "address"),
+        server_of(c, "port"));
+    if (args) { logv(ow, "warn", args); Py_DECREF(args); } else report();
+    set_attr(ow, "conn", o);
+    set_attr(ow, "old_conn", Py_None);
+    request(m, S_ATTACHED);
+  } else if (alive) {
+    if (o) call_void(o, "destroy");
+    request(m, S_DETACHED);
+  } else {
+    if (o) call_void(o, "close");
+    request(m, S_EXPIRED);
+  }
+  Py_XDECREF(o);
+  Py_XDECREF(c);
+}
+
+void sess_event(Machine* m, int kind, PyObject* src, PyObject* args) {
+  PyObject* ow = m->owner;
+  PyObject* a0 = PyTuple_GET_SIZE(args) > 0 ? PyTuple_GET_ITEM(args, 0) : nullptr;
+  PyObject* c = peer(m, "conn");
+  // connection events only from the session's current connection
+  const bool from_conn = kind >= SE_LOST && c != nullptr && src == c;
+  Py_XDECREF(c);
+  if (kind >= SE_LOST && !from_conn) return;
+  switch (m->state) {
+    case S_DETACHED:
+      if (kind == SE_ATTACH && a0 != nullptr) {
+        set_attr(ow, "conn", a0);
+        request(m, S_ATTACHING);
+      } else if (kind == SE_CLOSE) {
+        request(m, S_CLOSED);
+      } else if (kind == SE_EXPIRY) {
+        request(m, S_EXPIRED);
+      }
+      break;
+    case S_ATTACHING:
+      if (kind == SE_LOST) {
+        if (sess_alive(m)) request(m, S_DETACHED);
+        else if (attr_i64(ow, "session_id") != 0) request(m, S_EXPIRED);
+        else request(m, S_DETACHED);
+      } else if (kind == SE_PACKET && a0 != nullptr) {
+        const int64_t sid = field_i64(a0, "sessionId");
+        if (sid == 0) { request(m, S_EXPIRED); break; }
+        const bool resumed = attr_i64(ow, "session_id") != 0;
+        PyObject* la = Py_BuildValue(
+            "(ssKL)", "%s zookeeper session %016x with timeout %d ms",
+            resumed ? "resumed" : "created", (unsigned long long)u64(sid),
+            (long long)field_i64(a0, "timeOut"));
+        if (la) { logv(ow, "info", la); Py_DECREF(la); } else report();
+        // the logger gains the session id (log.child(id=...))
+        PyObject* log = attr(ow, "log");
+        if (log != nullptr) {
+          char buf[20];
+          snprintf(buf, sizeof buf, "%016llx", (unsigned long long)u64(sid));
+          PyObject* child = attr(log, "child");
+          PyObject* kw = Py_BuildValue("{ss}", "id", buf);
+          PyObject* empty = PyTuple_New(0);
+          PyObject* nl = child && kw && empty ? PyObject_Call(child, empty, kw)
+                                              : nullptr;
+          if (nl != nullptr) { set_attr(ow, "log", nl); Py_DECREF(nl); }
+          else report();
+          Py_XDECREF(child); Py_XDECREF(kw); Py_XDECREF(empty);
+          Py_DECREF(log);
+        }
+        sess_adopt(m, a0);
+        request(m, S_ATTACHED);
+      } else if (kind == SE_EXPIRY) {
+        request(m, S_EXPIRED);
+      } else if (kind == SE_CLOSE) {
+        request(m, S_CLOSING);
+      }
+      break;
+    case S_ATTACHED:
+      if (kind == SE_PACKET && a0 != nullptr) {
+        // every packet keeps the session alive; replies carry the zxid the
+        // next ConnectRequest reports, notifications go to the watchers
+        call_void(ow, "resetExpiryTimer");
+        if (!field_is(a0, "opcode", "NOTIFICATION")) {
+          PyObject* z = field(a0, "zxid");
+          if (z != nullptr && PyLong_Check(z) &&
+              PyLong_AsLongLong(z) > attr_i64(ow, "_last_zxid"))
+            set_attr(ow, "_last_zxid", z);
+          if (PyErr_Occurred()) PyErr_Clear();
+        } else {
+          PyObject* r = PyObject_CallMethod(ow, "processNotification", "O", a0);
+          if (r == nullptr) report();
+          Py_XDECREF(r);
+        }
+      } else if (kind == SE_LOST) {
+        request(m, sess_alive(m) ? S_DETACHED : S_EXPIRED);
+      } else if (kind == SE_EXPIRY) {
+        request(m, S_EXPIRED);
+      } else if (kind == SE_CLOSE) {
+        request(m, S_CLOSING);
+      } else if (kind == SE_CSTATE && a0 != nullptr) {
+        if (PyUnicode_Check(a0) &&
+            PyUnicode_CompareWithASCIIString(a0, "connected") == 0) {
+          PyObject* o = peer(m, "old_conn");
+          if (o != nullptr) {
+            call_void(o, "destroy");
+            set_attr(ow, "old_conn", Py_None);
+            Py_DECREF(o);
+            sess_sync_subs(m);
+          }
+          call_void(ow, "resumeWatches");
+        }
+        PyObject* wt = attr(ow, "wt");
+        if (!is_none(wt)) call_void(ow, "_wt_sync");   // (after SET_WATCHES)
+        Py_XDECREF(wt);
+      } else if (kind == SE_ATTACH && a0 != nullptr) {
+        PyObject* cur = peer(m, "conn");
+        set_attr(ow, "old_conn", cur ? cur : Py_None);
+        Py_XDECREF(cur);
+        set_attr(ow, "conn", a0);
+        request(m, S_REATTACHING);
+      }
+      break;
+    case S_REATTACHING:
+      if (kind == SE_PACKET && a0 != nullptr) {
+        const int64_t sid = field_i64(a0, "sessionId");
+        if (sid == 0) { sess_revert(m); break; }
+        // the old connection goes once the new one is 'connected'
+        PyObject* c2 = peer(m, "conn");
+        PyObject* la = Py_BuildValue(
+            "(sKNNL)",
+            "moved zookeeper session %016x to more preferred backend (%s:%d) "
+            "with timeout %d ms",
+            (unsigned long long)u64(sid),
+            server_of(c2, "address"),
+            server_of(c2, "port"),
+            (long long)field_i64(a0, "timeOut"));
+        Py_XDECREF(c2);
+        if (la) { logv(ow, "info", la); Py_DECREF(la); } else report();
+        sess_adopt(m, a0);
+        call_void(ow, "watchersDisconnected");
+        request(m, S_ATTACHED);
+      } else if (kind == SE_LOST || kind == SE_EXPIRY) {
+        sess_revert(m);
+      } else if (kind == SE_CLOSE) {
+        PyObject* o = peer(m, "old_conn");
+        if (o) { call_void(o, "close"); Py_DECREF(o); }
+        request(m, S_CLOSING);
+      }
+      break;
+    case S_CLOSING:
+      if (kind == SE_LOST || kind == SE_EXPIRY) request(m, S_CLOSED);
+      break;
+    default:
+      break;          // expired, closed: final
+  }
+}
+
+const Spec SESSION{S_NAMES, S_N, sess_enter, sess_event};
+
+// ---- Python surface ---------------------------------------------------------
+
+int Machine_traverse(Machine* m, visitproc visit, void* arg) {
+  Py_VISIT(m->owner);
+  Py_VISIT(m->loop);
+  Py_VISIT(m->entered);
+  Py_VISIT(m->peer);
+  Py_VISIT(m->ping_iv);
+  Py_VISIT(m->close_xid);
+  if (m->subs != nullptr)
+    for (auto& s : *m->subs) {
+      Py_VISIT(s.src);
+      Py_VISIT(s.evt);
+      Py_VISIT(s.relay);
+    }
+  return 0;
+}
+
+int Machine_clear(Machine* m) {
+  if (m->subs != nullptr) {
+    std::vector<Sub> ss;
+    ss.swap(*m->subs);
+    for (auto& s : ss) {
+      Py_XDECREF(s.src);
+      Py_XDECREF(s.evt);
+      Py_XDECREF(s.relay);
+    }
+  }
+  Py_CLEAR(m->owner);
+  Py_CLEAR(m->loop);
+  Py_CLEAR(m->entered);
+  Py_CLEAR(m->peer);
+  Py_CLEAR(m->ping_iv);
+  Py_CLEAR(m->close_xid);
+  return 0;
+}
+
+void Machine_dealloc(Machine* m) {
+  PyObject_GC_UnTrack(m);
+  Machine_clear(m);
+  delete m->queue;
+  delete m->subs;
+  delete m->history;
+  PyObject_GC_Del(m);
+}
+
+const Spec* spec_of(const char* kind) {
+  if (strcmp(kind, "session") == 0) return &SESSION;
+  return nullptr;
+}
+
+// Machine(kind, owner, loop): not started (start(initial) enters the first
+// state, so the owner can finish its constructor first).
+PyObject* Machine_new(PyTypeObject*, PyObject* args, PyObject*) {
+  const char* kind;
+  PyObject *owner, *loop;
+  if (!PyArg_ParseTuple(args, "sOO", &kind, &owner, &loop)) return nullptr;
+  const Spec* sp = spec_of(kind);
+  if (sp == nullptr) {
+    PyErr_Format(PyExc_ValueError, "unknown machine %s", kind);
+    return nullptr;
+  }
+  Machine* m = PyObject_GC_New(Machine, &MachineType);
+  if (m == nullptr) return nullptr;
+  m->spec = sp;
+  Py_INCREF(owner);
+  m->owner = owner;
+  Py_INCREF(loop);
+  m->loop = loop;
+  m->state = -1;
+  m->queue = new std::vector<int>();
+  m->subs = new std::vector<Sub>();
+  m->history = new std::vector<int>();
+  m->entered = PyObject_GetAttrString(owner, "_fsm_entered");
+  if (m->entered == nullptr) PyErr_Clear();
+  m->busy = m->pending = false;
+  m->transitions = 0;
+  m->peer = m->ping_iv = m->close_xid = nullptr;
+  m->close_n = 0;
+  PyObject_GC_Track((PyObject*)m);
+  return (PyObject*)m;
+}
+
+int state_index(Machine* m, PyObject* name) {
+  if (!PyUnicode_Check(name)) return -1;
+  for (int i = 0; i < m->spec->n; ++i)
+    if (PyUnicode_CompareWithASCIIString(name, m->spec->names[i]) == 0)
+      return i;
+  return -1;
+}
+
+PyObject* Machine_start(Machine* m, PyObject* name) {
+  const int st = state_index(m, name);
+  if (st < 0 || m->state >= 0) {
+    PyErr_SetString(PyExc_ValueError, "start: unknown state or started");
+    return nullptr;
+  }
+  request(m, st);
+  if (PyErr_Occurred()) return nullptr;
+  Py_RETURN_NONE;
+}
+
+// fire(kind, *args): an input that is not an emitter event (the owner's API
+// calls: attach, close; a source of None)
+PyObject* Machine_fire(Machine* m, PyObject* args) {
+  if (PyTuple_GET_SIZE(args) < 1) {
+    PyErr_SetString(PyExc_TypeError, "fire(kind, *args)");
+    return nullptr;
+  }
+  const long kind = PyLong_AsLong(PyTuple_GET_ITEM(args, 0));
+  if (kind == -1 && PyErr_Occurred()) return nullptr;
+  if (m->state < 0 || m->pending) Py_RETURN_NONE;
+  PyObject* rest = PyTuple_GetSlice(args, 1, PyTuple_GET_SIZE(args));
+  if (rest == nullptr) return nullptr;
+  Py_INCREF(m);
+  m->spec->event(m, (int)kind, Py_None, rest);
+  Py_DECREF(m);
+  Py_DECREF(rest);
+  if (PyErr_Occurred()) return nullptr;
+  Py_RETURN_NONE;
+}
+
+// watch(emitter, evt, kind): subscribe a relay (the owner's fixed inputs,
+// e.g. the session's expiry timer)
+PyObject* Machine_watch(Machine* m, PyObject* args) {
+  PyObject* em;
+  const char* evt;
+  int kind;
+  if (!PyArg_ParseTuple(args, "Osi", &em, &evt, &kind)) return nullptr;
+  if (subscribe(m, em, evt, kind) < 0) return nullptr;
+  Py_RETURN_NONE;
+}
+
+PyObject* Machine_in_state(Machine* m, PyObject* name) {
+  if (m->state < 0) Py_RETURN_FALSE;
+  return PyBool_FromLong(PyUnicode_Check(name) &&
+                         PyUnicode_CompareWithASCIIString(
+                             name, m->spec->names[m->state]) == 0);
+}
+
+PyObject* Machine_get_state(Machine* m, void*) {
+  if (m->state < 0) Py_RETURN_NONE;
+  return PyUnicode_FromString(m->spec->names[m->state]);
+}
+
+PyObject* Machine_get_history(Machine* m, void*) {
+  PyObject* l = PyList_New((Py_ssize_t)m->history->size());
+  if (l == nullptr) return nullptr;
+  for (size_t i = 0; i < m->history->size(); ++i)
+    PyList_SET_ITEM(l, (Py_ssize_t)i,
+                    PyUnicode_FromString(m->spec->names[(*m->history)[i]]));
+  return l;
+}
+
+PyObject* Machine_get_subs(Machine* m, void*) {
+  return PyLong_FromSize_t(m->subs->size());
+}
+
+PyObject* Machine_get_transitions(Machine* m, void*) {
+  return PyLong_FromLongLong(m->transitions);
+}
+
+PyMethodDef Machine_methods[] = {
+    {"start", (PyCFunction)Machine_start, METH_O, "start(state)"},
+    {"fire", (PyCFunction)Machine_fire, METH_VARARGS, "fire(kind, *args)"},
+    {"watch", (PyCFunction)Machine_watch, METH_VARARGS,
+     "watch(emitter, evt, kind)"},
+    {"in_state", (PyCFunction)Machine_in_state, METH_O, "in_state(name)"},
+    {nullptr, nullptr, 0, nullptr}};
+
+PyGetSetDef Machine_getset[] = {
+    {"state", (getter)Machine_get_state, nullptr, "current state", nullptr},
+    {"history", (getter)Machine_get_history, nullptr, "recent states",
+     nullptr},
+    {"subscriptions", (getter)Machine_get_subs, nullptr,
+     "relays subscribed", nullptr},
+    {"transitions", (getter)Machine_get_transitions, nullptr,
+     "transitions so far", nullptr},
+    {nullptr, nullptr, nullptr, nullptr, nullptr}};
+
+PyModuleDef module = {PyModuleDef_HEAD_INIT, "_zkmach",
+                      "the client's state machines (session, connection, "
+                      "client) in C++", -1, nullptr};
+
+}  // namespace
+
+PyMODINIT_FUNC PyInit__zkmach() {
+  MachineType.tp_name = "zkmi._zkmach.Machine";
+  MachineType.tp_basicsize = sizeof(Machine);
+  MachineType.tp_flags = Py_TPFLAGS_DEFAULT | Py_TPFLAGS_HAVE_GC;
+  MachineType.tp_traverse = (traverseproc)Machine_traverse;
+  MachineType.tp_clear = (inquiry)Machine_clear;
+  MachineType.tp_dealloc = (destructor)Machine_dealloc;
+  MachineType.tp_methods = Machine_methods;
+  MachineType.tp_getset = Machine_getset;
+  MachineType.tp_new = Machine_new;
+  RelayType.tp_name = "zkmi._zkmach.Relay";
+  RelayType.tp_basicsize = sizeof(Relay);
+  RelayType.tp_flags = Py_TPFLAGS_DEFAULT | Py_TPFLAGS_HAVE_GC;
+  RelayType.tp_traverse = (traverseproc)Relay_traverse;
+  RelayType.tp_clear = (inquiry)Relay_clear;
+  RelayType.tp_dealloc = (destructor)Relay_dealloc;
+  RelayType.tp_call = (ternaryfunc)Relay_call;
+  if (PyType_Ready(&MachineType) < 0 || PyType_Ready(&RelayType) < 0)
+    return nullptr;
+  PyObject* m = PyModule_Create(&module);
+  if (m == nullptr) return nullptr;
+  Py_INCREF(&MachineType);
+  if (PyModule_AddObject(m, "Machine", (PyObject*)&MachineType) < 0)
+    return nullptr;
+  // the session's input kinds (Machine.fire / watch)
+  PyModule_AddIntConstant(m, "SE_ATTACH", SE_ATTACH);
+  PyModule_AddIntConstant(m, "SE_CLOSE", SE_CLOSE);
+  PyModule_AddIntConstant(m, "SE_EXPIRY", SE_EXPIRY);
+  return m;
+}

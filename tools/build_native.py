@@ -139,7 +139,8 @@ def _ext_path(name):
 HOST_EXTS = {'_zkhost': 'zk_host_codec.cpp',     # Jute host codec
              '_zkloop': 'zk_loop.cpp',           # epoll event loop
              '_zkwatch': 'zk_watch.cpp',         # watch-event engine
-             '_zkfsm': 'zk_fsm.cpp'}             # FSM runtime
+             '_zkfsm': 'zk_fsm.cpp',             # FSM runtime
+             '_zkmach': 'zk_machines.cpp'}       # session / connection / client machines
 
 
 FAST_SERVER = os.path.join(ROOT, 'zkmi', 'bin', 'zk_fastserver')

@@ -25,6 +25,11 @@ try:
     from .. import _zkwatch
 except ImportError:                      # not built: the Python FSMs
     _zkwatch = None
+try:                                     # the native machines
+    from .. import _zkmach
+except ImportError:
+    _zkmach = None
+from ..runtime import fsm as _fsm
 from ..runtime.fsm import FSM
 from ..utils.metrics import METRIC_ZK_NOTIFICATION_COUNTER
 
@@ -93,7 +98,22 @@ def _camel(evt_type):
     return c
 
 
-class ZKSession(FSM):
+def native_machines():
+    """True when new sessions / connections / clients run on the C++
+    machines (csrc/host/zk_machines.cpp); ``ZKMI_PY_FSM=1`` selects the
+    Python state functions below, kept as the test oracle."""
+    return _zkmach is not None and _fsm.native()
+
+
+def ZKSession(timeout, log, collector, loop, config):
+    """The session: the native machine, or the Python oracle."""
+    cls = NativeZKSession if native_machines() else PyZKSession
+    return cls(timeout, log, collector, loop, config)
+
+
+class _SessionBase(object):
+    """What the session is besides its state graph: credentials, liveness,
+    the watch registry and dispatch, SET_WATCHES resume."""
 
     def __init__(self, timeout, log, collector, loop, config):
         self.conn = None
@@ -126,7 +146,6 @@ class ZKSession(FSM):
             self.wt = _zkwatch.WatchTable(self._wt_emit, loop,
                                           float(config.doublecheck_ms),
                                           float(config.doublecheck_rand_ms))
-        FSM.__init__(self, 'detached', loop)
 
     def _fsm_entered(self, state):
         # after every transition (the FSM runtime's hook)
@@ -189,13 +208,6 @@ class ZKSession(FSM):
                     last_rx_ms + ex.timeout_ms > ex.deadline:
                 ex.deadline = last_rx_ms + ex.timeout_ms
 
-    def attachAndSendCR(self, conn):
-        if not self.isInState('detached') and not self.isInState('attached'):
-            raise Exception('ZKSession#attachAndSendCR may only be called in '
-                            'state "attached" or "detached" (is in %s)'
-                            % self.getState())
-        self.emit('assertAttach', conn)
-
     def resetExpiryTimer(self):
         self.last_pkt = time.monotonic()
         self.expiry.reset(self.timeout)
@@ -227,13 +239,148 @@ class ZKSession(FSM):
         self.timeout = cred.get('timeout', self.timeout)
         self.last_pkt = time.monotonic()
 
-    def close(self):
-        self.emit('closeAsserted')
-
     def _connect_request(self):
         return {'protocolVersion': 0, 'lastZxidSeen': self.last_zxid,
                 'timeOut': self.timeout, 'sessionId': self.session_id,
                 'passwd': self.passwd}
+
+    # -- watches --------------------------------------------------------------
+
+    def watchersDisconnected(self):
+        if self.wt is not None:
+            self.wt.disconnected()
+        for w in list(self.watchers.values()):
+            for ev in w.events():
+                ev.disconnected()
+
+    def _wt_emit(self, path, evt, *args):
+        """The native engine's user-visible events, to the path's
+        ZKWatcher listeners."""
+        w = self.watchers.get(path)
+        if w is not None:
+            EventEmitter.emit(w, evt, *args)
+
+    def _wt_sync(self):
+        """Tell the native engine whether watch requests can go out: the
+        session attached and its connection connected (the reference's
+        wait_session / wait_connected)."""
+        wt = self.wt
+        conn = self.conn
+        if self.isInState('attached') and conn is not None and \
+                conn.isInState('connected'):
+            wt.ready(conn)
+        else:
+            wt.unready()
+
+    def processNotification(self, pkt):
+        if pkt['state'] != 'SYNC_CONNECTED':
+            self.log.warn({'xid': pkt['xid'], 'state': pkt['state'],
+                           'type': pkt['type']},
+                          'received notification with bad state %s',
+                          pkt['state'])
+            return
+        watcher = self.watchers.get(pkt['path'])
+        evt = _camel(pkt['type'])
+        self.log.trace({'zxid': pkt['zxid'], 'type': pkt['type']},
+                       'notification %s for %s', evt, pkt['path'])
+        self.collector.getCollector(METRIC_ZK_NOTIFICATION_COUNTER) \
+            .increment({'event': evt})
+        if watcher is not None:
+            watcher.notify(evt)
+
+    def resumeWatches(self):
+        events = {'dataChanged': [], 'createdOrDestroyed': [],
+                  'childrenChanged': []}
+        count = 0
+        all_evts = []
+        for path, w in list(self.watchers.items()):
+            cod = False
+            for ev in w.events():
+                if isinstance(ev, _NativeWatchEvent) or \
+                        not ev.isInState('resuming'):
+                    continue               # (the engine's: resume_lists)
+                e = ev.getEvent()
+                if e == 'createdOrDeleted':
+                    if cod:
+                        continue
+                    events['createdOrDestroyed'].append(path)
+                    cod = True
+                elif e == 'dataChanged':
+                    events['dataChanged'].append(path)
+                elif e == 'childrenChanged':
+                    events['childrenChanged'].append(path)
+                else:
+                    raise AssertionError('unknown event: ' + e)
+                count += 1
+                all_evts.append(ev)
+        batch = None
+        if self.wt is not None:
+            batch, dw, ew, cw = self.wt.resume_lists()
+            events['dataChanged'] += dw
+            events['createdOrDestroyed'] += ew
+            events['childrenChanged'] += cw
+            count += len(dw) + len(ew) + len(cw)
+        if self.bulk_watches:
+            events['dataChanged'] = events['dataChanged'] + self._bulk_packed
+            count += self._bulk_packed.n
+        if count < 1:
+            return
+        zxid = self.last_zxid
+        self.log.info('re-arming %d node watchers at zxid %x', count, zxid)
+        self.rearmed += count
+        if len(self.resumes) < 64:
+            self.resumes.append((zxid, count))
+
+        def done(err):
+            if err is not None:
+                # The reference emits 'pingTimeout' on the session here,
+                # which nothing listens to (SURVEY Appendix C-6).  The events
+                # stay in 'resuming' and are re-sent on the next attach.
+                self.log.warn(err, 'SET_WATCHES failed; will retry on '
+                              'next attach')
+                return
+            for ev in all_evts:
+                ev.resume()
+            if batch is not None:
+                self.wt.resumed(batch)
+        self.conn.setWatches(events, zxid, done)
+
+    def add_bulk_watches(self, paths):
+        """Paths watched in bulk (:meth:`~zkmi.models.client.Client.
+        watch_bulk`): every resume re-arms them with the session's other
+        watches."""
+        new = [p for p in dict.fromkeys(paths) if p not in self.bulk_watches]
+        if not new:
+            return
+        self.bulk_watches.update(new)
+        self._bulk_packed = (self._bulk_packed or jute.PackedStrings()) + new
+
+    def watcher(self, path):
+        w = self.watchers.get(path)
+        if w is None:
+            w = ZKWatcher(self, path, self.log)
+            self.watchers[path] = w
+        return w
+
+
+class PyZKSession(_SessionBase, FSM):
+    """The session's state graph as mooremachine-style state functions
+    (``lib/zk-session.js:38-375``): the test oracle of the native machine
+    (``ZKMI_PY_FSM=1``)."""
+
+    def __init__(self, timeout, log, collector, loop, config):
+        _SessionBase.__init__(self, timeout, log, collector, loop, config)
+        FSM.__init__(self, 'detached', loop)
+
+    def attachAndSendCR(self, conn):
+        if not self.isInState('detached') and not self.isInState('attached'):
+            raise Exception('ZKSession#attachAndSendCR may only be called in '
+                            'state "attached" or "detached" (is in %s)'
+                            % self.getState())
+        self.emit('assertAttach', conn)
+
+    def close(self):
+        self.emit('closeAsserted')
 
     # -- states ---------------------------------------------------------------
 
@@ -403,123 +550,42 @@ class ZKSession(FSM):
             self.wt.close()
         self.log.info('ZK session closed')
 
-    # -- watches --------------------------------------------------------------
 
-    def watchersDisconnected(self):
-        if self.wt is not None:
-            self.wt.disconnected()
-        for w in list(self.watchers.values()):
-            for ev in w.events():
-                ev.disconnected()
+class NativeZKSession(_SessionBase, EventEmitter):
+    """The session on the C++ machine (``_zkmach.Machine('session')``,
+    csrc/host/zk_machines.cpp): its transitions, guards and entry actions
+    run there; this object keeps the API, the listener surface and the
+    watch registry."""
 
-    def _wt_emit(self, path, evt, *args):
-        """The native engine's user-visible events, to the path's
-        ZKWatcher listeners."""
-        w = self.watchers.get(path)
-        if w is not None:
-            EventEmitter.emit(w, evt, *args)
+    def __init__(self, timeout, log, collector, loop, config):
+        EventEmitter.__init__(self)
+        _SessionBase.__init__(self, timeout, log, collector, loop, config)
+        self.fsm_loop = loop
+        self._m = _zkmach.Machine('session', self, loop)
+        self._m.watch(self.expiry, 'timeout', _zkmach.SE_EXPIRY)
+        self._m.start('detached')
 
-    def _wt_sync(self):
-        """Tell the native engine whether watch requests can go out: the
-        session attached and its connection connected (the reference's
-        wait_session / wait_connected)."""
-        wt = self.wt
-        conn = self.conn
-        if self.isInState('attached') and conn is not None and \
-                conn.isInState('connected'):
-            wt.ready(conn)
-        else:
-            wt.unready()
+    def getState(self):
+        return self._m.state
 
-    def processNotification(self, pkt):
-        if pkt['state'] != 'SYNC_CONNECTED':
-            self.log.warn({'xid': pkt['xid'], 'state': pkt['state'],
-                           'type': pkt['type']},
-                          'received notification with bad state %s',
-                          pkt['state'])
-            return
-        watcher = self.watchers.get(pkt['path'])
-        evt = _camel(pkt['type'])
-        self.log.trace({'zxid': pkt['zxid'], 'type': pkt['type']},
-                       'notification %s for %s', evt, pkt['path'])
-        self.collector.getCollector(METRIC_ZK_NOTIFICATION_COUNTER) \
-            .increment({'event': evt})
-        if watcher is not None:
-            watcher.notify(evt)
+    _fsm_state = property(getState)
 
-    def resumeWatches(self):
-        events = {'dataChanged': [], 'createdOrDestroyed': [],
-                  'childrenChanged': []}
-        count = 0
-        all_evts = []
-        for path, w in list(self.watchers.items()):
-            cod = False
-            for ev in w.events():
-                if isinstance(ev, _NativeWatchEvent) or \
-                        not ev.isInState('resuming'):
-                    continue               # (the engine's: resume_lists)
-                e = ev.getEvent()
-                if e == 'createdOrDeleted':
-                    if cod:
-                        continue
-                    events['createdOrDestroyed'].append(path)
-                    cod = True
-                elif e == 'dataChanged':
-                    events['dataChanged'].append(path)
-                elif e == 'childrenChanged':
-                    events['childrenChanged'].append(path)
-                else:
-                    raise AssertionError('unknown event: ' + e)
-                count += 1
-                all_evts.append(ev)
-        batch = None
-        if self.wt is not None:
-            batch, dw, ew, cw = self.wt.resume_lists()
-            events['dataChanged'] += dw
-            events['createdOrDestroyed'] += ew
-            events['childrenChanged'] += cw
-            count += len(dw) + len(ew) + len(cw)
-        if self.bulk_watches:
-            events['dataChanged'] = events['dataChanged'] + self._bulk_packed
-            count += self._bulk_packed.n
-        if count < 1:
-            return
-        zxid = self.last_zxid
-        self.log.info('re-arming %d node watchers at zxid %x', count, zxid)
-        self.rearmed += count
-        if len(self.resumes) < 64:
-            self.resumes.append((zxid, count))
+    def isInState(self, state):
+        return self._m.in_state(state)
 
-        def done(err):
-            if err is not None:
-                # The reference emits 'pingTimeout' on the session here,
-                # which nothing listens to (SURVEY Appendix C-6).  The events
-                # stay in 'resuming' and are re-sent on the next attach.
-                self.log.warn(err, 'SET_WATCHES failed; will retry on '
-                              'next attach')
-                return
-            for ev in all_evts:
-                ev.resume()
-            if batch is not None:
-                self.wt.resumed(batch)
-        self.conn.setWatches(events, zxid, done)
+    @property
+    def fsm_history(self):
+        return self._m.history
 
-    def add_bulk_watches(self, paths):
-        """Paths watched in bulk (:meth:`~zkmi.models.client.Client.
-        watch_bulk`): every resume re-arms them with the session's other
-        watches."""
-        new = [p for p in dict.fromkeys(paths) if p not in self.bulk_watches]
-        if not new:
-            return
-        self.bulk_watches.update(new)
-        self._bulk_packed = (self._bulk_packed or jute.PackedStrings()) + new
+    def attachAndSendCR(self, conn):
+        if not self.isInState('detached') and not self.isInState('attached'):
+            raise Exception('ZKSession#attachAndSendCR may only be called in '
+                            'state "attached" or "detached" (is in %s)'
+                            % self.getState())
+        self._m.fire(_zkmach.SE_ATTACH, conn)
 
-    def watcher(self, path):
-        w = self.watchers.get(path)
-        if w is None:
-            w = ZKWatcher(self, path, self.log)
-            self.watchers[path] = w
-        return w
+    def close(self):
+        self._m.fire(_zkmach.SE_CLOSE)
 
 
 class ZKWatcher(EventEmitter):

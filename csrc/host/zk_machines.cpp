@@ -613,6 +613,379 @@ void sess_event(Machine* m, int kind, PyObject* src, PyObject* args) {
 
 const Spec SESSION{S_NAMES, S_N, sess_enter, sess_event};
 
+// ---- the connection ---------------------------------------------------------
+// lib/connection-fsm.js:27-351.  Peers: owner.socket (its TcpSocket) and
+// owner.session (the session it handshakes for).  The Python shell keeps
+// the byte plumbing that belongs to the transport (the decoder, bulk
+// batches, bulk notification capture, the native reply router) behind
+// _fx_* / _rx_* effect methods; the states, guards, timers and the close
+// handshake are here.
+
+enum { C_INIT, C_CONNECTING, C_HANDSHAKING, C_CONNECTED, C_CLOSING, C_ERROR,
+       C_CLOSED, C_N };
+const char* const C_NAMES[] = {"init", "connecting", "handshaking",
+                               "connected", "closing", "error", "closed"};
+enum {
+  // the owner's inputs (Machine.fire)
+  CE_CONNECT, CE_CLOSE, CE_DESTROY, CE_UNWANTED, CE_RX, CE_RXERR,
+  CE_PING_TIMEOUT, CE_BULKDONE,
+  // relays: the socket's events, the session's state, timers
+  CE_SOCK_CONNECT, CE_SOCK_ERROR, CE_SOCK_END, CE_SOCK_CLOSE, CE_SESS_STATE,
+  CE_PING_TICK, CE_IMM
+};
+
+// A timer whose callback is a relay of `kind` (src None); new ref to the
+// loop's handle.  ms < 0: call_soon.
+PyObject* schedule(Machine* m, double ms, int kind) {
+  Relay* r = PyObject_GC_New(Relay, &RelayType);
+  if (r == nullptr) return nullptr;
+  Py_INCREF(m);
+  r->m = m;
+  r->src = Py_NewRef(Py_None);
+  r->kind = kind;
+  PyObject_GC_Track((PyObject*)r);
+  PyObject* h = ms < 0 ? PyObject_CallMethod(m->loop, "call_soon", "O",
+                                             (PyObject*)r)
+                       : PyObject_CallMethod(m->loop, "call_later", "dO", ms,
+                                             (PyObject*)r);
+  Py_DECREF(r);
+  return h;
+}
+
+void cancel(PyObject*& h) {
+  if (h == nullptr) return;
+  PyObject* r = callm(h, "cancel");
+  if (r == nullptr) report();
+  Py_XDECREF(r);
+  Py_CLEAR(h);
+}
+
+void conn_sync_subs(Machine* m) {
+  PyObject* sock = peer(m, "socket");
+  // the session's state matters only while handshaking (its 'attached')
+  PyObject* sess = m->state == C_HANDSHAKING ? peer(m, "session") : nullptr;
+  PyObject* keep[2] = {sock, sess};
+  unsubscribe_others(m, keep, 2);
+  if (sock != nullptr &&
+      (subscribe(m, sock, "connect", CE_SOCK_CONNECT) < 0 ||
+       subscribe(m, sock, "error", CE_SOCK_ERROR) < 0 ||
+       subscribe(m, sock, "end", CE_SOCK_END) < 0 ||
+       subscribe(m, sock, "close", CE_SOCK_CLOSE) < 0))
+    report();
+  if (sess != nullptr && subscribe(m, sess, "stateChanged", CE_SESS_STATE) < 0)
+    report();
+  Py_XDECREF(sock);
+  Py_XDECREF(sess);
+}
+
+// owner.last_error = owner._proto_error(code, msg)
+void conn_fail_with(Machine* m, const char* code, const char* msg) {
+  PyObject* e = PyObject_CallMethod(m->owner, "_proto_error", "ss", code, msg);
+  if (e == nullptr) { report(); return; }
+  set_attr(m->owner, "last_error", e);
+  Py_DECREF(e);
+}
+
+void conn_set_error(Machine* m, PyObject* err) {
+  set_attr(m->owner, "last_error", err != nullptr ? err : Py_None);
+}
+
+bool conn_drained(Machine* m) {
+  PyObject* reqs = attr(m->owner, "reqs");
+  PyObject* bulks = attr(m->owner, "bulks");
+  const bool d = (reqs == nullptr || PyObject_Length(reqs) < 1) &&
+                 (bulks == nullptr || PyObject_Length(bulks) < 1);
+  if (PyErr_Occurred()) PyErr_Clear();
+  Py_XDECREF(reqs);
+  Py_XDECREF(bulks);
+  return d;
+}
+
+// CLOSE_SESSION once, when nothing is outstanding (lib/connection-fsm.js
+// closing state)
+void conn_send_close(Machine* m) {
+  if (m->close_xid != nullptr) return;
+  PyObject* x = callm(m->owner, "nextXid");
+  if (x == nullptr) { report(); return; }
+  m->close_xid = x;
+  PyObject* r = PyObject_CallMethod(m->owner, "_fx_send_close", "O", x);
+  if (r == nullptr) report();
+  Py_XDECREF(r);
+}
+
+double conn_ping_interval(Machine* m) {
+  PyObject* sess = peer(m, "session");
+  PyObject* cfg = attr(m->owner, "config");
+  double T = 0, div = 1, floor_ms = 0;
+  if (sess != nullptr) {
+    PyObject* t = callm(sess, "getTimeout");
+    if (t != nullptr) { T = PyFloat_AsDouble(t); Py_DECREF(t); }
+  }
+  if (cfg != nullptr) {
+    PyObject* a = attr(cfg, "ping_interval_divisor");
+    PyObject* b = attr(cfg, "ping_floor_ms");
+    if (a) { div = PyFloat_AsDouble(a); Py_DECREF(a); }
+    if (b) { floor_ms = PyFloat_AsDouble(b); Py_DECREF(b); }
+  }
+  if (PyErr_Occurred()) PyErr_Clear();
+  Py_XDECREF(sess);
+  Py_XDECREF(cfg);
+  const double v = div > 0 ? T / div : T;
+  return v > floor_ms ? v : floor_ms;
+}
+
+void conn_enter(Machine* m, int st) {
+  PyObject* ow = m->owner;
+  // leaving connected / closing: their timers and the close xid go
+  cancel(m->ping_iv);
+  Py_CLEAR(m->close_xid);
+  switch (st) {
+    case C_INIT:
+      break;
+    case C_CONNECTING: {
+      // decoder, encoder, codec, socket (with its data listener) made by
+      // the shell; the relays go on the new socket before it dials
+      PyObject* r = callm(ow, "_fx_open");
+      if (r == nullptr) { report(); break; }
+      Py_DECREF(r);
+      conn_sync_subs(m);
+      r = callm(ow, "_fx_dial");
+      if (r == nullptr) report();
+      Py_XDECREF(r);
+      return;
+    }
+    case C_HANDSHAKING: {
+      PyObject* wanted = attr(ow, "wanted");
+      const bool w = wanted != nullptr && PyObject_IsTrue(wanted) == 1;
+      Py_XDECREF(wanted);
+      if (!w) { request(m, C_CLOSED); break; }
+      PyObject* cl = attr(ow, "client");
+      PyObject* nc = cl ? attr(cl, "note_capture") : nullptr;
+      if (nc != nullptr && PyObject_IsTrue(nc) == 1)
+        call_void(ow, "start_note_capture");
+      Py_XDECREF(nc);
+      PyObject* sess = cl ? callm(cl, "getSession") : nullptr;
+      Py_XDECREF(cl);
+      if (sess == nullptr) { report(); sess = Py_NewRef(Py_None); }
+      set_attr(ow, "session", sess);
+      if (sess == Py_None) {
+        Py_DECREF(sess);
+        request(m, C_CLOSED);
+        break;
+      }
+      conn_sync_subs(m);
+      PyObject* att = callm(sess, "isAttaching");
+      const bool attaching = att != nullptr && PyObject_IsTrue(att) == 1;
+      Py_XDECREF(att);
+      if (attaching) {
+        PyObject* gs = callm(sess, "getState");
+        PyObject* args = Py_BuildValue(
+            "(sN)", "found ZKSession in state %s while handshaking",
+            gs != nullptr ? gs : Py_NewRef(Py_None));
+        if (args) { logv(ow, "debug", args); Py_DECREF(args); }
+        PyObject* e = PyObject_CallFunction(PyExc_Exception, "s",
+                                            "ZKSession attaching to another "
+                                            "connection");
+        if (e) { set_attr(ow, "last_error", e); Py_DECREF(e); }
+        Py_DECREF(sess);
+        request(m, C_ERROR);
+        break;
+      }
+      PyObject* r = PyObject_CallMethod(sess, "attachAndSendCR", "O", ow);
+      if (r == nullptr) report();
+      Py_XDECREF(r);
+      Py_DECREF(sess);
+      break;
+    }
+    case C_CONNECTED: {
+      m->ping_iv = schedule(m, conn_ping_interval(m), CE_PING_TICK);
+      if (m->ping_iv == nullptr) report();
+      call_void(ow, "_fx_connected");      // logger, native reply router on
+      // 'connect' on the next tick, unless the state is left before it
+      m->close_n = (int)m->transitions;
+      PyObject* h = schedule(m, -1, CE_IMM);
+      if (h == nullptr) report();
+      Py_XDECREF(h);
+      break;
+    }
+    case C_CLOSING:
+      call_void(ow, "_fx_route_off");
+      if (conn_drained(m)) conn_send_close(m);
+      break;
+    case C_ERROR:
+      // fail the outstanding requests, 'error' emitted even though the
+      // state is left at once (lib/connection-fsm.js:318-323)
+      call_void(ow, "_fx_error");
+      request(m, C_CLOSED);
+      break;
+    case C_CLOSED: {
+      call_void(ow, "_fx_closed");
+      m->close_n = (int)m->transitions;
+      PyObject* h = schedule(m, -1, CE_IMM);
+      if (h == nullptr) report();
+      Py_XDECREF(h);
+      break;
+    }
+  }
+  conn_sync_subs(m);
+}
+
+void conn_event(Machine* m, int kind, PyObject* src, PyObject* args) {
+  PyObject* ow = m->owner;
+  const Py_ssize_t na = PyTuple_GET_SIZE(args);
+  PyObject* a0 = na > 0 ? PyTuple_GET_ITEM(args, 0) : nullptr;
+  PyObject* a1 = na > 1 ? PyTuple_GET_ITEM(args, 1) : nullptr;
+  // relayed events only from the current socket / session
+  if (kind >= CE_SOCK_CONNECT && kind <= CE_SOCK_CLOSE) {
+    PyObject* sock = peer(m, "socket");
+    const bool cur = sock != nullptr && sock == src;
+    Py_XDECREF(sock);
+    if (!cur) return;
+  } else if (kind == CE_SESS_STATE) {
+    PyObject* sess = peer(m, "session");
+    const bool cur = sess != nullptr && sess == src;
+    Py_XDECREF(sess);
+    if (!cur) return;
+  }
+  const int st = m->state;
+  // the closing / error paths every live state shares
+  auto lost = [&](int to) {
+    conn_fail_with(m, "CONNECTION_LOSS", "Connection closed unexpectedly.");
+    request(m, to);
+  };
+  switch (st) {
+    case C_INIT:
+      if (kind == CE_CONNECT) request(m, C_CONNECTING);
+      break;
+    case C_CONNECTING:
+      if (kind == CE_SOCK_CONNECT) request(m, C_HANDSHAKING);
+      else if (kind == CE_SOCK_ERROR) { conn_set_error(m, a0); request(m, C_ERROR); }
+      else if (kind == CE_SOCK_CLOSE || kind == CE_CLOSE || kind == CE_DESTROY)
+        request(m, C_CLOSED);
+      break;
+    case C_HANDSHAKING:
+      if (kind == CE_RX && a0 != nullptr) {
+        const long more = a1 != nullptr ? PyLong_AsLong(a1) : 0;
+        if (more > 0) {
+          conn_fail_with(m, "UNEXPECTED_PACKET",
+                         "Received unexpected additional packet during "
+                         "connect phase");
+          request(m, C_ERROR);
+          break;
+        }
+        // the ConnectResponse (host codec or the GPU K9 decoder); a decode
+        // failure comes back as the error to fail with
+        PyObject* pkt = PyObject_CallMethod(ow, "_decode_cr", "O", a0);
+        if (pkt == nullptr) { report(); break; }
+        if (!PyDict_Check(pkt)) {
+          conn_set_error(m, pkt);
+          Py_DECREF(pkt);
+          request(m, C_ERROR);
+          break;
+        }
+        if (field_i64(pkt, "protocolVersion") != 0) {
+          Py_DECREF(pkt);
+          conn_fail_with(m, "VERSION_INCOMPAT",
+                         "Server version is not compatible");
+          request(m, C_ERROR);
+          break;
+        }
+        PyObject* r = PyObject_CallMethod(ow, "emit", "sO", "packet", pkt);
+        Py_DECREF(pkt);
+        if (r == nullptr) report();
+        Py_XDECREF(r);
+      } else if (kind == CE_RXERR || kind == CE_SOCK_ERROR) {
+        conn_set_error(m, a0);
+        request(m, C_ERROR);
+      } else if (kind == CE_SOCK_END || kind == CE_SOCK_CLOSE) {
+        lost(C_ERROR);
+      } else if (kind == CE_CLOSE || kind == CE_DESTROY || kind == CE_UNWANTED) {
+        request(m, C_CLOSED);
+      } else if (kind == CE_SESS_STATE && a0 != nullptr) {
+        // only when the session attached through THIS connection (after a
+        // reattach revert the rejected connection must not turn
+        // 'connected'; the reference advances on any 'attached')
+        if (PyUnicode_Check(a0) &&
+            PyUnicode_CompareWithASCIIString(a0, "attached") == 0) {
+          PyObject* sess = peer(m, "session");
+          PyObject* sc = sess ? attr(sess, "conn") : nullptr;
+          const bool mine = sc == ow;
+          Py_XDECREF(sc);
+          Py_XDECREF(sess);
+          if (mine) request(m, C_CONNECTED);
+        }
+      }
+      break;
+    case C_CONNECTED:
+      if (kind == CE_RX && a0 != nullptr) {
+        // replies, notifications, bulk frames: the shell's plumbing; a
+        // decode failure comes back as the error
+        PyObject* e = PyObject_CallMethod(ow, "_rx_connected", "O", a0);
+        if (e == nullptr) { report(); break; }
+        if (e != Py_None) { conn_set_error(m, e); request(m, C_ERROR); }
+        Py_DECREF(e);
+      } else if (kind == CE_RXERR || kind == CE_SOCK_ERROR) {
+        conn_set_error(m, a0);
+        request(m, C_ERROR);
+      } else if (kind == CE_SOCK_END || kind == CE_SOCK_CLOSE) {
+        lost(C_ERROR);
+      } else if (kind == CE_CLOSE) {
+        request(m, C_CLOSING);
+      } else if (kind == CE_DESTROY) {
+        request(m, C_CLOSED);
+      } else if (kind == CE_PING_TIMEOUT) {
+        PyObject* e = callm(ow, "_ping_timeout_error");
+        if (e == nullptr) { report(); break; }
+        conn_set_error(m, e);
+        Py_DECREF(e);
+        request(m, C_ERROR);
+      } else if (kind == CE_PING_TICK) {
+        // re-armed before the ping (a slow ping does not drift the period)
+        Py_CLEAR(m->ping_iv);
+        m->ping_iv = schedule(m, conn_ping_interval(m), CE_PING_TICK);
+        if (m->ping_iv == nullptr) report();
+        call_void(ow, "ping");
+      } else if (kind == CE_IMM && m->close_n == (int)m->transitions) {
+        PyObject* r = PyObject_CallMethod(ow, "emit", "s", "connect");
+        if (r == nullptr) report();
+        Py_XDECREF(r);
+      }
+      break;
+    case C_CLOSING:
+      if (kind == CE_RX && a0 != nullptr) {
+        // 0: a reply settled, 1: the CLOSE_SESSION reply (or an undecodable
+        // frame: last_error set) — done
+        PyObject* r = PyObject_CallMethod(
+            ow, "_rx_closing", "OO", a0,
+            m->close_xid != nullptr ? m->close_xid : Py_None);
+        if (r == nullptr) { report(); break; }
+        const long v = PyLong_AsLong(r);
+        Py_DECREF(r);
+        if (v == 1) { request(m, C_CLOSED); break; }
+        if (conn_drained(m)) conn_send_close(m);
+      } else if (kind == CE_BULKDONE) {
+        if (conn_drained(m)) conn_send_close(m);
+      } else if (kind == CE_RXERR || kind == CE_SOCK_ERROR) {
+        conn_set_error(m, a0);
+        request(m, C_CLOSED);
+      } else if (kind == CE_SOCK_END || kind == CE_SOCK_CLOSE) {
+        request(m, C_CLOSED);
+      }
+      // destroy() is ignored while closing, as in the reference: the
+      // CLOSE_SESSION exchange completes (or the socket dies)
+      break;
+    case C_CLOSED:
+      if (kind == CE_IMM && m->close_n == (int)m->transitions) {
+        call_void(ow, "_fx_closed_later");
+      }
+      break;
+    default:
+      break;
+  }
+}
+
+const Spec CONNECTION{C_NAMES, C_N, conn_enter, conn_event};
+
 // ---- Python surface ---------------------------------------------------------
 
 int Machine_traverse(Machine* m, visitproc visit, void* arg) {
@@ -661,6 +1034,7 @@ void Machine_dealloc(Machine* m) {
 
 const Spec* spec_of(const char* kind) {
   if (strcmp(kind, "session") == 0) return &SESSION;
+  if (strcmp(kind, "connection") == 0) return &CONNECTION;
   return nullptr;
 }
 
@@ -827,5 +1201,14 @@ PyMODINIT_FUNC PyInit__zkmach() {
   PyModule_AddIntConstant(m, "SE_ATTACH", SE_ATTACH);
   PyModule_AddIntConstant(m, "SE_CLOSE", SE_CLOSE);
   PyModule_AddIntConstant(m, "SE_EXPIRY", SE_EXPIRY);
+  // the connection's
+  PyModule_AddIntConstant(m, "CE_CONNECT", CE_CONNECT);
+  PyModule_AddIntConstant(m, "CE_CLOSE", CE_CLOSE);
+  PyModule_AddIntConstant(m, "CE_DESTROY", CE_DESTROY);
+  PyModule_AddIntConstant(m, "CE_UNWANTED", CE_UNWANTED);
+  PyModule_AddIntConstant(m, "CE_RX", CE_RX);
+  PyModule_AddIntConstant(m, "CE_RXERR", CE_RXERR);
+  PyModule_AddIntConstant(m, "CE_PING_TIMEOUT", CE_PING_TIMEOUT);
+  PyModule_AddIntConstant(m, "CE_BULKDONE", CE_BULKDONE);
   return m;
 }

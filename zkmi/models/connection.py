@@ -27,6 +27,7 @@ from ..runtime.fsm import FSM
 from ..runtime.tcp import TcpSocket
 from ..streams import ZKDecoder, ZKEncoder
 from . import gpucodec
+from .session import _zkmach, native_machines
 
 
 
@@ -59,7 +60,16 @@ class ZKRequest(EventEmitter):
             self.emit(evt, *args)
 
 
-class ZKConnectionFSM(FSM):
+def ZKConnectionFSM(client, backend, log, loop, config, tracer=None):
+    """A connection: the native machine, or the Python oracle."""
+    cls = NativeZKConnectionFSM if native_machines() else PyZKConnectionFSM
+    return cls(client, backend, log, loop, config, tracer=tracer)
+
+
+class _ConnBase(object):
+    """The connection's transport plumbing (framing, request table, the
+    native reply router, bulk batches, bulk notification capture) — what it
+    is besides its state graph."""
 
     def __init__(self, client, backend, log, loop, config, tracer=None):
         self.client = client
@@ -88,28 +98,6 @@ class ZKConnectionFSM(FSM):
         self.session = None
         self.wanted = True
         self.last_error = None
-        FSM.__init__(self, 'init', loop)
-
-    # -- reference method names ---------------------------------------------
-
-    def connect(self):
-        assert self.isInState('closed') or self.isInState('init')
-        self.emit('connectAsserted')
-
-    def setUnwanted(self):
-        self.wanted = False
-        self.log.debug('connection now unwanted')
-        self.emit('unwanted')
-
-    def close(self):
-        if self.isInState('closed'):
-            return
-        self.emit('closeAsserted')
-
-    def destroy(self):
-        if self.isInState('closed'):
-            return
-        self.emit('destroyAsserted')
 
     def nextXid(self):
         with self.xid_lock:
@@ -128,9 +116,9 @@ class ZKConnectionFSM(FSM):
         for i, body in enumerate(bodies):
             if self.decoder is not dec:
                 return              # torn down mid-chunk
-            self.emit('_rx', body, n - i - 1)
+            self._in_rx(body, n - i - 1)
         if err is not None and self.decoder is dec:
-            self.emit('_rxerr', err)
+            self._in_rxerr(err)
 
     def _decode_reply(self, body):
         try:
@@ -142,248 +130,6 @@ class ZKConnectionFSM(FSM):
         if xid >= 0:
             self.xid_map.pop(xid, None)
         return pkt
-
-    # -- states ---------------------------------------------------------------
-
-    def state_init(self, S):
-        S.on(self, 'connectAsserted', lambda: S.gotoState('connecting'))
-
-    def state_connecting(self, S):
-        self.decoder = ZKDecoder(self.config.max_packet)
-        self.gpu = gpucodec.for_device(self.config.codec_device)
-        self.encoder = ZKEncoder(self.xid_map, self.gpu)
-        self.log = self.log.child(zkAddress=self.server['address'],
-                                  zkPort=self.server['port'])
-        self.log.trace('attempting new connection')
-        sock = TcpSocket(self.fsm_loop)
-        self.socket = sock
-        sock.on('data', self._on_data)
-
-        def on_error(err):
-            self.last_error = err
-            S.gotoState('error')
-        S.on(sock, 'connect', lambda: S.gotoState('handshaking'))
-        S.on(sock, 'error', on_error)
-        S.on(sock, 'close', lambda: S.gotoState('closed'))
-        S.on(self, 'closeAsserted', lambda: S.gotoState('closed'))
-        S.on(self, 'destroyAsserted', lambda: S.gotoState('closed'))
-        sock.connect(self.server['address'], self.server['port'])
-
-    def state_handshaking(self, S):
-        if not self.wanted:
-            S.gotoState('closed')
-            return
-        if getattr(self.client, 'note_capture', False):
-            self.start_note_capture()
-
-        def on_rx(body, more):
-            if more > 0:
-                self.last_error = ZKProtocolError(
-                    'UNEXPECTED_PACKET', 'Received unexpected additional '
-                    'packet during connect phase')
-                S.gotoState('error')
-                return
-            try:
-                if self.gpu is not None:
-                    pkt = self.gpu.connect_response(body)
-                else:
-                    pkt = codec.decode_connect_response(body)
-            except (ZKDecodeError, ValueError) as e:
-                self.last_error = ZKProtocolError(
-                    'BAD_DECODE', 'Failed to decode ConnectResponse: %s: %s'
-                    % (type(e).__name__, e))
-                S.gotoState('error')
-                return
-            if pkt['protocolVersion'] != 0:
-                self.last_error = ZKProtocolError(
-                    'VERSION_INCOMPAT', 'Server version is not compatible')
-                S.gotoState('error')
-                return
-            self.emit('packet', pkt)
-
-        def on_error(err):
-            self.last_error = err
-            S.gotoState('error')
-
-        def on_end():
-            self.last_error = ZKProtocolError(
-                'CONNECTION_LOSS', 'Connection closed unexpectedly.')
-            S.gotoState('error')
-
-        S.on(self, '_rx', on_rx)
-        S.on(self, '_rxerr', on_error)
-        S.on(self.socket, 'error', on_error)
-        S.on(self.socket, 'end', on_end)
-        S.on(self.socket, 'close', on_end)
-        S.on(self, 'closeAsserted', lambda: S.gotoState('closed'))
-        S.on(self, 'destroyAsserted', lambda: S.gotoState('closed'))
-        S.on(self, 'unwanted', lambda: S.gotoState('closed'))
-
-        self.session = self.client.getSession()
-        if self.session is None:
-            S.gotoState('closed')
-            return
-        if self.session.isAttaching():
-            self.log.debug('found ZKSession in state %s while handshaking',
-                           self.session.getState())
-            self.last_error = Exception('ZKSession attaching to another '
-                                        'connection')
-            S.gotoState('error')
-            return
-
-        def on_session(st):
-            # Only when the session attached through THIS connection.  The
-            # reference advances on any 'attached', so after a reattach
-            # revert (zk-session.js:298-320) the rejected connection would
-            # turn 'connected', get preferred by the set, and kill the
-            # connection the session actually lives on.
-            if st == 'attached' and self.session.conn is self:
-                S.gotoState('connected')
-        S.on(self.session, 'stateChanged', on_session)
-        self.session.attachAndSendCR(self)
-
-    def state_connected(self, S):
-        T = self.session.getTimeout()
-        cfg = self.config
-        interval = max(T / cfg.ping_interval_divisor, cfg.ping_floor_ms)
-        S.interval(interval, lambda: self.ping()).unref()
-        self.log = self.log.child(sessionId=self.session.getSessionId())
-
-        def on_rx(body, more):
-            if self.bulks and len(body) >= 16:
-                xid = int.from_bytes(body[0:4], 'big', signed=True)
-                if xid >= 0 and self._bulk_rx(xid, body):
-                    return
-            if self.notes is not None and len(body) >= 16 and \
-                    body[0:4] == b'\xff\xff\xff\xff' and \
-                    not self._note_keep(body):
-                return
-            try:
-                pkt = self._decode_reply(body)
-            except ZKProtocolError as e:
-                self.last_error = e
-                S.gotoState('error')
-                return
-            self.emit('packet', pkt)
-            # Notifications are handled by the session (watchers).
-            if pkt['opcode'] == 'NOTIFICATION':
-                return
-            self.processReply(pkt)
-
-        def on_error(err):
-            self.last_error = err
-            S.gotoState('error')
-
-        def on_end():
-            self.last_error = ZKProtocolError(
-                'CONNECTION_LOSS', 'Connection closed unexpectedly.')
-            S.gotoState('error')
-
-        def on_ping_timeout():
-            self.last_error = ZKPingTimeoutError()
-            S.gotoState('error')
-
-        S.on(self, '_rx', on_rx)
-        S.on(self, '_rxerr', on_error)
-        S.on(self.socket, 'error', on_error)
-        S.on(self.socket, 'end', on_end)
-        S.on(self.socket, 'close', on_end)
-        S.on(self, 'closeAsserted', lambda: S.gotoState('closing'))
-        S.on(self, 'destroyAsserted', lambda: S.gotoState('closed'))
-        S.on(self, 'pingTimeout', on_ping_timeout)
-        self._route(True)
-        S.immediate(lambda: self.emit('connect'))
-
-    def state_closing(self, S):
-        self._route(False)
-        box = {'xid': None}
-
-        def send_close_session():
-            if box['xid'] is not None:
-                return
-            box['xid'] = xid = self.nextXid()
-            self.log.info({'xid': xid}, 'sent CLOSE_SESSION request')
-            data = self.encoder.request({'opcode': 'CLOSE_SESSION',
-                                         'xid': xid})
-            self.socket.end(data)
-
-        def on_rx(body, more):
-            if self.bulks and len(body) >= 16:
-                xid = int.from_bytes(body[0:4], 'big', signed=True)
-                if xid >= 0 and self._bulk_rx(xid, body):
-                    if len(self.reqs) < 1 and not self.bulks:
-                        send_close_session()
-                    return
-            try:
-                pkt = self._decode_reply(body)
-            except ZKProtocolError as e:
-                self.last_error = e
-                S.gotoState('closed')
-                return
-            if box['xid'] is None or pkt['xid'] != box['xid']:
-                self.processReply(pkt)
-                if len(self.reqs) < 1 and not self.bulks:
-                    send_close_session()
-            else:
-                S.gotoState('closed')
-
-        def on_error(err):
-            self.last_error = err
-            S.gotoState('closed')
-
-        def on_bulk_done():
-            if len(self.reqs) < 1 and not self.bulks:
-                send_close_session()
-
-        S.on(self, '_rx', on_rx)
-        S.on(self, '_rxerr', on_error)
-        S.on(self, '_bulkdone', on_bulk_done)
-        S.on(self.socket, 'error', on_error)
-        S.on(self.socket, 'end', lambda: S.gotoState('closed'))
-        S.on(self.socket, 'close', lambda: S.gotoState('closed'))
-        # destroy() is ignored while closing, as in the reference: the
-        # CLOSE_SESSION exchange completes (or the socket dies).  In-flight
-        # bulk batches drain like ordinary requests.
-        if len(self.reqs) < 1 and not self.bulks:
-            send_close_session()
-
-    def state_error(self, S):
-        self._route(False)
-        err = self.last_error
-        self.log.warn(err if isinstance(err, BaseException) else {},
-                      'error communicating with ZK')
-        reqs, self.reqs = self.reqs, {}
-        for req in list(reqs.values()):
-            req.settle('error', err)
-        self._fail_bulks(err)
-        # Not S.immediate: this must be emitted even though we leave the
-        # state right away (lib/connection-fsm.js:318-323).
-        self.fsm_loop.call_soon(self._emit_error, err)
-        S.gotoState('closed')
-
-    def _emit_error(self, err):
-        if self.listenerCount('error') > 0:
-            self.emit('error', err)
-
-    def state_closed(self, S):
-        self._route(False)
-        self.encoder = None
-        if self.socket is not None and self.note_native:
-            # the notifications the transport kept outlive it
-            self.notes_left = self.socket.take_notes()
-        if self.socket is not None:
-            self.socket.destroy()
-        self.socket = None
-        self.decoder = None
-
-        def later():
-            self.emit('close')
-            err = ZKProtocolError('CONNECTION_LOSS', 'Connection closed.')
-            reqs, self.reqs = self.reqs, {}
-            for req in list(reqs.values()):
-                req.settle('error', err)
-            self._fail_bulks(err)
-        S.immediate(later)
 
     # -- native completion path ----------------------------------------------
 
@@ -644,7 +390,7 @@ class ZKConnectionFSM(FSM):
             b.cb(e)
         else:
             b.cb(None, res)
-        self.emit('_bulkdone')
+        self._in_bulkdone()
 
     def _bulk_rx(self, xid, body):
         for b in self.bulks:
@@ -703,7 +449,7 @@ class ZKConnectionFSM(FSM):
 
         def on_timeout():
             req.removeListener('reply', on_packet)
-            self.emit('pingTimeout')
+            self._in_ping_timeout()
 
         def on_error(err, *_):
             if self.reqs.get(xid) is req:
@@ -749,3 +495,475 @@ class ZKConnectionFSM(FSM):
     @property
     def zcf_socket(self):
         return self.socket
+
+
+class PyZKConnectionFSM(_ConnBase, FSM):
+    """The connection's state graph as mooremachine-style state functions
+    (``lib/connection-fsm.js:27-351``): the test oracle of the native machine
+    (``ZKMI_PY_FSM=1``)."""
+
+    def __init__(self, client, backend, log, loop, config, tracer=None):
+        _ConnBase.__init__(self, client, backend, log, loop, config, tracer)
+        FSM.__init__(self, 'init', loop)
+
+    # -- reference method names ---------------------------------------------
+
+    def connect(self):
+        assert self.isInState('closed') or self.isInState('init')
+        self.emit('connectAsserted')
+
+    def setUnwanted(self):
+        self.wanted = False
+        self.log.debug('connection now unwanted')
+        self.emit('unwanted')
+
+    def close(self):
+        if self.isInState('closed'):
+            return
+        self.emit('closeAsserted')
+
+    def destroy(self):
+        if self.isInState('closed'):
+            return
+        self.emit('destroyAsserted')
+
+    # -- inputs (the native machine takes them as fire() calls) ------------
+
+    def _in_rx(self, body, more):
+        self.emit('_rx', body, more)
+
+    def _in_rxerr(self, err):
+        self.emit('_rxerr', err)
+
+    def _in_ping_timeout(self):
+        self.emit('pingTimeout')
+
+    def _in_bulkdone(self):
+        self.emit('_bulkdone')
+
+    # -- states ---------------------------------------------------------------
+
+    def state_init(self, S):
+        S.on(self, 'connectAsserted', lambda: S.gotoState('connecting'))
+
+    def state_connecting(self, S):
+        self.decoder = ZKDecoder(self.config.max_packet)
+        self.gpu = gpucodec.for_device(self.config.codec_device)
+        self.encoder = ZKEncoder(self.xid_map, self.gpu)
+        self.log = self.log.child(zkAddress=self.server['address'],
+                                  zkPort=self.server['port'])
+        self.log.trace('attempting new connection')
+        sock = TcpSocket(self.fsm_loop)
+        self.socket = sock
+        sock.on('data', self._on_data)
+
+        def on_error(err):
+            self.last_error = err
+            S.gotoState('error')
+        S.on(sock, 'connect', lambda: S.gotoState('handshaking'))
+        S.on(sock, 'error', on_error)
+        S.on(sock, 'close', lambda: S.gotoState('closed'))
+        S.on(self, 'closeAsserted', lambda: S.gotoState('closed'))
+        S.on(self, 'destroyAsserted', lambda: S.gotoState('closed'))
+        sock.connect(self.server['address'], self.server['port'])
+
+    def state_handshaking(self, S):
+        if not self.wanted:
+            S.gotoState('closed')
+            return
+        if getattr(self.client, 'note_capture', False):
+            self.start_note_capture()
+
+        def on_rx(body, more):
+            if more > 0:
+                self.last_error = ZKProtocolError(
+                    'UNEXPECTED_PACKET', 'Received unexpected additional '
+                    'packet during connect phase')
+                S.gotoState('error')
+                return
+            try:
+                if self.gpu is not None:
+                    pkt = self.gpu.connect_response(body)
+                else:
+                    pkt = codec.decode_connect_response(body)
+            except (ZKDecodeError, ValueError) as e:
+                self.last_error = ZKProtocolError(
+                    'BAD_DECODE', 'Failed to decode ConnectResponse: %s: %s'
+                    % (type(e).__name__, e))
+                S.gotoState('error')
+                return
+            if pkt['protocolVersion'] != 0:
+                self.last_error = ZKProtocolError(
+                    'VERSION_INCOMPAT', 'Server version is not compatible')
+                S.gotoState('error')
+                return
+            self.emit('packet', pkt)
+
+        def on_error(err):
+            self.last_error = err
+            S.gotoState('error')
+
+        def on_end():
+            self.last_error = ZKProtocolError(
+                'CONNECTION_LOSS', 'Connection closed unexpectedly.')
+            S.gotoState('error')
+
+        S.on(self, '_rx', on_rx)
+        S.on(self, '_rxerr', on_error)
+        S.on(self.socket, 'error', on_error)
+        S.on(self.socket, 'end', on_end)
+        S.on(self.socket, 'close', on_end)
+        S.on(self, 'closeAsserted', lambda: S.gotoState('closed'))
+        S.on(self, 'destroyAsserted', lambda: S.gotoState('closed'))
+        S.on(self, 'unwanted', lambda: S.gotoState('closed'))
+
+        self.session = self.client.getSession()
+        if self.session is None:
+            S.gotoState('closed')
+            return
+        if self.session.isAttaching():
+            self.log.debug('found ZKSession in state %s while handshaking',
+                           self.session.getState())
+            self.last_error = Exception('ZKSession attaching to another '
+                                        'connection')
+            S.gotoState('error')
+            return
+
+        def on_session(st):
+            # Only when the session attached through THIS connection.  The
+            # reference advances on any 'attached', so after a reattach
+            # revert (zk-session.js:298-320) the rejected connection would
+            # turn 'connected', get preferred by the set, and kill the
+            # connection the session actually lives on.
+            if st == 'attached' and self.session.conn is self:
+                S.gotoState('connected')
+        S.on(self.session, 'stateChanged', on_session)
+        self.session.attachAndSendCR(self)
+
+    def state_connected(self, S):
+        T = self.session.getTimeout()
+        cfg = self.config
+        interval = max(T / cfg.ping_interval_divisor, cfg.ping_floor_ms)
+        S.interval(interval, lambda: self.ping()).unref()
+        self.log = self.log.child(sessionId=self.session.getSessionId())
+
+        def on_rx(body, more):
+            if self.bulks and len(body) >= 16:
+                xid = int.from_bytes(body[0:4], 'big', signed=True)
+                if xid >= 0 and self._bulk_rx(xid, body):
+                    return
+            if self.notes is not None and len(body) >= 16 and \
+                    body[0:4] == b'\xff\xff\xff\xff' and \
+                    not self._note_keep(body):
+                return
+            try:
+                pkt = self._decode_reply(body)
+            except ZKProtocolError as e:
+                self.last_error = e
+                S.gotoState('error')
+                return
+            self.emit('packet', pkt)
+            # Notifications are handled by the session (watchers).
+            if pkt['opcode'] == 'NOTIFICATION':
+                return
+            self.processReply(pkt)
+
+        def on_error(err):
+            self.last_error = err
+            S.gotoState('error')
+
+        def on_end():
+            self.last_error = ZKProtocolError(
+                'CONNECTION_LOSS', 'Connection closed unexpectedly.')
+            S.gotoState('error')
+
+        def on_ping_timeout():
+            self.last_error = ZKPingTimeoutError()
+            S.gotoState('error')
+
+        S.on(self, '_rx', on_rx)
+        S.on(self, '_rxerr', on_error)
+        S.on(self.socket, 'error', on_error)
+        S.on(self.socket, 'end', on_end)
+        S.on(self.socket, 'close', on_end)
+        S.on(self, 'closeAsserted', lambda: S.gotoState('closing'))
+        S.on(self, 'destroyAsserted', lambda: S.gotoState('closed'))
+        S.on(self, 'pingTimeout', on_ping_timeout)
+        self._route(True)
+        S.immediate(lambda: self.emit('connect'))
+
+    def state_closing(self, S):
+        self._route(False)
+        box = {'xid': None}
+
+        def send_close_session():
+            if box['xid'] is not None:
+                return
+            box['xid'] = xid = self.nextXid()
+            self.log.info({'xid': xid}, 'sent CLOSE_SESSION request')
+            data = self.encoder.request({'opcode': 'CLOSE_SESSION',
+                                         'xid': xid})
+            self.socket.end(data)
+
+        def on_rx(body, more):
+            if self.bulks and len(body) >= 16:
+                xid = int.from_bytes(body[0:4], 'big', signed=True)
+                if xid >= 0 and self._bulk_rx(xid, body):
+                    if len(self.reqs) < 1 and not self.bulks:
+                        send_close_session()
+                    return
+            try:
+                pkt = self._decode_reply(body)
+            except ZKProtocolError as e:
+                self.last_error = e
+                S.gotoState('closed')
+                return
+            if box['xid'] is None or pkt['xid'] != box['xid']:
+                self.processReply(pkt)
+                if len(self.reqs) < 1 and not self.bulks:
+                    send_close_session()
+            else:
+                S.gotoState('closed')
+
+        def on_error(err):
+            self.last_error = err
+            S.gotoState('closed')
+
+        def on_bulk_done():
+            if len(self.reqs) < 1 and not self.bulks:
+                send_close_session()
+
+        S.on(self, '_rx', on_rx)
+        S.on(self, '_rxerr', on_error)
+        S.on(self, '_bulkdone', on_bulk_done)
+        S.on(self.socket, 'error', on_error)
+        S.on(self.socket, 'end', lambda: S.gotoState('closed'))
+        S.on(self.socket, 'close', lambda: S.gotoState('closed'))
+        # destroy() is ignored while closing, as in the reference: the
+        # CLOSE_SESSION exchange completes (or the socket dies).  In-flight
+        # bulk batches drain like ordinary requests.
+        if len(self.reqs) < 1 and not self.bulks:
+            send_close_session()
+
+    def state_error(self, S):
+        self._route(False)
+        err = self.last_error
+        self.log.warn(err if isinstance(err, BaseException) else {},
+                      'error communicating with ZK')
+        reqs, self.reqs = self.reqs, {}
+        for req in list(reqs.values()):
+            req.settle('error', err)
+        self._fail_bulks(err)
+        # Not S.immediate: this must be emitted even though we leave the
+        # state right away (lib/connection-fsm.js:318-323).
+        self.fsm_loop.call_soon(self._emit_error, err)
+        S.gotoState('closed')
+
+    def _emit_error(self, err):
+        if self.listenerCount('error') > 0:
+            self.emit('error', err)
+
+    def state_closed(self, S):
+        self._route(False)
+        self.encoder = None
+        if self.socket is not None and self.note_native:
+            # the notifications the transport kept outlive it
+            self.notes_left = self.socket.take_notes()
+        if self.socket is not None:
+            self.socket.destroy()
+        self.socket = None
+        self.decoder = None
+
+        def later():
+            self.emit('close')
+            err = ZKProtocolError('CONNECTION_LOSS', 'Connection closed.')
+            reqs, self.reqs = self.reqs, {}
+            for req in list(reqs.values()):
+                req.settle('error', err)
+            self._fail_bulks(err)
+        S.immediate(later)
+
+
+class NativeZKConnectionFSM(_ConnBase, EventEmitter):
+    """The connection on the C++ machine (``_zkmach.Machine('connection')``,
+    csrc/host/zk_machines.cpp): states, guards (the handshake's packet
+    count and protocol version, the session's attach), the ping timer and
+    the close handshake run there; the effect methods below do what the
+    machine asks of the transport."""
+
+    def __init__(self, client, backend, log, loop, config, tracer=None):
+        EventEmitter.__init__(self)
+        _ConnBase.__init__(self, client, backend, log, loop, config, tracer)
+        self.fsm_loop = loop
+        self._m = _zkmach.Machine('connection', self, loop)
+        self._m.start('init')
+
+    # -- FSM surface ----------------------------------------------------------
+
+    def getState(self):
+        return self._m.state
+
+    _fsm_state = property(getState)
+
+    def isInState(self, state):
+        return self._m.in_state(state)
+
+    @property
+    def fsm_history(self):
+        return self._m.history
+
+    # -- reference method names ---------------------------------------------
+
+    def connect(self):
+        assert self.isInState('closed') or self.isInState('init')
+        self._m.fire(_zkmach.CE_CONNECT)
+
+    def setUnwanted(self):
+        self.wanted = False
+        self.log.debug('connection now unwanted')
+        self._m.fire(_zkmach.CE_UNWANTED)
+
+    def close(self):
+        if self.isInState('closed'):
+            return
+        self._m.fire(_zkmach.CE_CLOSE)
+
+    def destroy(self):
+        if self.isInState('closed'):
+            return
+        self._m.fire(_zkmach.CE_DESTROY)
+
+    # -- inputs -------------------------------------------------------------
+
+    def _in_rx(self, body, more):
+        self._m.fire(_zkmach.CE_RX, body, more)
+
+    def _in_rxerr(self, err):
+        self._m.fire(_zkmach.CE_RXERR, err)
+
+    def _in_ping_timeout(self):
+        self._m.fire(_zkmach.CE_PING_TIMEOUT)
+
+    def _in_bulkdone(self):
+        self._m.fire(_zkmach.CE_BULKDONE)
+
+    # -- effects the machine asks for -----------------------------------------
+
+    @staticmethod
+    def _proto_error(code, msg):
+        return ZKProtocolError(code, msg)
+
+    @staticmethod
+    def _ping_timeout_error():
+        return ZKPingTimeoutError()
+
+    def _fx_open(self):
+        """connecting: framing, codec, a new socket (its data listener
+        first; the machine's relays go on after)."""
+        self.decoder = ZKDecoder(self.config.max_packet)
+        self.gpu = gpucodec.for_device(self.config.codec_device)
+        self.encoder = ZKEncoder(self.xid_map, self.gpu)
+        self.log = self.log.child(zkAddress=self.server['address'],
+                                  zkPort=self.server['port'])
+        self.log.trace('attempting new connection')
+        sock = TcpSocket(self.fsm_loop)
+        self.socket = sock
+        sock.on('data', self._on_data)
+
+    def _fx_dial(self):
+        self.socket.connect(self.server['address'], self.server['port'])
+
+    def _decode_cr(self, body):
+        """The ConnectResponse, or the error to fail with."""
+        try:
+            if self.gpu is not None:
+                return self.gpu.connect_response(body)
+            return codec.decode_connect_response(body)
+        except (ZKDecodeError, ValueError) as e:
+            return ZKProtocolError(
+                'BAD_DECODE', 'Failed to decode ConnectResponse: %s: %s'
+                % (type(e).__name__, e))
+
+    def _fx_connected(self):
+        self.log = self.log.child(sessionId=self.session.getSessionId())
+        self._route(True)
+
+    def _rx_connected(self, body):
+        """A frame in 'connected': bulk batches, kept notifications, then
+        the reply / notification path.  Returns the error to fail with."""
+        if self.bulks and len(body) >= 16:
+            xid = int.from_bytes(body[0:4], 'big', signed=True)
+            if xid >= 0 and self._bulk_rx(xid, body):
+                return None
+        if self.notes is not None and len(body) >= 16 and \
+                body[0:4] == b'\xff\xff\xff\xff' and \
+                not self._note_keep(body):
+            return None
+        try:
+            pkt = self._decode_reply(body)
+        except ZKProtocolError as e:
+            return e
+        self.emit('packet', pkt)
+        # Notifications are handled by the session (watchers).
+        if pkt['opcode'] != 'NOTIFICATION':
+            self.processReply(pkt)
+        return None
+
+    def _fx_route_off(self):
+        self._route(False)
+
+    def _fx_send_close(self, xid):
+        self.log.info({'xid': xid}, 'sent CLOSE_SESSION request')
+        data = self.encoder.request({'opcode': 'CLOSE_SESSION', 'xid': xid})
+        self.socket.end(data)
+
+    def _rx_closing(self, body, close_xid):
+        """A frame in 'closing': 1 when it ends the exchange (the
+        CLOSE_SESSION reply, or an undecodable frame), else 0."""
+        if self.bulks and len(body) >= 16:
+            xid = int.from_bytes(body[0:4], 'big', signed=True)
+            if xid >= 0 and self._bulk_rx(xid, body):
+                return 0
+        try:
+            pkt = self._decode_reply(body)
+        except ZKProtocolError as e:
+            self.last_error = e
+            return 1
+        if close_xid is None or pkt['xid'] != close_xid:
+            self.processReply(pkt)
+            return 0
+        return 1
+
+    def _fx_error(self):
+        self._route(False)
+        err = self.last_error
+        self.log.warn(err if isinstance(err, BaseException) else {},
+                      'error communicating with ZK')
+        reqs, self.reqs = self.reqs, {}
+        for req in list(reqs.values()):
+            req.settle('error', err)
+        self._fail_bulks(err)
+        self.fsm_loop.call_soon(self._emit_error, err)
+
+    def _emit_error(self, err):
+        if self.listenerCount('error') > 0:
+            self.emit('error', err)
+
+    def _fx_closed(self):
+        self._route(False)
+        self.encoder = None
+        if self.socket is not None and self.note_native:
+            # the notifications the transport kept outlive it
+            self.notes_left = self.socket.take_notes()
+        if self.socket is not None:
+            self.socket.destroy()
+        self.socket = None
+        self.decoder = None
+
+    def _fx_closed_later(self):
+        self.emit('close')
+        err = ZKProtocolError('CONNECTION_LOSS', 'Connection closed.')
+        reqs, self.reqs = self.reqs, {}
+        for req in list(reqs.values()):
+            req.settle('error', err)
+        self._fail_bulks(err)

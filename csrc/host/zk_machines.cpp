@@ -241,6 +241,7 @@ int subscribe(Machine* m, PyObject* src, const char* evt, int kind) {
 
 // Drop every subscription whose emitter is not in keep[0..nk).
 void unsubscribe_others(Machine* m, PyObject* const* keep, int nk) {
+  if (keep == nullptr) nk = 0;
   std::vector<Sub> drop;
   std::vector<Sub> stay;
   for (auto& s : *m->subs) {
@@ -986,6 +987,113 @@ void conn_event(Machine* m, int kind, PyObject* src, PyObject* args) {
 
 const Spec CONNECTION{C_NAMES, C_N, conn_enter, conn_event};
 
+// ---- the client lifecycle -----------------------------------------------------
+// lib/client.js:123-181: normal -> closing (the session, the connection set
+// and the resolver each wind down; all three done) -> closed.
+
+enum { K_NORMAL, K_CLOSING, K_CLOSED, K_N };
+const char* const K_NAMES[] = {"normal", "closing", "closed"};
+enum { KE_CLOSE, KE_SESS_STATE, KE_SET_STATE, KE_RES_STATE, KE_LOG_TICK };
+
+bool str_is(PyObject* v, const char* s) {
+  return v != nullptr && PyUnicode_Check(v) &&
+         PyUnicode_CompareWithASCIIString(v, s) == 0;
+}
+
+double cfg_ms(Machine* m, const char* name) {
+  PyObject* cfg = attr(m->owner, "config");
+  PyObject* v = cfg ? attr(cfg, name) : nullptr;
+  const double r = v ? PyFloat_AsDouble(v) : 1000.0;
+  if (PyErr_Occurred()) PyErr_Clear();
+  Py_XDECREF(v);
+  Py_XDECREF(cfg);
+  return r;
+}
+
+void client_bump(Machine* m) {
+  if (++m->close_n == 3) request(m, K_CLOSED);
+}
+
+void client_enter(Machine* m, int st) {
+  PyObject* ow = m->owner;
+  switch (st) {
+    case K_NORMAL: {
+      call_void(ow, "_fx_normal");          // the first session, resolver
+      if (subscribe(m, ow, "closeAsserted", KE_CLOSE) < 0) report();
+      break;
+    }
+    case K_CLOSING: {
+      PyObject* sess = peer(m, "session");
+      PyObject* cset = peer(m, "cset");
+      PyObject* res = peer(m, "resolver");
+      PyObject* keep[3] = {sess, cset, res};
+      unsubscribe_others(m, keep, 3);
+      if ((sess && subscribe(m, sess, "stateChanged", KE_SESS_STATE) < 0) ||
+          (cset && subscribe(m, cset, "stateChanged", KE_SET_STATE) < 0) ||
+          (res && subscribe(m, res, "stateChanged", KE_RES_STATE) < 0))
+        report();
+      m->close_n = 0;
+      if (sess && (in_state(sess, "closed") || in_state(sess, "expired")))
+        ++m->close_n;
+      if (cset && in_state(cset, "stopped")) ++m->close_n;
+      if (res && in_state(res, "stopped")) ++m->close_n;
+      if (m->close_n == 3) {
+        request(m, K_CLOSED);
+      } else {
+        if (cset) call_void(cset, "stop");
+        if (res) call_void(res, "stop");
+        if (sess) call_void(sess, "close");
+        m->ping_iv = schedule(m, cfg_ms(m, "close_log_interval_ms"),
+                              KE_LOG_TICK);
+        if (m->ping_iv == nullptr) report();
+      }
+      Py_XDECREF(sess);
+      Py_XDECREF(cset);
+      Py_XDECREF(res);
+      break;
+    }
+    case K_CLOSED: {
+      cancel(m->ping_iv);
+      unsubscribe_others(m, nullptr, 0);
+      PyObject* r = PyObject_CallMethod(ow, "emit", "s", "close");
+      if (r == nullptr) report();
+      Py_XDECREF(r);
+      break;
+    }
+  }
+}
+
+void client_event(Machine* m, int kind, PyObject* src, PyObject* args) {
+  (void)src;
+  PyObject* a0 = PyTuple_GET_SIZE(args) > 0 ? PyTuple_GET_ITEM(args, 0) : nullptr;
+  if (m->state == K_NORMAL) {
+    if (kind == KE_CLOSE) request(m, K_CLOSING);
+    return;
+  }
+  if (m->state != K_CLOSING) return;
+  switch (kind) {
+    case KE_SESS_STATE:
+      if (str_is(a0, "closed") || str_is(a0, "expired")) client_bump(m);
+      break;
+    case KE_SET_STATE:
+    case KE_RES_STATE:
+      if (str_is(a0, "stopped")) client_bump(m);
+      break;
+    case KE_LOG_TICK: {
+      Py_CLEAR(m->ping_iv);
+      m->ping_iv = schedule(m, cfg_ms(m, "close_log_interval_ms"),
+                            KE_LOG_TICK);
+      PyObject* la = Py_BuildValue(
+          "(si)", "still waiting for zk client to shut down, %d/3 done",
+          m->close_n);
+      if (la) { logv(m->owner, "trace", la); Py_DECREF(la); }
+      break;
+    }
+  }
+}
+
+const Spec CLIENT{K_NAMES, K_N, client_enter, client_event};
+
 // ---- Python surface ---------------------------------------------------------
 
 int Machine_traverse(Machine* m, visitproc visit, void* arg) {
@@ -1035,6 +1143,7 @@ void Machine_dealloc(Machine* m) {
 const Spec* spec_of(const char* kind) {
   if (strcmp(kind, "session") == 0) return &SESSION;
   if (strcmp(kind, "connection") == 0) return &CONNECTION;
+  if (strcmp(kind, "client") == 0) return &CLIENT;
   return nullptr;
 }
 

@@ -36,7 +36,7 @@ from .connection_set import ConnectionSet, StaticResolver
 # than the round trip and does nothing); off on small hosts, where the
 # poller competes with the loop thread for the GIL.
 _SYNC_SPIN_US_AUTO = 100.0 if (os.cpu_count() or 1) >= 16 else 0.0
-from .session import ZKSession
+from .session import ZKSession, _zkmach, native_machines
 
 
 def _check_str(v, name):
@@ -158,7 +158,14 @@ class Client(FSM):
         self.cset.on('added', self._onSetAdded)
         self.cset.on('removed', self._onSetRemoved)
         self.cset.on('stateChanged', self._onSetStateChanged)
-        FSM.__init__(self, 'normal', self.loop)
+        if native_machines():
+            # the lifecycle on the C++ machine (csrc/host/zk_machines.cpp
+            # 'client'); FSM's getState / isInState read it as their core
+            self.fsm_loop = self.loop
+            self._fsm_core = _zkmach.Machine('client', self, self.loop)
+            self._fsm_core.start('normal')
+        else:
+            FSM.__init__(self, 'normal', self.loop)
 
     # aliases matching the reference's private field names used by tests
     @property
@@ -167,12 +174,19 @@ class Client(FSM):
 
     # -- lifecycle ------------------------------------------------------------
 
-    def state_normal(self, S):
+    def _fx_normal(self):
+        """Entering 'normal': the first session, then the resolver."""
         self._newSession()
         if self._resume_cred is not None:
             self.session.adopt_credentials(self._resume_cred)
             self._resume_cred = None
         self.resolver.start()
+
+    # the lifecycle as state functions: the Python oracle (ZKMI_PY_FSM=1)
+    # of the native machine
+
+    def state_normal(self, S):
+        self._fx_normal()
         S.on(self, 'closeAsserted', lambda: S.gotoState('closing'))
 
     def state_closing(self, S):

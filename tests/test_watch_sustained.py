@@ -37,5 +37,5 @@ def test_watch_steps_do_not_stall(gpu):
     print('watch steps: median %.3f ms, max %.3f ms (step %d)'
           % (med, ms.max(), worst))
     # every step delivered and checked every notification
-    assert int(acc.sum().item()) == steps * n
+    assert int(acc.sum().item()) == steps * pipe.n
     assert ms.max() < 2 * med, (ms.max(), med, worst)

@@ -1006,11 +1006,13 @@ static int enc_swz() {
   if (v < 0) { const char* e = getenv("ZKMI_ENC_SWZ"); v = e ? atoi(e) : 1; }
   return v;
 }
-// ZKMI_ENC_UNIFORM=0: uniform GET_DATA reply blocks through the LDS image
-// like any other (emit_uniform off)
+// ZKMI_ENC_UNIFORM=1: uniform GET_DATA reply blocks written straight from
+// the slots (emit_uniform).  Off by default: measured 0.651 -> 0.958 ms a GET
+// step (a 64-bit division and per-dword slot loads per 16-byte piece;
+// profiles/r5_regression_ab.md), the LDS image is faster.
 static int enc_uniform() {
   static int v = -1;
-  if (v < 0) { const char* e = getenv("ZKMI_ENC_UNIFORM"); v = e ? atoi(e) : 1; }
+  if (v < 0) { const char* e = getenv("ZKMI_ENC_UNIFORM"); v = e ? atoi(e) : 0; }
   return v;
 }
 static bool enc_fused() {

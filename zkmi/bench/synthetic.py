@@ -22,6 +22,7 @@ sync-free and no byte past a stream's end is walked.
 version CAS and ACL encode (BASELINE config 3).
 """
 
+import os
 import time
 
 import numpy as np
@@ -32,6 +33,14 @@ from ..ops import _lib
 from ..ops import batch as B
 
 I64, I32, U8 = torch.int64, torch.int32, torch.uint8
+
+# ZKMI_SERVE_TICKETS=1: the serve launch's last workgroup does the tree
+# finish (sign-off tickets) instead of a tree_finish_k launch.  Off by
+# default: every workgroup's release fence costs an L2 writeback on a
+# multi-XCD part — tree_serve 90 -> 231 us, the GET step 0.651 -> 0.718 ms
+# (profiles/r5_regression_ab.md); the extra launch is far cheaper.
+_SERVE_TICKETS = os.environ.get('ZKMI_SERVE_TICKETS', '0') == '1'
+
 
 def _len(total):
     """A stream length for K1: the encoder's device total (no host read)."""
@@ -439,7 +448,8 @@ class GpuServer(object):
             L.tree_serve_frames(self.tree.tensors, rx, ft.off, ft.length,
                                 ft.count, self.cap_frames, out, session, now,
                                 wslot, self.fired if self.tree.watch
-                                is not None else None, self.tickets)
+                                is not None else None,
+                                self.tickets if _SERVE_TICKETS else None)
         out, rec_off, total, err = B.encode_responses(
             r, self.tree.store, self.out.numel(), out=self.out,
             presized=self.presized, terminate=terminate)

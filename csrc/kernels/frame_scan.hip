@@ -88,6 +88,8 @@ constexpr int FL_NB = 2;                   // broken links the check saw
 constexpr int FL_GW = FL_NB + 1;
 constexpr int FL_LOC = 1024;               // a block's own broken links
 constexpr int FL_BROUNDS = 8;             // the last block's repair rounds
+constexpr int FL_DBG_BLOCKS = 16;          // fs_link blocks with a debug clock
+constexpr int FL_DBG_ROWS = 6;             // fs_link's debug rows past the tiles
 constexpr int FL_LOCAL_MIN = 64;           // ... walked by the block when
                                            // it found more than this many
 // Count blocks: frame counts scanned per FK_T tiles (one wave's worth)
@@ -2596,6 +2598,12 @@ __global__ __launch_bounds__(FL_T) void fs_link(
   __syncthreads();
   fl_check(ntiles, rec_entry, rec_exit, rec_meta, base, bsum, mins, &g[FL_NB],
            blist, lloc, &s_lcnt);
+  if (ldbg != nullptr && tid == 0 && blockIdx.x < FL_DBG_BLOCKS) {
+    // (ZKMI_FS_DBG: every block's entry and check-done clocks, rows 1-4 of
+    // fs_link's debug rows)
+    ldbg[8 + 2 * blockIdx.x] = t_in;
+    ldbg[8 + 2 * blockIdx.x + 1] = wall_clock64();
+  }
   // the big repair (see FL_BIG_NOSPEC): barrier rounds over the grid, then
   // block 0 goes on as the last block does
   const bool big = (uint32_t)ld_agent((const int64_t*)&stats[LW_NOSPEC]) >
@@ -2659,9 +2667,11 @@ __global__ __launch_bounds__(FL_T) void fs_link(
     // no broken link before the first terminal (the blocks re-walked only
     // links past it, whose counts no row uses): the row bases are bsum's
     // block offsets + the check's in-block bases
+    if (ldbg != nullptr && tid == 0) ldbg[40] = wall_clock64();
     fl_bases(n, ntiles, ft0, rec_exit, rec_meta, base, bsum, cap, result,
              lastk, red);
     if (tid == 0 && rew) g[1] = 0;
+    if (ldbg != nullptr && tid == 0) ldbg[41] = wall_clock64();
     return;
   }
   if (tid == 0) g[1] = 0;
@@ -2926,8 +2936,11 @@ static int64_t* fs_dbg_buf(int64_t tiles) {
   if (!on) return nullptr;
   if (tiles > g_dbg_tiles) {
     if (g_dbg) (void)hipFree(g_dbg);
-    // a row per tile (fs_tile) + one for fs_link's phase clock
-    if (hipMalloc(&g_dbg, (tiles + 1) * 8 * 8) != hipSuccess) return nullptr;
+    // a row per tile (fs_tile) + fs_link's: its phase clock, every block's
+    // entry / check-done clocks, the common path's ticket / end clocks
+    if (hipMalloc(&g_dbg, (tiles + FL_DBG_ROWS) * 8 * 8) != hipSuccess)
+      return nullptr;
+    (void)hipMemset(g_dbg, 0, (tiles + FL_DBG_ROWS) * 8 * 8);
     g_dbg_tiles = tiles;
   }
   return g_dbg;
@@ -3099,11 +3112,12 @@ int zk_frame_scan_stats(const uint8_t* ws, int64_t n_cap, int32_t window,
   return hipStreamSynchronize(st) == hipSuccess ? 0 : -1;
 }
 
-// rows = tiles + 1: the last row is fs_link's phase clock of a chase repair
-// (start, chases done, barrier, links checked, end; [6] / [7] the exact
-// chase's start and end)
+// rows = tiles + FL_DBG_ROWS: past the tiles' rows, fs_link's phase clock of
+// a chase repair (start, chases done, barrier, links checked, end; [6] / [7]
+// the exact chase's start and end), then every block's entry and check-done
+// clocks (4 rows), then the common path's bases start / end ([0] / [1])
 int zk_frame_scan_dbg(int64_t* host, int64_t tiles) {
-  if (!zk::g_dbg || tiles > zk::g_dbg_tiles + 1) return -1;
+  if (!zk::g_dbg || tiles > zk::g_dbg_tiles + zk::FL_DBG_ROWS) return -1;
   return hipMemcpy(host, zk::g_dbg, tiles * 8 * 8, hipMemcpyDeviceToHost) ==
                  hipSuccess ? 0 : -1;
 }

@@ -24,18 +24,26 @@ from zkmi.ops import _lib  # noqa: E402
 
 
 def fs_clock(cap_bytes):
-    """fs_link's phase clock row (the debug buffer's row past the tiles of
-    the scanned buffer's capacity)."""
+    """fs_link's debug rows past the tiles of the scanned buffer's
+    capacity: every block's entry and check-done clocks, the common path's
+    bases start / end (us from the earliest block entry; 100 MHz clock)."""
     tiles = (cap_bytes + 4095) // 4096
     try:
-        host = _lib.lib().frame_scan_dbg(tiles + 1).numpy().reshape(-1)
+        host = _lib.lib().frame_scan_dbg(tiles + 6).numpy().reshape(-1)
     except RuntimeError:
         return None                   # ZKMI_FS_DBG not set
-    row = host[tiles * 8:(tiles + 1) * 8]
-    t0 = row[5]
-    return {'path': int(row[4]) >> 56,
-            'us': [round((int(v) & ((1 << 56) - 1)) / 100.0 - t0 / 100.0, 1)
-                   if v else None for v in row[:5]]}
+    rows = host[tiles * 8:(tiles + 6) * 8]
+    blk = rows[8:40].reshape(16, 2).astype(np.int64)
+    live = blk[:, 0] > 0
+    if not live.any():
+        return None
+    t0 = int(blk[live, 0].min())
+    us = lambda v: round((int(v) - t0) / 100.0, 2)     # noqa: E731
+    return {'block_entry': [us(v) for v in blk[live, 0]],
+            'block_check_done': [us(v) for v in blk[live, 1]],
+            'bases': [us(rows[40]) if rows[40] else None,
+                      us(rows[41]) if rows[41] else None],
+            'repair_path': int(rows[4]) >> 56}
 
 
 def main():

@@ -1387,15 +1387,17 @@ int64_t zk_serve_tickets(int64_t ncap) {
   return 1 + (nb + 63) / 64;
 }
 
-int zk_tree_serve_frames(const ZkTree* t, const uint8_t* rx,
-                         const int64_t* foff, const int32_t* flen,
-                         const int64_t* n_dev, int64_t ncap, int32_t* r_op,
-                         int32_t* r_xid, int32_t* r_err, int64_t* r_node,
-                         int64_t* r_zxid, int64_t* r_path_off,
-                         int32_t* r_path_len, int64_t* r_slot,
-                         int64_t* r_sizes, int64_t* r_bsum, int64_t session,
-                         int64_t now_ms, int32_t wslot, int64_t* fired,
-                         unsigned* tickets, hipStream_t st) {
+// finish = 0: no finish at all (the caller launches zk_tree_finish, e.g. on
+// a side stream joined before the tree's next batch)
+int zk_tree_serve_frames2(const ZkTree* t, const uint8_t* rx,
+                          const int64_t* foff, const int32_t* flen,
+                          const int64_t* n_dev, int64_t ncap, int32_t* r_op,
+                          int32_t* r_xid, int32_t* r_err, int64_t* r_node,
+                          int64_t* r_zxid, int64_t* r_path_off,
+                          int32_t* r_path_len, int64_t* r_slot,
+                          int64_t* r_sizes, int64_t* r_bsum, int64_t session,
+                          int64_t now_ms, int32_t wslot, int64_t* fired,
+                          unsigned* tickets, int32_t finish, hipStream_t st) {
   if (ncap <= 0) return 0;
   if ((r_sizes == nullptr) != (r_bsum == nullptr)) return -1;
   ZkReqOut none{};
@@ -1406,7 +1408,31 @@ int zk_tree_serve_frames(const ZkTree* t, const uint8_t* rx,
       now_ms, nullptr, 0, 1, 0, 0, nullptr, wslot, fired, tickets);
   ZK_LAUNCH_CHECK();
   // tickets: the serve launch's last workgroup did the finish
-  return tickets != nullptr ? 0 : finish_launch(t, ncap, n_dev, 0, st);
+  return tickets != nullptr || !finish ? 0
+                                       : finish_launch(t, ncap, n_dev, 0, st);
+}
+
+int zk_tree_serve_frames(const ZkTree* t, const uint8_t* rx,
+                         const int64_t* foff, const int32_t* flen,
+                         const int64_t* n_dev, int64_t ncap, int32_t* r_op,
+                         int32_t* r_xid, int32_t* r_err, int64_t* r_node,
+                         int64_t* r_zxid, int64_t* r_path_off,
+                         int32_t* r_path_len, int64_t* r_slot,
+                         int64_t* r_sizes, int64_t* r_bsum, int64_t session,
+                         int64_t now_ms, int32_t wslot, int64_t* fired,
+                         unsigned* tickets, hipStream_t st) {
+  return zk_tree_serve_frames2(t, rx, foff, flen, n_dev, ncap, r_op, r_xid,
+                               r_err, r_node, r_zxid, r_path_off, r_path_len,
+                               r_slot, r_sizes, r_bsum, session, now_ms, wslot,
+                               fired, tickets, 1, st);
+}
+
+// The between-batch finish of a serve (parent Stat fix-up, free-ring
+// publish, zxid += *n_dev or bump) on its own: the partner of
+// zk_tree_serve_frames2(..., finish = 0).
+int zk_tree_finish(const ZkTree* t, const int64_t* n_dev, int64_t bump,
+                   int32_t publish, hipStream_t st) {
+  return finish_launch(t, 0, n_dev, bump, st, publish);
 }
 
 // Ordering workspace layout for up to ncap requests: the zeroed prefix

@@ -204,6 +204,14 @@ int zk_tree_serve_frames(const ZkTree*, const uint8_t*, const int64_t*,
                          int32_t*, int64_t*, int64_t*, int64_t*, int64_t,
                          int64_t, int32_t, int64_t*, unsigned*,
                          hipStream_t);
+int zk_tree_serve_frames2(const ZkTree*, const uint8_t*, const int64_t*,
+                          const int32_t*, const int64_t*, int64_t, int32_t*,
+                          int32_t*, int32_t*, int64_t*, int64_t*, int64_t*,
+                          int32_t*, int64_t*, int64_t*, int64_t*, int64_t,
+                          int64_t, int32_t, int64_t*, unsigned*, int32_t,
+                          hipStream_t);
+int zk_tree_finish(const ZkTree*, const int64_t*, int64_t, int32_t,
+                   hipStream_t);
 int zk_tree_serve_ordered(const ZkTree*, const uint8_t*, const ZkReqOut*,
                           const int64_t*, int64_t, int32_t*, int32_t*,
                           int32_t*, int64_t*, int64_t*, int64_t*, int32_t*,

@@ -564,13 +564,13 @@ void tree_serve_frames(const std::vector<Tensor>& t, const Tensor& rx,
                        const std::vector<Tensor>& r, int64_t session,
                        int64_t now_ms, int64_t wslot,
                        const c10::optional<Tensor>& fired,
-                       const c10::optional<Tensor>& tickets) {
+                       const c10::optional<Tensor>& tickets, bool finish) {
   ZkTree s = tree(t);
   const Tensor* d = &t[0];
   need(r, 10, "serve outputs");
   TORCH_CHECK(wslot >= -1 && wslot < 64, "zkmi: watcher slot -1..63");
   const int64_t nb = (ncap + 255) / 256;
-  hip_ok(zk_tree_serve_frames(
+  hip_ok(zk_tree_serve_frames2(
              &s, P<uint8_t>(rx, U8, 1, "rx", d),
              P<int64_t>(foff, I64, ncap, "frame_off", d),
              P<int32_t>(flen, I32, ncap, "frame_len", d),
@@ -588,8 +588,18 @@ void tree_serve_frames(const std::vector<Tensor>& t, const Tensor& rx,
              (int32_t)wslot, Popt<int64_t>(fired, I64, 5 * ncap, "fired", d),
              reinterpret_cast<unsigned*>(Popt<int32_t>(
                  tickets, I32, zk_serve_tickets(ncap), "tickets", d)),
-             cur_stream()),
+             finish ? 1 : 0, cur_stream()),
          "tree_serve_frames");
+}
+
+// The serve's finish on its own (after tree_serve_frames(..., finish=False)):
+// zxid += *n_dev (or bump when n_dev is None).
+void tree_finish(const std::vector<Tensor>& t, const c10::optional<Tensor>& n_dev,
+                 int64_t bump, bool publish) {
+  ZkTree s = tree(t);
+  hip_ok(zk_tree_finish(&s, Popt<int64_t>(n_dev, I64, 1, "count", &t[0]), bump,
+                        publish ? 1 : 0, cur_stream()),
+         "tree_finish");
 }
 
 int64_t tree_order_workspace(int64_t n) {
@@ -959,7 +969,10 @@ TORCH_LIBRARY(zkmi, m) {
   m.def("tree_serve_frames(Tensor(a!)[] tree, Tensor rx, Tensor frame_off, "
         "Tensor frame_len, Tensor count, int ncap, Tensor(b!)[] out, "
         "int session, int now_ms, int wslot=-1, Tensor(c!)? fired=None, "
-        "Tensor(d!)? tickets=None) -> ()", &tree_serve_frames);
+        "Tensor(d!)? tickets=None, bool finish=True) -> ()",
+        &tree_serve_frames);
+  m.def("tree_finish(Tensor(a!)[] tree, Tensor? count, int bump=0, "
+        "bool publish=True) -> ()", &tree_finish);
   m.def("tree_order_workspace(int n) -> int", &tree_order_workspace);
   m.def("tree_order_stats_offset(int n) -> int", &tree_order_stats_offset);
   m.def("tree_serve_ordered(Tensor(a!)[] tree, Tensor rx, Tensor[] requests, "

@@ -40,6 +40,10 @@ I64, I32, U8 = torch.int64, torch.int32, torch.uint8
 # multi-XCD part — tree_serve 90 -> 231 us, the GET step 0.651 -> 0.718 ms
 # (profiles/r5_regression_ab.md); the extra launch is far cheaper.
 _SERVE_TICKETS = os.environ.get('ZKMI_SERVE_TICKETS', '0') == '1'
+# GET pipelines fork the serve's tree finish to a side stream (off the reply
+# path; the single-workgroup kernel waited 15 us for a CU behind the other
+# connection's kernels); ZKMI_SIDE_FINISH=0 keeps it in line
+_SIDE_FINISH = os.environ.get('ZKMI_SIDE_FINISH', '1') != '0'
 
 
 def _len(total):
@@ -419,10 +423,15 @@ class GpuServer(object):
         return self.result
 
     def serve_steps(self, rx, n, session=0, terminate=False, ordered=False,
-                    passes=4, wslot=-1, resume=False):
+                    passes=4, wslot=-1, resume=False, side=None):
         """:meth:`serve` as a generator yielding once, between the request
         decode and the tree; the return tuple lands in ``self.result`` (a
-        pipelined caller interleaves another connection's work there)."""
+        pipelined caller interleaves another connection's work there).
+
+        ``side`` (a read-only batch only: GET_DATA / EXISTS / GET_CHILDREN):
+        the tree's between-batch finish (zxid, free-ring publish) runs on
+        that stream, forked after the serve and off the reply path; the
+        caller joins it with :meth:`join` before the tree's next batch."""
         L = _lib.lib()
         ft = self.scanner.scan(rx, n)
         # ordered serving ranks the batch from K12's request table; the
@@ -449,7 +458,13 @@ class GpuServer(object):
                                 ft.count, self.cap_frames, out, session, now,
                                 wslot, self.fired if self.tree.watch
                                 is not None else None,
-                                self.tickets if _SERVE_TICKETS else None)
+                                self.tickets if _SERVE_TICKETS else None,
+                                side is None)
+            if side is not None:
+                side.wait_stream(torch.cuda.current_stream(self.tree.device))
+                with torch.cuda.stream(side):
+                    L.tree_finish(self.tree.tensors, ft.count, 0, True)
+                self._side = side
         out, rec_off, total, err = B.encode_responses(
             r, self.tree.store, self.out.numel(), out=self.out,
             presized=self.presized, terminate=terminate)
@@ -461,6 +476,14 @@ class GpuServer(object):
                 if wslot < 0:
                     raise ValueError('resume needs the watcher slot')
                 self._resume(rx, ft, wslot)
+
+    def join(self):
+        """Wait (on the current stream) for a finish forked by
+        ``serve_steps(..., side=...)``."""
+        side = getattr(self, '_side', None)
+        if side is not None:
+            torch.cuda.current_stream(self.tree.device).wait_stream(side)
+            self._side = None
 
     def order_stats(self):
         """(largest same-path rank, scratch bytes used) of the last ordered
@@ -538,6 +561,10 @@ class GetPipeline(object):
         self.step_no = 0
         self.idx = torch.empty(n, dtype=I64, device=dev)
         self.xid = torch.empty(n, dtype=I32, device=dev)
+        # the serve's tree finish on a side stream (a GET batch changes
+        # nothing the replies read: off the reply path; ZKMI_SIDE_FINISH=0
+        # keeps it in line)
+        self.side = torch.cuda.Stream(dev) if _SIDE_FINISH else None
         self.poff = torch.empty(n, dtype=I64, device=dev)
         self.plen = torch.empty(n, dtype=I32, device=dev)
         self.gstate = None      # device {seed, step} (see capture)
@@ -641,7 +668,7 @@ class GetPipeline(object):
                             self.acl_len, self.acl_arena)
         tx, rec_off, total, err = B.encode_requests(rb, self.xt, out=self.tx)
         yield
-        srv = self.server.serve_steps(tx, _len(total))
+        srv = self.server.serve_steps(tx, _len(total), side=self.side)
         next(srv)
         yield
         for _ in srv:
@@ -660,6 +687,7 @@ class GetPipeline(object):
                                tick=self.gstate if validate else None)
         if self.gstate is not None and not validate:
             self.gstate[1:].add_(1)
+        self.server.join()
         self.last = (self.idx, rep, rx, ft)
 
 

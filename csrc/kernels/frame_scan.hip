@@ -2570,7 +2570,7 @@ __global__ __launch_bounds__(FL_T) void fs_link(
     int64_t* __restrict__ bsum, uint64_t* mins,
     int64_t* __restrict__ lastk, unsigned long long* g,
     const uint64_t* lbw, const int64_t* __restrict__ cx,
-    int64_t* __restrict__ ldbg) {
+    int64_t* __restrict__ ldbg, int32_t local_min) {
   __shared__ __attribute__((aligned(16)))
       uint8_t win[(FL_T / 64) * (FC_WIN + 16)];      // one per wave
   __shared__ int64_t red[2 * (FL_T / 64) + 2];
@@ -2626,7 +2626,7 @@ __global__ __launch_bounds__(FL_T) void fs_link(
   // the ends of a phantom chain's region — are the last block's chases:
   // an exact chase runs on through a region of consistent-but-wrong links
   // that no per-link walk sees broken)
-  if (!big && s_lcnt > FL_LOCAL_MIN) {
+  if (!big && s_lcnt > local_min) {
     const uint32_t w = fl_local_round(buf, n, ntiles, maxp, sx, list, rcount,
                                       pre, rec_entry, rec_exit, rec_meta, lloc,
                                       min(s_lcnt, FL_LOC), win);
@@ -2903,6 +2903,17 @@ static FsPlan fs_plan(int64_t n) {
   return p;
 }
 
+// A block re-walks its own broken links before its ticket when it found
+// more than this many (ZKMI_FL_LOCAL_MIN overrides FL_LOCAL_MIN, for A/B)
+static int32_t fl_local_min() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("ZKMI_FL_LOCAL_MIN");
+    v = e ? atoi(e) : FL_LOCAL_MIN;
+  }
+  return v;
+}
+
 // fs_link's grid: the check's workgroups (the last to finish goes on).
 static unsigned fl_blocks() { return 16; }
 
@@ -3063,7 +3074,8 @@ int zk_frame_scan5(const uint8_t* buf, const int64_t* n_dev, int64_t n_cap,
   fs_link<<<fl_blocks(), FL_T, 0, st>>>(buf, n_dev, n_cap, maxp, sx, list, rcnt,
                                  pre, rent, rexit, rmeta, base, cap, result,
                                  lbw + 2 * tiles, blist, bsum, mins, lastk,
-                                 grid, lbw, cx, dbg ? dbg + 8 * tiles : nullptr);
+                                 grid, lbw, cx, dbg ? dbg + 8 * tiles : nullptr,
+                                 fl_local_min());
   ZK_LAUNCH_CHECK();
   fs_rows<<<(unsigned)((tiles + 3) / 4), 256, 0, st>>>(
       buf, n_dev, n_cap, list, pre, rmeta, rent, rexit, base, bsum, lastk,

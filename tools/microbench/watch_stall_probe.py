@@ -49,7 +49,21 @@ def fs_clock(cap_bytes):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--steps', type=int, default=130)
+    ap.add_argument('--gc', choices=('on', 'off', 'freeze'), default='on',
+                    help='the Python collector during the steps')
+    ap.add_argument('--all', action='store_true',
+                    help='every step (no stop at the first slow one)')
     a = ap.parse_args()
+    import gc
+    gcs = []            # (step, generation, ms) of every collection
+
+    def on_gc(phase, info, box={}):
+        if phase == 'start':
+            box['t'] = time.perf_counter()
+        else:
+            gcs.append((len(times), info['generation'],
+                        1e3 * (time.perf_counter() - box.get('t', 0))))
+    gc.callbacks.append(on_gc)
     dev = torch.device('cuda', 0)
     n = 1 << 20
     tree = S.GpuTree(1000000, 100, device=dev, seed=0, watch_cap=2 * n)
@@ -57,6 +71,11 @@ def main():
     acc = torch.zeros(64, dtype=torch.int64, device=dev)
     pipe.nscan.chain_stats()
     times = []
+    if a.gc == 'off':
+        gc.disable()
+    elif a.gc == 'freeze':
+        gc.collect()
+        gc.freeze()
     for s in range(a.steps):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -66,7 +85,11 @@ def main():
         st = pipe.nscan.chain_stats()
         med = float(np.median(times)) if times else ms
         times.append(ms)
-        if s < 5 or ms < 5 * med:
+        slow_gc = [g for g in gcs if g[0] == s and g[2] > 5]
+        if slow_gc:
+            print('step %d %.2f ms: collections %r' % (s, ms, slow_gc),
+                  flush=True)
+        if s < 5 or ms < 5 * med or a.all:
             if s % 10 == 0:
                 print('step %d %.2f ms %r' % (s, ms, st), flush=True)
             continue
@@ -91,8 +114,12 @@ def main():
                 pipe.nscan.chain_stats(), fs_clock(pipe.rx.numel())),
                 flush=True)
         break
-    print('done', int(acc.sum().item()), 'median %.3f ms max %.3f ms' % (
-        float(np.median(times)), max(times)), flush=True)
+    print('done', int(acc.sum().item()), 'median %.3f ms max %.3f ms '
+          '(step %d); gc %s: %d collections, gen2 %r' % (
+              float(np.median(times[1:])), max(times[1:]),
+              int(np.argmax(times[1:])) + 1, a.gc, len(gcs),
+              [(g[0], round(g[2], 1)) for g in gcs if g[1] == 2]),
+          flush=True)
 
 
 if __name__ == '__main__':

@@ -166,6 +166,9 @@ int64_t zk_frame_scan_workspace(int64_t n);
 int zk_frame_scan5(const uint8_t*, const int64_t*, int64_t, int64_t,
                    uint8_t*, int64_t, int64_t*, int32_t*, int64_t, int64_t*,
                    int32_t, int32_t, int32_t, hipStream_t);
+int zk_frame_scan6(const uint8_t*, const int64_t*, int64_t, int64_t, uint8_t*,
+                   int64_t, int64_t*, int32_t*, int64_t, int64_t*, int32_t,
+                   int32_t, int32_t, hipStream_t, hipStream_t);
 int zk_frame_scan_stats(const uint8_t*, int64_t, int32_t, uint32_t*,
                         hipStream_t);
 int zk_frame_scan_dbg(int64_t* host, int64_t tiles);

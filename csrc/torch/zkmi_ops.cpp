@@ -358,21 +358,22 @@ int64_t frame_scan_workspace(int64_t n) { return zk_frame_scan_workspace(n); }
 void frame_scan(const Tensor& buf, const c10::optional<Tensor>& n_dev,
                 int64_t n_cap, int64_t max_packet, const Tensor& ws,
                 const Tensor& foff, const Tensor& flen, const Tensor& result,
-                int64_t window, bool clean, int64_t flags) {
+                int64_t window, bool clean, int64_t flags, int64_t link_stream) {
   TORCH_CHECK(n_cap >= 0 && n_cap <= buf.numel(),
               "zkmi: frame_scan length ", n_cap, " past the buffer (",
               buf.numel(), " bytes)");
   TORCH_CHECK(ws.numel() >= zk_frame_scan_workspace(n_cap),
               "zkmi: frame_scan workspace too small");
   const int64_t cap = foff.numel();
-  hip_ok(zk_frame_scan5(
+  hip_ok(zk_frame_scan6(
              P<uint8_t>(buf, U8, 1, "buf"),
              Popt<int64_t>(n_dev, I64, 1, "n", &buf), n_cap, max_packet,
              P<uint8_t>(ws, U8, 1, "ws", &buf), ws.numel(),
              P<int64_t>(foff, I64, 1, "frame_off", &buf),
              P<int32_t>(flen, I32, cap, "frame_len", &buf), cap,
              P<int64_t>(result, I64, 4, "result", &buf), (int32_t)window,
-             clean ? 1 : 0, (int32_t)flags, cur_stream()),
+             clean ? 1 : 0, (int32_t)flags, cur_stream(),
+             reinterpret_cast<hipStream_t>(link_stream)),
          "frame_scan");
 }
 
@@ -934,7 +935,8 @@ TORCH_LIBRARY(zkmi, m) {
   m.def("frame_scan_workspace(int n) -> int", &frame_scan_workspace);
   m.def("frame_scan(Tensor buf, Tensor? n, int n_cap, int max_packet, "
         "Tensor(a!) ws, Tensor(b!) frame_off, Tensor(c!) frame_len, "
-        "Tensor(d!) result, int window, bool clean=False, int flags=0) -> ()",
+        "Tensor(d!) result, int window, bool clean=False, int flags=0, "
+        "int link_stream=0) -> ()",
         &frame_scan);
   m.def("frame_scan_stats(Tensor ws, int n_cap, int window) -> int[]",
         &frame_scan_stats);

@@ -44,6 +44,7 @@ _SERVE_TICKETS = os.environ.get('ZKMI_SERVE_TICKETS', '0') == '1'
 # path; the single-workgroup kernel waited 15 us for a CU behind the other
 # connection's kernels); ZKMI_SIDE_FINISH=0 keeps it in line
 _SIDE_FINISH = os.environ.get('ZKMI_SIDE_FINISH', '1') != '0'
+_LINK_PRIO = os.environ.get('ZKMI_LINK_PRIO', '1') != '0'
 
 
 def _len(total):
@@ -551,9 +552,14 @@ class GetPipeline(object):
                                 window=B.frame_window(17 + maxpath))
         self.rwindow = B.frame_window(4 + 16 + 4 + dmax + 68)
         lo, hi = tree.data_dist or (tree.data_bytes, tree.data_bytes)
+        # fs_link of both scans on a high-priority stream (its workgroups
+        # go ahead of the other connection's waiting ones; ZKMI_LINK_PRIO=0
+        # keeps it in line)
+        self.link = torch.cuda.Stream(dev, priority=-1) if _LINK_PRIO \
+            else None
         self.rscanner = B.FrameScanner(n, dev, window=self.rwindow,
                                        frame_hint=4 + 16 + 4 + 68 +
-                                       (lo + hi) // 2)
+                                       (lo + hi) // 2, link_stream=self.link)
         self.reply = B.alloc_replies(n, dev)
         self.xid_base = 0
         self.last = None
@@ -565,6 +571,7 @@ class GetPipeline(object):
         # nothing the replies read: off the reply path; ZKMI_SIDE_FINISH=0
         # keeps it in line)
         self.side = torch.cuda.Stream(dev) if _SIDE_FINISH else None
+        self.server.scanner.link_stream = self.link
         self.poff = torch.empty(n, dtype=I64, device=dev)
         self.plen = torch.empty(n, dtype=I32, device=dev)
         self.gstate = None      # device {seed, step} (see capture)

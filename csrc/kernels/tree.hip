@@ -155,21 +155,31 @@ ZK_DEV bool bytes_eq(const uint8_t* a, const uint8_t* b, int32_t n) {
   return true;
 }
 
-ZK_DEV int64_t* ht_key(const ZkTree& t, int64_t s) { return &t.ht[2 * s]; }
-ZK_DEV int64_t* ht_val(const ZkTree& t, int64_t s) { return &t.ht[2 * s + 1]; }
+// One 64-byte entry per slot (a cache line; open addressing, linear
+// probing): int64 words [0] key = path hash | 1 (0 empty), [1] val (node |
+// slot offset, below; -2 tombstone, -3 empty or being published), [2] path
+// length | data length << 32, [3, 8) the path's first EN_PATH bytes.  A
+// lookup loads the entry in one burst and verifies the path and gets a GET
+// reply's data length from it: ONE random line per lookup (rounds 2-4 read
+// the 16-byte {key, val} entry and then the node's 64-byte lookup line, a
+// second dependent random read).  Longer paths compare their tail in the
+// arena.  The node lookup lines (node_line) are no longer read.
+constexpr int HT_W = 8;                    // int64 words per entry
+constexpr int EN_PATH = 40;                // path bytes held in the entry
+
+ZK_DEV int64_t* ht_ent(const ZkTree& t, int64_t s) { return &t.ht[HT_W * s]; }
+ZK_DEV int64_t* ht_key(const ZkTree& t, int64_t s) { return &t.ht[HT_W * s]; }
+ZK_DEV int64_t* ht_val(const ZkTree& t, int64_t s) { return &t.ht[HT_W * s + 1]; }
+
 // Node v's path as one word (offset << 24 | length; paths < 16 MiB like
-// the frames that carry them): a lookup verifies against it with one random
-// read instead of two (node_path_off / node_path_len stay the primary
-// record; create keeps the word in step).
+// the frames that carry them): the arena tail of a long path.
 ZK_DEV int64_t pw_pack(int64_t off, int32_t len) {
   return (off << 24) | (int64_t)(uint32_t)len;
 }
-// Node lookup line (64 bytes, one cache line per node): path length, data
-// length and the path's first LN_PATH bytes.  A hash hit verifies the path
-// and gets a GET reply's data length from this one line — the hash entry
-// and the line are a lookup's only random reads (round 2 read the path
-// word, the path bytes in the arena and data_len[]: four).  Longer paths
-// compare their tail in the arena.
+
+// Node lookup line (64 bytes per node): path length, data length and the
+// path's first LN_PATH bytes.  Written for the node table's record; the
+// lookups use the hash entries' copy.
 constexpr int LN_BYTES = 64, LN_PATH = 56;
 
 ZK_DEV void line_set(const ZkTree& t, int64_t v, const uint8_t* p, int32_t n,
@@ -180,24 +190,60 @@ ZK_DEV void line_set(const ZkTree& t, int64_t v, const uint8_t* p, int32_t n,
   copy_bytes(ln + 8, p, n < LN_PATH ? n : LN_PATH);
 }
 
-ZK_DEV void line_set_dlen(const ZkTree& t, int64_t v, int32_t dl) {
-  __builtin_memcpy(t.node_line + v * LN_BYTES + 4, &dl, 4);
+// The entry's path / data length words (everything but key and val); plain
+// stores before the val is published.
+ZK_DEV void ent_fill(const ZkTree& t, int64_t s, const uint8_t* p, int32_t n,
+                     int32_t dl) {
+  int64_t* e = ht_ent(t, s);
+  e[2] = (int64_t)(uint32_t)n | ((int64_t)dl << 32);
+  uint8_t* pb = (uint8_t*)&e[3];
+  const int32_t h = n < EN_PATH ? n : EN_PATH;
+  copy_bytes(pb, p, h);
 }
 
-// Is node v's path p[0, n)?  *dl gets its data length (from the same line).
-ZK_DEV bool path_is(const ZkTree& t, int64_t v, const uint8_t* p, int32_t n,
-                    int32_t* dl = nullptr) {
-  const uint8_t* ln = t.node_line + v * LN_BYTES;
-  int32_t hd[2];
-  __builtin_memcpy(hd, ln, 8);
-  if (dl != nullptr) *dl = hd[1];
-  if (hd[0] != n) return false;
-  const int32_t head = n < LN_PATH ? n : LN_PATH;
-  if (!bytes_eq(ln + 8, p, head)) return false;
-  if (n <= LN_PATH) return true;
+ZK_DEV void ent_set_dlen(const ZkTree& t, int64_t s, int32_t dl) {
+  __builtin_memcpy((uint8_t*)ht_ent(t, s) + 20, &dl, 4);
+}
+
+// 8 bytes of p at o (up to n: a shorter tail is zero-filled)
+ZK_DEV uint64_t path_word(const uint8_t* p, int32_t o, int32_t n) {
+  uint64_t w = 0;
+  if (o + 8 <= n) {
+    __builtin_memcpy(&w, p + o, 8);
+  } else {
+    for (int32_t k = 0; o + k < n; ++k) w |= (uint64_t)p[o + k] << (8 * k);
+  }
+  return w;
+}
+
+// Does entry e (its words loaded) name path p[0, n) of node v?
+ZK_DEV bool ent_is(const ZkTree& t, const int64_t (&e)[HT_W], int64_t v,
+                   const uint8_t* p, int32_t n) {
+  if ((int32_t)(uint32_t)e[2] != n) return false;
+  const int32_t h = n < EN_PATH ? n : EN_PATH;
+#pragma unroll
+  for (int w = 0; w < EN_PATH / 8; ++w) {
+    if (8 * w >= h) break;
+    uint64_t x = (uint64_t)e[3 + w];
+    const int32_t left = h - 8 * w;
+    if (left < 8) x &= (1ull << (8 * left)) - 1;   // (copy_bytes left the
+                                                   // rest of the word as is)
+    if (x != path_word(p, 8 * w, h)) return false;
+  }
+  if (n <= EN_PATH) return true;
   const int64_t pw = t.node_pw[v];
-  return bytes_eq(t.path_arena + (pw >> 24) + LN_PATH, p + LN_PATH,
-                  n - LN_PATH);
+  return bytes_eq(t.path_arena + (pw >> 24) + EN_PATH, p + EN_PATH,
+                  n - EN_PATH);
+}
+
+ZK_DEV void ent_load(const ZkTree& t, int64_t s, int64_t (&e)[HT_W]) {
+  const uint4* q = (const uint4*)ht_ent(t, s);
+#pragma unroll
+  for (int k = 0; k < HT_W / 2; ++k) {
+    const uint4 v = q[k];
+    e[2 * k] = (int64_t)((uint64_t)v.x | (uint64_t)v.y << 32);
+    e[2 * k + 1] = (int64_t)((uint64_t)v.z | (uint64_t)v.w << 32);
+  }
 }
 
 // A hash val holds the node index (low 32 bits) and its slot offset / 16
@@ -209,36 +255,35 @@ ZK_DEV int64_t val_pack(int64_t v, int64_t slot) {
 ZK_DEV int64_t val_node(int64_t x) { return x & 0xFFFFFFFFll; }
 ZK_DEV int64_t val_slot(int64_t x) { return (int64_t)((uint64_t)x >> 32) << 4; }
 
-// Node of path p (node -1 if absent) and its slot offset.
+// Node of path p (node -1 if absent), its slot offset and data length, and
+// the hash entry (for a SET_DATA's data length update).
 struct Found {
   int64_t node, slot;
-  int32_t dlen;      // data length (DLEN lookups only)
+  int32_t dlen;
+  int64_t ent;
 };
 
-// DLEN: also fetch the node's data length, issued with the path-word load
-// right after the hash hit (before verification) so a GET's reply size is
-// not one more dependent round trip.
 template <bool DLEN = false>
 ZK_DEV Found tree_lookup(const ZkTree& t, const uint8_t* p, int32_t n) {
+  (void)DLEN;
   const int64_t key = (int64_t)(path_hash(p, n) | 1ull);
   int64_t s = key & t.mask;
   for (int64_t probe = 0; probe <= t.mask; ++probe) {
-    // one 16-byte {key, val} entry per probe; entries being written
-    // concurrently in this launch may read torn (val -3): not found, as the
-    // batch contract allows for same-batch conflicts on one path
-    const int64_t* ent = ht_key(t, s);
-    const int64_t k = ent[0];
-    const int64_t v = ent[1];
-    if (k == 0) break;
-    if (k == key && v >= 0) {
-      const int64_t node = val_node(v);
-      int32_t dl = 0;
-      if (path_is(t, node, p, n, DLEN ? &dl : nullptr))
-        return Found{node, val_slot(v), dl};
+    // one 64-byte entry per probe, loaded in one burst; entries being
+    // written concurrently in this launch may read torn (val -3): not
+    // found, as the batch contract allows for same-batch conflicts on one
+    // path
+    int64_t e[HT_W];
+    ent_load(t, s, e);
+    if (e[0] == 0) break;
+    if (e[0] == key && e[1] >= 0) {
+      const int64_t node = val_node(e[1]);
+      if (ent_is(t, e, node, p, n))
+        return Found{node, val_slot(e[1]), (int32_t)(e[2] >> 32), s};
     }
     s = (s + 1) & t.mask;
   }
-  return Found{-1, -1, 0};
+  return Found{-1, -1, 0, -1};
 }
 
 ZK_DEV int64_t tree_find(const ZkTree& t, const uint8_t* p, int32_t n) {
@@ -251,7 +296,7 @@ ZK_DEV int64_t tree_find(const ZkTree& t, const uint8_t* p, int32_t n) {
 // answers SYSTEMERROR rather than probing on and indexing the path twice).
 constexpr int64_t TREE_INSERT_TIMEOUT = -4;
 ZK_DEV int64_t tree_insert(const ZkTree& t, int64_t v, const uint8_t* p,
-                           int32_t n) {
+                           int32_t n, int32_t dl) {
   const int64_t key = (int64_t)(path_hash(p, n) | 1ull);
   const int64_t pv = val_pack(v, t.store.slot_off[v]);
   int64_t s = key & t.mask;
@@ -259,6 +304,7 @@ ZK_DEV int64_t tree_insert(const ZkTree& t, int64_t v, const uint8_t* p,
     const int64_t k = atomicCAS((unsigned long long*)ht_key(t, s), 0ull,
                                 (unsigned long long)key);
     if (k == 0) {                         // claimed an empty slot
+      ent_fill(t, s, p, n, dl);
       __hip_atomic_store(ht_val(t, s), pv, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
       return v;
@@ -270,11 +316,21 @@ ZK_DEV int64_t tree_insert(const ZkTree& t, int64_t v, const uint8_t* p,
         w = __hip_atomic_load(ht_val(t, s), __ATOMIC_RELAXED,
                               __HIP_MEMORY_SCOPE_AGENT);
       if (w == -3) return TREE_INSERT_TIMEOUT;
-      if (w >= 0 && path_is(t, val_node(w), p, n)) return val_node(w);
-      if (w == -2 &&                      // tombstone of the same key: reuse
+      if (w >= 0) {
+        int64_t e[HT_W];
+        ent_load(t, s, e);
+        if (ent_is(t, e, val_node(w), p, n)) return val_node(w);
+      }
+      // a tombstone of the same key: claim it (-3 while its words are
+      // rewritten), then publish
+      if (w == -2 &&
           atomicCAS((unsigned long long*)ht_val(t, s), (unsigned long long)-2,
-                    (unsigned long long)pv) == (unsigned long long)-2)
+                    (unsigned long long)-3) == (unsigned long long)-2) {
+        ent_fill(t, s, p, n, dl);
+        __hip_atomic_store(ht_val(t, s), pv, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
         return v;
+      }
     }
     s = (s + 1) & t.mask;
   }
@@ -425,7 +481,8 @@ __global__ __launch_bounds__(TR_T) void tree_build_k(ZkTree t, int64_t n0,
                                                     int64_t n) {
   const int64_t v = n0 + (int64_t)blockIdx.x * TR_T + threadIdx.x;
   if (v >= n || t.node_parent[v] == NODE_FREE) return;
-  tree_insert(t, v, t.path_arena + t.node_path_off[v], t.node_path_len[v]);
+  tree_insert(t, v, t.path_arena + t.node_path_off[v], t.node_path_len[v],
+              t.store.data_len[v]);
 }
 
 // Write "%010d" of a non-negative sequence number (ZooKeeper's sequential
@@ -491,7 +548,6 @@ ZK_DEV int32_t do_create(const ZkTree& t, Lane& L, const uint8_t* data,
   copy_bytes(slot + ZK_SLOT_DATA, data, dl);
   t.node_path_len[v] = npl;
   s.data_len[v] = dl;
-  line_set(t, v, pd, npl, dl);
   t.cver[v] = 0;
   t.nchild[v] = 0;
   t.pzxid[v] = L.zx;
@@ -502,7 +558,7 @@ ZK_DEV int32_t do_create(const ZkTree& t, Lane& L, const uint8_t* data,
   // batch contract; every field it could read is in bounds), and the next
   // launch sees everything.  A __threadfence here is an XCD-L2 writeback
   // per wave (MI355X_MICROARCH.md: ~3.5 us each) and cost milliseconds.
-  const int64_t ins = tree_insert(t, v, pd, npl);
+  const int64_t ins = tree_insert(t, v, pd, npl, dl);
   if (ins == TREE_INSERT_TIMEOUT) return ERR_SYSTEM;
   if (ins != v) return ERR_NODE_EXISTS;
   if (par >= 0) parent_touch(t, par, 1, !seq, L.zx);
@@ -675,7 +731,7 @@ __global__ __launch_bounds__(TR_T) void tree_serve_k(
         copy_bytes(slot + ZK_SLOT_DATA, rx + rq.doff, L.dl);
         st_be32(slot + ZK_SLOT_LEN, L.dl > 0 ? L.dl : -1);
         s.data_len[node] = L.dl;
-        line_set_dlen(t, node, L.dl);
+        ent_set_dlen(t, f.ent, L.dl);
         st_be64(slot + 8, L.zx);                      // mzxid
         st_be64(slot + 24, now_ms);                   // mtime
         st_be32(slot + 52, L.dl);                     // dataLength

@@ -118,11 +118,14 @@ ZkTree tree(const std::vector<Tensor>& v) {
               v.size());
   const Tensor* r = &v[0];
   ZkTree t;
-  const int64_t hw = v[0].numel() / 2;          // {key, val} entries
-  TORCH_CHECK(hw > 0 && (hw & (hw - 1)) == 0,
-              "zkmi: tree.ht must hold a power of two of 2-word entries");
+  // 64-byte entries: key, val, lengths, the path's head (tree.hip HT_W)
+  const int64_t hw = v[0].numel() / 8;
+  TORCH_CHECK(hw > 0 && (hw & (hw - 1)) == 0 && v[0].numel() % 8 == 0,
+              "zkmi: tree.ht must hold a power of two of 8-word entries");
   const int64_t cap = v[7].numel();
-  t.ht = P<int64_t>(v[0], I64, 2, "tree.ht", r);
+  t.ht = P<int64_t>(v[0], I64, 8, "tree.ht", r);
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.ht) % 64 == 0,
+              "zkmi: tree.ht must be 64-byte aligned");
   t.mask = hw - 1;
   t.node_path_off = P<int64_t>(v[1], I64, cap, "tree.node_path_off", r);
   t.node_path_len = P<int32_t>(v[2], I32, cap, "tree.node_path_len", r);

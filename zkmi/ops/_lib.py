@@ -38,7 +38,7 @@ TC_FREE_HEAD, TC_FREE_TAIL, TC_FREE_PUB, TC_DIRTY = 4, 5, 6, 7
 TC_SESS, TC_N = 8, 9
 # serve / expire `session` argument: the one in counters[TC_SESS]
 SESS_DEV = -2
-HT_WORDS = 2     # int64 words per hash entry {key, val}
+HT_WORDS = 8     # int64 words per hash entry: key, val, lengths, path head
 
 SCAN_SHFL, SCAN_MFMA, SCAN_MFMA_W1, SCAN_MFMA_W4 = 0, 1, 2, 3
 

@@ -90,8 +90,13 @@ constexpr int FL_LOC = 1024;               // a block's own broken links
 constexpr int FL_BROUNDS = 8;             // the last block's repair rounds
 constexpr int FL_DBG_BLOCKS = 16;          // fs_link blocks with a debug clock
 constexpr int FL_DBG_ROWS = 6;             // fs_link's debug rows past the tiles
-constexpr int FL_LOCAL_MIN = 64;           // ... walked by the block when
-                                           // it found more than this many
+// A block's own round over the broken links it found, before its ticket:
+// off (the threshold is past any count).  Measured with the threshold at 64
+// (tools/microbench/fl_probe.py, profiles/r5_fs_link_ab.md): the phantom-chain
+// stream 0.69 ms a scan (one block walked 82 tiles serially before the last
+// block could chase the region), 0.27 ms without; the dense and no-spec
+// streams the same either way.
+constexpr int FL_LOCAL_MIN = 1 << 30;
 // Count blocks: frame counts scanned per FK_T tiles (one wave's worth)
 constexpr int FK_T = 64;
 // The workspace's words after the X flags (uint64, lbw + 2 * tiles): [0..3]

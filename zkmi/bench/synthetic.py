@@ -44,7 +44,10 @@ _SERVE_TICKETS = os.environ.get('ZKMI_SERVE_TICKETS', '0') == '1'
 # path; the single-workgroup kernel waited 15 us for a CU behind the other
 # connection's kernels); ZKMI_SIDE_FINISH=0 keeps it in line
 _SIDE_FINISH = os.environ.get('ZKMI_SIDE_FINISH', '1') != '0'
-_LINK_PRIO = os.environ.get('ZKMI_LINK_PRIO', '1') != '0'
+# ZKMI_LINK_PRIO=1: the GET scans' fs_link on a high-priority stream (fork
+# and join by events inside the scan).  Off: a captured step with it
+# segfaulted in hipStreamEndCapture (test_gpu_get_pipeline_graph_replay)
+_LINK_PRIO = os.environ.get('ZKMI_LINK_PRIO', '0') == '1'
 
 
 def _len(total):
@@ -553,8 +556,8 @@ class GetPipeline(object):
         self.rwindow = B.frame_window(4 + 16 + 4 + dmax + 68)
         lo, hi = tree.data_dist or (tree.data_bytes, tree.data_bytes)
         # fs_link of both scans on a high-priority stream (its workgroups
-        # go ahead of the other connection's waiting ones; ZKMI_LINK_PRIO=0
-        # keeps it in line)
+        # would go ahead of the other connection's waiting ones;
+        # ZKMI_LINK_PRIO, off by default)
         self.link = torch.cuda.Stream(dev, priority=-1) if _LINK_PRIO \
             else None
         self.rscanner = B.FrameScanner(n, dev, window=self.rwindow,

@@ -40,10 +40,12 @@ I64, I32, U8 = torch.int64, torch.int32, torch.uint8
 # multi-XCD part — tree_serve 90 -> 231 us, the GET step 0.651 -> 0.718 ms
 # (profiles/r5_regression_ab.md); the extra launch is far cheaper.
 _SERVE_TICKETS = os.environ.get('ZKMI_SERVE_TICKETS', '0') == '1'
-# GET pipelines fork the serve's tree finish to a side stream (off the reply
-# path; the single-workgroup kernel waited 15 us for a CU behind the other
-# connection's kernels); ZKMI_SIDE_FINISH=0 keeps it in line
-_SIDE_FINISH = os.environ.get('ZKMI_SIDE_FINISH', '1') != '0'
+# ZKMI_SIDE_FINISH=1: GET pipelines fork the serve's tree finish to a side
+# stream (off the reply path: the single-workgroup kernel waits ~15 us for
+# a CU behind the other connection's kernels).  Off by default: no gain
+# measured (0.655 vs 0.655 ms) and the captured step segfaulted in
+# capture_end (test_gpu_get_pipeline_graph_replay)
+_SIDE_FINISH = os.environ.get('ZKMI_SIDE_FINISH', '0') == '1'
 # ZKMI_LINK_PRIO=1: the GET scans' fs_link on a high-priority stream (fork
 # and join by events inside the scan).  Off: a captured step with it
 # segfaulted in hipStreamEndCapture (test_gpu_get_pipeline_graph_replay)
@@ -571,8 +573,7 @@ class GetPipeline(object):
         self.idx = torch.empty(n, dtype=I64, device=dev)
         self.xid = torch.empty(n, dtype=I32, device=dev)
         # the serve's tree finish on a side stream (a GET batch changes
-        # nothing the replies read: off the reply path; ZKMI_SIDE_FINISH=0
-        # keeps it in line)
+        # nothing the replies read; ZKMI_SIDE_FINISH, off by default)
         self.side = torch.cuda.Stream(dev) if _SIDE_FINISH else None
         self.server.scanner.link_stream = self.link
         self.poff = torch.empty(n, dtype=I64, device=dev)

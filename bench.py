@@ -55,6 +55,7 @@ the previous one's callback), the way the single-threaded reference runs
 """
 
 import argparse
+import gc
 import json
 import os
 import statistics
@@ -559,6 +560,13 @@ def _time_steps(pipe, a, world, dev):
                   file=sys.stderr)
             graph = False
             run = lambda: pipe.step(acc=ok_total)    # noqa: E731
+    # everything built so far (the tree's host tables, torch, the pipelines)
+    # out of the collector's reach: a full collection walks every tracked
+    # object of the process, tens of ms with the GPU idle behind it (the
+    # watch workload's one-step-in-a-hundred stall,
+    # tools/microbench/watch_stall_probe.py)
+    gc.collect()
+    gc.freeze()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

@@ -53,6 +53,10 @@ def main():
                     help='the Python collector during the steps')
     ap.add_argument('--all', action='store_true',
                     help='every step (no stop at the first slow one)')
+    ap.add_argument('--prelaunch', type=int, default=0,
+                    help='tiny kernel launches before the steps (is the '
+                         'slow step the process\'s N-th launch?)')
+    ap.add_argument('--seed', type=int, default=0)
     a = ap.parse_args()
     import gc
     gcs = []            # (step, generation, ms) of every collection
@@ -67,7 +71,21 @@ def main():
     dev = torch.device('cuda', 0)
     n = 1 << 20
     tree = S.GpuTree(1000000, 100, device=dev, seed=0, watch_cap=2 * n)
-    pipe = S.WatchPipeline(tree, n, seed=0)
+    pipe = S.WatchPipeline(tree, n, seed=a.seed)
+    if a.prelaunch:
+        x = torch.zeros(1, device=dev)
+        t0 = time.perf_counter()
+        worst = 0.0
+        for k in range(a.prelaunch):
+            t1 = time.perf_counter()
+            x.add_(1)
+            if k % 256 == 255:
+                torch.cuda.synchronize()
+            worst = max(worst, time.perf_counter() - t1)
+        torch.cuda.synchronize()
+        print('prelaunch %d launches %.1f ms, slowest launch call %.2f ms'
+              % (a.prelaunch, 1e3 * (time.perf_counter() - t0),
+                 1e3 * worst), flush=True)
     acc = torch.zeros(64, dtype=torch.int64, device=dev)
     pipe.nscan.chain_stats()
     times = []

@@ -703,56 +703,66 @@ ZK_DEV void staged_emit_holes(int64_t r0, int64_t r1, const int64_t* off,
 // Uniform GET_DATA replies (every record of the block a successful
 // GET_DATA of the same size S, S a multiple of 16, the block's span
 // 16-byte aligned — a read batch of equal-sized znodes): the block's span
-// is written straight from the slots, 16 bytes a lane per step, every
+// is written straight from the slots, 16 bytes a lane per piece, every
 // store of a wave 1 KiB contiguous, no LDS image.  A record is
 //   [0,4) S - 4 | [4,8) xid | [8,16) zxid | [16,20) err |
 //   [20, S - 68) the slot's [len | data] | [S - 68, S) the slot's Stat,
 // and S % 16 == 0 makes the data length a multiple of 4, so every dword of
 // a 16-byte piece is one aligned dword of the slot (or of the header).
-// Lanes take consecutive pieces: a wave reads a run of slots front to back.
-ZK_DEV uint32_t slot_dw(const uint8_t* slot, int64_t p, int64_t dl) {
-  // record byte p (>= 20, 4-aligned) of a reply of data length dl
-  const int64_t so = p < 24 + dl ? p - 20 + ZK_SLOT_LEN : p - 24 - dl;
-  return *(const uint32_t*)(slot + so);
-}
-
+// The records' header words and slot offsets are staged in LDS once per
+// block (coalesced loads); a piece's record is c / P by a float reciprocal
+// (P = S / 16 pieces a record) — the first version divided 64-bit integers
+// and loaded the header fields per piece, and ran the GET step at 0.96 ms
+// against the LDS image's 0.65.
 ZK_DEV void emit_uniform(const ZkRespBatch& r, const ZkNodeStore& s,
                          int64_t r0, int64_t nrec, int64_t S, int64_t B0,
-                         uint8_t* __restrict__ out) {
-  const int64_t dl = S - 4 - 16 - 4 - STAT_BYTES;
-  const int64_t pieces = nrec * (S >> 4);
+                         uint8_t* __restrict__ out, uint32_t* lw) {
+  uint32_t* hx = lw;                                // [nrec][5] header words
+  int64_t* hs = (int64_t*)(lw + 5 * ENC_T);         // [nrec] slot offsets
+  if ((int64_t)threadIdx.x < nrec) {
+    const int64_t i = r0 + threadIdx.x;
+    const uint64_t z = (uint64_t)r.zxid[i];
+    uint32_t* h = hx + 5 * threadIdx.x;
+    h[0] = bswap32((uint32_t)(S - 4));
+    h[1] = bswap32((uint32_t)r.xid[i]);
+    h[2] = bswap32((uint32_t)(z >> 32));
+    h[3] = bswap32((uint32_t)z);
+    h[4] = bswap32((uint32_t)r.err[i]);
+    hs[threadIdx.x] = r.slot ? r.slot[i] : s.slot_off[r.node[i]];
+  }
+  __syncthreads();
+  const uint32_t P = (uint32_t)(S >> 4);
+  const uint32_t split = (uint32_t)(S - STAT_BYTES);   // 24 + data length
+  const uint32_t pieces = (uint32_t)nrec * P;
+  const float invP = 1.0f / (float)P;
   constexpr int U = 4;                   // pieces in flight per lane
-  for (int64_t c0 = threadIdx.x; c0 < pieces; c0 += (int64_t)U * ENC_T) {
-    uint32_t v[U][4];
-    int64_t xo[U];
+  for (uint32_t c0 = threadIdx.x; c0 < pieces; c0 += U * ENC_T) {
+    uint4 v[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int64_t c = c0 + (int64_t)u * ENC_T;
-      xo[u] = -1;
+      const uint32_t c = c0 + (uint32_t)u * ENC_T;
       if (c >= pieces) continue;
-      const int64_t x = c << 4;
-      const int64_t k = x / S, b = x - k * S;
-      const int64_t i = r0 + k;
-      const uint8_t* slot = s.slab + (r.slot ? r.slot[i] : s.slot_off[r.node[i]]);
-      xo[u] = x;
+      uint32_t k = (uint32_t)((float)c * invP);
+      if (k * P > c) --k;
+      else if ((k + 1) * P <= c) ++k;
+      const uint32_t p0 = (c - k * P) << 4;          // the piece's record byte
+      const uint8_t* slot = s.slab + hs[k];
+      uint32_t w[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const int64_t p = b + 4 * q;
-        uint32_t w;
-        if (p == 0) w = bswap32((uint32_t)(S - 4));
-        else if (p == 4) w = bswap32((uint32_t)r.xid[i]);
-        else if (p == 8) w = bswap32((uint32_t)((uint64_t)r.zxid[i] >> 32));
-        else if (p == 12) w = bswap32((uint32_t)r.zxid[i]);
-        else if (p == 16) w = bswap32((uint32_t)r.err[i]);
-        else w = slot_dw(slot, p, dl);
-        v[u][q] = w;
+        const uint32_t p = p0 + 4 * q;
+        w[q] = p < 20 ? hx[5 * k + (p >> 2)]
+                      : *(const uint32_t*)(slot + (p < split
+                                                       ? p + (ZK_SLOT_LEN - 20)
+                                                       : p - split));
       }
+      v[u] = make_uint4(w[0], w[1], w[2], w[3]);
     }
 #pragma unroll
-    for (int u = 0; u < U; ++u)
-      if (xo[u] >= 0)
-        *(uint4*)(out + B0 + xo[u]) = make_uint4(v[u][0], v[u][1], v[u][2],
-                                                 v[u][3]);
+    for (int u = 0; u < U; ++u) {
+      const uint32_t c = c0 + (uint32_t)u * ENC_T;
+      if (c < pieces) *(uint4*)(out + B0 + ((int64_t)c << 4)) = v[u];
+    }
   }
 }
 
@@ -785,15 +795,15 @@ __global__ __launch_bounds__(ENC_T) void resp_write(
   if (bsum != nullptr && base + bsum[blockIdx.x] > cap) return;
   block_offsets(r0, r1, sizes, base, rec_off, E);
   // uniform GET_DATA replies: straight from the slots (emit_uniform)
-  {
+  if (uniform) {                                  // (a kernel argument)
     const int64_t i = r0 + threadIdx.x;
     const int64_t S = E.sz[0];
     const bool u = i >= r1 ||
                    (r.opcode[i] == OP_GET_DATA && r.err[i] == ERR_OK &&
                     E.sz[threadIdx.x] == S);
     if (__syncthreads_and(u) && (S & 15) == 0 && (E.off[0] & 15) == 0 &&
-        uniform) {
-      emit_uniform(r, s, r0, r1 - r0, S, E.off[0], out);
+        S >= 96 && stage >= 5 * 4 * ENC_T + 8 * ENC_T) {
+      emit_uniform(r, s, r0, r1 - r0, S, E.off[0], out, lw);
       return;
     }
   }
@@ -1007,9 +1017,10 @@ static int enc_swz() {
   return v;
 }
 // ZKMI_ENC_UNIFORM=1: uniform GET_DATA reply blocks written straight from
-// the slots (emit_uniform).  Off by default: measured 0.651 -> 0.958 ms a GET
-// step (a 64-bit division and per-dword slot loads per 16-byte piece;
-// profiles/r5_regression_ab.md), the LDS image is faster.
+// the slots (emit_uniform).  Off by default: its first version ran the GET
+// step at 0.958 ms against 0.651 (a 64-bit division and per-record loads per
+// 16-byte piece; profiles/r5_regression_ab.md); the reworked one is A/B'd
+// against the LDS image.
 static int enc_uniform() {
   static int v = -1;
   if (v < 0) { const char* e = getenv("ZKMI_ENC_UNIFORM"); v = e ? atoi(e) : 0; }

@@ -2,6 +2,8 @@
 oracle (zkmi/jute.py), which itself is pinned to the reference's golden
 vectors in test_proto.py.  All tests here need an MI355X."""
 
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -535,6 +537,54 @@ def test_encode_responses_serve_mix_matches_oracle(gpu, dist, mix):
         starts.append(o)
         o += 4 + int.from_bytes(want[o:o + 4], 'big')
     assert rec_off[:n].cpu().tolist() == starts
+
+
+def test_encode_responses_get_blocks_matches_oracle(gpu):
+    """K13 on blocks of equal-size successful GET_DATA replies (the GET
+    workload's reply stream: the blocks the uniform writer takes when
+    ZKMI_ENC_UNIFORM=1), a ragged last block and one block with an error
+    reply in it, against jute.encode_response."""
+    from zkmi.ops import batch as B
+    tree = _small_tree(gpu)
+    r = synth.rng(23)
+    n = 256 * 5 + 33
+    nodes = [r.randrange(tree.leaf0, tree.n_static) for _ in range(n)]
+    zx = [r.randint(0, 2**40) for _ in range(n)]
+    errs = [0] * n
+    errs[256 * 2 + 17] = -101
+    T = lambda a, dt: torch.tensor(a, dtype=dt, device=gpu)  # noqa: E731
+    resp = B.ResponseBatch(
+        T([consts.OP_CODES['GET_DATA']] * n, torch.int32),
+        T(list(range(n)), torch.int32), T(errs, torch.int32),
+        T(nodes, torch.int64), T(zx, torch.int64),
+        T([0] * n, torch.int64), T([0] * n, torch.int32),
+        _dev_bytes(b'\0' * 16, gpu), T([1] * n, torch.int32),
+        T([n], torch.int64))
+    out, rec_off, total, err = B.encode_responses(resp, tree.store, 1 << 22)
+    torch.cuda.synchronize()
+    assert err.item() == 0
+    got = bytes(out[:total.item()].cpu().numpy().tobytes())
+    want = []
+    for i in range(n):
+        data, st = tree.node_slot_host(nodes[i])
+        want.append(jute.frame(jute.encode_response(
+            {'xid': i, 'zxid': zx[i], 'err': errs[i], 'opcode': 'GET_DATA',
+             'stat': st, 'data': data})))
+    assert got == b''.join(want)
+
+
+def test_encode_responses_uniform_writer(gpu):
+    """The same blocks through the uniform writer (ZKMI_ENC_UNIFORM=1 is
+    read once per process: a child process)."""
+    import subprocess
+    import sys
+    env = dict(os.environ, ZKMI_ENC_UNIFORM='1')
+    res = subprocess.run(
+        [sys.executable, '-m', 'pytest', '-q', '-x', '-p', 'no:cacheprovider',
+         os.path.abspath(__file__) +
+         '::test_encode_responses_get_blocks_matches_oracle'],
+        env=env, capture_output=True, text=True, timeout=300)
+    assert res.returncode == 0, res.stdout[-3000:] + res.stderr[-2000:]
 
 
 def test_gpu_get_pipeline_end_to_end(gpu):

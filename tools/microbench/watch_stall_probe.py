@@ -88,6 +88,29 @@ def main():
                  1e3 * worst), flush=True)
     acc = torch.zeros(64, dtype=torch.int64, device=dev)
     pipe.nscan.chain_stats()
+    # a CUDA event after each of the step's launches-worth of host calls
+    # (the pipeline's own methods wrapped), to time its phases on the GPU
+    marks = []
+
+    def mark(name):
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        marks.append((name, e))
+
+    def wrap(obj, meth, name):
+        f = getattr(obj, meth)
+
+        def g(*args, **kw):
+            r = f(*args, **kw)
+            mark(name)
+            return r
+        setattr(obj, meth, g)
+    from zkmi.ops import batch as B
+    for sc, nm in ((pipe.server.scanner, 'req_scan'), (pipe.rscan, 'rep_scan'),
+                   (pipe.nscan, 'note_scan')):
+        wrap(sc, 'scan', nm)
+    wrap(pipe.server, 'serve', 'serve')
+    wrap(pipe.fan, 'gather_slots', 'gather')
     times = []
     if a.gc == 'off':
         gc.disable()
@@ -96,16 +119,24 @@ def main():
         gc.freeze()
     for s in range(a.steps):
         torch.cuda.synchronize()
+        marks.clear()
+        mark('start')
         t0 = time.perf_counter()
         pipe.step(acc=acc)
+        mark('end')
         torch.cuda.synchronize()
         ms = 1e3 * (time.perf_counter() - t0)
+        phases = [(marks[j][0], round(marks[j - 1][1].elapsed_time(
+            marks[j][1]), 3)) for j in range(1, len(marks))]
         st = pipe.nscan.chain_stats()
         med = float(np.median(times)) if times else ms
         times.append(ms)
         slow_gc = [g for g in gcs if g[0] == s and g[2] > 5]
         if slow_gc:
             print('step %d %.2f ms: collections %r' % (s, ms, slow_gc),
+                  flush=True)
+        if ms >= 5 * med and s >= 5 and a.all:
+            print('SLOW step %d %.2f ms: GPU phases %r' % (s, ms, phases),
                   flush=True)
         if s < 5 or ms < 5 * med or a.all:
             if s % 10 == 0:
@@ -116,6 +147,7 @@ def main():
         print('SLOW step %d %.2f ms (median %.2f) stats %r stream %d B '
               'zxid %d' % (s, ms, med, st, nb, int(tree.counters[1].item())),
               flush=True)
+        print('GPU phases (ms since the mark before):', phases, flush=True)
         print('fs_link clock', fs_clock(pipe.rx.numel()), flush=True)
         buf = pipe.rx[:nb].clone()
         out = os.path.join(ROOT, 'gpurun_out')

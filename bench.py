@@ -560,13 +560,6 @@ def _time_steps(pipe, a, world, dev):
                   file=sys.stderr)
             graph = False
             run = lambda: pipe.step(acc=ok_total)    # noqa: E731
-    # everything built so far (the tree's host tables, torch, the pipelines)
-    # out of the collector's reach: a full collection walks every tracked
-    # object of the process, tens of ms with the GPU idle behind it (the
-    # watch workload's one-step-in-a-hundred stall,
-    # tools/microbench/watch_stall_probe.py)
-    gc.collect()
-    gc.freeze()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -905,7 +898,6 @@ def run_rank(a):
     # pipelines holding them) before the group goes — destroying an RCCL
     # group under a live graph waits forever in its shutdown
     pipe = None
-    import gc
     gc.collect()
     torch.cuda.synchronize()
     if dist.is_initialized():

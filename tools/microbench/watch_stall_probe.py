@@ -112,6 +112,7 @@ def main():
     wrap(pipe.server, 'serve', 'serve')
     wrap(pipe.fan, 'gather_slots', 'gather')
     times = []
+    prev_seg = (0, 0, 0)
     if a.gc == 'off':
         gc.disable()
     elif a.gc == 'freeze':
@@ -129,6 +130,15 @@ def main():
         phases = [(marks[j][0], round(marks[j - 1][1].elapsed_time(
             marks[j][1]), 3)) for j in range(1, len(marks))]
         st = pipe.nscan.chain_stats()
+        mst = torch.cuda.memory_stats(dev)
+        seg = (mst.get('segment.all.allocated', 0),
+               mst.get('reserved_bytes.all.current', 0),
+               mst.get('num_alloc_retries', 0))
+        if s > 0 and seg != prev_seg:
+            print('step %d %.2f ms: allocator segments %d (+%d), reserved '
+                  '%.1f MB, retries %d' % (s, ms, seg[0], seg[0] - prev_seg[0],
+                                           seg[1] / 1e6, seg[2]), flush=True)
+        prev_seg = seg
         med = float(np.median(times)) if times else ms
         times.append(ms)
         slow_gc = [g for g in gcs if g[0] == s and g[2] > 5]

@@ -1016,14 +1016,14 @@ static int enc_swz() {
   if (v < 0) { const char* e = getenv("ZKMI_ENC_SWZ"); v = e ? atoi(e) : 1; }
   return v;
 }
-// ZKMI_ENC_UNIFORM=1: uniform GET_DATA reply blocks written straight from
-// the slots (emit_uniform).  Off by default: its first version ran the GET
-// step at 0.958 ms against 0.651 (a 64-bit division and per-record loads per
-// 16-byte piece; profiles/r5_regression_ab.md); the reworked one is A/B'd
-// against the LDS image.
+// Uniform GET_DATA reply blocks written straight from the slots
+// (emit_uniform; ZKMI_ENC_UNIFORM=0 sends them through the LDS image).
+// Its first version ran the GET step at 0.958 ms against the image's 0.651
+// (a 64-bit division and per-record loads per 16-byte piece); reworked,
+// 0.575 against 0.615 (profiles/r5_uniform_writer_ab.md).
 static int enc_uniform() {
   static int v = -1;
-  if (v < 0) { const char* e = getenv("ZKMI_ENC_UNIFORM"); v = e ? atoi(e) : 0; }
+  if (v < 0) { const char* e = getenv("ZKMI_ENC_UNIFORM"); v = e ? atoi(e) : 1; }
   return v;
 }
 static bool enc_fused() {

@@ -541,9 +541,9 @@ def test_encode_responses_serve_mix_matches_oracle(gpu, dist, mix):
 
 def test_encode_responses_get_blocks_matches_oracle(gpu):
     """K13 on blocks of equal-size successful GET_DATA replies (the GET
-    workload's reply stream: the blocks the uniform writer takes when
-    ZKMI_ENC_UNIFORM=1), a ragged last block and one block with an error
-    reply in it, against jute.encode_response."""
+    workload's reply stream: the blocks the uniform writer takes), a ragged
+    last block and one block with an error reply in it (the LDS image's),
+    against jute.encode_response."""
     from zkmi.ops import batch as B
     tree = _small_tree(gpu)
     r = synth.rng(23)
@@ -573,12 +573,12 @@ def test_encode_responses_get_blocks_matches_oracle(gpu):
     assert got == b''.join(want)
 
 
-def test_encode_responses_uniform_writer(gpu):
-    """The same blocks through the uniform writer (ZKMI_ENC_UNIFORM=1 is
-    read once per process: a child process)."""
+def test_encode_responses_get_blocks_lds_image(gpu):
+    """The same blocks through the LDS image writer instead of the uniform
+    one (ZKMI_ENC_UNIFORM=0 is read once per process: a child process)."""
     import subprocess
     import sys
-    env = dict(os.environ, ZKMI_ENC_UNIFORM='1')
+    env = dict(os.environ, ZKMI_ENC_UNIFORM='0')
     res = subprocess.run(
         [sys.executable, '-m', 'pytest', '-q', '-x', '-p', 'no:cacheprovider',
          os.path.abspath(__file__) +

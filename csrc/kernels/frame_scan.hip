@@ -97,6 +97,9 @@ constexpr int FL_DBG_ROWS = 6;             // fs_link's debug rows past the tile
 // block could chase the region), 0.27 ms without; the dense and no-spec
 // streams the same either way.
 constexpr int FL_LOCAL_MIN = 1 << 30;
+// The last block's one exact chase before its rounds (many broken links):
+// tiles it may walk before it leaves the rest to the rounds
+constexpr uint32_t FL_CHASE_WALKS = 64;
 // Count blocks: frame counts scanned per FK_T tiles (one wave's worth)
 constexpr int FK_T = 64;
 // The workspace's words after the X flags (uint64, lbw + 2 * tiles): [0..3]
@@ -2062,7 +2065,8 @@ ZK_DEV int64_t fl_chase_run(const uint8_t* __restrict__ buf, int64_t n,
                             int64_t* rec_meta, const uint64_t* lbw,
                             const int64_t* cx,
                             uint8_t* mywin, FlChase& ch, int64_t k0,
-                            bool exact, bool& term, uint32_t& walked) {
+                            bool exact, bool& term, uint32_t& walked,
+                            uint32_t walk_budget = 0) {
   const int lane = threadIdx.x & 63;
   term = false;
   // everything that steers the chase is wave-uniform; saying so keeps its
@@ -2251,6 +2255,8 @@ ZK_DEV int64_t fl_chase_run(const uint8_t* __restrict__ buf, int64_t n,
       const int64_t oldx = rfl64(ld_agent(&rec_exit[t]));
       const bool nh = t + 1 < ntiles &&
                       rfl64(ld_agent(&rec_entry[t + 1])) == oldx;
+      // (a budgeted chase leaves the walking to the caller's rounds)
+      if (walk_budget != 0 && walked >= walk_budget) return t - 1;
       const int32_t m0 = __builtin_amdgcn_readfirstlane(rcount[t]);
       const FcWalk fw = fc_walk(buf, n, maxp, ts, E, list + t * FT_LMAX, m0,
                                 sx[t], mywin, pre + t * FT_LMAX, lane);
@@ -2575,7 +2581,7 @@ __global__ __launch_bounds__(FL_T) void fs_link(
     int64_t* __restrict__ bsum, uint64_t* mins,
     int64_t* __restrict__ lastk, unsigned long long* g,
     const uint64_t* lbw, const int64_t* __restrict__ cx,
-    int64_t* __restrict__ ldbg, int32_t local_min) {
+    int64_t* __restrict__ ldbg, int32_t local_min, int32_t fflags) {
   __shared__ __attribute__((aligned(16)))
       uint8_t win[(FL_T / 64) * (FC_WIN + 16)];      // one per wave
   __shared__ int64_t red[2 * (FL_T / 64) + 2];
@@ -2698,6 +2704,31 @@ __global__ __launch_bounds__(FL_T) void fs_link(
   // blocks' round continued here); after each, the links still broken are
   // listed again.  What the rounds leave goes to the tail.
   bool changed = rew != 0 || big;       // records changed beyond the chases' dirty
+  if (nb > (int64_t)FL_SMALL && fb0 != INF && (fflags & 1)) {
+    // many broken links: first ONE exact chase from the leftmost, wave 0,
+    // through fs_tile's candidate exits 64 tiles a batch.  A stream whose
+    // every frame carries a phantom chain of the frame's own period (SET_DATA
+    // replies of version 84: both chains survive every tile, about half the
+    // tiles speculate the phantom) is settled by it in one pass of lookups
+    // (ms) where the rounds walked every broken tile (84 ms a scan).  Its
+    // walks are budgeted: on a stream whose entries are not candidates
+    // (dense payload words) it stops early and the rounds walk in parallel.
+    if (wv == 0) {
+      bool term = false;
+      uint32_t walked = 0;
+      const int64_t kend = fl_chase_run(buf, n, ntiles, maxp, sx, list, rcount,
+                                        pre, rec_entry, rec_exit, rec_meta, lbw,
+                                        cx, win, ch, fb0, true, term, walked,
+                                        FL_CHASE_WALKS);
+      (void)kend;
+      if (lane == 0) {
+        if (walked) fc_stat(stats, 2, walked);
+        fc_stat(stats, 3, 1);
+      }
+    }
+    __syncthreads();
+    changed = true;
+  }
   for (int round = 0; round < FL_BROUNDS; ++round) {
     if (changed) {
       int64_t fbv, ftv;
@@ -2919,6 +2950,17 @@ static int32_t fl_local_min() {
   return v;
 }
 
+// fs_link's switches: bit 0 the exact chase before the rounds
+// (ZKMI_FL_CHASE_FIRST=0 turns it off, for A/B)
+static int32_t fl_flags() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("ZKMI_FL_CHASE_FIRST");
+    v = (e ? atoi(e) : 1) ? 1 : 0;
+  }
+  return v;
+}
+
 // fs_link's grid: the check's workgroups (the last to finish goes on).
 static unsigned fl_blocks() { return 16; }
 
@@ -3113,7 +3155,7 @@ int zk_frame_scan6(const uint8_t* buf, const int64_t* n_dev, int64_t n_cap,
                                  pre, rent, rexit, rmeta, base, cap, result,
                                  lbw + 2 * tiles, blist, bsum, mins, lastk,
                                  grid, lbw, cx, dbg ? dbg + 8 * tiles : nullptr,
-                                 fl_local_min());
+                                 fl_local_min(), fl_flags());
   ZK_LAUNCH_CHECK();
   if (lst != st && (hipEventRecord(ev[1], lst) != hipSuccess ||
                     hipStreamWaitEvent(st, ev[1], 0) != hipSuccess))

@@ -183,6 +183,47 @@ def test_phantom_chain_region_is_chased_not_walked(gpu):
     assert ms < max(3 * base_ms, 0.6), (ms, base_ms)
 
 
+def _set_replies(n, version=84, xid0=0x5000, zxid0=0xA12C929):
+    """SET_DATA replies of nodes whose version is 84: 88-byte frames {len
+    84, xid, zxid, err 0, Stat} — the Stat's version word reads as the
+    frame length, so a phantom chain of the frame's own period runs through
+    the whole stream beside the true one (the watch workload's write
+    replies at its 84th write of every node: an 84 ms fs_link repair at
+    step 83 of every run, rounds 4-5)."""
+    i = np.arange(n, dtype=np.int64)
+    rec = np.zeros((n, 88), np.uint8)
+
+    def be(col, v, w):
+        for b in range(w):
+            rec[:, col + b] = (v >> (8 * (w - 1 - b))) & 0xff
+    be(0, np.full(n, 84), 4)
+    be(4, xid0 + i, 4)
+    be(8, zxid0 + i, 8)
+    st = 20                                            # the Stat
+    be(st + 0, 1000 + i, 8)                            # czxid
+    be(st + 8, zxid0 + i, 8)                           # mzxid
+    be(st + 16, np.full(n, 0x19A3F2C1D00), 8)          # ctime
+    be(st + 24, np.full(n, 0x19A3F2C2E11), 8)          # mtime
+    be(st + 32, np.full(n, version), 4)                # version
+    be(st + 52, np.full(n, 100), 4)                    # dataLength
+    be(st + 60, 1000 + i, 8)                           # pzxid
+    return rec.reshape(-1), np.arange(n, dtype=np.int64) * 88
+
+
+def test_phantom_chain_through_the_whole_stream(gpu):
+    """Every frame carries a phantom chain of its own period: both chains
+    survive every tile, about half the tiles speculate the phantom one.
+    One exact chase through fs_tile's candidate exits settles the stream
+    (looked up, not walked tile by tile)."""
+    n = 1 << 20
+    clean, _ = _set_replies(n, version=3)
+    _, _, base_ms, _ = _scan_timed(clean, n, 256)
+    buf, starts = _set_replies(n)
+    r, off, ms, st = _scan_timed(buf, n, 256)
+    _check(r, off, buf, starts)
+    assert ms < max(10 * base_ms, 5.0), (ms, base_ms, st)
+
+
 def test_get_replies_exact_below_the_largest_frame(gpu, monkeypatch):
     """0-1024 B GET replies scanned at a 512 B window (half the largest
     frame, long-frame mode: frontier passes past the window, survivor exits

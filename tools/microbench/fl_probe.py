@@ -24,6 +24,8 @@ def stream(case):
     rng = np.random.default_rng(9)
     if case == 'phantom':
         return T._create_replies(1 << 20, zxid0=0x2E0000 - 500000), 256, 1
+    if case == 'period':
+        return T._set_replies(1 << 20), 256, 1
     if case == 'clean':
         return T._create_replies(1 << 20, zxid0=0x500000), 256, 1
     if case.startswith('dense'):

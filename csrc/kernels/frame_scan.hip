@@ -99,7 +99,7 @@ constexpr int FL_DBG_ROWS = 6;             // fs_link's debug rows past the tile
 constexpr int FL_LOCAL_MIN = 1 << 30;
 // The last block's one exact chase before its rounds (many broken links):
 // tiles it may walk before it leaves the rest to the rounds
-constexpr uint32_t FL_CHASE_WALKS = 64;
+constexpr uint32_t FL_CHASE_WALKS = 16;
 // Count blocks: frame counts scanned per FK_T tiles (one wave's worth)
 constexpr int FK_T = 64;
 // The workspace's words after the X flags (uint64, lbw + 2 * tiles): [0..3]
@@ -2704,7 +2704,7 @@ __global__ __launch_bounds__(FL_T) void fs_link(
   // blocks' round continued here); after each, the links still broken are
   // listed again.  What the rounds leave goes to the tail.
   bool changed = rew != 0 || big;       // records changed beyond the chases' dirty
-  if (nb > (int64_t)FL_SMALL && fb0 != INF && (fflags & 1)) {
+  if (!big && nb > (int64_t)FL_SMALL && fb0 != INF && (fflags & 1)) {
     // many broken links: first ONE exact chase from the leftmost, wave 0,
     // through fs_tile's candidate exits 64 tiles a batch.  A stream whose
     // every frame carries a phantom chain of the frame's own period (SET_DATA
@@ -2712,7 +2712,8 @@ __global__ __launch_bounds__(FL_T) void fs_link(
     // tiles speculate the phantom) is settled by it in one pass of lookups
     // (ms) where the rounds walked every broken tile (84 ms a scan).  Its
     // walks are budgeted: on a stream whose entries are not candidates
-    // (dense payload words) it stops early and the rounds walk in parallel.
+    // (dense payload words) it stops early and the rounds walk in parallel
+    // (profiles/r5_fs_link_ab.md).  Not after the grid's big repair.
     if (wv == 0) {
       bool term = false;
       uint32_t walked = 0;

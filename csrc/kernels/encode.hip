@@ -1120,11 +1120,33 @@ int zk_encode_connect_requests(const int32_t* proto, const int64_t* zxid,
 // presized != 0: `sizes` (frame size per reply, 0 past *n_dev) and the
 // per-256-reply block sums in scan_ws[0, nblk(ncap)) were already written
 // by the producer (zk_tree_serve), so the sizes pass is skipped.
+// stage (bytes, 0: STAGE_BYTES): the LDS each workgroup gets — the image of
+// its replies, or the uniform writer's header table (7 KiB).  A caller whose
+// replies are uniform GET_DATA blocks (the GET pipeline) asks for little, so
+// more workgroups (and another stream's kernels) fit a CU.
+int zk_encode_responses3(const ZkRespBatch* r, const ZkNodeStore* s,
+                         const int64_t* n_dev, int64_t ncap, int64_t* sizes,
+                         int64_t* rec_off, int64_t* total, int64_t* scan_ws,
+                         uint8_t* out, int64_t out_cap, int32_t* err,
+                         int32_t presized, int32_t terminate, int64_t stage,
+                         hipStream_t st);
+
 int zk_encode_responses2(const ZkRespBatch* r, const ZkNodeStore* s,
                          const int64_t* n_dev, int64_t ncap, int64_t* sizes,
                          int64_t* rec_off, int64_t* total, int64_t* scan_ws,
                          uint8_t* out, int64_t out_cap, int32_t* err,
                          int32_t presized, int32_t terminate, hipStream_t st) {
+  return zk_encode_responses3(r, s, n_dev, ncap, sizes, rec_off, total,
+                              scan_ws, out, out_cap, err, presized, terminate,
+                              0, st);
+}
+
+int zk_encode_responses3(const ZkRespBatch* r, const ZkNodeStore* s,
+                         const int64_t* n_dev, int64_t ncap, int64_t* sizes,
+                         int64_t* rec_off, int64_t* total, int64_t* scan_ws,
+                         uint8_t* out, int64_t out_cap, int32_t* err,
+                         int32_t presized, int32_t terminate, int64_t stage_req,
+                         hipStream_t st) {
   if (ncap <= 0) {
     int rc = hipMemsetAsync(total, 0, 8, st);
     if (!rc) rc = hipMemsetAsync(err, 0, 4, st);
@@ -1146,7 +1168,11 @@ int zk_encode_responses2(const ZkRespBatch* r, const ZkNodeStore* s,
   }
   // reply image per workgroup (a 56 KiB image gained 0.5 % on 0-1024 B
   // payloads and cost GET 2 %)
-  const int64_t stage = zk::STAGE_BYTES;
+  // (at least the uniform writer's header table and a few records' image)
+  const int64_t stage = stage_req <= 0 ? zk::STAGE_BYTES
+                        : stage_req < 8192 ? 8192
+                        : stage_req > zk::STAGE_BYTES ? zk::STAGE_BYTES
+                                                      : (stage_req + 15) & ~15;
   if (zk::enc_swz() == 1)
     zk::resp_write<1><<<nb, zk::ENC_T, (size_t)stage, st>>>(
         *r, *s, n_dev, ncap, sizes, bbase, fused ? bsum : nullptr, rec_off,

@@ -301,8 +301,14 @@ ZK_DEV int64_t tree_insert(const ZkTree& t, int64_t v, const uint8_t* p,
   const int64_t pv = val_pack(v, t.store.slot_off[v]);
   int64_t s = key & t.mask;
   for (int64_t probe = 0; probe <= t.mask; ++probe) {
-    const int64_t k = atomicCAS((unsigned long long*)ht_key(t, s), 0ull,
-                                (unsigned long long)key);
+    // a plain load first: an occupied slot of another key (the usual probe
+    // past a tombstone or a collision) costs a load, not an L2 atomic on
+    // another line each (keys only ever go 0 -> key within a launch, so a
+    // stale 0 just means the CAS below answers)
+    int64_t k = *ht_key(t, s);
+    if (k == 0)
+      k = atomicCAS((unsigned long long*)ht_key(t, s), 0ull,
+                    (unsigned long long)key);
     if (k == 0) {                         // claimed an empty slot
       ent_fill(t, s, p, n, dl);
       __hip_atomic_store(ht_val(t, s), pv, __ATOMIC_RELAXED,
@@ -475,6 +481,19 @@ __global__ __launch_bounds__(TR_T) void tree_fill_k(ZkTree t, int64_t n0,
   t.nchild[v] = nkids[v];
   t.pzxid[v] = v + 1;
   t.dirty[v] = 0;
+}
+
+// Every hash entry back to empty (key 0, val -3, the rest 0): one pass of
+// 16-byte stores over the table (was a zero fill and a strided fill of the
+// val words, 2 passes and a 460 us strided one at 16M entries).
+__global__ __launch_bounds__(TR_T) void ht_reset_k(int64_t* __restrict__ ht,
+                                                   int64_t nchunk) {
+  uint4* q = (uint4*)ht;
+  const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+  const uint4 kv = make_uint4(0u, 0u, 0xFFFFFFFDu, 0xFFFFFFFFu);
+  for (int64_t c = (int64_t)blockIdx.x * TR_T + threadIdx.x; c < nchunk;
+       c += (int64_t)gridDim.x * TR_T)
+    q[c] = (c & (HT_W / 2 - 1)) == 0 ? kv : z;
 }
 
 __global__ __launch_bounds__(TR_T) void tree_build_k(ZkTree t, int64_t n0,
@@ -1386,6 +1405,15 @@ int zk_tree_fill(const ZkTree* t, int64_t n0, int64_t n, const int32_t* nkids,
   const int64_t m = n - n0;
   zk::tree_fill_k<<<(unsigned)((m + zk::TR_T - 1) / zk::TR_T), zk::TR_T, 0,
                     st>>>(*t, n0, n, nkids, now_ms);
+  ZK_LAUNCH_CHECK();
+  return 0;
+}
+
+int zk_tree_ht_reset(const ZkTree* t, hipStream_t st) {
+  const int64_t nchunk = (t->mask + 1) * (zk::HT_W / 2);
+  int64_t nb = (nchunk + zk::TR_T - 1) / zk::TR_T;
+  if (nb > 8192) nb = 8192;                    // grid-stride past 2M lanes
+  zk::ht_reset_k<<<(unsigned)nb, zk::TR_T, 0, st>>>(t->ht, nchunk);
   ZK_LAUNCH_CHECK();
   return 0;
 }

@@ -162,6 +162,10 @@ int zk_encode_responses2(const ZkRespBatch*, const ZkNodeStore*,
                          const int64_t*, int64_t, int64_t*, int64_t*,
                          int64_t*, int64_t*, uint8_t*, int64_t, int32_t*,
                          int32_t, int32_t, hipStream_t);
+int zk_encode_responses3(const ZkRespBatch*, const ZkNodeStore*,
+                         const int64_t*, int64_t, int64_t*, int64_t*, int64_t*,
+                         int64_t*, uint8_t*, int64_t, int32_t*, int32_t,
+                         int32_t, int64_t, hipStream_t);
 int64_t zk_frame_scan_workspace(int64_t n);
 int zk_frame_scan5(const uint8_t*, const int64_t*, int64_t, int64_t,
                    uint8_t*, int64_t, int64_t*, int32_t*, int64_t, int64_t*,
@@ -196,6 +200,8 @@ int zk_decode_connect_responses(const uint8_t*, const int64_t*,
 int zk_tree_fill(const ZkTree*, int64_t, int64_t, const int32_t*, int64_t,
                  hipStream_t);
 int zk_tree_build(const ZkTree*, int64_t, int64_t, hipStream_t);
+// every hash entry back to empty (before a rebuild)
+int zk_tree_ht_reset(const ZkTree*, hipStream_t);
 int zk_tree_serve(const ZkTree*, const uint8_t*, const ZkReqOut*,
                   const int64_t*, int64_t, int32_t*, int32_t*, int32_t*,
                   int64_t*, int64_t*, int64_t*, int32_t*, int64_t*, int64_t*,

@@ -338,13 +338,14 @@ void encode_responses(const std::vector<Tensor>& resp,
                       const std::vector<Tensor>& store, const Tensor& n_dev,
                       int64_t ncap, const Tensor& sizes, const Tensor& rec_off,
                       const Tensor& total, const Tensor& ws, const Tensor& out,
-                      const Tensor& err, bool presized, bool terminate) {
+                      const Tensor& err, bool presized, bool terminate,
+                      int64_t stage) {
   need(store, 4, "node store");
   const Tensor* r = &resp[0];
   ZkRespBatch b = resp_batch(resp, slot, ncap, r);
   ZkNodeStore s = node_store(store, 0, r);
   const int64_t m = std::max<int64_t>(ncap, 1);
-  hip_ok(zk_encode_responses2(
+  hip_ok(zk_encode_responses3(
              &b, &s, P<int64_t>(n_dev, I64, 1, "count", r), ncap,
              P<int64_t>(sizes, I64, m, "sizes", r),
              P<int64_t>(rec_off, I64, m, "rec_off", r),
@@ -352,7 +353,7 @@ void encode_responses(const std::vector<Tensor>& resp,
              P<int64_t>(ws, I64, zk_scan_workspace(m), "ws", r),
              P<uint8_t>(out, U8, 1, "out", r), out.numel(),
              P<int32_t>(err, I32, 1, "err", r), presized ? 1 : 0,
-             terminate ? 1 : 0, cur_stream()),
+             terminate ? 1 : 0, stage, cur_stream()),
          "encode_responses");
 }
 
@@ -525,6 +526,11 @@ void tree_fill(const std::vector<Tensor>& t, int64_t n0, int64_t n,
   hip_ok(zk_tree_fill(&s, n0, n, P<int32_t>(nkids, I32, n, "nkids", &t[0]),
                       now_ms, cur_stream()),
          "tree_fill");
+}
+
+void tree_ht_reset(const std::vector<Tensor>& t) {
+  ZkTree s = tree(t);
+  hip_ok(zk_tree_ht_reset(&s, cur_stream()), "tree_ht_reset");
 }
 
 void tree_build(const std::vector<Tensor>& t, int64_t n0, int64_t n) {
@@ -934,7 +940,8 @@ TORCH_LIBRARY(zkmi, m) {
   m.def("encode_responses(Tensor[] resp, Tensor? slot, Tensor[] store, "
         "Tensor count, int ncap, Tensor(a!) sizes, Tensor(b!) rec_off, "
         "Tensor(c!) total, Tensor(d!) ws, Tensor(e!) out, Tensor(f!) err, "
-        "bool presized, bool terminate) -> ()", &encode_responses);
+        "bool presized, bool terminate, int stage=0) -> ()",
+        &encode_responses);
   m.def("frame_scan_workspace(int n) -> int", &frame_scan_workspace);
   m.def("frame_scan(Tensor buf, Tensor? n, int n_cap, int max_packet, "
         "Tensor(a!) ws, Tensor(b!) frame_off, Tensor(c!) frame_len, "
@@ -968,6 +975,7 @@ TORCH_LIBRARY(zkmi, m) {
   m.def("tree_fill(Tensor(a!)[] tree, int n0, int n, Tensor nkids, "
         "int now_ms) -> ()", &tree_fill);
   m.def("tree_build(Tensor(a!)[] tree, int n0, int n) -> ()", &tree_build);
+  m.def("tree_ht_reset(Tensor(a!)[] tree) -> ()", &tree_ht_reset);
   m.def("tree_serve(Tensor(a!)[] tree, Tensor rx, Tensor[] requests, "
         "Tensor count, int ncap, Tensor(b!)[] out, int session, int now_ms) "
         "-> ()", &tree_serve);

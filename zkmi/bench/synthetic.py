@@ -50,6 +50,10 @@ _SIDE_FINISH = os.environ.get('ZKMI_SIDE_FINISH', '0') == '1'
 # and join by events inside the scan).  Off: a captured step with it
 # segfaulted in hipStreamEndCapture (test_gpu_get_pipeline_graph_replay)
 _LINK_PRIO = os.environ.get('ZKMI_LINK_PRIO', '0') == '1'
+# ZKMI_GET_STAGE: the LDS bytes per workgroup the GET pipelines' reply
+# encode asks for (uniform GET replies need only the writer's 7 KiB header
+# table; 0: the encoder's 28 KiB default)
+_GET_STAGE = int(os.environ.get('ZKMI_GET_STAGE', '8192'))
 
 
 def _len(total):
@@ -265,8 +269,7 @@ class GpuTree(object):
         by deleted paths that are never re-created, e.g. SEQUENTIAL names).
         One host read of the node high-water mark."""
         n = int(self.counters[_lib.TC_NODES].item())
-        self.ht.zero_()
-        self.ht.view(-1, _lib.HT_WORDS)[:, 1] = -3
+        _lib.lib().tree_ht_reset(self._tensors)
         _lib.lib().tree_build(self._tensors, 0, min(n, self.cap))
 
     def find_host(self, path):
@@ -322,6 +325,7 @@ class GpuServer(object):
         self.cap_frames = cap_frames
         self.scanner = B.FrameScanner(cap_frames, dev, window=window)
         self.ows = None                   # ordered-serve workspace (lazy)
+        self.enc_stage = 0                # K13 LDS per workgroup (0: default)
         # the serve launch's sign-off counters (its last workgroup does the
         # tree's finish: no separate launch); this server's own, zero
         self.tickets = torch.zeros(_lib.lib().serve_tickets(cap_frames),
@@ -473,7 +477,8 @@ class GpuServer(object):
                 self._side = side
         out, rec_off, total, err = B.encode_responses(
             r, self.tree.store, self.out.numel(), out=self.out,
-            presized=self.presized, terminate=terminate)
+            presized=self.presized, terminate=terminate,
+            stage=self.enc_stage)
         self.last_rec_off = rec_off         # reply frame starts (R2 splits)
         self.result = (out, total, err, ft)
         if self.tree.watch is not None:
@@ -555,6 +560,7 @@ class GetPipeline(object):
         # K1 windows: the largest request / reply frame of this workload
         self.server = GpuServer(tree, n, n * (4 + 16 + 4 + dmax + 68) + 64,
                                 window=B.frame_window(17 + maxpath))
+        self.server.enc_stage = _GET_STAGE
         self.rwindow = B.frame_window(4 + 16 + 4 + dmax + 68)
         lo, hi = tree.data_dist or (tree.data_bytes, tree.data_bytes)
         # fs_link of both scans on a high-priority stream (its workgroups

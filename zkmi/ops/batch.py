@@ -668,12 +668,14 @@ def response_workspace(cap, device):
 
 
 def encode_responses(resp, store, out_cap, out=None, stream=None,
-                     presized=None, terminate=False):
+                     presized=None, terminate=False, stage=0):
     """K13: server-mode reply encode -> (bytes, rec_off, total, err).
     ``store``: the node store's tensors [slab, slot_off, data_len,
     slot_cap] (:attr:`zkmi.bench.synthetic.GpuTree.store`).
     ``presized``: the (sizes, workspace) pair of :func:`response_workspace`
-    already filled by the producer; the sizes pass is then skipped."""
+    already filled by the producer; the sizes pass is then skipped.
+    ``stage``: LDS bytes per workgroup (0: the encoder's default; uniform
+    GET_DATA replies need only 8 KiB, more workgroups then fit a CU)."""
     L = _lib.lib()
     cap = resp.opcode.numel()
     dev = resp.opcode.device
@@ -689,7 +691,8 @@ def encode_responses(resp, store, out_cap, out=None, stream=None,
     with _on(stream):
         L.encode_responses(resp.tensors(), resp.slot, list(store), resp.count,
                            cap, sizes, rec_off, total, ws, out, err,
-                           presized is not None, bool(terminate))
+                           presized is not None, bool(terminate),
+                           int(stage))
     return out, rec_off, total, err
 
 

@@ -460,6 +460,9 @@ def main():
                          'tree (no collective in the step) instead of the '
                          'path-hash-sharded tree with R2 routing over '
                          'RCCL/xGMI (the default)')
+    ap.add_argument('--hash-factor', type=int, default=0,
+                    help='hash entries per node slot, rounded up to a power '
+                    'of two (0: 4 for the storm, 2 otherwise)')
     ap.add_argument('--force-route', action='store_true',
                     help='get, N = 1: run the multi-rank sharded step over a '
                          'one-rank RCCL group (router, slots, '
@@ -700,7 +703,9 @@ def run_rank(a):
         # every rank (seed 0), every member applies every member's writes
         tree = S.GpuTree(a.nodes, a.data_bytes, device=dev,
                          seed=0 if a.workload == 'storm' else rank,
-                         spare=spare + 0.05, scratch=scratch)
+                         spare=spare + 0.05, scratch=scratch,
+                         hash_factor=a.hash_factor or (
+                             4 if a.workload == 'storm' else 2))
         if a.workload == 'chain':
             pipe = S.ChainPipeline(tree, a.batch, a.data_bytes, seed=rank)
             per_step = pipe.n

@@ -257,13 +257,17 @@ int zk_route_requests(int64_t, int32_t, const int64_t*, const int32_t*,
                       const uint8_t*, const int64_t*, const int32_t*,
                       int32_t*, int64_t*, int32_t*, int64_t*, int32_t*,
                       int64_t*, int64_t*, hipStream_t);
+int zk_route_requests2(int64_t, int32_t, int32_t, const int64_t*,
+                       const int32_t*, const uint8_t*, const int64_t*,
+                       const int32_t*, int32_t*, int64_t*, int32_t*, int64_t*,
+                       int32_t*, int64_t*, int64_t*, hipStream_t);
 int zk_seg_pack(const uint8_t*, int64_t, const int64_t*, const int64_t*,
                 int64_t, const int64_t*, const int64_t*, int32_t, int32_t,
-                int64_t, uint8_t*, unsigned long long*, uint8_t*,
+                int64_t, uint8_t*, unsigned long long*, uint8_t*, int32_t,
                 hipStream_t);
 int zk_seg_unpack(const uint8_t*, int32_t, int32_t, int64_t, uint8_t*,
                   int64_t*, int64_t*, unsigned long long*, const uint8_t*,
-                  hipStream_t);
+                  int32_t, hipStream_t);
 int zk_session_connect(const uint8_t*, const int64_t*, const int32_t*,
                        const int64_t*, int64_t, const ZkSessionTable*,
                        int64_t, uint64_t, int32_t, int32_t, const int64_t*,

@@ -803,11 +803,13 @@ void route_requests(int64_t n, int64_t world, const Tensor& poff,
                     const Tensor& idx, const Tensor& xid, const Tensor& owner,
                     const Tensor& idx_s, const Tensor& xid_s,
                     const Tensor& poff_s, const Tensor& plen_s,
-                    const Tensor& counts, const Tensor& ws) {
+                    const Tensor& counts, const Tensor& ws, int64_t self) {
   TORCH_CHECK(world >= 1 && world <= 64, "zkmi: route world 1..64");
+  TORCH_CHECK(self >= 0 && self < world, "zkmi: route self rank");
   const Tensor* r = &poff;
-  hip_ok(zk_route_requests(
-             n, (int32_t)world, P<int64_t>(poff, I64, n, "path_off"),
+  hip_ok(zk_route_requests2(
+             n, (int32_t)world, (int32_t)self,
+             P<int64_t>(poff, I64, n, "path_off"),
              P<int32_t>(plen, I32, n, "path_len", r),
              P<uint8_t>(arena, U8, 1, "arena", r),
              P<int64_t>(idx, I64, n, "idx", r),
@@ -828,7 +830,10 @@ void seg_pack(const Tensor& src, const Tensor& rec_off,
               const c10::optional<Tensor>& nrec, int64_t nrec_cap,
               const Tensor& total, const Tensor& counts, int64_t world,
               int64_t self, int64_t slot_cap, const Tensor& out,
-              const Tensor& stats, const c10::optional<Tensor>& self_out) {
+              const Tensor& stats, const c10::optional<Tensor>& self_out,
+              bool inplace) {
+  TORCH_CHECK(!inplace || self_out.has_value(),
+              "zkmi: seg_pack inplace needs the self header (self_out)");
   TORCH_CHECK(world >= 1 && world <= 64, "zkmi: seg_pack world 1..64");
   TORCH_CHECK(self >= 0 && self < world, "zkmi: seg_pack self rank");
   TORCH_CHECK(slot_cap >= 32 && slot_cap % 16 == 0,
@@ -847,15 +852,18 @@ void seg_pack(const Tensor& src, const Tensor& rec_off,
                                          : world * slot_cap, "out", r),
                      reinterpret_cast<unsigned long long*>(
                          P<int64_t>(stats, I64, 3, "stats", r)),
-                     Popt<uint8_t>(self_out, U8, slot_cap, "self_out", r),
-                     cur_stream()),
+                     Popt<uint8_t>(self_out, U8, inplace ? 16 : slot_cap,
+                                   "self_out", r),
+                     inplace ? 1 : 0, cur_stream()),
          "seg_pack");
 }
 
 void seg_unpack(const Tensor& inp, int64_t world, int64_t self,
                 int64_t slot_cap, const Tensor& out, const Tensor& total,
                 const Tensor& counts, const c10::optional<Tensor>& stats,
-                const c10::optional<Tensor>& self_in) {
+                const c10::optional<Tensor>& self_in, bool inplace) {
+  TORCH_CHECK(!inplace || self_in.has_value(),
+              "zkmi: seg_unpack inplace needs the self header (self_in)");
   TORCH_CHECK(world >= 1 && world <= 64, "zkmi: seg_unpack world 1..64");
   TORCH_CHECK(self >= 0 && self < world, "zkmi: seg_unpack self rank");
   TORCH_CHECK(slot_cap >= 32 && slot_cap % 16 == 0,
@@ -870,8 +878,9 @@ void seg_unpack(const Tensor& inp, int64_t world, int64_t self,
                        P<int64_t>(counts, I64, world, "counts", r),
                        reinterpret_cast<unsigned long long*>(
                            Popt<int64_t>(stats, I64, 1, "stats", r)),
-                       Popt<uint8_t>(self_in, U8, slot_cap, "self_in", r),
-                       cur_stream()),
+                       Popt<uint8_t>(self_in, U8, inplace ? 16 : slot_cap,
+                                     "self_in", r),
+                       inplace ? 1 : 0, cur_stream()),
          "seg_unpack");
 }
 
@@ -1017,15 +1026,18 @@ TORCH_LIBRARY(zkmi, m) {
   m.def("route_requests(int n, int world, Tensor path_off, Tensor path_len, "
         "Tensor arena, Tensor idx, Tensor xid, Tensor(a!) owner, "
         "Tensor(b!) idx_s, Tensor(c!) xid_s, Tensor(d!) path_off_s, "
-        "Tensor(e!) path_len_s, Tensor(f!) counts, Tensor(g!) ws) -> ()",
+        "Tensor(e!) path_len_s, Tensor(f!) counts, Tensor(g!) ws, "
+        "int self=0) -> ()",
         &route_requests);
   m.def("seg_pack(Tensor src, Tensor rec_off, Tensor? nrec, int nrec_cap, "
         "Tensor total, Tensor counts, int world, int self, int slot_cap, "
-        "Tensor(a!) out, Tensor(b!) stats, Tensor(c!)? self_out=None) -> ()",
+        "Tensor(a!) out, Tensor(b!) stats, Tensor(c!)? self_out=None, "
+        "bool inplace=False) -> ()",
         &seg_pack);
   m.def("seg_unpack(Tensor inp, int world, int self, int slot_cap, "
         "Tensor(a!) out, Tensor(b!) total, Tensor(c!) counts, "
-        "Tensor(d!)? stats=None, Tensor? self_in=None) -> ()", &seg_unpack);
+        "Tensor(d!)? stats=None, Tensor? self_in=None, "
+        "bool inplace=False) -> ()", &seg_unpack);
   m.def("session_connect(Tensor buf, Tensor frame_off, Tensor frame_len, "
         "Tensor count, int ncap, Tensor(a!)[] table, int server_id, "
         "int secret, int min_to, int max_to, Tensor zxid_now, Tensor(b!) out, "

@@ -42,6 +42,15 @@ def test_router_matches_host_hash(gpu):
         assert idx_s.cpu().numpy().tolist() == \
             c.idx.cpu().numpy()[order].tolist()
         assert cnt.cpu().tolist() == np.bincount(want, minlength=W).tolist()
+        # grouped from owner `me` on (rotation): the local group first
+        me = W - 2
+        L.route_requests(5000, W, c.poff, c.plen, tree.path_arena, c.idx,
+                         c.xid, owner, idx_s, xid_s, poff_s, plen_s, cnt,
+                         rws, me)
+        order = np.argsort((want - me) % W, kind='stable')
+        assert idx_s.cpu().numpy().tolist() == \
+            c.idx.cpu().numpy()[order].tolist()
+        assert cnt.cpu().tolist() == np.bincount(want, minlength=W).tolist()
 
 
 def test_seg_pack_unpack_roundtrip(gpu):
@@ -127,6 +136,67 @@ def test_seg_pack_unpack_roundtrip(gpu):
     L.seg_unpack(coll, W, me, slot, back2, tot, rc, None, own)
     assert tot.item() == len(want)
     assert back2[:len(want)].cpu().numpy().tobytes() == want
+
+
+def test_seg_pack_unpack_inplace(gpu):
+    """SEG_INPLACE: segments in rotation order from this rank (its own
+    first, at offset 0), only the own segment's header written apart, and
+    the peers' payloads unpacked after it in the same buffer — the local
+    bytes never move."""
+    from zkmi.ops import _lib
+    L = _lib.lib()
+    rng = np.random.default_rng(5)
+    W, me = 4, 2
+    counts = [5, 9, 11, 3]                 # records owned by rank w
+    rot = [(me + k) % W for k in range(W)]  # stream order: 2, 3, 0, 1
+    sizes = rng.integers(1, 70, sum(counts))
+    stream = rng.integers(0, 256, int(sizes.sum()), dtype=np.uint8)
+    rec_off = np.zeros(len(sizes), np.int64)
+    rec_off[1:] = np.cumsum(sizes)[:-1]
+    segs, f = {}, 0
+    for w in rot:
+        a = rec_off[f] if f < len(sizes) else len(stream)
+        b = rec_off[f + counts[w]] if f + counts[w] < len(sizes) \
+            else len(stream)
+        segs[w] = bytes(stream[a:b])
+        f += counts[w]
+    slot = 16 + 16 * 60
+    cap = W * (slot - 16) + 64
+    dev = gpu
+    buf = torch.zeros(cap, dtype=torch.uint8, device=dev)
+    buf[:len(stream)] = torch.from_numpy(stream).to(dev)
+    ro = torch.from_numpy(rec_off).to(dev)
+    total = torch.tensor([len(stream)], dtype=torch.int64, device=dev)
+    cnt = torch.tensor(counts, dtype=torch.int64, device=dev)
+    coll = torch.full(((W - 1) * slot + 16,), 0xEE, dtype=torch.uint8,
+                      device=dev)
+    hdr = torch.zeros(16, dtype=torch.uint8, device=dev)
+    st = torch.zeros(3, dtype=torch.int64, device=dev)
+    L.seg_pack(buf, ro, None, len(sizes), total, cnt, W, me, slot, coll, st,
+               hdr, True)
+    cb = coll.cpu().numpy().tobytes()
+    assert tuple(np.frombuffer(hdr.cpu().numpy().tobytes(), np.int64)) == \
+        (len(segs[me]), counts[me])
+    for w in range(W):
+        if w == me:
+            continue
+        p0 = w * slot if w < me else (w - 1) * slot + 16
+        hb, hr = np.frombuffer(cb[p0:p0 + 16], np.int64)
+        assert (hb, hr) == (len(segs[w]), counts[w])
+        assert cb[p0 + 16:p0 + 16 + hb] == segs[w]
+    peers = [w for w in range(W) if w != me]
+    assert st.cpu().tolist() == [0, sum(len(segs[w]) for w in peers),
+                                 sum(counts[w] for w in peers)]
+    # the peers' part of the buffer is free once packed: scribble over it,
+    # then unpack in place behind the untouched local segment
+    buf[len(segs[me]):] = 0x5A
+    tot = torch.zeros(1, dtype=torch.int64, device=dev)
+    rc = torch.zeros(W, dtype=torch.int64, device=dev)
+    L.seg_unpack(coll, W, me, slot, buf, tot, rc, None, hdr, True)
+    want = b''.join(segs[w] for w in rot)
+    assert tot.item() == len(want)
+    assert buf[:len(want)].cpu().numpy().tobytes() == want
+    assert rc.cpu().tolist() == counts
 
 
 def test_sharded_get_one_rank(gpu):

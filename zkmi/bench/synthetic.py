@@ -108,7 +108,8 @@ class GpuTree(object):
 
     def __init__(self, n_nodes=1_000_000, data_bytes=100, fanout=1000,
                  device=None, spare=0.25, seed=0, shard=None, ctime_ms=None,
-                 data_dist=None, name_pad=None, scratch=0, watch_cap=0):
+                 data_dist=None, name_pad=None, scratch=0, watch_cap=0,
+                 hash_factor=2):
         dev = torch.device(device) if device is not None else \
             torch.device('cuda', torch.cuda.current_device())
         self.device = dev
@@ -201,7 +202,11 @@ class GpuTree(object):
         nkids[1:leaf0] = np.bincount(np.arange(n_nodes) // fanout,
                                      minlength=ndirs)[:ndirs]
         nk = torch.from_numpy(nkids).to(dev)
-        hcap = _next_pow2(2 * cap)
+        # hash entries per node slot (a power of two above it): 2 keeps a
+        # read-mostly tree's table under half full; a write-heavy one
+        # (SEQUENTIAL names never reused) fills with tombstones between
+        # rebuilds, and a wider table rebuilds less often
+        hcap = _next_pow2(hash_factor * cap)
         # interleaved 16-byte {key, val} entries (csrc/kernels/tree.hip)
         self.ht = torch.zeros(_lib.HT_WORDS * hcap, dtype=I64, device=dev)
         self.ht.view(-1, _lib.HT_WORDS)[:, 1] = -3

@@ -15,15 +15,19 @@ on rank ``r`` is, per pipelined connection:
           ``nccl``): fixed splits, no size exchange; the local segment
           stays in a slot of its own and crosses no collective (a 16-byte
           stub stands in for it)
-  server  ``seg_unpack`` concatenates the received payloads (source rank
-          order) with their device length; K1 + K12 over that stream,
+  server  ``seg_unpack`` appends the received payloads to this rank's own
+          segment, which never moved (the router groups requests by owner
+          from this rank on, so it heads the stream; route.hip
+          SEG_INPLACE); K1 + K12 over that stream,
           lookup in my shard, K13 encode; ``seg_pack`` cuts the reply
           stream back into one slot per source rank (the per-source record
           counts came with the request headers)
   R2      ``all_to_all_single`` of the reply slots
-  client  ``seg_unpack``, K1 + K2-K4 over the replies (they come back owner
+  client  ``seg_unpack`` after the local replies, in the server's own
+          reply buffer; K1 + K2-K4 over the replies (they come back owner
           by owner, in the order the router sent them) and the on-device
-          check of every reply
+          check of every reply.  With one rank (``force_route``) the step
+          copies nothing
 
 A step makes **no device-to-host read**: every length the kernels need
 travels in the slot headers, so with RCCL the whole step (collectives
@@ -241,10 +245,12 @@ class ShardedGetPipeline(object):
         W = self.world
         wire = sum((W - 1) * (c.req_slot + c.rep_slot) for c in self.subs) \
             * self.steps if W > 1 else 0
-        # bytes the step's kernels copy per connection: the segments into
-        # the slots (seg_pack) and out of them (seg_unpack), requests and
-        # replies; the all-to-all moves the peers' slots only
-        copied = sum(2 * (c.n * c.req_max + c.n * c.rep_max)
+        # bytes the step's kernels copy per connection at most: the peers'
+        # segments into the slots (seg_pack) and out of them (seg_unpack),
+        # requests and replies (a uniform hash sends (W-1)/W of them); this
+        # rank's own segments stay in place and the all-to-all moves the
+        # peers' slots only
+        copied = sum(2 * (c.n * c.req_max + c.n * c.rep_max) * (W - 1) // W
                      for c in self.subs)
         slots = [b for c in self.subs for b in (c.req_slot, c.rep_slot)]
         return {'bytes_sent': rq[1] + rp[1], 'bytes_recv': rv[0],
@@ -298,14 +304,21 @@ class _Conn(object):
         maxdata = int(t.data_len.max().item())
         self.req_max = 17 + maxpath
         self.rep_max = 4 + 16 + 4 + maxdata + 68
-        self.tx = torch.empty(n * self.req_max + 64, dtype=U8, device=dev)
         k = slot_records(n, W)
         self.slot_recs = k
         cap = W * k                      # requests this rank can receive
         self.req_slot = _r16(SEG_HDR + k * self.req_max)
         self.rep_slot = _r16(SEG_HDR + k * self.rep_max)
-        self.server = GpuServer(t, cap, cap * self.rep_max + 64,
-                                window=B.frame_window(self.req_max))
+        # routed: the request stream buffer is also the server's input (the
+        # peers' segments land after this rank's own, which stays in place),
+        # and the server's reply buffer the client's (same for the replies)
+        self.tx = torch.empty(max(n * self.req_max,
+                                  W * (self.req_slot - SEG_HDR)) + 64,
+                              dtype=U8, device=dev)
+        self.server = GpuServer(t, cap, max(cap * self.rep_max,
+                                            W * (self.rep_slot - SEG_HDR))
+                                + 64, window=B.frame_window(self.req_max))
+        self.server.enc_stage = 8192     # uniform GET replies (K13 writer)
         # the replies to this connection's own n requests come back
         lo, hi = t.data_dist or (t.data_bytes, t.data_bytes)
         self.rscanner = B.FrameScanner(n, dev,
@@ -321,9 +334,9 @@ class _Conn(object):
             cp = (W - 1) * self.rep_slot + SEG_HDR
             self.sq, self.rq = u8(cq), u8(cq)
             self.sp, self.rp = u8(cp), u8(cp)
-            self.sq_self, self.sp_self = u8(self.req_slot), u8(self.rep_slot)
-            self.rxq = u8(W * (self.req_slot - SEG_HDR) + 64)
-            self.crx = u8(W * (self.rep_slot - SEG_HDR) + 64)
+            # this rank's own segments stay in the streams (SEG_INPLACE):
+            # only their 16-byte {bytes, records} headers are written apart
+            self.sq_self, self.sp_self = u8(SEG_HDR), u8(SEG_HDR)
             self.nrx = torch.zeros(1, dtype=I64, device=dev)
             self.ncrx = torch.zeros(1, dtype=I64, device=dev)
             self.src_counts = torch.zeros(W, dtype=I64, device=dev)
@@ -358,10 +371,12 @@ class _Conn(object):
                         self.gstate)
         self.xid_base = (self.xid_base + n) & 0x7fffffff
         if p.route:
+            # grouped by owner from this rank on (rotation): the local
+            # segment heads the stream and is never copied
             L.route_requests(n, W, self.poff, self.plen, t.path_arena,
                              self.idx, self.xid, self.owner, self.idx_s,
                              self.xid_s, self.poff_s, self.plen_s,
-                             self.counts, self.rws)
+                             self.counts, self.rws, p.rank)
         rb = B.RequestBatch(n, self.opcode, self.xid_s, self.zero32,
                             self.poff_s, self.plen_s, self.zero64,
                             self.zero32, self.zero32, t.path_arena, t.slab,
@@ -369,15 +384,18 @@ class _Conn(object):
         tx, rec_off, total, _ = B.encode_requests(rb, self.xt, out=self.tx)
         if p.route:
             L.seg_pack(tx, rec_off, None, n, total, self.counts, W, p.rank,
-                       self.req_slot, self.sq, p.req_stats, self.sq_self)
+                       self.req_slot, self.sq, p.req_stats, self.sq_self,
+                       True)
         yield
         if p.route:
             p.a2a(self.rq, self.sq, self.req_slot)
         yield
         if p.route:
-            L.seg_unpack(self.rq, W, p.rank, self.req_slot, self.rxq,
-                         self.nrx, self.src_counts, None, self.sq_self)
-            rxq, nrx = self.rxq, self.nrx
+            # the peers' segments after this rank's own, in the request
+            # stream's buffer (its peer part went out with seg_pack)
+            L.seg_unpack(self.rq, W, p.rank, self.req_slot, tx,
+                         self.nrx, self.src_counts, None, self.sq_self, True)
+            rxq, nrx = tx, self.nrx
         else:
             rxq, nrx = tx, total
         srv = self.server.serve_steps(rxq, nrx)
@@ -392,16 +410,16 @@ class _Conn(object):
             L.seg_pack(rout, self.server.last_rec_off, ft.count,
                        self.server.cap_frames, rtotal, self.src_counts, W,
                        p.rank, self.rep_slot, self.sp, p.rep_stats,
-                       self.sp_self)
+                       self.sp_self, True)
         yield
         if p.route:
             p.a2a(self.rp, self.sp, self.rep_slot)
         yield
         if p.route:
-            L.seg_unpack(self.rp, W, p.rank, self.rep_slot, self.crx,
+            L.seg_unpack(self.rp, W, p.rank, self.rep_slot, rout,
                          self.ncrx, self.back_counts, p.recv_stats,
-                         self.sp_self)
-            crx, ncrx = self.crx, self.ncrx
+                         self.sp_self, True)
+            crx, ncrx = rout, self.ncrx
         else:
             crx, ncrx = rout, rtotal
         cft = self.rscanner.scan(crx, ncrx)

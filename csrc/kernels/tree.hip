@@ -496,6 +496,56 @@ __global__ __launch_bounds__(TR_T) void ht_reset_k(int64_t* __restrict__ ht,
     q[c] = (c & (HT_W / 2 - 1)) == 0 ? kv : z;
 }
 
+// Free-ring compaction between batches: the ring's pending entries rebuilt
+// as every free node in ascending order.  Frees go to the ring in the
+// order the workgroups of a batch happened to take their tickets, and
+// creates take the ring in ticket order too, so over a few hundred batches
+// of create / delete the nodes one workgroup creates scatter over the whole
+// node table (each per-node field a random line instead of a shared one):
+// the mix step drifted 1.42 -> 1.65 ms and the nest step 6.26 -> 7.78 ms
+// over 600 / 200 steps (profiles/r5_free_ring_locality.md).  Sorted, a
+// workgroup's creates take nodes from one dense run again.  Two passes and
+// a scan over the node high-water mark; at a batch boundary the pending
+// entries are exactly the free nodes (the finish published every free).
+__global__ __launch_bounds__(TR_T) void free_count_k(ZkTree t,
+                                                    int64_t* __restrict__ bsum) {
+  __shared__ int32_t c[TR_T / 64];
+  const int64_t nn = min(t.counters[TC_NODES], t.store.cap);
+  const int64_t v = (int64_t)blockIdx.x * TR_T + threadIdx.x;
+  const bool f = v < nn && t.node_parent[v] == NODE_FREE;
+  const uint64_t m = __ballot(f);
+  if ((threadIdx.x & 63) == 0) c[threadIdx.x >> 6] = __popcll(m);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int64_t s = 0;
+    for (int k = 0; k < TR_T / 64; ++k) s += c[k];
+    bsum[blockIdx.x] = s;
+  }
+}
+
+__global__ __launch_bounds__(TR_T) void free_scatter_k(
+    ZkTree t, const int64_t* __restrict__ bbase,
+    const int64_t* __restrict__ total) {
+  __shared__ int32_t c[TR_T / 64];
+  const int64_t head = t.counters[TC_FREE_HEAD];
+  const int64_t nn = min(t.counters[TC_NODES], t.store.cap);
+  const int64_t v = (int64_t)blockIdx.x * TR_T + threadIdx.x;
+  const bool f = v < nn && t.node_parent[v] == NODE_FREE;
+  const uint64_t m = __ballot(f);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) c[w] = __popcll(m);
+  __syncthreads();
+  int64_t r = bbase[blockIdx.x] +
+              __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                        __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+  for (int k = 0; k < w; ++k) r += c[k];
+  if (f) t.free_list[(head + r) % t.free_cap] = v;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    t.counters[TC_FREE_TAIL] = head + *total;
+    t.counters[TC_FREE_PUB] = head + *total;
+  }
+}
+
 __global__ __launch_bounds__(TR_T) void tree_build_k(ZkTree t, int64_t n0,
                                                     int64_t n) {
   const int64_t v = n0 + (int64_t)blockIdx.x * TR_T + threadIdx.x;
@@ -1405,6 +1455,28 @@ int zk_tree_fill(const ZkTree* t, int64_t n0, int64_t n, const int32_t* nkids,
   const int64_t m = n - n0;
   zk::tree_fill_k<<<(unsigned)((m + zk::TR_T - 1) / zk::TR_T), zk::TR_T, 0,
                     st>>>(*t, n0, n, nkids, now_ms);
+  ZK_LAUNCH_CHECK();
+  return 0;
+}
+
+// Workspace (int64) of zk_tree_free_compact for a node capacity.
+int64_t zk_tree_free_workspace(int64_t cap) {
+  const int64_t nb = (cap + zk::TR_T - 1) / zk::TR_T;
+  return 2 * nb + 8 + zk_scan_workspace(nb);
+}
+
+// The free ring's pending entries rebuilt in node order (free_count_k).
+int zk_tree_free_compact(const ZkTree* t, int64_t* ws, hipStream_t st) {
+  const int64_t nb = (t->store.cap + zk::TR_T - 1) / zk::TR_T;
+  if (nb <= 0) return 0;
+  int64_t* bsum = ws;
+  int64_t* bbase = ws + nb;
+  int64_t* total = ws + 2 * nb;
+  zk::free_count_k<<<(unsigned)nb, zk::TR_T, 0, st>>>(*t, bsum);
+  ZK_LAUNCH_CHECK();
+  int rc = zk_scan_excl_i64(bsum, bbase, nb, total, ws + 2 * nb + 8, st);
+  if (rc) return rc;
+  zk::free_scatter_k<<<(unsigned)nb, zk::TR_T, 0, st>>>(*t, bbase, total);
   ZK_LAUNCH_CHECK();
   return 0;
 }

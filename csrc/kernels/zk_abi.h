@@ -202,6 +202,9 @@ int zk_tree_fill(const ZkTree*, int64_t, int64_t, const int32_t*, int64_t,
 int zk_tree_build(const ZkTree*, int64_t, int64_t, hipStream_t);
 // every hash entry back to empty (before a rebuild)
 int zk_tree_ht_reset(const ZkTree*, hipStream_t);
+// the free ring's pending entries rebuilt in node order (between batches)
+int64_t zk_tree_free_workspace(int64_t cap);
+int zk_tree_free_compact(const ZkTree*, int64_t*, hipStream_t);
 int zk_tree_serve(const ZkTree*, const uint8_t*, const ZkReqOut*,
                   const int64_t*, int64_t, int32_t*, int32_t*, int32_t*,
                   int64_t*, int64_t*, int64_t*, int32_t*, int64_t*, int64_t*,

@@ -528,6 +528,19 @@ void tree_fill(const std::vector<Tensor>& t, int64_t n0, int64_t n,
          "tree_fill");
 }
 
+int64_t tree_free_workspace(int64_t cap) {
+  return zk_tree_free_workspace(cap);
+}
+
+void tree_free_compact(const std::vector<Tensor>& t, const Tensor& ws) {
+  ZkTree s = tree(t);
+  hip_ok(zk_tree_free_compact(
+             &s, P<int64_t>(ws, I64, zk_tree_free_workspace(s.store.cap),
+                            "ws", &t[0]),
+             cur_stream()),
+         "tree_free_compact");
+}
+
 void tree_ht_reset(const std::vector<Tensor>& t) {
   ZkTree s = tree(t);
   hip_ok(zk_tree_ht_reset(&s, cur_stream()), "tree_ht_reset");
@@ -985,6 +998,9 @@ TORCH_LIBRARY(zkmi, m) {
         "int now_ms) -> ()", &tree_fill);
   m.def("tree_build(Tensor(a!)[] tree, int n0, int n) -> ()", &tree_build);
   m.def("tree_ht_reset(Tensor(a!)[] tree) -> ()", &tree_ht_reset);
+  m.def("tree_free_workspace(int cap) -> int", &tree_free_workspace);
+  m.def("tree_free_compact(Tensor(a!)[] tree, Tensor(b!) ws) -> ()",
+        &tree_free_compact);
   m.def("tree_serve(Tensor(a!)[] tree, Tensor rx, Tensor[] requests, "
         "Tensor count, int ncap, Tensor(b!)[] out, int session, int now_ms) "
         "-> ()", &tree_serve);

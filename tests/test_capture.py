@@ -13,10 +13,10 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _tree(gpu, scratch=0):
+def _tree(gpu, scratch=0, **kw):
     from zkmi.bench.synthetic import GpuTree
     return GpuTree(20000, 37, fanout=100, device=gpu, spare=1.0,
-                   scratch=scratch)
+                   scratch=scratch, **kw)
 
 
 def _replays(pipe, gpu, eager=3, replays=6):
@@ -46,6 +46,44 @@ def test_mix_replays_three_rotations(gpu):
     assert int(tree.counters[_lib.TC_NODES].item()) <= hw + pipe.m
     # and eager steps go on after the replays
     assert int(pipe.step().item()) == pipe.n
+
+
+def _pending_free(tree):
+    from zkmi.ops import _lib
+    c = tree.counters.cpu().tolist()
+    h, pub = c[_lib.TC_FREE_HEAD], c[_lib.TC_FREE_PUB]
+    assert c[_lib.TC_FREE_TAIL] == pub
+    idx = torch.arange(h, pub, device=tree.device) % tree.free_list.numel()
+    return tree.free_list[idx].cpu().tolist()
+
+
+@pytest.mark.parametrize('hash_factor', [2, 8])
+def test_mix_free_ring_compacted(gpu, hash_factor):
+    """compact_free: after every served batch the free ring's pending
+    entries are exactly the free nodes, ascending (csrc/kernels/tree.hip
+    free_count_k / free_scatter_k), eager and replayed; every reply still
+    checks out and the tree stays steady.  Wider hash tables (bench.py
+    --hash-factor) serve the same."""
+    from zkmi.bench.synthetic import MixPipeline
+    from zkmi.ops import _lib
+    tree = _tree(gpu, compact_free=True, hash_factor=hash_factor)
+    assert tree.compact_free
+    pipe = MixPipeline(tree, 3 * 4096, ndirs=64)
+    acc = torch.zeros(64, dtype=torch.int64, device=gpu)
+    for k in range(4):
+        pipe.step(acc=acc)
+        torch.cuda.synchronize()
+        pend = _pending_free(tree)
+        assert pend == sorted(pend)
+        nn = min(int(tree.counters[_lib.TC_NODES].item()), tree.cap)
+        free = torch.nonzero(tree.node_parent[:nn] == -2).flatten()
+        assert pend == free.cpu().tolist(), k
+    assert int(acc.sum().item()) == 4 * pipe.n
+    hw = int(tree.counters[_lib.TC_NODES].item())
+    assert _replays(pipe, gpu, eager=2, replays=6) == 6 * pipe.n
+    pend = _pending_free(tree)
+    assert pend == sorted(pend) and len(pend) > 0
+    assert int(tree.counters[_lib.TC_NODES].item()) <= hw + pipe.m
 
 
 def test_chain_replays(gpu):

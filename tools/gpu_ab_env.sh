@@ -12,7 +12,7 @@ if [ -n "$AB_SETS" ]; then
 else
   SETS=""
   for v in ${AB_VALUES:-1 0}; do SETS="$SETS $AB_VAR=$v"; done
-  TAG=$AB_VAR
+  TAG=${AB_TAG:-$AB_VAR}
 fi
 OUT=gpurun_out/ab_${TAG}.log
 : > $OUT
@@ -26,7 +26,9 @@ for i in $(seq ${ROUNDS:-3}); do
 import json, sys
 line = [l for l in open(sys.argv[2]) if l.startswith('{')][-1]
 d = json.loads(line)
+s = d.get('sustained') or {}
 print(sys.argv[1], '%.4f ms' % d['ms_per_step'],
+      'sustained %.4f ms' % s.get('ms_per_step', float('nan')),
       '%.3f G ops/s' % (d['value'] / 1e9))
 PY
   done

@@ -23,6 +23,12 @@ ap.add_argument('--chunk', type=int, default=50)
 ap.add_argument('--batch', type=int, default=1 << 20)
 ap.add_argument('--nodes', type=int, default=1000000)
 ap.add_argument('--eager', action='store_true')
+ap.add_argument('--no-compact', action='store_true',
+                help='no free-ring compaction after each batch')
+ap.add_argument('--hash-factor', type=int, default=8)
+ap.add_argument('--sort-free', type=int, default=0,
+                help='sort the pending free ring after every N chunks '
+                '(0: never): tests the free-ring locality hypothesis')
 ap.add_argument('--zxid', type=lambda x: int(x, 0), default=None,
                 help='start the tree at this zxid')
 a = ap.parse_args()
@@ -35,7 +41,8 @@ else:
     spare = (a.batch + 8192) / a.nodes
     scratch = (a.batch // 2 + 64) * (80 + 112) if w in ('chain', 'nest') else 0
     tree = S.GpuTree(a.nodes, 100, device=dev, seed=0, spare=spare + 0.05,
-                     scratch=scratch)
+                     scratch=scratch, hash_factor=a.hash_factor,
+                     compact_free=not a.no_compact)
     pipe = {'mix': lambda: S.MixPipeline(tree, a.batch, 100, seed=0),
             'nest': lambda: S.NestPipeline(tree, a.batch, seed=0),
             'chain': lambda: S.ChainPipeline(tree, a.batch, 100, seed=0)}[w]()
@@ -51,8 +58,14 @@ if not a.eager:
 torch.cuda.synchronize()
 acc.zero_()
 done = 0
+chunks = 0
 print('workload', w, 'per step', getattr(pipe, 'n', a.batch), flush=True)
 while done < a.steps:
+    if a.sort_free and chunks % a.sort_free == 0:
+        torch.cuda.synchronize()
+        n_sorted = tree.sort_free()
+        print('sorted %d free entries' % n_sorted, flush=True)
+    chunks += 1
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(a.chunk):
@@ -61,6 +74,7 @@ while done < a.steps:
     dt = time.perf_counter() - t0
     done += a.chunk
     ok = int(acc.sum().item())
-    print('steps %5d  %.3f ms/step  ok %d  counters %s' % (
-        done, 1e3 * dt / a.chunk, ok, tree.counters.cpu().tolist()),
-        flush=True)
+    pend, near = tree.free_order()
+    print('steps %5d  %.3f ms/step  ok %d  free pending %d  one-apart %.3f '
+          ' counters %s' % (done, 1e3 * dt / a.chunk, ok, pend, near,
+                            tree.counters.cpu().tolist()), flush=True)

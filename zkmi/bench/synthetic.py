@@ -54,6 +54,9 @@ _LINK_PRIO = os.environ.get('ZKMI_LINK_PRIO', '0') == '1'
 # encode asks for (uniform GET replies need only the writer's 7 KiB header
 # table; 0: the encoder's 28 KiB default)
 _GET_STAGE = int(os.environ.get('ZKMI_GET_STAGE', '8192'))
+# ZKMI_FREE_COMPACT=0: no free-ring compaction after write batches (trees
+# built with compact_free=True; GpuTree.free_compact)
+_FREE_COMPACT = os.environ.get('ZKMI_FREE_COMPACT', '1') == '1'
 
 
 def _len(total):
@@ -109,7 +112,7 @@ class GpuTree(object):
     def __init__(self, n_nodes=1_000_000, data_bytes=100, fanout=1000,
                  device=None, spare=0.25, seed=0, shard=None, ctime_ms=None,
                  data_dist=None, name_pad=None, scratch=0, watch_cap=0,
-                 hash_factor=2):
+                 hash_factor=2, compact_free=False):
         dev = torch.device(device) if device is not None else \
             torch.device('cuda', torch.cuda.current_device())
         self.device = dev
@@ -222,6 +225,10 @@ class GpuTree(object):
         self.dirty = torch.zeros(cap, dtype=I32, device=dev)
         self.dirty_list = torch.empty(cap, dtype=I64, device=dev)
         self.hcap = hcap
+        # write workloads: the free ring's pending entries re-sorted after
+        # every served batch (free_compact; ZKMI_FREE_COMPACT=0 turns it off)
+        self.compact_free = compact_free and _FREE_COMPACT
+        self.free_ws = None
         # the tree / node-store descriptor lists torch.ops.zkmi takes
         # (csrc/torch/zkmi_ops.cpp tree() / node_store() field order)
         self.store = [self.slab_all, self.slot_off, self.data_len,
@@ -276,6 +283,45 @@ class GpuTree(object):
         n = int(self.counters[_lib.TC_NODES].item())
         _lib.lib().tree_ht_reset(self._tensors)
         _lib.lib().tree_build(self._tensors, 0, min(n, self.cap))
+
+    def free_compact(self):
+        """Rebuild the free ring's pending entries as the free nodes in node
+        order, on the device (csrc/kernels/tree.hip free_count_k): the next
+        batch's creates take nodes from dense runs.  Capturable."""
+        L = _lib.lib()
+        if self.free_ws is None:
+            self.free_ws = torch.empty(L.tree_free_workspace(self.cap),
+                                       dtype=I64, device=self.device)
+        L.tree_free_compact(self._tensors, self.free_ws)
+
+    def free_order(self):
+        """(pending free-ring entries, fraction of neighbours one apart):
+        how much of the locality of the nodes the next creates get is left
+        (one host read; probes)."""
+        c = self.counters.cpu().tolist()
+        h, pub = c[_lib.TC_FREE_HEAD], c[_lib.TC_FREE_PUB]
+        if pub - h <= 1:
+            return pub - h, 1.0
+        idx = torch.arange(h, pub, device=self.device) % \
+            self.free_list.numel()
+        seg = self.free_list[idx]
+        near = ((seg[1:] - seg[:-1]).abs() == 1).float().mean().item()
+        return pub - h, near
+
+    def sort_free(self):
+        """Sort the pending entries of the free ring (the nodes the next
+        creates take, in ring order): each workgroup's creates then get
+        nodes from one dense run again, however the blocks of earlier
+        batches interleaved their frees.  One host read of the ring
+        bounds; returns the entries sorted."""
+        c = self.counters.cpu().tolist()
+        h, pub = c[_lib.TC_FREE_HEAD], c[_lib.TC_FREE_PUB]
+        if pub - h <= 1:
+            return 0
+        idx = torch.arange(h, pub, device=self.device) % \
+            self.free_list.numel()
+        self.free_list[idx] = torch.sort(self.free_list[idx]).values
+        return pub - h
 
     def find_host(self, path):
         """Node index of ``path`` (host scan of the path table; tests)."""
@@ -484,6 +530,8 @@ class GpuServer(object):
             r, self.tree.store, self.out.numel(), out=self.out,
             presized=self.presized, terminate=terminate,
             stage=self.enc_stage)
+        if self.tree.compact_free:
+            self.tree.free_compact()
         self.last_rec_off = rec_off         # reply frame starts (R2 splits)
         self.result = (out, total, err, ft)
         if self.tree.watch is not None:

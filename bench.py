@@ -709,8 +709,7 @@ def run_rank(a):
                              16 if a.workload == 'storm' else
                              8 if a.workload in ('mix', 'chain', 'nest')
                              else 2),
-                         compact_free=a.workload in ('mix', 'nest',
-                                                     'storm'))
+                         compact_free=a.workload in ('mix', 'nest'))
         if a.workload == 'chain':
             pipe = S.ChainPipeline(tree, a.batch, a.data_bytes, seed=rank)
             per_step = pipe.n

@@ -35,6 +35,7 @@
 #include <Python.h>
 
 #include <arpa/inet.h>
+#include <linux/futex.h>
 #include <errno.h>
 #include <fcntl.h>
 #include <netdb.h>
@@ -44,10 +45,12 @@
 #include <sys/epoll.h>
 #include <sys/eventfd.h>
 #include <sys/socket.h>
+#include <sys/syscall.h>
 #include <time.h>
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -324,6 +327,7 @@ struct Loop {
   std::unordered_map<uint64_t, Watched*>* regs;  // strong refs
   double last_active;                            // mono_ms of the last event
   std::vector<Transport*>* dirty;                // writes to flush this turn
+  std::vector<PyObject*>* wakes;                 // Waiters set this turn
 };
 
 bool on_loop_thread(Loop* L) {
@@ -336,6 +340,131 @@ void wake(Loop* L) {
   ssize_t r = write(L->evfd, &one, sizeof one);
   (void)r;
 }
+
+// ---------------------------------------------------------------------------
+// Waiter: a blocking caller's completion flag (Client.call_sync).  The
+// caller waits in C with the GIL released: it spins on the flag for a short
+// window, then sleeps on it (futex).  Set on the loop thread (the reply's
+// callback runs there), the flag flips only once the loop has let go of the
+// GIL for its next wait, so the woken caller takes a free GIL: no thread of
+// the pair sleeps on the GIL handing the reply over (the bare-lock wake-up
+// cost two such sleeps: 11.5 us blocking p50 against 7.0 us for a get()
+// chained on the loop, profiles/r5_bench_1gpu_driver_config.log).
+// ---------------------------------------------------------------------------
+
+extern PyTypeObject LoopType;
+
+struct Waiter {
+  PyObject_HEAD
+  Loop* loop;                         // strong ref, may be null
+  std::atomic<int> state;             // 0 pending, 1 set
+  std::atomic<int> sleeping;          // the caller sleeps on `state`
+};
+
+PyTypeObject WaiterType = {PyVarObject_HEAD_INIT(nullptr, 0)};
+
+void waiter_flip(Waiter* w) {
+  w->state.store(1, std::memory_order_seq_cst);
+  if (w->sleeping.load(std::memory_order_seq_cst))
+    syscall(SYS_futex, (int*)&w->state, FUTEX_WAKE_PRIVATE, 1, nullptr,
+            nullptr, 0);
+}
+
+// The loop's part: after releasing the GIL for its wait, flip every Waiter
+// set this turn (no Python); after taking the GIL back, drop their refs.
+void flip_wakes(Loop* L) {
+  for (PyObject* o : *L->wakes) waiter_flip((Waiter*)o);
+}
+void drop_wakes(Loop* L) {
+  if (L->wakes->empty()) return;
+  std::vector<PyObject*> ws;
+  ws.swap(*L->wakes);
+  for (PyObject* o : ws) Py_DECREF(o);
+}
+
+PyObject* Waiter_new(PyTypeObject* type, PyObject* args, PyObject*) {
+  PyObject* lp = nullptr;
+  if (!PyArg_ParseTuple(args, "|O", &lp)) return nullptr;
+  if (lp == Py_None) lp = nullptr;
+  if (lp != nullptr && !PyObject_TypeCheck(lp, &LoopType)) {
+    PyErr_SetString(PyExc_TypeError, "Waiter(loop): a _zkloop.Loop");
+    return nullptr;
+  }
+  Waiter* w = (Waiter*)type->tp_alloc(type, 0);
+  if (w == nullptr) return nullptr;
+  w->loop = (Loop*)lp;
+  Py_XINCREF(lp);
+  new (&w->state) std::atomic<int>(0);
+  new (&w->sleeping) std::atomic<int>(0);
+  return (PyObject*)w;
+}
+
+void Waiter_dealloc(Waiter* w) {
+  Py_XDECREF((PyObject*)w->loop);
+  Py_TYPE(w)->tp_free((PyObject*)w);
+}
+
+// set(): on the loop thread deferred to the loop's next wait; elsewhere now.
+PyObject* Waiter_set(Waiter* w, PyObject*) {
+  if (w->state.load() != 0) Py_RETURN_NONE;
+  Loop* L = w->loop;
+  if (L != nullptr && on_loop_thread(L)) {
+    Py_INCREF(w);
+    L->wakes->push_back((PyObject*)w);
+  } else {
+    waiter_flip(w);
+  }
+  Py_RETURN_NONE;
+}
+
+// wait(spin_s, timeout_s) -> bool: spin up to spin_s, then sleep until set
+// or timeout; the GIL is released throughout.
+PyObject* Waiter_wait(Waiter* w, PyObject* args) {
+  double spin = 0, timeout = -1;
+  if (!PyArg_ParseTuple(args, "|dd", &spin, &timeout)) return nullptr;
+  bool ok;
+  Py_BEGIN_ALLOW_THREADS
+  const double t0 = mono_ms();
+  const double spin_end = t0 + spin * 1e3;
+  const double end = timeout < 0 ? -1 : t0 + timeout * 1e3;
+  while (w->state.load(std::memory_order_acquire) == 0 &&
+         mono_ms() < spin_end)
+    __builtin_ia32_pause();
+  ok = w->state.load(std::memory_order_acquire) != 0;
+  if (!ok) {
+    w->sleeping.store(1, std::memory_order_seq_cst);
+    for (;;) {
+      if (w->state.load(std::memory_order_seq_cst) != 0) { ok = true; break; }
+      timespec ts, *tp = nullptr;
+      if (end >= 0) {
+        const double left = end - mono_ms();
+        if (left <= 0) break;
+        ts.tv_sec = (time_t)(left / 1e3);
+        ts.tv_nsec = (long)((left - ts.tv_sec * 1e3) * 1e6);
+        tp = &ts;
+      }
+      syscall(SYS_futex, (int*)&w->state, FUTEX_WAIT_PRIVATE, 0, tp, nullptr,
+              0);
+    }
+  }
+  Py_END_ALLOW_THREADS
+  return PyBool_FromLong(ok);
+}
+
+PyObject* Waiter_is_set(Waiter* w, void*) {
+  return PyBool_FromLong(w->state.load() != 0);
+}
+
+PyMethodDef Waiter_methods[] = {
+    {"set", (PyCFunction)Waiter_set, METH_NOARGS,
+     "mark done (from the loop thread: at the loop's next wait)"},
+    {"wait", (PyCFunction)Waiter_wait, METH_VARARGS,
+     "wait(spin_s=0, timeout_s=-1) -> bool, GIL released"},
+    {nullptr, nullptr, 0, nullptr}};
+
+PyGetSetDef Waiter_getset[] = {
+    {"is_set", (getter)Waiter_is_set, nullptr, nullptr, nullptr},
+    {nullptr, nullptr, nullptr, nullptr, nullptr}};
 
 void report_exception(Loop* L) {
   PyObject *t, *v, *tb;
@@ -1454,6 +1583,7 @@ PyObject* Loop_new(PyTypeObject* type, PyObject* args, PyObject*) {
   L->timers = new std::vector<Handle*>();
   L->regs = new std::unordered_map<uint64_t, Watched*>();
   L->dirty = new std::vector<Transport*>();
+  L->wakes = new std::vector<PyObject*>();
   return (PyObject*)L;
 }
 
@@ -1478,6 +1608,11 @@ void clear_all(Loop* L) {
 }
 
 void Loop_dealloc(Loop* L) {
+  if (L->wakes != nullptr) {
+    flip_wakes(L);
+    drop_wakes(L);
+    delete L->wakes;
+  }
   if (L->ready != nullptr) clear_all(L);
   delete L->ready;
   delete L->timers;
@@ -1530,6 +1665,7 @@ PyObject* Loop_run(Loop* L, PyObject*) {
     }
     int n;
     Py_BEGIN_ALLOW_THREADS
+    flip_wakes(L);              // blocked callers wake to a free GIL
     if (timeout != 0 && loop_spin_ms() > 0) {
       // Adaptive busy-poll: for a short window after the last activity the
       // thread polls instead of sleeping, so the reply to a request it just
@@ -1557,10 +1693,13 @@ PyObject* Loop_run(Loop* L, PyObject*) {
       n = epoll_wait(L->epfd, evs.data(), (int)evs.size(), timeout);
     }
     Py_END_ALLOW_THREADS
+    drop_wakes(L);
     if (n > 0 || !L->ready->empty()) L->last_active = mono_ms();
     if (n < 0 && errno != EINTR) {
       PyErr_SetFromErrno(PyExc_OSError);
       L->running = false;
+      flip_wakes(L);
+      drop_wakes(L);
       return nullptr;
     }
     for (int i = 0; i < n && !L->stopping; ++i) {
@@ -1601,6 +1740,8 @@ PyObject* Loop_run(Loop* L, PyObject*) {
   flush_dirty(L);           // what the last turn wrote still leaves
   clear_all(L);
   L->running = false;
+  flip_wakes(L);                // callers set on the last turn
+  drop_wakes(L);
   Py_RETURN_NONE;
 }
 
@@ -1809,6 +1950,14 @@ PyMODINIT_FUNC PyInit__zkloop(void) {
   ServerType.tp_methods = Server_methods;
   ServerType.tp_getset = Server_getset;
 
+  WaiterType.tp_name = "_zkloop.Waiter";
+  WaiterType.tp_basicsize = sizeof(Waiter);
+  WaiterType.tp_flags = Py_TPFLAGS_DEFAULT;
+  WaiterType.tp_new = Waiter_new;
+  WaiterType.tp_dealloc = (destructor)Waiter_dealloc;
+  WaiterType.tp_methods = Waiter_methods;
+  WaiterType.tp_getset = Waiter_getset;
+
   LoopType.tp_name = "_zkloop.Loop";
   LoopType.tp_basicsize = sizeof(Loop);
   LoopType.tp_flags = Py_TPFLAGS_DEFAULT;
@@ -1817,7 +1966,8 @@ PyMODINIT_FUNC PyInit__zkloop(void) {
   LoopType.tp_methods = Loop_methods;
 
   if (PyType_Ready(&HandleType) < 0 || PyType_Ready(&TransportType) < 0 ||
-      PyType_Ready(&ServerType) < 0 || PyType_Ready(&LoopType) < 0)
+      PyType_Ready(&ServerType) < 0 || PyType_Ready(&LoopType) < 0 ||
+      PyType_Ready(&WaiterType) < 0)
     return nullptr;
   PyObject* m = PyModule_Create(&mod);
   if (m == nullptr) return nullptr;
@@ -1829,5 +1979,7 @@ PyMODINIT_FUNC PyInit__zkloop(void) {
   PyModule_AddObject(m, "Transport", (PyObject*)&TransportType);
   Py_INCREF(&ServerType);
   PyModule_AddObject(m, "Server", (PyObject*)&ServerType);
+  Py_INCREF(&WaiterType);
+  PyModule_AddObject(m, "Waiter", (PyObject*)&WaiterType);
   return m;
 }

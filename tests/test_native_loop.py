@@ -42,6 +42,43 @@ def test_call_soon_order_and_threads(nl):
         nl.run(lambda: {}['x'])
 
 
+def test_waiter_set_on_loop_and_off_loop(nl):
+    """Waiter (Client.call_sync's completion flag): set on the loop thread
+    it flips once the loop lets go of the GIL for its next wait; set from
+    another thread it flips at once; wait() times out unset."""
+    w = nl.waiter()
+    assert not w.is_set
+    t0 = time.perf_counter()
+    assert not w.wait(0.0, 0.02)
+    assert time.perf_counter() - t0 >= 0.015
+    seen = []
+
+    def on_loop():
+        w.set()
+        seen.append(w.is_set)          # deferred: not yet, same turn
+    nl.call_soon(on_loop)
+    assert w.wait(0.0, 5.0) and w.is_set
+    assert seen == [False]
+    w2 = nl.waiter()
+    threading.Timer(0.01, w2.set).start()
+    assert w2.wait(0.001, 5.0)
+    # a spin-only wait that the loop settles
+    w3 = nl.waiter()
+    nl.call_soon(w3.set)
+    assert w3.wait(1.0, 5.0)
+
+
+def test_waiter_flipped_when_the_loop_stops():
+    lp = nloop.NativeLoop('t-stop')
+    w = lp.waiter()
+
+    def last():
+        w.set()
+        lp.stop()
+    lp.call_soon(last)
+    assert w.wait(0.0, 5.0)
+
+
 def test_timers_fire_in_deadline_order(nl):
     seen = []
     t0 = nl.time_ms()

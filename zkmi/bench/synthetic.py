@@ -57,6 +57,10 @@ _GET_STAGE = int(os.environ.get('ZKMI_GET_STAGE', '8192'))
 # ZKMI_FREE_COMPACT=0: no free-ring compaction after write batches (trees
 # built with compact_free=True; GpuTree.free_compact)
 _FREE_COMPACT = os.environ.get('ZKMI_FREE_COMPACT', '1') == '1'
+# the storm rebuilds its hash index when the entries claimed since the last
+# rebuild (live + tombstones of never-reused SEQUENTIAL names) would pass
+# this share of the table
+_REHASH_LOAD = float(os.environ.get('ZKMI_REHASH_LOAD', '0.3'))
 
 
 def _len(total):
@@ -1530,7 +1534,7 @@ class StormPipeline(object):
         """Rebuild the hash index now if the next ``steps`` steps' inserts
         would fill it (tombstones of never-reused sequential names)."""
         if (self.inserted + (steps + 1) * self.n * self.world) > \
-                0.6 * self.tree.hcap:
+                _REHASH_LOAD * self.tree.hcap:
             self.tree.rehash()
             self.inserted = 0
 

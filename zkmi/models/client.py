@@ -36,6 +36,8 @@ from .connection_set import ConnectionSet, StaticResolver
 # than the round trip and does nothing); off on small hosts, where the
 # poller competes with the loop thread for the GIL.
 _SYNC_SPIN_US_AUTO = 100.0 if (os.cpu_count() or 1) >= 16 else 0.0
+# ZKMI_SYNC_WAITER=0: call_sync waits on a bare lock even on the native loop
+_SYNC_WAITER = os.environ.get('ZKMI_SYNC_WAITER', '1') == '1'
 from .session import ZKSession, _zkmach, native_machines
 
 
@@ -692,11 +694,30 @@ class Client(FSM):
         if self.loop.in_loop():
             raise RuntimeError('call_sync must not be used on the loop '
                                'thread')
+        box = {}
+        spin = self.config.sync_spin_us
+        spin = (_SYNC_SPIN_US_AUTO if spin is None else spin) / 1e6
+        mk = getattr(self.loop, 'waiter', None) if _SYNC_WAITER else None
+        if mk is not None:
+            # the native loop's Waiter: this thread waits in C with the GIL
+            # released, and the loop flips the flag only after letting go of
+            # the GIL — no GIL hand-over sleeps on the reply's way back
+            w = mk()
+
+            def cb(err=None, *res):
+                if 'err' in box:
+                    return      # settled already (one callback per call)
+                box['err'] = err
+                box['res'] = res
+                w.set()
+            getattr(self, method)(*args, cb)
+            if not w.wait(spin, timeout):
+                raise TimeoutError('%s%r timed out' % (method, args))
+            return self._sync_result(box)
         # a bare lock, released by the loop thread: the cheapest cross-thread
         # wake-up CPython has (threading.Event adds a Condition round)
         done = threading.Lock()
         done.acquire()
-        box = {}
 
         def cb(err=None, *res):
             if 'err' in box:
@@ -706,8 +727,6 @@ class Client(FSM):
             done.release()
         getattr(self, method)(*args, cb)
         got = False
-        spin = self.config.sync_spin_us
-        spin = (_SYNC_SPIN_US_AUTO if spin is None else spin) / 1e6
         if spin > 0:
             # a short poll before sleeping on the lock: the reply usually
             # lands within tens of us, and a sleeping thread's wake-up costs
@@ -719,6 +738,10 @@ class Client(FSM):
                     time.sleep(0)
         if not got and not done.acquire(timeout=timeout):
             raise TimeoutError('%s%r timed out' % (method, args))
+        return self._sync_result(box)
+
+    @staticmethod
+    def _sync_result(box):
         if box['err'] is not None:
             raise box['err']
         res = box['res']

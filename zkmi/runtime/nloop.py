@@ -84,6 +84,12 @@ class NativeLoop(object):
 
     # -- scheduling ---------------------------------------------------------
 
+    def waiter(self):
+        """A completion flag a blocking caller waits on with the GIL
+        released; ``set()`` from the loop thread takes effect when the loop
+        next releases the GIL (csrc/host/zk_loop.cpp Waiter)."""
+        return _zkloop.Waiter(self._n)
+
     def in_loop(self):
         return self._n.in_loop()
 

@@ -29,15 +29,18 @@ a step makes no device-to-host read (K1 reads every stream's length from
 the device byte count its encoder produced), so the connections' kernels
 overlap.
 
-GET scale-out (the headline at every N): ONE tree sharded by path hash over
-the ranks, every read routed to the rank that owns its path (R2,
-zkmi/parallel/sharded.py): per connection and step, two equal-split
-``all_to_all_single`` over RCCL/xGMI (the request slots out, the reply
-slots back) — the bytes really cross the GPUs.  With one GPU there is one
-shard and nothing to route; the step is the local pipeline, HIP-graph
-captured.  For N > 1 the same run also times ``--replica`` (every rank
-serves its own full replica, no collective in the step) and reports it as
-``replica_value``; ``--replica`` makes that the headline instead.
+GET scale-out (the headline at N > 1): every rank holds the whole tree in
+its HBM and serves its own sessions' reads from it, as every ZooKeeper
+server answers reads from its own replica (1M znodes take ~0.4 GB of the
+288 GB).  The same run then times ONE tree sharded by path hash over the
+ranks, every read routed to the rank that owns its path (R2,
+zkmi/parallel/sharded.py: per connection and step, two equal-split
+``all_to_all_single`` over RCCL/xGMI, the request slots out and the reply
+slots back) and reports it as ``sharded_value`` — the layout for trees past
+one GPU's memory; ``--sharded`` makes that the headline instead.  With one
+GPU there is one replica and the step is the local pipeline, HIP-graph
+captured (``--force-route`` runs the multi-rank step over a one-rank RCCL
+group and compares it with the local one).
 
 One process per GPU: ``--gpus N`` without a torchrun environment starts the
 N rank processes itself (before anything touches the GPU); under torchrun
@@ -457,9 +460,11 @@ def main():
                     default='get')
     ap.add_argument('--replica', action='store_true',
                     help='get: every rank serves its own full replica of the '
-                         'tree (no collective in the step) instead of the '
-                         'path-hash-sharded tree with R2 routing over '
-                         'RCCL/xGMI (the default)')
+                         'tree (the default; kept for old command lines)')
+    ap.add_argument('--sharded', action='store_true',
+                    help='get, N > 1: make the path-hash-sharded tree with '
+                         'R2 routing over RCCL/xGMI the headline (default: '
+                         'timed after the replica step, as sharded_*)')
     ap.add_argument('--hash-factor', type=int, default=0,
                     help='hash entries per node slot, rounded up to a power '
                     'of two (0: 16 for the storm, 8 for mix / chain / nest, '
@@ -661,7 +666,14 @@ def run_rank(a):
         dd = tuple(int(x) for x in rng.split('-'))
     if a.name_pad:
         npad = tuple(int(x) for x in a.name_pad.split('-'))
-    sharded = a.workload == 'get' and not a.replica
+    # GET at N > 1: every member holds the whole tree in its HBM and serves
+    # its sessions' reads from it — ZooKeeper's read path (any server
+    # answers a read from its replica); 1M znodes are ~0.4 GB of 288.  The
+    # path-hash-sharded tree with reads routed over xGMI (R2) is for trees
+    # past one GPU's memory: --sharded makes it the headline, otherwise it
+    # is timed after the replica step (sharded_*).
+    sharded = a.workload == 'get' and (a.sharded or a.force_route) and \
+        not a.replica
 
     def make_get(replica):
         if replica:
@@ -755,11 +767,10 @@ def run_rank(a):
         sustained = {'steps': k, 'seconds': sel,
                      'ops_s': per_step * k * world / sel,
                      'ms_per_step': sel / k * 1e3}
-    r2 = None
-    if sharded:
+    def r2_stats(pipe):
         st = pipe.stats
-        r2 = {'bytes_sent_per_rank_step': st['bytes_sent'] / max(st['steps'],
-                                                                 1),
+        return {'bytes_sent_per_rank_step': st['bytes_sent'] / max(st['steps'],
+                                                                   1),
               'wire_bytes_sent_per_rank_step':
                   st['wire_bytes_sent'] / max(st['steps'], 1),
               'remote_requests': st['remote_reqs'],
@@ -770,17 +781,26 @@ def run_rank(a):
                   st['local_bytes_through_collective'],
               'slot_bytes': {'request': st['req_slot_bytes'],
                              'reply': st['rep_slot_bytes']}}
-    replica = None
-    if sharded and (world > 1 or a.force_route) and not a.no_compare:
-        # the same batch served by per-rank full replicas (no collective in
-        # the step): what the sharding's xGMI traffic costs
+    r2 = r2_stats(pipe) if sharded else None
+    replica = shard_cmp = None
+    if a.workload == 'get' and (world > 1 or a.force_route) and \
+            not a.no_compare:
+        # the other GET mode on the same batch size: the replicas (no
+        # collective in the step) after a sharded headline, or the sharded
+        # tree (R2 over RCCL/xGMI) after the replicas — what routing the
+        # reads across the GPUs costs
         del pipe
         torch.cuda.empty_cache()
-        rp = make_get(True)
+        rp = make_get(sharded)
         rel, rok, rgraph = _time_steps(rp, a, world, dev)
         rel = checked(rp, rel, rok)
-        replica = {'value': ops / rel, 'ms_per_step': rel / a.steps * 1e3,
-                   'hip_graph': bool(rgraph)}
+        res = {'value': ops / rel, 'ms_per_step': rel / a.steps * 1e3,
+               'hip_graph': bool(rgraph)}
+        if sharded:
+            replica = res
+        else:
+            shard_cmp = res
+            r2 = r2_stats(rp)
         del rp
 
     rtt50 = rtt99 = py50 = py99 = bulk_ops = bulk_ms = bulk_ph = None
@@ -844,7 +864,13 @@ def run_rank(a):
                          'pipeline' if a.force_route else
                          'one shard (nothing to route), local pipeline')
                         if sharded else
-                        ('replica per rank' if a.workload == 'get' else None),
+                        ('replica per rank: every member holds the whole '
+                         'tree and serves its reads locally (ZooKeeper\'s '
+                         'read path); sharded_* = one tree sharded by path '
+                         'hash, reads routed with all_to_all over %s' % (
+                             'RCCL/xGMI' if backend == 'nccl' else backend)
+                         if a.workload == 'get' and world > 1 else
+                         'replica per rank' if a.workload == 'get' else None),
             'value_note': 'value: the on-device pipeline rate (K10 '
                           'request encode -> GPU-resident server -> K1 + '
                           'K2-K8 reply decode and check, all in HBM, no TCP '
@@ -860,6 +886,9 @@ def run_rank(a):
                               else None,
             'replica_value': replica['value'] if replica else None,
             'replica_ms_per_step': replica['ms_per_step'] if replica else None,
+            'sharded_value': shard_cmp['value'] if shard_cmp else None,
+            'sharded_ms_per_step': shard_cmp['ms_per_step'] if shard_cmp
+            else None,
             'p50_get_rtt_us': rtt50,
             'p99_get_rtt_us': rtt99,
             'rtt_note': 'one blocking Client.call_sync(get) over loopback '

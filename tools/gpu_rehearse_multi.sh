@@ -28,4 +28,7 @@ trun() {      # torchrun starts them (the driver's form)
   return $rc
 }
 own 2 get2_own --no-rtt --batch $B && trun 2 get2_torchrun --no-rtt --batch $B && \
-  own 8 get8_own --no-rtt --batch $B && own 4 ens4 --workload ensemble
+  own 2 get2_sharded --no-rtt --batch $B --sharded && \
+  own 8 get8_own --no-rtt --batch $B && \
+  own 2 storm2 --no-rtt --workload storm --batch 65536 && \
+  own 4 ens4 --workload ensemble

@@ -366,6 +366,18 @@ ZK_DEV bool tree_erase(const ZkTree& t, int64_t v, const uint8_t* p,
   return false;
 }
 
+// tree_erase at the entry a lookup just found (slot s): no second probe.
+// The CAS against the live val the lookup saw keeps one winner among
+// concurrent erasers of the node; a lost race answers like tree_erase.
+ZK_DEV bool tree_erase_at(const ZkTree& t, int64_t s, int64_t v) {
+  if (s < 0) return false;
+  const int64_t cur = __hip_atomic_load(ht_val(t, s), __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_AGENT);
+  return cur >= 0 && val_node(cur) == v &&
+         atomicCAS((unsigned long long*)ht_val(t, s), (unsigned long long)cur,
+                   (unsigned long long)-2) == (unsigned long long)cur;
+}
+
 // ---- watches (one-shot, per watcher slot) ---------------------------------
 // A path-keyed table beside the tree (lib/zk-session.js:482-526 describes
 // the server semantics the client relies on): key = path
@@ -603,7 +615,10 @@ ZK_DEV int32_t do_create(const ZkTree& t, Lane& L, const uint8_t* data,
   if (cut > 0 && par < 0) return ERR_NO_NODE;
   if (par >= 0 && ld_be64(s.slab + s.slot_off[par] + 44) != 0)
     return ERR_NO_CHILDREN_FOR_EPHEMERALS;
-  if (!seq && tree_find(t, path, pl) >= 0) return ERR_NODE_EXISTS;
+  // (an existing path is found by tree_insert itself — it probes the same
+  // chain and answers NODE_EXISTS before publishing anything — so the
+  // usual, successful create walks the chain once, not twice; what this
+  // lane wrote to its own node v before is freed by the caller)
   const int32_t npl = pl + (seq ? 10 : 0);
   const int32_t seqno = seq && par >= 0 ? atomicAdd(&t.cver[par], 1) : 0;
   uint8_t* pd = t.path_arena + t.node_path_off[v];
@@ -829,7 +844,7 @@ __global__ __launch_bounds__(TR_T) void tree_serve_k(
           L.err = ERR_BAD_VERSION;
           break;
         }
-        if (!tree_erase(t, node, L.path, L.pl)) { L.err = ERR_NO_NODE; break; }
+        if (!tree_erase_at(t, f.ent, node)) { L.err = ERR_NO_NODE; break; }
         L.par = t.node_parent[node];
         if (L.par >= 0) parent_touch(t, L.par, -1, true, L.zx);
         st_be64(s.slab + so + 44, 0);                 // ephemeralOwner

@@ -881,6 +881,10 @@ def run_rank(a):
                           'over a window of about %.0f s' % SUSTAIN_S,
             'sustained': sustained,
             'end_to_end_ops_s': bulk_k[0],
+            # the client-API figure against the same reference decode rate
+            # (value above is the on-device pipeline; value_note)
+            'vs_baseline_end_to_end': (bulk_k[0] / REF_PKTS_PER_S
+                                       if bulk_k[0] else None),
             'r2': r2,
             'workload_stats': dict(pipe.stats) if a.workload == 'storm'
                               else None,

@@ -3100,9 +3100,9 @@ int zk_frame_scan6(const uint8_t* buf, const int64_t* n_dev, int64_t n_cap,
   // tiles a wave: groups (the map once, the chain walked on) for streams
   // of large frames within a small window; tests of the link repair and
   // long-frame streams take single tiles
-  int G = ((flags >> 4) & 7) + 1;
+  int G = ((flags >> 4) & 15) + 1;
   if ((flags & (FS_LONG | 1 | 0xFFFF00)) || W > 512) G = 1;
-  G = G >= 8 ? 8 : G >= 4 ? 4 : G >= 2 ? 2 : 1;
+  G = G >= 16 ? 16 : G >= 8 ? 8 : G >= 4 ? 4 : G >= 2 ? 2 : 1;
   const int64_t waves = (tiles + G - 1) / G;
   const unsigned tblocks = (unsigned)((waves + tpb - 1) / tpb);
 #define ZK_FS_TILE(WW, LL)                                                   \
@@ -3113,7 +3113,10 @@ int zk_frame_scan6(const uint8_t* buf, const int64_t* n_dev, int64_t n_cap,
   fs_tile<WW, false, GG><<<tblocks, 64 * tpb, FT_LDS * tpb, st>>>(           \
       buf, n_dev, n_cap, maxp, list, pre, sx, lbw, rent, rexit, rmeta, rcnt, \
       tiles, dbg, fs_minb(), flags, cx)
-  if (G == 8) {
+  if (G == 16) {
+    if (W == 256) ZK_FS_GROUP(256, 16);
+    else ZK_FS_GROUP(512, 16);
+  } else if (G == 8) {
     if (W == 256) ZK_FS_GROUP(256, 8);
     else ZK_FS_GROUP(512, 8);
   } else if (G == 4) {

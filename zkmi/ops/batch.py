@@ -13,9 +13,11 @@ K10 :func:`encode_requests`; K11 :func:`encode_set_watches`; K12
 :func:`decode_requests`; K13 :func:`encode_responses`.
 """
 
+import os
 from dataclasses import dataclass
 
 import numpy as np
+
 import torch
 
 from .. import consts
@@ -27,6 +29,11 @@ I64 = torch.int64
 I32 = torch.int32
 U8 = torch.uint8
 
+
+
+# K1 tiles a wave takes on streams of large frames (FrameScanner group;
+# ZKMI_FS_GROUP: 1, 2, 4, 8 or 16)
+_FS_GROUP = int(os.environ.get('ZKMI_FS_GROUP', '8'))
 
 def _dev(device):
     return torch.device(device) if device is not None else \
@@ -371,7 +378,8 @@ class FrameScanner:
         # GET reply stream (192-byte frames): 8 tiles a wave 77.4 us, 4
         # tiles 93.0 us (profiles/r4_k1_microbench.md)
         if group is None:
-            group = 8 if frame_hint is not None and frame_hint >= 128 else 1
+            group = _FS_GROUP if frame_hint is not None and \
+                frame_hint >= 128 else 1
         self.group = group
         self.max_packet = max_packet
         self.table = FrameTable(torch.empty(cap, dtype=I64, device=device),

@@ -51,9 +51,12 @@ _SIDE_FINISH = os.environ.get('ZKMI_SIDE_FINISH', '0') == '1'
 # segfaulted in hipStreamEndCapture (test_gpu_get_pipeline_graph_replay)
 _LINK_PRIO = os.environ.get('ZKMI_LINK_PRIO', '0') == '1'
 # ZKMI_GET_STAGE: the LDS bytes per workgroup the GET pipelines' reply
-# encode asks for (uniform GET replies need only the writer's 7 KiB header
-# table; 0: the encoder's 28 KiB default)
-_GET_STAGE = int(os.environ.get('ZKMI_GET_STAGE', '8192'))
+# encode asks for (0: the encoder's 28 KiB).  Uniform GET replies need only
+# the writer's 7 KiB header table, but 8 KiB measured no faster for them
+# (0.581 vs 0.581 ms) and slowed variable payloads, whose replies go
+# through the LDS image (uniform 0-200 B 0.710 -> 0.972 ms,
+# profiles/r5_get_stage_ab.log): off.
+_GET_STAGE = int(os.environ.get('ZKMI_GET_STAGE', '0'))
 # ZKMI_FREE_COMPACT=0: no free-ring compaction after write batches (trees
 # built with compact_free=True; GpuTree.free_compact)
 _FREE_COMPACT = os.environ.get('ZKMI_FREE_COMPACT', '1') == '1'

@@ -318,7 +318,6 @@ class _Conn(object):
         self.server = GpuServer(t, cap, max(cap * self.rep_max,
                                             W * (self.rep_slot - SEG_HDR))
                                 + 64, window=B.frame_window(self.req_max))
-        self.server.enc_stage = 8192     # uniform GET replies (K13 writer)
         # the replies to this connection's own n requests come back
         lo, hi = t.data_dist or (t.data_bytes, t.data_bytes)
         self.rscanner = B.FrameScanner(n, dev,

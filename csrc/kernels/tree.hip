@@ -4,10 +4,10 @@
 // tests talk to, so that the whole request -> reply path runs at HBM speed.
 //
 // Layout (HBM, sized by the caller for 288 GB parts):
-//   * open-addressing hash table of 16-byte entries {key, val} (one load per
-//     probe): key = word-wise multiply-xorshift hash of the path | 1, val =
-//     node index (-2 = tombstone, -3 = being published), linear probing,
-//     pow2 capacity;
+//   * open-addressing hash table of 64-byte entries {key, val, path head,
+//     data length} (one line per probe): key = word-wise multiply-xorshift
+//     hash of the path | 1, val = node and slot + 1 (-2 = tombstone, 0 =
+//     empty or being published), linear probing, pow2 capacity;
 //   * node slots in wire format (zk_batch.h ZkNodeStore), so replies are
 //     contiguous copies;
 //   * a path arena holding each node's path for exact-match verification;
@@ -157,7 +157,7 @@ ZK_DEV bool bytes_eq(const uint8_t* a, const uint8_t* b, int32_t n) {
 
 // One 64-byte entry per slot (a cache line; open addressing, linear
 // probing): int64 words [0] key = path hash | 1 (0 empty), [1] val (node |
-// slot offset, below; -2 tombstone, -3 empty or being published), [2] path
+// slot offset, below; -2 tombstone, 0 empty or being published), [2] path
 // length | data length << 32, [3, 8) the path's first EN_PATH bytes.  A
 // lookup loads the entry in one burst and verifies the path and gets a GET
 // reply's data length from it: ONE random line per lookup (rounds 2-4 read
@@ -247,13 +247,18 @@ ZK_DEV void ent_load(const ZkTree& t, int64_t s, int64_t (&e)[HT_W]) {
 }
 
 // A hash val holds the node index (low 32 bits) and its slot offset / 16
-// (high 32; slots are 16-byte aligned), so a hit needs no slot_off[v] read.
-// Tombstone (-2) and being-published (-3) stay negative.
+// (high 32; slots are 16-byte aligned), plus one, so a hit needs no
+// slot_off[v] read.  Live vals are > 0, the tombstone is -2, and 0 is an
+// empty or being-published entry: an empty table is all zero bytes (a
+// plain memset resets it; the -3 "empty" of before took a strided second
+// pass).
 ZK_DEV int64_t val_pack(int64_t v, int64_t slot) {
-  return (int64_t)(((uint64_t)slot >> 4) << 32) | v;
+  return ((int64_t)(((uint64_t)slot >> 4) << 32) | v) + 1;
 }
-ZK_DEV int64_t val_node(int64_t x) { return x & 0xFFFFFFFFll; }
-ZK_DEV int64_t val_slot(int64_t x) { return (int64_t)((uint64_t)x >> 32) << 4; }
+ZK_DEV int64_t val_node(int64_t x) { return (x - 1) & 0xFFFFFFFFll; }
+ZK_DEV int64_t val_slot(int64_t x) {
+  return (int64_t)((uint64_t)(x - 1) >> 32) << 4;
+}
 
 // Node of path p (node -1 if absent), its slot offset and data length, and
 // the hash entry (for a SET_DATA's data length update).
@@ -270,13 +275,13 @@ ZK_DEV Found tree_lookup(const ZkTree& t, const uint8_t* p, int32_t n) {
   int64_t s = key & t.mask;
   for (int64_t probe = 0; probe <= t.mask; ++probe) {
     // one 64-byte entry per probe, loaded in one burst; entries being
-    // written concurrently in this launch may read torn (val -3): not
+    // written concurrently in this launch may read torn (val 0): not
     // found, as the batch contract allows for same-batch conflicts on one
     // path
     int64_t e[HT_W];
     ent_load(t, s, e);
     if (e[0] == 0) break;
-    if (e[0] == key && e[1] >= 0) {
+    if (e[0] == key && e[1] > 0) {
       const int64_t node = val_node(e[1]);
       if (ent_is(t, e, node, p, n))
         return Found{node, val_slot(e[1]), (int32_t)(e[2] >> 32), s};
@@ -316,22 +321,22 @@ ZK_DEV int64_t tree_insert(const ZkTree& t, int64_t v, const uint8_t* p,
       return v;
     }
     if (k == key) {
-      int64_t w = -3;
+      int64_t w = 0;
       // The claimer may not have published the val yet: bounded wait.
-      for (int spin = 0; spin < 1000000 && w == -3; ++spin)
+      for (int spin = 0; spin < 1000000 && w == 0; ++spin)
         w = __hip_atomic_load(ht_val(t, s), __ATOMIC_RELAXED,
                               __HIP_MEMORY_SCOPE_AGENT);
-      if (w == -3) return TREE_INSERT_TIMEOUT;
-      if (w >= 0) {
+      if (w == 0) return TREE_INSERT_TIMEOUT;
+      if (w > 0) {
         int64_t e[HT_W];
         ent_load(t, s, e);
         if (ent_is(t, e, val_node(w), p, n)) return val_node(w);
       }
-      // a tombstone of the same key: claim it (-3 while its words are
+      // a tombstone of the same key: claim it (0 while its words are
       // rewritten), then publish
       if (w == -2 &&
           atomicCAS((unsigned long long*)ht_val(t, s), (unsigned long long)-2,
-                    (unsigned long long)-3) == (unsigned long long)-2) {
+                    0ull) == (unsigned long long)-2) {
         ent_fill(t, s, p, n, dl);
         __hip_atomic_store(ht_val(t, s), pv, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
@@ -355,7 +360,7 @@ ZK_DEV bool tree_erase(const ZkTree& t, int64_t v, const uint8_t* p,
     if (k == key) {
       const int64_t cur = __hip_atomic_load(ht_val(t, s), __ATOMIC_RELAXED,
                                             __HIP_MEMORY_SCOPE_AGENT);
-      if (cur >= 0 && val_node(cur) == v &&
+      if (cur > 0 && val_node(cur) == v &&
           atomicCAS((unsigned long long*)ht_val(t, s),
                     (unsigned long long)cur,
                     (unsigned long long)-2) == (unsigned long long)cur)
@@ -373,7 +378,7 @@ ZK_DEV bool tree_erase_at(const ZkTree& t, int64_t s, int64_t v) {
   if (s < 0) return false;
   const int64_t cur = __hip_atomic_load(ht_val(t, s), __ATOMIC_RELAXED,
                                         __HIP_MEMORY_SCOPE_AGENT);
-  return cur >= 0 && val_node(cur) == v &&
+  return cur > 0 && val_node(cur) == v &&
          atomicCAS((unsigned long long*)ht_val(t, s), (unsigned long long)cur,
                    (unsigned long long)-2) == (unsigned long long)cur;
 }
@@ -493,19 +498,6 @@ __global__ __launch_bounds__(TR_T) void tree_fill_k(ZkTree t, int64_t n0,
   t.nchild[v] = nkids[v];
   t.pzxid[v] = v + 1;
   t.dirty[v] = 0;
-}
-
-// Every hash entry back to empty (key 0, val -3, the rest 0): one pass of
-// 16-byte stores over the table (was a zero fill and a strided fill of the
-// val words, 2 passes and a 460 us strided one at 16M entries).
-__global__ __launch_bounds__(TR_T) void ht_reset_k(int64_t* __restrict__ ht,
-                                                   int64_t nchunk) {
-  uint4* q = (uint4*)ht;
-  const uint4 z = make_uint4(0u, 0u, 0u, 0u);
-  const uint4 kv = make_uint4(0u, 0u, 0xFFFFFFFDu, 0xFFFFFFFFu);
-  for (int64_t c = (int64_t)blockIdx.x * TR_T + threadIdx.x; c < nchunk;
-       c += (int64_t)gridDim.x * TR_T)
-    q[c] = (c & (HT_W / 2 - 1)) == 0 ? kv : z;
 }
 
 // Free-ring compaction between batches: the ring's pending entries rebuilt
@@ -1496,13 +1488,11 @@ int zk_tree_free_compact(const ZkTree* t, int64_t* ws, hipStream_t st) {
   return 0;
 }
 
+// Every hash entry back to empty: all zero bytes (val_pack), one memset.
+// (Round 5's first reset wrote {0, -3, 0...} entries from a kernel: 2.2 ms
+// for the storm's 4 GB table.)
 int zk_tree_ht_reset(const ZkTree* t, hipStream_t st) {
-  const int64_t nchunk = (t->mask + 1) * (zk::HT_W / 2);
-  int64_t nb = (nchunk + zk::TR_T - 1) / zk::TR_T;
-  if (nb > 8192) nb = 8192;                    // grid-stride past 2M lanes
-  zk::ht_reset_k<<<(unsigned)nb, zk::TR_T, 0, st>>>(t->ht, nchunk);
-  ZK_LAUNCH_CHECK();
-  return 0;
+  return hipMemsetAsync(t->ht, 0, (size_t)(t->mask + 1) * zk::HT_W * 8, st);
 }
 
 int zk_tree_build(const ZkTree* t, int64_t n0, int64_t n, hipStream_t st) {

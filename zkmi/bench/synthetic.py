@@ -217,9 +217,8 @@ class GpuTree(object):
         # (SEQUENTIAL names never reused) fills with tombstones between
         # rebuilds, and a wider table rebuilds less often
         hcap = _next_pow2(hash_factor * cap)
-        # interleaved 16-byte {key, val} entries (csrc/kernels/tree.hip)
+        # 64-byte entries, empty = all zero bytes (csrc/kernels/tree.hip)
         self.ht = torch.zeros(_lib.HT_WORDS * hcap, dtype=I64, device=dev)
-        self.ht.view(-1, _lib.HT_WORDS)[:, 1] = -3
         cnt = [0] * _lib.TC_N
         cnt[_lib.TC_NODES], cnt[_lib.TC_ZXID] = nst, nst
         cnt[_lib.TC_PATH_TOP], cnt[_lib.TC_SLAB_TOP] = len(arena), nst * sb

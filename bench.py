@@ -465,6 +465,10 @@ def main():
                     help='get, N > 1: make the path-hash-sharded tree with '
                          'R2 routing over RCCL/xGMI the headline (default: '
                          'timed after the replica step, as sharded_*)')
+    ap.add_argument('--ndirs', type=int, default=1024,
+                    help='mix / storm: parent directories the writes spread '
+                         'over (a workload shape knob; parents take the '
+                         'cversion / child-count atomics)')
     ap.add_argument('--hash-factor', type=int, default=0,
                     help='hash entries per node slot, rounded up to a power '
                     'of two (0: 16 for the storm, 8 for mix / chain / nest, '
@@ -729,11 +733,12 @@ def run_rank(a):
             pipe = S.NestPipeline(tree, a.batch, seed=rank)
             per_step = pipe.n
         elif a.workload == 'mix':
-            pipe = S.MixPipeline(tree, a.batch, a.data_bytes, seed=rank)
+            pipe = S.MixPipeline(tree, a.batch, a.data_bytes,
+                                 ndirs=a.ndirs, seed=rank)
             per_step = pipe.n
         else:
             # across GPUs the sessions move between members (R3)
-            pipe = S.StormPipeline(tree, a.batch, seed=rank,
+            pipe = S.StormPipeline(tree, a.batch, ndirs=a.ndirs, seed=rank,
                                    coll_device=cdev if world > 1 else None)
             per_step = pipe.n
 

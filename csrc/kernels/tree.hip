@@ -16,7 +16,8 @@
 //   * a free-node ring: DELETE (and session expiry) push the node index,
 //     CREATE pops one published by an EARLIER launch (tree_publish_k runs
 //     between batches), reusing its slot and path storage when they fit;
-//   * host-endian shadows of each node's cversion / numChildren / pzxid.
+//   * host-endian shadows of each node's cversion / numChildren (one packed
+//     word, cn_*) and pzxid.
 //     Children come and go with plain atomicAdd / atomicMax on these (a
 //     big-endian Stat word would need a CAS retry loop, and ~1000 parents
 //     shared by a million writes contend); every parent touched in a launch
@@ -163,7 +164,7 @@ ZK_DEV bool bytes_eq(const uint8_t* a, const uint8_t* b, int32_t n) {
 // reply's data length from it: ONE random line per lookup (rounds 2-4 read
 // the 16-byte {key, val} entry and then the node's 64-byte lookup line, a
 // second dependent random read).  Longer paths compare their tail in the
-// arena.  The node lookup lines (node_line) are no longer read.
+// arena.  (The per-node 64-byte lookup lines of round 4 are gone.)
 constexpr int HT_W = 8;                    // int64 words per entry
 constexpr int EN_PATH = 40;                // path bytes held in the entry
 
@@ -175,19 +176,6 @@ ZK_DEV int64_t* ht_val(const ZkTree& t, int64_t s) { return &t.ht[HT_W * s + 1];
 // the frames that carry them): the arena tail of a long path.
 ZK_DEV int64_t pw_pack(int64_t off, int32_t len) {
   return (off << 24) | (int64_t)(uint32_t)len;
-}
-
-// Node lookup line (64 bytes per node): path length, data length and the
-// path's first LN_PATH bytes.  Written for the node table's record; the
-// lookups use the hash entries' copy.
-constexpr int LN_BYTES = 64, LN_PATH = 56;
-
-ZK_DEV void line_set(const ZkTree& t, int64_t v, const uint8_t* p, int32_t n,
-                     int32_t dl) {
-  uint8_t* ln = t.node_line + v * LN_BYTES;
-  __builtin_memcpy(ln, &n, 4);
-  __builtin_memcpy(ln + 4, &dl, 4);
-  copy_bytes(ln + 8, p, n < LN_PATH ? n : LN_PATH);
 }
 
 // The entry's path / data length words (everything but key and val); plain
@@ -452,13 +440,26 @@ ZK_DEV void fill_stat(uint8_t* st, int64_t cz, int64_t mz, int64_t ct,
   st_be32(st + 56, nkids); st_be64(st + 60, pz);
 }
 
+// The parent counters (cversion << 32 | numChildren in one word, so a
+// child's create or delete moves both with one device-scope atomic: on the
+// multi-XCD part each is a trip to the coherence point).  numChildren never
+// goes negative, so a signed add of (dc << 32) + dk never borrows across.
+ZK_DEV int64_t cn_pack(int32_t cver, int32_t nchild) {
+  return (int64_t)((uint64_t)(uint32_t)cver << 32 | (uint32_t)nchild);
+}
+ZK_DEV int32_t cn_cver(int64_t x) { return (int32_t)((uint64_t)x >> 32); }
+ZK_DEV int32_t cn_nchild(int64_t x) { return (int32_t)(uint32_t)x; }
+ZK_DEV int64_t cn_add(const ZkTree& t, int64_t v, int32_t dc, int32_t dk) {
+  return (int64_t)atomicAdd((unsigned long long*)&t.cn[v],
+                            (unsigned long long)(((int64_t)dc << 32) + dk));
+}
+
 // ---- parent bookkeeping ----------------------------------------------------
 // Child added (dkids = 1) / removed (-1) under `par` by the txn `zx`;
 // `bump_cver` is false when a SEQUENTIAL create already took the cversion.
 ZK_DEV void parent_touch(const ZkTree& t, int64_t par, int32_t dkids,
                          bool bump_cver, int64_t zx) {
-  if (bump_cver) atomicAdd(&t.cver[par], 1);
-  atomicAdd(&t.nchild[par], dkids);
+  cn_add(t, par, bump_cver ? 1 : 0, dkids);
   atomicMax((unsigned long long*)&t.pzxid[par], (unsigned long long)zx);
 }
 
@@ -493,9 +494,7 @@ __global__ __launch_bounds__(TR_T) void tree_fill_k(ZkTree t, int64_t n0,
             nkids[v], v + 1);
   st_be32(slot + 68, 0);
   st_be32(slot + ZK_SLOT_LEN, dl > 0 ? dl : -1);
-  line_set(t, v, t.path_arena + t.node_path_off[v], t.node_path_len[v], dl);
-  t.cver[v] = nkids[v];
-  t.nchild[v] = nkids[v];
+  t.cn[v] = cn_pack(nkids[v], nkids[v]);
   t.pzxid[v] = v + 1;
   t.dirty[v] = 0;
 }
@@ -612,7 +611,9 @@ ZK_DEV int32_t do_create(const ZkTree& t, Lane& L, const uint8_t* data,
   // usual, successful create walks the chain once, not twice; what this
   // lane wrote to its own node v before is freed by the caller)
   const int32_t npl = pl + (seq ? 10 : 0);
-  const int32_t seqno = seq && par >= 0 ? atomicAdd(&t.cver[par], 1) : 0;
+  // a SEQUENTIAL name takes the parent's cversion, bumped in the same
+  // atomic as its child count (taken back if the create fails below)
+  const int32_t seqno = seq && par >= 0 ? cn_cver(cn_add(t, par, 1, 1)) : 0;
   uint8_t* pd = t.path_arena + t.node_path_off[v];
   copy_bytes(pd, path, pl);
   if (seq) put_seq10(pd + pl, seqno);
@@ -624,8 +625,7 @@ ZK_DEV int32_t do_create(const ZkTree& t, Lane& L, const uint8_t* data,
   copy_bytes(slot + ZK_SLOT_DATA, data, dl);
   t.node_path_len[v] = npl;
   s.data_len[v] = dl;
-  t.cver[v] = 0;
-  t.nchild[v] = 0;
+  t.cn[v] = 0;
   t.pzxid[v] = L.zx;
   t.node_parent[v] = par;
   t.node_pw[v] = pw_pack(pd - t.path_arena, npl);
@@ -635,9 +635,17 @@ ZK_DEV int32_t do_create(const ZkTree& t, Lane& L, const uint8_t* data,
   // launch sees everything.  A __threadfence here is an XCD-L2 writeback
   // per wave (MI355X_MICROARCH.md: ~3.5 us each) and cost milliseconds.
   const int64_t ins = tree_insert(t, v, pd, npl, dl);
-  if (ins == TREE_INSERT_TIMEOUT) return ERR_SYSTEM;
-  if (ins != v) return ERR_NODE_EXISTS;
-  if (par >= 0) parent_touch(t, par, 1, !seq, L.zx);
+  if (ins != v) {
+    if (seq && par >= 0) cn_add(t, par, 0, -1);   // the child was not made
+    return ins == TREE_INSERT_TIMEOUT ? ERR_SYSTEM : ERR_NODE_EXISTS;
+  }
+  if (par >= 0) {
+    if (seq) {
+      atomicMax((unsigned long long*)&t.pzxid[par], (unsigned long long)L.zx);
+    } else {
+      parent_touch(t, par, 1, true, L.zx);
+    }
+  }
   L.par = par;
   L.node = v;
   L.slot = s.slot_off[v];
@@ -826,8 +834,8 @@ __global__ __launch_bounds__(TR_T) void tree_serve_k(
         const Found f = tree_lookup(t, L.path, L.pl);
         const int64_t node = f.node, so = f.slot;
         if (node < 0) { L.err = ERR_NO_NODE; break; }
-        if (__hip_atomic_load(&t.nchild[node], __ATOMIC_RELAXED,
-                              __HIP_MEMORY_SCOPE_AGENT) > 0) {
+        if (cn_nchild(__hip_atomic_load(&t.cn[node], __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_AGENT)) > 0) {
           L.err = ERR_NOT_EMPTY;
           break;
         }
@@ -1188,10 +1196,10 @@ ZK_DEV void finish_body(const ZkTree& t, const int64_t* n_dev,
     const int64_t p = __hip_atomic_load(&t.dirty_list[k], __ATOMIC_RELAXED,
                                         __HIP_MEMORY_SCOPE_AGENT);
     uint8_t* slot = t.store.slab + t.store.slot_off[p];
-    st_be32(slot + 36, __hip_atomic_load(&t.cver[p], __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_AGENT));
-    st_be32(slot + 56, __hip_atomic_load(&t.nchild[p], __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_AGENT));
+    const int64_t cn = __hip_atomic_load(&t.cn[p], __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+    st_be32(slot + 36, cn_cver(cn));
+    st_be32(slot + 56, cn_nchild(cn));
     st_be64(slot + 60, __hip_atomic_load(&t.pzxid[p], __ATOMIC_RELAXED,
                                          __HIP_MEMORY_SCOPE_AGENT));
     t.dirty[p] = 0;

@@ -112,14 +112,14 @@ struct ZkTree {
   ZkNodeStore store;
   int64_t* free_list;          // ring of deleted node indices
   int64_t free_cap;
-  int32_t* cver;               // [cap] host-endian cversion
-  int32_t* nchild;             // [cap] host-endian numChildren
+  // [cap] cversion << 32 | numChildren, host-endian: a child's create or
+  // delete updates both with one atomic
+  int64_t* cn;
   int64_t* pzxid;              // [cap] host-endian pzxid
   int32_t* dirty;              // [cap] parent-on-dirty-list flag
   int64_t* dirty_list;         // [cap]
   int64_t* node_pw;            // [cap] path word: offset << 24 | length
   int32_t* node_path_cap;      // [cap] bytes of the node's path storage
-  uint8_t* node_line;          // [cap * 64] lookup line, see LN_* below
   // watch table (null wt_key: the tree keeps no watches), see wt_* below
   int64_t* wt_key;             // [wt_hmask + 1] path hash | 1, 0 = empty
   unsigned long long* wt_mask; // [2 * (wt_hmask + 1)] data / child masks
@@ -291,10 +291,10 @@ static_assert(sizeof(ZkRespBatch) == 10 * 8, "ZkRespBatch layout");
 static_assert(sizeof(ZkReplyOut) == 12 * 8, "ZkReplyOut layout");
 static_assert(sizeof(ZkReqOut) == 12 * 8, "ZkReqOut layout");
 static_assert(sizeof(ZkSessionTable) == 7 * 8, "ZkSessionTable layout");
-static_assert(sizeof(ZkTree) == 27 * 8, "ZkTree layout");
+static_assert(sizeof(ZkTree) == 25 * 8, "ZkTree layout");
 static_assert(offsetof(ZkTree, store) == 9 * 8, "ZkTree.store");
 static_assert(offsetof(ZkTree, free_list) == 14 * 8, "ZkTree.free_list");
-static_assert(offsetof(ZkTree, wt_hmask) == 26 * 8, "ZkTree.wt_hmask");
+static_assert(offsetof(ZkTree, wt_hmask) == 24 * 8, "ZkTree.wt_hmask");
 static_assert(offsetof(ZkRespBatch, slot) == 9 * 8, "ZkRespBatch.slot");
 static_assert(offsetof(ZkReplyOut, cap) == 11 * 8, "ZkReplyOut.cap");
 static_assert(offsetof(ZkReqOut, rel_zxid) == 10 * 8, "ZkReqOut.rel_zxid");

@@ -106,15 +106,12 @@ ZkNodeStore node_store(const std::vector<Tensor>& v, size_t at,
 }
 
 // [ht, node_path_off, node_path_len, node_parent, path_arena, counters,
-//  slab, slot_off, data_len, slot_cap, free_list, cver, nchild, pzxid,
-//  dirty, dirty_list, node_pw]; sizes give mask, caps
-// [ht, node_path_off, node_path_len, node_parent, path_arena, counters,
-//  slab, slot_off, data_len, slot_cap, free_list, cver, nchild, pzxid,
-//  dirty, dirty_list, node_pw, node_path_cap, node_line] + optionally
-//  [wt_key, wt_mask] (watches)
+//  slab, slot_off, data_len, slot_cap, free_list, cn, pzxid, dirty,
+//  dirty_list, node_pw, node_path_cap] + optionally [wt_key, wt_mask]
+//  (watches); sizes give mask, caps
 ZkTree tree(const std::vector<Tensor>& v) {
-  TORCH_CHECK(v.size() == 19 || v.size() == 21,
-              "zkmi: tree needs 19 tensors (21 with a watch table), got ",
+  TORCH_CHECK(v.size() == 17 || v.size() == 19,
+              "zkmi: tree needs 17 tensors (19 with a watch table), got ",
               v.size());
   const Tensor* r = &v[0];
   ZkTree t;
@@ -137,26 +134,22 @@ ZkTree tree(const std::vector<Tensor>& v) {
   t.slab_cap = v[6].numel();
   t.free_list = P<int64_t>(v[10], I64, 1, "tree.free_list", r);
   t.free_cap = v[10].numel();
-  t.cver = P<int32_t>(v[11], I32, cap, "tree.cver", r);
-  t.nchild = P<int32_t>(v[12], I32, cap, "tree.nchild", r);
-  t.pzxid = P<int64_t>(v[13], I64, cap, "tree.pzxid", r);
-  t.dirty = P<int32_t>(v[14], I32, cap, "tree.dirty", r);
-  t.dirty_list = P<int64_t>(v[15], I64, cap, "tree.dirty_list", r);
-  t.node_pw = P<int64_t>(v[16], I64, cap, "tree.node_pw", r);
-  t.node_path_cap = P<int32_t>(v[17], I32, cap, "tree.node_path_cap", r);
-  t.node_line = P<uint8_t>(v[18], U8, 64 * cap, "tree.node_line", r);
-  TORCH_CHECK((reinterpret_cast<uintptr_t>(t.node_line) & 63) == 0,
-              "zkmi: tree.node_line must be 64-byte aligned");
+  t.cn = P<int64_t>(v[11], I64, cap, "tree.cn", r);
+  t.pzxid = P<int64_t>(v[12], I64, cap, "tree.pzxid", r);
+  t.dirty = P<int32_t>(v[13], I32, cap, "tree.dirty", r);
+  t.dirty_list = P<int64_t>(v[14], I64, cap, "tree.dirty_list", r);
+  t.node_pw = P<int64_t>(v[15], I64, cap, "tree.node_pw", r);
+  t.node_path_cap = P<int32_t>(v[16], I32, cap, "tree.node_path_cap", r);
   t.wt_key = nullptr;
   t.wt_mask = nullptr;
   t.wt_hmask = 0;
-  if (v.size() == 21) {
-    const int64_t h = v[19].numel();
+  if (v.size() == 19) {
+    const int64_t h = v[17].numel();
     TORCH_CHECK(h > 0 && (h & (h - 1)) == 0,
                 "zkmi: tree.wt_key must hold a power of two of entries");
-    t.wt_key = P<int64_t>(v[19], I64, h, "tree.wt_key", r);
+    t.wt_key = P<int64_t>(v[17], I64, h, "tree.wt_key", r);
     t.wt_mask = reinterpret_cast<unsigned long long*>(
-        P<int64_t>(v[20], I64, 2 * h, "tree.wt_mask", r));
+        P<int64_t>(v[18], I64, 2 * h, "tree.wt_mask", r));
     t.wt_hmask = h - 1;
   }
   return t;

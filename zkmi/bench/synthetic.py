@@ -174,9 +174,6 @@ class GpuTree(object):
         # bytes of each node's path storage (the static paths are packed)
         self.node_path_cap = torch.zeros(cap, dtype=I32, device=dev)
         self.node_path_cap[:nst] = self.node_path_len[:nst]
-        # per-node lookup line: path and data length + the path's first 56
-        # bytes (csrc/kernels/tree.hip LN_*), written by tree_fill / create
-        self.node_line = torch.zeros(cap * 64, dtype=U8, device=dev)
         # path word (offset << 24 | length) the hash lookups verify against
         self.node_pw = torch.zeros(cap, dtype=I64, device=dev)
         self.node_pw[:nst] = torch.from_numpy(
@@ -225,8 +222,8 @@ class GpuTree(object):
         self.counters = torch.tensor(cnt, dtype=I64, device=dev)
         self.free_list = torch.empty(cap, dtype=I64, device=dev)
         # host-endian cversion / numChildren / pzxid shadows + dirty list
-        self.cver = torch.zeros(cap, dtype=I32, device=dev)
-        self.nchild = torch.zeros(cap, dtype=I32, device=dev)
+        # cversion << 32 | numChildren per node (one atomic per child write)
+        self.cn = torch.zeros(cap, dtype=I64, device=dev)
         self.pzxid = torch.zeros(cap, dtype=I64, device=dev)
         self.dirty = torch.zeros(cap, dtype=I32, device=dev)
         self.dirty_list = torch.empty(cap, dtype=I64, device=dev)
@@ -242,10 +239,9 @@ class GpuTree(object):
         self._tensors = [self.ht, self.node_path_off, self.node_path_len,
                          self.node_parent, self.path_arena, self.counters,
                          self.slab, self.slot_off, self.data_len,
-                         self.slot_cap, self.free_list, self.cver,
-                         self.nchild, self.pzxid, self.dirty,
-                         self.dirty_list, self.node_pw, self.node_path_cap,
-                         self.node_line]
+                         self.slot_cap, self.free_list, self.cn,
+                         self.pzxid, self.dirty, self.dirty_list,
+                         self.node_pw, self.node_path_cap]
         # watch table (watch_cap > 0): path-keyed one-shot watches of up to
         # 64 watcher slots (csrc/kernels/tree.hip wt_*); every serve of a
         # tree with one fires the watches its writes hit

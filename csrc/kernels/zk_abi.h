@@ -120,6 +120,7 @@ struct ZkTree {
   int64_t* dirty_list;         // [cap]
   int64_t* node_pw;            // [cap] path word: offset << 24 | length
   int32_t* node_path_cap;      // [cap] bytes of the node's path storage
+  int64_t* eph;                // [cap] host-endian ephemeralOwner shadow
   // watch table (null wt_key: the tree keeps no watches), see wt_* below
   int64_t* wt_key;             // [wt_hmask + 1] path hash | 1, 0 = empty
   unsigned long long* wt_mask; // [2 * (wt_hmask + 1)] data / child masks
@@ -291,10 +292,10 @@ static_assert(sizeof(ZkRespBatch) == 10 * 8, "ZkRespBatch layout");
 static_assert(sizeof(ZkReplyOut) == 12 * 8, "ZkReplyOut layout");
 static_assert(sizeof(ZkReqOut) == 12 * 8, "ZkReqOut layout");
 static_assert(sizeof(ZkSessionTable) == 7 * 8, "ZkSessionTable layout");
-static_assert(sizeof(ZkTree) == 25 * 8, "ZkTree layout");
+static_assert(sizeof(ZkTree) == 26 * 8, "ZkTree layout");
 static_assert(offsetof(ZkTree, store) == 9 * 8, "ZkTree.store");
 static_assert(offsetof(ZkTree, free_list) == 14 * 8, "ZkTree.free_list");
-static_assert(offsetof(ZkTree, wt_hmask) == 24 * 8, "ZkTree.wt_hmask");
+static_assert(offsetof(ZkTree, wt_hmask) == 25 * 8, "ZkTree.wt_hmask");
 static_assert(offsetof(ZkRespBatch, slot) == 9 * 8, "ZkRespBatch.slot");
 static_assert(offsetof(ZkReplyOut, cap) == 11 * 8, "ZkReplyOut.cap");
 static_assert(offsetof(ZkReqOut, rel_zxid) == 10 * 8, "ZkReqOut.rel_zxid");

@@ -107,11 +107,11 @@ ZkNodeStore node_store(const std::vector<Tensor>& v, size_t at,
 
 // [ht, node_path_off, node_path_len, node_parent, path_arena, counters,
 //  slab, slot_off, data_len, slot_cap, free_list, cn, pzxid, dirty,
-//  dirty_list, node_pw, node_path_cap] + optionally [wt_key, wt_mask]
+//  dirty_list, node_pw, node_path_cap, eph] + optionally [wt_key, wt_mask]
 //  (watches); sizes give mask, caps
 ZkTree tree(const std::vector<Tensor>& v) {
-  TORCH_CHECK(v.size() == 17 || v.size() == 19,
-              "zkmi: tree needs 17 tensors (19 with a watch table), got ",
+  TORCH_CHECK(v.size() == 18 || v.size() == 20,
+              "zkmi: tree needs 18 tensors (20 with a watch table), got ",
               v.size());
   const Tensor* r = &v[0];
   ZkTree t;
@@ -140,16 +140,17 @@ ZkTree tree(const std::vector<Tensor>& v) {
   t.dirty_list = P<int64_t>(v[14], I64, cap, "tree.dirty_list", r);
   t.node_pw = P<int64_t>(v[15], I64, cap, "tree.node_pw", r);
   t.node_path_cap = P<int32_t>(v[16], I32, cap, "tree.node_path_cap", r);
+  t.eph = P<int64_t>(v[17], I64, cap, "tree.eph", r);
   t.wt_key = nullptr;
   t.wt_mask = nullptr;
   t.wt_hmask = 0;
-  if (v.size() == 19) {
-    const int64_t h = v[17].numel();
+  if (v.size() == 20) {
+    const int64_t h = v[18].numel();
     TORCH_CHECK(h > 0 && (h & (h - 1)) == 0,
                 "zkmi: tree.wt_key must hold a power of two of entries");
-    t.wt_key = P<int64_t>(v[17], I64, h, "tree.wt_key", r);
+    t.wt_key = P<int64_t>(v[18], I64, h, "tree.wt_key", r);
     t.wt_mask = reinterpret_cast<unsigned long long*>(
-        P<int64_t>(v[18], I64, 2 * h, "tree.wt_mask", r));
+        P<int64_t>(v[19], I64, 2 * h, "tree.wt_mask", r));
     t.wt_hmask = h - 1;
   }
   return t;

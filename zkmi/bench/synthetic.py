@@ -224,6 +224,8 @@ class GpuTree(object):
         # host-endian cversion / numChildren / pzxid shadows + dirty list
         # cversion << 32 | numChildren per node (one atomic per child write)
         self.cn = torch.zeros(cap, dtype=I64, device=dev)
+        # ephemeralOwner per node, host-endian (session expiry scans it)
+        self.eph = torch.zeros(cap, dtype=I64, device=dev)
         self.pzxid = torch.zeros(cap, dtype=I64, device=dev)
         self.dirty = torch.zeros(cap, dtype=I32, device=dev)
         self.dirty_list = torch.empty(cap, dtype=I64, device=dev)
@@ -241,7 +243,7 @@ class GpuTree(object):
                          self.slab, self.slot_off, self.data_len,
                          self.slot_cap, self.free_list, self.cn,
                          self.pzxid, self.dirty, self.dirty_list,
-                         self.node_pw, self.node_path_cap]
+                         self.node_pw, self.node_path_cap, self.eph]
         # watch table (watch_cap > 0): path-keyed one-shot watches of up to
         # 64 watcher slots (csrc/kernels/tree.hip wt_*); every serve of a
         # tree with one fires the watches its writes hit

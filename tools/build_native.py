@@ -140,7 +140,8 @@ HOST_EXTS = {'_zkhost': 'zk_host_codec.cpp',     # Jute host codec
              '_zkloop': 'zk_loop.cpp',           # epoll event loop
              '_zkwatch': 'zk_watch.cpp',         # watch-event engine
              '_zkfsm': 'zk_fsm.cpp',             # FSM runtime
-             '_zkmach': 'zk_machines.cpp'}       # session / connection / client machines
+             # session / connection / client machines
+             '_zkmach': 'zk_machines.cpp'}
 
 
 FAST_SERVER = os.path.join(ROOT, 'zkmi', 'bin', 'zk_fastserver')

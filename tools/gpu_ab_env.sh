@@ -3,9 +3,10 @@
 # (default 3) so box drift hits every setting alike.
 #   AB_VAR=<name> AB_VALUES="1 0"     one variable over values, or
 #   AB_SETS="A=1,B=2 -"               whole settings ("-" = the defaults)
-# BENCH_ARGS is passed through (e.g. AB_VAR=ZKMI_FREE_COMPACT AB_VALUES="1 0"
-# BENCH_ARGS="--workload nest" for the free-ring compaction A/B).  Output: gpurun_out/ab_<tag>.log, one line
-# per run (setting, ms per step, ops/s).
+# BENCH_ARGS is passed through (e.g. AB_VAR=ZKMI_FREE_COMPACT
+# AB_VALUES="1 0" BENCH_ARGS="--workload nest" for the free-ring compaction
+# A/B).  Output: gpurun_out/ab_<tag>.log, one line per run (setting, ms per
+# step, sustained ms per step, ops/s).
 set -o pipefail
 mkdir -p gpurun_out
 if [ -n "$AB_SETS" ]; then

@@ -14,7 +14,8 @@ def main():
                 d = int(r['End_Timestamp']) - int(r['Start_Timestamp'])
             except (KeyError, ValueError):
                 continue
-            rows.append((d, int(r['Start_Timestamp']), r.get('Kernel_Name', '')[:90],
+            rows.append((d, int(r['Start_Timestamp']),
+                         r.get('Kernel_Name', '')[:90],
                          r.get('Correlation_Id', '')))
     if not rows:
         print('no rows')

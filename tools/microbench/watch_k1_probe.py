@@ -39,14 +39,17 @@ for s in range(a.steps):
         print('step %d %.2f ms %r window %d zxid %d' % (
             s, ms, st, pipe.nscan.window, int(tree.counters[1].item())),
             flush=True)
-        nb = int(pipe.nrx.item()) if hasattr(pipe.nrx, 'item') else int(pipe.nrx)
+        nb = int(pipe.nrx.item()) if hasattr(pipe.nrx, 'item') \
+            else int(pipe.nrx)
         buf = pipe.rx[:nb].cpu().numpy()
-        w = (buf[:-3].astype(np.uint32) << 24 | buf[1:-2].astype(np.uint32) << 16 |
-             buf[2:-1].astype(np.uint32) << 8 | buf[3:].astype(np.uint32))
+        u = buf.astype(np.uint32)
+        w = u[:-3] << 24 | u[1:-2] << 16 | u[2:-1] << 8 | u[3:]
         W = pipe.nscan.window
         pos = np.arange(len(w)) % 4096
-        node = ((w >= 16) & (w <= W - 4)) | ((pos < W) & (w >= 16) & (w <= 1 << 20))
-        per = np.add.reduceat(node.astype(np.int64), np.arange(0, len(w), 4096))
+        node = ((w >= 16) & (w <= W - 4)) | \
+            ((pos < W) & (w >= 16) & (w <= 1 << 20))
+        per = np.add.reduceat(node.astype(np.int64),
+                              np.arange(0, len(w), 4096))
         print('stream %d B, tiles %d, nodes per tile p50 %d p99 %d max %d, '
               'tiles over 512: %d' % (nb, len(per), np.median(per),
                                       np.percentile(per, 99), per.max(),

@@ -105,7 +105,6 @@ def main():
             mark(name)
             return r
         setattr(obj, meth, g)
-    from zkmi.ops import batch as B
     for sc, nm in ((pipe.server.scanner, 'req_scan'), (pipe.rscan, 'rep_scan'),
                    (pipe.nscan, 'note_scan')):
         wrap(sc, 'scan', nm)

@@ -1652,7 +1652,7 @@ class StormPipeline(object):
         acc[:1] += good
         return acc
 
-    # -- the replicated tree ----------------------------------------------------
+    # -- the replicated tree --------------------------------------------------
 
     def _stream_len(self, total, attr):
         """The byte length of a batch's encoded stream: the same every step

@@ -33,7 +33,8 @@ import os
 
 from .emitter import EventEmitter
 
-try:                                 # the native runtime (csrc/host/zk_fsm.cpp)
+# the native runtime (csrc/host/zk_fsm.cpp)
+try:
     from .. import _zkfsm
 except ImportError:                  # not built: PyCore
     _zkfsm = None

@@ -1161,8 +1161,11 @@ int zk_encode_responses3(const ZkRespBatch* r, const ZkNodeStore* s,
                                              bsum);
     ZK_LAUNCH_CHECK();
   }
-  const bool fused = nb <= zk::FUSED_SCAN_BLOCKS && zk::enc_fused();
-  if (!fused) {
+  // presized == 2: the block bases and *total are already in place
+  // (zk_tree_finish_scan scanned the serve's block sums)
+  const bool fused = presized != 2 && nb <= zk::FUSED_SCAN_BLOCKS &&
+                     zk::enc_fused();
+  if (!fused && presized != 2) {
     int rc = zk_scan_small_i64(bsum, bbase, nb, total, st);
     if (rc) return rc;
   }

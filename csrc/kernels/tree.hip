@@ -1228,6 +1228,35 @@ __global__ __launch_bounds__(NT) void tree_finish_k(ZkTree t,
   finish_body(t, n_dev, bump_zxid, publish);
 }
 
+// The between-batch finish and the reply encoder's block-sum scan in ONE
+// launch of two workgroups: they are independent one-workgroup jobs that
+// ran back to back on the connection's stream (tree_finish_k, then K13's
+// scan_one_block), each waiting for a CU behind the other connection's
+// kernels.  Workgroup 1 scans the serve's per-256-reply size sums (bsum,
+// nb of them) into the encoder's block bases and writes the stream total
+// (zk_encode_responses3 `prescanned`).
+template <int NT>
+__global__ __launch_bounds__(NT) void tree_finish_scan_k(
+    ZkTree t, const int64_t* n_dev, int64_t bump_zxid, int32_t publish,
+    const int64_t* __restrict__ bsum, int64_t nb, int64_t* __restrict__ bbase,
+    int64_t* __restrict__ total) {
+  if (blockIdx.x == 0) {
+    finish_body(t, n_dev, bump_zxid, publish);
+    return;
+  }
+  __shared__ int64_t sm[NT / 64 + 1];
+  int64_t carry = 0;
+  for (int64_t c0 = 0; c0 < nb; c0 += NT) {          // (uniform)
+    const int64_t i = c0 + threadIdx.x;
+    const int64_t v = i < nb ? bsum[i] : 0;
+    int64_t tot;
+    const int64_t p = carry + block_excl_scan(v, sm, &tot);
+    if (i < nb) bbase[i] = p;
+    carry += tot;
+  }
+  if (threadIdx.x == 0) *total = carry;
+}
+
 // Is this the serve launch's last workgroup to finish?  Tickets in groups
 // of 64 workgroups (tickets[1 + g]; the last of a group takes one of
 // tickets[0]), so no counter takes more than 64 atomics — one counter
@@ -1607,6 +1636,19 @@ int zk_tree_serve_frames(const ZkTree* t, const uint8_t* rx,
 int zk_tree_finish(const ZkTree* t, const int64_t* n_dev, int64_t bump,
                    int32_t publish, hipStream_t st) {
   return finish_launch(t, 0, n_dev, bump, st, publish);
+}
+
+// zk_tree_finish + the presized reply encode's block-sum scan (the serve's
+// r_bsum for ncap replies, in scan_ws[0, nb)) -> scan_ws[nb, 2 nb) and
+// *total, in one launch (tree_finish_scan_k).
+int zk_tree_finish_scan(const ZkTree* t, const int64_t* n_dev, int64_t bump,
+                        int32_t publish, int64_t ncap, int64_t* scan_ws,
+                        int64_t* total, hipStream_t st) {
+  const int64_t nb = ncap > 0 ? (ncap + 255) / 256 : 0;
+  zk::tree_finish_scan_k<256><<<2, 256, 0, st>>>(
+      *t, n_dev, bump, publish, scan_ws, nb, scan_ws + nb, total);
+  ZK_LAUNCH_CHECK();
+  return 0;
 }
 
 // Ordering workspace layout for up to ncap requests: the zeroed prefix

@@ -225,6 +225,8 @@ int zk_tree_serve_frames2(const ZkTree*, const uint8_t*, const int64_t*,
                           hipStream_t);
 int zk_tree_finish(const ZkTree*, const int64_t*, int64_t, int32_t,
                    hipStream_t);
+int zk_tree_finish_scan(const ZkTree*, const int64_t*, int64_t, int32_t,
+                        int64_t, int64_t*, int64_t*, hipStream_t);
 int zk_tree_serve_ordered(const ZkTree*, const uint8_t*, const ZkReqOut*,
                           const int64_t*, int64_t, int32_t*, int32_t*,
                           int32_t*, int64_t*, int64_t*, int64_t*, int32_t*,

@@ -333,7 +333,9 @@ void encode_responses(const std::vector<Tensor>& resp,
                       int64_t ncap, const Tensor& sizes, const Tensor& rec_off,
                       const Tensor& total, const Tensor& ws, const Tensor& out,
                       const Tensor& err, bool presized, bool terminate,
-                      int64_t stage) {
+                      int64_t stage, bool prescanned) {
+  TORCH_CHECK(!prescanned || presized,
+              "zkmi: encode_responses prescanned needs presized");
   need(store, 4, "node store");
   const Tensor* r = &resp[0];
   ZkRespBatch b = resp_batch(resp, slot, ncap, r);
@@ -346,7 +348,8 @@ void encode_responses(const std::vector<Tensor>& resp,
              P<int64_t>(total, I64, 1, "total", r),
              P<int64_t>(ws, I64, zk_scan_workspace(m), "ws", r),
              P<uint8_t>(out, U8, 1, "out", r), out.numel(),
-             P<int32_t>(err, I32, 1, "err", r), presized ? 1 : 0,
+             P<int32_t>(err, I32, 1, "err", r),
+             presized ? (prescanned ? 2 : 1) : 0,
              terminate ? 1 : 0, stage, cur_stream()),
          "encode_responses");
 }
@@ -533,6 +536,23 @@ void tree_free_compact(const std::vector<Tensor>& t, const Tensor& ws) {
                             "ws", &t[0]),
              cur_stream()),
          "tree_free_compact");
+}
+
+// tree_finish + the presized reply encode's block-sum scan in one launch
+// (ws: the response workspace the serve wrote its block sums into; total:
+// the encode's total, then encode_responses(prescanned=True)).
+void tree_finish_scan(const std::vector<Tensor>& t,
+                      const c10::optional<Tensor>& n_dev, int64_t bump,
+                      bool publish, int64_t ncap, const Tensor& ws,
+                      const Tensor& total) {
+  ZkTree s = tree(t);
+  const int64_t nb = (ncap + 255) / 256;
+  hip_ok(zk_tree_finish_scan(&s, Popt<int64_t>(n_dev, I64, 1, "count", &t[0]),
+                             bump, publish ? 1 : 0, ncap,
+                             P<int64_t>(ws, I64, 2 * nb, "ws", &t[0]),
+                             P<int64_t>(total, I64, 1, "total", &t[0]),
+                             cur_stream()),
+         "tree_finish_scan");
 }
 
 void tree_ht_reset(const std::vector<Tensor>& t) {
@@ -956,7 +976,8 @@ TORCH_LIBRARY(zkmi, m) {
   m.def("encode_responses(Tensor[] resp, Tensor? slot, Tensor[] store, "
         "Tensor count, int ncap, Tensor(a!) sizes, Tensor(b!) rec_off, "
         "Tensor(c!) total, Tensor(d!) ws, Tensor(e!) out, Tensor(f!) err, "
-        "bool presized, bool terminate, int stage=0) -> ()",
+        "bool presized, bool terminate, int stage=0, "
+        "bool prescanned=False) -> ()",
         &encode_responses);
   m.def("frame_scan_workspace(int n) -> int", &frame_scan_workspace);
   m.def("frame_scan(Tensor buf, Tensor? n, int n_cap, int max_packet, "
@@ -992,6 +1013,9 @@ TORCH_LIBRARY(zkmi, m) {
         "int now_ms) -> ()", &tree_fill);
   m.def("tree_build(Tensor(a!)[] tree, int n0, int n) -> ()", &tree_build);
   m.def("tree_ht_reset(Tensor(a!)[] tree) -> ()", &tree_ht_reset);
+  m.def("tree_finish_scan(Tensor(a!)[] tree, Tensor? count, int bump, "
+        "bool publish, int ncap, Tensor(b!) ws, Tensor(c!) total) -> ()",
+        &tree_finish_scan);
   m.def("tree_free_workspace(int cap) -> int", &tree_free_workspace);
   m.def("tree_free_compact(Tensor(a!)[] tree, Tensor(b!) ws) -> ()",
         &tree_free_compact);

@@ -60,6 +60,9 @@ _GET_STAGE = int(os.environ.get('ZKMI_GET_STAGE', '0'))
 # ZKMI_FREE_COMPACT=0: no free-ring compaction after write batches (trees
 # built with compact_free=True; GpuTree.free_compact)
 _FREE_COMPACT = os.environ.get('ZKMI_FREE_COMPACT', '1') == '1'
+# ZKMI_FINISH_SCAN=0: the tree finish and the reply encode's block-sum scan
+# as two launches again (tree_finish_scan_k runs them as one)
+_FINISH_SCAN = os.environ.get('ZKMI_FINISH_SCAN', '1') == '1'
 # the storm rebuilds its hash index when the entries claimed since the last
 # rebuild (live + tombstones of never-reused SEQUENTIAL names) would pass
 # this share of the table
@@ -381,6 +384,7 @@ class GpuServer(object):
         self.scanner = B.FrameScanner(cap_frames, dev, window=window)
         self.ows = None                   # ordered-serve workspace (lazy)
         self.enc_stage = 0                # K13 LDS per workgroup (0: default)
+        self.total_err = B._total_err(dev)  # the reply encode's scalars
         # the serve launch's sign-off counters (its last workgroup does the
         # tree's finish: no separate launch); this server's own, zero
         self.tickets = torch.zeros(_lib.lib().serve_tickets(cap_frames),
@@ -508,6 +512,7 @@ class GpuServer(object):
         out = [r.opcode, r.xid, r.err, r.node, r.zxid, r.path_off,
                r.path_len, r.slot, self.presized[0], self.presized[1]]
         now = int(time.time() * 1000)
+        fuse = False
         if ordered:
             if self.ows is None:
                 self.ows = torch.empty(
@@ -519,12 +524,18 @@ class GpuServer(object):
                                  wslot, self.fired if self.tree.watch
                                  is not None else None)
         else:
+            fuse = _FINISH_SCAN and side is None and not _SERVE_TICKETS
             L.tree_serve_frames(self.tree.tensors, rx, ft.off, ft.length,
                                 ft.count, self.cap_frames, out, session, now,
                                 wslot, self.fired if self.tree.watch
                                 is not None else None,
                                 self.tickets if _SERVE_TICKETS else None,
-                                side is None)
+                                side is None and not fuse)
+            if fuse:
+                # the finish and K13's block-sum scan: one launch
+                L.tree_finish_scan(self.tree.tensors, ft.count, 0, True,
+                                   self.cap_frames, self.presized[1],
+                                   self.total_err[0])
             if side is not None:
                 side.wait_stream(torch.cuda.current_stream(self.tree.device))
                 with torch.cuda.stream(side):
@@ -533,7 +544,8 @@ class GpuServer(object):
         out, rec_off, total, err = B.encode_responses(
             r, self.tree.store, self.out.numel(), out=self.out,
             presized=self.presized, terminate=terminate,
-            stage=self.enc_stage)
+            stage=self.enc_stage, total_err=self.total_err,
+            prescanned=fuse)
         if self.tree.compact_free:
             self.tree.free_compact()
         self.last_rec_off = rec_off         # reply frame starts (R2 splits)

@@ -676,14 +676,18 @@ def response_workspace(cap, device):
 
 
 def encode_responses(resp, store, out_cap, out=None, stream=None,
-                     presized=None, terminate=False, stage=0):
+                     presized=None, terminate=False, stage=0,
+                     total_err=None, prescanned=False):
     """K13: server-mode reply encode -> (bytes, rec_off, total, err).
     ``store``: the node store's tensors [slab, slot_off, data_len,
     slot_cap] (:attr:`zkmi.bench.synthetic.GpuTree.store`).
     ``presized``: the (sizes, workspace) pair of :func:`response_workspace`
     already filled by the producer; the sizes pass is then skipped.
     ``stage``: LDS bytes per workgroup (0: the encoder's default; uniform
-    GET_DATA replies need only 8 KiB, more workgroups then fit a CU)."""
+    GET_DATA replies need only 8 KiB, more workgroups then fit a CU).
+    ``total_err``: the (total, err) pair to write (default: new ones);
+    ``prescanned``: the presized workspace's block bases and ``total`` were
+    already computed (the tree's finish_scan launch)."""
     L = _lib.lib()
     cap = resp.opcode.numel()
     dev = resp.opcode.device
@@ -693,14 +697,14 @@ def encode_responses(resp, store, out_cap, out=None, stream=None,
         sizes = torch.empty(cap, dtype=I64, device=dev)
         ws = torch.empty(L.scan_workspace(cap), dtype=I64, device=dev)
     rec_off = torch.empty(cap, dtype=I64, device=dev)
-    total, err = _total_err(dev)
+    total, err = total_err if total_err is not None else _total_err(dev)
     if out is None:
         out = torch.empty(out_cap, dtype=U8, device=dev)
     with _on(stream):
         L.encode_responses(resp.tensors(), resp.slot, list(store), resp.count,
                            cap, sizes, rec_off, total, ws, out, err,
                            presized is not None, bool(terminate),
-                           int(stage))
+                           int(stage), bool(prescanned))
     return out, rec_off, total, err
 
 

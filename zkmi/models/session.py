@@ -13,6 +13,7 @@ checked by one lazily re-armed timer, instead of a ``clearTimeout`` +
 SURVEY §7.1 "Expiry is a deadline, not a timer per packet").
 """
 
+import os
 import random
 import re
 import threading
@@ -25,13 +26,31 @@ try:
     from .. import _zkwatch
 except ImportError:                      # not built: the Python FSMs
     _zkwatch = None
-try:                                     # the native machines
-    from .. import _zkmach
-except ImportError:
-    _zkmach = None
+
 from ..runtime import fsm as _fsm
 from ..runtime.fsm import FSM
 from ..utils.metrics import METRIC_ZK_NOTIFICATION_COUNTER
+
+
+def _load_machines():
+    """The native machines (csrc/host/zk_machines.cpp): the in-tree
+    extension, or the one at ``ZKMI_MACHINES_PATH`` (the sanitizer build,
+    tools/sanitize_host.sh); None when not built (the Python FSMs)."""
+    path = os.environ.get('ZKMI_MACHINES_PATH')
+    if path:
+        import importlib.util
+        spec = importlib.util.spec_from_file_location('_zkmach', path)
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+        return mod
+    try:
+        from .. import _zkmach as mod
+    except ImportError:
+        return None
+    return mod
+
+
+_zkmach = _load_machines()
 
 
 class ExpiryTimer(EventEmitter):

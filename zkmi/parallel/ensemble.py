@@ -569,6 +569,15 @@ class EnsembleWorkload(object):
             mine = cp[self.rank::self.world]
             if mine:
                 res = self._bulk(self.client.bulk_set, mine, data)
+                t = getattr(res, 'phases', None) or {}
+                if t.get('submit') and 'finished' in t:
+                    ph = self.phase_ms
+                    ph['wb_encode'] = ph.get('wb_encode', 0.0) + \
+                        (t['encoded'] - t['submit']) * 1e3
+                    ph['wb_wire'] = ph.get('wb_wire', 0.0) + \
+                        (t['captured'] - t['encoded']) * 1e3
+                    ph['wb_finish'] = ph.get('wb_finish', 0.0) + \
+                        (t['finished'] - t['captured']) * 1e3
                 bad = [e for e in res.errors() if e != 'OK']
                 if bad:
                     raise RuntimeError('set failed: %r' % bad[:3])

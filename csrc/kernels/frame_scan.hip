@@ -2978,6 +2978,16 @@ constexpr int32_t FS_LONG = 2;
 // it when the window is below the stream's largest frame)
 constexpr int32_t FS_WIN_LONG = 1 << 16;
 
+static int fs_tpb() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("ZKMI_FS_TPB");
+    const int x = e ? atoi(e) : 4;
+    v = (x == 1 || x == 2) ? x : 4;
+  }
+  return v;
+}
+
 static int fs_window(int32_t window) {
   window &= FS_WIN_LONG - 1;
   return window <= 256 ? 256 : window <= 512 ? 512
@@ -3095,8 +3105,11 @@ int zk_frame_scan6(const uint8_t* buf, const int64_t* n_dev, int64_t n_cap,
           hipSuccess)
     return -4;
   int64_t* dbg = fs_dbg_buf(tiles);
-  // tiles (waves) per block: two 12 KiB slices, 6 blocks a CU
-  constexpr int tpb = 2;
+  // tiles (waves) per block: four 12 KiB slices, 3 blocks a CU (as many
+  // waves as two-slice blocks, half the workgroups to dispatch: GET 0.585
+  // -> 0.581 ms, mix and watch -0.7 %, profiles/r5_fs_tpb_ab.log;
+  // ZKMI_FS_TPB = 1 / 2 / 4 for A/B runs)
+  const int tpb = fs_tpb();
   // tiles a wave: groups (the map once, the chain walked on) for streams
   // of large frames within a small window; tests of the link repair and
   // long-frame streams take single tiles

@@ -60,6 +60,7 @@ def main():
     a = ap.parse_args()
     import gc
     gcs = []            # (step, generation, ms) of every collection
+    times = []          # (filled by the step loop below)
 
     def on_gc(phase, info, box={}):
         if phase == 'start':
@@ -110,7 +111,7 @@ def main():
         wrap(sc, 'scan', nm)
     wrap(pipe.server, 'serve', 'serve')
     wrap(pipe.fan, 'gather_slots', 'gather')
-    times = []
+    del times[:]
     prev_seg = (0, 0, 0)
     if a.gc == 'off':
         gc.disable()

@@ -216,7 +216,10 @@ class GpuTree(object):
         # read-mostly tree's table under half full; a write-heavy one
         # (SEQUENTIAL names never reused) fills with tombstones between
         # rebuilds, and a wider table rebuilds less often
-        hcap = _next_pow2(hash_factor * cap)
+        # (capped at 2^28 entries, 16 GB, unless 2 a slot needs more: the
+        # storm's replicated tree at 8 ranks holds ~25M node slots)
+        hcap = max(min(_next_pow2(hash_factor * cap), 1 << 28),
+                   _next_pow2(2 * cap))
         # 64-byte entries, empty = all zero bytes (csrc/kernels/tree.hip)
         self.ht = torch.zeros(_lib.HT_WORDS * hcap, dtype=I64, device=dev)
         cnt = [0] * _lib.TC_N

@@ -2982,8 +2982,8 @@ static int fs_tpb() {
   static int v = -1;
   if (v < 0) {
     const char* e = getenv("ZKMI_FS_TPB");
-    const int x = e ? atoi(e) : 2;
-    v = (x == 1 || x == 4) ? x : 2;
+    const int x = e ? atoi(e) : 4;
+    v = (x == 1 || x == 2) ? x : 4;
   }
   return v;
 }
@@ -3105,11 +3105,13 @@ int zk_frame_scan6(const uint8_t* buf, const int64_t* n_dev, int64_t n_cap,
           hipSuccess)
     return -4;
   int64_t* dbg = fs_dbg_buf(tiles);
-  // tiles (waves) per block: two 12 KiB slices, 6 blocks a CU.  Four
-  // slices (ZKMI_FS_TPB=4) measured 0.5-0.8 % faster (profiles/
-  // r5_fs_tpb_ab.log) but its first watch-sustained run had one 23 ms step
-  // (step 90, tests/test_watch_sustained.py) that two-slice blocks never
-  // showed: kept at 2 until that is understood.
+  // tiles (waves) per block: four 12 KiB slices, 3 blocks a CU (as many
+  // waves as two-slice blocks, half the workgroups to dispatch: GET 0.585
+  // -> 0.581 ms, mix and watch -0.7 %, profiles/r5_fs_tpb_ab.log).  (One
+  // 23 ms watch step seen once in a full-suite process was a host pause
+  // between the test's event records — the collector — not K1: six full
+  // and isolated runs since, either width, show none.)  ZKMI_FS_TPB = 1 /
+  // 2 / 4 for A/B runs.
   const int tpb = fs_tpb();
   // tiles a wave: groups (the map once, the chain walked on) for streams
   // of large frames within a small window; tests of the link repair and

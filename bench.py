@@ -471,7 +471,7 @@ def main():
                          'cversion / child-count atomics)')
     ap.add_argument('--hash-factor', type=int, default=0,
                     help='hash entries per node slot, rounded up to a power '
-                    'of two (0: 32 for the storm, 16 for mix / chain / nest, '
+                    'of two (0: 32 for storm / mix, 16 for chain / nest, '
                     '2 otherwise; profiles/r5_storm_hash_factor_ab.log)')
     ap.add_argument('--force-route', action='store_true',
                     help='get, N = 1: run the multi-rank sharded step over a '
@@ -722,8 +722,8 @@ def run_rank(a):
                          seed=0 if a.workload == 'storm' else rank,
                          spare=spare + 0.05, scratch=scratch,
                          hash_factor=a.hash_factor or (
-                             32 if a.workload == 'storm' else
-                             16 if a.workload in ('mix', 'chain', 'nest')
+                             32 if a.workload in ('storm', 'mix') else
+                             16 if a.workload in ('chain', 'nest')
                              else 2),
                          compact_free=a.workload in ('mix', 'nest'))
         if a.workload == 'chain':

@@ -2839,19 +2839,25 @@ __global__ __launch_bounds__(256) void fs_rows(
   const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int64_t t = (int64_t)blockIdx.x * 4 + wv;
   const int64_t n = stream_len(n_dev, n_cap);
+  if (t == 0) {
+    // fs_link's minima and broken-link count, for the next scan; and its
+    // barrier words (the big repair): every fs_link workgroup has ended
+    // (stream order), so a late one of an abandoned barrier can no longer
+    // leave an arrival or the abort flag to the next scan
+    if (lane == 0) {
+      lbw_tail[LW_MINS] = 0;
+      lbw_tail[LW_MINS + 1] = 0;
+      lbw_tail[LW_NOSPEC] = 0;
+      lbw_tail[LW_GRID + FL_NB] = 0;
+    }
+    if (lane < LW_END - LW_BIG) lbw_tail[LW_BIG + lane] = 0;
+  }
   if (t * FT_S >= n) return;
   // the scan is over for this tile: clear its candidate flags, so the next
   // scan of this workspace needs no memset (zk_frame_scan4 clean=1)
   if (lane == 0) {
     lbw[2 * t] = 0;
     lbw[2 * t + 1] = 0;
-  }
-  if (t == 0 && lane == 0) {
-    // fs_link's minima and broken-link count, for the next scan
-    lbw_tail[LW_MINS] = 0;
-    lbw_tail[LW_MINS + 1] = 0;
-    lbw_tail[LW_NOSPEC] = 0;
-    lbw_tail[LW_GRID + FL_NB] = 0;
   }
   if (t > *lastk) return;
   const int64_t b = bsum[t / FK_T] + base[t];
@@ -3051,31 +3057,10 @@ int64_t zk_frame_scan_workspace(int64_t n) {
 // below the stream's largest frame: fs_tile's frontier passes); tests of
 // the link repair: bit 0 no speculated tile entries; bits 8..23 P > 0:
 // every P-th tile (t % P == 1) takes a garbage entry.
-// link_st (may be null or st): fs_link runs there, forked after fs_tile and
-// joined before fs_rows through two events — a high-priority stream puts
-// its 16 workgroups ahead of another connection's waiting workgroups (they
-// waited ~20 us for CUs behind them in the overlapped GET step).  Event
-// record / wait pairs are issued back to back, so one pair of events
-// serves every scan of a thread (and a graph capture records the edges).
-int zk_frame_scan6(const uint8_t* buf, const int64_t* n_dev, int64_t n_cap,
-                   int64_t maxp, uint8_t* ws, int64_t ws_bytes, int64_t* foff,
-                   int32_t* flen, int64_t cap, int64_t* result, int32_t window,
-                   int32_t clean, int32_t flags, hipStream_t st,
-                   hipStream_t link_st);
-
 int zk_frame_scan5(const uint8_t* buf, const int64_t* n_dev, int64_t n_cap,
                    int64_t maxp, uint8_t* ws, int64_t ws_bytes, int64_t* foff,
                    int32_t* flen, int64_t cap, int64_t* result, int32_t window,
                    int32_t clean, int32_t flags, hipStream_t st) {
-  return zk_frame_scan6(buf, n_dev, n_cap, maxp, ws, ws_bytes, foff, flen,
-                        cap, result, window, clean, flags, st, nullptr);
-}
-
-int zk_frame_scan6(const uint8_t* buf, const int64_t* n_dev, int64_t n_cap,
-                   int64_t maxp, uint8_t* ws, int64_t ws_bytes, int64_t* foff,
-                   int32_t* flen, int64_t cap, int64_t* result, int32_t window,
-                   int32_t clean, int32_t flags, hipStream_t st,
-                   hipStream_t link_st) {
   using namespace zk;
   const int W = fs_window(window);
   if (window & FS_WIN_LONG) flags |= FS_LONG;
@@ -3159,27 +3144,12 @@ int zk_frame_scan6(const uint8_t* buf, const int64_t* n_dev, int64_t n_cap,
 #undef ZK_FS_TILE
 #undef ZK_FS_GROUP
   ZK_LAUNCH_CHECK();
-  hipStream_t lst = st;
-  static thread_local hipEvent_t ev[2] = {nullptr, nullptr};
-  if (link_st != nullptr && link_st != st) {
-    if (ev[0] == nullptr &&
-        (hipEventCreateWithFlags(&ev[0], hipEventDisableTiming) != hipSuccess ||
-         hipEventCreateWithFlags(&ev[1], hipEventDisableTiming) != hipSuccess))
-      return -5;
-    if (hipEventRecord(ev[0], st) != hipSuccess ||
-        hipStreamWaitEvent(link_st, ev[0], 0) != hipSuccess)
-      return -5;
-    lst = link_st;
-  }
-  fs_link<<<fl_blocks(), FL_T, 0, lst>>>(buf, n_dev, n_cap, maxp, sx, list, rcnt,
+  fs_link<<<fl_blocks(), FL_T, 0, st>>>(buf, n_dev, n_cap, maxp, sx, list, rcnt,
                                  pre, rent, rexit, rmeta, base, cap, result,
                                  lbw + 2 * tiles, blist, bsum, mins, lastk,
                                  grid, lbw, cx, dbg ? dbg + 8 * tiles : nullptr,
                                  fl_local_min(), fl_flags());
   ZK_LAUNCH_CHECK();
-  if (lst != st && (hipEventRecord(ev[1], lst) != hipSuccess ||
-                    hipStreamWaitEvent(st, ev[1], 0) != hipSuccess))
-    return -5;
   fs_rows<<<(unsigned)((tiles + 3) / 4), 256, 0, st>>>(
       buf, n_dev, n_cap, list, pre, rmeta, rent, rexit, base, bsum, lastk,
       foff, flen, cap, lbw, lbw + 2 * tiles);

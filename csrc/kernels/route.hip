@@ -35,7 +35,8 @@ ZK_DEV uint32_t fnv_word(uint32_t h, uint32_t w, int nb) {
 }
 
 // FNV-1a 32 over the path bytes.  A path of up to 48 bytes (the usual) is
-// loaded first, three 16-byte loads issued together (unaligned mode), then
+// loaded first, its whole 16-byte chunks issued together (unaligned mode)
+// and the last partial one in 8 / 4 / 2 / 1-byte pieces, then
 // hashed from registers: one memory round trip a request (a dword a step
 // was one dependent load per 4 bytes, 49 us per 1M-request route).
 ZK_DEV uint32_t path_fnv1a(const uint8_t* p, int32_t n) {
@@ -43,8 +44,22 @@ ZK_DEV uint32_t path_fnv1a(const uint8_t* p, int32_t n) {
   if (n <= 48) {
     uint4 q[3];
 #pragma unroll
-    for (int j = 0; j < 3; ++j)
-      if (16 * j < n) __builtin_memcpy(&q[j], p + 16 * j, 16);
+    for (int j = 0; j < 3; ++j) {
+      const int32_t o = 16 * j, left = n - o;
+      if (left >= 16) {
+        __builtin_memcpy(&q[j], p + o, 16);
+      } else if (left > 0) {
+        // the path's last partial chunk, read no further than its end (the
+        // last path of an arena can end at its allocation's end)
+        uint8_t* d = reinterpret_cast<uint8_t*>(&q[j]);
+        q[j] = uint4{0, 0, 0, 0};
+        int32_t k = 0;
+        if (left - k >= 8) { __builtin_memcpy(d + k, p + o + k, 8); k += 8; }
+        if (left - k >= 4) { __builtin_memcpy(d + k, p + o + k, 4); k += 4; }
+        if (left - k >= 2) { __builtin_memcpy(d + k, p + o + k, 2); k += 2; }
+        if (left - k >= 1) d[k] = p[o + k];
+      }
+    }
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
       const uint32_t w[4] = {q[j].x, q[j].y, q[j].z, q[j].w};

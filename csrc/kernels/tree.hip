@@ -75,10 +75,12 @@ ZK_DEV int lane_id() {
 
 // One ticket per thread with `want`: returns base + rank, or -1.  Ranks come
 // from ballot/mbcnt within a wave and an LDS prefix over the block's waves;
-// ONE atomic per 256-thread block (a single word sustains only ~88
+// ONE atomic per block of NT threads (a single word sustains only ~88
 // returning atomics/us, MI355X_MICROARCH.md "dequeue").  Every thread of the
 // block must call it.
+template <int NT = TR_T>
 ZK_DEV int64_t block_ticket(int64_t* ctr, bool want) {
+  constexpr int TR_T = NT;
   __shared__ int64_t part[TR_T / 64 + 1];
   const int w = threadIdx.x >> 6;
   const uint64_t m = __ballot(want);
@@ -244,6 +246,26 @@ ZK_DEV int64_t val_pack(int64_t v, int64_t slot) {
   return ((int64_t)(((uint64_t)slot >> 4) << 32) | v) + 1;
 }
 ZK_DEV int64_t val_node(int64_t x) { return (x - 1) & 0xFFFFFFFFll; }
+// Order this thread's earlier global accesses before its later ones
+// without a cache writeback or invalidate: a workgroup-scope fence is a
+// wait for the outstanding accesses (the agent-scope atomics around it are
+// served at L2, where the order then holds for other CUs too).  An
+// agent-scope release / acquire writes back / invalidates caches, ~us each
+// (MI355X_MICROARCH.md): in round 6's first expiry with them, 3.9 ms.
+ZK_DEV void order_wait() {
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+}
+
+// Tombstones: any val <= -2.  -2 is the plain one (DELETE, an insert's
+// claim); a session expiry tags its own with its txn's zxid (ht_shift
+// tells the holes of the launch it runs in from older tombstones).
+// -1: an entry being moved (ht_shift).
+constexpr int64_t VAL_TOMB = -2;
+constexpr int64_t VAL_MOVING = -1;
+ZK_DEV bool val_tomb(int64_t x) { return x <= VAL_TOMB; }
+ZK_DEV int64_t tomb_tag(int64_t zx) {
+  return VAL_TOMB - 1 - (zx & 0x3FFFFFFFFFFFll);
+}
 ZK_DEV int64_t val_slot(int64_t x) {
   return (int64_t)((uint64_t)(x - 1) >> 32) << 4;
 }
@@ -288,12 +310,48 @@ ZK_DEV int64_t tree_find(const ZkTree& t, const uint8_t* p, int32_t n) {
 // concurrent claimer of the same key never published its value (the caller
 // answers SYSTEMERROR rather than probing on and indexing the path twice).
 constexpr int64_t TREE_INSERT_TIMEOUT = -4;
+// REUSE: the caller knows no other request of the launch inserts this path
+// (a SEQUENTIAL name numbered by zk_tree_seq_order: unique in its batch and
+// above every number its parent gave before).  The probe still walks to the
+// first empty slot (an existing node of that name answers NODE_EXISTS), but
+// then the first tombstone passed on the way — of any key — is taken
+// instead: entries of dead names are recycled by the next batch's names.
+template <bool REUSE = false>
 ZK_DEV int64_t tree_insert(const ZkTree& t, int64_t v, const uint8_t* p,
                            int32_t n, int32_t dl) {
   const int64_t key = (int64_t)(path_hash(p, n) | 1ull);
   const int64_t pv = val_pack(v, t.store.slot_off[v]);
   int64_t s = key & t.mask;
+  int64_t tomb = -1, tv = 0;
   for (int64_t probe = 0; probe <= t.mask; ++probe) {
+    if (REUSE) {
+      int64_t k = __hip_atomic_load(ht_key(t, s), __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_AGENT);
+      if (k != 0 && k != key) {
+        if (tomb < 0) {
+          tv = __hip_atomic_load(ht_val(t, s), __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+          if (val_tomb(tv)) tomb = s;
+        }
+        s = (s + 1) & t.mask;
+        continue;
+      }
+      if (k == 0 && tomb >= 0) {
+        // the name is absent: take the tombstone (val -2 -> 0 claims it;
+        // a lookup in between sees a key with val 0 and probes on)
+        if (atomicCAS((unsigned long long*)ht_val(t, tomb),
+                      (unsigned long long)tv, 0ull) ==
+            (unsigned long long)tv) {
+          ent_fill(t, tomb, p, n, dl);
+          __hip_atomic_store(ht_key(t, tomb), key, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(ht_val(t, tomb), pv, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+          return v;
+        }
+        tomb = -1;                     // taken by another name: the empty
+      }
+    }
     // a plain load first: an occupied slot of another key (the usual probe
     // past a tombstone or a collision) costs a load, not an L2 atomic on
     // another line each (keys only ever go 0 -> key within a launch, so a
@@ -322,9 +380,9 @@ ZK_DEV int64_t tree_insert(const ZkTree& t, int64_t v, const uint8_t* p,
       }
       // a tombstone of the same key: claim it (0 while its words are
       // rewritten), then publish
-      if (w == -2 &&
-          atomicCAS((unsigned long long*)ht_val(t, s), (unsigned long long)-2,
-                    0ull) == (unsigned long long)-2) {
+      if (val_tomb(w) &&
+          atomicCAS((unsigned long long*)ht_val(t, s), (unsigned long long)w,
+                    0ull) == (unsigned long long)w) {
         ent_fill(t, s, p, n, dl);
         __hip_atomic_store(ht_val(t, s), pv, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
@@ -336,27 +394,164 @@ ZK_DEV int64_t tree_insert(const ZkTree& t, int64_t v, const uint8_t* p,
   return -1;
 }
 
-// Tombstone node `v`'s hash entry.  Returns true for exactly one caller when
-// several erase the same node concurrently (the CAS winner owns the free).
-ZK_DEV bool tree_erase(const ZkTree& t, int64_t v, const uint8_t* p,
-                       int32_t n) {
+// Tombstone node `v`'s hash entry.  Returns its slot for exactly one caller
+// when several erase the same node concurrently (the CAS winner owns the
+// free), else -1.
+ZK_DEV int64_t tree_erase_slot(const ZkTree& t, int64_t v, const uint8_t* p,
+                               int32_t n, int64_t tag = VAL_TOMB) {
   const int64_t key = (int64_t)(path_hash(p, n) | 1ull);
   int64_t s = key & t.mask;
   for (int64_t probe = 0; probe <= t.mask; ++probe) {
-    const int64_t k = *ht_key(t, s);
-    if (k == 0) return false;
+    const int64_t k = __hip_atomic_load(ht_key(t, s), __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_AGENT);
+    if (k == 0) return -1;
     if (k == key) {
       const int64_t cur = __hip_atomic_load(ht_val(t, s), __ATOMIC_RELAXED,
                                             __HIP_MEMORY_SCOPE_AGENT);
       if (cur > 0 && val_node(cur) == v &&
           atomicCAS((unsigned long long*)ht_val(t, s),
                     (unsigned long long)cur,
-                    (unsigned long long)-2) == (unsigned long long)cur)
-        return true;
+                    (unsigned long long)tag) == (unsigned long long)cur)
+        return s;
     }
     s = (s + 1) & t.mask;
   }
-  return false;
+  return -1;
+}
+
+ZK_DEV bool tree_erase(const ZkTree& t, int64_t v, const uint8_t* p,
+                       int32_t n) {
+  return tree_erase_slot(t, v, p, n) >= 0;
+}
+
+// Tombstone reclaim, in a launch where nothing INSERTS (session expiry): a
+// tombstone whose next slot is empty lies on no probe chain that reaches a
+// live entry (linear probing: an entry's chain from its home slot is
+// contiguous non-empty slots), so it can be emptied, and then so can the
+// tombstones before it.  Concurrent erasers stay correct: a slot before a
+// live entry of its chain never has an empty successor, and the only
+// writer of a live entry's val is its own eraser.  Emptiness only grows in
+// such a launch, so racing reclaims agree; a missed one is just a tombstone
+// left for later.  Without it the storm's never-reused SEQUENTIAL names
+// left 1M tombstones a step and the index was rebuilt every few hundred
+// steps (round 5: 1.29 ms timed, 1.40 ms sustained).
+ZK_DEV int64_t ht_reclaim(const ZkTree& t, int64_t s);
+
+// Backward shift from the hole s (a tombstone this thread just made), in a
+// launch where nothing inserts and the only erasers are those of `session`
+// (session expiry): the first live entry after s whose probe chain covers s
+// moves into it, its old slot becomes the hole, and so on; the last hole is
+// then reclaimed.  Without it, a tombstone right before a live entry (a
+// static node, another session's) could only go when an insert passed it,
+// and at ~2/3 of the expired names the index filled up anyway (40 create /
+// expire rounds: 0 -> 21 % of a 32K-entry table, still growing).  Entries
+// of `session` are never moved (their erasers may be probing for them);
+// every other live entry has no eraser in the launch, and its val is
+// claimed (-3: no lookup matches it) while it moves, so one thread moves it
+// and it is found at one slot or the other by any later launch.
+ZK_DEV void ht_shift(const ZkTree& t, int64_t s, int64_t session,
+                     int64_t tag) {
+  for (int moves = 0; moves < 16; ++moves) {
+    // the first entry after the hole whose chain covers it: movable (any
+    // live entry but `session`'s), or blocking (`session`'s, one moving or
+    // being written); none before the run's end: no chain passes the hole
+    int64_t j = (s + 1) & t.mask, cand = -1, cv = 0;
+    bool blocked = true, tombs = false;
+    for (int k = 0; k < 64; ++k, j = (j + 1) & t.mask) {
+      // val, key, val: a hole another thread fills between the loads
+      // would pair its old key with the new val (the key decides whether
+      // the entry covers s), so a val that changed blocks
+      const int64_t v1 = __hip_atomic_load(ht_val(t, j), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+      order_wait();
+      const int64_t key = __hip_atomic_load(ht_key(t, j), __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT);
+      if (key == 0) {
+        // (a tombstone on the way may be another thread's hole that an
+        // entry covering s is moving into right now — seen here as the
+        // tombstone before, and at its old slot as the tombstone after:
+        // then s is not emptied)
+        blocked = tombs;
+        break;
+      }
+      order_wait();
+      const int64_t val = __hip_atomic_load(ht_val(t, j), __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT);
+      if (val != v1) break;                         // (blocking)
+      if (val_tomb(val)) {                          // tombstone
+        if (val == tag) tombs = true;               // (of this launch)
+        continue;
+      }
+      if (val > 0 &&
+          ((j - (key & t.mask)) & t.mask) < ((j - s) & t.mask))
+        continue;                                   // home after the hole
+      if (val > 0 && t.eph[val_node(val)] != session) {
+        cand = j;
+        cv = val;
+      }
+      break;                                        // (else: blocking)
+    }
+    if (cand < 0) {
+      if (!blocked) {
+        // nothing reaches past the hole: empty it, then the tombstones
+        // before it (their successor is now empty)
+        __hip_atomic_store(ht_val(t, s), (int64_t)0, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        order_wait();
+        __hip_atomic_store(ht_key(t, s), (int64_t)0, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        ht_reclaim(t, (s - 1) & t.mask);
+      }
+      return;
+    }
+    if (atomicCAS((unsigned long long*)ht_val(t, cand), (unsigned long long)cv,
+                  (unsigned long long)VAL_MOVING) != (unsigned long long)cv)
+      return;
+    if (atomicCAS((unsigned long long*)ht_val(t, s), (unsigned long long)tag,
+                  0ull) != (unsigned long long)tag) {
+      __hip_atomic_store(ht_val(t, cand), cv, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+    int64_t e[HT_W];
+    ent_load(t, cand, e);
+    int64_t* d = ht_ent(t, s);
+#pragma unroll
+    for (int w = 2; w < HT_W; ++w) d[w] = e[w];
+    __hip_atomic_store(ht_key(t, s), e[0], __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    order_wait();                       // the key before the val ...
+    __hip_atomic_store(ht_val(t, s), cv, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    order_wait();                       // ... and the copy before the vacate
+    __hip_atomic_store(ht_val(t, cand), tag, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    s = cand;                                       // the new hole
+  }
+  ht_reclaim(t, s);
+}
+
+ZK_DEV int64_t ht_reclaim(const ZkTree& t, int64_t s) {
+  int64_t n = 0;
+  for (int k = 0; k < 64; ++k) {
+    const int64_t nx = (s + 1) & t.mask;
+    if (__hip_atomic_load(ht_key(t, nx), __ATOMIC_RELAXED,
+                          __HIP_MEMORY_SCOPE_AGENT) != 0)
+      break;
+    if (!val_tomb(__hip_atomic_load(ht_val(t, s), __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_AGENT)))
+      break;
+    // val first: a reader between the two stores sees a key with val 0
+    // (no match, probe on), then the empty key (end of chain)
+    __hip_atomic_store(ht_val(t, s), (int64_t)0, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    order_wait();
+    __hip_atomic_store(ht_key(t, s), (int64_t)0, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    ++n;
+    s = (s - 1) & t.mask;
+  }
+  return n;
 }
 
 // tree_erase at the entry a lookup just found (slot s): no second probe.
@@ -368,7 +563,7 @@ ZK_DEV bool tree_erase_at(const ZkTree& t, int64_t s, int64_t v) {
                                         __HIP_MEMORY_SCOPE_AGENT);
   return cur > 0 && val_node(cur) == v &&
          atomicCAS((unsigned long long*)ht_val(t, s), (unsigned long long)cur,
-                   (unsigned long long)-2) == (unsigned long long)cur;
+                   (unsigned long long)VAL_TOMB) == (unsigned long long)cur;
 }
 
 // ---- watches (one-shot, per watcher slot) ---------------------------------
@@ -594,7 +789,7 @@ ZK_DEV int64_t served_reply_size(int32_t op, int32_t err, int32_t dl,
 // for this lane in phase A; on failure the caller frees it.
 ZK_DEV int32_t do_create(const ZkTree& t, Lane& L, const uint8_t* data,
                          int32_t nacl, int64_t session, int64_t now_ms,
-                         int64_t v) {
+                         int64_t v, int64_t i) {
   const ZkNodeStore& s = t.store;
   const bool eph = L.flags & CF_EPHEMERAL, seq = L.flags & CF_SEQUENTIAL;
   if (nacl <= 0) return ERR_INVALID_ACL;
@@ -612,9 +807,18 @@ ZK_DEV int32_t do_create(const ZkTree& t, Lane& L, const uint8_t* data,
   // usual, successful create walks the chain once, not twice; what this
   // lane wrote to its own node v before is freed by the caller)
   const int32_t npl = pl + (seq ? 10 : 0);
-  // a SEQUENTIAL name takes the parent's cversion, bumped in the same
-  // atomic as its child count (taken back if the create fails below)
-  const int32_t seqno = seq && par >= 0 ? cn_cver(cn_add(t, par, 1, 1)) : 0;
+  // a SEQUENTIAL name: the number zk_tree_seq_order assigned it in stream
+  // order (the parent's cversion at the batch's start + the request's rank
+  // among the batch's sequential creates under that parent; the parent was
+  // bumped once for all of them, and a failed create leaves a gap, never a
+  // number handed back).  Without one (no ordering pass, or a parent the
+  // pass did not find) the parent's cversion is taken here, bumped in the
+  // same atomic as its child count — unique, but in arrival order.
+  const int32_t pre = seq && t.seqno != nullptr ? t.seqno[i] : -1;
+  const bool taken = seq && par >= 0 && pre < 0;
+  const int32_t seqno = !seq || par < 0 ? 0
+                        : pre >= 0      ? pre
+                                        : cn_cver(cn_add(t, par, 1, 1));
   uint8_t* pd = t.path_arena + t.node_path_off[v];
   copy_bytes(pd, path, pl);
   if (seq) put_seq10(pd + pl, seqno);
@@ -635,14 +839,17 @@ ZK_DEV int32_t do_create(const ZkTree& t, Lane& L, const uint8_t* data,
   // batch contract; every field it could read is in bounds), and the next
   // launch sees everything.  A __threadfence here is an XCD-L2 writeback
   // per wave (MI355X_MICROARCH.md: ~3.5 us each) and cost milliseconds.
-  const int64_t ins = tree_insert(t, v, pd, npl, dl);
+  const int64_t ins = pre >= 0 ? tree_insert<true>(t, v, pd, npl, dl)
+                               : tree_insert(t, v, pd, npl, dl);
   if (ins != v) {
-    if (seq && par >= 0) cn_add(t, par, 0, -1);   // the child was not made
+    if (taken) cn_add(t, par, 0, -1);   // the child was not made (the
+                                        // cversion it took stays: a gap)
     return ins == TREE_INSERT_TIMEOUT ? ERR_SYSTEM : ERR_NODE_EXISTS;
   }
   t.eph[v] = eph ? session : 0;
   if (par >= 0) {
     if (seq) {
+      if (!taken) cn_add(t, par, 0, 1);             // cversion: the pass
       atomicMax((unsigned long long*)&t.pzxid[par], (unsigned long long)L.zx);
     } else {
       parent_touch(t, par, 1, true, L.zx);
@@ -826,7 +1033,7 @@ __global__ __launch_bounds__(TR_T) void tree_serve_k(
       }
       case OP_CREATE:
         L.err = do_create(t, L, rx + rq.doff, rq.vc, session,
-                          now_ms, v);
+                          now_ms, v, i);
         if (L.err == ERR_OK && r_path_off != nullptr) {
           r_path_off[i] = t.node_path_off[v];
           r_path_len[i] = t.node_path_len[v];
@@ -1171,6 +1378,305 @@ __global__ __launch_bounds__(TR_T) void ord_rank_k(int64_t ncap, OrderWs w,
   }
 }
 
+// ---- SEQUENTIAL numbers in stream order (seq_*) ----------------------------
+// A ZooKeeper leader names a SEQUENTIAL create once, from the parent's
+// cversion when it prepares the txn, in zxid order; followers apply the
+// name.  The serve applies a batch's creates concurrently, so a number
+// taken from an atomic at create time follows wave scheduling: one
+// session's pipelined creates came out in any order, and the members of a
+// replicated tree, each re-executing the same batch, named them
+// differently.  Here every SEQUENTIAL create of a batch is numbered
+//     base(parent) + its rank among the batch's SEQUENTIAL creates under
+//     that parent, in stream order,
+// base being the parent's cversion before the batch, which then moves once
+// by the group's size (a create that fails leaves a gap).  The numbers are
+// a function of the batch and the tree before it: the same on every
+// member and every run (reference: test/basic.test.js:550-611 names;
+// test/multi-node.test.js:107-165 one tree behind every member).
+//
+// Five launches, no host read, O(n) work apart from a 1024-element LDS
+// sort per chunk; a group is named by its slot e in a scratch hash of the
+// parent paths (no dense ids: nothing waits for another workgroup):
+//  1. seq_group_k, one 1024-request chunk per workgroup: parse, the parent
+//     path's slot, the chunk's (slot, lane) pairs sorted in LDS (bitonic):
+//     each request's rank in its chunk and group, each (group, chunk)
+//     count, the group's chunk bit; a new group goes on the group list;
+//  2. seq_alloc_k: per group, one count slot per chunk it appears in, and
+//     the bitmap's per-word popcount prefix;
+//  3. seq_index_k: per request, its chunk's index among its group's chunks
+//     (chunk order = stream order); chunk leaders store their counts there;
+//  4. seq_scan_k, a wave per group: exclusive scan of its chunk counts;
+//     the parent looked up and bumped once; scratch left zero;
+//  5. seq_out_k: number = base + chunk prefix + rank in the chunk.
+// A group is keyed by the 64-bit hash of the parent path (a collision merges
+// two parents' numbering: 2^-64 a pair).  A parent the pass does not find
+// (created in the same batch) leaves its creates to the serve's atomic.
+// (A first version gave groups dense ids, published by the claiming
+// workgroup while the others spun on them: 134 us of the storm's 1M-create
+// step in seq_group_k alone.)
+constexpr int SQ_C = 1024;                 // requests per chunk (workgroup)
+constexpr uint64_t SQ_NONE = ~0ull;
+constexpr int64_t SQ_MAX = 1 << 24;        // requests a batch
+
+struct SeqWs {
+  int64_t* ctr;       // [8] groups, count slots used
+  int64_t* key;       // [h] parent path hash | 1 (0 empty)
+  uint64_t* mask;     // [h * mw] chunk bitmap per group slot
+  uint16_t* pp;       // [h * mw] popcount of the bitmap words before
+  int64_t* goff;      // [h] group -> its first count slot
+  int32_t* gbase;     // [h] group -> parent cversion before the batch (-1)
+  int32_t* rep;       // [h] group -> one of its requests
+  int32_t* glist;     // [ncap] the batch's group slots
+  int32_t* cnts;      // [ncap] chunk counts, then their group prefixes
+  int32_t* gid;       // [ncap] request -> group slot (-1)
+  int32_t* rin;       // [ncap] request -> rank within its chunk and group
+  int32_t* lcnt;      // [ncap] chunk leader -> its group's count there
+  int32_t* kk;        // [ncap] request -> its chunk among its group's chunks
+  int64_t hmask;
+  int32_t mw;         // bitmap words per group (<= SQ_MW)
+};
+
+// The parent path of a well-formed SEQUENTIAL create frame ([p, p + cut));
+// cut 0 for anything else (a root child has no parent node either).
+ZK_DEV int32_t seq_parent(const uint8_t* rx, int64_t off, int32_t len,
+                          const uint8_t** p) {
+  const ReqFields rq = parse_request(rx, off, len);
+  if (rq.status != ST_OK || rq.op != OP_CREATE || !(rq.arg & CF_SEQUENTIAL))
+    return 0;
+  *p = rx + rq.poff;
+  int32_t cut = rq.pl - 1;
+  while (cut > 0 && (*p)[cut] != '/') --cut;
+  return cut;
+}
+
+__global__ __launch_bounds__(SQ_C) void seq_group_k(
+    const uint8_t* __restrict__ rx, const int64_t* __restrict__ foff,
+    const int32_t* __restrict__ flen, const int64_t* __restrict__ n_dev,
+    int64_t ncap, SeqWs w) {
+  __shared__ uint64_t sk[SQ_C];
+  __shared__ int32_t hs[SQ_C];
+  const int tid = threadIdx.x;
+  const int64_t c = blockIdx.x;
+  const int64_t i = c * SQ_C + tid;
+  const bool in = i < ncap && i < *n_dev;
+  int64_t e = -1;
+  bool first = false;
+  if (in) {
+    const uint8_t* p = nullptr;
+    const int32_t cut = seq_parent(rx, foff[i], flen[i], &p);
+    if (cut > 0) {
+      const int64_t key = (int64_t)(path_hash(p, cut) | 1ull);
+      int64_t s = key & w.hmask;
+      for (int64_t probe = 0; probe <= w.hmask; ++probe) {
+        int64_t k = __hip_atomic_load(&w.key[s], __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT);
+        if (k == 0)
+          k = (int64_t)atomicCAS((unsigned long long*)&w.key[s], 0ull,
+                                 (unsigned long long)key);
+        if (k == 0) { first = true; e = s; break; }
+        if (k == key) { e = s; break; }
+        s = (s + 1) & w.hmask;
+      }
+    }
+  }
+  if (i < ncap) {
+    w.lcnt[i] = 0;
+    w.gid[i] = (int32_t)e;
+  }
+  // the group list: one ticket per new group, one atomic per workgroup
+  const int64_t k = block_ticket<SQ_C>(&w.ctr[0], first);
+  if (first) {
+    w.glist[k] = (int32_t)e;
+    w.rep[e] = (int32_t)i;
+  }
+  // (slot, lane) sorted in LDS: a group's requests of the chunk come out
+  // together, in lane (= stream) order
+  sk[tid] = e >= 0 ? ((uint64_t)e << 10) | (uint64_t)tid : SQ_NONE;
+  __syncthreads();
+  for (int kb = 2; kb <= SQ_C; kb <<= 1) {
+    for (int j = kb >> 1; j > 0; j >>= 1) {
+      const int q = tid ^ j;
+      if (q > tid) {
+        const uint64_t a = sk[tid], b = sk[q];
+        if ((a > b) == ((tid & kb) == 0)) {
+          sk[tid] = b;
+          sk[q] = a;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  const uint64_t v = sk[tid];
+  const uint64_t gv = v >> 10;
+  const bool valid = v != SQ_NONE;
+  hs[tid] = valid && (tid == 0 || (sk[tid - 1] >> 10) != gv) ? tid : 0;
+  __syncthreads();
+  for (int d = 1; d < SQ_C; d <<= 1) {          // segment starts: max-scan
+    const int32_t x = tid >= d ? hs[tid - d] : 0;
+    __syncthreads();
+    if (x > hs[tid]) hs[tid] = x;
+    __syncthreads();
+  }
+  if (valid) {
+    const int32_t st = hs[tid];
+    w.rin[c * SQ_C + (int64_t)(v & 1023u)] = tid - st;
+    if (tid == SQ_C - 1 || (sk[tid + 1] >> 10) != gv) {     // segment end
+      w.lcnt[c * SQ_C + (int64_t)(sk[st] & 1023u)] = tid - st + 1;
+      atomicOr((unsigned long long*)&w.mask[(int64_t)gv * w.mw + (c >> 6)],
+               1ull << (c & 63));
+    }
+  }
+}
+
+__global__ __launch_bounds__(TR_T) void seq_alloc_k(SeqWs w) {
+  const int64_t ng = w.ctr[0];
+  const int64_t stride = (int64_t)gridDim.x * TR_T;
+  // (g0 is wave-uniform: wave_bytes needs the whole wave)
+  for (int64_t g0 = (int64_t)blockIdx.x * TR_T + (threadIdx.x & ~63);
+       g0 < ng; g0 += stride) {
+    const int64_t g = g0 + (threadIdx.x & 63);
+    const int64_t e = g < ng ? w.glist[g] : -1;
+    int64_t n = 0;
+    if (e >= 0) {
+      const uint64_t* m = w.mask + e * w.mw;
+      uint16_t* pp = w.pp + e * w.mw;
+      for (int k = 0; k < w.mw; ++k) {
+        pp[k] = (uint16_t)n;
+        n += __popcll(m[k]);
+      }
+    }
+    const int64_t o = wave_bytes(&w.ctr[1], n);
+    if (e >= 0) w.goff[e] = o;
+  }
+}
+
+__global__ __launch_bounds__(TR_T) void seq_index_k(int64_t ncap, SeqWs w) {
+  const int64_t i = (int64_t)blockIdx.x * TR_T + threadIdx.x;
+  if (i >= ncap) return;
+  const int64_t e = w.gid[i];
+  if (e < 0) return;
+  const int64_t c = i / SQ_C;
+  const int64_t wd = e * w.mw + (c >> 6);
+  const int32_t x = (int32_t)w.pp[wd] +
+                    __popcll(w.mask[wd] & ((1ull << (c & 63)) - 1));
+  w.kk[i] = x;
+  const int32_t lc = w.lcnt[i];
+  if (lc > 0) w.cnts[w.goff[e] + x] = lc;
+}
+
+__global__ __launch_bounds__(TR_T) void seq_scan_k(
+    ZkTree t, const uint8_t* __restrict__ rx, const int64_t* __restrict__ foff,
+    const int32_t* __restrict__ flen, SeqWs w) {
+  const int lane = threadIdx.x & 63;
+  const int64_t ng = w.ctr[0];
+  const int64_t nwv = ((int64_t)gridDim.x * TR_T) >> 6;
+  for (int64_t g = ((int64_t)blockIdx.x * TR_T + threadIdx.x) >> 6; g < ng;
+       g += nwv) {
+    const int64_t e = w.glist[g];
+    uint64_t* m = w.mask + e * w.mw;
+    int64_t n = 0;
+    for (int k = lane; k < w.mw; k += 64) n += __popcll(m[k]);
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) n += __shfl_xor(n, d, 64);
+    const int64_t o = w.goff[e];
+    int64_t run = 0;
+    for (int64_t b = 0; b < n; b += 64) {
+      const int64_t j = b + lane;
+      const int64_t x = j < n ? w.cnts[o + j] : 0;
+      const int64_t inc = wave_incl_scan(x);
+      if (j < n) w.cnts[o + j] = (int32_t)(run + inc - x);
+      run += __shfl(inc, 63, 64);
+    }
+    // the parent, found and bumped once for the whole group
+    if (lane == 0) {
+      int32_t base = -1;
+      const int32_t r = w.rep[e];
+      const uint8_t* p = nullptr;
+      const int32_t cut = seq_parent(rx, foff[r], flen[r], &p);
+      const int64_t par = cut > 0 ? tree_find(t, p, cut) : -1;
+      if (par >= 0 && t.eph[par] == 0)
+        base = cn_cver(cn_add(t, par, (int32_t)run, 0));
+      w.gbase[e] = base;
+      w.key[e] = 0;
+    }
+    for (int k = lane; k < w.mw; k += 64) m[k] = 0;
+  }
+}
+
+__global__ __launch_bounds__(TR_T) void seq_out_k(int64_t ncap, SeqWs w,
+                                                  int32_t* __restrict__ seqno) {
+  const int64_t i = (int64_t)blockIdx.x * TR_T + threadIdx.x;
+  if (i >= ncap) return;
+  const int64_t e = w.gid[i];
+  int32_t s = -1;
+  if (e >= 0) {
+    const int32_t b = w.gbase[e];
+    if (b >= 0) s = b + w.cnts[w.goff[e] + w.kk[i]] + w.rin[i];
+  }
+  seqno[i] = s;
+}
+
+// ---- tree digest (tests / replica checks) ----------------------------------
+// Sum over live nodes of a hash of (path, czxid, mzxid, version, cversion |
+// numChildren, pzxid, ephemeralOwner, data): equal on two trees that hold
+// the same znodes with the same Stat (times aside) and data, whatever node
+// slots and hash entries they sit in.
+ZK_DEV uint64_t wave_sum_u64(uint64_t x) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
+  return x;
+}
+
+__global__ __launch_bounds__(TR_T) void tree_digest_k(
+    ZkTree t, unsigned long long* __restrict__ out) {
+  const int64_t v = (int64_t)blockIdx.x * TR_T + threadIdx.x;
+  const int64_t nn = min(t.counters[TC_NODES], t.store.cap);
+  uint64_t h = 0, live = 0;
+  if (v < nn && t.node_parent[v] != NODE_FREE) {
+    const int64_t pw = t.node_pw[v];
+    const uint8_t* slot = t.store.slab + t.store.slot_off[v];
+    const int32_t dl = t.store.data_len[v];
+    h = path_hash(node_path(t, pw), pw_len(pw));
+    auto mix = [&](uint64_t x) {
+      h = (h ^ x) * 0x9E3779B97F4A7C15ull;
+      h ^= h >> 29;
+    };
+    mix((uint64_t)ld_be64(slot));                  // czxid
+    mix((uint64_t)ld_be64(slot + 8));              // mzxid
+    mix((uint32_t)ld_be32(slot + 32));             // version
+    mix((uint64_t)t.cn[v]);
+    mix((uint64_t)t.pzxid[v]);
+    mix((uint64_t)t.eph[v]);
+    mix((uint64_t)(uint32_t)dl);
+    mix(path_hash(slot + ZK_SLOT_DATA, max(dl, 0)));
+    live = 1;
+  }
+  h = wave_sum_u64(h);
+  live = wave_sum_u64(live);
+  if ((threadIdx.x & 63) == 0 && live) {
+    atomicAdd(&out[0], (unsigned long long)h);
+    atomicAdd(&out[1], (unsigned long long)live);
+  }
+}
+
+__global__ __launch_bounds__(TR_T) void ht_census_k(
+    ZkTree t, unsigned long long* __restrict__ out) {
+  uint64_t used = 0, tomb = 0;
+  for (int64_t s = (int64_t)blockIdx.x * TR_T + threadIdx.x; s <= t.mask;
+       s += (int64_t)gridDim.x * TR_T) {
+    if (*ht_key(t, s) != 0) {
+      ++used;
+      if (val_tomb(*ht_val(t, s))) ++tomb;
+    }
+  }
+  used = wave_sum_u64(used);
+  tomb = wave_sum_u64(tomb);
+  if ((threadIdx.x & 63) == 0) {
+    atomicAdd(&out[2], (unsigned long long)used);
+    atomicAdd(&out[3], (unsigned long long)tomb);
+  }
+}
+
 // After a serve / expire launch, one kernel:
 //  1. rewrite the wire-format Stat words of every dirty parent from the
 //     shadows;
@@ -1306,9 +1812,12 @@ __global__ __launch_bounds__(TR_T) void tree_expire_k(
   const int64_t zx = t.counters[TC_ZXID] + 1;
   int64_t par = -1;
   if (hit) {
-    hit = tree_erase(t, v, t.path_arena + t.node_path_off[v],
-                     t.node_path_len[v]);
+    const int64_t tag = tomb_tag(zx);
+    const int64_t es = tree_erase_slot(t, v, t.path_arena + t.node_path_off[v],
+                                       t.node_path_len[v], tag);
+    hit = es >= 0;
     if (hit) {
+      ht_shift(t, es, session, tag);
       par = t.node_parent[v];
       if (par >= 0) parent_touch(t, par, -1, true, zx);
       st_be64(s.slab + s.slot_off[v] + 44, 0);
@@ -1764,6 +2273,102 @@ int zk_tree_serve_ordered(const ZkTree* t, const uint8_t* rx, const ZkReqOut* q,
 int64_t zk_tree_order_stats_offset(int64_t ncap) {
   (void)ncap;
   return 8;
+}
+
+// Workspace of zk_tree_seq_order: the prefix that must start zeroed (and is
+// left zeroed: hash keys, published ids, chunk bitmaps), then the counters
+// (reset every call) and the per-group / per-request arrays.
+static int64_t seq_layout(int64_t ncap, uint8_t* ws, zk::SeqWs* w,
+                          int64_t* zeroed) {
+  int64_t h = 1024;
+  while (h < 2 * ncap) h <<= 1;
+  const int64_t nch = (ncap + zk::SQ_C - 1) / zk::SQ_C;
+  const int32_t mw = (int32_t)((nch + 63) / 64 > 0 ? (nch + 63) / 64 : 1);
+  auto at = [&](int64_t o) { return ws != nullptr ? ws + o : nullptr; };
+  auto a16 = [](int64_t x) { return (x + 15) & ~(int64_t)15; };
+  int64_t o = 0;
+  if (w != nullptr) {
+    w->hmask = h - 1;
+    w->mw = mw;
+    w->key = (int64_t*)at(o);
+  }
+  o += h * 8;
+  if (w != nullptr) w->mask = (uint64_t*)at(o);
+  o += h * mw * 8;
+  if (zeroed != nullptr) *zeroed = o;
+  if (w != nullptr) w->ctr = (int64_t*)at(o);
+  o += 64;
+  if (w != nullptr) w->pp = (uint16_t*)at(o);
+  o += a16(h * mw * 2);
+  if (w != nullptr) w->goff = (int64_t*)at(o);
+  o += h * 8;
+  if (w != nullptr) w->gbase = (int32_t*)at(o);
+  o += h * 4;
+  if (w != nullptr) w->rep = (int32_t*)at(o);
+  o += h * 4;
+  int32_t** arr[] = {w ? &w->glist : nullptr, w ? &w->cnts : nullptr,
+                     w ? &w->gid : nullptr,   w ? &w->rin : nullptr,
+                     w ? &w->lcnt : nullptr,  w ? &w->kk : nullptr};
+  for (int32_t** p : arr) {
+    if (p != nullptr) *p = (int32_t*)at(o);
+    o += a16(ncap * 4);
+  }
+  return o;
+}
+
+int64_t zk_tree_seq_workspace(int64_t ncap) {
+  return ncap > 0 ? seq_layout(ncap, nullptr, nullptr, nullptr) : 0;
+}
+
+int64_t zk_tree_seq_zeroed(int64_t ncap) {
+  int64_t z = 0;
+  if (ncap > 0) seq_layout(ncap, nullptr, nullptr, &z);
+  return z;
+}
+
+// SEQUENTIAL numbers of the batch's create frames (foff / flen, *n_dev of
+// them) in stream order -> seqno[ncap] (-1: none); see seq_* above.  Run
+// it before the serve of the same frames, with t->seqno = seqno there.
+int zk_tree_seq_order(const ZkTree* t, const uint8_t* rx, const int64_t* foff,
+                      const int32_t* flen, const int64_t* n_dev, int64_t ncap,
+                      uint8_t* ws, int64_t ws_bytes, int32_t* seqno,
+                      hipStream_t st) {
+  if (ncap <= 0) return 0;
+  if (ncap > zk::SQ_MAX) return -1;
+  if (ws_bytes < zk_tree_seq_workspace(ncap) || ((uintptr_t)ws & 15))
+    return -1;
+  zk::SeqWs w;
+  int64_t zeroed = 0;
+  seq_layout(ncap, ws, &w, &zeroed);
+  if (hipMemsetAsync(w.ctr, 0, 64, st) != hipSuccess) return -4;
+  const unsigned nchunk = (unsigned)((ncap + zk::SQ_C - 1) / zk::SQ_C);
+  const unsigned nb = (unsigned)((ncap + zk::TR_T - 1) / zk::TR_T);
+  const unsigned ng = nb < 1024 ? nb : 1024;   // grid-stride over groups
+  zk::seq_group_k<<<nchunk, zk::SQ_C, 0, st>>>(rx, foff, flen, n_dev, ncap, w);
+  ZK_LAUNCH_CHECK();
+  zk::seq_alloc_k<<<ng, zk::TR_T, 0, st>>>(w);
+  ZK_LAUNCH_CHECK();
+  zk::seq_index_k<<<nb, zk::TR_T, 0, st>>>(ncap, w);
+  ZK_LAUNCH_CHECK();
+  zk::seq_scan_k<<<ng, zk::TR_T, 0, st>>>(*t, rx, foff, flen, w);
+  ZK_LAUNCH_CHECK();
+  zk::seq_out_k<<<nb, zk::TR_T, 0, st>>>(ncap, w, seqno);
+  ZK_LAUNCH_CHECK();
+  return 0;
+}
+
+// out[4] (zeroed here): node digest sum, live nodes, hash entries in use,
+// tombstones (zk_abi.h).
+int zk_tree_digest(const ZkTree* t, unsigned long long* out, hipStream_t st) {
+  if (hipMemsetAsync(out, 0, 32, st) != hipSuccess) return -4;
+  const int64_t nb = (t->store.cap + zk::TR_T - 1) / zk::TR_T;
+  if (nb > 0) {
+    zk::tree_digest_k<<<(unsigned)nb, zk::TR_T, 0, st>>>(*t, out);
+    ZK_LAUNCH_CHECK();
+  }
+  zk::ht_census_k<<<2048, zk::TR_T, 0, st>>>(*t, out);
+  ZK_LAUNCH_CHECK();
+  return 0;
 }
 
 int zk_tree_expire(const ZkTree* t, int64_t session, int64_t ncap,

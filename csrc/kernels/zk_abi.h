@@ -125,6 +125,10 @@ struct ZkTree {
   int64_t* wt_key;             // [wt_hmask + 1] path hash | 1, 0 = empty
   unsigned long long* wt_mask; // [2 * (wt_hmask + 1)] data / child masks
   int64_t wt_hmask;
+  // [ncap] per request of the batch being served: its SEQUENTIAL number,
+  // assigned in stream order by zk_tree_seq_order (-1: none; the serve then
+  // takes the parent's cversion atomically).  Null: no request has one.
+  const int32_t* seqno;
 };
 
 // Server-side session table (session.hip, K9 server mode).
@@ -171,9 +175,6 @@ int64_t zk_frame_scan_workspace(int64_t n);
 int zk_frame_scan5(const uint8_t*, const int64_t*, int64_t, int64_t,
                    uint8_t*, int64_t, int64_t*, int32_t*, int64_t, int64_t*,
                    int32_t, int32_t, int32_t, hipStream_t);
-int zk_frame_scan6(const uint8_t*, const int64_t*, int64_t, int64_t, uint8_t*,
-                   int64_t, int64_t*, int32_t*, int64_t, int64_t*, int32_t,
-                   int32_t, int32_t, hipStream_t, hipStream_t);
 int zk_frame_scan_stats(const uint8_t*, int64_t, int32_t, uint32_t*,
                         hipStream_t);
 int zk_frame_scan_dbg(int64_t* host, int64_t tiles);
@@ -244,6 +245,20 @@ int64_t zk_tree_order_workspace(int64_t);
 int64_t zk_tree_order_stats_offset(int64_t);
 int zk_tree_expire(const ZkTree*, int64_t, int64_t, unsigned long long*,
                    hipStream_t);
+// SEQUENTIAL numbers of a batch in stream order (tree.hip seq_*): bytes of
+// the workspace for ncap requests, the prefix of it that must be zero when
+// it is first used (the kernels leave it zero), and the ordering itself
+// (writes seqno[ncap]; bumps each parent's cversion once per batch).
+int64_t zk_tree_seq_workspace(int64_t ncap);
+int64_t zk_tree_seq_zeroed(int64_t ncap);
+int zk_tree_seq_order(const ZkTree*, const uint8_t*, const int64_t*,
+                      const int32_t*, const int64_t*, int64_t, uint8_t*,
+                      int64_t, int32_t*, hipStream_t);
+// order-independent digest of the live nodes: out[0] = sum of per-node
+// hashes (path, czxid, mzxid, version, cversion, numChildren, owner, pzxid,
+// data), out[1] = live nodes, out[2] = hash entries in use (live +
+// tombstones), out[3] = tombstones
+int zk_tree_digest(const ZkTree*, unsigned long long*, hipStream_t);
 int zk_bench_gen_get(int64_t, uint64_t, int64_t, int64_t, int32_t,
                      const int64_t*, int64_t*, int32_t*, int64_t*, int32_t*,
                      const int64_t*, hipStream_t);
@@ -294,7 +309,7 @@ static_assert(sizeof(ZkRespBatch) == 10 * 8, "ZkRespBatch layout");
 static_assert(sizeof(ZkReplyOut) == 12 * 8, "ZkReplyOut layout");
 static_assert(sizeof(ZkReqOut) == 12 * 8, "ZkReqOut layout");
 static_assert(sizeof(ZkSessionTable) == 7 * 8, "ZkSessionTable layout");
-static_assert(sizeof(ZkTree) == 26 * 8, "ZkTree layout");
+static_assert(sizeof(ZkTree) == 27 * 8, "ZkTree layout");
 static_assert(offsetof(ZkTree, store) == 9 * 8, "ZkTree.store");
 static_assert(offsetof(ZkTree, free_list) == 14 * 8, "ZkTree.free_list");
 static_assert(offsetof(ZkTree, wt_hmask) == 25 * 8, "ZkTree.wt_hmask");

@@ -153,6 +153,7 @@ ZkTree tree(const std::vector<Tensor>& v) {
         P<int64_t>(v[19], I64, 2 * h, "tree.wt_mask", r));
     t.wt_hmask = h - 1;
   }
+  t.seqno = nullptr;
   return t;
 }
 
@@ -359,22 +360,21 @@ int64_t frame_scan_workspace(int64_t n) { return zk_frame_scan_workspace(n); }
 void frame_scan(const Tensor& buf, const c10::optional<Tensor>& n_dev,
                 int64_t n_cap, int64_t max_packet, const Tensor& ws,
                 const Tensor& foff, const Tensor& flen, const Tensor& result,
-                int64_t window, bool clean, int64_t flags, int64_t link_stream) {
+                int64_t window, bool clean, int64_t flags) {
   TORCH_CHECK(n_cap >= 0 && n_cap <= buf.numel(),
               "zkmi: frame_scan length ", n_cap, " past the buffer (",
               buf.numel(), " bytes)");
   TORCH_CHECK(ws.numel() >= zk_frame_scan_workspace(n_cap),
               "zkmi: frame_scan workspace too small");
   const int64_t cap = foff.numel();
-  hip_ok(zk_frame_scan6(
+  hip_ok(zk_frame_scan5(
              P<uint8_t>(buf, U8, 1, "buf"),
              Popt<int64_t>(n_dev, I64, 1, "n", &buf), n_cap, max_packet,
              P<uint8_t>(ws, U8, 1, "ws", &buf), ws.numel(),
              P<int64_t>(foff, I64, 1, "frame_off", &buf),
              P<int32_t>(flen, I32, cap, "frame_len", &buf), cap,
              P<int64_t>(result, I64, 4, "result", &buf), (int32_t)window,
-             clean ? 1 : 0, (int32_t)flags, cur_stream(),
-             reinterpret_cast<hipStream_t>(link_stream)),
+             clean ? 1 : 0, (int32_t)flags, cur_stream()),
          "frame_scan");
 }
 
@@ -601,10 +601,12 @@ void tree_serve_frames(const std::vector<Tensor>& t, const Tensor& rx,
                        const std::vector<Tensor>& r, int64_t session,
                        int64_t now_ms, int64_t wslot,
                        const c10::optional<Tensor>& fired,
-                       const c10::optional<Tensor>& tickets, bool finish) {
+                       const c10::optional<Tensor>& tickets, bool finish,
+                       const c10::optional<Tensor>& seqno) {
   ZkTree s = tree(t);
   const Tensor* d = &t[0];
   need(r, 10, "serve outputs");
+  s.seqno = Popt<int32_t>(seqno, I32, ncap, "seqno", d);
   TORCH_CHECK(wslot >= -1 && wslot < 64, "zkmi: watcher slot -1..63");
   const int64_t nb = (ncap + 255) / 256;
   hip_ok(zk_tree_serve_frames2(
@@ -659,10 +661,12 @@ void tree_serve_ordered(const std::vector<Tensor>& t, const Tensor& rx,
                         int64_t ncap, const std::vector<Tensor>& r,
                         int64_t session, int64_t now_ms, const Tensor& ws,
                         int64_t passes, const c10::optional<Tensor>& scratch,
-                        int64_t wslot, const c10::optional<Tensor>& fired) {
+                        int64_t wslot, const c10::optional<Tensor>& fired,
+                        const c10::optional<Tensor>& seqno) {
   TORCH_CHECK(wslot >= -1 && wslot < 64, "zkmi: watcher slot -1..63");
   ZkTree s = tree(t);
   const Tensor* d = &t[0];
+  s.seqno = Popt<int32_t>(seqno, I32, ncap, "seqno", d);
   ZkReqOut qo = req_out(q, ncap, d);
   need(r, 10, "serve outputs");
   TORCH_CHECK(passes >= 1 && passes <= 127, "zkmi: passes in 1..127");
@@ -742,6 +746,47 @@ void watch_resume(const std::vector<Tensor>& t, const Tensor& rx,
              P<int32_t>(ev_plen, I32, cap, "ev_path_len", d),
              P<int64_t>(out, I64, 3, "out", d), cur_stream()),
          "watch_resume");
+}
+
+// SEQUENTIAL numbers in stream order (tree.hip seq_*): workspace bytes for
+// ncap requests (zero the first tree_seq_zeroed(ncap) once), then per batch
+// the ordering of the request frames -> seqno (int32 [ncap]) for the serve.
+int64_t tree_seq_workspace(int64_t n) {
+  TORCH_CHECK(n >= 0, "zkmi: tree_seq_workspace n");
+  return zk_tree_seq_workspace(n);
+}
+
+int64_t tree_seq_zeroed(int64_t n) {
+  TORCH_CHECK(n >= 0, "zkmi: tree_seq_zeroed n");
+  return zk_tree_seq_zeroed(n);
+}
+
+void tree_seq_order(const std::vector<Tensor>& t, const Tensor& rx,
+                    const Tensor& foff, const Tensor& flen, const Tensor& n_dev,
+                    int64_t ncap, const Tensor& ws, const Tensor& seqno) {
+  ZkTree s = tree(t);
+  const Tensor* d = &t[0];
+  TORCH_CHECK(ncap <= (1 << 24), "zkmi: tree_seq_order: ncap <= 16M");
+  hip_ok(zk_tree_seq_order(
+             &s, P<uint8_t>(rx, U8, 1, "rx", d),
+             P<int64_t>(foff, I64, ncap, "frame_off", d),
+             P<int32_t>(flen, I32, ncap, "frame_len", d),
+             P<int64_t>(n_dev, I64, 1, "count", d), ncap,
+             P<uint8_t>(ws, U8, zk_tree_seq_workspace(ncap), "seq workspace",
+                        d),
+             ws.numel(), P<int32_t>(seqno, I32, ncap, "seqno", d),
+             cur_stream()),
+         "tree_seq_order");
+}
+
+// out (int64 [4]): node digest, live nodes, hash entries used, tombstones
+void tree_digest(const std::vector<Tensor>& t, const Tensor& out) {
+  ZkTree s = tree(t);
+  hip_ok(zk_tree_digest(&s,
+                        reinterpret_cast<unsigned long long*>(
+                            P<int64_t>(out, I64, 4, "digest", &t[0])),
+                        cur_stream()),
+         "tree_digest");
 }
 
 void tree_expire(const std::vector<Tensor>& t, int64_t session, int64_t ncap,
@@ -982,8 +1027,8 @@ TORCH_LIBRARY(zkmi, m) {
   m.def("frame_scan_workspace(int n) -> int", &frame_scan_workspace);
   m.def("frame_scan(Tensor buf, Tensor? n, int n_cap, int max_packet, "
         "Tensor(a!) ws, Tensor(b!) frame_off, Tensor(c!) frame_len, "
-        "Tensor(d!) result, int window, bool clean=False, int flags=0, "
-        "int link_stream=0) -> ()",
+        "Tensor(d!) result, int window, bool clean=False, int flags=0) "
+        "-> ()",
         &frame_scan);
   m.def("frame_scan_stats(Tensor ws, int n_cap, int window) -> int[]",
         &frame_scan_stats);
@@ -1025,8 +1070,8 @@ TORCH_LIBRARY(zkmi, m) {
   m.def("tree_serve_frames(Tensor(a!)[] tree, Tensor rx, Tensor frame_off, "
         "Tensor frame_len, Tensor count, int ncap, Tensor(b!)[] out, "
         "int session, int now_ms, int wslot=-1, Tensor(c!)? fired=None, "
-        "Tensor(d!)? tickets=None, bool finish=True) -> ()",
-        &tree_serve_frames);
+        "Tensor(d!)? tickets=None, bool finish=True, Tensor? seqno=None) "
+        "-> ()", &tree_serve_frames);
   m.def("tree_finish(Tensor(a!)[] tree, Tensor? count, int bump=0, "
         "bool publish=True) -> ()", &tree_finish);
   m.def("tree_order_workspace(int n) -> int", &tree_order_workspace);
@@ -1034,7 +1079,14 @@ TORCH_LIBRARY(zkmi, m) {
   m.def("tree_serve_ordered(Tensor(a!)[] tree, Tensor rx, Tensor[] requests, "
         "Tensor count, int ncap, Tensor(b!)[] out, int session, int now_ms, "
         "Tensor(c!) ws, int passes, Tensor? scratch, int wslot=-1, "
-        "Tensor(d!)? fired=None) -> ()", &tree_serve_ordered);
+        "Tensor(d!)? fired=None, Tensor? seqno=None) -> ()",
+        &tree_serve_ordered);
+  m.def("tree_seq_workspace(int n) -> int", &tree_seq_workspace);
+  m.def("tree_seq_zeroed(int n) -> int", &tree_seq_zeroed);
+  m.def("tree_seq_order(Tensor(a!)[] tree, Tensor rx, Tensor frame_off, "
+        "Tensor frame_len, Tensor count, int ncap, Tensor(b!) ws, "
+        "Tensor(c!) seqno) -> ()", &tree_seq_order);
+  m.def("tree_digest(Tensor[] tree, Tensor(a!) out) -> ()", &tree_digest);
   m.def("watch_events(Tensor r_op, Tensor r_err, Tensor count, int ncap, "
         "Tensor fired, Tensor(a!) bsum, Tensor(b!) ev_slot, "
         "Tensor(c!) ev_type, Tensor(d!) ev_path_off, Tensor(e!) ev_path_len, "

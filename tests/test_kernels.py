@@ -816,9 +816,11 @@ def test_gpu_free_ring_recycles_nodes(gpu):
 
 
 def test_gpu_ephemeral_sequential_and_expire(gpu):
-    """SEQUENTIAL appends the parent's cversion as %010d, EPHEMERAL records
-    the session, children of ephemerals are refused, and expiring the
-    session removes exactly its ephemerals."""
+    """SEQUENTIAL appends the parent's cversion as %010d — in stream (xid)
+    order: one session's pipelined creates are numbered in the order it
+    sent them, as a ZooKeeper leader names them —, EPHEMERAL records the
+    session, children of ephemerals are refused, and expiring the session
+    removes exactly its ephemerals."""
     from zkmi.bench.synthetic import GpuServer
     tree = _small_tree(gpu, 1000, 16)
     srv = GpuServer(tree, 64, 1 << 16)
@@ -840,7 +842,7 @@ def test_gpu_ephemeral_sequential_and_expire(gpu):
     reps = serve([create(i, '/bench/d000001/q-', ES) for i in range(5)] +
                  [create(9, '/bench/d000001/eph', E)], session=0x1234)
     assert all(r['err'] == 'OK' for r in reps)
-    seqs = sorted(r['path'] for r in reps[:5])
+    seqs = [r['path'] for r in reps[:5]]          # reply (= xid) order
     # d000001 has 100 children, cversion 100 after the fill
     assert seqs == ['/bench/d000001/q-%010d' % k for k in range(100, 105)]
     reps = serve([create(10, '/bench/d000001/eph/child', [])], session=0x1234)
@@ -855,6 +857,127 @@ def test_gpu_ephemeral_sequential_and_expire(gpu):
     reps = serve([{'xid': 12, 'opcode': 'EXISTS', 'path': '/bench/d000001',
                    'watch': False}], session=0)
     assert reps[0]['stat'].numChildren == 101
+
+
+def _seq_batch(parents, n, xid0=0, flags=('EPHEMERAL', 'SEQUENTIAL')):
+    """n SEQUENTIAL creates cycling over `parents` (request k under
+    parents[k % len]), in xid order."""
+    return [{'xid': xid0 + k, 'opcode': 'CREATE',
+             'path': parents[k % len(parents)] + '/s-', 'data': b'%d' % k,
+             'acl': jute.DEFAULT_ACL, 'flags': list(flags)} for k in range(n)]
+
+
+def _serve_decode(srv, pk, gpu, session=0):
+    s = b''.join(jute.frame(jute.encode_request(p)) for p in pk)
+    out, total, _, _ = srv.serve(_dev_bytes(s, gpu), len(s), session=session)
+    rx = bytes(out[:total.item()].cpu().numpy().tobytes())
+    frames, _, _ = jute.scan_frames(rx)
+    xmap = {p['xid']: p['opcode'] for p in pk}
+    return [jute.decode_response(rx[o:o + ln], xmap) for o, ln in frames]
+
+
+@pytest.mark.parametrize('n,nparents', [(7, 1), (3000, 3), (2500, 700)])
+def test_gpu_sequential_names_in_stream_order(gpu, n, nparents):
+    """SEQUENTIAL numbers follow the stream: under each parent the batch's
+    creates are numbered cversion-before-the-batch + their rank in request
+    order — across the 1024-request chunks of the ordering pass (3000 under
+    3 parents: 1000 a parent spanning 3 chunks), for many small groups, and
+    for one pipelined session.  The parent's cversion moves by the count;
+    a second batch continues after it.  (reference test/basic.test.js:
+    550-611; a ZooKeeper leader names them in zxid order.)"""
+    from zkmi.bench.synthetic import GpuServer
+    tree = _small_tree(gpu, 1000 * 10, 16, spare=1.0)
+    srv = GpuServer(tree, 4096, 1 << 22)
+    parents = ['/bench/d%06d' % (d % 10) for d in range(nparents)]
+    if nparents > 10:     # more parents than directories: create them
+        parents = ['/bench/d000003/p%04d' % d for d in range(nparents)]
+        reps = _serve_decode(srv, [
+            {'xid': 100000 + d, 'opcode': 'CREATE', 'path': p, 'data': b'',
+             'acl': jute.DEFAULT_ACL, 'flags': []}
+            for d, p in enumerate(parents)], gpu)
+        assert all(r['err'] == 'OK' for r in reps)
+    base = {}
+    for p in parents:
+        st = _serve_decode(srv, [{'xid': 1, 'opcode': 'EXISTS', 'path': p,
+                                  'watch': False}], gpu)[0]['stat']
+        base[p] = st.cversion
+    for rnd in range(2):
+        pk = _seq_batch(parents, n, xid0=rnd * n)
+        reps = _serve_decode(srv, pk, gpu, session=0x77)
+        assert [r['err'] for r in reps] == ['OK'] * n
+        rank = {}
+        for k, r in enumerate(reps):
+            p = parents[k % nparents]
+            want = '%s/s-%010d' % (p, base[p] + rank.get(p, 0))
+            assert r['path'] == want, (k, r['path'], want)
+            rank[p] = rank.get(p, 0) + 1
+        for p in set(parents):
+            base[p] += rank[p]
+    # the parents' Stat: cversion = before + creates, numChildren with it
+    p = parents[0]
+    st = _serve_decode(srv, [{'xid': 9, 'opcode': 'EXISTS', 'path': p,
+                              'watch': False}], gpu)[0]['stat']
+    assert st.cversion == base[p]
+
+
+def test_gpu_sequential_replicas_agree(gpu):
+    """Two replicas of one tree serving the same batches come out with the
+    same znodes, names, zxids, owners and data (GpuTree.digest), whatever
+    order their waves ran in; a failed SEQUENTIAL create leaves a gap (its
+    number is not reused), and the next batch numbers after it."""
+    from zkmi.bench.synthetic import GpuServer
+    trees = [_small_tree(gpu, 4000, 16, spare=2.0) for _ in range(2)]
+    srvs = [GpuServer(t, 4096, 1 << 22) for t in trees]
+    parents = ['/bench/d%06d' % d for d in range(40)]
+    pk = _seq_batch(parents, 4000)
+    # request 40 (parents[0]'s second) has no ACL: INVALID_ACL after its
+    # number was assigned — a gap under parents[0]
+    pk[40]['acl'] = []
+    got = []
+    for srv, t in zip(srvs, trees):
+        r1 = _serve_decode(srv, pk, gpu, session=5)
+        r2 = _serve_decode(srv, _seq_batch(parents[:3], 300, xid0=5000),
+                           gpu, session=6)
+        got.append(([r.get('path') for r in r1 + r2], t.digest()))
+    assert got[0][0] == got[1][0]
+    assert got[0][1][:2] == got[1][1][:2]
+    assert got[0][1][1] == trees[0].n_static + 3999 + 300
+    names = got[0][0]
+    assert names[40] is None
+    assert names[0] == '/bench/d000000/s-%010d' % 100
+    assert names[80] == '/bench/d000000/s-%010d' % 102      # the gap
+    # the next batch numbers after the whole first one (100 creates a
+    # parent: cversion 100 -> 200)
+    assert names[4000] == '/bench/d000000/s-%010d' % 200
+
+
+def test_gpu_expiry_reclaims_tombstones(gpu):
+    """Never-reused SEQUENTIAL names do not fill the hash index: session
+    expiry empties the entries it tombstones when nothing after them
+    continues a probe chain (tree.hip ht_reclaim), and the next batch's
+    names take over the tombstones their probes pass (tree_insert<true>),
+    so the tombstone count settles instead of growing until a rebuild."""
+    from zkmi.bench.synthetic import GpuServer
+    tree = _small_tree(gpu, 4000, 16, spare=1.5)
+    srv = GpuServer(tree, 4096, 1 << 22)
+    parents = ['/bench/d%06d' % d for d in range(40)]
+    d0, live0, used0, tomb0 = tree.digest()
+    assert tomb0 == 0 and used0 == live0
+    tombs = []
+    for k in range(40):
+        reps = _serve_decode(srv, _seq_batch(parents, 4000, xid0=k * 4000),
+                             gpu, session=100 + k)
+        assert all(r['err'] == 'OK' for r in reps)
+        assert int(tree.expire(100 + k).item()) == 4000
+        d, live, used, tomb = tree.digest()
+        assert live == live0
+        assert used - tomb == live
+        tombs.append(tomb)
+    print('tombstones per round', tombs, 'of', tree.hcap, 'entries')
+    # settled: the last ten rounds no higher than the ten before, and the
+    # index (live + tombstones) under half full
+    assert max(tombs[30:]) <= max(tombs[20:30]) * 1.15 + 50, tombs
+    assert live0 + tombs[-1] < tree.hcap // 2
 
 
 def test_gpu_mix_pipeline(gpu):
@@ -876,7 +999,7 @@ def test_gpu_storm_pipeline(gpu):
     from zkmi.bench.synthetic import StormPipeline
     tree = _small_tree(gpu, 20000, 37, spare=1.5)
     pipe = StormPipeline(tree, 8192, ndirs=64)
-    for _ in range(12):                 # crosses at least one rehash
+    for _ in range(12):
         ok = pipe.step()
         assert int(ok.item()) == 8192
     # 13 steps: 7 sessions born, 6 resumed (5 next to a refused expired
@@ -890,8 +1013,8 @@ def test_gpu_storm_pipeline(gpu):
 def test_gpu_storm_pipeline_captured(gpu):
     """The storm step replayed from HIP graphs: session ids come from the
     device (TC_SESS), so every replay serves, expires and checks the NEXT
-    session; rehashes run between replays.  Then eager steps carry on from
-    the replayed state."""
+    session; the hash index is never rebuilt (the expiry reclaims it).
+    Then eager steps carry on from the replayed state."""
     from zkmi.bench.synthetic import StormPipeline
     tree = _small_tree(gpu, 20000, 37, spare=1.5)
     pipe = StormPipeline(tree, 8192, ndirs=64)
@@ -899,10 +1022,12 @@ def test_gpu_storm_pipeline_captured(gpu):
     g = pipe.capture(acc)
     torch.cuda.synchronize()
     acc.zero_()
-    for _ in range(14):                 # crosses rehashes
+    for _ in range(14):
         g.replay()
     torch.cuda.synchronize()
     assert int(acc.sum().item()) == 14 * 8192
+    _, live, used, tomb = tree.digest()
+    assert used - tomb == live and tomb < tree.hcap // 20
     for _ in range(2):
         assert int(pipe.step().item()) == 8192
     assert bool(pipe.hs_ok.item())

@@ -13,6 +13,9 @@ there, owned by its session (write visibility across members).  Everything
 is checked on the device (the pipeline's reply / handshake / removed-count
 checks).
 
+Every member's tree digest (path, czxid, mzxid, version, cversion, owner,
+data of every live znode) must agree at the end.
+
 Runs world 2 and 3 with gloo on one GPU (ranks share it; RCCL needs one GPU
 per rank).  Reference: lib/zk-session.js:265-339 (reattach to another
 backend), test/multi-node.test.js:107-165 (a write through one server is
@@ -47,10 +50,13 @@ def _rank(rank, world, port, q, steps, n):
         sids = pipe.sessions.sid[pipe.sessions.state == 1].cpu().tolist()
         # one tree: every member's zxid counter agrees
         zx = int(tree.counters[1].item())
+        # one tree, byte for byte: every znode's path (the SEQUENTIAL names
+        # included), czxid, mzxid, version, cversion, owner and data
+        dig = tree.digest()[:2]
         q.put((rank, oks, dict(pipe.stats), bool(pipe.hs_ok.item()),
-               sorted({s >> 56 for s in sids}), found, zx))
+               sorted({s >> 56 for s in sids}), found, zx, dig))
     except BaseException as e:          # reported by the parent
-        q.put((rank, repr(e), None, None, None, None, None))
+        q.put((rank, repr(e), None, None, None, None, None, None))
         raise
     finally:
         dist.destroy_process_group()
@@ -77,8 +83,8 @@ def test_storm_sessions_move_between_members(gpu, world):
         r = q.get(timeout=10)
         res[r[0]] = r[1:]
     assert all(p.exitcode == 0 for p in procs), res
-    zxids = set()
-    for rank, (oks, st, hs_ok, members, found, zx) in res.items():
+    zxids, digests = set(), set()
+    for rank, (oks, st, hs_ok, members, found, zx, dig) in res.items():
         assert oks == [n] * steps, (rank, oks)
         assert hs_ok
         # steps 1..9 after the birth in __init__: 5 resumes, all on the
@@ -93,4 +99,9 @@ def test_storm_sessions_move_between_members(gpu, world):
         assert members == list(range(1, world + 1)), (rank, members)
         assert found == n, (rank, found)
         zxids.add(zx)
+        digests.add(tuple(dig))
     assert len(zxids) == 1, zxids
+    # the members re-execute every batch: with SEQUENTIAL numbers assigned
+    # in stream order they build the same tree (round 5's atomic numbering
+    # named the same creates differently on each member)
+    assert len(digests) == 1, digests

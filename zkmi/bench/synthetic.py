@@ -40,16 +40,6 @@ I64, I32, U8 = torch.int64, torch.int32, torch.uint8
 # multi-XCD part — tree_serve 90 -> 231 us, the GET step 0.651 -> 0.718 ms
 # (profiles/r5_regression_ab.md); the extra launch is far cheaper.
 _SERVE_TICKETS = os.environ.get('ZKMI_SERVE_TICKETS', '0') == '1'
-# ZKMI_SIDE_FINISH=1: GET pipelines fork the serve's tree finish to a side
-# stream (off the reply path: the single-workgroup kernel waits ~15 us for
-# a CU behind the other connection's kernels).  Off by default: no gain
-# measured (0.655 vs 0.655 ms) and the captured step segfaulted in
-# capture_end (test_gpu_get_pipeline_graph_replay)
-_SIDE_FINISH = os.environ.get('ZKMI_SIDE_FINISH', '0') == '1'
-# ZKMI_LINK_PRIO=1: the GET scans' fs_link on a high-priority stream (fork
-# and join by events inside the scan).  Off: a captured step with it
-# segfaulted in hipStreamEndCapture (test_gpu_get_pipeline_graph_replay)
-_LINK_PRIO = os.environ.get('ZKMI_LINK_PRIO', '0') == '1'
 # ZKMI_GET_STAGE: the LDS bytes per workgroup the GET pipelines' reply
 # encode asks for (0: the encoder's 28 KiB).  Uniform GET replies need only
 # the writer's 7 KiB header table, but 8 KiB measured no faster for them
@@ -63,10 +53,8 @@ _FREE_COMPACT = os.environ.get('ZKMI_FREE_COMPACT', '1') == '1'
 # ZKMI_FINISH_SCAN=0: the tree finish and the reply encode's block-sum scan
 # as two launches again (tree_finish_scan_k runs them as one)
 _FINISH_SCAN = os.environ.get('ZKMI_FINISH_SCAN', '1') == '1'
-# the storm rebuilds its hash index when the entries claimed since the last
-# rebuild (live + tombstones of never-reused SEQUENTIAL names) would pass
-# this share of the table
-_REHASH_LOAD = float(os.environ.get('ZKMI_REHASH_LOAD', '0.3'))
+# the largest batch tree_seq_order numbers
+_SEQ_MAX = 1 << 24
 
 
 def _len(total):
@@ -294,6 +282,17 @@ class GpuTree(object):
         _lib.lib().tree_ht_reset(self._tensors)
         _lib.lib().tree_build(self._tensors, 0, min(n, self.cap))
 
+    def digest(self):
+        """(digest, live nodes, hash entries in use, tombstones): the digest
+        is an order-independent hash of every live znode's path, czxid,
+        mzxid, version, cversion / numChildren, pzxid, ephemeralOwner and
+        data (times aside): two replicas of one tree agree on it whatever
+        slots and hash entries their nodes sit in.  One host read."""
+        out = torch.zeros(4, dtype=I64, device=self.device)
+        _lib.lib().tree_digest(self._tensors, out)
+        d, live, used, tomb = out.cpu().tolist()
+        return d & ((1 << 64) - 1), live, used, tomb
+
     def free_compact(self):
         """Rebuild the free ring's pending entries as the free nodes in node
         order, on the device (csrc/kernels/tree.hip free_count_k): the next
@@ -362,9 +361,18 @@ class GpuServer(object):
     """Server half of the pipeline: frame-scan + decode requests, apply them
     to a :class:`GpuTree`, encode replies."""
 
-    def __init__(self, tree, cap_frames, out_cap, window=2048):
+    def __init__(self, tree, cap_frames, out_cap, window=2048,
+                 seq_order=True):
         self.tree = tree
         self.window = window              # K1 entry window of the requests
+        # SEQUENTIAL creates numbered in stream order before each serve
+        # (csrc/kernels/tree.hip seq_*: five launches); a server whose
+        # batches never carry one (the GET pipeline, the write mixes
+        # without SEQUENTIAL) skips them.  Off, a SEQUENTIAL create still
+        # gets a unique number, in arrival order.
+        self.seq_order = seq_order and cap_frames <= _SEQ_MAX
+        self.seq_ws = None
+        self.seqno = None
         dev = tree.device
         self.rt = B.alloc_request_table(cap_frames, dev)
         # CREATE replies carry the created path from the tree's arena
@@ -495,15 +503,12 @@ class GpuServer(object):
         return self.result
 
     def serve_steps(self, rx, n, session=0, terminate=False, ordered=False,
-                    passes=4, wslot=-1, resume=False, side=None):
+                    passes=4, wslot=-1, resume=False):
         """:meth:`serve` as a generator yielding once, between the request
         decode and the tree; the return tuple lands in ``self.result`` (a
         pipelined caller interleaves another connection's work there).
 
-        ``side`` (a read-only batch only: GET_DATA / EXISTS / GET_CHILDREN):
-        the tree's between-batch finish (zxid, free-ring publish) runs on
-        that stream, forked after the serve and off the reply path; the
-        caller joins it with :meth:`join` before the tree's next batch."""
+"""
         L = _lib.lib()
         ft = self.scanner.scan(rx, n)
         # ordered serving ranks the batch from K12's request table; the
@@ -516,6 +521,7 @@ class GpuServer(object):
                r.path_len, r.slot, self.presized[0], self.presized[1]]
         now = int(time.time() * 1000)
         fuse = False
+        seqno = self._seq_order(rx, ft) if self.seq_order else None
         if ordered:
             if self.ows is None:
                 self.ows = torch.empty(
@@ -525,25 +531,20 @@ class GpuServer(object):
                                  ft.count, self.cap_frames, out, session,
                                  now, self.ows, passes, self.tree.scratch,
                                  wslot, self.fired if self.tree.watch
-                                 is not None else None)
+                                 is not None else None, seqno)
         else:
-            fuse = _FINISH_SCAN and side is None and not _SERVE_TICKETS
+            fuse = _FINISH_SCAN and not _SERVE_TICKETS
             L.tree_serve_frames(self.tree.tensors, rx, ft.off, ft.length,
                                 ft.count, self.cap_frames, out, session, now,
                                 wslot, self.fired if self.tree.watch
                                 is not None else None,
                                 self.tickets if _SERVE_TICKETS else None,
-                                side is None and not fuse)
+                                not fuse, seqno)
             if fuse:
                 # the finish and K13's block-sum scan: one launch
                 L.tree_finish_scan(self.tree.tensors, ft.count, 0, True,
                                    self.cap_frames, self.presized[1],
                                    self.total_err[0])
-            if side is not None:
-                side.wait_stream(torch.cuda.current_stream(self.tree.device))
-                with torch.cuda.stream(side):
-                    L.tree_finish(self.tree.tensors, ft.count, 0, True)
-                self._side = side
         out, rec_off, total, err = B.encode_responses(
             r, self.tree.store, self.out.numel(), out=self.out,
             presized=self.presized, terminate=terminate,
@@ -560,13 +561,21 @@ class GpuServer(object):
                     raise ValueError('resume needs the watcher slot')
                 self._resume(rx, ft, wslot)
 
-    def join(self):
-        """Wait (on the current stream) for a finish forked by
-        ``serve_steps(..., side=...)``."""
-        side = getattr(self, '_side', None)
-        if side is not None:
-            torch.cuda.current_stream(self.tree.device).wait_stream(side)
-            self._side = None
+    def _seq_order(self, rx, ft):
+        """Number the batch's SEQUENTIAL creates in stream order (parent's
+        cversion before the batch + rank among its sequential creates
+        here): returns the int32 [cap_frames] numbers for the serve."""
+        L = _lib.lib()
+        dev = self.tree.device
+        if self.seq_ws is None:
+            n = self.cap_frames
+            self.seq_ws = torch.empty(L.tree_seq_workspace(n), dtype=U8,
+                                      device=dev)
+            self.seq_ws[:L.tree_seq_zeroed(n)].zero_()
+            self.seqno = torch.empty(n, dtype=I32, device=dev)
+        L.tree_seq_order(self.tree.tensors, rx, ft.off, ft.length, ft.count,
+                         self.cap_frames, self.seq_ws, self.seqno)
+        return self.seqno
 
     def order_stats(self):
         """(largest same-path rank, scratch bytes used) of the last ordered
@@ -631,18 +640,14 @@ class GetPipeline(object):
         dmax = max(tree.data_bytes, 128)
         # K1 windows: the largest request / reply frame of this workload
         self.server = GpuServer(tree, n, n * (4 + 16 + 4 + dmax + 68) + 64,
-                                window=B.frame_window(17 + maxpath))
+                                window=B.frame_window(17 + maxpath),
+                                seq_order=False)
         self.server.enc_stage = _GET_STAGE
         self.rwindow = B.frame_window(4 + 16 + 4 + dmax + 68)
         lo, hi = tree.data_dist or (tree.data_bytes, tree.data_bytes)
-        # fs_link of both scans on a high-priority stream (its workgroups
-        # would go ahead of the other connection's waiting ones;
-        # ZKMI_LINK_PRIO, off by default)
-        self.link = torch.cuda.Stream(dev, priority=-1) if _LINK_PRIO \
-            else None
         self.rscanner = B.FrameScanner(n, dev, window=self.rwindow,
                                        frame_hint=4 + 16 + 4 + 68 +
-                                       (lo + hi) // 2, link_stream=self.link)
+                                       (lo + hi) // 2)
         self.reply = B.alloc_replies(n, dev)
         self.xid_base = 0
         self.last = None
@@ -650,10 +655,6 @@ class GetPipeline(object):
         self.step_no = 0
         self.idx = torch.empty(n, dtype=I64, device=dev)
         self.xid = torch.empty(n, dtype=I32, device=dev)
-        # the serve's tree finish on a side stream (a GET batch changes
-        # nothing the replies read; ZKMI_SIDE_FINISH, off by default)
-        self.side = torch.cuda.Stream(dev) if _SIDE_FINISH else None
-        self.server.scanner.link_stream = self.link
         self.poff = torch.empty(n, dtype=I64, device=dev)
         self.plen = torch.empty(n, dtype=I32, device=dev)
         self.gstate = None      # device {seed, step} (see capture)
@@ -757,7 +758,7 @@ class GetPipeline(object):
                             self.acl_len, self.acl_arena)
         tx, rec_off, total, err = B.encode_requests(rb, self.xt, out=self.tx)
         yield
-        srv = self.server.serve_steps(tx, _len(total), side=self.side)
+        srv = self.server.serve_steps(tx, _len(total))
         next(srv)
         yield
         for _ in srv:
@@ -776,7 +777,6 @@ class GetPipeline(object):
                                tick=self.gstate if validate else None)
         if self.gstate is not None and not validate:
             self.gstate[1:].add_(1)
-        self.server.join()
         self.last = (self.idx, rep, rx, ft)
 
 
@@ -859,7 +859,8 @@ class _Driver(object):
     batch (xids recorded in the HBM xid table), the GPU server, then K1 +
     K2-K8 decode of the reply stream."""
 
-    def __init__(self, tree, batch, max_path, data_bytes, seed):
+    def __init__(self, tree, batch, max_path, data_bytes, seed,
+                 seq_order=False):
         self.tree = tree
         self.batch = batch
         self.dev = dev = tree.device
@@ -872,7 +873,8 @@ class _Driver(object):
         # two-entry ACL; a GET_DATA-sized reply)
         self.server = GpuServer(
             tree, batch, batch * (4 + 16 + 4 + max(dmax, max_path + 16) + 68)
-            + 64, window=B.frame_window(33 + max_path + data_bytes + 128))
+            + 64, window=B.frame_window(33 + max_path + data_bytes + 128),
+            seq_order=seq_order)
         self.rwindow = B.frame_window(4 + 16 + 4 + max(dmax, max_path + 16)
                                       + 68)
         self.reply = B.alloc_replies(batch, dev)
@@ -1316,8 +1318,12 @@ class StormPipeline(object):
 
     Every check (replies, handshake outcome, ids, password, removed count)
     runs on the device; a step makes no device-to-host read.  The hash
-    index is rebuilt whenever the tombstones left by never-reused sequential
-    names would fill it.
+    index needs no rebuild: the expiry moves live entries back over the
+    holes it leaves and empties the rest (csrc/kernels/tree.hip ht_shift),
+    and the next batch's names take over the tombstones their probes pass,
+    so never-reused SEQUENTIAL names leave a bounded number of tombstones
+    (~0.6 % of the index at the bench's size,
+    tools/microbench/storm_census.py).
 
     Across GPUs (a process group of ``world`` > 1 ranks: the members of one
     ensemble, each rank's GPU server a member) the session MOVES, as
@@ -1368,7 +1374,8 @@ class StormPipeline(object):
         self.world = W = dist.get_world_size(group) if on else 1
         self.rank = dist.get_rank(group) if on else 0
         self.coll = torch.device(coll_device) if coll_device else dev
-        self.drv = _Driver(tree, batch, 32, data_bytes, seed)
+        self.drv = _Driver(tree, batch, 32, data_bytes, seed,
+                           seq_order=True)
         self.sessions = GpuSessionTable(tree, server_id=self.rank + 1,
                                         members=W)
         if W > 1:
@@ -1427,7 +1434,6 @@ class StormPipeline(object):
         self.sid0 = self.sessions.sid_of(0)
         self._capturing = False
         self.step_no = 0
-        self.inserted = 0
         self.stats = {'born': 0, 'resumed': 0, 'expired': 0,
                       'expired_resume_refused': 0, 'cross_rank_resumes': 0}
         # replicated tree (see the class docs): the step's stream slots
@@ -1520,16 +1526,14 @@ class StormPipeline(object):
         HIP graphs; ``replay()`` runs the next step.  Session ids live on
         the device (``kdev`` -> the tree's TC_SESS word), so a replay serves,
         expires and checks the next session; the host keeps only its
-        bookkeeping (counts, the rehash due every few hundred steps, run
-        eagerly between replays).  One member only: the ensemble's steps
+        bookkeeping (counts).  One member only: the ensemble's steps
         gather over the process group."""
         if self.world > 1:
             raise RuntimeError('storm capture: one member only')
         while self.step_no < 2 or self.step_no % 2:
             self.step(acc=acc)
-        self._check_rehash(2)
         torch.cuda.synchronize(self.dev)
-        keep = (self.step_no, self.k, self.inserted, dict(self.stats),
+        keep = (self.step_no, self.k, dict(self.stats),
                 self.sessions.allocated)
         graphs = []
         self._capturing = True
@@ -1541,26 +1545,16 @@ class StormPipeline(object):
                 graphs.append(g)
         finally:
             self._capturing = False
-        (self.step_no, self.k, self.inserted, self.stats,
+        (self.step_no, self.k, self.stats,
          self.sessions.allocated) = keep
         return _StormCycle(self, graphs)
 
-    def _check_rehash(self, steps=1):
-        """Rebuild the hash index now if the next ``steps`` steps' inserts
-        would fill it (tombstones of never-reused sequential names)."""
-        if (self.inserted + (steps + 1) * self.n * self.world) > \
-                _REHASH_LOAD * self.tree.hcap:
-            self.tree.rehash()
-            self.inserted = 0
-
     def _advance(self):
         """The host side of a step (eager and replayed alike): step and
-        session counters, stats, the rehash decision.  Returns resume."""
+        session counters, stats.  Returns resume."""
         s = self.step_no
         self.step_no += 1
         resume = s % 2 == 1
-        if not self._capturing:
-            self._check_rehash()
         if resume:
             self.stats['resumed'] += 1
             self.stats['expired_resume_refused'] += int(self.k >= 1)
@@ -1570,7 +1564,6 @@ class StormPipeline(object):
             self.stats['born'] += 1
             if self.k >= 1:
                 self.stats['expired'] += 1
-        self.inserted += self.n * self.world
         return resume
 
     def step(self, validate=True, acc=None):
@@ -1882,7 +1875,8 @@ class WatchPipeline(object):
         rep_max = 4 + 16 + 4 + max(tree.data_bytes, 128) + 68
         self.server = GpuServer(tree, n, n * rep_max + 64,
                                 window=B.frame_window(33 + maxpath +
-                                                      self.data_bytes))
+                                                      self.data_bytes),
+                                seq_order=False)
         self.rscan = B.FrameScanner(n, dev, window=B.frame_window(rep_max))
         self.reply = B.alloc_replies(n, dev)
         # R1 slots: one notification stream per rank

@@ -365,13 +365,9 @@ class FrameScanner:
     instead of four allocations."""
 
     def __init__(self, cap, device, window=2048,
-                 max_packet=consts.MAX_PACKET, frame_hint=None, group=None,
-                 link_stream=None):
+                 max_packet=consts.MAX_PACKET, frame_hint=None, group=None):
         self.cap = cap
         self.window = window
-        # a stream (e.g. high priority) for fs_link, forked and joined
-        # inside the scan (csrc/kernels/frame_scan.hip zk_frame_scan6)
-        self.link_stream = link_stream
         # the stream's usual frame size: >= 128 bytes within a small window
         # lets a wave take a group of tiles (the chain map once, then the
         # chain walked on; csrc/kernels/frame_scan.hip fs_group_rest).
@@ -412,9 +408,7 @@ class FrameScanner:
                          t.length, t.result, int(self.window),
                          ncap == self.clean_for,
                          (1 if nospec else 0) | (int(misspec) << 8) |
-                         ((self.group - 1) << 4),
-                         self.link_stream.cuda_stream
-                         if self.link_stream is not None else 0)
+                         ((self.group - 1) << 4))
         self.clean_for = ncap
         self.last_cap = ncap
         return t

@@ -60,6 +60,14 @@ __all__ = ['EnsembleControl', 'EnsembleWorkload', 'owner_of']
 _DIGITS = 5                      # paths are /ens/pNNNNN
 
 
+def _phased(t):
+    """A bulk call's phase clock has every mark the split needs (the
+    'captured' mark exists only when the native transport captured the
+    batch; a per-frame or non-native path has none)."""
+    return bool(t.get('submit')) and all(
+        k in t for k in ('encoded', 'captured', 'finished'))
+
+
 class EnsembleControl(object):
     """The ensemble as a child process — the native server with ``n``
     members (``zkmi.server.fast``), or with ``native=False`` the Python
@@ -364,7 +372,7 @@ class EnsembleWorkload(object):
         ph = self.phase_ms
         ph['rearm_bulk_get'] += (time.perf_counter() - t0) * 1e3
         t = getattr(res, 'phases', None) or {}
-        if t.get('submit') and 'finished' in t:
+        if _phased(t):
             ph['rb_encode'] += (t['encoded'] - t['submit']) * 1e3
             ph['rb_wire'] += (t['captured'] - t['encoded']) * 1e3
             ph['rb_finish'] += (t['finished'] - t['captured']) * 1e3
@@ -570,7 +578,7 @@ class EnsembleWorkload(object):
             if mine:
                 res = self._bulk(self.client.bulk_set, mine, data)
                 t = getattr(res, 'phases', None) or {}
-                if t.get('submit') and 'finished' in t:
+                if _phased(t):
                     ph = self.phase_ms
                     ph['wb_encode'] = ph.get('wb_encode', 0.0) + \
                         (t['encoded'] - t['submit']) * 1e3

@@ -317,7 +317,8 @@ class _Conn(object):
                               dtype=U8, device=dev)
         self.server = GpuServer(t, cap, max(cap * self.rep_max,
                                             W * (self.rep_slot - SEG_HDR))
-                                + 64, window=B.frame_window(self.req_max))
+                                + 64, window=B.frame_window(self.req_max),
+                                seq_order=False)
         # the replies to this connection's own n requests come back
         lo, hi = t.data_dist or (t.data_bytes, t.data_bytes)
         self.rscanner = B.FrameScanner(n, dev,

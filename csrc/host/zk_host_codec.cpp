@@ -9,6 +9,7 @@
 // per-packet memmove).
 #define PY_SSIZE_T_CLEAN
 #include <Python.h>
+#include <structmember.h>
 
 #include <cstdint>
 #include <cstring>
@@ -17,6 +18,10 @@
 namespace {
 
 PyObject* g_stat_cls = nullptr;     // zkmi.jute.Stat
+// the byte offsets of Stat's 11 __slots__ in field order (init): replies
+// build their Stat by filling the slots (g_stat_fast)
+Py_ssize_t g_stat_off[11];
+bool g_stat_fast = false;
 PyObject* g_decode_err = nullptr;   // zkmi.errors.ZKDecodeError
 
 // -- interned names -----------------------------------------------------------
@@ -134,6 +139,20 @@ struct Reader {
           i32(&cv) && i32(&av) && i64(&eo) && i32(&dl) && i32(&nc) &&
           i64(&pz)))
       return nullptr;
+    if (g_stat_fast) {
+      // the Stat's slots filled straight from here: no argument tuple and
+      // no Python __init__ frame (one per reply on the interactive path)
+      PyTypeObject* tp = (PyTypeObject*)g_stat_cls;
+      PyObject* o = tp->tp_alloc(tp, 0);
+      if (o == nullptr) return nullptr;
+      const long long f[11] = {cz, mz, ct, mt, v, cv, av, eo, dl, nc, pz};
+      for (int k = 0; k < 11; ++k) {
+        PyObject* x = PyLong_FromLongLong(f[k]);
+        if (x == nullptr) { Py_DECREF(o); return nullptr; }
+        *(PyObject**)((char*)o + g_stat_off[k]) = x;
+      }
+      return o;
+    }
     return PyObject_CallFunction(g_stat_cls, "LLLLiiiLiiL", (long long)cz,
                                  (long long)mz, (long long)ct, (long long)mt,
                                  v, cv, av, (long long)eo, dl, nc,
@@ -524,6 +543,20 @@ PyObject* init(PyObject*, PyObject* args) {
   Py_XDECREF(g_stat_cls);
   Py_INCREF(stat);
   g_stat_cls = stat;
+  static const char* fields[11] = {
+      "czxid", "mzxid", "ctime", "mtime", "version", "cversion", "aversion",
+      "ephemeralOwner", "dataLength", "numChildren", "pzxid"};
+  g_stat_fast = PyType_Check(stat);
+  for (int k = 0; k < 11 && g_stat_fast; ++k) {
+    PyObject* d = PyObject_GetAttrString(stat, fields[k]);
+    if (d == nullptr) { PyErr_Clear(); g_stat_fast = false; break; }
+    if (Py_TYPE(d) == &PyMemberDescr_Type &&
+        ((PyMemberDescrObject*)d)->d_member->type == T_OBJECT_EX)
+      g_stat_off[k] = ((PyMemberDescrObject*)d)->d_member->offset;
+    else
+      g_stat_fast = false;
+    Py_DECREF(d);
+  }
   if (derr) {
     Py_XDECREF(g_decode_err);
     Py_INCREF(derr);

@@ -30,6 +30,7 @@
 
 #include <cstdint>
 #include <ctime>
+#include <unordered_map>
 #include <vector>
 
 namespace {
@@ -261,6 +262,25 @@ void unsubscribe_others(Machine* m, PyObject* const* keep, int nk) {
   }
 }
 
+// The state names as interned str objects, made once per name: the
+// `state` getter (read on every data-API request: the client, session and
+// connection states) and stateChanged hand out these instead of a new str.
+PyObject* state_name(const Spec* sp, int st) {
+  static std::unordered_map<const char*, PyObject*>* cache = nullptr;
+  if (cache == nullptr) cache = new std::unordered_map<const char*, PyObject*>;
+  const char* k = sp->names[st];
+  auto it = cache->find(k);
+  if (it != cache->end()) {
+    Py_INCREF(it->second);
+    return it->second;
+  }
+  PyObject* o = PyUnicode_InternFromString(k);
+  if (o == nullptr) return nullptr;
+  Py_INCREF(o);                            // the cache's reference
+  cache->emplace(k, o);
+  return o;
+}
+
 // Enter state `st`: entry action, stateChanged, the owner's hook.
 void enter(Machine* m, int st) {
   m->state = st;
@@ -271,7 +291,7 @@ void enter(Machine* m, int st) {
   m->history->push_back(st);
   m->spec->enter(m, st);
   if (PyErr_Occurred()) report();
-  PyObject* name = PyUnicode_FromString(m->spec->names[st]);
+  PyObject* name = state_name(m->spec, st);
   if (name == nullptr) { report(); return; }
   PyObject* r = PyObject_CallMethod(m->owner, "emit", "sO", "stateChanged",
                                     name);
@@ -1238,7 +1258,7 @@ PyObject* Machine_in_state(Machine* m, PyObject* name) {
 
 PyObject* Machine_get_state(Machine* m, void*) {
   if (m->state < 0) Py_RETURN_NONE;
-  return PyUnicode_FromString(m->spec->names[m->state]);
+  return state_name(m->spec, m->state);
 }
 
 PyObject* Machine_get_history(Machine* m, void*) {

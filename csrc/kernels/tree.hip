@@ -42,6 +42,7 @@
 // write request is assigned a zxid, failed ones included (ZooKeeper logs an
 // error txn for them).
 #include "zk_common.h"
+#include "zk_mfma_scan.h"
 #include "zk_reqparse.h"
 
 namespace zk {
@@ -1741,13 +1742,23 @@ __global__ __launch_bounds__(NT) void tree_finish_k(ZkTree t,
 // kernels.  Workgroup 1 scans the serve's per-256-reply size sums (bsum,
 // nb of them) into the encoder's block bases and writes the stream total
 // (zk_encode_responses3 `prescanned`).
-template <int NT>
+// MFMA: workgroup 1 scans on the matrix cores (zk_mfma_scan.h: 2048 block
+// sums of a 512K-reply connection are one 4096-value chunk of four waves).
+template <int NT, bool MFMA>
 __global__ __launch_bounds__(NT) void tree_finish_scan_k(
     ZkTree t, const int64_t* n_dev, int64_t bump_zxid, int32_t publish,
     const int64_t* __restrict__ bsum, int64_t nb, int64_t* __restrict__ bbase,
     int64_t* __restrict__ total) {
   if (blockIdx.x == 0) {
     finish_body(t, n_dev, bump_zxid, publish);
+    return;
+  }
+  if (MFMA) {
+    __shared__ int64_t stage[ms_stage_slots<NT>()];
+    __shared__ int64_t wsum[NT / 64 + 1];
+    const int64_t tot = mfma_scan_block<int64_t, NT>(bsum, nb, bbase, stage,
+                                                     wsum);
+    if (threadIdx.x == 0) *total = tot;
     return;
   }
   __shared__ int64_t sm[NT / 64 + 1];
@@ -2154,8 +2165,12 @@ int zk_tree_finish_scan(const ZkTree* t, const int64_t* n_dev, int64_t bump,
                         int32_t publish, int64_t ncap, int64_t* scan_ws,
                         int64_t* total, hipStream_t st) {
   const int64_t nb = ncap > 0 ? (ncap + 255) / 256 : 0;
-  zk::tree_finish_scan_k<256><<<2, 256, 0, st>>>(
-      *t, n_dev, bump, publish, scan_ws, nb, scan_ws + nb, total);
+  if (zk_scan_small_mode() == 1)
+    zk::tree_finish_scan_k<256, true><<<2, 256, 0, st>>>(
+        *t, n_dev, bump, publish, scan_ws, nb, scan_ws + nb, total);
+  else
+    zk::tree_finish_scan_k<256, false><<<2, 256, 0, st>>>(
+        *t, n_dev, bump, publish, scan_ws, nb, scan_ws + nb, total);
   ZK_LAUNCH_CHECK();
   return 0;
 }

@@ -148,6 +148,11 @@ struct ZkSessionTable {
 // ---- launchers (stream-ordered; return 0 or a hipError_t) ----------------
 int64_t zk_scan_workspace(int64_t n);
 int zk_scan_set_mode(int mode);
+// engine of the one-workgroup scans (ZKMI_SMALL_SCAN): 1 MFMA, 0 shuffle
+int zk_scan_small_mode(void);
+// the one-workgroup exclusive scan with an explicit engine (1 MFMA, 0 shfl)
+int zk_scan_small_i64_mode(const int64_t*, int64_t*, int64_t, int64_t*, int,
+                           hipStream_t);
 int zk_scan_excl_i64(const int64_t*, int64_t*, int64_t, int64_t*, int64_t*,
                      hipStream_t);
 int zk_scan_excl_i32(const int32_t*, int64_t*, int64_t, int64_t*, int64_t*,

@@ -243,6 +243,18 @@ ZkSessionTable session_table(const std::vector<Tensor>& v, int64_t span) {
 int64_t scan_workspace(int64_t n) { return zk_scan_workspace(n); }
 int64_t serve_tickets(int64_t ncap) { return zk_serve_tickets(ncap); }
 int64_t scan_set_mode(int64_t m) { return zk_scan_set_mode((int)m); }
+int64_t scan_small_mode() { return zk_scan_small_mode(); }
+
+// the one-workgroup scan (K10 / K13 block sums) on a chosen engine
+void scan_small(const Tensor& x, const Tensor& base, const Tensor& total,
+                bool mfma) {
+  const int64_t n = x.numel();
+  hip_ok(zk_scan_small_i64_mode(P<int64_t>(x, I64, n, "x"),
+                                P<int64_t>(base, I64, n, "base", &x), n,
+                                P<int64_t>(total, I64, 1, "total", &x),
+                                mfma ? 1 : 0, cur_stream()),
+         "scan_small");
+}
 
 void scan_excl(const Tensor& x, const Tensor& base, const Tensor& total,
                const Tensor& ws) {
@@ -1004,6 +1016,9 @@ void session_install(const std::vector<Tensor>& tab, const Tensor& rec,
 TORCH_LIBRARY(zkmi, m) {
   m.def("scan_workspace(int n) -> int", &scan_workspace);
   m.def("scan_set_mode(int mode) -> int", &scan_set_mode);
+  m.def("scan_small_mode() -> int", &scan_small_mode);
+  m.def("scan_small(Tensor x, Tensor(a!) base, Tensor(b!) total, "
+        "bool mfma) -> ()", &scan_small);
   m.def("scan_excl(Tensor x, Tensor(a!) base, Tensor(b!) total, "
         "Tensor(c!) ws) -> ()", &scan_excl);
   m.def("encode_requests(Tensor[] batch, int n, Tensor(a!) sizes, "

@@ -326,3 +326,51 @@ def test_parallel_read_burst_matches_serial():
         return rep
     assert len(got[0]) == len(got[4])
     assert [norm(b) for b in got[0]] == [norm(b) for b in got[4]]
+
+
+def test_parallel_write_burst_matches_serial():
+    """A connection's burst of >= 1024 SET_DATAs on distinct paths (config
+    4's bulk write) is applied on the helper threads: lookups and checks in
+    parallel, zxids in request order, nodes updated and replies built in
+    chunks, watches fired in request order with one wake per watching
+    connection.  Its replies and the watcher's notifications must be the
+    serial server's, in order: version CAS hits and misses, missing nodes,
+    watched and unwatched paths."""
+    n = 3000
+    ops = []
+    for i in range(n):
+        p = leaf(i) if i % 97 else '/bench/missing%d' % i
+        ops.append({'opcode': 'SET_DATA', 'path': p, 'data': b'v%d' % i,
+                    'version': -1 if i % 5 else (0 if i % 2 else 3)})
+    reqs = b''.join(jute.frame(jute.encode_request(dict(o, xid=i + 1)))
+                    for i, o in enumerate(ops))
+    got, notes = {}, {}
+    for st in (0, 4):
+        srv = fast.FastZKServer(preload=n, data_bytes=8, fanout=FANOUT,
+                                serve_threads=st)
+        try:
+            w = Raw(srv.port)
+            for i in range(0, n, 3):
+                w.call(_get(leaf(i)))                 # data watch
+            got[st] = _read_burst(srv.port, reqs, n)
+            w.sync()
+            notes[st] = list(w.notes)
+            w.close()
+            t = srv.timing()
+        finally:
+            srv.shutdown()
+        assert (t['par_bursts'] > 0) == (st > 0), t
+    xmap = {i + 1: o['opcode'] for i, o in enumerate(ops)}
+
+    def norm(body):
+        rep = jute.decode_response(body, xmap)
+        st = rep.get('stat')
+        if st is not None:
+            rep['stat'] = (st.czxid, st.mzxid, st.version, st.dataLength)
+        return rep
+    a = [norm(b) for b in got[0]]
+    assert a == [norm(b) for b in got[4]]
+    errs = {r['err'] for r in a}
+    assert errs == {'OK', 'BAD_VERSION', 'NO_NODE'}, errs
+    assert notes[0] == notes[4]
+    assert len(notes[0]) > 500

@@ -11,8 +11,9 @@ from zkmi.ops import _lib
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=[_lib.SCAN_MFMA_W1, _lib.SCAN_MFMA_W4, _lib.SCAN_SHFL],
-                ids=['mfma_w1', 'mfma_w4', 'shfl'])
+@pytest.fixture(params=[_lib.SCAN_MFMA_W1, _lib.SCAN_MFMA_W4,
+                        _lib.SCAN_MFMA_FORCE, _lib.SCAN_SHFL],
+                ids=['mfma_w1', 'mfma_w4', 'mfma_force', 'shfl'])
 def mode(request, gpu):
     old = _lib.set_scan_mode(request.param)
     yield request.param
@@ -62,6 +63,46 @@ def test_scan_zero_and_sparse(mode, gpu):
     x[12346] = 256
     x[69999] = (1 << 24) + 1
     base, total = B.exclusive_scan(x.to(gpu))
+    ref, tot = _ref(x)
+    assert torch.equal(base.cpu(), ref)
+    assert int(total.item()) == tot
+
+
+@pytest.mark.parametrize('n', [2048, 16384, 65536])
+def test_scan_mfma_forced_small(gpu, n):
+    """The multi-block MFMA path forced below the one-workgroup threshold
+    (round 5's crash: the host recursed on one block forever): block
+    levels down to one block, each scanned on MFMA."""
+    from zkmi.ops import batch as B
+    old = _lib.set_scan_mode(_lib.SCAN_MFMA_FORCE)
+    try:
+        g = torch.Generator().manual_seed(n)
+        x = torch.randint(0, 50000, (n,), generator=g, dtype=torch.int64)
+        base, total = B.exclusive_scan(x.to(gpu))
+        ref, tot = _ref(x)
+        assert torch.equal(base.cpu(), ref)
+        assert int(total.item()) == tot
+    finally:
+        _lib.set_scan_mode(old)
+
+
+@pytest.mark.parametrize('mfma', [True, False], ids=['mfma', 'shfl'])
+@pytest.mark.parametrize('n', [1, 100, 2048, 2049, 4096, 16384, 65541])
+def test_scan_small_one_workgroup(gpu, n, mfma):
+    """The one-workgroup scan of the encoders' block sums (K10 / K13: 2048
+    of them per 512K-record connection of the GET step) on the MFMA
+    byte-plane engine and on the shuffle engine, against torch.cumsum;
+    values of 1-3 byte planes plus a few past 2^32 (the lane-serial path
+    of their wave)."""
+    L = _lib.lib()
+    g = torch.Generator().manual_seed(n + mfma)
+    x = torch.randint(0, 60000, (n,), generator=g, dtype=torch.int64)
+    if n > 1000:
+        x[777] = (1 << 33) + 5
+    xd = x.to(gpu)
+    base = torch.empty(n, dtype=torch.int64, device=gpu)
+    total = torch.empty(1, dtype=torch.int64, device=gpu)
+    L.scan_small(xd, base, total, mfma)
     ref, tot = _ref(x)
     assert torch.equal(base.cpu(), ref)
     assert int(total.item()) == tot

@@ -1379,6 +1379,13 @@ class StormPipeline(object):
         self.sessions = GpuSessionTable(tree, server_id=self.rank + 1,
                                         members=W)
         if W > 1:
+            # the current session of every member on the device (member m's
+            # k-th session is (m + 1) << 56 | k + 1, k = kdev): serve and
+            # expiry take theirs through the tree's TC_SESS word, so a
+            # captured step replays with the next generation's ids
+            self.sid_base = torch.tensor([(m + 1) << 56 for m in range(W)],
+                                         dtype=I64, device=dev)
+            self.sess_tab = torch.zeros(W, dtype=I64, device=dev)
             # this step's new sessions of every member ([W, 4] records),
             # the generation before's (expired at the next birth), and the
             # handshake slots
@@ -1508,7 +1515,6 @@ class StormPipeline(object):
             # (`outcome`: how this member answered the previous rank's
             # client — every member checks the one it served, the client
             # checks the answer it got)
-            self.stats['cross_rank_resumes'] += 1
             return o, bound, outcome, resp
         resp, bound, outcome = self.sessions.connect(
             self.cr_tx[:nbytes], nbytes, 0)
@@ -1518,18 +1524,25 @@ class StormPipeline(object):
 
     @property
     def capturable(self):
-        return self.world == 1
+        """One member, or an ensemble whose all-gathers run on RCCL on the
+        pipeline's device (a host backend cannot be captured)."""
+        if self.world == 1:
+            return True
+        return self.coll == self.dev and \
+            self.dist.get_backend(self.group) == 'nccl'
 
     def capture(self, acc):
         """Capture the steady state's two step shapes (a birth that expires
         the session before, a resume that also tries the expired one) as
         HIP graphs; ``replay()`` runs the next step.  Session ids live on
-        the device (``kdev`` -> the tree's TC_SESS word), so a replay serves,
-        expires and checks the next session; the host keeps only its
-        bookkeeping (counts).  One member only: the ensemble's steps
-        gather over the process group."""
-        if self.world > 1:
-            raise RuntimeError('storm capture: one member only')
+        the device (``kdev`` -> the tree's TC_SESS word; across members the
+        table of every member's current id), so a replay serves, expires
+        and checks the next session; the host keeps only its bookkeeping
+        (counts).  Across members the all-gathers are captured with the
+        rest (RCCL; see ``capturable``)."""
+        if not self.capturable:
+            raise RuntimeError('storm capture: the process group cannot be '
+                               'captured (host backend)')
         while self.step_no < 2 or self.step_no % 2:
             self.step(acc=acc)
         torch.cuda.synchronize(self.dev)
@@ -1555,6 +1568,9 @@ class StormPipeline(object):
         s = self.step_no
         self.step_no += 1
         resume = s % 2 == 1
+        if self.world > 1:
+            self.stats['replicated_writes'] += self.world * self.n
+            self.stats['cross_rank_resumes'] += int(resume)
         if resume:
             self.stats['resumed'] += 1
             self.stats['expired_resume_refused'] += int(self.k >= 1)
@@ -1576,6 +1592,8 @@ class StormPipeline(object):
         # ensemble passes host ids, see _replicated_run)
         sess_dev = t.counters[_lib.TC_SESS:_lib.TC_SESS + 1]
         torch.add(self.kdev, self.sid0, out=sess_dev)
+        if self.world > 1:
+            torch.add(self.sid_base, self.kdev + 1, out=self.sess_tab)
         o, bound, outcome, resp = self._handshake(resume)
         if resume:
             # current session back with the same id and password; the
@@ -1592,7 +1610,7 @@ class StormPipeline(object):
         else:
             # the id the server handed out: member r's k-th session
             want = sess_dev[0] if self.world == 1 else \
-                self.sid(self.rank, self.k)
+                self.sess_tab[self.rank]
             ok = ((o['status'][0] == 0) & (outcome[0] == _lib.SC_NEW) &
                   (o['sessionId'][0] == want) & (bound[0] == want))
             # credentials: the new session becomes current, the old one prev
@@ -1636,7 +1654,9 @@ class StormPipeline(object):
             # them created two batches
             self.removed.zero_()
             for m in range(self.world):
-                t.expire(self.sid(m, self.k - 1), self.removed)
+                # member m's session of the generation before
+                torch.sub(self.sess_tab[m:m + 1], 1, out=sess_dev)
+                t.expire(_lib.SESS_DEV, self.removed)
             self.sessions.close(self.prev_recs[:, 0].contiguous())
             expire_ok = self.removed[0] == 2 * n * self.world
         elif not resume and self.k >= 1:
@@ -1687,9 +1707,11 @@ class StormPipeline(object):
         # the client this member answers: its own, or after a move the
         # previous member's
         ans = (r - 1) % W if resume else r
+        sess_dev = self.tree.counters[_lib.TC_SESS:_lib.TC_SESS + 1]
         for m in range(W):
+            sess_dev.copy_(self.sess_tab[m:m + 1])
             rx, rtotal, _, _ = d.server.serve(
-                self.tx_all[m * S:(m + 1) * S], S, session=self.sid(m, self.k),
+                self.tx_all[m * S:(m + 1) * S], S, session=_lib.SESS_DEV,
                 ordered=d.passes > 0, passes=max(d.passes, 1))
             if m == ans:
                 R = self._stream_len(rtotal, 'rep_bytes')
@@ -1701,7 +1723,6 @@ class StormPipeline(object):
                     self.my_rx = torch.empty(R + 64, dtype=U8,
                                              device=self.dev)
                 self.rep_out[:R].copy_(rx[:R])
-        self.stats['replicated_writes'] += W * n
         R = self.rep_bytes
         if resume:
             # my answers come from the member my session moved to

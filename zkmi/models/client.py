@@ -431,8 +431,9 @@ class Client(FSM):
                       lambda pkt: cb(None, pkt['children'], pkt['stat']))
 
     def get(self, path, cb):
-        _check_str(path, 'path')
-        _check_func(cb)
+        if path.__class__ is not str or not callable(cb):
+            _check_str(path, 'path')
+            _check_func(cb)
         self._request({'opcode': 'GET_DATA', 'path': path, 'watch': False},
                       cb, lambda pkt: cb(None, pkt['data'], pkt['stat']))
 

@@ -15,6 +15,7 @@ table keyed by xid, and the xid->opcode map the reply decoder needs because
 ZooKeeper replies are not self-describing (SURVEY §7.4 hard part 1).
 """
 
+import operator
 import threading
 import time
 
@@ -41,9 +42,9 @@ class ZKRequest(EventEmitter):
     __slots__ = ('packet', 't_submit', 'fast')
 
     def __init__(self, packet):
-        EventEmitter.__init__(self)
+        self._listeners = {}
         self.packet = packet
-        self.t_submit = time.perf_counter()
+        self.t_submit = 0.0             # set when a tracer records it
         self.fast = None
 
     def then(self, on_reply, on_error):
@@ -218,10 +219,12 @@ class _ConnBase(object):
     def request(self, pkt, req=None):
         """Send ``pkt``; returns the request (``req``: an object with the
         ZKRequest surface the reply settles — the native watch engine's)."""
-        if not self.isInState('connected'):
+        if self._fsm_state != 'connected':
             raise Exception('Client must be connected to send requests')
         if req is None:
             req = ZKRequest(pkt)
+            if self.tracer is not None:
+                req.t_submit = time.perf_counter()
         with self.xid_lock:
             xid = self.xid
             self.xid = (xid + 1) & 0x7fffffff
@@ -803,7 +806,7 @@ class NativeZKConnectionFSM(_ConnBase, EventEmitter):
     def getState(self):
         return self._m.state
 
-    _fsm_state = property(getState)
+    _fsm_state = property(operator.attrgetter('_m.state'))
 
     def isInState(self, state):
         return self._m.in_state(state)

@@ -13,6 +13,7 @@ checked by one lazily re-armed timer, instead of a ``clearTimeout`` +
 SURVEY §7.1 "Expiry is a deadline, not a timer per packet").
 """
 
+import operator
 import os
 import random
 import re
@@ -587,7 +588,7 @@ class NativeZKSession(_SessionBase, EventEmitter):
     def getState(self):
         return self._m.state
 
-    _fsm_state = property(getState)
+    _fsm_state = property(operator.attrgetter('_m.state'))
 
     def isInState(self, state):
         return self._m.in_state(state)

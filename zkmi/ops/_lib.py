@@ -41,6 +41,7 @@ SESS_DEV = -2
 HT_WORDS = 8     # int64 words per hash entry: key, val, lengths, path head
 
 SCAN_SHFL, SCAN_MFMA, SCAN_MFMA_W1, SCAN_MFMA_W4 = 0, 1, 2, 3
+SCAN_MFMA_FORCE = 4      # the multi-block MFMA path at any n (tests)
 
 _ops = None
 

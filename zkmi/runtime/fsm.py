@@ -29,6 +29,7 @@ Semantics implemented (inferred from the reference's use):
     every transition (after ``stateChanged``).
 """
 
+import operator
 import os
 
 from .emitter import EventEmitter
@@ -203,9 +204,8 @@ class FSM(EventEmitter):
                           else PyCore(self, loop))
         self._fsm_core.request(initial)
 
-    @property
-    def _fsm_state(self):
-        return self._fsm_core.state
+    # (a C-level getter: read on every data-API request)
+    _fsm_state = property(operator.attrgetter('_fsm_core.state'))
 
     @property
     def fsm_history(self):

@@ -64,6 +64,8 @@ class NativeLoop(object):
                                '`python tools/build_native.py`')
         self.errors = []
         self._n = _zkloop.Loop(self._on_exception)
+        # (the C method itself: asked on every data-API request)
+        self.in_loop = self._n.in_loop
         self._thread = threading.Thread(target=self._main, name=name,
                                         daemon=True)
         started = threading.Event()

@@ -1012,7 +1012,7 @@ struct Worker {
   // must sit between this connection's replies) — returns false before
   // anything changed: the serial path serves the burst.  Round 5's config
   // 4 spent 51 ms of its 70.8 ms write phase (20 steps) here serially.
-  static constexpr size_t WPAR_MIN = 1024;
+  static constexpr size_t WPAR_MIN = 512;
   struct WJob {
     Node* nd;
     const uint8_t* d;
@@ -1037,7 +1037,7 @@ struct Worker {
     }
     const size_t nf = fr.size();
     if (nf < WPAR_MIN) return false;
-    const int K = std::min<int>(S->pool->size() + 1, (int)(nf / 256));
+    const int K = std::min<int>(S->pool->size() + 1, (int)(nf / 128));
     const uint8_t* base = (const uint8_t*)c.in.data() + c.in_off;
     const int64_t sid = c.sid;
     wj.resize(nf);
@@ -1120,11 +1120,13 @@ struct Worker {
       }
     }
     for (auto& kv : notes) {
+      bool was_empty;
       {
         std::lock_guard<std::mutex> g(kv.first->nmu);
+        was_empty = kv.first->notes.empty();
         kv.first->notes.append(kv.second);
       }
-      kv.first->w->wake(kv.first->fd);
+      if (was_empty) kv.first->w->wake(kv.first->fd);
     }
     for (auto& x : outs) c.out.append(x);
     c.in_off = o;
@@ -1254,11 +1256,16 @@ void Server::notify(int64_t sid, int32_t type, const std::string& path,
     c->out.append(f);
     return;
   }
+  // one wake per batch of notes: a connection whose notes are not empty
+  // has a wake pending since they last were (its worker drains them all
+  // under nmu) — a write burst firing 4096 watches made 4096 eventfd writes
+  bool was_empty;
   {
     std::lock_guard<std::mutex> g(c->nmu);
+    was_empty = c->notes.empty();
     c->notes.append(f);
   }
-  c->w->wake(c->fd);
+  if (was_empty) c->w->wake(c->fd);
 }
 
 // -- members and the fault channel (main thread) ------------------------------

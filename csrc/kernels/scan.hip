@@ -172,23 +172,24 @@ __global__ __launch_bounds__(NT) void scan_apply_mfma(
 // quickly beside the other connection's kernels.
 constexpr int SB_T_MFMA = 128;
 
-template <typename T, int NT = SB_T_MFMA>
+template <int NT = SB_T_MFMA>
 __global__ __launch_bounds__(NT) void scan_one_block_mfma(
-    const T* __restrict__ in, int64_t n, int64_t* __restrict__ out,
+    const int64_t* __restrict__ in, int64_t n, int64_t* __restrict__ out,
     int64_t* __restrict__ total) {
-  __shared__ int64_t stage[ms_stage_slots<NT>()];
   __shared__ int64_t wsum[NT / 64 + 1];
-  const int64_t t = mfma_scan_block<T, NT>(in, n, out, stage, wsum);
+  const int64_t t = mfma_scan_block_direct<NT>(in, n, out, wsum);
   if (total != nullptr && threadIdx.x == 0) *total = t;
 }
 
 // ZKMI_SMALL_SCAN: the engine of the one-workgroup scans (zk_scan_small_i64:
-// K10 / K13's block sums; tree_finish_scan): "mfma" (default) or "shfl".
+// K10 / K13's block sums; tree_finish_scan): "shfl" (default) or "mfma".
+// The MFMA version costs the GET step 2.6 % (profiles/r6_mfma_ab.md): a
+// 2048-value scan is latency, not arithmetic.
 static int small_scan_mode() {
   static int v = -1;
   if (v < 0) {
     const char* e = getenv("ZKMI_SMALL_SCAN");
-    v = (e != nullptr && e[0] == 's') ? 0 : 1;
+    v = (e != nullptr && e[0] == 'm') ? 1 : 0;
   }
   return v;
 }
@@ -302,8 +303,7 @@ int zk_scan_small_i64_mode(const int64_t* in, int64_t* out, int64_t n,
     return 0;
   }
   if (mode == 1)
-    zk::scan_one_block_mfma<int64_t><<<1, zk::SB_T_MFMA, 0, st>>>(in, n, out,
-                                                                   total);
+    zk::scan_one_block_mfma<><<<1, zk::SB_T_MFMA, 0, st>>>(in, n, out, total);
   else
     zk::launch_one_block<int64_t>(in, n, out, total, st);
   ZK_LAUNCH_CHECK();

@@ -783,6 +783,17 @@ ZK_DEV int64_t served_reply_size(int32_t op, int32_t err, int32_t dl,
   }
 }
 
+// The ordering pass's word for request i (zk_tree_seq_order): parent node
+// << 32 | its SEQUENTIAL number, -1 when it has none.
+ZK_DEV int32_t seq_num(const ZkTree& t, int64_t i) {
+  if (t.seqno == nullptr) return -1;
+  const int64_t x = t.seqno[i];
+  return x < 0 ? -1 : (int32_t)(uint32_t)x;
+}
+ZK_DEV int64_t seq_par(const ZkTree& t, int64_t i) {
+  return t.seqno == nullptr || t.seqno[i] < 0 ? -1 : t.seqno[i] >> 32;
+}
+
 // CREATE (lib/zk-buffer.js:97-136 request shape; semantics of the server the
 // reference talks to): parent must exist and not be ephemeral, ACL must be
 // non-empty, SEQUENTIAL appends the parent's cversion, EPHEMERAL records the
@@ -793,6 +804,10 @@ ZK_DEV int32_t do_create(const ZkTree& t, Lane& L, const uint8_t* data,
                          int64_t v, int64_t i) {
   const ZkNodeStore& s = t.store;
   const bool eph = L.flags & CF_EPHEMERAL, seq = L.flags & CF_SEQUENTIAL;
+  // a create the ordering pass numbered: the pass also counted it as its
+  // parent's child (one atomic per parent a batch, not one per create); if
+  // it fails, tree_serve_k takes the count back (seq_par)
+  const int32_t pre = seq ? seq_num(t, i) : -1;
   if (nacl <= 0) return ERR_INVALID_ACL;
   if (v < 0) return ERR_SYSTEM;                       // tree full
   const uint8_t* path = L.path;
@@ -815,7 +830,6 @@ ZK_DEV int32_t do_create(const ZkTree& t, Lane& L, const uint8_t* data,
   // number handed back).  Without one (no ordering pass, or a parent the
   // pass did not find) the parent's cversion is taken here, bumped in the
   // same atomic as its child count — unique, but in arrival order.
-  const int32_t pre = seq && t.seqno != nullptr ? t.seqno[i] : -1;
   const bool taken = seq && par >= 0 && pre < 0;
   const int32_t seqno = !seq || par < 0 ? 0
                         : pre >= 0      ? pre
@@ -843,14 +857,14 @@ ZK_DEV int32_t do_create(const ZkTree& t, Lane& L, const uint8_t* data,
   const int64_t ins = pre >= 0 ? tree_insert<true>(t, v, pd, npl, dl)
                                : tree_insert(t, v, pd, npl, dl);
   if (ins != v) {
-    if (taken) cn_add(t, par, 0, -1);   // the child was not made (the
-                                        // cversion it took stays: a gap)
+    // the child was not made (the cversion it took stays: a gap)
+    if (taken) cn_add(t, par, 0, -1);
     return ins == TREE_INSERT_TIMEOUT ? ERR_SYSTEM : ERR_NODE_EXISTS;
   }
   t.eph[v] = eph ? session : 0;
   if (par >= 0) {
     if (seq) {
-      if (!taken) cn_add(t, par, 0, 1);             // cversion: the pass
+      // (cversion and child count: taken above, or by the ordering pass)
       atomicMax((unsigned long long*)&t.pzxid[par], (unsigned long long)L.zx);
     } else {
       parent_touch(t, par, 1, true, L.zx);
@@ -876,7 +890,12 @@ ZK_DEV void finish_body(const ZkTree& t, const int64_t* n_dev,
                         int64_t bump_zxid, int32_t publish);
 ZK_DEV bool serve_last(unsigned* tickets);
 
-template <bool PARSE>
+// RO: a batch of reads only (GET_DATA / EXISTS; the GET pipeline's): no
+// node / storage claims, frees or dirty parents, so none of their five
+// block-wide ticket barriers per workgroup; any other op is answered
+// UNIMPLEMENTED.  (A run-time vote of the block for the same skip cost the
+// create storm 10 %; a template costs the write batches nothing.)
+template <bool PARSE, bool RO = false>
 __global__ __launch_bounds__(TR_T) void tree_serve_k(
     ZkTree t, const uint8_t* __restrict__ rx, ZkReqOut q,
     const int64_t* __restrict__ foff, const int32_t* __restrict__ flen,
@@ -942,14 +961,16 @@ __global__ __launch_bounds__(TR_T) void tree_serve_k(
                                 L.op == OP_DELETE);
   const int64_t zbase = t.counters[TC_ZXID];
   L.zx = write ? zbase + i + 1 : zbase;
-  const bool create = ok_req && L.op == OP_CREATE;
+  const bool create = !RO && ok_req && L.op == OP_CREATE;
   int64_t v = -1;
   int32_t npl = 0, cap = 0;
   if (create) {
     npl = L.pl + ((L.flags & CF_SEQUENTIAL) ? 10 : 0);
     cap = max(L.dl, 128);
   }
-  {
+  if (RO && ok_req && L.op != OP_GET_DATA && L.op != OP_EXISTS)
+    L.err = ERR_UNIMPLEMENTED;
+  if (!RO) {
     const int64_t pub = t.counters[TC_FREE_PUB];
     const int64_t h = block_ticket(&t.counters[TC_FREE_HEAD], create);
     if (create && h < pub) v = t.free_list[h % t.free_cap];
@@ -992,6 +1013,12 @@ __global__ __launch_bounds__(TR_T) void tree_serve_k(
   }
   // ---- phase B: the operation -------------------------------------------
   int64_t freed = -1;
+  // a SEQUENTIAL create the ordering pass numbered (and counted as its
+  // parent's child) that never reaches do_create — refused by the ordered
+  // passes, or out of arena — takes that child back below
+  // (the pass reads a frame's op, path and flags only: a frame it numbered
+  // that the full parse refuses is taken back here too)
+  bool numbered = !RO && live && seq_num(t, i) >= 0;
   if (ok_req && L.err == ERR_OK) {
     switch (L.op) {
       case OP_GET_DATA: case OP_EXISTS:
@@ -1035,6 +1062,7 @@ __global__ __launch_bounds__(TR_T) void tree_serve_k(
       case OP_CREATE:
         L.err = do_create(t, L, rx + rq.doff, rq.vc, session,
                           now_ms, v, i);
+        if (L.err == ERR_OK) numbered = false;      // the child is made
         if (L.err == ERR_OK && r_path_off != nullptr) {
           r_path_off[i] = t.node_path_off[v];
           r_path_len[i] = t.node_path_len[v];
@@ -1072,6 +1100,7 @@ __global__ __launch_bounds__(TR_T) void tree_serve_k(
         L.err = ERR_UNIMPLEMENTED;
     }
   }
+  if (numbered) cn_add(t, seq_par(t, i), 0, -1);
   // ---- watches: reads with watch=1 arm (this session's slot), successful
   // writes fire (lib/zk-session.js:558-574 is the client side of the
   // trigger table; the server rules are SURVEY Appendix D)
@@ -1127,9 +1156,12 @@ __global__ __launch_bounds__(TR_T) void tree_serve_k(
   // ---- phase C: wave-aggregated frees and dirty parents -----------------
   if (create && L.err != ERR_OK && v >= 0) freed = v;  // return the claim
   // (A read-only block could skip these claims, but guarding them with a
-  // block vote cost the create storm 10% in measurement; they stay.)
-  wave_free(t, freed);
-  wave_mark_dirty(t, L.err == ERR_OK ? L.par : -1);
+  // block vote cost the create storm 10% in measurement; they stay, except
+  // in the RO instance.)
+  if (!RO) {
+    wave_free(t, freed);
+    wave_mark_dirty(t, L.err == ERR_OK ? L.par : -1);
+  }
   if (r_sizes != nullptr) {                       // block-uniform
     __shared__ int64_t sm[TR_T / 64 + 1];
     int64_t sz = 0;
@@ -1416,7 +1448,6 @@ __global__ __launch_bounds__(TR_T) void ord_rank_k(int64_t ncap, OrderWs w,
 // workgroup while the others spun on them: 134 us of the storm's 1M-create
 // step in seq_group_k alone.)
 constexpr int SQ_C = 1024;                 // requests per chunk (workgroup)
-constexpr uint64_t SQ_NONE = ~0ull;
 constexpr int64_t SQ_MAX = 1 << 24;        // requests a batch
 
 struct SeqWs {
@@ -1426,6 +1457,7 @@ struct SeqWs {
   uint16_t* pp;       // [h * mw] popcount of the bitmap words before
   int64_t* goff;      // [h] group -> its first count slot
   int32_t* gbase;     // [h] group -> parent cversion before the batch (-1)
+  int32_t* gpar;      // [h] group -> its parent node
   int32_t* rep;       // [h] group -> one of its requests
   int32_t* glist;     // [ncap] the batch's group slots
   int32_t* cnts;      // [ncap] chunk counts, then their group prefixes
@@ -1437,26 +1469,48 @@ struct SeqWs {
   int32_t mw;         // bitmap words per group (<= SQ_MW)
 };
 
-// The parent path of a well-formed SEQUENTIAL create frame ([p, p + cut));
-// cut 0 for anything else (a root child has no parent node either).
+// The parent path of a SEQUENTIAL create frame ([p, p + cut)); cut 0 for
+// anything else (a root child has no parent node either).  Only what the
+// numbering needs is read — the op, the path and the flags, the frame's
+// last word — in three dependent loads, not the full parse's walk of the
+// data and ACL (whose many dependent loads, a million frames in flight,
+// re-fetched the stream's lines ~3x: 300 MB for an 83 MB batch).  A frame
+// the serve's full parse then refuses is un-numbered there (tree_serve_k).
 ZK_DEV int32_t seq_parent(const uint8_t* rx, int64_t off, int32_t len,
                           const uint8_t** p) {
-  const ReqFields rq = parse_request(rx, off, len);
-  if (rq.status != ST_OK || rq.op != OP_CREATE || !(rq.arg & CF_SEQUENTIAL))
+  if (len < 28) return 0;            // xid op path(4) data(4) acl(4) flags
+  const uint8_t* b = rx + off;
+  uint32_t h[3];
+  __builtin_memcpy(h, b, 12);
+  const int32_t pl = (int32_t)bswap32(h[2]);
+  if ((int32_t)bswap32(h[1]) != OP_CREATE || pl < 2 || 12 + pl + 12 > len)
     return 0;
-  *p = rx + rq.poff;
-  int32_t cut = rq.pl - 1;
+  if (!(ld_be32(b + len - 4) & CF_SEQUENTIAL)) return 0;
+  *p = b + 12;
+  int32_t cut = pl - 1;
   while (cut > 0 && (*p)[cut] != '/') --cut;
   return cut;
 }
 
+// Within the chunk, each request's rank among the chunk's requests of its
+// group (in lane = stream order) and each group's count, without a sort:
+// the group slots get chunk-local dense ids through an LDS hash, a wave
+// finds each lane's peers (same id) with one ballot per distinct id, and
+// per-wave counts cnt[wave][id] in LDS give the count of the waves before.
+// Four barriers; a bitonic sort of the chunk's 1024 (slot, lane) pairs
+// took 75 barrier stages: 44 us a launch with nothing to sort, 145 us for
+// the storm's 1M creates.
+constexpr int SQ_W = SQ_C / 64;              // waves a chunk
+constexpr int SQ_LH = 2 * SQ_C;              // LDS hash slots
 __global__ __launch_bounds__(SQ_C) void seq_group_k(
     const uint8_t* __restrict__ rx, const int64_t* __restrict__ foff,
     const int32_t* __restrict__ flen, const int64_t* __restrict__ n_dev,
     int64_t ncap, SeqWs w) {
-  __shared__ uint64_t sk[SQ_C];
-  __shared__ int32_t hs[SQ_C];
-  const int tid = threadIdx.x;
+  __shared__ int32_t lkey[SQ_LH];            // group slot e (-1 empty)
+  __shared__ int32_t lid[SQ_LH];             // its chunk-local dense id
+  __shared__ uint16_t cnt[SQ_W][SQ_C];       // [wave][dense id] counts
+  __shared__ int32_t ndense;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int64_t c = blockIdx.x;
   const int64_t i = c * SQ_C + tid;
   const bool in = i < ncap && i < *n_dev;
@@ -1469,8 +1523,8 @@ __global__ __launch_bounds__(SQ_C) void seq_group_k(
       const int64_t key = (int64_t)(path_hash(p, cut) | 1ull);
       int64_t s = key & w.hmask;
       for (int64_t probe = 0; probe <= w.hmask; ++probe) {
-        int64_t k = __hip_atomic_load(&w.key[s], __ATOMIC_RELAXED,
-                                      __HIP_MEMORY_SCOPE_AGENT);
+        // a plain load first (a stale 0 only means the CAS answers)
+        int64_t k = w.key[s];
         if (k == 0)
           k = (int64_t)atomicCAS((unsigned long long*)&w.key[s], 0ull,
                                  (unsigned long long)key);
@@ -1490,40 +1544,56 @@ __global__ __launch_bounds__(SQ_C) void seq_group_k(
     w.glist[k] = (int32_t)e;
     w.rep[e] = (int32_t)i;
   }
-  // (slot, lane) sorted in LDS: a group's requests of the chunk come out
-  // together, in lane (= stream) order
-  sk[tid] = e >= 0 ? ((uint64_t)e << 10) | (uint64_t)tid : SQ_NONE;
+  if (!__syncthreads_or(e >= 0)) return;     // (block-uniform)
+  // 1. chunk-local dense ids
+  for (int x = tid; x < SQ_LH; x += SQ_C) lkey[x] = -1;
+  for (int x = tid; x < SQ_C * SQ_W / 2; x += SQ_C)
+    reinterpret_cast<uint32_t*>(&cnt[0][0])[x] = 0;   // (uint16 pairs)
+  if (tid == 0) ndense = 0;
   __syncthreads();
-  for (int kb = 2; kb <= SQ_C; kb <<= 1) {
-    for (int j = kb >> 1; j > 0; j >>= 1) {
-      const int q = tid ^ j;
-      if (q > tid) {
-        const uint64_t a = sk[tid], b = sk[q];
-        if ((a > b) == ((tid & kb) == 0)) {
-          sk[tid] = b;
-          sk[q] = a;
-        }
+  int ls = -1;
+  if (e >= 0) {
+    const int32_t ek = (int32_t)e;
+    ls = (int)(((uint32_t)ek * 2654435761u) >> 21) & (SQ_LH - 1);
+    for (;;) {
+      const int32_t o = atomicCAS(&lkey[ls], -1, ek);
+      if (o == -1) {
+        lid[ls] = atomicAdd(&ndense, 1);
+        break;
       }
-      __syncthreads();
+      if (o == ek) break;
+      ls = (ls + 1) & (SQ_LH - 1);
     }
   }
-  const uint64_t v = sk[tid];
-  const uint64_t gv = v >> 10;
-  const bool valid = v != SQ_NONE;
-  hs[tid] = valid && (tid == 0 || (sk[tid - 1] >> 10) != gv) ? tid : 0;
   __syncthreads();
-  for (int d = 1; d < SQ_C; d <<= 1) {          // segment starts: max-scan
-    const int32_t x = tid >= d ? hs[tid - d] : 0;
-    __syncthreads();
-    if (x > hs[tid]) hs[tid] = x;
-    __syncthreads();
+  const int d = e >= 0 ? lid[ls] : -1;
+  // 2. peers in the wave: one ballot per distinct id
+  uint64_t peers = 0;
+  uint64_t todo = __ballot(d >= 0);
+  while (todo) {
+    const int src = __ffsll((unsigned long long)todo) - 1;
+    const int dk = __shfl(d, src, 64);
+    const uint64_t m = __ballot(d == dk);
+    if (d == dk) peers = m;
+    todo &= ~m;
   }
-  if (valid) {
-    const int32_t st = hs[tid];
-    w.rin[c * SQ_C + (int64_t)(v & 1023u)] = tid - st;
-    if (tid == SQ_C - 1 || (sk[tid + 1] >> 10) != gv) {     // segment end
-      w.lcnt[c * SQ_C + (int64_t)(sk[st] & 1023u)] = tid - st + 1;
-      atomicOr((unsigned long long*)&w.mask[(int64_t)gv * w.mw + (c >> 6)],
+  const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+  const int rw = __popcll(peers & below);
+  if (d >= 0 && rw == 0) cnt[wv][d] = (uint16_t)__popcll(peers);
+  __syncthreads();
+  // 3. the waves before, the chunk's count (its first request leads)
+  if (d >= 0) {
+    int pre = 0, tot = 0;
+#pragma unroll
+    for (int x = 0; x < SQ_W; ++x) {
+      const int v = cnt[x][d];
+      pre += x < wv ? v : 0;
+      tot += v;
+    }
+    w.rin[i] = pre + rw;
+    if (pre + rw == 0) {
+      w.lcnt[i] = tot;
+      atomicOr((unsigned long long*)&w.mask[e * w.mw + (c >> 6)],
                1ull << (c & 63));
     }
   }
@@ -1595,9 +1665,12 @@ __global__ __launch_bounds__(TR_T) void seq_scan_k(
       const uint8_t* p = nullptr;
       const int32_t cut = seq_parent(rx, foff[r], flen[r], &p);
       const int64_t par = cut > 0 ? tree_find(t, p, cut) : -1;
+      // cversion and numChildren move by the group's size in one atomic
+      // (the serve takes a failed create's child back)
       if (par >= 0 && t.eph[par] == 0)
-        base = cn_cver(cn_add(t, par, (int32_t)run, 0));
+        base = cn_cver(cn_add(t, par, (int32_t)run, (int32_t)run));
       w.gbase[e] = base;
+      w.gpar[e] = (int32_t)par;
       w.key[e] = 0;
     }
     for (int k = lane; k < w.mw; k += 64) m[k] = 0;
@@ -1605,14 +1678,15 @@ __global__ __launch_bounds__(TR_T) void seq_scan_k(
 }
 
 __global__ __launch_bounds__(TR_T) void seq_out_k(int64_t ncap, SeqWs w,
-                                                  int32_t* __restrict__ seqno) {
+                                                  int64_t* __restrict__ seqno) {
   const int64_t i = (int64_t)blockIdx.x * TR_T + threadIdx.x;
   if (i >= ncap) return;
   const int64_t e = w.gid[i];
-  int32_t s = -1;
+  int64_t s = -1;
   if (e >= 0) {
     const int32_t b = w.gbase[e];
-    if (b >= 0) s = b + w.cnts[w.goff[e] + w.kk[i]] + w.rin[i];
+    const int32_t x = b >= 0 ? b + w.cnts[w.goff[e] + w.kk[i]] + w.rin[i] : -1;
+    if (x >= 0) s = ((int64_t)w.gpar[e] << 32) | (uint32_t)x;
   }
   seqno[i] = s;
 }
@@ -1754,10 +1828,8 @@ __global__ __launch_bounds__(NT) void tree_finish_scan_k(
     return;
   }
   if (MFMA) {
-    __shared__ int64_t stage[ms_stage_slots<NT>()];
     __shared__ int64_t wsum[NT / 64 + 1];
-    const int64_t tot = mfma_scan_block<int64_t, NT>(bsum, nb, bbase, stage,
-                                                     wsum);
+    const int64_t tot = mfma_scan_block_direct<NT>(bsum, nb, bbase, wsum);
     if (threadIdx.x == 0) *total = tot;
     return;
   }
@@ -2110,8 +2182,9 @@ int64_t zk_serve_tickets(int64_t ncap) {
   return 1 + (nb + 63) / 64;
 }
 
-// finish = 0: no finish at all (the caller launches zk_tree_finish, e.g. on
-// a side stream joined before the tree's next batch)
+// finish: ZK_SERVE_FINISH (else no finish at all: the caller launches
+// zk_tree_finish or zk_tree_finish_scan) | ZK_SERVE_RO (a batch of GET_DATA
+// / EXISTS only: tree_serve_k's RO instance)
 int zk_tree_serve_frames2(const ZkTree* t, const uint8_t* rx,
                           const int64_t* foff, const int32_t* flen,
                           const int64_t* n_dev, int64_t ncap, int32_t* r_op,
@@ -2124,15 +2197,22 @@ int zk_tree_serve_frames2(const ZkTree* t, const uint8_t* rx,
   if (ncap <= 0) return 0;
   if ((r_sizes == nullptr) != (r_bsum == nullptr)) return -1;
   ZkReqOut none{};
-  zk::tree_serve_k<true><<<(unsigned)((ncap + zk::TR_T - 1) / zk::TR_T),
-                           zk::TR_T, 0, st>>>(
-      *t, rx, none, foff, flen, n_dev, ncap, r_op, r_xid, r_err, r_node,
-      r_zxid, r_path_off, r_path_len, r_slot, r_sizes, r_bsum, session,
-      now_ms, nullptr, 0, 1, 0, 0, nullptr, wslot, fired, tickets);
+  const unsigned nb = (unsigned)((ncap + zk::TR_T - 1) / zk::TR_T);
+  if (finish & ZK_SERVE_RO)
+    zk::tree_serve_k<true, true><<<nb, zk::TR_T, 0, st>>>(
+        *t, rx, none, foff, flen, n_dev, ncap, r_op, r_xid, r_err, r_node,
+        r_zxid, r_path_off, r_path_len, r_slot, r_sizes, r_bsum, session,
+        now_ms, nullptr, 0, 1, 0, 0, nullptr, wslot, fired, tickets);
+  else
+    zk::tree_serve_k<true><<<nb, zk::TR_T, 0, st>>>(
+        *t, rx, none, foff, flen, n_dev, ncap, r_op, r_xid, r_err, r_node,
+        r_zxid, r_path_off, r_path_len, r_slot, r_sizes, r_bsum, session,
+        now_ms, nullptr, 0, 1, 0, 0, nullptr, wslot, fired, tickets);
   ZK_LAUNCH_CHECK();
   // tickets: the serve launch's last workgroup did the finish
-  return tickets != nullptr || !finish ? 0
-                                       : finish_launch(t, ncap, n_dev, 0, st);
+  return tickets != nullptr || !(finish & ZK_SERVE_FINISH)
+             ? 0
+             : finish_launch(t, ncap, n_dev, 0, st);
 }
 
 int zk_tree_serve_frames(const ZkTree* t, const uint8_t* rx,
@@ -2147,7 +2227,7 @@ int zk_tree_serve_frames(const ZkTree* t, const uint8_t* rx,
   return zk_tree_serve_frames2(t, rx, foff, flen, n_dev, ncap, r_op, r_xid,
                                r_err, r_node, r_zxid, r_path_off, r_path_len,
                                r_slot, r_sizes, r_bsum, session, now_ms, wslot,
-                               fired, tickets, 1, st);
+                               fired, tickets, ZK_SERVE_FINISH, st);
 }
 
 // The between-batch finish of a serve (parent Stat fix-up, free-ring
@@ -2321,6 +2401,8 @@ static int64_t seq_layout(int64_t ncap, uint8_t* ws, zk::SeqWs* w,
   o += h * 4;
   if (w != nullptr) w->rep = (int32_t*)at(o);
   o += h * 4;
+  if (w != nullptr) w->gpar = (int32_t*)at(o);
+  o += h * 4;
   int32_t** arr[] = {w ? &w->glist : nullptr, w ? &w->cnts : nullptr,
                      w ? &w->gid : nullptr,   w ? &w->rin : nullptr,
                      w ? &w->lcnt : nullptr,  w ? &w->kk : nullptr};
@@ -2342,11 +2424,12 @@ int64_t zk_tree_seq_zeroed(int64_t ncap) {
 }
 
 // SEQUENTIAL numbers of the batch's create frames (foff / flen, *n_dev of
-// them) in stream order -> seqno[ncap] (-1: none); see seq_* above.  Run
+// them) in stream order -> seqno[ncap] (parent node << 32 | number; -1:
+// none); see seq_* above.  Run
 // it before the serve of the same frames, with t->seqno = seqno there.
 int zk_tree_seq_order(const ZkTree* t, const uint8_t* rx, const int64_t* foff,
                       const int32_t* flen, const int64_t* n_dev, int64_t ncap,
-                      uint8_t* ws, int64_t ws_bytes, int32_t* seqno,
+                      uint8_t* ws, int64_t ws_bytes, int64_t* seqno,
                       hipStream_t st) {
   if (ncap <= 0) return 0;
   if (ncap > zk::SQ_MAX) return -1;

@@ -125,10 +125,11 @@ struct ZkTree {
   int64_t* wt_key;             // [wt_hmask + 1] path hash | 1, 0 = empty
   unsigned long long* wt_mask; // [2 * (wt_hmask + 1)] data / child masks
   int64_t wt_hmask;
-  // [ncap] per request of the batch being served: its SEQUENTIAL number,
-  // assigned in stream order by zk_tree_seq_order (-1: none; the serve then
-  // takes the parent's cversion atomically).  Null: no request has one.
-  const int32_t* seqno;
+  // [ncap] per request of the batch being served: its parent node << 32 |
+  // its SEQUENTIAL number, assigned in stream order by zk_tree_seq_order
+  // (-1: none; the serve then takes the parent's cversion atomically).
+  // Null: no request has one.
+  const int64_t* seqno;
 };
 
 // Server-side session table (session.hip, K9 server mode).
@@ -229,6 +230,9 @@ int zk_tree_serve_frames2(const ZkTree*, const uint8_t*, const int64_t*,
                           int32_t*, int64_t*, int64_t*, int64_t*, int64_t,
                           int64_t, int32_t, int64_t*, unsigned*, int32_t,
                           hipStream_t);
+// zk_tree_serve_frames2's last flag word
+#define ZK_SERVE_FINISH 1
+#define ZK_SERVE_RO 2
 int zk_tree_finish(const ZkTree*, const int64_t*, int64_t, int32_t,
                    hipStream_t);
 int zk_tree_finish_scan(const ZkTree*, const int64_t*, int64_t, int32_t,
@@ -258,7 +262,7 @@ int64_t zk_tree_seq_workspace(int64_t ncap);
 int64_t zk_tree_seq_zeroed(int64_t ncap);
 int zk_tree_seq_order(const ZkTree*, const uint8_t*, const int64_t*,
                       const int32_t*, const int64_t*, int64_t, uint8_t*,
-                      int64_t, int32_t*, hipStream_t);
+                      int64_t, int64_t*, hipStream_t);
 // order-independent digest of the live nodes: out[0] = sum of per-node
 // hashes (path, czxid, mzxid, version, cversion, numChildren, owner, pzxid,
 // data), out[1] = live nodes, out[2] = hash entries in use (live +

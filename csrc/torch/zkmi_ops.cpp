@@ -614,11 +614,11 @@ void tree_serve_frames(const std::vector<Tensor>& t, const Tensor& rx,
                        int64_t now_ms, int64_t wslot,
                        const c10::optional<Tensor>& fired,
                        const c10::optional<Tensor>& tickets, bool finish,
-                       const c10::optional<Tensor>& seqno) {
+                       const c10::optional<Tensor>& seqno, bool read_only) {
   ZkTree s = tree(t);
   const Tensor* d = &t[0];
   need(r, 10, "serve outputs");
-  s.seqno = Popt<int32_t>(seqno, I32, ncap, "seqno", d);
+  s.seqno = Popt<int64_t>(seqno, I64, ncap, "seqno", d);
   TORCH_CHECK(wslot >= -1 && wslot < 64, "zkmi: watcher slot -1..63");
   const int64_t nb = (ncap + 255) / 256;
   hip_ok(zk_tree_serve_frames2(
@@ -639,7 +639,8 @@ void tree_serve_frames(const std::vector<Tensor>& t, const Tensor& rx,
              (int32_t)wslot, Popt<int64_t>(fired, I64, 5 * ncap, "fired", d),
              reinterpret_cast<unsigned*>(Popt<int32_t>(
                  tickets, I32, zk_serve_tickets(ncap), "tickets", d)),
-             finish ? 1 : 0, cur_stream()),
+             (finish ? ZK_SERVE_FINISH : 0) | (read_only ? ZK_SERVE_RO : 0),
+             cur_stream()),
          "tree_serve_frames");
 }
 
@@ -678,7 +679,7 @@ void tree_serve_ordered(const std::vector<Tensor>& t, const Tensor& rx,
   TORCH_CHECK(wslot >= -1 && wslot < 64, "zkmi: watcher slot -1..63");
   ZkTree s = tree(t);
   const Tensor* d = &t[0];
-  s.seqno = Popt<int32_t>(seqno, I32, ncap, "seqno", d);
+  s.seqno = Popt<int64_t>(seqno, I64, ncap, "seqno", d);
   ZkReqOut qo = req_out(q, ncap, d);
   need(r, 10, "serve outputs");
   TORCH_CHECK(passes >= 1 && passes <= 127, "zkmi: passes in 1..127");
@@ -762,7 +763,7 @@ void watch_resume(const std::vector<Tensor>& t, const Tensor& rx,
 
 // SEQUENTIAL numbers in stream order (tree.hip seq_*): workspace bytes for
 // ncap requests (zero the first tree_seq_zeroed(ncap) once), then per batch
-// the ordering of the request frames -> seqno (int32 [ncap]) for the serve.
+// the ordering of the request frames -> seqno (int64 [ncap]) for the serve.
 int64_t tree_seq_workspace(int64_t n) {
   TORCH_CHECK(n >= 0, "zkmi: tree_seq_workspace n");
   return zk_tree_seq_workspace(n);
@@ -786,7 +787,7 @@ void tree_seq_order(const std::vector<Tensor>& t, const Tensor& rx,
              P<int64_t>(n_dev, I64, 1, "count", d), ncap,
              P<uint8_t>(ws, U8, zk_tree_seq_workspace(ncap), "seq workspace",
                         d),
-             ws.numel(), P<int32_t>(seqno, I32, ncap, "seqno", d),
+             ws.numel(), P<int64_t>(seqno, I64, ncap, "seqno", d),
              cur_stream()),
          "tree_seq_order");
 }
@@ -1085,8 +1086,8 @@ TORCH_LIBRARY(zkmi, m) {
   m.def("tree_serve_frames(Tensor(a!)[] tree, Tensor rx, Tensor frame_off, "
         "Tensor frame_len, Tensor count, int ncap, Tensor(b!)[] out, "
         "int session, int now_ms, int wslot=-1, Tensor(c!)? fired=None, "
-        "Tensor(d!)? tickets=None, bool finish=True, Tensor? seqno=None) "
-        "-> ()", &tree_serve_frames);
+        "Tensor(d!)? tickets=None, bool finish=True, Tensor? seqno=None, "
+        "bool read_only=False) -> ()", &tree_serve_frames);
   m.def("tree_finish(Tensor(a!)[] tree, Tensor? count, int bump=0, "
         "bool publish=True) -> ()", &tree_finish);
   m.def("tree_order_workspace(int n) -> int", &tree_order_workspace);

@@ -329,7 +329,7 @@ def test_parallel_read_burst_matches_serial():
 
 
 def test_parallel_write_burst_matches_serial():
-    """A connection's burst of >= 1024 SET_DATAs on distinct paths (config
+    """A connection's burst of >= 512 SET_DATAs on distinct paths (config
     4's bulk write) is applied on the helper threads: lookups and checks in
     parallel, zxids in request order, nodes updated and replies built in
     chunks, watches fired in request order with one wake per watching

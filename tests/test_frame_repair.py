@@ -297,3 +297,41 @@ def test_dense_length_words_walk_the_candidates(gpu, group):
     print('group %d: random payloads %.3f ms, length words %.3f ms %r'
           % (group, ms_r, ms_p, st))
     assert ms_p < 8.0, (ms_p, ms_r, st)
+
+
+def test_big_repair_beside_another_connection(gpu):
+    """The grid-barrier repair (every tile without a speculated entry)
+    while another connection's GET steps fill the GPU on a second stream:
+    fs_link's 16 workgroups wait in their barrier for the ones still
+    queued behind the other stream's kernels, which drain in microseconds;
+    the scan stays exact and far below the barrier's 0.5 s abandon (no
+    fallback to the serial repair)."""
+    from zkmi.bench.synthetic import GpuTree, GetPipeline
+    rng = np.random.default_rng(29)
+    lens = rng.integers(88, 1113, 60000)
+    buf, starts = _stream(rng, lens)
+    dev = torch.device('cuda', 0)
+    d = torch.from_numpy(buf).to(dev)
+    sc = B.FrameScanner(len(lens) + 16, dev, window=2048)
+    sc.scan(d, len(buf), nospec=True)                   # warm
+    tree = GpuTree(100_000, 100, fanout=100, device=dev)
+    pipe = GetPipeline(tree, 1 << 18)
+    pipe.step()
+    torch.cuda.synchronize()
+    other = torch.cuda.Stream(dev)
+    worst = 0.0
+    for _ in range(3):
+        with torch.cuda.stream(other):
+            for _ in range(12):
+                pipe.step()
+        t0 = torch.cuda.Event(enable_timing=True)
+        t1 = torch.cuda.Event(enable_timing=True)
+        t0.record()
+        ft = sc.scan(d, len(buf), nospec=True)
+        t1.record()
+        torch.cuda.synchronize()
+        worst = max(worst, t0.elapsed_time(t1))
+        r = ft.host_result()
+        off = ft.off[:min(r['frames'], len(lens))].cpu().numpy()
+        _check(r, off, buf, starts)
+    assert worst < 20.0, worst

@@ -896,11 +896,12 @@ def test_gpu_sequential_names_in_stream_order(gpu, n, nparents):
              'acl': jute.DEFAULT_ACL, 'flags': []}
             for d, p in enumerate(parents)], gpu)
         assert all(r['err'] == 'OK' for r in reps)
-    base = {}
+    base, kids0 = {}, {}
     for p in parents:
         st = _serve_decode(srv, [{'xid': 1, 'opcode': 'EXISTS', 'path': p,
                                   'watch': False}], gpu)[0]['stat']
         base[p] = st.cversion
+        kids0[p] = st.numChildren
     for rnd in range(2):
         pk = _seq_batch(parents, n, xid0=rnd * n)
         reps = _serve_decode(srv, pk, gpu, session=0x77)
@@ -918,6 +919,7 @@ def test_gpu_sequential_names_in_stream_order(gpu, n, nparents):
     st = _serve_decode(srv, [{'xid': 9, 'opcode': 'EXISTS', 'path': p,
                               'watch': False}], gpu)[0]['stat']
     assert st.cversion == base[p]
+    assert st.numChildren == kids0[p] + 2 * rank[p]
 
 
 def test_gpu_sequential_replicas_agree(gpu):
@@ -949,6 +951,11 @@ def test_gpu_sequential_replicas_agree(gpu):
     # the next batch numbers after the whole first one (100 creates a
     # parent: cversion 100 -> 200)
     assert names[4000] == '/bench/d000000/s-%010d' % 200
+    # the failed create's child count was taken back: 100 + 99 + 100
+    st = _serve_decode(srvs[0], [{'xid': 9999, 'opcode': 'EXISTS',
+                                  'path': parents[0], 'watch': False}],
+                       gpu)[0]['stat']
+    assert st.numChildren == 299 and st.cversion == 300
 
 
 def test_gpu_expiry_reclaims_tombstones(gpu):

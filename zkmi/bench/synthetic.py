@@ -47,6 +47,9 @@ _SERVE_TICKETS = os.environ.get('ZKMI_SERVE_TICKETS', '0') == '1'
 # through the LDS image (uniform 0-200 B 0.710 -> 0.972 ms,
 # profiles/r5_get_stage_ab.log): off.
 _GET_STAGE = int(os.environ.get('ZKMI_GET_STAGE', '0'))
+# ZKMI_SERVE_RO=0: the GET pipelines serve with the general serve kernel
+# instead of its read-only instance
+_SERVE_RO = os.environ.get('ZKMI_SERVE_RO', '1') == '1'
 # ZKMI_FREE_COMPACT=0: no free-ring compaction after write batches (trees
 # built with compact_free=True; GpuTree.free_compact)
 _FREE_COMPACT = os.environ.get('ZKMI_FREE_COMPACT', '1') == '1'
@@ -373,6 +376,10 @@ class GpuServer(object):
         self.seq_order = seq_order and cap_frames <= _SEQ_MAX
         self.seq_ws = None
         self.seqno = None
+        # batches of GET_DATA / EXISTS only (the GET pipeline): the serve's
+        # read-only instance (no claim / free / dirty-parent barriers; any
+        # other op is refused UNIMPLEMENTED)
+        self.read_only = False
         dev = tree.device
         self.rt = B.alloc_request_table(cap_frames, dev)
         # CREATE replies carry the created path from the tree's arena
@@ -539,7 +546,7 @@ class GpuServer(object):
                                 wslot, self.fired if self.tree.watch
                                 is not None else None,
                                 self.tickets if _SERVE_TICKETS else None,
-                                not fuse, seqno)
+                                not fuse, seqno, self.read_only)
             if fuse:
                 # the finish and K13's block-sum scan: one launch
                 L.tree_finish_scan(self.tree.tensors, ft.count, 0, True,
@@ -564,7 +571,8 @@ class GpuServer(object):
     def _seq_order(self, rx, ft):
         """Number the batch's SEQUENTIAL creates in stream order (parent's
         cversion before the batch + rank among its sequential creates
-        here): returns the int32 [cap_frames] numbers for the serve."""
+        here): returns the int64 [cap_frames] words for the serve (parent
+        node << 32 | number; -1 none)."""
         L = _lib.lib()
         dev = self.tree.device
         if self.seq_ws is None:
@@ -572,7 +580,7 @@ class GpuServer(object):
             self.seq_ws = torch.empty(L.tree_seq_workspace(n), dtype=U8,
                                       device=dev)
             self.seq_ws[:L.tree_seq_zeroed(n)].zero_()
-            self.seqno = torch.empty(n, dtype=I32, device=dev)
+            self.seqno = torch.empty(n, dtype=I64, device=dev)
         L.tree_seq_order(self.tree.tensors, rx, ft.off, ft.length, ft.count,
                          self.cap_frames, self.seq_ws, self.seqno)
         return self.seqno
@@ -642,6 +650,7 @@ class GetPipeline(object):
         self.server = GpuServer(tree, n, n * (4 + 16 + 4 + dmax + 68) + 64,
                                 window=B.frame_window(17 + maxpath),
                                 seq_order=False)
+        self.server.read_only = _SERVE_RO
         self.server.enc_stage = _GET_STAGE
         self.rwindow = B.frame_window(4 + 16 + 4 + dmax + 68)
         lo, hi = tree.data_dist or (tree.data_bytes, tree.data_bytes)

@@ -176,6 +176,7 @@ struct Watchers {
 struct Node {
   std::string data;
   Stat st;
+  std::string path;       // its own path (the index's key check)
   std::set<std::string> kids;
   // the node's own watchers: arming and firing cost no lookup (round 3's
   // path-keyed tables made a watched SET 4 us and a re-arming GET 2.6 us)
@@ -344,9 +345,83 @@ struct Server {
   // members: connections per member (under mu, exclusive to change)
   std::vector<std::set<Conn*>> mconns;
 
+  // The path index: open addressing over a 64-bit path hash (linear
+  // probing, backward-shift deletion, at most half full), one slot per
+  // node beside `nodes` (which owns them).  A lookup is one slot line, the
+  // node and its path; std::unordered_map's bucket, list node and key
+  // buffer made a GET ~1.2 us of cache misses on a 1M-node tree, and the
+  // slots are what a read burst prefetches ahead (serve_parallel).
+  struct IxEnt {
+    uint64_t h;
+    Node* nd;
+  };
+  std::vector<IxEnt> ix = std::vector<IxEnt>(1024, IxEnt{0, nullptr});
+  size_t ix_used = 0;
+  static uint64_t phash(const char* s, size_t n) {
+    uint64_t h = 0x9E3779B97F4A7C15ull ^ (n * 0xFF51AFD7ED558CCDull);
+    size_t i = 0;
+    for (; i + 8 <= n; i += 8) {
+      uint64_t w;
+      memcpy(&w, s + i, 8);
+      h = (h ^ w) * 0xC4CEB9FE1A85EC53ull;
+      h ^= h >> 29;
+    }
+    uint64_t w = 0;
+    for (size_t k = 0; i + k < n; ++k) w |= (uint64_t)(uint8_t)s[i + k] << (8 * k);
+    h = (h ^ w) * 0x9E3779B97F4A7C15ull;
+    h ^= h >> 32;
+    return h;
+  }
+  const IxEnt* ix_slot(uint64_t h) const { return &ix[h & (ix.size() - 1)]; }
+  Node* ix_find(const char* p, size_t n, uint64_t h) const {
+    const size_t m = ix.size() - 1;
+    for (size_t s = h & m;; s = (s + 1) & m) {
+      const IxEnt& e = ix[s];
+      if (e.nd == nullptr) return nullptr;
+      if (e.h == h && e.nd->path.size() == n &&
+          memcmp(e.nd->path.data(), p, n) == 0)
+        return e.nd;
+    }
+  }
+  void ix_put(Node* nd) {
+    if (2 * (ix_used + 1) > ix.size()) {
+      std::vector<IxEnt> old(ix.size() * 2, IxEnt{0, nullptr});
+      old.swap(ix);
+      ix_used = 0;
+      for (const IxEnt& e : old)
+        if (e.nd != nullptr) ix_put(e.nd);
+    }
+    const uint64_t h = phash(nd->path.data(), nd->path.size());
+    const size_t m = ix.size() - 1;
+    for (size_t s = h & m;; s = (s + 1) & m) {
+      IxEnt& e = ix[s];
+      if (e.nd == nullptr) { e = IxEnt{h, nd}; ++ix_used; return; }
+      if (e.h == h && e.nd->path == nd->path) { e.nd = nd; return; }
+    }
+  }
+  void ix_del(const std::string& p) {
+    const uint64_t h = phash(p.data(), p.size());
+    const size_t m = ix.size() - 1;
+    size_t s = h & m;
+    for (;; s = (s + 1) & m) {
+      if (ix[s].nd == nullptr) return;
+      if (ix[s].h == h && ix[s].nd->path == p) break;
+    }
+    // backward shift: an entry after the hole moves into it unless its
+    // home lies in (hole, its slot]
+    for (size_t j = (s + 1) & m;; j = (j + 1) & m) {
+      if (ix[j].nd == nullptr) break;
+      const size_t home = ix[j].h & m;
+      if (((j - home) & m) >= ((j - s) & m)) {
+        ix[s] = ix[j];
+        s = j;
+      }
+    }
+    ix[s] = IxEnt{0, nullptr};
+    --ix_used;
+  }
   Node* find(const std::string& p) {
-    auto it = nodes.find(p);
-    return it == nodes.end() ? nullptr : it->second.get();
+    return ix_find(p.data(), p.size(), phash(p.data(), p.size()));
   }
   static std::string parent_of(const std::string& p) {
     size_t k = p.rfind('/');
@@ -360,8 +435,10 @@ struct Server {
     nd->st.ctime = nd->st.mtime = t;
     nd->st.eph = eph;
     nd->st.dlen = (int32_t)n;
+    nd->path = path;
     Node* raw = nd.get();
     nodes[path] = std::move(nd);
+    ix_put(raw);
     if (path != "/") {
       Node* par = find(parent_of(path));
       if (par != nullptr) {
@@ -538,6 +615,9 @@ struct Server {
     std::string* o = out != nullptr ? out : &c->out;
     Rd r{b, b + n};
     const int32_t xid = r.i32(), op = r.i32();
+    if ((op == OP_GET_DATA || op == OP_EXISTS) && r.ok &&
+        serve_read(r, xid, op, sid, key, o))
+      return true;
     // a SET_WATCHES catch-up notifies this connection before its reply
     if (op == OP_SET_WATCHES && r.ok) set_watches(r, sid, c);
     Wr w{o};
@@ -696,6 +776,7 @@ struct Server {
             note = o->substr(mark);
             o->resize(mark);
           }
+          ix_del(*key);
           nodes.erase(*key);
           if (!note.empty()) {
             o->insert(at, note);
@@ -708,6 +789,55 @@ struct Server {
       }
     }
     return finish(o, at, zat, eat, err, nullptr, keep);
+  }
+
+  // GET_DATA / EXISTS: the reply sized first and written in place (the
+  // general path's ~25 string appends a reply were ~230 ns of a GET's
+  // ~1 us on a 1M-node tree).  False: a malformed request, for the general
+  // path to answer.
+  bool serve_read(Rd r, int32_t xid, int32_t op, int64_t sid,
+                  std::string* key, std::string* o) {
+    const uint8_t* ps;
+    int32_t pl;
+    if (!r.buf(&ps, &pl)) return false;
+    const bool watch = r.boolean();
+    if (!r.ok) return false;
+    Node* nd = ix_find((const char*)ps, (size_t)pl,
+                       phash((const char*)ps, (size_t)pl));
+    // EXISTS arms on a missing node too (an exist watch); GET_DATA only on
+    // a node it returns
+    if (watch && (nd != nullptr || op == OP_EXISTS)) {
+      key->assign((const char*)ps, pl);
+      std::lock_guard<std::mutex> g(wmu);
+      arm(0, *key, nd, sid);
+    }
+    const size_t dl = nd != nullptr && op == OP_GET_DATA ? nd->data.size() : 0;
+    const size_t body = 16 + (nd == nullptr ? 0
+                              : (op == OP_GET_DATA ? 4 + dl : 0) + 68);
+    const size_t at = o->size();
+    o->resize(at + 4 + body);
+    uint8_t* q = (uint8_t*)&(*o)[at];
+    auto p32 = [&](int32_t v) {
+      const uint32_t x = htonl((uint32_t)v);
+      memcpy(q, &x, 4);
+      q += 4;
+    };
+    auto p64 = [&](int64_t v) { p32((int32_t)(v >> 32)); p32((int32_t)v); };
+    p32((int32_t)body);
+    p32(xid);
+    p64(zxid);
+    p32(nd == nullptr ? E_NO_NODE : E_OK);
+    if (nd == nullptr) return true;
+    if (op == OP_GET_DATA) {
+      p32(dl == 0 ? -1 : (int32_t)dl);          // (an empty buffer: -1)
+      if (dl) memcpy(q, nd->data.data(), dl);
+      q += dl;
+    }
+    const Stat& st = nd->st;
+    p64(st.czxid); p64(st.mzxid); p64(st.ctime); p64(st.mtime);
+    p32(st.version); p32(st.cversion); p32(st.aversion); p64(st.eph);
+    p32(st.dlen); p32(st.nkids); p64(st.pzxid);
+    return true;
   }
 
   // Patch a reply frame's header (the zxid after the request, err, length);
@@ -926,8 +1056,31 @@ struct Worker {
     if (S->pool != nullptr && c.hs &&
         (writes ? serve_parallel_writes(c) : serve_parallel(c)))
       return true;
+    // the burst's leading run of reads, for the lookahead
+    size_t nread = 0;
+    if (c.hs) {
+      fr.clear();
+      for (size_t o = c.in_off; c.in.size() - o >= 12;) {
+        uint32_t l, opw;
+        memcpy(&l, c.in.data() + o, 4);
+        const int32_t len = (int32_t)ntohl(l);
+        if (len < 8 || len > MAX_PACKET || c.in.size() - o < 4 + (size_t)len)
+          break;
+        memcpy(&opw, c.in.data() + o + 8, 4);
+        const int32_t op = (int32_t)ntohl(opw);
+        if (op != OP_GET_DATA && op != OP_EXISTS) break;
+        fr.emplace_back((uint32_t)(o + 4 - c.in_off), (uint32_t)len);
+        o += 4 + (size_t)len;
+      }
+      nread = fr.size();
+    }
+    Ahead ah{S, (const uint8_t*)c.in.data() + c.in_off, &fr, nread};
+    if (nread > 1) ah.start(0);
+    size_t fi = 0;
     bool dead = false;
     while (!c.closing && c.in.size() - c.in_off >= 4) {
+      if (fi < nread) ah.step(fi);
+      ++fi;
       uint32_t l;
       memcpy(&l, c.in.data() + c.in_off, 4);
       const int32_t len = (int32_t)ntohl(l);
@@ -957,6 +1110,61 @@ struct Worker {
   // served in chunks on the pool; the replies appended in request order.
   // False: not such a burst (or the pool is busy): the serial path.
   static constexpr size_t PAR_MIN = 8192;
+
+  // Read lookups' cache misses overlapped (a 1M-node tree is ~0.5 GB of
+  // nodes, paths and data: each GET's index slot, node, path and data are
+  // DRAM and TLB misses, ~1 us a GET served one after another): while
+  // frame f is served, frame f + 12's index slot, f + 8's node and f + 4's
+  // path and data are prefetched.  Frames (body offset, length) from
+  // `base`; frames without a leading path prefetch nothing.
+  struct Ahead {
+    Server* S;
+    const uint8_t* base;
+    const std::vector<std::pair<uint32_t, uint32_t>>* fr;
+    size_t end;
+    uint64_t hs[16];
+    void stage(size_t g, int st) {
+      if (g >= end) return;
+      if (st == 0) {
+        const uint8_t* b = base + (*fr)[g].first;
+        const uint32_t n = (*fr)[g].second;
+        hs[g & 15] = 0;
+        if (n < 12) return;
+        uint32_t pl;
+        memcpy(&pl, b + 8, 4);
+        pl = ntohl(pl);
+        if (pl > n - 12) return;
+        const uint64_t h = Server::phash((const char*)b + 12, pl);
+        hs[g & 15] = h ? h : 1;
+        __builtin_prefetch(S->ix_slot(h));
+        return;
+      }
+      const uint64_t h = hs[g & 15];
+      if (h == 0) return;
+      const Server::IxEnt* e = S->ix_slot(h);
+      if (e->nd == nullptr || e->h != h) return;
+      const char* nd = (const char*)e->nd;
+      if (st == 1) {
+        __builtin_prefetch(nd);
+        __builtin_prefetch(nd + 64);
+        __builtin_prefetch(nd + 128);
+      } else {
+        __builtin_prefetch(e->nd->path.data());
+        __builtin_prefetch(e->nd->data.data());
+        __builtin_prefetch(e->nd->data.data() + 64);
+      }
+    }
+    void start(size_t f0) {
+      for (size_t g = f0; g < f0 + 12; ++g) stage(g, 0);
+      for (size_t g = f0; g < f0 + 8; ++g) stage(g, 1);
+      for (size_t g = f0; g < f0 + 4; ++g) stage(g, 2);
+    }
+    void step(size_t f) {
+      stage(f + 12, 0);
+      stage(f + 8, 1);
+      stage(f + 4, 2);
+    }
+  };
   std::vector<std::pair<uint32_t, uint32_t>> fr;   // (body offset, length)
   bool serve_parallel(Conn& c) {
     fr.clear();
@@ -985,10 +1193,14 @@ struct Worker {
     const bool ran = S->pool->run(K, [&](int k) {
       std::string key;
       const size_t f0 = nf * k / K, f1 = nf * (k + 1) / K;
-      outs[k].reserve((f1 - f0) * 128);
-      for (size_t f = f0; f < f1; ++f)
+      outs[k].reserve((f1 - f0) * 200);
+      Ahead ah{S, base, &fr, f1};
+      ah.start(f0);
+      for (size_t f = f0; f < f1; ++f) {
+        ah.step(f);
         S->serve(base + fr[f].first, (int32_t)fr[f].second, &c, &key,
                  &outs[k]);
+      }
     });
     if (!ran) return false;
     wclock.add(WireClock::PAR_BURSTS, 1);
@@ -1007,16 +1219,20 @@ struct Worker {
   // the replies built in parallel chunks (appended in order), and the
   // watches fire on this thread in request order, each watching
   // connection's notifications appended and its worker woken once (not
-  // once per notification).  Anything else — another op, a repeated path,
-  // a malformed frame, a watch of this very session (its notification
-  // must sit between this connection's replies) — returns false before
-  // anything changed: the serial path serves the burst.  Round 5's config
-  // 4 spent 51 ms of its 70.8 ms write phase (20 steps) here serially.
+  // once per notification).  A watch of the writing session itself (config
+  // 4 at one rank: the writer watches every path) is answered as the
+  // serial path answers it, its notification right before the write's
+  // reply, inside the chunk.  Anything else — another op, a repeated path,
+  // a malformed frame, a session routed to another connection — returns
+  // false before anything changed: the serial path serves the burst.
+  // Round 5's config 4 spent 51 ms of its 70.8 ms write phase (20 steps)
+  // here serially.
   static constexpr size_t WPAR_MIN = 512;
   struct WJob {
     Node* nd;
     const uint8_t* d;
     int32_t dl, ver, xid, err;
+    bool self;             // the writing session watches the node
     int64_t z;
     std::string path;
   };
@@ -1040,6 +1256,8 @@ struct Worker {
     const int K = std::min<int>(S->pool->size() + 1, (int)(nf / 128));
     const uint8_t* base = (const uint8_t*)c.in.data() + c.in_off;
     const int64_t sid = c.sid;
+    const auto rt = S->route.find(sid);
+    const bool routed = rt != S->route.end() && rt->second == &c;
     wj.resize(nf);
     std::atomic<bool> bad{false};
     const int64_t tp = mono_ns();
@@ -1060,9 +1278,13 @@ struct Worker {
             j.err = j.nd == nullptr ? E_NO_NODE
                     : (j.ver != -1 && j.ver != j.nd->st.version) ? E_BAD_VERSION
                                                                  : E_OK;
+            j.self = false;
             if (j.err == E_OK)
               for (int64_t x : j.nd->dw.s)
-                if (x == sid) { bad = true; return; }
+                if (x == sid) {
+                  if (!routed) { bad = true; return; }
+                  j.self = true;
+                }
           }
         }))
       return false;
@@ -1098,6 +1320,8 @@ struct Worker {
         nd->st.mzxid = j.z;
         nd->st.mtime = t;
         nd->st.dlen = j.dl;
+        // (the session's own watch: its notification, then the reply)
+        if (j.self) Server::note_frame(&out, EV_DATA_CHANGED, j.path);
         w.i32(84); w.i32(j.xid); w.i64(j.z); w.i32(E_OK);
         w.stat(nd->st);
       }
@@ -1114,8 +1338,9 @@ struct Worker {
           S->unlist(x, 0, j.nd, j.path);
           auto it = S->route.find(x);
           if (it == S->route.end()) continue;
-          Server::note_frame(&notes[it->second], EV_DATA_CHANGED, j.path);
           S->n_notes.fetch_add(1, std::memory_order_relaxed);
+          if (x == sid) continue;              // (in the replies, step 3)
+          Server::note_frame(&notes[it->second], EV_DATA_CHANGED, j.path);
         }
       }
     }

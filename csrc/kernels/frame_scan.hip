@@ -1479,13 +1479,44 @@ __global__ __launch_bounds__(256) void fs_tile(
   {
     const int32_t P0 = lane * 64;
     uint32_t d[17];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint4 q = *(const uint4*)(sb + P0 + 16 * j);
-      d[4 * j] = q.x; d[4 * j + 1] = q.y; d[4 * j + 2] = q.z;
-      d[4 * j + 3] = q.w;
+    {
+      // lane l reads its 16-byte chunks in the order rotated by (l >> 2) & 3:
+      // a ds_read_b128 lane group (16 lanes) then covers the 64 banks once
+      // (in plain order four lanes share each 16-byte slot: 4-way); the
+      // dword past the lane's 64 bytes is the next lane's first (a shuffle,
+      // not a 16-way ds_read_b32 at a 64-byte stride)
+      const int r = (lane >> 2) & 3;
+      uint4 x0 = *(const uint4*)(sb + P0 + 16 * (r & 3));
+      uint4 x1 = *(const uint4*)(sb + P0 + 16 * ((1 + r) & 3));
+      uint4 x2 = *(const uint4*)(sb + P0 + 16 * ((2 + r) & 3));
+      uint4 x3 = *(const uint4*)(sb + P0 + 16 * ((3 + r) & 3));
+      const uint32_t pad = *(const uint32_t*)(sb + FT_S);   // (broadcast)
+      // back to chunk order (x_j held chunk j + r): rotate right by r in two
+      // conditional stages (named registers and selects: an indexed array
+      // went to scratch)
+      auto sel = [](bool c, uint4 a, uint4 b) {
+        return make_uint4(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z,
+                          c ? a.w : b.w);
+      };
+      {
+        const bool c = r & 1;
+        const uint4 y0 = sel(c, x3, x0), y1 = sel(c, x0, x1),
+                    y2 = sel(c, x1, x2), y3 = sel(c, x2, x3);
+        x0 = y0; x1 = y1; x2 = y2; x3 = y3;
+      }
+      {
+        const bool c = r & 2;
+        const uint4 y0 = sel(c, x2, x0), y1 = sel(c, x3, x1),
+                    y2 = sel(c, x0, x2), y3 = sel(c, x1, x3);
+        x0 = y0; x1 = y1; x2 = y2; x3 = y3;
+      }
+      d[0] = x0.x; d[1] = x0.y; d[2] = x0.z; d[3] = x0.w;
+      d[4] = x1.x; d[5] = x1.y; d[6] = x1.z; d[7] = x1.w;
+      d[8] = x2.x; d[9] = x2.y; d[10] = x2.z; d[11] = x2.w;
+      d[12] = x3.x; d[13] = x3.y; d[14] = x3.z; d[15] = x3.w;
+      const uint32_t nx = (uint32_t)__shfl_down((int)d[0], 1, 64);
+      d[16] = lane == 63 ? pad : nx;
     }
-    d[16] = *(const uint32_t*)(sb + P0 + 64);
     // minb <= len <= W - 4 past the entry window (the window covers the
     // stream's frames: a longer length is a byte pattern, not a frame; the
     // rare real one meets the map as a SHORT root and is walked exactly),

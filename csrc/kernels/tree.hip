@@ -1467,6 +1467,7 @@ struct SeqWs {
   int32_t* kk;        // [ncap] request -> its chunk among its group's chunks
   int64_t hmask;
   int32_t mw;         // bitmap words per group (<= SQ_MW)
+  int64_t* dbg;       // optional: 4 phase clocks per chunk (zk_tree_seq_debug)
 };
 
 // The parent path of a SEQUENTIAL create frame ([p, p + cut)); cut 0 for
@@ -1492,6 +1493,70 @@ ZK_DEV int32_t seq_parent(const uint8_t* rx, int64_t off, int32_t len,
   return cut;
 }
 
+// The group key (path_hash of the parent path | 1; 0: not a SEQUENTIAL
+// create) of the create frame [b, b + len): the frame's first 64 bytes and
+// its last word are loaded at once — one round trip after the frame table,
+// not seq_parent's chain of a header load, the flags load, a byte load per
+// step of the '/' search and the hash's own loads (the probe's clocks: 32
+// us a chunk for those, tools/microbench/seq_probe.py) — and the op, the
+// flags, the last '/' and the hash come from registers.  A path past the
+// 64 bytes (pl > 52) or a frame under them takes seq_parent.
+ZK_DEV uint64_t seq_key(const uint8_t* rx, int64_t off, int32_t len) {
+  if (len < 64) {
+    const uint8_t* p = nullptr;
+    const int32_t cut = seq_parent(rx, off, len, &p);
+    return cut > 0 ? path_hash(p, cut) | 1ull : 0;
+  }
+  const uint8_t* b = rx + off;
+  uint32_t W[16], fl;
+  __builtin_memcpy(W, b, 64);
+  __builtin_memcpy(&fl, b + len - 4, 4);
+  // (every load issued before the first test: the compiler otherwise sinks
+  // the path words and the flags below the op test, one wait each)
+  asm volatile("" ::"v"(W[0]), "v"(W[1]), "v"(W[2]), "v"(W[3]), "v"(W[4]),
+               "v"(W[5]), "v"(W[6]), "v"(W[7]), "v"(W[8]), "v"(W[9]),
+               "v"(W[10]), "v"(W[11]), "v"(W[12]), "v"(W[13]), "v"(W[14]),
+               "v"(W[15]), "v"(fl));
+  const int32_t pl = (int32_t)bswap32(W[2]);
+  if ((int32_t)bswap32(W[1]) != OP_CREATE || pl < 2 || 12 + pl + 12 > len ||
+      !(bswap32(fl) & CF_SEQUENTIAL))
+    return 0;
+  if (pl > 52) {
+    const uint8_t* p = nullptr;
+    const int32_t cut = seq_parent(rx, off, len, &p);
+    return cut > 0 ? path_hash(p, cut) | 1ull : 0;
+  }
+  // '/' bytes of path positions 1 .. pl - 1 (path byte q: word 3 + q / 4)
+  uint64_t slash = 0;
+#pragma unroll
+  for (int k = 3; k < 16; ++k) {
+    const uint32_t x = W[k] ^ 0x2F2F2F2Fu;
+    const uint32_t z = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);
+    const uint64_t nib = ((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) |
+                         ((z >> 28) & 8u);
+    slash |= nib << (4 * (k - 3));
+  }
+  slash &= ((1ull << pl) - 1) & ~1ull;
+  if (!slash) return 0;
+  const int32_t cut = 63 - __builtin_clzll(slash);
+  // path_hash(path, cut) from the words: 8-byte pieces, the last masked
+  uint64_t h = 0x9E3779B97F4A7C15ull ^ (uint64_t)cut;
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    if (8 * j < cut) {
+      uint64_t x = (uint64_t)W[3 + 2 * j] | (uint64_t)W[4 + 2 * j] << 32;
+      const int32_t left = cut - 8 * j;
+      if (left < 8) x &= (1ull << (8 * left)) - 1;
+      h = (h ^ x) * 0xFF51AFD7ED558CCDull;
+      h ^= h >> 32;
+    }
+  }
+  h ^= h >> 33;
+  h *= 0xC4CEB9FE1A85EC53ull;
+  h ^= h >> 33;
+  return h | 1ull;
+}
+
 // Within the chunk, each request's rank among the chunk's requests of its
 // group (in lane = stream order) and each group's count, without a sort:
 // the group slots get chunk-local dense ids through an LDS hash, a wave
@@ -1513,14 +1578,21 @@ __global__ __launch_bounds__(SQ_C) void seq_group_k(
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int64_t c = blockIdx.x;
   const int64_t i = c * SQ_C + tid;
+  int64_t* const dbg = w.dbg ? w.dbg + 5 * c : nullptr;
+  if (dbg && tid == 0) dbg[0] = wall_clock64();
+  // (the frame table and the count loaded together)
+  const int64_t fo = i < ncap ? foff[i] : 0;
+  const int32_t fn = i < ncap ? flen[i] : 0;
   const bool in = i < ncap && i < *n_dev;
   int64_t e = -1;
   bool first = false;
-  if (in) {
-    const uint8_t* p = nullptr;
-    const int32_t cut = seq_parent(rx, foff[i], flen[i], &p);
-    if (cut > 0) {
-      const int64_t key = (int64_t)(path_hash(p, cut) | 1ull);
+  const int64_t key = in ? (int64_t)seq_key(rx, fo, fn) : 0;
+  if (dbg) {
+    __syncthreads();
+    if (tid == 0) dbg[4] = wall_clock64();
+  }
+  {
+    if (key != 0) {
       int64_t s = key & w.hmask;
       for (int64_t probe = 0; probe <= w.hmask; ++probe) {
         // a plain load first (a stale 0 only means the CAS answers)
@@ -1544,6 +1616,7 @@ __global__ __launch_bounds__(SQ_C) void seq_group_k(
     w.glist[k] = (int32_t)e;
     w.rep[e] = (int32_t)i;
   }
+  if (dbg && tid == 0) dbg[1] = wall_clock64();   // (after the ticket's barriers)
   if (!__syncthreads_or(e >= 0)) return;     // (block-uniform)
   // 1. chunk-local dense ids
   for (int x = tid; x < SQ_LH; x += SQ_C) lkey[x] = -1;
@@ -1566,6 +1639,7 @@ __global__ __launch_bounds__(SQ_C) void seq_group_k(
     }
   }
   __syncthreads();
+  if (dbg && tid == 0) dbg[2] = wall_clock64();
   const int d = e >= 0 ? lid[ls] : -1;
   // 2. peers in the wave: one ballot per distinct id
   uint64_t peers = 0;
@@ -1596,6 +1670,10 @@ __global__ __launch_bounds__(SQ_C) void seq_group_k(
       atomicOr((unsigned long long*)&w.mask[e * w.mw + (c >> 6)],
                1ull << (c & 63));
     }
+  }
+  if (dbg) {
+    __syncthreads();
+    if (tid == 0) dbg[3] = wall_clock64();
   }
 }
 
@@ -2413,6 +2491,13 @@ static int64_t seq_layout(int64_t ncap, uint8_t* ws, zk::SeqWs* w,
   return o;
 }
 
+// Phase clocks of seq_group_k (tools/microbench/seq_probe.py): buf holds
+// 5 int64 per 1024-request chunk — start, the key table probe and group
+// ticket done, chunk-local ids done, end, and (an extra barrier) the parse
+// done (wall_clock64 ticks, 100 MHz); nullptr turns them off.
+static int64_t* g_seq_dbg = nullptr;
+void zk_tree_seq_debug(int64_t* buf) { g_seq_dbg = buf; }
+
 int64_t zk_tree_seq_workspace(int64_t ncap) {
   return ncap > 0 ? seq_layout(ncap, nullptr, nullptr, nullptr) : 0;
 }
@@ -2438,6 +2523,7 @@ int zk_tree_seq_order(const ZkTree* t, const uint8_t* rx, const int64_t* foff,
   zk::SeqWs w;
   int64_t zeroed = 0;
   seq_layout(ncap, ws, &w, &zeroed);
+  w.dbg = g_seq_dbg;
   if (hipMemsetAsync(w.ctr, 0, 64, st) != hipSuccess) return -4;
   const unsigned nchunk = (unsigned)((ncap + zk::SQ_C - 1) / zk::SQ_C);
   const unsigned nb = (unsigned)((ncap + zk::TR_T - 1) / zk::TR_T);

@@ -792,6 +792,19 @@ void tree_seq_order(const std::vector<Tensor>& t, const Tensor& rx,
          "tree_seq_order");
 }
 
+// seq_group_k's phase clocks into buf (int64, 5 per 1024-request chunk of
+// the batches that follow; an empty tensor turns them off)
+void tree_seq_debug(const Tensor& buf) {
+  if (buf.numel() == 0) {
+    zk_tree_seq_debug(nullptr);
+    return;
+  }
+  TORCH_CHECK(buf.is_cuda() && buf.scalar_type() == at::kLong &&
+                  buf.is_contiguous(),
+              "zkmi: tree_seq_debug wants a contiguous device int64 tensor");
+  zk_tree_seq_debug(buf.data_ptr<int64_t>());
+}
+
 // out (int64 [4]): node digest, live nodes, hash entries used, tombstones
 void tree_digest(const std::vector<Tensor>& t, const Tensor& out) {
   ZkTree s = tree(t);
@@ -1099,6 +1112,7 @@ TORCH_LIBRARY(zkmi, m) {
         &tree_serve_ordered);
   m.def("tree_seq_workspace(int n) -> int", &tree_seq_workspace);
   m.def("tree_seq_zeroed(int n) -> int", &tree_seq_zeroed);
+  m.def("tree_seq_debug(Tensor buf) -> ()", &tree_seq_debug);
   m.def("tree_seq_order(Tensor(a!)[] tree, Tensor rx, Tensor frame_off, "
         "Tensor frame_len, Tensor count, int ncap, Tensor(b!) ws, "
         "Tensor(c!) seqno) -> ()", &tree_seq_order);

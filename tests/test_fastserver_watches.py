@@ -374,3 +374,56 @@ def test_parallel_write_burst_matches_serial():
     assert errs == {'OK', 'BAD_VERSION', 'NO_NODE'}, errs
     assert notes[0] == notes[4]
     assert len(notes[0]) > 500
+
+
+def test_parallel_write_burst_own_watches():
+    """The writer watches some of the paths it writes (config 4 at one
+    rank): the parallel burst must still match the serial server frame for
+    frame — each own notification right before its write's reply — and
+    the other watcher's notifications too."""
+    n = 2000
+    ops = [{'opcode': 'SET_DATA', 'path': leaf(i), 'data': b'w%d' % i,
+            'version': -1} for i in range(n)]
+    reqs = b''.join(jute.frame(jute.encode_request(dict(o, xid=1000 + i)))
+                    for i, o in enumerate(ops))
+    got, notes = {}, {}
+    for st in (0, 4):
+        srv = fast.FastZKServer(preload=n, data_bytes=8, fanout=FANOUT,
+                                serve_threads=st)
+        try:
+            other = Raw(srv.port)
+            for i in range(0, n, 5):
+                other.call(_get(leaf(i)))
+            r = Raw(srv.port)
+            for i in range(0, n, 2):
+                r.call(_get(leaf(i)))                 # the writer's own
+            r.s.sendall(reqs)
+            frames, replies = [], 0
+            while replies < n:
+                b = r._frame()
+                frames.append(b)
+                if int.from_bytes(b[:4], 'big', signed=True) != -1:
+                    replies += 1
+            got[st] = frames
+            other.sync()
+            notes[st] = list(other.notes)
+            r.close()
+            other.close()
+            t = srv.timing()
+        finally:
+            srv.shutdown()
+        assert (t['par_bursts'] > 0) == (st > 0), t
+    xmap = {1000 + i: 'SET_DATA' for i in range(n)}
+
+    def norm(body):
+        rep = jute.decode_response(body, xmap)
+        st = rep.get('stat')
+        if st is not None:
+            rep['stat'] = (st.czxid, st.mzxid, st.version, st.dataLength)
+        return rep
+    a = [norm(b) for b in got[0]]
+    assert a == [norm(b) for b in got[4]]
+    own = [x for x in a if x['xid'] == consts.XID_NOTIFICATION]
+    assert len(own) == n // 2
+    assert notes[0] == notes[4] and len(notes[0]) == n // 5
+

@@ -58,6 +58,10 @@ _FREE_COMPACT = os.environ.get('ZKMI_FREE_COMPACT', '1') == '1'
 _FINISH_SCAN = os.environ.get('ZKMI_FINISH_SCAN', '1') == '1'
 # the largest batch tree_seq_order numbers
 _SEQ_MAX = 1 << 24
+# ZKMI_SRV_GROUP: K1 tiles a wave on the GPU server's request streams
+# (unset: one, the scanner's default without a frame hint)
+_SRV_GROUP = (int(os.environ['ZKMI_SRV_GROUP'])
+              if os.environ.get('ZKMI_SRV_GROUP') else None)
 
 
 def _len(total):
@@ -399,7 +403,8 @@ class GpuServer(object):
         self.presized = B.response_workspace(cap_frames, dev)
         self.out = torch.empty(out_cap, dtype=U8, device=dev)
         self.cap_frames = cap_frames
-        self.scanner = B.FrameScanner(cap_frames, dev, window=window)
+        self.scanner = B.FrameScanner(cap_frames, dev, window=window,
+                                      group=_SRV_GROUP)
         self.ows = None                   # ordered-serve workspace (lazy)
         self.enc_stage = 0                # K13 LDS per workgroup (0: default)
         self.total_err = B._total_err(dev)  # the reply encode's scalars

@@ -227,6 +227,28 @@ struct Wr {
   }
 };
 
+// Big-endian writes at a cursor into space already sized (a reply built in
+// place: one resize, no per-field append).
+struct Put {
+  uint8_t* q;
+  void i32(int32_t v) {
+    const uint32_t x = htonl((uint32_t)v);
+    memcpy(q, &x, 4);
+    q += 4;
+  }
+  void i64(int64_t v) { i32((int32_t)(v >> 32)); i32((int32_t)v); }
+  void raw(const void* s, size_t n) {
+    if (n) memcpy(q, s, n);
+    q += n;
+  }
+  void stat(const Stat& s) {
+    i64(s.czxid); i64(s.mzxid); i64(s.ctime); i64(s.mtime);
+    i32(s.version); i32(s.cversion); i32(s.aversion); i64(s.eph);
+    i32(s.dlen); i32(s.nkids); i64(s.pzxid);
+  }
+};
+constexpr size_t STAT_LEN = 68;
+
 struct Worker;
 
 // Helper threads that serve one connection's large read burst in parallel
@@ -813,30 +835,20 @@ struct Server {
     }
     const size_t dl = nd != nullptr && op == OP_GET_DATA ? nd->data.size() : 0;
     const size_t body = 16 + (nd == nullptr ? 0
-                              : (op == OP_GET_DATA ? 4 + dl : 0) + 68);
+                              : (op == OP_GET_DATA ? 4 + dl : 0) + STAT_LEN);
     const size_t at = o->size();
     o->resize(at + 4 + body);
-    uint8_t* q = (uint8_t*)&(*o)[at];
-    auto p32 = [&](int32_t v) {
-      const uint32_t x = htonl((uint32_t)v);
-      memcpy(q, &x, 4);
-      q += 4;
-    };
-    auto p64 = [&](int64_t v) { p32((int32_t)(v >> 32)); p32((int32_t)v); };
-    p32((int32_t)body);
-    p32(xid);
-    p64(zxid);
-    p32(nd == nullptr ? E_NO_NODE : E_OK);
+    Put w{(uint8_t*)&(*o)[at]};
+    w.i32((int32_t)body);
+    w.i32(xid);
+    w.i64(zxid);
+    w.i32(nd == nullptr ? E_NO_NODE : E_OK);
     if (nd == nullptr) return true;
     if (op == OP_GET_DATA) {
-      p32(dl == 0 ? -1 : (int32_t)dl);          // (an empty buffer: -1)
-      if (dl) memcpy(q, nd->data.data(), dl);
-      q += dl;
+      w.i32(dl == 0 ? -1 : (int32_t)dl);          // (an empty buffer: -1)
+      w.raw(nd->data.data(), dl);
     }
-    const Stat& st = nd->st;
-    p64(st.czxid); p64(st.mzxid); p64(st.ctime); p64(st.mtime);
-    p32(st.version); p32(st.cversion); p32(st.aversion); p64(st.eph);
-    p32(st.dlen); p32(st.nkids); p64(st.pzxid);
+    w.stat(nd->st);
     return true;
   }
 
@@ -1264,7 +1276,10 @@ struct Worker {
     // 1. parse, look up, check (the tree is only read)
     if (!S->pool->run(K, [&](int k) {
           const size_t f0 = nf * k / K, f1 = nf * (k + 1) / K;
+          Ahead ah{S, base, &fr, f1};
+          ah.start(f0);
           for (size_t f = f0; f < f1; ++f) {
+            ah.step(f);
             WJob& j = wj[f];
             Rd r{base + fr[f].first, base + fr[f].first + fr[f].second};
             j.xid = r.i32();
@@ -1306,8 +1321,16 @@ struct Worker {
     S->pool->run(K, [&](int k) {
       const size_t f0 = nf * k / K, f1 = nf * (k + 1) / K;
       std::string& out = outs[k];
-      out.reserve((f1 - f0) * 88);
-      Wr w{&out};
+      // sized once: replies (header + Stat, or the header alone) and the
+      // session's own notifications
+      size_t need = 0;
+      for (size_t f = f0; f < f1; ++f) {
+        const WJob& j = wj[f];
+        need += j.err != E_OK ? 20 : 20 + STAT_LEN;
+        if (j.err == E_OK && j.self) need += 32 + j.path.size();
+      }
+      out.resize(need);
+      Put w{(uint8_t*)&out[0]};
       for (size_t f = f0; f < f1; ++f) {
         WJob& j = wj[f];
         if (j.err != E_OK) {
@@ -1320,9 +1343,16 @@ struct Worker {
         nd->st.mzxid = j.z;
         nd->st.mtime = t;
         nd->st.dlen = j.dl;
-        // (the session's own watch: its notification, then the reply)
-        if (j.self) Server::note_frame(&out, EV_DATA_CHANGED, j.path);
-        w.i32(84); w.i32(j.xid); w.i64(j.z); w.i32(E_OK);
+        // (the session's own watch: its notification, then the reply;
+        // note_frame's layout)
+        if (j.self) {
+          w.i32(28 + (int32_t)j.path.size());
+          w.i32(-1); w.i64(-1); w.i32(E_OK);
+          w.i32(EV_DATA_CHANGED); w.i32(ST_SYNC_CONNECTED);
+          w.i32((int32_t)j.path.size());
+          w.raw(j.path.data(), j.path.size());
+        }
+        w.i32(16 + (int32_t)STAT_LEN); w.i32(j.xid); w.i64(j.z); w.i32(E_OK);
         w.stat(nd->st);
       }
     });
@@ -1330,18 +1360,33 @@ struct Worker {
     std::unordered_map<Conn*, std::string> notes;
     {
       std::lock_guard<std::mutex> g(S->wmu);
+      // (a burst's watchers are a few sessions: the last one's index entry,
+      // route and note buffer are kept across jobs; each list is cleared in
+      // place, its capacity kept for the re-arm)
+      int64_t lsid = 0;
+      bool known = false;
+      Server::SessW* lsw = nullptr;
+      Conn* lconn = nullptr;
+      std::string* lnotes = nullptr;
       for (WJob& j : wj) {
         if (j.err != E_OK || j.nd->dw.s.empty()) continue;
-        std::vector<int64_t> sids;
-        sids.swap(j.nd->dw.s);
-        for (int64_t x : sids) {
-          S->unlist(x, 0, j.nd, j.path);
-          auto it = S->route.find(x);
-          if (it == S->route.end()) continue;
+        for (int64_t x : j.nd->dw.s) {
+          if (!known || x != lsid) {
+            known = true;
+            lsid = x;
+            auto a = S->sw.find(x);
+            lsw = a == S->sw.end() ? nullptr : &a->second;
+            auto b = S->route.find(x);
+            lconn = b == S->route.end() ? nullptr : b->second;
+            lnotes = lconn != nullptr && x != sid ? &notes[lconn] : nullptr;
+          }
+          if (lsw != nullptr) lsw->d.erase(j.nd);          // (unlist)
+          if (lconn == nullptr) continue;
           S->n_notes.fetch_add(1, std::memory_order_relaxed);
           if (x == sid) continue;              // (in the replies, step 3)
-          Server::note_frame(&notes[it->second], EV_DATA_CHANGED, j.path);
+          Server::note_frame(lnotes, EV_DATA_CHANGED, j.path);
         }
+        j.nd->dw.s.clear();
       }
     }
     for (auto& kv : notes) {

@@ -29,8 +29,24 @@ class FastZKServer(object):
             raise RuntimeError('zk_fastserver not built '
                                '(tools/build_native.py)')
         # a sanitizer runtime preloaded into the caller (tools/
-        # sanitize_host.sh) is not for this uninstrumented program
-        env = {k: v for k, v in os.environ.items() if k != 'LD_PRELOAD'}
+        # sanitize_host.sh) is not for this uninstrumented program (only
+        # those entries go; anything else preloaded stays)
+        env = dict(os.environ)
+        if env.get('LD_PRELOAD'):
+            keep = [x for x in env['LD_PRELOAD'].replace(':', ' ').split()
+                    if 'san.so' not in os.path.basename(x)]
+            if keep:
+                env['LD_PRELOAD'] = ' '.join(keep)
+            else:
+                del env['LD_PRELOAD']
+        # transparent huge pages for the node heap (THP in madvise mode):
+        # a GET or SET is a handful of dependent misses into ~0.5 GB of
+        # nodes, paths and data per 1M znodes, each a TLB miss on 4 KiB
+        # pages (ZKMI_FAST_HUGEPAGES=0: off)
+        if os.environ.get('ZKMI_FAST_HUGEPAGES', '1') == '1':
+            tun = env.get('GLIBC_TUNABLES', '')
+            env['GLIBC_TUNABLES'] = (tun + ':' if tun else '') + \
+                'glibc.malloc.hugetlb=1'
         self.p = subprocess.Popen(
             [BINARY, '--port', str(port), '--preload', str(preload),
              '--data-bytes', str(data_bytes), '--fanout', str(fanout)] +

@@ -19,29 +19,48 @@ ZK_DEV uint64_t splitmix64(uint64_t x) {
   return x ^ (x >> 31);
 }
 
+
+// With `sizes` / `bsum`, also the K10 encode's sizes pass for these
+// GET_DATA requests (zk_encode_requests_presized: one launch less a step):
+// each frame's bytes (length word, xid, op, path buffer, watch flag) and
+// each 256-request block's sum, as req_sizes writes them.
 __global__ __launch_bounds__(BG_T) void bench_gen_get(
     int64_t n, uint64_t seed, int64_t leaf0, int64_t nleaves,
     int32_t xid_base, const int64_t* __restrict__ node_pw,
     int64_t* __restrict__ idx, int32_t* __restrict__ xid,
     int64_t* __restrict__ path_off, int32_t* __restrict__ path_len,
-    const int64_t* __restrict__ state) {
+    const int64_t* __restrict__ state, int64_t* __restrict__ sizes,
+    int64_t* __restrict__ bsum) {
+  static_assert(BG_T == 256, "the encoder's blocks (ENC_T)");
   const int64_t i = (int64_t)blockIdx.x * BG_T + threadIdx.x;
-  if (i >= n) return;
-  if (state != nullptr) {
-    // device-resident {seed, step} (a captured graph replays new batches):
-    // the step's seed and xids derive from the step counter
-    const uint64_t st = (uint64_t)state[1];
-    seed = (uint64_t)state[0] * 0x9E3779B97F4A7C15ull + st;
-    xid_base = (int32_t)((st * (uint64_t)n) & 0x7fffffffu);
+  int64_t sz = 0;
+  if (i < n) {
+    if (state != nullptr) {
+      // device-resident {seed, step} (a captured graph replays new
+      // batches): the step's seed and xids derive from the step counter
+      const uint64_t st = (uint64_t)state[1];
+      seed = (uint64_t)state[0] * 0x9E3779B97F4A7C15ull + st;
+      xid_base = (int32_t)((st * (uint64_t)n) & 0x7fffffffu);
+    }
+    const uint64_t r = splitmix64(seed ^ (uint64_t)i * 0xD1B54A32D192ED03ull);
+    // multiply-shift range reduction (bias < 2^-32 for 1M leaves)
+    const int64_t v = leaf0 + (int64_t)(((r >> 32) * (uint64_t)nleaves) >> 32);
+    idx[i] = v;
+    xid[i] = (int32_t)(((uint32_t)xid_base + (uint32_t)i) & 0x7fffffffu);
+    const int64_t pw = node_pw[v];         // offset << 24 | length (tree.hip)
+    const int32_t pl = (int32_t)(pw & 0xFFFFFF);
+    path_off[i] = pw >> 24;
+    path_len[i] = pl;
+    // the frame: length word, xid, op, path buffer, watch flag
+    sz = 4 + 4 + 4 + 4 + pl + 1;
+    if (sizes != nullptr) sizes[i] = sz;
   }
-  const uint64_t r = splitmix64(seed ^ (uint64_t)i * 0xD1B54A32D192ED03ull);
-  // multiply-shift range reduction (bias < 2^-32 for 1M leaves)
-  const int64_t v = leaf0 + (int64_t)(((r >> 32) * (uint64_t)nleaves) >> 32);
-  idx[i] = v;
-  xid[i] = (int32_t)(((uint32_t)xid_base + (uint32_t)i) & 0x7fffffffu);
-  const int64_t pw = node_pw[v];           // offset << 24 | length (tree.hip)
-  path_off[i] = pw >> 24;
-  path_len[i] = (int32_t)(pw & 0xFFFFFF);
+  if (sizes != nullptr) {                  // (block-uniform)
+    __shared__ int64_t sm[BG_T / 64 + 1];
+    int64_t tot;
+    block_excl_scan(sz, sm, &tot);
+    if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
+  }
 }
 
 // Grid-stride with a bounded grid: one device-scope atomic per block, and a
@@ -143,14 +162,18 @@ int zk_bench_check_notif(int64_t total, int64_t n_per, const uint64_t* seeds,
   return 0;
 }
 
+// sizes / bsum (both or neither): the encode's sizes pass too (see the
+// kernel; bsum holds one int64 per 256 requests)
 int zk_bench_gen_get(int64_t n, uint64_t seed, int64_t leaf0, int64_t nleaves,
                      int32_t xid_base, const int64_t* node_pw, int64_t* idx,
                      int32_t* xid, int64_t* path_off, int32_t* path_len,
-                     const int64_t* state, hipStream_t st) {
+                     const int64_t* state, int64_t* sizes, int64_t* bsum,
+                     hipStream_t st) {
   if (n <= 0) return 0;
+  if ((sizes == nullptr) != (bsum == nullptr)) return (int)hipErrorInvalidValue;
   zk::bench_gen_get<<<(unsigned)((n + zk::BG_T - 1) / zk::BG_T), zk::BG_T, 0,
                       st>>>(n, seed, leaf0, nleaves, xid_base, node_pw, idx,
-                            xid, path_off, path_len, state);
+                            xid, path_off, path_len, state, sizes, bsum);
   ZK_LAUNCH_CHECK();
   return 0;
 }

@@ -1071,6 +1071,37 @@ int zk_encode_requests2(const ZkReqBatch* b, int64_t n, int64_t* sizes,
   return 0;
 }
 
+// zk_encode_requests2 with the sizes pass done by the producer of the batch
+// (bench_gen_get): `sizes` (frame bytes per request) and `bsum` (their sum
+// per 256-request block) are given, every request well-formed.  Two
+// launches: the block sums' scan, the write.
+int zk_encode_requests_presized(const ZkReqBatch* b, int64_t n,
+                                const int64_t* sizes, const int64_t* bsum,
+                                int64_t* rec_off, int64_t* total,
+                                int64_t* scan_ws, uint8_t* out,
+                                int64_t out_cap, int64_t* xid_tab,
+                                int64_t xid_mask, int32_t* err,
+                                int32_t terminate, hipStream_t st) {
+  if (n <= 0)
+    return zk_encode_requests2(b, n, nullptr, rec_off, total, scan_ws, out,
+                               out_cap, xid_tab, xid_mask, err, terminate,
+                               st);
+  const unsigned nb = zk::nblk(n);
+  int64_t* bbase = scan_ws + nb;
+  int rc = zk_scan_small_i64(bsum, bbase, nb, total, st);
+  if (rc) return rc;
+  if (zk::enc_swz() == 1)
+    zk::req_write<1><<<nb, zk::ENC_T, zk::STAGE_BYTES, st>>>(
+        *b, n, sizes, bbase, nullptr, rec_off, total, out, out_cap, xid_tab,
+        xid_mask, err, terminate, nullptr, 0);
+  else
+    zk::req_write<0><<<nb, zk::ENC_T, zk::STAGE_BYTES, st>>>(
+        *b, n, sizes, bbase, nullptr, rec_off, total, out, out_cap, xid_tab,
+        xid_mask, err, terminate, nullptr, 0);
+  ZK_LAUNCH_CHECK();
+  return 0;
+}
+
 int zk_encode_requests(const ZkReqBatch* b, int64_t n, int64_t* sizes,
                        int64_t* rec_off, int64_t* total, int64_t* scan_ws,
                        uint8_t* out, int64_t out_cap, int64_t* xid_tab,

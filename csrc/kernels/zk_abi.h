@@ -161,6 +161,10 @@ int zk_scan_excl_i32(const int32_t*, int64_t*, int64_t, int64_t*, int64_t*,
 int zk_encode_requests2(const ZkReqBatch*, int64_t, int64_t*, int64_t*,
                         int64_t*, int64_t*, uint8_t*, int64_t, int64_t*,
                         int64_t, int32_t*, int32_t, hipStream_t);
+int zk_encode_requests_presized(const ZkReqBatch*, int64_t, const int64_t*,
+                                const int64_t*, int64_t*, int64_t*, int64_t*,
+                                uint8_t*, int64_t, int64_t*, int64_t,
+                                int32_t*, int32_t, hipStream_t);
 int zk_encode_set_watches(const int64_t*, const int32_t*, const uint8_t*,
                           int64_t, int64_t, int64_t, int64_t, int64_t*,
                           int64_t*, int64_t*, int64_t*, uint8_t*, int64_t,
@@ -271,7 +275,7 @@ int zk_tree_seq_order(const ZkTree*, const uint8_t*, const int64_t*,
 int zk_tree_digest(const ZkTree*, unsigned long long*, hipStream_t);
 int zk_bench_gen_get(int64_t, uint64_t, int64_t, int64_t, int32_t,
                      const int64_t*, int64_t*, int32_t*, int64_t*, int32_t*,
-                     const int64_t*, hipStream_t);
+                     const int64_t*, int64_t*, int64_t*, hipStream_t);
 int zk_bench_check_get(int64_t, const int32_t*, const int32_t*,
                        const int32_t*, const int32_t*, const int64_t*,
                        const int32_t*, const int64_t*, const int32_t*,

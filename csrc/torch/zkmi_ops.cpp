@@ -291,6 +291,31 @@ void encode_requests(const std::vector<Tensor>& batch, int64_t n,
          "encode_requests");
 }
 
+// encode_requests with the sizes and block sums given (bench_gen_get wrote
+// them): the encode's scan and write only
+void encode_requests_presized(const std::vector<Tensor>& batch, int64_t n,
+                              const Tensor& sizes, const Tensor& bsum,
+                              const Tensor& rec_off, const Tensor& total,
+                              const Tensor& ws, const Tensor& out,
+                              const c10::optional<Tensor>& xid_tab,
+                              int64_t xid_mask, const Tensor& err,
+                              bool terminate) {
+  ZkReqBatch b = req_batch(batch, n);
+  const Tensor* r = &batch[0];
+  const int64_t m = std::max<int64_t>(n, 1);
+  int64_t* tab = Popt<int64_t>(xid_tab, I64, xid_mask + 1, "xid_tab", r);
+  hip_ok(zk_encode_requests_presized(
+             &b, n, P<int64_t>(sizes, I64, m, "sizes", r),
+             P<int64_t>(bsum, I64, (m + 255) / 256, "bsum", r),
+             P<int64_t>(rec_off, I64, m, "rec_off", r),
+             P<int64_t>(total, I64, 1, "total", r),
+             P<int64_t>(ws, I64, zk_scan_workspace(m), "ws", r),
+             P<uint8_t>(out, U8, 1, "out", r), out.numel(), tab, xid_mask,
+             P<int32_t>(err, I32, 1, "err", r), terminate ? 1 : 0,
+             cur_stream()),
+         "encode_requests_presized");
+}
+
 void encode_set_watches(const Tensor& poff, const Tensor& plen,
                         const Tensor& arena, int64_t n, int64_t c0,
                         int64_t c1, int64_t rel_zxid, const Tensor& sizes,
@@ -829,7 +854,11 @@ void tree_expire(const std::vector<Tensor>& t, int64_t session, int64_t ncap,
 void bench_gen_get(int64_t n, int64_t seed, int64_t leaf0, int64_t nleaves,
                    int64_t xid_base, const Tensor& node_pw, const Tensor& idx,
                    const Tensor& xid, const Tensor& poff, const Tensor& plen,
-                   const c10::optional<Tensor>& state) {
+                   const c10::optional<Tensor>& state,
+                   const c10::optional<Tensor>& sizes,
+                   const c10::optional<Tensor>& bsum) {
+  TORCH_CHECK(sizes.has_value() == bsum.has_value(),
+              "zkmi: bench_gen_get: sizes and bsum together");
   TORCH_CHECK(leaf0 >= 0 && leaf0 + nleaves <= node_pw.numel(),
               "zkmi: bench_gen_get leaf range");
   TORCH_CHECK(nleaves > 0, "zkmi: bench_gen_get needs leaves");
@@ -841,6 +870,9 @@ void bench_gen_get(int64_t n, int64_t seed, int64_t leaf0, int64_t nleaves,
                           P<int64_t>(poff, I64, n, "path_off", &node_pw),
                           P<int32_t>(plen, I32, n, "path_len", &node_pw),
                           Popt<int64_t>(state, I64, 2, "state", &node_pw),
+                          Popt<int64_t>(sizes, I64, n, "sizes", &node_pw),
+                          Popt<int64_t>(bsum, I64, (n + 255) / 256, "bsum",
+                                        &node_pw),
                           cur_stream()),
          "bench_gen_get");
 }
@@ -1039,6 +1071,10 @@ TORCH_LIBRARY(zkmi, m) {
         "Tensor(b!) rec_off, Tensor(c!) total, Tensor(d!) ws, "
         "Tensor(e!) out, Tensor(f!)? xid_tab, int xid_mask, Tensor(g!) err, "
         "bool terminate) -> ()", &encode_requests);
+  m.def("encode_requests_presized(Tensor[] batch, int n, Tensor sizes, "
+        "Tensor bsum, Tensor(b!) rec_off, Tensor(c!) total, Tensor(d!) ws, "
+        "Tensor(e!) out, Tensor(f!)? xid_tab, int xid_mask, Tensor(g!) err, "
+        "bool terminate) -> ()", &encode_requests_presized);
   m.def("encode_set_watches(Tensor poff, Tensor plen, Tensor arena, int n, "
         "int c0, int c1, int rel_zxid, Tensor(a!) sizes, Tensor(b!) off, "
         "Tensor(c!) total, Tensor(d!) ws, Tensor(e!) out, Tensor(f!) err) "
@@ -1129,8 +1165,9 @@ TORCH_LIBRARY(zkmi, m) {
         "Tensor(b!) removed) -> ()", &tree_expire);
   m.def("bench_gen_get(int n, int seed, int leaf0, int nleaves, "
         "int xid_base, Tensor node_pw, Tensor(a!) idx, Tensor(b!) xid, "
-        "Tensor(c!) path_off, Tensor(d!) path_len, Tensor? state=None) "
-        "-> ()", &bench_gen_get);
+        "Tensor(c!) path_off, Tensor(d!) path_len, Tensor? state=None, "
+        "Tensor(e!)? sizes=None, Tensor(f!)? bsum=None) -> ()",
+        &bench_gen_get);
   m.def("bench_check_get(int n, Tensor[] reply, Tensor idx, Tensor xid, "
         "Tensor data_len, Tensor(a!) acc) -> ()", &bench_check_get);
   m.def("bench_check_notif(int total, int n_per, Tensor seeds, int leaf0, "

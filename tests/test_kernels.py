@@ -604,6 +604,37 @@ def test_gpu_get_pipeline_end_to_end(gpu):
         assert bytes(hb[po[k]:po[k] + 37].tobytes()) == data
 
 
+def test_gpu_presized_request_encode_matches(gpu):
+    """The GET pipeline's request encode takes its sizes and block sums from
+    the generator (bench_gen_get) instead of its own sizes pass: the stream,
+    the record offsets and the total must be the general encode's, byte for
+    byte, for a batch that is not a multiple of the 256-request block."""
+    from zkmi.bench.synthetic import GetPipeline
+    from zkmi.ops import batch as B
+    from zkmi.ops import _lib
+    tree = _small_tree(gpu, 20000, 37)
+    n = 5000
+    pipe = GetPipeline(tree, n)
+    pipe.step()
+    t = tree
+    L = _lib.lib()
+    sizes = torch.empty(n, dtype=torch.int64, device=gpu)
+    bsum = torch.empty((n + 255) // 256, dtype=torch.int64, device=gpu)
+    L.bench_gen_get(n, 77, t.leaf0, t.n_leaves, 5, t.node_pw, pipe.idx,
+                    pipe.xid, pipe.poff, pipe.plen, None, sizes, bsum)
+    rb = B.RequestBatch(n, pipe.opcode, pipe.xid, pipe.arg, pipe.poff,
+                        pipe.plen, pipe.zero64, pipe.zero32, pipe.zero32,
+                        t.path_arena, t.slab, pipe.acl_off, pipe.acl_len,
+                        pipe.acl_arena)
+    out_a, off_a, tot_a, err_a = B.encode_requests(rb)
+    out_b, off_b, tot_b, err_b = B.encode_requests(rb, presized=(sizes, bsum))
+    ta, tb = int(tot_a.item()), int(tot_b.item())
+    assert ta == tb and int(err_a.item()) == int(err_b.item()) == 0
+    assert torch.equal(off_a, off_b)
+    assert torch.equal(out_a[:ta], out_b[:tb])
+    assert int(bsum.sum().item()) == ta
+
+
 def test_gpu_get_check_samples_payload_bytes(gpu):
     """The fused GET check compares the payload bytes of one reply in 16
     with its node's slot: a reply stream whose every payload has one byte

@@ -58,6 +58,9 @@ _FREE_COMPACT = os.environ.get('ZKMI_FREE_COMPACT', '1') == '1'
 _FINISH_SCAN = os.environ.get('ZKMI_FINISH_SCAN', '1') == '1'
 # the largest batch tree_seq_order numbers
 _SEQ_MAX = 1 << 24
+# ZKMI_GET_PRESIZED=0: the GET pipelines' request encode runs its own sizes
+# pass instead of taking the generator's (bench_gen_get sizes / bsum)
+_GET_PRESIZED = os.environ.get('ZKMI_GET_PRESIZED', '1') == '1'
 # ZKMI_SRV_GROUP: K1 tiles a wave on the GPU server's request streams
 # (unset: one, the scanner's default without a frame hint)
 _SRV_GROUP = (int(os.environ['ZKMI_SRV_GROUP'])
@@ -671,6 +674,11 @@ class GetPipeline(object):
         self.xid = torch.empty(n, dtype=I32, device=dev)
         self.poff = torch.empty(n, dtype=I64, device=dev)
         self.plen = torch.empty(n, dtype=I32, device=dev)
+        # the encode's sizes pass, written by the generator
+        self.sizes = torch.empty(n, dtype=I64, device=dev) \
+            if _GET_PRESIZED else None
+        self.bsum = torch.empty((n + 255) // 256, dtype=I64, device=dev) \
+            if _GET_PRESIZED else None
         self.gstate = None      # device {seed, step} (see capture)
 
     def _device_seed(self):
@@ -763,14 +771,17 @@ class GetPipeline(object):
         self.step_no += 1
         L.bench_gen_get(n, _i64(seed), t.leaf0, t.n_leaves, self.xid_base,
                         t.node_pw, self.idx, self.xid, self.poff, self.plen,
-                        self.gstate)
+                        self.gstate, self.sizes, self.bsum)
         xid = self.xid
         self.xid_base = (self.xid_base + n) & 0x7fffffff
         rb = B.RequestBatch(n, self.opcode, xid, self.arg, self.poff,
                             self.plen, self.zero64, self.zero32, self.zero32,
                             t.path_arena, t.slab, self.acl_off,
                             self.acl_len, self.acl_arena)
-        tx, rec_off, total, err = B.encode_requests(rb, self.xt, out=self.tx)
+        tx, rec_off, total, err = B.encode_requests(
+            rb, self.xt, out=self.tx,
+            presized=(self.sizes, self.bsum) if self.sizes is not None
+            else None)
         yield
         srv = self.server.serve_steps(tx, _len(total))
         next(srv)

@@ -163,7 +163,7 @@ def _total_err(dev):
 
 
 def encode_requests(batch, xid_table=None, out=None, stream=None,
-                    terminate=False):
+                    terminate=False, presized=None):
     """K10: encode ``batch`` into one framed byte stream.
 
     Returns ``(stream_bytes, rec_off, total)`` — ``total`` is a device
@@ -171,11 +171,15 @@ def encode_requests(batch, xid_table=None, out=None, stream=None,
     ``[:total]``).  When ``out`` is None a buffer sized on the host from the
     batch is allocated (one small D2H copy).  ``terminate``: four 0xFF bytes
     follow the stream when they fit, so :func:`frame_scan` over any host
-    upper bound of its length stops exactly at its end (BAD_LENGTH there)."""
+    upper bound of its length stops exactly at its end (BAD_LENGTH there).
+    ``presized`` = (sizes, bsum): the batch's producer already wrote each
+    frame's bytes and each 256-request block's sum (``bench_gen_get``), so
+    the encode skips its sizes pass."""
     L = _lib.lib()
     n = batch.n
     dev = batch.opcode.device
-    sizes = torch.empty(max(n, 1), dtype=I64, device=dev)
+    sizes = presized[0] if presized is not None else \
+        torch.empty(max(n, 1), dtype=I64, device=dev)
     rec_off = torch.empty(max(n, 1), dtype=I64, device=dev)
     total, err = _total_err(dev)
     ws = torch.empty(L.scan_workspace(max(n, 1)), dtype=I64, device=dev)
@@ -187,8 +191,13 @@ def encode_requests(batch, xid_table=None, out=None, stream=None,
     tab = xid_table.tab if xid_table is not None else None
     mask = xid_table.mask if xid_table is not None else 0
     with _on(stream):
-        L.encode_requests(batch.tensors(), n, sizes, rec_off, total, ws, out,
-                          tab, mask, err, bool(terminate))
+        if presized is not None:
+            L.encode_requests_presized(batch.tensors(), n, sizes, presized[1],
+                                       rec_off, total, ws, out, tab, mask,
+                                       err, bool(terminate))
+        else:
+            L.encode_requests(batch.tensors(), n, sizes, rec_off, total, ws,
+                              out, tab, mask, err, bool(terminate))
     return out, rec_off[:n], total, err
 
 

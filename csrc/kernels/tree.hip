@@ -1911,14 +1911,28 @@ __global__ __launch_bounds__(NT) void tree_finish_scan_k(
     if (threadIdx.x == 0) *total = tot;
     return;
   }
+  // a thread owns FS_V consecutive sums, so a 512K-reply connection's 2048
+  // are one block scan (one value a thread per chunk took eight: 9.9 us
+  // against scan_one_block's 4.2, profiles/r6_get_pmc.md)
+  constexpr int FS_V = 8;
   __shared__ int64_t sm[NT / 64 + 1];
   int64_t carry = 0;
-  for (int64_t c0 = 0; c0 < nb; c0 += NT) {          // (uniform)
-    const int64_t i = c0 + threadIdx.x;
-    const int64_t v = i < nb ? bsum[i] : 0;
+  for (int64_t c0 = 0; c0 < nb; c0 += (int64_t)NT * FS_V) {   // (uniform)
+    const int64_t b = c0 + (int64_t)threadIdx.x * FS_V;
+    int64_t v[FS_V];
+    int64_t s = 0;
+#pragma unroll
+    for (int j = 0; j < FS_V; ++j) {
+      v[j] = b + j < nb ? bsum[b + j] : 0;
+      s += v[j];
+    }
     int64_t tot;
-    const int64_t p = carry + block_excl_scan(v, sm, &tot);
-    if (i < nb) bbase[i] = p;
+    int64_t p = carry + block_excl_scan(s, sm, &tot);
+#pragma unroll
+    for (int j = 0; j < FS_V; ++j) {
+      if (b + j < nb) bbase[b + j] = p;
+      p += v[j];
+    }
     carry += tot;
   }
   if (threadIdx.x == 0) *total = carry;

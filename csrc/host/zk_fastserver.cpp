@@ -183,6 +183,65 @@ struct Node {
   Watchers dw, cw;        // data (GET_DATA / EXISTS), child (GET_CHILDREN)
 };
 
+// A set of node pointers (a session's watched nodes): open addressing,
+// linear probing, backward-shift erase, at most half full — no allocation
+// per element (std::unordered_set's node malloc was most of arming a
+// 65536-path SET_WATCHES).
+struct PtrSet {
+  std::vector<Node*> t = std::vector<Node*>(16, nullptr);
+  size_t n = 0;
+  static size_t hp(const Node* p) {
+    uint64_t x = (uint64_t)(uintptr_t)p;
+    x ^= x >> 33;
+    x *= 0xFF51AFD7ED558CCDull;
+    x ^= x >> 29;
+    return (size_t)x;
+  }
+  size_t size() const { return n; }
+  void reserve(size_t k) {
+    if (2 * k <= t.size()) return;
+    size_t cap = t.size();
+    while (cap < 2 * k) cap *= 2;
+    std::vector<Node*> old(cap, nullptr);
+    old.swap(t);
+    n = 0;
+    for (Node* p : old)
+      if (p != nullptr) insert(p);
+  }
+  bool insert(Node* p) {
+    if (2 * (n + 1) > t.size()) reserve(n + 1);
+    const size_t m = t.size() - 1;
+    for (size_t s = hp(p) & m;; s = (s + 1) & m) {
+      if (t[s] == p) return false;
+      if (t[s] == nullptr) { t[s] = p; ++n; return true; }
+    }
+  }
+  bool erase(Node* p) {
+    const size_t m = t.size() - 1;
+    size_t s = hp(p) & m;
+    for (;; s = (s + 1) & m) {
+      if (t[s] == nullptr) return false;
+      if (t[s] == p) break;
+    }
+    for (size_t j = (s + 1) & m;; j = (j + 1) & m) {
+      if (t[j] == nullptr) break;
+      const size_t home = hp(t[j]) & m;
+      if (((j - home) & m) >= ((j - s) & m)) {
+        t[s] = t[j];
+        s = j;
+      }
+    }
+    t[s] = nullptr;
+    --n;
+    return true;
+  }
+  template <class F>
+  void each(F f) const {
+    for (Node* p : t)
+      if (p != nullptr) f(p);
+  }
+};
+
 // -- big-endian reader / writer ---------------------------------------------
 
 struct Rd {
@@ -358,7 +417,7 @@ struct Server {
   // what each session armed (the index drop_watches walks instead of the
   // tree): nodes it data-/child-watches, missing paths it exist-watches
   struct SessW {
-    std::unordered_set<Node*> d, c;
+    PtrSet d, c;
     std::unordered_set<std::string> e;
   };
   std::unordered_map<int64_t, SessW> sw;
@@ -535,8 +594,8 @@ struct Server {
   void drop_watches(int64_t sid) {
     auto it = sw.find(sid);
     if (it == sw.end()) return;
-    for (Node* nd : it->second.d) nd->dw.drop(sid);
-    for (Node* nd : it->second.c) nd->cw.drop(sid);
+    it->second.d.each([&](Node* nd) { nd->dw.drop(sid); });
+    it->second.c.each([&](Node* nd) { nd->cw.drop(sid); });
     for (const std::string& p : it->second.e) {
       auto e = ew.find(p);
       if (e == ew.end()) continue;
@@ -588,43 +647,72 @@ struct Server {
     }
     const size_t n = es.size();
     std::vector<Node*> nds(n);
+    // the lookups' misses overlapped (serve_parallel's lookahead): path
+    // i + 12's index slot, i + 8's node, i + 4's path bytes prefetched
     auto look = [&](size_t a, size_t b) {
-      std::string p;
+      uint64_t hs[16];
+      auto slot = [&](size_t g) -> const IxEnt* {
+        const IxEnt* e = ix_slot(hs[g & 15]);
+        return e->nd != nullptr && e->h == hs[g & 15] ? e : nullptr;
+      };
+      auto stage = [&](size_t g, int st) {
+        if (g >= b) return;
+        if (st == 0) {
+          hs[g & 15] = phash(es[g].s, (size_t)es[g].l);
+          __builtin_prefetch(ix_slot(hs[g & 15]));
+        } else if (const IxEnt* e = slot(g)) {
+          if (st == 1) {
+            __builtin_prefetch(e->nd);
+            __builtin_prefetch((const char*)e->nd + 64);
+            __builtin_prefetch((const char*)e->nd + 128);
+          } else {
+            __builtin_prefetch(e->nd->path.data());
+          }
+        }
+      };
+      for (size_t g = a; g < a + 12; ++g) stage(g, 0);
+      for (size_t g = a; g < a + 8; ++g) stage(g, 1);
+      for (size_t g = a; g < a + 4; ++g) stage(g, 2);
       for (size_t i = a; i < b; ++i) {
-        p.assign(es[i].s, (size_t)es[i].l);
-        nds[i] = find(p);
+        stage(i + 12, 0);
+        stage(i + 8, 1);
+        stage(i + 4, 2);
+        nds[i] = ix_find(es[i].s, (size_t)es[i].l, hs[i & 15]);
       }
     };
-    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-    const size_t T = n >= SW_PAR_MIN ? std::min<size_t>(SW_THREADS, hw) : 1;
-    if (T > 1) {
-      std::vector<std::thread> th;
-      for (size_t t = 1; t < T; ++t)
-        th.emplace_back(look, n * t / T, n * (t + 1) / T);
-      look(0, n / T);
-      for (auto& t : th) t.join();
-    } else {
+    // on the read-burst helpers when they are free (no thread started per
+    // call), else on this thread
+    const int K = n >= SW_PAR_MIN && pool != nullptr
+                      ? std::min<int>(pool->size() + 1, (int)SW_THREADS)
+                      : 1;
+    if (K <= 1 || !pool->run(K, [&](int k) {
+          look(n * k / K, n * (k + 1) / K);
+        }))
       look(0, n);
-    }
     std::lock_guard<std::mutex> g(wmu);
     SessW& ss = sw[sid];
     ss.d.reserve(ss.d.size() + n);
     std::string path;
-    for (size_t i = 0; i < n; ++i) {
-      Node* nd = nds[i];
+    auto P = [&](size_t i) -> const std::string& {
       path.assign(es[i].s, (size_t)es[i].l);
+      return path;
+    };
+    for (size_t i = 0; i < n; ++i) {
+      if (i + 8 < n && nds[i + 8] != nullptr)
+        __builtin_prefetch(nds[i + 8]->dw.s.data());
+      Node* nd = nds[i];
       if (es[i].list == 0) {
-        if (nd == nullptr) notify(sid, EV_DELETED, path, self);
-        else if (nd->st.mzxid > rel) notify(sid, EV_DATA_CHANGED, path, self);
-        else arm(0, path, nd, sid, &ss);
+        if (nd == nullptr) notify(sid, EV_DELETED, P(i), self);
+        else if (nd->st.mzxid > rel) notify(sid, EV_DATA_CHANGED, P(i), self);
+        else if (nd->dw.add(sid)) ss.d.insert(nd);        // (arm 0)
       } else if (es[i].list == 1) {
-        if (nd != nullptr) notify(sid, EV_CREATED, path, self);
-        else arm(0, path, nullptr, sid, &ss);
+        if (nd != nullptr) notify(sid, EV_CREATED, P(i), self);
+        else arm(0, P(i), nullptr, sid, &ss);
       } else {
-        if (nd == nullptr) notify(sid, EV_DELETED, path, self);
+        if (nd == nullptr) notify(sid, EV_DELETED, P(i), self);
         else if (nd->st.pzxid > rel)
-          notify(sid, EV_CHILDREN_CHANGED, path, self);
-        else arm(1, path, nd, sid, &ss);
+          notify(sid, EV_CHILDREN_CHANGED, P(i), self);
+        else arm(1, P(i), nd, sid, &ss);
       }
     }
   }

@@ -232,6 +232,44 @@ def test_set_watches_catch_up_matches_fake_server():
         m.close()
 
 
+def test_large_set_watches_catch_up_and_rearm():
+    """A SET_WATCHES past the server's parallel lookup size (8192 paths:
+    the lookups run on the helper threads with a prefetch lookahead, the
+    session's watch index is a flat set) replays the changes since relZxid
+    in list order and re-arms the rest: later writes fire exactly those."""
+    n = 12000
+    srv = fast.FastZKServer(preload=n, data_bytes=8, fanout=FANOUT,
+                            serve_threads=4)
+    try:
+        a = Raw(srv.port)
+        w = Raw(srv.port)
+        rel = a.call(_get(leaf(0), False))['zxid']
+        changed = list(range(5, n, 997))
+        for i in changed:
+            w.call(_set(leaf(i)))
+        paths = [leaf(i) for i in range(n)] + ['/bench/none%d' % k
+                                               for k in range(3)]
+        rep = a.call({'opcode': 'SET_WATCHES', 'relZxid': rel,
+                      'events': {'dataChanged': paths}})
+        assert rep['err'] == 'OK'
+        assert a.notes == [('DATA_CHANGED', leaf(i)) for i in changed] + \
+            [('DELETED', '/bench/none%d' % k) for k in range(3)]
+        later = [7, 4001, 11999]
+        for i in later:
+            w.call(_set(leaf(i)))
+        a.sync()
+        assert a.notes[len(changed) + 3:] == [('DATA_CHANGED', leaf(i))
+                                              for i in later]
+        a.close()
+        for i in (8, 9):                   # the closed session's watches
+            w.call(_set(leaf(i)))
+        w.sync()
+        assert w.notes == []
+        w.close()
+    finally:
+        srv.shutdown()
+
+
 def test_member_outage_and_resume():
     """A session on member 0 watches two nodes; member 0 goes down while
     one of them is written; the session resumes on member 1, SET_WATCHES

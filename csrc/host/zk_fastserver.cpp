@@ -421,6 +421,25 @@ struct Server {
     std::unordered_set<std::string> e;
   };
   std::unordered_map<int64_t, SessW> sw;
+  uint64_t sw_epoch = 0;         // bumped (under wmu) when an entry goes
+  // a thread's last session index entry (arming reads: one lookup a burst,
+  // not one a GET); valid while sw_epoch holds
+  struct SwCache {
+    const void* srv = nullptr;
+    int64_t sid = 0;
+    uint64_t epoch = ~0ull;
+    SessW* ss = nullptr;
+  };
+  SessW* sess_w(int64_t sid) {       // (under wmu)
+    static thread_local SwCache tl;
+    if (tl.srv != this || tl.sid != sid || tl.epoch != sw_epoch) {
+      tl.ss = &sw[sid];
+      tl.srv = this;
+      tl.sid = sid;
+      tl.epoch = sw_epoch;
+    }
+    return tl.ss;
+  }
   std::unordered_map<int64_t, Conn*> route;
   std::atomic<uint64_t> n_notes{0};
   // members: connections per member (under mu, exclusive to change)
@@ -603,6 +622,7 @@ struct Server {
       if (e->second.s.empty()) ew.erase(e);
     }
     sw.erase(it);
+    ++sw_epoch;
   }
 
   // -- writes (exclusive tree lock; they take wmu to fire) -------------------
@@ -917,9 +937,14 @@ struct Server {
     // EXISTS arms on a missing node too (an exist watch); GET_DATA only on
     // a node it returns
     if (watch && (nd != nullptr || op == OP_EXISTS)) {
-      key->assign((const char*)ps, pl);
       std::lock_guard<std::mutex> g(wmu);
-      arm(0, *key, nd, sid);
+      SessW* ss = sess_w(sid);
+      if (nd != nullptr) {
+        if (nd->dw.add(sid)) ss->d.insert(nd);          // (arm 0)
+      } else {
+        key->assign((const char*)ps, pl);
+        arm(0, *key, nullptr, sid, ss);
+      }
     }
     const size_t dl = nd != nullptr && op == OP_GET_DATA ? nd->data.size() : 0;
     const size_t body = 16 + (nd == nullptr ? 0

@@ -1105,12 +1105,18 @@ ZK_DEV void ft_group_tail(const FtCtx& C, int64_t send0, bool alive,
     const bool live = alive && !(send & TERM) && c >= tsk &&
                       c < tsk + FT_S;
     if (!live) break;
+    // (dbg: a walked tile's row holds its clocks — before the store, after
+    // it (the load's wait), after the walk, after the records)
+    int64_t* const dk = C.dbg ? C.dbg + 8 * tk : nullptr;
+    const int64_t k_0 = dk ? wall_clock64() : 0;
     ft_store(sb, nxt, lane);
+    const int64_t k_1 = dk ? wall_clock64() : 0;
     if (k + 1 < G && tk + 1 < ntiles) ft_load(C.buf, n, tsk + FT_S, lane, nxt);
     int32_t m;
     const int32_t nrelk = (int32_t)min(n - tsk, (int64_t)1 << 30);
     send = ft_walk(sb, (int32_t)(c - tsk), nrelk, maxp32, tsk,
                    C.list + tk * FT_LMAX, m, lane);
+    const int64_t k_2 = dk ? wall_clock64() : 0;
     FcWalk wk{c, m, 0, m > 0 ? 0 : -1, false, false};
     fc_join_end(wk, send, n);
     if (lane == 0) {
@@ -1123,6 +1129,13 @@ ZK_DEV void ft_group_tail(const FtCtx& C, int64_t send0, bool alive,
       C.rec_entry[tk] = c;
       C.rec_exit[tk] = wk.exit;
       C.rec_meta[tk] = fc_meta(wk);
+      if (dk) {
+        dk[0] = k_0;
+        dk[1] = k_1;
+        dk[2] = k_2;
+        dk[3] = wall_clock64();
+        dk[5] = (int64_t)m;
+      }
     }
     if (lane >= 1 && lane < 5) C.cx[5 * tk + lane] = FC_DEAD;
     kdone = k + 1;

@@ -30,6 +30,27 @@ def host_frames(buf, n):
     return off, ln, stop, bad
 
 
+def walked(tiles, group):
+    """A group's walked tiles (all but its first): medians / p90 (us) of
+    the wait for the tile's load (+ its LDS store), the chain walk through
+    it and the records, and the frames walked per tile."""
+    if group <= 1:
+        return ''
+    d = _lib.lib().frame_scan_dbg(tiles + 1).cpu().numpy().reshape(-1)
+    d = d[:8 * tiles].reshape(tiles, 8)
+    rows = np.array([t for t in range(tiles) if t % group and d[t, 3]])
+    if len(rows) == 0:
+        return ''
+    c = d[rows].astype(np.float64)
+    us = 1.0 / 100.0
+    cols = {'load+store': (c[:, 1] - c[:, 0]) * us,
+            'walk': (c[:, 2] - c[:, 1]) * us,
+            'records': (c[:, 3] - c[:, 2]) * us}
+    out = ' '.join('%s %.2f/%.2f' % (k, np.median(v), np.percentile(v, 90))
+                   for k, v in cols.items())
+    return out + ' frames/tile %d' % int(np.median(c[:, 5]))
+
+
 def phases(tiles, step=1):
     """Per-tile phase medians / p90 (us) of fs_tile's clock: stage, node
     detection, map build (successors + pointer jumping), publish, wait for
@@ -92,6 +113,9 @@ def bench(tag, buf, n_dev, window, reps, group=1):
         sc.scan(buf, n_dev)
         torch.cuda.synchronize()
         line += '\n         ' + phases(tiles, sc.group)
+        wl = walked(tiles, sc.group)
+        if wl:
+            line += '\n         walked tiles: ' + wl
     print(line, flush=True)
     return ok
 

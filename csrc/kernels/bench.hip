@@ -138,9 +138,74 @@ __global__ __launch_bounds__(BG_T) void bench_check_notif(
   if (threadIdx.x == 0 && tot) atomicAdd(ok, (unsigned long long)tot);
 }
 
+// A write batch's consecutive xids: xid[i] = (*base + i) mod 2^31 (the
+// session's next xid on the device; the caller advances it).  One launch
+// for what took an add, a mask and a narrowing copy of a 64-bit iota.
+__global__ __launch_bounds__(BG_T) void bench_xids(
+    int64_t n, const int64_t* __restrict__ base, int32_t* __restrict__ xid) {
+  const int64_t i = (int64_t)blockIdx.x * BG_T + threadIdx.x;
+  if (i < n) xid[i] = (int32_t)((uint64_t)(*base + i) & 0x7fffffffu);
+}
+
+// The write pipelines' per-reply check in one pass (the storm's: clean
+// decode, err OK, the request's xid, the expected payload length) counted
+// into *ok, and the batch's largest reply zxid folded into *zmax — eight
+// element-wise launches and two reductions over the batch before.
+// want_len: per request (want_len_c < 0) or the constant want_len_c.
+__global__ __launch_bounds__(BG_T) void bench_check_writes(
+    int64_t n, const int32_t* __restrict__ status,
+    const int32_t* __restrict__ err, const int32_t* __restrict__ rxid,
+    const int32_t* __restrict__ xid, const int32_t* __restrict__ pay_len,
+    const int32_t* __restrict__ want_len, int32_t want_len_c,
+    const int64_t* __restrict__ zxid, unsigned long long* __restrict__ ok,
+    unsigned long long* __restrict__ zmax) {
+  __shared__ int64_t sm[BG_T / 64 + 1];
+  int64_t good = 0;
+  unsigned long long zm = 0;             // (zxids are >= 0)
+  for (int64_t i = (int64_t)blockIdx.x * BG_T + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * BG_T) {
+    const int32_t wl = want_len_c >= 0 ? want_len_c : want_len[i];
+    good += status[i] == 0 && err[i] == 0 && rxid[i] == xid[i] &&
+            pay_len[i] == wl;
+    zm = max(zm, (unsigned long long)zxid[i]);
+  }
+  int64_t tot;
+  block_excl_scan(good, sm, &tot);
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1)
+    zm = max(zm, (unsigned long long)__shfl_xor((long long)zm, d, 64));
+  if ((threadIdx.x & 63) == 0 && zm) atomicMax(zmax, zm);
+  if (threadIdx.x == 0 && tot) atomicAdd(ok, (unsigned long long)tot);
+}
+
 }  // namespace zk
 
 extern "C" {
+
+int zk_bench_xids(int64_t n, const int64_t* base, int32_t* xid,
+                  hipStream_t st) {
+  if (n <= 0) return 0;
+  zk::bench_xids<<<(unsigned)((n + zk::BG_T - 1) / zk::BG_T), zk::BG_T, 0,
+                   st>>>(n, base, xid);
+  ZK_LAUNCH_CHECK();
+  return 0;
+}
+
+int zk_bench_check_writes(int64_t n, const int32_t* status, const int32_t* err,
+                          const int32_t* rxid, const int32_t* xid,
+                          const int32_t* pay_len, const int32_t* want_len,
+                          int32_t want_len_c, const int64_t* zxid,
+                          unsigned long long* ok, unsigned long long* zmax,
+                          hipStream_t st) {
+  if (n <= 0) return 0;
+  const int64_t nb = min((n + zk::BG_T - 1) / zk::BG_T,
+                         (int64_t)zk::BG_CHECK_BLOCKS);
+  zk::bench_check_writes<<<(unsigned)nb, zk::BG_T, 0, st>>>(
+      n, status, err, rxid, xid, pay_len, want_len, want_len_c, zxid, ok,
+      zmax);
+  ZK_LAUNCH_CHECK();
+  return 0;
+}
 
 int zk_bench_check_notif(int64_t total, int64_t n_per, const uint64_t* seeds,
                          const int64_t* want, int64_t leaf0, int64_t nleaves,

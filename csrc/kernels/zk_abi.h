@@ -276,6 +276,12 @@ int zk_tree_digest(const ZkTree*, unsigned long long*, hipStream_t);
 int zk_bench_gen_get(int64_t, uint64_t, int64_t, int64_t, int32_t,
                      const int64_t*, int64_t*, int32_t*, int64_t*, int32_t*,
                      const int64_t*, int64_t*, int64_t*, hipStream_t);
+int zk_bench_xids(int64_t, const int64_t*, int32_t*, hipStream_t);
+int zk_bench_check_writes(int64_t, const int32_t*, const int32_t*,
+                          const int32_t*, const int32_t*, const int32_t*,
+                          const int32_t*, int32_t, const int64_t*,
+                          unsigned long long*, unsigned long long*,
+                          hipStream_t);
 int zk_bench_check_get(int64_t, const int32_t*, const int32_t*,
                        const int32_t*, const int32_t*, const int64_t*,
                        const int32_t*, const int64_t*, const int32_t*,

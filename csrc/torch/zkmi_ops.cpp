@@ -877,6 +877,39 @@ void bench_gen_get(int64_t n, int64_t seed, int64_t leaf0, int64_t nleaves,
          "bench_gen_get");
 }
 
+void bench_xids(int64_t n, const Tensor& base, const Tensor& xid) {
+  hip_ok(zk_bench_xids(n, P<int64_t>(base, I64, 1, "xid base"),
+                       P<int32_t>(xid, I32, n, "xid", &base), cur_stream()),
+         "bench_xids");
+}
+
+// reply: the decode's SoA (status, err, xid, pay_len, zxid used); want_len
+// per request, or want_len_c >= 0 for all
+void bench_check_writes(int64_t n, const Tensor& status, const Tensor& err,
+                        const Tensor& rxid, const Tensor& xid,
+                        const Tensor& pay_len,
+                        const c10::optional<Tensor>& want_len,
+                        int64_t want_len_c, const Tensor& zxid,
+                        const Tensor& ok, const Tensor& zmax) {
+  TORCH_CHECK(want_len.has_value() || want_len_c >= 0,
+              "zkmi: bench_check_writes needs a want_len");
+  const Tensor* d = &status;
+  hip_ok(zk_bench_check_writes(
+             n, P<int32_t>(status, I32, n, "status", d),
+             P<int32_t>(err, I32, n, "err", d),
+             P<int32_t>(rxid, I32, n, "reply xid", d),
+             P<int32_t>(xid, I32, n, "xid", d),
+             P<int32_t>(pay_len, I32, n, "pay_len", d),
+             Popt<int32_t>(want_len, I32, n, "want_len", d),
+             (int32_t)want_len_c, P<int64_t>(zxid, I64, n, "zxid", d),
+             reinterpret_cast<unsigned long long*>(
+                 P<int64_t>(ok, I64, 1, "ok", d)),
+             reinterpret_cast<unsigned long long*>(
+                 P<int64_t>(zmax, I64, 1, "zmax", d)),
+             cur_stream()),
+         "bench_check_writes");
+}
+
 void bench_check_get(int64_t n, const std::vector<Tensor>& reply,
                      const Tensor& idx, const Tensor& xid,
                      const Tensor& data_len, const Tensor& acc) {
@@ -1168,6 +1201,11 @@ TORCH_LIBRARY(zkmi, m) {
         "Tensor(c!) path_off, Tensor(d!) path_len, Tensor? state=None, "
         "Tensor(e!)? sizes=None, Tensor(f!)? bsum=None) -> ()",
         &bench_gen_get);
+  m.def("bench_xids(int n, Tensor base, Tensor(a!) xid) -> ()", &bench_xids);
+  m.def("bench_check_writes(int n, Tensor status, Tensor err, Tensor rxid, "
+        "Tensor xid, Tensor pay_len, Tensor? want_len, int want_len_c, "
+        "Tensor zxid, Tensor(a!) ok, Tensor(b!) zmax) -> ()",
+        &bench_check_writes);
   m.def("bench_check_get(int n, Tensor[] reply, Tensor idx, Tensor xid, "
         "Tensor data_len, Tensor(a!) acc) -> ()", &bench_check_get);
   m.def("bench_check_notif(int total, int n_per, Tensor seeds, int leaf0, "

@@ -1033,6 +1033,43 @@ def test_gpu_mix_pipeline(gpu):
     assert int(tree.counters[_lib.TC_NODES].item()) == hw
 
 
+def test_gpu_bench_check_writes_and_xids(gpu):
+    """The write pipelines' fused check counts exactly the clean replies
+    (status, err, xid, payload length — per request or one constant) and
+    folds the largest zxid into zmax; the fused xids wrap at 2^31."""
+    from zkmi.ops import _lib
+    L = _lib.lib()
+    n = 70000
+    g = torch.Generator(device=gpu).manual_seed(5)
+    i32 = dict(dtype=torch.int32, device=gpu)
+    status = torch.zeros(n, **i32)
+    err = torch.zeros(n, **i32)
+    xid = torch.arange(n, **i32)
+    rxid = xid.clone()
+    want = torch.randint(1, 50, (n,), generator=g, device=gpu).to(torch.int32)
+    pay = want.clone()
+    zx = torch.randint(0, 1 << 40, (n,), generator=g, device=gpu)
+    status[3] = 1
+    err[700] = -101
+    rxid[4096] += 1
+    pay[69999] += 1
+    ok = torch.zeros(1, dtype=torch.int64, device=gpu)
+    zmax = torch.tensor([5], dtype=torch.int64, device=gpu)
+    L.bench_check_writes(n, status, err, rxid, xid, pay, want, -1, zx, ok,
+                         zmax)
+    assert int(ok.item()) == n - 4
+    assert int(zmax.item()) == int(zx.max().item())
+    ok.zero_()
+    L.bench_check_writes(n, status, err, rxid, xid, want * 0 + 7, None, 7,
+                         zx, ok, zmax)
+    assert int(ok.item()) == n - 3
+    base = torch.tensor([(1 << 31) - 5], dtype=torch.int64, device=gpu)
+    out = torch.empty(10, **i32)
+    L.bench_xids(10, base, out)
+    assert out.cpu().tolist() == [(1 << 31) - 5 + k if k < 5 else k - 5
+                                  for k in range(10)]
+
+
 def test_gpu_storm_pipeline(gpu):
     from zkmi.bench.synthetic import StormPipeline
     tree = _small_tree(gpu, 20000, 37, spare=1.5)

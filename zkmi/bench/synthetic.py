@@ -911,7 +911,8 @@ class _Driver(object):
         self.passes = 0          # > 0: ordered serving in that many passes
 
     def xids(self, n):
-        x = ((self.iota[:n] + self.xid_dev) & 0x7fffffff).to(I32)
+        x = torch.empty(n, dtype=I32, device=self.dev)
+        _lib.lib().bench_xids(n, self.xid_dev, x)     # (one fused launch)
         self.xid_dev.add_(n)
         return x
 
@@ -1441,6 +1442,7 @@ class StormPipeline(object):
         self.cred_sid = torch.zeros(2, dtype=I64, device=dev)
         self.cred_pw = torch.zeros(32, dtype=U8, device=dev)
         self.last_zxid = torch.zeros(1, dtype=I64, device=dev)
+        self.chk = torch.zeros(1, dtype=I64, device=dev)
         self.hs_ok = torch.ones(1, dtype=torch.bool, device=dev)
         self.cr_tx = torch.empty(256, dtype=U8, device=dev)
         self.cr_ws = torch.empty(_lib.lib().scan_workspace(2),
@@ -1667,8 +1669,12 @@ class StormPipeline(object):
             # the reply stream kept with them), for cross_read
             self.first = (self.my_rx.clone(), rep.pay_off[:n].clone(),
                           rep.pay_len[:n].clone())
-        torch.maximum(self.last_zxid, rep.zxid[:n].max().view(1),
-                      out=self.last_zxid)
+        # the replies' check (counted into chk) and the batch's largest
+        # zxid (into last_zxid), one fused pass (csrc/kernels/bench.hip)
+        self.chk.zero_()
+        _lib.lib().bench_check_writes(n, rep.status, rep.err, rep.xid, rb.xid,
+                                      rep.pay_len, self.want_len, -1,
+                                      rep.zxid, self.chk, self.last_zxid)
         expire_ok = True
         if not resume and self.k >= 1 and self.world > 1:
             # the generation before expires on every member: here its first
@@ -1695,11 +1701,8 @@ class StormPipeline(object):
             expire_ok = self.removed[0] == 2 * n
         if not validate:
             return None
-        good = ((rep.status[:n] == 0) & (rep.err[:n] == 0) &
-                (rep.xid[:n] == rb.xid) &
-                (rep.pay_len[:n] == self.want_len)).sum()
-        good = torch.where(self.hs_ok[0] & self.len_ok[0] & expire_ok, good,
-                           0)
+        good = torch.where(self.hs_ok[0] & self.len_ok[0] & expire_ok,
+                           self.chk[0], 0)
         if acc is None:
             return good
         acc[:1] += good

@@ -160,27 +160,101 @@ __global__ __launch_bounds__(BG_T) void bench_check_writes(
     const int64_t* __restrict__ zxid, unsigned long long* __restrict__ ok,
     unsigned long long* __restrict__ zmax) {
   __shared__ int64_t sm[BG_T / 64 + 1];
+  __shared__ unsigned long long zw[BG_T / 64];
+  constexpr int U = 4;               // requests a thread, loads issued first
   int64_t good = 0;
-  unsigned long long zm = 0;             // (zxids are >= 0)
-  for (int64_t i = (int64_t)blockIdx.x * BG_T + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * BG_T) {
-    const int32_t wl = want_len_c >= 0 ? want_len_c : want_len[i];
-    good += status[i] == 0 && err[i] == 0 && rxid[i] == xid[i] &&
-            pay_len[i] == wl;
-    zm = max(zm, (unsigned long long)zxid[i]);
+  unsigned long long zm = 0;         // (zxids are >= 0)
+  const int64_t stride = (int64_t)gridDim.x * BG_T;
+  for (int64_t i0 = (int64_t)blockIdx.x * BG_T + threadIdx.x; i0 < n;
+       i0 += U * stride) {
+    int32_t s[U], e[U], rx[U], x[U], pl[U], wl[U];
+    int64_t z[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + u * stride;
+      const bool in = i < n;
+      s[u] = in ? status[i] : 1;
+      e[u] = in ? err[i] : 0;
+      rx[u] = in ? rxid[i] : 0;
+      x[u] = in ? xid[i] : 0;
+      pl[u] = in ? pay_len[i] : 0;
+      wl[u] = in ? (want_len_c >= 0 ? want_len_c : want_len[i]) : 0;
+      z[u] = in ? zxid[i] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      good += s[u] == 0 && e[u] == 0 && rx[u] == x[u] && pl[u] == wl[u];
+      zm = max(zm, (unsigned long long)z[u]);
+    }
   }
   int64_t tot;
   block_excl_scan(good, sm, &tot);
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1)
     zm = max(zm, (unsigned long long)__shfl_xor((long long)zm, d, 64));
-  if ((threadIdx.x & 63) == 0 && zm) atomicMax(zmax, zm);
-  if (threadIdx.x == 0 && tot) atomicAdd(ok, (unsigned long long)tot);
+  if ((threadIdx.x & 63) == 0) zw[threadIdx.x >> 6] = zm;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long b = 0;
+#pragma unroll
+    for (int w = 0; w < BG_T / 64; ++w) b = max(b, zw[w]);
+    if (b) atomicMax(zmax, b);
+    if (tot) atomicAdd(ok, (unsigned long long)tot);
+  }
+}
+
+// The storm's handshake check and credential update in one single-lane
+// launch (about fifteen one-element tensor ops a step before, each a
+// kernel): a resume must come back RESUMED with the current session's id,
+// password and timeout, and the expired session tried beside it (`prev`)
+// refused with id 0; a birth must be NEW with the id the step expects
+// (`want`), which with its password becomes the current credentials (the
+// old current ones the previous).  hs_ok &= the outcome.
+__global__ void bench_storm_hs(int32_t resume, int32_t prev, int32_t timeout,
+                               const int32_t* __restrict__ status,
+                               const int64_t* __restrict__ sid,
+                               const int32_t* __restrict__ tmo,
+                               const int32_t* __restrict__ outcome,
+                               const int64_t* __restrict__ bound,
+                               const uint8_t* __restrict__ resp,
+                               const int64_t* __restrict__ want,
+                               int64_t* __restrict__ cred_sid,
+                               uint8_t* __restrict__ cred_pw,
+                               bool* __restrict__ hs_ok) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  bool ok;
+  if (resume) {
+    ok = status[0] == 0 && sid[0] == cred_sid[0] && outcome[0] == SC_RESUMED &&
+         tmo[0] == timeout;
+    for (int k = 0; k < 16; ++k) ok = ok && resp[24 + k] == cred_pw[k];
+    if (prev) ok = ok && outcome[1] == SC_EXPIRED && sid[1] == 0;
+  } else {
+    const int64_t w = *want;
+    ok = status[0] == 0 && outcome[0] == SC_NEW && sid[0] == w && bound[0] == w;
+    cred_sid[1] = cred_sid[0];
+    for (int k = 0; k < 16; ++k) cred_pw[16 + k] = cred_pw[k];
+    cred_sid[0] = sid[0];
+    for (int k = 0; k < 16; ++k) cred_pw[k] = resp[24 + k];
+  }
+  *hs_ok = *hs_ok && ok;
 }
 
 }  // namespace zk
 
 extern "C" {
+
+int zk_bench_storm_hs(int32_t resume, int32_t prev, int32_t timeout,
+                      const int32_t* status, const int64_t* sid,
+                      const int32_t* tmo, const int32_t* outcome,
+                      const int64_t* bound, const uint8_t* resp,
+                      const int64_t* want, int64_t* cred_sid,
+                      uint8_t* cred_pw, bool* hs_ok, hipStream_t st) {
+  zk::bench_storm_hs<<<1, 64, 0, st>>>(resume, prev, timeout, status, sid, tmo,
+                                       outcome, bound, resp, want, cred_sid,
+                                       cred_pw, hs_ok);
+  ZK_LAUNCH_CHECK();
+  return 0;
+}
 
 int zk_bench_xids(int64_t n, const int64_t* base, int32_t* xid,
                   hipStream_t st) {
@@ -198,8 +272,10 @@ int zk_bench_check_writes(int64_t n, const int32_t* status, const int32_t* err,
                           unsigned long long* ok, unsigned long long* zmax,
                           hipStream_t st) {
   if (n <= 0) return 0;
-  const int64_t nb = min((n + zk::BG_T - 1) / zk::BG_T,
-                         (int64_t)zk::BG_CHECK_BLOCKS);
+  // four requests a thread in one pass (two atomics a block: 2048 for a
+  // 1M-request batch)
+  const int64_t nb = min((n + 4 * zk::BG_T - 1) / (4 * zk::BG_T),
+                         (int64_t)(2 * zk::BG_CHECK_BLOCKS));
   zk::bench_check_writes<<<(unsigned)nb, zk::BG_T, 0, st>>>(
       n, status, err, rxid, xid, pay_len, want_len, want_len_c, zxid, ok,
       zmax);

@@ -23,9 +23,7 @@ namespace zk {
 constexpr int SS_T = 256;
 constexpr int32_t CR_RESP_BYTES = 41;
 enum : int32_t { SS_FREE = 0, SS_ALIVE = 1, SS_CLOSED = 2 };
-// per-request outcome
-enum : int32_t { SC_NEW = 0, SC_RESUMED = 1, SC_EXPIRED = 2, SC_REFUSED = 3,
-                 SC_BAD = 4, SC_FULL = 5 };
+// (per-request outcomes: SC_* in zk_common.h)
 
 // The table slot of session id s (-1: not one this table can hold).
 ZK_DEV int64_t sess_slot(const ZkSessionTable& tab, int64_t s,

@@ -277,6 +277,10 @@ int zk_bench_gen_get(int64_t, uint64_t, int64_t, int64_t, int32_t,
                      const int64_t*, int64_t*, int32_t*, int64_t*, int32_t*,
                      const int64_t*, int64_t*, int64_t*, hipStream_t);
 int zk_bench_xids(int64_t, const int64_t*, int32_t*, hipStream_t);
+int zk_bench_storm_hs(int32_t, int32_t, int32_t, const int32_t*,
+                      const int64_t*, const int32_t*, const int32_t*,
+                      const int64_t*, const uint8_t*, const int64_t*,
+                      int64_t*, uint8_t*, bool*, hipStream_t);
 int zk_bench_check_writes(int64_t, const int32_t*, const int32_t*,
                           const int32_t*, const int32_t*, const int32_t*,
                           const int32_t*, int32_t, const int64_t*,

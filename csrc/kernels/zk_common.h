@@ -15,6 +15,10 @@
 
 namespace zk {
 
+// Handshake outcome per ConnectRequest (session.hip; zkmi/ops/_lib.py SC_*)
+enum : int32_t { SC_NEW = 0, SC_RESUMED = 1, SC_EXPIRED = 2, SC_REFUSED = 3,
+                 SC_BAD = 4, SC_FULL = 5 };
+
 constexpr int WAVE = 64;
 
 // opcodes (lib/zk-consts.js:84-105; csrc/proto mirror, tests check parity)

@@ -877,6 +877,32 @@ void bench_gen_get(int64_t n, int64_t seed, int64_t leaf0, int64_t nleaves,
          "bench_gen_get");
 }
 
+// the storm's handshake check + credential update (bench.hip)
+void bench_storm_hs(bool resume, bool prev, int64_t timeout,
+                    const Tensor& status, const Tensor& sid, const Tensor& tmo,
+                    const Tensor& outcome, const Tensor& bound,
+                    const Tensor& resp, const Tensor& want,
+                    const Tensor& cred_sid, const Tensor& cred_pw,
+                    const Tensor& hs_ok) {
+  const Tensor* d = &status;
+  const int64_t m = resume && prev ? 2 : 1;
+  TORCH_CHECK(hs_ok.scalar_type() == at::kBool && hs_ok.is_cuda(),
+              "zkmi: bench_storm_hs hs_ok");
+  hip_ok(zk_bench_storm_hs(
+             resume ? 1 : 0, prev ? 1 : 0, (int32_t)timeout,
+             P<int32_t>(status, I32, m, "status", d),
+             P<int64_t>(sid, I64, m, "sessionId", d),
+             P<int32_t>(tmo, I32, m, "timeOut", d),
+             P<int32_t>(outcome, I32, m, "outcome", d),
+             P<int64_t>(bound, I64, 1, "bound", d),
+             P<uint8_t>(resp, U8, 40, "resp", d),
+             P<int64_t>(want, I64, 1, "want", d),
+             P<int64_t>(cred_sid, I64, 2, "cred_sid", d),
+             P<uint8_t>(cred_pw, U8, 32, "cred_pw", d),
+             hs_ok.data_ptr<bool>(), cur_stream()),
+         "bench_storm_hs");
+}
+
 void bench_xids(int64_t n, const Tensor& base, const Tensor& xid) {
   hip_ok(zk_bench_xids(n, P<int64_t>(base, I64, 1, "xid base"),
                        P<int32_t>(xid, I32, n, "xid", &base), cur_stream()),
@@ -1202,6 +1228,10 @@ TORCH_LIBRARY(zkmi, m) {
         "Tensor(e!)? sizes=None, Tensor(f!)? bsum=None) -> ()",
         &bench_gen_get);
   m.def("bench_xids(int n, Tensor base, Tensor(a!) xid) -> ()", &bench_xids);
+  m.def("bench_storm_hs(bool resume, bool prev, int timeout, Tensor status, "
+        "Tensor sid, Tensor tmo, Tensor outcome, Tensor bound, Tensor resp, "
+        "Tensor want, Tensor(a!) cred_sid, Tensor(b!) cred_pw, "
+        "Tensor(c!) hs_ok) -> ()", &bench_storm_hs);
   m.def("bench_check_writes(int n, Tensor status, Tensor err, Tensor rxid, "
         "Tensor xid, Tensor pay_len, Tensor? want_len, int want_len_c, "
         "Tensor zxid, Tensor(a!) ok, Tensor(b!) zmax) -> ()",

@@ -1436,7 +1436,6 @@ class StormPipeline(object):
         self.acl_id = torch.zeros(batch, dtype=I32, device=dev)
         self.want_len = self.path_len + 10
         self.removed = torch.zeros(1, dtype=I64, device=dev)
-        self.prev_sid = torch.zeros(1, dtype=I64, device=dev)
         # client-side credentials, device only: [cur, prev] session ids and
         # passwords (what the last ConnectResponses carried)
         self.cred_sid = torch.zeros(2, dtype=I64, device=dev)
@@ -1622,38 +1621,24 @@ class StormPipeline(object):
         if self.world > 1:
             torch.add(self.sid_base, self.kdev + 1, out=self.sess_tab)
         o, bound, outcome, resp = self._handshake(resume)
-        if resume:
-            # current session back with the same id and password; the
-            # expired one refused (only once there is one)
-            pw = resp[24:40]
-            ok = ((o['status'][0] == 0) & (o['sessionId'][0] ==
-                                             self.cred_sid[0]) &
-                  (outcome[0] == _lib.SC_RESUMED) &
-                  (o['timeOut'][0] == self.TIMEOUT) &
-                  (pw == self.cred_pw[:16]).all())
-            if self.k >= 1:
-                ok &= (outcome[1] == _lib.SC_EXPIRED) & \
-                    (o['sessionId'][1] == 0)
-        else:
-            # the id the server handed out: member r's k-th session
-            want = sess_dev[0] if self.world == 1 else \
-                self.sess_tab[self.rank]
-            ok = ((o['status'][0] == 0) & (outcome[0] == _lib.SC_NEW) &
-                  (o['sessionId'][0] == want) & (bound[0] == want))
-            # credentials: the new session becomes current, the old one prev
-            self.cred_sid[1:2].copy_(self.cred_sid[0:1])
-            self.cred_pw[16:32].copy_(self.cred_pw[0:16])
-            self.cred_sid[0:1].copy_(o['sessionId'][0:1])
-            self.cred_pw[0:16].copy_(resp[24:40])
-            if self.world > 1:
-                # R3: every member's new session to every member
-                self.prev_recs.copy_(self.recs)
-                mine = torch.cat([o['sessionId'][0:1],
-                                  o['timeOut'][0:1].to(I64),
-                                  resp[24:40].view(I64)])
-                self._gather(self.recs.view(-1), mine)
-                self.sessions.install(self.recs)
-        self.hs_ok &= ok
+        # the outcome check (and, at a birth, the credentials' update) in
+        # one launch: a resume comes back RESUMED with the same id, password
+        # and timeout, the expired one beside it refused; a birth is NEW
+        # with member r's k-th session id (csrc/kernels/bench.hip)
+        want = sess_dev if self.world == 1 else \
+            self.sess_tab[self.rank:self.rank + 1]
+        _lib.lib().bench_storm_hs(
+            resume, resume and self.k >= 1, self.TIMEOUT, o['status'],
+            o['sessionId'], o['timeOut'], outcome, bound, resp, want,
+            self.cred_sid, self.cred_pw, self.hs_ok)
+        if not resume and self.world > 1:
+            # R3: every member's new session to every member
+            self.prev_recs.copy_(self.recs)
+            mine = torch.cat([o['sessionId'][0:1],
+                              o['timeOut'][0:1].to(I64),
+                              resp[24:40].view(I64)])
+            self._gather(self.recs.view(-1), mine)
+            self.sessions.install(self.recs)
         rb = B.RequestBatch(n, self.opcode, self.drv.xids(n), self.arg,
                             self.path_off, self.path_len, self.data_off,
                             self.data_len, self.acl_id, self.path_arena,
@@ -1696,8 +1681,7 @@ class StormPipeline(object):
             sess_dev.sub_(1)
             self.removed.zero_()
             t.expire(_lib.SESS_DEV, self.removed)
-            self.prev_sid.copy_(sess_dev)
-            self.sessions.close(self.prev_sid)
+            self.sessions.close(sess_dev)        # (the expired id, on the device)
             expire_ok = self.removed[0] == 2 * n
         if not validate:
             return None

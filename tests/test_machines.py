@@ -72,7 +72,9 @@ def _scenario_expiry(zk):
     rec = Recorder(c)
     c.wait_connected(10)
     sess = c.loop.run(lambda: c.getSession())
-    zk.drop_connections()
+    # the expiry closes the session's connection itself (server side, in
+    # the server's loop): dropping the connection first let the client's
+    # reconnect race the expiry, and the histories differed by timing
     zk.run(lambda: [zk.db.expire_session(s) for s in list(zk.db.sessions)])
     rec.wait('expire', 1, 15)
     hist = c.loop.run(lambda: list(sess.fsm_history))

@@ -2961,6 +2961,50 @@ __global__ __launch_bounds__(256) void fs_rows(
   }
 }
 
+// A stream of one tile at most (handshakes, a SET_WATCHES frame, small
+// batches): staged once and walked frame by frame by one wave — one launch
+// instead of fs_tile, fs_link and fs_rows (the storm's two handshake
+// streams a step were six launches).  Same results as the tiled scan.
+__global__ __launch_bounds__(64) void fs_small(
+    const uint8_t* __restrict__ buf, const int64_t* __restrict__ n_dev,
+    int64_t n_cap, int64_t maxp, int64_t* __restrict__ foff,
+    int32_t* __restrict__ flen, int64_t cap, int64_t* __restrict__ result) {
+  __shared__ __attribute__((aligned(16))) uint8_t sb[FT_STAGE];
+  const int lane = threadIdx.x;
+  const int64_t n = stream_len(n_dev, n_cap);       // (<= FT_S)
+  fc_stage<FT_S>(buf, n, 0, sb, lane);
+  int32_t c = 0, k = 0;
+  bool bad = false;
+  const int32_t n32 = (int32_t)n;
+  while (c + 4 <= n32) {
+    const int32_t len = __builtin_amdgcn_readfirstlane(lds_be32(sb, c));
+    if (len < 0 || (int64_t)len > maxp) { bad = true; break; }
+    if (c + 4 + len > n32) break;                   // the carry
+    if (lane == 0 && k < cap) {
+      foff[k] = c + 4;
+      flen[k] = len;
+    }
+    ++k;
+    c += 4 + len;
+  }
+  if (lane == 0) {
+    result[0] = k;
+    result[1] = c;
+    result[2] = bad ? 1 : 0;
+    result[3] = k > cap ? 1 : 0;
+  }
+}
+
+// ZKMI_FS_SMALL=0: one-tile streams take the tiled scan too (A/B)
+static bool fs_small_on() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("ZKMI_FS_SMALL");
+    v = (e ? atoi(e) : 1) ? 1 : 0;
+  }
+  return v != 0;
+}
+
 struct FsPlan {
   int64_t tiles;
   size_t off_list, off_pre, off_sx, off_lbw, off_rent, off_rexit, off_rmeta,
@@ -3112,6 +3156,13 @@ int zk_frame_scan5(const uint8_t* buf, const int64_t* n_dev, int64_t n_cap,
   FsPlan p = fs_plan(n_cap);
   if ((int64_t)p.total > ws_bytes) return -1;
   const int64_t tiles = p.tiles;
+  if (n_cap <= FT_S && !(flags & (1 | 0xFFFF00)) && fs_small_on() &&
+      fs_dbg_buf(tiles) == nullptr) {
+    fs_small<<<1, 64, 0, st>>>(buf, n_dev, n_cap, maxp, foff, flen, cap,
+                               result);
+    ZK_LAUNCH_CHECK();
+    return 0;
+  }
   uint16_t* list = (uint16_t*)(ws + p.off_list);
   uint16_t* pre = (uint16_t*)(ws + p.off_pre);
   int64_t* sx = (int64_t*)(ws + p.off_sx);

@@ -61,6 +61,9 @@ _SEQ_MAX = 1 << 24
 # ZKMI_GET_PRESIZED=0: the GET pipelines' request encode runs its own sizes
 # pass instead of taking the generator's (bench_gen_get sizes / bsum)
 _GET_PRESIZED = os.environ.get('ZKMI_GET_PRESIZED', '1') == '1'
+# ZKMI_STORM_STREAMS=1: the one-member storm step on one stream (its
+# handshake and expiry no longer beside the encode / the reply decode)
+_STORM_STREAMS = os.environ.get('ZKMI_STORM_STREAMS', '2') != '1'
 # ZKMI_SRV_GROUP: K1 tiles a wave on the GPU server's request streams
 # (unset: one, the scanner's default without a frame hint)
 _SRV_GROUP = (int(os.environ['ZKMI_SRV_GROUP'])
@@ -1443,6 +1446,10 @@ class StormPipeline(object):
         self.last_zxid = torch.zeros(1, dtype=I64, device=dev)
         self.chk = torch.zeros(1, dtype=I64, device=dev)
         self.hs_ok = torch.ones(1, dtype=torch.bool, device=dev)
+        # one member: the handshake beside the request encode, the expiry
+        # beside the reply decode, on this second stream (ZKMI_STORM_STREAMS=1:
+        # everything on the caller's)
+        self.side = torch.cuda.Stream(dev) if _STORM_STREAMS else None
         self.cr_tx = torch.empty(256, dtype=U8, device=dev)
         self.cr_ws = torch.empty(_lib.lib().scan_workspace(2),
                                  dtype=I64, device=dev)
@@ -1620,11 +1627,46 @@ class StormPipeline(object):
         torch.add(self.kdev, self.sid0, out=sess_dev)
         if self.world > 1:
             torch.add(self.sid_base, self.kdev + 1, out=self.sess_tab)
+        if self.world == 1 and self.side is not None:
+            return self._step_two_streams(resume, sess_dev, validate, acc)
         o, bound, outcome, resp = self._handshake(resume)
-        # the outcome check (and, at a birth, the credentials' update) in
-        # one launch: a resume comes back RESUMED with the same id, password
-        # and timeout, the expired one beside it refused; a birth is NEW
-        # with member r's k-th session id (csrc/kernels/bench.hip)
+        self._check_handshake(resume, sess_dev, o, bound, outcome, resp)
+        rb = self._batch()
+        if self.world > 1:
+            rep = self._replicated_run(rb, resume)
+        else:
+            rep, _ = self.drv.run(rb, session=_lib.SESS_DEV)
+        self.last = (rb, rep)
+        if not resume and self.world > 1:
+            # the new session's first batch: the created paths (offsets into
+            # the reply stream kept with them), for cross_read
+            self.first = (self.my_rx.clone(), rep.pay_off[:n].clone(),
+                          rep.pay_len[:n].clone())
+        self._check_replies(rb, rep)
+        expire_ok = True
+        if not resume and self.k >= 1 and self.world > 1:
+            # the generation before expires on every member, which holds
+            # all members' sessions' nodes (the replicated tree): each of
+            # them created two batches — here its first batch (our
+            # session) and its second (the previous member's, which moved
+            # here); every member closes all of them
+            self.removed.zero_()
+            for m in range(self.world):
+                # member m's session of the generation before
+                torch.sub(self.sess_tab[m:m + 1], 1, out=sess_dev)
+                t.expire(_lib.SESS_DEV, self.removed)
+            self.sessions.close(self.prev_recs[:, 0].contiguous())
+            expire_ok = self.removed[0] == 2 * n * self.world
+        elif not resume and self.k >= 1:
+            self._expire_prev(sess_dev)
+            expire_ok = self.removed[0] == 2 * n
+        return self._tally(validate, acc, expire_ok)
+
+    def _check_handshake(self, resume, sess_dev, o, bound, outcome, resp):
+        """The outcome check (and, at a birth, the credentials' update) in
+        one launch: a resume comes back RESUMED with the same id, password
+        and timeout, the expired one beside it refused; a birth is NEW with
+        member r's k-th session id (csrc/kernels/bench.hip)."""
         want = sess_dev if self.world == 1 else \
             self.sess_tab[self.rank:self.rank + 1]
         _lib.lib().bench_storm_hs(
@@ -1639,50 +1681,32 @@ class StormPipeline(object):
                               resp[24:40].view(I64)])
             self._gather(self.recs.view(-1), mine)
             self.sessions.install(self.recs)
-        rb = B.RequestBatch(n, self.opcode, self.drv.xids(n), self.arg,
-                            self.path_off, self.path_len, self.data_off,
-                            self.data_len, self.acl_id, self.path_arena,
-                            self.data_arena, self.acl_off, self.acl_len,
-                            self.acl_arena)
-        if self.world > 1:
-            rep = self._replicated_run(rb, resume)
-        else:
-            rep, _ = self.drv.run(rb, session=_lib.SESS_DEV)
-        self.last = (rb, rep)
-        if not resume and self.world > 1:
-            # the new session's first batch: the created paths (offsets into
-            # the reply stream kept with them), for cross_read
-            self.first = (self.my_rx.clone(), rep.pay_off[:n].clone(),
-                          rep.pay_len[:n].clone())
-        # the replies' check (counted into chk) and the batch's largest
-        # zxid (into last_zxid), one fused pass (csrc/kernels/bench.hip)
+
+    def _batch(self):
+        n = self.n
+        return B.RequestBatch(n, self.opcode, self.drv.xids(n), self.arg,
+                              self.path_off, self.path_len, self.data_off,
+                              self.data_len, self.acl_id, self.path_arena,
+                              self.data_arena, self.acl_off, self.acl_len,
+                              self.acl_arena)
+
+    def _check_replies(self, rb, rep):
+        """The replies' check (counted into chk) and the batch's largest
+        zxid (into last_zxid), one fused pass (csrc/kernels/bench.hip)."""
         self.chk.zero_()
-        _lib.lib().bench_check_writes(n, rep.status, rep.err, rep.xid, rb.xid,
-                                      rep.pay_len, self.want_len, -1,
+        _lib.lib().bench_check_writes(self.n, rep.status, rep.err, rep.xid,
+                                      rb.xid, rep.pay_len, self.want_len, -1,
                                       rep.zxid, self.chk, self.last_zxid)
-        expire_ok = True
-        if not resume and self.k >= 1 and self.world > 1:
-            # the generation before expires on every member: here its first
-            # batch (our session) and its second (the previous member's,
-            # which moved here); every member closes all of them
-            # the generation before expires on every member, which holds
-            # all members' sessions' nodes (the replicated tree): each of
-            # them created two batches
-            self.removed.zero_()
-            for m in range(self.world):
-                # member m's session of the generation before
-                torch.sub(self.sess_tab[m:m + 1], 1, out=sess_dev)
-                t.expire(_lib.SESS_DEV, self.removed)
-            self.sessions.close(self.prev_recs[:, 0].contiguous())
-            expire_ok = self.removed[0] == 2 * n * self.world
-        elif not resume and self.k >= 1:
-            # the previous session expires: both of its batches go (its id,
-            # the current one's less one, through TC_SESS)
-            sess_dev.sub_(1)
-            self.removed.zero_()
-            t.expire(_lib.SESS_DEV, self.removed)
-            self.sessions.close(sess_dev)        # (the expired id, on the device)
-            expire_ok = self.removed[0] == 2 * n
+
+    def _expire_prev(self, sess_dev):
+        """The previous session expires: both of its batches go (its id, the
+        current one's less one, through TC_SESS); `removed` counts them."""
+        sess_dev.sub_(1)
+        self.removed.zero_()
+        self.tree.expire(_lib.SESS_DEV, self.removed)
+        self.sessions.close(sess_dev)        # (the expired id, on the device)
+
+    def _tally(self, validate, acc, expire_ok):
         if not validate:
             return None
         good = torch.where(self.hs_ok[0] & self.len_ok[0] & expire_ok,
@@ -1691,6 +1715,46 @@ class StormPipeline(object):
             return good
         acc[:1] += good
         return acc
+
+    def _step_two_streams(self, resume, sess_dev, validate, acc):
+        """One member's step on two streams: the handshake (K9 encode, the
+        server's session table, K1 + K9 decode, its check) on the side
+        stream beside the request encode; the serve once both are done; then
+        the expiry of the previous session on the side stream beside the
+        reply-stream scan, decode and check.  The tree is touched by one
+        stream at a time (the handshake reads the zxid counter before the
+        serve, the expiry writes the tree after it, the reply decode never
+        reads it)."""
+        d = self.drv
+        cur = torch.cuda.current_stream(self.dev)
+        side = self.side
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            o, bound, outcome, resp = self._handshake(resume)
+            self._check_handshake(resume, sess_dev, o, bound, outcome, resp)
+        rb = self._batch()
+        tx, _, total, _ = B.encode_requests(rb, d.xt, out=d.tx)
+        cur.wait_stream(side)
+        rx, rtotal, _, _ = d.server.serve(tx, _len(total),
+                                          session=_lib.SESS_DEV,
+                                          ordered=d.passes > 0,
+                                          passes=max(d.passes, 1))
+        expiring = not resume and self.k >= 1
+        if expiring:
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):
+                self._expire_prev(sess_dev)
+        if d.rscanner is None:
+            d.rscanner = B.FrameScanner(self.n, self.dev, window=d.rwindow)
+        ft = d.rscanner.scan(rx, _len(rtotal))
+        rep = B.decode_replies(rx, ft, d.xt, out=d.reply)
+        self.last = (rb, rep)
+        self._check_replies(rb, rep)
+        expire_ok = True
+        if expiring:
+            cur.wait_stream(side)
+            expire_ok = self.removed[0] == 2 * self.n
+        return self._tally(validate, acc, expire_ok)
 
     # -- the replicated tree --------------------------------------------------
 

@@ -1085,7 +1085,6 @@ __global__ __launch_bounds__(TR_T) void tree_serve_k(
         if (!tree_erase_at(t, f.ent, node)) { L.err = ERR_NO_NODE; break; }
         L.par = t.node_parent[node];
         if (L.par >= 0) parent_touch(t, L.par, -1, true, L.zx);
-        st_be64(s.slab + so + 44, 0);                 // ephemeralOwner
         t.eph[node] = 0;
         freed = node;
         break;
@@ -1979,10 +1978,12 @@ __global__ __launch_bounds__(TR_T) void tree_expire_k(
     unsigned long long* __restrict__ removed) {
   session = sess_of(t, session);
   const int64_t v = (int64_t)blockIdx.x * TR_T + threadIdx.x;
-  const ZkNodeStore& s = t.store;
   // the owner from the contiguous shadow (a node's slab line per node was
   // 256 MB of random reads over a 4M-node tree, 335 us an expiry); a
-  // freed node's shadow is 0
+  // freed node's shadow is 0.  The slab's ephemeralOwner of a freed node is
+  // left as it was: nothing reads a freed slot, and the create that reuses
+  // it writes the whole Stat (fill_stat) — zeroing it was one random slab
+  // line written back per removal (256 MB an expiry of 2M nodes)
   bool hit = v < ncap && v < t.counters[TC_NODES] && t.eph[v] == session;
   const int64_t zx = t.counters[TC_ZXID] + 1;
   int64_t par = -1;
@@ -1995,7 +1996,6 @@ __global__ __launch_bounds__(TR_T) void tree_expire_k(
       ht_shift(t, es, session, tag);
       par = t.node_parent[v];
       if (par >= 0) parent_touch(t, par, -1, true, zx);
-      st_be64(s.slab + s.slot_off[v] + 44, 0);
       t.eph[v] = 0;
     }
   }

@@ -635,13 +635,14 @@ ZK_DEV int32_t ft_chain(const FtNodes<NK>& me, const uint8_t* sb,
   if (D == 0) return 0;
   const uint32_t root = w >> 16;
   int32_t hits = 0;
+  bool on[NK];
 #pragma unroll
   for (int k = 0; k < NK; ++k) {
     const int32_t c = (int32_t)rk_cnt(me.w[k]);
     const int32_t p = me.p[k];
-    const bool on = p >= e && (me.w[k] >> 16) == root && c >= 1 && c <= D;
-    if (on) slot[D - c] = (uint16_t)p;
-    hits += __popcll(__ballot(on));
+    on[k] = p >= e && (me.w[k] >> 16) == root && c >= 1 && c <= D;
+    if (on[k]) slot[D - c] = (uint16_t)p;
+    hits += __popcll(__ballot(on[k]));
   }
   __builtin_amdgcn_wave_barrier();
   // the chain's nodes: its D frame starts, less the last one when that
@@ -659,17 +660,47 @@ ZK_DEV int32_t ft_chain(const FtNodes<NK>& me, const uint8_t* sb,
   // as many hits as chain nodes: no side branch shares the root and a
   // count, every slot holds the chain's start
   if (hits == want) return D;
-  bool ok = true;
-  for (int32_t k = lane; k < D; k += 64) {
-    const int32_t p = slot[k];
-    const int32_t nx = ft_next(sb, p);
-    if (k + 1 < D) {
-      ok &= nx == (int32_t)slot[k + 1];
-    } else if (kind == RK_PART) {
-      ok &= nx == (int32_t)rk_val(w);
+  // the successor check: every slot's frame ends at the next slot
+  auto linked = [&]() {
+    bool ok = true;
+    for (int32_t k = lane; k < D; k += 64) {
+      const int32_t p = slot[k];
+      const int32_t nx = ft_next(sb, p);
+      if (k + 1 < D) {
+        ok &= nx == (int32_t)slot[k + 1];
+      } else if (kind == RK_PART) {
+        ok &= nx == (int32_t)rk_val(w);
+      }
     }
+    return __ballot(!ok) == 0;
+  };
+  if (linked()) return D;
+  // Side branches share the root and a count: a length-like word inside a
+  // frame that ends where its frame does — a create reply's path length
+  // (4 + len past it is the next frame's start: every storm reply frame) —
+  // lands on the chain one frame on, and the slot may hold it.  The chain's
+  // start is the first of them, so each slot keeps its smallest position
+  // (a few rounds: lanes writing one slot at once leave any of their
+  // values), and the successor check decides again.  Without it every storm
+  // reply tile took the serial walk (24 us of its 77,
+  // tools/microbench/k1_bench.py --workload storm).
+  for (int it = 0; it < 8; ++it) {
+    int32_t cur[NK];
+#pragma unroll
+    for (int k = 0; k < NK; ++k)
+      cur[k] = on[k] ? (int32_t)slot[D - (int32_t)rk_cnt(me.w[k])] : 0;
+    bool wr = false;
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+      if (on[k] && me.p[k] < cur[k]) {
+        slot[D - (int32_t)rk_cnt(me.w[k])] = (uint16_t)me.p[k];
+        wr = true;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (!__ballot(wr)) break;
   }
-  return __ballot(!ok) ? -1 : D;
+  return linked() ? D : -1;
 }
 
 ZK_DEV int64_t ft_walk(const uint8_t* sb, int32_t c, int32_t nrel,

@@ -265,6 +265,9 @@ int zk_tree_expire(const ZkTree*, int64_t, int64_t, unsigned long long*,
 int64_t zk_tree_seq_workspace(int64_t ncap);
 int64_t zk_tree_seq_zeroed(int64_t ncap);
 void zk_tree_seq_debug(int64_t* buf);
+// tree_expire_k's phase clocks: 4 int32 per node of the expiries that follow
+// (the buffer covers the tree's node capacity; nullptr turns them off)
+void zk_tree_expire_debug(int32_t* buf);
 int zk_tree_seq_order(const ZkTree*, const uint8_t*, const int64_t*,
                       const int32_t*, const int64_t*, int64_t, uint8_t*,
                       int64_t, int64_t*, hipStream_t);

@@ -830,6 +830,20 @@ void tree_seq_debug(const Tensor& buf) {
   zk_tree_seq_debug(buf.data_ptr<int64_t>());
 }
 
+// tree_expire_k's phase clocks into buf (int32, 4 per node slot: start,
+// lookup + tombstone, backward shift, whole thread; an empty tensor turns
+// them off).  buf must cover 4 x the tree's node capacity.
+void tree_expire_debug(const Tensor& buf) {
+  if (buf.numel() == 0) {
+    zk_tree_expire_debug(nullptr);
+    return;
+  }
+  TORCH_CHECK(buf.is_cuda() && buf.scalar_type() == at::kInt &&
+                  buf.is_contiguous(),
+              "zkmi: tree_expire_debug wants a contiguous device int32 tensor");
+  zk_tree_expire_debug(buf.data_ptr<int32_t>());
+}
+
 // out (int64 [4]): node digest, live nodes, hash entries used, tombstones
 void tree_digest(const std::vector<Tensor>& t, const Tensor& out) {
   ZkTree s = tree(t);
@@ -1208,6 +1222,7 @@ TORCH_LIBRARY(zkmi, m) {
   m.def("tree_seq_workspace(int n) -> int", &tree_seq_workspace);
   m.def("tree_seq_zeroed(int n) -> int", &tree_seq_zeroed);
   m.def("tree_seq_debug(Tensor buf) -> ()", &tree_seq_debug);
+  m.def("tree_expire_debug(Tensor buf) -> ()", &tree_expire_debug);
   m.def("tree_seq_order(Tensor(a!)[] tree, Tensor rx, Tensor frame_off, "
         "Tensor frame_len, Tensor count, int ncap, Tensor(b!) ws, "
         "Tensor(c!) seqno) -> ()", &tree_seq_order);

@@ -131,7 +131,9 @@ def main():
                     help='batch.FS_WINDOW_AUTO_MAX for this run (the largest '
                          'window chosen without long-frame mode)')
     ap.add_argument('--workload', default='get',
-                    help='get, or mix (create / set / delete replies)')
+                    help='get, mix (create / set / delete replies) or storm '
+                         '(EPHEMERAL|SEQUENTIAL creates, --batch 1M for the '
+                         "bench's shape)")
     ap.add_argument('--zxid', type=lambda x: int(x, 0), default=None,
                     help='the tree zxid the GET replies carry (their header '
                          'bytes: length-like words for some ranges)')
@@ -149,10 +151,16 @@ def main():
     if a.workload == 'mix':
         tree = S.GpuTree(1_000_000, 100, device=dev, seed=0,
                          spare=(2 * a.batch + 8192) / 1e6 + 0.05)
+    if a.workload == 'storm':
+        tree = S.GpuTree(1_000_000, 100, device=dev, seed=0, hash_factor=2,
+                         spare=(3 * a.batch + 8192) / 1e6 + 0.05)
     if a.zxid is not None:
         tree.counters[_lib.TC_ZXID] = a.zxid
-    if a.workload == 'mix':
-        pipe = S.MixPipeline(tree, 2 * a.batch, 100, seed=1)
+    if a.workload in ('mix', 'storm'):
+        if a.workload == 'mix':
+            pipe = S.MixPipeline(tree, 2 * a.batch, 100, seed=1)
+        else:
+            pipe = S.StormPipeline(tree, a.batch)
         for _ in range(2):
             pipe.step()
         drv = pipe.drv

@@ -165,6 +165,28 @@ def test_garbage_entries_variable_and_long_frames(gpu):
         _check(r, off, buf, starts)
 
 
+def test_side_branches_on_the_chain_keep_the_map(gpu):
+    """Every create reply's path-length word (26, 20 past its frame's start)
+    is a node whose frame ends at the next frame's start: a side branch
+    with the chain node's root and count (fs_tile's ft_chain keeps each
+    slot's smallest position, then checks the links).  Every 7th frame also
+    holds a word 30 past its start reading 66 — a side branch BEFORE the
+    next frame's node (it ends two frames on) that wins its slot, so the
+    link check must send the tile to the exact walk.  Both exact; the
+    clean stream no slower than a few times a plain one."""
+    n = 1 << 19
+    buf, starts = _create_replies(n, zxid0=0x500000)
+    _, _, base_ms, _ = _scan_timed(buf, n, 256)
+    r, off, ms, st = _scan_timed(buf, n, 256)
+    _check(r, off, buf, starts)
+    early = buf.copy()
+    for p in starts[::7]:
+        early[p + 30:p + 34] = (0, 0, 0, 66)
+    r, off, ms2, st = _scan_timed(early, n, 256)
+    _check(r, off, early, starts)
+    assert ms2 < max(8 * base_ms, 2.0), (ms2, base_ms)
+
+
 def test_phantom_chain_region_is_chased_not_walked(gpu):
     """Create replies whose zxids run through 0x2Exxxx: the bytes 10 past
     every frame start then read as the frame length 46, a phantom chain

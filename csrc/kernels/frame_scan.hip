@@ -1054,32 +1054,77 @@ ZK_DEV void ft_store(uint8_t* sb, const FtTileRegs& r, int lane) {
 
 // The chain from tile-relative c through the staged tile (wave-uniform),
 // its frame starts into L; returns the end code (sx) and the count.
+// After two frames of one size, a hop reads besides the frame's length
+// word (lane 0) the words where the next 63 frames start if they are of
+// that size too (lane l: l frames on), so a run of equal frames — every GET
+// reply of a 100-byte node is 192 bytes — is taken in one step: the
+// leading lanes whose word repeats the length.  One LDS round trip a step
+// either way (a group's walked tiles were ~20 dependent hops each, 34 us
+// of a 47 us group, tools/microbench/k1_bench.py); streams of varied
+// frames keep the one-address hop (a vector address on every hop cost the
+// 0-200 B GET stream 3 %) and the records gathered 64 to a store.
 ZK_DEV int64_t ft_walk(const uint8_t* sb, int32_t c, int32_t nrel,
                        int32_t maxp32, int64_t ts, uint16_t* L, int32_t& mo,
                        int lane) {
-  int32_t m = 0;
+  int32_t m = 0, pb = 0;              // records [pb, m) pending in ent
   uint32_t ent = 0;
   int64_t send;
-  // (the walk is wave-uniform: the position and the bounds in SGPRs keep
-  // a hop to one LDS read and a few scalar instructions)
+  // (the walk is wave-uniform: the position and the bounds in SGPRs)
   c = __builtin_amdgcn_readfirstlane(c);
   nrel = __builtin_amdgcn_readfirstlane(nrel);
   const int32_t lim = min((int32_t)FT_S, nrel);
   if (c >= nrel) {
     send = TERM | (ts + c);
   } else {
-    int32_t len, nx;
-    bool ok;
-    for (;;) {
+    int32_t len = 0, nx = 0, last = 0;      // last: the last frame's size
+    bool ok = true, fin = false;
+    while (!fin) {
       len = __builtin_amdgcn_readfirstlane(lds_be32(sb, c));
       nx = c + 4 + len;
       ok = (uint32_t)len <= (uint32_t)maxp32 && nx <= nrel;
       if (!ok) break;
       ent = lane == (m & 63) ? (uint32_t)c : ent;
       ++m;
-      if ((m & 63) == 0) L[m - 64 + lane] = (uint16_t)ent;
+      if ((m & 63) == 0) {
+        const int32_t q = m - 64 + lane;
+        if (q >= pb) L[q] = (uint16_t)ent;
+        pb = m;
+      }
       if (nx >= lim) break;
       c = nx;
+      if (4 + len != last) {
+        last = 4 + len;
+        continue;
+      }
+      // two frames of one size: steps over the run (lane l reads where
+      // frame l of it would start); frames 0 .. a-1 lie back to back with
+      // that length, and the walk ends after the first reaching the tile's
+      // end.  A step that takes none goes back to the hop above.
+      const int32_t st = last;
+      for (;;) {
+        const int64_t s64 = (int64_t)c + (int64_t)lane * st;
+        const int32_t sp = s64 < lim ? (int32_t)s64 : lim;
+        const int32_t lv = sp < lim ? lds_be32(sb, sp) : -1;
+        const bool acc = sp < lim && lv == st - 4 && sp + st <= nrel;
+        const uint64_t no = ~__ballot(acc);
+        const int32_t a = no ? (int32_t)__builtin_ctzll(no) : 64;
+        if (a == 0) break;
+        const uint64_t end = __ballot(acc && sp + st >= lim);
+        const int32_t f = end ? (int32_t)__builtin_ctzll(end) : 64;
+        const int32_t r = min(a, f + 1);
+        const int32_t q = (m & ~63) + lane;
+        if (q >= pb && q < m) L[q] = (uint16_t)ent;
+        if (lane < r) L[m + lane] = (uint16_t)sp;
+        m += r;
+        pb = m;
+        nx = c + r * st;
+        len = st - 4;
+        if (nx >= lim) {
+          fin = true;
+          break;
+        }
+        c = nx;
+      }
     }
     if (!ok) {
       const bool bad = (c + 4 <= nrel) && ((len < 0) | (len > maxp32));
@@ -1090,7 +1135,10 @@ ZK_DEV int64_t ft_walk(const uint8_t* sb, int32_t c, int32_t nrel,
       send = TERM | (ts + nx);               // the stream ends at nx
     }
   }
-  if (lane < (m & 63)) L[(m & ~63) + lane] = (uint16_t)ent;
+  {
+    const int32_t q = (m & ~63) + lane;
+    if (q >= pb && q < m) L[q] = (uint16_t)ent;
+  }
   mo = m;
   return send;
 }

@@ -65,9 +65,14 @@ _GET_PRESIZED = os.environ.get('ZKMI_GET_PRESIZED', '1') == '1'
 # handshake and expiry no longer beside the encode / the reply decode)
 _STORM_STREAMS = os.environ.get('ZKMI_STORM_STREAMS', '2') != '1'
 # ZKMI_SRV_GROUP: K1 tiles a wave on the GPU server's request streams
-# (unset: one, the scanner's default without a frame hint)
+# (unset: one, the scanner's default without a frame hint; GET request
+# streams take _GET_SRV_GROUP)
 _SRV_GROUP = (int(os.environ['ZKMI_SRV_GROUP'])
               if os.environ.get('ZKMI_SRV_GROUP') else None)
+# GET / routed-GET request streams (equal-sized frames: a group's walk takes
+# a tile's run of them in a step or two): 4 tiles a wave, 0.5255 vs 0.5337
+# ms a step at 1 (profiles/r6_srv_group_ab.log)
+_GET_SRV_GROUP = _SRV_GROUP if _SRV_GROUP is not None else 4
 
 
 def _len(total):
@@ -375,7 +380,7 @@ class GpuServer(object):
     to a :class:`GpuTree`, encode replies."""
 
     def __init__(self, tree, cap_frames, out_cap, window=2048,
-                 seq_order=True):
+                 seq_order=True, group=_SRV_GROUP):
         self.tree = tree
         self.window = window              # K1 entry window of the requests
         # SEQUENTIAL creates numbered in stream order before each serve
@@ -410,7 +415,7 @@ class GpuServer(object):
         self.out = torch.empty(out_cap, dtype=U8, device=dev)
         self.cap_frames = cap_frames
         self.scanner = B.FrameScanner(cap_frames, dev, window=window,
-                                      group=_SRV_GROUP)
+                                      group=group)
         self.ows = None                   # ordered-serve workspace (lazy)
         self.enc_stage = 0                # K13 LDS per workgroup (0: default)
         self.total_err = B._total_err(dev)  # the reply encode's scalars
@@ -660,7 +665,7 @@ class GetPipeline(object):
         # K1 windows: the largest request / reply frame of this workload
         self.server = GpuServer(tree, n, n * (4 + 16 + 4 + dmax + 68) + 64,
                                 window=B.frame_window(17 + maxpath),
-                                seq_order=False)
+                                seq_order=False, group=_GET_SRV_GROUP)
         self.server.read_only = _SERVE_RO
         self.server.enc_stage = _GET_STAGE
         self.rwindow = B.frame_window(4 + 16 + 4 + dmax + 68)

@@ -56,7 +56,7 @@ import torch.distributed as dist
 from .. import consts
 from ..ops import _lib
 from ..ops import batch as B
-from ..bench.synthetic import _SERVE_RO, _i64
+from ..bench.synthetic import _GET_SRV_GROUP, _SERVE_RO, _i64
 
 I64, I32, U8 = torch.int64, torch.int32, torch.uint8
 
@@ -318,7 +318,7 @@ class _Conn(object):
         self.server = GpuServer(t, cap, max(cap * self.rep_max,
                                             W * (self.rep_slot - SEG_HDR))
                                 + 64, window=B.frame_window(self.req_max),
-                                seq_order=False)
+                                seq_order=False, group=_GET_SRV_GROUP)
         # every routed request is a GET_DATA: the serve's read-only instance
         self.server.read_only = _SERVE_RO
         # the replies to this connection's own n requests come back

@@ -64,15 +64,17 @@ _GET_PRESIZED = os.environ.get('ZKMI_GET_PRESIZED', '1') == '1'
 # ZKMI_STORM_STREAMS=1: the one-member storm step on one stream (its
 # handshake and expiry no longer beside the encode / the reply decode)
 _STORM_STREAMS = os.environ.get('ZKMI_STORM_STREAMS', '2') != '1'
-# ZKMI_SRV_GROUP: K1 tiles a wave on the GPU server's request streams
-# (unset: one, the scanner's default without a frame hint; GET request
-# streams take _GET_SRV_GROUP)
-_SRV_GROUP = (int(os.environ['ZKMI_SRV_GROUP'])
-              if os.environ.get('ZKMI_SRV_GROUP') else None)
-# GET / routed-GET request streams (equal-sized frames: a group's walk takes
-# a tile's run of them in a step or two): 4 tiles a wave, 0.5255 vs 0.5337
-# ms a step at 1 (profiles/r6_srv_group_ab.log)
-_GET_SRV_GROUP = _SRV_GROUP if _SRV_GROUP is not None else 4
+# ZKMI_SRV_GROUP: K1 tiles a wave on the GPU server's request streams, for
+# every workload (unset: the defaults below).  Request streams run long
+# stretches of equal-sized frames, which the groups' walk takes a run at a
+# step: 4 tiles a wave (GET 0.5255 vs 0.5337 ms a step at 1, mix 1.215 vs
+# 1.230), the storm's identical creates 8 (1.298 vs 1.316 at 4, 1.344 at
+# 1; profiles/r6_srv_group_ab.log, r6_srv_group_storm_mix_ab.log)
+_SRV_GROUP_ENV = (int(os.environ['ZKMI_SRV_GROUP'])
+                  if os.environ.get('ZKMI_SRV_GROUP') else None)
+_SRV_GROUP = _SRV_GROUP_ENV or 4
+_GET_SRV_GROUP = _SRV_GROUP
+_STORM_SRV_GROUP = _SRV_GROUP_ENV or 8
 
 
 def _len(total):
@@ -893,7 +895,7 @@ class _Driver(object):
     K2-K8 decode of the reply stream."""
 
     def __init__(self, tree, batch, max_path, data_bytes, seed,
-                 seq_order=False):
+                 seq_order=False, group=_SRV_GROUP):
         self.tree = tree
         self.batch = batch
         self.dev = dev = tree.device
@@ -907,7 +909,7 @@ class _Driver(object):
         self.server = GpuServer(
             tree, batch, batch * (4 + 16 + 4 + max(dmax, max_path + 16) + 68)
             + 64, window=B.frame_window(33 + max_path + data_bytes + 128),
-            seq_order=seq_order)
+            seq_order=seq_order, group=group)
         self.rwindow = B.frame_window(4 + 16 + 4 + max(dmax, max_path + 16)
                                       + 68)
         self.reply = B.alloc_replies(batch, dev)
@@ -1409,7 +1411,7 @@ class StormPipeline(object):
         self.rank = dist.get_rank(group) if on else 0
         self.coll = torch.device(coll_device) if coll_device else dev
         self.drv = _Driver(tree, batch, 32, data_bytes, seed,
-                           seq_order=True)
+                           seq_order=True, group=_STORM_SRV_GROUP)
         self.sessions = GpuSessionTable(tree, server_id=self.rank + 1,
                                         members=W)
         if W > 1:

@@ -403,18 +403,18 @@ ZK_DEV int64_t tree_erase_slot(const ZkTree& t, int64_t v, const uint8_t* p,
   const int64_t key = (int64_t)(path_hash(p, n) | 1ull);
   int64_t s = key & t.mask;
   for (int64_t probe = 0; probe <= t.mask; ++probe) {
+    // key and val in one round trip: a live val names its node alone (one
+    // slot holds it at a time: a move parks the old slot at VAL_MOVING
+    // first), and the CAS decides; the key only ends the probe
     const int64_t k = __hip_atomic_load(ht_key(t, s), __ATOMIC_RELAXED,
                                         __HIP_MEMORY_SCOPE_AGENT);
+    const int64_t cur = __hip_atomic_load(ht_val(t, s), __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
     if (k == 0) return -1;
-    if (k == key) {
-      const int64_t cur = __hip_atomic_load(ht_val(t, s), __ATOMIC_RELAXED,
-                                            __HIP_MEMORY_SCOPE_AGENT);
-      if (cur > 0 && val_node(cur) == v &&
-          atomicCAS((unsigned long long*)ht_val(t, s),
-                    (unsigned long long)cur,
-                    (unsigned long long)tag) == (unsigned long long)cur)
-        return s;
-    }
+    if (k == key && cur > 0 && val_node(cur) == v &&
+        atomicCAS((unsigned long long*)ht_val(t, s), (unsigned long long)cur,
+                  (unsigned long long)tag) == (unsigned long long)cur)
+      return s;
     s = (s + 1) & t.mask;
   }
   return -1;
@@ -459,6 +459,13 @@ ZK_DEV void ht_shift(const ZkTree& t, int64_t s, int64_t session,
     int64_t j = (s + 1) & t.mask, cand = -1, cv = 0;
     bool blocked = true, tombs = false;
     for (int k = 0; k < 64; ++k, j = (j + 1) & t.mask) {
+      // an empty key ends the run whatever the val: the usual first slot
+      // (a sparse index) costs one round trip
+      if (__hip_atomic_load(ht_key(t, j), __ATOMIC_RELAXED,
+                            __HIP_MEMORY_SCOPE_AGENT) == 0) {
+        blocked = tombs;
+        break;
+      }
       // val, key, val: a hole another thread fills between the loads
       // would pair its old key with the new val (the key decides whether
       // the entry covers s), so a val that changed blocks
@@ -536,12 +543,12 @@ ZK_DEV int64_t ht_reclaim(const ZkTree& t, int64_t s) {
   int64_t n = 0;
   for (int k = 0; k < 64; ++k) {
     const int64_t nx = (s + 1) & t.mask;
-    if (__hip_atomic_load(ht_key(t, nx), __ATOMIC_RELAXED,
-                          __HIP_MEMORY_SCOPE_AGENT) != 0)
-      break;
-    if (!val_tomb(__hip_atomic_load(ht_val(t, s), __ATOMIC_RELAXED,
-                                    __HIP_MEMORY_SCOPE_AGENT)))
-      break;
+    // (both loads in one round trip)
+    const int64_t kn = __hip_atomic_load(ht_key(t, nx), __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+    const int64_t vs = __hip_atomic_load(ht_val(t, s), __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+    if (kn != 0 || !val_tomb(vs)) break;
     // val first: a reader between the two stores sees a key with val 0
     // (no match, probe on), then the empty key (end of chain)
     __hip_atomic_store(ht_val(t, s), (int64_t)0, __ATOMIC_RELAXED,

@@ -328,18 +328,23 @@ ZK_DEV int64_t tree_insert(const ZkTree& t, int64_t v, const uint8_t* p,
   int64_t s = key & t.mask;
   int64_t tomb = -1, tv = 0;
   for (int64_t probe = 0; probe <= t.mask; ++probe) {
+    int64_t k0 = -1;                   // REUSE: the key loaded below
     if (REUSE) {
+      // key and val in one round trip (the val only matters as a
+      // tombstone to take, and the CAS on it decides)
       int64_t k = __hip_atomic_load(ht_key(t, s), __ATOMIC_RELAXED,
                                     __HIP_MEMORY_SCOPE_AGENT);
+      const int64_t vv = __hip_atomic_load(ht_val(t, s), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
       if (k != 0 && k != key) {
-        if (tomb < 0) {
-          tv = __hip_atomic_load(ht_val(t, s), __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_AGENT);
-          if (val_tomb(tv)) tomb = s;
+        if (tomb < 0 && val_tomb(vv)) {
+          tomb = s;
+          tv = vv;
         }
         s = (s + 1) & t.mask;
         continue;
       }
+      k0 = k;
       if (k == 0 && tomb >= 0) {
         // the name is absent: take the tombstone (val -2 -> 0 claims it;
         // a lookup in between sees a key with val 0 and probes on)
@@ -359,8 +364,8 @@ ZK_DEV int64_t tree_insert(const ZkTree& t, int64_t v, const uint8_t* p,
     // a plain load first: an occupied slot of another key (the usual probe
     // past a tombstone or a collision) costs a load, not an L2 atomic on
     // another line each (keys only ever go 0 -> key within a launch, so a
-    // stale 0 just means the CAS below answers)
-    int64_t k = *ht_key(t, s);
+    // stale 0 just means the CAS below answers); REUSE has just loaded it
+    int64_t k = REUSE ? k0 : *ht_key(t, s);
     if (k == 0)
       k = atomicCAS((unsigned long long*)ht_key(t, s), 0ull,
                     (unsigned long long)key);

@@ -322,9 +322,9 @@ constexpr int64_t TREE_INSERT_TIMEOUT = -4;
 // instead: entries of dead names are recycled by the next batch's names.
 template <bool REUSE = false>
 ZK_DEV int64_t tree_insert(const ZkTree& t, int64_t v, const uint8_t* p,
-                           int32_t n, int32_t dl) {
+                           int32_t n, int32_t dl, int64_t so = -1) {
   const int64_t key = (int64_t)(path_hash(p, n) | 1ull);
-  const int64_t pv = val_pack(v, t.store.slot_off[v]);
+  const int64_t pv = val_pack(v, so >= 0 ? so : t.store.slot_off[v]);
   int64_t s = key & t.mask;
   int64_t tomb = -1, tv = 0;
   for (int64_t probe = 0; probe <= t.mask; ++probe) {
@@ -834,6 +834,10 @@ ZK_DEV int32_t do_create(const ZkTree& t, Lane& L, const uint8_t* data,
   const int32_t pre = seq ? seq_num(t, i) : -1;
   if (nacl <= 0) return ERR_INVALID_ACL;
   if (v < 0) return ERR_SYSTEM;                       // tree full
+  // node v's path and slot offsets, loaded before the parent lookup: their
+  // round trip rides under it (a create is a chain of dependent trips)
+  const int64_t vpo = t.node_path_off[v];
+  const int64_t vso = s.slot_off[v];
   const uint8_t* path = L.path;
   const int32_t pl = L.pl;
   int32_t cut = pl - 1;
@@ -858,11 +862,11 @@ ZK_DEV int32_t do_create(const ZkTree& t, Lane& L, const uint8_t* data,
   const int32_t seqno = !seq || par < 0 ? 0
                         : pre >= 0      ? pre
                                         : cn_cver(cn_add(t, par, 1, 1));
-  uint8_t* pd = t.path_arena + t.node_path_off[v];
+  uint8_t* pd = t.path_arena + vpo;
   copy_bytes(pd, path, pl);
   if (seq) put_seq10(pd + pl, seqno);
   const int32_t dl = L.dl;
-  uint8_t* slot = s.slab + s.slot_off[v];
+  uint8_t* slot = s.slab + vso;
   fill_stat(slot, L.zx, L.zx, now_ms, now_ms, 0, 0, 0, eph ? session : 0, dl,
             0, L.zx);
   st_be32(slot + ZK_SLOT_LEN, dl > 0 ? dl : -1);
@@ -878,8 +882,8 @@ ZK_DEV int32_t do_create(const ZkTree& t, Lane& L, const uint8_t* data,
   // batch contract; every field it could read is in bounds), and the next
   // launch sees everything.  A __threadfence here is an XCD-L2 writeback
   // per wave (MI355X_MICROARCH.md: ~3.5 us each) and cost milliseconds.
-  const int64_t ins = pre >= 0 ? tree_insert<true>(t, v, pd, npl, dl)
-                               : tree_insert(t, v, pd, npl, dl);
+  const int64_t ins = pre >= 0 ? tree_insert<true>(t, v, pd, npl, dl, vso)
+                               : tree_insert(t, v, pd, npl, dl, vso);
   if (ins != v) {
     // the child was not made (the cversion it took stays: a gap)
     if (taken) cn_add(t, par, 0, -1);

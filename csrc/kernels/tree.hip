@@ -551,12 +551,16 @@ ZK_DEV int64_t ht_reclaim(const ZkTree& t, int64_t s) {
   int64_t n = 0;
   for (int k = 0; k < 64; ++k) {
     const int64_t nx = (s + 1) & t.mask;
-    // (both loads in one round trip)
-    const int64_t kn = __hip_atomic_load(ht_key(t, nx), __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_AGENT);
-    const int64_t vs = __hip_atomic_load(ht_val(t, s), __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_AGENT);
-    if (kn != 0 || !val_tomb(vs)) break;
+    // the successor's key first, the val after it: a val read before an
+    // entry moved into s (from past nx, which was emptied after) paired
+    // with the emptied key would drop the live entry — both loads in one
+    // round trip lost a storm node in a 400-step run
+    if (__hip_atomic_load(ht_key(t, nx), __ATOMIC_RELAXED,
+                          __HIP_MEMORY_SCOPE_AGENT) != 0)
+      break;
+    if (!val_tomb(__hip_atomic_load(ht_val(t, s), __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_AGENT)))
+      break;
     // val first: a reader between the two stores sees a key with val 0
     // (no match, probe on), then the empty key (end of chain)
     __hip_atomic_store(ht_val(t, s), (int64_t)0, __ATOMIC_RELAXED,

@@ -65,15 +65,20 @@ _GET_PRESIZED = os.environ.get('ZKMI_GET_PRESIZED', '1') == '1'
 # handshake and expiry no longer beside the encode / the reply decode)
 _STORM_STREAMS = os.environ.get('ZKMI_STORM_STREAMS', '2') != '1'
 # ZKMI_SRV_GROUP: K1 tiles a wave on the GPU server's request streams, for
-# every workload (unset: the defaults below).  Request streams run long
-# stretches of equal-sized frames, which the groups' walk takes a run at a
-# step: 4 tiles a wave (GET 0.5255 vs 0.5337 ms a step at 1, mix 1.215 vs
-# 1.230), the storm's identical creates 8 (1.298 vs 1.316 at 4, 1.344 at
-# 1; profiles/r6_srv_group_ab.log, r6_srv_group_storm_mix_ab.log)
+# every workload (unset: the defaults below).  Request streams of equal-
+# sized frames without length-like words take groups (the groups' walk
+# steps over a run of equal frames): GET 4 tiles a wave (0.5255 vs 0.5337
+# ms a step at 1), the storm's identical creates 8 (1.298 vs 1.316 at 4,
+# 1.344 at 1; profiles/r6_srv_group_ab.log,
+# r6_srv_group_storm_mix_ab.log).  The others stay at one: SET_DATA
+# versions read as frame lengths make phantom chains, which the per-tile
+# maps settle and a group's walked tiles do not (the watch workload's
+# version-84 step took 32.6 ms against a 2.4 ms median at 4 tiles a wave,
+# tests/test_watch_sustained.py; mix gained 1.2 % at 4).
 _SRV_GROUP_ENV = (int(os.environ['ZKMI_SRV_GROUP'])
                   if os.environ.get('ZKMI_SRV_GROUP') else None)
-_SRV_GROUP = _SRV_GROUP_ENV or 4
-_GET_SRV_GROUP = _SRV_GROUP
+_SRV_GROUP = _SRV_GROUP_ENV
+_GET_SRV_GROUP = _SRV_GROUP_ENV or 4
 _STORM_SRV_GROUP = _SRV_GROUP_ENV or 8
 
 

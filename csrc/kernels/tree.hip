@@ -444,7 +444,7 @@ ZK_DEV bool tree_erase(const ZkTree& t, int64_t v, const uint8_t* p,
 // left for later.  Without it the storm's never-reused SEQUENTIAL names
 // left 1M tombstones a step and the index was rebuilt every few hundred
 // steps (round 5: 1.29 ms timed, 1.40 ms sustained).
-ZK_DEV int64_t ht_reclaim(const ZkTree& t, int64_t s);
+ZK_DEV int64_t ht_reclaim(const ZkTree& t, int64_t s, bool succ_empty = false);
 
 // Backward shift from the hole s (a tombstone this thread just made), in a
 // launch where nothing inserts and the only erasers are those of `session`
@@ -516,7 +516,10 @@ ZK_DEV void ht_shift(const ZkTree& t, int64_t s, int64_t session,
         order_wait();
         __hip_atomic_store(ht_key(t, s), (int64_t)0, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
-        ht_reclaim(t, (s - 1) & t.mask);
+        // (s's key is this thread's 0 — an empty slot stays empty in the
+        // launch — so the reclaim's first step reads only the val before;
+        // it is read after the run's end was seen empty, as it must be)
+        ht_reclaim(t, (s - 1) & t.mask, true);
       }
       return;
     }
@@ -547,10 +550,23 @@ ZK_DEV void ht_shift(const ZkTree& t, int64_t s, int64_t session,
   ht_reclaim(t, s);
 }
 
-ZK_DEV int64_t ht_reclaim(const ZkTree& t, int64_t s) {
+ZK_DEV int64_t ht_reclaim(const ZkTree& t, int64_t s, bool succ_empty) {
   int64_t n = 0;
   for (int k = 0; k < 64; ++k) {
     const int64_t nx = (s + 1) & t.mask;
+    if (succ_empty && k == 0) {
+      if (!val_tomb(__hip_atomic_load(ht_val(t, s), __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT)))
+        break;
+      __hip_atomic_store(ht_val(t, s), (int64_t)0, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+      order_wait();
+      __hip_atomic_store(ht_key(t, s), (int64_t)0, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+      ++n;
+      s = (s - 1) & t.mask;
+      continue;
+    }
     // the successor's key first, the val after it: a val read before an
     // entry moved into s (from past nx, which was emptied after) paired
     // with the emptied key would drop the live entry — both loads in one
